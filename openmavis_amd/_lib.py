@@ -1,0 +1,110 @@
+"""ctypes binding of libomv_hip.so (the C ABI in include/omv.h).
+
+There is deliberately no CPU fallback: if the HIP library is missing or no GPU is visible, every
+product entry point raises.  The CPU oracle under oracle/ is test infrastructure only.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libomv_hip.so")
+
+OMV_OK = 0
+OMV_ERR_ARG = 1
+OMV_ERR_HIP = 2
+OMV_ERR_CAPACITY = 3
+OMV_ERR_NO_DEVICE = 4
+_ERRS = {1: "bad argument", 2: "HIP runtime error", 3: "device capacity exceeded", 4: "no HIP device"}
+
+
+class OmvError(RuntimeError):
+    pass
+
+
+def check(status, what="omv call"):
+    if status != OMV_OK:
+        raise OmvError(f"{what} failed: {_ERRS.get(status, status)} ({status})")
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
+                ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int)]
+
+
+class KeyPoint(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
+                ("angle", ctypes.c_float), ("response", ctypes.c_float), ("octave", ctypes.c_int32)]
+
+
+class FrameGeom(ctypes.Structure):
+    _fields_ = [("n_cams", ctypes.c_int), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int),
+                ("scale_factors", ctypes.c_float * 16)]
+
+
+class MpView(ctypes.Structure):
+    _fields_ = [("desc", ctypes.c_void_p), ("proj_x", ctypes.c_void_p), ("proj_y", ctypes.c_void_p),
+                ("view_cos", ctypes.c_void_p), ("level", ctypes.c_void_p), ("in_view", ctypes.c_void_p),
+                ("track_depth", ctypes.c_void_p), ("is_bad", ctypes.c_void_p), ("has_obs", ctypes.c_void_p)]
+
+
+# numpy dtype with the omv_kp layout (24 bytes)
+try:
+    import numpy as _np
+
+    KP_DTYPE = _np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                          ("response", "<f4"), ("octave", "<i4")])
+except ImportError:  # pragma: no cover
+    KP_DTYPE = None
+
+# Every symbol include/omv.h declares: (name, restype, argtypes)
+_VP, _I, _F, _SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+SIGNATURES = {
+    "omv_orb_create": (_I, [ctypes.POINTER(OrbParams), _I, _I, _I, ctypes.POINTER(_VP)]),
+    "omv_orb_destroy": (_I, [_VP]),
+    "omv_orb_max_keypoints": (_I, [_VP]),
+    "omv_orb_scale_tables": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "omv_orb_extract_batch": (_I, [_VP, _I, _VP, _SZ, _SZ, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "omv_orb_extract_host": (_I, [_VP, _VP, _SZ, _I, _I, _VP, _VP, _VP, _VP]),
+    "omv_orb_last_error": (_I, [_VP]),
+    "omv_orb_debug_level": (_I, [_VP, _I, _I, _VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "omv_bf_knn2": (_I, [_I, _VP, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP]),
+    "omv_grid_sizes": (None, [_I, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "omv_grid_build": (_I, [_I, ctypes.POINTER(FrameGeom), _VP, _I, _VP, _VP, _VP, _VP]),
+    "omv_match_project": (_I, [_I, ctypes.POINTER(FrameGeom), _VP, _VP, _I, _VP, _VP, _VP,
+                               ctypes.POINTER(MpView), _I, _F, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP]),
+}
+
+_lib = None
+missing = []
+
+
+def load(path=LIB_PATH):
+    """Load libomv_hip.so and bind every declared symbol; raises if absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OmvError(f"{path} not built: run `python -m openmavis_amd.build` (hipcc, gfx950). "
+                       "There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    missing.clear()
+    for name, (res, args) in SIGNATURES.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:  # a declared symbol the build does not export (tests flag this)
+            missing.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(t):
+    """Device/host pointer of a torch tensor or numpy array as c_void_p."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return ctypes.c_void_p(t.data_ptr())
+    return ctypes.c_void_p(t.ctypes.data)

@@ -1,0 +1,57 @@
+"""Build the native pieces in-tree (no JIT caches, so the .so files travel to the GPU box).
+
+- openmavis_amd/libomv_hip.so : the product — hand-written gfx950 HIP kernels + the C ABI of
+  include/omv.h (hipcc --offload-arch=gfx950, -ffp-contract=off for the bit-exact float paths).
+- oracle/liboracle.so          : test infrastructure — the CPU restatement used as checker and as
+  bench.py's cpu_baseline leg (built with g++, never linked into the product).
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "openmavis_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libomv_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("OMV_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = ["orb_extract.hip", "match.hip"]
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+             f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force=False, verbose=True):
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
+    deps.append(os.path.join(ROOT, "include", "omv.h"))
+    if not force and not _newer(LIB, deps):
+        return LIB
+    cmd = [HIPCC] + HIP_FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + srcs
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(verbose=True):
+    odir = os.path.join(ROOT, "oracle")
+    subprocess.check_call(["make", "-s", "-C", odir], stdout=None if verbose else subprocess.DEVNULL)
+    return os.path.join(odir, "liboracle.so")
+
+
+def build_all(force=False, verbose=True):
+    build_oracle(verbose)
+    return build_hip(force, verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,104 @@
+// Device-side arithmetic helpers for the gfx950 kernels.  Every float path here must be compiled
+// with -ffp-contract=off: the reference's float expressions are evaluated without fused
+// multiply-adds, and bit-exact keypoints/descriptors depend on reproducing their rounding.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace omv {
+
+// cvRound(float): round half to even (x86 cvtss2si under the default MXCSR).
+__device__ __forceinline__ int round_even(float v) { return (int)__builtin_rintf(v); }
+
+// cv::fastAtan2 (OpenCV 4.x atan_f32, degrees, float).  Coefficients are the float products
+// 0.99978784f*(float)(180/pi) etc., folded exactly as the host compiler folds them.
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+    const float r2d = (float)(180.0 / 3.14159265358979323846);
+    const float k1 = 0.9997878412794807f * r2d;
+    const float k3 = -0.3258083974640975f * r2d;
+    const float k5 = 0.1555786518463281f * r2d;
+    const float k7 = -0.04432655554792128f * r2d;
+    const float eps = (float)2.220446049250313080847e-16;   // (float)DBL_EPSILON
+    float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((k7 * c2 + k5) * c2 + k3) * c2 + k1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((k7 * c2 + k5) * c2 + k3) * c2 + k1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ---- single-precision sin/cos, bit-identical to the host glibc (2.35) cosf/sinf ------------------
+// The reference calls cos()/sin() on a float (src/ORBextractor.cc:49), i.e. glibc's cosf/sinf.
+// Those evaluate a double-precision polynomial after a one-step pi/2 reduction; we restate that
+// published algorithm with the same constants and explicit fma() where the x86-64 FMA build fuses.
+// Verified bit-exact against the host libm over every float in [0, 2*pi] (tests/test_oracle.py
+// re-checks a sample; tools/check_sincosf.c is the exhaustive sweep).
+struct SinCosTab {
+    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+__device__ __forceinline__ float sincosf_poly(double x, double x2, const SinCosTab &p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = __builtin_fma(x2, p.s3, p.s2);
+        double x7 = x3 * x2;
+        double s = __builtin_fma(x3, p.s1, x);
+        return (float)__builtin_fma(x7, s1, s);
+    }
+    double x4 = x2 * x2;
+    double c2 = __builtin_fma(x2, p.c4, p.c3);
+    double c1 = __builtin_fma(x2, p.c1, p.c0);
+    double x6 = x4 * x2;
+    double c = __builtin_fma(x4, p.c2, c1);
+    return (float)__builtin_fma(x6, c2, c);
+}
+__device__ __forceinline__ uint32_t top12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+
+// Valid for |y| < 120 (the reduce_fast range), which covers every angle in [0, 2*pi).
+__device__ __forceinline__ void glibc_sincosf(float y, float *sinp, float *cosp) {
+    const SinCosTab t0 = {0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+                          0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
+                          -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    const SinCosTab t1 = {0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+                          -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
+                          -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    double x = y;
+    if (top12(y) < top12(0x1.921FB6p-1f)) {
+        if (top12(y) < top12(0x1p-12f)) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        double x2 = x * x;
+        *sinp = sincosf_poly(x, x2, t0, 0);
+        *cosp = sincosf_poly(x, x2, t0, 1);
+        return;
+    }
+    double r = x * t0.hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    double xr = __builtin_fma(-(double)n, t0.hpi, x);
+    const double sgn[4] = {1.0, -1.0, -1.0, 1.0};
+    double s = sgn[n & 3];
+    const SinCosTab &p = (n & 2) ? t1 : t0;
+    *sinp = sincosf_poly(xr * s, xr * xr, p, n);
+    *cosp = sincosf_poly(xr * s, xr * xr, p, n ^ 1);
+}
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+    // single reflection suffices: callers stay within one image width of the border
+    p = p < 0 ? -p : p;
+    return p >= n ? 2 * n - 2 - p : p;
+}
+
+// Hamming distance of two 256-bit descriptors held as 4 x u64.
+__device__ __forceinline__ int hamming256(const uint64_t *a, const uint64_t *b) {
+    return __popcll(a[0] ^ b[0]) + __popcll(a[1] ^ b[1]) + __popcll(a[2] ^ b[2]) + __popcll(a[3] ^ b[3]);
+}
+
+}  // namespace omv

@@ -1,0 +1,1077 @@
+// MI355X-native ORB extractor: the path of ORBextractor::operator() (src/ORBextractor.cc:987-1071)
+// as four gfx950 kernels over a batch of device-resident images.
+//
+//   K1 pyr_resize   one launch per pyramid level l >= 1, level l from level l-1 (ComputePyramid
+//                   :1073-1104; cv::resize INTER_LINEAR 8U fixed point), coefficient tables
+//                   precomputed on the host in the reference's float/double order.
+//   K2 fast_cells   one wavefront per FAST cell (ComputeKeyPointsOctTree :709-794): the cell region
+//                   is staged in LDS, each lane evaluates FAST-9 "strength" S for pixels (corner at
+//                   threshold t <=> S > t, cornerScore = S - 1), then the cell-local 3x3 NMS at
+//                   iniThFAST with the minThFAST fallback; keypoints emitted in row-major order.
+//   K3 octree       one workgroup per (image, level): DistributeOctTree (:496-702) as a parallel
+//                   list rebuild per subdivision round (prefix scans over the node list, atomics in
+//                   LDS for quadrant counts) plus the libstdc++ introsort replica for the
+//                   (size, UL.x) refinement ordering; picks max-response key per node; classifies
+//                   lapping/non-lapping for the output split (:1045-1067).
+//   K4 describe     one wavefront per keypoint: the 43x43 reflect-101 patch goes to LDS once;
+//                   intensity-centroid angle (IC_Angle :19-43, fastAtan2), the 7x7 sigma-2 blur of
+//                   the 37x37 sampling window (GaussianBlur 8U bit-exact path), steered rBRIEF via
+//                   4 ballots (computeOrbDescriptor :46-90); writes the keypoint and descriptor
+//                   straight into its final (mono-front / lapping-back) row.
+//
+// All float code is compiled with -ffp-contract=off (see omv_device.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/omv.h"
+#include "omv_device.h"
+#include "omv_introsort.h"
+
+namespace {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdge = 19;     // EDGE_THRESHOLD
+constexpr int kMinB = kEdge - 3;
+constexpr int kPatchR = 21;   // 18 (max steered pattern radius) + 3 (blur half-width)
+constexpr int kPatchW = 2 * kPatchR + 1;   // 43
+constexpr int kWinR = 18;
+constexpr int kWinW = 2 * kWinR + 1;       // 37
+
+__constant__ int c_pattern[256 * 4] = {
+#define OMV_PATTERN_TABLE_BEGIN
+#define OMV_PATTERN_TABLE_END
+#include "orb_pattern_31.inc"
+};
+__constant__ int c_umax[16];
+__constant__ int c_gauss7[7] = {18, 34, 48, 56, 48, 34, 18};
+
+struct LevelGeom {
+    int w, h, pitch;        // level l pixels; pitch of the level in the pyramid buffer
+    long long off;          // byte offset of level l inside one image's pyramid block (l >= 1)
+    int maxBX, maxBY;       // FAST region bounds (cols - 16, rows - 16)
+    int cell_begin, cell_end;
+    int quota;              // mnFeaturesPerLevel
+    int out_cap;            // max keypoints this level can emit (quota + 2, or 4 * nIni)
+    int out_off;            // offset of this level's slots in the per-image level-output block
+    long long cand_off;     // offset of this level's compact candidates in the per-image block
+    int cand_cap;
+    int nIni;
+    float hX;
+    float scale;            // mvScaleFactor[l]
+    float size;             // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
+    int xtab_off, ytab_off; // resize tables (l >= 1)
+};
+
+struct Cell {
+    int level, y0, y1, x0, x1;   // region rows [y0,y1), cols [x0,x1) in level coordinates
+};
+
+struct Geom {
+    int nlevels;
+    int W, H;
+    int ini_th, min_th;
+    int n_cells;            // cells per image
+    int cell_cap;           // keypoint slots per cell
+    long long pyr_bytes;    // pyramid block per image (levels >= 1)
+    long long cand_per_img;
+    int out_per_img;        // level-output slots per image
+    int n_max;              // output rows per image
+    int node_cap;           // octree LDS node capacity
+    LevelGeom lv[kMaxLevels];
+};
+
+struct XTab {
+    int sx0, sx1, coef;   // coef = a0 | (a1 << 16)
+};
+
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_t *images, size_t img_stride,
+                                                     size_t pitch0, const uint8_t *pyr, int img, int l,
+                                                     int *pitch) {
+    if (l == 0) {
+        *pitch = (int)pitch0;
+        return images + (size_t)img * img_stride;
+    }
+    *pitch = g.lv[l].pitch;
+    return pyr + (size_t)img * g.pyr_bytes + g.lv[l].off;
+}
+
+// K1 --------------------------------------------------------------------------------------------
+// One thread per output pixel of level l; rows of level l-1 are re-read from L2.
+__global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const uint8_t *images, size_t img_stride,
+                                                         size_t pitch0, uint8_t *pyr, const XTab *xt,
+                                                         const XTab *yt, int n_images) {
+    const LevelGeom &L = g.lv[l];
+    const long long per_img = (long long)L.w * L.h;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= per_img * n_images) return;
+    const int img = (int)(gid / per_img);
+    const int rem = (int)(gid - (long long)img * per_img);
+    const int dy = rem / L.w, dx = rem - dy * L.w;
+    int sp;
+    const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, l - 1, &sp);
+    uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off;
+    const XTab x = xt[L.xtab_off + dx];
+    const XTab y = yt[L.ytab_off + dy];
+    const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
+    const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
+    const uint8_t *r0 = src + (size_t)y.sx0 * sp, *r1 = src + (size_t)y.sx1 * sp;
+    const int h0 = r0[x.sx0] * a0 + r0[x.sx1] * a1;
+    const int h1 = r1[x.sx0] * a0 + r1[x.sx1] * a1;
+    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    dst[(size_t)dy * L.pitch + dx] = (uint8_t)min(v, 255);
+}
+
+// K2 --------------------------------------------------------------------------------------------
+// FAST-9 strength: max over the 16 circular 9-arcs of min(d) (darker) and of min(-d) (brighter),
+// d = centre - ring.  A pixel is a FAST corner at threshold t iff S > t, and OpenCV's
+// cornerScore<16>(t) then returns S - 1 (the threshold floor max(t, .) never binds for a corner).
+__device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * stride];
+    d[1] = v - p[3 * stride + 1];
+    d[2] = v - p[2 * stride + 2];
+    d[3] = v - p[stride + 3];
+    d[4] = v - p[3];
+    d[5] = v - p[-stride + 3];
+    d[6] = v - p[-2 * stride + 2];
+    d[7] = v - p[-3 * stride + 1];
+    d[8] = v - p[-3 * stride];
+    d[9] = v - p[-3 * stride - 1];
+    d[10] = v - p[-2 * stride - 2];
+    d[11] = v - p[-stride - 3];
+    d[12] = v - p[-3];
+    d[13] = v - p[stride - 3];
+    d[14] = v - p[2 * stride - 2];
+    d[15] = v - p[3 * stride - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int a = -1000, b = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int m9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int M9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        a = max(a, m9);
+        b = min(b, M9);
+    }
+    return max(a, -b);
+}
+
+// One wavefront (= one workgroup of 64) per cell.
+__global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
+                                                        size_t img_stride, size_t pitch0, const uint8_t *pyr,
+                                                        int *cell_cnt, uint32_t *cell_kp, int rmax) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int img = blockIdx.x / g.n_cells;
+    const int ci = blockIdx.x - img * g.n_cells;
+    const Cell c = cells[ci];
+    const int lane = threadIdx.x;
+    uint8_t *pix = smem;
+    uint8_t *S = smem + rmax;
+    const int rw = c.x1 - c.x0, rh = c.y1 - c.y0;
+    int sp;
+    const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, c.level, &sp);
+    for (int i = lane; i < rw * rh; i += 64) {
+        const int r = i / rw, q = i - r * rw;
+        pix[i] = src[(size_t)(c.y0 + r) * sp + c.x0 + q];
+        S[i] = 0;
+    }
+    __syncthreads();
+    const int dw = rw - 6, dh = rh - 6;   // detection window [3, rw-4] x [3, rh-4]
+    const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
+    for (int i = lane; i < ndet; i += 64) {
+        const int r = 3 + i / dw, q = 3 + i % dw;
+        const int s = fast_strength(pix + r * rw + q, rw);
+        S[r * rw + q] = (uint8_t)min(max(s, 0), 255);
+    }
+    __syncthreads();
+    // NMS at iniThFAST, minThFAST fallback if the cell yields nothing (:764-782)
+    int th = g.ini_th;
+    int total = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        total = 0;
+        for (int i0 = 0; i0 < ndet; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            if (i < ndet) {
+                const int r = 3 + i / dw, q = 3 + i % dw;
+                const uint8_t *s = S + r * rw + q;
+                const int v = s[0];
+                if (v > th) {
+                    keep = true;
+                    const int sc = v - 1;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) {
+                        if (k == 4) continue;
+                        const int nv = s[(k / 3 - 1) * rw + (k % 3 - 1)];
+                        const int ns = nv > th ? nv - 1 : 0;
+                        keep = keep && (sc > ns);
+                    }
+                }
+            }
+            total += __popcll(__ballot(keep));
+        }
+        if (total > 0 || pass == 1) break;
+        th = g.min_th;
+    }
+    if (total > g.cell_cap) {   // cannot happen by construction (cap = max NMS survivors)
+        if (lane == 0) cell_cnt[blockIdx.x] = -1;
+        return;
+    }
+    // emit row-major; coordinates relative to the FAST border (minBorder = 16)
+    uint32_t *out = cell_kp + (size_t)blockIdx.x * g.cell_cap;
+    int base = 0;
+    for (int i0 = 0; i0 < ndet; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = false;
+        uint32_t packed = 0;
+        if (i < ndet) {
+            const int r = 3 + i / dw, q = 3 + i % dw;
+            const uint8_t *s = S + r * rw + q;
+            const int v = s[0];
+            if (v > th) {
+                keep = true;
+                const int sc = v - 1;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    if (k == 4) continue;
+                    const int nv = s[(k / 3 - 1) * rw + (k % 3 - 1)];
+                    const int ns = nv > th ? nv - 1 : 0;
+                    keep = keep && (sc > ns);
+                }
+                const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
+                packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)sc << 24);
+            }
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const int off = __popcll(m & ((1ull << lane) - 1ull));
+            out[base + off] = packed;
+        }
+        base += __popcll(m);
+    }
+    if (lane == 0) cell_cnt[blockIdx.x] = total;
+}
+
+// K3 --------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// In-place exclusive scan of a[0..n) in LDS by the whole (256-thread) block; returns the total.
+__device__ int block_excl_scan(int *a, int n, int *tmp) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int chunk = (n + T - 1) / T;
+    const int b = min(n, tid * chunk), e = min(n, b + chunk);
+    int s = 0;
+    for (int i = b; i < e; ++i) s += a[i];
+    const int incl = wave_incl_scan(s);
+    const int wave = tid >> 6, nw = T >> 6;
+    __syncthreads();
+    if ((tid & 63) == 63) tmp[wave] = incl;
+    __syncthreads();
+    int woff = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        if (w < wave) woff += tmp[w];
+        tot += tmp[w];
+    }
+    int run = woff + incl - s;
+    for (int i = b; i < e; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return tot;
+}
+
+__device__ int block_sum(int v, int *tmp) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += tmp[w];
+    __syncthreads();
+    return t;
+}
+
+struct NodeSoA {
+    int *x0, *x1, *y0, *y1, *cnt;
+};
+
+// Quadrant of key (x, y) in node i: 0 = n1 (UL), 1 = n2 (UR), 2 = n3 (BL), 3 = n4 (BR)  (DivideNode)
+__device__ __forceinline__ int node_mid_x(const NodeSoA &A, int i) {
+    return A.x0[i] + (int)ceilf((float)(A.x1[i] - A.x0[i]) / 2);
+}
+__device__ __forceinline__ int node_mid_y(const NodeSoA &A, int i) {
+    return A.y0[i] + (int)ceilf((float)(A.y1[i] - A.y0[i]) / 2);
+}
+__device__ __forceinline__ void child_rect(const NodeSoA &A, int i, int t, int &x0, int &x1, int &y0, int &y1) {
+    const int xm = node_mid_x(A, i), ym = node_mid_y(A, i);
+    x0 = (t & 1) ? xm : A.x0[i];
+    x1 = (t & 1) ? A.x1[i] : xm;
+    y0 = (t & 2) ? ym : A.y0[i];
+    y1 = (t & 2) ? A.y1[i] : ym;
+}
+
+constexpr uint32_t kSplitFlag = 0x80000000u;
+
+struct OctArgs {
+    const int *cell_cnt;
+    const uint32_t *cell_kp;
+    uint32_t *cand;        // compact candidates scratch
+    uint32_t *nid;         // per-candidate node id scratch
+    uint32_t *lvl_out;     // [img][out_per_img] packed x|y|score of selected keypoints
+    uint32_t *lvl_cls;     // [img][out_per_img] rank | lap << 31
+    int *lvl_cnt;          // [img][L][3] total, mono, lap
+    const int *lapping;    // device [img][2]
+    int *err;
+};
+
+__global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int osm[];
+    const int img = blockIdx.x / g.nlevels;
+    const int l = blockIdx.x - img * g.nlevels;
+    const LevelGeom &L = g.lv[l];
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int NC = g.node_cap;
+    // LDS carve-up
+    int *tmp = osm;                  // 16
+    int *shared_int = osm + 16;      // 16 scalars
+    int *buf = osm + 32;
+    NodeSoA A{buf, buf + NC, buf + 2 * NC, buf + 3 * NC, buf + 4 * NC};
+    NodeSoA B{buf + 5 * NC, buf + 6 * NC, buf + 7 * NC, buf + 8 * NC, buf + 9 * NC};
+    int *ccnt = buf + 10 * NC;       // 4 * NC
+    int *scanA = buf + 14 * NC;      // NC
+    int *scanB = buf + 15 * NC;      // NC
+    int *map = buf + 16 * NC;        // NC: new index of an unsplit/unprocessed node, or -1
+    int *vlist = buf + 17 * NC;      // NC
+    int *vpos = buf + 18 * NC;       // NC: position in the sorted V list, or -1
+    int *cellscan = buf + 19 * NC;   // cells of this level (<= NC by host check)
+    omv::SortItem *items = reinterpret_cast<omv::SortItem *>(buf + 20 * NC);   // NC items (3 ints)
+    int *sstack = buf + 23 * NC;     // 192
+
+    const int ncell = L.cell_end - L.cell_begin;
+    uint32_t *cand = a.cand + (size_t)img * g.cand_per_img + L.cand_off;
+    uint32_t *nid = a.nid + (size_t)img * g.cand_per_img + L.cand_off;
+    const int N = L.quota;
+
+    // ---- gather candidates of this level in cell order (vToDistributeKeys order) ----
+    for (int i = tid; i < ncell; i += T) {
+        const int cc = a.cell_cnt[(size_t)img * g.n_cells + L.cell_begin + i];
+        if (cc < 0) atomicOr(a.err, OMV_ERR_CAPACITY);
+        cellscan[i] = max(cc, 0);
+    }
+    __syncthreads();
+    const int K = block_excl_scan(cellscan, ncell, tmp);
+    if (K > L.cand_cap) {
+        if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
+        return;
+    }
+    for (int i = 0; i < ncell; ++i) {
+        const int b = cellscan[i];
+        const int n = (i + 1 < ncell ? cellscan[i + 1] : K) - b;
+        const uint32_t *src = a.cell_kp + ((size_t)img * g.n_cells + L.cell_begin + i) * g.cell_cap;
+        for (int k = tid; k < n; k += T) cand[b + k] = src[k];
+    }
+    __syncthreads();
+
+    int *cnt_out = a.lvl_cnt + ((size_t)img * g.nlevels + l) * 3;
+    uint32_t *out = a.lvl_out + (size_t)img * g.out_per_img + L.out_off;
+    uint32_t *cls = a.lvl_cls + (size_t)img * g.out_per_img + L.out_off;
+    if (K == 0) {
+        if (tid == 0) cnt_out[0] = cnt_out[1] = cnt_out[2] = 0;
+        return;
+    }
+
+    // ---- initial vertical strips ----
+    const int nIni = L.nIni;
+    const float hX = L.hX;
+    const int Hn = L.maxBY - kMinB;
+    if (nIni > NC) {
+        if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
+        return;
+    }
+    for (int i = tid; i < nIni; i += T) {
+        B.x0[i] = (int)(hX * (float)i);
+        B.x1[i] = (int)(hX * (float)(i + 1));
+        B.y0[i] = 0;
+        B.y1[i] = Hn;
+        B.cnt[i] = 0;
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const float x = (float)(cand[k] & 0xfff);
+        const int n = (int)(x / hX);
+        nid[k] = (uint32_t)n;
+        atomicAdd(&B.cnt[n], 1);
+    }
+    __syncthreads();
+    // drop empty strips, keep order
+    for (int i = tid; i < nIni; i += T) scanA[i] = B.cnt[i] > 0 ? 1 : 0;
+    __syncthreads();
+    int m = block_excl_scan(scanA, nIni, tmp);
+    for (int i = tid; i < nIni; i += T)
+        if (B.cnt[i] > 0) {
+            const int j = scanA[i];
+            A.x0[j] = B.x0[i], A.x1[j] = B.x1[i], A.y0[j] = B.y0[i], A.y1[j] = B.y1[i], A.cnt[j] = B.cnt[i];
+        }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) nid[k] = (uint32_t)scanA[nid[k]];
+    __syncthreads();
+
+    // ---- subdivision rounds ----
+    // phase 1: every node with > 1 key splits (list walk :562-613)
+    // phase 2: only the expandable list of the last round, largest (size, UL.x) first (:621-679)
+    bool phase2 = false;
+    int nv = 0;   // phase 2: |V|, V stored in vlist (indices into A, creation order)
+    for (int guard = 0; guard < 4096; ++guard) {
+        const int prev = m;
+        // 1. mark which nodes split this round, zero child counts
+        for (int i = tid; i < m; i += T) {
+            map[i] = -1;
+            vpos[i] = -1;
+            ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
+        }
+        __syncthreads();
+        if (!phase2) {
+            for (int i = tid; i < m; i += T) vpos[i] = A.cnt[i] > 1 ? 0 : -1;
+        } else {
+            // sort V by (size, UL.x) with the libstdc++ introsort replica (one lane)
+            if (tid == 0) {
+                for (int j = 0; j < nv; ++j) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
+                omv::libstdcxx_sort(items, nv, sstack);
+            }
+            __syncthreads();
+            for (int j = tid; j < nv; j += T) vpos[items[j].payload] = j;
+        }
+        __syncthreads();
+        // 2. quadrant counts for the candidate nodes
+        for (int k = tid; k < K; k += T) {
+            const uint32_t n = nid[k] & ~kSplitFlag;
+            if (vpos[n] >= 0) {
+                const uint32_t p = cand[k];
+                const int x = p & 0xfff, y = (p >> 12) & 0xfff;
+                const int t = (x < node_mid_x(A, n) ? 0 : 1) + (y < node_mid_y(A, n) ? 0 : 2);
+                atomicAdd(&ccnt[4 * n + t], 1);
+                nid[k] = kSplitFlag | (n << 2) | t;
+            } else {
+                nid[k] = n;
+            }
+        }
+        __syncthreads();
+        // 3. which candidate nodes are actually divided, and in what order children are created
+        //    processed[i]: scanA holds #non-empty children in creation order position
+        int n_proc_nodes;   // number of divided nodes
+        if (!phase2) {
+            // creation order = list order; every candidate node is divided
+            for (int i = tid; i < m; i += T) {
+                int nk = 0;
+                if (vpos[i] >= 0)
+                    for (int t = 0; t < 4; ++t) nk += ccnt[4 * i + t] > 0;
+                scanA[i] = nk;
+                scanB[i] = vpos[i] >= 0 ? 0 : 1;
+            }
+            n_proc_nodes = m;   // scan domain
+        } else {
+            // divide from the back of the sorted list until the list holds >= N nodes (:633-675)
+            if (tid == 0) {
+                int size = m, jstar = nv;
+                for (int j = nv - 1; j >= 0; --j) {
+                    const int n = items[j].payload;
+                    int nk = 0;
+                    for (int t = 0; t < 4; ++t) nk += ccnt[4 * n + t] > 0;
+                    size += nk - 1;
+                    jstar = j;
+                    if (size >= N) break;
+                }
+                shared_int[0] = jstar;
+            }
+            __syncthreads();
+            const int jstar = shared_int[0];
+            n_proc_nodes = nv - jstar;
+            // processing position p = 0.. corresponds to items[nv-1-p]
+            for (int p = tid; p < n_proc_nodes; p += T) {
+                const int n = items[nv - 1 - p].payload;
+                int nk = 0;
+                for (int t = 0; t < 4; ++t) nk += ccnt[4 * n + t] > 0;
+                scanA[p] = nk;
+            }
+            // vpos now marks processed nodes only: position p, else -1
+            __syncthreads();
+            for (int i = tid; i < m; i += T) vpos[i] = -1;
+            __syncthreads();
+            for (int p = tid; p < n_proc_nodes; p += T) vpos[items[nv - 1 - p].payload] = p;
+            __syncthreads();
+            for (int i = tid; i < m; i += T) scanB[i] = vpos[i] >= 0 ? 0 : 1;
+        }
+        __syncthreads();
+        const int Q = block_excl_scan(scanA, n_proc_nodes, tmp);
+        const int U = block_excl_scan(scanB, m, tmp);
+        const int newm = Q + U;
+        if (newm > NC) {
+            if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
+            return;
+        }
+        // 4. build the new list: children (reverse creation order) then survivors (old order)
+        for (int i = tid; i < m; i += T) {
+            const int p = phase2 ? vpos[i] : (vpos[i] >= 0 ? i : -1);
+            if (p >= 0) {
+                int r = scanA[p];
+                for (int t = 0; t < 4; ++t) {
+                    const int c = ccnt[4 * i + t];
+                    if (c > 0) {
+                        const int j = Q - 1 - r;
+                        child_rect(A, i, t, B.x0[j], B.x1[j], B.y0[j], B.y1[j]);
+                        B.cnt[j] = c;
+                        ccnt[4 * i + t] = -(j + 1);   // remember the child's new index
+                        ++r;
+                    }
+                }
+            } else {
+                const int j = Q + scanB[i];
+                B.x0[j] = A.x0[i], B.x1[j] = A.x1[i], B.y0[j] = A.y0[i], B.y1[j] = A.y1[i], B.cnt[j] = A.cnt[i];
+                map[i] = j;
+            }
+        }
+        __syncthreads();
+        // 5. relabel keys
+        for (int k = tid; k < K; k += T) {
+            const uint32_t v = nid[k];
+            if (v & kSplitFlag) {
+                const int n = (v & ~kSplitFlag) >> 2, t = v & 3;
+                const bool divided = phase2 ? vpos[n] >= 0 : true;
+                nid[k] = divided ? (uint32_t)(-ccnt[4 * n + t] - 1) : (uint32_t)map[n];
+            } else {
+                nid[k] = (uint32_t)map[v];
+            }
+        }
+        // 6. expandable children (> 1 key) in creation order = new indices Q-1 down to 0
+        for (int j = tid; j < Q; j += T) scanA[j] = B.cnt[Q - 1 - j] > 1 ? 1 : 0;
+        __syncthreads();
+        const int nexp = block_excl_scan(scanA, Q, tmp);
+        for (int j = tid; j < Q; j += T)
+            if (B.cnt[Q - 1 - j] > 1) vlist[scanA[j]] = Q - 1 - j;
+        // swap A <-> B
+        for (int i = tid; i < newm; i += T) {
+            A.x0[i] = B.x0[i], A.x1[i] = B.x1[i], A.y0[i] = B.y0[i], A.y1[i] = B.y1[i], A.cnt[i] = B.cnt[i];
+        }
+        __syncthreads();
+        m = newm;
+        if (m >= N || m == prev) break;
+        if (!phase2) {
+            if (m + nexp * 3 > N) phase2 = true;
+        }
+        nv = nexp;
+        if (phase2 && nv == 0) {
+            // nothing left to expand: the next round would leave the size unchanged
+            break;
+        }
+    }
+
+    // ---- keep the strongest key of each node (first on ties) ----
+    int *best = scanA;
+    for (int i = tid; i < m; i += T) best[i] = -1;
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const int n = (int)nid[k];
+        const int key = (int)((cand[k] >> 24) << 23) | (0x7fffff - k);
+        atomicMax(&best[n], key);
+    }
+    __syncthreads();
+    const int lap0 = a.lapping[2 * img], lap1 = a.lapping[2 * img + 1];
+    for (int i = tid; i < m; i += T) {
+        const int k = 0x7fffff - (best[i] & 0x7fffff);
+        const uint32_t p = cand[k];
+        out[i] = p;
+        float xs = (float)((int)(p & 0xfff) + kMinB);
+        if (l != 0) xs *= L.scale;
+        scanB[i] = (xs >= (float)lap0 && xs <= (float)lap1) ? 1 : 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < m; i += T) map[i] = scanB[i];
+    __syncthreads();
+    const int nlap = block_excl_scan(scanB, m, tmp);
+    for (int i = tid; i < m; i += T) {
+        const int lapf = map[i];
+        const int rank = lapf ? scanB[i] : i - scanB[i];
+        cls[i] = (uint32_t)rank | ((uint32_t)lapf << 31);
+    }
+    if (tid == 0) {
+        cnt_out[0] = m;
+        cnt_out[1] = m - nlap;
+        cnt_out[2] = nlap;
+    }
+}
+
+// K4 --------------------------------------------------------------------------------------------
+struct DescArgs {
+    const uint8_t *images;
+    size_t img_stride, pitch0;
+    const uint8_t *pyr;
+    const uint32_t *lvl_out, *lvl_cls;
+    const int *lvl_cnt;
+    omv_kp *kps;
+    uint8_t *desc;
+    int *n_out, *mono;
+    int n_images;
+};
+
+__global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchW + 7];
+    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kWinW];
+    __shared__ __attribute__((aligned(16))) uint8_t win[4][kWinW * kWinW + 7];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + wave;
+    int img = slot / g.out_per_img;
+    const int s = slot - img * g.out_per_img;
+    const bool in_range = img < a.n_images;
+    if (!in_range) img = a.n_images - 1;   // tail waves of the last block: compute nothing
+    // which level does slot s belong to
+    int l = 0;
+    while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_off) ++l;
+    const LevelGeom &L = g.lv[l];
+    const int j = s - L.out_off;
+    const int *cnts = a.lvl_cnt + (size_t)img * g.nlevels * 3;
+    if (in_range && s == 0 && lane == 0) {
+        int tot = 0, mono = 0;
+        for (int q = 0; q < g.nlevels; ++q) tot += cnts[3 * q], mono += cnts[3 * q + 1];
+        a.n_out[img] = tot;
+        a.mono[img] = mono;
+    }
+    // Inactive waves (slot beyond this level's count) still take part in the block barriers.
+    const bool active = in_range && j < cnts[3 * l];
+    const uint32_t p = active ? a.lvl_out[(size_t)img * g.out_per_img + s] : 0u;
+    const uint32_t cl = active ? a.lvl_cls[(size_t)img * g.out_per_img + s] : 0u;
+    const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
+    const int score = (int)(p >> 24);
+    int sp;
+    const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
+    uint8_t *P = patch[wave];
+    for (int i = active ? lane : kPatchW * kPatchW; i < kPatchW * kPatchW; i += 64) {
+        const int r = i / kPatchW, q = i - r * kPatchW;
+        const int yy = omv::reflect101(cy - kPatchR + r, L.h), xx = omv::reflect101(cx - kPatchR + q, L.w);
+        P[i] = src[(size_t)yy * sp + xx];
+    }
+    __syncthreads();
+    // intensity centroid over the r = 15 disc (umax rows), exact integer sums
+    int m01 = 0, m10 = 0;
+    for (int i = lane; i < 31 * 31; i += 64) {
+        const int v = i / 31 - 15, u = i % 31 - 15;
+        const int av = v < 0 ? -v : v;
+        if ((u < 0 ? -u : u) <= c_umax[av]) {
+            const int I = P[(kPatchR + v) * kPatchW + kPatchR + u];
+            m10 += u * I;
+            m01 += v * I;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        m01 += __shfl_xor(m01, d, 64);
+        m10 += __shfl_xor(m10, d, 64);
+    }
+    const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
+    // 7x7 sigma-2 blur of the 37x37 window: horizontal (exact u16), vertical ((+2^15) >> 16)
+    uint16_t *Hs = hsum[wave];
+    for (int i = lane; i < kPatchW * kWinW; i += 64) {
+        const int r = i / kWinW, q = i - r * kWinW;
+        const uint8_t *row = P + r * kPatchW + q;
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) acc += c_gauss7[k] * row[k];
+        Hs[i] = (uint16_t)acc;
+    }
+    __syncthreads();
+    uint8_t *Wn = win[wave];
+    for (int i = lane; i < kWinW * kWinW; i += 64) {
+        const int r = i / kWinW, q = i - r * kWinW;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * Hs[(r + k) * kWinW + q];
+        Wn[i] = (uint8_t)min((acc + 32768u) >> 16, 255u);
+    }
+    __syncthreads();
+    // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
+    float sn, cs;
+    omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
+    const float fa = cs, fb = sn;
+    uint64_t words[4];
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) {
+        const int i = rd * 64 + lane;
+        const int ax = c_pattern[4 * i], ay = c_pattern[4 * i + 1];
+        const int bx = c_pattern[4 * i + 2], by = c_pattern[4 * i + 3];
+        const int ady = omv::round_even((float)ax * fb + (float)ay * fa);
+        const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
+        const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
+        const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
+        const int ia = Wn[(kWinR + ady) * kWinW + kWinR + adx];
+        const int ib = Wn[(kWinR + bdy) * kWinW + kWinR + bdx];
+        words[rd] = __ballot(ia < ib);
+    }
+    if (!active) return;   // after the last barrier
+    // final row: monoIndex order (front) or lapping order (back, reversed)
+    int mono_before = 0, lap_before = 0, total = 0;
+    for (int q = 0; q < g.nlevels; ++q) {
+        total += cnts[3 * q];
+        if (q < l) mono_before += cnts[3 * q + 1], lap_before += cnts[3 * q + 2];
+    }
+    const int rank = (int)(cl & 0x7fffffffu);
+    const int row = (cl >> 31) ? total - 1 - (lap_before + rank) : mono_before + rank;
+    omv_kp *kp = a.kps + (size_t)img * g.n_max + row;
+    uint64_t *dst = reinterpret_cast<uint64_t *>(a.desc + ((size_t)img * g.n_max + row) * 32);
+    if (lane < 4) dst[lane] = words[lane];
+    if (lane == 0) {
+        float x = (float)cx, y = (float)cy;
+        if (l != 0) x *= L.scale, y *= L.scale;
+        *kp = omv_kp{x, y, L.size, angle, (float)score, l};
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+#define HIP_OK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "omv: %s failed: %s\n", #x, hipGetErrorString(e_));      \
+            return OMV_ERR_HIP;                                                      \
+        }                                                                            \
+    } while (0)
+
+inline int host_round_even(float v) { return (int)std::nearbyint(v); }
+
+}  // namespace
+
+struct omv_orb {
+    omv_orb_params p;
+    int W, H, max_images;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> quota;
+    int umax[16];
+    Geom g;
+    // device
+    Cell *d_cells = nullptr;
+    XTab *d_xt = nullptr, *d_yt = nullptr;
+    uint8_t *d_pyr = nullptr;
+    int *d_cell_cnt = nullptr;
+    uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
+    int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
+    int rmax = 0;
+    size_t oct_lds = 0;
+    // host staging for the synchronous path
+    uint8_t *d_img1 = nullptr;
+    omv_kp *d_kp1 = nullptr;
+    uint8_t *d_desc1 = nullptr;
+    int *d_n1 = nullptr;
+    std::vector<int> h_lap;
+    hipStream_t last_stream = nullptr;
+    int device = 0;
+};
+
+static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vector<XTab> &xt, std::vector<XTab> &yt) {
+    const omv_orb_params &p = o->p;
+    const int nl = p.nlevels;
+    // ORBextractor ctor tables (:362-391): scaleFactor is a double member
+    const double sf = (double)p.scale_factor;
+    o->scale.assign(nl, 1.f), o->sigma2.assign(nl, 1.f), o->inv_scale.resize(nl), o->inv_sigma2.resize(nl);
+    for (int i = 1; i < nl; ++i) {
+        o->scale[i] = (float)(o->scale[i - 1] * sf);
+        o->sigma2[i] = o->scale[i] * o->scale[i];
+    }
+    for (int i = 0; i < nl; ++i) o->inv_scale[i] = 1.0f / o->scale[i], o->inv_sigma2[i] = 1.0f / o->sigma2[i];
+    o->quota.assign(nl, 0);
+    const float f = (float)(1.0f / sf);
+    float per = p.nfeatures * (1 - f) / (1 - (float)std::pow((double)f, (double)nl));
+    int sum = 0;
+    for (int l = 0; l < nl - 1; ++l) {
+        o->quota[l] = host_round_even(per);
+        sum += o->quota[l];
+        per *= f;
+    }
+    o->quota[nl - 1] = std::max(p.nfeatures - sum, 0);
+    const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) o->umax[v] = (int)std::nearbyint(std::sqrt(225.0 - v * v));
+    for (int v = 15, v0 = 0; v >= vmin; --v) {
+        while (o->umax[v0] == o->umax[v0 + 1]) ++v0;
+        o->umax[v] = v0;
+        ++v0;
+    }
+
+    Geom &g = o->g;
+    memset(&g, 0, sizeof(g));
+    g.nlevels = nl, g.W = o->W, g.H = o->H, g.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+    g.min_th = std::min(std::max(p.min_th_fast, 0), 255);
+    long long pyr_off = 0, cand_off = 0;
+    int out_off = 0, max_rw = 0, max_rh = 0, max_cells_lvl = 0, max_nodes = 0;
+    int prev_w = o->W, prev_h = o->H;
+    for (int l = 0; l < nl; ++l) {
+        LevelGeom &L = g.lv[l];
+        L.w = host_round_even((float)o->W * o->inv_scale[l]);
+        L.h = host_round_even((float)o->H * o->inv_scale[l]);
+        if (L.w > 4000 || L.h > 4000) return OMV_ERR_ARG;   // 12-bit packed coordinates
+        L.pitch = (L.w + 15) & ~15;
+        L.off = l == 0 ? 0 : pyr_off;
+        if (l > 0) pyr_off += (long long)L.pitch * L.h;
+        L.maxBX = L.w - kEdge + 3;
+        L.maxBY = L.h - kEdge + 3;
+        L.scale = o->scale[l];
+        L.size = (float)(int)(31 * o->scale[l]);
+        L.quota = o->quota[l];
+        // FAST cells (:718-742)
+        const float width = (float)(L.maxBX - kMinB), height = (float)(L.maxBY - kMinB);
+        const int nCols = (int)(width / 35.f), nRows = (int)(height / 35.f);
+        if (nCols < 1 || nRows < 1) return OMV_ERR_ARG;   // level too small: the reference divides by 0
+        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        L.cell_begin = (int)cells.size();
+        long long cap_lvl = 0;
+        for (int i = 0; i < nRows; ++i) {
+            const float iniY = (float)(kMinB + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= L.maxBY - 3) continue;
+            if (maxY > L.maxBY) maxY = (float)L.maxBY;
+            for (int j = 0; j < nCols; ++j) {
+                const float iniX = (float)(kMinB + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= L.maxBX - 6) continue;
+                if (maxX > L.maxBX) maxX = (float)L.maxBX;
+                Cell c{l, (int)iniY, (int)maxY, (int)iniX, (int)maxX};
+                cells.push_back(c);
+                max_rw = std::max(max_rw, c.x1 - c.x0);
+                max_rh = std::max(max_rh, c.y1 - c.y0);
+            }
+        }
+        L.cell_end = (int)cells.size();
+        max_cells_lvl = std::max(max_cells_lvl, L.cell_end - L.cell_begin);
+        // octree initial strips (:505-507)
+        const int Wn = L.maxBX - kMinB, Hn = L.maxBY - kMinB;
+        L.nIni = (int)std::round((float)Wn / Hn);
+        if (L.nIni < 1) return OMV_ERR_ARG;   // the reference divides by zero here
+        L.hX = (float)Wn / L.nIni;
+        L.out_cap = std::max(L.quota + 2, 4 * L.nIni);
+        L.out_off = out_off;
+        out_off += L.out_cap;
+        max_nodes = std::max(max_nodes, std::max(L.quota + 3, 4 * L.nIni + 4));
+        (void)cap_lvl;
+        // resize tables (cv::resize INTER_LINEAR, :1083)
+        if (l > 0) {
+            const int sw = prev_w, sh = prev_h, dw = L.w, dh = L.h;
+            L.xtab_off = (int)xt.size();
+            L.ytab_off = (int)yt.size();
+            const double sx_scale = 1.0 / ((double)dw / sw), sy_scale = 1.0 / ((double)dh / sh);
+            int xmax = dw;
+            std::vector<XTab> row(dw);
+            for (int dx = 0; dx < dw; ++dx) {
+                float fx = (float)((dx + 0.5) * sx_scale - 0.5);
+                int sx = (int)std::floor(fx);
+                fx -= sx;
+                if (sx < 0) fx = 0, sx = 0;
+                if (sx + 1 >= sw) {
+                    xmax = std::min(xmax, dx);
+                    if (sx >= sw - 1) fx = 0, sx = sw - 1;
+                }
+                int a0 = (short)host_round_even((1.f - fx) * 2048.f), a1 = (short)host_round_even(fx * 2048.f);
+                row[dx] = XTab{sx, std::min(sx + 1, sw - 1), (a0 & 0xffff) | (a1 << 16)};
+            }
+            for (int dx = xmax; dx < dw; ++dx) row[dx].coef = 2048, row[dx].sx1 = row[dx].sx0;
+            xt.insert(xt.end(), row.begin(), row.end());
+            for (int dy = 0; dy < dh; ++dy) {
+                float fy = (float)((dy + 0.5) * sy_scale - 0.5);
+                int sy = (int)std::floor(fy);
+                fy -= sy;
+                int b0 = (short)host_round_even((1.f - fy) * 2048.f), b1 = (short)host_round_even(fy * 2048.f);
+                const int r0 = std::min(std::max(sy, 0), sh - 1), r1 = std::min(std::max(sy + 1, 0), sh - 1);
+                yt.push_back(XTab{r0, r1, (b0 & 0xffff) | (b1 << 16)});
+            }
+        }
+        prev_w = L.w, prev_h = L.h;
+    }
+    g.n_cells = (int)cells.size();
+    const int dw = max_rw - 6, dh = max_rh - 6;
+    g.cell_cap = ((dw + 1) / 2) * ((dh + 1) / 2);
+    for (int l = 0; l < nl; ++l) {
+        LevelGeom &L = g.lv[l];
+        L.cand_off = cand_off;
+        L.cand_cap = (L.cell_end - L.cell_begin) * g.cell_cap;
+        cand_off += L.cand_cap;
+    }
+    g.pyr_bytes = (pyr_off + 255) & ~255LL;
+    g.cand_per_img = cand_off;
+    g.out_per_img = out_off;
+    g.n_max = out_off;
+    g.node_cap = std::max(max_nodes, max_cells_lvl);
+    g.node_cap = (g.node_cap + 15) & ~15;
+    o->rmax = max_rw * max_rh;
+    o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
+    return OMV_OK;
+}
+
+extern "C" {
+
+omv_status omv_orb_create(const omv_orb_params *params, int width, int height, int max_images, omv_orb **out) {
+    if (!params || !out || width <= 0 || height <= 0 || max_images <= 0) return OMV_ERR_ARG;
+    if (params->nlevels < 1 || params->nlevels > kMaxLevels || params->nfeatures <= 0) return OMV_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
+    omv_orb *o = new omv_orb();
+    o->p = *params;
+    o->W = width, o->H = height, o->max_images = max_images;
+    (void)hipGetDevice(&o->device);
+    std::vector<Cell> cells;
+    std::vector<XTab> xt, yt;
+    omv_status st = build_geometry(o, cells, xt, yt);
+    if (st != OMV_OK) {
+        delete o;
+        return st;
+    }
+    if (o->oct_lds > 160 * 1024) {
+        delete o;
+        return OMV_ERR_ARG;
+    }
+    const Geom &g = o->g;
+    const size_t n = (size_t)max_images;
+    HIP_OK(hipMalloc(&o->d_cells, sizeof(Cell) * cells.size()));
+    HIP_OK(hipMemcpy(o->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&o->d_xt, sizeof(XTab) * std::max<size_t>(1, xt.size())));
+    HIP_OK(hipMalloc(&o->d_yt, sizeof(XTab) * std::max<size_t>(1, yt.size())));
+    if (!xt.empty()) HIP_OK(hipMemcpy(o->d_xt, xt.data(), sizeof(XTab) * xt.size(), hipMemcpyHostToDevice));
+    if (!yt.empty()) HIP_OK(hipMemcpy(o->d_yt, yt.data(), sizeof(XTab) * yt.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&o->d_pyr, std::max<size_t>(256, (size_t)g.pyr_bytes * n)));
+    HIP_OK(hipMalloc(&o->d_cell_cnt, sizeof(int) * g.n_cells * n));
+    HIP_OK(hipMalloc(&o->d_cell_kp, sizeof(uint32_t) * (size_t)g.n_cells * g.cell_cap * n));
+    HIP_OK(hipMalloc(&o->d_cand, sizeof(uint32_t) * (size_t)g.cand_per_img * n));
+    HIP_OK(hipMalloc(&o->d_nid, sizeof(uint32_t) * (size_t)g.cand_per_img * n));
+    HIP_OK(hipMalloc(&o->d_lvl_out, sizeof(uint32_t) * (size_t)g.out_per_img * n));
+    HIP_OK(hipMalloc(&o->d_lvl_cls, sizeof(uint32_t) * (size_t)g.out_per_img * n));
+    HIP_OK(hipMalloc(&o->d_lvl_cnt, sizeof(int) * 3 * g.nlevels * n));
+    HIP_OK(hipMalloc(&o->d_lap, sizeof(int) * 2 * n));
+    HIP_OK(hipMalloc(&o->d_err, sizeof(int)));
+    HIP_OK(hipMemset(o->d_err, 0, sizeof(int)));
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), o->umax, sizeof(o->umax)));
+    *out = o;
+    return OMV_OK;
+}
+
+omv_status omv_orb_destroy(omv_orb *o) {
+    if (!o) return OMV_ERR_ARG;
+    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+                    o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
+                    o->d_desc1, o->d_n1};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete o;
+    return OMV_OK;
+}
+
+int omv_orb_max_keypoints(const omv_orb *o) { return o ? o->g.n_max : 0; }
+
+omv_status omv_orb_scale_tables(const omv_orb *o, float *scale, float *inv_scale, float *sigma2, float *inv_sigma2) {
+    if (!o) return OMV_ERR_ARG;
+    for (int l = 0; l < o->p.nlevels; ++l) {
+        if (scale) scale[l] = o->scale[l];
+        if (inv_scale) inv_scale[l] = o->inv_scale[l];
+        if (sigma2) sigma2[l] = o->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = o->inv_sigma2[l];
+    }
+    return OMV_OK;
+}
+
+omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_t image_stride, size_t pitch,
+                                 const int *lapping, omv_kp *kps, uint8_t *desc, int *n_out, int *mono_index,
+                                 void *stream) {
+    if (!o || n <= 0 || n > o->max_images || !images || !lapping || !kps || !desc || !n_out || !mono_index)
+        return OMV_ERR_ARG;
+    if (pitch < (size_t)o->W || image_stride < pitch * o->H) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    o->last_stream = st;
+    const Geom &g = o->g;
+    HIP_OK(hipMemcpyAsync(o->d_lap, lapping, sizeof(int) * 2 * n, hipMemcpyHostToDevice, st));
+    // K1: pyramid, level by level
+    for (int l = 1; l < g.nlevels; ++l) {
+        const long long tot = (long long)g.lv[l].w * g.lv[l].h * n;
+        const int blocks = (int)((tot + 255) / 256);
+        pyr_resize_kernel<<<blocks, 256, 0, st>>>(g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, n);
+    }
+    // K2: FAST per cell
+    fast_cells_kernel<<<g.n_cells * n, 64, 2 * o->rmax, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
+                                                               o->d_cell_cnt, o->d_cell_kp, o->rmax);
+    // K3: octree per (image, level)
+    OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
+    octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
+    // K4: orientation + descriptors, one wave per output slot
+    DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
+    const int waves = g.out_per_img * n;
+    describe_kernel<<<(waves + 3) / 4, 256, 0, st>>>(g, da);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_orb_last_error(omv_orb *o) {
+    if (!o) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(o->last_stream));
+    int e = 0;
+    HIP_OK(hipMemcpy(&e, o->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(o->d_err, 0, sizeof(int)));
+    return e;
+}
+
+omv_status omv_orb_extract_host(omv_orb *o, const uint8_t *image, size_t pitch, int lap0, int lap1, omv_kp *kps,
+                                uint8_t *desc, int *n_out, int *mono_index) {
+    if (!o || !image || !kps || !desc || !n_out || !mono_index) return OMV_ERR_ARG;
+    const size_t dp = (size_t)o->W;
+    if (!o->d_img1) {
+        HIP_OK(hipMalloc(&o->d_img1, dp * o->H));
+        HIP_OK(hipMalloc(&o->d_kp1, sizeof(omv_kp) * o->g.n_max));
+        HIP_OK(hipMalloc(&o->d_desc1, 32 * (size_t)o->g.n_max));
+        HIP_OK(hipMalloc(&o->d_n1, 2 * sizeof(int)));
+    }
+    HIP_OK(hipMemcpy2D(o->d_img1, dp, image, pitch, o->W, o->H, hipMemcpyHostToDevice));
+    int lap[2] = {lap0, lap1};
+    omv_status s = omv_orb_extract_batch(o, 1, o->d_img1, dp * o->H, dp, lap, o->d_kp1, o->d_desc1, o->d_n1,
+                                         o->d_n1 + 1, nullptr);
+    if (s != OMV_OK) return s;
+    s = omv_orb_last_error(o);
+    if (s != OMV_OK) return s;
+    int hn[2];
+    HIP_OK(hipMemcpy(hn, o->d_n1, sizeof(hn), hipMemcpyDeviceToHost));
+    *n_out = hn[0];
+    *mono_index = hn[1];
+    HIP_OK(hipMemcpy(kps, o->d_kp1, sizeof(omv_kp) * hn[0], hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(desc, o->d_desc1, 32 * (size_t)hn[0], hipMemcpyDeviceToHost));
+    return OMV_OK;
+}
+
+omv_status omv_orb_debug_level(omv_orb *o, int img, int level, uint8_t *out, int *w, int *h) {
+    if (!o || level < 1 || level >= o->p.nlevels || img < 0 || img >= o->max_images) return OMV_ERR_ARG;
+    const LevelGeom &L = o->g.lv[level];
+    *w = L.w, *h = L.h;
+    if (!out) return OMV_OK;
+    HIP_OK(hipStreamSynchronize(o->last_stream));
+    HIP_OK(hipMemcpy2D(out, L.w, o->d_pyr + (size_t)img * o->g.pyr_bytes + L.off, L.pitch, L.w, L.h,
+                       hipMemcpyDeviceToHost));
+    return OMV_OK;
+}
+
+}  // extern "C"
