@@ -79,66 +79,92 @@ omv_status omv_orb_extract_host(omv_orb *orb, const uint8_t *image, size_t pitch
 /* Device-side error word of the last batch (OMV_ERR_CAPACITY if a bound was hit); syncs the stream. */
 omv_status omv_orb_last_error(omv_orb *orb);
 
+/* Per-stage device time (HIP events on the launch stream) for measurement: stages are
+ * 0 pyramid, 1 FAST cells, 2 octree, 3 orientation+descriptor.  omv_orb_stage_ms syncs, returns the
+ * accumulated milliseconds since the last reset and the number of timed batches. */
+omv_status omv_orb_enable_timing(omv_orb *orb, int on);
+omv_status omv_orb_stage_ms(omv_orb *orb, double *ms4, long long *calls, int reset);
+
 /* Debug/parity hooks: copy pyramid level `level` of image `img` of the last batch to host. */
 omv_status omv_orb_debug_level(omv_orb *orb, int img, int level, uint8_t *out, int *w, int *h);
 
 /* ------------------------------------------------------------------------------------------------
- * Hamming matching
+ * Hamming matching on multi-camera frames
+ *
+ * Frame layout (device): keypoints/descriptors padded per camera block, kps [frame][cam][kp_cap],
+ * desc [frame][cam][kp_cap][32], n_kp [frame][cam] (the extractor's batched output as-is).  Block 0
+ * is the left camera, block 1 the right camera, blocks >= 2 side cameras — the reference's
+ * [L|R|SL|SR] concatenation (src/Frame.cc:1936-1939) generalised to n_cams.  A keypoint "slot" is
+ * cam * kp_cap + i; per-slot arrays (kp_to_mp, occupancy) are [frame][n_cams * kp_cap].
  * ---------------------------------------------------------------------------------------------- */
-
-/* cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) as used by Frame::ComputeMultiFishEyeMatches
- * (src/Frame.cc:1483): for each query row the two nearest train rows (first index wins ties).
- * Batched over n_pairs independent (query, train) sets laid out [pair][rows][32].
- *   idx2/dist2 device [n_pairs][q_cap][2]; -1 / INT32_MAX when fewer than 1 / 2 train rows. */
-omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *nq, const uint8_t *train,
-                       int t_cap, const int *nt, int32_t *idx2, int32_t *dist2, void *stream);
-
-/* Camera-block view of one multi-camera Frame (the reference's Frame after the multi ctor,
- * src/Frame.cc:1767-1949): keypoints and descriptors concatenated [cam0|cam1|...] with per-camera
- * offsets, and per-camera 64x48 grids (AssignFeaturesToGrid, src/Frame.cc:541-582). */
 typedef struct omv_frame_geom {
-    int n_cams;          /* camera blocks: 0 = left, 1 = right, >=2 side cameras                */
-    float min_x, max_x;  /* Frame::mnMinX/mnMaxX (bounds of imLeft, shared by all cameras)       */
+    int n_cams;
+    float min_x, max_x;  /* Frame::mnMinX/mnMaxX (bounds of imLeft, shared by all cameras, Frame.cc:1875) */
     float min_y, max_y;
     int nlevels;
-    float scale_factors[16]; /* Frame::mvScaleFactors                                            */
+    float scale_factors[16]; /* Frame::mvScaleFactors                                              */
 } omv_frame_geom;
 
-/* Build the per-camera grids on device.  kps/desc are [frame][n_cams][kp_cap]; n_kp [frame][cam].
- * grid_start/grid_idx are device outputs sized by omv_grid_sizes(). */
-void omv_grid_sizes(int n_frames, int n_cams, int kp_cap, size_t *start_ints, size_t *idx_ints);
-omv_status omv_grid_build(int n_frames, const omv_frame_geom *geom, const omv_kp *kps, int kp_cap,
-                          const int *n_kp, int32_t *grid_start, int32_t *grid_idx, void *stream);
-
-/* Local map points projected into a frame (the fields SearchByProjection reads from MapPoint after
- * Frame::isInFrustum, src/ORBmatcher.cc:33-60; src/Frame.cc:736-826).  SoA, [frame][M] per field
- * except the per-camera arrays which are [frame][M][n_cams]. */
+/* Local map points projected into a frame (the MapPoint fields SearchByProjection reads after
+ * Frame::isInFrustum, src/ORBmatcher.cc:33-60).  Device SoA: per-point arrays are [frame][M],
+ * per-camera arrays [frame][M][n_cams]. */
 typedef struct omv_mp_view {
-    const uint8_t *desc;      /* [M][32] MapPoint::GetDescriptor()                                */
-    const float *proj_x;      /* [M][n_cams] mTrackProjX / XR / XSL / XSR ...                     */
-    const float *proj_y;      /* [M][n_cams]                                                      */
-    const float *view_cos;    /* [M][n_cams] mTrackViewCos*                                       */
-    const int32_t *level;     /* [M][n_cams] mnTrackScaleLevel* (-1 = none)                       */
-    const uint8_t *in_view;   /* [M][n_cams] mbTrackInView*                                       */
-    const float *track_depth; /* [M] mTrackDepth                                                  */
-    const uint8_t *is_bad;    /* [M] MapPoint::isBad()                                            */
-    const uint8_t *has_obs;   /* [M] Observations() > 0                                           */
+    const uint8_t *desc;      /* [M][32] MapPoint::GetDescriptor()                                  */
+    const float *proj_x;      /* [M][n_cams] mTrackProjX / XR / XSL / XSR ...                       */
+    const float *proj_y;      /* [M][n_cams]                                                        */
+    const float *view_cos;    /* [M][n_cams] mTrackViewCos*                                         */
+    const int32_t *level;     /* [M][n_cams] mnTrackScaleLevel* (-1 = none)                         */
+    const uint8_t *in_view;   /* [M][n_cams] mbTrackInView*                                         */
+    const float *track_depth; /* [M] mTrackDepth                                                    */
+    const uint8_t *is_bad;    /* [M] MapPoint::isBad()                                              */
+    const uint8_t *has_obs;   /* [M] Observations() > 0                                             */
 } omv_mp_view;
 
+typedef struct omv_matcher omv_matcher;
+
+/* Workspace for up to max_frames frames of n_cams blocks x kp_cap keypoints and max_mps points. */
+omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out);
+omv_status omv_matcher_destroy(omv_matcher *m);
+
+/* Frame::AssignFeaturesToGrid (src/Frame.cc:541-582) for n_frames frames: per camera a 64x48 grid
+ * (cell = ix*48 + iy) of ascending keypoint indices, kept in the handle for the searches below. */
+omv_status omv_matcher_assign_grid(omv_matcher *m, int n_frames, const omv_frame_geom *geom, const omv_kp *kps,
+                                   const int *n_kp, void *stream);
+/* Copy one camera's grid to host: cell_start [64*48+1], idx [kp_cap]. Syncs. */
+omv_status omv_matcher_grid_debug(omv_matcher *m, int frame, int cam, int32_t *cell_start, int32_t *idx);
+
 /* ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
- * (src/ORBmatcher.cc:23-340), batched over n_frames independent frames.
- *   kp_to_mp      device [frame][N_total] in/out: MapPoint index per keypoint (-1 = none), i.e.
- *                 F.mvpMapPoints as dense indices; entries >= 0 on entry whose point has
- *                 observations block the keypoint (the `Observations() > 0` test, :77-79) —
- *                 pass kp_occ_init for points outside this call's list.
- *   l2r / r2l     device [frame][N_cam0] / [frame][N_cam1] mvLeftToRightMatch/mvRightToLeftMatch
- *   n_matches     device [frame] return value.
- * Semantics are the reference's sequential ones (earlier map points claim keypoints first). */
-omv_status omv_match_project(int n_frames, const omv_frame_geom *geom, const omv_kp *kps, const uint8_t *desc,
-                             int kp_cap, const int *n_kp, const int32_t *grid_start, const int32_t *grid_idx,
-                             const omv_mp_view *mps, int M, float th, int far_points, float th_far,
-                             float nnratio, const int32_t *l2r, const int32_t *r2l, const uint8_t *kp_occ_init,
-                             int32_t *kp_to_mp, int *n_matches, void *stream);
+ * (src/ORBmatcher.cc:23-340) on n_frames frames with the grid of the last assign_grid call.
+ *   l2r / r2l     [frame][kp_cap] mvLeftToRightMatch / mvRightToLeftMatch (block-local indices, -1 none)
+ *   kp_occ_init   [frame][slots] 1 where F.mvpMapPoints[slot] is already a point with observations
+ *                 (may be NULL = none)
+ *   kp_to_mp      [frame][slots] in/out: map point index assigned to each keypoint (F.mvpMapPoints)
+ *   n_matches     [frame] the return value
+ * Exactly the reference's sequential semantics: earlier points claim keypoints first, a failed
+ * ratio test skips the point's remaining cameras, th scales only the left-camera window. */
+omv_status omv_matcher_search_projection(omv_matcher *m, int n_frames, const omv_frame_geom *geom, const omv_kp *kps,
+                                         const uint8_t *desc, const int *n_kp, const omv_mp_view *mps, int M, float th,
+                                         int far_points, float th_far, float nnratio, const int32_t *l2r,
+                                         const int32_t *r2l, const uint8_t *kp_occ_init, int32_t *kp_to_mp,
+                                         int *n_matches, void *stream);
+
+/* Lapping-area stereo candidates of Frame::ComputeMultiFishEyeMatches (src/Frame.cc:1461-1491):
+ * knnMatch(k=2) of camera-0 rows [mono0, n0) against camera-1 rows [mono1, n1), Lowe ratio
+ * d0 < ratio * d1.  Writes l2r/r2l [frame][kp_cap] (later left index wins a shared right keypoint).
+ * The KannalaBrandt8::TriangulateMatches depth check that follows in the reference is not applied. */
+omv_status omv_matcher_stereo_lapping(omv_matcher *m, int n_frames, const uint8_t *desc, const int *n_kp,
+                                      const int *mono, double ratio, int32_t *l2r, int32_t *r2l, void *stream);
+
+/* Per-stage device time: 0 grid, 1 lapping knn, 2 projection candidates, 3 claim resolution. */
+omv_status omv_matcher_enable_timing(omv_matcher *m, int on);
+omv_status omv_matcher_stage_ms(omv_matcher *m, double *ms4, int reset);
+
+/* cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) (src/Frame.cc:1483) over n_pairs independent sets:
+ * query [pair][q_cap][32] with nq[pair] rows, train [pair][t_cap][32] with nt[pair] rows.
+ * idx2/dist2 [pair][q_cap][2]: two nearest train rows, first index wins ties; -1 / INT32_MAX when
+ * fewer than 1 / 2 train rows exist. */
+omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *nq, const uint8_t *train, int t_cap,
+                       const int *nt, int32_t *idx2, int32_t *dist2, void *stream);
 
 #ifdef __cplusplus
 }

@@ -67,12 +67,20 @@ SIGNATURES = {
     "omv_orb_extract_batch": (_I, [_VP, _I, _VP, _SZ, _SZ, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_orb_extract_host": (_I, [_VP, _VP, _SZ, _I, _I, _VP, _VP, _VP, _VP]),
     "omv_orb_last_error": (_I, [_VP]),
+    "omv_orb_enable_timing": (_I, [_VP, _I]),
+    "omv_orb_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(ctypes.c_longlong), _I]),
     "omv_orb_debug_level": (_I, [_VP, _I, _I, _VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "omv_matcher_create": (_I, [_I, _I, _I, _I, ctypes.POINTER(_VP)]),
+    "omv_matcher_destroy": (_I, [_VP]),
+    "omv_matcher_assign_grid": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP]),
+    "omv_matcher_grid_debug": (_I, [_VP, _I, _I, _VP, _VP]),
+    "omv_matcher_enable_timing": (_I, [_VP, _I]),
+    "omv_matcher_stage_ms": (_I, [_VP, _VP, _I]),
+    "omv_matcher_search_projection": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP,
+                                           ctypes.POINTER(MpView), _I, _F, _I, _F, _F, _VP, _VP, _VP, _VP,
+                                           _VP, _VP]),
+    "omv_matcher_stereo_lapping": (_I, [_VP, _I, _VP, _VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
     "omv_bf_knn2": (_I, [_I, _VP, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP]),
-    "omv_grid_sizes": (None, [_I, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
-    "omv_grid_build": (_I, [_I, ctypes.POINTER(FrameGeom), _VP, _I, _VP, _VP, _VP, _VP]),
-    "omv_match_project": (_I, [_I, ctypes.POINTER(FrameGeom), _VP, _VP, _I, _VP, _VP, _VP,
-                               ctypes.POINTER(MpView), _I, _F, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP]),
 }
 
 _lib = None
@@ -87,6 +95,12 @@ def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise OmvError(f"{path} not built: run `python -m openmavis_amd.build` (hipcc, gfx950). "
                        "There is no CPU fallback.")
+    # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Import it first so this
+    # library binds to the runtime torch uses: one HIP runtime per process, shared device pointers.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover
+        pass
     lib = ctypes.CDLL(path)
     missing.clear()
     for name, (res, args) in SIGNATURES.items():

@@ -1,0 +1,664 @@
+// MI355X-native Hamming matchers for the multi-camera frame.
+//
+//   grid_kernel      Frame::AssignFeaturesToGrid / PosInGrid (src/Frame.cc:541-582, :969-978):
+//                    one wavefront per (frame, camera) builds a 64x48 CSR grid with a counting sort
+//                    that keeps ascending keypoint order inside each cell (the reference push_backs
+//                    in index order, and GetFeaturesInArea's output order depends on it).
+//   cand_kernel      ORBmatcher::SearchByProjection (src/ORBmatcher.cc:23-340), speculative part:
+//                    one thread per (frame, map point, camera block) walks the GetFeaturesInArea
+//                    window (src/Frame.cc:890-967) and keeps the 4 best candidates by
+//                    (Hamming distance, window order) — best/second-best are exactly the first two
+//                    of that order, so claims made by earlier map points only need the next ones.
+//   resolve_kernel   the order-dependent part: one wavefront per frame takes map points 64 at a
+//                    time, each lane evaluates its point against the claims committed so far, and
+//                    the wave commits the longest prefix of lanes whose best/second candidates were
+//                    not claimed by an earlier lane of the same batch; the first conflicting lane is
+//                    re-evaluated.  Results are identical to the reference's sequential loop
+//                    (a keypoint taken by an earlier point with Observations() > 0 is skipped).
+//   knn2_kernel      cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) (src/Frame.cc:1483): train tiles in
+//                    LDS, one query per lane, 4 x popcount64 per pair, first index wins ties.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "../../include/omv.h"
+#include "omv_device.h"
+
+namespace {
+
+constexpr int kGridCols = 64, kGridRows = 48, kCells = kGridCols * kGridRows;
+constexpr int kTH_HIGH = 100;
+constexpr int kTop = 4;
+constexpr int kMaxCams = 8;
+
+#define HIP_OK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "omv: %s failed: %s\n", #x, hipGetErrorString(e_));      \
+            return OMV_ERR_HIP;                                                      \
+        }                                                                            \
+    } while (0)
+
+struct FrameArgs {
+    int n_cams, kp_cap, nlevels;
+    float min_x, max_x, min_y, max_y, invW, invH;
+    float scale[16];
+    const omv_kp *kps;        // [frame][cam][kp_cap]
+    const uint8_t *desc;      // [frame][cam][kp_cap][32]
+    const int *n_kp;          // [frame][cam]
+    const int32_t *cell_start;   // [frame][cam][kCells + 1]
+    const int32_t *cell_idx;     // [frame][cam][kp_cap]
+};
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) grid_kernel(FrameArgs f, int32_t *cell_start, int32_t *cell_idx) {
+    __shared__ int cnt[kCells];
+    const int fc = blockIdx.x;   // frame * n_cams + cam
+    const int lane = threadIdx.x;
+    const int n = f.n_kp[fc];
+    const omv_kp *kp = f.kps + (size_t)fc * f.kp_cap;
+    for (int c = lane; c < kCells; c += 64) cnt[c] = 0;
+    __syncthreads();
+    auto cell_of = [&](int i) {
+        const int px = (int)roundf((kp[i].x - f.min_x) * f.invW);
+        const int py = (int)roundf((kp[i].y - f.min_y) * f.invH);
+        if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
+        return px * kGridRows + py;   // mGrid[ix][iy]
+    };
+    for (int i = lane; i < n; i += 64) {
+        const int c = cell_of(i);
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+    }
+    __syncthreads();
+    // exclusive scan of 3072 counts: 48 per lane
+    constexpr int per = kCells / 64;
+    int s = 0;
+    for (int k = 0; k < per; ++k) s += cnt[lane * per + k];
+    int incl = s;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+    }
+    int run = incl - s;
+    __syncthreads();
+    int32_t *cs = cell_start + (size_t)fc * (kCells + 1);
+    for (int k = 0; k < per; ++k) {
+        const int c = lane * per + k;
+        const int v = cnt[c];
+        cnt[c] = run;
+        cs[c] = run;
+        run += v;
+    }
+    if (lane == 63) cs[kCells] = run;
+    __syncthreads();
+    // order-preserving scatter, 64 keypoints at a time
+    int32_t *out = cell_idx + (size_t)fc * f.kp_cap;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        const int c = i < n ? cell_of(i) : -1;
+        int before = 0, after = 0;
+        for (int j = 0; j < 64; ++j) {
+            const int cj = __shfl(c, j, 64);
+            if (cj == c) {
+                before += j < lane;
+                after += j > lane;
+            }
+        }
+        int pos = 0;
+        if (c >= 0) {
+            pos = cnt[c] + before;
+            out[pos] = i;
+        }
+        __syncthreads();
+        if (c >= 0 && after == 0) cnt[c] = pos + 1;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct MpArgs {
+    const uint8_t *desc;
+    const float *proj_x, *proj_y, *view_cos;
+    const int32_t *level;
+    const uint8_t *in_view;
+    const float *track_depth;
+    const uint8_t *is_bad, *has_obs;
+    int M;
+};
+
+struct Rec {
+    int idx[kTop];
+    int16_t dist[kTop];
+    int8_t oct[kTop];
+    int count;   // candidates in the window that were not blocked when the record was built
+};
+
+struct Top {
+    int idx[kTop], dist[kTop], oct[kTop];
+    int n, count;
+};
+
+__device__ __forceinline__ void load_desc(const uint8_t *p, uint64_t d[4]) {
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
+    d[0] = q[0], d[1] = q[1], d[2] = q[2], d[3] = q[3];
+}
+
+// Window of GetFeaturesInArea(x, y, r, level-1, level, cam), in the reference's iteration order;
+// keeps the kTop best unblocked candidates by (dist, order).
+template <class Blocked>
+__device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, float y, float r, int minL, int maxL,
+                            const uint64_t dmp[4], Blocked blocked, Top &t) {
+    t.n = 0, t.count = 0;
+    const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (nMaxCellY < 0) return;
+    const bool checkLevels = (minL > 0) || (maxL >= 0);
+    const size_t fc = (size_t)frame * f.n_cams + cam;
+    const int32_t *cs = f.cell_start + fc * (kCells + 1);
+    const int32_t *ci = f.cell_idx + fc * f.kp_cap;
+    const omv_kp *kp = f.kps + fc * f.kp_cap;
+    const uint8_t *dd = f.desc + fc * f.kp_cap * 32;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int c0 = ix * kGridRows + nMinCellY, c1 = ix * kGridRows + nMaxCellY;
+        const int e = cs[c1 + 1];
+        for (int p = cs[c0]; p < e; ++p) {   // cells iy = min..max of column ix are contiguous
+            const int i = ci[p];
+            const omv_kp k = kp[i];
+            if (checkLevels) {
+                if (k.octave < minL) continue;
+                if (maxL >= 0 && k.octave > maxL) continue;
+            }
+            if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+            if (blocked(cam * f.kp_cap + i)) continue;
+            ++t.count;
+            uint64_t d[4];
+            load_desc(dd + (size_t)i * 32, d);
+            const int dist = omv::hamming256(dmp, d);
+            // insert after every entry with dist <= this one (window order breaks ties)
+            int pos = t.n;
+            while (pos > 0 && dist < t.dist[pos - 1]) --pos;
+            if (pos >= kTop) continue;
+            for (int q = min(t.n, kTop - 1); q > pos; --q) t.idx[q] = t.idx[q - 1], t.dist[q] = t.dist[q - 1], t.oct[q] = t.oct[q - 1];
+            t.idx[pos] = i, t.dist[pos] = dist, t.oct[pos] = k.octave;
+            if (t.n < kTop) ++t.n;
+        }
+    }
+}
+
+__device__ __forceinline__ bool mp_skipped(const MpArgs &m, int frame, int i, int C, int far_points, float th_far) {
+    const size_t b = (size_t)frame * m.M + i;
+    bool any = false;
+    for (int c = 0; c < C; ++c) any = any || m.in_view[b * C + c];
+    if (!any) return true;
+    if (far_points && m.track_depth[b] > th_far) return true;
+    return m.is_bad[b] != 0;
+}
+
+__device__ __forceinline__ float window_radius(const FrameArgs &f, const MpArgs &m, size_t bc, int c, float th,
+                                               bool bFactor) {
+    float r = m.view_cos[bc] > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (:342-347)
+    if (c == 0 && bFactor) r *= th;                   // th scales the left block only (:51-52)
+    return r * f.scale[m.level[bc]];
+}
+
+// One thread per (frame, map point, camera).
+__global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
+                                                   const uint8_t *occ_init, Rec *recs) {
+    const int C = f.n_cams;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long long)n_frames * m.M * C) return;
+    const int c = (int)(gid % C);
+    const long long fm = gid / C;
+    const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
+    const size_t bc = (size_t)fm * C + c;
+    Rec &out = recs[bc];
+    Top t;
+    t.n = 0, t.count = 0;
+    const int lvl = m.level[bc];
+    if (m.in_view[bc] && lvl >= 0 && lvl < f.nlevels) {
+        uint64_t dmp[4];
+        load_desc(m.desc + (size_t)fm * 32, dmp);
+        const float r = window_radius(f, m, bc, c, th, th != 1.0f);
+        const uint8_t *occ = occ_init ? occ_init + (size_t)frame * C * f.kp_cap : nullptr;
+        scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, lvl - 1, lvl, dmp,
+                    [&](int slot) { return occ && occ[slot]; }, t);
+    }
+    for (int q = 0; q < kTop; ++q) {
+        out.idx[q] = q < t.n ? t.idx[q] : -1;
+        out.dist[q] = q < t.n ? t.dist[q] : 256;
+        out.oct[q] = q < t.n ? t.oct[q] : -1;
+    }
+    out.count = t.count;
+}
+
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxClaims = 2 * kMaxCams;
+
+struct Eval {
+    int nclaim;
+    int claim[kMaxClaims];
+    int nrel;
+    int rel[kMaxClaims];   // slots whose blocked status decided the result (best / second)
+    int nmatch;
+    bool fallback;         // needed a full window rescan
+    bool unblock;          // overwrote a blocked slot while having no observations
+};
+
+struct ResolveArgs {
+    FrameArgs f;
+    MpArgs m;
+    const Rec *recs;
+    const int32_t *l2r, *r2l;
+    const uint8_t *occ_init;
+    int32_t *kp_to_mp;
+    int *n_matches;
+    float th, th_far, nnratio;
+    int far_points;
+};
+
+__device__ void evaluate(const ResolveArgs &a, int frame, int i, const uint32_t *bits, bool force_rescan, Eval &e) {
+    const FrameArgs &f = a.f;
+    const MpArgs &m = a.m;
+    const int C = f.n_cams, cap = f.kp_cap;
+    e.nclaim = e.nrel = e.nmatch = 0;
+    e.fallback = e.unblock = false;
+    if (mp_skipped(m, frame, i, C, a.far_points, a.th_far)) return;
+    const size_t fm = (size_t)frame * m.M + i;
+    const bool obs = m.has_obs[fm] != 0;
+    auto is_blocked = [&](int slot) {
+        if ((bits[slot >> 5] >> (slot & 31)) & 1u) {
+            // an own earlier claim of a point without observations unblocks it
+            for (int q = 0; q < e.nclaim; ++q)
+                if (e.claim[q] == slot) return obs;
+            return true;
+        }
+        if (obs)
+            for (int q = 0; q < e.nclaim; ++q)
+                if (e.claim[q] == slot) return true;
+        return false;
+    };
+    auto add_claim = [&](int slot) {
+        if (!obs && ((bits[slot >> 5] >> (slot & 31)) & 1u)) e.unblock = true;
+        e.claim[e.nclaim++] = slot;
+    };
+    const int32_t *l2r = a.l2r + (size_t)frame * cap;
+    const int32_t *r2l = a.r2l + (size_t)frame * cap;
+    uint64_t dmp[4];
+    bool have_desc = false;
+    for (int c = 0; c < C; ++c) {
+        const size_t bc = fm * C + c;
+        if (!m.in_view[bc]) continue;
+        const int lvl = m.level[bc];
+        if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
+        const Rec &r = a.recs[bc];
+        if (r.count == 0 && !force_rescan) continue;   // vIndices empty or all initially blocked
+        int b1 = -1, b2 = -1, d1 = 256, d2 = 256, o1 = -1, o2 = -1;
+        bool need_rescan = force_rescan;
+        if (!need_rescan) {
+            const int avail = min(r.count, kTop);
+            int k = 0;
+            for (; k < avail && b2 < 0; ++k) {
+                const int slot = c * cap + r.idx[k];
+                if (is_blocked(slot)) continue;
+                if (b1 < 0) b1 = r.idx[k], d1 = r.dist[k], o1 = r.oct[k];
+                else b2 = r.idx[k], d2 = r.dist[k], o2 = r.oct[k];
+            }
+            if (b2 < 0 && r.count > kTop) need_rescan = true;
+        }
+        if (need_rescan) {
+            e.fallback = true;
+            if (!have_desc) load_desc(m.desc + fm * 32, dmp), have_desc = true;
+            Top t;
+            scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f),
+                        lvl - 1, lvl, dmp, is_blocked, t);
+            b1 = b2 = -1, d1 = d2 = 256, o1 = o2 = -1;
+            if (t.n > 0) b1 = t.idx[0], d1 = t.dist[0], o1 = t.oct[0];
+            if (t.n > 1) b2 = t.idx[1], d2 = t.dist[1], o2 = t.oct[1];
+        }
+        if (b1 >= 0) e.rel[e.nrel++] = c * cap + b1;
+        if (b2 >= 0) e.rel[e.nrel++] = c * cap + b2;
+        if (d1 <= kTH_HIGH) {
+            if (o1 == o2 && (float)d1 > a.nnratio * d2) return;   // `continue` to the next map point
+            if (c == 0) {
+                add_claim(b1);
+                if (C > 1 && l2r[b1] != -1) add_claim(cap + l2r[b1]), e.nmatch++;
+                e.nmatch++;
+            } else if (c == 1) {
+                if (r2l[b1] != -1) add_claim(r2l[b1]), e.nmatch++;
+                add_claim(cap + b1);
+                e.nmatch++;
+            } else {
+                add_claim(c * cap + b1);
+                e.nmatch++;
+            }
+        }
+    }
+}
+
+// One wavefront (one 64-thread workgroup) per frame.
+__global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    const int frame = blockIdx.x, lane = threadIdx.x;
+    const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap;
+    const int nwords = (S + 31) >> 5;
+    uint32_t *bits = rsm;
+    int *owner = reinterpret_cast<int *>(rsm + nwords);
+    const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
+    for (int w = lane; w < nwords; w += 64) {
+        uint32_t v = 0;
+        for (int b = 0; b < 32; ++b) {
+            const int s = w * 32 + b;
+            if (s < S && occ && occ[s]) v |= 1u << b;
+        }
+        bits[w] = v;
+    }
+    for (int s = lane; s < S; s += 64) owner[s] = 64;
+    __syncthreads();
+    int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
+    int total = 0;
+    bool dirty = false;   // a claim unblocked a keypoint: records may miss candidates from now on
+    const int M = a.m.M;
+    for (int base = 0; base < M; base += 64) {
+        const int i = base + lane;
+        int start = 0;
+        const int nb = min(64, M - base);
+        while (start < nb) {
+            const bool active = lane >= start && lane < nb;
+            Eval e;
+            if (active) evaluate(a, frame, i, bits, dirty, e);
+            else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
+            const bool obs = active && a.m.has_obs[(size_t)frame * M + i];
+            if (obs)
+                for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], lane);
+            __syncthreads();
+            bool conflict = false;
+            if (active && lane > start) {
+                conflict = e.fallback;
+                for (int q = 0; q < e.nrel && !conflict; ++q) conflict = owner[e.rel[q]] < lane;
+            }
+            __syncthreads();
+            if (obs)
+                for (int q = 0; q < e.nclaim; ++q) owner[e.claim[q]] = 64;
+            uint64_t cm = __ballot(conflict);
+            const uint64_t um = __ballot(active && e.unblock);
+            if (um) {
+                const int u = __ffsll((long long)um) - 1;
+                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));   // everything after the unblocking lane
+            }
+            const int j0 = cm ? min(nb, __ffsll((long long)cm) - 1) : nb;
+            __syncthreads();
+            // commit lanes [start, j0) in map-point order
+            for (int q = start; q < j0; ++q) {
+                if (lane == q) {
+                    for (int t = 0; t < e.nclaim; ++t) {
+                        const int s = e.claim[t];
+                        k2m[s] = i;
+                        if (obs) atomicOr(&bits[s >> 5], 1u << (s & 31));
+                        else atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
+                    }
+                }
+                __syncthreads();
+            }
+            const bool committed = lane >= start && lane < j0;
+            int nm = committed ? e.nmatch : 0;
+            for (int d = 32; d >= 1; d >>= 1) nm += __shfl_xor(nm, d, 64);
+            total += nm;
+            if (__ballot(committed && e.unblock)) dirty = true;
+            start = j0;
+        }
+    }
+    if (lane == 0) a.n_matches[frame] = total;
+}
+
+// ---------------------------------------------------------------------------------------------
+// knnMatch(k=2): block = 256 queries of one (query set, train set) pair.
+struct KnnArgs {
+    const uint8_t *q, *t;
+    long long q_stride, t_stride;   // bytes between pairs
+    const int *nq, *nt;             // per pair
+    const int *q_off, *t_off;       // per pair row offset (may be null)
+    int pair_stride_off;            // stride of q_off/t_off arrays
+    int32_t *idx2, *dist2;          // [pair][out_cap][2]
+    int out_cap;
+};
+
+__global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
+    __shared__ __attribute__((aligned(16))) uint64_t tile[256][4];
+    const int pair = blockIdx.y;
+    const int qo = a.q_off ? a.q_off[pair * a.pair_stride_off] : 0;
+    const int to = a.t_off ? a.t_off[pair * a.pair_stride_off] : 0;
+    const int nq = a.nq[pair * a.pair_stride_off] - qo;
+    const int nt = a.nt[pair * a.pair_stride_off] - to;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= max(nq, 0)) return;   // block-uniform
+    uint64_t dq[4] = {0, 0, 0, 0};
+    if (qi < nq) load_desc(a.q + pair * a.q_stride + (size_t)(qo + qi) * 32, dq);
+    int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
+    for (int b = 0; b < nt; b += 256) {
+        __syncthreads();
+        const int j = b + threadIdx.x;
+        if (j < nt) load_desc(a.t + pair * a.t_stride + (size_t)(to + j) * 32, tile[threadIdx.x]);
+        __syncthreads();
+        const int e = min(256, nt - b);
+        for (int k = 0; k < e; ++k) {
+            const int d = omv::hamming256(dq, tile[k]);
+            if (d < d1) {
+                if (d0 > d) d1 = d0, i1 = i0, d0 = d, i0 = b + k;
+                else d1 = d, i1 = b + k;
+            }
+        }
+    }
+    if (qi < nq) {
+        int32_t *oi = a.idx2 + ((size_t)pair * a.out_cap + qi) * 2;
+        int32_t *od = a.dist2 + ((size_t)pair * a.out_cap + qi) * 2;
+        oi[0] = i0, oi[1] = i1, od[0] = d0, od[1] = d1;
+    }
+}
+
+// Lowe ratio on the lapping-area knn of camera blocks 0 and 1 (Frame.cc:1488-1491); candidate
+// stereo pairs before the TriangulateMatches depth check.
+__global__ void stereo_pairs_kernel(const int32_t *idx2, const int32_t *dist2, int out_cap, const int *n_kp,
+                                    const int *mono, int n_cams, int kp_cap, double ratio, int32_t *l2r,
+                                    int32_t *r2l, int n_frames) {
+    const int frame = blockIdx.y;
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m0 = mono[frame * n_cams], m1 = mono[frame * n_cams + 1];
+    const int nq = n_kp[frame * n_cams] - m0;
+    if (qi >= nq) return;
+    const int32_t *oi = idx2 + ((size_t)frame * out_cap + qi) * 2;
+    const int32_t *od = dist2 + ((size_t)frame * out_cap + qi) * 2;
+    if (oi[1] < 0) return;   // fewer than 2 matches
+    if ((double)od[0] < (double)od[1] * ratio) {   // `distance * 0.8`: a double product (:1491)
+        l2r[(size_t)frame * kp_cap + m0 + qi] = m1 + oi[0];
+        atomicMax(&r2l[(size_t)frame * kp_cap + m1 + oi[0]], m0 + qi);   // later left index wins
+    }
+}
+
+}  // namespace
+
+// =============================================================================================
+struct omv_matcher {
+    int max_frames, n_cams, kp_cap, max_mps;
+    int32_t *d_cell_start = nullptr, *d_cell_idx = nullptr;
+    Rec *d_recs = nullptr;
+    int32_t *d_knn_i = nullptr, *d_knn_d = nullptr;
+    FrameArgs f{};
+    hipStream_t last = nullptr;
+    // optional per-stage HIP-event timing: 0 grid, 1 stereo knn, 2 candidates, 3 resolve
+    bool timing = false;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
+    double stage_ms[4] = {0, 0, 0, 0};
+};
+
+static hipEvent_t mk_event(hipStream_t st) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, st);
+    return e;
+}
+
+static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kps, const uint8_t *desc, const int *n_kp,
+                       FrameArgs &f) {
+    f.n_cams = h->n_cams;
+    f.kp_cap = h->kp_cap;
+    f.nlevels = g->nlevels;
+    f.min_x = g->min_x, f.max_x = g->max_x, f.min_y = g->min_y, f.max_y = g->max_y;
+    f.invW = (float)kGridCols / (g->max_x - g->min_x);   // Frame.cc:1878-1879
+    f.invH = (float)kGridRows / (g->max_y - g->min_y);
+    for (int l = 0; l < 16; ++l) f.scale[l] = g->scale_factors[l];
+    f.kps = kps, f.desc = desc, f.n_kp = n_kp;
+    f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
+}
+
+extern "C" {
+
+omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
+    if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || max_mps < 0) return OMV_ERR_ARG;
+    if ((size_t)n_cams * kp_cap * 5 > 150 * 1024) return OMV_ERR_ARG;   // resolve LDS (bits + owners)
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
+    omv_matcher *h = new omv_matcher();
+    h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
+    const size_t fc = (size_t)max_frames * n_cams;
+    HIP_OK(hipMalloc(&h->d_cell_start, sizeof(int32_t) * fc * (kCells + 1)));
+    HIP_OK(hipMalloc(&h->d_cell_idx, sizeof(int32_t) * fc * kp_cap));
+    HIP_OK(hipMalloc(&h->d_recs, sizeof(Rec) * std::max<size_t>(1, fc * max_mps)));
+    HIP_OK(hipMalloc(&h->d_knn_i, sizeof(int32_t) * 2 * max_frames * kp_cap));
+    HIP_OK(hipMalloc(&h->d_knn_d, sizeof(int32_t) * 2 * max_frames * kp_cap));
+    *out = h;
+    return OMV_OK;
+}
+
+omv_status omv_matcher_enable_timing(omv_matcher *h, int on) {
+    if (!h) return OMV_ERR_ARG;
+    h->timing = on != 0;
+    return OMV_OK;
+}
+
+omv_status omv_matcher_stage_ms(omv_matcher *h, double *ms4, int reset) {
+    if (!h || !ms4) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(h->last));
+    for (auto &p : h->ev) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, p.second.first, p.second.second);
+        h->stage_ms[p.first] += ms;
+        (void)hipEventDestroy(p.second.first);
+        (void)hipEventDestroy(p.second.second);
+    }
+    h->ev.clear();
+    for (int k = 0; k < 4; ++k) ms4[k] = h->stage_ms[k];
+    if (reset)
+        for (int k = 0; k < 4; ++k) h->stage_ms[k] = 0;
+    return OMV_OK;
+}
+
+omv_status omv_matcher_destroy(omv_matcher *h) {
+    if (!h) return OMV_ERR_ARG;
+    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_knn_i, h->d_knn_d};
+    for (void *q : p)
+        if (q) (void)hipFree(q);
+    delete h;
+    return OMV_OK;
+}
+
+omv_status omv_matcher_assign_grid(omv_matcher *h, int n_frames, const omv_frame_geom *g, const omv_kp *kps,
+                                   const int *n_kp, void *stream) {
+    if (!h || !g || !kps || !n_kp || n_frames <= 0 || n_frames > h->max_frames || g->n_cams != h->n_cams)
+        return OMV_ERR_ARG;
+    FrameArgs f;
+    fill_frame(h, g, kps, nullptr, n_kp, f);
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
+    grid_kernel<<<n_frames * h->n_cams, 64, 0, st>>>(f, h->d_cell_start, h->d_cell_idx);
+    if (h->timing) h->ev.push_back({0, {e0, mk_event(st)}});
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_matcher_grid_debug(omv_matcher *h, int frame, int cam, int32_t *cell_start, int32_t *idx) {
+    if (!h || frame < 0 || frame >= h->max_frames || cam < 0 || cam >= h->n_cams) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(h->last));
+    const size_t fc = (size_t)frame * h->n_cams + cam;
+    HIP_OK(hipMemcpy(cell_start, h->d_cell_start + fc * (kCells + 1), sizeof(int32_t) * (kCells + 1),
+                     hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(idx, h->d_cell_idx + fc * h->kp_cap, sizeof(int32_t) * h->kp_cap, hipMemcpyDeviceToHost));
+    return OMV_OK;
+}
+
+omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv_frame_geom *g, const omv_kp *kps,
+                                         const uint8_t *desc, const int *n_kp, const omv_mp_view *mps, int M, float th,
+                                         int far_points, float th_far, float nnratio, const int32_t *l2r,
+                                         const int32_t *r2l, const uint8_t *kp_occ_init, int32_t *kp_to_mp,
+                                         int *n_matches, void *stream) {
+    if (!h || !g || !kps || !desc || !n_kp || !mps || !kp_to_mp || !n_matches || n_frames <= 0 ||
+        n_frames > h->max_frames || M < 0 || M > h->max_mps || g->n_cams != h->n_cams)
+        return OMV_ERR_ARG;
+    if (h->n_cams > 1 && (!l2r || !r2l)) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    FrameArgs f;
+    fill_frame(h, g, kps, desc, n_kp, f);
+    MpArgs m{mps->desc, mps->proj_x, mps->proj_y, mps->view_cos, mps->level, mps->in_view, mps->track_depth,
+             mps->is_bad, mps->has_obs, M};
+    hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
+    if (M > 0) {
+        const long long tot = (long long)n_frames * M * h->n_cams;
+        cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs);
+    }
+    hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
+    ResolveArgs ra{f, m, h->d_recs, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, th, th_far, nnratio, far_points};
+    const int S = h->n_cams * h->kp_cap;
+    const size_t lds = sizeof(uint32_t) * ((S + 31) / 32) + sizeof(int) * S;
+    resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
+    if (h->timing) {
+        h->ev.push_back({2, {e0, e1}});
+        h->ev.push_back({3, {e1, mk_event(st)}});
+    }
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *nq, const uint8_t *train, int t_cap,
+                       const int *nt, int32_t *idx2, int32_t *dist2, void *stream) {
+    if (n_pairs <= 0 || !query || !train || !nq || !nt || !idx2 || !dist2 || q_cap <= 0 || t_cap <= 0)
+        return OMV_ERR_ARG;
+    KnnArgs a{query, train, (long long)q_cap * 32, (long long)t_cap * 32, nq, nt, nullptr, nullptr, 1, idx2, dist2, q_cap};
+    dim3 grid((q_cap + 255) / 256, n_pairs);
+    knn2_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a, n_pairs);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_matcher_stereo_lapping(omv_matcher *h, int n_frames, const uint8_t *desc, const int *n_kp,
+                                      const int *mono, double ratio, int32_t *l2r, int32_t *r2l, void *stream) {
+    if (!h || h->n_cams < 2 || !desc || !n_kp || !mono || !l2r || !r2l || n_frames <= 0 || n_frames > h->max_frames)
+        return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    const int cap = h->kp_cap, C = h->n_cams;
+    hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
+    HIP_OK(hipMemsetAsync(l2r, 0xff, sizeof(int32_t) * n_frames * cap, st));
+    HIP_OK(hipMemsetAsync(r2l, 0xff, sizeof(int32_t) * n_frames * cap, st));
+    // query = camera 0 rows [mono0, n0), train = camera 1 rows [mono1, n1)
+    KnnArgs a{desc, desc + (size_t)cap * 32, (long long)C * cap * 32, (long long)C * cap * 32, n_kp, n_kp + 1,
+              mono, mono + 1, C, h->d_knn_i, h->d_knn_d, cap};
+    dim3 grid((cap + 255) / 256, n_frames);
+    knn2_kernel<<<grid, 256, 0, st>>>(a, n_frames);
+    dim3 g2((cap + 255) / 256, n_frames);
+    stereo_pairs_kernel<<<g2, 256, 0, st>>>(h->d_knn_i, h->d_knn_d, cap, n_kp, mono, C, cap, ratio, l2r, r2l, n_frames);
+    if (h->timing) h->ev.push_back({1, {e0, mk_event(st)}});
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+}  // extern "C"

@@ -788,7 +788,33 @@ struct omv_orb {
     std::vector<int> h_lap;
     hipStream_t last_stream = nullptr;
     int device = 0;
+    // optional per-stage HIP-event timing (bench.py): events recorded on the launch stream
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // 5 events per batch: before K1, K2, K3, K4, after K4
+    double stage_ms[4] = {0, 0, 0, 0};
+    long long stage_calls = 0;
 };
+
+static void flush_timing(omv_orb *o) {
+    for (size_t b = 0; b + 5 <= o->ev.size(); b += 5) {
+        for (int k = 0; k < 4; ++k) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, o->ev[b + k], o->ev[b + k + 1]);
+            o->stage_ms[k] += ms;
+        }
+        o->stage_calls++;
+    }
+    for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
+    o->ev.clear();
+}
+
+static void mark(omv_orb *o, hipStream_t st) {
+    if (!o->timing) return;
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, st);
+    o->ev.push_back(e);
+}
 
 static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vector<XTab> &xt, std::vector<XTab> &yt) {
     const omv_orb_params &p = o->p;
@@ -976,6 +1002,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
+    for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
     void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
@@ -1008,23 +1035,47 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     o->last_stream = st;
     const Geom &g = o->g;
     HIP_OK(hipMemcpyAsync(o->d_lap, lapping, sizeof(int) * 2 * n, hipMemcpyHostToDevice, st));
+    mark(o, st);
     // K1: pyramid, level by level
     for (int l = 1; l < g.nlevels; ++l) {
         const long long tot = (long long)g.lv[l].w * g.lv[l].h * n;
         const int blocks = (int)((tot + 255) / 256);
         pyr_resize_kernel<<<blocks, 256, 0, st>>>(g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, n);
     }
+    mark(o, st);
     // K2: FAST per cell
     fast_cells_kernel<<<g.n_cells * n, 64, 2 * o->rmax, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
                                                                o->d_cell_cnt, o->d_cell_kp, o->rmax);
+    mark(o, st);
     // K3: octree per (image, level)
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
     octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
+    mark(o, st);
     // K4: orientation + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
     const int waves = g.out_per_img * n;
     describe_kernel<<<(waves + 3) / 4, 256, 0, st>>>(g, da);
+    mark(o, st);
     HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_orb_enable_timing(omv_orb *o, int on) {
+    if (!o) return OMV_ERR_ARG;
+    o->timing = on != 0;
+    return OMV_OK;
+}
+
+omv_status omv_orb_stage_ms(omv_orb *o, double *ms4, long long *calls, int reset) {
+    if (!o || !ms4) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(o->last_stream));
+    flush_timing(o);
+    for (int k = 0; k < 4; ++k) ms4[k] = o->stage_ms[k];
+    if (calls) *calls = o->stage_calls;
+    if (reset) {
+        for (int k = 0; k < 4; ++k) o->stage_ms[k] = 0;
+        o->stage_calls = 0;
+    }
     return OMV_OK;
 }
 

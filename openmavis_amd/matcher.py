@@ -1,0 +1,162 @@
+"""Host-side mirror of the reference's ORBmatcher for the multi-camera frame (include/ORBmatcher.h),
+running on the HIP matchers of libomv_hip.so.
+
+    m = ORBmatcher(nnratio=0.8, checkOri=True)
+    n = m.SearchByProjection(frames, mps, th, bFarPoints, thFarPoints)
+
+`frames` is a FrameBatch (device tensors of the extractor's batched output plus per-frame
+mvLeftToRightMatch / mvRightToLeftMatch / mvpMapPoints), `mps` a MapPointBatch (the SoA the
+reference reads from MapPoint after Frame::isInFrustum).  Like the reference, SearchByProjection
+returns the match count and mutates the frame's map-point assignment (frames.kp_to_mp).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+FRAME_GRID_COLS = 64
+FRAME_GRID_ROWS = 48
+TH_HIGH = 100
+TH_LOW = 50
+HISTO_LENGTH = 30
+
+
+def frame_geom(n_cams, width, height, scale_factors):
+    g = _lib.FrameGeom()
+    g.n_cams = n_cams
+    g.min_x, g.max_x, g.min_y, g.max_y = 0.0, float(width), 0.0, float(height)   # KB8: no undistortion
+    g.nlevels = len(scale_factors)
+    for i, s in enumerate(scale_factors):
+        g.scale_factors[i] = float(s)
+    return g
+
+
+class FrameBatch:
+    """n_frames multi-camera frames resident on the GPU (torch tensors, padded per camera)."""
+
+    def __init__(self, torch, n_frames, n_cams, kp_cap, width, height, scale_factors, device="cuda"):
+        self.torch = torch
+        self.n_frames, self.n_cams, self.kp_cap = n_frames, n_cams, kp_cap
+        self.geom = frame_geom(n_cams, width, height, scale_factors)
+        z = dict(device=device)
+        self.kps = torch.zeros((n_frames, n_cams, kp_cap, 6), dtype=torch.int32, **z)
+        self.desc = torch.zeros((n_frames, n_cams, kp_cap, 32), dtype=torch.uint8, **z)
+        self.n_kp = torch.zeros((n_frames, n_cams), dtype=torch.int32, **z)
+        self.mono = torch.zeros((n_frames, n_cams), dtype=torch.int32, **z)
+        self.l2r = torch.full((n_frames, kp_cap), -1, dtype=torch.int32, **z)
+        self.r2l = torch.full((n_frames, kp_cap), -1, dtype=torch.int32, **z)
+        self.kp_to_mp = torch.full((n_frames, n_cams * kp_cap), -1, dtype=torch.int32, **z)
+        self.occ_init = None
+        self.n_matches = torch.zeros(n_frames, dtype=torch.int32, **z)
+
+
+class MapPointBatch:
+    """Local map points per frame: device SoA of the fields SearchByProjection reads."""
+
+    FIELDS = ("desc", "proj_x", "proj_y", "view_cos", "level", "in_view", "track_depth", "is_bad", "has_obs")
+
+    def __init__(self, **arrays):
+        for k in self.FIELDS:
+            setattr(self, k, arrays[k])
+        self.M = arrays["desc"].shape[-2]
+
+    def view(self):
+        v = _lib.MpView()
+        for k in self.FIELDS:
+            setattr(v, k, _lib.ptr(getattr(self, k)))
+        return v
+
+
+class ORBmatcher:
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+        self._lib = _lib.load()
+        self._h = None
+        self._shape = None
+
+    def _handle(self, frames, M):
+        shape = (frames.n_frames, frames.n_cams, frames.kp_cap, M)
+        if self._h is None or any(a < b for a, b in zip(self._shape, shape)) or self._shape[1:3] != shape[1:3]:
+            self.close()
+            h = ctypes.c_void_p()
+            _lib.check(self._lib.omv_matcher_create(frames.n_frames, frames.n_cams, frames.kp_cap, max(M, 1),
+                                                    ctypes.byref(h)), "omv_matcher_create")
+            self._h, self._shape = h, (frames.n_frames, frames.n_cams, frames.kp_cap, max(M, 1))
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            self._lib.omv_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _stream(stream):
+        return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+
+    def AssignFeaturesToGrid(self, frames, stream=None):
+        h = self._handle(frames, 1)
+        _lib.check(self._lib.omv_matcher_assign_grid(h, frames.n_frames, ctypes.byref(frames.geom),
+                                                     _lib.ptr(frames.kps), _lib.ptr(frames.n_kp),
+                                                     self._stream(stream)), "omv_matcher_assign_grid")
+
+    STAGES = ("grid", "stereo_knn", "proj_candidates", "proj_resolve")
+
+    def enable_timing(self, on=True):
+        _lib.check(self._lib.omv_matcher_enable_timing(self._h, int(bool(on))))
+
+    def stage_ms(self, reset=True):
+        ms = np.zeros(4, np.float64)
+        _lib.check(self._lib.omv_matcher_stage_ms(self._h, _lib.ptr(ms), int(bool(reset))))
+        return dict(zip(self.STAGES, ms.tolist()))
+
+    def grid(self, frame, cam):
+        cs = np.zeros(FRAME_GRID_COLS * FRAME_GRID_ROWS + 1, np.int32)
+        idx = np.zeros(self._shape[2], np.int32)
+        _lib.check(self._lib.omv_matcher_grid_debug(self._h, frame, cam, _lib.ptr(cs), _lib.ptr(idx)))
+        return cs, idx[:cs[-1]]
+
+    def StereoLapping(self, frames, ratio=0.8, stream=None):
+        """Lowe-ratio knn candidates of ComputeMultiFishEyeMatches (before triangulation)."""
+        h = self._handle(frames, 1)
+        _lib.check(self._lib.omv_matcher_stereo_lapping(h, frames.n_frames, _lib.ptr(frames.desc),
+                                                        _lib.ptr(frames.n_kp), _lib.ptr(frames.mono),
+                                                        ctypes.c_double(ratio), _lib.ptr(frames.l2r),
+                                                        _lib.ptr(frames.r2l), self._stream(stream)),
+                   "omv_matcher_stereo_lapping")
+
+    def SearchByProjection(self, frames, mps, th=3.0, bFarPoints=False, thFarPoints=50.0, stream=None,
+                           grid_ready=False):
+        """Returns the per-frame match counts (device tensor); mutates frames.kp_to_mp."""
+        h = self._handle(frames, mps.M)
+        if not grid_ready:
+            self.AssignFeaturesToGrid(frames, stream)
+        v = mps.view()
+        _lib.check(self._lib.omv_matcher_search_projection(
+            h, frames.n_frames, ctypes.byref(frames.geom), _lib.ptr(frames.kps), _lib.ptr(frames.desc),
+            _lib.ptr(frames.n_kp), ctypes.byref(v), mps.M, ctypes.c_float(th), int(bool(bFarPoints)),
+            ctypes.c_float(thFarPoints), ctypes.c_float(self.mfNNratio), _lib.ptr(frames.l2r),
+            _lib.ptr(frames.r2l), _lib.ptr(frames.occ_init), _lib.ptr(frames.kp_to_mp),
+            _lib.ptr(frames.n_matches), self._stream(stream)), "omv_matcher_search_projection")
+        return frames.n_matches
+
+
+def bf_knn2(query, nq, train, nt, stream=None):
+    """knnMatch(k=2) over a batch of (query, train) sets: torch uint8 [P, Q, 32], [P, T, 32]; counts
+    int32 [P].  Returns (idx2, dist2) int32 [P, Q, 2]."""
+    import torch
+    lib = _lib.load()
+    P, Q = query.shape[0], query.shape[1]
+    idx2 = torch.empty((P, Q, 2), dtype=torch.int32, device=query.device)
+    dist2 = torch.empty((P, Q, 2), dtype=torch.int32, device=query.device)
+    s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    _lib.check(lib.omv_bf_knn2(P, _lib.ptr(query), Q, _lib.ptr(nq), _lib.ptr(train), train.shape[1], _lib.ptr(nt),
+                               _lib.ptr(idx2), _lib.ptr(dist2), s), "omv_bf_knn2")
+    return idx2, dist2

@@ -58,3 +58,46 @@ def flip_bits(desc, rng, max_flips=8):
             for b in bits:
                 out[i, b >> 3] ^= np.uint8(1 << (b & 7))
     return out
+
+
+def make_map_points(kps, desc, n_kp, M, seed, width, height, nlevels=8, frac_true=0.6):
+    """Synthetic local map: `frac_true` of the points derive from true
+    keypoints of the frame (descriptor with U{0..8} bit flips, projection = keypoint + N(0, 1 px),
+    level = octave), the rest are random.  Some points are also visible in a second camera so the
+    multi-camera claim / `continue` logic is exercised.  Inputs are host numpy arrays of one frame:
+    kps [C][cap] (KP dtype), desc [C][cap][32], n_kp [C].  Returns a dict of numpy arrays."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    C = kps.shape[0]
+    out = dict(
+        desc=np.zeros((M, 32), np.uint8),
+        proj_x=np.zeros((M, C), np.float32),
+        proj_y=np.zeros((M, C), np.float32),
+        view_cos=rng.uniform(0.99, 1.0, (M, C)).astype(np.float32),
+        level=np.full((M, C), -1, np.int32),
+        in_view=np.zeros((M, C), np.uint8),
+        track_depth=rng.uniform(1.0, 60.0, M).astype(np.float32),
+        is_bad=(rng.random(M) < 0.02).astype(np.uint8),
+        has_obs=(rng.random(M) > 0.03).astype(np.uint8),
+    )
+    n_true = int(M * frac_true)
+    for m in range(M):
+        cams = [int(rng.integers(0, C))]
+        if rng.random() < 0.3 and C > 1:
+            cams.append(int(rng.integers(0, C)))
+        for j, c in enumerate(cams):
+            if m < n_true and n_kp[c] > 0 and j == 0:
+                i = int(rng.integers(0, n_kp[c]))
+                k = kps[c, i]
+                out["desc"][m] = desc[c, i]
+                out["proj_x"][m, c] = k["x"] + rng.normal(0.0, 1.0)
+                out["proj_y"][m, c] = k["y"] + rng.normal(0.0, 1.0)
+                out["level"][m, c] = k["octave"]
+            else:
+                if j == 0:
+                    out["desc"][m] = rng.integers(0, 256, 32, dtype=np.uint8)
+                out["proj_x"][m, c] = rng.uniform(0, width)
+                out["proj_y"][m, c] = rng.uniform(0, height)
+                out["level"][m, c] = int(rng.integers(0, nlevels))
+            out["in_view"][m, c] = 1
+    out["desc"][:n_true] = flip_bits(out["desc"][:n_true], rng)
+    return out

@@ -101,3 +101,77 @@ def fast_atan2(y, x):
     f = lib().oracle_fast_atan2
     f.restype = ctypes.c_float
     return f(ctypes.c_float(y), ctypes.c_float(x))
+
+
+class FrameGeom(ctypes.Structure):
+    _fields_ = [("n_cams", ctypes.c_int), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int),
+                ("scale_factors", ctypes.c_float * 16)]
+
+
+def frame_geom(n_cams, width, height, scale_factors):
+    g = FrameGeom()
+    g.n_cams, g.min_x, g.max_x, g.min_y, g.max_y = n_cams, 0.0, float(width), 0.0, float(height)
+    g.nlevels = len(scale_factors)
+    for i, s in enumerate(scale_factors):
+        g.scale_factors[i] = float(s)
+    return g
+
+
+def grid(geom, kps, n_kp, cam):
+    """Frame::AssignFeaturesToGrid of one camera: (cell_start[3073], idx[])."""
+    kps = np.ascontiguousarray(kps)
+    n_kp = np.ascontiguousarray(n_kp, np.int32)
+    cap = kps.shape[1]
+    cs = np.zeros(64 * 48 + 1, np.int32)
+    idx = np.zeros(cap, np.int32)
+    n = lib().oracle_grid(ctypes.byref(geom), _p(kps), cap, _p(n_kp), cam, _p(cs), _p(idx))
+    return cs, idx[:n]
+
+
+def features_in_area(geom, kps, n_kp, x, y, r, min_level, max_level, cam):
+    kps = np.ascontiguousarray(kps)
+    n_kp = np.ascontiguousarray(n_kp, np.int32)
+    out = np.zeros(kps.shape[1], np.int32)
+    n = lib().oracle_features_in_area(ctypes.byref(geom), _p(kps), kps.shape[1], _p(n_kp), ctypes.c_float(x),
+                                      ctypes.c_float(y), ctypes.c_float(r), min_level, max_level, cam, _p(out),
+                                      kps.shape[1])
+    return out[:n]
+
+
+def search_by_projection(geom, kps, desc, n_kp, mp, th, far_points, th_far, nnratio, l2r, r2l, occ_init, kp_to_mp):
+    """ORBmatcher::SearchByProjection(Frame&, MPs, ...) restated; mutates kp_to_mp, returns nmatches."""
+    kps = np.ascontiguousarray(kps)
+    desc = np.ascontiguousarray(desc)
+    n_kp = np.ascontiguousarray(n_kp, np.int32)
+    cap = kps.shape[1]
+    M = mp["desc"].shape[0]
+    a = {k: np.ascontiguousarray(v) for k, v in mp.items()}
+    l2r = np.ascontiguousarray(l2r, np.int32)
+    r2l = np.ascontiguousarray(r2l, np.int32)
+    occ = np.ascontiguousarray(occ_init, np.uint8) if occ_init is not None else np.zeros(kps.shape[0] * cap, np.uint8)
+    assert kp_to_mp.dtype == np.int32 and kp_to_mp.flags.c_contiguous
+    f = lib().oracle_search_by_projection
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + \
+        [ctypes.c_void_p] * 9 + [ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_float] + \
+        [ctypes.c_void_p] * 4
+    return f(ctypes.cast(ctypes.byref(geom), ctypes.c_void_p), _p(kps), _p(desc), cap, _p(n_kp), _p(a["desc"]),
+             _p(a["proj_x"]), _p(a["proj_y"]), _p(a["view_cos"]), _p(a["level"]), _p(a["in_view"]),
+             _p(a["track_depth"]), _p(a["is_bad"]), _p(a["has_obs"]), M, th, int(far_points), th_far, nnratio,
+             _p(l2r), _p(r2l), _p(occ), _p(kp_to_mp))
+
+
+def bf_knn2(q, t):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    nq, nt = q.shape[0], t.shape[0]
+    idx2 = np.zeros((nq, 2), np.int32)
+    dist2 = np.zeros((nq, 2), np.int32)
+    lib().oracle_bf_knn2(_p(q), nq, _p(t), nt, _p(idx2), _p(dist2))
+    return idx2, dist2
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(_p(a), _p(b))

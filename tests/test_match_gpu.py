@@ -1,0 +1,137 @@
+"""GPU parity of the HIP matchers (grid, lapping knn, SearchByProjection, knn2) against the oracle.
+
+Bar: bit-exact — identical grids, knn indices/distances, keypoint->map-point assignments and match
+counts (integer work).
+"""
+import numpy as np
+import pytest
+
+from openmavis_amd import synth
+from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher, bf_knn2
+from openmavis_amd.orb import ORBextractor
+
+pytestmark = pytest.mark.gpu
+
+W, H, C, NF = 720, 540, 5, 1200
+LAP = np.array([[0, 720], [0, 720], [0, 0], [0, 0], [0, 0]], np.int32)
+
+
+@pytest.fixture(scope="module")
+def frames(torch_cuda):
+    torch = torch_cuda
+    n_frames = 3
+    ex = ORBextractor(NF, 1.2, 8, 15, 7, width=W, height=H, max_images=n_frames * C)
+    cap = ex.max_keypoints()
+    imgs = np.concatenate([synth.hilti_frame(f) for f in range(n_frames)])
+    fb = FrameBatch(torch, n_frames, C, cap, W, H, ex.GetScaleFactors())
+    d_img = torch.from_numpy(imgs).cuda()
+    ex.extract_batch(d_img, np.tile(LAP, (n_frames, 1)), fb.kps.view(-1, cap, 6), fb.desc.view(-1, cap, 32),
+                     fb.n_kp.view(-1), fb.mono.view(-1))
+    torch.cuda.synchronize()
+    assert ex.last_error() == 0
+    return fb
+
+
+def host(fb, oracle):
+    kps = fb.kps.cpu().numpy().view(oracle.KP_DTYPE).reshape(fb.n_frames, fb.n_cams, fb.kp_cap)
+    return kps, fb.desc.cpu().numpy(), fb.n_kp.cpu().numpy(), fb.mono.cpu().numpy()
+
+
+def test_grid_matches_oracle(frames, oracle):
+    kps, desc, n_kp, mono = host(frames, oracle)
+    m = ORBmatcher(0.8)
+    m.AssignFeaturesToGrid(frames)
+    for f in range(frames.n_frames):
+        g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+        for c in range(C):
+            cs_o, idx_o = oracle.grid(g, kps[f], n_kp[f], c)
+            cs_g, idx_g = m.grid(f, c)
+            assert np.array_equal(cs_o, cs_g), f"frame {f} cam {c} cell starts differ"
+            assert np.array_equal(idx_o, idx_g), f"frame {f} cam {c} cell contents differ"
+
+
+def test_stereo_lapping_matches_oracle(frames, oracle):
+    kps, desc, n_kp, mono = host(frames, oracle)
+    m = ORBmatcher(0.8)
+    m.StereoLapping(frames, 0.8)
+    l2r = frames.l2r.cpu().numpy()
+    r2l = frames.r2l.cpu().numpy()
+    for f in range(frames.n_frames):
+        q = desc[f, 0, mono[f, 0]:n_kp[f, 0]]
+        t = desc[f, 1, mono[f, 1]:n_kp[f, 1]]
+        i2, d2 = oracle.bf_knn2(q, t)
+        el2r = np.full(frames.kp_cap, -1, np.int32)
+        er2l = np.full(frames.kp_cap, -1, np.int32)
+        for qi in range(len(q)):
+            if i2[qi, 1] >= 0 and float(d2[qi, 0]) < float(d2[qi, 1]) * 0.8:
+                el2r[mono[f, 0] + qi] = mono[f, 1] + i2[qi, 0]
+                er2l[mono[f, 1] + i2[qi, 0]] = mono[f, 0] + qi
+        assert np.array_equal(el2r, l2r[f]) and np.array_equal(er2l, r2l[f]), f"frame {f}"
+        assert (el2r >= 0).sum() > 5
+
+
+def _mps_for(frames, oracle, M, seed, torch):
+    kps, desc, n_kp, _ = host(frames, oracle)
+    per = [synth.make_map_points(kps[f], desc[f], n_kp[f], M, seed + f, W, H) for f in range(frames.n_frames)]
+    stacked = {k: np.stack([p[k] for p in per]) for k in per[0]}
+    dev = {k: torch.from_numpy(v).cuda() for k, v in stacked.items()}
+    return per, MapPointBatch(**dev)
+
+
+@pytest.mark.parametrize("th,far,nnratio,occ_frac,obs_all", [
+    (6.0, False, 0.8, 0.0, False),
+    (1.0, False, 0.8, 0.0, True),
+    (3.0, True, 0.6, 0.05, False),
+    (15.0, False, 0.9, 0.02, True),
+])
+def test_search_by_projection_matches_oracle(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs_all):
+    torch = torch_cuda
+    M = 5000
+    per, mpb = _mps_for(frames, oracle, M, 7 + int(th), torch)
+    if obs_all:
+        mpb.has_obs.fill_(1)
+        for p in per:
+            p["has_obs"][:] = 1
+    m = ORBmatcher(nnratio)
+    m.StereoLapping(frames, 0.8)
+    rng = np.random.default_rng(11)
+    S = C * frames.kp_cap
+    occ = (rng.random((frames.n_frames, S)) < occ_frac).astype(np.uint8)
+    init = np.where(occ > 0, 123456, -1).astype(np.int32)
+    frames.occ_init = torch.from_numpy(occ).cuda()
+    frames.kp_to_mp.copy_(torch.from_numpy(init))
+    m.SearchByProjection(frames, mpb, th, far, 20.0)
+    torch.cuda.synchronize()
+    got = frames.kp_to_mp.cpu().numpy()
+    got_n = frames.n_matches.cpu().numpy()
+    kps, desc, n_kp, _ = host(frames, oracle)
+    l2r, r2l = frames.l2r.cpu().numpy(), frames.r2l.cpu().numpy()
+    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+    for f in range(frames.n_frames):
+        exp = init[f].copy()
+        n = oracle.search_by_projection(g, kps[f], desc[f], n_kp[f], per[f], th, far, 20.0, nnratio, l2r[f], r2l[f],
+                                        occ[f], exp)
+        assert n == got_n[f], f"frame {f}: nmatches {got_n[f]} != {n}"
+        bad = np.nonzero(exp != got[f])[0]
+        assert bad.size == 0, f"frame {f}: {bad.size} assignments differ, first slots {bad[:8]}"
+        assert n > 300
+    frames.occ_init = None
+    frames.kp_to_mp.fill_(-1)
+
+
+def test_knn2_matches_oracle_with_ties(oracle, torch_cuda):
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    P, Q, T = 3, 700, 900
+    base = rng.integers(0, 256, (64, 32), dtype=np.uint8)   # few distinct rows -> many ties
+    q = base[rng.integers(0, 64, (P, Q))]
+    t = base[rng.integers(0, 64, (P, T))]
+    t[1, :5] = base[0]
+    nq = np.array([Q, 300, 1], np.int32)
+    nt = np.array([T, 1, 0], np.int32)
+    i2, d2 = bf_knn2(torch.from_numpy(q).cuda(), torch.from_numpy(nq).cuda(), torch.from_numpy(t).cuda(),
+                     torch.from_numpy(nt).cuda())
+    i2, d2 = i2.cpu().numpy(), d2.cpu().numpy()
+    for p in range(P):
+        ei, ed = oracle.bf_knn2(q[p, :nq[p]], t[p, :nt[p]])
+        assert np.array_equal(ei, i2[p, :nq[p]]) and np.array_equal(ed, d2[p, :nq[p]]), f"pair {p}"
