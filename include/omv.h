@@ -155,6 +155,9 @@ omv_status omv_matcher_search_projection(omv_matcher *m, int n_frames, const omv
 omv_status omv_matcher_stereo_lapping(omv_matcher *m, int n_frames, const uint8_t *desc, const int *n_kp,
                                       const int *mono, double ratio, int32_t *l2r, int32_t *r2l, void *stream);
 
+/* Device-side error word (OMV_ERR_CAPACITY if a bound was hit) since the last call; syncs. */
+omv_status omv_matcher_last_error(omv_matcher *m);
+
 /* Per-stage device time: 0 grid, 1 lapping knn, 2 projection candidates, 3 claim resolution. */
 omv_status omv_matcher_enable_timing(omv_matcher *m, int on);
 omv_status omv_matcher_stage_ms(omv_matcher *m, double *ms4, int reset);

@@ -75,6 +75,7 @@ SIGNATURES = {
     "omv_matcher_assign_grid": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP]),
     "omv_matcher_grid_debug": (_I, [_VP, _I, _I, _VP, _VP]),
     "omv_matcher_enable_timing": (_I, [_VP, _I]),
+    "omv_matcher_last_error": (_I, [_VP]),
     "omv_matcher_stage_ms": (_I, [_VP, _VP, _I]),
     "omv_matcher_search_projection": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP,
                                            ctypes.POINTER(MpView), _I, _F, _I, _F, _F, _VP, _VP, _VP, _VP,

@@ -31,7 +31,7 @@ namespace {
 
 constexpr int kGridCols = 64, kGridRows = 48, kCells = kGridCols * kGridRows;
 constexpr int kTH_HIGH = 100;
-constexpr int kTop = 4;
+constexpr int kTop = 16;   // candidates kept per (point, camera): rescans only when >14 are claimed
 constexpr int kMaxCams = 8;
 
 #define HIP_OK(x)                                                                    \
@@ -130,12 +130,13 @@ struct MpArgs {
     int M;
 };
 
+// Record entry: keypoint index (bits 0-15) | Hamming distance (bits 16-24) | octave (bits 25-29).
 struct Rec {
-    int idx[kTop];
-    int16_t dist[kTop];
-    int8_t oct[kTop];
-    int count;   // candidates in the window that were not blocked when the record was built
+    uint32_t e[kTop];
 };
+__device__ __forceinline__ int rec_idx(uint32_t v) { return (int)(v & 0xffff); }
+__device__ __forceinline__ int rec_dist(uint32_t v) { return (int)((v >> 16) & 0x1ff); }
+__device__ __forceinline__ int rec_oct(uint32_t v) { return (int)((v >> 25) & 0x1f); }
 
 struct Top {
     int idx[kTop], dist[kTop], oct[kTop];
@@ -212,7 +213,7 @@ __device__ __forceinline__ float window_radius(const FrameArgs &f, const MpArgs 
 
 // One thread per (frame, map point, camera).
 __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
-                                                   const uint8_t *occ_init, Rec *recs) {
+                                                   const uint8_t *occ_init, Rec *recs, int *counts) {
     const int C = f.n_cams;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long long)n_frames * m.M * C) return;
@@ -232,16 +233,14 @@ __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_
         scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, lvl - 1, lvl, dmp,
                     [&](int slot) { return occ && occ[slot]; }, t);
     }
-    for (int q = 0; q < kTop; ++q) {
-        out.idx[q] = q < t.n ? t.idx[q] : -1;
-        out.dist[q] = q < t.n ? t.dist[q] : 256;
-        out.oct[q] = q < t.n ? t.oct[q] : -1;
-    }
-    out.count = t.count;
+    for (int q = 0; q < kTop; ++q)
+        out.e[q] = q < t.n ? (uint32_t)t.idx[q] | ((uint32_t)t.dist[q] << 16) | ((uint32_t)t.oct[q] << 25) : 0u;
+    counts[bc] = t.count;
 }
 
 // ---------------------------------------------------------------------------------------------
 constexpr int kMaxClaims = 2 * kMaxCams;
+constexpr int kMaxRevived = 64;   // initially-occupied keypoints freed during the call (rare)
 
 struct Eval {
     int nclaim;
@@ -257,25 +256,54 @@ struct ResolveArgs {
     FrameArgs f;
     MpArgs m;
     const Rec *recs;
+    const int *counts;   // candidates in the window not blocked when the record was built
     const int32_t *l2r, *r2l;
     const uint8_t *occ_init;
     int32_t *kp_to_mp;
     int *n_matches;
+    int *err;
     float th, th_far, nnratio;
     int far_points;
 };
 
-__device__ void evaluate(const ResolveArgs &a, int frame, int i, const uint32_t *bits, bool force_rescan, Eval &e) {
+// Shared per-block staging of the 64 points a wavefront evaluates.
+struct BlockStage {
+    Rec rec[64 * kMaxCams];
+    int count[64 * kMaxCams];
+    int8_t level[64 * kMaxCams];
+    uint8_t in_view[64 * kMaxCams];
+    uint8_t skip[64];
+    uint8_t obs[64];
+};
+
+__device__ __forceinline__ bool bit_of(const uint32_t *bits, int s) { return (bits[s >> 5] >> (s & 31)) & 1u; }
+
+// Does keypoint slot `slot` (camera c) fall in the GetFeaturesInArea window of (x, y, r, lvl)?
+__device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float x, float y, float r, int lvl) {
+    const omv_kp k = f.kps[((size_t)frame * f.n_cams) * f.kp_cap + slot];
+    const int px = (int)roundf((k.x - f.min_x) * f.invW), py = (int)roundf((k.y - f.min_y) * f.invH);
+    if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return false;   // not in the grid
+    const int x0 = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    const int x1 = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    const int y0 = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    const int y1 = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (px < x0 || px > x1 || py < y0 || py > y1) return false;
+    if (k.octave < lvl - 1 || k.octave > lvl) return false;
+    return fabsf(k.x - x) < r && fabsf(k.y - y) < r;
+}
+
+__device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
+                         const int *revived, int nrevived, Eval &e) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     const int C = f.n_cams, cap = f.kp_cap;
     e.nclaim = e.nrel = e.nmatch = 0;
     e.fallback = e.unblock = false;
-    if (mp_skipped(m, frame, i, C, a.far_points, a.th_far)) return;
+    if (bs.skip[l]) return;
     const size_t fm = (size_t)frame * m.M + i;
-    const bool obs = m.has_obs[fm] != 0;
+    const bool obs = bs.obs[l] != 0;
     auto is_blocked = [&](int slot) {
-        if ((bits[slot >> 5] >> (slot & 31)) & 1u) {
+        if (bit_of(bits, slot)) {
             // an own earlier claim of a point without observations unblocks it
             for (int q = 0; q < e.nclaim; ++q)
                 if (e.claim[q] == slot) return obs;
@@ -287,36 +315,44 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, const uint32_t 
         return false;
     };
     auto add_claim = [&](int slot) {
-        if (!obs && ((bits[slot >> 5] >> (slot & 31)) & 1u)) e.unblock = true;
+        if (!obs && bit_of(bits, slot)) e.unblock = true;
         e.claim[e.nclaim++] = slot;
     };
     const int32_t *l2r = a.l2r + (size_t)frame * cap;
     const int32_t *r2l = a.r2l + (size_t)frame * cap;
-    uint64_t dmp[4];
-    bool have_desc = false;
     for (int c = 0; c < C; ++c) {
-        const size_t bc = fm * C + c;
-        if (!m.in_view[bc]) continue;
-        const int lvl = m.level[bc];
+        if (!bs.in_view[l * C + c]) continue;
+        const int lvl = bs.level[l * C + c];
         if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
-        const Rec &r = a.recs[bc];
-        if (r.count == 0 && !force_rescan) continue;   // vIndices empty or all initially blocked
-        int b1 = -1, b2 = -1, d1 = 256, d2 = 256, o1 = -1, o2 = -1;
-        bool need_rescan = force_rescan;
-        if (!need_rescan) {
-            const int avail = min(r.count, kTop);
-            int k = 0;
-            for (; k < avail && b2 < 0; ++k) {
-                const int slot = c * cap + r.idx[k];
-                if (is_blocked(slot)) continue;
-                if (b1 < 0) b1 = r.idx[k], d1 = r.dist[k], o1 = r.oct[k];
-                else b2 = r.idx[k], d2 = r.dist[k], o2 = r.oct[k];
+        const Rec &r = bs.rec[l * C + c];
+        const int rcount = bs.count[l * C + c];
+        const size_t bc = fm * C + c;
+        // a freed initially-occupied keypoint inside this window is missing from the record
+        bool need_rescan = nrevived > kMaxRevived;   // list overflowed: rescan every window (exact, slow)
+        if (nrevived > 0 && !need_rescan) {
+            const float rad = window_radius(f, m, bc, c, a.th, a.th != 1.0f);
+            for (int q = 0; q < nrevived && !need_rescan; ++q) {
+                const int s = revived[q];
+                if (s / cap == c) need_rescan = in_window(f, frame, c, s, m.proj_x[bc], m.proj_y[bc], rad, lvl);
             }
-            if (b2 < 0 && r.count > kTop) need_rescan = true;
+        }
+        if (rcount == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
+        int b1 = -1, b2 = -1, d1 = 256, d2 = 256, o1 = -1, o2 = -1;
+        if (!need_rescan) {
+            const int avail = min(rcount, kTop);
+            for (int k = 0; k < avail && b2 < 0; ++k) {
+                const uint32_t v = r.e[k];
+                const int slot = c * cap + rec_idx(v);
+                if (is_blocked(slot)) continue;
+                if (b1 < 0) b1 = rec_idx(v), d1 = rec_dist(v), o1 = rec_oct(v);
+                else b2 = rec_idx(v), d2 = rec_dist(v), o2 = rec_oct(v);
+            }
+            if (b2 < 0 && rcount > kTop) need_rescan = true;
         }
         if (need_rescan) {
             e.fallback = true;
-            if (!have_desc) load_desc(m.desc + fm * 32, dmp), have_desc = true;
+            uint64_t dmp[4];
+            load_desc(m.desc + fm * 32, dmp);
             Top t;
             scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f),
                         lvl - 1, lvl, dmp, is_blocked, t);
@@ -347,11 +383,16 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, const uint32_t 
 // One wavefront (one 64-thread workgroup) per frame.
 __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    __shared__ BlockStage bs;
+    __shared__ int revived[kMaxRevived];
+    __shared__ int nrevived;
     const int frame = blockIdx.x, lane = threadIdx.x;
     const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap;
     const int nwords = (S + 31) >> 5;
-    uint32_t *bits = rsm;
-    int *owner = reinterpret_cast<int *>(rsm + nwords);
+    uint32_t *bits = rsm;                                         // blocked: mvpMapPoints[s] has observations
+    uint32_t *occ0 = rsm + nwords;                                // initially occupied (not in the records)
+    int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);       // first blocking claimer lane in a batch
+    int *lastw = owner + S;                                       // last writer lane among committing lanes
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
     for (int w = lane; w < nwords; w += 64) {
         uint32_t v = 0;
@@ -360,29 +401,49 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             if (s < S && occ && occ[s]) v |= 1u << b;
         }
         bits[w] = v;
+        occ0[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = 64;
+    for (int s = lane; s < S; s += 64) owner[s] = 64, lastw[s] = -1;
+    if (lane == 0) nrevived = 0;
     __syncthreads();
     int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
     int total = 0;
-    bool dirty = false;   // a claim unblocked a keypoint: records may miss candidates from now on
     const int M = a.m.M;
     for (int base = 0; base < M; base += 64) {
+        const int nb = min(64, M - base);
+        // stage the block's records and flags in LDS (coalesced)
+        {
+            const int4 *src = reinterpret_cast<const int4 *>(a.recs + ((size_t)frame * M + base) * C);
+            int4 *dst = reinterpret_cast<int4 *>(bs.rec);
+            const int n16 = nb * C * (int)(sizeof(Rec) / 16);
+            for (int q = lane; q < n16; q += 64) dst[q] = src[q];
+            const size_t o = ((size_t)frame * M + base) * C;
+            for (int q = lane; q < nb * C; q += 64) {
+                bs.level[q] = (int8_t)max(-1, min(127, a.m.level[o + q]));
+                bs.in_view[q] = a.m.in_view[o + q];
+            }
+            for (int q = lane; q < nb * C; q += 64) bs.count[q] = a.counts[o + q];
+            if (lane < nb) {
+                bs.skip[lane] = mp_skipped(a.m, frame, base + lane, C, a.far_points, a.th_far);
+                bs.obs[lane] = a.m.has_obs[(size_t)frame * M + base + lane] != 0;
+            }
+        }
+        __syncthreads();
         const int i = base + lane;
         int start = 0;
-        const int nb = min(64, M - base);
         while (start < nb) {
             const bool active = lane >= start && lane < nb;
             Eval e;
-            if (active) evaluate(a, frame, i, bits, dirty, e);
+            const int nrev = nrevived;
+            if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, e);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
-            const bool obs = active && a.m.has_obs[(size_t)frame * M + i];
+            const bool obs = active && bs.obs[lane];
             if (obs)
                 for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], lane);
             __syncthreads();
             bool conflict = false;
             if (active && lane > start) {
-                conflict = e.fallback;
+                conflict = e.fallback;   // a full rescan saw the whole window: only safe at the batch head
                 for (int q = 0; q < e.nrel && !conflict; ++q) conflict = owner[e.rel[q]] < lane;
             }
             __syncthreads();
@@ -391,29 +452,39 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             uint64_t cm = __ballot(conflict);
             const uint64_t um = __ballot(active && e.unblock);
             if (um) {
+                // a point without observations overwrote a blocked keypoint: later lanes saw it blocked
                 const int u = __ffsll((long long)um) - 1;
-                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));   // everything after the unblocking lane
+                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));
             }
             const int j0 = cm ? min(nb, __ffsll((long long)cm) - 1) : nb;
+            // commit lanes [start, j0): the highest committing lane writes a shared slot last
+            const bool committed = lane >= start && lane < j0;
+            if (committed)
+                for (int t = 0; t < e.nclaim; ++t) atomicMax(&lastw[e.claim[t]], lane);
             __syncthreads();
-            // commit lanes [start, j0) in map-point order
-            for (int q = start; q < j0; ++q) {
-                if (lane == q) {
-                    for (int t = 0; t < e.nclaim; ++t) {
-                        const int s = e.claim[t];
-                        k2m[s] = i;
-                        if (obs) atomicOr(&bits[s >> 5], 1u << (s & 31));
-                        else atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
+            if (committed)
+                for (int t = 0; t < e.nclaim; ++t) {
+                    const int s = e.claim[t];
+                    if (lastw[s] != lane) continue;
+                    k2m[s] = i;
+                    if (obs) {
+                        atomicOr(&bits[s >> 5], 1u << (s & 31));
+                    } else {
+                        if (bit_of(occ0, s) && bit_of(bits, s)) {   // an initially occupied keypoint is freed
+                            const int q = atomicAdd(&nrevived, 1);
+                            if (q < kMaxRevived) revived[q] = s;
+                        }
+                        atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
                     }
                 }
-                __syncthreads();
-            }
-            const bool committed = lane >= start && lane < j0;
+            __syncthreads();
+            if (committed)
+                for (int t = 0; t < e.nclaim; ++t) lastw[e.claim[t]] = -1;
             int nm = committed ? e.nmatch : 0;
             for (int d = 32; d >= 1; d >>= 1) nm += __shfl_xor(nm, d, 64);
             total += nm;
-            if (__ballot(committed && e.unblock)) dirty = true;
             start = j0;
+            __syncthreads();
         }
     }
     if (lane == 0) a.n_matches[frame] = total;
@@ -490,7 +561,9 @@ struct omv_matcher {
     int max_frames, n_cams, kp_cap, max_mps;
     int32_t *d_cell_start = nullptr, *d_cell_idx = nullptr;
     Rec *d_recs = nullptr;
+    int *d_counts = nullptr;
     int32_t *d_knn_i = nullptr, *d_knn_d = nullptr;
+    int *d_err = nullptr;
     FrameArgs f{};
     hipStream_t last = nullptr;
     // optional per-stage HIP-event timing: 0 grid, 1 stereo knn, 2 candidates, 3 resolve
@@ -522,8 +595,9 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
 extern "C" {
 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
-    if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || max_mps < 0) return OMV_ERR_ARG;
-    if ((size_t)n_cams * kp_cap * 5 > 150 * 1024) return OMV_ERR_ARG;   // resolve LDS (bits + owners)
+    if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)
+        return OMV_ERR_ARG;
+    if ((size_t)n_cams * kp_cap * 9 + sizeof(BlockStage) > 150 * 1024) return OMV_ERR_ARG;   // resolve LDS
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
     omv_matcher *h = new omv_matcher();
@@ -532,8 +606,11 @@ omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mp
     HIP_OK(hipMalloc(&h->d_cell_start, sizeof(int32_t) * fc * (kCells + 1)));
     HIP_OK(hipMalloc(&h->d_cell_idx, sizeof(int32_t) * fc * kp_cap));
     HIP_OK(hipMalloc(&h->d_recs, sizeof(Rec) * std::max<size_t>(1, fc * max_mps)));
+    HIP_OK(hipMalloc(&h->d_counts, sizeof(int) * std::max<size_t>(1, fc * max_mps)));
     HIP_OK(hipMalloc(&h->d_knn_i, sizeof(int32_t) * 2 * max_frames * kp_cap));
     HIP_OK(hipMalloc(&h->d_knn_d, sizeof(int32_t) * 2 * max_frames * kp_cap));
+    HIP_OK(hipMalloc(&h->d_err, sizeof(int)));
+    HIP_OK(hipMemset(h->d_err, 0, sizeof(int)));
     *out = h;
     return OMV_OK;
 }
@@ -561,9 +638,18 @@ omv_status omv_matcher_stage_ms(omv_matcher *h, double *ms4, int reset) {
     return OMV_OK;
 }
 
+omv_status omv_matcher_last_error(omv_matcher *h) {
+    if (!h) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(h->last));
+    int e = 0;
+    HIP_OK(hipMemcpy(&e, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(h->d_err, 0, sizeof(int)));
+    return e;
+}
+
 omv_status omv_matcher_destroy(omv_matcher *h) {
     if (!h) return OMV_ERR_ARG;
-    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_knn_i, h->d_knn_d};
+    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_knn_i, h->d_knn_d, h->d_err};
     for (void *q : p)
         if (q) (void)hipFree(q);
     delete h;
@@ -613,16 +699,19 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
-        cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs);
+        cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs,
+                                                              h->d_counts);
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
-    ResolveArgs ra{f, m, h->d_recs, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, th, th_far, nnratio, far_points};
+    hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
+    ResolveArgs ra{f, m, h->d_recs, h->d_counts, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
+                   far_points};
     const int S = h->n_cams * h->kp_cap;
-    const size_t lds = sizeof(uint32_t) * ((S + 31) / 32) + sizeof(int) * S;
+    const size_t lds = sizeof(uint32_t) * 2 * ((S + 31) / 32) + 2 * sizeof(int) * S;
     resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
     if (h->timing) {
         h->ev.push_back({2, {e0, e1}});
-        h->ev.push_back({3, {e1, mk_event(st)}});
+        h->ev.push_back({3, {e2, mk_event(st)}});
     }
     HIP_OK(hipGetLastError());
     return OMV_OK;

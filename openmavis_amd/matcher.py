@@ -76,7 +76,9 @@ class ORBmatcher:
         self._h = None
         self._shape = None
 
-    def _handle(self, frames, M):
+    def _handle(self, frames, M=0):
+        # one workspace per (frames, cams, kp_cap); grows (and drops the grid) only when M exceeds it
+        M = max(M, self._shape[3] if self._shape else 1)
         shape = (frames.n_frames, frames.n_cams, frames.kp_cap, M)
         if self._h is None or any(a < b for a, b in zip(self._shape, shape)) or self._shape[1:3] != shape[1:3]:
             self.close()
@@ -102,7 +104,7 @@ class ORBmatcher:
         return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
 
     def AssignFeaturesToGrid(self, frames, stream=None):
-        h = self._handle(frames, 1)
+        h = self._handle(frames)
         _lib.check(self._lib.omv_matcher_assign_grid(h, frames.n_frames, ctypes.byref(frames.geom),
                                                      _lib.ptr(frames.kps), _lib.ptr(frames.n_kp),
                                                      self._stream(stream)), "omv_matcher_assign_grid")
@@ -117,6 +119,9 @@ class ORBmatcher:
         _lib.check(self._lib.omv_matcher_stage_ms(self._h, _lib.ptr(ms), int(bool(reset))))
         return dict(zip(self.STAGES, ms.tolist()))
 
+    def last_error(self):
+        return self._lib.omv_matcher_last_error(self._h)
+
     def grid(self, frame, cam):
         cs = np.zeros(FRAME_GRID_COLS * FRAME_GRID_ROWS + 1, np.int32)
         idx = np.zeros(self._shape[2], np.int32)
@@ -125,7 +130,7 @@ class ORBmatcher:
 
     def StereoLapping(self, frames, ratio=0.8, stream=None):
         """Lowe-ratio knn candidates of ComputeMultiFishEyeMatches (before triangulation)."""
-        h = self._handle(frames, 1)
+        h = self._handle(frames)
         _lib.check(self._lib.omv_matcher_stereo_lapping(h, frames.n_frames, _lib.ptr(frames.desc),
                                                         _lib.ptr(frames.n_kp), _lib.ptr(frames.mono),
                                                         ctypes.c_double(ratio), _lib.ptr(frames.l2r),
@@ -135,6 +140,8 @@ class ORBmatcher:
     def SearchByProjection(self, frames, mps, th=3.0, bFarPoints=False, thFarPoints=50.0, stream=None,
                            grid_ready=False):
         """Returns the per-frame match counts (device tensor); mutates frames.kp_to_mp."""
+        if self._h is None or mps.M > self._shape[3]:
+            grid_ready = False   # a new workspace has no grid yet
         h = self._handle(frames, mps.M)
         if not grid_ready:
             self.AssignFeaturesToGrid(frames, stream)

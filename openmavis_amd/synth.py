@@ -49,27 +49,38 @@ def rig_frame(frame, n_cams, w, h, base_seed):
 
 def flip_bits(desc, rng, max_flips=8):
     """Copy of a (n,32) u8 descriptor array with U{0..max_flips} random bit flips per row."""
-    out = desc.copy()
     n = desc.shape[0]
+    out = desc.copy()
+    if n == 0:
+        return out
     nflip = rng.integers(0, max_flips + 1, n)
-    for i in range(n):
-        if nflip[i]:
-            bits = rng.choice(256, nflip[i], replace=False)
-            for b in bits:
-                out[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    order = np.argsort(rng.random((n, 256)), axis=1)[:, :max_flips]   # distinct bits per row
+    use = np.arange(max_flips)[None, :] < nflip[:, None]
+    rows = np.repeat(np.arange(n), max_flips)[use.ravel()]
+    bits = order.ravel()[use.ravel()]
+    np.bitwise_xor.at(out, (rows, bits >> 3), (1 << (bits & 7)).astype(np.uint8))
     return out
 
 
 def make_map_points(kps, desc, n_kp, M, seed, width, height, nlevels=8, frac_true=0.6):
     """Synthetic local map: `frac_true` of the points derive from true
     keypoints of the frame (descriptor with U{0..8} bit flips, projection = keypoint + N(0, 1 px),
-    level = octave), the rest are random.  Some points are also visible in a second camera so the
-    multi-camera claim / `continue` logic is exercised.  Inputs are host numpy arrays of one frame:
-    kps [C][cap] (KP dtype), desc [C][cap][32], n_kp [C].  Returns a dict of numpy arrays."""
+    level = octave), the rest are random.  30% of the points are also visible in a second, random
+    camera at a random position, so the multi-camera claim / `continue` logic is exercised.
+    Inputs are host numpy arrays of one frame: kps [C][cap] (KP dtype), desc [C][cap][32], n_kp [C].
+    Returns a dict of numpy arrays (the omv_mp_view fields)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     C = kps.shape[0]
+    n_kp = np.asarray(n_kp)
+    n_true = int(M * frac_true)
+    cam0 = rng.integers(0, C, M)
+    two = (rng.random(M) < 0.3) & (C > 1)
+    cam1 = rng.integers(0, C, M)
+    true = (np.arange(M) < n_true) & (n_kp[cam0] > 0)
+    kidx = np.minimum((rng.random(M) * np.maximum(n_kp[cam0], 1)).astype(np.int64), np.maximum(n_kp[cam0] - 1, 0))
+    src = kps[cam0, kidx]
     out = dict(
-        desc=np.zeros((M, 32), np.uint8),
+        desc=rng.integers(0, 256, (M, 32), dtype=np.uint8),
         proj_x=np.zeros((M, C), np.float32),
         proj_y=np.zeros((M, C), np.float32),
         view_cos=rng.uniform(0.99, 1.0, (M, C)).astype(np.float32),
@@ -79,25 +90,20 @@ def make_map_points(kps, desc, n_kp, M, seed, width, height, nlevels=8, frac_tru
         is_bad=(rng.random(M) < 0.02).astype(np.uint8),
         has_obs=(rng.random(M) > 0.03).astype(np.uint8),
     )
-    n_true = int(M * frac_true)
-    for m in range(M):
-        cams = [int(rng.integers(0, C))]
-        if rng.random() < 0.3 and C > 1:
-            cams.append(int(rng.integers(0, C)))
-        for j, c in enumerate(cams):
-            if m < n_true and n_kp[c] > 0 and j == 0:
-                i = int(rng.integers(0, n_kp[c]))
-                k = kps[c, i]
-                out["desc"][m] = desc[c, i]
-                out["proj_x"][m, c] = k["x"] + rng.normal(0.0, 1.0)
-                out["proj_y"][m, c] = k["y"] + rng.normal(0.0, 1.0)
-                out["level"][m, c] = k["octave"]
-            else:
-                if j == 0:
-                    out["desc"][m] = rng.integers(0, 256, 32, dtype=np.uint8)
-                out["proj_x"][m, c] = rng.uniform(0, width)
-                out["proj_y"][m, c] = rng.uniform(0, height)
-                out["level"][m, c] = int(rng.integers(0, nlevels))
-            out["in_view"][m, c] = 1
-    out["desc"][:n_true] = flip_bits(out["desc"][:n_true], rng)
+    ar = np.arange(M)
+    rx, ry = rng.uniform(0, width, M), rng.uniform(0, height, M)
+    rl = rng.integers(0, nlevels, M)
+    nx, ny = rng.normal(0.0, 1.0, M), rng.normal(0.0, 1.0, M)
+    out["proj_x"][ar, cam0] = np.where(true, src["x"] + nx, rx)
+    out["proj_y"][ar, cam0] = np.where(true, src["y"] + ny, ry)
+    out["level"][ar, cam0] = np.where(true, src["octave"], rl)
+    out["in_view"][ar, cam0] = 1
+    out["desc"][true] = flip_bits(desc[cam0[true], kidx[true]], rng)
+    sx, sy = rng.uniform(0, width, M), rng.uniform(0, height, M)
+    sl = rng.integers(0, nlevels, M)
+    m2 = two & (cam1 != cam0)
+    out["proj_x"][ar[m2], cam1[m2]] = sx[m2]
+    out["proj_y"][ar[m2], cam1[m2]] = sy[m2]
+    out["level"][ar[m2], cam1[m2]] = sl[m2]
+    out["in_view"][ar[m2], cam1[m2]] = 1
     return out

@@ -78,22 +78,40 @@ def _mps_for(frames, oracle, M, seed, torch):
     return per, MapPointBatch(**dev)
 
 
-@pytest.mark.parametrize("th,far,nnratio,occ_frac,obs_all", [
-    (6.0, False, 0.8, 0.0, False),
-    (1.0, False, 0.8, 0.0, True),
-    (3.0, True, 0.6, 0.05, False),
-    (15.0, False, 0.9, 0.02, True),
+@pytest.mark.parametrize("th,far,nnratio,occ_frac,obs,rand_stereo", [
+    (6.0, False, 0.8, 0.0, None, False),
+    (1.0, False, 0.8, 0.0, 1.0, False),
+    (3.0, True, 0.6, 0.05, None, False),
+    (15.0, False, 0.9, 0.02, 1.0, False),
+    # many points without observations + dense stereo links + occupied keypoints: exercises
+    # overwrites of blocked keypoints (unblocking) and freed initially-occupied keypoints
+    (6.0, False, 0.8, 0.25, 0.5, True),
+    (10.0, False, 1.0, 0.1, 0.0, True),
 ])
-def test_search_by_projection_matches_oracle(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs_all):
+def test_search_by_projection_matches_oracle(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs,
+                                             rand_stereo):
     torch = torch_cuda
     M = 5000
     per, mpb = _mps_for(frames, oracle, M, 7 + int(th), torch)
-    if obs_all:
-        mpb.has_obs.fill_(1)
-        for p in per:
-            p["has_obs"][:] = 1
+    rng0 = np.random.default_rng(int(th * 10) + int(occ_frac * 100))
+    if obs is not None:
+        for f, p in enumerate(per):
+            p["has_obs"][:] = (rng0.random(M) < obs).astype(np.uint8)
+        mpb.has_obs.copy_(torch.from_numpy(np.stack([p["has_obs"] for p in per])))
     m = ORBmatcher(nnratio)
     m.StereoLapping(frames, 0.8)
+    if rand_stereo:
+        _, _, n_kp, _ = host(frames, oracle)
+        l2r = np.full((frames.n_frames, frames.kp_cap), -1, np.int32)
+        r2l = np.full((frames.n_frames, frames.kp_cap), -1, np.int32)
+        for f in range(frames.n_frames):
+            n = min(n_kp[f, 0], n_kp[f, 1])
+            left = rng0.permutation(n_kp[f, 0])[: n // 2]
+            right = rng0.permutation(n_kp[f, 1])[: n // 2]
+            l2r[f, left] = right
+            r2l[f, right] = left
+        frames.l2r.copy_(torch.from_numpy(l2r))
+        frames.r2l.copy_(torch.from_numpy(r2l))
     rng = np.random.default_rng(11)
     S = C * frames.kp_cap
     occ = (rng.random((frames.n_frames, S)) < occ_frac).astype(np.uint8)
@@ -115,6 +133,7 @@ def test_search_by_projection_matches_oracle(frames, oracle, torch_cuda, th, far
         bad = np.nonzero(exp != got[f])[0]
         assert bad.size == 0, f"frame {f}: {bad.size} assignments differ, first slots {bad[:8]}"
         assert n > 300
+    assert m.last_error() == 0
     frames.occ_init = None
     frames.kp_to_mp.fill_(-1)
 
