@@ -128,6 +128,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
+    from openmavis_amd.dist import job_seconds
     from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher
     from openmavis_amd.orb import ORBextractor
 
@@ -179,11 +180,7 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = job_seconds(time.perf_counter() - t0, dev)   # max over ranks
     assert ex.last_error() == 0
     n_matches = int(fb.n_matches.sum().item())
 

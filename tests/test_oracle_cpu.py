@@ -1,0 +1,120 @@
+"""CPU tests of the oracle (test infrastructure): known-answer constants of the reference
+extractor, the committed golden fixtures, and matcher semantics."""
+import hashlib
+import math
+import os
+
+import numpy as np
+import pytest
+
+from openmavis_amd import synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_quota_and_umax_kats(oracle):
+    # per-level quotas (ORBextractor.cc:380-391) at the BASELINE configs
+    assert list(oracle.orb_tables(1200)["quota"]) == [261, 217, 181, 151, 126, 105, 87, 72]
+    assert list(oracle.orb_tables(1000)["quota"]) == [217, 181, 151, 126, 105, 87, 73, 60]
+    assert list(oracle.orb_tables(2000)["quota"]) == [434, 362, 302, 251, 209, 175, 145, 122]
+    assert list(oracle.orb_tables(500)["quota"]) == [109, 90, 75, 63, 52, 44, 36, 31]
+    # circular patch rows (ORBextractor.cc:399-413)
+    assert list(oracle.orb_tables(1200)["umax"]) == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    sc = oracle.orb_tables(1200)["scale"]
+    assert sc[0] == 1.0 and abs(sc[7] - 1.2 ** 7) < 1e-5
+    # scaled patch sizes (int)(31 * scale)
+    assert [int(np.float32(31) * s) for s in sc] == [31, 37, 44, 53, 64, 77, 92, 111]
+
+
+@pytest.mark.parametrize("w,h,sizes", [
+    (720, 540, [(720, 540), (600, 450), (500, 375), (417, 312), (347, 260), (289, 217), (241, 181), (201, 151)]),
+    (752, 480, [(752, 480), (627, 400), (522, 333), (435, 278), (363, 231), (302, 193), (252, 161), (210, 134)]),
+    (1920, 1080, [(1920, 1080), (1600, 900), (1333, 750), (1111, 625), (926, 521), (772, 434), (643, 362),
+                  (536, 301)]),
+])
+def test_level_geometry_kat(oracle, w, h, sizes):
+    img = np.zeros((h, w), np.uint8)
+    for l, (lw, lh) in enumerate(sizes):
+        assert oracle.pyramid_level(img, l).shape == (lh, lw)
+
+
+def test_fast_atan2_close_to_atan2(oracle):
+    rng = np.random.default_rng(0)
+    for y, x in rng.integers(-3_000_000, 3_000_000, (2000, 2)):
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        got = oracle.fast_atan2(float(y), float(x))
+        d = abs(got - ref)
+        assert min(d, 360 - d) < 0.02
+
+
+def _img_sha(img):
+    return hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["orb_hilti_720x540", "orb_euroc_752x480", "orb_side_320x240"])
+def test_oracle_matches_golden(oracle, name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    img = synth.synth_image(int(z["seed"]), int(z["w"]), int(z["h"]))
+    assert _img_sha(img) == str(z["image_sha256"]), "synthetic image generator changed"
+    mono, kps, desc = oracle.orb_extract(img, int(z["nfeatures"]), 1.2, 8, int(z["ini"]), int(z["mn"]),
+                                         tuple(z["lapping"]))
+    assert mono == int(z["mono"])
+    assert np.array_equal(kps.view(np.uint32).reshape(-1, 6), z["kps"])
+    assert np.array_equal(desc, z["desc"])
+
+
+def test_matcher_golden(oracle):
+    z = np.load(os.path.join(GOLD, "match_hilti_frame0.npz"))
+    kps = z["kps"].view(oracle.KP_DTYPE).reshape(z["kps"].shape[:2])
+    desc = z["desc"]
+    mono, n_kp = z["mono"], z["n_kp"]
+    i2, d2 = oracle.bf_knn2(desc[0, mono[0]:n_kp[0]], desc[1, mono[1]:n_kp[1]])
+    assert np.array_equal(i2, z["knn_idx"]) and np.array_equal(d2, z["knn_dist"])
+    mp = {k[3:]: z[k] for k in z.files if k.startswith("mp_")}
+    g = oracle.frame_geom(5, 720, 540, oracle.orb_tables(1200)["scale"])
+    k2m = np.full(z["kp_to_mp"].shape, -1, np.int32)
+    n = oracle.search_by_projection(g, kps, desc, n_kp, mp, 6.0, False, 50.0, 0.8, z["l2r"], z["r2l"], None, k2m)
+    assert n == int(z["n_matches"]) and np.array_equal(k2m, z["kp_to_mp"])
+
+
+def test_knn_ties_first_index_wins(oracle):
+    a = np.zeros((1, 32), np.uint8)
+    t = np.zeros((4, 32), np.uint8)
+    t[0, 0] = 1          # dist 1
+    t[2, 0] = 1          # dist 1 (tie, later)
+    t[1, :] = 255        # dist 256
+    t[3, 1] = 3          # dist 2
+    i2, d2 = oracle.bf_knn2(a, t)
+    assert list(i2[0]) == [0, 2] and list(d2[0]) == [1, 1]
+    i2, d2 = oracle.bf_knn2(a, t[:1])
+    assert list(i2[0]) == [0, -1] and d2[0, 1] == 2 ** 31 - 1
+
+
+def test_grid_excludes_right_border_and_keeps_order(oracle):
+    # PosInGrid rounds (x - minX) * 64 / 720: x > 714.375 lands in column 64 -> not in the grid
+    kp = np.zeros((1, 4), oracle.KP_DTYPE)
+    kp[0, 0] = (719.0, 10.0, 31, 0, 20, 0)
+    kp[0, 1] = (5.0, 5.0, 31, 0, 20, 0)
+    kp[0, 2] = (5.2, 5.1, 31, 0, 20, 1)
+    kp[0, 3] = (714.0, 10.0, 31, 0, 20, 0)
+    g = oracle.frame_geom(1, 720, 540, oracle.orb_tables(1200)["scale"])
+    cs, idx = oracle.grid(g, kp, np.array([4], np.int32), 0)
+    assert cs[-1] == 3 and 0 not in idx
+    c = 0 * 48 + 0
+    assert list(idx[cs[c]:cs[c + 1]]) == [1, 2]
+    # window: square, strict |dx| < r, level filter [minLevel, maxLevel]
+    assert list(oracle.features_in_area(g, kp, np.array([4], np.int32), 5.0, 5.0, 0.5, 0, 0, 0)) == [1]
+    assert list(oracle.features_in_area(g, kp, np.array([4], np.int32), 5.0, 5.0, 0.5, -1, 1, 0)) == [1, 2]
+
+
+def test_map_point_generator_is_seeded():
+    imgs = synth.hilti_frame(0)
+    assert imgs.shape == (5, 540, 720) and imgs.dtype == np.uint8
+    kps = np.zeros((5, 10), [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                             ("response", "<f4"), ("octave", "<i4")])
+    desc = np.random.default_rng(0).integers(0, 256, (5, 10, 32), dtype=np.uint8)
+    a = synth.make_map_points(kps, desc, np.full(5, 10), 100, 9, 720, 540)
+    b = synth.make_map_points(kps, desc, np.full(5, 10), 100, 9, 720, 540)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
+    assert (a["in_view"].sum(1) >= 1).all()

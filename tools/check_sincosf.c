@@ -1,3 +1,6 @@
+/* Exhaustive check that the glibc 2.35 sinf/cosf restatement (same constants and fma placement as
+ * openmavis_amd/csrc/omv_device.h::glibc_sincosf) is bit-identical to the host libm over every float
+ * in [0, 2*pi].  gcc -O2 -ffp-contract=off -DUSEFMA tools/check_sincosf.c -lm && ./a.out */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -28,8 +31,11 @@ float mycos(float y){ double x=y; const tab_t*p=&T[0]; int n;
 float mysin(float y){ double x=y; const tab_t*p=&T[0]; int n;
   if(top12(y)<top12(0x1.921FB6p-1f)){ if(top12(y)<top12(0x1p-12f)) return y; return poly(x,x*x,p,0);}
   x=red(x,p,&n); double s=p->sign[n&3]; if(n&2) p=&T[1]; return poly(x*s,x*x,p,n);}
+#ifndef STRIDE
+#define STRIDE 1
+#endif
 int main(){ long bc=0,bs=0,tot=0; float lim=6.2831855f; uint32_t u0=0, u1; memcpy(&u1,&lim,4);
- for(uint32_t u=u0; u<=u1; u++){ float x; memcpy(&x,&u,4); tot++;
+ for(uint32_t u=u0; u<=u1; u+=STRIDE){ float x; memcpy(&x,&u,4); tot++;
    volatile float c=cosf(x), s=sinf(x); float mc=mycos(x), ms=mysin(x);
    if(memcmp((const void*)&c,&mc,4)) { if(bc<5) printf("cos mismatch %a %a %a\n",x,c,mc); bc++;}
    if(memcmp((const void*)&s,&ms,4)) { if(bs<5) printf("sin mismatch %a %a %a\n",x,s,ms); bs++;} }
