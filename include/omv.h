@@ -169,6 +169,82 @@ omv_status omv_matcher_stage_ms(omv_matcher *m, double *ms4, int reset);
 omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *nq, const uint8_t *train, int t_cap,
                        const int *nt, int32_t *idx2, int32_t *dist2, void *stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Local inertial bundle adjustment — replaces the optimisation inside Optimizer::LocalInertialBA
+ * (src/Optimizer.cc:2728-3385): EdgeMono / EdgeInertial / EdgeGyroRW / EdgeAccRW
+ * (src/G2oTypes.cc, include/G2oTypes.h:283-633), g2o's Levenberg-Marquardt
+ * (Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-169) with the landmark Schur
+ * complement (block_solver.hpp:353-486).  The host adapter flattens the KeyFrame/MapPoint graph
+ * (window selection, vertex ids, edge creation stay host-side, :2740-3267) into this problem and
+ * writes the state back unless status == OMV_LBA_FAIL (the reference's FAIL guard, :3317-3321).
+ * ---------------------------------------------------------------------------------------------- */
+/* Per inertial edge: IMU::Preintegrated members in float, in this order:
+ *   dR[9] dV[3] dP[3] JRg[9] JVg[9] JVa[9] JPg[9] JPa[9] b[6] (bax bay baz bwx bwy bwz) dT[1] C[225]
+ * (3x3 / 15x15 row-major).  Information matrices are derived from C like EdgeInertial's ctor. */
+#define OMV_PREINT_FLOATS 292
+#define OMV_LBA_OK 0
+#define OMV_LBA_FAIL 1   /* (2*err < err_end || isnan) && !bLarge: the reference discards the result */
+
+typedef struct omv_lba_problem {
+    int n_cams;
+    const float *cam;          /* [n_cams][8] KannalaBrandt8 mvParameters: fx fy cx cy k1 k2 k3 k4 */
+    const double *Rcb, *tcb;   /* [n_cams][9] row-major, [n_cams][3]: body -> camera (ImuCamPose) */
+    const double *Rbc, *tbc;   /* [n_cams][9], [n_cams][3]: camera -> body */
+    int n_kf;                  /* KeyFrame vertices; the first n_opt are optimisable, the rest fixed */
+    int n_opt;
+    const uint8_t *kf_imu;     /* [n_kf] KeyFrame::bImu: velocity / gyro / acc bias vertices exist */
+    double *Rwb, *twb;         /* [n_kf][9], [n_kf][3] body pose (in/out) */
+    double *Rcw, *tcw;         /* [n_kf][n_cams][9], [n_kf][n_cams][3] camera poses (in/out) */
+    double *vel, *bg, *ba;     /* [n_kf][3] (in/out) */
+    int n_pts;
+    double *pts;               /* [n_pts][3] world points (in/out) */
+    const float *pt_track_depth;   /* [n_pts] MapPoint::mTrackDepth (bClose = < 10 m, :3284) */
+    int n_mono;
+    const int32_t *mono_pt, *mono_kf, *mono_cam;   /* [n_mono] */
+    const double *mono_obs;    /* [n_mono][2] keypoint (u, v) */
+    const float *mono_inv_sigma2;  /* [n_mono] information = I * invSigma2 / uncertainty2 */
+    int n_imu;                 /* inertial edges; each also carries one EdgeGyroRW and one EdgeAccRW */
+    const int32_t *imu_kf1, *imu_kf2;
+    const float *preint;       /* [n_imu][OMV_PREINT_FLOATS] */
+    const uint8_t *imu_robust; /* Huber sqrt(16.92) on this inertial edge (last one / bRecInit) */
+    const float *imu_info_scale;   /* 1, or 1e-2 on the last edge of the window (:2986) */
+} omv_lba_problem;
+
+typedef struct omv_lba_opts {
+    int opt_it;            /* 10, or 4 when bLarge */
+    double lambda_init;    /* setUserLambdaInit: 1e0, or 1e-2 when bLarge */
+    int max_trials;        /* maxTrialsAfterFailure (10) */
+    int large;             /* bLarge: disables the FAIL guard */
+} omv_lba_opts;
+
+typedef struct omv_lba_result {
+    float err, err_end;    /* activeRobustChi2 before / after optimize(), as floats like the reference */
+    int status;            /* OMV_LBA_OK / OMV_LBA_FAIL */
+    int iterations;        /* LM iterations run (solve() calls) */
+    int trials;            /* LM trials (linear solves) in total */
+    double lambda;         /* final lambda */
+    double *mono_chi2;     /* optional [n_mono]: e->chi2() after optimize (may be NULL) */
+    uint8_t *mono_outlier; /* optional [n_mono]: the :3282-3296 outlier test (may be NULL) */
+} omv_lba_result;
+
+typedef struct omv_lba omv_lba;
+
+/* Workspace for problems up to the given sizes. */
+omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, int max_imu, omv_lba **out);
+omv_status omv_lba_destroy(omv_lba *h);
+/* Upload a problem (host arrays); the structure (point -> keyframe slots, reduced-system layout,
+ * block fill pattern) is analysed on the host once here. */
+omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p);
+/* Run the optimisation on the uploaded problem; on return the state arrays of `p` (Rwb, twb, Rcw,
+ * tcw, vel, bg, ba, pts) hold the optimised state and `r` the outcome.  Synchronous. */
+omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *r);
+/* Residual/Jacobian evaluation at the uploaded state for parity: mono_err [n_mono][2],
+ * mono_jx [n_mono][6] (2x3), mono_jp [n_mono][12] (2x6), imu_err [n_imu][9] (any may be NULL). */
+omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err);
+/* Per-stage device time of the last optimize: 0 linearise+build, 1 Schur, 2 reduced solve,
+ * 3 back-substitution+update+errors; plus the number of trials. */
+omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials);
+
 #ifdef __cplusplus
 }
 #endif

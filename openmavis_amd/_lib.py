@@ -48,6 +48,32 @@ class MpView(ctypes.Structure):
                 ("track_depth", ctypes.c_void_p), ("is_bad", ctypes.c_void_p), ("has_obs", ctypes.c_void_p)]
 
 
+class LbaProblem(ctypes.Structure):
+    """omv_lba_problem (include/omv.h)."""
+    _fields_ = [("n_cams", ctypes.c_int), ("cam", ctypes.c_void_p), ("Rcb", ctypes.c_void_p),
+                ("tcb", ctypes.c_void_p), ("Rbc", ctypes.c_void_p), ("tbc", ctypes.c_void_p),
+                ("n_kf", ctypes.c_int), ("n_opt", ctypes.c_int), ("kf_imu", ctypes.c_void_p),
+                ("Rwb", ctypes.c_void_p), ("twb", ctypes.c_void_p), ("Rcw", ctypes.c_void_p),
+                ("tcw", ctypes.c_void_p), ("vel", ctypes.c_void_p), ("bg", ctypes.c_void_p),
+                ("ba", ctypes.c_void_p), ("n_pts", ctypes.c_int), ("pts", ctypes.c_void_p),
+                ("pt_track_depth", ctypes.c_void_p), ("n_mono", ctypes.c_int), ("mono_pt", ctypes.c_void_p),
+                ("mono_kf", ctypes.c_void_p), ("mono_cam", ctypes.c_void_p), ("mono_obs", ctypes.c_void_p),
+                ("mono_inv_sigma2", ctypes.c_void_p), ("n_imu", ctypes.c_int), ("imu_kf1", ctypes.c_void_p),
+                ("imu_kf2", ctypes.c_void_p), ("preint", ctypes.c_void_p), ("imu_robust", ctypes.c_void_p),
+                ("imu_info_scale", ctypes.c_void_p)]
+
+
+class LbaOpts(ctypes.Structure):
+    _fields_ = [("opt_it", ctypes.c_int), ("lambda_init", ctypes.c_double), ("max_trials", ctypes.c_int),
+                ("large", ctypes.c_int)]
+
+
+class LbaResult(ctypes.Structure):
+    _fields_ = [("err", ctypes.c_float), ("err_end", ctypes.c_float), ("status", ctypes.c_int),
+                ("iterations", ctypes.c_int), ("trials", ctypes.c_int), ("lambda_", ctypes.c_double),
+                ("mono_chi2", ctypes.c_void_p), ("mono_outlier", ctypes.c_void_p)]
+
+
 # numpy dtype with the omv_kp layout (24 bytes)
 try:
     import numpy as _np
@@ -82,6 +108,12 @@ SIGNATURES = {
                                            _VP, _VP]),
     "omv_matcher_stereo_lapping": (_I, [_VP, _I, _VP, _VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
     "omv_bf_knn2": (_I, [_I, _VP, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP]),
+    "omv_lba_create": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(_VP)]),
+    "omv_lba_destroy": (_I, [_VP]),
+    "omv_lba_set_problem": (_I, [_VP, ctypes.POINTER(LbaProblem)]),
+    "omv_lba_optimize": (_I, [_VP, ctypes.POINTER(LbaOpts), ctypes.POINTER(LbaProblem), ctypes.POINTER(LbaResult)]),
+    "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
 }
 
 _lib = None

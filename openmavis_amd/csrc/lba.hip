@@ -1,0 +1,1663 @@
+// MI355X-native LocalInertialBA inner loop (Optimizer::LocalInertialBA's optimize(),
+// src/Optimizer.cc:3270-3321): g2o's Levenberg-Marquardt over EdgeMono / EdgeInertial / EdgeGyroRW /
+// EdgeAccRW with the landmark Schur complement, as batched gfx950 kernels on device-resident state.
+//
+// Per LM iteration (optimization_algorithm_levenberg.cpp:61-169):
+//   errors   1 thread / visual edge (+1 thread / inertial edge): residual, chi2, Huber rho; deterministic
+//            two-level chi2 reduction (computeActiveErrors + activeRobustChi2)
+//   build    1 thread / landmark (edges sorted landmark-major): EdgeMono Jacobians, the landmark's
+//            Hll / bl and per-keyframe Hpl blocks in registers; the pose-diagonal JpT W Jp terms are
+//            reduced in LDS per workgroup (landmarks are ordered by keyframe window, so a workgroup
+//            touches a few keyframes) and flushed with f64 atomics into the dense reduced matrix;
+//            1 wavefront / inertial edge for the 9x24 Jacobian and its 24x24 quadratic form
+//   per trial (lambda):
+//     schur    1 thread / landmark: Dinv = (Hll + lambda I)^-1, Hpl Dinv Hpl^T into the reduced
+//              system (LDS pre-reduction again), coefficients Hpl Dinv bl
+//     ldlt     1 workgroup: block LDL^T of the reduced system (keyframe blocks of 15 / 6) on the
+//              symbolic block pattern (host-computed fill-in), the nonzero blocks staged in LDS,
+//              then block forward / backward substitution (SimplicialLDLT semantics: no pivoting,
+//              failure on a zero or non-finite pivot)
+//     update   1 thread / landmark: back-substitution xl = Dinv (bl - Hpl^T xp) and the point update;
+//              1 thread / keyframe: ImuCamPose::Update (body-frame SE3 with ExpSO3) + v, bg, ba;
+//              the step's computeScale term; errors of the trial state
+//   The accept / reject decision (rho, lambda schedule, push/pop) runs on the host from two scalars
+//   per trial, exactly as the reference; push/pop is a double-buffered state.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <numeric>
+#include <set>
+#include <vector>
+
+#include "../../include/omv.h"
+#include "omv_device.h"
+
+namespace {
+
+constexpr int kMaxCams = 8;
+constexpr int kSpan = 8;          // keyframes a workgroup may touch for LDS pre-reduction
+constexpr int kPF = OMV_PREINT_FLOATS;
+
+#define HIP_OK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "omv: %s failed: %s\n", #x, hipGetErrorString(e_));      \
+            return OMV_ERR_HIP;                                                      \
+        }                                                                            \
+    } while (0)
+
+// ---- glibc atan2f (fdlibm e_atan2f.c / s_atanf.c), float, no contraction --------------------------
+// KannalaBrandt8::project(Vector3d) computes theta / psi with atan2f (KannalaBrandt8.cpp:30-31); this
+// restatement is bit-identical to the host libm (tests/test_native_cpu.py sweeps it).
+__device__ __forceinline__ uint32_t fb(float f) { return __float_as_uint(f); }
+__device__ float glibc_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float aT[11] = {3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                          9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                          4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f};
+    const int32_t hx = (int32_t)fb(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) id = 0, x = (2.0f * x - 1.0f) / (2.0f + x);
+            else id = 1, x = (x - 1.0f) / (x + 1.0f);
+        } else {
+            if (ix < 0x401c0000) id = 2, x = (x - 1.5f) / (1.0f + 1.5f * x);
+            else id = 3, x = -1.0f / x;
+        }
+    }
+    const float z = x * x, w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+__device__ float glibc_atan2f(float y, float x) {
+    const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+                pi_lo = -8.7422776573e-08f, tiny = 1.0e-30f;
+    const int32_t hx = (int32_t)fb(x), ix = hx & 0x7fffffff, hy = (int32_t)fb(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return glibc_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        if (m < 2) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            const float r[4] = {pi_o_4 + tiny, -pi_o_4 - tiny, 3.0f * pi_o_4 + tiny, -3.0f * pi_o_4 - tiny};
+            return r[m];
+        }
+        const float r[4] = {0.0f, -0.0f, pi + tiny, -pi - tiny};
+        return r[m];
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = glibc_atanf(fabsf(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return __uint_as_float(fb(z) ^ 0x80000000u);
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// Correctly rounded f32 sqrt (libm sqrtf): v_sqrt_f32 alone is 1 ulp; the f64 sqrt is correctly
+// rounded and 53 >= 2*24+2 bits make the second rounding innocuous.
+__device__ __forceinline__ float sqrtf_cr(float x) { return (float)sqrt((double)x); }
+
+// ---- small f64 helpers (row-major 3x3) ----------------------------------------------------------
+struct D3 {
+    double v[3];
+};
+__device__ __forceinline__ void mv3(const double *R, const double *x, double *y) {
+    for (int i = 0; i < 3; ++i) y[i] = R[3 * i] * x[0] + R[3 * i + 1] * x[1] + R[3 * i + 2] * x[2];
+}
+__device__ __forceinline__ void mtv3(const double *R, const double *x, double *y) {   // R^T x
+    for (int i = 0; i < 3; ++i) y[i] = R[i] * x[0] + R[3 + i] * x[1] + R[6 + i] * x[2];
+}
+__device__ __forceinline__ void mm3(const double *a, const double *b, double *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+__device__ __forceinline__ void mtm3(const double *a, const double *b, double *r) {   // a^T b
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[i] * b[j] + a[3 + i] * b[3 + j] + a[6 + i] * b[6 + j];
+}
+__device__ __forceinline__ void tr3(const double *a, double *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * j + i];
+}
+__device__ __forceinline__ void hat3(const double *w, double *W) {
+    W[0] = 0, W[1] = -w[2], W[2] = w[1], W[3] = w[2], W[4] = 0, W[5] = -w[0], W[6] = -w[1], W[7] = w[0], W[8] = 0;
+}
+template <typename T>
+__host__ __device__ inline bool inv3(const T *a, T *r) {
+    T c[9];
+    c[0] = a[4] * a[8] - a[5] * a[7];
+    c[1] = a[2] * a[7] - a[1] * a[8];
+    c[2] = a[1] * a[5] - a[2] * a[4];
+    c[3] = a[5] * a[6] - a[3] * a[8];
+    c[4] = a[0] * a[8] - a[2] * a[6];
+    c[5] = a[2] * a[3] - a[0] * a[5];
+    c[6] = a[3] * a[7] - a[4] * a[6];
+    c[7] = a[1] * a[6] - a[0] * a[7];
+    c[8] = a[0] * a[4] - a[1] * a[3];
+    const T det = a[0] * c[0] + a[1] * c[3] + a[2] * c[6];
+    const T id = T(1) / det;
+    for (int k = 0; k < 9; ++k) r[k] = c[k] * id;
+    return det != T(0);
+}
+// NormalizeRotation (Eigen JacobiSVD U V^T) = polar factor, by Newton iteration X <- (X + X^-T)/2
+template <typename T>
+__host__ __device__ inline void polar3(T *r) {
+    for (int it = 0; it < 20; ++it) {
+        T c[9];
+        c[0] = r[4] * r[8] - r[5] * r[7];
+        c[1] = r[5] * r[6] - r[3] * r[8];
+        c[2] = r[3] * r[7] - r[4] * r[6];
+        c[3] = r[2] * r[7] - r[1] * r[8];
+        c[4] = r[0] * r[8] - r[2] * r[6];
+        c[5] = r[1] * r[6] - r[0] * r[7];
+        c[6] = r[1] * r[5] - r[2] * r[4];
+        c[7] = r[2] * r[3] - r[0] * r[5];
+        c[8] = r[0] * r[4] - r[1] * r[3];
+        const T det = r[0] * c[0] + r[1] * c[1] + r[2] * c[2];
+        T diff = 0;
+        for (int k = 0; k < 9; ++k) {
+            const T nv = (r[k] + c[k] / det) * T(0.5);
+            const T dd = nv > r[k] ? nv - r[k] : r[k] - nv;
+            diff = dd > diff ? dd : diff;
+            r[k] = nv;
+        }
+        if (diff == T(0)) break;
+    }
+}
+
+// ---- camera + pose math -------------------------------------------------------------------------
+struct Rig {
+    int n_cams;
+    float cam[kMaxCams][8];
+    double Rcb[kMaxCams][9], tcb[kMaxCams][3], Rbc[kMaxCams][9], tbc[kMaxCams][3];
+};
+
+// KannalaBrandt8::project(const Eigen::Vector3d&) (KannalaBrandt8.cpp:28-46)
+__device__ __forceinline__ void kb8_project(const float *k, const double *X, double &u, double &v) {
+    const double x2y2 = X[0] * X[0] + X[1] * X[1];
+    const double theta = glibc_atan2f(sqrtf_cr((float)x2y2), (float)X[2]);
+    const double psi = glibc_atan2f((float)X[1], (float)X[0]);
+    const double t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const double r = theta + (double)k[4] * t3 + (double)k[5] * t5 + (double)k[6] * t7 + (double)k[7] * t9;
+    u = (double)k[0] * r * cos(psi) + (double)k[2];
+    v = (double)k[1] * r * sin(psi) + (double)k[3];
+}
+// KannalaBrandt8::projectJac (:128-158), 2x3 row-major
+__device__ __forceinline__ void kb8_jac(const float *k, const double *X, double *J) {
+    const double x2 = X[0] * X[0], y2 = X[1] * X[1], z2 = X[2] * X[2];
+    const double r2 = x2 + y2, r = sqrt(r2), r3 = r2 * r;
+    const double theta = atan2(r, X[2]);
+    const double t2 = theta * theta, t3 = t2 * theta, t4 = t2 * t2, t5 = t4 * theta, t6 = t2 * t4, t7 = t6 * theta,
+                 t8 = t4 * t4, t9 = t8 * theta;
+    const double k4 = k[4], k5 = k[5], k6 = k[6], k7 = k[7];
+    const double f = theta + t3 * k4 + t5 * k5 + t7 * k6 + t9 * k7;
+    const double fd = 1 + 3 * k4 * t2 + 5 * k5 * t4 + 7 * k6 * t6 + 9 * k7 * t8;
+    const double q = r2 * (r2 + z2);
+    J[0] = (double)k[0] * (fd * X[2] * x2 / q + f * y2 / r3);
+    J[3] = (double)k[1] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
+    J[1] = (double)k[0] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
+    J[4] = (double)k[1] * (fd * X[2] * y2 / q + f * x2 / r3);
+    J[2] = -(double)k[0] * fd * X[0] / (r2 + z2);
+    J[5] = -(double)k[1] * fd * X[1] / (r2 + z2);
+}
+
+struct State {   // one of the two state buffers
+    double *Rwb, *twb, *Rcw, *tcw, *vel, *bg, *ba, *pts;
+};
+
+struct Edges {   // landmark-major visual edges
+    const int32_t *pt, *kf, *cam, *slot;
+    const double *obs;
+    const float *w;   // invSigma2
+    int n;
+};
+
+// Huber (robust_kernel_impl.cpp:78-91)
+__device__ __forceinline__ void huber(double e2, double delta, double dsqr, double &r0, double &r1) {
+    if (e2 <= dsqr) {
+        r0 = e2, r1 = 1.0;
+    } else {
+        const double s = sqrt(e2);
+        r0 = 2 * s * delta - dsqr;
+        r1 = delta / s;
+    }
+}
+
+// ---- errors ------------------------------------------------------------------------------------
+__device__ double block_reduce_sum(double v, double *sh) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0;
+    for (int q = 0; q < nw; ++q) t += sh[q];
+    return t;
+}
+
+__global__ void __launch_bounds__(256) mono_err_kernel(Rig rig, State s, Edges E, double delta, double dsqr,
+                                                       double *err, double *chi2, double *partial) {
+    __shared__ double sh[8];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double r0 = 0;
+    if (e < E.n) {
+        const int k = E.kf[e], c = E.cam[e], C = rig.n_cams;
+        const double *R = s.Rcw + ((size_t)k * C + c) * 9, *t = s.tcw + ((size_t)k * C + c) * 3;
+        const double *X = s.pts + (size_t)E.pt[e] * 3;
+        double Xc[3];
+        mv3(R, X, Xc);
+        Xc[0] += t[0], Xc[1] += t[1], Xc[2] += t[2];
+        double u, v;
+        kb8_project(rig.cam[c], Xc, u, v);
+        const double e0 = E.obs[2 * e] - u, e1 = E.obs[2 * e + 1] - v;
+        const double w = (double)E.w[e];
+        const double c2 = e0 * w * e0 + e1 * w * e1;
+        err[2 * e] = e0, err[2 * e + 1] = e1;
+        chi2[e] = c2;
+        double r1;
+        huber(c2, delta, dsqr, r0, r1);
+    }
+    const double t = block_reduce_sum(r0, sh);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+struct Imu {
+    int n;
+    const int32_t *kf1, *kf2;
+    const float *pre;        // [n][kPF]
+    const double *info9;     // [n][81] (scaled)
+    const double *infoG, *infoA;   // [n][9]
+    const uint8_t *robust;
+    const int *offP, *offV, *offG, *offA;   // per keyframe, -1 if not in the reduced system
+};
+
+// IMU::Preintegrated::GetDeltaRotation/Velocity/Position (ImuTypes.cc:288-309) in float
+__device__ void so3f_exp(const float *w, float *R) {
+    const float theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    float imag, real;
+    if (theta_sq < 1e-5f * 1e-5f) {
+        const float t4 = theta_sq * theta_sq;
+        imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * t4;
+        real = 1.0f - (float)(1.0 / 8.0) * theta_sq + (float)(1.0 / 384.0) * t4;
+    } else {
+        const float theta = sqrtf_cr(theta_sq);
+        const float half = 0.5f * theta;
+        float sh, ch;
+        omv::glibc_sincosf(half, &sh, &ch);
+        imag = sh / theta;
+        real = ch;
+    }
+    const float qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    R[0] = 1.0f - (tyy + tzz), R[1] = txy - twz, R[2] = txz + twy;
+    R[3] = txy + twz, R[4] = 1.0f - (txx + tzz), R[5] = tyz - twx;
+    R[6] = txz - twy, R[7] = tyz + twx, R[8] = 1.0f - (txx + tyy);
+}
+__device__ void f33mulv(const float *a, const float *x, float *r) {
+    for (int i = 0; i < 3; ++i) r[i] = a[3 * i] * x[0] + a[3 * i + 1] * x[1] + a[3 * i + 2] * x[2];
+}
+struct PreView {   // offsets inside one preintegration record
+    static constexpr int dR = 0, dV = 9, dP = 12, JRg = 15, JVg = 24, JVa = 33, JPg = 42, JPa = 51, b = 60, dT = 66,
+                         C = 67;
+};
+__device__ void delta_rot(const float *p, const float *b1, double *dR) {
+    const float dbg[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    float w[3], E[9], R[9];
+    f33mulv(p + PreView::JRg, dbg, w);
+    so3f_exp(w, E);
+    const float *A = p + PreView::dR;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = A[3 * i] * E[j] + A[3 * i + 1] * E[3 + j] + A[3 * i + 2] * E[6 + j];
+    polar3(R);
+    for (int q = 0; q < 9; ++q) dR[q] = (double)R[q];
+}
+__device__ void delta_vp(const float *p, int d, int jg, int ja, const float *b1, double *out) {
+    const float dbg[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    const float dba[3] = {b1[0] - p[PreView::b], b1[1] - p[PreView::b + 1], b1[2] - p[PreView::b + 2]};
+    float g[3], a[3];
+    f33mulv(p + jg, dbg, g);
+    f33mulv(p + ja, dba, a);
+    for (int q = 0; q < 3; ++q) out[q] = (double)((p[d + q] + g[q]) + a[q]);
+}
+__device__ void log_so3(const double *R, double *w) {
+    const double t = R[0] + R[4] + R[8];
+    w[0] = (R[7] - R[5]) / 2, w[1] = (R[2] - R[6]) / 2, w[2] = (R[3] - R[1]) / 2;
+    const double costheta = (t - 1.0) * 0.5f;
+    if (costheta > 1 || costheta < -1) return;
+    const double theta = acos(costheta);
+    const double s = sin(theta);
+    if (fabs(s) < 1e-5) return;
+    for (int q = 0; q < 3; ++q) w[q] = theta * w[q] / s;
+}
+
+// EdgeInertial::computeError (G2oTypes.cc:502-531)
+__device__ void imu_error(const State &s, const Imu &I, int i, double *e) {
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const float *p = I.pre + (size_t)i * kPF;
+    float b1[6];
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+    double dR[9], dV[3], dP[3];
+    delta_rot(p, b1, dR);
+    delta_vp(p, PreView::dV, PreView::JVg, PreView::JVa, b1, dV);
+    delta_vp(p, PreView::dP, PreView::JPg, PreView::JPa, b1, dP);
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    const double *R1 = s.Rwb + 9 * k1, *R2 = s.Rwb + 9 * k2;
+    double A[9], B[9];
+    double R1t[9];
+    tr3(R1, R1t);
+    double dRt[9];
+    tr3(dR, dRt);
+    mm3(dRt, R1t, A);
+    mm3(A, R2, B);
+    log_so3(B, e);
+    double t[3];
+    for (int q = 0; q < 3; ++q) t[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+    double ev[3];
+    mtv3(R1, t, ev);
+    for (int q = 0; q < 3; ++q) e[3 + q] = ev[q] - dV[q];
+    for (int q = 0; q < 3; ++q)
+        t[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - g[q] * dt * dt / 2;
+    mtv3(R1, t, ev);
+    for (int q = 0; q < 3; ++q) e[6 + q] = ev[q] - dP[q];
+}
+
+__global__ void imu_err_kernel(State s, Imu I, double delta, double dsqr, double *err9, double *partial) {
+    __shared__ double sh[8];
+    const int i = threadIdx.x;
+    double r0 = 0;
+    if (i < I.n) {
+        double e[9];
+        imu_error(s, I, i, e);
+        const double *W = I.info9 + (size_t)i * 81;
+        double c2 = 0;
+        for (int r = 0; r < 9; ++r) {
+            double t = 0;
+            for (int c = 0; c < 9; ++c) t += W[r * 9 + c] * e[c];
+            c2 += e[r] * t;
+        }
+        for (int q = 0; q < 9; ++q) err9[9 * i + q] = e[q];
+        err9[(size_t)9 * I.n + i] = c2;   // chi2 after the errors
+        if (I.robust[i]) {
+            double r1;
+            huber(c2, delta, dsqr, r0, r1);
+        } else {
+            r0 = c2;
+        }
+        const int k1 = I.kf1[i], k2 = I.kf2[i];
+        double eg[3], ea[3];
+        for (int q = 0; q < 3; ++q) eg[q] = s.bg[3 * k2 + q] - s.bg[3 * k1 + q], ea[q] = s.ba[3 * k2 + q] - s.ba[3 * k1 + q];
+        double tg[3], ta[3];
+        mv3(I.infoG + 9 * i, eg, tg);
+        mv3(I.infoA + 9 * i, ea, ta);
+        r0 += eg[0] * tg[0] + eg[1] * tg[1] + eg[2] * tg[2];
+        r0 += ea[0] * ta[0] + ea[1] * ta[1] + ea[2] * ta[2];
+    }
+    const double t = block_reduce_sum(r0, sh);
+    if (threadIdx.x == 0) partial[0] = t;
+}
+
+// Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
+__global__ void __launch_bounds__(256) finish_kernel(const double *mono_partial, int n_mono_blocks, const double *imu_partial,
+                                                     const double *scale_partial, int n_scale, double *out) {
+    __shared__ double sh[8];
+    double v = 0;
+    for (int i = threadIdx.x; i < n_mono_blocks; i += blockDim.x) v += mono_partial[i];
+    double t = block_reduce_sum(v, sh);
+    double s = 0;
+    for (int i = threadIdx.x; i < n_scale; i += blockDim.x) s += scale_partial[i];
+    __syncthreads();
+    const double st = block_reduce_sum(s, sh);
+    if (threadIdx.x == 0) {
+        out[0] = imu_partial[0] + t;   // activeRobustChi2
+        out[1] = st;                   // computeScale
+    }
+}
+
+// ---- build: landmark part ---------------------------------------------------------------------
+struct Land {
+    const int *edge_start;   // [P+1]
+    const int *slot_start;   // [P+1]
+    const int *slot_kf;      // [nslots]
+    const int *wg_kf0;       // [n_wg] first keyframe of the workgroup's span, or -1 (span too wide)
+    double *Hll;             // [P][9]
+    double *bl;              // [P][3]
+    double *Hpl;             // [nslots][18] pose rows x point cols
+    int n;
+};
+
+struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lower triangle used
+    double *H, *b;
+    int n;
+    const int *offP;   // per keyframe, -1 for fixed
+    int n_kf;
+};
+
+// LDS accumulators of a workgroup: kSpan keyframes x (36 + 6)
+__global__ void __launch_bounds__(256) build_land_kernel(Rig rig, State s, Edges E, Land L, Red R, double delta,
+                                                         double dsqr, const double *err, const double *chi2) {
+    __shared__ double acc[kSpan * 42];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int kf0 = L.wg_kf0[blockIdx.x];
+    for (int q = threadIdx.x; q < kSpan * 42; q += blockDim.x) acc[q] = 0;
+    __syncthreads();
+    if (p < L.n) {
+        double Hll[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+        double Hpl[18];
+        int cur_slot = -1;
+        const int C = rig.n_cams;
+        const double *X = s.pts + (size_t)p * 3;
+        for (int e = L.edge_start[p]; e < L.edge_start[p + 1]; ++e) {
+            const int k = E.kf[e], c = E.cam[e];
+            const double *Rcw = s.Rcw + ((size_t)k * C + c) * 9, *tcw = s.tcw + ((size_t)k * C + c) * 3;
+            double Xc[3], Xb[3];
+            mv3(Rcw, X, Xc);
+            for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
+            mv3(rig.Rbc[c], Xc, Xb);
+            for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
+            double pj[6];
+            kb8_jac(rig.cam[c], Xc, pj);
+            double JX[6];
+            for (int r = 0; r < 2; ++r)
+                for (int q = 0; q < 3; ++q)
+                    JX[3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
+            double pr[6];
+            for (int r = 0; r < 2; ++r)
+                for (int q = 0; q < 3; ++q)
+                    pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
+            const double x = Xb[0], y = Xb[1], z = Xb[2];
+            const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+            double JP[12];
+            for (int r = 0; r < 2; ++r)
+                for (int q = 0; q < 6; ++q)
+                    JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+            double r0, r1;
+            huber(chi2[e], delta, dsqr, r0, r1);
+            const double wi = (double)E.w[e];
+            const double w = wi * r1;
+            const double om0 = -wi * err[2 * e] * r1, om1 = -wi * err[2 * e + 1] * r1;
+            for (int r = 0; r < 3; ++r) {
+                bl[r] += JX[r] * om0 + JX[3 + r] * om1;
+                for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * (JX[r] * JX[q] + JX[3 + r] * JX[3 + q]);
+            }
+            const int slot = E.slot[e];
+            if (slot != cur_slot) {
+                if (cur_slot >= 0)
+                    for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
+                for (int q = 0; q < 18; ++q) Hpl[q] = 0;
+                cur_slot = slot;
+            }
+            for (int r = 0; r < 6; ++r)
+                for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * (JP[r] * JX[q] + JP[6 + r] * JX[3 + q]);
+            const int o = R.offP[k];
+            if (o < 0) continue;   // fixed keyframe: no pose terms
+            if (kf0 >= 0 && k - kf0 >= 0 && k - kf0 < kSpan) {
+                double *a = acc + (k - kf0) * 42;
+                for (int r = 0; r < 6; ++r) {
+                    unsafeAtomicAdd(a + 36 + r, JP[r] * om0 + JP[6 + r] * om1);
+                    for (int q = 0; q <= r; ++q) unsafeAtomicAdd(a + 6 * r + q, w * (JP[r] * JP[q] + JP[6 + r] * JP[6 + q]));
+                }
+            } else {
+                for (int r = 0; r < 6; ++r) {
+                    unsafeAtomicAdd(R.b + o + r, JP[r] * om0 + JP[6 + r] * om1);
+                    for (int q = 0; q <= r; ++q)
+                        unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + q, w * (JP[r] * JP[q] + JP[6 + r] * JP[6 + q]));
+                }
+            }
+        }
+        if (cur_slot >= 0)
+            for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
+        for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = Hll[q];
+        for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = bl[q];
+    }
+    __syncthreads();
+    if (kf0 >= 0)
+        for (int q = threadIdx.x; q < kSpan * 42; q += blockDim.x) {
+            const int k = kf0 + q / 42, j = q % 42;
+            if (acc[q] == 0.0 || k >= R.n_kf) continue;
+            const int o = R.offP[k];
+            if (o < 0) continue;
+            if (j < 36) {
+                const int r = j / 6, c = j % 6;
+                if (c <= r) unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + c, acc[q]);
+            } else {
+                unsafeAtomicAdd(R.b + o + (j - 36), acc[q]);
+            }
+        }
+}
+
+// ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
+__device__ void inv_right_jac(const double *v, double *J) {
+    const double d2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double d = sqrt(d2);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) J[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double W[9], WW[9];
+    hat3(v, W);
+    mm3(W, W, WW);
+    const double k = 1.0 / d2 - (1.0 + cos(d)) / (2.0 * d * sin(d));
+    for (int q = 0; q < 9; ++q) J[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] / 2 + WW[q] * k;
+}
+__device__ void right_jac(const double *v, double *J) {
+    const double d2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double d = sqrt(d2);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) J[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double W[9], WW[9];
+    hat3(v, W);
+    mm3(W, W, WW);
+    for (int q = 0; q < 9; ++q)
+        J[q] = ((q % 4 == 0) ? 1.0 : 0.0) - W[q] * (1.0 - cos(d)) / d2 + WW[q] * (d - sin(d)) / (d2 * d);
+}
+
+// EdgeInertial::linearizeOplus (G2oTypes.cc:533-599): J [9][24], columns P1(6) V1 G1 A1 P2(6) V2
+__device__ void imu_jacobian(const State &s, const Imu &I, int i, double *J) {
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const float *p = I.pre + (size_t)i * kPF;
+    float b1[6];
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+    const float dbgf[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    const double dbg[3] = {(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]};
+    const double *Rwb1 = s.Rwb + 9 * k1, *Rwb2 = s.Rwb + 9 * k2;
+    double Rbw1[9];
+    tr3(Rwb1, Rbw1);
+    double dR[9], dRt[9], t1[9], eR[9], er[3], invJr[9];
+    delta_rot(p, b1, dR);
+    tr3(dR, dRt);
+    mm3(dRt, Rbw1, t1);
+    mm3(t1, Rwb2, eR);
+    log_so3(eR, er);
+    inv_right_jac(er, invJr);
+    double JRg[9], JVg[9], JPg[9], JVa[9], JPa[9];
+    for (int q = 0; q < 9; ++q) {
+        JRg[q] = p[PreView::JRg + q], JVg[q] = p[PreView::JVg + q], JPg[q] = p[PreView::JPg + q];
+        JVa[q] = p[PreView::JVa + q], JPa[q] = p[PreView::JPa + q];
+    }
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    for (int q = 0; q < 216; ++q) J[q] = 0;
+    auto put = [&](int r0, int c0, const double *B, double sgn) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) J[(r0 + r) * 24 + c0 + c] = sgn * B[3 * r + c];
+    };
+    double R2t[9], A[9], B[9], W[9], v[3], w[3];
+    tr3(Rwb2, R2t);
+    mm3(invJr, R2t, A);
+    mm3(A, Rwb1, B);
+    put(0, 0, B, -1.0);
+    for (int q = 0; q < 3; ++q) v[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+    mv3(Rbw1, v, w);
+    hat3(w, W);
+    put(3, 0, W, 1.0);
+    for (int q = 0; q < 3; ++q)
+        v[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - 0.5 * g[q] * dt * dt;
+    mv3(Rbw1, v, w);
+    hat3(w, W);
+    put(6, 0, W, 1.0);
+    for (int q = 0; q < 3; ++q) J[(6 + q) * 24 + 3 + q] = -1.0;
+    put(3, 6, Rbw1, -1.0);
+    put(6, 6, Rbw1, -dt);
+    double eRt[9], Jg[9], RJ[9], w3[3];
+    tr3(eR, eRt);
+    mv3(JRg, dbg, w3);
+    right_jac(w3, RJ);
+    mm3(invJr, eRt, A);
+    mm3(A, RJ, B);
+    mm3(B, JRg, Jg);
+    put(0, 9, Jg, -1.0);
+    put(3, 9, JVg, -1.0);
+    put(6, 9, JPg, -1.0);
+    put(3, 12, JVa, -1.0);
+    put(6, 12, JPa, -1.0);
+    put(0, 15, invJr, 1.0);
+    mm3(Rbw1, Rwb2, A);
+    put(6, 18, A, 1.0);
+    put(3, 21, Rbw1, 1.0);
+}
+
+__global__ void __launch_bounds__(64) build_imu_kernel(State s, Imu I, Red R, double delta, double dsqr, const double *err9) {
+    __shared__ double J[216];
+    __shared__ double WJ[216];   // Omega' J  (9 x 24)
+    __shared__ double om[9];
+    const int i = blockIdx.x, lane = threadIdx.x;
+    if (lane == 0) imu_jacobian(s, I, i, J);
+    __syncthreads();
+    const double *e = err9 + 9 * i;
+    const double c2 = err9[(size_t)9 * I.n + i];
+    double r0, r1 = 1.0;
+    if (I.robust[i]) huber(c2, delta, dsqr, r0, r1);
+    const double *W = I.info9 + (size_t)i * 81;
+    for (int q = lane; q < 216; q += 64) {
+        const int r = q / 24, c = q % 24;
+        double t = 0;
+        for (int k = 0; k < 9; ++k) t += W[r * 9 + k] * J[k * 24 + c];
+        WJ[q] = t * r1;
+    }
+    if (lane < 9) {
+        double t = 0;
+        for (int k = 0; k < 9; ++k) t += W[lane * 9 + k] * e[k];
+        om[lane] = -t * r1;
+    }
+    __syncthreads();
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const int off[6] = {I.offP[k1], I.offV[k1], I.offG[k1], I.offA[k1], I.offP[k2], I.offV[k2]};
+    const int col0[6] = {0, 6, 9, 12, 15, 21};
+    const int dim[6] = {6, 3, 3, 3, 6, 3};
+    // map a J column to its reduced-system index (-1 fixed)
+    auto red = [&](int c) {
+        int v = 0;
+        while (v < 5 && c >= col0[v + 1]) ++v;
+        return off[v] < 0 ? -1 : off[v] + (c - col0[v]);
+    };
+    for (int q = lane; q < 24 * 24; q += 64) {
+        const int a = q / 24, b = q % 24;
+        const int ra = red(a), rb = red(b);
+        if (ra < 0 || rb < 0 || rb > ra) continue;   // lower triangle of the reduced matrix
+        double t = 0;
+        for (int k = 0; k < 9; ++k) t += J[k * 24 + a] * WJ[k * 24 + b];
+        unsafeAtomicAdd(R.H + (size_t)ra * R.n + rb, t);
+    }
+    if (lane < 24) {
+        const int ra = red(lane);
+        if (ra >= 0) {
+            double t = 0;
+            for (int k = 0; k < 9; ++k) t += J[k * 24 + lane] * om[k];
+            unsafeAtomicAdd(R.b + ra, t);
+        }
+    }
+    // EdgeGyroRW / EdgeAccRW (J1 = -I, J2 = I): lanes 0..17 -> (which, r, c) blocks
+    (void)dim;
+    if (lane < 18) {
+        const int which = lane / 9, rc = lane % 9, r = rc / 3, c = rc % 3;
+        const double *Iw = which ? I.infoA + 9 * i : I.infoG + 9 * i;
+        const int o1 = which ? I.offA[k1] : I.offG[k1], o2 = which ? I.offA[k2] : I.offG[k2];
+        const double *b1v = which ? s.ba : s.bg;
+        if (o1 >= 0) unsafeAtomicAdd(R.H + (size_t)(o1 + r) * R.n + o1 + c, Iw[rc]);
+        if (o2 >= 0) unsafeAtomicAdd(R.H + (size_t)(o2 + r) * R.n + o2 + c, Iw[rc]);
+        if (o1 >= 0 && o2 >= 0) {
+            // block (o2, o1) lies in the lower triangle when o2 > o1: -Iw^T
+            if (o2 > o1) unsafeAtomicAdd(R.H + (size_t)(o2 + r) * R.n + o1 + c, -Iw[3 * c + r]);
+            else unsafeAtomicAdd(R.H + (size_t)(o1 + r) * R.n + o2 + c, -Iw[rc]);
+        }
+        if (c == 0) {
+            double ee[3];
+            for (int q = 0; q < 3; ++q) ee[q] = b1v[3 * k2 + q] - b1v[3 * k1 + q];
+            const double Oe = Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+            if (o1 >= 0) unsafeAtomicAdd(R.b + o1 + r, Oe);
+            if (o2 >= 0) unsafeAtomicAdd(R.b + o2 + r, -Oe);
+        }
+    }
+}
+
+// ---- trial: Schur complement ----------------------------------------------------------------------
+__global__ void prep_kernel(const double *H, double *S, int n, double lambda, double *coef) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (long long)n * n) {
+        const int r = (int)(i / n), c = (int)(i % n);
+        S[i] = c <= r ? H[i] + (r == c ? lambda : 0.0) : 0.0;
+    }
+    if (i < n) coef[i] = 0;
+}
+
+__global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, double lambda, double *S, double *coef) {
+    __shared__ double acc[kSpan * kSpan * 36 / 2 + kSpan * 36 / 2 + kSpan * 6];   // lower block triangle + coef
+    // block (a, b), a >= b, stored at ((a * (a + 1)) / 2 + b) * 36
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int kf0 = L.wg_kf0[blockIdx.x];
+    const int nblk = kSpan * (kSpan + 1) / 2;
+    double *cacc = acc + nblk * 36;
+    for (int q = threadIdx.x; q < nblk * 36 + kSpan * 6; q += blockDim.x) acc[q] = 0;
+    __syncthreads();
+    if (p < L.n) {
+        double D[9], Dinv[9];
+        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+        D[0] += lambda, D[4] += lambda, D[8] += lambda;
+        inv3(D, Dinv);
+        const double *bl = L.bl + (size_t)p * 3;
+        double db[3];
+        mv3(Dinv, bl, db);
+        const int s0 = L.slot_start[p], s1 = L.slot_start[p + 1];
+        for (int a = s0; a < s1; ++a) {
+            const int ka = L.slot_kf[a];
+            const int oa = R.offP[ka];
+            if (oa < 0) continue;
+            const double *Ba = L.Hpl + (size_t)a * 18;
+            double BD[18];
+            for (int r = 0; r < 6; ++r)
+                for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ba[3 * r] * Dinv[c] + Ba[3 * r + 1] * Dinv[3 + c] + Ba[3 * r + 2] * Dinv[6 + c];
+            const bool local_a = kf0 >= 0 && ka - kf0 >= 0 && ka - kf0 < kSpan;
+            for (int r = 0; r < 6; ++r) {
+                const double cv = Ba[3 * r] * db[0] + Ba[3 * r + 1] * db[1] + Ba[3 * r + 2] * db[2];
+                if (local_a) unsafeAtomicAdd(cacc + (ka - kf0) * 6 + r, cv);
+                else unsafeAtomicAdd(coef + oa + r, cv);
+            }
+            for (int b = s0; b < s1; ++b) {
+                const int kb = L.slot_kf[b];
+                const int ob = R.offP[kb];
+                if (ob < 0 || ob > oa) continue;   // lower triangle: row block oa >= col block ob
+                const double *Bb = L.Hpl + (size_t)b * 18;
+                const bool local = local_a && kb - kf0 >= 0 && kb - kf0 < kSpan;
+                const int la = ka - kf0, lb = kb - kf0;
+                // keyframe order == reduced order (offsets increase with keyframe index)
+                double *blk = local ? acc + ((la * (la + 1)) / 2 + lb) * 36 : nullptr;
+                for (int r = 0; r < 6; ++r)
+                    for (int c = 0; c < 6; ++c) {
+                        if (ob == oa && c > r) continue;
+                        const double v = BD[3 * r] * Bb[3 * c] + BD[3 * r + 1] * Bb[3 * c + 1] + BD[3 * r + 2] * Bb[3 * c + 2];
+                        if (local) unsafeAtomicAdd(blk + 6 * r + c, -v);
+                        else unsafeAtomicAdd(S + (size_t)(oa + r) * R.n + ob + c, -v);
+                    }
+            }
+        }
+    }
+    __syncthreads();
+    if (kf0 >= 0) {
+        for (int q = threadIdx.x; q < nblk * 36; q += blockDim.x) {
+            if (acc[q] == 0.0) continue;
+            const int blk = q / 36, e = q % 36;
+            int la = 0;
+            while ((la + 1) * (la + 2) / 2 <= blk) ++la;
+            const int lb = blk - la * (la + 1) / 2;
+            const int ka = kf0 + la, kb = kf0 + lb;
+            const int oa = R.offP[ka], ob = R.offP[kb];
+            unsafeAtomicAdd(S + (size_t)(oa + e / 6) * R.n + ob + e % 6, acc[q]);
+        }
+        for (int q = threadIdx.x; q < kSpan * 6; q += blockDim.x) {
+            if (cacc[q] == 0.0) continue;
+            const int ka = kf0 + q / 6;
+            unsafeAtomicAdd(coef + R.offP[ka] + q % 6, cacc[q]);
+        }
+    }
+}
+
+// ---- trial: block LDL^T of the reduced system (one workgroup) ------------------------------------
+struct BlockPat {
+    int nb;
+    const int *off, *dim;   // per block (keyframe) offset / size in the reduced system
+    const int *slot;        // [nb*nb] storage slot of block (i,j), i >= j, in the packed buffer; -1 zero
+    const int *slot_off;    // [n_slots] double offset of each slot in the packed buffer
+    int n_slots;
+    long long packed_doubles;
+};
+
+__device__ __forceinline__ double *blk(double *pk, const BlockPat &P, int i, int j) {
+    const int s = P.slot[i * P.nb + j];
+    return s < 0 ? nullptr : pk + P.slot_off[s];
+}
+
+__global__ void __launch_bounds__(256) ldlt_kernel(const double *S, int n, BlockPat P, const double *b, const double *coef,
+                                                   double *x, double *scratch, int use_lds, int *fail) {
+    extern __shared__ __attribute__((aligned(16))) double lsm[];
+    double *pk = use_lds ? lsm : scratch;
+    __shared__ double dk[16];
+    __shared__ int bad;
+    const int tid = threadIdx.x, T = blockDim.x;
+    if (tid == 0) bad = 0;
+    // gather the nonzero lower blocks
+    for (int i = 0; i < P.nb; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double *B = blk(pk, P, i, j);
+            if (!B) continue;
+            const int di = P.dim[i], dj = P.dim[j], oi = P.off[i], oj = P.off[j];
+            for (int q = tid; q < di * dj; q += T) {
+                const int r = q / dj, c = q % dj;
+                B[q] = S[(size_t)(oi + r) * n + oj + c];
+            }
+        }
+    __syncthreads();
+    double *dvec = scratch + (use_lds ? 0 : P.packed_doubles);   // [n] pivots
+    double *y = dvec + n;                        // [n] work vector
+    for (int k = 0; k < P.nb; ++k) {
+        const int dkk = P.dim[k], ok = P.off[k];
+        double *Bkk = blk(pk, P, k, k);
+        // 1. factor the diagonal block in place (lower part): unit L_kk and pivots d
+        if (tid < 64) {
+            for (int c = 0; c < dkk; ++c) {
+                const double dc = Bkk[c * dkk + c];
+                if (tid == 0) {
+                    dk[c] = dc;
+                    if (dc == 0.0 || !isfinite(dc)) bad = 1;
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (int q = tid; q < dkk * dkk; q += 64) {
+                    const int r = q / dkk, s = q % dkk;
+                    if (r > c && s > c && s <= r) Bkk[q] -= Bkk[r * dkk + c] / dc * Bkk[s * dkk + c];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                for (int r = c + 1 + tid; r < dkk; r += 64) Bkk[r * dkk + c] /= dc;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __syncthreads();
+        if (tid < dkk) dvec[ok + tid] = dk[tid];
+        // 2. panel: Y_i = S_ik L_kk^-T (rows solve forward), L_ik = Y_i D^-1; Y kept for the update
+        for (int i = k + 1; i < P.nb; ++i) {
+            double *Bik = blk(pk, P, i, k);
+            if (!Bik) continue;
+            const int di = P.dim[i];
+            for (int r = tid; r < di; r += T) {
+                double *row = Bik + r * dkk;
+                for (int c = 0; c < dkk; ++c) {
+                    double v = row[c];
+                    for (int m = 0; m < c; ++m) v -= Bkk[c * dkk + m] * row[m];   // row holds y_m for m < c
+                    row[c] = v;
+                }
+            }
+        }
+        __syncthreads();
+        // 3. trailing update S_ij -= Y_i D^-1 Y_j^T for i >= j > k (lower part)
+        for (int i = k + 1; i < P.nb; ++i) {
+            double *Bik = blk(pk, P, i, k);
+            if (!Bik) continue;
+            for (int j = k + 1; j <= i; ++j) {
+                double *Bjk = blk(pk, P, j, k);
+                if (!Bjk) continue;
+                double *Bij = blk(pk, P, i, j);
+                const int di = P.dim[i], dj = P.dim[j];
+                for (int q = tid; q < di * dj; q += T) {
+                    const int r = q / dj, c = q % dj;
+                    if (i == j && c > r) continue;
+                    double v = 0;
+                    for (int m = 0; m < dkk; ++m) v += Bik[r * dkk + m] * Bjk[c * dkk + m] / dk[m];
+                    Bij[q] -= v;
+                }
+            }
+        }
+        __syncthreads();
+        // 4. scale the panel to L_ik = Y_i D^-1
+        for (int i = k + 1; i < P.nb; ++i) {
+            double *Bik = blk(pk, P, i, k);
+            if (!Bik) continue;
+            const int di = P.dim[i];
+            for (int q = tid; q < di * dkk; q += T) Bik[q] /= dk[q % dkk];
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (tid == 0) *fail = 1;
+        return;
+    }
+    // forward: L y = b - coef
+    for (int q = tid; q < n; q += T) y[q] = b[q] - coef[q];
+    __syncthreads();
+    for (int k = 0; k < P.nb; ++k) {
+        const int dkk = P.dim[k], ok = P.off[k];
+        for (int r = tid; r < dkk; r += T) {
+            double v = y[ok + r];
+            for (int j = 0; j < k; ++j) {
+                const double *Bkj = blk(pk, P, k, j);
+                if (!Bkj) continue;
+                const int dj = P.dim[j], oj = P.off[j];
+                for (int c = 0; c < dj; ++c) v -= Bkj[r * dj + c] * y[oj + c];
+            }
+            y[ok + r] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const double *Bkk = blk(pk, P, k, k);
+            for (int r = 0; r < dkk; ++r) {
+                double v = y[ok + r];
+                for (int c = 0; c < r; ++c) v -= Bkk[r * dkk + c] * y[ok + c];
+                y[ok + r] = v;
+            }
+        }
+        __syncthreads();
+    }
+    for (int q = tid; q < n; q += T) y[q] /= dvec[q];
+    __syncthreads();
+    // backward: L^T x = z
+    for (int k = P.nb - 1; k >= 0; --k) {
+        const int dkk = P.dim[k], ok = P.off[k];
+        for (int c = tid; c < dkk; c += T) {
+            double v = y[ok + c];
+            for (int i = k + 1; i < P.nb; ++i) {
+                const double *Bik = blk(pk, P, i, k);
+                if (!Bik) continue;
+                const int di = P.dim[i], oi = P.off[i];
+                for (int r = 0; r < di; ++r) v -= Bik[r * dkk + c] * x[oi + r];
+            }
+            y[ok + c] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const double *Bkk = blk(pk, P, k, k);
+            for (int c = dkk - 1; c >= 0; --c) {
+                double v = y[ok + c];
+                for (int r = c + 1; r < dkk; ++r) v -= Bkk[r * dkk + c] * x[ok + r];
+                x[ok + c] = v;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *fail = 0;
+}
+
+// ---- trial: back-substitution + updates + scale ----------------------------------------------------
+__global__ void __launch_bounds__(256) backsub_kernel(Land L, Red R, double lambda, const double *xp, State a, State bst,
+                                                      double *scale_partial) {
+    __shared__ double sh[8];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    double sc = 0;
+    if (p < L.n) {
+        double D[9], Dinv[9];
+        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+        D[0] += lambda, D[4] += lambda, D[8] += lambda;
+        inv3(D, Dinv);
+        const double *bl = L.bl + (size_t)p * 3;
+        double c[3] = {bl[0], bl[1], bl[2]};
+        for (int s = L.slot_start[p]; s < L.slot_start[p + 1]; ++s) {
+            const int o = R.offP[L.slot_kf[s]];
+            if (o < 0) continue;
+            const double *B = L.Hpl + (size_t)s * 18;
+            for (int q = 0; q < 3; ++q)
+                for (int r = 0; r < 6; ++r) c[q] -= B[3 * r + q] * xp[o + r];
+        }
+        double xl[3];
+        mv3(Dinv, c, xl);
+        for (int q = 0; q < 3; ++q) {
+            bst.pts[(size_t)p * 3 + q] = a.pts[(size_t)p * 3 + q] + xl[q];
+            sc += xl[q] * (lambda * xl[q] + bl[q]);
+        }
+    }
+    const double t = block_reduce_sum(sc, sh);
+    if (threadIdx.x == 0) scale_partial[blockIdx.x] = t;
+}
+
+__device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:802-815)
+    const double x = w[0], y = w[1], z = w[2];
+    const double d2 = x * x + y * y + z * z;
+    const double d = sqrt(d2);
+    double W[9], WW[9];
+    hat3(w, W);
+    mm3(W, W, WW);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] + 0.5 * WW[q];
+    } else {
+        const double s = sin(d), c = cos(d);
+        for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] * s / d + WW[q] * (1.0 - c) / d2;
+    }
+    polar3(R);
+}
+
+// ImuCamPose::Update (G2oTypes.cc:211-235) + vertex adds; the pose part of computeScale.
+__global__ void update_kf_kernel(Rig rig, Red R, const int *offV, const int *offG, const int *offA, int n_opt, double lambda,
+                                 const double *xp, State a, State bst, double *scale_partial) {
+    __shared__ double sh[8];
+    const int C = rig.n_cams;
+    for (int k = threadIdx.x; k < n_opt; k += blockDim.x) {
+        const double *u = xp + R.offP[k];
+        double Rwb[9], twb[3], dRw[9], t[3];
+        for (int q = 0; q < 9; ++q) Rwb[q] = a.Rwb[9 * k + q];
+        mv3(Rwb, u + 3, t);
+        for (int q = 0; q < 3; ++q) twb[q] = a.twb[3 * k + q] + t[q];
+        exp_so3(u, dRw);
+        double Rn[9];
+        mm3(Rwb, dRw, Rn);
+        double Rbw[9], tbw[3];
+        tr3(Rn, Rbw);
+        mv3(Rbw, twb, tbw);
+        for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
+        for (int q = 0; q < 9; ++q) bst.Rwb[9 * k + q] = Rn[q];
+        for (int q = 0; q < 3; ++q) bst.twb[3 * k + q] = twb[q];
+        for (int c = 0; c < C; ++c) {
+            double Rc[9], tc[3];
+            mm3(rig.Rcb[c], Rbw, Rc);
+            mv3(rig.Rcb[c], tbw, tc);
+            for (int q = 0; q < 9; ++q) bst.Rcw[((size_t)k * C + c) * 9 + q] = Rc[q];
+            for (int q = 0; q < 3; ++q) bst.tcw[((size_t)k * C + c) * 3 + q] = tc[q] + rig.tcb[c][q];
+        }
+        for (int q = 0; q < 3; ++q) {
+            bst.vel[3 * k + q] = a.vel[3 * k + q] + (offV[k] >= 0 ? xp[offV[k] + q] : 0.0);
+            bst.bg[3 * k + q] = a.bg[3 * k + q] + (offG[k] >= 0 ? xp[offG[k] + q] : 0.0);
+            bst.ba[3 * k + q] = a.ba[3 * k + q] + (offA[k] >= 0 ? xp[offA[k] + q] : 0.0);
+        }
+    }
+    // pose part of sum_j x_j (lambda x_j + b_j)
+    double sc = 0;
+    for (int q = threadIdx.x; q < R.n; q += blockDim.x) sc += xp[q] * (lambda * xp[q] + R.b[q]);
+    const double tt = block_reduce_sum(sc, sh);
+    if (threadIdx.x == 0) scale_partial[0] = tt;
+}
+
+// ---- evaluation helpers for parity ---------------------------------------------------------------
+__global__ void mono_jac_kernel(Rig rig, State s, Edges E, double *jx, double *jp) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E.n) return;
+    const int k = E.kf[e], c = E.cam[e], C = rig.n_cams;
+    const double *Rcw = s.Rcw + ((size_t)k * C + c) * 9, *tcw = s.tcw + ((size_t)k * C + c) * 3;
+    const double *X = s.pts + (size_t)E.pt[e] * 3;
+    double Xc[3], Xb[3];
+    mv3(Rcw, X, Xc);
+    for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
+    mv3(rig.Rbc[c], Xc, Xb);
+    for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
+    double pj[6];
+    kb8_jac(rig.cam[c], Xc, pj);
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 3; ++q)
+            jx[6 * e + 3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
+    double pr[6];
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 3; ++q)
+            pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
+    const double x = Xb[0], y = Xb[1], z = Xb[2];
+    const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 6; ++q)
+            jp[12 * e + 6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+}
+
+// ---- host-side analysis ------------------------------------------------------------------------------
+void host_inv(std::vector<double> &A, int n) {   // Gauss-Jordan with partial pivoting
+    std::vector<double> I(n * n, 0.0);
+    for (int i = 0; i < n; ++i) I[i * n + i] = 1;
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        for (int r = c + 1; r < n; ++r)
+            if (std::fabs(A[r * n + c]) > std::fabs(A[p * n + c])) p = r;
+        if (p != c)
+            for (int k = 0; k < n; ++k) std::swap(A[p * n + k], A[c * n + k]), std::swap(I[p * n + k], I[c * n + k]);
+        const double d = A[c * n + c];
+        for (int k = 0; k < n; ++k) A[c * n + k] /= d, I[c * n + k] /= d;
+        for (int r = 0; r < n; ++r)
+            if (r != c && A[r * n + c] != 0) {
+                const double f = A[r * n + c];
+                for (int k = 0; k < n; ++k) A[r * n + k] -= f * A[c * n + k], I[r * n + k] -= f * I[c * n + k];
+            }
+    }
+    A = I;
+}
+void host_sym_eig(std::vector<double> A, int n, std::vector<double> &w, std::vector<double> &V) {
+    V.assign(n * n, 0.0);
+    for (int i = 0; i < n; ++i) V[i * n + i] = 1;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = A[p * n + q];
+                if (apq == 0) continue;
+                const double th = (A[q * n + q] - A[p * n + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    const double akp = A[k * n + p], akq = A[k * n + q];
+                    A[k * n + p] = c * akp - s * akq, A[k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double apk = A[p * n + k], aqk = A[q * n + k];
+                    A[p * n + k] = c * apk - s * aqk, A[q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq, V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    w.resize(n);
+    for (int i = 0; i < n; ++i) w[i] = A[i * n + i];
+}
+
+template <typename T>
+T *dalloc(std::vector<void *> &owned, size_t n) {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)) != hipSuccess) return nullptr;
+    owned.push_back(p);
+    return (T *)p;
+}
+
+}  // namespace
+
+// =============================================================================================
+struct omv_lba {
+    int max_kf, max_cams, max_pts, max_mono, max_imu;
+    std::vector<void *> owned;   // device allocations of the current problem
+    // problem
+    Rig rig{};
+    int n_kf = 0, n_opt = 0, n_pts = 0, n_mono = 0, n_imu = 0, n_red = 0, n_slots = 0;
+    State st[2]{};
+    int cur = 0;
+    Edges E{};
+    Land L{};
+    Red R{};
+    Imu I{};
+    BlockPat BP{};
+    int n_wg_land = 0, n_wg_edge = 0;
+    int *d_offP = nullptr, *d_offV = nullptr, *d_offG = nullptr, *d_offA = nullptr;
+    double *d_err = nullptr, *d_chi2 = nullptr, *d_err9 = nullptr;
+    double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
+    double *d_S = nullptr, *d_coef = nullptr, *d_x = nullptr, *d_scratch = nullptr;
+    int *d_fail = nullptr;
+    size_t ldlt_lds = 0;
+    int use_lds = 0;
+    bool lds_ok = false;
+    std::vector<int> perm_pt;     // device point index -> caller index
+    std::vector<int> perm_edge;   // device edge index -> caller index
+    double delta_mono, dsqr_mono, delta_imu, dsqr_imu;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8];
+    double stage_ms[4] = {0, 0, 0, 0};
+    int last_trials = 0;
+};
+
+static void free_problem(omv_lba *h) {
+    for (void *p : h->owned) (void)hipFree(p);
+    h->owned.clear();
+}
+
+extern "C" {
+
+omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, int max_imu, omv_lba **out) {
+    if (!out || max_kf <= 0 || max_cams <= 0 || max_cams > kMaxCams || max_pts < 0 || max_mono < 0 || max_imu < 0)
+        return OMV_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
+    omv_lba *h = new omv_lba();
+    h->max_kf = max_kf, h->max_cams = max_cams, h->max_pts = max_pts, h->max_mono = max_mono, h->max_imu = max_imu;
+    HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    for (auto &e : h->ev) HIP_OK(hipEventCreate(&e));
+    // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
+    h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    150 * 1024) == hipSuccess;
+    (void)hipGetLastError();
+    *out = h;
+    return OMV_OK;
+}
+
+omv_status omv_lba_destroy(omv_lba *h) {
+    if (!h) return OMV_ERR_ARG;
+    free_problem(h);
+    for (auto &e : h->ev) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return OMV_OK;
+}
+
+omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
+    if (!h || !p) return OMV_ERR_ARG;
+    if (p->n_cams <= 0 || p->n_cams > h->max_cams || p->n_kf > h->max_kf || p->n_pts > h->max_pts ||
+        p->n_mono > h->max_mono || p->n_imu > h->max_imu || p->n_opt > p->n_kf || p->n_opt < 1)
+        return OMV_ERR_ARG;
+    free_problem(h);
+    const int C = p->n_cams, K = p->n_kf, P = p->n_pts, E = p->n_mono, NI = p->n_imu;
+    h->n_kf = K, h->n_opt = p->n_opt, h->n_pts = P, h->n_mono = E, h->n_imu = NI;
+    // rig
+    Rig &rig = h->rig;
+    rig.n_cams = C;
+    for (int c = 0; c < C; ++c) {
+        for (int q = 0; q < 8; ++q) rig.cam[c][q] = p->cam[8 * c + q];
+        for (int q = 0; q < 9; ++q) rig.Rcb[c][q] = p->Rcb[9 * c + q], rig.Rbc[c][q] = p->Rbc[9 * c + q];
+        for (int q = 0; q < 3; ++q) rig.tcb[c][q] = p->tcb[3 * c + q], rig.tbc[c][q] = p->tbc[3 * c + q];
+    }
+    // reduced-system layout: per optimisable keyframe pose (6) [+ v bg ba (9)]
+    std::vector<int> offP(K, -1), offV(K, -1), offG(K, -1), offA(K, -1), bdim;
+    int nred = 0;
+    for (int k = 0; k < p->n_opt; ++k) {
+        offP[k] = nred, nred += 6;
+        if (p->kf_imu[k]) offV[k] = nred, offG[k] = nred + 3, offA[k] = nred + 6, nred += 9;
+        bdim.push_back(p->kf_imu[k] ? 15 : 6);
+    }
+    h->n_red = nred;
+    // landmark order: by the first optimisable keyframe observing them (workgroup keyframe spans stay small)
+    std::vector<std::vector<int>> pe(P);
+    for (int e = 0; e < E; ++e) {
+        if (p->mono_pt[e] < 0 || p->mono_pt[e] >= P || p->mono_kf[e] < 0 || p->mono_kf[e] >= K ||
+            p->mono_cam[e] < 0 || p->mono_cam[e] >= C)
+            return OMV_ERR_ARG;
+        pe[p->mono_pt[e]].push_back(e);
+    }
+    std::vector<int> key(P, 1 << 30);
+    for (int q = 0; q < P; ++q)
+        for (int e : pe[q]) key[q] = std::min(key[q], p->mono_kf[e] < p->n_opt ? p->mono_kf[e] : (1 << 29) + p->mono_kf[e]);
+    std::vector<int> order(P);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
+    h->perm_pt = order;
+    std::vector<int> e_pt, e_kf, e_cam, e_slot, pt_edge(P + 1, 0), pt_slot(P + 1, 0), slot_kf;
+    std::vector<double> e_obs;
+    std::vector<float> e_w;
+    h->perm_edge.clear();
+    for (int q = 0; q < P; ++q) {
+        std::vector<int> es = pe[order[q]];
+        std::stable_sort(es.begin(), es.end(), [&](int a, int b) { return p->mono_kf[a] < p->mono_kf[b]; });
+        pt_edge[q] = (int)e_pt.size();
+        pt_slot[q] = (int)slot_kf.size();
+        int last_kf = -1;
+        for (int e : es) {
+            if (p->mono_kf[e] != last_kf) slot_kf.push_back(p->mono_kf[e]), last_kf = p->mono_kf[e];
+            e_pt.push_back(q), e_kf.push_back(p->mono_kf[e]), e_cam.push_back(p->mono_cam[e]);
+            e_slot.push_back((int)slot_kf.size() - 1);
+            e_obs.push_back(p->mono_obs[2 * e]), e_obs.push_back(p->mono_obs[2 * e + 1]);
+            e_w.push_back(p->mono_inv_sigma2[e]);
+            h->perm_edge.push_back(e);
+        }
+    }
+    pt_edge[P] = (int)e_pt.size();
+    pt_slot[P] = (int)slot_kf.size();
+    h->n_slots = (int)slot_kf.size();
+    // workgroup keyframe spans (256 landmarks per workgroup)
+    h->n_wg_land = (P + 255) / 256;
+    std::vector<int> wg_kf0(std::max(1, h->n_wg_land), -1);
+    for (int g = 0; g < h->n_wg_land; ++g) {
+        int lo = 1 << 30, hi = -1;
+        for (int q = g * 256; q < std::min(P, (g + 1) * 256); ++q)
+            for (int s = pt_slot[q]; s < pt_slot[q + 1]; ++s)
+                if (slot_kf[s] < p->n_opt) lo = std::min(lo, slot_kf[s]), hi = std::max(hi, slot_kf[s]);
+        wg_kf0[g] = (hi >= 0 && hi - lo < kSpan) ? lo : (hi < 0 ? 0 : -1);
+    }
+    // block pattern of the reduced system (keyframe blocks) + symbolic LDL^T fill-in
+    const int nb = p->n_opt;
+    std::vector<uint8_t> pat((size_t)nb * nb, 0);
+    for (int k = 0; k < nb; ++k) pat[k * nb + k] = 1;
+    for (int q = 0; q < P; ++q)
+        for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
+            for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
+                const int i = slot_kf[a], j = slot_kf[b];
+                if (i < nb && j < nb && j <= i) pat[i * nb + j] = 1;
+            }
+    for (int i = 0; i < NI; ++i) {
+        if (p->imu_kf1[i] < 0 || p->imu_kf1[i] >= K || p->imu_kf2[i] < 0 || p->imu_kf2[i] >= K ||
+            p->imu_kf1[i] == p->imu_kf2[i])
+            return OMV_ERR_ARG;
+        const int a = std::max(p->imu_kf1[i], p->imu_kf2[i]), b = std::min(p->imu_kf1[i], p->imu_kf2[i]);
+        if (a < nb && b < nb) pat[a * nb + b] = 1;
+    }
+    // reduced order follows keyframe index: block i sits after block j for i > j (offP increasing)
+    for (int k = 0; k < nb; ++k)
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[i * nb + k])
+                for (int j = k + 1; j <= i; ++j)
+                    if (pat[j * nb + k]) pat[i * nb + j] = 1;
+    std::vector<int> slot((size_t)nb * nb, -1), slot_off;
+    long long packed = 0;
+    for (int i = 0; i < nb; ++i)
+        for (int j = 0; j <= i; ++j)
+            if (pat[i * nb + j]) {
+                slot[i * nb + j] = (int)slot_off.size();
+                slot_off.push_back((int)packed);
+                packed += (long long)bdim[i] * bdim[j];
+            }
+    h->use_lds = h->lds_ok && (size_t)packed * sizeof(double) <= 150 * 1024 ? 1 : 0;
+    h->ldlt_lds = h->use_lds ? (size_t)packed * sizeof(double) : 0;
+    // inertial information (EdgeInertial ctor :486-495) and random-walk information
+    std::vector<double> info9((size_t)NI * 81), infoG((size_t)NI * 9), infoA((size_t)NI * 9);
+    for (int i = 0; i < NI; ++i) {
+        const float *pr = p->preint + (size_t)i * kPF + PreView::C;
+        std::vector<double> A(81);
+        for (int r = 0; r < 9; ++r)
+            for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)pr[r * 15 + c];
+        host_inv(A, 9);
+        for (int r = 0; r < 9; ++r)
+            for (int c = r + 1; c < 9; ++c) A[r * 9 + c] = A[c * 9 + r] = (A[r * 9 + c] + A[c * 9 + r]) / 2;
+        std::vector<double> w, V;
+        host_sym_eig(A, 9, w, V);
+        for (double &x : w)
+            if (x < 1e-12) x = 0;
+        const double sc = p->imu_info_scale ? (double)p->imu_info_scale[i] : 1.0;
+        for (int r = 0; r < 9; ++r)
+            for (int c = 0; c < 9; ++c) {
+                double s = 0;
+                for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
+                info9[(size_t)i * 81 + r * 9 + c] = s * sc;
+            }
+        double g[9], a[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) g[3 * r + c] = pr[(9 + r) * 15 + 9 + c], a[3 * r + c] = pr[(12 + r) * 15 + 12 + c];
+        inv3(g, &infoG[(size_t)9 * i]);
+        inv3(a, &infoA[(size_t)9 * i]);
+    }
+    h->delta_mono = (double)(float)std::sqrt(5.991);
+    h->dsqr_mono = h->delta_mono * h->delta_mono;
+    h->delta_imu = std::sqrt(16.92);
+    h->dsqr_imu = h->delta_imu * h->delta_imu;
+    // ---- device allocations + uploads
+    std::vector<void *> &ow = h->owned;
+    auto up = [&](auto *dst, const auto *src, size_t n) {
+        return hipMemcpy(dst, src, n * sizeof(*src), hipMemcpyHostToDevice);
+    };
+    for (int b = 0; b < 2; ++b) {
+        State &s = h->st[b];
+        s.Rwb = dalloc<double>(ow, 9 * K), s.twb = dalloc<double>(ow, 3 * K);
+        s.Rcw = dalloc<double>(ow, 9 * K * C), s.tcw = dalloc<double>(ow, 3 * K * C);
+        s.vel = dalloc<double>(ow, 3 * K), s.bg = dalloc<double>(ow, 3 * K), s.ba = dalloc<double>(ow, 3 * K);
+        s.pts = dalloc<double>(ow, 3 * (size_t)P);
+        if (!s.pts) return OMV_ERR_HIP;
+        HIP_OK(up(s.Rwb, p->Rwb, 9 * K));
+        HIP_OK(up(s.twb, p->twb, 3 * K));
+        HIP_OK(up(s.Rcw, p->Rcw, 9 * K * C));
+        HIP_OK(up(s.tcw, p->tcw, 3 * K * C));
+        HIP_OK(up(s.vel, p->vel, 3 * K));
+        HIP_OK(up(s.bg, p->bg, 3 * K));
+        HIP_OK(up(s.ba, p->ba, 3 * K));
+        std::vector<double> pts((size_t)3 * P);
+        for (int q = 0; q < P; ++q)
+            for (int d = 0; d < 3; ++d) pts[3 * q + d] = p->pts[3 * (size_t)order[q] + d];
+        HIP_OK(up(s.pts, pts.data(), pts.size()));
+    }
+    h->cur = 0;
+    int *d_e_pt = dalloc<int>(ow, E), *d_e_kf = dalloc<int>(ow, E), *d_e_cam = dalloc<int>(ow, E),
+        *d_e_slot = dalloc<int>(ow, E);
+    double *d_e_obs = dalloc<double>(ow, 2 * (size_t)E);
+    float *d_e_w = dalloc<float>(ow, E);
+    if (!d_e_w) return OMV_ERR_HIP;
+    HIP_OK(up(d_e_pt, e_pt.data(), E));
+    HIP_OK(up(d_e_kf, e_kf.data(), E));
+    HIP_OK(up(d_e_cam, e_cam.data(), E));
+    HIP_OK(up(d_e_slot, e_slot.data(), E));
+    HIP_OK(up(d_e_obs, e_obs.data(), 2 * (size_t)E));
+    HIP_OK(up(d_e_w, e_w.data(), E));
+    h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, E};
+    int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots),
+        *d_wg = dalloc<int>(ow, wg_kf0.size());
+    double *d_Hll = dalloc<double>(ow, 9 * (size_t)P), *d_bl = dalloc<double>(ow, 3 * (size_t)P),
+           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots);
+    if (!d_Hpl) return OMV_ERR_HIP;
+    HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
+    HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
+    HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
+    HIP_OK(up(d_wg, wg_kf0.data(), wg_kf0.size()));
+    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_wg, d_Hll, d_bl, d_Hpl, P};
+    h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
+    h->d_offA = dalloc<int>(ow, K);
+    HIP_OK(up(h->d_offP, offP.data(), K));
+    HIP_OK(up(h->d_offV, offV.data(), K));
+    HIP_OK(up(h->d_offG, offG.data(), K));
+    HIP_OK(up(h->d_offA, offA.data(), K));
+    double *d_H = dalloc<double>(ow, (size_t)nred * nred), *d_b = dalloc<double>(ow, nred);
+    h->R = Red{d_H, d_b, nred, h->d_offP, K};
+    // inertial
+    int *d_k1 = dalloc<int>(ow, NI), *d_k2 = dalloc<int>(ow, NI);
+    float *d_pre = dalloc<float>(ow, (size_t)NI * kPF);
+    double *d_i9 = dalloc<double>(ow, (size_t)NI * 81), *d_iG = dalloc<double>(ow, (size_t)NI * 9),
+           *d_iA = dalloc<double>(ow, (size_t)NI * 9);
+    uint8_t *d_rob = dalloc<uint8_t>(ow, NI);
+    if (!d_rob) return OMV_ERR_HIP;
+    if (NI > 0) {
+        HIP_OK(up(d_k1, p->imu_kf1, NI));
+        HIP_OK(up(d_k2, p->imu_kf2, NI));
+        HIP_OK(up(d_pre, p->preint, (size_t)NI * kPF));
+        HIP_OK(up(d_i9, info9.data(), info9.size()));
+        HIP_OK(up(d_iG, infoG.data(), infoG.size()));
+        HIP_OK(up(d_iA, infoA.data(), infoA.size()));
+        std::vector<uint8_t> rob(NI, 0);
+        if (p->imu_robust) std::copy(p->imu_robust, p->imu_robust + NI, rob.begin());
+        HIP_OK(up(d_rob, rob.data(), NI));
+    }
+    h->I = Imu{NI, d_k1, d_k2, d_pre, d_i9, d_iG, d_iA, d_rob, h->d_offP, h->d_offV, h->d_offG, h->d_offA};
+    // block pattern
+    int *d_boff = dalloc<int>(ow, nb), *d_bdim = dalloc<int>(ow, nb), *d_slot = dalloc<int>(ow, (size_t)nb * nb),
+        *d_slot_off = dalloc<int>(ow, slot_off.size());
+    std::vector<int> boff(nb);
+    for (int k = 0; k < nb; ++k) boff[k] = offP[k];
+    if (nb > 0) {
+        HIP_OK(up(d_boff, boff.data(), nb));
+        HIP_OK(up(d_bdim, bdim.data(), nb));
+        HIP_OK(up(d_slot, slot.data(), (size_t)nb * nb));
+        HIP_OK(up(d_slot_off, slot_off.data(), slot_off.size()));
+    }
+    h->BP = BlockPat{nb, d_boff, d_bdim, d_slot, d_slot_off, (int)slot_off.size(), packed};
+    // work buffers
+    h->n_wg_edge = (E + 255) / 256;
+    h->d_err = dalloc<double>(ow, 2 * (size_t)E);
+    h->d_chi2 = dalloc<double>(ow, E);
+    h->d_err9 = dalloc<double>(ow, 10 * (size_t)NI);
+    h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
+    h->d_imu_partial = dalloc<double>(ow, 1);
+    h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
+    h->d_out = dalloc<double>(ow, 4);
+    h->d_S = dalloc<double>(ow, (size_t)nred * nred);
+    h->d_coef = dalloc<double>(ow, nred);
+    h->d_x = dalloc<double>(ow, nred);
+    h->d_scratch = dalloc<double>(ow, (size_t)(h->use_lds ? 0 : packed) + 2 * nred + 8);
+    h->d_fail = dalloc<int>(ow, 1);
+    if (!h->d_fail) return OMV_ERR_HIP;
+    HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
+    return OMV_OK;
+}
+
+}  // extern "C"
+
+// ---- the LM driver ---------------------------------------------------------------------------------
+static omv_status lba_errors(omv_lba *h, const State &s) {
+    hipStream_t st = h->stream;
+    if (h->n_mono > 0)
+        mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->d_err, h->d_chi2,
+                                                       h->d_partial);
+    if (h->n_imu > 0) imu_err_kernel<<<1, 64, 0, st>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
+    return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
+}
+
+static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[2]) {
+    finish_kernel<<<1, 256, 0, h->stream>>>(h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
+                                           h->d_scale_partial, n_scale, h->d_out);
+    HIP_OK(hipMemcpyAsync(out, h->d_out, 2 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    return OMV_OK;
+}
+
+extern "C" {
+
+omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err) {
+    if (!h) return OMV_ERR_ARG;
+    const State &s = h->st[h->cur];
+    omv_status r = lba_errors(h, s);
+    if (r != OMV_OK) return r;
+    std::vector<double> jx, jp;
+    double *d_jx = nullptr, *d_jp = nullptr;
+    const int E = h->n_mono;
+    if ((mono_jx || mono_jp) && E > 0) {
+        HIP_OK(hipMalloc(&d_jx, sizeof(double) * 6 * E));
+        HIP_OK(hipMalloc(&d_jp, sizeof(double) * 12 * E));
+        mono_jac_kernel<<<(E + 255) / 256, 256, 0, h->stream>>>(h->rig, s, h->E, d_jx, d_jp);
+    }
+    HIP_OK(hipStreamSynchronize(h->stream));
+    std::vector<double> err(2 * (size_t)E), e9(10 * (size_t)h->n_imu);
+    if (E > 0) HIP_OK(hipMemcpy(err.data(), h->d_err, err.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (h->n_imu > 0) HIP_OK(hipMemcpy(e9.data(), h->d_err9, e9.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (d_jx) {
+        jx.resize(6 * (size_t)E), jp.resize(12 * (size_t)E);
+        HIP_OK(hipMemcpy(jx.data(), d_jx, jx.size() * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(jp.data(), d_jp, jp.size() * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(d_jx);
+        (void)hipFree(d_jp);
+    }
+    for (int e = 0; e < E; ++e) {   // back to the caller's edge order
+        const int o = h->perm_edge[e];
+        if (mono_err) mono_err[2 * o] = err[2 * e], mono_err[2 * o + 1] = err[2 * e + 1];
+        if (mono_jx) std::memcpy(mono_jx + 6 * (size_t)o, &jx[6 * (size_t)e], 48);
+        if (mono_jp) std::memcpy(mono_jp + 12 * (size_t)o, &jp[12 * (size_t)e], 96);
+    }
+    if (imu_err) std::memcpy(imu_err, e9.data(), 9 * sizeof(double) * h->n_imu);
+    return OMV_OK;
+}
+
+omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
+    if (!h || !o || !p || !res) return OMV_ERR_ARG;
+    hipStream_t st = h->stream;
+    const int nred = h->n_red;
+    double sc[2];
+    omv_status rs;
+    for (double &m : h->stage_ms) m = 0;
+    // err = activeRobustChi2 at the initial state (Optimizer.cc:3273-3274)
+    if ((rs = lba_errors(h, h->st[h->cur])) != OMV_OK) return rs;
+    if ((rs = lba_read_scalars(h, 0, sc)) != OMV_OK) return rs;
+    res->err = (float)sc[0];
+    double errors_chi = sc[0];
+    bool errors_of_current = true;
+    double lambda = 0, ni = 2;
+    int nBad = 0, trials = 0, its = 0;
+    const int gl = std::max(1, h->n_wg_land);
+    for (int it = 0; it < o->opt_it; ++it) {
+        ++its;
+        State &A = h->st[h->cur];
+        State &B = h->st[1 - h->cur];
+        if (!errors_of_current) {
+            if ((rs = lba_errors(h, A)) != OMV_OK) return rs;
+            if ((rs = lba_read_scalars(h, 0, sc)) != OMV_OK) return rs;
+            errors_chi = sc[0];
+            errors_of_current = true;
+        }
+        double currentChi = errors_chi;
+        const double iniChi = currentChi;
+        // buildSystem
+        HIP_OK(hipEventRecord(h->ev[0], st));
+        HIP_OK(hipMemsetAsync(h->R.H, 0, sizeof(double) * (size_t)nred * nred, st));
+        HIP_OK(hipMemsetAsync(h->R.b, 0, sizeof(double) * nred, st));
+        if (h->n_pts > 0)
+            build_land_kernel<<<gl, 256, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono, h->d_err,
+                                                  h->d_chi2);
+        if (h->n_imu > 0) build_imu_kernel<<<h->n_imu, 64, 0, st>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
+        HIP_OK(hipEventRecord(h->ev[1], st));
+        HIP_OK(hipGetLastError());
+        if (it == 0) {
+            lambda = o->lambda_init;
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        float ms;
+        HIP_OK(hipEventSynchronize(h->ev[1]));
+        HIP_OK(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        h->stage_ms[0] += ms;
+        do {
+            HIP_OK(hipEventRecord(h->ev[2], st));
+            const long long nn = (long long)nred * nred;
+            prep_kernel<<<(int)((nn + 255) / 256), 256, 0, st>>>(h->R.H, h->d_S, nred, lambda, h->d_coef);
+            if (h->n_pts > 0) schur_kernel<<<gl, 256, 0, st>>>(h->L, h->R, lambda, h->d_S, h->d_coef);
+            HIP_OK(hipEventRecord(h->ev[3], st));
+            ldlt_kernel<<<1, 256, h->ldlt_lds, st>>>(h->d_S, nred, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
+                                                     h->use_lds, h->d_fail);
+            HIP_OK(hipEventRecord(h->ev[4], st));
+            int fail = 0;
+            HIP_OK(hipMemcpyAsync(&fail, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, st));
+            if (h->n_pts > 0)
+                backsub_kernel<<<gl, 256, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
+            update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, h->d_offV, h->d_offG, h->d_offA, h->n_opt, lambda, h->d_x,
+                                                A, B, h->d_scale_partial);
+            if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
+            if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc)) != OMV_OK) return rs;
+            HIP_OK(hipEventRecord(h->ev[5], st));
+            HIP_OK(hipEventSynchronize(h->ev[5]));
+            HIP_OK(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
+            h->stage_ms[1] += ms;
+            HIP_OK(hipEventElapsedTime(&ms, h->ev[3], h->ev[4]));
+            h->stage_ms[2] += ms;
+            HIP_OK(hipEventElapsedTime(&ms, h->ev[4], h->ev[5]));
+            h->stage_ms[3] += ms;
+            const bool ok = fail == 0;
+            double tempChi = sc[0];
+            errors_chi = sc[0];
+            errors_of_current = false;   // the last computed errors belong to the trial state
+            if (!ok) tempChi = std::numeric_limits<double>::max();
+            double scale = ok ? sc[1] : 0.0;
+            scale += 1e-3;
+            rho = (currentChi - tempChi) / scale;
+            ++trials;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                lambda *= std::max(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+                // fixed keyframes are identical in both buffers; make B the current state
+                h->cur = 1 - h->cur;
+                errors_of_current = true;
+                // the next trial rewrites every optimisable keyframe and every point of the other buffer
+            } else {
+                lambda *= ni;
+                ni *= 2;
+            }
+            qmax++;
+        } while (rho < 0 && qmax < o->max_trials);
+        if (qmax == o->max_trials || rho == 0) break;
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+        else nBad = 0;
+        if (nBad >= 3) break;
+    }
+    h->last_trials = trials;
+    res->err_end = (float)errors_chi;
+    res->iterations = its;
+    res->trials = trials;
+    res->lambda = lambda;
+    // write back the state (caller order)
+    const State &s = h->st[h->cur];
+    const int K = h->n_kf, C = h->rig.n_cams, P = h->n_pts, E = h->n_mono;
+    HIP_OK(hipMemcpy(p->Rwb, s.Rwb, sizeof(double) * 9 * K, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->twb, s.twb, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->Rcw, s.Rcw, sizeof(double) * 9 * K * C, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->tcw, s.tcw, sizeof(double) * 3 * K * C, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->vel, s.vel, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->bg, s.bg, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(p->ba, s.ba, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
+    std::vector<double> pts(3 * (size_t)P), chi2(E);
+    HIP_OK(hipMemcpy(pts.data(), s.pts, sizeof(double) * pts.size(), hipMemcpyDeviceToHost));
+    for (int q = 0; q < P; ++q)
+        for (int d = 0; d < 3; ++d) p->pts[3 * (size_t)h->perm_pt[q] + d] = pts[3 * (size_t)q + d];
+    if (E > 0) HIP_OK(hipMemcpy(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost));
+    for (int e = 0; e < E; ++e) {
+        const int oe = h->perm_edge[e];
+        if (res->mono_chi2) res->mono_chi2[oe] = chi2[e];
+        if (res->mono_outlier) {
+            const int k = p->mono_kf[oe], c = p->mono_cam[oe], pt = p->mono_pt[oe];
+            const double *R = p->Rcw + ((size_t)k * C + c) * 9, *t = p->tcw + ((size_t)k * C + c) * 3;
+            const double *X = p->pts + 3 * (size_t)pt;
+            const bool depth_pos = (R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2]) > 0.0;
+            const bool close = p->pt_track_depth[pt] < 10.f;
+            const double c2 = chi2[e];
+            res->mono_outlier[oe] = ((c2 > 5.991f && !close) || (c2 > 1.5f * 5.991f && close) || !depth_pos) ? 1 : 0;
+        }
+    }
+    const bool fail = (2 * res->err < res->err_end || std::isnan(res->err) || std::isnan(res->err_end)) && !o->large;
+    res->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
+    return OMV_OK;
+}
+
+omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials) {
+    if (!h || !ms4) return OMV_ERR_ARG;
+    for (int k = 0; k < 4; ++k) ms4[k] = h->stage_ms[k];
+    if (trials) *trials = h->last_trials;
+    return OMV_OK;
+}
+
+}  // extern "C"

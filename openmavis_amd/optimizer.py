@@ -1,0 +1,83 @@
+"""Host-side mirror of Optimizer::LocalInertialBA's optimisation (src/Optimizer.cc:2728-3385) on the
+device LM of libomv_hip.so (openmavis_amd/csrc/lba.hip).
+
+The reference builds a g2o graph from the local window (:2740-3267: VertexPose / VertexVelocity /
+VertexGyroBias / VertexAccBias, EdgeInertial + EdgeGyroRW + EdgeAccRW per keyframe pair, EdgeMono per
+observation) and runs `optimizer.optimize(opt_it)` with Levenberg-Marquardt (:3270-3274), then the
+outlier test (:3282-3296) and the FAIL guard (:3317-3321).  Here the flattened graph is a problem dict
+(see openmavis_amd.synth_ba.make_lba_problem for the field list, which is omv_lba_problem's):
+
+    ba = LocalInertialBA(max_kf=64, max_cams=5, max_pts=40000, max_mono=300000, max_imu=64)
+    ba.set_problem(prob)
+    res, state = ba.optimize(opt_it=10, lambda_init=1.0, large=False)
+
+`res` carries err / err_end (activeRobustChi2 before/after, as floats like the reference), status
+(OMV_LBA_OK / OMV_LBA_FAIL), the LM iteration / trial counts and per-edge chi2 + outlier flags; `state`
+the optimised Rwb, twb, Rcw, tcw, vel, bg, ba, pts.  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .synth_ba import as_struct, read_state
+
+OMV_LBA_OK = 0
+OMV_LBA_FAIL = 1
+
+
+def lba_options(large):
+    """LocalInertialBA's LM settings: bLarge -> 4 iterations, user lambda 1e-2; else 10 and 1e0."""
+    return dict(opt_it=4, lambda_init=1e-2) if large else dict(opt_it=10, lambda_init=1e0)
+
+
+class LocalInertialBA:
+    def __init__(self, max_kf=64, max_cams=5, max_pts=40000, max_mono=400000, max_imu=64):
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(lib.omv_lba_create(max_kf, max_cams, max_pts, max_mono, max_imu, ctypes.byref(h)),
+                   "omv_lba_create")
+        self._lib, self._h = lib, h
+        self._s = None
+        self._keep = None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.omv_lba_destroy(self._h)
+            self._h = None
+
+    def set_problem(self, prob):
+        s, keep = as_struct(prob, _lib.LbaProblem)
+        _lib.check(self._lib.omv_lba_set_problem(self._h, ctypes.byref(s)), "omv_lba_set_problem")
+        self._s, self._keep = s, keep
+        return self
+
+    def optimize(self, opt_it=10, lambda_init=1e0, max_trials=10, large=False):
+        if self._s is None:
+            raise _lib.OmvError("LocalInertialBA.optimize: no problem set")
+        o = _lib.LbaOpts(int(opt_it), float(lambda_init), int(max_trials), int(bool(large)))
+        E = self._s.n_mono
+        chi2 = np.zeros(E)
+        outl = np.zeros(E, np.uint8)
+        r = _lib.LbaResult()
+        r.mono_chi2, r.mono_outlier = _lib.ptr(chi2), _lib.ptr(outl)
+        _lib.check(self._lib.omv_lba_optimize(self._h, ctypes.byref(o), ctypes.byref(self._s), ctypes.byref(r)),
+                   "omv_lba_optimize")
+        res = dict(err=r.err, err_end=r.err_end, status=r.status, iterations=r.iterations, trials=r.trials,
+                   lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl)
+        return res, read_state(self._keep)
+
+    def evaluate(self):
+        """Residuals and visual Jacobians at the uploaded state (caller's edge order)."""
+        E, I = self._s.n_mono, self._s.n_imu
+        me, jx, jp, ie = np.zeros((E, 2)), np.zeros((E, 6)), np.zeros((E, 12)), np.zeros((I, 9))
+        _lib.check(self._lib.omv_lba_evaluate(self._h, _lib.ptr(me), _lib.ptr(jx), _lib.ptr(jp), _lib.ptr(ie)),
+                   "omv_lba_evaluate")
+        return dict(mono_err=me, mono_jx=jx, mono_jp=jp, imu_err=ie)
+
+    def stage_ms(self):
+        """Device ms of the last optimize: build, schur, solve, update+errors; and the trial count."""
+        ms = np.zeros(4)
+        t = ctypes.c_int(0)
+        _lib.check(self._lib.omv_lba_stage_ms(self._h, _lib.ptr(ms), ctypes.byref(t)), "omv_lba_stage_ms")
+        return dict(build=ms[0], schur=ms[1], solve=ms[2], update=ms[3], trials=t.value)

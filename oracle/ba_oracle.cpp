@@ -1,0 +1,949 @@
+// =====================================================================================================
+// TEST INFRASTRUCTURE ONLY — CPU oracle for the LocalInertialBA inner loop. Never linked into the
+// product path.
+//
+// Scalar restatement (double, single thread like g2o with OpenMP off, Thirdparty/g2o/CMakeLists.txt:48) of
+//   ImuCamPose::Update / isDepthPositive        src/G2oTypes.cc:192-235
+//   EdgeMono computeError / linearizeOplus      include/G2oTypes.h:293-299, src/G2oTypes.cc:356-380
+//   EdgeInertial ctor / computeError / lin.     src/G2oTypes.cc:478-599
+//   EdgeGyroRW / EdgeAccRW                      include/G2oTypes.h:567-633
+//   ExpSO3 / LogSO3 / (Inverse)RightJacobianSO3 src/G2oTypes.cc:797-860
+//   IMU::Preintegrated::GetDelta*               src/ImuTypes.cc:277-309 (float, Sophus SO3f::exp)
+//   KannalaBrandt8::project(Vector3d) / projectJac  src/CameraModels/KannalaBrandt8.cpp:28-46, 128-158
+//   RobustKernelHuber::robustify                Thirdparty/g2o/g2o/core/robust_kernel_impl.cpp:78-91
+//   constructQuadraticForm (binary / multi)     base_binary_edge.hpp:55-116, base_multi_edge.hpp:36-48,171+
+//   BlockSolver::solve / setLambda (Schur)      block_solver.hpp:353-486, 563-604
+//   OptimizationAlgorithmLevenberg::solve        optimization_algorithm_levenberg.cpp:61-169
+//   LocalInertialBA: err / optimize / outlier test / FAIL guard   src/Optimizer.cc:3270-3321
+// Linear-algebra kernels the reference takes from Eigen (absent here) are replaced by textbook
+// equivalents: 3x3 inverse by cofactors, 9x9 inverse by Gauss-Jordan with partial pivoting, symmetric
+// eigen-decomposition by cyclic Jacobi, NormalizeRotation (JacobiSVD U*V^T) by the polar factor
+// (Newton iteration), SimplicialLDLT by a dense LDL^T without pivoting.  These agree with the Eigen
+// results to rounding, so BA parity is tolerance-based (north star: 1e-5 relative).
+// =====================================================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <vector>
+
+#include "../include/omv.h"
+
+namespace {
+
+// ---- glibc atan2f (fdlibm e_atan2f.c / s_atanf.c), float, no contraction ---------------------------
+// KannalaBrandt8::project(Vector3d) evaluates theta and psi with atan2f (:30-31); the host libm is the
+// reference here, so the oracle simply calls it.
+
+// ---- small fixed-size linear algebra (row-major) -------------------------------------------------
+struct M3 {
+    double m[9];
+    double &operator()(int r, int c) { return m[3 * r + c]; }
+    double operator()(int r, int c) const { return m[3 * r + c]; }
+};
+struct V3 {
+    double v[3];
+    double &operator[](int i) { return v[i]; }
+    double operator[](int i) const { return v[i]; }
+};
+M3 eye() {
+    M3 r{};
+    r(0, 0) = r(1, 1) = r(2, 2) = 1;
+    return r;
+}
+M3 mul(const M3 &a, const M3 &b) {
+    M3 r{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r(i, j) = a(i, 0) * b(0, j) + a(i, 1) * b(1, j) + a(i, 2) * b(2, j);
+    return r;
+}
+V3 mul(const M3 &a, const V3 &x) {
+    V3 r;
+    for (int i = 0; i < 3; ++i) r[i] = a(i, 0) * x[0] + a(i, 1) * x[1] + a(i, 2) * x[2];
+    return r;
+}
+M3 tr(const M3 &a) {
+    M3 r;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r(i, j) = a(j, i);
+    return r;
+}
+M3 add(const M3 &a, const M3 &b) {
+    M3 r;
+    for (int k = 0; k < 9; ++k) r.m[k] = a.m[k] + b.m[k];
+    return r;
+}
+M3 scale(const M3 &a, double s) {
+    M3 r;
+    for (int k = 0; k < 9; ++k) r.m[k] = a.m[k] * s;
+    return r;
+}
+V3 add(const V3 &a, const V3 &b) { return V3{{a[0] + b[0], a[1] + b[1], a[2] + b[2]}}; }
+V3 sub(const V3 &a, const V3 &b) { return V3{{a[0] - b[0], a[1] - b[1], a[2] - b[2]}}; }
+V3 scale(const V3 &a, double s) { return V3{{a[0] * s, a[1] * s, a[2] * s}}; }
+M3 hat(const V3 &w) {
+    M3 r{};
+    r(0, 1) = -w[2], r(0, 2) = w[1], r(1, 0) = w[2], r(1, 2) = -w[0], r(2, 0) = -w[1], r(2, 1) = w[0];
+    return r;
+}
+M3 inv3(const M3 &a) {   // cofactors / determinant
+    M3 c;
+    c(0, 0) = a(1, 1) * a(2, 2) - a(1, 2) * a(2, 1);
+    c(0, 1) = a(0, 2) * a(2, 1) - a(0, 1) * a(2, 2);
+    c(0, 2) = a(0, 1) * a(1, 2) - a(0, 2) * a(1, 1);
+    c(1, 0) = a(1, 2) * a(2, 0) - a(1, 0) * a(2, 2);
+    c(1, 1) = a(0, 0) * a(2, 2) - a(0, 2) * a(2, 0);
+    c(1, 2) = a(0, 2) * a(1, 0) - a(0, 0) * a(1, 2);
+    c(2, 0) = a(1, 0) * a(2, 1) - a(1, 1) * a(2, 0);
+    c(2, 1) = a(0, 1) * a(2, 0) - a(0, 0) * a(2, 1);
+    c(2, 2) = a(0, 0) * a(1, 1) - a(0, 1) * a(1, 0);
+    const double det = a(0, 0) * c(0, 0) + a(0, 1) * c(1, 0) + a(0, 2) * c(2, 0);
+    return scale(c, 1.0 / det);
+}
+
+// Polar factor (NormalizeRotation's U*V^T) by Newton iteration X <- (X + X^-T) / 2.
+template <typename T>
+void polar3(T *r) {
+    for (int it = 0; it < 20; ++it) {
+        T c[9];
+        c[0] = r[4] * r[8] - r[5] * r[7];
+        c[1] = r[5] * r[6] - r[3] * r[8];
+        c[2] = r[3] * r[7] - r[4] * r[6];
+        c[3] = r[2] * r[7] - r[1] * r[8];
+        c[4] = r[0] * r[8] - r[2] * r[6];
+        c[5] = r[1] * r[6] - r[0] * r[7];
+        c[6] = r[1] * r[5] - r[2] * r[4];
+        c[7] = r[2] * r[3] - r[0] * r[5];
+        c[8] = r[0] * r[4] - r[1] * r[3];
+        const T det = r[0] * c[0] + r[1] * c[1] + r[2] * c[2];   // cofactor matrix = det * inv^T
+        T diff = 0;
+        for (int k = 0; k < 9; ++k) {
+            const T nv = (r[k] + c[k] / det) * T(0.5);
+            diff = std::max(diff, (T)std::fabs(nv - r[k]));
+            r[k] = nv;
+        }
+        if (diff == T(0)) break;
+    }
+}
+
+M3 normalize_rotation(M3 r) {
+    polar3(r.m);
+    return r;
+}
+
+// ---- SO3 helpers (src/G2oTypes.cc:797-860) -----------------------------------------------------------
+M3 expSO3(double x, double y, double z) {
+    const double d2 = x * x + y * y + z * z;
+    const double d = std::sqrt(d2);
+    const M3 W = hat(V3{{x, y, z}});
+    M3 res;
+    if (d < 1e-5) {
+        const M3 WW = mul(W, W);
+        for (int k = 0; k < 9; ++k) res.m[k] = eye().m[k] + W.m[k] + 0.5 * WW.m[k];
+    } else {
+        const M3 WW = mul(W, W);
+        const double s = std::sin(d), c = std::cos(d);
+        for (int k = 0; k < 9; ++k) res.m[k] = eye().m[k] + W.m[k] * s / d + WW.m[k] * (1.0 - c) / d2;
+    }
+    return normalize_rotation(res);
+}
+V3 logSO3(const M3 &R) {
+    const double t = R(0, 0) + R(1, 1) + R(2, 2);
+    V3 w{{(R(2, 1) - R(1, 2)) / 2, (R(0, 2) - R(2, 0)) / 2, (R(1, 0) - R(0, 1)) / 2}};
+    const double costheta = (t - 1.0) * 0.5f;
+    if (costheta > 1 || costheta < -1) return w;
+    const double theta = std::acos(costheta);
+    const double s = std::sin(theta);
+    if (std::fabs(s) < 1e-5) return w;
+    return V3{{theta * w[0] / s, theta * w[1] / s, theta * w[2] / s}};
+}
+M3 invRightJ(const V3 &v) {
+    const double x = v[0], y = v[1], z = v[2];
+    const double d2 = x * x + y * y + z * z;
+    const double d = std::sqrt(d2);
+    const M3 W = hat(v);
+    if (d < 1e-5) return eye();
+    const M3 WW = mul(W, W);
+    const double k = 1.0 / d2 - (1.0 + std::cos(d)) / (2.0 * d * std::sin(d));
+    M3 r;
+    for (int q = 0; q < 9; ++q) r.m[q] = eye().m[q] + W.m[q] / 2 + WW.m[q] * k;
+    return r;
+}
+M3 rightJ(const V3 &v) {
+    const double x = v[0], y = v[1], z = v[2];
+    const double d2 = x * x + y * y + z * z;
+    const double d = std::sqrt(d2);
+    const M3 W = hat(v);
+    if (d < 1e-5) return eye();
+    const M3 WW = mul(W, W);
+    M3 r;
+    for (int q = 0; q < 9; ++q)
+        r.m[q] = eye().m[q] - W.m[q] * (1.0 - std::cos(d)) / d2 + WW.m[q] * (d - std::sin(d)) / (d2 * d);
+    return r;
+}
+
+// ---- float preintegration getters (src/ImuTypes.cc:283-309) ----------------------------------------
+struct Preint {
+    float dR[9], dV[3], dP[3], JRg[9], JVg[9], JVa[9], JPg[9], JPa[9], b[6], dT, C[225];
+};
+void f33mul(const float *a, const float *b, float *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+void f33mulv(const float *a, const float *x, float *r) {
+    for (int i = 0; i < 3; ++i) r[i] = a[3 * i] * x[0] + a[3 * i + 1] * x[1] + a[3 * i + 2] * x[2];
+}
+// Sophus::SO3f::exp(w).matrix() (sophus/so3.hpp:583-621 + Eigen Quaternion::toRotationMatrix)
+void so3f_exp(const float *w, float *R) {
+    const float theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    float imag, real;
+    if (theta_sq < 1e-5f * 1e-5f) {
+        const float t4 = theta_sq * theta_sq;
+        imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * t4;
+        real = 1.0f - (float)(1.0 / 8.0) * theta_sq + (float)(1.0 / 384.0) * t4;
+    } else {
+        const float theta = std::sqrt(theta_sq);
+        const float half = 0.5f * theta;
+        imag = sinf(half) / theta;
+        real = cosf(half);
+    }
+    const float qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    R[0] = 1.0f - (tyy + tzz), R[1] = txy - twz, R[2] = txz + twy;
+    R[3] = txy + twz, R[4] = 1.0f - (txx + tzz), R[5] = tyz - twx;
+    R[6] = txz - twy, R[7] = tyz + twx, R[8] = 1.0f - (txx + tyy);
+}
+// b1 = (bax bay baz bwx bwy bwz) as floats (IMU::Bias ctor)
+void delta_rotation(const Preint &p, const float *b1, M3 &out) {
+    const float dbg[3] = {b1[3] - p.b[3], b1[4] - p.b[4], b1[5] - p.b[5]};
+    float w[3], E[9], R[9];
+    f33mulv(p.JRg, dbg, w);
+    so3f_exp(w, E);
+    f33mul(p.dR, E, R);
+    polar3(R);
+    for (int k = 0; k < 9; ++k) out.m[k] = (double)R[k];
+}
+V3 delta_vp(const float *d, const float *Jg, const float *Ja, const Preint &p, const float *b1) {
+    const float dbg[3] = {b1[3] - p.b[3], b1[4] - p.b[4], b1[5] - p.b[5]};
+    const float dba[3] = {b1[0] - p.b[0], b1[1] - p.b[1], b1[2] - p.b[2]};
+    float g[3], a[3];
+    f33mulv(Jg, dbg, g);
+    f33mulv(Ja, dba, a);
+    return V3{{(double)((d[0] + g[0]) + a[0]), (double)((d[1] + g[1]) + a[1]), (double)((d[2] + g[2]) + a[2])}};
+}
+
+// ---- KannalaBrandt8 (src/CameraModels/KannalaBrandt8.cpp:28-46, 128-158) ---------------------------
+void kb8_project(const float *k, const V3 &X, double &u, double &v) {
+    const double x2y2 = X[0] * X[0] + X[1] * X[1];
+    const double theta = atan2f(sqrtf((float)x2y2), (float)X[2]);
+    const double psi = atan2f((float)X[1], (float)X[0]);
+    const double t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const double r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+    u = k[0] * r * std::cos(psi) + k[2];
+    v = k[1] * r * std::sin(psi) + k[3];
+}
+void kb8_jac(const float *k, const V3 &X, double J[6]) {   // 2x3 row-major
+    const double x2 = X[0] * X[0], y2 = X[1] * X[1], z2 = X[2] * X[2];
+    const double r2 = x2 + y2, r = std::sqrt(r2), r3 = r2 * r;
+    const double theta = std::atan2(r, X[2]);
+    const double t2 = theta * theta, t3 = t2 * theta, t4 = t2 * t2, t5 = t4 * theta, t6 = t2 * t4, t7 = t6 * theta,
+                 t8 = t4 * t4, t9 = t8 * theta;
+    const double f = theta + t3 * k[4] + t5 * k[5] + t7 * k[6] + t9 * k[7];
+    const double fd = 1 + 3 * k[4] * t2 + 5 * k[5] * t4 + 7 * k[6] * t6 + 9 * k[7] * t8;
+    J[0] = k[0] * (fd * X[2] * x2 / (r2 * (r2 + z2)) + f * y2 / r3);
+    J[3] = k[1] * (fd * X[2] * X[1] * X[0] / (r2 * (r2 + z2)) - f * X[1] * X[0] / r3);
+    J[1] = k[0] * (fd * X[2] * X[1] * X[0] / (r2 * (r2 + z2)) - f * X[1] * X[0] / r3);
+    J[4] = k[1] * (fd * X[2] * y2 / (r2 * (r2 + z2)) + f * x2 / r3);
+    J[2] = -k[0] * fd * X[0] / (r2 + z2);
+    J[5] = -k[1] * fd * X[1] / (r2 + z2);
+}
+
+// ---- dense helpers ---------------------------------------------------------------------------------
+bool invert_gj(std::vector<double> &A, int n) {   // in place, partial pivoting
+    std::vector<double> I(n * n, 0.0);
+    for (int i = 0; i < n; ++i) I[i * n + i] = 1;
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        for (int r = c + 1; r < n; ++r)
+            if (std::fabs(A[r * n + c]) > std::fabs(A[p * n + c])) p = r;
+        if (A[p * n + c] == 0) return false;
+        if (p != c)
+            for (int k = 0; k < n; ++k) std::swap(A[p * n + k], A[c * n + k]), std::swap(I[p * n + k], I[c * n + k]);
+        const double d = A[c * n + c];
+        for (int k = 0; k < n; ++k) A[c * n + k] /= d, I[c * n + k] /= d;
+        for (int r = 0; r < n; ++r)
+            if (r != c) {
+                const double f = A[r * n + c];
+                if (f == 0) continue;
+                for (int k = 0; k < n; ++k) A[r * n + k] -= f * A[c * n + k], I[r * n + k] -= f * I[c * n + k];
+            }
+    }
+    A = I;
+    return true;
+}
+// cyclic Jacobi eigen-decomposition of a symmetric n x n matrix: A = V diag(w) V^T
+void sym_eig(std::vector<double> A, int n, std::vector<double> &w, std::vector<double> &V) {
+    V.assign(n * n, 0.0);
+    for (int i = 0; i < n; ++i) V[i * n + i] = 1;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = A[p * n + q];
+                if (apq == 0) continue;
+                const double th = (A[q * n + q] - A[p * n + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    const double akp = A[k * n + p], akq = A[k * n + q];
+                    A[k * n + p] = c * akp - s * akq;
+                    A[k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double apk = A[p * n + k], aqk = A[q * n + k];
+                    A[p * n + k] = c * apk - s * aqk;
+                    A[q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq;
+                    V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    w.resize(n);
+    for (int i = 0; i < n; ++i) w[i] = A[i * n + i];
+}
+
+// ---- the problem -------------------------------------------------------------------------------------
+struct Pose {
+    M3 Rwb;
+    V3 twb;
+    std::vector<M3> Rcw;
+    std::vector<V3> tcw;
+};
+
+struct Solver {
+    const omv_lba_problem &P;
+    int C;
+    std::vector<M3> Rcb, Rbc;
+    std::vector<V3> tcb, tbc;
+    // state
+    std::vector<Pose> pose;
+    std::vector<V3> vel, bg, ba, pts;
+    // inertial edges
+    std::vector<Preint> pre;
+    std::vector<std::vector<double>> info9;   // 81 each (robust/scale applied to scale only)
+    std::vector<M3> infoG, infoA;
+    // reduced-system layout
+    std::vector<int> offP, offV, offG, offA;
+    int nred = 0;
+    // errors (last computeActiveErrors)
+    std::vector<double> e_mono;   // 2 per edge
+    std::vector<double> e_imu;    // 9 per edge
+    std::vector<V3> e_gr, e_ar;
+    double delta_mono, dsqr_mono, delta_imu, dsqr_imu;
+
+    explicit Solver(const omv_lba_problem &p) : P(p), C(p.n_cams) {
+        for (int c = 0; c < C; ++c) {
+            M3 a, b;
+            std::memcpy(a.m, p.Rcb + 9 * c, 72);
+            std::memcpy(b.m, p.Rbc + 9 * c, 72);
+            Rcb.push_back(a), Rbc.push_back(b);
+            tcb.push_back(V3{{p.tcb[3 * c], p.tcb[3 * c + 1], p.tcb[3 * c + 2]}});
+            tbc.push_back(V3{{p.tbc[3 * c], p.tbc[3 * c + 1], p.tbc[3 * c + 2]}});
+        }
+        pose.resize(p.n_kf);
+        vel.resize(p.n_kf), bg.resize(p.n_kf), ba.resize(p.n_kf);
+        for (int k = 0; k < p.n_kf; ++k) {
+            std::memcpy(pose[k].Rwb.m, p.Rwb + 9 * k, 72);
+            std::memcpy(pose[k].twb.v, p.twb + 3 * k, 24);
+            pose[k].Rcw.resize(C), pose[k].tcw.resize(C);
+            for (int c = 0; c < C; ++c) {
+                std::memcpy(pose[k].Rcw[c].m, p.Rcw + 9 * (k * C + c), 72);
+                std::memcpy(pose[k].tcw[c].v, p.tcw + 3 * (k * C + c), 24);
+            }
+            std::memcpy(vel[k].v, p.vel + 3 * k, 24);
+            std::memcpy(bg[k].v, p.bg + 3 * k, 24);
+            std::memcpy(ba[k].v, p.ba + 3 * k, 24);
+        }
+        pts.resize(p.n_pts);
+        for (int i = 0; i < p.n_pts; ++i) std::memcpy(pts[i].v, p.pts + 3 * i, 24);
+        // EdgeInertial ctor: Info = sym(C[0:9,0:9]^-1), eigenvalues < 1e-12 zeroed (:486-495)
+        pre.resize(p.n_imu);
+        info9.resize(p.n_imu);
+        infoG.resize(p.n_imu), infoA.resize(p.n_imu);
+        for (int i = 0; i < p.n_imu; ++i) {
+            std::memcpy(&pre[i], p.preint + (size_t)i * OMV_PREINT_FLOATS, sizeof(float) * OMV_PREINT_FLOATS);
+            std::vector<double> A(81);
+            for (int r = 0; r < 9; ++r)
+                for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)pre[i].C[r * 15 + c];
+            invert_gj(A, 9);
+            for (int r = 0; r < 9; ++r)
+                for (int c = r + 1; c < 9; ++c) {
+                    const double s = (A[r * 9 + c] + A[c * 9 + r]) / 2;
+                    A[r * 9 + c] = A[c * 9 + r] = s;
+                }
+            std::vector<double> w, V;
+            sym_eig(A, 9, w, V);
+            for (double &x : w)
+                if (x < 1e-12) x = 0;
+            std::vector<double> I9(81, 0.0);
+            for (int r = 0; r < 9; ++r)
+                for (int c = 0; c < 9; ++c) {
+                    double s = 0;
+                    for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
+                    I9[r * 9 + c] = s;
+                }
+            const double sc = p.imu_info_scale ? (double)p.imu_info_scale[i] : 1.0;
+            for (double &x : I9) x *= sc;
+            info9[i] = I9;
+            M3 g, a;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    g(r, c) = (double)pre[i].C[(9 + r) * 15 + 9 + c];
+                    a(r, c) = (double)pre[i].C[(12 + r) * 15 + 12 + c];
+                }
+            infoG[i] = inv3(g), infoA[i] = inv3(a);
+        }
+        // vertex layout of the non-marginalised part: per optimisable KF pose (6) [+ v, bg, ba]
+        offP.assign(p.n_kf, -1), offV.assign(p.n_kf, -1), offG.assign(p.n_kf, -1), offA.assign(p.n_kf, -1);
+        for (int k = 0; k < p.n_opt; ++k) {
+            offP[k] = nred, nred += 6;
+            if (p.kf_imu[k]) offV[k] = nred, offG[k] = nred + 3, offA[k] = nred + 6, nred += 9;
+        }
+        delta_mono = (double)(float)std::sqrt(5.991);   // thHuberMono is a float (:3036)
+        dsqr_mono = delta_mono * delta_mono;           // RobustKernel::setDelta: dsqr = delta * delta
+        delta_imu = std::sqrt(16.92);
+        dsqr_imu = delta_imu * delta_imu;
+        e_mono.assign(2 * (size_t)p.n_mono, 0.0);
+        e_imu.assign(9 * (size_t)p.n_imu, 0.0);
+        e_gr.resize(p.n_imu), e_ar.resize(p.n_imu);
+    }
+
+    const float *camk(int c) const { return P.cam + 8 * c; }
+
+    // --- errors ---
+    void mono_error(int e, double out[2]) const {
+        const int k = P.mono_kf[e], c = P.mono_cam[e];
+        const V3 Xc = add(mul(pose[k].Rcw[c], pts[P.mono_pt[e]]), pose[k].tcw[c]);
+        double u, v;
+        kb8_project(camk(c), Xc, u, v);
+        out[0] = P.mono_obs[2 * e] - u;
+        out[1] = P.mono_obs[2 * e + 1] - v;
+    }
+    void bias_floats(int k, float b1[6]) const {   // IMU::Bias(ba, bg) as floats
+        for (int q = 0; q < 3; ++q) b1[q] = (float)ba[k][q], b1[3 + q] = (float)bg[k][q];
+    }
+    void imu_error(int i, double out[9]) const {
+        const int k1 = P.imu_kf1[i], k2 = P.imu_kf2[i];
+        const Preint &p = pre[i];
+        float b1[6];
+        bias_floats(k1, b1);
+        M3 dR;
+        delta_rotation(p, b1, dR);
+        const V3 dV = delta_vp(p.dV, p.JVg, p.JVa, p, b1);
+        const V3 dP = delta_vp(p.dP, p.JPg, p.JPa, p, b1);
+        const double dt = (double)p.dT;
+        const V3 g{{0, 0, -(double)9.81f}};
+        const V3 er = logSO3(mul(mul(tr(dR), tr(pose[k1].Rwb)), pose[k2].Rwb));
+        const V3 ev = sub(mul(tr(pose[k1].Rwb), sub(sub(vel[k2], vel[k1]), scale(g, dt))), dV);
+        const V3 gdt2 = V3{{g[0] * dt * dt / 2, g[1] * dt * dt / 2, g[2] * dt * dt / 2}};
+        const V3 ep = sub(mul(tr(pose[k1].Rwb), sub(sub(sub(pose[k2].twb, pose[k1].twb), scale(vel[k1], dt)), gdt2)), dP);
+        for (int q = 0; q < 3; ++q) out[q] = er[q], out[3 + q] = ev[q], out[6 + q] = ep[q];
+    }
+    void compute_errors() {
+        for (int e = 0; e < P.n_mono; ++e) mono_error(e, &e_mono[2 * e]);
+        for (int i = 0; i < P.n_imu; ++i) {
+            imu_error(i, &e_imu[9 * i]);
+            e_gr[i] = sub(bg[P.imu_kf2[i]], bg[P.imu_kf1[i]]);
+            e_ar[i] = sub(ba[P.imu_kf2[i]], ba[P.imu_kf1[i]]);
+        }
+    }
+    double mono_chi2(int e) const {
+        const double w = (double)P.mono_inv_sigma2[e];
+        return e_mono[2 * e] * w * e_mono[2 * e] + e_mono[2 * e + 1] * w * e_mono[2 * e + 1];
+    }
+    double imu_chi2(int i) const {
+        const double *e = &e_imu[9 * i];
+        const std::vector<double> &I = info9[i];
+        double s = 0;
+        for (int r = 0; r < 9; ++r) {
+            double t = 0;
+            for (int c = 0; c < 9; ++c) t += I[r * 9 + c] * e[c];
+            s += e[r] * t;
+        }
+        return s;
+    }
+    static double quad3(const V3 &e, const M3 &I) {
+        const V3 t = mul(I, e);
+        return e[0] * t[0] + e[1] * t[1] + e[2] * t[2];
+    }
+    static void huber(double e2, double delta, double dsqr, double rho[3]) {
+        if (e2 <= dsqr) {
+            rho[0] = e2, rho[1] = 1, rho[2] = 0;
+        } else {
+            const double s = std::sqrt(e2);
+            rho[0] = 2 * s * delta - dsqr;
+            rho[1] = delta / s;
+            rho[2] = -0.5 * rho[1] / e2;
+        }
+    }
+    double robust_chi2() const {
+        double chi = 0, rho[3];
+        for (int i = 0; i < P.n_imu; ++i) {
+            const double c = imu_chi2(i);
+            if (P.imu_robust && P.imu_robust[i]) {
+                huber(c, delta_imu, dsqr_imu, rho);
+                chi += rho[0];
+            } else {
+                chi += c;
+            }
+            chi += quad3(e_gr[i], infoG[i]);
+            chi += quad3(e_ar[i], infoA[i]);
+        }
+        for (int e = 0; e < P.n_mono; ++e) {
+            huber(mono_chi2(e), delta_mono, dsqr_mono, rho);
+            chi += rho[0];
+        }
+        return chi;
+    }
+
+    // --- linearisation (Jacobians at the current state) ---
+    void mono_jac(int e, double JX[6], double JP[12]) const {
+        const int k = P.mono_kf[e], c = P.mono_cam[e];
+        const M3 &Rcw = pose[k].Rcw[c];
+        const V3 Xc = add(mul(Rcw, pts[P.mono_pt[e]]), pose[k].tcw[c]);
+        const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
+        double pj[6];
+        kb8_jac(camk(c), Xc, pj);
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 3; ++q)
+                JX[3 * r + q] = -(pj[3 * r] * Rcw(0, q) + pj[3 * r + 1] * Rcw(1, q) + pj[3 * r + 2] * Rcw(2, q));
+        const double x = Xb[0], y = Xb[1], z = Xb[2];
+        const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+        double pr[6];   // proj_jac * Rcb
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 3; ++q)
+                pr[3 * r + q] = pj[3 * r] * Rcb[c](0, q) + pj[3 * r + 1] * Rcb[c](1, q) + pj[3 * r + 2] * Rcb[c](2, q);
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 6; ++q)
+                JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    }
+    // EdgeInertial::linearizeOplus (:542-599): J[v] 9 x dim(v), v = P1 V1 G1 A1 P2 V2
+    void imu_jac(int i, std::vector<double> J[6]) const {
+        const int k1 = P.imu_kf1[i], k2 = P.imu_kf2[i];
+        const Preint &p = pre[i];
+        float b1[6];
+        bias_floats(k1, b1);
+        const float dbgf[3] = {b1[3] - p.b[3], b1[4] - p.b[4], b1[5] - p.b[5]};
+        const V3 dbg{{(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]}};
+        const M3 Rwb1 = pose[k1].Rwb, Rbw1 = tr(Rwb1), Rwb2 = pose[k2].Rwb;
+        M3 dR;
+        delta_rotation(p, b1, dR);
+        const M3 eR = mul(mul(tr(dR), Rbw1), Rwb2);
+        const V3 er = logSO3(eR);
+        const M3 invJr = invRightJ(er);
+        M3 JRg, JVg, JPg, JVa, JPa;
+        for (int q = 0; q < 9; ++q)
+            JRg.m[q] = p.JRg[q], JVg.m[q] = p.JVg[q], JPg.m[q] = p.JPg[q], JVa.m[q] = p.JVa[q], JPa.m[q] = p.JPa[q];
+        const double dt = (double)p.dT;
+        const V3 g{{0, 0, -(double)9.81f}};
+        const int dims[6] = {6, 3, 3, 3, 6, 3};
+        for (int v = 0; v < 6; ++v) J[v].assign(9 * dims[v], 0.0);
+        auto put = [&](std::vector<double> &A, int cols, int r0, int c0, const M3 &B) {
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) A[(r0 + r) * cols + c0 + c] = B(r, c);
+        };
+        put(J[0], 6, 0, 0, scale(mul(mul(invJr, tr(Rwb2)), Rwb1), -1.0));
+        put(J[0], 6, 3, 0, hat(mul(Rbw1, sub(sub(vel[k2], vel[k1]), scale(g, dt)))));
+        const V3 half{{0.5 * g[0] * dt * dt, 0.5 * g[1] * dt * dt, 0.5 * g[2] * dt * dt}};
+        put(J[0], 6, 6, 0, hat(mul(Rbw1, sub(sub(sub(pose[k2].twb, pose[k1].twb), scale(vel[k1], dt)), half))));
+        put(J[0], 6, 6, 3, scale(eye(), -1.0));
+        put(J[1], 3, 3, 0, scale(Rbw1, -1.0));
+        put(J[1], 3, 6, 0, scale(Rbw1, -dt));
+        put(J[2], 3, 0, 0, scale(mul(mul(mul(invJr, tr(eR)), rightJ(mul(JRg, dbg))), JRg), -1.0));
+        put(J[2], 3, 3, 0, scale(JVg, -1.0));
+        put(J[2], 3, 6, 0, scale(JPg, -1.0));
+        put(J[3], 3, 3, 0, scale(JVa, -1.0));
+        put(J[3], 3, 6, 0, scale(JPa, -1.0));
+        put(J[4], 6, 0, 0, invJr);
+        put(J[4], 6, 6, 3, mul(Rbw1, Rwb2));
+        put(J[5], 3, 3, 0, Rbw1);
+    }
+
+    // --- system: dense reduced part + per-landmark blocks ---
+    struct Landmark {
+        double Hll[9] = {0}, bl[3] = {0};
+        std::map<int, std::vector<double>> Hpl;   // kf -> 6x3 (pose rows x point cols)
+    };
+    std::vector<double> H, b;   // nred x nred, nred
+    std::vector<Landmark> lm;
+
+    void add_block(int r0, int rdim, int c0, int cdim, const double *A, int lda) {
+        for (int r = 0; r < rdim; ++r)
+            for (int c = 0; c < cdim; ++c) H[(size_t)(r0 + r) * nred + c0 + c] += A[r * lda + c];
+    }
+
+    void build_system() {
+        H.assign((size_t)nred * nred, 0.0);
+        b.assign(nred, 0.0);
+        lm.assign(P.n_pts, Landmark());
+        double rho[3];
+        // inertial + random-walk edges
+        for (int i = 0; i < P.n_imu; ++i) {
+            const int k1 = P.imu_kf1[i], k2 = P.imu_kf2[i];
+            std::vector<double> J[6];
+            imu_jac(i, J);
+            const double *e = &e_imu[9 * i];
+            double w = 1.0;
+            if (P.imu_robust && P.imu_robust[i]) {
+                huber(imu_chi2(i), delta_imu, dsqr_imu, rho);
+                w = rho[1];
+            }
+            const std::vector<double> &I = info9[i];
+            double Ie[9];
+            for (int r = 0; r < 9; ++r) {
+                double t = 0;
+                for (int c = 0; c < 9; ++c) t += I[r * 9 + c] * e[c];
+                Ie[r] = -t * w;   // omega_r = -Omega e, times rho'
+            }
+            const int off[6] = {offP[k1], offV[k1], offG[k1], offA[k1], offP[k2], offV[k2]};
+            const int dims[6] = {6, 3, 3, 3, 6, 3};
+            for (int a = 0; a < 6; ++a) {
+                if (off[a] < 0) continue;
+                // AtO = J_a^T Omega' (dims[a] x 9)
+                std::vector<double> AtO(dims[a] * 9, 0.0);
+                for (int r = 0; r < dims[a]; ++r)
+                    for (int c = 0; c < 9; ++c) {
+                        double s = 0;
+                        for (int k = 0; k < 9; ++k) s += J[a][k * dims[a] + r] * I[k * 9 + c];
+                        AtO[r * 9 + c] = s * w;
+                    }
+                for (int r = 0; r < dims[a]; ++r) {
+                    double s = 0;
+                    for (int k = 0; k < 9; ++k) s += J[a][k * dims[a] + r] * Ie[k];
+                    b[off[a] + r] += s;
+                }
+                for (int bb = a; bb < 6; ++bb) {
+                    if (off[bb] < 0) continue;
+                    std::vector<double> blk(dims[a] * dims[bb], 0.0);
+                    for (int r = 0; r < dims[a]; ++r)
+                        for (int c = 0; c < dims[bb]; ++c) {
+                            double s = 0;
+                            for (int k = 0; k < 9; ++k) s += AtO[r * 9 + k] * J[bb][k * dims[bb] + c];
+                            blk[r * dims[bb] + c] = s;
+                        }
+                    add_block(off[a], dims[a], off[bb], dims[bb], blk.data(), dims[bb]);
+                    if (bb != a) {   // keep H symmetric (dense storage of both triangles)
+                        std::vector<double> t(dims[a] * dims[bb]);
+                        for (int r = 0; r < dims[a]; ++r)
+                            for (int c = 0; c < dims[bb]; ++c) t[c * dims[a] + r] = blk[r * dims[bb] + c];
+                        add_block(off[bb], dims[bb], off[a], dims[a], t.data(), dims[a]);
+                    }
+                }
+            }
+            // EdgeGyroRW / EdgeAccRW: J1 = -I, J2 = I, no robust kernel
+            for (int which = 0; which < 2; ++which) {
+                const V3 &er = which ? e_ar[i] : e_gr[i];
+                const M3 &Iw = which ? infoA[i] : infoG[i];
+                const int o1 = which ? offA[k1] : offG[k1], o2 = which ? offA[k2] : offG[k2];
+                const V3 Oe = mul(Iw, er);
+                if (o1 >= 0) {
+                    add_block(o1, 3, o1, 3, Iw.m, 3);
+                    for (int r = 0; r < 3; ++r) b[o1 + r] += Oe[r];   // (-I)^T (-Omega e)
+                }
+                if (o2 >= 0) {
+                    add_block(o2, 3, o2, 3, Iw.m, 3);
+                    for (int r = 0; r < 3; ++r) b[o2 + r] -= Oe[r];
+                }
+                if (o1 >= 0 && o2 >= 0) {
+                    const M3 m = scale(Iw, -1.0);
+                    add_block(o1, 3, o2, 3, m.m, 3);
+                    add_block(o2, 3, o1, 3, tr(m).m, 3);
+                }
+            }
+        }
+        // visual edges
+        for (int e = 0; e < P.n_mono; ++e) {
+            double JX[6], JP[12];
+            mono_jac(e, JX, JP);
+            huber(mono_chi2(e), delta_mono, dsqr_mono, rho);
+            const double w = (double)P.mono_inv_sigma2[e] * rho[1];   // robust information
+            const double om0 = -(double)P.mono_inv_sigma2[e] * e_mono[2 * e] * rho[1];
+            const double om1 = -(double)P.mono_inv_sigma2[e] * e_mono[2 * e + 1] * rho[1];
+            Landmark &L = lm[P.mono_pt[e]];
+            for (int r = 0; r < 3; ++r) {
+                L.bl[r] += JX[r] * om0 + JX[3 + r] * om1;
+                for (int c = 0; c < 3; ++c) L.Hll[3 * r + c] += w * (JX[r] * JX[c] + JX[3 + r] * JX[3 + c]);
+            }
+            const int k = P.mono_kf[e];
+            const int o = offP[k];
+            if (o < 0) continue;
+            for (int r = 0; r < 6; ++r) {
+                b[o + r] += JP[r] * om0 + JP[6 + r] * om1;
+                for (int c = 0; c < 6; ++c) H[(size_t)(o + r) * nred + o + c] += w * (JP[r] * JP[c] + JP[6 + r] * JP[6 + c]);
+            }
+            std::vector<double> &B = L.Hpl[k];
+            if (B.empty()) B.assign(18, 0.0);
+            for (int r = 0; r < 6; ++r)
+                for (int c = 0; c < 3; ++c) B[3 * r + c] += w * (JP[r] * JX[c] + JP[6 + r] * JX[3 + c]);
+        }
+    }
+
+    // --- one LM trial: damped Schur solve; x = [poses | landmarks] ---
+    bool solve(double lambda, std::vector<double> &xp, std::vector<double> &xl) {
+        std::vector<double> S = H;
+        for (int i = 0; i < nred; ++i) S[(size_t)i * nred + i] += lambda;
+        std::vector<double> coef(nred, 0.0);
+        std::vector<M3> Dinv(P.n_pts);
+        for (int p = 0; p < P.n_pts; ++p) {
+            Landmark &L = lm[p];
+            M3 D;
+            std::memcpy(D.m, L.Hll, 72);
+            for (int q = 0; q < 3; ++q) D(q, q) += lambda;
+            Dinv[p] = inv3(D);
+            const V3 db = mul(Dinv[p], V3{{L.bl[0], L.bl[1], L.bl[2]}});
+            for (auto it = L.Hpl.begin(); it != L.Hpl.end(); ++it) {
+                const double *Bi = it->second.data();
+                const int oi = offP[it->first];
+                for (int r = 0; r < 6; ++r) coef[oi + r] += Bi[3 * r] * db[0] + Bi[3 * r + 1] * db[1] + Bi[3 * r + 2] * db[2];
+                double BD[18];   // Bi * Dinv
+                for (int r = 0; r < 6; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        BD[3 * r + c] = Bi[3 * r] * Dinv[p](0, c) + Bi[3 * r + 1] * Dinv[p](1, c) + Bi[3 * r + 2] * Dinv[p](2, c);
+                for (auto jt = L.Hpl.begin(); jt != L.Hpl.end(); ++jt) {
+                    const double *Bj = jt->second.data();
+                    const int oj = offP[jt->first];
+                    for (int r = 0; r < 6; ++r)
+                        for (int c = 0; c < 6; ++c)
+                            S[(size_t)(oi + r) * nred + oj + c] -=
+                                BD[3 * r] * Bj[3 * c] + BD[3 * r + 1] * Bj[3 * c + 1] + BD[3 * r + 2] * Bj[3 * c + 2];
+                }
+            }
+        }
+        std::vector<double> bs(nred);
+        for (int i = 0; i < nred; ++i) bs[i] = b[i] - coef[i];
+        // dense LDL^T without pivoting (SimplicialLDLT fails only on a zero pivot)
+        const int n = nred;
+        std::vector<double> Lm(S), d(n);
+        for (int j = 0; j < n; ++j) {
+            double dj = Lm[(size_t)j * n + j];
+            for (int k = 0; k < j; ++k) dj -= Lm[(size_t)j * n + k] * Lm[(size_t)j * n + k] * d[k];
+            if (dj == 0 || !std::isfinite(dj)) return false;
+            d[j] = dj;
+            for (int i = j + 1; i < n; ++i) {
+                double s = Lm[(size_t)i * n + j];
+                for (int k = 0; k < j; ++k) s -= Lm[(size_t)i * n + k] * Lm[(size_t)j * n + k] * d[k];
+                Lm[(size_t)i * n + j] = s / dj;
+            }
+        }
+        xp.assign(n, 0.0);
+        for (int i = 0; i < n; ++i) {
+            double s = bs[i];
+            for (int k = 0; k < i; ++k) s -= Lm[(size_t)i * n + k] * xp[k];
+            xp[i] = s;
+        }
+        for (int i = 0; i < n; ++i) xp[i] /= d[i];
+        for (int i = n - 1; i >= 0; --i) {
+            double s = xp[i];
+            for (int k = i + 1; k < n; ++k) s -= Lm[(size_t)k * n + i] * xp[k];
+            xp[i] = s;
+        }
+        xl.assign(3 * (size_t)P.n_pts, 0.0);
+        for (int p = 0; p < P.n_pts; ++p) {
+            const Landmark &L = lm[p];
+            V3 c{{L.bl[0], L.bl[1], L.bl[2]}};
+            for (auto it = L.Hpl.begin(); it != L.Hpl.end(); ++it) {
+                const double *Bi = it->second.data();
+                const int oi = offP[it->first];
+                for (int q = 0; q < 3; ++q)
+                    for (int r = 0; r < 6; ++r) c[q] -= Bi[3 * r + q] * xp[oi + r];
+            }
+            const V3 x = mul(Dinv[p], c);
+            for (int q = 0; q < 3; ++q) xl[3 * p + q] = x[q];
+        }
+        return true;
+    }
+
+    void update(const std::vector<double> &xp, const std::vector<double> &xl) {
+        for (int k = 0; k < P.n_opt; ++k) {
+            const double *u = &xp[offP[k]];
+            Pose &ps = pose[k];
+            ps.twb = add(ps.twb, mul(ps.Rwb, V3{{u[3], u[4], u[5]}}));
+            ps.Rwb = mul(ps.Rwb, expSO3(u[0], u[1], u[2]));
+            const M3 Rbw = tr(ps.Rwb);
+            const V3 tbw = scale(mul(Rbw, ps.twb), -1.0);
+            for (int c = 0; c < C; ++c) {
+                ps.Rcw[c] = mul(Rcb[c], Rbw);
+                ps.tcw[c] = add(mul(Rcb[c], tbw), tcb[c]);
+            }
+            if (offV[k] >= 0) {
+                for (int q = 0; q < 3; ++q) {
+                    vel[k][q] += xp[offV[k] + q];
+                    bg[k][q] += xp[offG[k] + q];
+                    ba[k][q] += xp[offA[k] + q];
+                }
+            }
+        }
+        for (int p = 0; p < P.n_pts; ++p)
+            for (int q = 0; q < 3; ++q) pts[p][q] += xl[3 * p + q];
+    }
+
+    double scale_of(const std::vector<double> &xp, const std::vector<double> &xl, double lambda) const {
+        // computeScale: sum_j x_j (lambda x_j + b_j) over the full vector [poses | landmarks]
+        double s = 0;
+        for (int i = 0; i < nred; ++i) s += xp[i] * (lambda * xp[i] + b[i]);
+        for (int p = 0; p < P.n_pts; ++p)
+            for (int q = 0; q < 3; ++q) s += xl[3 * p + q] * (lambda * xl[3 * p + q] + lm[p].bl[q]);
+        return s;
+    }
+
+    struct Snapshot {
+        std::vector<Pose> pose;
+        std::vector<V3> vel, bg, ba, pts;
+    };
+    Snapshot push() const { return Snapshot{pose, vel, bg, ba, pts}; }
+    void pop(const Snapshot &s) { pose = s.pose, vel = s.vel, bg = s.bg, ba = s.ba, pts = s.pts; }
+
+    void write_state(omv_lba_problem &p) const {
+        for (int k = 0; k < p.n_kf; ++k) {
+            std::memcpy(p.Rwb + 9 * k, pose[k].Rwb.m, 72);
+            std::memcpy(p.twb + 3 * k, pose[k].twb.v, 24);
+            for (int c = 0; c < C; ++c) {
+                std::memcpy(p.Rcw + 9 * (k * C + c), pose[k].Rcw[c].m, 72);
+                std::memcpy(p.tcw + 3 * (k * C + c), pose[k].tcw[c].v, 24);
+            }
+            std::memcpy(p.vel + 3 * k, vel[k].v, 24);
+            std::memcpy(p.bg + 3 * k, bg[k].v, 24);
+            std::memcpy(p.ba + 3 * k, ba[k].v, 24);
+        }
+        for (int i = 0; i < p.n_pts; ++i) std::memcpy(p.pts + 3 * i, pts[i].v, 24);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+// Residuals and Jacobians at the given state (parity of the edge math).
+int oracle_lba_evaluate(const omv_lba_problem *p, double *mono_err, double *mono_jx, double *mono_jp,
+                        double *imu_err, double *imu_jac /* [n_imu][9*24] v = P1 V1 G1 A1 P2 V2 */) {
+    Solver s(*p);
+    s.compute_errors();
+    for (int e = 0; e < p->n_mono; ++e) {
+        if (mono_err) mono_err[2 * e] = s.e_mono[2 * e], mono_err[2 * e + 1] = s.e_mono[2 * e + 1];
+        if (mono_jx || mono_jp) {
+            double JX[6], JP[12];
+            s.mono_jac(e, JX, JP);
+            if (mono_jx) std::memcpy(mono_jx + 6 * e, JX, 48);
+            if (mono_jp) std::memcpy(mono_jp + 12 * e, JP, 96);
+        }
+    }
+    for (int i = 0; i < p->n_imu; ++i) {
+        if (imu_err) std::memcpy(imu_err + 9 * i, &s.e_imu[9 * i], 72);
+        if (imu_jac) {
+            std::vector<double> J[6];
+            s.imu_jac(i, J);
+            const int dims[6] = {6, 3, 3, 3, 6, 3};
+            int c0 = 0;
+            for (int v = 0; v < 6; ++v) {
+                for (int r = 0; r < 9; ++r)
+                    for (int c = 0; c < dims[v]; ++c) imu_jac[(size_t)i * 216 + r * 24 + c0 + c] = J[v][r * dims[v] + c];
+                c0 += dims[v];
+            }
+        }
+    }
+    return 0;
+}
+
+// Optimizer::LocalInertialBA's optimisation (:3270-3321): err, optimize(opt_it), err_end, outlier test,
+// FAIL guard.  Writes the final state into p; trial_log (optional) gets [chi2_before, chi2_after,
+// lambda] per trial.
+int oracle_lba_optimize(omv_lba_problem *p, const omv_lba_opts *o, omv_lba_result *r, double *trial_log,
+                        int log_cap) {
+    Solver s(*p);
+    s.compute_errors();
+    r->err = (float)s.robust_chi2();
+    double lambda = 0, ni = 2;
+    int nBad = 0, trials = 0, its = 0;
+    for (int it = 0; it < o->opt_it; ++it) {
+        ++its;
+        s.compute_errors();
+        double currentChi = s.robust_chi2();
+        const double iniChi = currentChi;
+        s.build_system();
+        if (it == 0) {
+            lambda = o->lambda_init;   // user lambda init > 0 (:171-176)
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            Solver::Snapshot snap = s.push();
+            std::vector<double> xp, xl;
+            const bool ok = s.solve(lambda, xp, xl);
+            if (ok) s.update(xp, xl);
+            s.compute_errors();
+            double tempChi = s.robust_chi2();
+            if (!ok) tempChi = std::numeric_limits<double>::max();
+            double sc = ok ? s.scale_of(xp, xl, lambda) : 0.0;
+            sc += 1e-3;
+            rho = (currentChi - tempChi) / sc;
+            if (trial_log && trials < log_cap) {
+                trial_log[3 * trials] = currentChi;
+                trial_log[3 * trials + 1] = tempChi;
+                trial_log[3 * trials + 2] = lambda;
+            }
+            ++trials;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                s.pop(snap);   // errors stay those of the rejected trial, as in g2o
+            }
+            qmax++;
+        } while (rho < 0 && qmax < o->max_trials);
+        if (qmax == o->max_trials || rho == 0) break;
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+        else nBad = 0;
+        if (nBad >= 3) break;
+    }
+    r->err_end = (float)s.robust_chi2();
+    r->iterations = its;
+    r->trials = trials;
+    r->lambda = lambda;
+    for (int e = 0; e < p->n_mono; ++e) {
+        const double c = s.mono_chi2(e);
+        if (r->mono_chi2) r->mono_chi2[e] = c;
+        if (r->mono_outlier) {
+            const bool close = p->pt_track_depth[p->mono_pt[e]] < 10.f;
+            const int k = p->mono_kf[e], cam = p->mono_cam[e];
+            const M3 &R = s.pose[k].Rcw[cam];
+            const V3 &X = s.pts[p->mono_pt[e]];
+            const bool depth_pos = (R(2, 0) * X[0] + R(2, 1) * X[1] + R(2, 2) * X[2] + s.pose[k].tcw[cam][2]) > 0.0;
+            r->mono_outlier[e] = ((c > 5.991f && !close) || (c > 1.5f * 5.991f && close) || !depth_pos) ? 1 : 0;
+        }
+    }
+    const bool fail = (2 * r->err < r->err_end || std::isnan(r->err) || std::isnan(r->err_end)) && !o->large;
+    r->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
+    s.write_state(*p);
+    return 0;
+}
+
+}  // extern "C"

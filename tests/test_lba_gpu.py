@@ -1,0 +1,116 @@
+"""GPU parity of the LocalInertialBA inner loop (openmavis_amd/csrc/lba.hip) against the CPU oracle
+(oracle/ba_oracle.cpp).
+
+Bar (north star: 1e-5 relative for floating point):
+  residuals            |gpu - oracle| <= 1e-9 px / 1e-9 (IMU)   (same formulas; f64 libm ulps only)
+  Jacobians            relative 1e-9
+  LM outcome           identical iteration / trial counts and status; err, err_end within 1e-5 relative
+  final state          poses / velocities / biases / points within 1e-5 relative of the oracle's step
+                       (|gpu - oracle| <= 1e-5 * max(|oracle - initial|, 1e-3))
+  outlier flags        identical except edges whose chi2 sits within 1e-6 of a threshold
+"""
+import numpy as np
+import pytest
+
+from openmavis_amd import synth_ba
+from openmavis_amd.optimizer import LocalInertialBA
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts")
+
+
+@pytest.fixture(scope="module")
+def small():
+    return synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11)
+
+
+@pytest.fixture(scope="module")
+def full():
+    return synth_ba.make_lba_problem()   # 50 keyframes (25 optimisable), 5 cameras, 20k points
+
+
+def _solver(prob):
+    return LocalInertialBA(max_kf=prob["n_kf"], max_cams=prob["n_cams"], max_pts=len(prob["pts"]),
+                           max_mono=len(prob["mono_pt"]), max_imu=max(1, len(prob["imu_kf1"])))
+
+
+def _compare_state(prob, st_g, st_o, rel=1e-5):
+    for k in STATE:
+        a, b, init = st_g[k], st_o[k], np.asarray(prob[k], np.float64).reshape(st_o[k].shape)
+        step = np.abs(b - init).max()
+        err = np.abs(a - b).max()
+        assert err <= rel * max(step, 1e-3), (k, err, step)
+
+
+def _compare_result(prob, rg, ro):
+    assert rg["iterations"] == ro["iterations"] and rg["trials"] == ro["trials"], (rg, ro)
+    assert rg["status"] == ro["status"]
+    for k in ("err", "err_end"):
+        assert abs(rg[k] - ro[k]) <= 1e-5 * abs(ro[k]), (k, rg[k], ro[k])
+    assert np.allclose(rg["mono_chi2"], ro["mono_chi2"], rtol=1e-6, atol=1e-9)
+    diff = rg["mono_outlier"] != ro["mono_outlier"]
+    if diff.any():
+        c = ro["mono_chi2"][diff]
+        near = np.minimum(np.abs(c - 5.991), np.abs(c - 1.5 * 5.991)) < 1e-6 * 5.991
+        assert near.all(), (int(diff.sum()), c[~near][:5])
+
+
+def test_residuals_and_jacobians(small, oracle):
+    ba = _solver(small).set_problem(small)
+    g = ba.evaluate()
+    o = oracle.lba_evaluate(small)
+    assert np.abs(g["mono_err"] - o["mono_err"]).max() <= 1e-9
+    assert np.abs(g["imu_err"] - o["imu_err"]).max() <= 1e-9
+    for k in ("mono_jx", "mono_jp"):
+        scale = np.abs(o[k]).max()
+        assert np.abs(g[k] - o[k]).max() <= 1e-9 * scale, k
+
+
+@pytest.mark.parametrize("large", [True, False])
+def test_optimize_small(small, oracle, large):
+    kw = dict(opt_it=4, lambda_init=1e-2) if large else dict(opt_it=10, lambda_init=1e0)
+    ro, so, _ = oracle.lba_optimize(small, max_trials=10, large=large, **kw)
+    rg, sg = _solver(small).set_problem(small).optimize(max_trials=10, large=large, **kw)
+    _compare_result(small, rg, ro)
+    _compare_state(small, sg, so)
+
+
+def test_optimize_visual_only_with_fixed_only_points(oracle):
+    """No inertial edges (kf_imu off), 6-dof pose blocks only; some points seen only by fixed keyframes."""
+    prob = synth_ba.make_lba_problem(n_kf=12, n_opt=4, n_pts=800, seed=3, n_cams=3)
+    prob = dict(prob)
+    prob["kf_imu"] = np.zeros(prob["n_kf"], np.uint8)
+    for k in ("imu_kf1", "imu_kf2"):
+        prob[k] = prob[k][:0]
+    for k in ("preint", "imu_robust", "imu_info_scale"):
+        prob[k] = prob[k][:0]
+    keep = ~((prob["mono_pt"] < 20) & (prob["mono_kf"] < prob["n_opt"]))   # points 0..19: fixed views only
+    for k in ("mono_pt", "mono_kf", "mono_cam", "mono_obs", "mono_inv_sigma2"):
+        prob[k] = prob[k][keep]
+    ro, so, _ = oracle.lba_optimize(prob, opt_it=10, lambda_init=1e0, max_trials=10, large=False)
+    rg, sg = _solver(prob).set_problem(prob).optimize(opt_it=10, lambda_init=1e0, max_trials=10, large=False)
+    _compare_result(prob, rg, ro)
+    _compare_state(prob, sg, so)
+
+
+def test_optimize_full_window(full, oracle):
+    """The bench configuration: 25 optimisable + 25 fixed keyframes, 5 cameras, 20k points, 120k edges."""
+    ro, so, _ = oracle.lba_optimize(full, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    ba = _solver(full).set_problem(full)
+    rg, sg = ba.optimize(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    _compare_result(full, rg, ro)
+    _compare_state(full, sg, so)
+    assert rg["err_end"] < 1e-3 * rg["err"]
+    t = ba.stage_ms()
+    assert t["trials"] == rg["trials"]
+
+
+def test_reoptimize_same_handle(small, oracle):
+    """set_problem twice on one handle (workspace reuse) gives the same answer."""
+    ba = _solver(small)
+    r1, s1 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
+    r2, s2 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
+    assert r1["trials"] == r2["trials"]
+    for k in STATE:
+        assert np.allclose(s1[k], s2[k], rtol=1e-9, atol=1e-12)

@@ -64,6 +64,17 @@ def test_sincosf_restatement_matches_libm():
         assert m and m.group(1) == "0" and m.group(2) == "0", out
 
 
+def test_atan2f_restatement_matches_libm():
+    """tools/check_atan2f.c carries the same constants/ops as lba.hip::glibc_atan2f (KB8 projection)."""
+    src = os.path.join(ROOT, "tools", "check_atan2f.c")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "at")
+        subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-DN=3000000L", src, "-o", exe, "-lm"])
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+        m = re.search(r"n (\d+) bad (\d+)", out)
+        assert m and int(m.group(1)) > 2000000 and m.group(2) == "0", out
+
+
 def _declared_symbols():
     hdr = open(os.path.join(ROOT, "include", "omv.h")).read()
     return sorted(set(re.findall(r"^\s*(?:omv_status|int|void)\s+(omv_\w+)\s*\(", hdr, re.M)))
