@@ -31,6 +31,8 @@ NFEAT, INI_TH, MIN_TH, NLEV, SCALE = 1200, 15, 7, 8, 1.2
 LAP = np.array([[0, 720], [0, 720], [0, 0], [0, 0], [0, 0]], np.int32)
 M_MPS, TH, NNRATIO = 5000, 6.0, 0.8
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# configs[4]: LocalInertialBA window, bLarge settings (Optimizer.cc:2742-2745, :3270-3274)
+LBA_CFG = dict(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
 
 
 def _gen_frame(f):
@@ -100,6 +102,81 @@ def cpu_baseline(n_frames=12, frames=None):
                        f"oracle C++ restatement, one thread per camera, {dt:.1f} s")
 
 
+def lba_bytes_per_trial(prob):
+    """2*E*40 (edge records read for build + chi2) + 3*P*24 (points read twice, written
+    once) + S(S+1)/2*8 (reduced system, S = 15 * N_opt)."""
+    E, P = len(prob["mono_pt"]), len(prob["pts"])
+    S = 15 * int(prob["n_opt"])
+    return 2 * E * 40 + 3 * P * 24 + S * (S + 1) // 2 * 8
+
+
+def lba_cpu_baseline(prob, runs=8):
+    """Oracle LocalInertialBA (scalar C++, single thread like g2o with OpenMP off) on the same window."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    trials = 0
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        r, _, _ = oracle.lba_optimize(prob, **LBA_CFG)
+        trials += r["trials"]
+    dt = time.perf_counter() - t0
+    return dict(value=trials / dt, unit="LM trials/s", cores=1, kind="port",
+                sample=f"{runs} LocalInertialBA optimize() calls on the config-5 window ({trials} trials), "
+                       f"oracle C++ restatement, 1 thread, {dt:.1f} s")
+
+
+def lba_leg(prob, steps, warmup, dev, world):
+    """LocalBA iters/s: one iteration = one LM trial (error eval + build + Schur + factor/solve + update
+    + chi2).  Each step is one full optimize() of the window from its uploaded state (reset is a
+    device copy outside the timed region); the state read-back and the outlier test are inside."""
+    import torch
+    from openmavis_amd.dist import job_seconds
+    from openmavis_amd.optimizer import LocalInertialBA
+    ba = LocalInertialBA(max_kf=prob["n_kf"], max_cams=prob["n_cams"], max_pts=len(prob["pts"]),
+                         max_mono=len(prob["mono_pt"]), max_imu=len(prob["imu_kf1"]))
+    t_set = time.perf_counter()
+    ba.set_problem(prob)
+    t_set = time.perf_counter() - t_set
+    for _ in range(warmup):
+        ba.reset().optimize(**LBA_CFG)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    total, trials, st_sum, res = 0.0, 0, {}, None
+    for _ in range(steps):
+        ba.reset()
+        t0 = time.perf_counter()
+        res, _ = ba.optimize(**LBA_CFG)
+        total += time.perf_counter() - t0
+        trials += res["trials"]
+        for k, v in ba.stage_ms().items():
+            st_sum[k] = st_sum.get(k, 0) + v
+    torch.cuda.synchronize(dev)
+    dt = job_seconds(total, dev)
+    trial_ms = dt / trials * 1e3
+    bpt = lba_bytes_per_trial(prob)
+    achieved = bpt / (trial_ms * 1e-3) / 1e9
+    stages = {k: round(v / trials, 4) for k, v in st_sum.items() if k != "trials"}
+    return {
+        "metric": "LocalBA iters/sec (LM trials/s)",
+        "value": round(trials * world / dt, 2),
+        "unit": "LM trials/s",
+        "ms_per_trial": round(trial_ms, 4),
+        "ms_per_optimize": round(dt / steps * 1e3, 3),
+        "trials_per_optimize": trials / steps,
+        "err": res["err"], "err_end": res["err_end"], "status": res["status"],
+        "set_problem_ms": round(t_set * 1e3, 2),
+        "stage_ms_per_trial": stages,
+        "config": {"workload": "LocalInertialBA 50 KFs (25 opt + 25 fixed) x 20k MapPoints x 5 cams, "
+                               f"{len(prob['mono_pt'])} EdgeMono + {len(prob['imu_kf1'])} inertial, bLarge",
+                   "parallelism": f"window-replicas x{world}"},
+        "dtype": "f64",
+        "roofline": {"kernel": "whole LM trial", "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": None, "algorithmic_bytes_per_trial": bpt},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +185,8 @@ def main():
     ap.add_argument("--frames", type=int, default=64, help="multi-cam frames per step per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-timing", type=int, default=1)
+    ap.add_argument("--lba-steps", type=int, default=10, help="LocalInertialBA optimize() calls timed (0: skip)")
+    ap.add_argument("--lba-warmup", type=int, default=2)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,6 +197,10 @@ def main():
     # inputs are generated before anything touches the GPU (worker pool = plain fork, no HIP yet)
     imgs = np.concatenate(_pool_map(_gen_frame, list(range(first, first + B))))   # [B*C, H, W]
     cpu_frames = [] if (args.no_cpu_baseline or world > 1) else _pool_map(_gen_frame, list(range(10_000, 10_012)))
+    lba_prob = None
+    if args.lba_steps > 0:
+        from openmavis_amd import synth_ba
+        lba_prob = synth_ba.make_lba_problem(seed=5)   # configs[4] window (same on every rank)
 
     import torch
     import torch.distributed as dist
@@ -190,6 +273,8 @@ def main():
         ms = matcher.stage_ms(reset=True)
         stages = {k: v / args.steps for k, v in {**es, **ms}.items()}
 
+    lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world) if lba_prob is not None else None
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -233,6 +318,8 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(len(cpu_frames), cpu_frames)
+        if lba is not None:
+            lba["cpu_baseline"] = lba_cpu_baseline(lba_prob)
     out = {
         "metric": "multi-cam frames/sec (ORB extract+match) + LocalBA iters/sec, 5x720x540",
         "value": round(value, 2),
@@ -253,6 +340,7 @@ def main():
         "matches_last_step": n_matches,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "local_ba": lba,
     }
     print(json.dumps(out))
     if world > 1:

@@ -241,6 +241,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
 /* Residual/Jacobian evaluation at the uploaded state for parity: mono_err [n_mono][2],
  * mono_jx [n_mono][6] (2x3), mono_jp [n_mono][12] (2x6), imu_err [n_imu][9] (any may be NULL). */
 omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err);
+/* Restore the state uploaded by the last set_problem (device-side copy; for re-runs and benchmarks). */
+omv_status omv_lba_reset(omv_lba *h);
 /* Per-stage device time of the last optimize: 0 linearise+build, 1 Schur, 2 reduced solve,
  * 3 back-substitution+update+errors; plus the number of trials. */
 omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials);

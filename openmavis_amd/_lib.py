@@ -114,6 +114,7 @@ SIGNATURES = {
     "omv_lba_optimize": (_I, [_VP, ctypes.POINTER(LbaOpts), ctypes.POINTER(LbaProblem), ctypes.POINTER(LbaResult)]),
     "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
+    "omv_lba_reset": (_I, [_VP]),
 }
 
 _lib = None

@@ -220,7 +220,9 @@ __device__ __forceinline__ void kb8_jac(const float *k, const double *X, double 
                  t8 = t4 * t4, t9 = t8 * theta;
     const double k4 = k[4], k5 = k[5], k6 = k[6], k7 = k[7];
     const double f = theta + t3 * k4 + t5 * k5 + t7 * k6 + t9 * k7;
-    const double fd = 1 + 3 * k4 * t2 + 5 * k5 * t4 + 7 * k6 * t6 + 9 * k7 * t8;
+    // `3 * mvParameters[4]` is an int x float product in the reference: rounded to float first
+    const double fd = 1 + (double)(3.0f * k[4]) * t2 + (double)(5.0f * k[5]) * t4 + (double)(7.0f * k[6]) * t6 +
+                      (double)(9.0f * k[7]) * t8;
     const double q = r2 * (r2 + z2);
     J[0] = (double)k[0] * (fd * X[2] * x2 / q + f * y2 / r3);
     J[3] = (double)k[1] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
@@ -725,17 +727,30 @@ __global__ void __launch_bounds__(64) build_imu_kernel(State s, Imu I, Red R, do
     }
 }
 
-// ---- trial: Schur complement ----------------------------------------------------------------------
-__global__ void prep_kernel(const double *H, double *S, int n, double lambda, double *coef) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < (long long)n * n) {
-        const int r = (int)(i / n), c = (int)(i % n);
-        S[i] = c <= r ? H[i] + (r == c ? lambda : 0.0) : 0.0;
-    }
-    if (i < n) coef[i] = 0;
+// ---- trial: Schur complement into the packed block layout ------------------------------------------
+// The reduced system is stored as 16x16 blocks (keyframe block = pose 6 | v 3 | bg 3 | ba 3 | pad 1,
+// padded to one f64 MFMA tile): slot(i, j) for block row i >= block column j on the symbolic LDL^T
+// pattern (fill-in included), row-major 16x16 each.  Padding rows have zero gradient and lambda on
+// the diagonal, so they solve to exactly zero and add nothing to computeScale.
+struct BlockPat {
+    int nb, n_slots;
+    const int *slot;                 // [nb*nb] slot of block (i, j), i >= j; -1 structurally zero
+    const int *slot_i, *slot_j;      // [n_slots]
+    const int *pan_start, *pan;      // step k's panel: blocks i > k with slot(i, k) >= 0
+    const int *pair_start;           // step k's trailing updates (i >= j > k, both in the panel)
+    const int4 *pair;                // (slot(i,j), slot(i,k), slot(j,k), 0)
+};
+
+__global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, double *Sp, double *coef) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) coef[q] = 0;
+    if (q >= P.n_slots * 256) return;
+    const int sl = q >> 8, e = q & 255, r = e >> 4, c = e & 15;
+    const int gr = 16 * P.slot_i[sl] + r, gc = 16 * P.slot_j[sl] + c;
+    Sp[q] = gc <= gr ? H[(size_t)gr * n + gc] + (gr == gc ? lambda : 0.0) : 0.0;
 }
 
-__global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, double lambda, double *S, double *coef) {
+__global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef) {
     __shared__ double acc[kSpan * kSpan * 36 / 2 + kSpan * 36 / 2 + kSpan * 6];   // lower block triangle + coef
     // block (a, b), a >= b, stored at ((a * (a + 1)) / 2 + b) * 36
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -781,7 +796,7 @@ __global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, double lambda
                         if (ob == oa && c > r) continue;
                         const double v = BD[3 * r] * Bb[3 * c] + BD[3 * r + 1] * Bb[3 * c + 1] + BD[3 * r + 2] * Bb[3 * c + 2];
                         if (local) unsafeAtomicAdd(blk + 6 * r + c, -v);
-                        else unsafeAtomicAdd(S + (size_t)(oa + r) * R.n + ob + c, -v);
+                        else unsafeAtomicAdd(S + (size_t)P.slot[ka * P.nb + kb] * 256 + 16 * r + c, -v);
                     }
             }
         }
@@ -795,8 +810,7 @@ __global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, double lambda
             while ((la + 1) * (la + 2) / 2 <= blk) ++la;
             const int lb = blk - la * (la + 1) / 2;
             const int ka = kf0 + la, kb = kf0 + lb;
-            const int oa = R.offP[ka], ob = R.offP[kb];
-            unsafeAtomicAdd(S + (size_t)(oa + e / 6) * R.n + ob + e % 6, acc[q]);
+            unsafeAtomicAdd(S + (size_t)P.slot[ka * P.nb + kb] * 256 + 16 * (e / 6) + e % 6, acc[q]);
         }
         for (int q = threadIdx.x; q < kSpan * 6; q += blockDim.x) {
             if (cacc[q] == 0.0) continue;
@@ -806,168 +820,231 @@ __global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, double lambda
     }
 }
 
-// ---- trial: block LDL^T of the reduced system (one workgroup) ------------------------------------
-struct BlockPat {
-    int nb;
-    const int *off, *dim;   // per block (keyframe) offset / size in the reduced system
-    const int *slot;        // [nb*nb] storage slot of block (i,j), i >= j, in the packed buffer; -1 zero
-    const int *slot_off;    // [n_slots] double offset of each slot in the packed buffer
-    int n_slots;
-    long long packed_doubles;
-};
+// ---- trial: block LDL^T of the reduced system (one workgroup, 16x16 f64 MFMA tiles) -------------
+typedef double v4d __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ double *blk(double *pk, const BlockPat &P, int i, int j) {
-    const int s = P.slot[i * P.nb + j];
-    return s < 0 ? nullptr : pk + P.slot_off[s];
+// Wave-synchronous step: LDS operations of one wavefront complete in order, so the fence only has
+// to stop the compiler (wavefront scope); the global-memory fallback needs workgroup scope.
+template <bool G>
+__device__ __forceinline__ void wave_sync() {
+    if (G) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 }
 
-__global__ void __launch_bounds__(256) ldlt_kernel(const double *S, int n, BlockPat P, const double *b, const double *coef,
-                                                   double *x, double *scratch, int use_lds, int *fail) {
+// One wavefront: D = L diag(d) L^T in place (unit L strictly below the diagonal, d on it) and, in the
+// same column passes, W = L^-1 by the same row eliminations, stored transposed in the strict upper
+// triangle (W[j][i] at D[i][j], i < j).  Lane l owns the entries e = l + 64 t, (i, j) = (e>>4, e&15), and
+// keeps them in registers; everything pass c reads is column c of the tile (pivot, L column, W row c),
+// which the owners of column c store at the end of pass c-1.  Per pass c and owned entry (i, j):
+//   lower, i > c, c < j <= i : D[i][j] -= D[i][c] D[j][c] / d_c        (trailing update)
+//   lower, j == c < i        : D[i][c] /= d_c                           (column of L)
+//   upper, i < j, j > c, i <= c : W[j][i] -= (D[j][c] / d_c) W[c][i]     (W[c][c] = 1; first touch at
+//                                 c == i starts from 0: the upper triangle holds stale values)
+template <bool G>
+__device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
+    const int q = lane >> 4, j = lane & 15;
+    double cur[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cur[t] = D[lane + 64 * t];
+    for (int c = 0; c < 16; ++c) {
+        const double dc = D[c * 17];
+        double col_i[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) col_i[t] = D[(q + 4 * t) * 16 + c];
+        const double col_j = D[j * 16 + c];
+        const double ic = 1.0 / dc;
+        if (lane == 0 && !(dc != 0.0 && isfinite(dc))) *bad = 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = q + 4 * t;
+            const double x = cur[t];
+            double r = x;
+            if (i >= j) {
+                if (i > c && j > c) r = x - col_i[t] * ic * col_j;
+                else if (j == c && i > c) r = x * ic;
+            } else if (j > c && i <= c) {
+                r = (i == c ? 0.0 : x) - col_j * ic * (i == c ? 1.0 : col_i[t]);
+            }
+            cur[t] = r;
+        }
+        if (j == c + 1) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) D[lane + 64 * t] = cur[t];
+        }
+        wave_sync<G>();
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) D[lane + 64 * t] = cur[t];
+    wave_sync<G>();
+}
+
+// One wavefront: L_ik = S_ik L_kk^-T diag(d)^-1 (f64 MFMA 16x16x4, four k-steps), in place.
+// A/B operand lane maps: A[l&15][4s + (l>>4)], B[4s + (l>>4)][l&15]; D: col l&15, row (l>>4) + 4i.
+__device__ __forceinline__ void panel16(double *A, const double *Dk, int lane) {
+    v4d acc = {0, 0, 0, 0};
+    const int rc = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int kk = 4 * s + kq;
+        const double a = A[rc * 16 + kk];
+        const double b = kk < rc ? Dk[kk * 16 + rc] : (kk == rc ? 1.0 : 0.0);   // (L^-T)[kk][col]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    const double id = 1.0 / Dk[rc * 17];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[(kq + 4 * i) * 16 + rc] = acc[i] * id;
+}
+
+// One wavefront: S_ij -= L_ik diag(d) L_jk^T.
+__device__ __forceinline__ void update16(double *Sij, const double *Lik, const double *Ljk, const double *Dk, int lane) {
+    const int rc = lane & 15, kq = lane >> 4;
+    v4d acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = Sij[(kq + 4 * i) * 16 + rc];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int kk = 4 * s + kq;
+        const double a = -Lik[rc * 16 + kk] * Dk[kk * 17];
+        const double b = Ljk[rc * 16 + kk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Sij[(kq + 4 * i) * 16 + rc] = acc[i];
+}
+
+constexpr int kLdltThreads = 512;
+constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (the static part is one int)
+
+template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
+__global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat P, const double *b,
+                                                            const double *coef, double *x, double *gscratch,
+                                                            int *fail) {
     extern __shared__ __attribute__((aligned(16))) double lsm[];
-    double *pk = use_lds ? lsm : scratch;
-    __shared__ double dk[16];
     __shared__ int bad;
-    const int tid = threadIdx.x, T = blockDim.x;
+    const int nb = P.nb, nv = 16 * nb;
+    double *pk = G ? gscratch : lsm;
+    double *y = pk + (size_t)P.n_slots * 256;
+    double *xs = y + nv;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     if (tid == 0) bad = 0;
-    // gather the nonzero lower blocks
-    for (int i = 0; i < P.nb; ++i)
-        for (int j = 0; j <= i; ++j) {
-            double *B = blk(pk, P, i, j);
-            if (!B) continue;
-            const int di = P.dim[i], dj = P.dim[j], oi = P.off[i], oj = P.off[j];
-            for (int q = tid; q < di * dj; q += T) {
-                const int r = q / dj, c = q % dj;
-                B[q] = S[(size_t)(oi + r) * n + oj + c];
-            }
-        }
+#ifdef OMV_LDLT_PROFILE
+    const long long t_0 = wall_clock64();
+    long long t_1 = 0, t_2 = 0, t_3 = 0, pf_fac = 0, pf_pan = 0, pf_upd = 0;
+#endif
+    {
+        const double2 *src = (const double2 *)Sp;
+        double2 *dst = (double2 *)pk;
+        for (int q = tid; q < P.n_slots * 128; q += blockDim.x) dst[q] = src[q];
+        for (int q = tid; q < nv; q += blockDim.x) y[q] = b[q] - coef[q];
+    }
     __syncthreads();
-    double *dvec = scratch + (use_lds ? 0 : P.packed_doubles);   // [n] pivots
-    double *y = dvec + n;                        // [n] work vector
-    for (int k = 0; k < P.nb; ++k) {
-        const int dkk = P.dim[k], ok = P.off[k];
-        double *Bkk = blk(pk, P, k, k);
-        // 1. factor the diagonal block in place (lower part): unit L_kk and pivots d
-        if (tid < 64) {
-            for (int c = 0; c < dkk; ++c) {
-                const double dc = Bkk[c * dkk + c];
-                if (tid == 0) {
-                    dk[c] = dc;
-                    if (dc == 0.0 || !isfinite(dc)) bad = 1;
-                }
-                __builtin_amdgcn_wave_barrier();
-                for (int q = tid; q < dkk * dkk; q += 64) {
-                    const int r = q / dkk, s = q % dkk;
-                    if (r > c && s > c && s <= r) Bkk[q] -= Bkk[r * dkk + c] / dc * Bkk[s * dkk + c];
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                for (int r = c + 1 + tid; r < dkk; r += 64) Bkk[r * dkk + c] /= dc;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-            }
+    for (int k = 0; k < nb; ++k) {
+        double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
+#ifdef OMV_LDLT_PROFILE
+        long long ta = wall_clock64();
+#endif
+        if (wave == 0) factor16<G>(Dk, lane, &bad);
+        __syncthreads();
+#ifdef OMV_LDLT_PROFILE
+        long long tb = wall_clock64();
+        pf_fac += tb - ta;
+#endif
+        const int p0 = P.pan_start[k], p1 = P.pan_start[k + 1];
+        for (int p = p0 + wave; p < p1; p += nw) panel16(pk + (size_t)P.slot[P.pan[p] * nb + k] * 256, Dk, lane);
+        __syncthreads();
+#ifdef OMV_LDLT_PROFILE
+        long long tc = wall_clock64();
+        pf_pan += tc - tb;
+#endif
+        const int q0 = P.pair_start[k], q1 = P.pair_start[k + 1];
+        for (int q = q0 + wave; q < q1; q += nw) {
+            const int4 pr = P.pair[q];
+            update16(pk + (size_t)pr.x * 256, pk + (size_t)pr.y * 256, pk + (size_t)pr.z * 256, Dk, lane);
         }
         __syncthreads();
-        if (tid < dkk) dvec[ok + tid] = dk[tid];
-        // 2. panel: Y_i = S_ik L_kk^-T (rows solve forward), L_ik = Y_i D^-1; Y kept for the update
-        for (int i = k + 1; i < P.nb; ++i) {
-            double *Bik = blk(pk, P, i, k);
-            if (!Bik) continue;
-            const int di = P.dim[i];
-            for (int r = tid; r < di; r += T) {
-                double *row = Bik + r * dkk;
-                for (int c = 0; c < dkk; ++c) {
-                    double v = row[c];
-                    for (int m = 0; m < c; ++m) v -= Bkk[c * dkk + m] * row[m];   // row holds y_m for m < c
-                    row[c] = v;
-                }
-            }
-        }
-        __syncthreads();
-        // 3. trailing update S_ij -= Y_i D^-1 Y_j^T for i >= j > k (lower part)
-        for (int i = k + 1; i < P.nb; ++i) {
-            double *Bik = blk(pk, P, i, k);
-            if (!Bik) continue;
-            for (int j = k + 1; j <= i; ++j) {
-                double *Bjk = blk(pk, P, j, k);
-                if (!Bjk) continue;
-                double *Bij = blk(pk, P, i, j);
-                const int di = P.dim[i], dj = P.dim[j];
-                for (int q = tid; q < di * dj; q += T) {
-                    const int r = q / dj, c = q % dj;
-                    if (i == j && c > r) continue;
-                    double v = 0;
-                    for (int m = 0; m < dkk; ++m) v += Bik[r * dkk + m] * Bjk[c * dkk + m] / dk[m];
-                    Bij[q] -= v;
-                }
-            }
-        }
-        __syncthreads();
-        // 4. scale the panel to L_ik = Y_i D^-1
-        for (int i = k + 1; i < P.nb; ++i) {
-            double *Bik = blk(pk, P, i, k);
-            if (!Bik) continue;
-            const int di = P.dim[i];
-            for (int q = tid; q < di * dkk; q += T) Bik[q] /= dk[q % dkk];
-        }
-        __syncthreads();
+#ifdef OMV_LDLT_PROFILE
+        pf_upd += wall_clock64() - tc;
+#endif
     }
-    if (bad) {
-        if (tid == 0) *fail = 1;
-        return;
+#ifdef OMV_LDLT_PROFILE
+    t_1 = wall_clock64();
+#endif
+    if (wave == 0) {
+        // forward: y_k <- L_kk^-1 y_k, then y_i -= L_ik y_k for the panel (four blocks per pass)
+        for (int k = 0; k < nb; ++k) {
+            const double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
+            const int r16 = lane & 15;
+            double v = y[16 * k + r16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const double w = Dk[m * 16 + r16];
+                v += (m < r16 ? w : 0.0) * y[16 * k + m];
+            }
+            wave_sync<G>();
+            if (lane < 16) y[16 * k + lane] = v;
+            wave_sync<G>();
+            for (int p = P.pan_start[k]; p < P.pan_start[k + 1]; p += 4) {
+                const int pp = p + (lane >> 4);
+                if (pp < P.pan_start[k + 1]) {
+                    const int i = P.pan[pp];
+                    const double *Lik = pk + (size_t)P.slot[i * nb + k] * 256 + r16 * 16;
+                    double acc = 0;
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) acc += Lik[m] * y[16 * k + m];
+                    y[16 * i + r16] -= acc;
+                }
+            }
+            wave_sync<G>();
+        }
+#ifdef OMV_LDLT_PROFILE
+        t_2 = wall_clock64();
+#endif
+        for (int q = lane; q < nv; q += 64) y[q] /= pk[(size_t)P.slot[(q >> 4) * nb + (q >> 4)] * 256 + (q & 15) * 17];
+        wave_sync<G>();
+        // backward: r_k = z_k - sum_i L_ik^T x_i, x_k = L_kk^-T r_k
+        for (int k = nb - 1; k >= 0; --k) {
+            const double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
+            const int c16 = lane & 15;
+            {
+                // lanes 16p + c: panel block p's contribution to entry c, summed over the four groups
+                double v = 0;
+                for (int p = P.pan_start[k] + (lane >> 4); p < P.pan_start[k + 1]; p += 4) {
+                    const int i = P.pan[p];
+                    const double *Lik = pk + (size_t)P.slot[i * nb + k] * 256 + c16;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v += Lik[r * 16] * xs[16 * i + r];
+                }
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                if (lane < 16) y[16 * k + lane] -= v;
+            }
+            wave_sync<G>();
+            {
+                double v = y[16 * k + c16];
+                const double *row = Dk + c16 * 16;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) v += (m > c16 ? row[m] : 0.0) * y[16 * k + m];
+                if (lane < 16) xs[16 * k + lane] = v;
+            }
+            wave_sync<G>();
+        }
     }
-    // forward: L y = b - coef
-    for (int q = tid; q < n; q += T) y[q] = b[q] - coef[q];
+#ifdef OMV_LDLT_PROFILE
+    t_3 = wall_clock64();
+    if (tid == 0)
+        printf("ldlt ticks(100MHz): factor %lld (diag %lld panel %lld update %lld) fwd %lld bwd %lld slots %d\n",
+               t_1 - t_0, pf_fac, pf_pan, pf_upd, t_2 - t_1, t_3 - t_2, P.n_slots);
+#endif
     __syncthreads();
-    for (int k = 0; k < P.nb; ++k) {
-        const int dkk = P.dim[k], ok = P.off[k];
-        for (int r = tid; r < dkk; r += T) {
-            double v = y[ok + r];
-            for (int j = 0; j < k; ++j) {
-                const double *Bkj = blk(pk, P, k, j);
-                if (!Bkj) continue;
-                const int dj = P.dim[j], oj = P.off[j];
-                for (int c = 0; c < dj; ++c) v -= Bkj[r * dj + c] * y[oj + c];
-            }
-            y[ok + r] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const double *Bkk = blk(pk, P, k, k);
-            for (int r = 0; r < dkk; ++r) {
-                double v = y[ok + r];
-                for (int c = 0; c < r; ++c) v -= Bkk[r * dkk + c] * y[ok + c];
-                y[ok + r] = v;
-            }
-        }
-        __syncthreads();
-    }
-    for (int q = tid; q < n; q += T) y[q] /= dvec[q];
-    __syncthreads();
-    // backward: L^T x = z
-    for (int k = P.nb - 1; k >= 0; --k) {
-        const int dkk = P.dim[k], ok = P.off[k];
-        for (int c = tid; c < dkk; c += T) {
-            double v = y[ok + c];
-            for (int i = k + 1; i < P.nb; ++i) {
-                const double *Bik = blk(pk, P, i, k);
-                if (!Bik) continue;
-                const int di = P.dim[i], oi = P.off[i];
-                for (int r = 0; r < di; ++r) v -= Bik[r * dkk + c] * x[oi + r];
-            }
-            y[ok + c] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const double *Bkk = blk(pk, P, k, k);
-            for (int c = dkk - 1; c >= 0; --c) {
-                double v = y[ok + c];
-                for (int r = c + 1; r < dkk; ++r) v -= Bkk[r * dkk + c] * x[ok + r];
-                x[ok + c] = v;
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0) *fail = 0;
+    for (int q = tid; q < nv; q += blockDim.x) x[q] = xs[q];
+    if (tid == 0) *fail = bad;
 }
 
 // ---- trial: back-substitution + updates + scale ----------------------------------------------------
@@ -1155,7 +1232,7 @@ struct omv_lba {
     // problem
     Rig rig{};
     int n_kf = 0, n_opt = 0, n_pts = 0, n_mono = 0, n_imu = 0, n_red = 0, n_slots = 0;
-    State st[2]{};
+    State st[3]{};   // current / trial (push-pop double buffer) / the uploaded initial state
     int cur = 0;
     Edges E{};
     Land L{};
@@ -1197,8 +1274,8 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     for (auto &e : h->ev) HIP_OK(hipEventCreate(&e));
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
-    h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    150 * 1024) == hipSuccess;
+    h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kLdltLds) == hipSuccess;
     (void)hipGetLastError();
     *out = h;
     return OMV_OK;
@@ -1230,12 +1307,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         for (int q = 0; q < 3; ++q) rig.tcb[c][q] = p->tcb[3 * c + q], rig.tbc[c][q] = p->tbc[3 * c + q];
     }
     // reduced-system layout: per optimisable keyframe pose (6) [+ v bg ba (9)]
-    std::vector<int> offP(K, -1), offV(K, -1), offG(K, -1), offA(K, -1), bdim;
-    int nred = 0;
+    // keyframe block k occupies reduced indices 16k .. 16k+15: pose 0-5, v 6-8, bg 9-11, ba 12-14, pad 15
+    std::vector<int> offP(K, -1), offV(K, -1), offG(K, -1), offA(K, -1);
+    const int nred = 16 * p->n_opt;
     for (int k = 0; k < p->n_opt; ++k) {
-        offP[k] = nred, nred += 6;
-        if (p->kf_imu[k]) offV[k] = nred, offG[k] = nred + 3, offA[k] = nred + 6, nred += 9;
-        bdim.push_back(p->kf_imu[k] ? 15 : 6);
+        offP[k] = 16 * k;
+        if (p->kf_imu[k]) offV[k] = 16 * k + 6, offG[k] = 16 * k + 9, offA[k] = 16 * k + 12;
     }
     h->n_red = nred;
     // landmark order: by the first optimisable keyframe observing them (workgroup keyframe spans stay small)
@@ -1308,17 +1385,32 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             if (pat[i * nb + k])
                 for (int j = k + 1; j <= i; ++j)
                     if (pat[j * nb + k]) pat[i * nb + j] = 1;
-    std::vector<int> slot((size_t)nb * nb, -1), slot_off;
-    long long packed = 0;
-    for (int i = 0; i < nb; ++i)
-        for (int j = 0; j <= i; ++j)
+    std::vector<int> slot((size_t)nb * nb, -1), slot_i, slot_j;
+    for (int j = 0; j < nb; ++j)   // column-major slot order: a step's panel blocks sit together
+        for (int i = j; i < nb; ++i)
             if (pat[i * nb + j]) {
-                slot[i * nb + j] = (int)slot_off.size();
-                slot_off.push_back((int)packed);
-                packed += (long long)bdim[i] * bdim[j];
+                slot[i * nb + j] = (int)slot_i.size();
+                slot_i.push_back(i), slot_j.push_back(j);
             }
-    h->use_lds = h->lds_ok && (size_t)packed * sizeof(double) <= 150 * 1024 ? 1 : 0;
-    h->ldlt_lds = h->use_lds ? (size_t)packed * sizeof(double) : 0;
+    const int n_slots = (int)slot_i.size();
+    std::vector<int> pan_start(nb + 1, 0), pan, pair_start(nb + 1, 0);
+    std::vector<int4> pair;
+    for (int k = 0; k < nb; ++k) {
+        pan_start[k] = (int)pan.size();
+        pair_start[k] = (int)pair.size();
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[i * nb + k]) pan.push_back(i);
+        for (int a = pan_start[k]; a < (int)pan.size(); ++a)
+            for (int c = pan_start[k]; c <= a; ++c) {
+                const int i = pan[a], j = pan[c];
+                pair.push_back(make_int4(slot[i * nb + j], slot[i * nb + k], slot[j * nb + k], 0));
+            }
+    }
+    pan_start[nb] = (int)pan.size();
+    pair_start[nb] = (int)pair.size();
+    const size_t ldlt_bytes = ((size_t)n_slots * 256 + 2 * (size_t)nred) * sizeof(double);
+    h->use_lds = h->lds_ok && ldlt_bytes <= kLdltLds ? 1 : 0;
+    h->ldlt_lds = h->use_lds ? ldlt_bytes : 0;
     // inertial information (EdgeInertial ctor :486-495) and random-walk information
     std::vector<double> info9((size_t)NI * 81), infoG((size_t)NI * 9), infoA((size_t)NI * 9);
     for (int i = 0; i < NI; ++i) {
@@ -1355,7 +1447,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     auto up = [&](auto *dst, const auto *src, size_t n) {
         return hipMemcpy(dst, src, n * sizeof(*src), hipMemcpyHostToDevice);
     };
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 3; ++b) {
         State &s = h->st[b];
         s.Rwb = dalloc<double>(ow, 9 * K), s.twb = dalloc<double>(ow, 3 * K);
         s.Rcw = dalloc<double>(ow, 9 * K * C), s.tcw = dalloc<double>(ow, 3 * K * C);
@@ -1425,17 +1517,19 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     }
     h->I = Imu{NI, d_k1, d_k2, d_pre, d_i9, d_iG, d_iA, d_rob, h->d_offP, h->d_offV, h->d_offG, h->d_offA};
     // block pattern
-    int *d_boff = dalloc<int>(ow, nb), *d_bdim = dalloc<int>(ow, nb), *d_slot = dalloc<int>(ow, (size_t)nb * nb),
-        *d_slot_off = dalloc<int>(ow, slot_off.size());
-    std::vector<int> boff(nb);
-    for (int k = 0; k < nb; ++k) boff[k] = offP[k];
-    if (nb > 0) {
-        HIP_OK(up(d_boff, boff.data(), nb));
-        HIP_OK(up(d_bdim, bdim.data(), nb));
-        HIP_OK(up(d_slot, slot.data(), (size_t)nb * nb));
-        HIP_OK(up(d_slot_off, slot_off.data(), slot_off.size()));
-    }
-    h->BP = BlockPat{nb, d_boff, d_bdim, d_slot, d_slot_off, (int)slot_off.size(), packed};
+    int *d_slot = dalloc<int>(ow, (size_t)nb * nb), *d_slot_i = dalloc<int>(ow, n_slots),
+        *d_slot_j = dalloc<int>(ow, n_slots), *d_pan_start = dalloc<int>(ow, nb + 1), *d_pan = dalloc<int>(ow, pan.size()),
+        *d_pair_start = dalloc<int>(ow, nb + 1);
+    int4 *d_pair = dalloc<int4>(ow, pair.size());
+    if (!d_pair) return OMV_ERR_HIP;
+    HIP_OK(up(d_slot, slot.data(), (size_t)nb * nb));
+    HIP_OK(up(d_slot_i, slot_i.data(), n_slots));
+    HIP_OK(up(d_slot_j, slot_j.data(), n_slots));
+    HIP_OK(up(d_pan_start, pan_start.data(), nb + 1));
+    if (!pan.empty()) HIP_OK(up(d_pan, pan.data(), pan.size()));
+    HIP_OK(up(d_pair_start, pair_start.data(), nb + 1));
+    if (!pair.empty()) HIP_OK(up(d_pair, pair.data(), pair.size()));
+    h->BP = BlockPat{nb, n_slots, d_slot, d_slot_i, d_slot_j, d_pan_start, d_pan, d_pair_start, d_pair};
     // work buffers
     h->n_wg_edge = (E + 255) / 256;
     h->d_err = dalloc<double>(ow, 2 * (size_t)E);
@@ -1445,10 +1539,10 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_imu_partial = dalloc<double>(ow, 1);
     h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
     h->d_out = dalloc<double>(ow, 4);
-    h->d_S = dalloc<double>(ow, (size_t)nred * nred);
+    h->d_S = dalloc<double>(ow, (size_t)n_slots * 256);
     h->d_coef = dalloc<double>(ow, nred);
     h->d_x = dalloc<double>(ow, nred);
-    h->d_scratch = dalloc<double>(ow, (size_t)(h->use_lds ? 0 : packed) + 2 * nred + 8);
+    h->d_scratch = dalloc<double>(ow, h->use_lds ? 8 : (size_t)n_slots * 256 + 2 * (size_t)nred + 8);
     h->d_fail = dalloc<int>(ow, 1);
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
@@ -1562,12 +1656,16 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         h->stage_ms[0] += ms;
         do {
             HIP_OK(hipEventRecord(h->ev[2], st));
-            const long long nn = (long long)nred * nred;
-            prep_kernel<<<(int)((nn + 255) / 256), 256, 0, st>>>(h->R.H, h->d_S, nred, lambda, h->d_coef);
-            if (h->n_pts > 0) schur_kernel<<<gl, 256, 0, st>>>(h->L, h->R, lambda, h->d_S, h->d_coef);
+            const int npk = std::max(h->BP.n_slots * 256, nred);
+            pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, lambda, h->d_S, h->d_coef);
+            if (h->n_pts > 0) schur_kernel<<<gl, 256, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef);
             HIP_OK(hipEventRecord(h->ev[3], st));
-            ldlt_kernel<<<1, 256, h->ldlt_lds, st>>>(h->d_S, nred, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
-                                                     h->use_lds, h->d_fail);
+            if (h->use_lds)
+                ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x,
+                                                                         h->d_scratch, h->d_fail);
+            else
+                ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
+                                                              h->d_fail);
             HIP_OK(hipEventRecord(h->ev[4], st));
             int fail = 0;
             HIP_OK(hipMemcpyAsync(&fail, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1650,6 +1748,29 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     }
     const bool fail = (2 * res->err < res->err_end || std::isnan(res->err) || std::isnan(res->err_end)) && !o->large;
     res->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
+    return OMV_OK;
+}
+
+omv_status omv_lba_reset(omv_lba *h) {
+    if (!h || !h->st[2].pts) return OMV_ERR_ARG;
+    const size_t K = h->n_kf, C = h->rig.n_cams, P = h->n_pts;
+    for (int b = 0; b < 2; ++b) {
+        const State &s = h->st[2];
+        State &d = h->st[b];
+        auto cp = [&](double *dst, const double *src, size_t n) {
+            return hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream);
+        };
+        HIP_OK(cp(d.Rwb, s.Rwb, 9 * K));
+        HIP_OK(cp(d.twb, s.twb, 3 * K));
+        HIP_OK(cp(d.Rcw, s.Rcw, 9 * K * C));
+        HIP_OK(cp(d.tcw, s.tcw, 3 * K * C));
+        HIP_OK(cp(d.vel, s.vel, 3 * K));
+        HIP_OK(cp(d.bg, s.bg, 3 * K));
+        HIP_OK(cp(d.ba, s.ba, 3 * K));
+        HIP_OK(cp(d.pts, s.pts, 3 * P));
+    }
+    h->cur = 0;
+    HIP_OK(hipStreamSynchronize(h->stream));
     return OMV_OK;
 }
 

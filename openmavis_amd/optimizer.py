@@ -67,6 +67,11 @@ class LocalInertialBA:
                    lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl)
         return res, read_state(self._keep)
 
+    def reset(self):
+        """Restore the state uploaded by set_problem (device copy)."""
+        _lib.check(self._lib.omv_lba_reset(self._h), "omv_lba_reset")
+        return self
+
     def evaluate(self):
         """Residuals and visual Jacobians at the uploaded state (caller's edge order)."""
         E, I = self._s.n_mono, self._s.n_imu
