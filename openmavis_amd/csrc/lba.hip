@@ -40,7 +40,8 @@
 namespace {
 
 constexpr int kMaxCams = 8;
-constexpr int kSpan = 8;          // keyframes a workgroup may touch for LDS pre-reduction
+constexpr int kSpan = 8;
+constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / back-substitution)          // keyframes a workgroup may touch for LDS pre-reduction
 constexpr int kPF = OMV_PREINT_FLOATS;
 
 #define HIP_OK(x)                                                                    \
@@ -183,14 +184,15 @@ __host__ __device__ inline void polar3(T *r) {
         c[7] = r[2] * r[3] - r[0] * r[5];
         c[8] = r[0] * r[4] - r[1] * r[3];
         const T det = r[0] * c[0] + r[1] * c[1] + r[2] * c[2];
+        const T id = T(1) / det;
         T diff = 0;
         for (int k = 0; k < 9; ++k) {
-            const T nv = (r[k] + c[k] / det) * T(0.5);
+            const T nv = (r[k] + c[k] * id) * T(0.5);
             const T dd = nv > r[k] ? nv - r[k] : r[k] - nv;
             diff = dd > diff ? dd : diff;
             r[k] = nv;
         }
-        if (diff == T(0)) break;
+        if (diff <= (sizeof(T) == 4 ? T(2.5e-7) : T(5e-16))) break;   // within ~2 ulp of a fixed point
     }
 }
 
@@ -433,7 +435,8 @@ __global__ void imu_err_kernel(State s, Imu I, double delta, double dsqr, double
 
 // Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
 __global__ void __launch_bounds__(256) finish_kernel(const double *mono_partial, int n_mono_blocks, const double *imu_partial,
-                                                     const double *scale_partial, int n_scale, double *out) {
+                                                     const double *scale_partial, int n_scale, const int *fail,
+                                                     double *out) {
     __shared__ double sh[8];
     double v = 0;
     for (int i = threadIdx.x; i < n_mono_blocks; i += blockDim.x) v += mono_partial[i];
@@ -445,6 +448,7 @@ __global__ void __launch_bounds__(256) finish_kernel(const double *mono_partial,
     if (threadIdx.x == 0) {
         out[0] = imu_partial[0] + t;   // activeRobustChi2
         out[1] = st;                   // computeScale
+        out[2] = fail ? (double)*fail : 0.0;   // the linear solve of this trial failed
     }
 }
 
@@ -468,7 +472,7 @@ struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lowe
 };
 
 // LDS accumulators of a workgroup: kSpan keyframes x (36 + 6)
-__global__ void __launch_bounds__(256) build_land_kernel(Rig rig, State s, Edges E, Land L, Red R, double delta,
+__global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, Edges E, Land L, Red R, double delta,
                                                          double dsqr, const double *err, const double *chi2) {
     __shared__ double acc[kSpan * 42];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -750,7 +754,7 @@ __global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, d
     Sp[q] = gc <= gr ? H[(size_t)gr * n + gc] + (gr == gc ? lambda : 0.0) : 0.0;
 }
 
-__global__ void __launch_bounds__(256) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef) {
+__global__ void __launch_bounds__(kLandWG) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef) {
     __shared__ double acc[kSpan * kSpan * 36 / 2 + kSpan * 36 / 2 + kSpan * 6];   // lower block triangle + coef
     // block (a, b), a >= b, stored at ((a * (a + 1)) / 2 + b) * 36
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -838,43 +842,60 @@ __device__ __forceinline__ void wave_sync() {
     }
 }
 
-// One wavefront: D = L diag(d) L^T in place (unit L strictly below the diagonal, d on it) and, in the
-// same column passes, W = L^-1 by the same row eliminations, stored transposed in the strict upper
-// triangle (W[j][i] at D[i][j], i < j).  Lane l owns the entries e = l + 64 t, (i, j) = (e>>4, e&15), and
-// keeps them in registers; everything pass c reads is column c of the tile (pivot, L column, W row c),
-// which the owners of column c store at the end of pass c-1.  Per pass c and owned entry (i, j):
-//   lower, i > c, c < j <= i : D[i][j] -= D[i][c] D[j][c] / d_c        (trailing update)
-//   lower, j == c < i        : D[i][c] /= d_c                           (column of L)
-//   upper, i < j, j > c, i <= c : W[j][i] -= (D[j][c] / d_c) W[c][i]     (W[c][c] = 1; first touch at
-//                                 c == i starts from 0: the upper triangle holds stale values)
+// One wavefront: D = L diag(d) L^T in place (unit L strictly below the diagonal, d on it) and W = L^-1
+// by the same eliminations, stored transposed in the strict upper triangle (W[j][i] at D[i][j], i < j).
+// Eight passes, each eliminating a 2x2 pivot block (c0, c0+1): with P = [p00 .; p10 p11],
+// l = p10/p00, d1 = p11 - l p10, and for a row x its pivot-column values b_x0, b_x1, u_x = b_x1 - l b_x0:
+//   lower trailing (i, j > c0+1) : A_ij -= b_i0 b_j0 / p00 + u_i u_j / d1
+//   lower pivot columns           : L_i,c0 = b_i0 / p00, L_i,c0+1 = u_i / d1, L_c0+1,c0 = l, d = (p00, d1)
+//   upper, column j >= c0+1        : W[j][i] <- W[j][i] - L_B[j] . (new W rows c0, c0+1)[i]
+//                                     (W[c0+1][.] = W[c0+1][.] - l W[c0][.]; entries first touched here,
+//                                     i in {c0, c0+1}, start from 0 -- the upper triangle holds stale values)
+// Lane l owns entries e = l + 64t, (i, j) = (e>>4, e&15), kept in registers; a pass reads only the tile's
+// columns c0, c0+1, which their owners store at the end of the previous pass.
 template <bool G>
 __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
     double cur[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) cur[t] = D[lane + 64 * t];
-    for (int c = 0; c < 16; ++c) {
-        const double dc = D[c * 17];
-        double col_i[4];
+    for (int c0 = 0; c0 < 16; c0 += 2) {
+        const double p00 = D[c0 * 17], p10 = D[(c0 + 1) * 16 + c0], p11 = D[(c0 + 1) * 17];
+        double bi0[4], bi1[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) col_i[t] = D[(q + 4 * t) * 16 + c];
-        const double col_j = D[j * 16 + c];
-        const double ic = 1.0 / dc;
-        if (lane == 0 && !(dc != 0.0 && isfinite(dc))) *bad = 1;
+        for (int t = 0; t < 4; ++t) {
+            bi0[t] = D[(q + 4 * t) * 16 + c0];
+            bi1[t] = D[(q + 4 * t) * 16 + c0 + 1];
+        }
+        const double bj0 = D[j * 16 + c0], bj1 = D[j * 16 + c0 + 1];
+        const double i0 = 1.0 / p00;
+        const double l = p10 * i0;
+        const double d1 = p11 - l * p10;
+        const double i1 = 1.0 / d1;
+        if (lane == 0 && !(p00 != 0.0 && isfinite(p00) && d1 != 0.0 && isfinite(d1))) *bad = 1;
+        const double uj = bj1 - l * bj0;
+        const double lb0 = bj0 * i0, lb1 = uj * i1;   // L_B row j (used when j is below the pivot)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = q + 4 * t;
             const double x = cur[t];
+            const double ui = bi1[t] - l * bi0[t];
             double r = x;
             if (i >= j) {
-                if (i > c && j > c) r = x - col_i[t] * ic * col_j;
-                else if (j == c && i > c) r = x * ic;
-            } else if (j > c && i <= c) {
-                r = (i == c ? 0.0 : x) - col_j * ic * (i == c ? 1.0 : col_i[t]);
+                if (j > c0 + 1) r = x - bi0[t] * bj0 * i0 - ui * uj * i1;
+                else if (j == c0 && i > c0 + 1) r = bi0[t] * i0;
+                else if (j == c0 + 1 && i > c0 + 1) r = ui * i1;
+                else if (i == c0 + 1 && j == c0) r = l;
+                else if (i == c0 + 1 && j == c0 + 1) r = d1;
+            } else if (j > c0 && i <= c0 + 1 && !(i == c0 + 1 && j == c0 + 1)) {
+                const double w0 = i == c0 ? 1.0 : (i == c0 + 1 ? 0.0 : bi0[t]);
+                const double w1 = i == c0 ? -l : (i == c0 + 1 ? 1.0 : ui);
+                const double base = i < c0 ? x : 0.0;
+                r = j == c0 + 1 ? base - l * w0 : base - (lb0 * w0 + lb1 * w1);
             }
             cur[t] = r;
         }
-        if (j == c + 1) {
+        if (j == c0 + 2 || j == c0 + 3) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) D[lane + 64 * t] = cur[t];
         }
@@ -1048,7 +1069,7 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 }
 
 // ---- trial: back-substitution + updates + scale ----------------------------------------------------
-__global__ void __launch_bounds__(256) backsub_kernel(Land L, Red R, double lambda, const double *xp, State a, State bst,
+__global__ void __launch_bounds__(kLandWG) backsub_kernel(Land L, Red R, double lambda, const double *xp, State a, State bst,
                                                       double *scale_partial) {
     __shared__ double sh[8];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1252,9 +1273,12 @@ struct omv_lba {
     std::vector<int> perm_edge;   // device edge index -> caller index
     double delta_mono, dsqr_mono, delta_imu, dsqr_imu;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;   // inertial edges run beside the visual kernels (fork / join events)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev[8];
     double stage_ms[4] = {0, 0, 0, 0};
     int last_trials = 0;
+    size_t state_doubles() const { return (size_t)n_kf * (24 + 12 * rig.n_cams) + 3 * (size_t)n_pts; }
 };
 
 static void free_problem(omv_lba *h) {
@@ -1272,6 +1296,9 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     omv_lba *h = new omv_lba();
     h->max_kf = max_kf, h->max_cams = max_cams, h->max_pts = max_pts, h->max_mono = max_mono, h->max_imu = max_imu;
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     for (auto &e : h->ev) HIP_OK(hipEventCreate(&e));
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
     h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1286,6 +1313,9 @@ omv_status omv_lba_destroy(omv_lba *h) {
     free_problem(h);
     for (auto &e : h->ev) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->side) (void)hipStreamDestroy(h->side);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     delete h;
     return OMV_OK;
 }
@@ -1352,12 +1382,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     pt_edge[P] = (int)e_pt.size();
     pt_slot[P] = (int)slot_kf.size();
     h->n_slots = (int)slot_kf.size();
-    // workgroup keyframe spans (256 landmarks per workgroup)
-    h->n_wg_land = (P + 255) / 256;
+    // workgroup keyframe spans (kLandWG landmarks per workgroup)
+    h->n_wg_land = (P + kLandWG - 1) / kLandWG;
     std::vector<int> wg_kf0(std::max(1, h->n_wg_land), -1);
     for (int g = 0; g < h->n_wg_land; ++g) {
         int lo = 1 << 30, hi = -1;
-        for (int q = g * 256; q < std::min(P, (g + 1) * 256); ++q)
+        for (int q = g * kLandWG; q < std::min(P, (g + 1) * kLandWG); ++q)
             for (int s = pt_slot[q]; s < pt_slot[q + 1]; ++s)
                 if (slot_kf[s] < p->n_opt) lo = std::min(lo, slot_kf[s]), hi = std::max(hi, slot_kf[s]);
         wg_kf0[g] = (hi >= 0 && hi - lo < kSpan) ? lo : (hi < 0 ? 0 : -1);
@@ -1448,12 +1478,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         return hipMemcpy(dst, src, n * sizeof(*src), hipMemcpyHostToDevice);
     };
     for (int b = 0; b < 3; ++b) {
+        // one contiguous block per state: Rwb | twb | Rcw | tcw | vel | bg | ba | pts (one copy to read back)
         State &s = h->st[b];
-        s.Rwb = dalloc<double>(ow, 9 * K), s.twb = dalloc<double>(ow, 3 * K);
-        s.Rcw = dalloc<double>(ow, 9 * K * C), s.tcw = dalloc<double>(ow, 3 * K * C);
-        s.vel = dalloc<double>(ow, 3 * K), s.bg = dalloc<double>(ow, 3 * K), s.ba = dalloc<double>(ow, 3 * K);
-        s.pts = dalloc<double>(ow, 3 * (size_t)P);
-        if (!s.pts) return OMV_ERR_HIP;
+        double *blk = dalloc<double>(ow, h->state_doubles());
+        if (!blk) return OMV_ERR_HIP;
+        s.Rwb = blk, s.twb = s.Rwb + 9 * K, s.Rcw = s.twb + 3 * K, s.tcw = s.Rcw + 9 * K * C;
+        s.vel = s.tcw + 3 * K * C, s.bg = s.vel + 3 * K, s.ba = s.bg + 3 * K, s.pts = s.ba + 3 * K;
         HIP_OK(up(s.Rwb, p->Rwb, 9 * K));
         HIP_OK(up(s.twb, p->twb, 3 * K));
         HIP_OK(up(s.Rcw, p->Rcw, 9 * K * C));
@@ -1552,19 +1582,37 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 }  // extern "C"
 
 // ---- the LM driver ---------------------------------------------------------------------------------
+// Fork the side stream off the main one / join it back (the inertial kernels are one workgroup each
+// and latency-bound, so they overlap the visual kernels instead of following them).
+static omv_status lba_fork(omv_lba *h) {
+    HIP_OK(hipEventRecord(h->ev_fork, h->stream));
+    HIP_OK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    return OMV_OK;
+}
+static omv_status lba_join(omv_lba *h) {
+    HIP_OK(hipEventRecord(h->ev_join, h->side));
+    HIP_OK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    return OMV_OK;
+}
+
 static omv_status lba_errors(omv_lba *h, const State &s) {
     hipStream_t st = h->stream;
+    omv_status r;
+    if (h->n_imu > 0) {
+        if ((r = lba_fork(h)) != OMV_OK) return r;
+        imu_err_kernel<<<1, 64, 0, h->side>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
+    }
     if (h->n_mono > 0)
         mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->d_err, h->d_chi2,
                                                        h->d_partial);
-    if (h->n_imu > 0) imu_err_kernel<<<1, 64, 0, st>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
+    if (h->n_imu > 0 && (r = lba_join(h)) != OMV_OK) return r;
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
-static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[2]) {
+static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[3], bool with_fail) {
     finish_kernel<<<1, 256, 0, h->stream>>>(h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
-                                           h->d_scale_partial, n_scale, h->d_out);
-    HIP_OK(hipMemcpyAsync(out, h->d_out, 2 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+                                           h->d_scale_partial, n_scale, with_fail ? h->d_fail : nullptr, h->d_out);
+    HIP_OK(hipMemcpyAsync(out, h->d_out, 3 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
     return OMV_OK;
 }
@@ -1609,12 +1657,12 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     if (!h || !o || !p || !res) return OMV_ERR_ARG;
     hipStream_t st = h->stream;
     const int nred = h->n_red;
-    double sc[2];
+    double sc[3];
     omv_status rs;
     for (double &m : h->stage_ms) m = 0;
     // err = activeRobustChi2 at the initial state (Optimizer.cc:3273-3274)
     if ((rs = lba_errors(h, h->st[h->cur])) != OMV_OK) return rs;
-    if ((rs = lba_read_scalars(h, 0, sc)) != OMV_OK) return rs;
+    if ((rs = lba_read_scalars(h, 0, sc, false)) != OMV_OK) return rs;
     res->err = (float)sc[0];
     double errors_chi = sc[0];
     bool errors_of_current = true;
@@ -1627,7 +1675,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         State &B = h->st[1 - h->cur];
         if (!errors_of_current) {
             if ((rs = lba_errors(h, A)) != OMV_OK) return rs;
-            if ((rs = lba_read_scalars(h, 0, sc)) != OMV_OK) return rs;
+            if ((rs = lba_read_scalars(h, 0, sc, false)) != OMV_OK) return rs;
             errors_chi = sc[0];
             errors_of_current = true;
         }
@@ -1637,10 +1685,15 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         HIP_OK(hipEventRecord(h->ev[0], st));
         HIP_OK(hipMemsetAsync(h->R.H, 0, sizeof(double) * (size_t)nred * nred, st));
         HIP_OK(hipMemsetAsync(h->R.b, 0, sizeof(double) * nred, st));
+        if (h->n_imu > 0) {
+            if ((rs = lba_fork(h)) != OMV_OK) return rs;
+            build_imu_kernel<<<h->n_imu, 64, 0, h->side>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
+        }
         if (h->n_pts > 0)
-            build_land_kernel<<<gl, 256, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono, h->d_err,
+            build_land_kernel<<<gl, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono, h->d_err,
                                                   h->d_chi2);
-        if (h->n_imu > 0) build_imu_kernel<<<h->n_imu, 64, 0, st>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
+        if (h->n_imu > 0 && (rs = lba_join(h)) != OMV_OK) return rs;
+        if (h->n_imu > 0) HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -1658,7 +1711,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             HIP_OK(hipEventRecord(h->ev[2], st));
             const int npk = std::max(h->BP.n_slots * 256, nred);
             pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, lambda, h->d_S, h->d_coef);
-            if (h->n_pts > 0) schur_kernel<<<gl, 256, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef);
+            if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef);
             HIP_OK(hipEventRecord(h->ev[3], st));
             if (h->use_lds)
                 ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x,
@@ -1667,14 +1720,16 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
                 ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
                                                               h->d_fail);
             HIP_OK(hipEventRecord(h->ev[4], st));
-            int fail = 0;
-            HIP_OK(hipMemcpyAsync(&fail, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, st));
+            // keyframe update beside the landmark back-substitution; both feed the trial's errors
+            if ((rs = lba_fork(h)) != OMV_OK) return rs;
+            update_kf_kernel<<<1, 256, 0, h->side>>>(h->rig, h->R, h->d_offV, h->d_offG, h->d_offA, h->n_opt, lambda,
+                                                     h->d_x, A, B, h->d_scale_partial);
             if (h->n_pts > 0)
-                backsub_kernel<<<gl, 256, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
-            update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, h->d_offV, h->d_offG, h->d_offA, h->n_opt, lambda, h->d_x,
-                                                A, B, h->d_scale_partial);
+                backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
+            if ((rs = lba_join(h)) != OMV_OK) return rs;
             if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
-            if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc)) != OMV_OK) return rs;
+            if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc, true)) != OMV_OK) return rs;
+            const int fail = sc[2] != 0.0;
             HIP_OK(hipEventRecord(h->ev[5], st));
             HIP_OK(hipEventSynchronize(h->ev[5]));
             HIP_OK(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
@@ -1721,18 +1776,21 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     // write back the state (caller order)
     const State &s = h->st[h->cur];
     const int K = h->n_kf, C = h->rig.n_cams, P = h->n_pts, E = h->n_mono;
-    HIP_OK(hipMemcpy(p->Rwb, s.Rwb, sizeof(double) * 9 * K, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->twb, s.twb, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->Rcw, s.Rcw, sizeof(double) * 9 * K * C, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->tcw, s.tcw, sizeof(double) * 3 * K * C, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->vel, s.vel, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->bg, s.bg, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(p->ba, s.ba, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
-    std::vector<double> pts(3 * (size_t)P), chi2(E);
-    HIP_OK(hipMemcpy(pts.data(), s.pts, sizeof(double) * pts.size(), hipMemcpyDeviceToHost));
-    for (int q = 0; q < P; ++q)
-        for (int d = 0; d < 3; ++d) p->pts[3 * (size_t)h->perm_pt[q] + d] = pts[3 * (size_t)q + d];
-    if (E > 0) HIP_OK(hipMemcpy(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost));
+    std::vector<double> stg(h->state_doubles()), chi2(E);
+    HIP_OK(hipMemcpyAsync(stg.data(), s.Rwb, stg.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (E > 0) HIP_OK(hipMemcpyAsync(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    {
+        const double *q = stg.data();
+        auto take = [&](double *dst, size_t n) {
+            std::memcpy(dst, q, n * sizeof(double));
+            q += n;
+        };
+        take(p->Rwb, 9 * (size_t)K), take(p->twb, 3 * (size_t)K), take(p->Rcw, 9 * (size_t)K * C);
+        take(p->tcw, 3 * (size_t)K * C), take(p->vel, 3 * (size_t)K), take(p->bg, 3 * (size_t)K), take(p->ba, 3 * (size_t)K);
+        for (int i = 0; i < P; ++i)
+            for (int d = 0; d < 3; ++d) p->pts[3 * (size_t)h->perm_pt[i] + d] = q[3 * (size_t)i + d];
+    }
     for (int e = 0; e < E; ++e) {
         const int oe = h->perm_edge[e];
         if (res->mono_chi2) res->mono_chi2[oe] = chi2[e];
@@ -1753,22 +1811,9 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
 
 omv_status omv_lba_reset(omv_lba *h) {
     if (!h || !h->st[2].pts) return OMV_ERR_ARG;
-    const size_t K = h->n_kf, C = h->rig.n_cams, P = h->n_pts;
-    for (int b = 0; b < 2; ++b) {
-        const State &s = h->st[2];
-        State &d = h->st[b];
-        auto cp = [&](double *dst, const double *src, size_t n) {
-            return hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream);
-        };
-        HIP_OK(cp(d.Rwb, s.Rwb, 9 * K));
-        HIP_OK(cp(d.twb, s.twb, 3 * K));
-        HIP_OK(cp(d.Rcw, s.Rcw, 9 * K * C));
-        HIP_OK(cp(d.tcw, s.tcw, 3 * K * C));
-        HIP_OK(cp(d.vel, s.vel, 3 * K));
-        HIP_OK(cp(d.bg, s.bg, 3 * K));
-        HIP_OK(cp(d.ba, s.ba, 3 * K));
-        HIP_OK(cp(d.pts, s.pts, 3 * P));
-    }
+    for (int b = 0; b < 2; ++b)
+        HIP_OK(hipMemcpyAsync(h->st[b].Rwb, h->st[2].Rwb, h->state_doubles() * sizeof(double), hipMemcpyDeviceToDevice,
+                              h->stream));
     h->cur = 0;
     HIP_OK(hipStreamSynchronize(h->stream));
     return OMV_OK;

