@@ -183,6 +183,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=64, help="multi-cam frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="frame groups per GPU, each on its own HIP stream (latency-bound matcher stages of one "
+                         "group overlap extraction of another)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-timing", type=int, default=1)
     ap.add_argument("--lba-steps", type=int, default=10, help="LocalInertialBA optimize() calls timed (0: skip)")
@@ -216,44 +219,61 @@ def main():
     from openmavis_amd.orb import ORBextractor
 
     d_img = torch.from_numpy(imgs).to(dev)
-    ex = ORBextractor(NFEAT, SCALE, NLEV, INI_TH, MIN_TH, width=W, height=H, max_images=B * C)
-    cap = ex.max_keypoints()
-    fb = FrameBatch(torch, B, C, cap, W, H, ex.GetScaleFactors(), device=dev)
-    lap = np.tile(LAP, (B, 1))
-    stream = torch.cuda.current_stream(dev)
+    G = max(1, args.streams)
+    if B % G:
+        raise SystemExit(f"--frames {B} is not a multiple of --streams {G}")
+    Bg = B // G
+    groups = []
+    for gi in range(G):
+        ex = ORBextractor(NFEAT, SCALE, NLEV, INI_TH, MIN_TH, width=W, height=H, max_images=Bg * C)
+        cap = ex.max_keypoints()
+        groups.append(dict(
+            ex=ex, cap=cap, fb=FrameBatch(torch, Bg, C, cap, W, H, ex.GetScaleFactors(), device=dev),
+            img=d_img[gi * Bg * C:(gi + 1) * Bg * C], lap=np.tile(LAP, (Bg, 1)), matcher=ORBmatcher(NNRATIO),
+            stream=torch.cuda.Stream(dev) if G > 1 else torch.cuda.current_stream(dev)))
 
-    def extract():
-        ex.extract_batch(d_img, lap, fb.kps.view(-1, cap, 6), fb.desc.view(-1, cap, 32), fb.n_kp.view(-1),
-                         fb.mono.view(-1), stream=stream)
+    def extract(gr):
+        gr["ex"].extract_batch(gr["img"], gr["lap"], gr["fb"].kps.view(-1, gr["cap"], 6),
+                               gr["fb"].desc.view(-1, gr["cap"], 32), gr["fb"].n_kp.view(-1), gr["fb"].mono.view(-1),
+                               stream=gr["stream"])
 
     # map points derived from this batch's keypoints (setup, untimed)
-    extract()
-    torch.cuda.synchronize(dev)
-    if ex.last_error() != 0:
-        raise RuntimeError("extractor capacity error")
-    kps_h = fb.kps.cpu().numpy().view(np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
-                                                ("response", "<f4"), ("octave", "<i4")])).reshape(B, C, cap)
-    desc_h = fb.desc.cpu().numpy()
-    nkp_h = fb.n_kp.cpu().numpy()
-    per = [_gen_mps((kps_h[f], desc_h[f], nkp_h[f], 7000 + first + f)) for f in range(B)]
-    mps = MapPointBatch(**{k: torch.from_numpy(np.stack([p[k] for p in per])).to(dev) for k in per[0]})
-    matcher = ORBmatcher(NNRATIO)
+    kp_dtype = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                         ("octave", "<i4")])
+    nkp_h = []
+    for gi, gr in enumerate(groups):
+        extract(gr)
+        torch.cuda.synchronize(dev)
+        if gr["ex"].last_error() != 0:
+            raise RuntimeError("extractor capacity error")
+        fb, cap = gr["fb"], gr["cap"]
+        kps_h = fb.kps.cpu().numpy().view(kp_dtype).reshape(Bg, C, cap)
+        desc_h = fb.desc.cpu().numpy()
+        nk = fb.n_kp.cpu().numpy()
+        nkp_h.append(nk)
+        per = [_gen_mps((kps_h[f], desc_h[f], nk[f], 7000 + first + gi * Bg + f)) for f in range(Bg)]
+        gr["mps"] = MapPointBatch(**{k: torch.from_numpy(np.stack([p[k] for p in per])).to(dev) for k in per[0]})
+    nkp_h = np.concatenate(nkp_h)
 
     def step():
-        extract()
-        fb.kp_to_mp.fill_(-1)                       # Frame ctor: mvpMapPoints = vector(N, nullptr)
-        matcher.AssignFeaturesToGrid(fb, stream=stream)
-        matcher.StereoLapping(fb, 0.8, stream=stream)
-        matcher.SearchByProjection(fb, mps, TH, False, 50.0, stream=stream, grid_ready=True)
+        for gr in groups:
+            fb, st = gr["fb"], gr["stream"]
+            extract(gr)
+            with torch.cuda.stream(st):
+                fb.kp_to_mp.fill_(-1)                   # Frame ctor: mvpMapPoints = vector(N, nullptr)
+            gr["matcher"].AssignFeaturesToGrid(fb, stream=st)
+            gr["matcher"].StereoLapping(fb, 0.8, stream=st)
+            gr["matcher"].SearchByProjection(fb, gr["mps"], TH, False, 50.0, stream=st, grid_ready=True)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if args.stage_timing:
-        ex.enable_timing(True)
-        matcher.enable_timing(True)
-        ex.stage_ms(reset=True)
-        matcher.stage_ms(reset=True)
+        for gr in groups:
+            gr["ex"].enable_timing(True)
+            gr["matcher"].enable_timing(True)
+            gr["ex"].stage_ms(reset=True)
+            gr["matcher"].stage_ms(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -264,14 +284,17 @@ def main():
     if world > 1:
         dist.barrier()
     dt = job_seconds(time.perf_counter() - t0, dev)   # max over ranks
-    assert ex.last_error() == 0
-    n_matches = int(fb.n_matches.sum().item())
+    assert all(gr["ex"].last_error() == 0 for gr in groups)
+    n_matches = int(sum(gr["fb"].n_matches.sum().item() for gr in groups))
 
+    # per-stage device time per step, summed over the stream groups (groups overlap in time)
     stages = {}
     if args.stage_timing:
-        es, calls = ex.stage_ms(reset=True)
-        ms = matcher.stage_ms(reset=True)
-        stages = {k: v / args.steps for k, v in {**es, **ms}.items()}
+        for gr in groups:
+            es, calls = gr["ex"].stage_ms(reset=True)
+            ms = gr["matcher"].stage_ms(reset=True)
+            for k, v in {**es, **ms}.items():
+                stages[k] = stages.get(k, 0.0) + v / args.steps
 
     lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world) if lba_prob is not None else None
 
@@ -303,7 +326,7 @@ def main():
     roof = None
     if stages:
         dom = max(stages, key=lambda k: stages[k])
-        launches = {"pyr_resize": NLEV - 1}.get(dom, 1)
+        launches = {"pyr_resize": NLEV - 1}.get(dom, 1) * G
         avg_ms = stages[dom] / launches
         achieved = per_step_bytes[dom] / launches / (avg_ms * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -335,7 +358,7 @@ def main():
         "data": "synthetic (seeded Hilti-like 5x720x540 frames; 5000-point local maps from the frames' own keypoints)",
         "config": {"workload": "Hilti-2022 exp04-like 5 cams 720x540, 1200 feat/cam, ORB extract + lapping knn + "
                                "SearchByProjection(M=5000, th=6)",
-                   "frames_per_step_per_gpu": B, "parallelism": f"frame-replicas x{world}"},
+                   "frames_per_step_per_gpu": B, "streams_per_gpu": G, "parallelism": f"frame-replicas x{world}"},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
         "matches_last_step": n_matches,
         "roofline": roof,

@@ -138,9 +138,31 @@ __device__ __forceinline__ int rec_idx(uint32_t v) { return (int)(v & 0xffff); }
 __device__ __forceinline__ int rec_dist(uint32_t v) { return (int)((v >> 16) & 0x1ff); }
 __device__ __forceinline__ int rec_oct(uint32_t v) { return (int)((v >> 25) & 0x1f); }
 
+// The kTop best candidates as sorted 64-bit keys dist << 40 | window order << 20 | octave << 16 | idx,
+// kept in registers: insertion is a branch-free compare-and-shift over compile-time indices (no
+// dynamically indexed arrays, hence no scratch).  Keys are unique (window order), so ties in
+// distance keep window order exactly like the reference's strict `<` scans.
 struct Top {
-    int idx[kTop], dist[kTop], oct[kTop];
-    int n, count;
+    uint64_t key[kTop];
+    int n, count, seq;
+    __device__ __forceinline__ void reset() {
+#pragma unroll
+        for (int q = 0; q < kTop; ++q) key[q] = ~0ull;
+        n = count = seq = 0;
+    }
+    __device__ __forceinline__ void insert(int idx, int dist, int oct) {
+        const uint64_t k = ((uint64_t)dist << 40) | ((uint64_t)(seq++) << 20) | ((uint64_t)oct << 16) | (uint64_t)idx;
+#pragma unroll
+        for (int q = kTop - 1; q > 0; --q) key[q] = k < key[q - 1] ? key[q - 1] : (k < key[q] ? k : key[q]);
+        key[0] = k < key[0] ? k : key[0];
+        n = min(n + 1, kTop);
+    }
+    __device__ __forceinline__ int idx(int q) const { return (int)(key[q] & 0xffff); }
+    __device__ __forceinline__ int oct(int q) const { return (int)((key[q] >> 16) & 0xf); }
+    __device__ __forceinline__ int dist(int q) const { return (int)(key[q] >> 40); }
+    __device__ __forceinline__ uint32_t rec(int q) const {   // Rec entry: idx | dist << 16 | oct << 25
+        return (uint32_t)idx(q) | ((uint32_t)dist(q) << 16) | ((uint32_t)oct(q) << 25);
+    }
 };
 
 __device__ __forceinline__ void load_desc(const uint8_t *p, uint64_t d[4]) {
@@ -153,7 +175,7 @@ __device__ __forceinline__ void load_desc(const uint8_t *p, uint64_t d[4]) {
 template <class Blocked>
 __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, float y, float r, int minL, int maxL,
                             const uint64_t dmp[4], Blocked blocked, Top &t) {
-    t.n = 0, t.count = 0;
+    t.reset();
     const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
     if (nMinCellX >= kGridCols) return;
     const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
@@ -183,14 +205,7 @@ __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, flo
             ++t.count;
             uint64_t d[4];
             load_desc(dd + (size_t)i * 32, d);
-            const int dist = omv::hamming256(dmp, d);
-            // insert after every entry with dist <= this one (window order breaks ties)
-            int pos = t.n;
-            while (pos > 0 && dist < t.dist[pos - 1]) --pos;
-            if (pos >= kTop) continue;
-            for (int q = min(t.n, kTop - 1); q > pos; --q) t.idx[q] = t.idx[q - 1], t.dist[q] = t.dist[q - 1], t.oct[q] = t.oct[q - 1];
-            t.idx[pos] = i, t.dist[pos] = dist, t.oct[pos] = k.octave;
-            if (t.n < kTop) ++t.n;
+            t.insert(i, omv::hamming256(dmp, d), k.octave);
         }
     }
 }
@@ -223,7 +238,7 @@ __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_
     const size_t bc = (size_t)fm * C + c;
     Rec &out = recs[bc];
     Top t;
-    t.n = 0, t.count = 0;
+    t.reset();
     const int lvl = m.level[bc];
     if (m.in_view[bc] && lvl >= 0 && lvl < f.nlevels) {
         uint64_t dmp[4];
@@ -233,8 +248,11 @@ __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_
         scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, lvl - 1, lvl, dmp,
                     [&](int slot) { return occ && occ[slot]; }, t);
     }
-    for (int q = 0; q < kTop; ++q)
-        out.e[q] = q < t.n ? (uint32_t)t.idx[q] | ((uint32_t)t.dist[q] << 16) | ((uint32_t)t.oct[q] << 25) : 0u;
+    uint4 *o4 = reinterpret_cast<uint4 *>(&out);   // 64-B record as four 16-B stores
+#pragma unroll
+    for (int v = 0; v < kTop / 4; ++v)
+        o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
+                           4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
     counts[bc] = t.count;
 }
 
@@ -242,11 +260,11 @@ __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_
 constexpr int kMaxClaims = 2 * kMaxCams;
 constexpr int kMaxRevived = 64;   // initially-occupied keypoints freed during the call (rare)
 
-struct Eval {
+struct Eval {                // claim / rel point at the lane's LDS rows (dynamic indexing stays out of scratch)
     int nclaim;
-    int claim[kMaxClaims];
+    int *claim;
     int nrel;
-    int rel[kMaxClaims];   // slots whose blocked status decided the result (best / second)
+    int *rel;              // slots whose blocked status decided the result (best / second)
     int nmatch;
     bool fallback;         // needed a full window rescan
     bool unblock;          // overwrote a blocked slot while having no observations
@@ -357,8 +375,8 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
             scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f),
                         lvl - 1, lvl, dmp, is_blocked, t);
             b1 = b2 = -1, d1 = d2 = 256, o1 = o2 = -1;
-            if (t.n > 0) b1 = t.idx[0], d1 = t.dist[0], o1 = t.oct[0];
-            if (t.n > 1) b2 = t.idx[1], d2 = t.dist[1], o2 = t.oct[1];
+            if (t.n > 0) b1 = t.idx(0), d1 = t.dist(0), o1 = t.oct(0);
+            if (t.n > 1) b2 = t.idx(1), d2 = t.dist(1), o2 = t.oct(1);
         }
         if (b1 >= 0) e.rel[e.nrel++] = c * cap + b1;
         if (b2 >= 0) e.rel[e.nrel++] = c * cap + b2;
@@ -386,6 +404,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     __shared__ BlockStage bs;
     __shared__ int revived[kMaxRevived];
     __shared__ int nrevived;
+    __shared__ int lane_claim[64 * kMaxClaims], lane_rel[64 * kMaxClaims];
     const int frame = blockIdx.x, lane = threadIdx.x;
     const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap;
     const int nwords = (S + 31) >> 5;
@@ -434,6 +453,8 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
         while (start < nb) {
             const bool active = lane >= start && lane < nb;
             Eval e;
+            e.claim = lane_claim + lane * kMaxClaims;
+            e.rel = lane_rel + lane * kMaxClaims;
             const int nrev = nrevived;
             if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, e);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;

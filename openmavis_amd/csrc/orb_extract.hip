@@ -173,7 +173,16 @@ __device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
     return max(a, -b);
 }
 
-// One wavefront (= one workgroup of 64) per cell.
+// One wavefront (= one workgroup of 64) per cell.  The cell's region is staged into LDS with dword
+// loads (row stride rs, 4-byte aligned; pixel (r, q) at pix[r * rs + q]); then
+//   1. prefilter at min(iniTh, minTh): a 9-arc of the 16-ring always holds two adjacent compass points
+//      (ring positions 0/4/8/12), so a pixel can be a corner only if some adjacent compass pair is
+//      brighter (d < -t) or darker (d > t) together -- exact, not a heuristic; survivors are compacted
+//      in row-major order (ballot prefix) into an LDS list;
+//   2. the full FAST strength for the survivors only (the strength map S stays 0 elsewhere, which is
+//      what the NMS of any threshold >= t sees for non-corners);
+//   3. NMS (3x3, strict >) at iniTh and minTh in one pass over the survivors;
+//   4. emission at iniTh, or minTh if the cell had no iniTh keypoint (ORBextractor.cc:764-782).
 __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
                                                         int *cell_cnt, uint32_t *cell_kp, int rmax) {
@@ -182,54 +191,88 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     const int ci = blockIdx.x - img * g.n_cells;
     const Cell c = cells[ci];
     const int lane = threadIdx.x;
-    uint8_t *pix = smem;
-    uint8_t *S = smem + rmax;
     const int rw = c.x1 - c.x0, rh = c.y1 - c.y0;
     int sp;
     const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, c.level, &sp);
-    for (int i = lane; i < rw * rh; i += 64) {
-        const int r = i / rw, q = i - r * rw;
-        pix[i] = src[(size_t)(c.y0 + r) * sp + c.x0 + q];
-        S[i] = 0;
+    const uint8_t *row0 = src + (size_t)c.y0 * sp + c.x0;
+    const bool dwords = ((sp & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
+    const int o = dwords ? (int)(((uintptr_t)row0) & 3) : 0;
+    const int rs = (rw + o + 3) & ~3;
+    uint8_t *pix = smem + o;
+    uint8_t *S = smem + rmax;
+    uint16_t *cand = (uint16_t *)(smem + 2 * rmax);
+    if (dwords) {
+        const int nd = rs >> 2;
+        const uint32_t *g0 = (const uint32_t *)(row0 - o);
+        const int sw = sp >> 2;
+        uint32_t *l0 = (uint32_t *)smem;
+        for (int i = lane; i < nd * rh; i += 64) {
+            const int r = i / nd, w = i - r * nd;
+            l0[i] = g0[(size_t)r * sw + w];
+        }
+    } else {
+        for (int i = lane; i < rw * rh; i += 64) {
+            const int r = i / rw, q = i - r * rw;
+            pix[r * rs + q] = row0[(size_t)r * sp + q];
+        }
     }
+    for (int i = lane; i < (rs * rh) >> 2; i += 64) ((uint32_t *)S)[i] = 0;
     __syncthreads();
     const int dw = rw - 6, dh = rh - 6;   // detection window [3, rw-4] x [3, rh-4]
     const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
-    for (int i = lane; i < ndet; i += 64) {
-        const int r = 3 + i / dw, q = 3 + i % dw;
-        const int s = fast_strength(pix + r * rw + q, rw);
-        S[r * rw + q] = (uint8_t)min(max(s, 0), 255);
+    const int t = min(g.ini_th, g.min_th);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int ncand = 0;
+    for (int i0 = 0; i0 < ndet; i0 += 64) {
+        const int i = i0 + lane;
+        bool pass = false;
+        if (i < ndet) {
+            const int r = 3 + i / dw, q = 3 + i % dw;
+            const uint8_t *p = pix + r * rs + q;
+            const int v = p[0];
+            const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
+            const bool a0 = d0 > t, a4 = d4 > t, a8 = d8 > t, a12 = d12 > t;
+            const bool b0 = d0 < -t, b4 = d4 < -t, b8 = d8 < -t, b12 = d12 < -t;
+            pass = (a0 && a4) || (a4 && a8) || (a8 && a12) || (a12 && a0) || (b0 && b4) || (b4 && b8) ||
+                   (b8 && b12) || (b12 && b0);
+        }
+        const uint64_t m = __ballot(pass);
+        if (pass) cand[ncand + __popcll(m & lt)] = (uint16_t)i;
+        ncand += __popcll(m);
     }
     __syncthreads();
-    // NMS at iniThFAST, minThFAST fallback if the cell yields nothing (:764-782)
-    int th = g.ini_th;
-    int total = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        total = 0;
-        for (int i0 = 0; i0 < ndet; i0 += 64) {
-            const int i = i0 + lane;
-            bool keep = false;
-            if (i < ndet) {
-                const int r = 3 + i / dw, q = 3 + i % dw;
-                const uint8_t *s = S + r * rw + q;
-                const int v = s[0];
-                if (v > th) {
-                    keep = true;
-                    const int sc = v - 1;
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) {
-                        if (k == 4) continue;
-                        const int nv = s[(k / 3 - 1) * rw + (k % 3 - 1)];
-                        const int ns = nv > th ? nv - 1 : 0;
-                        keep = keep && (sc > ns);
-                    }
-                }
-            }
-            total += __popcll(__ballot(keep));
-        }
-        if (total > 0 || pass == 1) break;
-        th = g.min_th;
+    for (int k = lane; k < ncand; k += 64) {
+        const int i = cand[k];
+        const int r = 3 + i / dw, q = 3 + i % dw;
+        const int sv = fast_strength(pix + r * rs + q, rs);
+        S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
     }
+    __syncthreads();
+    int tot_ini = 0, tot_min = 0;
+    for (int k0 = 0; k0 < ncand; k0 += 64) {
+        const int k = k0 + lane;
+        bool ki = false, km = false;
+        if (k < ncand) {
+            const int i = cand[k];
+            const int r = 3 + i / dw, q = 3 + i % dw;
+            const uint8_t *sp8 = S + r * rs + q;
+            const int v = sp8[0];
+            const int sc = v - 1;
+            ki = v > g.ini_th;
+            km = v > g.min_th;
+#pragma unroll
+            for (int n = 0; n < 9; ++n) {
+                if (n == 4) continue;
+                const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
+                ki = ki && (sc > (nv > g.ini_th ? nv - 1 : 0));
+                km = km && (sc > (nv > g.min_th ? nv - 1 : 0));
+            }
+        }
+        tot_ini += __popcll(__ballot(ki));
+        tot_min += __popcll(__ballot(km));
+    }
+    const int th = tot_ini > 0 ? g.ini_th : g.min_th;
+    const int total = tot_ini > 0 ? tot_ini : tot_min;
     if (total > g.cell_cap) {   // cannot happen by construction (cap = max NMS survivors)
         if (lane == 0) cell_cnt[blockIdx.x] = -1;
         return;
@@ -237,33 +280,30 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     // emit row-major; coordinates relative to the FAST border (minBorder = 16)
     uint32_t *out = cell_kp + (size_t)blockIdx.x * g.cell_cap;
     int base = 0;
-    for (int i0 = 0; i0 < ndet; i0 += 64) {
-        const int i = i0 + lane;
+    for (int k0 = 0; k0 < ncand; k0 += 64) {
+        const int k = k0 + lane;
         bool keep = false;
         uint32_t packed = 0;
-        if (i < ndet) {
+        if (k < ncand) {
+            const int i = cand[k];
             const int r = 3 + i / dw, q = 3 + i % dw;
-            const uint8_t *s = S + r * rw + q;
-            const int v = s[0];
+            const uint8_t *sp8 = S + r * rs + q;
+            const int v = sp8[0];
             if (v > th) {
                 keep = true;
                 const int sc = v - 1;
 #pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    if (k == 4) continue;
-                    const int nv = s[(k / 3 - 1) * rw + (k % 3 - 1)];
-                    const int ns = nv > th ? nv - 1 : 0;
-                    keep = keep && (sc > ns);
+                for (int n = 0; n < 9; ++n) {
+                    if (n == 4) continue;
+                    const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
+                    keep = keep && (sc > (nv > th ? nv - 1 : 0));
                 }
                 const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
                 packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)sc << 24);
             }
         }
         const uint64_t m = __ballot(keep);
-        if (keep) {
-            const int off = __popcll(m & ((1ull << lane) - 1ull));
-            out[base + off] = packed;
-        }
+        if (keep) out[base + __popcll(m & lt)] = packed;
         base += __popcll(m);
     }
     if (lane == 0) cell_cnt[blockIdx.x] = total;
@@ -949,7 +989,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.n_max = out_off;
     g.node_cap = std::max(max_nodes, max_cells_lvl);
     g.node_cap = (g.node_cap + 15) & ~15;
-    o->rmax = max_rw * max_rh;
+    o->rmax = ((max_rw + 6) & ~3) * max_rh;   // LDS row stride rounds (rw + misalignment) up to 4 bytes
     o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
     return OMV_OK;
 }
@@ -1044,7 +1084,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    fast_cells_kernel<<<g.n_cells * n, 64, 2 * o->rmax, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
+    fast_cells_kernel<<<g.n_cells * n, 64, 4 * o->rmax, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
                                                                o->d_cell_cnt, o->d_cell_kp, o->rmax);
     mark(o, st);
     // K3: octree per (image, level)
