@@ -33,6 +33,7 @@ constexpr int kGridCols = 64, kGridRows = 48, kCells = kGridCols * kGridRows;
 constexpr int kTH_HIGH = 100;
 constexpr int kTop = 16;   // candidates kept per (point, camera): rescans only when >14 are claimed
 constexpr int kMaxCams = 8;
+constexpr size_t kResolveLds = 150 * 1024;   // dynamic LDS of the resolve workgroup (set as its maximum)
 
 #define HIP_OK(x)                                                                    \
     do {                                                                             \
@@ -227,8 +228,13 @@ __device__ __forceinline__ float window_radius(const FrameArgs &f, const MpArgs 
 }
 
 // One thread per (frame, map point, camera).
+// Per-point flag word for the resolve stage: bits 0..C-1 in_view per camera, bit 16 skipped
+// (mp_skipped), bit 17 has observations.
+constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
+
 __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
-                                                   const uint8_t *occ_init, Rec *recs, int *counts) {
+                                                   const uint8_t *occ_init, Rec *recs, int *counts, int *flags,
+                                                   int far_points, float th_far) {
     const int C = f.n_cams;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long long)n_frames * m.M * C) return;
@@ -236,6 +242,13 @@ __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_
     const long long fm = gid / C;
     const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
     const size_t bc = (size_t)fm * C + c;
+    if (c == 0) {
+        int fl = 0;
+        for (int q = 0; q < C; ++q) fl |= m.in_view[(size_t)fm * C + q] ? (1 << q) : 0;
+        if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
+        if (m.has_obs[fm]) fl |= kFlagObs;
+        flags[fm] = fl;
+    }
     Rec &out = recs[bc];
     Top t;
     t.reset();
@@ -275,6 +288,7 @@ struct ResolveArgs {
     MpArgs m;
     const Rec *recs;
     const int *counts;   // candidates in the window not blocked when the record was built
+    const int *flags;    // per point: in_view bits | kFlagSkip | kFlagObs
     const int32_t *l2r, *r2l;
     const uint8_t *occ_init;
     int32_t *kp_to_mp;
@@ -285,14 +299,46 @@ struct ResolveArgs {
 };
 
 // Shared per-block staging of the 64 points a wavefront evaluates.
+// LDS image of one block of 64 points: raw copies of the global SoA rows [point][cam] (and [point]),
+// filled asynchronously by global_load_lds while the previous block is being resolved.
 struct BlockStage {
-    Rec rec[64 * kMaxCams];
-    int count[64 * kMaxCams];
-    int8_t level[64 * kMaxCams];
-    uint8_t in_view[64 * kMaxCams];
-    uint8_t skip[64];
-    uint8_t obs[64];
+    const Rec *rec;
+    const int *count, *level, *flags;
 };
+
+// Byte offsets of one stage buffer's arrays (16-byte aligned), for C cameras.
+struct StageLayout {
+    int rec, count, level, flags, bytes;
+    __host__ __device__ StageLayout(int C) {
+        rec = 0;
+        count = rec + 64 * C * (int)sizeof(Rec);
+        level = count + 64 * C * 4;
+        flags = level + 64 * C * 4;
+        bytes = flags + 64 * 4;
+    }
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+// Async copy of n bytes global -> LDS (n a multiple of SZ; lane-linear image), SZ in {4, 16}.
+#define OMV_GLDS_COPY(NAME, SZ)                                                                                \
+    __device__ __forceinline__ void NAME(const void *g, void *l, int n, int lane) {                             \
+        for (int off = 0; off < n; off += 64 * SZ)                                                             \
+            if (off + lane * SZ < n)                                                                           \
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)((const char *)g + off + lane * SZ),            \
+                                                 (lds_void_t *)((char *)l + off), SZ, 0, 0);                   \
+    }
+OMV_GLDS_COPY(glds_copy16, 16)
+OMV_GLDS_COPY(glds_copy4, 4)
+#undef OMV_GLDS_COPY
+// The resolve workgroup is ONE wavefront: its LDS operations complete in order, so a wavefront-scope
+// fence (compiler ordering only; no vmcnt drain of the in-flight global_load_lds) replaces barriers.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bits, int s) { return (bits[s >> 5] >> (s & 31)) & 1u; }
 
@@ -311,15 +357,16 @@ __device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float 
 }
 
 __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
-                         const int *revived, int nrevived, Eval &e) {
+                         const int *revived, int nrevived, const int32_t *l2r, const int32_t *r2l, Eval &e) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     const int C = f.n_cams, cap = f.kp_cap;
     e.nclaim = e.nrel = e.nmatch = 0;
     e.fallback = e.unblock = false;
-    if (bs.skip[l]) return;
+    const int fl = bs.flags[l];
+    if (fl & kFlagSkip) return;
     const size_t fm = (size_t)frame * m.M + i;
-    const bool obs = bs.obs[l] != 0;
+    const bool obs = (fl & kFlagObs) != 0;
     auto is_blocked = [&](int slot) {
         if (bit_of(bits, slot)) {
             // an own earlier claim of a point without observations unblocks it
@@ -336,10 +383,8 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
         if (!obs && bit_of(bits, slot)) e.unblock = true;
         e.claim[e.nclaim++] = slot;
     };
-    const int32_t *l2r = a.l2r + (size_t)frame * cap;
-    const int32_t *r2l = a.r2l + (size_t)frame * cap;
     for (int c = 0; c < C; ++c) {
-        if (!bs.in_view[l * C + c]) continue;
+        if (!((fl >> c) & 1)) continue;
         const int lvl = bs.level[l * C + c];
         if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
         const Rec &r = bs.rec[l * C + c];
@@ -401,7 +446,6 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
 // One wavefront (one 64-thread workgroup) per frame.
 __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    __shared__ BlockStage bs;
     __shared__ int revived[kMaxRevived];
     __shared__ int nrevived;
     __shared__ int lane_claim[64 * kMaxClaims], lane_rel[64 * kMaxClaims];
@@ -412,6 +456,22 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     uint32_t *occ0 = rsm + nwords;                                // initially occupied (not in the records)
     int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);       // first blocking claimer lane in a batch
     int *lastw = owner + S;                                       // last writer lane among committing lanes
+    int32_t *l2r_s = lastw + S;                                   // this frame's mvLeftToRightMatch
+    int32_t *r2l_s = l2r_s + cap;                                 // and mvRightToLeftMatch
+    uint8_t *stage0 = reinterpret_cast<uint8_t *>(rsm) + ((8 * (size_t)nwords + 8 * (size_t)S + 8 * (size_t)cap + 15) & ~(size_t)15);
+    const StageLayout SL(C);
+    const int M = a.m.M;
+    // issue the async copy of block `base` into stage buffer `buf`
+    auto issue = [&](int buf, int base) {
+        uint8_t *b = stage0 + buf * SL.bytes;
+        const int nb = min(64, M - base);
+        const size_t o = ((size_t)frame * M + base) * C, op = (size_t)frame * M + base;
+        glds_copy16(a.recs + o, b + SL.rec, nb * C * (int)sizeof(Rec), lane);
+        glds_copy4(a.counts + o, b + SL.count, nb * C * 4, lane);
+        glds_copy4(a.m.level + o, b + SL.level, nb * C * 4, lane);
+        glds_copy4(a.flags + op, b + SL.flags, nb * 4, lane);
+    };
+    if (M > 0) issue(0, 0);
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
     for (int w = lane; w < nwords; w += 64) {
         uint32_t v = 0;
@@ -423,31 +483,23 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
         occ0[w] = v;
     }
     for (int s = lane; s < S; s += 64) owner[s] = 64, lastw[s] = -1;
+    for (int s = lane; s < cap; s += 64) {
+        l2r_s[s] = a.l2r[(size_t)frame * cap + s];
+        r2l_s[s] = a.r2l[(size_t)frame * cap + s];
+    }
     if (lane == 0) nrevived = 0;
-    __syncthreads();
+    wave_sync();
     int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
     int total = 0;
-    const int M = a.m.M;
-    for (int base = 0; base < M; base += 64) {
+    for (int base = 0, buf = 0; base < M; base += 64, buf ^= 1) {
         const int nb = min(64, M - base);
-        // stage the block's records and flags in LDS (coalesced)
-        {
-            const int4 *src = reinterpret_cast<const int4 *>(a.recs + ((size_t)frame * M + base) * C);
-            int4 *dst = reinterpret_cast<int4 *>(bs.rec);
-            const int n16 = nb * C * (int)(sizeof(Rec) / 16);
-            for (int q = lane; q < n16; q += 64) dst[q] = src[q];
-            const size_t o = ((size_t)frame * M + base) * C;
-            for (int q = lane; q < nb * C; q += 64) {
-                bs.level[q] = (int8_t)max(-1, min(127, a.m.level[o + q]));
-                bs.in_view[q] = a.m.in_view[o + q];
-            }
-            for (int q = lane; q < nb * C; q += 64) bs.count[q] = a.counts[o + q];
-            if (lane < nb) {
-                bs.skip[lane] = mp_skipped(a.m, frame, base + lane, C, a.far_points, a.th_far);
-                bs.obs[lane] = a.m.has_obs[(size_t)frame * M + base + lane] != 0;
-            }
-        }
-        __syncthreads();
+        // block `base` has landed in LDS; start copying the next block into the other buffer
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_sync();
+        if (base + 64 < M) issue(buf ^ 1, base + 64);
+        const uint8_t *sb = stage0 + buf * SL.bytes;
+        const BlockStage bs{reinterpret_cast<const Rec *>(sb + SL.rec), reinterpret_cast<const int *>(sb + SL.count),
+                            reinterpret_cast<const int *>(sb + SL.level), reinterpret_cast<const int *>(sb + SL.flags)};
         const int i = base + lane;
         int start = 0;
         while (start < nb) {
@@ -456,18 +508,18 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             e.claim = lane_claim + lane * kMaxClaims;
             e.rel = lane_rel + lane * kMaxClaims;
             const int nrev = nrevived;
-            if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, e);
+            if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, l2r_s, r2l_s, e);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
-            const bool obs = active && bs.obs[lane];
+            const bool obs = active && (bs.flags[lane] & kFlagObs);
             if (obs)
                 for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], lane);
-            __syncthreads();
+            wave_sync();
             bool conflict = false;
             if (active && lane > start) {
                 conflict = e.fallback;   // a full rescan saw the whole window: only safe at the batch head
                 for (int q = 0; q < e.nrel && !conflict; ++q) conflict = owner[e.rel[q]] < lane;
             }
-            __syncthreads();
+            wave_sync();
             if (obs)
                 for (int q = 0; q < e.nclaim; ++q) owner[e.claim[q]] = 64;
             uint64_t cm = __ballot(conflict);
@@ -482,7 +534,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             const bool committed = lane >= start && lane < j0;
             if (committed)
                 for (int t = 0; t < e.nclaim; ++t) atomicMax(&lastw[e.claim[t]], lane);
-            __syncthreads();
+            wave_sync();
             if (committed)
                 for (int t = 0; t < e.nclaim; ++t) {
                     const int s = e.claim[t];
@@ -498,14 +550,14 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
                         atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
                     }
                 }
-            __syncthreads();
+            wave_sync();
             if (committed)
                 for (int t = 0; t < e.nclaim; ++t) lastw[e.claim[t]] = -1;
             int nm = committed ? e.nmatch : 0;
             for (int d = 32; d >= 1; d >>= 1) nm += __shfl_xor(nm, d, 64);
             total += nm;
             start = j0;
-            __syncthreads();
+            wave_sync();
         }
     }
     if (lane == 0) a.n_matches[frame] = total;
@@ -583,6 +635,7 @@ struct omv_matcher {
     int32_t *d_cell_start = nullptr, *d_cell_idx = nullptr;
     Rec *d_recs = nullptr;
     int *d_counts = nullptr;
+    int *d_flags = nullptr;   // per (frame, point): in_view bits | skip | has_obs (cand -> resolve)
     int32_t *d_knn_i = nullptr, *d_knn_d = nullptr;
     int *d_err = nullptr;
     FrameArgs f{};
@@ -613,14 +666,24 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
     f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
 }
 
+static size_t resolve_lds_bytes(int C, int cap) {
+    const size_t S = (size_t)C * cap;
+    size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + 2 * sizeof(int) * S + 2 * sizeof(int32_t) * cap;
+    b = (b + 15) & ~(size_t)15;
+    return b + 2 * (size_t)StageLayout(C).bytes;
+}
+
 extern "C" {
 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
     if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)
         return OMV_ERR_ARG;
-    if ((size_t)n_cams * kp_cap * 9 + sizeof(BlockStage) > 150 * 1024) return OMV_ERR_ARG;   // resolve LDS
+    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds) return OMV_ERR_ARG;   // resolve workspace must fit LDS
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
+    if (hipFuncSetAttribute((const void *)resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds) !=
+        hipSuccess)
+        return OMV_ERR_HIP;
     omv_matcher *h = new omv_matcher();
     h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
     const size_t fc = (size_t)max_frames * n_cams;
@@ -628,6 +691,7 @@ omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mp
     HIP_OK(hipMalloc(&h->d_cell_idx, sizeof(int32_t) * fc * kp_cap));
     HIP_OK(hipMalloc(&h->d_recs, sizeof(Rec) * std::max<size_t>(1, fc * max_mps)));
     HIP_OK(hipMalloc(&h->d_counts, sizeof(int) * std::max<size_t>(1, fc * max_mps)));
+    HIP_OK(hipMalloc(&h->d_flags, sizeof(int) * std::max<size_t>(1, (size_t)max_frames * max_mps)));
     HIP_OK(hipMalloc(&h->d_knn_i, sizeof(int32_t) * 2 * max_frames * kp_cap));
     HIP_OK(hipMalloc(&h->d_knn_d, sizeof(int32_t) * 2 * max_frames * kp_cap));
     HIP_OK(hipMalloc(&h->d_err, sizeof(int)));
@@ -670,7 +734,7 @@ omv_status omv_matcher_last_error(omv_matcher *h) {
 
 omv_status omv_matcher_destroy(omv_matcher *h) {
     if (!h) return OMV_ERR_ARG;
-    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_knn_i, h->d_knn_d, h->d_err};
+    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_flags, h->d_knn_i, h->d_knn_d, h->d_err};
     for (void *q : p)
         if (q) (void)hipFree(q);
     delete h;
@@ -721,14 +785,14 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
         cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs,
-                                                              h->d_counts);
+                                                              h->d_counts, h->d_flags, far_points, th_far);
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
-    ResolveArgs ra{f, m, h->d_recs, h->d_counts, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
+    ResolveArgs ra{f, m, h->d_recs, h->d_counts, h->d_flags, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
                    far_points};
     const int S = h->n_cams * h->kp_cap;
-    const size_t lds = sizeof(uint32_t) * 2 * ((S + 31) / 32) + 2 * sizeof(int) * S;
+    const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap);
     resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
     if (h->timing) {
         h->ev.push_back({2, {e0, e1}});
