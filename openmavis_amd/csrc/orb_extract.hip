@@ -41,6 +41,7 @@ constexpr int kPatchR = 21;   // 18 (max steered pattern radius) + 3 (blur half-
 constexpr int kPatchW = 2 * kPatchR + 1;   // 43
 constexpr int kWinR = 18;
 constexpr int kWinW = 2 * kWinR + 1;       // 37
+constexpr int kPatchS = 48;                 // LDS row stride of the staged patch: 12 dwords cover 43 + 3
 
 __constant__ int c_pattern[256 * 4] = {
 #define OMV_PATTERN_TABLE_BEGIN
@@ -681,9 +682,8 @@ struct DescArgs {
 };
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchW + 7];
+    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
     __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kWinW];
-    __shared__ __attribute__((aligned(16))) uint8_t win[4][kWinW * kWinW + 7];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + wave;
     int img = slot / g.out_per_img;
@@ -710,11 +710,35 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
     const int score = (int)(p >> 24);
     int sp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
+    // stage the 43x43 patch (row stride kPatchS): interior patches as 12 aligned dwords per row, all
+    // loads issued before any LDS store; patches touching the level border take reflect101 byte loads
     uint8_t *P = patch[wave];
-    for (int i = active ? lane : kPatchW * kPatchW; i < kPatchW * kPatchW; i += 64) {
-        const int r = i / kPatchW, q = i - r * kPatchW;
-        const int yy = omv::reflect101(cy - kPatchR + r, L.h), xx = omv::reflect101(cx - kPatchR + q, L.w);
-        P[i] = src[(size_t)yy * sp + xx];
+    const int x0 = cx - kPatchR, y0 = cy - kPatchR;
+    const bool inner = x0 >= 0 && y0 >= 0 && x0 + kPatchW <= L.w && y0 + kPatchW <= L.h && (sp & 3) == 0 &&
+                       (((uintptr_t)src) & 3) == 0;
+    if (active && inner) {
+        const uint8_t *r0 = src + (size_t)y0 * sp + x0;
+        const int o = (int)(((uintptr_t)r0) & 3);
+        const uint32_t *g0 = (const uint32_t *)(r0 - o);
+        const int sw = sp >> 2;
+        uint32_t v[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int d = lane + 64 * k;
+            if (d < kPatchW * 12) v[k] = g0[(size_t)(d / 12) * sw + d % 12];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int d = lane + 64 * k;
+            if (d < kPatchW * 12) reinterpret_cast<uint32_t *>(P)[d] = v[k];
+        }
+        P += o;
+    } else if (active) {
+        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
+            const int r = i / kPatchW, q = i - r * kPatchW;
+            const int yy = omv::reflect101(y0 + r, L.h), xx = omv::reflect101(x0 + q, L.w);
+            P[r * kPatchS + q] = src[(size_t)yy * sp + xx];
+        }
     }
     __syncthreads();
     // intensity centroid over the r = 15 disc (umax rows), exact integer sums
@@ -723,7 +747,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         const int v = i / 31 - 15, u = i % 31 - 15;
         const int av = v < 0 ? -v : v;
         if ((u < 0 ? -u : u) <= c_umax[av]) {
-            const int I = P[(kPatchR + v) * kPatchW + kPatchR + u];
+            const int I = P[(kPatchR + v) * kPatchS + kPatchR + u];
             m10 += u * I;
             m01 += v * I;
         }
@@ -733,26 +757,29 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         m10 += __shfl_xor(m10, d, 64);
     }
     const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
-    // 7x7 sigma-2 blur of the 37x37 window: horizontal (exact u16), vertical ((+2^15) >> 16)
+    // 7x7 sigma-2 blur (GaussianBlur's bit-exact 8U path): horizontal sums exact in u16 over the 43 patch
+    // rows x 37 window columns, 7 taps as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
+    // vertical ((sum + 2^15) >> 16) evaluated only at the 512 steered sample points.
     uint16_t *Hs = hsum[wave];
-    for (int i = lane; i < kPatchW * kWinW; i += 64) {
-        const int r = i / kWinW, q = i - r * kWinW;
-        const uint8_t *row = P + r * kPatchW + q;
-        int acc = 0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) acc += c_gauss7[k] * row[k];
-        Hs[i] = (uint16_t)acc;
+    {
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch[wave]);
+        const int pofs = (int)(P - patch[wave]);
+        constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+        for (int i = lane; i < kPatchW * kWinW; i += 64) {
+            const int r = i / kWinW, q = i - r * kWinW;
+            const int off = pofs + r * kPatchS + q, dw = off >> 2, sh = off & 3;
+            const uint32_t d0 = pw[dw], d1 = pw[dw + 1], d2 = pw[dw + 2];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            Hs[i] = (uint16_t)__builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
+        }
     }
     __syncthreads();
-    uint8_t *Wn = win[wave];
-    for (int i = lane; i < kWinW * kWinW; i += 64) {
-        const int r = i / kWinW, q = i - r * kWinW;
+    auto blurred = [&](int r, int q) {   // window coordinates (0..36)
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * Hs[(r + k) * kWinW + q];
-        Wn[i] = (uint8_t)min((acc + 32768u) >> 16, 255u);
-    }
-    __syncthreads();
+        return (int)min((acc + 32768u) >> 16, 255u);
+    };
     // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
     float sn, cs;
     omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
@@ -767,8 +794,8 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
         const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
         const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
-        const int ia = Wn[(kWinR + ady) * kWinW + kWinR + adx];
-        const int ib = Wn[(kWinR + bdy) * kWinW + kWinR + bdx];
+        const int ia = blurred(kWinR + ady, kWinR + adx);
+        const int ib = blurred(kWinR + bdy, kWinR + bdx);
         words[rd] = __ballot(ia < ib);
     }
     if (!active) return;   // after the last barrier
