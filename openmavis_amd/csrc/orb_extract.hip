@@ -103,29 +103,55 @@ __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_
 }
 
 // K1 --------------------------------------------------------------------------------------------
-// One thread per output pixel of level l; rows of level l-1 are re-read from L2.
+// One workgroup per (output row, image) of level l: the two source rows of level l-1 (y.sx0, y.sx1)
+// are staged in LDS with dword loads, each thread computes 4 adjacent output pixels and stores them
+// as one dword (level pitches are 16-byte aligned).
+constexpr int kPyrRowDw = 1024;   // staged source row capacity in dwords (levels up to 4096 px wide)
+
 __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const uint8_t *images, size_t img_stride,
                                                          size_t pitch0, uint8_t *pyr, const XTab *xt,
                                                          const XTab *yt, int n_images) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2][kPyrRowDw];
     const LevelGeom &L = g.lv[l];
-    const long long per_img = (long long)L.w * L.h;
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= per_img * n_images) return;
-    const int img = (int)(gid / per_img);
-    const int rem = (int)(gid - (long long)img * per_img);
-    const int dy = rem / L.w, dx = rem - dy * L.w;
+    const int dy = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
     int sp;
     const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, l - 1, &sp);
-    uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off;
-    const XTab x = xt[L.xtab_off + dx];
+    const int sw = g.lv[l - 1].w;
+    uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
     const XTab y = yt[L.ytab_off + dy];
-    const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
-    const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
     const uint8_t *r0 = src + (size_t)y.sx0 * sp, *r1 = src + (size_t)y.sx1 * sp;
-    const int h0 = r0[x.sx0] * a0 + r0[x.sx1] * a1;
-    const int h1 = r1[x.sx0] * a0 + r1[x.sx1] * a1;
-    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-    dst[(size_t)dy * L.pitch + dx] = (uint8_t)min(v, 255);
+    const int ndw = (sw + 3) >> 2;
+    const bool dwords = (sp & 3) == 0 && ((((uintptr_t)src) & 3) == 0) && ndw * 4 <= sp;
+    if (dwords) {
+        const uint32_t *w0 = (const uint32_t *)r0, *w1 = (const uint32_t *)r1;
+        for (int i = tid; i < ndw; i += 256) rows[0][i] = w0[i], rows[1][i] = w1[i];
+    } else {
+        uint8_t *b0 = (uint8_t *)rows[0], *b1 = (uint8_t *)rows[1];
+        for (int i = tid; i < sw; i += 256) b0[i] = r0[i], b1[i] = r1[i];
+    }
+    __syncthreads();
+    const uint8_t *R0 = (const uint8_t *)rows[0], *R1 = (const uint8_t *)rows[1];
+    const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
+    for (int dx0 = tid * 4; dx0 < L.w; dx0 += 1024) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int dx = dx0 + j;
+            if (dx < L.w) {
+                const XTab x = xt[L.xtab_off + dx];
+                const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
+                const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
+                const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
+                const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                packed |= (uint32_t)min(v, 255) << (8 * j);
+            }
+        }
+        if (dx0 + 3 < L.w) {
+            *reinterpret_cast<uint32_t *>(dst + dx0) = packed;
+        } else {
+            for (int j = 0; j < 4 && dx0 + j < L.w; ++j) dst[dx0 + j] = (uint8_t)(packed >> (8 * j));
+        }
+    }
 }
 
 // K2 --------------------------------------------------------------------------------------------
@@ -1105,9 +1131,8 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K1: pyramid, level by level
     for (int l = 1; l < g.nlevels; ++l) {
-        const long long tot = (long long)g.lv[l].w * g.lv[l].h * n;
-        const int blocks = (int)((tot + 255) / 256);
-        pyr_resize_kernel<<<blocks, 256, 0, st>>>(g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, n);
+        pyr_resize_kernel<<<dim3(g.lv[l].h, n), 256, 0, st>>>(g, l, images, image_stride, pitch, o->d_pyr, o->d_xt,
+                                                               o->d_yt, n);
     }
     mark(o, st);
     // K2: FAST per cell
