@@ -158,46 +158,45 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
 // FAST-9 strength: max over the 16 circular 9-arcs of min(d) (darker) and of min(-d) (brighter),
 // d = centre - ring.  A pixel is a FAST corner at threshold t iff S > t, and OpenCV's
 // cornerScore<16>(t) then returns S - 1 (the threshold floor max(t, .) never binds for a corner).
+typedef short pk16 __attribute__((ext_vector_type(2)));   // packed int16 pair (v_pk_* ops)
+
+// (x, y) -> (y, x)
+__device__ __forceinline__ pk16 pk_swap(pk16 x) { return pk16{x.y, x.x}; }
+
+// Ring values are handled as pairs (k, k+8), so each min/max below is one v_pk_min/max_i16 for two
+// arcs; Q(k) for k >= 8 is the swapped pair of k-8.
 __device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
-    const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * stride];
-    d[1] = v - p[3 * stride + 1];
-    d[2] = v - p[2 * stride + 2];
-    d[3] = v - p[stride + 3];
-    d[4] = v - p[3];
-    d[5] = v - p[-stride + 3];
-    d[6] = v - p[-2 * stride + 2];
-    d[7] = v - p[-3 * stride + 1];
-    d[8] = v - p[-3 * stride];
-    d[9] = v - p[-3 * stride - 1];
-    d[10] = v - p[-2 * stride - 2];
-    d[11] = v - p[-stride - 3];
-    d[12] = v - p[-3];
-    d[13] = v - p[stride - 3];
-    d[14] = v - p[2 * stride - 2];
-    d[15] = v - p[3 * stride - 1];
-    int mn2[16], mx2[16];
+    const short v = p[0];
+    const int o[16] = {3 * stride, 3 * stride + 1, 2 * stride + 2, stride + 3, 3, -stride + 3, -2 * stride + 2,
+                       -3 * stride + 1, -3 * stride, -3 * stride - 1, -2 * stride - 2, -stride - 3, -3, stride - 3,
+                       2 * stride - 2, 3 * stride - 1};
+    pk16 d[8];
+    const pk16 vv{v, v};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int mn4[16], mx4[16];
+    for (int k = 0; k < 8; ++k) d[k] = vv - pk16{(short)p[o[k]], (short)p[o[k + 8]]};
+    auto Q = [&](const pk16 *a, int k) { return k < 8 ? a[k] : pk_swap(a[k - 8]); };
+    pk16 mn2[8], mx2[8], mn4[8], mx4[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    for (int k = 0; k < 8; ++k) {
+        mn2[k] = __builtin_elementwise_min(d[k], Q(d, k + 1));
+        mx2[k] = __builtin_elementwise_max(d[k], Q(d, k + 1));
     }
-    int a = -1000, b = 1000;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int m9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int M9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        a = max(a, m9);
-        b = min(b, M9);
+    for (int k = 0; k < 8; ++k) {
+        mn4[k] = __builtin_elementwise_min(mn2[k], Q(mn2, k + 2));
+        mx4[k] = __builtin_elementwise_max(mx2[k], Q(mx2, k + 2));
     }
-    return max(a, -b);
+    pk16 a{-1000, -1000}, b{1000, 1000};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const pk16 opp = pk_swap(d[k]);   // d[k + 8] paired with d[k]
+        const pk16 m9 = __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], Q(mn4, k + 4)), opp);
+        const pk16 M9 = __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], Q(mx4, k + 4)), opp);
+        a = __builtin_elementwise_max(a, m9);
+        b = __builtin_elementwise_min(b, M9);
+    }
+    const int A = max((int)a.x, (int)a.y), B = min((int)b.x, (int)b.y);
+    return max(A, -B);
 }
 
 // One wavefront (= one workgroup of 64) per cell.  The cell's region is staged into LDS with dword
@@ -247,6 +246,12 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     __syncthreads();
     const int dw = rw - 6, dh = rh - 6;   // detection window [3, rw-4] x [3, rh-4]
     const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
+    // i / dw by multiply-shift with m = floor(2^20/dw) + 1: exact while i * dw < 2^20 (cells are < 80 px wide)
+    const uint32_t mdw = dw > 0 ? (1u << 20) / (uint32_t)dw + 1u : 0u;
+    auto rowcol = [&](int i, int &r, int &q) {
+        const int rr = (int)(((uint32_t)i * mdw) >> 20);
+        r = 3 + rr, q = 3 + i - rr * dw;
+    };
     const int t = min(g.ini_th, g.min_th);
     const uint64_t lt = (1ull << lane) - 1ull;
     int ncand = 0;
@@ -254,7 +259,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         const int i = i0 + lane;
         bool pass = false;
         if (i < ndet) {
-            const int r = 3 + i / dw, q = 3 + i % dw;
+            int r, q;
+            rowcol(i, r, q);
             const uint8_t *p = pix + r * rs + q;
             const int v = p[0];
             const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
@@ -270,7 +276,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     __syncthreads();
     for (int k = lane; k < ncand; k += 64) {
         const int i = cand[k];
-        const int r = 3 + i / dw, q = 3 + i % dw;
+        int r, q;
+        rowcol(i, r, q);
         const int sv = fast_strength(pix + r * rs + q, rs);
         S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
     }
@@ -281,7 +288,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         bool ki = false, km = false;
         if (k < ncand) {
             const int i = cand[k];
-            const int r = 3 + i / dw, q = 3 + i % dw;
+            int r, q;
+            rowcol(i, r, q);
             const uint8_t *sp8 = S + r * rs + q;
             const int v = sp8[0];
             const int sc = v - 1;
@@ -313,7 +321,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         uint32_t packed = 0;
         if (k < ncand) {
             const int i = cand[k];
-            const int r = 3 + i / dw, q = 3 + i % dw;
+            int r, q;
+            rowcol(i, r, q);
             const uint8_t *sp8 = S + r * rs + q;
             const int v = sp8[0];
             if (v > th) {
