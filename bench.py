@@ -190,6 +190,8 @@ def main():
     ap.add_argument("--stage-timing", type=int, default=1)
     ap.add_argument("--lba-steps", type=int, default=10, help="LocalInertialBA optimize() calls timed (0: skip)")
     ap.add_argument("--lba-warmup", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=120, help="frames in the CPU-baseline sample (~6 s)")
+    ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,7 +201,8 @@ def main():
     first = rank * B
     # inputs are generated before anything touches the GPU (worker pool = plain fork, no HIP yet)
     imgs = np.concatenate(_pool_map(_gen_frame, list(range(first, first + B))))   # [B*C, H, W]
-    cpu_frames = [] if (args.no_cpu_baseline or world > 1) else _pool_map(_gen_frame, list(range(10_000, 10_012)))
+    cpu_frames = [] if (args.no_cpu_baseline or world > 1) else _pool_map(
+        _gen_frame, list(range(10_000, 10_000 + args.cpu_frames)))
     lba_prob = None
     if args.lba_steps > 0:
         from openmavis_amd import synth_ba
@@ -342,7 +345,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(len(cpu_frames), cpu_frames)
         if lba is not None:
-            lba["cpu_baseline"] = lba_cpu_baseline(lba_prob)
+            lba["cpu_baseline"] = lba_cpu_baseline(lba_prob, args.cpu_lba_runs)
     out = {
         "metric": "multi-cam frames/sec (ORB extract+match) + LocalBA iters/sec, 5x720x540",
         "value": round(value, 2),
