@@ -170,6 +170,46 @@ omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *
                        const int *nt, int32_t *idx2, int32_t *dist2, void *stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Frame::isInFrustum (src/Frame.cc:736-826; the multi-camera isInFrustumChecks, :1529-1653) with
+ * MapPoint::PredictScale (src/MapPoint.cc:624-637) and KannalaBrandt8::project(Vector3f)
+ * (src/CameraModels/KannalaBrandt8.cpp:48-67), for every local map point of every frame — the loop
+ * of Tracking::SearchLocalPoints.  Writes the projection fields SearchByProjection reads.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct omv_rig {
+    int n_cams;
+    float cam[8][8];               /* KannalaBrandt8 mvParameters per camera block                 */
+    float R_cl[8][9], t_cl[8][3];  /* camera block c from block 0: mTrl / mTsll / mTsrl (c=0: I, 0) */
+    float t_lc[8][3];              /* translation of the inverse: mTlr / mTlsl / mTlsr (c=0: 0)     */
+    float min_x, max_x, min_y, max_y;  /* mnMinX .. mnMaxY                                          */
+    float log_scale_factor;        /* mfLogScaleFactor                                              */
+    int n_levels;                  /* mnScaleLevels                                                 */
+} omv_rig;
+
+typedef struct omv_frame_pose {   /* block-0 camera: mRcw, mtcw and the inverse mRwc, mOw */
+    float Rcw[9], tcw[3], Rwc[9], Ow[3];
+} omv_frame_pose;
+
+typedef struct omv_mp_world {     /* device SoA, [frame][M] */
+    const float *pos;              /* [M][3] GetWorldPos()                                          */
+    const float *normal;           /* [M][3] GetNormal()                                            */
+    const float *min_dist;         /* [M] mfMinDistance                                             */
+    const float *max_dist;         /* [M] mfMaxDistance                                             */
+} omv_mp_world;
+
+typedef struct omv_mp_track {     /* outputs, same layout as omv_mp_view */
+    float *proj_x, *proj_y;        /* [M][n_cams] -1 when not in view (reset like the reference)    */
+    float *view_cos;               /* [M][n_cams] written when in view                              */
+    int32_t *level;                /* [M][n_cams] predicted level, -1 when not in view              */
+    uint8_t *in_view;              /* [M][n_cams]                                                   */
+    float *track_depth;            /* [M] block-0 distance, written only when block 0 sees the point */
+} omv_mp_track;
+
+/* poses: device [n_frames]; n_in_view (optional, device [n_frames], accumulated): points for which
+ * isInFrustum returned true. */
+omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig *rig, const omv_mp_world *mp, int M,
+                       float viewing_cos_limit, const omv_mp_track *out, int32_t *n_in_view, void *stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Local inertial bundle adjustment — replaces the optimisation inside Optimizer::LocalInertialBA
  * (src/Optimizer.cc:2728-3385): EdgeMono / EdgeInertial / EdgeGyroRW / EdgeAccRW
  * (src/G2oTypes.cc, include/G2oTypes.h:283-633), g2o's Levenberg-Marquardt

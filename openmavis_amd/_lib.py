@@ -48,6 +48,28 @@ class MpView(ctypes.Structure):
                 ("track_depth", ctypes.c_void_p), ("is_bad", ctypes.c_void_p), ("has_obs", ctypes.c_void_p)]
 
 
+class Rig(ctypes.Structure):
+    """omv_rig (include/omv.h)."""
+    _fields_ = [("n_cams", ctypes.c_int), ("cam", (ctypes.c_float * 8) * 8), ("R_cl", (ctypes.c_float * 9) * 8),
+                ("t_cl", (ctypes.c_float * 3) * 8), ("t_lc", (ctypes.c_float * 3) * 8), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int)]
+
+
+class MpWorld(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_void_p), ("normal", ctypes.c_void_p), ("min_dist", ctypes.c_void_p),
+                ("max_dist", ctypes.c_void_p)]
+
+
+class MpTrack(ctypes.Structure):
+    _fields_ = [("proj_x", ctypes.c_void_p), ("proj_y", ctypes.c_void_p), ("view_cos", ctypes.c_void_p),
+                ("level", ctypes.c_void_p), ("in_view", ctypes.c_void_p), ("track_depth", ctypes.c_void_p)]
+
+
+# omv_frame_pose: Rcw[9] tcw[3] Rwc[9] Ow[3] floats = 24 floats per frame (pass a float32 [F, 24] array)
+FRAME_POSE_FLOATS = 24
+
+
 class LbaProblem(ctypes.Structure):
     """omv_lba_problem (include/omv.h)."""
     _fields_ = [("n_cams", ctypes.c_int), ("cam", ctypes.c_void_p), ("Rcb", ctypes.c_void_p),
@@ -108,6 +130,8 @@ SIGNATURES = {
                                            _VP, _VP]),
     "omv_matcher_stereo_lapping": (_I, [_VP, _I, _VP, _VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
     "omv_bf_knn2": (_I, [_I, _VP, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP]),
+    "omv_frustum": (_I, [_I, _VP, ctypes.POINTER(Rig), ctypes.POINTER(MpWorld), _I, _F, ctypes.POINTER(MpTrack), _VP,
+                         _VP]),
     "omv_lba_create": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(_VP)]),
     "omv_lba_destroy": (_I, [_VP]),
     "omv_lba_set_problem": (_I, [_VP, ctypes.POINTER(LbaProblem)]),

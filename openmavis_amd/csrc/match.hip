@@ -627,6 +627,91 @@ __global__ void stereo_pairs_kernel(const int32_t *idx2, const int32_t *dist2, i
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Frame::isInFrustum, multi-camera branch: one thread per (frame, map point), the camera-block
+// transforms of the frame composed once per workgroup in LDS (same float operation order as the
+// reference's per-point Eigen expressions: 3x3 products summed left to right, no contraction).
+// KannalaBrandt8.cpp / MapPoint.cc call the C double cos / sin / log on float arguments.
+__device__ __forceinline__ void mat3f(const float *a, const float *b, float *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+__device__ __forceinline__ void matvec3f(const float *a, const float *x, float *r) {
+    for (int i = 0; i < 3; ++i) r[i] = a[3 * i] * x[0] + a[3 * i + 1] * x[1] + a[3 * i + 2] * x[2];
+}
+
+__global__ void __launch_bounds__(256) frustum_kernel(const omv_frame_pose *poses, omv_rig rig, omv_mp_world mp, int M,
+                                                      float cos_limit, omv_mp_track out, int32_t *n_in_view) {
+    __shared__ float Rc[kMaxCams][9], tc[kMaxCams][3], twc[kMaxCams][3];
+    const int frame = blockIdx.y, C = rig.n_cams;
+    const omv_frame_pose &pose = poses[frame];
+    if (threadIdx.x < C) {
+        const int c = threadIdx.x;
+        if (c == 0) {
+            for (int q = 0; q < 9; ++q) Rc[0][q] = pose.Rcw[q];
+            for (int q = 0; q < 3; ++q) tc[0][q] = pose.tcw[q], twc[0][q] = pose.Ow[q];
+        } else {
+            float R[9], t[3];
+            mat3f(rig.R_cl[c], pose.Rcw, R);
+            for (int q = 0; q < 9; ++q) Rc[c][q] = R[q];
+            matvec3f(rig.R_cl[c], pose.tcw, t);
+            for (int q = 0; q < 3; ++q) tc[c][q] = t[q] + rig.t_cl[c][q];
+            matvec3f(pose.Rwc, rig.t_lc[c], t);
+            for (int q = 0; q < 3; ++q) twc[c][q] = t[q] + pose.Ow[q];
+        }
+    }
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const size_t fm = (size_t)frame * M + i;
+    const float P[3] = {mp.pos[3 * fm], mp.pos[3 * fm + 1], mp.pos[3 * fm + 2]};
+    const float Pn[3] = {mp.normal[3 * fm], mp.normal[3 * fm + 1], mp.normal[3 * fm + 2]};
+    const float mind = mp.min_dist[fm], maxd = mp.max_dist[fm];
+    bool any = false;
+    for (int c = 0; c < C; ++c) {
+        const size_t o = fm * C + c;
+        float px = -1.f, py = -1.f;
+        int lvl = -1;
+        bool vis = false;
+        float Pc[3];
+        matvec3f(Rc[c], P, Pc);
+        for (int q = 0; q < 3; ++q) Pc[q] = Pc[q] + tc[c][q];
+        const float Pc_dist = omv::sqrtf_cr(Pc[0] * Pc[0] + Pc[1] * Pc[1] + Pc[2] * Pc[2]);
+        if (Pc[2] >= 0.0f) {
+            const float *k = rig.cam[c];
+            const float x2y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
+            const float theta = omv::glibc_atan2f(omv::sqrtf_cr(x2y2), Pc[2]);
+            const float psi = omv::glibc_atan2f(Pc[1], Pc[0]);
+            const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+            const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+            const float u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
+            const float v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
+            if (!(u < rig.min_x || u > rig.max_x || v < rig.min_y || v > rig.max_y)) {
+                const float maxD = 1.2f * maxd, minD = 0.8f * mind;
+                const float PO[3] = {P[0] - twc[c][0], P[1] - twc[c][1], P[2] - twc[c][2]};
+                const float dist = omv::sqrtf_cr(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+                if (!(dist < minD || dist > maxD)) {
+                    const float vc = (PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2]) / dist;
+                    if (!(vc < cos_limit)) {
+                        const float ratio = maxd / dist;
+                        int ns = (int)ceil(log((double)ratio) / (double)rig.log_scale_factor);
+                        ns = ns < 0 ? 0 : (ns >= rig.n_levels ? rig.n_levels - 1 : ns);
+                        px = u, py = v, lvl = ns, vis = true;
+                        out.view_cos[o] = vc;
+                        if (c == 0) out.track_depth[fm] = Pc_dist;
+                    }
+                }
+            }
+        }
+        out.proj_x[o] = px, out.proj_y[o] = py, out.level[o] = lvl, out.in_view[o] = vis ? 1 : 0;
+        any = any || vis;
+    }
+    if (n_in_view) {
+        const uint64_t m = __ballot(any);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_in_view + frame, __popcll(m));
+    }
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -674,6 +759,19 @@ static size_t resolve_lds_bytes(int C, int cap) {
 }
 
 extern "C" {
+
+omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig *rig, const omv_mp_world *mp, int M,
+                       float viewing_cos_limit, const omv_mp_track *out, int32_t *n_in_view, void *stream) {
+    if (n_frames <= 0 || !poses || !rig || !mp || !out || M < 0 || rig->n_cams <= 0 || rig->n_cams > kMaxCams ||
+        rig->n_levels <= 0)
+        return OMV_ERR_ARG;
+    if (M == 0) return OMV_OK;
+    hipStream_t st = (hipStream_t)stream;
+    frustum_kernel<<<dim3((M + 255) / 256, n_frames), 256, 0, st>>>(poses, *rig, *mp, M, viewing_cos_limit, *out,
+                                                                    n_in_view);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
     if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)

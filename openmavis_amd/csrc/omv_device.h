@@ -101,4 +101,79 @@ __device__ __forceinline__ int hamming256(const uint64_t *a, const uint64_t *b) 
     return __popcll(a[0] ^ b[0]) + __popcll(a[1] ^ b[1]) + __popcll(a[2] ^ b[2]) + __popcll(a[3] ^ b[3]);
 }
 
+
+// glibc atan2f (fdlibm e_atan2f.c / s_atanf.c), float, no contraction.  KannalaBrandt8::project
+// computes theta / psi with atan2f (KannalaBrandt8.cpp:30-31, :50-51); this restatement is
+// bit-identical to the host libm (tools/check_atan2f.c, tests/test_native_cpu.py).
+__device__ __forceinline__ uint32_t f32_bits(float f) { return __float_as_uint(f); }
+__device__ inline float glibc_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float aT[11] = {3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                          9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                          4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f};
+    const int32_t hx = (int32_t)f32_bits(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) id = 0, x = (2.0f * x - 1.0f) / (2.0f + x);
+            else id = 1, x = (x - 1.0f) / (x + 1.0f);
+        } else {
+            if (ix < 0x401c0000) id = 2, x = (x - 1.5f) / (1.0f + 1.5f * x);
+            else id = 3, x = -1.0f / x;
+        }
+    }
+    const float z = x * x, w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+__device__ inline float glibc_atan2f(float y, float x) {
+    const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+                pi_lo = -8.7422776573e-08f, tiny = 1.0e-30f;
+    const int32_t hx = (int32_t)f32_bits(x), ix = hx & 0x7fffffff, hy = (int32_t)f32_bits(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return glibc_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        if (m < 2) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            const float r[4] = {pi_o_4 + tiny, -pi_o_4 - tiny, 3.0f * pi_o_4 + tiny, -3.0f * pi_o_4 - tiny};
+            return r[m];
+        }
+        const float r[4] = {0.0f, -0.0f, pi + tiny, -pi - tiny};
+        return r[m];
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = glibc_atanf(fabsf(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return __uint_as_float(f32_bits(z) ^ 0x80000000u);
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// Correctly rounded f32 sqrt (libm sqrtf): v_sqrt_f32 alone is 1 ulp; the f64 sqrt is correctly
+// rounded and 53 >= 2*24+2 bits make the second rounding innocuous.
+__device__ __forceinline__ float sqrtf_cr(float x) { return (float)sqrt((double)x); }
+
 }  // namespace omv

@@ -155,6 +155,45 @@ class ORBmatcher:
         return frames.n_matches
 
 
+def make_rig(cams, R_cl, t_cl, width, height, scale_factor=1.2, nlevels=8):
+    """omv_rig from per-camera KB8 parameters and the block-c-from-block-0 transforms (float32)."""
+    r = _lib.Rig()
+    C = len(cams)
+    r.n_cams = C
+    for c in range(C):
+        for q in range(8):
+            r.cam[c][q] = float(cams[c][q])
+        Rc = np.asarray(R_cl[c], np.float32).reshape(3, 3)
+        tc = np.asarray(t_cl[c], np.float32).reshape(3)
+        tlc = (-(Rc.astype(np.float64).T @ tc.astype(np.float64))).astype(np.float32)
+        for q in range(9):
+            r.R_cl[c][q] = float(Rc.reshape(-1)[q])
+        for q in range(3):
+            r.t_cl[c][q] = float(tc[q])
+            r.t_lc[c][q] = float(tlc[q]) if c else 0.0
+    r.min_x, r.max_x, r.min_y, r.max_y = 0.0, float(width), 0.0, float(height)
+    r.log_scale_factor = float(np.float32(np.log(np.float64(np.float32(scale_factor)))))
+    r.n_levels = nlevels
+    return r
+
+
+def isInFrustum(poses, rig, world, track, viewingCosLimit=0.5, n_in_view=None, stream=None):
+    """Frame::isInFrustum for every local map point of every frame (src/Frame.cc:736-826, :1529-1653).
+
+    poses: device float32 [F, 24] (omv_frame_pose); world: dict of device tensors pos [F, M, 3],
+    normal [F, M, 3], min_dist / max_dist [F, M]; track: a MapPointBatch whose proj_x / proj_y /
+    view_cos / level / in_view / track_depth are written in place (the SearchByProjection inputs)."""
+    lib = _lib.load()
+    F, M = world["pos"].shape[0], world["pos"].shape[1]
+    w = _lib.MpWorld(_lib.ptr(world["pos"]), _lib.ptr(world["normal"]), _lib.ptr(world["min_dist"]),
+                     _lib.ptr(world["max_dist"]))
+    t = _lib.MpTrack(_lib.ptr(track.proj_x), _lib.ptr(track.proj_y), _lib.ptr(track.view_cos), _lib.ptr(track.level),
+                     _lib.ptr(track.in_view), _lib.ptr(track.track_depth))
+    s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    _lib.check(lib.omv_frustum(F, _lib.ptr(poses), ctypes.byref(rig), ctypes.byref(w), M, ctypes.c_float(viewingCosLimit),
+                               ctypes.byref(t), _lib.ptr(n_in_view), s), "omv_frustum")
+
+
 def bf_knn2(query, nq, train, nt, stream=None):
     """knnMatch(k=2) over a batch of (query, train) sets: torch uint8 [P, Q, 32], [P, T, 32]; counts
     int32 [P].  Returns (idx2, dist2) int32 [P, Q, 2]."""

@@ -107,3 +107,90 @@ def make_map_points(kps, desc, n_kp, M, seed, width, height, nlevels=8, frac_tru
     out["level"][ar[m2], cam1[m2]] = sl[m2]
     out["in_view"][ar[m2], cam1[m2]] = 1
     return out
+
+
+# ---- 3-D local maps for Frame::isInFrustum (BASELINE config 2 with geometry) ---------------------------
+def hilti_rig(n_cams=5):
+    """KB8 parameters [C][8] and the block-c-from-block-0 transforms (R_cl [C][3][3], t_cl [C][3]) of the
+    Hilti-2022 rig (block 0 = cam0 left, 1 = cam1 right, >= 2 side cameras), float32."""
+    from .synth_ba import rig as ba_rig
+    cams, Rbc, tbc = ba_rig()
+    Rcb = np.transpose(Rbc, (0, 2, 1))
+    tcb = -np.einsum("cij,cj->ci", Rcb, tbc)
+    R_cl = np.einsum("cij,jk->cik", Rcb, Rbc[0])
+    t_cl = np.einsum("cij,j->ci", Rcb, tbc[0]) + tcb
+    return cams[:n_cams].astype(np.float32), R_cl[:n_cams].astype(np.float32), t_cl[:n_cams].astype(np.float32)
+
+
+def random_pose(rng):
+    """omv_frame_pose as float32[24]: Rcw, tcw, Rwc, Ow of block 0."""
+    q = rng.normal(0, 1, 4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    t = rng.uniform(-5, 5, 3)
+    Rwc = R.T
+    Ow = -Rwc @ t
+    return np.concatenate([R.reshape(-1), t, Rwc.reshape(-1), Ow]).astype(np.float32)
+
+
+def kb8_unproject(k, u, v, iters=10):
+    """Ray (unit) of pixel (u, v) through KannalaBrandt8 k (Newton on theta, like unproject())."""
+    k = np.asarray(k, np.float64)
+    px, py = (np.asarray(u, np.float64) - k[2]) / k[0], (np.asarray(v, np.float64) - k[3]) / k[1]
+    r = np.sqrt(px * px + py * py)
+    th = r.copy()
+    for _ in range(iters):
+        t2 = th * th
+        f = th * (1 + t2 * (k[4] + t2 * (k[5] + t2 * (k[6] + t2 * k[7])))) - r
+        fd = 1 + t2 * (3 * k[4] + t2 * (5 * k[5] + t2 * (7 * k[6] + t2 * 9 * k[7])))
+        th = th - f / fd
+    s = np.where(r > 1e-12, np.sin(th) / np.maximum(r, 1e-12), 1.0)
+    return np.stack([px * s, py * s, np.cos(th)], -1)
+
+
+def make_world_map(kps, desc, n_kp, M, seed, cams, R_cl, t_cl, pose, width, height, nlevels=8, frac_true=0.6,
+                   scale=1.2):
+    """Local map points in 3-D for one frame: `frac_true` are keypoints of a random camera block
+    unprojected to a depth U(2, 20) m (descriptor with U{0..8} bit flips, mfMaxDistance chosen so
+    PredictScale returns the keypoint's octave), the rest random pixels/depths/octaves.  Normals point
+    from the observing camera to the point (+ noise).  Returns (world dict, map-point dict)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    C = kps.shape[0]
+    n_kp = np.asarray(n_kp)
+    cam = rng.integers(0, C, M)
+    true = (np.arange(M) < int(M * frac_true)) & (n_kp[cam] > 0)
+    kidx = np.minimum((rng.random(M) * np.maximum(n_kp[cam], 1)).astype(np.int64), np.maximum(n_kp[cam] - 1, 0))
+    src = kps[cam, kidx]
+    u = np.where(true, src["x"], rng.uniform(0, width, M))
+    v = np.where(true, src["y"], rng.uniform(0, height, M))
+    octv = np.where(true, src["octave"], rng.integers(0, nlevels, M))
+    ray = np.zeros((M, 3))
+    for c in range(C):
+        sel = cam == c
+        ray[sel] = kb8_unproject(cams[c], u[sel], v[sel])
+    depth = rng.uniform(2.0, 20.0, M)
+    Xc = ray * depth[:, None]
+    Rcl, tcl = R_cl[cam].astype(np.float64), t_cl[cam].astype(np.float64)
+    Xl = np.einsum("mji,mj->mi", Rcl, Xc - tcl)
+    Rwc, Ow = pose[12:21].reshape(3, 3).astype(np.float64), pose[21:24].astype(np.float64)
+    Xw = Xl @ Rwc.T + Ow
+    Oc = np.einsum("mji,mj->mi", Rcl, -tcl) @ Rwc.T + Ow
+    d = Xw - Oc
+    dist = np.linalg.norm(d, axis=1)
+    nrm = d / dist[:, None] + rng.normal(0, 0.05, (M, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    maxd = dist * np.float64(scale) ** octv * rng.uniform(0.86, 0.97, M)
+    mind = maxd / np.float64(scale) ** (nlevels - 1)
+    world = dict(pos=Xw.astype(np.float32), normal=nrm.astype(np.float32), min_dist=mind.astype(np.float32),
+                 max_dist=maxd.astype(np.float32))
+    mp = dict(
+        desc=rng.integers(0, 256, (M, 32), dtype=np.uint8),
+        proj_x=np.full((M, C), -1, np.float32), proj_y=np.full((M, C), -1, np.float32),
+        view_cos=np.zeros((M, C), np.float32), level=np.full((M, C), -1, np.int32),
+        in_view=np.zeros((M, C), np.uint8), track_depth=rng.uniform(1.0, 60.0, M).astype(np.float32),
+        is_bad=(rng.random(M) < 0.02).astype(np.uint8), has_obs=(rng.random(M) > 0.03).astype(np.uint8))
+    mp["desc"][true] = flip_bits(desc[cam[true], kidx[true]], rng)
+    return world, mp

@@ -7,6 +7,9 @@
 //   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
 //                                                    src/ORBmatcher.cc:23-340 (+ RadiusByViewingCos :342-347)
 //   ORBmatcher::DescriptorDistance                   src/ORBmatcher.cc:2577-2591
+//   Frame::isInFrustum / isInFrustumChecks           src/Frame.cc:736-826, :1529-1653 (multi-camera branch)
+//     + MapPoint::PredictScale                       src/MapPoint.cc:624-637
+//     + KannalaBrandt8::project(Eigen::Vector3f)     src/CameraModels/KannalaBrandt8.cpp:48-67
 //   cv::BFMatcher(NORM_HAMMING).knnMatch(k = 2)      as called by Frame::ComputeMultiFishEyeMatches,
 //                                                    src/Frame.cc:1483 (OpenCV batchDistance K = 2:
 //                                                    strict '<' insertion, first train index wins ties)
@@ -237,5 +240,96 @@ void oracle_bf_knn2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t 
 }
 
 int oracle_descriptor_distance(const uint8_t *a, const uint8_t *b) { return descriptor_distance(a, b); }
+
+// ---- Frame::isInFrustum, multi-camera branch (one frame) ----------------------------------------------
+// Float arithmetic in Eigen's evaluation order without contraction: 3x3 products and dot products sum
+// left to right, norm() = sqrt((x*x + y*y) + z*z).  KannalaBrandt8.cpp and MapPoint.cc have no
+// `using namespace std`, so cos(float) / sin(float) / log(float) there resolve to the C double
+// functions: the float argument is promoted and the double result feeds the float expression.
+struct RigF {
+    int n_cams;
+    float cam[8][8];
+    float R_cl[8][9], t_cl[8][3];   // camera block c from camera 0 (mTrl / mTsll / mTsrl)
+    float t_lc[8][3];               // translation of the inverse (mTlr / mTlsl / mTlsr)
+    float min_x, max_x, min_y, max_y;
+    float log_scale_factor;         // mfLogScaleFactor = (float)log(mfScaleFactor)
+    int n_levels;
+};
+struct PoseF {
+    float Rcw[9], tcw[3], Rwc[9], Ow[3];
+};
+
+static void mat3f(const float *a, const float *b, float *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+static void matvec3f(const float *a, const float *x, float *r) {
+    for (int i = 0; i < 3; ++i) r[i] = a[3 * i] * x[0] + a[3 * i + 1] * x[1] + a[3 * i + 2] * x[2];
+}
+
+// KannalaBrandt8::project(const Eigen::Vector3f&)
+static void kb8_project_f(const float *k, const float *X, float &u, float &v) {
+    const float x2y2 = X[0] * X[0] + X[1] * X[1];
+    const float theta = atan2f(sqrtf(x2y2), X[2]);
+    const float psi = atan2f(X[1], X[0]);
+    const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+    u = (float)(k[0] * r * std::cos((double)psi) + k[2]);
+    v = (float)(k[1] * r * std::sin((double)psi) + k[3]);
+}
+
+int oracle_frustum(const RigF *rig, const PoseF *pose, const float *pos, const float *normal, const float *min_d,
+                   const float *max_d, int M, float cos_limit, float *proj_x, float *proj_y, float *view_cos,
+                   int32_t *level, uint8_t *in_view, float *track_depth) {
+    const int C = rig->n_cams;
+    float Rc[8][9], tc[8][3], twc[8][3];
+    for (int c = 0; c < C; ++c) {
+        if (c == 0) {
+            std::memcpy(Rc[0], pose->Rcw, 36), std::memcpy(tc[0], pose->tcw, 12), std::memcpy(twc[0], pose->Ow, 12);
+            continue;
+        }
+        mat3f(rig->R_cl[c], pose->Rcw, Rc[c]);         // mR = Rrl * mRcw
+        float t[3];
+        matvec3f(rig->R_cl[c], pose->tcw, t);          // mt = Rrl * mtcw + trl
+        for (int i = 0; i < 3; ++i) tc[c][i] = t[i] + rig->t_cl[c][i];
+        matvec3f(pose->Rwc, rig->t_lc[c], t);          // twc = mRwc * mTlr.translation() + mOw
+        for (int i = 0; i < 3; ++i) twc[c][i] = t[i] + pose->Ow[i];
+    }
+    int n_any = 0;
+    for (int i = 0; i < M; ++i) {
+        const float *P = pos + 3 * i, *Pn = normal + 3 * i;
+        bool any = false;
+        for (int c = 0; c < C; ++c) {   // isInFrustum resets the projections and levels first
+            proj_x[i * C + c] = -1, proj_y[i * C + c] = -1, level[i * C + c] = -1, in_view[i * C + c] = 0;
+        }
+        for (int c = 0; c < C; ++c) {
+            float Pc[3];
+            matvec3f(Rc[c], P, Pc);
+            for (int q = 0; q < 3; ++q) Pc[q] = Pc[q] + tc[c][q];
+            const float Pc_dist = std::sqrt(Pc[0] * Pc[0] + Pc[1] * Pc[1] + Pc[2] * Pc[2]);
+            if (Pc[2] < 0.0f) continue;
+            float u, v;
+            kb8_project_f(rig->cam[c], Pc, u, v);
+            if (u < rig->min_x || u > rig->max_x) continue;
+            if (v < rig->min_y || v > rig->max_y) continue;
+            const float maxD = 1.2f * max_d[i], minD = 0.8f * min_d[i];
+            const float PO[3] = {P[0] - twc[c][0], P[1] - twc[c][1], P[2] - twc[c][2]};
+            const float dist = std::sqrt(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+            if (dist < minD || dist > maxD) continue;
+            const float vc = (PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2]) / dist;
+            if (vc < cos_limit) continue;
+            const float ratio = max_d[i] / dist;   // PredictScale
+            int ns = (int)std::ceil(std::log((double)ratio) / (double)rig->log_scale_factor);
+            if (ns < 0) ns = 0;
+            else if (ns >= rig->n_levels) ns = rig->n_levels - 1;
+            proj_x[i * C + c] = u, proj_y[i * C + c] = v, level[i * C + c] = ns, view_cos[i * C + c] = vc;
+            in_view[i * C + c] = 1;
+            if (c == 0) track_depth[i] = Pc_dist;
+            any = true;
+        }
+        n_any += any;
+    }
+    return n_any;
+}
 
 }  // extern "C"

@@ -177,6 +177,34 @@ def descriptor_distance(a, b):
     return lib().oracle_descriptor_distance(_p(a), _p(b))
 
 
+class RigF(ctypes.Structure):
+    _fields_ = [("n_cams", ctypes.c_int), ("cam", (ctypes.c_float * 8) * 8), ("R_cl", (ctypes.c_float * 9) * 8),
+                ("t_cl", (ctypes.c_float * 3) * 8), ("t_lc", (ctypes.c_float * 3) * 8), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int)]
+
+
+def frustum(rig, pose, pos, normal, min_dist, max_dist, cos_limit=0.5, view_cos=None, track_depth=None):
+    """Frame::isInFrustum restated for one frame.  rig: a ctypes struct with omv_rig's layout (copied);
+    pose: float32 [24]; pos/normal [M, 3], min/max_dist [M].  view_cos / track_depth: prior values
+    (left untouched where the reference leaves them).  Returns (dict, n_in_view)."""
+    r = RigF.from_buffer_copy(bytes(rig))
+    M, C = len(pos), r.n_cams
+    pose = np.ascontiguousarray(pose, np.float32)
+    pos = np.ascontiguousarray(pos, np.float32)
+    normal = np.ascontiguousarray(normal, np.float32)
+    mind = np.ascontiguousarray(min_dist, np.float32)
+    maxd = np.ascontiguousarray(max_dist, np.float32)
+    out = dict(proj_x=np.zeros((M, C), np.float32), proj_y=np.zeros((M, C), np.float32),
+               view_cos=np.array(view_cos if view_cos is not None else np.zeros((M, C)), np.float32),
+               level=np.zeros((M, C), np.int32), in_view=np.zeros((M, C), np.uint8),
+               track_depth=np.array(track_depth if track_depth is not None else np.zeros(M), np.float32))
+    n = lib().oracle_frustum(ctypes.byref(r), _p(pose), _p(pos), _p(normal), _p(mind), _p(maxd), M,
+                             ctypes.c_float(cos_limit), _p(out["proj_x"]), _p(out["proj_y"]), _p(out["view_cos"]),
+                             _p(out["level"]), _p(out["in_view"]), _p(out["track_depth"]))
+    return out, n
+
+
 # ---- LocalInertialBA ------------------------------------------------------------------------------
 _VP = ctypes.c_void_p
 

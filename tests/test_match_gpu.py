@@ -154,3 +154,49 @@ def test_knn2_matches_oracle_with_ties(oracle, torch_cuda):
     for p in range(P):
         ei, ed = oracle.bf_knn2(q[p, :nq[p]], t[p, :nt[p]])
         assert np.array_equal(ei, i2[p, :nq[p]]) and np.array_equal(ed, d2[p, :nq[p]]), f"pair {p}"
+
+
+def test_frustum_then_search_by_projection_matches_oracle(frames, oracle, torch_cuda):
+    """Frame::isInFrustum on device (bit-exact projections, levels, view cosines, depths) feeding
+    SearchByProjection, against the oracle's isInFrustum -> SearchByProjection on the same 3-D maps."""
+    from openmavis_amd.matcher import isInFrustum, make_rig
+    torch = torch_cuda
+    M = 4000
+    kps, desc, n_kp, _ = host(frames, oracle)
+    cams, R_cl, t_cl = synth.hilti_rig(C)
+    rig = make_rig(cams, R_cl, t_cl, W, H)
+    rng = np.random.default_rng(5)
+    poses = np.stack([synth.random_pose(rng) for _ in range(frames.n_frames)])
+    maps = [synth.make_world_map(kps[f], desc[f], n_kp[f], M, 40 + f, cams, R_cl, t_cl, poses[f], W, H)
+            for f in range(frames.n_frames)]
+    world = {k: torch.from_numpy(np.stack([w[k] for w, _ in maps])).cuda() for k in maps[0][0]}
+    mpb = MapPointBatch(**{k: torch.from_numpy(np.stack([p[k] for _, p in maps])).cuda() for k in maps[0][1]})
+    n_in = torch.zeros(frames.n_frames, dtype=torch.int32, device="cuda")
+    isInFrustum(torch.from_numpy(poses).cuda(), rig, world, mpb, 0.5, n_in)
+    torch.cuda.synchronize()
+    exp_tracks = []
+    for f, (w, p) in enumerate(maps):
+        exp, n = oracle.frustum(rig, poses[f], w["pos"], w["normal"], w["min_dist"], w["max_dist"], 0.5,
+                                p["view_cos"], p["track_depth"])
+        for k in ("in_view", "level"):
+            assert np.array_equal(getattr(mpb, k)[f].cpu().numpy(), exp[k]), (f, k)
+        for k in ("proj_x", "proj_y", "view_cos", "track_depth"):
+            g = getattr(mpb, k)[f].cpu().numpy()
+            assert np.array_equal(g.view(np.uint32), exp[k].view(np.uint32)), (f, k, np.abs(g - exp[k]).max())
+        assert int(n_in[f].item()) == n and n > M // 4
+        exp_tracks.append(dict(p, **exp))
+    m = ORBmatcher(0.8)
+    m.StereoLapping(frames, 0.8)
+    frames.kp_to_mp.fill_(-1)
+    m.SearchByProjection(frames, mpb, 6.0, False, 50.0)
+    torch.cuda.synchronize()
+    got, got_n = frames.kp_to_mp.cpu().numpy(), frames.n_matches.cpu().numpy()
+    l2r, r2l = frames.l2r.cpu().numpy(), frames.r2l.cpu().numpy()
+    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+    for f in range(frames.n_frames):
+        exp = np.full(C * frames.kp_cap, -1, np.int32)
+        n = oracle.search_by_projection(g, kps[f], desc[f], n_kp[f], exp_tracks[f], 6.0, False, 50.0, 0.8, l2r[f],
+                                        r2l[f], None, exp)
+        assert n == got_n[f] and np.array_equal(exp, got[f]), f"frame {f}"
+        assert n > 300
+    frames.kp_to_mp.fill_(-1)

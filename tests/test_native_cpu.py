@@ -65,7 +65,7 @@ def test_sincosf_restatement_matches_libm():
 
 
 def test_atan2f_restatement_matches_libm():
-    """tools/check_atan2f.c carries the same constants/ops as lba.hip::glibc_atan2f (KB8 projection)."""
+    """tools/check_atan2f.c carries the same constants/ops as omv_device.h::glibc_atan2f (KB8 projection)."""
     src = os.path.join(ROOT, "tools", "check_atan2f.c")
     with tempfile.TemporaryDirectory() as d:
         exe = os.path.join(d, "at")

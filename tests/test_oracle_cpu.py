@@ -118,3 +118,30 @@ def test_map_point_generator_is_seeded():
     for k in a:
         assert np.array_equal(a[k], b[k])
     assert (a["in_view"].sum(1) >= 1).all()
+
+
+def test_frustum_oracle_kats(oracle):
+    """Frame::isInFrustum restatement: a point on block 0's optical axis projects to the principal
+    point; the distance-invariance window, the viewing-cosine limit, negative depth and PredictScale's
+    ceil(log(ratio)/log(1.2)) behave as in src/Frame.cc:1529-1653 / src/MapPoint.cc:624-637."""
+    import numpy as np
+    from openmavis_amd import synth
+    from openmavis_amd.matcher import make_rig
+    cams, R_cl, t_cl = synth.hilti_rig(2)
+    rig = make_rig(cams, R_cl, t_cl, 720, 540)
+    I = np.eye(3, dtype=np.float32).reshape(-1)
+    pose = np.concatenate([I, np.zeros(3), I, np.zeros(3)]).astype(np.float32)
+    pos = np.array([[0, 0, 5], [0, 0, 5], [0, 0, 5], [0, 0, -5], [0, 0, 5]], np.float32)
+    normal = np.array([[0, 0, 1], [0, 0, 1], [1, 0, 0], [0, 0, -1], [0, 0, 1]], np.float32)
+    maxd = np.array([5 * 1.2 ** 2 * 0.9, 3.0, 10, 10, 5 * 1.2 ** 9], np.float32)   # #1: 5 > 1.2 * 3
+    mind = maxd / np.float32(1.2 ** 7)
+    mind[4] = 1.0
+    out, n = oracle.frustum(rig, pose, pos, normal, mind, maxd, 0.5)
+    assert out["in_view"][0, 0] == 1 and out["level"][0, 0] == 2
+    assert abs(out["proj_x"][0, 0] - cams[0][2]) < 1e-3 and abs(out["proj_y"][0, 0] - cams[0][3]) < 1e-3
+    assert out["track_depth"][0] == np.float32(5.0)
+    assert out["in_view"][1, 0] == 0 and out["level"][1, 0] == -1 and out["proj_x"][1, 0] == -1   # too far
+    assert out["in_view"][2, 0] == 0                                                             # viewCos 0
+    assert out["in_view"][3].sum() == 0                                                          # behind
+    assert out["level"][4, 0] == 7                                                               # clamped
+    assert n == int((out["in_view"].sum(1) > 0).sum())

@@ -1,5 +1,5 @@
 /* Check that the glibc fdlibm atan2f restatement (same constants and operation order as
- * openmavis_amd/csrc/lba.hip::glibc_atan2f, used by KannalaBrandt8::project) is bit-identical to the
+ * openmavis_amd/csrc/omv_device.h::glibc_atan2f, used by KannalaBrandt8::project) is bit-identical to the
  * host libm.  Random bit patterns + integer / scaled-integer grids; 200M pairs by default (0 mismatches),
  * -DN=... for a shorter run.  gcc -O2 -ffp-contract=off tools/check_atan2f.c -lm && ./a.out */
 #ifndef N
