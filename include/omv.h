@@ -169,6 +169,34 @@ omv_status omv_matcher_stage_ms(omv_matcher *m, double *ms4, int reset);
 omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *nq, const uint8_t *train, int t_cap,
                        const int *nt, int32_t *idx2, int32_t *dist2, void *stream);
 
+/* ORBmatcher::SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, th, bMono)
+ * (src/ORBmatcher.cc:1985-2413, ComputeThreeMaxima :2537-2573): motion-model matching of the last
+ * frame's tracked map points, multi-camera branch, generalised to n_cams blocks (block 1 searched at
+ * Trl * x projected with the LEFT camera model, blocks >= 2 at the left projection — both as in the
+ * reference), rotation-consistency filter when check_ori. */
+typedef struct omv_se3f {          /* Sophus::SE3f: unit quaternion (x, y, z, w) and translation */
+    float q[4];
+    float t[3];
+} omv_se3f;
+
+typedef struct omv_last_frame {    /* device SoA per LastFrame keypoint slot s = cam * last_cap + i */
+    const float *pos;              /* [frame][S][3] mvpMapPoints[s]->GetWorldPos()                  */
+    const uint8_t *desc;           /* [frame][S][32] GetDescriptor()                                */
+    const uint8_t *valid;          /* [frame][S] mvpMapPoints[s] && !mvbOutlier[s]                  */
+    const uint8_t *has_obs;        /* [frame][S] Observations() > 0                                 */
+    const omv_kp *kps;             /* [frame][S] LastFrame keypoint s (octave, angle)               */
+    int S;                         /* slots per last frame (n_cams * last_cap), <= the matcher's max_mps */
+} omv_last_frame;
+
+/* cams: host [n_cams][8] KB8 parameters (block 0 is used for every projection, as the reference);
+ * Tcw / Tlw: device [n_frames] current / last block-0 poses; Trl: host, block 1 from block 0;
+ * kp_to_mp [frame][n_cams*kp_cap] in/out receives last-frame slots; n_matches [frame] (device). */
+omv_status omv_matcher_search_last_frame(omv_matcher *m, int n_frames, const omv_frame_geom *geom, const omv_kp *kps,
+                                         const uint8_t *desc, const int *n_kp, const float *cams, const omv_se3f *Tcw,
+                                         const omv_se3f *Tlw, const omv_se3f *Trl, const omv_last_frame *last, float th,
+                                         int bMono, float mb, int check_ori, const uint8_t *kp_occ_init,
+                                         int32_t *kp_to_mp, int32_t *n_matches, void *stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Frame::isInFrustum (src/Frame.cc:736-826; the multi-camera isInFrustumChecks, :1529-1653) with
  * MapPoint::PredictScale (src/MapPoint.cc:624-637) and KannalaBrandt8::project(Vector3f)

@@ -56,6 +56,16 @@ class Rig(ctypes.Structure):
                 ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int)]
 
 
+class SE3f(ctypes.Structure):
+    """omv_se3f: Sophus::SE3f as unit quaternion (x, y, z, w) + translation."""
+    _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3)]
+
+
+class LastFrame(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+                ("has_obs", ctypes.c_void_p), ("kps", ctypes.c_void_p), ("S", ctypes.c_int)]
+
+
 class MpWorld(ctypes.Structure):
     _fields_ = [("pos", ctypes.c_void_p), ("normal", ctypes.c_void_p), ("min_dist", ctypes.c_void_p),
                 ("max_dist", ctypes.c_void_p)]
@@ -130,6 +140,9 @@ SIGNATURES = {
                                            _VP, _VP]),
     "omv_matcher_stereo_lapping": (_I, [_VP, _I, _VP, _VP, _VP, ctypes.c_double, _VP, _VP, _VP]),
     "omv_bf_knn2": (_I, [_I, _VP, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP]),
+    "omv_matcher_search_last_frame": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _VP, _VP, _VP,
+                                           ctypes.POINTER(SE3f), ctypes.POINTER(LastFrame), _F, _I, _F, _I, _VP, _VP,
+                                           _VP, _VP]),
     "omv_frustum": (_I, [_I, _VP, ctypes.POINTER(Rig), ctypes.POINTER(MpWorld), _I, _F, ctypes.POINTER(MpTrack), _VP,
                          _VP]),
     "omv_lba_create": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(_VP)]),

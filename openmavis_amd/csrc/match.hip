@@ -712,6 +712,309 @@ __global__ void __launch_bounds__(256) frustum_kernel(const omv_frame_pose *pose
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// SearchByProjection(Frame&, const Frame& LastFrame, th, bMono): a candidate pass per (frame, last
+// slot, block) — projection (Sophus quaternion rotation, float KB8) and the 16 best window candidates
+// by (distance, window order) — then one wave per frame resolving slots in order against the claims
+// (a claimed keypoint with observations blocks later points), then the rotation-histogram filter.
+struct LastArgs {
+    const float *pos;
+    const uint8_t *desc, *valid, *has_obs;
+    const omv_kp *kps;
+    int S;
+};
+struct LfGeo {
+    float cam0[8];
+    omv_se3f Trl;
+    float th, mb;
+    int bMono;
+};
+
+__device__ __forceinline__ void cross3f(const float *a, const float *b, float *r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Eigen Quaternion::_transformVector: uv = 2 (q.vec x v); v + w uv + q.vec x uv
+__device__ __forceinline__ void quat_rotate(const float *q, const float *v, float *r) {
+    float uv[3], c[3];
+    cross3f(q, v, uv);
+    for (int i = 0; i < 3; ++i) uv[i] = uv[i] + uv[i];
+    cross3f(q, uv, c);
+    for (int i = 0; i < 3; ++i) r[i] = v[i] + q[3] * uv[i] + c[i];
+}
+__device__ __forceinline__ void se3_apply(const omv_se3f &T, const float *p, float *r) {
+    quat_rotate(T.q, p, r);
+    for (int i = 0; i < 3; ++i) r[i] = r[i] + T.t[i];
+}
+// KannalaBrandt8::project(const Eigen::Vector3f&) (KannalaBrandt8.cpp:48-67)
+__device__ __forceinline__ void kb8_project_f(const float *k, const float *X, float &u, float &v) {
+    const float x2y2 = X[0] * X[0] + X[1] * X[1];
+    const float theta = omv::glibc_atan2f(omv::sqrtf_cr(x2y2), X[2]);
+    const float psi = omv::glibc_atan2f(X[1], X[0]);
+    const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+    u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
+    v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
+}
+
+// Window of last slot s in block c of frame `frame`: false if the point is skipped entirely.
+__device__ bool lf_window(const FrameArgs &f, const LastArgs &L, const LfGeo &G, const omv_se3f &Tcw,
+                          const omv_se3f &Tlw, int frame, int s, int c, float &x, float &y, float &r, int &minL,
+                          int &maxL) {
+    const size_t fs = (size_t)frame * L.S + s;
+    if (!L.valid[fs]) return false;
+    float x3[3];
+    se3_apply(Tcw, L.pos + 3 * fs, x3);
+    const float invzc = (float)(1.0 / (double)x3[2]);
+    if (invzc < 0) return false;
+    float u, v;
+    kb8_project_f(G.cam0, x3, u, v);
+    if (u < f.min_x || u > f.max_x || v < f.min_y || v > f.max_y) return false;
+    x = u, y = v;
+    if (c == 1) {
+        float xr[3];
+        se3_apply(G.Trl, x3, xr);
+        kb8_project_f(G.cam0, xr, x, y);
+    }
+    // bForward / bBackward from tlc = Tlw * twc, twc = -(q^-1 t)
+    const omv_se3f inv{{-Tcw.q[0], -Tcw.q[1], -Tcw.q[2], Tcw.q[3]}, {0, 0, 0}};
+    float twc[3], tlc[3];
+    quat_rotate(inv.q, Tcw.t, twc);
+    for (int i = 0; i < 3; ++i) twc[i] = -twc[i];
+    se3_apply(Tlw, twc, tlc);
+    const bool fwd = tlc[2] > G.mb && !G.bMono, bwd = -tlc[2] > G.mb && !G.bMono;
+    const int oct = L.kps[fs].octave;
+    r = G.th * f.scale[oct];
+    if (fwd) minL = oct, maxL = -1;
+    else if (bwd) minL = 0, maxL = oct;
+    else minL = oct - 1, maxL = oct + 1;
+    return true;
+}
+
+__global__ void __launch_bounds__(256) lf_cand_kernel(FrameArgs f, LastArgs L, LfGeo G, const omv_se3f *Tcw,
+                                                      const omv_se3f *Tlw, int n_frames, const uint8_t *occ_init,
+                                                      Rec *recs, int *counts) {
+    const int C = f.n_cams;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long long)n_frames * L.S * C) return;
+    const int c = (int)(gid % C);
+    const long long fs = gid / C;
+    const int frame = (int)(fs / L.S), s = (int)(fs % L.S);
+    Top t;
+    t.reset();
+    float x, y, r;
+    int minL, maxL;
+    if (lf_window(f, L, G, Tcw[frame], Tlw[frame], frame, s, c, x, y, r, minL, maxL)) {
+        uint64_t dmp[4];
+        load_desc(L.desc + (size_t)fs * 32, dmp);
+        const uint8_t *occ = occ_init ? occ_init + (size_t)frame * C * f.kp_cap : nullptr;
+        scan_window(f, frame, c, x, y, r, minL, maxL, dmp, [&](int slot) { return occ && occ[slot]; }, t);
+    }
+    Rec &out = recs[(size_t)fs * C + c];
+    uint4 *o4 = reinterpret_cast<uint4 *>(&out);
+#pragma unroll
+    for (int v = 0; v < kTop / 4; ++v)
+        o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
+                           4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
+    counts[(size_t)fs * C + c] = t.count;
+}
+
+struct LfResolveArgs {
+    FrameArgs f;
+    LastArgs L;
+    LfGeo G;
+    const omv_se3f *Tcw, *Tlw;
+    const Rec *recs;
+    const int *counts;
+    const uint8_t *occ_init;
+    int32_t *kp_to_mp;
+    int *n_matches;
+    int2 *pushes;   // [frame][S * C] (slot, bin) in claim order
+    int *n_push;
+    int check_ori;
+};
+
+// One wavefront per frame; lanes evaluate 64 consecutive last-frame slots, the longest prefix whose
+// chosen keypoints were not claimed (with observations) by an earlier lane of the batch commits.
+__global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
+    const int frame = blockIdx.x, lane = threadIdx.x;
+    const FrameArgs &f = a.f;
+    const int C = f.n_cams, cap = f.kp_cap, S = C * cap;
+    const int nwords = (S + 31) >> 5;
+    uint32_t *bits = lsm;                                        // blocked slots
+    int *owner = reinterpret_cast<int *>(lsm + nwords);          // first claiming lane (with obs) in a batch
+    int *lastw = owner + S;                                      // last committing writer
+    const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
+    for (int w = lane; w < nwords; w += 64) {
+        uint32_t v = 0;
+        for (int b = 0; b < 32; ++b) {
+            const int s = w * 32 + b;
+            if (s < S && occ && occ[s]) v |= 1u << b;
+        }
+        bits[w] = v;
+    }
+    for (int s = lane; s < S; s += 64) owner[s] = 64, lastw[s] = -1;
+    wave_sync();
+    int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
+    int2 *push = a.pushes + (size_t)frame * a.L.S * C;
+    int total = 0, npush = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int base = 0; base < a.L.S; base += 64) {
+        const int nb = min(64, a.L.S - base);
+        const int s = base + lane;
+        int start = 0;
+        while (start < nb) {
+            const bool active = lane >= start && lane < nb;
+            int claim[kMaxCams], bin[kMaxCams];
+            int nclaim = 0;
+            bool fallback = false, unblock = false;
+            const size_t fs = (size_t)frame * a.L.S + s;
+            const bool obs = active && a.L.has_obs[fs];
+            if (active && a.L.valid[fs]) {
+                for (int c = 0; c < C; ++c) {
+                    const size_t rc = fs * C + c;
+                    const int cnt = a.counts[rc];
+                    int best = -1, bd = 256;
+                    if (cnt > 0) {
+                        const Rec &r = a.recs[rc];
+                        const int avail = min(cnt, kTop);
+                        for (int k = 0; k < avail; ++k) {
+                            const uint32_t v = r.e[k];
+                            if (bit_of(bits, c * cap + rec_idx(v))) continue;
+                            best = rec_idx(v), bd = rec_dist(v);
+                            break;
+                        }
+                        if (best < 0 && cnt > kTop) {   // every kept candidate is claimed: rescan the window
+                            fallback = true;
+                            float x, y, rr;
+                            int minL, maxL;
+                            lf_window(f, a.L, a.G, a.Tcw[frame], a.Tlw[frame], frame, s, c, x, y, rr, minL, maxL);
+                            uint64_t dmp[4];
+                            load_desc(a.L.desc + fs * 32, dmp);
+                            Top t;
+                            scan_window(f, frame, c, x, y, rr, minL, maxL, dmp,
+                                        [&](int slot) { return bit_of(bits, slot); }, t);
+                            if (t.n > 0) best = t.idx(0), bd = t.dist(0);
+                        }
+                    }
+                    if (best >= 0 && bd <= kTH_HIGH) {
+                        const int slot = c * cap + best;
+                        if (!obs && bit_of(bits, slot)) unblock = true;
+                        claim[nclaim] = slot;
+                        float rot = a.L.kps[fs].angle - f.kps[(size_t)frame * S + slot].angle;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int b = (int)roundf(rot * (1.0f / 30));
+                        if (b == 30) b = 0;
+                        bin[nclaim++] = b;
+                    }
+                }
+            }
+            if (obs)
+                for (int q = 0; q < nclaim; ++q) atomicMin(&owner[claim[q]], lane);
+            wave_sync();
+            bool conflict = false;
+            if (active && lane > start) {
+                conflict = fallback;   // a rescan saw the whole window: only safe at the batch head
+                for (int q = 0; q < nclaim && !conflict; ++q) conflict = owner[claim[q]] < lane;
+            }
+            wave_sync();
+            if (obs)
+                for (int q = 0; q < nclaim; ++q) owner[claim[q]] = 64;
+            uint64_t cm = __ballot(conflict);
+            const uint64_t um = __ballot(active && unblock);
+            if (um) {
+                const int u = __ffsll((long long)um) - 1;
+                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));
+            }
+            const int j0 = cm ? min(nb, __ffsll((long long)cm) - 1) : nb;
+            const bool committed = lane >= start && lane < j0;
+            // pushes of committed lanes in lane order
+            int np = committed ? nclaim : 0, incl = np;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += t;
+            }
+            const int ptot = __shfl(incl, 63, 64);
+            if (committed) {
+                for (int q = 0; q < nclaim; ++q) {
+                    atomicMax(&lastw[claim[q]], lane);
+                    if (a.check_ori) push[npush + incl - np + q] = make_int2(claim[q], bin[q]);
+                }
+            }
+            npush += ptot;
+            total += ptot;
+            wave_sync();
+            if (committed)
+                for (int q = 0; q < nclaim; ++q) {
+                    const int slot = claim[q];
+                    if (lastw[slot] != lane) continue;
+                    k2m[slot] = s;
+                    if (obs) atomicOr(&bits[slot >> 5], 1u << (slot & 31));
+                    else atomicAnd(&bits[slot >> 5], ~(1u << (slot & 31)));
+                }
+            wave_sync();
+            if (committed)
+                for (int q = 0; q < nclaim; ++q) lastw[claim[q]] = -1;
+            start = j0;
+            wave_sync();
+            (void)lt;
+        }
+    }
+    if (lane == 0) {
+        a.n_matches[frame] = total;
+        a.n_push[frame] = npush;
+    }
+}
+
+// Rotation consistency (ORBmatcher.cc:2396-2410 + ComputeThreeMaxima): keep the three largest bins
+// (second / third only when >= 10% of the first), undo every claim pushed into another bin.
+__global__ void __launch_bounds__(256) lf_histo_kernel(const int2 *pushes, const int *n_push, int per_frame,
+                                                       int S, int32_t *kp_to_mp, int *n_matches) {
+    __shared__ int hist[30];
+    __shared__ int keep[3];
+    __shared__ int removed;
+    const int frame = blockIdx.x;
+    const int n = n_push[frame];
+    const int2 *p = pushes + (size_t)frame * per_frame;
+    if (threadIdx.x < 30) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) removed = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[p[i].y], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < 30; i++) {
+            const int sz = hist[i];
+            if (sz > max1) {
+                max3 = max2, max2 = max1, max1 = sz, ind3 = ind2, ind2 = ind1, ind1 = i;
+            } else if (sz > max2) {
+                max3 = max2, max2 = sz, ind3 = ind2, ind2 = i;
+            } else if (sz > max3) {
+                max3 = sz, ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+        else if (max3 < 0.1f * (float)max1) ind3 = -1;
+        keep[0] = ind1, keep[1] = ind2, keep[2] = ind3;
+    }
+    __syncthreads();
+    int32_t *k2m = kp_to_mp + (size_t)frame * S;
+    int rm = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int b = p[i].y;
+        if (b != keep[0] && b != keep[1] && b != keep[2]) {
+            k2m[p[i].x] = -1;
+            ++rm;
+        }
+    }
+    atomicAdd(&removed, rm);
+    __syncthreads();
+    if (threadIdx.x == 0) n_matches[frame] -= removed;
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -721,6 +1024,9 @@ struct omv_matcher {
     Rec *d_recs = nullptr;
     int *d_counts = nullptr;
     int *d_flags = nullptr;   // per (frame, point): in_view bits | skip | has_obs (cand -> resolve)
+    int2 *d_push = nullptr;   // SearchByProjection(last frame): (slot, rotation bin) per claim, in order
+    int *d_npush = nullptr;
+    size_t push_cap = 0;
     int32_t *d_knn_i = nullptr, *d_knn_d = nullptr;
     int *d_err = nullptr;
     FrameArgs f{};
@@ -832,7 +1138,8 @@ omv_status omv_matcher_last_error(omv_matcher *h) {
 
 omv_status omv_matcher_destroy(omv_matcher *h) {
     if (!h) return OMV_ERR_ARG;
-    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_flags, h->d_knn_i, h->d_knn_d, h->d_err};
+    void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_flags, h->d_knn_i, h->d_knn_d, h->d_err,
+                 h->d_push, h->d_npush};
     for (void *q : p)
         if (q) (void)hipFree(q);
     delete h;
@@ -896,6 +1203,48 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
         h->ev.push_back({2, {e0, e1}});
         h->ev.push_back({3, {e2, mk_event(st)}});
     }
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_matcher_search_last_frame(omv_matcher *h, int n_frames, const omv_frame_geom *g, const omv_kp *kps,
+                                         const uint8_t *desc, const int *n_kp, const float *cams, const omv_se3f *Tcw,
+                                         const omv_se3f *Tlw, const omv_se3f *Trl, const omv_last_frame *last, float th,
+                                         int bMono, float mb, int check_ori, const uint8_t *kp_occ_init,
+                                         int32_t *kp_to_mp, int32_t *n_matches, void *stream) {
+    if (!h || !g || !kps || !desc || !n_kp || !cams || !Tcw || !Tlw || !last || !kp_to_mp || !n_matches ||
+        n_frames <= 0 || n_frames > h->max_frames || g->n_cams != h->n_cams || last->S < 0 || last->S > h->max_mps ||
+        (h->n_cams > 1 && !Trl))
+        return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    FrameArgs f;
+    fill_frame(h, g, kps, desc, n_kp, f);
+    LastArgs L{last->pos, last->desc, last->valid, last->has_obs, last->kps, last->S};
+    LfGeo G{};
+    for (int q = 0; q < 8; ++q) G.cam0[q] = cams[q];
+    if (Trl) G.Trl = *Trl;
+    G.th = th, G.mb = mb, G.bMono = bMono;
+    const int C = h->n_cams;
+    const size_t per_frame = (size_t)std::max(1, last->S) * C;
+    if (h->push_cap < per_frame * n_frames) {
+        if (h->d_push) (void)hipFree(h->d_push);
+        if (h->d_npush) (void)hipFree(h->d_npush);
+        HIP_OK(hipMalloc(&h->d_push, sizeof(int2) * per_frame * n_frames));
+        HIP_OK(hipMalloc(&h->d_npush, sizeof(int) * h->max_frames));
+        h->push_cap = per_frame * n_frames;
+    }
+    if (last->S > 0) {
+        const long long tot = (long long)n_frames * last->S * C;
+        lf_cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, L, G, Tcw, Tlw, n_frames, kp_occ_init, h->d_recs,
+                                                                 h->d_counts);
+    }
+    LfResolveArgs ra{f, L, G, Tcw, Tlw, h->d_recs, h->d_counts, kp_occ_init, kp_to_mp, n_matches, h->d_push, h->d_npush,
+                     check_ori};
+    const int S = C * h->kp_cap;
+    const size_t lds = sizeof(uint32_t) * ((S + 31) / 32) + 2 * sizeof(int) * S;
+    lf_resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
+    if (check_ori) lf_histo_kernel<<<n_frames, 256, 0, st>>>(h->d_push, h->d_npush, (int)per_frame, S, kp_to_mp, n_matches);
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }

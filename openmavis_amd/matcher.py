@@ -128,6 +128,33 @@ class ORBmatcher:
         _lib.check(self._lib.omv_matcher_grid_debug(self._h, frame, cam, _lib.ptr(cs), _lib.ptr(idx)))
         return cs, idx[:cs[-1]]
 
+    def SearchByProjectionLastFrame(self, frames, last, Tcw, Tlw, cams, Trl, th, bMono=False, mb=0.0, stream=None):
+        """ORBmatcher::SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, th, bMono)
+        (src/ORBmatcher.cc:1985-2413): the last frames' tracked points (`last`: dict of device tensors
+        pos [F, S, 3], desc [F, S, 32], valid / has_obs [F, S] uint8, kps [F, S, 6] (omv_kp rows)) are
+        projected with the current poses Tcw and matched into frames.kp_to_mp (last-frame slots).
+        Tcw / Tlw: device float32 [F, 7] (qx qy qz qw tx ty tz); cams: [C][8]; Trl: 7 floats.
+        Returns the per-frame match counts (device tensor)."""
+        h = self._handle(frames, last["pos"].shape[1])
+        self.AssignFeaturesToGrid(frames, stream)
+        S = last["pos"].shape[1]
+        lf = _lib.LastFrame(_lib.ptr(last["pos"]), _lib.ptr(last["desc"]), _lib.ptr(last["valid"]),
+                            _lib.ptr(last["has_obs"]), _lib.ptr(last["kps"]), S)
+        c = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(-1, 8)[:frames.n_cams])
+        trl = _lib.SE3f()
+        t7 = np.asarray(Trl, np.float32).reshape(7)
+        for q in range(4):
+            trl.q[q] = float(t7[q])
+        for q in range(3):
+            trl.t[q] = float(t7[4 + q])
+        _lib.check(self._lib.omv_matcher_search_last_frame(
+            h, frames.n_frames, ctypes.byref(frames.geom), _lib.ptr(frames.kps), _lib.ptr(frames.desc),
+            _lib.ptr(frames.n_kp), _lib.ptr(c), _lib.ptr(Tcw), _lib.ptr(Tlw), ctypes.byref(trl), ctypes.byref(lf),
+            ctypes.c_float(th), int(bool(bMono)), ctypes.c_float(mb), int(self.mbCheckOrientation),
+            _lib.ptr(frames.occ_init), _lib.ptr(frames.kp_to_mp), _lib.ptr(frames.n_matches), self._stream(stream)),
+            "omv_matcher_search_last_frame")
+        return frames.n_matches
+
     def StereoLapping(self, frames, ratio=0.8, stream=None):
         """Lowe-ratio knn candidates of ComputeMultiFishEyeMatches (before triangulation)."""
         h = self._handle(frames)

@@ -194,3 +194,50 @@ def make_world_map(kps, desc, n_kp, M, seed, cams, R_cl, t_cl, pose, width, heig
         is_bad=(rng.random(M) < 0.02).astype(np.uint8), has_obs=(rng.random(M) > 0.03).astype(np.uint8))
     mp["desc"][true] = flip_bits(desc[cam[true], kidx[true]], rng)
     return world, mp
+
+
+def quat_from_R(R):
+    """Unit quaternion (x, y, z, w) of a rotation matrix (float64)."""
+    R = np.asarray(R, np.float64)
+    w = np.sqrt(max(0.0, 1 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    x = np.copysign(np.sqrt(max(0.0, 1 + R[0, 0] - R[1, 1] - R[2, 2])) / 2, R[2, 1] - R[1, 2])
+    y = np.copysign(np.sqrt(max(0.0, 1 - R[0, 0] + R[1, 1] - R[2, 2])) / 2, R[0, 2] - R[2, 0])
+    z = np.copysign(np.sqrt(max(0.0, 1 - R[0, 0] - R[1, 1] + R[2, 2])) / 2, R[1, 0] - R[0, 1])
+    q = np.array([x, y, z, w])
+    return q / np.linalg.norm(q)
+
+
+def make_last_frame(kps, desc, n_kp, seed, cams, Tcw7, frac_valid=0.7, rand_angle=0.2):
+    """LastFrame for SearchByProjection(Frame&, const Frame&): the current frame's keypoints as the last
+    frame's tracked points (unprojected through block 0's camera at depth U(2, 20) and moved to world
+    with Tcw), descriptors with U{0..8} bit flips, `frac_valid` valid, angles perturbed (a `rand_angle`
+    share at random) so the rotation histogram rejects some.  Returns numpy SoA of omv_last_frame."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    C, cap = kps.shape[0], kps.shape[1]
+    S = C * cap
+    flat = kps.reshape(-1)
+    ar = np.arange(S)
+    exists = (ar % cap) < np.repeat(np.asarray(n_kp), cap)
+    valid = exists & (rng.random(S) < frac_valid)
+    ray = kb8_unproject(cams[0], flat["x"], flat["y"])
+    Xc = ray * rng.uniform(2.0, 20.0, S)[:, None]
+    q = np.asarray(Tcw7[:4], np.float64)
+    t = np.asarray(Tcw7[4:], np.float64)
+    x, y, z, w = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    Xw = (Xc - t) @ R   # R^T (Xc - t)
+    lk = flat.copy()
+    ang = lk["angle"] + rng.normal(0, 3.0, S)
+    rnd = rng.random(S) < rand_angle
+    ang = np.where(rnd, rng.uniform(0, 360, S), ang) % 360.0
+    lk["angle"] = ang.astype(np.float32)
+    d = desc.reshape(S, 32)
+    return dict(pos=Xw.astype(np.float32), desc=flip_bits(d, rng), valid=valid.astype(np.uint8),
+                has_obs=(rng.random(S) > 0.05).astype(np.uint8), kps=lk)
+
+
+def random_se3(rng, scale=5.0):
+    R = random_pose(rng)[:9].reshape(3, 3).astype(np.float64)
+    return np.concatenate([quat_from_R(R), rng.uniform(-scale, scale, 3)]).astype(np.float32)

@@ -10,6 +10,8 @@
 //   Frame::isInFrustum / isInFrustumChecks           src/Frame.cc:736-826, :1529-1653 (multi-camera branch)
 //     + MapPoint::PredictScale                       src/MapPoint.cc:624-637
 //     + KannalaBrandt8::project(Eigen::Vector3f)     src/CameraModels/KannalaBrandt8.cpp:48-67
+//   ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
+//                                                    src/ORBmatcher.cc:1985-2413 (+ ComputeThreeMaxima :2537-2573)
 //   cv::BFMatcher(NORM_HAMMING).knnMatch(k = 2)      as called by Frame::ComputeMultiFishEyeMatches,
 //                                                    src/Frame.cc:1483 (OpenCV batchDistance K = 2:
 //                                                    strict '<' insertion, first train index wins ties)
@@ -241,6 +243,133 @@ void oracle_bf_knn2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t 
 
 int oracle_descriptor_distance(const uint8_t *a, const uint8_t *b) { return descriptor_distance(a, b); }
 
+// ---- ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono) (multi-camera) ----------
+// Sophus::SE3f * p = q._transformVector(p) + t with Eigen's formula uv = 2 (q.vec x p),
+// p + w uv + q.vec x uv (Quaternion.h), in float without contraction.
+struct SE3F {
+    float q[4];   // x y z w
+    float t[3];
+};
+static void cross3f(const float *a, const float *b, float *r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = a[2] * b[0] - a[0] * b[2];
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+static void quat_rotate(const float *q, const float *v, float *r) {
+    float uv[3], c[3];
+    cross3f(q, v, uv);
+    for (int i = 0; i < 3; ++i) uv[i] = uv[i] + uv[i];
+    cross3f(q, uv, c);
+    for (int i = 0; i < 3; ++i) r[i] = v[i] + q[3] * uv[i] + c[i];
+}
+static void se3_apply(const SE3F &T, const float *p, float *r) {
+    quat_rotate(T.q, p, r);
+    for (int i = 0; i < 3; ++i) r[i] = r[i] + T.t[i];
+}
+static void kb8_project_f(const float *k, const float *X, float &u, float &v);
+
+}  // extern "C"
+
+extern "C" {
+
+// cur_*: the current frame (kps/desc [C][kp_cap], n_kp [C]), its pose Tcw, the rig (R_cl/t_cl unused here:
+// Trl is passed as SE3), last_*: per LastFrame keypoint slot s = cam * last_cap + i: the tracked map point's
+// world position / descriptor / Observations() > 0, validity (mvpMapPoints[s] && !mvbOutlier[s]) and the
+// keypoint itself (octave, angle).  kp_to_mp [C * kp_cap] in/out receives last-frame slots.
+int oracle_search_last_frame(const FrameGeom *g, const KP *kps, const uint8_t *desc, int kp_cap, const int *n_kp,
+                             const float *cams /* [C][8] */, const SE3F *Tcw, const SE3F *Tlw, const SE3F *Trl,
+                             const float *last_pos, const uint8_t *last_desc, const uint8_t *last_valid,
+                             const uint8_t *last_obs, const KP *last_kps, int S_last, float th, int bMono, float mb,
+                             int check_ori, const uint8_t *occ_init, int32_t *kp_to_mp) {
+    View v{g, 0, 0, {}, kps, kp_cap, n_kp};
+    build_grids(v);
+    const int C = g->n_cams;
+    const int HISTO_LENGTH = 30;
+    const float factor = 1.0f / HISTO_LENGTH;
+    std::vector<std::vector<int>> rotHist(HISTO_LENGTH);
+    std::vector<uint8_t> blocked(occ_init, occ_init + (size_t)C * kp_cap);
+    // twc = Tcw.inverse().translation() = -(q^-1 * t); tlc = Tlw * twc
+    SE3F inv{{-Tcw->q[0], -Tcw->q[1], -Tcw->q[2], Tcw->q[3]}, {0, 0, 0}};
+    float twc[3], tlc[3];
+    quat_rotate(inv.q, Tcw->t, twc);
+    for (int i = 0; i < 3; ++i) twc[i] = -twc[i];
+    se3_apply(*Tlw, twc, tlc);
+    const bool bForward = tlc[2] > mb && !bMono;
+    const bool bBackward = -tlc[2] > mb && !bMono;
+    int nmatches = 0;
+    for (int s = 0; s < S_last; ++s) {
+        if (!last_valid[s]) continue;
+        float x3Dc[3];
+        se3_apply(*Tcw, last_pos + 3 * (size_t)s, x3Dc);
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        if (invzc < 0) continue;
+        float u, vv;
+        kb8_project_f(cams, x3Dc, u, vv);
+        if (u < g->min_x || u > g->max_x) continue;
+        if (vv < g->min_y || vv > g->max_y) continue;
+        const int oct = last_kps[s].octave;
+        const float radius = th * g->scale_factors[oct];
+        const uint8_t *dmp = last_desc + (size_t)s * 32;
+        auto window = [&](float x, float y, int cam) {
+            if (bForward) return features_in_area(v, x, y, radius, oct, -1, cam);
+            if (bBackward) return features_in_area(v, x, y, radius, 0, oct, cam);
+            return features_in_area(v, x, y, radius, oct - 1, oct + 1, cam);
+        };
+        auto search = [&](float x, float y, int cam) {
+            int bestDist = 256, bestIdx = -1;
+            for (int i2 : window(x, y, cam)) {
+                const int slot = cam * kp_cap + i2;
+                if (blocked[slot]) continue;
+                const int dist = descriptor_distance(dmp, desc + (size_t)slot * 32);
+                if (dist < bestDist) bestDist = dist, bestIdx = i2;
+            }
+            if (bestDist <= TH_HIGH) {
+                const int slot = cam * kp_cap + bestIdx;
+                kp_to_mp[slot] = s;
+                blocked[slot] = last_obs[s] ? 1 : 0;
+                nmatches++;
+                if (check_ori) {
+                    float rot = last_kps[s].angle - kps[slot].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)std::round(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    rotHist[bin].push_back(slot);
+                }
+            }
+        };
+        search(u, vv, 0);
+        if (C > 1) {   // right block: Trl * x3Dc projected with the LEFT camera model, no bounds check
+            float x3Dr[3], ur, vr;
+            se3_apply(*Trl, x3Dc, x3Dr);
+            kb8_project_f(cams, x3Dr, ur, vr);
+            search(ur, vr, 1);
+        }
+        for (int cam = 2; cam < C; ++cam) search(u, vv, cam);   // side blocks search at the LEFT projection
+    }
+    if (check_ori) {   // ComputeThreeMaxima + removal of every push outside the three top bins
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int sz = (int)rotHist[i].size();
+            if (sz > max1) {
+                max3 = max2, max2 = max1, max1 = sz, ind3 = ind2, ind2 = ind1, ind1 = i;
+            } else if (sz > max2) {
+                max3 = max2, max2 = sz, ind3 = ind2, ind2 = i;
+            } else if (sz > max3) {
+                max3 = sz, ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+        else if (max3 < 0.1f * (float)max1) ind3 = -1;
+        for (int i = 0; i < HISTO_LENGTH; i++)
+            if (i != ind1 && i != ind2 && i != ind3)
+                for (int slot : rotHist[i]) kp_to_mp[slot] = -1, nmatches--;
+    }
+    return nmatches;
+}
+
+}  // extern "C"
+
+extern "C" {
 // ---- Frame::isInFrustum, multi-camera branch (one frame) ----------------------------------------------
 // Float arithmetic in Eigen's evaluation order without contraction: 3x3 products and dot products sum
 // left to right, norm() = sqrt((x*x + y*y) + z*z).  KannalaBrandt8.cpp and MapPoint.cc have no

@@ -205,6 +205,38 @@ def frustum(rig, pose, pos, normal, min_dist, max_dist, cos_limit=0.5, view_cos=
     return out, n
 
 
+class SE3F(ctypes.Structure):
+    _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3)]
+
+
+def _se3(v):
+    v = np.asarray(v, np.float32).reshape(7)
+    return SE3F((ctypes.c_float * 4)(*v[:4].tolist()), (ctypes.c_float * 3)(*v[4:].tolist()))
+
+
+def search_last_frame(geom, kps, desc, n_kp, cams, Tcw, Tlw, Trl, last_pos, last_desc, last_valid, last_obs,
+                      last_kps, th, bMono, mb, check_ori, occ_init, kp_to_mp):
+    """ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) restated for one frame.
+    kp_to_mp is modified in place (last-frame slots); returns nmatches."""
+    C, cap = kps.shape[0], kps.shape[1]
+    kps = np.ascontiguousarray(kps)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    n_kp = np.ascontiguousarray(n_kp, np.int32)
+    cams = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(-1, 8))
+    S = len(last_valid)
+    lp = np.ascontiguousarray(last_pos, np.float32)
+    ld = np.ascontiguousarray(last_desc, np.uint8)
+    lv = np.ascontiguousarray(last_valid, np.uint8)
+    lo = np.ascontiguousarray(last_obs, np.uint8)
+    lk = np.ascontiguousarray(last_kps)
+    occ = np.ascontiguousarray(occ_init if occ_init is not None else np.zeros(C * cap), np.uint8)
+    t1, t2, t3 = _se3(Tcw), _se3(Tlw), _se3(Trl)
+    return lib().oracle_search_last_frame(ctypes.byref(geom), _p(kps), _p(desc), cap, _p(n_kp), _p(cams),
+                                          ctypes.byref(t1), ctypes.byref(t2), ctypes.byref(t3), _p(lp), _p(ld), _p(lv),
+                                          _p(lo), _p(lk), S, ctypes.c_float(th), int(bMono), ctypes.c_float(mb),
+                                          int(check_ori), _p(occ), _p(kp_to_mp))
+
+
 # ---- LocalInertialBA ------------------------------------------------------------------------------
 _VP = ctypes.c_void_p
 

@@ -200,3 +200,44 @@ def test_frustum_then_search_by_projection_matches_oracle(frames, oracle, torch_
         assert n == got_n[f] and np.array_equal(exp, got[f]), f"frame {f}"
         assert n > 300
     frames.kp_to_mp.fill_(-1)
+
+
+@pytest.mark.parametrize("motion,check_ori", [("none", True), ("forward", True), ("backward", False)])
+def test_search_by_projection_last_frame_matches_oracle(frames, oracle, torch_cuda, motion, check_ori):
+    """SearchByProjection(Frame&, const Frame& LastFrame, th, bMono) on device vs the oracle: assignments
+    (last-frame slots), counts, the rotation-histogram removals; forward / backward / neither window."""
+    torch = torch_cuda
+    kps, desc, n_kp, _ = host(frames, oracle)
+    cams, R_cl, t_cl = synth.hilti_rig(C)
+    rng = np.random.default_rng({"none": 1, "forward": 2, "backward": 3}[motion])
+    F, cap = frames.n_frames, frames.kp_cap
+    Tcw = np.stack([synth.random_se3(rng) for _ in range(F)])
+    lasts = [synth.make_last_frame(kps[f], desc[f], n_kp[f], 90 + f, cams, Tcw[f]) for f in range(F)]
+    # last pose: the current one moved along the optical axis (tlc.z vs mb decides the level window)
+    dz = {"none": 0.0, "forward": 0.5, "backward": -0.5}[motion]
+    Tlw = Tcw.copy()
+    Tlw[:, 6] -= np.float32(dz)
+    Trl_R = R_cl[1].astype(np.float64)
+    Trl = np.concatenate([synth.quat_from_R(Trl_R), t_cl[1]]).astype(np.float32)
+    mb = 0.11
+    last = {k: torch.from_numpy(np.stack([l[k] for l in lasts])).cuda() for k in ("pos", "desc", "valid", "has_obs")}
+    last["kps"] = torch.from_numpy(np.stack([l["kps"].view(np.int32).reshape(-1, 6) for l in lasts])).cuda()
+    occ = (rng.random((F, C * cap)) < 0.03).astype(np.uint8)
+    frames.occ_init = torch.from_numpy(occ).cuda()
+    frames.kp_to_mp.fill_(-1)
+    m = ORBmatcher(0.9, checkOri=check_ori)
+    m.SearchByProjectionLastFrame(frames, last, torch.from_numpy(Tcw).cuda(), torch.from_numpy(Tlw).cuda(), cams, Trl,
+                                  th=7.0, bMono=False, mb=mb)
+    torch.cuda.synchronize()
+    got, got_n = frames.kp_to_mp.cpu().numpy(), frames.n_matches.cpu().numpy()
+    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+    for f in range(F):
+        exp = np.full(C * cap, -1, np.int32)
+        n = oracle.search_last_frame(g, kps[f], desc[f], n_kp[f], cams, Tcw[f], Tlw[f], Trl, lasts[f]["pos"],
+                                     lasts[f]["desc"], lasts[f]["valid"], lasts[f]["has_obs"], lasts[f]["kps"], 7.0,
+                                     False, mb, check_ori, occ[f], exp)
+        bad = np.nonzero(exp != got[f])[0]
+        assert n == got_n[f] and bad.size == 0, (f, n, int(got_n[f]), bad[:8])
+        assert n > 200
+    frames.occ_init = None
+    frames.kp_to_mp.fill_(-1)
