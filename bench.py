@@ -193,7 +193,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=64, help="multi-cam frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=256, help="multi-cam frames per step per GPU")
     ap.add_argument("--streams", type=int, default=2,
                     help="frame groups per GPU, each on its own HIP stream (latency-bound matcher stages of one "
                          "group overlap extraction of another)")
