@@ -136,15 +136,21 @@ def lba_cpu_baseline(prob, runs=8):
                        f"oracle C++ restatement, 1 thread, {dt:.1f} s")
 
 
-def lba_leg(prob, steps, warmup, dev, world):
+def lba_leg(prob, steps, warmup, dev, world, shard=False):
     """LocalBA iters/s: one iteration = one LM trial (error eval + build + Schur + factor/solve + update
     + chi2).  Each step is one full optimize() of the window from its uploaded state (reset is a
-    device copy outside the timed region); the state read-back and the outlier test are inside."""
+    device copy outside the timed region); the state read-back and the outlier test are inside.
+    world > 1: window replicas (weak scaling), or with shard=True ONE window with its landmarks
+    sharded over the ranks and one RCCL all-reduce of the partial Schur system per trial (strong)."""
     import torch
-    from openmavis_amd.dist import job_seconds
+    from openmavis_amd.dist import LbaAllReduce, job_seconds
     from openmavis_amd.optimizer import LocalInertialBA
+    shard = shard and world > 1
+    comm = {}
+    if shard:
+        comm = dict(rank=torch.distributed.get_rank(), world=world, allreduce=LbaAllReduce("device", device=dev))
     ba = LocalInertialBA(max_kf=prob["n_kf"], max_cams=prob["n_cams"], max_pts=len(prob["pts"]),
-                         max_mono=len(prob["mono_pt"]), max_imu=len(prob["imu_kf1"]))
+                         max_mono=len(prob["mono_pt"]), max_imu=len(prob["imu_kf1"]), **comm)
     t_set = time.perf_counter()
     ba.set_problem(prob)
     t_set = time.perf_counter() - t_set
@@ -170,7 +176,7 @@ def lba_leg(prob, steps, warmup, dev, world):
     stages = {k: round(v / trials, 4) for k, v in st_sum.items() if k != "trials"}
     return {
         "metric": "LocalBA iters/sec (LM trials/s)",
-        "value": round(trials * world / dt, 2),
+        "value": round(trials * (1 if shard else world) / dt, 2),
         "unit": "LM trials/s",
         "ms_per_trial": round(trial_ms, 4),
         "ms_per_optimize": round(dt / steps * 1e3, 3),
@@ -180,7 +186,8 @@ def lba_leg(prob, steps, warmup, dev, world):
         "stage_ms_per_trial": stages,
         "config": {"workload": "LocalInertialBA 50 KFs (25 opt + 25 fixed) x 20k MapPoints x 5 cams, "
                                f"{len(prob['mono_pt'])} EdgeMono + {len(prob['imu_kf1'])} inertial, bLarge",
-                   "parallelism": f"window-replicas x{world}"},
+                   "parallelism": f"landmark-sharded x{world}" if shard else f"window-replicas x{world}"},
+        "scaling": "strong" if shard else "weak",
         "dtype": "f64",
         "roofline": {"kernel": "whole LM trial", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
@@ -201,6 +208,9 @@ def main():
     ap.add_argument("--stage-timing", type=int, default=1)
     ap.add_argument("--lba-steps", type=int, default=10, help="LocalInertialBA optimize() calls timed (0: skip)")
     ap.add_argument("--lba-warmup", type=int, default=2)
+    ap.add_argument("--lba-shard", action="store_true",
+                    help="N>1: shard one window's landmarks over the ranks (RCCL all-reduce per LM trial) "
+                         "instead of running a window replica per rank")
     ap.add_argument("--cpu-frames", type=int, default=120, help="frames in the CPU-baseline sample (~6 s)")
     ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
     args = ap.parse_args()
@@ -328,7 +338,7 @@ def main():
                 stages[k] = stages.get(k, 0.0) + v / args.steps
             stages["frustum"] = stages.get("frustum", 0.0) + sum(a.elapsed_time(b) for a, b in gr["ev"]) / args.steps
 
-    lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world) if lba_prob is not None else None
+    lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world, args.lba_shard) if lba_prob is not None else None
 
     if rank != 0:
         if world > 1:

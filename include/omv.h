@@ -315,6 +315,24 @@ omv_status omv_lba_reset(omv_lba *h);
  * 3 back-substitution+update+errors; plus the number of trials. */
 omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials);
 
+/* Landmark sharding across ranks: one exchange per LM trial.
+ * Call before omv_lba_set_problem.  Every rank then passes the SAME full problem; the handle keeps
+ * the rank's contiguous share of the landmarks (in its landmark order) with their edges, and rank 0
+ * alone evaluates the inertial / random-walk edges, adds lambda to the pose diagonal and the pose
+ * part of computeScale.  Per trial the handle calls
+ *     allreduce(ctx, buf, count, stream)   — in-place SUM of `count` doubles of device memory,
+ * once on the partial Schur system [packed blocks | b | coef] and once on [chi2, scale] (the
+ * initial / per-iteration chi2 too).  The call must be enqueued on (or ordered after) `stream`;
+ * it returns 0 on success.  ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream)
+ * is exactly that.  Every rank solves the identical reduced system; after omv_lba_optimize each
+ * rank has written its own landmarks / edges (chi2, outlier) and all keyframes; err / err_end are
+ * global.  world == 1 (the default) is the single-GPU path with no calls. */
+typedef int (*omv_allreduce_fn)(void *ctx, double *buf, size_t count, void *stream);
+omv_status omv_lba_set_comm(omv_lba *h, int rank, int world, omv_allreduce_fn allreduce, void *ctx);
+/* Landmarks / visual edges this rank owns after set_problem, and (optional, [n_pts]) the caller
+ * indices of its landmarks.  Any pointer may be NULL. */
+omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *pt_index);
+
 #ifdef __cplusplus
 }
 #endif

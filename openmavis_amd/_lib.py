@@ -117,6 +117,8 @@ except ImportError:  # pragma: no cover
 
 # Every symbol include/omv.h declares: (name, restype, argtypes)
 _VP, _I, _F, _SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+# omv_allreduce_fn: int (*)(void *ctx, double *buf, size_t count, void *stream)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 SIGNATURES = {
     "omv_orb_create": (_I, [ctypes.POINTER(OrbParams), _I, _I, _I, ctypes.POINTER(_VP)]),
     "omv_orb_destroy": (_I, [_VP]),
@@ -152,6 +154,8 @@ SIGNATURES = {
     "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
     "omv_lba_reset": (_I, [_VP]),
+    "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),
+    "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
 }
 
 _lib = None

@@ -1046,8 +1046,8 @@ __device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:8
 }
 
 // ImuCamPose::Update (G2oTypes.cc:211-235) + vertex adds; the pose part of computeScale.
-__global__ void update_kf_kernel(Rig rig, Red R, const int *offV, const int *offG, const int *offA, int n_opt, double lambda,
-                                 const double *xp, State a, State bst, double *scale_partial) {
+__global__ void update_kf_kernel(Rig rig, Red R, const double *b, const int *offV, const int *offG, const int *offA,
+                                 int n_opt, double lambda, const double *xp, State a, State bst, double *scale_partial) {
     __shared__ double sh[8];
     const int C = rig.n_cams;
     for (int k = threadIdx.x; k < n_opt; k += blockDim.x) {
@@ -1080,7 +1080,7 @@ __global__ void update_kf_kernel(Rig rig, Red R, const int *offV, const int *off
     }
     // pose part of sum_j x_j (lambda x_j + b_j)
     double sc = 0;
-    for (int q = threadIdx.x; q < R.n; q += blockDim.x) sc += xp[q] * (lambda * xp[q] + R.b[q]);
+    for (int q = threadIdx.x; q < R.n; q += blockDim.x) sc += xp[q] * (lambda * xp[q] + b[q]);
     const double tt = block_reduce_sum(sc, sh);
     if (threadIdx.x == 0) scale_partial[0] = tt;
 }
@@ -1196,6 +1196,12 @@ struct omv_lba {
     double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
     double *d_S = nullptr, *d_coef = nullptr, *d_x = nullptr, *d_scratch = nullptr;
     int *d_fail = nullptr;
+    double *d_bb = nullptr;    // the trial's copy of b (all-reduced with the packed system when sharded)
+    size_t n_reduce = 0;
+    int rank = 0, world = 1;   // landmark sharding (omv_lba_set_comm)
+    omv_allreduce_fn allreduce = nullptr;
+    void *ar_ctx = nullptr;
+    bool imu_here = false;     // this rank evaluates the inertial edges (rank 0)
     size_t ldlt_lds = 0;
     int use_lds = 0;
     bool lds_ok = false;
@@ -1252,12 +1258,13 @@ omv_status omv_lba_destroy(omv_lba *h) {
 
 omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     if (!h || !p) return OMV_ERR_ARG;
-    if (p->n_cams <= 0 || p->n_cams > h->max_cams || p->n_kf > h->max_kf || p->n_pts > h->max_pts ||
-        p->n_mono > h->max_mono || p->n_imu > h->max_imu || p->n_opt > p->n_kf || p->n_opt < 1)
+    if (p->n_cams <= 0 || p->n_cams > h->max_cams || p->n_kf > h->max_kf || p->n_pts < 0 || p->n_mono < 0 ||
+        p->n_imu > h->max_imu || p->n_opt > p->n_kf || p->n_opt < 1)
         return OMV_ERR_ARG;
     free_problem(h);
-    const int C = p->n_cams, K = p->n_kf, P = p->n_pts, E = p->n_mono, NI = p->n_imu;
-    h->n_kf = K, h->n_opt = p->n_opt, h->n_pts = P, h->n_mono = E, h->n_imu = NI;
+    const int C = p->n_cams, K = p->n_kf, P_all = p->n_pts, E_all = p->n_mono, NI = p->n_imu;
+    h->n_kf = K, h->n_opt = p->n_opt, h->n_imu = NI;
+    h->imu_here = NI > 0 && h->rank == 0;
     // rig
     Rig &rig = h->rig;
     rig.n_cams = C;
@@ -1276,19 +1283,40 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     }
     h->n_red = nred;
     // landmark order: by the first optimisable keyframe observing them (workgroup keyframe spans stay small)
-    std::vector<std::vector<int>> pe(P);
-    for (int e = 0; e < E; ++e) {
-        if (p->mono_pt[e] < 0 || p->mono_pt[e] >= P || p->mono_kf[e] < 0 || p->mono_kf[e] >= K ||
+    std::vector<std::vector<int>> pe(P_all);
+    for (int e = 0; e < E_all; ++e) {
+        if (p->mono_pt[e] < 0 || p->mono_pt[e] >= P_all || p->mono_kf[e] < 0 || p->mono_kf[e] >= K ||
             p->mono_cam[e] < 0 || p->mono_cam[e] >= C)
             return OMV_ERR_ARG;
         pe[p->mono_pt[e]].push_back(e);
     }
-    std::vector<int> key(P, 1 << 30);
-    for (int q = 0; q < P; ++q)
+    std::vector<int> key(P_all, 1 << 30);
+    for (int q = 0; q < P_all; ++q)
         for (int e : pe[q]) key[q] = std::min(key[q], p->mono_kf[e] < p->n_opt ? p->mono_kf[e] : (1 << 29) + p->mono_kf[e]);
-    std::vector<int> order(P);
+    std::vector<int> order(P_all);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
+    // block pattern of the reduced system (keyframe blocks) from ALL landmarks: every rank of a
+    // sharded solve lays out the identical packed system
+    const int nb = p->n_opt;
+    std::vector<uint8_t> pat((size_t)nb * nb, 0);
+    for (int k = 0; k < nb; ++k) pat[k * nb + k] = 1;
+    for (int q = 0; q < P_all; ++q)
+        for (int a : pe[q])
+            for (int b : pe[q]) {
+                const int i = p->mono_kf[a], j = p->mono_kf[b];
+                if (i < nb && j < nb && j <= i) pat[i * nb + j] = 1;
+            }
+    // this rank's landmarks: a contiguous share of the landmark order
+    if (h->world > 1) {
+        const size_t lo = (size_t)P_all * h->rank / h->world, hi = (size_t)P_all * (h->rank + 1) / h->world;
+        order = std::vector<int>(order.begin() + lo, order.begin() + hi);
+    }
+    const int P = (int)order.size();
+    int E = 0;
+    for (int q : order) E += (int)pe[q].size();
+    if (P > h->max_pts || E > h->max_mono) return OMV_ERR_ARG;
+    h->n_pts = P, h->n_mono = E;
     h->perm_pt = order;
     std::vector<int> e_pt, e_kf, e_cam, e_slot, pt_edge(P + 1, 0), pt_slot(P + 1, 0), slot_kf;
     std::vector<double> e_obs;
@@ -1322,16 +1350,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
                 if (slot_kf[s] < p->n_opt) lo = std::min(lo, slot_kf[s]), hi = std::max(hi, slot_kf[s]);
         wg_kf0[g] = (hi >= 0 && hi - lo < kSpan) ? lo : (hi < 0 ? 0 : -1);
     }
-    // block pattern of the reduced system (keyframe blocks) + symbolic LDL^T fill-in
-    const int nb = p->n_opt;
-    std::vector<uint8_t> pat((size_t)nb * nb, 0);
-    for (int k = 0; k < nb; ++k) pat[k * nb + k] = 1;
-    for (int q = 0; q < P; ++q)
-        for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
-            for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
-                const int i = slot_kf[a], j = slot_kf[b];
-                if (i < nb && j < nb && j <= i) pat[i * nb + j] = 1;
-            }
+    // inertial blocks + symbolic LDL^T fill-in
     for (int i = 0; i < NI; ++i) {
         if (p->imu_kf1[i] < 0 || p->imu_kf1[i] >= K || p->imu_kf2[i] < 0 || p->imu_kf2[i] >= K ||
             p->imu_kf1[i] == p->imu_kf2[i])
@@ -1499,8 +1518,11 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_imu_partial = dalloc<double>(ow, 1);
     h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
     h->d_out = dalloc<double>(ow, 4);
-    h->d_S = dalloc<double>(ow, (size_t)n_slots * 256);
-    h->d_coef = dalloc<double>(ow, nred);
+    // [packed blocks | b | coef]: contiguous, the one buffer a sharded solve all-reduces per trial
+    h->d_S = dalloc<double>(ow, (size_t)n_slots * 256 + 2 * (size_t)nred);
+    h->d_bb = h->d_S + (size_t)n_slots * 256;
+    h->d_coef = h->d_bb + nred;
+    h->n_reduce = (size_t)n_slots * 256 + 2 * (size_t)nred;
     h->d_x = dalloc<double>(ow, nred);
     h->d_scratch = dalloc<double>(ow, h->use_lds ? 8 : (size_t)n_slots * 256 + 2 * (size_t)nred + 8);
     h->d_fail = dalloc<int>(ow, 1);
@@ -1528,20 +1550,32 @@ static omv_status lba_join(omv_lba *h) {
 static omv_status lba_errors(omv_lba *h, const State &s) {
     hipStream_t st = h->stream;
     omv_status r;
-    if (h->n_imu > 0) {
+    if (h->imu_here) {
         if ((r = lba_fork(h)) != OMV_OK) return r;
         imu_err_kernel<<<1, 64, 0, h->side>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
     }
     if (h->n_mono > 0)
         mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->d_err, h->d_chi2,
                                                        h->d_partial);
-    if (h->n_imu > 0 && (r = lba_join(h)) != OMV_OK) return r;
+    if (h->imu_here && (r = lba_join(h)) != OMV_OK) return r;
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
+// In-place SUM over the ranks of a sharded solve (no-op on one rank).
+static omv_status lba_allreduce(omv_lba *h, double *buf, size_t n) {
+    if (h->world <= 1) return OMV_OK;
+    HIP_OK(hipGetLastError());
+    return h->allreduce(h->ar_ctx, buf, n, (void *)h->stream) == 0 ? OMV_OK : OMV_ERR_HIP;
+}
+
+// n_scale counts the update's partials (pose part first); only rank 0 contributes the pose part.
 static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[3], bool with_fail) {
+    const int s0 = (h->rank > 0 && n_scale > 0) ? 1 : 0;
     finish_kernel<<<1, 256, 0, h->stream>>>(h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
-                                           h->d_scale_partial, n_scale, with_fail ? h->d_fail : nullptr, h->d_out);
+                                           h->d_scale_partial + s0, n_scale - s0, with_fail ? h->d_fail : nullptr,
+                                           h->d_out);
+    omv_status rs = lba_allreduce(h, h->d_out, 2);
+    if (rs != OMV_OK) return rs;
     HIP_OK(hipMemcpyAsync(out, h->d_out, 3 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
     return OMV_OK;
@@ -1615,15 +1649,15 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         HIP_OK(hipEventRecord(h->ev[0], st));
         HIP_OK(hipMemsetAsync(h->R.H, 0, sizeof(double) * (size_t)nred * nred, st));
         HIP_OK(hipMemsetAsync(h->R.b, 0, sizeof(double) * nred, st));
-        if (h->n_imu > 0) {
+        if (h->imu_here) {
             if ((rs = lba_fork(h)) != OMV_OK) return rs;
             build_imu_kernel<<<h->n_imu, 64, 0, h->side>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
         }
         if (h->n_pts > 0)
             build_land_kernel<<<gl, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono, h->d_err,
                                                   h->d_chi2);
-        if (h->n_imu > 0 && (rs = lba_join(h)) != OMV_OK) return rs;
-        if (h->n_imu > 0) HIP_OK(hipGetLastError());
+        if (h->imu_here && (rs = lba_join(h)) != OMV_OK) return rs;
+        if (h->imu_here) HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -1640,20 +1674,28 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         do {
             HIP_OK(hipEventRecord(h->ev[2], st));
             const int npk = std::max(h->BP.n_slots * 256, nred);
-            pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, lambda, h->d_S, h->d_coef);
+            // lambda on the pose diagonal once (rank 0 of a sharded solve)
+            pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, h->rank == 0 ? lambda : 0.0, h->d_S,
+                                                           h->d_coef);
             if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef);
+            const double *bsys = h->R.b;
+            if (h->world > 1) {   // one exchange: sum the partial Schur systems of the landmark shards
+                HIP_OK(hipMemcpyAsync(h->d_bb, h->R.b, sizeof(double) * nred, hipMemcpyDeviceToDevice, st));
+                if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
+                bsys = h->d_bb;
+            }
             HIP_OK(hipEventRecord(h->ev[3], st));
             if (h->use_lds)
-                ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x,
+                ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x,
                                                                          h->d_scratch, h->d_fail);
             else
-                ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
+                ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x, h->d_scratch,
                                                               h->d_fail);
             HIP_OK(hipEventRecord(h->ev[4], st));
             // keyframe update beside the landmark back-substitution; both feed the trial's errors
             if ((rs = lba_fork(h)) != OMV_OK) return rs;
-            update_kf_kernel<<<1, 256, 0, h->side>>>(h->rig, h->R, h->d_offV, h->d_offG, h->d_offA, h->n_opt, lambda,
-                                                     h->d_x, A, B, h->d_scale_partial);
+            update_kf_kernel<<<1, 256, 0, h->side>>>(h->rig, h->R, bsys, h->d_offV, h->d_offG, h->d_offA, h->n_opt,
+                                                     lambda, h->d_x, A, B, h->d_scale_partial);
             if (h->n_pts > 0)
                 backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
             if ((rs = lba_join(h)) != OMV_OK) return rs;
@@ -1746,6 +1788,20 @@ omv_status omv_lba_reset(omv_lba *h) {
                               h->stream));
     h->cur = 0;
     HIP_OK(hipStreamSynchronize(h->stream));
+    return OMV_OK;
+}
+
+omv_status omv_lba_set_comm(omv_lba *h, int rank, int world, omv_allreduce_fn allreduce, void *ctx) {
+    if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !allreduce)) return OMV_ERR_ARG;
+    h->rank = rank, h->world = world, h->allreduce = allreduce, h->ar_ctx = ctx;
+    return OMV_OK;
+}
+
+omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *pt_index) {
+    if (!h) return OMV_ERR_ARG;
+    if (n_pts) *n_pts = h->n_pts;
+    if (n_mono) *n_mono = h->n_mono;
+    if (pt_index) std::copy(h->perm_pt.begin(), h->perm_pt.end(), pt_index);
     return OMV_OK;
 }
 

@@ -59,3 +59,58 @@ def allgather_camera_slabs(kps, desc, n_kp, group=None):
     g_kps = out[:, 1:1 + kp_cap * 6].reshape(world, kp_cap, 6).clone()
     g_desc = out[:, 1 + kp_cap * 6:].contiguous().view(torch.uint8).reshape(world, kp_cap, 32).clone()
     return g_kps, g_desc, g_n
+
+
+class LbaAllReduce:
+    """The omv_allreduce_fn of a landmark-sharded LocalInertialBA over torch.distributed.
+
+    mode "device" (backend nccl = RCCL): the handle's device buffer is staged through a torch tensor
+    on the handle's own HIP stream (torch.cuda.ExternalStream), so the copy, the ring all-reduce over
+    xGMI and the copy back stay ordered with the LM kernels and the host never waits.
+    mode "host" (backend gloo): the stream is drained and the buffer goes through host memory — the
+    CPU-collective rehearsal of the same exchange (tests, a GPU box with one card).
+    """
+
+    def __init__(self, mode="device", group=None, device=None):
+        import ctypes
+        import torch
+        if mode not in ("device", "host"):
+            raise ValueError(mode)
+        self.mode, self.group, self.device = mode, group, device
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.c_void_p]
+        self._hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        self._buf = None
+        self._torch = torch
+
+    def _staging(self, n, device):
+        t = self._torch
+        if self._buf is None or self._buf.numel() < n or self._buf.device != t.device(device):
+            self._buf = t.empty(max(n, 1), dtype=t.float64, device=device)
+        return self._buf[:n]
+
+    def __call__(self, ptr, count, stream):
+        import torch.distributed as dist
+        t = self._torch
+        nbytes = int(count) * 8
+        if self.mode == "host":
+            buf = self._staging(count, "cpu")
+            if self._hip.hipStreamSynchronize(stream) != 0:
+                raise RuntimeError("hipStreamSynchronize")
+            if self._hip.hipMemcpyAsync(buf.data_ptr(), ptr, nbytes, 2, stream) != 0:   # D2H
+                raise RuntimeError("hipMemcpyAsync D2H")
+            self._hip.hipStreamSynchronize(stream)
+            dist.all_reduce(buf, group=self.group)
+            if self._hip.hipMemcpyAsync(ptr, buf.data_ptr(), nbytes, 1, stream) != 0:   # H2D
+                raise RuntimeError("hipMemcpyAsync H2D")
+            self._hip.hipStreamSynchronize(stream)   # buf is reused by the next call
+            return
+        ext = t.cuda.ExternalStream(stream, device=self.device)
+        with t.cuda.stream(ext):
+            buf = self._staging(count, self.device or t.cuda.current_device())
+            if self._hip.hipMemcpyAsync(buf.data_ptr(), ptr, nbytes, 3, stream) != 0:   # D2D
+                raise RuntimeError("hipMemcpyAsync D2D")
+            dist.all_reduce(buf, group=self.group)   # ordered after the copy (current stream = ext)
+            if self._hip.hipMemcpyAsync(ptr, buf.data_ptr(), nbytes, 3, stream) != 0:
+                raise RuntimeError("hipMemcpyAsync D2D")

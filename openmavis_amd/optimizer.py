@@ -32,7 +32,13 @@ def lba_options(large):
 
 
 class LocalInertialBA:
-    def __init__(self, max_kf=64, max_cams=5, max_pts=40000, max_mono=400000, max_imu=64):
+    """`rank`, `world`, `allreduce`: landmark sharding (omv_lba_set_comm).  Every rank
+    passes the same full problem; `allreduce(ptr, count, stream)` sums `count` doubles of device
+    memory in place over the ranks (openmavis_amd.dist.LbaAllReduce).  After optimize() a rank's
+    result holds its own landmarks / edges (`shard()` names them) and every keyframe."""
+
+    def __init__(self, max_kf=64, max_cams=5, max_pts=40000, max_mono=400000, max_imu=64, rank=0, world=1,
+                 allreduce=None):
         lib = _lib.load()
         h = ctypes.c_void_p()
         _lib.check(lib.omv_lba_create(max_kf, max_cams, max_pts, max_mono, max_imu, ctypes.byref(h)),
@@ -40,6 +46,21 @@ class LocalInertialBA:
         self._lib, self._h = lib, h
         self._s = None
         self._keep = None
+        self._cb = None
+        if world > 1:
+            if allreduce is None:
+                raise ValueError("LocalInertialBA: world > 1 needs an allreduce")
+
+            def _cb(_ctx, buf, count, stream):
+                try:
+                    allreduce(buf, count, stream)
+                    return 0
+                except Exception as exc:   # reported by the failing omv_lba_optimize status
+                    print(f"LocalInertialBA allreduce failed: {exc!r}")
+                    return 1
+            self._cb = _lib.ALLREDUCE_FN(_cb)
+            _lib.check(lib.omv_lba_set_comm(h, int(rank), int(world), ctypes.cast(self._cb, ctypes.c_void_p), None),
+                       "omv_lba_set_comm")
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -79,6 +100,14 @@ class LocalInertialBA:
         _lib.check(self._lib.omv_lba_evaluate(self._h, _lib.ptr(me), _lib.ptr(jx), _lib.ptr(jp), _lib.ptr(ie)),
                    "omv_lba_evaluate")
         return dict(mono_err=me, mono_jx=jx, mono_jp=jp, imu_err=ie)
+
+    def shard(self):
+        """(caller indices of the landmarks this rank owns, number of its visual edges)."""
+        n_p, n_e = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(self._lib.omv_lba_shard(self._h, ctypes.byref(n_p), ctypes.byref(n_e), None), "omv_lba_shard")
+        idx = np.zeros(n_p.value, np.int32)
+        _lib.check(self._lib.omv_lba_shard(self._h, None, None, _lib.ptr(idx)), "omv_lba_shard")
+        return idx, n_e.value
 
     def stage_ms(self):
         """Device ms of the last optimize: build, schur, solve, update+errors; and the trial count."""

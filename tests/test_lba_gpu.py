@@ -142,5 +142,35 @@ def test_reoptimize_same_handle(small, oracle):
     r1, s1 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
     r2, s2 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
     assert r1["trials"] == r2["trials"]
-    for k in STATE:
-        assert np.allclose(s1[k], s2[k], rtol=1e-9, atol=1e-12)
+    # the device sums use float atomics (order varies run to run), so "the same answer" is the parity
+    # bar, not bit equality
+    _compare_state(small, s2, s1, oracle)
+
+
+def test_landmark_sharded_two_ranks(oracle, tmp_path):
+    """landmarks sharded over 2 ranks (gloo, both on this box's GPU), one all-reduce of the
+    partial Schur system per trial.  The merged outcome meets the same bar against the oracle, and
+    every rank holds the identical keyframe state (asserted inside the worker)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "shard.npz"
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tools", "lba_shard_run.py"),
+           "--out", str(out), "--backend", "gloo", "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    g = dict(np.load(out))
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=3000, seed=11)
+    assert int(g["world"]) == 2 and (g["owner"] >= 0).all() and len(set(g["owner"].tolist())) == 2
+    ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    rg = {k: (g[k].item() if g[k].ndim == 0 else g[k]) for k in
+          ("err", "err_end", "status", "iterations", "trials", "mono_chi2", "mono_outlier")}
+    _compare_result(prob, rg, ro)
+    _compare_state(prob, {k: g[k] for k in STATE}, so, oracle)
