@@ -276,6 +276,15 @@ typedef struct omv_lba_problem {
     const float *preint;       /* [n_imu][OMV_PREINT_FLOATS] */
     const uint8_t *imu_robust; /* Huber sqrt(16.92) on this inertial edge (last one / bRecInit) */
     const float *imu_info_scale;   /* 1, or 1e-2 on the last edge of the window (:2986) */
+    /* EdgeStereo (include/G2oTypes.h:364-402, src/G2oTypes.cc:402-431): left-camera (cam 0)
+     * observations with mvuRight >= 0 (Optimizer.cc:3108-3143): obs (u, v, u_R), information
+     * I3 * invSigma2, Huber sqrt(7.815); u_R predicted as u - bf / z (ImuCamPose::ProjectStereo,
+     * G2oTypes.cc:198-205).  n_stereo = 0 when there is no depth / right coordinate. */
+    int n_stereo;
+    const int32_t *stereo_pt, *stereo_kf;   /* [n_stereo] */
+    const double *stereo_obs;  /* [n_stereo][3] (kpUn.pt.x, kpUn.pt.y, mvuRight); mvuRight >= 0 */
+    const float *stereo_inv_sigma2;   /* [n_stereo] */
+    float bf;                  /* KeyFrame::mbf (ImuCamPose::bf) */
 } omv_lba_problem;
 
 typedef struct omv_lba_opts {
@@ -293,11 +302,14 @@ typedef struct omv_lba_result {
     double lambda;         /* final lambda */
     double *mono_chi2;     /* optional [n_mono]: e->chi2() after optimize (may be NULL) */
     uint8_t *mono_outlier; /* optional [n_mono]: the :3282-3296 outlier test (may be NULL) */
+    double *stereo_chi2;   /* optional [n_stereo] */
+    uint8_t *stereo_outlier;   /* optional [n_stereo]: chi2 > 7.815 (:3299-3311) */
 } omv_lba_result;
 
 typedef struct omv_lba omv_lba;
 
-/* Workspace for problems up to the given sizes. */
+/* Workspace for problems up to the given sizes (max_mono bounds the visual edges a handle holds:
+ * EdgeMono + EdgeStereo; with sharding, the rank's share). */
 omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, int max_imu, omv_lba **out);
 omv_status omv_lba_destroy(omv_lba *h);
 /* Upload a problem (host arrays); the structure (point -> keyframe slots, reduced-system layout,
@@ -309,6 +321,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
 /* Residual/Jacobian evaluation at the uploaded state for parity: mono_err [n_mono][2],
  * mono_jx [n_mono][6] (2x3), mono_jp [n_mono][12] (2x6), imu_err [n_imu][9] (any may be NULL). */
 omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err);
+/* The same for the EdgeStereo edges: err [n_stereo][3], jx [n_stereo][9] (3x3), jp [n_stereo][18] (3x6). */
+omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stereo_jx, double *stereo_jp);
 /* Restore the state uploaded by the last set_problem (device-side copy; for re-runs and benchmarks). */
 omv_status omv_lba_reset(omv_lba *h);
 /* Per-stage device time of the last optimize: 0 linearise+build, 1 Schur, 2 reduced solve,

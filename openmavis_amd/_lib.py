@@ -92,7 +92,9 @@ class LbaProblem(ctypes.Structure):
                 ("mono_kf", ctypes.c_void_p), ("mono_cam", ctypes.c_void_p), ("mono_obs", ctypes.c_void_p),
                 ("mono_inv_sigma2", ctypes.c_void_p), ("n_imu", ctypes.c_int), ("imu_kf1", ctypes.c_void_p),
                 ("imu_kf2", ctypes.c_void_p), ("preint", ctypes.c_void_p), ("imu_robust", ctypes.c_void_p),
-                ("imu_info_scale", ctypes.c_void_p)]
+                ("imu_info_scale", ctypes.c_void_p), ("n_stereo", ctypes.c_int), ("stereo_pt", ctypes.c_void_p),
+                ("stereo_kf", ctypes.c_void_p), ("stereo_obs", ctypes.c_void_p),
+                ("stereo_inv_sigma2", ctypes.c_void_p), ("bf", ctypes.c_float)]
 
 
 class LbaOpts(ctypes.Structure):
@@ -103,7 +105,8 @@ class LbaOpts(ctypes.Structure):
 class LbaResult(ctypes.Structure):
     _fields_ = [("err", ctypes.c_float), ("err_end", ctypes.c_float), ("status", ctypes.c_int),
                 ("iterations", ctypes.c_int), ("trials", ctypes.c_int), ("lambda_", ctypes.c_double),
-                ("mono_chi2", ctypes.c_void_p), ("mono_outlier", ctypes.c_void_p)]
+                ("mono_chi2", ctypes.c_void_p), ("mono_outlier", ctypes.c_void_p),
+                ("stereo_chi2", ctypes.c_void_p), ("stereo_outlier", ctypes.c_void_p)]
 
 
 # numpy dtype with the omv_kp layout (24 bytes)
@@ -152,6 +155,7 @@ SIGNATURES = {
     "omv_lba_set_problem": (_I, [_VP, ctypes.POINTER(LbaProblem)]),
     "omv_lba_optimize": (_I, [_VP, ctypes.POINTER(LbaOpts), ctypes.POINTER(LbaProblem), ctypes.POINTER(LbaResult)]),
     "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "omv_lba_evaluate_stereo": (_I, [_VP, _VP, _VP, _VP]),
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
     "omv_lba_reset": (_I, [_VP]),
     "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),

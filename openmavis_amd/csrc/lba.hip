@@ -131,6 +131,7 @@ struct Rig {
     int n_cams;
     float cam[kMaxCams][8];
     double Rcb[kMaxCams][9], tcb[kMaxCams][3], Rbc[kMaxCams][9], tbc[kMaxCams][3];
+    double bf;   // ImuCamPose::bf = KeyFrame::mbf (EdgeStereo)
 };
 
 // KannalaBrandt8::project(const Eigen::Vector3d&) (KannalaBrandt8.cpp:28-46)
@@ -168,12 +169,19 @@ struct State {   // one of the two state buffers
     double *Rwb, *twb, *Rcw, *tcw, *vel, *bg, *ba, *pts;
 };
 
-struct Edges {   // landmark-major visual edges
+struct Edges {   // landmark-major visual edges (EdgeMono, and EdgeStereo where ur >= 0)
     const int32_t *pt, *kf, *cam, *slot;
     const double *obs;
-    const float *w;   // invSigma2
+    const float *w;    // invSigma2
+    const float *ur;   // EdgeStereo's third measurement (mvuRight >= 0); -1 on an EdgeMono
     int n;
 };
+
+// ImuCamPose::ProjectStereo's third row (G2oTypes.cc:198-205): u - bf * (1 / z)
+__device__ __forceinline__ double stereo_ur(double u, double bf, double z) {
+    const double invZ = 1 / z;
+    return u - bf * invZ;
+}
 
 // Huber (robust_kernel_impl.cpp:78-91)
 __device__ __forceinline__ void huber(double e2, double delta, double dsqr, double &r0, double &r1) {
@@ -199,7 +207,8 @@ __device__ double block_reduce_sum(double v, double *sh) {
 }
 
 __global__ void __launch_bounds__(256) mono_err_kernel(Rig rig, State s, Edges E, double delta, double dsqr,
-                                                       double *err, double *chi2, double *partial) {
+                                                       double delta_st, double dsqr_st, double *err, double *err3,
+                                                       double *chi2, double *partial) {
     __shared__ double sh[8];
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     double r0 = 0;
@@ -214,11 +223,18 @@ __global__ void __launch_bounds__(256) mono_err_kernel(Rig rig, State s, Edges E
         kb8_project(rig.cam[c], Xc, u, v);
         const double e0 = E.obs[2 * e] - u, e1 = E.obs[2 * e + 1] - v;
         const double w = (double)E.w[e];
-        const double c2 = e0 * w * e0 + e1 * w * e1;
+        double c2 = e0 * w * e0 + e1 * w * e1;
         err[2 * e] = e0, err[2 * e + 1] = e1;
+        const float ur = E.ur[e];
+        if (ur >= 0.f) {   // EdgeStereo
+            const double e2 = (double)ur - stereo_ur(u, rig.bf, Xc[2]);
+            err3[e] = e2;
+            c2 += e2 * w * e2;
+        }
         chi2[e] = c2;
         double r1;
-        huber(c2, delta, dsqr, r0, r1);
+        if (ur >= 0.f) huber(c2, delta_st, dsqr_st, r0, r1);
+        else huber(c2, delta, dsqr, r0, r1);
     }
     const double t = block_reduce_sum(r0, sh);
     if (threadIdx.x == 0) partial[blockIdx.x] = t;
@@ -403,7 +419,8 @@ struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lowe
 
 // LDS accumulators of a workgroup: kSpan keyframes x (36 + 6)
 __global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, Edges E, Land L, Red R, double delta,
-                                                         double dsqr, const double *err, const double *chi2) {
+                                                         double dsqr, double delta_st, double dsqr_st, const double *err,
+                                                         const double *err3, const double *chi2) {
     __shared__ double acc[kSpan * 42];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int kf0 = L.wg_kf0[blockIdx.x];
@@ -423,30 +440,51 @@ __global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, E
             for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
             mv3(rig.Rbc[c], Xc, Xb);
             for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
-            double pj[6];
+            const bool st = E.ur[e] >= 0.f;   // EdgeStereo: proj_jac row 2 = row 0, (2,2) += bf / z^2
+            double pj[9];
             kb8_jac(rig.cam[c], Xc, pj);
-            double JX[6];
-            for (int r = 0; r < 2; ++r)
+            const int nr = st ? 3 : 2;
+            if (st) {
+                const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+                pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
+            }
+            double JX[9], JP[18];
+            for (int r = 0; r < nr; ++r)
                 for (int q = 0; q < 3; ++q)
                     JX[3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
-            double pr[6];
-            for (int r = 0; r < 2; ++r)
-                for (int q = 0; q < 3; ++q)
-                    pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
-            const double x = Xb[0], y = Xb[1], z = Xb[2];
-            const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-            double JP[12];
-            for (int r = 0; r < 2; ++r)
-                for (int q = 0; q < 6; ++q)
-                    JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+            {
+                double pr[9];
+                for (int r = 0; r < nr; ++r)
+                    for (int q = 0; q < 3; ++q)
+                        pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] +
+                                        pj[3 * r + 2] * rig.Rcb[c][6 + q];
+                const double x = Xb[0], y = Xb[1], z = Xb[2];
+                const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+                for (int r = 0; r < nr; ++r)
+                    for (int q = 0; q < 6; ++q)
+                        JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+            }
             double r0, r1;
-            huber(chi2[e], delta, dsqr, r0, r1);
+            if (st) huber(chi2[e], delta_st, dsqr_st, r0, r1);
+            else huber(chi2[e], delta, dsqr, r0, r1);
             const double wi = (double)E.w[e];
             const double w = wi * r1;
             const double om0 = -wi * err[2 * e] * r1, om1 = -wi * err[2 * e + 1] * r1;
+            const double om2 = st ? -wi * err3[e] * r1 : 0.0;
+            // sums over the residual rows: the EdgeStereo row is added last (mono edges: 2 rows as before)
+            auto rows = [&](const double *A, int ia, const double *B, int ib, int lda, int ldb) {
+                double t = A[ia] * B[ib] + A[lda + ia] * B[ldb + ib];
+                if (st) t += A[2 * lda + ia] * B[2 * ldb + ib];
+                return t;
+            };
+            auto rows_om = [&](const double *A, int ia, int lda) {
+                double t = A[ia] * om0 + A[lda + ia] * om1;
+                if (st) t += A[2 * lda + ia] * om2;
+                return t;
+            };
             for (int r = 0; r < 3; ++r) {
-                bl[r] += JX[r] * om0 + JX[3 + r] * om1;
-                for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * (JX[r] * JX[q] + JX[3 + r] * JX[3 + q]);
+                bl[r] += rows_om(JX, r, 3);
+                for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * rows(JX, r, JX, q, 3, 3);
             }
             const int slot = E.slot[e];
             if (slot != cur_slot) {
@@ -456,20 +494,20 @@ __global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, E
                 cur_slot = slot;
             }
             for (int r = 0; r < 6; ++r)
-                for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * (JP[r] * JX[q] + JP[6 + r] * JX[3 + q]);
+                for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * rows(JP, r, JX, q, 6, 3);
             const int o = R.offP[k];
             if (o < 0) continue;   // fixed keyframe: no pose terms
             if (kf0 >= 0 && k - kf0 >= 0 && k - kf0 < kSpan) {
                 double *a = acc + (k - kf0) * 42;
                 for (int r = 0; r < 6; ++r) {
-                    unsafeAtomicAdd(a + 36 + r, JP[r] * om0 + JP[6 + r] * om1);
-                    for (int q = 0; q <= r; ++q) unsafeAtomicAdd(a + 6 * r + q, w * (JP[r] * JP[q] + JP[6 + r] * JP[6 + q]));
+                    unsafeAtomicAdd(a + 36 + r, rows_om(JP, r, 6));
+                    for (int q = 0; q <= r; ++q) unsafeAtomicAdd(a + 6 * r + q, w * rows(JP, r, JP, q, 6, 6));
                 }
             } else {
                 for (int r = 0; r < 6; ++r) {
-                    unsafeAtomicAdd(R.b + o + r, JP[r] * om0 + JP[6 + r] * om1);
+                    unsafeAtomicAdd(R.b + o + r, rows_om(JP, r, 6));
                     for (int q = 0; q <= r; ++q)
-                        unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + q, w * (JP[r] * JP[q] + JP[6 + r] * JP[6 + q]));
+                        unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + q, w * rows(JP, r, JP, q, 6, 6));
                 }
             }
         }
@@ -1086,6 +1124,7 @@ __global__ void update_kf_kernel(Rig rig, Red R, const double *b, const int *off
 }
 
 // ---- evaluation helpers for parity ---------------------------------------------------------------
+// [9] / [18] per edge: 3 residual rows (the third is zero on an EdgeMono)
 __global__ void mono_jac_kernel(Rig rig, State s, Edges E, double *jx, double *jp) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E.n) return;
@@ -1097,20 +1136,24 @@ __global__ void mono_jac_kernel(Rig rig, State s, Edges E, double *jx, double *j
     for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
     mv3(rig.Rbc[c], Xc, Xb);
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
-    double pj[6];
+    double pj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     kb8_jac(rig.cam[c], Xc, pj);
-    for (int r = 0; r < 2; ++r)
+    if (E.ur[e] >= 0.f) {
+        const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+        pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
+    }
+    for (int r = 0; r < 3; ++r)
         for (int q = 0; q < 3; ++q)
-            jx[6 * e + 3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
-    double pr[6];
-    for (int r = 0; r < 2; ++r)
+            jx[9 * e + 3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
+    double pr[9];
+    for (int r = 0; r < 3; ++r)
         for (int q = 0; q < 3; ++q)
             pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
     const double x = Xb[0], y = Xb[1], z = Xb[2];
     const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < 3; ++r)
         for (int q = 0; q < 6; ++q)
-            jp[12 * e + 6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+            jp[18 * e + 6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
 }
 
 // ---- host-side analysis ------------------------------------------------------------------------------
@@ -1207,7 +1250,9 @@ struct omv_lba {
     bool lds_ok = false;
     std::vector<int> perm_pt;     // device point index -> caller index
     std::vector<int> perm_edge;   // device edge index -> caller index
-    double delta_mono, dsqr_mono, delta_imu, dsqr_imu;
+    double delta_mono, dsqr_mono, delta_st, dsqr_st, delta_imu, dsqr_imu;
+    int n_mono_all = 0, n_stereo_all = 0;   // caller edge counts (perm_edge >= n_mono_all: EdgeStereo)
+    double *d_err3 = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;   // inertial edges run beside the visual kernels (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1262,7 +1307,16 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         p->n_imu > h->max_imu || p->n_opt > p->n_kf || p->n_opt < 1)
         return OMV_ERR_ARG;
     free_problem(h);
-    const int C = p->n_cams, K = p->n_kf, P_all = p->n_pts, E_all = p->n_mono, NI = p->n_imu;
+    const int C = p->n_cams, K = p->n_kf, P_all = p->n_pts, NI = p->n_imu;
+    const int EM = p->n_mono, ES = p->n_stereo > 0 ? p->n_stereo : 0, E_all = EM + ES;
+    if (ES > 0 && (!p->stereo_pt || !p->stereo_kf || !p->stereo_obs || !p->stereo_inv_sigma2)) return OMV_ERR_ARG;
+    for (int e = 0; e < ES; ++e)   // an EdgeStereo exists only where mvuRight >= 0 (Optimizer.cc:3075, :3108)
+        if (!(p->stereo_obs[3 * (size_t)e + 2] >= 0.0)) return OMV_ERR_ARG;
+    h->n_mono_all = EM, h->n_stereo_all = ES;
+    // visual edge e < EM: EdgeMono e; e >= EM: EdgeStereo e - EM (camera 0, EdgeStereo(0) at :3118)
+    auto e_pt_of = [&](int e) { return e < EM ? p->mono_pt[e] : p->stereo_pt[e - EM]; };
+    auto e_kf_of = [&](int e) { return e < EM ? p->mono_kf[e] : p->stereo_kf[e - EM]; };
+    auto e_cam_of = [&](int e) { return e < EM ? p->mono_cam[e] : 0; };
     h->n_kf = K, h->n_opt = p->n_opt, h->n_imu = NI;
     h->imu_here = NI > 0 && h->rank == 0;
     // rig
@@ -1285,14 +1339,14 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     // landmark order: by the first optimisable keyframe observing them (workgroup keyframe spans stay small)
     std::vector<std::vector<int>> pe(P_all);
     for (int e = 0; e < E_all; ++e) {
-        if (p->mono_pt[e] < 0 || p->mono_pt[e] >= P_all || p->mono_kf[e] < 0 || p->mono_kf[e] >= K ||
-            p->mono_cam[e] < 0 || p->mono_cam[e] >= C)
+        if (e_pt_of(e) < 0 || e_pt_of(e) >= P_all || e_kf_of(e) < 0 || e_kf_of(e) >= K || e_cam_of(e) < 0 ||
+            e_cam_of(e) >= C)
             return OMV_ERR_ARG;
-        pe[p->mono_pt[e]].push_back(e);
+        pe[e_pt_of(e)].push_back(e);
     }
     std::vector<int> key(P_all, 1 << 30);
     for (int q = 0; q < P_all; ++q)
-        for (int e : pe[q]) key[q] = std::min(key[q], p->mono_kf[e] < p->n_opt ? p->mono_kf[e] : (1 << 29) + p->mono_kf[e]);
+        for (int e : pe[q]) key[q] = std::min(key[q], e_kf_of(e) < p->n_opt ? e_kf_of(e) : (1 << 29) + e_kf_of(e));
     std::vector<int> order(P_all);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
@@ -1304,7 +1358,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     for (int q = 0; q < P_all; ++q)
         for (int a : pe[q])
             for (int b : pe[q]) {
-                const int i = p->mono_kf[a], j = p->mono_kf[b];
+                const int i = e_kf_of(a), j = e_kf_of(b);
                 if (i < nb && j < nb && j <= i) pat[i * nb + j] = 1;
             }
     // this rank's landmarks: a contiguous share of the landmark order
@@ -1320,20 +1374,30 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->perm_pt = order;
     std::vector<int> e_pt, e_kf, e_cam, e_slot, pt_edge(P + 1, 0), pt_slot(P + 1, 0), slot_kf;
     std::vector<double> e_obs;
-    std::vector<float> e_w;
+    std::vector<float> e_w, e_ur;
     h->perm_edge.clear();
     for (int q = 0; q < P; ++q) {
         std::vector<int> es = pe[order[q]];
-        std::stable_sort(es.begin(), es.end(), [&](int a, int b) { return p->mono_kf[a] < p->mono_kf[b]; });
+        std::stable_sort(es.begin(), es.end(), [&](int a, int b) { return e_kf_of(a) < e_kf_of(b); });
         pt_edge[q] = (int)e_pt.size();
         pt_slot[q] = (int)slot_kf.size();
         int last_kf = -1;
         for (int e : es) {
-            if (p->mono_kf[e] != last_kf) slot_kf.push_back(p->mono_kf[e]), last_kf = p->mono_kf[e];
-            e_pt.push_back(q), e_kf.push_back(p->mono_kf[e]), e_cam.push_back(p->mono_cam[e]);
+            const int kf = e_kf_of(e);
+            if (kf != last_kf) slot_kf.push_back(kf), last_kf = kf;
+            e_pt.push_back(q), e_kf.push_back(kf), e_cam.push_back(e_cam_of(e));
             e_slot.push_back((int)slot_kf.size() - 1);
-            e_obs.push_back(p->mono_obs[2 * e]), e_obs.push_back(p->mono_obs[2 * e + 1]);
-            e_w.push_back(p->mono_inv_sigma2[e]);
+            if (e < EM) {
+                e_obs.push_back(p->mono_obs[2 * e]), e_obs.push_back(p->mono_obs[2 * e + 1]);
+                e_w.push_back(p->mono_inv_sigma2[e]);
+                e_ur.push_back(-1.f);
+            } else {
+                const double *o = p->stereo_obs + 3 * (size_t)(e - EM);
+                e_obs.push_back(o[0]), e_obs.push_back(o[1]);
+                e_w.push_back(p->stereo_inv_sigma2[e - EM]);
+                // the reference stores mvuRight (a float >= 0) in the double measurement
+                e_ur.push_back((float)o[2]);
+            }
             h->perm_edge.push_back(e);
         }
     }
@@ -1417,8 +1481,11 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         inv3(g, &infoG[(size_t)9 * i]);
         inv3(a, &infoA[(size_t)9 * i]);
     }
-    h->delta_mono = (double)(float)std::sqrt(5.991);
+    h->delta_mono = (double)(float)std::sqrt(5.991);   // thHuberMono / thHuberStereo are floats (:3028-3031)
     h->dsqr_mono = h->delta_mono * h->delta_mono;
+    h->delta_st = (double)(float)std::sqrt(7.815);
+    h->dsqr_st = h->delta_st * h->delta_st;
+    rig.bf = (double)p->bf;
     h->delta_imu = std::sqrt(16.92);
     h->dsqr_imu = h->delta_imu * h->delta_imu;
     // ---- device allocations + uploads
@@ -1449,7 +1516,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     int *d_e_pt = dalloc<int>(ow, E), *d_e_kf = dalloc<int>(ow, E), *d_e_cam = dalloc<int>(ow, E),
         *d_e_slot = dalloc<int>(ow, E);
     double *d_e_obs = dalloc<double>(ow, 2 * (size_t)E);
-    float *d_e_w = dalloc<float>(ow, E);
+    float *d_e_w = dalloc<float>(ow, E), *d_e_ur = dalloc<float>(ow, E);
     if (!d_e_w) return OMV_ERR_HIP;
     HIP_OK(up(d_e_pt, e_pt.data(), E));
     HIP_OK(up(d_e_kf, e_kf.data(), E));
@@ -1457,7 +1524,9 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     HIP_OK(up(d_e_slot, e_slot.data(), E));
     HIP_OK(up(d_e_obs, e_obs.data(), 2 * (size_t)E));
     HIP_OK(up(d_e_w, e_w.data(), E));
-    h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, E};
+    if (!d_e_ur) return OMV_ERR_HIP;
+    HIP_OK(up(d_e_ur, e_ur.data(), E));
+    h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, d_e_ur, E};
     int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots),
         *d_wg = dalloc<int>(ow, wg_kf0.size());
     double *d_Hll = dalloc<double>(ow, 9 * (size_t)P), *d_bl = dalloc<double>(ow, 3 * (size_t)P),
@@ -1513,6 +1582,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->n_wg_edge = (E + 255) / 256;
     h->d_err = dalloc<double>(ow, 2 * (size_t)E);
     h->d_chi2 = dalloc<double>(ow, E);
+    h->d_err3 = dalloc<double>(ow, E);
     h->d_err9 = dalloc<double>(ow, 10 * (size_t)NI);
     h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
     h->d_imu_partial = dalloc<double>(ow, 1);
@@ -1555,7 +1625,8 @@ static omv_status lba_errors(omv_lba *h, const State &s) {
         imu_err_kernel<<<1, 64, 0, h->side>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
     }
     if (h->n_mono > 0)
-        mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->d_err, h->d_chi2,
+        mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->delta_st,
+                                                       h->dsqr_st, h->d_err, h->d_err3, h->d_chi2,
                                                        h->d_partial);
     if (h->imu_here && (r = lba_join(h)) != OMV_OK) return r;
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
@@ -1581,9 +1652,10 @@ static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[3], bool 
     return OMV_OK;
 }
 
-extern "C" {
-
-omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err) {
+// Residuals + Jacobians of the visual edges at the current state, in the caller's order; EdgeMono
+// rows go to the mono_* arrays (2 rows), EdgeStereo rows to the stereo_* arrays (3 rows).
+static omv_status lba_eval(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err,
+                           double *st_err, double *st_jx, double *st_jp) {
     if (!h) return OMV_ERR_ARG;
     const State &s = h->st[h->cur];
     omv_status r = lba_errors(h, s);
@@ -1591,30 +1663,52 @@ omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, doubl
     std::vector<double> jx, jp;
     double *d_jx = nullptr, *d_jp = nullptr;
     const int E = h->n_mono;
-    if ((mono_jx || mono_jp) && E > 0) {
-        HIP_OK(hipMalloc(&d_jx, sizeof(double) * 6 * E));
-        HIP_OK(hipMalloc(&d_jp, sizeof(double) * 12 * E));
+    const bool jac = mono_jx || mono_jp || st_jx || st_jp;
+    if (jac && E > 0) {
+        HIP_OK(hipMalloc(&d_jx, sizeof(double) * 9 * E));
+        HIP_OK(hipMalloc(&d_jp, sizeof(double) * 18 * E));
         mono_jac_kernel<<<(E + 255) / 256, 256, 0, h->stream>>>(h->rig, s, h->E, d_jx, d_jp);
     }
     HIP_OK(hipStreamSynchronize(h->stream));
-    std::vector<double> err(2 * (size_t)E), e9(10 * (size_t)h->n_imu);
-    if (E > 0) HIP_OK(hipMemcpy(err.data(), h->d_err, err.size() * sizeof(double), hipMemcpyDeviceToHost));
-    if (h->n_imu > 0) HIP_OK(hipMemcpy(e9.data(), h->d_err9, e9.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> err(2 * (size_t)E), err3(E), e9(10 * (size_t)h->n_imu);
+    if (E > 0) {
+        HIP_OK(hipMemcpy(err.data(), h->d_err, err.size() * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(err3.data(), h->d_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (h->imu_here) HIP_OK(hipMemcpy(e9.data(), h->d_err9, e9.size() * sizeof(double), hipMemcpyDeviceToHost));
     if (d_jx) {
-        jx.resize(6 * (size_t)E), jp.resize(12 * (size_t)E);
+        jx.resize(9 * (size_t)E), jp.resize(18 * (size_t)E);
         HIP_OK(hipMemcpy(jx.data(), d_jx, jx.size() * sizeof(double), hipMemcpyDeviceToHost));
         HIP_OK(hipMemcpy(jp.data(), d_jp, jp.size() * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(d_jx);
         (void)hipFree(d_jp);
     }
+    const int EM = h->n_mono_all;
     for (int e = 0; e < E; ++e) {   // back to the caller's edge order
         const int o = h->perm_edge[e];
-        if (mono_err) mono_err[2 * o] = err[2 * e], mono_err[2 * o + 1] = err[2 * e + 1];
-        if (mono_jx) std::memcpy(mono_jx + 6 * (size_t)o, &jx[6 * (size_t)e], 48);
-        if (mono_jp) std::memcpy(mono_jp + 12 * (size_t)o, &jp[12 * (size_t)e], 96);
+        if (o < EM) {
+            if (mono_err) mono_err[2 * o] = err[2 * e], mono_err[2 * o + 1] = err[2 * e + 1];
+            if (mono_jx) std::memcpy(mono_jx + 6 * (size_t)o, &jx[9 * (size_t)e], 48);
+            if (mono_jp) std::memcpy(mono_jp + 12 * (size_t)o, &jp[18 * (size_t)e], 96);
+        } else {
+            const size_t q = (size_t)(o - EM);
+            if (st_err) st_err[3 * q] = err[2 * e], st_err[3 * q + 1] = err[2 * e + 1], st_err[3 * q + 2] = err3[e];
+            if (st_jx) std::memcpy(st_jx + 9 * q, &jx[9 * (size_t)e], 72);
+            if (st_jp) std::memcpy(st_jp + 18 * q, &jp[18 * (size_t)e], 144);
+        }
     }
-    if (imu_err) std::memcpy(imu_err, e9.data(), 9 * sizeof(double) * h->n_imu);
+    if (imu_err && h->imu_here) std::memcpy(imu_err, e9.data(), 9 * sizeof(double) * h->n_imu);
     return OMV_OK;
+}
+
+extern "C" {
+
+omv_status omv_lba_evaluate(omv_lba *h, double *mono_err, double *mono_jx, double *mono_jp, double *imu_err) {
+    return lba_eval(h, mono_err, mono_jx, mono_jp, imu_err, nullptr, nullptr, nullptr);
+}
+
+omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stereo_jx, double *stereo_jp) {
+    return lba_eval(h, nullptr, nullptr, nullptr, nullptr, stereo_err, stereo_jx, stereo_jp);
 }
 
 omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
@@ -1654,7 +1748,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             build_imu_kernel<<<h->n_imu, 64, 0, h->side>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
         }
         if (h->n_pts > 0)
-            build_land_kernel<<<gl, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono, h->d_err,
+            build_land_kernel<<<gl, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono,
+                                                      h->delta_st, h->dsqr_st, h->d_err, h->d_err3,
                                                   h->d_chi2);
         if (h->imu_here && (rs = lba_join(h)) != OMV_OK) return rs;
         if (h->imu_here) HIP_OK(hipGetLastError());
@@ -1765,6 +1860,12 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     }
     for (int e = 0; e < E; ++e) {
         const int oe = h->perm_edge[e];
+        if (oe >= h->n_mono_all) {   // EdgeStereo: chi2 > chi2Stereo2 (:3299-3311)
+            const int q = oe - h->n_mono_all;
+            if (res->stereo_chi2) res->stereo_chi2[q] = chi2[e];
+            if (res->stereo_outlier) res->stereo_outlier[q] = chi2[e] > 7.815f ? 1 : 0;
+            continue;
+        }
         if (res->mono_chi2) res->mono_chi2[oe] = chi2[e];
         if (res->mono_outlier) {
             const int k = p->mono_kf[oe], c = p->mono_cam[oe], pt = p->mono_pt[oe];

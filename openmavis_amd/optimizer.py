@@ -77,15 +77,18 @@ class LocalInertialBA:
         if self._s is None:
             raise _lib.OmvError("LocalInertialBA.optimize: no problem set")
         o = _lib.LbaOpts(int(opt_it), float(lambda_init), int(max_trials), int(bool(large)))
-        E = self._s.n_mono
+        E, S = self._s.n_mono, self._s.n_stereo
         chi2 = np.zeros(E)
         outl = np.zeros(E, np.uint8)
+        s_chi2 = np.zeros(S)
+        s_outl = np.zeros(S, np.uint8)
         r = _lib.LbaResult()
         r.mono_chi2, r.mono_outlier = _lib.ptr(chi2), _lib.ptr(outl)
+        r.stereo_chi2, r.stereo_outlier = _lib.ptr(s_chi2), _lib.ptr(s_outl)
         _lib.check(self._lib.omv_lba_optimize(self._h, ctypes.byref(o), ctypes.byref(self._s), ctypes.byref(r)),
                    "omv_lba_optimize")
         res = dict(err=r.err, err_end=r.err_end, status=r.status, iterations=r.iterations, trials=r.trials,
-                   lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl)
+                   lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl, stereo_chi2=s_chi2, stereo_outlier=s_outl)
         return res, read_state(self._keep)
 
     def reset(self):
@@ -99,7 +102,11 @@ class LocalInertialBA:
         me, jx, jp, ie = np.zeros((E, 2)), np.zeros((E, 6)), np.zeros((E, 12)), np.zeros((I, 9))
         _lib.check(self._lib.omv_lba_evaluate(self._h, _lib.ptr(me), _lib.ptr(jx), _lib.ptr(jp), _lib.ptr(ie)),
                    "omv_lba_evaluate")
-        return dict(mono_err=me, mono_jx=jx, mono_jp=jp, imu_err=ie)
+        S = self._s.n_stereo
+        se, sx, sp = np.zeros((S, 3)), np.zeros((S, 9)), np.zeros((S, 18))
+        _lib.check(self._lib.omv_lba_evaluate_stereo(self._h, _lib.ptr(se), _lib.ptr(sx), _lib.ptr(sp)),
+                   "omv_lba_evaluate_stereo")
+        return dict(mono_err=me, mono_jx=jx, mono_jp=jp, imu_err=ie, stereo_err=se, stereo_jx=sx, stereo_jp=sp)
 
     def shard(self):
         """(caller indices of the landmarks this rank owns, number of its visual edges)."""

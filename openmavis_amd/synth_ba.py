@@ -152,7 +152,11 @@ def _log(R):
 
 
 def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_noise=0.05, rot_noise_deg=0.5,
-                     trans_noise=0.02, n_cams=5):
+                     trans_noise=0.02, n_cams=5, stereo_frac=0.0, bf=40.0):
+    """stereo_frac > 0: that fraction of the camera-0 observations become EdgeStereo observations
+    (u, v, u_R = u - bf / z + noise), as LocalInertialBA creates them for keypoints with a right
+    coordinate / depth (Optimizer.cc:3108-3143); drawn from a separate stream, so the rest of the
+    window is the same as with stereo_frac = 0."""
     rng = np.random.Generator(np.random.PCG64(seed))
     cams, Rbc, tbc = rig()
     cams, Rbc, tbc = cams[:n_cams], Rbc[:n_cams], tbc[:n_cams]
@@ -252,12 +256,30 @@ def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_n
     imu_scale = np.ones(n_opt, np.float32)
     imu_scale[n_opt - 1] = 1e-2
     inv_sig = (1.0 / np.float32(1.2) ** (2 * rng.integers(0, 8, len(obs_pt)))).astype(np.float32)
-    return dict(
+    obs_pt, obs_kf, obs_cam = np.array(obs_pt, np.int32), np.array(obs_kf, np.int32), np.array(obs_cam, np.int32)
+    obs_uv = np.array(obs_uv, np.float64)
+    st = np.zeros(len(obs_pt), bool)
+    if stereo_frac > 0:
+        srng = np.random.Generator(np.random.PCG64(seed + 7919))
+        st = (obs_cam == 0) & (srng.random(len(obs_pt)) < stereo_frac)
+    st_obs = np.zeros((len(obs_pt), 3))
+    for e in np.nonzero(st)[0]:
+        k = obs_kf[e]
+        Rc_t, tc_t = cam_pose(Rwb_t[k], twb_t[k])
+        z = (Rc_t[0] @ pts_t[obs_pt[e]] + tc_t[0])[2]
+        st_obs[e, :2] = obs_uv[e]
+        st_obs[e, 2] = np.float32(obs_uv[e, 0] - bf / z + srng.normal(0, obs_noise))   # mvuRight is a float
+    st &= st_obs[:, 2] >= 0   # mvuRight < 0 means "no right coordinate": an EdgeMono (:3075)
+    st_obs = st_obs[st]
+    extra = dict(n_stereo=int(st.sum()), stereo_pt=obs_pt[st], stereo_kf=obs_kf[st], stereo_obs=st_obs,
+                 stereo_inv_sigma2=inv_sig[st], bf=np.float32(bf)) if stereo_frac > 0 else {}
+    keep_m = ~st
+    obs_pt, obs_kf, obs_cam, obs_uv, inv_sig = obs_pt[keep_m], obs_kf[keep_m], obs_cam[keep_m], obs_uv[keep_m], inv_sig[keep_m]
+    return dict(**extra,
         n_cams=n_cams, cam=cams, Rcb=Rcb, tcb=tcb, Rbc=Rbc, tbc=tbc, n_kf=n_kf, n_opt=n_opt,
         kf_imu=np.ones(n_kf, np.uint8), Rwb=Rwb, twb=twb, Rcw=Rcw, tcw=tcw, vel=vel, bg=bg, ba=ba,
         pts=pts, pt_track_depth=rng.uniform(1.0, 60.0, len(pts)).astype(np.float32),
-        mono_pt=np.array(obs_pt, np.int32), mono_kf=np.array(obs_kf, np.int32), mono_cam=np.array(obs_cam, np.int32),
-        mono_obs=np.array(obs_uv, np.float64), mono_inv_sigma2=inv_sig,
+        mono_pt=obs_pt, mono_kf=obs_kf, mono_cam=obs_cam, mono_obs=obs_uv, mono_inv_sigma2=inv_sig,
         imu_kf1=np.array(imu_kf1, np.int32), imu_kf2=np.array(imu_kf2, np.int32), preint=np.stack(pre),
         imu_robust=imu_robust, imu_info_scale=imu_scale,
         truth=dict(Rwb=Rwb_t, twb=twb_t, pts=pts_t),
@@ -295,6 +317,13 @@ def as_struct(prob, struct_cls):
     s.preint = arr("preint", np.float32)
     s.imu_robust = arr("imu_robust", np.uint8)
     s.imu_info_scale = arr("imu_info_scale", np.float32)
+    s.n_stereo = int(len(prob.get("stereo_pt", ())))
+    if s.n_stereo:
+        for f in ("stereo_pt", "stereo_kf"):
+            setattr(s, f, arr(f, np.int32))
+        s.stereo_obs = arr("stereo_obs", np.float64)
+        s.stereo_inv_sigma2 = arr("stereo_inv_sigma2", np.float32)
+    s.bf = float(prob.get("bf", 0.0))
     return s, keep
 
 

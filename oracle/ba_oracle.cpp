@@ -349,9 +349,11 @@ struct Solver {
     int nred = 0;
     // errors (last computeActiveErrors)
     std::vector<double> e_mono;   // 2 per edge
+    std::vector<double> e_st;     // 3 per EdgeStereo
     std::vector<double> e_imu;    // 9 per edge
     std::vector<V3> e_gr, e_ar;
-    double delta_mono, dsqr_mono, delta_imu, dsqr_imu;
+    double delta_mono, dsqr_mono, delta_st, dsqr_st, delta_imu, dsqr_imu;
+    int NS;
 
     explicit Solver(const omv_lba_problem &p) : P(p), C(p.n_cams) {
         for (int c = 0; c < C; ++c) {
@@ -426,6 +428,10 @@ struct Solver {
         delta_imu = std::sqrt(16.92);
         dsqr_imu = delta_imu * delta_imu;
         e_mono.assign(2 * (size_t)p.n_mono, 0.0);
+        NS = p.n_stereo > 0 ? p.n_stereo : 0;
+        e_st.assign(3 * (size_t)NS, 0.0);
+        delta_st = (double)(float)std::sqrt(7.815);    // thHuberStereo (:3030)
+        dsqr_st = delta_st * delta_st;
         e_imu.assign(9 * (size_t)p.n_imu, 0.0);
         e_gr.resize(p.n_imu), e_ar.resize(p.n_imu);
     }
@@ -440,6 +446,23 @@ struct Solver {
         kb8_project(camk(c), Xc, u, v);
         out[0] = P.mono_obs[2 * e] - u;
         out[1] = P.mono_obs[2 * e + 1] - v;
+    }
+    // EdgeStereo::computeError (G2oTypes.h:364-380): obs - ProjectStereo(X, 0) (G2oTypes.cc:198-205)
+    void stereo_error(int e, double out[3]) const {
+        const int k = P.stereo_kf[e];
+        const V3 Xc = add(mul(pose[k].Rcw[0], pts[P.stereo_pt[e]]), pose[k].tcw[0]);
+        double u, v;
+        kb8_project(camk(0), Xc, u, v);
+        const double invZ = 1 / Xc[2];
+        const double ur = u - (double)P.bf * invZ;
+        out[0] = P.stereo_obs[3 * e] - u;
+        out[1] = P.stereo_obs[3 * e + 1] - v;
+        out[2] = P.stereo_obs[3 * e + 2] - ur;
+    }
+    double stereo_chi2(int e) const {
+        const double w = (double)P.stereo_inv_sigma2[e];
+        const double *r = &e_st[3 * e];
+        return r[0] * w * r[0] + r[1] * w * r[1] + r[2] * w * r[2];
     }
     void bias_floats(int k, float b1[6]) const {   // IMU::Bias(ba, bg) as floats
         for (int q = 0; q < 3; ++q) b1[q] = (float)ba[k][q], b1[3 + q] = (float)bg[k][q];
@@ -463,6 +486,7 @@ struct Solver {
     }
     void compute_errors() {
         for (int e = 0; e < P.n_mono; ++e) mono_error(e, &e_mono[2 * e]);
+        for (int e = 0; e < NS; ++e) stereo_error(e, &e_st[3 * e]);
         for (int i = 0; i < P.n_imu; ++i) {
             imu_error(i, &e_imu[9 * i]);
             e_gr[i] = sub(bg[P.imu_kf2[i]], bg[P.imu_kf1[i]]);
@@ -515,6 +539,10 @@ struct Solver {
             huber(mono_chi2(e), delta_mono, dsqr_mono, rho);
             chi += rho[0];
         }
+        for (int e = 0; e < NS; ++e) {
+            huber(stereo_chi2(e), delta_st, dsqr_st, rho);
+            chi += rho[0];
+        }
         return chi;
     }
 
@@ -536,6 +564,29 @@ struct Solver {
             for (int q = 0; q < 3; ++q)
                 pr[3 * r + q] = pj[3 * r] * Rcb[c](0, q) + pj[3 * r + 1] * Rcb[c](1, q) + pj[3 * r + 2] * Rcb[c](2, q);
         for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 6; ++q)
+                JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    }
+    // EdgeStereo::linearizeOplus (G2oTypes.cc:402-431): proj_jac row 2 = row 0 with (2,2) += bf / z^2
+    void stereo_jac(int e, double JX[9], double JP[18]) const {
+        const int k = P.stereo_kf[e], c = 0;
+        const M3 &Rcw = pose[k].Rcw[c];
+        const V3 Xc = add(mul(Rcw, pts[P.stereo_pt[e]]), pose[k].tcw[c]);
+        const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
+        double pj[9];
+        kb8_jac(camk(c), Xc, pj);
+        const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+        pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + (double)P.bf * inv_z2;
+        for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q)
+                JX[3 * r + q] = -(pj[3 * r] * Rcw(0, q) + pj[3 * r + 1] * Rcw(1, q) + pj[3 * r + 2] * Rcw(2, q));
+        const double x = Xb[0], y = Xb[1], z = Xb[2];
+        const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+        double pr[9];
+        for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q)
+                pr[3 * r + q] = pj[3 * r] * Rcb[c](0, q) + pj[3 * r + 1] * Rcb[c](1, q) + pj[3 * r + 2] * Rcb[c](2, q);
+        for (int r = 0; r < 3; ++r)
             for (int q = 0; q < 6; ++q)
                 JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
     }
@@ -698,6 +749,37 @@ struct Solver {
             for (int r = 0; r < 6; ++r)
                 for (int c = 0; c < 3; ++c) B[3 * r + c] += w * (JP[r] * JX[c] + JP[6 + r] * JX[3 + c]);
         }
+        // EdgeStereo: 3 residual rows; the third row's terms are added after the first two
+        for (int e = 0; e < NS; ++e) {
+            double JX[9], JP[18];
+            stereo_jac(e, JX, JP);
+            huber(stereo_chi2(e), delta_st, dsqr_st, rho);
+            const double wi = (double)P.stereo_inv_sigma2[e];
+            const double w = wi * rho[1];
+            const double om[3] = {-wi * e_st[3 * e] * rho[1], -wi * e_st[3 * e + 1] * rho[1], -wi * e_st[3 * e + 2] * rho[1]};
+            auto rows = [](const double *A, int ia, const double *B, int ib, int lda, int ldb) {
+                return A[ia] * B[ib] + A[lda + ia] * B[ldb + ib] + A[2 * lda + ia] * B[2 * ldb + ib];
+            };
+            auto rows_om = [&](const double *A, int ia, int lda) {
+                return A[ia] * om[0] + A[lda + ia] * om[1] + A[2 * lda + ia] * om[2];
+            };
+            Landmark &L = lm[P.stereo_pt[e]];
+            for (int r = 0; r < 3; ++r) {
+                L.bl[r] += rows_om(JX, r, 3);
+                for (int c = 0; c < 3; ++c) L.Hll[3 * r + c] += w * rows(JX, r, JX, c, 3, 3);
+            }
+            const int k = P.stereo_kf[e];
+            const int o = offP[k];
+            if (o < 0) continue;
+            for (int r = 0; r < 6; ++r) {
+                b[o + r] += rows_om(JP, r, 6);
+                for (int c = 0; c < 6; ++c) H[(size_t)(o + r) * nred + o + c] += w * rows(JP, r, JP, c, 6, 6);
+            }
+            std::vector<double> &B = L.Hpl[k];
+            if (B.empty()) B.assign(18, 0.0);
+            for (int r = 0; r < 6; ++r)
+                for (int c = 0; c < 3; ++c) B[3 * r + c] += w * rows(JP, r, JX, c, 6, 3);
+        }
     }
 
     // --- one LM trial: damped Schur solve; x = [poses | landmarks] ---
@@ -837,9 +919,19 @@ extern "C" {
 
 // Residuals and Jacobians at the given state (parity of the edge math).
 int oracle_lba_evaluate(const omv_lba_problem *p, double *mono_err, double *mono_jx, double *mono_jp,
-                        double *imu_err, double *imu_jac /* [n_imu][9*24] v = P1 V1 G1 A1 P2 V2 */) {
+                        double *imu_err, double *imu_jac /* [n_imu][9*24] v = P1 V1 G1 A1 P2 V2 */,
+                        double *st_err, double *st_jx, double *st_jp /* [n_stereo][3 | 9 | 18] */) {
     Solver s(*p);
     s.compute_errors();
+    for (int e = 0; e < s.NS; ++e) {
+        if (st_err) std::memcpy(st_err + 3 * e, &s.e_st[3 * e], 24);
+        if (st_jx || st_jp) {
+            double JX[9], JP[18];
+            s.stereo_jac(e, JX, JP);
+            if (st_jx) std::memcpy(st_jx + 9 * e, JX, 72);
+            if (st_jp) std::memcpy(st_jp + 18 * e, JP, 144);
+        }
+    }
     for (int e = 0; e < p->n_mono; ++e) {
         if (mono_err) mono_err[2 * e] = s.e_mono[2 * e], mono_err[2 * e + 1] = s.e_mono[2 * e + 1];
         if (mono_jx || mono_jp) {
@@ -940,6 +1032,11 @@ int oracle_lba_optimize(omv_lba_problem *p, const omv_lba_opts *o, omv_lba_resul
             const bool depth_pos = (R(2, 0) * X[0] + R(2, 1) * X[1] + R(2, 2) * X[2] + s.pose[k].tcw[cam][2]) > 0.0;
             r->mono_outlier[e] = ((c > 5.991f && !close) || (c > 1.5f * 5.991f && close) || !depth_pos) ? 1 : 0;
         }
+    }
+    for (int e = 0; e < s.NS; ++e) {   // :3299-3311
+        const double c = s.stereo_chi2(e);
+        if (r->stereo_chi2) r->stereo_chi2[e] = c;
+        if (r->stereo_outlier) r->stereo_outlier[e] = c > 7.815f ? 1 : 0;
     }
     const bool fail = (2 * r->err < r->err_end || std::isnan(r->err) || std::isnan(r->err_end)) && !o->large;
     r->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;

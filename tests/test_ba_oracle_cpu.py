@@ -129,3 +129,54 @@ def test_noise_free_window_recovers_the_truth(oracle):
     dR = np.einsum("kji,kjl->kil", st["Rwb"][:n], t["Rwb"][:n])
     ang = np.arccos(np.clip((np.trace(dR, axis1=1, axis2=2) - 1) / 2, -1, 1))
     assert ang.max() < np.deg2rad(0.05)
+
+
+@pytest.fixture(scope="module")
+def prob_st():
+    return synth_ba.make_lba_problem(n_kf=12, n_opt=6, n_pts=300, seed=21, stereo_frac=0.5)
+
+
+def test_stereo_window_shape(prob_st, prob):
+    """stereo_frac moves camera-0 observations into EdgeStereo without touching the rest of the window."""
+    assert prob_st["n_stereo"] > 50
+    assert len(prob_st["mono_pt"]) + prob_st["n_stereo"] == len(prob["mono_pt"])
+    for k in ("Rwb", "twb", "pts", "vel"):
+        assert np.array_equal(prob_st[k], prob[k])
+
+
+def test_stereo_jacobians_match_finite_differences(prob_st, oracle):
+    """EdgeStereo::linearizeOplus (G2oTypes.cc:402-431) vs central differences of computeError
+    (obs - ProjectStereo, G2oTypes.cc:198-205)."""
+    ev = oracle.lba_evaluate(prob_st)
+    S = prob_st["n_stereo"]
+    rng = np.random.default_rng(1)
+    h = 1e-3
+    for e in rng.choice(S, 25, replace=False):
+        pt, k = prob_st["stereo_pt"][e], prob_st["stereo_kf"][e]
+        fd = np.zeros((3, 3))
+        for a in range(3):
+            pp, pm = dict(prob_st), dict(prob_st)
+            pp["pts"], pm["pts"] = prob_st["pts"].copy(), prob_st["pts"].copy()
+            pp["pts"][pt, a] += h
+            pm["pts"][pt, a] -= h
+            fd[:, a] = (oracle.lba_evaluate(pp)["stereo_err"][e] - oracle.lba_evaluate(pm)["stereo_err"][e]) / (2 * h)
+        jx = ev["stereo_jx"][e].reshape(3, 3)
+        assert np.abs(jx - fd).max() <= 2e-3 * np.abs(jx).max() + 1e-3, (e, jx, fd)
+        if k >= prob_st["n_opt"]:
+            continue
+        fdp = np.zeros((3, 6))
+        for a in range(6):
+            d = np.zeros(6)
+            d[a] = h if a >= 3 else h * 1e-1
+            ep = oracle.lba_evaluate(_pose_oplus(prob_st, k, d))["stereo_err"][e]
+            em = oracle.lba_evaluate(_pose_oplus(prob_st, k, -d))["stereo_err"][e]
+            fdp[:, a] = (ep - em) / (2 * d[a])
+        jp = ev["stereo_jp"][e].reshape(3, 6)
+        assert np.abs(jp - fdp).max() <= 5e-3 * np.abs(jp).max() + 1e-2, (e, jp, fdp)
+
+
+def test_stereo_window_optimises(prob_st, oracle):
+    res, st, _ = oracle.lba_optimize(prob_st, opt_it=10, lambda_init=1e0, max_trials=10, large=False)
+    assert res["status"] == 0 and res["err_end"] < 0.2 * res["err"]
+    # stereo residuals at the optimum are at the noise level (0.7 px per row)
+    assert np.median(res["stereo_chi2"] / np.asarray(prob_st["stereo_inv_sigma2"], np.float64)) < 3 * 0.7 ** 2 * 3

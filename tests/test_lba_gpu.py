@@ -34,7 +34,8 @@ def full():
 
 def _solver(prob):
     return LocalInertialBA(max_kf=prob["n_kf"], max_cams=prob["n_cams"], max_pts=len(prob["pts"]),
-                           max_mono=len(prob["mono_pt"]), max_imu=max(1, len(prob["imu_kf1"])))
+                           max_mono=len(prob["mono_pt"]) + int(prob.get("n_stereo", 0)),
+                           max_imu=max(1, len(prob["imu_kf1"])))
 
 
 def _compare_state(prob, st_g, st_o, oracle, rel=1e-5):
@@ -56,6 +57,10 @@ def _compare_state(prob, st_g, st_o, oracle, rel=1e-5):
     w = np.asarray(prob["mono_inv_sigma2"], np.float64)
     H = np.zeros((len(d), 3, 3))
     np.add.at(H, prob["mono_pt"], w[:, None, None] * np.einsum("eri,erj->eij", jx, jx))
+    if prob.get("n_stereo", 0):
+        sx = oracle.lba_evaluate(fin)["stereo_jx"].reshape(-1, 3, 3)
+        ws = np.asarray(prob["stereo_inv_sigma2"], np.float64)
+        np.add.at(H, prob["stereo_pt"], ws[:, None, None] * np.einsum("eri,erj->eij", sx, sx))
     maha = np.sqrt(np.maximum(np.einsum("pi,pij,pj->p", d, H, d), 0))
     assert maha.max() <= 1e-3, (maha.max(), int(np.argmax(maha)))
     step = np.abs(st_o["pts"] - np.asarray(prob["pts"])).max(axis=1)
@@ -76,6 +81,13 @@ def _compare_result(prob, rg, ro):
     if diff.any():
         near = np.minimum(np.abs(c - 5.991), np.abs(c - 1.5 * 5.991)) <= tol
         assert near[diff].all(), (int(diff.sum()), c[diff & ~near][:5])
+    if len(ro.get("stereo_chi2", ())):
+        c = ro["stereo_chi2"]
+        tol = _chi2_tol(c)
+        bad = np.abs(rg["stereo_chi2"] - c) > tol
+        assert not bad.any(), (int(bad.sum()), rg["stereo_chi2"][bad][:5], c[bad][:5])
+        diff = rg["stereo_outlier"] != ro["stereo_outlier"]
+        assert (np.abs(c[diff] - 7.815) <= tol[diff]).all()
 
 
 def _chi2_tol(chi2):
@@ -104,6 +116,31 @@ def test_optimize_small(small, oracle, large):
     rg, sg = _solver(small).set_problem(small).optimize(max_trials=10, large=large, **kw)
     _compare_result(small, rg, ro)
     _compare_state(small, sg, so, oracle)
+
+
+@pytest.fixture(scope="module")
+def small_st():
+    return synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11, stereo_frac=0.5)
+
+
+def test_stereo_residuals_and_jacobians(small_st, oracle):
+    """EdgeStereo (G2oTypes.cc:402-431) on the device vs the oracle: same bar as EdgeMono."""
+    g = _solver(small_st).set_problem(small_st).evaluate()
+    o = oracle.lba_evaluate(small_st)
+    assert small_st["n_stereo"] > 500
+    assert np.abs(g["stereo_err"] - o["stereo_err"]).max() <= 1e-9
+    assert np.abs(g["mono_err"] - o["mono_err"]).max() <= 1e-9
+    for k in ("stereo_jx", "stereo_jp", "mono_jx", "mono_jp"):
+        assert np.abs(g[k] - o[k]).max() <= 1e-9 * np.abs(o[k]).max(), k
+
+
+@pytest.mark.parametrize("large", [True, False])
+def test_optimize_with_stereo_edges(small_st, oracle, large):
+    kw = dict(opt_it=4, lambda_init=1e-2) if large else dict(opt_it=10, lambda_init=1e0)
+    ro, so, _ = oracle.lba_optimize(small_st, max_trials=10, large=large, **kw)
+    rg, sg = _solver(small_st).set_problem(small_st).optimize(max_trials=10, large=large, **kw)
+    _compare_result(small_st, rg, ro)
+    _compare_state(small_st, sg, so, oracle)
 
 
 def test_optimize_visual_only_with_fixed_only_points(oracle):
