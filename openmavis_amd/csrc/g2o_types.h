@@ -1,0 +1,381 @@
+// Device-side restatement of the g2o vertex / edge math OpenMAVIS defines in src/G2oTypes.cc and
+// include/G2oTypes.h (ImuCamPose, KannalaBrandt8 projection, EdgeMono / EdgeStereo rows, EdgeInertial
+// with IMU::Preintegrated's bias-corrected deltas, Huber), shared by the LocalInertialBA kernels
+// (lba.hip) and the batched pose-inertial optimisation (pose.hip).  Header-only, f64 unless the
+// reference computes in float (marked where it does).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/omv.h"
+#include "omv_device.h"
+
+namespace omv_g2o {
+
+constexpr int kMaxCams = 8;
+constexpr int kPF = OMV_PREINT_FLOATS;
+
+using omv::glibc_atan2f;
+using omv::sqrtf_cr;
+
+// ---- small f64 helpers (row-major 3x3) ----------------------------------------------------------
+struct D3 {
+    double v[3];
+};
+__device__ __forceinline__ void mv3(const double *R, const double *x, double *y) {
+    for (int i = 0; i < 3; ++i) y[i] = R[3 * i] * x[0] + R[3 * i + 1] * x[1] + R[3 * i + 2] * x[2];
+}
+__device__ __forceinline__ void mtv3(const double *R, const double *x, double *y) {   // R^T x
+    for (int i = 0; i < 3; ++i) y[i] = R[i] * x[0] + R[3 + i] * x[1] + R[6 + i] * x[2];
+}
+__device__ __forceinline__ void mm3(const double *a, const double *b, double *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+__device__ __forceinline__ void mtm3(const double *a, const double *b, double *r) {   // a^T b
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[i] * b[j] + a[3 + i] * b[3 + j] + a[6 + i] * b[6 + j];
+}
+__device__ __forceinline__ void tr3(const double *a, double *r) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * j + i];
+}
+__device__ __forceinline__ void hat3(const double *w, double *W) {
+    W[0] = 0, W[1] = -w[2], W[2] = w[1], W[3] = w[2], W[4] = 0, W[5] = -w[0], W[6] = -w[1], W[7] = w[0], W[8] = 0;
+}
+template <typename T>
+__host__ __device__ inline bool inv3(const T *a, T *r) {
+    T c[9];
+    c[0] = a[4] * a[8] - a[5] * a[7];
+    c[1] = a[2] * a[7] - a[1] * a[8];
+    c[2] = a[1] * a[5] - a[2] * a[4];
+    c[3] = a[5] * a[6] - a[3] * a[8];
+    c[4] = a[0] * a[8] - a[2] * a[6];
+    c[5] = a[2] * a[3] - a[0] * a[5];
+    c[6] = a[3] * a[7] - a[4] * a[6];
+    c[7] = a[1] * a[6] - a[0] * a[7];
+    c[8] = a[0] * a[4] - a[1] * a[3];
+    const T det = a[0] * c[0] + a[1] * c[3] + a[2] * c[6];
+    const T id = T(1) / det;
+    for (int k = 0; k < 9; ++k) r[k] = c[k] * id;
+    return det != T(0);
+}
+// NormalizeRotation (Eigen JacobiSVD U V^T) = polar factor, by Newton iteration X <- (X + X^-T)/2
+template <typename T>
+__host__ __device__ inline void polar3(T *r) {
+    for (int it = 0; it < 20; ++it) {
+        T c[9];
+        c[0] = r[4] * r[8] - r[5] * r[7];
+        c[1] = r[5] * r[6] - r[3] * r[8];
+        c[2] = r[3] * r[7] - r[4] * r[6];
+        c[3] = r[2] * r[7] - r[1] * r[8];
+        c[4] = r[0] * r[8] - r[2] * r[6];
+        c[5] = r[1] * r[6] - r[0] * r[7];
+        c[6] = r[1] * r[5] - r[2] * r[4];
+        c[7] = r[2] * r[3] - r[0] * r[5];
+        c[8] = r[0] * r[4] - r[1] * r[3];
+        const T det = r[0] * c[0] + r[1] * c[1] + r[2] * c[2];
+        const T id = T(1) / det;
+        T diff = 0;
+        for (int k = 0; k < 9; ++k) {
+            const T nv = (r[k] + c[k] * id) * T(0.5);
+            const T dd = nv > r[k] ? nv - r[k] : r[k] - nv;
+            diff = dd > diff ? dd : diff;
+            r[k] = nv;
+        }
+        if (diff <= (sizeof(T) == 4 ? T(2.5e-7) : T(5e-16))) break;   // within ~2 ulp of a fixed point
+    }
+}
+
+// ---- camera + pose math -------------------------------------------------------------------------
+struct Rig {
+    int n_cams;
+    float cam[kMaxCams][8];
+    double Rcb[kMaxCams][9], tcb[kMaxCams][3], Rbc[kMaxCams][9], tbc[kMaxCams][3];
+    double bf;   // ImuCamPose::bf = KeyFrame::mbf (EdgeStereo)
+};
+
+// KannalaBrandt8::project(const Eigen::Vector3d&) (KannalaBrandt8.cpp:28-46)
+__device__ __forceinline__ void kb8_project(const float *k, const double *X, double &u, double &v) {
+    const double x2y2 = X[0] * X[0] + X[1] * X[1];
+    const double theta = glibc_atan2f(sqrtf_cr((float)x2y2), (float)X[2]);
+    const double psi = glibc_atan2f((float)X[1], (float)X[0]);
+    const double t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const double r = theta + (double)k[4] * t3 + (double)k[5] * t5 + (double)k[6] * t7 + (double)k[7] * t9;
+    u = (double)k[0] * r * cos(psi) + (double)k[2];
+    v = (double)k[1] * r * sin(psi) + (double)k[3];
+}
+// KannalaBrandt8::projectJac (:128-158), 2x3 row-major
+__device__ __forceinline__ void kb8_jac(const float *k, const double *X, double *J) {
+    const double x2 = X[0] * X[0], y2 = X[1] * X[1], z2 = X[2] * X[2];
+    const double r2 = x2 + y2, r = sqrt(r2), r3 = r2 * r;
+    const double theta = atan2(r, X[2]);
+    const double t2 = theta * theta, t3 = t2 * theta, t4 = t2 * t2, t5 = t4 * theta, t6 = t2 * t4, t7 = t6 * theta,
+                 t8 = t4 * t4, t9 = t8 * theta;
+    const double k4 = k[4], k5 = k[5], k6 = k[6], k7 = k[7];
+    const double f = theta + t3 * k4 + t5 * k5 + t7 * k6 + t9 * k7;
+    // `3 * mvParameters[4]` is an int x float product in the reference: rounded to float first
+    const double fd = 1 + (double)(3.0f * k[4]) * t2 + (double)(5.0f * k[5]) * t4 + (double)(7.0f * k[6]) * t6 +
+                      (double)(9.0f * k[7]) * t8;
+    const double q = r2 * (r2 + z2);
+    J[0] = (double)k[0] * (fd * X[2] * x2 / q + f * y2 / r3);
+    J[3] = (double)k[1] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
+    J[1] = (double)k[0] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
+    J[4] = (double)k[1] * (fd * X[2] * y2 / q + f * x2 / r3);
+    J[2] = -(double)k[0] * fd * X[0] / (r2 + z2);
+    J[5] = -(double)k[1] * fd * X[1] / (r2 + z2);
+}
+
+struct State {   // one of the two state buffers
+    double *Rwb, *twb, *Rcw, *tcw, *vel, *bg, *ba, *pts;
+};
+
+struct Edges {   // landmark-major visual edges (EdgeMono, and EdgeStereo where ur >= 0)
+    const int32_t *pt, *kf, *cam, *slot;
+    const double *obs;
+    const float *w;    // invSigma2
+    const float *ur;   // EdgeStereo's third measurement (mvuRight >= 0); -1 on an EdgeMono
+    int n;
+};
+
+// ImuCamPose::ProjectStereo's third row (G2oTypes.cc:198-205): u - bf * (1 / z)
+__device__ __forceinline__ double stereo_ur(double u, double bf, double z) {
+    const double invZ = 1 / z;
+    return u - bf * invZ;
+}
+
+// Huber (robust_kernel_impl.cpp:78-91)
+__device__ __forceinline__ void huber(double e2, double delta, double dsqr, double &r0, double &r1) {
+    if (e2 <= dsqr) {
+        r0 = e2, r1 = 1.0;
+    } else {
+        const double s = sqrt(e2);
+        r0 = 2 * s * delta - dsqr;
+        r1 = delta / s;
+    }
+}
+
+// ---- errors ------------------------------------------------------------------------------------
+__device__ double block_reduce_sum(double v, double *sh) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0;
+    for (int q = 0; q < nw; ++q) t += sh[q];
+    return t;
+}
+
+struct Imu {
+    int n;
+    const int32_t *kf1, *kf2;
+    const float *pre;        // [n][kPF]
+    const double *info9;     // [n][81] (scaled)
+    const double *infoG, *infoA;   // [n][9]
+    const uint8_t *robust;
+    const int *offP, *offV, *offG, *offA;   // per keyframe, -1 if not in the reduced system
+};
+
+// IMU::Preintegrated::GetDeltaRotation/Velocity/Position (ImuTypes.cc:288-309) in float
+__device__ void so3f_exp(const float *w, float *R) {
+    const float theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    float imag, real;
+    if (theta_sq < 1e-5f * 1e-5f) {
+        const float t4 = theta_sq * theta_sq;
+        imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * t4;
+        real = 1.0f - (float)(1.0 / 8.0) * theta_sq + (float)(1.0 / 384.0) * t4;
+    } else {
+        const float theta = sqrtf_cr(theta_sq);
+        const float half = 0.5f * theta;
+        float sh, ch;
+        omv::glibc_sincosf(half, &sh, &ch);
+        imag = sh / theta;
+        real = ch;
+    }
+    const float qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    R[0] = 1.0f - (tyy + tzz), R[1] = txy - twz, R[2] = txz + twy;
+    R[3] = txy + twz, R[4] = 1.0f - (txx + tzz), R[5] = tyz - twx;
+    R[6] = txz - twy, R[7] = tyz + twx, R[8] = 1.0f - (txx + tyy);
+}
+__device__ void f33mulv(const float *a, const float *x, float *r) {
+    for (int i = 0; i < 3; ++i) r[i] = a[3 * i] * x[0] + a[3 * i + 1] * x[1] + a[3 * i + 2] * x[2];
+}
+struct PreView {   // offsets inside one preintegration record
+    static constexpr int dR = 0, dV = 9, dP = 12, JRg = 15, JVg = 24, JVa = 33, JPg = 42, JPa = 51, b = 60, dT = 66,
+                         C = 67;
+};
+__device__ void delta_rot(const float *p, const float *b1, double *dR) {
+    const float dbg[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    float w[3], E[9], R[9];
+    f33mulv(p + PreView::JRg, dbg, w);
+    so3f_exp(w, E);
+    const float *A = p + PreView::dR;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = A[3 * i] * E[j] + A[3 * i + 1] * E[3 + j] + A[3 * i + 2] * E[6 + j];
+    polar3(R);
+    for (int q = 0; q < 9; ++q) dR[q] = (double)R[q];
+}
+__device__ void delta_vp(const float *p, int d, int jg, int ja, const float *b1, double *out) {
+    const float dbg[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    const float dba[3] = {b1[0] - p[PreView::b], b1[1] - p[PreView::b + 1], b1[2] - p[PreView::b + 2]};
+    float g[3], a[3];
+    f33mulv(p + jg, dbg, g);
+    f33mulv(p + ja, dba, a);
+    for (int q = 0; q < 3; ++q) out[q] = (double)((p[d + q] + g[q]) + a[q]);
+}
+__device__ void log_so3(const double *R, double *w) {
+    const double t = R[0] + R[4] + R[8];
+    w[0] = (R[7] - R[5]) / 2, w[1] = (R[2] - R[6]) / 2, w[2] = (R[3] - R[1]) / 2;
+    const double costheta = (t - 1.0) * 0.5f;
+    if (costheta > 1 || costheta < -1) return;
+    const double theta = acos(costheta);
+    const double s = sin(theta);
+    if (fabs(s) < 1e-5) return;
+    for (int q = 0; q < 3; ++q) w[q] = theta * w[q] / s;
+}
+
+// EdgeInertial::computeError (G2oTypes.cc:502-531)
+__device__ void imu_error(const State &s, const Imu &I, int i, double *e) {
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const float *p = I.pre + (size_t)i * kPF;
+    float b1[6];
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+    double dR[9], dV[3], dP[3];
+    delta_rot(p, b1, dR);
+    delta_vp(p, PreView::dV, PreView::JVg, PreView::JVa, b1, dV);
+    delta_vp(p, PreView::dP, PreView::JPg, PreView::JPa, b1, dP);
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    const double *R1 = s.Rwb + 9 * k1, *R2 = s.Rwb + 9 * k2;
+    double A[9], B[9];
+    double R1t[9];
+    tr3(R1, R1t);
+    double dRt[9];
+    tr3(dR, dRt);
+    mm3(dRt, R1t, A);
+    mm3(A, R2, B);
+    log_so3(B, e);
+    double t[3];
+    for (int q = 0; q < 3; ++q) t[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+    double ev[3];
+    mtv3(R1, t, ev);
+    for (int q = 0; q < 3; ++q) e[3 + q] = ev[q] - dV[q];
+    for (int q = 0; q < 3; ++q)
+        t[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - g[q] * dt * dt / 2;
+    mtv3(R1, t, ev);
+    for (int q = 0; q < 3; ++q) e[6 + q] = ev[q] - dP[q];
+}
+
+__device__ void inv_right_jac(const double *v, double *J) {
+    const double d2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double d = sqrt(d2);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) J[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double W[9], WW[9];
+    hat3(v, W);
+    mm3(W, W, WW);
+    const double k = 1.0 / d2 - (1.0 + cos(d)) / (2.0 * d * sin(d));
+    for (int q = 0; q < 9; ++q) J[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] / 2 + WW[q] * k;
+}
+__device__ void right_jac(const double *v, double *J) {
+    const double d2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double d = sqrt(d2);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) J[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double W[9], WW[9];
+    hat3(v, W);
+    mm3(W, W, WW);
+    for (int q = 0; q < 9; ++q)
+        J[q] = ((q % 4 == 0) ? 1.0 : 0.0) - W[q] * (1.0 - cos(d)) / d2 + WW[q] * (d - sin(d)) / (d2 * d);
+}
+
+// EdgeInertial::linearizeOplus (G2oTypes.cc:533-599): J [9][24], columns P1(6) V1 G1 A1 P2(6) V2
+__device__ void imu_jacobian(const State &s, const Imu &I, int i, double *J) {
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const float *p = I.pre + (size_t)i * kPF;
+    float b1[6];
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+    const float dbgf[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+    const double dbg[3] = {(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]};
+    const double *Rwb1 = s.Rwb + 9 * k1, *Rwb2 = s.Rwb + 9 * k2;
+    double Rbw1[9];
+    tr3(Rwb1, Rbw1);
+    double dR[9], dRt[9], t1[9], eR[9], er[3], invJr[9];
+    delta_rot(p, b1, dR);
+    tr3(dR, dRt);
+    mm3(dRt, Rbw1, t1);
+    mm3(t1, Rwb2, eR);
+    log_so3(eR, er);
+    inv_right_jac(er, invJr);
+    double JRg[9], JVg[9], JPg[9], JVa[9], JPa[9];
+    for (int q = 0; q < 9; ++q) {
+        JRg[q] = p[PreView::JRg + q], JVg[q] = p[PreView::JVg + q], JPg[q] = p[PreView::JPg + q];
+        JVa[q] = p[PreView::JVa + q], JPa[q] = p[PreView::JPa + q];
+    }
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    for (int q = 0; q < 216; ++q) J[q] = 0;
+    auto put = [&](int r0, int c0, const double *B, double sgn) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) J[(r0 + r) * 24 + c0 + c] = sgn * B[3 * r + c];
+    };
+    double R2t[9], A[9], B[9], W[9], v[3], w[3];
+    tr3(Rwb2, R2t);
+    mm3(invJr, R2t, A);
+    mm3(A, Rwb1, B);
+    put(0, 0, B, -1.0);
+    for (int q = 0; q < 3; ++q) v[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+    mv3(Rbw1, v, w);
+    hat3(w, W);
+    put(3, 0, W, 1.0);
+    for (int q = 0; q < 3; ++q)
+        v[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - 0.5 * g[q] * dt * dt;
+    mv3(Rbw1, v, w);
+    hat3(w, W);
+    put(6, 0, W, 1.0);
+    for (int q = 0; q < 3; ++q) J[(6 + q) * 24 + 3 + q] = -1.0;
+    put(3, 6, Rbw1, -1.0);
+    put(6, 6, Rbw1, -dt);
+    double eRt[9], Jg[9], RJ[9], w3[3];
+    tr3(eR, eRt);
+    mv3(JRg, dbg, w3);
+    right_jac(w3, RJ);
+    mm3(invJr, eRt, A);
+    mm3(A, RJ, B);
+    mm3(B, JRg, Jg);
+    put(0, 9, Jg, -1.0);
+    put(3, 9, JVg, -1.0);
+    put(6, 9, JPg, -1.0);
+    put(3, 12, JVa, -1.0);
+    put(6, 12, JPa, -1.0);
+    put(0, 15, invJr, 1.0);
+    mm3(Rbw1, Rwb2, A);
+    put(6, 18, A, 1.0);
+    put(3, 21, Rbw1, 1.0);
+}
+
+__device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:802-815)
+    const double x = w[0], y = w[1], z = w[2];
+    const double d2 = x * x + y * y + z * z;
+    const double d = sqrt(d2);
+    double W[9], WW[9];
+    hat3(w, W);
+    mm3(W, W, WW);
+    if (d < 1e-5) {
+        for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] + 0.5 * WW[q];
+    } else {
+        const double s = sin(d), c = cos(d);
+        for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] * s / d + WW[q] * (1.0 - c) / d2;
+    }
+    polar3(R);
+}
+
+}  // namespace omv_g2o
