@@ -347,6 +347,56 @@ omv_status omv_lba_set_comm(omv_lba *h, int rank, int world, omv_allreduce_fn al
  * indices of its landmarks.  Any pointer may be NULL. */
 omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *pt_index);
 
+/* ------------------------------------------------------------------------------------------------
+ * Pose-inertial optimisation of tracked frames — replaces Optimizer::PoseInertialOptimizationLastKeyFrame
+ * (src/Optimizer.cc:5021-5578): Gauss-Newton (4 rounds x 10 iterations, dense LDLT) over the frame's
+ * VertexPose / VertexVelocity / VertexGyroBias / VertexAccBias with the last keyframe's vertices fixed;
+ * EdgeMonoOnlyPose (G2oTypes.h:330-362, G2oTypes.cc:382-400) and EdgeStereoOnlyPose (:404-431,
+ * :433-456) per matched keypoint, one EdgeInertial + EdgeGyroRW + EdgeAccRW; the outlier
+ * classification between rounds (chi2 thresholds 12 / 7.5 / 5.991 / 5.991, stereo 15.6 / 9.8 / 7.815 /
+ * 7.815, robust kernels dropped after round 3), the "recover not too bad points" pass, and the
+ * marginal Hessian the reference stores in Frame::mpcpi.  A batch of frames runs in one launch
+ * (one workgroup per frame).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct omv_pose_batch {
+    int n_frames;
+    /* rig (as omv_lba_problem): per camera KannalaBrandt8 parameters and body <-> camera */
+    int n_cams;
+    const float *cam;                   /* host [n_cams][8] */
+    const double *Rcb, *tcb, *Rbc, *tbc;   /* host [n_cams][9] / [3] */
+    float bf;                           /* Frame::mbf (EdgeStereoOnlyPose) */
+    /* device: frame state (in/out) — ImuCamPose(Frame*) (G2oTypes.cc:74-133) */
+    double *Rwb, *twb;                  /* [F][9], [F][3] */
+    double *Rcw, *tcw;                  /* [F][n_cams][9], [F][n_cams][3] initial camera poses, updated */
+    double *vel, *bg, *ba;              /* [F][3] */
+    /* device: Frame::mpLastKeyFrame's vertices (fixed) */
+    const double *kf_Rwb, *kf_twb, *kf_vel, *kf_bg, *kf_ba;
+    const float *preint;                /* [F][OMV_PREINT_FLOATS] Frame::mpImuPreintegrated */
+    /* device: visual edges, frame-major (edges of frame f: [start[f], start[f+1])) */
+    const int32_t *mono_start;          /* [F+1] */
+    const int32_t *mono_cam, *mono_kp;  /* camera index, keypoint index i of the frame (mvbOutlier[i]) */
+    const double *mono_obs;             /* [E][2] */
+    const float *mono_inv_sigma2;       /* [E] mvInvLevelSigma2[octave] / uncertainty2 */
+    const float *mono_xw;               /* [E][3] MapPoint::GetWorldPos() */
+    const uint8_t *mono_close;          /* [E] MapPoint::mTrackDepth < 10 (bClose) */
+    const int32_t *stereo_start;        /* [F+1] (all zero: no stereo edges) */
+    const int32_t *stereo_cam, *stereo_kp;
+    const double *stereo_obs;           /* [S][3] (u, v, mvuRight) */
+    const float *stereo_inv_sigma2, *stereo_xw;
+    int kp_cap;                         /* per-frame stride of kp_outlier */
+    int n_mono, n_stereo;               /* edge totals of the batch (mono_start[F], stereo_start[F]) */
+} omv_pose_batch;
+
+typedef struct omv_pose omv_pose;
+omv_status omv_pose_create(int max_frames, int max_edges, omv_pose **out);
+omv_status omv_pose_destroy(omv_pose *h);
+/* PoseInertialOptimizationLastKeyFrame on every frame of the batch.  kp_outlier (device
+ * [F][kp_cap], Frame::mvbOutlier of the keypoints that carry an edge; others untouched), n_good
+ * (device [F], the return value nInitialCorrespondences - nBad), H (device [F][225] or NULL, the
+ * 15x15 Hessian of ConstraintPoseImu: pose 0-5, v 6-8, bg 9-11, ba 12-14).  Asynchronous. */
+omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
+                                     int32_t *n_good, double *H, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,6 +97,17 @@ class LbaProblem(ctypes.Structure):
                 ("stereo_inv_sigma2", ctypes.c_void_p), ("bf", ctypes.c_float)]
 
 
+class PoseBatch(ctypes.Structure):
+    """omv_pose_batch (include/omv.h)."""
+    _fields_ = [("n_frames", ctypes.c_int), ("n_cams", ctypes.c_int), ("cam", ctypes.c_void_p),
+                ("Rcb", ctypes.c_void_p), ("tcb", ctypes.c_void_p), ("Rbc", ctypes.c_void_p), ("tbc", ctypes.c_void_p),
+                ("bf", ctypes.c_float)] + [(n, ctypes.c_void_p) for n in (
+                    "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba",
+                    "preint", "mono_start", "mono_cam", "mono_kp", "mono_obs", "mono_inv_sigma2", "mono_xw",
+                    "mono_close", "stereo_start", "stereo_cam", "stereo_kp", "stereo_obs", "stereo_inv_sigma2",
+                    "stereo_xw")] + [("kp_cap", ctypes.c_int), ("n_mono", ctypes.c_int), ("n_stereo", ctypes.c_int)]
+
+
 class LbaOpts(ctypes.Structure):
     _fields_ = [("opt_it", ctypes.c_int), ("lambda_init", ctypes.c_double), ("max_trials", ctypes.c_int),
                 ("large", ctypes.c_int)]
@@ -159,6 +170,9 @@ SIGNATURES = {
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
     "omv_lba_reset": (_I, [_VP]),
     "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),
+    "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),
+    "omv_pose_destroy": (_I, [_VP]),
+    "omv_pose_inertial_last_kf": (_I, [_VP, ctypes.POINTER(PoseBatch), _I, _VP, _VP, _VP, _VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
 }
 

@@ -379,3 +379,151 @@ __device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:8
 }
 
 }  // namespace omv_g2o
+
+namespace omv_g2o {
+
+// EdgeInertial's information (ctor, G2oTypes.cc:486-495): Info = C[0:9,0:9]^-1, symmetrised, projected
+// onto its non-negative eigen-space (eigenvalues < 1e-12 zeroed) — Gauss-Jordan with partial pivoting and
+// cyclic Jacobi, the same arithmetic as the host path of lba.hip and the oracle.  Single thread.
+__device__ inline void inertial_info9(const float *C15, double *out) {
+    double A[81], I[81], V[81], w[9];
+    for (int r = 0; r < 9; ++r)
+        for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)C15[r * 15 + c], I[r * 9 + c] = r == c ? 1.0 : 0.0;
+    for (int c = 0; c < 9; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 9; ++r)
+            if (fabs(A[r * 9 + c]) > fabs(A[p * 9 + c])) p = r;
+        if (p != c)
+            for (int k = 0; k < 9; ++k) {
+                double t = A[p * 9 + k];
+                A[p * 9 + k] = A[c * 9 + k], A[c * 9 + k] = t;
+                t = I[p * 9 + k];
+                I[p * 9 + k] = I[c * 9 + k], I[c * 9 + k] = t;
+            }
+        const double d = A[c * 9 + c];
+        for (int k = 0; k < 9; ++k) A[c * 9 + k] /= d, I[c * 9 + k] /= d;
+        for (int r = 0; r < 9; ++r)
+            if (r != c && A[r * 9 + c] != 0) {
+                const double f = A[r * 9 + c];
+                for (int k = 0; k < 9; ++k) A[r * 9 + k] -= f * A[c * 9 + k], I[r * 9 + k] -= f * I[c * 9 + k];
+            }
+    }
+    for (int r = 0; r < 9; ++r)
+        for (int c = r + 1; c < 9; ++c) I[r * 9 + c] = I[c * 9 + r] = (I[r * 9 + c] + I[c * 9 + r]) / 2;
+    for (int q = 0; q < 81; ++q) V[q] = (q % 10 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+        for (int p = 0; p < 9; ++p)
+            for (int q = p + 1; q < 9; ++q) off += I[p * 9 + q] * I[p * 9 + q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < 9; ++p)
+            for (int q = p + 1; q < 9; ++q) {
+                const double apq = I[p * 9 + q];
+                if (apq == 0) continue;
+                const double th = (I[q * 9 + q] - I[p * 9 + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+                const double c = 1 / sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < 9; ++k) {
+                    const double akp = I[k * 9 + p], akq = I[k * 9 + q];
+                    I[k * 9 + p] = c * akp - s * akq, I[k * 9 + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    const double apk = I[p * 9 + k], aqk = I[q * 9 + k];
+                    I[p * 9 + k] = c * apk - s * aqk, I[q * 9 + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 9; ++k) {
+                    const double vkp = V[k * 9 + p], vkq = V[k * 9 + q];
+                    V[k * 9 + p] = c * vkp - s * vkq, V[k * 9 + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < 9; ++i) w[i] = I[i * 9 + i] < 1e-12 ? 0.0 : I[i * 9 + i];
+    for (int r = 0; r < 9; ++r)
+        for (int c = 0; c < 9; ++c) {
+            double s = 0;
+            for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
+            out[r * 9 + c] = s;
+        }
+}
+
+// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting; ldlt_inplace::unblocked) + LDLT::_solve_impl with
+// the D pseudo-inverse below DBL_MIN.  A is n x n row-major (destroyed).  Returns isPositive().
+template <int N>
+__device__ inline bool ldlt_pivot_solve(double *A, const double *b, double *x) {
+    int tr[N];
+    double temp[N];
+    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
+    bool found_zero = false;
+    for (int k = 0; k < N; ++k) {
+        int big = k;
+        for (int i = k + 1; i < N; ++i)
+            if (fabs(A[i * N + i]) > fabs(A[big * N + big])) big = i;
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; ++j) {
+                const double t = A[k * N + j];
+                A[k * N + j] = A[big * N + j], A[big * N + j] = t;
+            }
+            for (int i = big + 1; i < N; ++i) {
+                const double t = A[i * N + k];
+                A[i * N + k] = A[i * N + big], A[i * N + big] = t;
+            }
+            const double t = A[k * N + k];
+            A[k * N + k] = A[big * N + big], A[big * N + big] = t;
+            for (int i = k + 1; i < big; ++i) {
+                const double u = A[i * N + k];
+                A[i * N + k] = A[big * N + i], A[big * N + i] = u;
+            }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = A[j * N + j] * A[k * N + j];
+            double s = 0;
+            for (int j = 0; j < k; ++j) s += A[k * N + j] * temp[j];
+            A[k * N + k] -= s;
+            for (int i = k + 1; i < N; ++i) {
+                double t = 0;
+                for (int j = 0; j < k; ++j) t += A[i * N + j] * temp[j];
+                A[i * N + k] -= t;
+            }
+        }
+        const double akk = A[k * N + k];
+        const bool valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            for (int j = 0; j < N; ++j) tr[j] = j;
+            break;
+        }
+        if (valid)
+            for (int i = k + 1; i < N; ++i) A[i * N + k] /= akk;
+        if (!valid) found_zero = true;
+        if (sign == 1) {
+            if (akk < 0) sign = 3;
+        } else if (sign == 2) {
+            if (akk > 0) sign = 3;
+        } else if (sign == 0) {
+            if (akk > 0) sign = 1;
+            else if (akk < 0) sign = 2;
+        }
+    }
+    (void)found_zero;
+    if (!(sign == 1 || sign == 0)) return false;
+    double y[N];
+    for (int i = 0; i < N; ++i) y[i] = b[i];
+    for (int k = 0; k < N; ++k) {
+        const double t = y[k];
+        y[k] = y[tr[k]], y[tr[k]] = t;
+    }
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < i; ++j) y[i] -= A[i * N + j] * y[j];
+    for (int i = 0; i < N; ++i) y[i] = fabs(A[i * N + i]) > 2.2250738585072014e-308 ? y[i] / A[i * N + i] : 0.0;
+    for (int i = N - 1; i >= 0; --i)
+        for (int j = i + 1; j < N; ++j) y[i] -= A[j * N + i] * y[j];
+    for (int k = N - 1; k >= 0; --k) {
+        const double t = y[k];
+        y[k] = y[tr[k]], y[tr[k]] = t;
+    }
+    for (int i = 0; i < N; ++i) x[i] = y[i];
+    return true;
+}
+
+}  // namespace omv_g2o

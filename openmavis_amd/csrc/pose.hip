@@ -1,0 +1,502 @@
+// MI355X-native pose-inertial optimisation of tracked frames: Optimizer::PoseInertialOptimizationLastKeyFrame
+// (src/Optimizer.cc:5021-5578) for a batch of frames, one workgroup per frame.
+//
+// The reference builds a 4-vertex g2o graph per frame (VertexPose / VertexVelocity / VertexGyroBias /
+// VertexAccBias of the frame; the last keyframe's four vertices fixed), one EdgeMonoOnlyPose per matched
+// keypoint (plus an EdgeStereoOnlyPose where the keypoint has a right coordinate), one EdgeInertial, one
+// EdgeGyroRW and one EdgeAccRW, and runs 4 rounds of optimize(10) with Gauss-Newton and a dense LDLT
+// (BlockSolverX + LinearSolverDense), classifying outliers between rounds.  Here, per Gauss-Newton
+// iteration (optimization_algorithm_gauss_newton.cpp:50-95):
+//   errors + build   every thread walks its share of the frame's active visual edges: residual, chi2
+//                    (kept per edge: e->chi2() is the value of the last computeError), Huber weight,
+//                    the 2x6 / 3x6 Jacobian and its 21 + 6 normal-equation terms; a fixed-order
+//                    wavefront + LDS reduction (deterministic run to run)
+//   inertial         thread 0 linearises EdgeInertial (9x24, only the frame's pose / velocity columns
+//                    are free); 81 threads form its 9x9 J^T Omega J block and the gradient
+//   solve + update   thread 0: 15x15 LDLT with diagonal pivoting (Eigen::LDLT semantics), then
+//                    ImuCamPose::Update and the additive velocity / bias updates
+// Between rounds every thread classifies its edges (mono pass, then stereo pass: the keypoint flag is
+// shared and the stereo pass sees the mono pass's writes, as in the reference's two loops).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "../../include/omv.h"
+#include "g2o_types.h"
+#include "omv_device.h"
+
+namespace {
+
+using namespace omv_g2o;
+
+#define HIP_OK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "omv: %s failed: %s\n", #x, hipGetErrorString(e_));      \
+            return OMV_ERR_HIP;                                                      \
+        }                                                                            \
+    } while (0)
+
+constexpr int kPoseThreads = 256;
+constexpr int kPoseWaves = kPoseThreads / 64;
+constexpr int kNormal = 27;   // 21 upper-triangle terms of the 6x6 pose block + 6 gradient terms
+
+struct PoseArgs {
+    double *Rwb, *twb, *Rcw, *tcw, *vel, *bg, *ba;
+    const double *kRwb, *ktwb, *kvel, *kbg, *kba;
+    const float *preint;
+    const int32_t *m_start, *m_cam, *m_kp;
+    const double *m_obs;
+    const float *m_w, *m_xw;
+    const uint8_t *m_close;
+    const int32_t *s_start, *s_cam, *s_kp;
+    const double *s_obs;
+    const float *s_w, *s_xw;
+    int kp_cap;
+    double *chi2_m, *chi2_s;   // e->chi2() of the last computeError, per edge
+    uint8_t *act_m, *act_s;    // edge level 0 (active)
+    uint8_t *kp_out;           // Frame::mvbOutlier
+    int32_t *n_good;
+    double *H;
+    int rec_init;
+};
+
+// One visual edge of the frame (EdgeMonoOnlyPose or EdgeStereoOnlyPose).
+struct VEdge {
+    int cam, kp;
+    bool stereo;
+    double obs[3];
+    double w;
+    double X[3];
+};
+
+__device__ __forceinline__ VEdge load_edge(const PoseArgs &A, bool stereo, int e) {
+    VEdge v;
+    v.stereo = stereo;
+    if (!stereo) {
+        v.cam = A.m_cam[e], v.kp = A.m_kp[e];
+        v.obs[0] = A.m_obs[2 * e], v.obs[1] = A.m_obs[2 * e + 1], v.obs[2] = 0;
+        v.w = (double)A.m_w[e];
+        for (int q = 0; q < 3; ++q) v.X[q] = (double)A.m_xw[3 * e + q];
+    } else {
+        v.cam = A.s_cam[e], v.kp = A.s_kp[e];
+        for (int q = 0; q < 3; ++q) v.obs[q] = A.s_obs[3 * e + q];
+        v.w = (double)A.s_w[e];
+        for (int q = 0; q < 3; ++q) v.X[q] = (double)A.s_xw[3 * e + q];
+    }
+    return v;
+}
+
+// computeError: obs - ImuCamPose::Project / ProjectStereo (G2oTypes.cc:192-205); returns chi2
+__device__ __forceinline__ double edge_error(const Rig &rig, const double *Rcw, const double *tcw, const VEdge &v,
+                                             double *r, double *Xc) {
+    const double *R = Rcw + 9 * v.cam, *t = tcw + 3 * v.cam;
+    mv3(R, v.X, Xc);
+    for (int q = 0; q < 3; ++q) Xc[q] += t[q];
+    double u, vv;
+    kb8_project(rig.cam[v.cam], Xc, u, vv);
+    r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv, r[2] = 0;
+    double c = r[0] * v.w * r[0] + r[1] * v.w * r[1];
+    if (v.stereo) {
+        r[2] = v.obs[2] - stereo_ur(u, rig.bf, Xc[2]);
+        c += r[2] * v.w * r[2];
+    }
+    return c;
+}
+
+// linearizeOplus of EdgeMonoOnlyPose (G2oTypes.cc:382-400) / EdgeStereoOnlyPose (:433-456):
+// J = proj_jac Rcb SE3deriv (2 or 3 rows)
+__device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const double *Xc, double *JP) {
+    const int c = v.cam;
+    double Xb[3];
+    mv3(rig.Rbc[c], Xc, Xb);
+    for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
+    double pj[9];
+    kb8_jac(rig.cam[c], Xc, pj);
+    const int nr = v.stereo ? 3 : 2;
+    if (v.stereo) {
+        const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+        pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
+    }
+    double pr[9];
+    for (int r = 0; r < nr; ++r)
+        for (int q = 0; q < 3; ++q)
+            pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
+    const double x = Xb[0], y = Xb[1], z = Xb[2];
+    const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+    for (int r = 0; r < nr; ++r)
+        for (int q = 0; q < 6; ++q)
+            JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+}
+
+// Per-thread normal-equation terms of one edge: acc[0..20] upper 6x6 (row-major i <= j), acc[21..26] b.
+__device__ __forceinline__ void edge_normal(const double *JP, bool stereo, double w, const double *om, double *acc) {
+    int q = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 6; ++j, ++q) {
+            double h = JP[i] * JP[j] + JP[6 + i] * JP[6 + j];
+            if (stereo) h += JP[12 + i] * JP[12 + j];
+            acc[q] += w * h;
+        }
+    for (int i = 0; i < 6; ++i) {
+        double t = JP[i] * om[0] + JP[6 + i] * om[1];
+        if (stereo) t += JP[12 + i] * om[2];
+        acc[21 + i] += t;
+    }
+}
+
+// Fixed-order workgroup sum of kNormal doubles per thread into out (valid in every thread after the call).
+__device__ __forceinline__ void reduce_normal(double *acc, double (*red)[kNormal], double *out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int q = 0; q < kNormal; ++q) {
+        double v = acc[q];
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        acc[q] = v;
+    }
+    if (lane == 0)
+        for (int q = 0; q < kNormal; ++q) red[wave][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < kNormal) {
+        double t = 0;
+        for (int w = 0; w < kPoseWaves; ++w) t += red[w][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int block_count(int v, int *sh) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < kPoseWaves; ++w) t += sh[w];
+    __syncthreads();
+    return t;
+}
+
+__global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, PoseArgs A) {
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int C = rig.n_cams;
+    // vertex states: index 0 = last keyframe (fixed), 1 = frame
+    __shared__ double sRwb[18], stwb[6], svel[6], sbg[6], sba[6];
+    __shared__ double sRcw[kMaxCams * 9], stcw[kMaxCams * 3];
+    __shared__ double red[kPoseWaves][kNormal];
+    __shared__ double nrm[kNormal];
+    __shared__ double J[216], WJ[216], om9[9], info9[81], infoG[9], infoA[9], e9[9];
+    __shared__ double Hs[225], bs[15], xs[15];
+    __shared__ int s_ok, cnt[kPoseWaves];
+    __shared__ int k1s, k2s;
+    if (tid == 0) {
+        for (int q = 0; q < 9; ++q) sRwb[q] = A.kRwb[9 * f + q], sRwb[9 + q] = A.Rwb[9 * f + q];
+        for (int q = 0; q < 3; ++q) {
+            stwb[q] = A.ktwb[3 * f + q], stwb[3 + q] = A.twb[3 * f + q];
+            svel[q] = A.kvel[3 * f + q], svel[3 + q] = A.vel[3 * f + q];
+            sbg[q] = A.kbg[3 * f + q], sbg[3 + q] = A.bg[3 * f + q];
+            sba[q] = A.kba[3 * f + q], sba[3 + q] = A.ba[3 * f + q];
+        }
+        k1s = 0, k2s = 1;
+    }
+    for (int q = tid; q < C * 9; q += kPoseThreads) sRcw[q] = A.Rcw[(size_t)f * C * 9 + q];
+    for (int q = tid; q < C * 3; q += kPoseThreads) stcw[q] = A.tcw[(size_t)f * C * 3 + q];
+    for (int q = tid; q < 15; q += kPoseThreads) xs[q] = 0.0;
+    const float *pre = A.preint + (size_t)f * kPF;
+    if (tid == 64) inertial_info9(pre + PreView::C, info9);   // EdgeInertial ctor (:486-495)
+    if (tid == 128) {   // EdgeGyroRW / EdgeAccRW information: C[9:12,9:12]^-1, C[12:15,12:15]^-1
+        double g[9], a[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                g[3 * r + c] = pre[PreView::C + (9 + r) * 15 + 9 + c], a[3 * r + c] = pre[PreView::C + (12 + r) * 15 + 12 + c];
+        inv3(g, infoG);
+        inv3(a, infoA);
+    }
+    const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0;
+    const int s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
+    const int ne = nm + ns;
+    uint8_t *kpo = A.kp_out + (size_t)f * A.kp_cap;
+    for (int q = tid; q < ne; q += kPoseThreads) {   // mvbOutlier[i] = false; level 0
+        if (q < nm) kpo[A.m_kp[m0 + q]] = 0, A.act_m[m0 + q] = 1;
+        else kpo[A.s_kp[s0 + q - nm]] = 0, A.act_s[s0 + q - nm] = 1;
+    }
+    __syncthreads();
+    State st{sRwb, stwb, nullptr, nullptr, svel, sbg, sba, nullptr};
+    Imu imu{};
+    imu.n = 1, imu.kf1 = &k1s, imu.kf2 = &k2s, imu.pre = pre;
+    const double dmono = (double)(float)sqrt(5.991), dst = (double)(float)sqrt(7.815);
+    const float chi2Mono[4] = {12.f, 7.5f, 5.991f, 5.991f};
+    const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
+    int nBad = 0, nIn = 0;
+    for (int it = 0; it < 4; ++it) {
+        const bool robust = it < 3;   // setRobustKernel(0) after the third classification
+        for (int gi = 0; gi < 10; ++gi) {
+            // computeActiveErrors + the visual part of buildSystem
+            double acc[kNormal];
+            for (int q = 0; q < kNormal; ++q) acc[q] = 0;
+            for (int q = tid; q < ne; q += kPoseThreads) {
+                const bool stq = q >= nm;
+                const int e = stq ? s0 + q - nm : m0 + q;
+                if (!(stq ? A.act_s[e] : A.act_m[e])) continue;
+                const VEdge v = load_edge(A, stq, e);
+                double r[3], Xc[3], JP[18];
+                const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+                (stq ? A.chi2_s : A.chi2_m)[e] = c2;
+                double w1 = 1.0;
+                if (robust) {
+                    double r0;
+                    if (stq) huber(c2, dst, dst * dst, r0, w1);
+                    else huber(c2, dmono, dmono * dmono, r0, w1);
+                }
+                edge_jac(rig, v, Xc, JP);
+                const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, stq ? -v.w * r[2] * w1 : 0.0};
+                edge_normal(JP, stq, v.w * w1, om, acc);
+            }
+            if (tid == 0) {   // EdgeInertial at the current state
+                imu_error(st, imu, 0, e9);
+                imu_jacobian(st, imu, 0, J);
+            }
+            reduce_normal(acc, red, nrm);   // (its barriers also publish J / e9)
+            // EdgeInertial: free columns 15-20 (frame pose) and 21-23 (frame velocity) -> state 0..8
+            for (int q = tid; q < 81; q += kPoseThreads) {
+                const int r = q / 9, c = q % 9;
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + 15 + c];
+                WJ[q] = t;
+            }
+            if (tid < 9) {
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += info9[tid * 9 + k] * e9[k];
+                om9[tid] = -t;
+            }
+            __syncthreads();
+            for (int q = tid; q < 225; q += kPoseThreads) {
+                const int i = q / 15, j = q % 15;
+                double h = 0;
+                if (i < 6 && j < 6) {   // visual 6x6 (symmetric from the upper triangle)
+                    const int a = min(i, j), b = max(i, j);
+                    h = nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+                }
+                if (i < 9 && j < 9) {
+                    double t = 0;
+                    for (int k = 0; k < 9; ++k) t += J[k * 24 + 15 + i] * WJ[k * 9 + j];
+                    h += t;
+                }
+                if (i >= 9 && j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+                Hs[q] = h;
+            }
+            if (tid < 15) {
+                double t = tid < 6 ? nrm[21 + tid] : 0.0;
+                if (tid < 9) {
+                    double u = 0;
+                    for (int k = 0; k < 9; ++k) u += J[k * 24 + 15 + tid] * om9[k];
+                    t += u;
+                }
+                if (tid >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b - b_kf, J = I
+                    const bool acc_rw = tid >= 12;
+                    const int r = (tid - 9) % 3;
+                    const double *Iw = acc_rw ? infoA : infoG;
+                    const double *bv = acc_rw ? sba : sbg;
+                    double ee[3];
+                    for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
+                    t -= Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                }
+                bs[tid] = t;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double x[15];
+                const bool ok = ldlt_pivot_solve<15>(Hs, bs, x);
+                if (ok)   // a failed solve leaves the solver's previous x in place
+                    for (int q = 0; q < 15; ++q) xs[q] = x[q];
+                s_ok = ok ? 1 : 0;
+                // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235)
+                double *Rw = sRwb + 9, *tw = stwb + 3;
+                double t[3], dR[9], Rn[9], Rbw[9], tbw[3];
+                mv3(Rw, xs + 3, t);
+                for (int q = 0; q < 3; ++q) tw[q] += t[q];
+                exp_so3(xs, dR);
+                mm3(Rw, dR, Rn);
+                for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
+                tr3(Rn, Rbw);
+                mv3(Rbw, tw, tbw);
+                for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
+                for (int c = 0; c < C; ++c) {
+                    double Rc[9], tc[3];
+                    mm3(rig.Rcb[c], Rbw, Rc);
+                    mv3(rig.Rcb[c], tbw, tc);
+                    for (int q = 0; q < 9; ++q) sRcw[9 * c + q] = Rc[q];
+                    for (int q = 0; q < 3; ++q) stcw[3 * c + q] = tc[q] + rig.tcb[c][q];
+                }
+                for (int q = 0; q < 3; ++q) svel[3 + q] += xs[6 + q], sbg[3 + q] += xs[9 + q], sba[3 + q] += xs[12 + q];
+            }
+            __syncthreads();
+            if (!s_ok) break;   // optimize() stops after a failed iteration
+        }
+        // classification (:5436-5490): the mono pass, then the stereo pass
+        int bad = 0, in = 0;
+        const float chi2close = 1.5f * chi2Mono[it];
+        for (int pass = 0; pass < 2; ++pass) {
+            const int n = pass ? ns : nm;
+            for (int q = tid; q < n; q += kPoseThreads) {
+                const bool stq = pass == 1;
+                const int e = stq ? s0 + q : m0 + q;
+                const VEdge v = load_edge(A, stq, e);
+                double *c2p = stq ? A.chi2_s + e : A.chi2_m + e;
+                double Xc[3];
+                if (kpo[v.kp]) {   // outliers of the last round: computeError at the current state
+                    double r[3];
+                    *c2p = edge_error(rig, sRcw, stcw, v, r, Xc);
+                }
+                const float chi2 = (float)*c2p;
+                bool out;
+                if (!stq) {
+                    const bool close = A.m_close[e] != 0;
+                    const double *R = sRcw + 9 * v.cam;
+                    const bool depth_pos = (R[6] * v.X[0] + R[7] * v.X[1] + R[8] * v.X[2] + stcw[3 * v.cam + 2]) > 0.0;
+                    out = (chi2 > chi2Mono[it] && !close) || (close && chi2 > chi2close) || !depth_pos;
+                } else {
+                    out = chi2 > chi2Stereo[it];
+                }
+                kpo[v.kp] = out ? 1 : 0;
+                (stq ? A.act_s : A.act_m)[e] = out ? 0 : 1;
+                bad += out ? 1 : 0;
+                in += out ? 0 : 1;
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        nBad = block_count(bad, cnt);
+        nIn = block_count(in, cnt);
+        if (ne + 3 < 10) break;   // optimizer.edges().size() < 10
+    }
+    if (nIn < 30 && !A.rec_init) {   // recover not too bad points (:5503-5526)
+        int bad = 0;
+        for (int q = tid; q < ne; q += kPoseThreads) {
+            const bool stq = q >= nm;
+            const int e = stq ? s0 + q - nm : m0 + q;
+            const VEdge v = load_edge(A, stq, e);
+            double r[3], Xc[3];
+            const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+            (stq ? A.chi2_s : A.chi2_m)[e] = c2;
+            if (c2 < (stq ? 24.f : 18.f)) kpo[v.kp] = 0;
+            else ++bad;
+        }
+        nBad = block_count(bad, cnt);
+    }
+    __threadfence_block();
+    __syncthreads();
+    // ConstraintPoseImu's Hessian (:5529-5571): information without robust weights, inlier edges only
+    if (A.H) {
+        double acc[kNormal];
+        for (int q = 0; q < kNormal; ++q) acc[q] = 0;
+        for (int q = tid; q < ne; q += kPoseThreads) {
+            const bool stq = q >= nm;
+            const int e = stq ? s0 + q - nm : m0 + q;
+            const VEdge v = load_edge(A, stq, e);
+            if (kpo[v.kp]) continue;
+            double r[3], Xc[3], JP[18];
+            edge_error(rig, sRcw, stcw, v, r, Xc);
+            edge_jac(rig, v, Xc, JP);
+            const double om[3] = {0, 0, 0};
+            edge_normal(JP, stq, v.w, om, acc);
+        }
+        if (tid == 0) imu_jacobian(st, imu, 0, J);
+        reduce_normal(acc, red, nrm);
+        for (int q = tid; q < 81; q += kPoseThreads) {
+            const int r = q / 9, c = q % 9;
+            double t = 0;
+            for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + 15 + c];
+            WJ[q] = t;
+        }
+        __syncthreads();
+        for (int q = tid; q < 225; q += kPoseThreads) {
+            const int i = q / 15, j = q % 15;
+            double h = 0;
+            if (i < 6 && j < 6) {
+                const int a = min(i, j), b = max(i, j);
+                h = nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+            }
+            if (i < 9 && j < 9) {
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += J[k * 24 + 15 + i] * WJ[k * 9 + j];
+                h += t;
+            }
+            if (i >= 9 && j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+            A.H[(size_t)f * 225 + q] = h;
+        }
+    }
+    // state back
+    if (tid == 0) {
+        for (int q = 0; q < 9; ++q) A.Rwb[9 * f + q] = sRwb[9 + q];
+        for (int q = 0; q < 3; ++q) {
+            A.twb[3 * f + q] = stwb[3 + q], A.vel[3 * f + q] = svel[3 + q];
+            A.bg[3 * f + q] = sbg[3 + q], A.ba[3 * f + q] = sba[3 + q];
+        }
+        A.n_good[f] = ne - nBad;
+    }
+    for (int q = tid; q < C * 9; q += kPoseThreads) A.Rcw[(size_t)f * C * 9 + q] = sRcw[q];
+    for (int q = tid; q < C * 3; q += kPoseThreads) A.tcw[(size_t)f * C * 3 + q] = stcw[q];
+}
+
+}  // namespace
+
+struct omv_pose {
+    int max_frames, max_edges;
+    double *chi2 = nullptr;   // [2][max_edges]
+    uint8_t *act = nullptr;   // [2][max_edges]
+};
+
+extern "C" {
+
+omv_status omv_pose_create(int max_frames, int max_edges, omv_pose **out) {
+    if (!out || max_frames <= 0 || max_edges < 0) return OMV_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
+    omv_pose *h = new omv_pose();
+    h->max_frames = max_frames, h->max_edges = max_edges;
+    const size_t n = 2 * (size_t)std::max(1, max_edges);
+    if (hipMalloc(&h->chi2, n * sizeof(double)) != hipSuccess || hipMalloc(&h->act, n) != hipSuccess) {
+        (void)hipFree(h->chi2);
+        delete h;
+        return OMV_ERR_HIP;
+    }
+    *out = h;
+    return OMV_OK;
+}
+
+omv_status omv_pose_destroy(omv_pose *h) {
+    if (!h) return OMV_ERR_ARG;
+    (void)hipFree(h->chi2);
+    (void)hipFree(h->act);
+    delete h;
+    return OMV_OK;
+}
+
+omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
+                                     int32_t *n_good, double *H, void *stream) {
+    if (!h || !b || !kp_outlier || !n_good) return OMV_ERR_ARG;
+    if (b->n_frames <= 0 || b->n_frames > h->max_frames || b->n_cams <= 0 || b->n_cams > kMaxCams ||
+        b->n_mono < 0 || b->n_stereo < 0 || b->n_mono > h->max_edges || b->n_stereo > h->max_edges || b->kp_cap <= 0)
+        return OMV_ERR_ARG;
+    Rig rig{};
+    rig.n_cams = b->n_cams;
+    for (int c = 0; c < b->n_cams; ++c) {
+        for (int q = 0; q < 8; ++q) rig.cam[c][q] = b->cam[8 * c + q];
+        for (int q = 0; q < 9; ++q) rig.Rcb[c][q] = b->Rcb[9 * c + q], rig.Rbc[c][q] = b->Rbc[9 * c + q];
+        for (int q = 0; q < 3; ++q) rig.tcb[c][q] = b->tcb[3 * c + q], rig.tbc[c][q] = b->tbc[3 * c + q];
+    }
+    rig.bf = (double)b->bf;
+    PoseArgs A{b->Rwb, b->twb, b->Rcw, b->tcw, b->vel, b->bg, b->ba, b->kf_Rwb, b->kf_twb, b->kf_vel, b->kf_bg,
+               b->kf_ba, b->preint, b->mono_start, b->mono_cam, b->mono_kp, b->mono_obs, b->mono_inv_sigma2,
+               b->mono_xw, b->mono_close, b->stereo_start, b->stereo_cam, b->stereo_kp, b->stereo_obs,
+               b->stereo_inv_sigma2, b->stereo_xw, b->kp_cap, h->chi2, h->chi2 + h->max_edges, h->act,
+               h->act + h->max_edges, kp_outlier, n_good, H, rec_init};
+    pose_lastkf_kernel<<<b->n_frames, kPoseThreads, 0, (hipStream_t)stream>>>(rig, A);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+}  // extern "C"

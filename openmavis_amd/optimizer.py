@@ -122,3 +122,42 @@ class LocalInertialBA:
         t = ctypes.c_int(0)
         _lib.check(self._lib.omv_lba_stage_ms(self._h, _lib.ptr(ms), ctypes.byref(t)), "omv_lba_stage_ms")
         return dict(build=ms[0], schur=ms[1], solve=ms[2], update=ms[3], trials=t.value)
+
+
+class PoseInertialOptimizer:
+    """Host-side mirror of Optimizer::PoseInertialOptimizationLastKeyFrame (src/Optimizer.cc:5021-5578)
+    for a batch of frames on the device (openmavis_amd/csrc/pose.hip).
+
+        opt = PoseInertialOptimizer(max_frames=256, max_edges=400000)
+        n_good = opt.PoseInertialOptimizationLastKeyFrame(batch, arrays, kp_outlier, H, bRecInit=False)
+
+    `batch` carries the rig (host numpy: cam, Rcb, tcb, Rbc, tbc, bf, n_frames, n_cams, kp_cap and the
+    edge arrays' lengths); `arrays` maps every omv_pose_batch pointer field (state in/out, the last
+    keyframe's fixed vertices, preintegration, frame-major edges) to a device tensor.  kp_outlier
+    (uint8 [F][kp_cap]) receives Frame::mvbOutlier, H (float64 [F][225] or None) the ConstraintPoseImu
+    Hessian; the int32 [F] return tensor holds the reference's return value per frame.  No CPU fallback.
+    """
+
+    def __init__(self, max_frames=256, max_edges=400000):
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(lib.omv_pose_create(int(max_frames), int(max_edges), ctypes.byref(h)), "omv_pose_create")
+        self._lib, self._h = lib, h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.omv_pose_destroy(self._h)
+            self._h = None
+
+    def PoseInertialOptimizationLastKeyFrame(self, batch, arrays, kp_outlier, H=None, bRecInit=False, stream=None):
+        import torch
+        from .synth_pose import as_pose_struct
+        s, keep = as_pose_struct(batch, _lib.PoseBatch, arrays)
+        n_good = torch.zeros(s.n_frames, dtype=torch.int32, device=kp_outlier.device)
+        st = stream if stream is not None else torch.cuda.current_stream(kp_outlier.device).cuda_stream
+        _lib.check(self._lib.omv_pose_inertial_last_kf(self._h, ctypes.byref(s), int(bool(bRecInit)),
+                                                       _lib.ptr(kp_outlier), _lib.ptr(n_good), _lib.ptr(H),
+                                                       ctypes.c_void_p(st)),
+                   "omv_pose_inertial_last_kf")
+        del keep
+        return n_good

@@ -1,0 +1,131 @@
+"""Seeded synthetic batches for Optimizer::PoseInertialOptimizationLastKeyFrame (Optimizer.cc:5021-5578).
+
+Each frame of the batch is a tracked frame 0.05-0.2 s after its last keyframe on the smooth trajectory of
+synth_ba (1 m/s arc), seen by the 5-camera Kannala-Brandt rig.  The keyframe's state is the truth (its
+vertices are fixed in the reference); the frame's initial state is the truth perturbed by ~0.5 deg /
+3 cm / 5 cm/s (what the IMU prediction hands the optimiser).  Matched map points: `n_pts` per frame in
+random cameras at 2-25 m, observed at the true projection + N(0, 0.7 px); a fraction of them are
+outliers (observation moved by 8-40 px).  stereo_frac adds an EdgeStereoOnlyPose on the same keypoint
+(kp_ur > 0, :5160-5186) with u_R = u - bf / z + noise.  The preintegration is synth_ba.preintegrate of
+the true motion (float32, the IMU::Preintegrated layout of include/omv.h).
+"""
+import numpy as np
+
+from . import synth_ba
+
+
+def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac=0.0, n_cams=5, bf=40.0,
+                    rot_noise_deg=0.5, trans_noise=0.03, vel_noise=0.05):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cams, Rbc, tbc = synth_ba.rig()
+    cams, Rbc, tbc = cams[:n_cams], Rbc[:n_cams], tbc[:n_cams]
+    Rcb = np.transpose(Rbc, (0, 2, 1))
+    tcb = -np.einsum("cij,cj->ci", Rcb, tbc)
+
+    def cam_pose(R, t):
+        Rbw = R.T
+        tbw = -Rbw @ t
+        return np.einsum("cij,jk->cik", Rcb, Rbw), np.einsum("cij,j->ci", Rcb, tbw) + tcb
+
+    F = n_frames
+    out = {k: [] for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg",
+                           "kf_ba", "preint", "true_Rwb", "true_twb", "true_vel")}
+    mono = {k: [] for k in ("cam", "kp", "obs", "w", "xw", "close", "outlier")}
+    st = {k: [] for k in ("cam", "kp", "obs", "w", "xw")}
+    m_start, s_start = [0], [0]
+    kp_cap = 0
+    for f in range(F):
+        t_kf = 0.37 * f + float(rng.uniform(0, 0.2))
+        dt = float(rng.choice([0.05, 0.1, 0.15, 0.2]))
+        Rk, pk, vk = synth_ba._pose_at(t_kf)
+        Rt, pt, vt = synth_ba._pose_at(t_kf + dt)
+        out["kf_Rwb"].append(Rk), out["kf_twb"].append(pk), out["kf_vel"].append(vk)
+        out["kf_bg"].append(np.zeros(3)), out["kf_ba"].append(np.zeros(3))
+        out["preint"].append(synth_ba.preintegrate(t_kf, t_kf + dt))
+        out["true_Rwb"].append(Rt), out["true_twb"].append(pt), out["true_vel"].append(vt)
+        ax = rng.normal(0, 1, 3)
+        ax /= np.linalg.norm(ax)
+        R0 = Rt @ synth_ba._exp(ax * np.deg2rad(rot_noise_deg))
+        u, _, vh = np.linalg.svd(R0)
+        R0 = u @ vh
+        t0 = pt + rng.normal(0, trans_noise, 3)
+        out["Rwb"].append(R0), out["twb"].append(t0)
+        out["vel"].append(vt + rng.normal(0, vel_noise, 3))
+        out["bg"].append(rng.normal(0, 1e-4, 3)), out["ba"].append(rng.normal(0, 1e-3, 3))
+        Rc0, tc0 = cam_pose(R0, t0)
+        out["Rcw"].append(Rc0), out["tcw"].append(tc0)
+        Rct, tct = cam_pose(Rt, pt)
+        kp = 0
+        while kp < n_pts:
+            c = int(rng.integers(0, n_cams))
+            d = rng.normal(0, 1, 3)
+            d[2] = abs(d[2]) * 1.5 + 0.6
+            d /= np.linalg.norm(d)
+            Xc = d * rng.uniform(2.0, 25.0)
+            uv = synth_ba.kb8_project(cams[c].astype(np.float64), Xc)
+            if not (5 <= uv[0] <= 715 and 5 <= uv[1] <= 535):
+                continue
+            Xw = (Rct[c].T @ (Xc - tct[c])).astype(np.float32)   # MapPoint::GetWorldPos is float
+            obs = uv + rng.normal(0, 0.7, 2)
+            bad = rng.random() < outlier_frac
+            if bad:
+                obs = obs + rng.uniform(8, 40, 2) * rng.choice([-1, 1], 2)
+            w = np.float32(1.0 / np.float32(1.2) ** (2 * int(rng.integers(0, 8))))
+            mono["cam"].append(c), mono["kp"].append(kp), mono["obs"].append(obs), mono["w"].append(w)
+            mono["xw"].append(Xw), mono["close"].append(rng.random() < 0.3), mono["outlier"].append(bad)
+            if stereo_frac > 0 and rng.random() < stereo_frac:
+                ur = np.float32(uv[0] - bf / Xc[2] + rng.normal(0, 0.7))
+                if ur > 0:
+                    st["cam"].append(c), st["kp"].append(kp), st["obs"].append([obs[0], obs[1], float(ur)])
+                    st["w"].append(w), st["xw"].append(Xw)
+            kp += 1
+        kp_cap = max(kp_cap, kp)
+        m_start.append(len(mono["cam"]))
+        s_start.append(len(st["cam"]))
+    b = {k: np.array(v, np.float64) for k, v in out.items() if k != "preint"}
+    b["preint"] = np.stack(out["preint"]).astype(np.float32)
+    b.update(n_frames=F, n_cams=n_cams, cam=cams, Rcb=Rcb, tcb=tcb, Rbc=Rbc, tbc=tbc, bf=np.float32(bf),
+             kp_cap=kp_cap,
+             mono_start=np.array(m_start, np.int32), mono_cam=np.array(mono["cam"], np.int32),
+             mono_kp=np.array(mono["kp"], np.int32), mono_obs=np.array(mono["obs"], np.float64).reshape(-1, 2),
+             mono_inv_sigma2=np.array(mono["w"], np.float32), mono_xw=np.array(mono["xw"], np.float32).reshape(-1, 3),
+             mono_close=np.array(mono["close"], np.uint8), mono_is_outlier=np.array(mono["outlier"], bool),
+             stereo_start=np.array(s_start, np.int32), stereo_cam=np.array(st["cam"], np.int32),
+             stereo_kp=np.array(st["kp"], np.int32), stereo_obs=np.array(st["obs"], np.float64).reshape(-1, 3),
+             stereo_inv_sigma2=np.array(st["w"], np.float32), stereo_xw=np.array(st["xw"], np.float32).reshape(-1, 3))
+    return b
+
+
+STATE_KEYS = ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba")
+INPUT_KEYS = ("kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba", "preint", "mono_start", "mono_cam", "mono_kp",
+              "mono_obs", "mono_inv_sigma2", "mono_xw", "mono_close", "stereo_start", "stereo_cam", "stereo_kp",
+              "stereo_obs", "stereo_inv_sigma2", "stereo_xw")
+
+
+def as_pose_struct(batch, struct_cls, arrays):
+    """Fill an omv_pose_batch from `batch` (host rig arrays) and `arrays` (name -> pointer-bearing array:
+    numpy for the oracle, torch device tensors for the product).  Returns (struct, keepalive)."""
+    import ctypes
+    keep = []
+
+    def hptr(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    def anyptr(a):
+        if hasattr(a, "data_ptr"):
+            return ctypes.c_void_p(a.data_ptr()) if a.numel() else None
+        return ctypes.c_void_p(a.ctypes.data) if a.size else None
+
+    s = struct_cls()
+    s.n_frames, s.n_cams = int(batch["n_frames"]), int(batch["n_cams"])
+    s.cam = hptr(batch["cam"], np.float32)
+    for k in ("Rcb", "tcb", "Rbc", "tbc"):
+        setattr(s, k, hptr(batch[k], np.float64))
+    s.bf = float(batch["bf"])
+    for k in STATE_KEYS + INPUT_KEYS:
+        setattr(s, k, anyptr(arrays[k]))
+    s.kp_cap = int(batch["kp_cap"])
+    s.n_mono, s.n_stereo = int(len(batch["mono_cam"])), int(len(batch["stereo_cam"]))
+    return s, keep

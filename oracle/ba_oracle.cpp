@@ -325,6 +325,93 @@ void sym_eig(std::vector<double> A, int n, std::vector<double> &w, std::vector<d
 }
 
 // ---- the problem -------------------------------------------------------------------------------------
+// ---- EdgeInertial over explicit vertex states (vertex 1 = previous, 2 = current) ---------------------
+struct ImuVerts {
+    M3 Rwb1;
+    V3 twb1, v1, bg1, ba1;
+    M3 Rwb2;
+    V3 twb2, v2;
+};
+// EdgeInertial::computeError (G2oTypes.cc:502-531)
+void inertial_error(const Preint &p, const ImuVerts &s, double out[9]) {
+    float b1[6];   // IMU::Bias(ba, bg) of vertex 1 as floats
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba1[q], b1[3 + q] = (float)s.bg1[q];
+    M3 dR;
+    delta_rotation(p, b1, dR);
+    const V3 dV = delta_vp(p.dV, p.JVg, p.JVa, p, b1);
+    const V3 dP = delta_vp(p.dP, p.JPg, p.JPa, p, b1);
+    const double dt = (double)p.dT;
+    const V3 g{{0, 0, -(double)9.81f}};
+    const V3 er = logSO3(mul(mul(tr(dR), tr(s.Rwb1)), s.Rwb2));
+    const V3 ev = sub(mul(tr(s.Rwb1), sub(sub(s.v2, s.v1), scale(g, dt))), dV);
+    const V3 gdt2 = V3{{g[0] * dt * dt / 2, g[1] * dt * dt / 2, g[2] * dt * dt / 2}};
+    const V3 ep = sub(mul(tr(s.Rwb1), sub(sub(sub(s.twb2, s.twb1), scale(s.v1, dt)), gdt2)), dP);
+    for (int q = 0; q < 3; ++q) out[q] = er[q], out[3 + q] = ev[q], out[6 + q] = ep[q];
+}
+// EdgeInertial::linearizeOplus (:542-599): J[v] 9 x dim(v), v = P1 V1 G1 A1 P2 V2
+void inertial_jac(const Preint &p, const ImuVerts &s, std::vector<double> J[6]) {
+    float b1[6];
+    for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba1[q], b1[3 + q] = (float)s.bg1[q];
+    const float dbgf[3] = {b1[3] - p.b[3], b1[4] - p.b[4], b1[5] - p.b[5]};
+    const V3 dbg{{(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]}};
+    const M3 Rwb1 = s.Rwb1, Rbw1 = tr(Rwb1), Rwb2 = s.Rwb2;
+    M3 dR;
+    delta_rotation(p, b1, dR);
+    const M3 eR = mul(mul(tr(dR), Rbw1), Rwb2);
+    const V3 er = logSO3(eR);
+    const M3 invJr = invRightJ(er);
+    M3 JRg, JVg, JPg, JVa, JPa;
+    for (int q = 0; q < 9; ++q)
+        JRg.m[q] = p.JRg[q], JVg.m[q] = p.JVg[q], JPg.m[q] = p.JPg[q], JVa.m[q] = p.JVa[q], JPa.m[q] = p.JPa[q];
+    const double dt = (double)p.dT;
+    const V3 g{{0, 0, -(double)9.81f}};
+    const int dims[6] = {6, 3, 3, 3, 6, 3};
+    for (int v = 0; v < 6; ++v) J[v].assign(9 * dims[v], 0.0);
+    auto put = [&](std::vector<double> &A, int cols, int r0, int c0, const M3 &B) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) A[(r0 + r) * cols + c0 + c] = B(r, c);
+    };
+    put(J[0], 6, 0, 0, scale(mul(mul(invJr, tr(Rwb2)), Rwb1), -1.0));
+    put(J[0], 6, 3, 0, hat(mul(Rbw1, sub(sub(s.v2, s.v1), scale(g, dt)))));
+    const V3 half{{0.5 * g[0] * dt * dt, 0.5 * g[1] * dt * dt, 0.5 * g[2] * dt * dt}};
+    put(J[0], 6, 6, 0, hat(mul(Rbw1, sub(sub(sub(s.twb2, s.twb1), scale(s.v1, dt)), half))));
+    put(J[0], 6, 6, 3, scale(eye(), -1.0));
+    put(J[1], 3, 3, 0, scale(Rbw1, -1.0));
+    put(J[1], 3, 6, 0, scale(Rbw1, -dt));
+    put(J[2], 3, 0, 0, scale(mul(mul(mul(invJr, tr(eR)), rightJ(mul(JRg, dbg))), JRg), -1.0));
+    put(J[2], 3, 3, 0, scale(JVg, -1.0));
+    put(J[2], 3, 6, 0, scale(JPg, -1.0));
+    put(J[3], 3, 3, 0, scale(JVa, -1.0));
+    put(J[3], 3, 6, 0, scale(JPa, -1.0));
+    put(J[4], 6, 0, 0, invJr);
+    put(J[4], 6, 6, 3, mul(Rbw1, Rwb2));
+    put(J[5], 3, 3, 0, Rbw1);
+}
+// EdgeInertial ctor information (:486-495): sym(C[0:9,0:9]^-1) with eigenvalues < 1e-12 zeroed
+std::vector<double> inertial_info(const Preint &p) {
+    std::vector<double> A(81);
+    for (int r = 0; r < 9; ++r)
+        for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)p.C[r * 15 + c];
+    invert_gj(A, 9);
+    for (int r = 0; r < 9; ++r)
+        for (int c = r + 1; c < 9; ++c) {
+            const double s = (A[r * 9 + c] + A[c * 9 + r]) / 2;
+            A[r * 9 + c] = A[c * 9 + r] = s;
+        }
+    std::vector<double> w, V;
+    sym_eig(A, 9, w, V);
+    for (double &x : w)
+        if (x < 1e-12) x = 0;
+    std::vector<double> I9(81, 0.0);
+    for (int r = 0; r < 9; ++r)
+        for (int c = 0; c < 9; ++c) {
+            double s = 0;
+            for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
+            I9[r * 9 + c] = s;
+        }
+    return I9;
+}
+
 struct Pose {
     M3 Rwb;
     V3 twb;
@@ -386,26 +473,7 @@ struct Solver {
         infoG.resize(p.n_imu), infoA.resize(p.n_imu);
         for (int i = 0; i < p.n_imu; ++i) {
             std::memcpy(&pre[i], p.preint + (size_t)i * OMV_PREINT_FLOATS, sizeof(float) * OMV_PREINT_FLOATS);
-            std::vector<double> A(81);
-            for (int r = 0; r < 9; ++r)
-                for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)pre[i].C[r * 15 + c];
-            invert_gj(A, 9);
-            for (int r = 0; r < 9; ++r)
-                for (int c = r + 1; c < 9; ++c) {
-                    const double s = (A[r * 9 + c] + A[c * 9 + r]) / 2;
-                    A[r * 9 + c] = A[c * 9 + r] = s;
-                }
-            std::vector<double> w, V;
-            sym_eig(A, 9, w, V);
-            for (double &x : w)
-                if (x < 1e-12) x = 0;
-            std::vector<double> I9(81, 0.0);
-            for (int r = 0; r < 9; ++r)
-                for (int c = 0; c < 9; ++c) {
-                    double s = 0;
-                    for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
-                    I9[r * 9 + c] = s;
-                }
+            std::vector<double> I9 = inertial_info(pre[i]);
             const double sc = p.imu_info_scale ? (double)p.imu_info_scale[i] : 1.0;
             for (double &x : I9) x *= sc;
             info9[i] = I9;
@@ -464,26 +532,11 @@ struct Solver {
         const double *r = &e_st[3 * e];
         return r[0] * w * r[0] + r[1] * w * r[1] + r[2] * w * r[2];
     }
-    void bias_floats(int k, float b1[6]) const {   // IMU::Bias(ba, bg) as floats
-        for (int q = 0; q < 3; ++q) b1[q] = (float)ba[k][q], b1[3 + q] = (float)bg[k][q];
-    }
-    void imu_error(int i, double out[9]) const {
+    ImuVerts imu_verts(int i) const {
         const int k1 = P.imu_kf1[i], k2 = P.imu_kf2[i];
-        const Preint &p = pre[i];
-        float b1[6];
-        bias_floats(k1, b1);
-        M3 dR;
-        delta_rotation(p, b1, dR);
-        const V3 dV = delta_vp(p.dV, p.JVg, p.JVa, p, b1);
-        const V3 dP = delta_vp(p.dP, p.JPg, p.JPa, p, b1);
-        const double dt = (double)p.dT;
-        const V3 g{{0, 0, -(double)9.81f}};
-        const V3 er = logSO3(mul(mul(tr(dR), tr(pose[k1].Rwb)), pose[k2].Rwb));
-        const V3 ev = sub(mul(tr(pose[k1].Rwb), sub(sub(vel[k2], vel[k1]), scale(g, dt))), dV);
-        const V3 gdt2 = V3{{g[0] * dt * dt / 2, g[1] * dt * dt / 2, g[2] * dt * dt / 2}};
-        const V3 ep = sub(mul(tr(pose[k1].Rwb), sub(sub(sub(pose[k2].twb, pose[k1].twb), scale(vel[k1], dt)), gdt2)), dP);
-        for (int q = 0; q < 3; ++q) out[q] = er[q], out[3 + q] = ev[q], out[6 + q] = ep[q];
+        return ImuVerts{pose[k1].Rwb, pose[k1].twb, vel[k1], bg[k1], ba[k1], pose[k2].Rwb, pose[k2].twb, vel[k2]};
     }
+    void imu_error(int i, double out[9]) const { inertial_error(pre[i], imu_verts(i), out); }
     void compute_errors() {
         for (int e = 0; e < P.n_mono; ++e) mono_error(e, &e_mono[2 * e]);
         for (int e = 0; e < NS; ++e) stereo_error(e, &e_st[3 * e]);
@@ -590,47 +643,7 @@ struct Solver {
             for (int q = 0; q < 6; ++q)
                 JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
     }
-    // EdgeInertial::linearizeOplus (:542-599): J[v] 9 x dim(v), v = P1 V1 G1 A1 P2 V2
-    void imu_jac(int i, std::vector<double> J[6]) const {
-        const int k1 = P.imu_kf1[i], k2 = P.imu_kf2[i];
-        const Preint &p = pre[i];
-        float b1[6];
-        bias_floats(k1, b1);
-        const float dbgf[3] = {b1[3] - p.b[3], b1[4] - p.b[4], b1[5] - p.b[5]};
-        const V3 dbg{{(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]}};
-        const M3 Rwb1 = pose[k1].Rwb, Rbw1 = tr(Rwb1), Rwb2 = pose[k2].Rwb;
-        M3 dR;
-        delta_rotation(p, b1, dR);
-        const M3 eR = mul(mul(tr(dR), Rbw1), Rwb2);
-        const V3 er = logSO3(eR);
-        const M3 invJr = invRightJ(er);
-        M3 JRg, JVg, JPg, JVa, JPa;
-        for (int q = 0; q < 9; ++q)
-            JRg.m[q] = p.JRg[q], JVg.m[q] = p.JVg[q], JPg.m[q] = p.JPg[q], JVa.m[q] = p.JVa[q], JPa.m[q] = p.JPa[q];
-        const double dt = (double)p.dT;
-        const V3 g{{0, 0, -(double)9.81f}};
-        const int dims[6] = {6, 3, 3, 3, 6, 3};
-        for (int v = 0; v < 6; ++v) J[v].assign(9 * dims[v], 0.0);
-        auto put = [&](std::vector<double> &A, int cols, int r0, int c0, const M3 &B) {
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) A[(r0 + r) * cols + c0 + c] = B(r, c);
-        };
-        put(J[0], 6, 0, 0, scale(mul(mul(invJr, tr(Rwb2)), Rwb1), -1.0));
-        put(J[0], 6, 3, 0, hat(mul(Rbw1, sub(sub(vel[k2], vel[k1]), scale(g, dt)))));
-        const V3 half{{0.5 * g[0] * dt * dt, 0.5 * g[1] * dt * dt, 0.5 * g[2] * dt * dt}};
-        put(J[0], 6, 6, 0, hat(mul(Rbw1, sub(sub(sub(pose[k2].twb, pose[k1].twb), scale(vel[k1], dt)), half))));
-        put(J[0], 6, 6, 3, scale(eye(), -1.0));
-        put(J[1], 3, 3, 0, scale(Rbw1, -1.0));
-        put(J[1], 3, 6, 0, scale(Rbw1, -dt));
-        put(J[2], 3, 0, 0, scale(mul(mul(mul(invJr, tr(eR)), rightJ(mul(JRg, dbg))), JRg), -1.0));
-        put(J[2], 3, 3, 0, scale(JVg, -1.0));
-        put(J[2], 3, 6, 0, scale(JPg, -1.0));
-        put(J[3], 3, 3, 0, scale(JVa, -1.0));
-        put(J[3], 3, 6, 0, scale(JPa, -1.0));
-        put(J[4], 6, 0, 0, invJr);
-        put(J[4], 6, 6, 3, mul(Rbw1, Rwb2));
-        put(J[5], 3, 3, 0, Rbw1);
-    }
+    void imu_jac(int i, std::vector<double> J[6]) const { inertial_jac(pre[i], imu_verts(i), J); }
 
     // --- system: dense reduced part + per-landmark blocks ---
     struct Landmark {
@@ -1041,6 +1054,397 @@ int oracle_lba_optimize(omv_lba_problem *p, const omv_lba_opts *o, omv_lba_resul
     const bool fail = (2 * r->err < r->err_end || std::isnan(r->err) || std::isnan(r->err_end)) && !o->large;
     r->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
     s.write_state(*p);
+    return 0;
+}
+
+}  // extern "C"
+
+// =============================================================================================
+// Optimizer::PoseInertialOptimizationLastKeyFrame (src/Optimizer.cc:5021-5578), one frame.
+namespace {
+
+// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting) as Eigen 3.3's ldlt_inplace::unblocked computes it,
+// and LDLT::_solve_impl (D pseudo-inverse below the smallest normal double).  Returns isPositive().
+bool ldlt_pivot_solve(std::vector<double> A, int n, const double *b, double *x) {
+    std::vector<int> tr(n);
+    std::vector<double> temp(n);
+    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
+    bool found_zero = false;
+    auto a = [&](int i, int j) -> double & { return A[(size_t)i * n + j]; };
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        for (int i = k + 1; i < n; ++i)
+            if (std::fabs(a(i, i)) > std::fabs(a(big, big))) big = i;
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; ++j) std::swap(a(k, j), a(big, j));
+            for (int i = big + 1; i < n; ++i) std::swap(a(i, k), a(i, big));
+            std::swap(a(k, k), a(big, big));
+            for (int i = k + 1; i < big; ++i) {
+                const double t = a(i, k);
+                a(i, k) = a(big, i);
+                a(big, i) = t;
+            }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = a(j, j) * a(k, j);
+            double s = 0;
+            for (int j = 0; j < k; ++j) s += a(k, j) * temp[j];
+            a(k, k) -= s;
+            for (int i = k + 1; i < n; ++i) {
+                double t = 0;
+                for (int j = 0; j < k; ++j) t += a(i, j) * temp[j];
+                a(i, k) -= t;
+            }
+        }
+        const double akk = a(k, k);
+        const bool valid = std::fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            for (int j = 0; j < n; ++j) tr[j] = j;
+            break;
+        }
+        if (valid)
+            for (int i = k + 1; i < n; ++i) a(i, k) /= akk;
+        if (!(found_zero && valid) && !valid) found_zero = true;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    const bool positive = sign == 1 || sign == 0;
+    if (!positive) return false;
+    std::vector<double> y(b, b + n);
+    for (int k = 0; k < n; ++k) std::swap(y[k], y[tr[k]]);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i; ++j) y[i] -= a(i, j) * y[j];
+    for (int i = 0; i < n; ++i) {
+        if (std::fabs(a(i, i)) > std::numeric_limits<double>::min()) y[i] /= a(i, i);
+        else y[i] = 0;
+    }
+    for (int i = n - 1; i >= 0; --i)
+        for (int j = i + 1; j < n; ++j) y[i] -= a(j, i) * y[j];
+    for (int k = n - 1; k >= 0; --k) std::swap(y[k], y[tr[k]]);
+    for (int i = 0; i < n; ++i) x[i] = y[i];
+    return true;
+}
+
+struct PoseEdge {
+    int cam, kp;
+    bool stereo;
+    double obs[3];
+    double w;
+    V3 Xw;
+    bool close;
+    bool active = true;    // level 0
+    bool robust = true;    // Huber (dropped after round 3)
+    double chi2 = 0;       // e->chi2() of the last computeError
+};
+
+struct PoseProblem {
+    int C;
+    const float *cam;
+    std::vector<M3> Rcb, Rbc;
+    std::vector<V3> tcb, tbc;
+    double bf;
+    // frame vertices
+    M3 Rwb;
+    V3 twb, v, bg, ba;
+    std::vector<M3> Rcw;
+    std::vector<V3> tcw;
+    // fixed keyframe vertices
+    M3 kRwb;
+    V3 ktwb, kv, kbg, kba;
+    Preint pre;
+    std::vector<double> info9;
+    M3 infoG, infoA;
+    std::vector<PoseEdge> E;   // EdgeMonoOnlyPose first, then EdgeStereoOnlyPose (creation order)
+    double dmono = (double)(float)std::sqrt(5.991), dst = (double)(float)std::sqrt(7.815);
+
+    // computeError of one visual edge (ImuCamPose::Project / ProjectStereo, G2oTypes.cc:192-205)
+    void error(const PoseEdge &e, double r[3]) const {
+        const V3 Xc = add(mul(Rcw[e.cam], e.Xw), tcw[e.cam]);
+        double u, vv;
+        kb8_project(cam + 8 * e.cam, Xc, u, vv);
+        r[0] = e.obs[0] - u;
+        r[1] = e.obs[1] - vv;
+        r[2] = 0;
+        if (e.stereo) {
+            const double invZ = 1 / Xc[2];
+            r[2] = e.obs[2] - (u - bf * invZ);
+        }
+    }
+    double chi2_of(const PoseEdge &e, const double r[3]) const {
+        double c = r[0] * e.w * r[0] + r[1] * e.w * r[1];
+        if (e.stereo) c += r[2] * e.w * r[2];
+        return c;
+    }
+    void compute_error(PoseEdge &e) const {
+        double r[3];
+        error(e, r);
+        e.chi2 = chi2_of(e, r);
+    }
+    bool depth_positive(const PoseEdge &e) const {   // ImuCamPose::isDepthPositive (:207-209)
+        const M3 &R = Rcw[e.cam];
+        return (R(2, 0) * e.Xw[0] + R(2, 1) * e.Xw[1] + R(2, 2) * e.Xw[2] + tcw[e.cam][2]) > 0.0;
+    }
+    // EdgeMonoOnlyPose / EdgeStereoOnlyPose::linearizeOplus: J = proj_jac Rcb SE3deriv (rows 2 or 3)
+    void jac(const PoseEdge &e, double JP[18]) const {
+        const int c = e.cam;
+        const V3 Xc = add(mul(Rcw[c], e.Xw), tcw[c]);
+        const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
+        double pj[9];
+        kb8_jac(cam + 8 * c, Xc, pj);
+        const int nr = e.stereo ? 3 : 2;
+        if (e.stereo) {
+            const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+            pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + bf * inv_z2;
+        }
+        double pr[9];
+        for (int r = 0; r < nr; ++r)
+            for (int q = 0; q < 3; ++q)
+                pr[3 * r + q] = pj[3 * r] * Rcb[c](0, q) + pj[3 * r + 1] * Rcb[c](1, q) + pj[3 * r + 2] * Rcb[c](2, q);
+        const double x = Xb[0], y = Xb[1], z = Xb[2];
+        const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+        for (int r = 0; r < nr; ++r)
+            for (int q = 0; q < 6; ++q)
+                JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    }
+    ImuVerts verts() const { return ImuVerts{kRwb, ktwb, kv, kbg, kba, Rwb, twb, v}; }
+
+    // one Gauss-Newton iteration (optimization_algorithm_gauss_newton.cpp:50-95): computeActiveErrors,
+    // buildSystem, dense LDLT solve, update.  Returns the solve's ok.
+    bool gn_iteration(std::vector<double> &x_prev) {
+        for (PoseEdge &e : E)
+            if (e.active) compute_error(e);
+        double H[225] = {0}, b[15] = {0}, rho[3];
+        for (PoseEdge &e : E) {
+            if (!e.active) continue;
+            double r[3], JP[18];
+            error(e, r);
+            jac(e, JP);
+            const int nr = e.stereo ? 3 : 2;
+            double w1 = 1.0;
+            if (e.robust) {
+                Solver::huber(e.chi2, e.stereo ? dst : dmono, e.stereo ? dst * dst : dmono * dmono, rho);
+                w1 = rho[1];
+            }
+            const double w = e.w * w1;
+            double om[3];
+            for (int q = 0; q < nr; ++q) om[q] = -e.w * r[q] * w1;
+            for (int i = 0; i < 6; ++i) {
+                double t = JP[i] * om[0] + JP[6 + i] * om[1];
+                if (nr == 3) t += JP[12 + i] * om[2];
+                b[i] += t;
+                for (int j = 0; j < 6; ++j) {
+                    double h = JP[i] * JP[j] + JP[6 + i] * JP[6 + j];
+                    if (nr == 3) h += JP[12 + i] * JP[12 + j];
+                    H[15 * i + j] += w * h;
+                }
+            }
+        }
+        // EdgeInertial: vertices 4 (pose, columns 15-20 of the 9x24 Jacobian) and 5 (velocity, 21-23)
+        {
+            double e9[9];
+            inertial_error(pre, verts(), e9);
+            std::vector<double> J[6];
+            inertial_jac(pre, verts(), J);
+            double Jc[9][9];   // [row][state col 0..8]: pose 0-5, v 6-8
+            for (int r = 0; r < 9; ++r) {
+                for (int c = 0; c < 6; ++c) Jc[r][c] = J[4][r * 6 + c];
+                for (int c = 0; c < 3; ++c) Jc[r][6 + c] = J[5][r * 3 + c];
+            }
+            double Oe[9];
+            for (int r = 0; r < 9; ++r) {
+                double t = 0;
+                for (int c = 0; c < 9; ++c) t += info9[r * 9 + c] * e9[c];
+                Oe[r] = t;
+            }
+            for (int i = 0; i < 9; ++i) {
+                double t = 0;
+                for (int r = 0; r < 9; ++r) t += Jc[r][i] * Oe[r];
+                b[i] -= t;
+                for (int j = 0; j < 9; ++j) {
+                    double h = 0;
+                    for (int r = 0; r < 9; ++r) {
+                        double oj = 0;
+                        for (int c = 0; c < 9; ++c) oj += info9[r * 9 + c] * Jc[c][j];
+                        h += Jc[r][i] * oj;
+                    }
+                    H[15 * i + j] += h;
+                }
+            }
+        }
+        // EdgeGyroRW / EdgeAccRW (G2oTypes.h:567-633): e = b - b_kf, J = I on the frame's bias
+        for (int which = 0; which < 2; ++which) {
+            const V3 er = which ? sub(ba, kba) : sub(bg, kbg);
+            const M3 &Iw = which ? infoA : infoG;
+            const int o = which ? 12 : 9;
+            const V3 Oe = mul(Iw, er);
+            for (int i = 0; i < 3; ++i) {
+                b[o + i] -= Oe[i];
+                for (int j = 0; j < 3; ++j) H[15 * (o + i) + o + j] += Iw(i, j);
+            }
+        }
+        std::vector<double> Hv(H, H + 225);
+        double x[15];
+        const bool ok = ldlt_pivot_solve(Hv, 15, b, x);
+        if (!ok)   // the solver's x keeps the previous solution (zero before the first)
+            for (int i = 0; i < 15; ++i) x[i] = x_prev[i];
+        for (int i = 0; i < 15; ++i) x_prev[i] = x[i];
+        // VertexPose::oplusImpl -> ImuCamPose::Update (:211-235); velocity / biases additive
+        twb = add(twb, mul(Rwb, V3{{x[3], x[4], x[5]}}));
+        Rwb = mul(Rwb, expSO3(x[0], x[1], x[2]));
+        const M3 Rbw = tr(Rwb);
+        const V3 tbw = scale(mul(Rbw, twb), -1.0);
+        for (int c = 0; c < C; ++c) {
+            Rcw[c] = mul(Rcb[c], Rbw);
+            tcw[c] = add(mul(Rcb[c], tbw), tcb[c]);
+        }
+        for (int q = 0; q < 3; ++q) v[q] += x[6 + q], bg[q] += x[9 + q], ba[q] += x[12 + q];
+        return ok;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+// One frame of the batch (host pointers in `b`); kp_outlier [kp_cap], H [225] (may be NULL).
+int oracle_pose_inertial_last_kf(const omv_pose_batch *b, int f, int rec_init, uint8_t *kp_outlier, int32_t *n_good,
+                                 double *Hout) {
+    PoseProblem P;
+    const int C = b->n_cams;
+    P.C = C, P.cam = b->cam, P.bf = (double)b->bf;
+    for (int c = 0; c < C; ++c) {
+        M3 a, r;
+        std::memcpy(a.m, b->Rcb + 9 * c, 72);
+        std::memcpy(r.m, b->Rbc + 9 * c, 72);
+        P.Rcb.push_back(a), P.Rbc.push_back(r);
+        P.tcb.push_back(V3{{b->tcb[3 * c], b->tcb[3 * c + 1], b->tcb[3 * c + 2]}});
+        P.tbc.push_back(V3{{b->tbc[3 * c], b->tbc[3 * c + 1], b->tbc[3 * c + 2]}});
+    }
+    auto v3 = [](const double *p) { return V3{{p[0], p[1], p[2]}}; };
+    std::memcpy(P.Rwb.m, b->Rwb + 9 * f, 72);
+    P.twb = v3(b->twb + 3 * f), P.v = v3(b->vel + 3 * f), P.bg = v3(b->bg + 3 * f), P.ba = v3(b->ba + 3 * f);
+    P.Rcw.resize(C), P.tcw.resize(C);
+    for (int c = 0; c < C; ++c) {
+        std::memcpy(P.Rcw[c].m, b->Rcw + 9 * ((size_t)f * C + c), 72);
+        P.tcw[c] = v3(b->tcw + 3 * ((size_t)f * C + c));
+    }
+    std::memcpy(P.kRwb.m, b->kf_Rwb + 9 * f, 72);
+    P.ktwb = v3(b->kf_twb + 3 * f), P.kv = v3(b->kf_vel + 3 * f), P.kbg = v3(b->kf_bg + 3 * f),
+    P.kba = v3(b->kf_ba + 3 * f);
+    std::memcpy(&P.pre, b->preint + (size_t)f * OMV_PREINT_FLOATS, sizeof(float) * OMV_PREINT_FLOATS);
+    P.info9 = inertial_info(P.pre);
+    {
+        M3 g, a;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+                g(r, c) = (double)P.pre.C[(9 + r) * 15 + 9 + c];
+                a(r, c) = (double)P.pre.C[(12 + r) * 15 + 12 + c];
+            }
+        P.infoG = inv3(g), P.infoA = inv3(a);
+    }
+    for (int e = b->mono_start[f]; e < b->mono_start[f + 1]; ++e) {
+        PoseEdge q;
+        q.cam = b->mono_cam[e], q.kp = b->mono_kp[e], q.stereo = false;
+        q.obs[0] = b->mono_obs[2 * e], q.obs[1] = b->mono_obs[2 * e + 1], q.obs[2] = 0;
+        q.w = (double)b->mono_inv_sigma2[e];
+        q.Xw = V3{{(double)b->mono_xw[3 * e], (double)b->mono_xw[3 * e + 1], (double)b->mono_xw[3 * e + 2]}};
+        q.close = b->mono_close[e] != 0;
+        P.E.push_back(q);
+    }
+    const int n_mono = (int)P.E.size();
+    for (int e = b->stereo_start[f]; e < b->stereo_start[f + 1]; ++e) {
+        PoseEdge q;
+        q.cam = b->stereo_cam[e], q.kp = b->stereo_kp[e], q.stereo = true;
+        for (int d = 0; d < 3; ++d) q.obs[d] = b->stereo_obs[3 * e + d];
+        q.w = (double)b->stereo_inv_sigma2[e];
+        q.Xw = V3{{(double)b->stereo_xw[3 * e], (double)b->stereo_xw[3 * e + 1], (double)b->stereo_xw[3 * e + 2]}};
+        q.close = false;
+        P.E.push_back(q);
+    }
+    const int n_edges = (int)P.E.size();
+    for (const PoseEdge &e : P.E) kp_outlier[e.kp] = 0;   // mvbOutlier[i] = false at edge creation
+    const float chi2Mono[4] = {12, 7.5, 5.991, 5.991};
+    const float chi2Stereo[4] = {15.6, 9.8, 7.815, 7.815};
+    int nBad = 0, nInliers = 0;
+    std::vector<double> x_prev(15, 0.0);
+    for (int it = 0; it < 4; ++it) {
+        for (int i = 0; i < 10; ++i)   // optimize(its[it]): stops after a failed solve
+            if (!P.gn_iteration(x_prev)) break;
+        nBad = 0, nInliers = 0;
+        const float chi2close = 1.5f * chi2Mono[it];
+        for (int q = 0; q < n_edges; ++q) {   // mono loop, then stereo loop (:5439-5490)
+            PoseEdge &e = P.E[q];
+            if (kp_outlier[e.kp]) P.compute_error(e);
+            const float chi2 = (float)e.chi2;
+            bool out;
+            if (!e.stereo) out = (chi2 > chi2Mono[it] && !e.close) || (e.close && chi2 > chi2close) || !P.depth_positive(e);
+            else out = chi2 > chi2Stereo[it];
+            kp_outlier[e.kp] = out ? 1 : 0;
+            e.active = !out;
+            if (out) ++nBad;
+            else ++nInliers;
+            if (it == 2) e.robust = false;
+        }
+        if (n_edges + 3 < 10) break;   // optimizer.edges().size() < 10
+    }
+    if (nInliers < 30 && !rec_init) {   // recover not too bad points (:5503-5526)
+        nBad = 0;
+        for (int q = 0; q < n_edges; ++q) {
+            PoseEdge &e = P.E[q];
+            P.compute_error(e);
+            if (e.chi2 < (e.stereo ? 24.f : 18.f)) kp_outlier[e.kp] = 0;
+            else ++nBad;
+        }
+    }
+    (void)n_mono;
+    // state back
+    std::memcpy(b->Rwb + 9 * f, P.Rwb.m, 72);
+    std::memcpy(b->twb + 3 * f, P.twb.v, 24);
+    std::memcpy(b->vel + 3 * f, P.v.v, 24);
+    std::memcpy(b->bg + 3 * f, P.bg.v, 24);
+    std::memcpy(b->ba + 3 * f, P.ba.v, 24);
+    for (int c = 0; c < C; ++c) {
+        std::memcpy(b->Rcw + 9 * ((size_t)f * C + c), P.Rcw[c].m, 72);
+        std::memcpy(b->tcw + 3 * ((size_t)f * C + c), P.tcw[c].v, 24);
+    }
+    *n_good = n_edges - nBad;
+    if (Hout) {   // ConstraintPoseImu Hessian (:5533-5571), information without robust weights
+        double H[225] = {0};
+        std::vector<double> J[6];
+        inertial_jac(P.pre, P.verts(), J);
+        double Jc[9][9];
+        for (int r = 0; r < 9; ++r) {
+            for (int c = 0; c < 6; ++c) Jc[r][c] = J[4][r * 6 + c];
+            for (int c = 0; c < 3; ++c) Jc[r][6 + c] = J[5][r * 3 + c];
+        }
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) {
+                double h = 0;
+                for (int r = 0; r < 9; ++r) {
+                    double oj = 0;
+                    for (int c = 0; c < 9; ++c) oj += P.info9[r * 9 + c] * Jc[c][j];
+                    h += Jc[r][i] * oj;
+                }
+                H[15 * i + j] += h;
+            }
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) H[15 * (9 + i) + 9 + j] += P.infoG(i, j), H[15 * (12 + i) + 12 + j] += P.infoA(i, j);
+        for (const PoseEdge &e : P.E) {
+            if (kp_outlier[e.kp]) continue;
+            double JP[18];
+            P.jac(e, JP);
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) {
+                    double h = JP[i] * JP[j] + JP[6 + i] * JP[6 + j];
+                    if (e.stereo) h += JP[12 + i] * JP[12 + j];
+                    H[15 * i + j] += e.w * h;
+                }
+        }
+        std::memcpy(Hout, H, sizeof H);
+    }
     return 0;
 }
 

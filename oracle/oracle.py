@@ -275,3 +275,26 @@ def lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True, lo
     res = dict(err=r.err, err_end=r.err_end, status=r.status, iterations=r.iterations, trials=r.trials,
                lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl, stereo_chi2=s_chi2, stereo_outlier=s_outl)
     return res, read_state(keep), log[:r.trials].copy()
+
+
+# ---- PoseInertialOptimizationLastKeyFrame ---------------------------------------------------------
+def pose_last_kf(batch, rec_init=False):
+    """Restated Optimizer::PoseInertialOptimizationLastKeyFrame on every frame of a synth_pose batch.
+    Returns (state dict, kp_outlier [F][kp_cap] uint8, n_good [F], H [F][225])."""
+    from openmavis_amd._lib import PoseBatch
+    from openmavis_amd.synth_pose import INPUT_KEYS, STATE_KEYS, as_pose_struct
+    arrays = {}
+    for k in STATE_KEYS:
+        arrays[k] = np.array(batch[k], np.float64, copy=True, order="C")
+    for k in INPUT_KEYS:
+        arrays[k] = np.ascontiguousarray(batch[k])
+    s, keep = as_pose_struct(batch, PoseBatch, arrays)
+    F, cap = int(batch["n_frames"]), int(batch["kp_cap"])
+    kpo = np.full((F, cap), 255, np.uint8)
+    n_good = np.zeros(F, np.int32)
+    H = np.zeros((F, 225))
+    for f in range(F):
+        lib().oracle_pose_inertial_last_kf(ctypes.byref(s), f, int(bool(rec_init)), _p(kpo[f]),
+                                           _p(n_good[f:f + 1]), _p(H[f]))
+    del keep
+    return {k: arrays[k] for k in STATE_KEYS}, kpo, n_good, H
