@@ -382,36 +382,76 @@ __device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:8
 
 namespace omv_g2o {
 
-// EdgeInertial's information (ctor, G2oTypes.cc:486-495): Info = C[0:9,0:9]^-1, symmetrised, projected
-// onto its non-negative eigen-space (eigenvalues < 1e-12 zeroed) — Gauss-Jordan with partial pivoting and
-// cyclic Jacobi, the same arithmetic as the host path of lba.hip and the oracle.  Single thread.
-__device__ inline void inertial_info9(const float *C15, double *out) {
-    double A[81], I[81], V[81], w[9];
-    for (int r = 0; r < 9; ++r)
-        for (int c = 0; c < 9; ++c) A[r * 9 + c] = (double)C15[r * 15 + c], I[r * 9 + c] = r == c ? 1.0 : 0.0;
-    for (int c = 0; c < 9; ++c) {
+}  // namespace omv_g2o
+
+namespace omv_g2o {
+
+// EdgeInertial error and the Jacobian columns of its second pose / velocity vertices (4, 5: columns
+// 15-23 of the 9x24 layout; the only free ones when the first keyframe's vertices are fixed, as in
+// PoseInertialOptimizationLastKeyFrame).  Same arithmetic as imu_error + imu_jacobian; other entries
+// of J are left untouched.
+__device__ inline void imu_error_jac_p2v2(const State &s, const Imu &I, int i, double *e, double *J) {
+    imu_error(s, I, i, e);
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    double Rbw1[9], A[9], invJr[9];
+    tr3(s.Rwb + 9 * k1, Rbw1);
+    inv_right_jac(e, invJr);
+    mm3(Rbw1, s.Rwb + 9 * k2, A);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            J[r * 24 + 15 + c] = invJr[3 * r + c];
+            J[(6 + r) * 24 + 18 + c] = A[3 * r + c];
+            J[(3 + r) * 24 + 21 + c] = Rbw1[3 * r + c];
+        }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// EdgeInertial's information (ctor, G2oTypes.cc:486-495): Info = C[0:9,0:9]^-1, symmetrised, projected onto
+// its non-negative eigen-space (eigenvalues < 1e-12 zeroed) — Gauss-Jordan with partial pivoting and cyclic
+// Jacobi, per element the same operations in the same order as lba.hip's host path and the oracle, spread
+// over one wavefront (lane = row / column index).  sm: 243 doubles of LDS (A | I | V).  Every lane of the wave must call it.
+__device__ inline void inertial_info9_wave(const float *C15, double *out, double *sm, int lane) {
+    double *A = sm, *I = sm + 81, *V = sm + 162;
+    for (int q = lane; q < 81; q += 64) {
+        const int r = q / 9, c = q % 9;
+        A[q] = (double)C15[r * 15 + c], I[q] = r == c ? 1.0 : 0.0, V[q] = r == c ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+    for (int c = 0; c < 9; ++c) {   // Gauss-Jordan, partial pivoting
         int p = c;
         for (int r = c + 1; r < 9; ++r)
             if (fabs(A[r * 9 + c]) > fabs(A[p * 9 + c])) p = r;
-        if (p != c)
-            for (int k = 0; k < 9; ++k) {
-                double t = A[p * 9 + k];
-                A[p * 9 + k] = A[c * 9 + k], A[c * 9 + k] = t;
-                t = I[p * 9 + k];
-                I[p * 9 + k] = I[c * 9 + k], I[c * 9 + k] = t;
-            }
+        wave_lds_sync();
+        if (p != c && lane < 9) {
+            double t = A[p * 9 + lane];
+            A[p * 9 + lane] = A[c * 9 + lane], A[c * 9 + lane] = t;
+            t = I[p * 9 + lane];
+            I[p * 9 + lane] = I[c * 9 + lane], I[c * 9 + lane] = t;
+        }
+        wave_lds_sync();
         const double d = A[c * 9 + c];
-        for (int k = 0; k < 9; ++k) A[c * 9 + k] /= d, I[c * 9 + k] /= d;
-        for (int r = 0; r < 9; ++r)
-            if (r != c && A[r * 9 + c] != 0) {
-                const double f = A[r * 9 + c];
-                for (int k = 0; k < 9; ++k) A[r * 9 + k] -= f * A[c * 9 + k], I[r * 9 + k] -= f * I[c * 9 + k];
-            }
+        wave_lds_sync();
+        if (lane < 9) A[c * 9 + lane] /= d, I[c * 9 + lane] /= d;
+        wave_lds_sync();
+        if (lane < 9 && lane != c && A[lane * 9 + c] != 0) {
+            const double f = A[lane * 9 + c];
+            for (int k = 0; k < 9; ++k) A[lane * 9 + k] -= f * A[c * 9 + k], I[lane * 9 + k] -= f * I[c * 9 + k];
+        }
+        wave_lds_sync();
     }
-    for (int r = 0; r < 9; ++r)
-        for (int c = r + 1; c < 9; ++c) I[r * 9 + c] = I[c * 9 + r] = (I[r * 9 + c] + I[c * 9 + r]) / 2;
-    for (int q = 0; q < 81; ++q) V[q] = (q % 10 == 0) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 100; ++sweep) {
+    for (int q = lane; q < 81; q += 64) {   // symmetrise: (I + I^T) / 2 in the upper-then-lower write order
+        const int r = q / 9, c = q % 9;
+        A[q] = r < c ? (I[r * 9 + c] + I[c * 9 + r]) / 2 : (r > c ? (I[c * 9 + r] + I[r * 9 + c]) / 2 : I[q]);
+    }
+    wave_lds_sync();
+    for (int q = lane; q < 81; q += 64) I[q] = A[q];
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 100; ++sweep) {   // cyclic Jacobi
         double off = 0;
         for (int p = 0; p < 9; ++p)
             for (int q = p + 1; q < 9; ++q) off += I[p * 9 + q] * I[p * 9 + q];
@@ -423,79 +463,89 @@ __device__ inline void inertial_info9(const float *C15, double *out) {
                 const double th = (I[q * 9 + q] - I[p * 9 + p]) / (2 * apq);
                 const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
                 const double c = 1 / sqrt(t * t + 1), s = t * c;
-                for (int k = 0; k < 9; ++k) {
-                    const double akp = I[k * 9 + p], akq = I[k * 9 + q];
-                    I[k * 9 + p] = c * akp - s * akq, I[k * 9 + q] = s * akp + c * akq;
+                wave_lds_sync();
+                if (lane < 9) {
+                    const double akp = I[lane * 9 + p], akq = I[lane * 9 + q];
+                    I[lane * 9 + p] = c * akp - s * akq, I[lane * 9 + q] = s * akp + c * akq;
                 }
-                for (int k = 0; k < 9; ++k) {
-                    const double apk = I[p * 9 + k], aqk = I[q * 9 + k];
-                    I[p * 9 + k] = c * apk - s * aqk, I[q * 9 + k] = s * apk + c * aqk;
+                wave_lds_sync();
+                if (lane < 9) {
+                    const double apk = I[p * 9 + lane], aqk = I[q * 9 + lane];
+                    I[p * 9 + lane] = c * apk - s * aqk, I[q * 9 + lane] = s * apk + c * aqk;
+                    const double vkp = V[lane * 9 + p], vkq = V[lane * 9 + q];
+                    V[lane * 9 + p] = c * vkp - s * vkq, V[lane * 9 + q] = s * vkp + c * vkq;
                 }
-                for (int k = 0; k < 9; ++k) {
-                    const double vkp = V[k * 9 + p], vkq = V[k * 9 + q];
-                    V[k * 9 + p] = c * vkp - s * vkq, V[k * 9 + q] = s * vkp + c * vkq;
-                }
+                wave_lds_sync();
             }
     }
-    for (int i = 0; i < 9; ++i) w[i] = I[i * 9 + i] < 1e-12 ? 0.0 : I[i * 9 + i];
-    for (int r = 0; r < 9; ++r)
-        for (int c = 0; c < 9; ++c) {
-            double s = 0;
-            for (int k = 0; k < 9; ++k) s += V[r * 9 + k] * w[k] * V[c * 9 + k];
-            out[r * 9 + c] = s;
+    for (int q = lane; q < 81; q += 64) {
+        const int r = q / 9, c = q % 9;
+        double s = 0;
+        for (int k = 0; k < 9; ++k) {
+            const double wk = I[k * 9 + k] < 1e-12 ? 0.0 : I[k * 9 + k];
+            s += V[r * 9 + k] * wk * V[c * 9 + k];
         }
+        out[q] = s;
+    }
 }
 
-// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting; ldlt_inplace::unblocked) + LDLT::_solve_impl with
-// the D pseudo-inverse below DBL_MIN.  A is n x n row-major (destroyed).  Returns isPositive().
+// Eigen::LDLT<MatrixXd> (lower, diagonal pivoting; ldlt_inplace::unblocked) + LDLT::_solve_impl with the
+// D pseudo-inverse below DBL_MIN, spread over one wavefront (lane = row); per element the same operations
+// in the same order as the oracle's ldlt_pivot_solve.  Returns isPositive().  A (N x N,
+// row-major), b, x and the scratch t[2N] live in LDS; every lane of the wave must call it.
 template <int N>
-__device__ inline bool ldlt_pivot_solve(double *A, const double *b, double *x) {
-    int tr[N];
-    double temp[N];
-    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
-    bool found_zero = false;
+__device__ inline bool ldlt_pivot_solve_wave(double *A, const double *b, double *x, double *t, int *tr, int lane) {
+    static_assert(N <= 64, "one row per lane");
+    int sign = 0;
     for (int k = 0; k < N; ++k) {
-        int big = k;
-        for (int i = k + 1; i < N; ++i)
-            if (fabs(A[i * N + i]) > fabs(A[big * N + big])) big = i;
-        tr[k] = big;
+        // largest |diagonal| in the trailing corner, first index on ties (Eigen maxCoeff)
+        double v = (lane >= k && lane < N) ? fabs(A[lane * N + lane]) : -1.0;
+        int idx = lane;
+        for (int d = 1; d < 64; d <<= 1) {
+            const double ov = __shfl_xor(v, d, 64);
+            const int oi = __shfl_xor(idx, d, 64);
+            if (ov > v || (ov == v && oi < idx)) v = ov, idx = oi;
+        }
+        const int big = idx;
+        if (lane == 0) tr[k] = big;
         if (k != big) {
-            for (int j = 0; j < k; ++j) {
-                const double t = A[k * N + j];
-                A[k * N + j] = A[big * N + j], A[big * N + j] = t;
+            if (lane < k) {
+                const double u = A[k * N + lane];
+                A[k * N + lane] = A[big * N + lane], A[big * N + lane] = u;
             }
-            for (int i = big + 1; i < N; ++i) {
-                const double t = A[i * N + k];
-                A[i * N + k] = A[i * N + big], A[i * N + big] = t;
+            if (lane > big && lane < N) {
+                const double u = A[lane * N + k];
+                A[lane * N + k] = A[lane * N + big], A[lane * N + big] = u;
             }
-            const double t = A[k * N + k];
-            A[k * N + k] = A[big * N + big], A[big * N + big] = t;
-            for (int i = k + 1; i < big; ++i) {
-                const double u = A[i * N + k];
-                A[i * N + k] = A[big * N + i], A[big * N + i] = u;
+            if (lane > k && lane < big) {
+                const double u = A[lane * N + k];
+                A[lane * N + k] = A[big * N + lane], A[big * N + lane] = u;
+            }
+            if (lane == 0) {
+                const double u = A[k * N + k];
+                A[k * N + k] = A[big * N + big], A[big * N + big] = u;
             }
         }
+        wave_lds_sync();
         if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = A[j * N + j] * A[k * N + j];
-            double s = 0;
-            for (int j = 0; j < k; ++j) s += A[k * N + j] * temp[j];
-            A[k * N + k] -= s;
-            for (int i = k + 1; i < N; ++i) {
-                double t = 0;
-                for (int j = 0; j < k; ++j) t += A[i * N + j] * temp[j];
-                A[i * N + k] -= t;
+            if (lane < k) t[lane] = A[lane * N + lane] * A[k * N + lane];
+            wave_lds_sync();
+            if (lane >= k && lane < N) {   // lane k: the pivot, lanes > k: the column below it
+                double s = 0;
+                for (int j = 0; j < k; ++j) s += A[lane * N + j] * t[j];
+                A[lane * N + k] -= s;
             }
+            wave_lds_sync();
         }
         const double akk = A[k * N + k];
         const bool valid = fabs(akk) > 0.0;
         if (k == 0 && !valid) {
             sign = 0;
-            for (int j = 0; j < N; ++j) tr[j] = j;
+            if (lane < N) tr[lane] = lane;
+            wave_lds_sync();
             break;
         }
-        if (valid)
-            for (int i = k + 1; i < N; ++i) A[i * N + k] /= akk;
-        if (!valid) found_zero = true;
+        if (valid && lane > k && lane < N) A[lane * N + k] /= akk;
         if (sign == 1) {
             if (akk < 0) sign = 3;
         } else if (sign == 2) {
@@ -504,25 +554,39 @@ __device__ inline bool ldlt_pivot_solve(double *A, const double *b, double *x) {
             if (akk > 0) sign = 1;
             else if (akk < 0) sign = 2;
         }
+        wave_lds_sync();
     }
-    (void)found_zero;
     if (!(sign == 1 || sign == 0)) return false;
-    double y[N];
-    for (int i = 0; i < N; ++i) y[i] = b[i];
-    for (int k = 0; k < N; ++k) {
-        const double t = y[k];
-        y[k] = y[tr[k]], y[tr[k]] = t;
+    // y = P b; L y' = y (column-oriented); D pseudo-inverse; L^T x = y'' (column-oriented, j descending)
+    double *y = t;
+    if (lane == 0) {
+        for (int i = 0; i < N; ++i) y[i] = b[i];
+        for (int k = 0; k < N; ++k) {
+            const double u = y[k];
+            y[k] = y[tr[k]], y[tr[k]] = u;
+        }
     }
-    for (int i = 0; i < N; ++i)
-        for (int j = 0; j < i; ++j) y[i] -= A[i * N + j] * y[j];
-    for (int i = 0; i < N; ++i) y[i] = fabs(A[i * N + i]) > 2.2250738585072014e-308 ? y[i] / A[i * N + i] : 0.0;
-    for (int i = N - 1; i >= 0; --i)
-        for (int j = i + 1; j < N; ++j) y[i] -= A[j * N + i] * y[j];
-    for (int k = N - 1; k >= 0; --k) {
-        const double t = y[k];
-        y[k] = y[tr[k]], y[tr[k]] = t;
+    wave_lds_sync();
+    for (int j = 0; j < N; ++j) {
+        const double yj = y[j];
+        if (lane > j && lane < N) y[lane] -= A[lane * N + j] * yj;
+        wave_lds_sync();
     }
-    for (int i = 0; i < N; ++i) x[i] = y[i];
+    if (lane < N) y[lane] = fabs(A[lane * N + lane]) > 2.2250738585072014e-308 ? y[lane] / A[lane * N + lane] : 0.0;
+    wave_lds_sync();
+    for (int j = N - 1; j >= 0; --j) {
+        const double yj = y[j];
+        if (lane < j) y[lane] -= A[j * N + lane] * yj;
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        for (int k = N - 1; k >= 0; --k) {
+            const double u = y[k];
+            y[k] = y[tr[k]], y[tr[k]] = u;
+        }
+        for (int i = 0; i < N; ++i) x[i] = y[i];
+    }
+    wave_lds_sync();
     return true;
 }
 

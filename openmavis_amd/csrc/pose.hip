@@ -11,10 +11,12 @@
 //                    (kept per edge: e->chi2() is the value of the last computeError), Huber weight,
 //                    the 2x6 / 3x6 Jacobian and its 21 + 6 normal-equation terms; a fixed-order
 //                    wavefront + LDS reduction (deterministic run to run)
-//   inertial         thread 0 linearises EdgeInertial (9x24, only the frame's pose / velocity columns
-//                    are free); 81 threads form its 9x9 J^T Omega J block and the gradient
-//   solve + update   thread 0: 15x15 LDLT with diagonal pivoting (Eigen::LDLT semantics), then
-//                    ImuCamPose::Update and the additive velocity / bias updates
+//   inertial         thread 0 linearises EdgeInertial (only the frame's pose / velocity columns of the
+//                    9x24 Jacobian are free); 81 threads form its 9x9 J^T Omega J block and the gradient
+//   solve + update   wavefront 0: 15x15 LDLT with diagonal pivoting (Eigen::LDLT semantics, one row per
+//                    lane); thread 0: ImuCamPose::Update and the additive velocity / bias updates
+// The edges' information matrices (EdgeInertial's PSD-projected inverse covariance) come from a small
+// one-thread-per-frame kernel launched first.
 // Between rounds every thread classifies its edges (mono pass, then stereo pass: the keypoint flag is
 // shared and the stereo pass sees the mono pass's writes, as in the reference's two loops).
 #include <hip/hip_runtime.h>
@@ -62,7 +64,26 @@ struct PoseArgs {
     int32_t *n_good;
     double *H;
     int rec_init;
+    const double *info;   // [F][99] EdgeInertial 9x9 | GyroRW 3x3 | AccRW 3x3 information (pose_info_kernel)
 };
+
+// The edges' information matrices (EdgeInertial ctor :486-495, InfoG / InfoA :5397-5406), one wavefront
+// per frame: kept out of the optimisation kernel so its Jacobi sweeps do not size that kernel's registers.
+__global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, double *info) {
+    __shared__ double sm[243];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const float *pre = preint + (size_t)f * kPF;
+    double *o = info + (size_t)f * 99;
+    inertial_info9_wave(pre + PreView::C, o, sm, lane);
+    if (lane == 0) {
+        double g[9], a[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                g[3 * r + c] = pre[PreView::C + (9 + r) * 15 + 9 + c], a[3 * r + c] = pre[PreView::C + (12 + r) * 15 + 12 + c];
+        inv3(g, o + 81);
+        inv3(a, o + 90);
+    }
+}
 
 // One visual edge of the frame (EdgeMonoOnlyPose or EdgeStereoOnlyPose).
 struct VEdge {
@@ -188,8 +209,8 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
     __shared__ double red[kPoseWaves][kNormal];
     __shared__ double nrm[kNormal];
     __shared__ double J[216], WJ[216], om9[9], info9[81], infoG[9], infoA[9], e9[9];
-    __shared__ double Hs[225], bs[15], xs[15];
-    __shared__ int s_ok, cnt[kPoseWaves];
+    __shared__ double Hs[225], bs[15], xs[15], xt[15], lt[30];
+    __shared__ int s_ok, cnt[kPoseWaves], ltr[15];
     __shared__ int k1s, k2s;
     if (tid == 0) {
         for (int q = 0; q < 9; ++q) sRwb[q] = A.kRwb[9 * f + q], sRwb[9 + q] = A.Rwb[9 * f + q];
@@ -204,15 +225,13 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
     for (int q = tid; q < C * 9; q += kPoseThreads) sRcw[q] = A.Rcw[(size_t)f * C * 9 + q];
     for (int q = tid; q < C * 3; q += kPoseThreads) stcw[q] = A.tcw[(size_t)f * C * 3 + q];
     for (int q = tid; q < 15; q += kPoseThreads) xs[q] = 0.0;
+    for (int q = tid; q < 216; q += kPoseThreads) J[q] = 0.0;   // only the free columns 15-23 get written
     const float *pre = A.preint + (size_t)f * kPF;
-    if (tid == 64) inertial_info9(pre + PreView::C, info9);   // EdgeInertial ctor (:486-495)
-    if (tid == 128) {   // EdgeGyroRW / EdgeAccRW information: C[9:12,9:12]^-1, C[12:15,12:15]^-1
-        double g[9], a[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c)
-                g[3 * r + c] = pre[PreView::C + (9 + r) * 15 + 9 + c], a[3 * r + c] = pre[PreView::C + (12 + r) * 15 + 12 + c];
-        inv3(g, infoG);
-        inv3(a, infoA);
+    for (int q = tid; q < 99; q += kPoseThreads) {
+        const double v = A.info[(size_t)f * 99 + q];
+        if (q < 81) info9[q] = v;
+        else if (q < 90) infoG[q - 81] = v;
+        else infoA[q - 90] = v;
     }
     const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0;
     const int s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
@@ -254,10 +273,7 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
                 const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, stq ? -v.w * r[2] * w1 : 0.0};
                 edge_normal(JP, stq, v.w * w1, om, acc);
             }
-            if (tid == 0) {   // EdgeInertial at the current state
-                imu_error(st, imu, 0, e9);
-                imu_jacobian(st, imu, 0, J);
-            }
+            if (tid == 0) imu_error_jac_p2v2(st, imu, 0, e9, J);   // EdgeInertial at the current state
             reduce_normal(acc, red, nrm);   // (its barriers also publish J / e9)
             // EdgeInertial: free columns 15-20 (frame pose) and 21-23 (frame velocity) -> state 0..8
             for (int q = tid; q < 81; q += kPoseThreads) {
@@ -306,12 +322,15 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
                 bs[tid] = t;
             }
             __syncthreads();
+            if (tid < 64) {
+                const bool ok = ldlt_pivot_solve_wave<15>(Hs, bs, xt, lt, ltr, tid);
+                if (tid == 0) {
+                    if (ok)   // a failed solve leaves the solver's previous x in place
+                        for (int q = 0; q < 15; ++q) xs[q] = xt[q];
+                    s_ok = ok ? 1 : 0;
+                }
+            }
             if (tid == 0) {
-                double x[15];
-                const bool ok = ldlt_pivot_solve<15>(Hs, bs, x);
-                if (ok)   // a failed solve leaves the solver's previous x in place
-                    for (int q = 0; q < 15; ++q) xs[q] = x[q];
-                s_ok = ok ? 1 : 0;
                 // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235)
                 double *Rw = sRwb + 9, *tw = stwb + 3;
                 double t[3], dR[9], Rn[9], Rbw[9], tbw[3];
@@ -403,7 +422,7 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
             const double om[3] = {0, 0, 0};
             edge_normal(JP, stq, v.w, om, acc);
         }
-        if (tid == 0) imu_jacobian(st, imu, 0, J);
+        if (tid == 0) imu_error_jac_p2v2(st, imu, 0, e9, J);
         reduce_normal(acc, red, nrm);
         for (int q = tid; q < 81; q += kPoseThreads) {
             const int r = q / 9, c = q % 9;
@@ -447,6 +466,7 @@ struct omv_pose {
     int max_frames, max_edges;
     double *chi2 = nullptr;   // [2][max_edges]
     uint8_t *act = nullptr;   // [2][max_edges]
+    double *info = nullptr;   // [max_frames][99]
 };
 
 extern "C" {
@@ -458,8 +478,10 @@ omv_status omv_pose_create(int max_frames, int max_edges, omv_pose **out) {
     omv_pose *h = new omv_pose();
     h->max_frames = max_frames, h->max_edges = max_edges;
     const size_t n = 2 * (size_t)std::max(1, max_edges);
-    if (hipMalloc(&h->chi2, n * sizeof(double)) != hipSuccess || hipMalloc(&h->act, n) != hipSuccess) {
+    if (hipMalloc(&h->chi2, n * sizeof(double)) != hipSuccess || hipMalloc(&h->act, n) != hipSuccess ||
+        hipMalloc(&h->info, (size_t)max_frames * 99 * sizeof(double)) != hipSuccess) {
         (void)hipFree(h->chi2);
+        (void)hipFree(h->act);
         delete h;
         return OMV_ERR_HIP;
     }
@@ -471,6 +493,7 @@ omv_status omv_pose_destroy(omv_pose *h) {
     if (!h) return OMV_ERR_ARG;
     (void)hipFree(h->chi2);
     (void)hipFree(h->act);
+    (void)hipFree(h->info);
     delete h;
     return OMV_OK;
 }
@@ -493,7 +516,8 @@ omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int r
                b->kf_ba, b->preint, b->mono_start, b->mono_cam, b->mono_kp, b->mono_obs, b->mono_inv_sigma2,
                b->mono_xw, b->mono_close, b->stereo_start, b->stereo_cam, b->stereo_kp, b->stereo_obs,
                b->stereo_inv_sigma2, b->stereo_xw, b->kp_cap, h->chi2, h->chi2 + h->max_edges, h->act,
-               h->act + h->max_edges, kp_outlier, n_good, H, rec_init};
+               h->act + h->max_edges, kp_outlier, n_good, H, rec_init, h->info};
+    pose_info_kernel<<<b->n_frames, 64, 0, (hipStream_t)stream>>>(b->preint, h->info);
     pose_lastkf_kernel<<<b->n_frames, kPoseThreads, 0, (hipStream_t)stream>>>(rig, A);
     HIP_OK(hipGetLastError());
     return OMV_OK;

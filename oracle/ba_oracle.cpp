@@ -1121,8 +1121,8 @@ bool ldlt_pivot_solve(std::vector<double> A, int n, const double *b, double *x) 
         if (std::fabs(a(i, i)) > std::numeric_limits<double>::min()) y[i] /= a(i, i);
         else y[i] = 0;
     }
-    for (int i = n - 1; i >= 0; --i)
-        for (int j = i + 1; j < n; ++j) y[i] -= a(j, i) * y[j];
+    for (int i = n - 1; i >= 0; --i)   // L^T x = y, column-oriented (j descending)
+        for (int j = n - 1; j > i; --j) y[i] -= a(j, i) * y[j];
     for (int k = n - 1; k >= 0; --k) std::swap(y[k], y[tr[k]]);
     for (int i = 0; i < n; ++i) x[i] = y[i];
     return true;
