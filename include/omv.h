@@ -348,6 +348,46 @@ omv_status omv_lba_set_comm(omv_lba *h, int rank, int world, omv_allreduce_fn al
 omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *pt_index);
 
 /* ------------------------------------------------------------------------------------------------
+ * ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, vector<pair<size_t,size_t>>&, bOnlyStereo,
+ * bCoarse) (src/ORBmatcher.cc:1131-1456) for multi-camera keyframes, with
+ * KannalaBrandt8::epipolarConstrain / TriangulateMatches / unproject / Triangulate
+ * (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429; Eigen::JacobiSVD<Matrix4f>
+ * restated).  One workgroup per keyframe pair; pairs are independent (vbMatched2 is never set).
+ * ---------------------------------------------------------------------------------------------- */
+#define OMV_TRI_PAIRS 10   /* LL, LR, RL, RR, L-SL, SL-L, SL-SL, R-SR, SR-R, SR-SR (ORBmatcher.cc:1300-1392) */
+
+/* A keyframe in the reference's concatenated keypoint order [L | R | SL | SR] (device pointers). */
+typedef struct omv_kf_view {
+    int n;                              /* KeyFrame::N */
+    int n_left, n_right, n_sideleft;    /* NLeft, NRight, NSideLeft: camera of idx by range (0..3) */
+    const omv_kp *kps;                  /* [n] mvKeys / mvKeysRight / mvKeysSideLeft / mvKeysSideRight by idx */
+    const uint8_t *desc;                /* [n][32] mDescriptors */
+    const uint8_t *has_mp;              /* [n] GetMapPoint(idx) != NULL */
+    int n_nodes;                        /* DBoW2::FeatureVector: node ids ascending, CSR of keypoint indices */
+    const uint32_t *node_id;            /* [n_nodes] */
+    const int32_t *node_start;          /* [n_nodes + 1] */
+    const int32_t *node_idx;
+    float level_sigma2[16];             /* mvLevelSigma2 (host values) */
+} omv_kf_view;
+
+typedef struct omv_tri_pair {
+    omv_kf_view kf1, kf2;
+    /* R12 (row-major 3x3) | t12 of the camera pairs in OMV_TRI_PAIRS order: T1w * Tw2 composed with the
+     * rig (Tll = T1w Tw2, Tlr = T1w Twr2, Trl = Tr1w Tw2, ...: ORBmatcher.cc:1157-1195). */
+    float T[OMV_TRI_PAIRS][12];
+    int32_t *match12;                   /* device [kf1.n]: vMatches12 (-1 = none); vMatchedPairs = (i, match12[i] >= 0) */
+} omv_tri_pair;
+
+/* cams: host [4][8] KannalaBrandt8 parameters of the rig's L, R, SL, SR cameras (both keyframes share
+ * the rig).  n_matches: device [n_pairs] (the return value).  The camera-pair transform of a pair of
+ * cameras the reference does not list ((L,SR), (SR,L), (R,SL), (SL,R), (SL,SR), (SR,SL)) is whatever the
+ * previous candidate of the scan assigned (the reference's R12/t12/pCamera1/pCamera2 persist across
+ * iterations); before any assignment it is LL (the reference's R12/t12 are uninitialised there). */
+omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
+                                                const float *cams, int only_stereo, int coarse, int check_ori,
+                                                int32_t *n_matches, void *stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Pose-inertial optimisation of tracked frames — replaces Optimizer::PoseInertialOptimizationLastKeyFrame
  * (src/Optimizer.cc:5021-5578): Gauss-Newton (4 rounds x 10 iterations, dense LDLT) over the frame's
  * VertexPose / VertexVelocity / VertexGyroBias / VertexAccBias with the last keyframe's vertices fixed;

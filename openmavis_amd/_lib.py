@@ -108,6 +108,23 @@ class PoseBatch(ctypes.Structure):
                     "stereo_xw")] + [("kp_cap", ctypes.c_int), ("n_mono", ctypes.c_int), ("n_stereo", ctypes.c_int)]
 
 
+class KfView(ctypes.Structure):
+    """omv_kf_view (include/omv.h)."""
+    _fields_ = [("n", ctypes.c_int), ("n_left", ctypes.c_int), ("n_right", ctypes.c_int),
+                ("n_sideleft", ctypes.c_int), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("has_mp", ctypes.c_void_p), ("n_nodes", ctypes.c_int), ("node_id", ctypes.c_void_p),
+                ("node_start", ctypes.c_void_p), ("node_idx", ctypes.c_void_p), ("level_sigma2", ctypes.c_float * 16)]
+
+
+OMV_TRI_PAIRS = 10
+
+
+class TriPair(ctypes.Structure):
+    """omv_tri_pair (include/omv.h)."""
+    _fields_ = [("kf1", KfView), ("kf2", KfView), ("T", (ctypes.c_float * 12) * OMV_TRI_PAIRS),
+                ("match12", ctypes.c_void_p)]
+
+
 class LbaOpts(ctypes.Structure):
     _fields_ = [("opt_it", ctypes.c_int), ("lambda_init", ctypes.c_double), ("max_trials", ctypes.c_int),
                 ("large", ctypes.c_int)]
@@ -170,6 +187,7 @@ SIGNATURES = {
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
     "omv_lba_reset": (_I, [_VP]),
     "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),
+    "omv_matcher_search_for_triangulation": (_I, [_VP, _I, ctypes.POINTER(TriPair), _VP, _I, _I, _I, _VP, _VP]),
     "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),
     "omv_pose_destroy": (_I, [_VP]),
     "omv_pose_inertial_last_kf": (_I, [_VP, ctypes.POINTER(PoseBatch), _I, _VP, _VP, _VP, _VP]),

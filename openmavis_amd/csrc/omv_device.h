@@ -176,4 +176,61 @@ __device__ inline float glibc_atan2f(float y, float x) {
 // rounded and 53 >= 2*24+2 bits make the second rounding innocuous.
 __device__ __forceinline__ float sqrtf_cr(float x) { return (float)sqrt((double)x); }
 
+// glibc 2.35 tanf (std::tan(float) in KannalaBrandt8::unproject): fdlibm's __kernel_tanf after a
+// double-precision reduction (pi/4 < |x| < 120: n = nearbyint(x 2/pi), r = x - n pi/2).  Bit-identical
+// to the host libm on every float with |x| < 120 (tools/check_tanf.c, exhaustive).
+__device__ inline float glibc_kernel_tanf(float x, float y, int iy) {
+    const float T[] = {3.3333334327e-01f, 1.3333334029e-01f, 5.3968254477e-02f, 2.1869488060e-02f,
+                       8.8632395491e-03f, 3.5920790397e-03f, 1.4562094584e-03f, 5.8804126456e-04f,
+                       2.4646313977e-04f, 7.8179444245e-05f, 7.1407252108e-05f, -1.8558637748e-05f,
+                       2.5907305826e-05f};
+    const float pio4 = 7.8539812565e-01f, pio4lo = 3.7748947079e-08f;
+    float z, r, v, w, s;
+    const int32_t hx = (int32_t)f32_bits(x), ix = hx & 0x7fffffff;
+    if (ix < 0x39000000) {   // |x| < 2**-13
+        if ((int)x == 0) {
+            if ((ix | (iy + 1)) == 0) return 1.0f / fabsf(x);
+            else if (iy == 1) return x;
+            else return -1.0f / x;
+        }
+    }
+    if (ix >= 0x3f2ca140) {   // |x| >= 0.6744
+        if (hx < 0) x = -x, y = -y;
+        z = pio4 - x;
+        w = pio4lo - y;
+        x = z + w;
+        y = 0.0f;
+        if (fabsf(x) < 0x1p-13f) return (1 - ((hx >> 30) & 2)) * iy * (1.0f - 2 * iy * x);
+    }
+    z = x * x;
+    w = z * z;
+    r = T[1] + w * (T[3] + w * (T[5] + w * (T[7] + w * (T[9] + w * T[11]))));
+    v = z * (T[2] + w * (T[4] + w * (T[6] + w * (T[8] + w * (T[10] + w * T[12])))));
+    s = z * x;
+    r = y + z * (s * (r + v) + y);
+    r += T[0] * s;
+    w = x + r;
+    if (ix >= 0x3f2ca140) {
+        v = (float)iy;
+        return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
+    }
+    if (iy == 1) return w;
+    float a, t;
+    z = __uint_as_float(f32_bits(w) & 0xfffff000u);
+    v = r - (z - x);
+    t = a = -1.0f / w;
+    t = __uint_as_float(f32_bits(t) & 0xfffff000u);
+    s = 1.0f + t * z;
+    return t + a * (s + t * v);
+}
+__device__ inline float glibc_tanf(float x) {
+    const int32_t ix = (int32_t)(f32_bits(x) & 0x7fffffffu);
+    if (ix <= 0x3f490fda) return glibc_kernel_tanf(x, 0.0f, 1);
+    const double xd = (double)x, nd = rint(xd * 0.6366197723675814);
+    const int n = (int)nd;
+    const double r = xd - nd * 1.5707963267948966;
+    const float y0 = (float)r, y1 = (float)(r - (double)y0);
+    return glibc_kernel_tanf(y0, y1, 1 - ((n & 1) << 1));
+}
+
 }  // namespace omv

@@ -298,3 +298,42 @@ def pose_last_kf(batch, rec_init=False):
                                            _p(n_good[f:f + 1]), _p(H[f]))
     del keep
     return {k: arrays[k] for k in STATE_KEYS}, kpo, n_good, H
+
+
+# ---- SearchForTriangulation -----------------------------------------------------------------------
+def search_for_triangulation(pair, only_stereo=False, coarse=False, check_ori=False):
+    """Restated ORBmatcher::SearchForTriangulation on a synth_tri pair: (nmatches, match12 [kf1.n])."""
+    from openmavis_amd._lib import KfView, TriPair
+    from openmavis_amd.synth_tri import kf_struct
+    keep = []
+
+    def arr(_name, a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    p = TriPair()
+    p.kf1 = kf_struct(pair["kf1"], KfView, pair["level_sigma2"], arr)
+    p.kf2 = kf_struct(pair["kf2"], KfView, pair["level_sigma2"], arr)
+    for i in range(10):
+        for j in range(12):
+            p.T[i][j] = float(pair["T"][i, j])
+    m12 = np.full(pair["kf1"]["n"], -7, np.int32)
+    p.match12 = ctypes.c_void_p(m12.ctypes.data)
+    cams = np.ascontiguousarray(pair["cams"], np.float32)
+    lib().oracle_search_for_triangulation.restype = ctypes.c_int
+    n = lib().oracle_search_for_triangulation(ctypes.byref(p), _p(cams), int(only_stereo), int(coarse), int(check_ori))
+    return n, m12
+
+
+def kb8_unproject(cam, x, y):
+    ray = np.zeros(3, np.float32)
+    lib().oracle_kb8_unproject(_p(np.ascontiguousarray(cam, np.float32)), ctypes.c_float(x), ctypes.c_float(y), _p(ray))
+    return ray
+
+
+def jacobi_svd4_v(A):
+    A = np.ascontiguousarray(A, np.float32).reshape(4, 4)
+    V = np.zeros((4, 4), np.float32)
+    lib().oracle_jacobi_svd4_v(_p(A), _p(V))
+    return V

@@ -1,0 +1,332 @@
+// =====================================================================================================
+// TEST INFRASTRUCTURE ONLY — CPU oracle for ORBmatcher::SearchForTriangulation. Never linked into the product.
+//
+// Scalar restatement of
+//   ORBmatcher::SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse)
+//                                                    src/ORBmatcher.cc:1131-1456 (+ ComputeThreeMaxima :2537-2573)
+//   KannalaBrandt8::epipolarConstrain                src/CameraModels/KannalaBrandt8.cpp:219-229
+//   KannalaBrandt8::TriangulateMatches               src/CameraModels/KannalaBrandt8.cpp:319-395
+//   KannalaBrandt8::unproject / unprojectEig         src/CameraModels/KannalaBrandt8.cpp:96-126, 91-94
+//   KannalaBrandt8::project(const Eigen::Vector3f&)  src/CameraModels/KannalaBrandt8.cpp:48-67
+//   KannalaBrandt8::Triangulate                      src/CameraModels/KannalaBrandt8.cpp:414-429
+//   Eigen::JacobiSVD<Eigen::Matrix4f>(A, ComputeFullV)  Eigen 3.3.5+ / 3.4 two-sided Jacobi SVD
+//       (third-party, not under /root/reference; restated from its published algorithm: square input, so
+//       no QR preconditioner; scale by max|a_ij|; sweeps over (p, q) with threshold
+//       max(FLT_MIN, 2 eps maxDiagEntry); real_2x2_jacobi_svd + JacobiRotation::makeJacobi; singular
+//       values sorted descending by first-max selection, V columns swapped with them)
+// Multi-camera keyframes only (mpCamera2 present): the single-camera epipole test and the monocular
+// bStereo branch are not part of this path.  Float arithmetic without contraction; Eigen's 3-element
+// products / dot products / norms are taken left to right (the convention of the other restatements
+// here).  glibc's sqrtf / atan2f / tanf and double cos / sin are used as the reference's
+// KannalaBrandt8.cpp resolves them.
+// Parity status: no reference test pins these functions; Eigen's exact JacobiSVD
+// rounding (version, FMA contraction) is unpinned.  The device path is bit-exact to THIS restatement.
+// =====================================================================================================
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../include/omv.h"
+
+namespace {
+
+const int TH_LOW = 50;
+const int HISTO_LENGTH = 30;
+
+int hamming(const uint8_t *a, const uint8_t *b) {
+    int d = 0;
+    for (int k = 0; k < 32; ++k) d += __builtin_popcount((unsigned)(a[k] ^ b[k]));
+    return d;
+}
+
+// KannalaBrandt8::project(const Eigen::Vector3f&): no `using namespace std` in KannalaBrandt8.cpp, so
+// cos(float) / sin(float) are the C double functions on the promoted argument.
+void kb8_project_f(const float *k, const float *X, float &u, float &v) {
+    const float x2y2 = X[0] * X[0] + X[1] * X[1];
+    const float theta = atan2f(sqrtf(x2y2), X[2]);
+    const float psi = atan2f(X[1], X[0]);
+    const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+    u = (float)(k[0] * r * std::cos((double)psi) + k[2]);
+    v = (float)(k[1] * r * std::sin((double)psi) + k[3]);
+}
+
+// KannalaBrandt8::unproject (precision 1e-6, 10 Newton steps, scale = std::tan(theta) / theta_d)
+void kb8_unproject_f(const float *k, float px, float py, float *ray) {
+    const float pwx = (px - k[2]) / k[0], pwy = (py - k[3]) / k[1];
+    float scale = 1.f;
+    float theta_d = sqrtf(pwx * pwx + pwy * pwy);
+    theta_d = fminf(fmaxf((float)(-M_PI / 2.f), theta_d), (float)(M_PI / 2.f));
+    if (theta_d > 1e-8) {
+        float theta = theta_d;
+        for (int j = 0; j < 10; j++) {
+            const float theta2 = theta * theta, theta4 = theta2 * theta2, theta6 = theta4 * theta2,
+                        theta8 = theta4 * theta4;
+            const float k0_theta2 = k[4] * theta2, k1_theta4 = k[5] * theta4;
+            const float k2_theta6 = k[6] * theta6, k3_theta8 = k[7] * theta8;
+            const float theta_fix = (theta * (1 + k0_theta2 + k1_theta4 + k2_theta6 + k3_theta8) - theta_d) /
+                                    (1 + 3 * k0_theta2 + 5 * k1_theta4 + 7 * k2_theta6 + 9 * k3_theta8);
+            theta = theta - theta_fix;
+            if (fabsf(theta_fix) < 1e-6f) break;
+        }
+        scale = std::tan(theta) / theta_d;
+    }
+    ray[0] = pwx * scale, ray[1] = pwy * scale, ray[2] = 1.f;
+}
+
+// Eigen::JacobiSVD<Matrix4f>(A, ComputeFullV).matrixV(), A and V row-major.
+void jacobi_svd4_v(const float *A, float *V) {
+    float W[16];
+    float scale = 0.f;
+    for (int c = 0; c < 4; ++c)   // cwiseAbs().maxCoeff() (column-major visit; max is order-free)
+        for (int r = 0; r < 4; ++r) scale = std::max(scale, std::fabs(A[4 * r + c]));
+    if (scale == 0.f) scale = 1.f;
+    for (int i = 0; i < 16; ++i) W[i] = A[i] / scale, V[i] = (i % 5 == 0) ? 1.f : 0.f;
+    const float considerAsZero = FLT_MIN, precision = 2.f * FLT_EPSILON;
+    float maxDiag = std::fabs(W[0]);
+    for (int i = 1; i < 4; ++i) maxDiag = std::max(maxDiag, std::fabs(W[5 * i]));
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        for (int p = 1; p < 4; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float threshold = std::max(considerAsZero, precision * maxDiag);
+                if (!(std::fabs(W[4 * p + q]) > threshold || std::fabs(W[4 * q + p]) > threshold)) continue;
+                finished = false;
+                // real_2x2_jacobi_svd
+                const float m00 = W[4 * p + p], m01 = W[4 * p + q], m10 = W[4 * q + p], m11 = W[4 * q + q];
+                float c1, s1;
+                const float t = m00 + m11, d = m10 - m01;
+                if (std::fabs(d) < FLT_MIN) {
+                    s1 = 0.f, c1 = 1.f;
+                } else {
+                    const float u = t / d;
+                    const float tmp = sqrtf(1.f + u * u);
+                    s1 = 1.f / tmp, c1 = u / tmp;
+                }
+                float n00 = m00, n01 = m01, n11 = m11;
+                if (!(c1 == 1.f && s1 == 0.f)) {   // m.applyOnTheLeft(0, 1, rot1)
+                    n00 = c1 * m00 + s1 * m10, n01 = c1 * m01 + s1 * m11;
+                    n11 = -s1 * m01 + c1 * m11;
+                }
+                float cr, sr;   // j_right.makeJacobi(m, 0, 1)
+                const float deno = 2.f * std::fabs(n01);
+                if (deno < FLT_MIN) {
+                    cr = 1.f, sr = 0.f;
+                } else {
+                    const float tau = (n00 - n11) / deno;
+                    const float w = sqrtf(tau * tau + 1.f);
+                    const float tt = tau > 0.f ? 1.f / (tau + w) : 1.f / (tau - w);
+                    const float sign_t = tt > 0.f ? 1.f : -1.f;
+                    const float n = 1.f / sqrtf(tt * tt + 1.f);
+                    sr = -sign_t * (n01 / std::fabs(n01)) * std::fabs(tt) * n;
+                    cr = n;
+                }
+                // j_left = rot1 * j_right.transpose()
+                const float cl = c1 * cr - s1 * -sr, sl = c1 * -sr + s1 * cr;
+                if (!(cl == 1.f && sl == 0.f))   // W.applyOnTheLeft(p, q, j_left): rows p, q
+                    for (int k = 0; k < 4; ++k) {
+                        const float xi = W[4 * p + k], yi = W[4 * q + k];
+                        W[4 * p + k] = cl * xi + sl * yi;
+                        W[4 * q + k] = -sl * xi + cl * yi;
+                    }
+                if (!(cr == 1.f && -sr == 0.f))   // applyOnTheRight(p, q, j_right): columns p, q, rotation (cr, -sr)
+                    for (int k = 0; k < 4; ++k) {
+                        float xi = W[4 * k + p], yi = W[4 * k + q];
+                        W[4 * k + p] = cr * xi + -sr * yi;
+                        W[4 * k + q] = -(-sr) * xi + cr * yi;
+                        xi = V[4 * k + p], yi = V[4 * k + q];
+                        V[4 * k + p] = cr * xi + -sr * yi;
+                        V[4 * k + q] = -(-sr) * xi + cr * yi;
+                    }
+                maxDiag = std::max(maxDiag, std::max(std::fabs(W[4 * p + p]), std::fabs(W[4 * q + q])));
+            }
+    }
+    float sv[4];
+    for (int i = 0; i < 4; ++i) sv[i] = std::fabs(W[5 * i]) * scale;
+    for (int i = 0; i < 4; ++i) {   // sort descending: tail(4 - i).maxCoeff(&pos), first max
+        int pos = i;
+        for (int j = i + 1; j < 4; ++j)
+            if (sv[j] > sv[pos]) pos = j;
+        if (sv[pos] == 0.f) break;
+        if (pos != i) {
+            std::swap(sv[i], sv[pos]);
+            for (int k = 0; k < 4; ++k) std::swap(V[4 * k + i], V[4 * k + pos]);
+        }
+    }
+}
+
+// KannalaBrandt8::TriangulateMatches (returns z1, or -1 .. -5)
+float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2, const float *R12,
+                          const float *t12, float sigmaLevel, float unc) {
+    float r1[3], r2[3], r21[3];
+    kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
+    kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
+    for (int i = 0; i < 3; ++i) r21[i] = R12[3 * i] * r2[0] + R12[3 * i + 1] * r2[1] + R12[3 * i + 2] * r2[2];
+    const float dot = r1[0] * r21[0] + r1[1] * r21[1] + r1[2] * r21[2];
+    const float n1 = sqrtf(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+    const float n21 = sqrtf(r21[0] * r21[0] + r21[1] * r21[1] + r21[2] * r21[2]);
+    const float cosParallaxRays = dot / (n1 * n21);
+    if (cosParallaxRays > 0.9998) return -1;
+    float R21[9], t2[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R21[3 * i + j] = R12[3 * j + i];
+    for (int i = 0; i < 3; ++i) t2[i] = -R21[3 * i] * t12[0] + -R21[3 * i + 1] * t12[1] + -R21[3 * i + 2] * t12[2];
+    // Triangulate: rows p.x * T.row(2) - T.row(0), p.y * T.row(2) - T.row(1); Tcw1 = [I | 0], Tcw2 = [R21 | t2]
+    const float T1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float T2[12] = {R21[0], R21[1], R21[2], t2[0], R21[3], R21[4], R21[5], t2[1], R21[6], R21[7], R21[8], t2[2]};
+    float A[16], V[16];
+    for (int j = 0; j < 4; ++j) {
+        A[j] = r1[0] * T1[8 + j] - T1[j];
+        A[4 + j] = r1[1] * T1[8 + j] - T1[4 + j];
+        A[8 + j] = r2[0] * T2[8 + j] - T2[j];
+        A[12 + j] = r2[1] * T2[8 + j] - T2[4 + j];
+    }
+    jacobi_svd4_v(A, V);
+    float x3D[3];
+    for (int i = 0; i < 3; ++i) x3D[i] = V[4 * i + 3] / V[4 * 3 + 3];
+    const float z1 = x3D[2];
+    if (z1 <= 0) return -2;
+    const float z2 = R21[6] * x3D[0] + R21[7] * x3D[1] + R21[8] * x3D[2] + t2[2];
+    if (z2 <= 0) return -3;
+    float u1, v1;
+    kb8_project_f(cam1, x3D, u1, v1);
+    const float ex1 = u1 - kp1.x, ey1 = v1 - kp1.y;
+    if ((ex1 * ex1 + ey1 * ey1) > 5.991 * sigmaLevel) return -4;
+    float x3D2[3];
+    for (int i = 0; i < 3; ++i) x3D2[i] = R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2] + t2[i];
+    float u2, v2;
+    kb8_project_f(cam2, x3D2, u2, v2);
+    const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
+    if ((ex2 * ex2 + ey2 * ey2) > 5.991 * unc) return -5;
+    return z1;
+}
+
+int cam_of(const omv_kf_view &k, int idx) {
+    return idx < k.n_left ? 0 : idx < k.n_left + k.n_right ? 1 : idx < k.n_left + k.n_right + k.n_sideleft ? 2 : 3;
+}
+
+// (cameraId1, cameraId2) -> pair index in OMV_TRI_PAIRS order, -1 if the reference leaves R12/t12 as they were
+// LL=0, LR=1, RL=2, RR=3, L-SL=4, SL-L=5, SL-SL=6, R-SR=7, SR-R=8, SR-SR=9 (ORBmatcher.cc:1300-1392)
+int pair_of(int c1, int c2) {
+    if (c1 == 0 && c2 == 0) return 0;
+    if (c1 == 0 && c2 == 1) return 1;
+    if (c1 == 1 && c2 == 0) return 2;
+    if (c1 == 1 && c2 == 1) return 3;
+    if (c1 == 0 && c2 == 2) return 4;
+    if (c1 == 2 && c2 == 0) return 5;
+    if (c1 == 2 && c2 == 2) return 6;
+    if (c1 == 1 && c2 == 3) return 7;
+    if (c1 == 3 && c2 == 1) return 8;
+    if (c1 == 3 && c2 == 3) return 9;
+    return -1;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:2537-2573)
+void three_maxima(const int *cnt, int &ind1, int &ind2, int &ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = cnt[i];
+        if (s > max1) {
+            max3 = max2, max2 = max1, max1 = s;
+            ind3 = ind2, ind2 = ind1, ind1 = i;
+        } else if (s > max2) {
+            max3 = max2, max2 = s;
+            ind3 = ind2, ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1, ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// One keyframe pair (host pointers in the views); writes match12 [kf1.n]; returns nmatches.
+int oracle_search_for_triangulation(const omv_tri_pair *P, const float *cams, int only_stereo, int coarse,
+                                    int check_ori) {
+    const omv_kf_view &K1 = P->kf1, &K2 = P->kf2;
+    for (int i = 0; i < K1.n; ++i) P->match12[i] = -1;
+    int nmatches = 0;
+    std::vector<int> hist[HISTO_LENGTH];
+    const float factor = 1.0f / HISTO_LENGTH;
+    // the persistent camera-pair state (R12, t12, pCamera1, pCamera2); LL before any assignment
+    int state = 0;
+    int a = 0, b = 0;
+    while (a < K1.n_nodes && b < K2.n_nodes) {
+        if (K1.node_id[a] == K2.node_id[b]) {
+            for (int i1 = K1.node_start[a]; i1 < K1.node_start[a + 1]; ++i1) {
+                const int idx1 = K1.node_idx[i1];
+                if (K1.has_mp[idx1]) continue;
+                if (only_stereo) continue;   // bStereo1 = (!mpCamera2 && ...) is false on multi-camera keyframes
+                const omv_kp &kp1 = K1.kps[idx1];
+                const int cam1 = cam_of(K1, idx1);
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int i2 = K2.node_start[b]; i2 < K2.node_start[b + 1]; ++i2) {
+                    const int idx2 = K2.node_idx[i2];
+                    if (K2.has_mp[idx2]) continue;
+                    const int dist = hamming(K1.desc + 32 * (size_t)idx1, K2.desc + 32 * (size_t)idx2);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const omv_kp &kp2 = K2.kps[idx2];
+                    const int cam2 = cam_of(K2, idx2);
+                    const int pr = pair_of(cam1, cam2);
+                    if (pr >= 0) state = pr;
+                    static const int pc1[10] = {0, 0, 1, 1, 0, 2, 2, 1, 3, 3}, pc2[10] = {0, 1, 0, 1, 2, 0, 2, 3, 1, 3};
+                    bool ok = coarse != 0;
+                    if (!ok)
+                        ok = triangulate_matches(cams + 8 * pc1[state], cams + 8 * pc2[state], kp1, kp2, P->T[state],
+                                                 P->T[state] + 9, K1.level_sigma2[kp1.octave],
+                                                 K2.level_sigma2[kp2.octave]) > 0.0001f;
+                    if (ok) bestIdx2 = idx2, bestDist = dist;
+                }
+                if (bestIdx2 >= 0) {
+                    const omv_kp &kp2 = K2.kps[bestIdx2];
+                    P->match12[idx1] = bestIdx2;
+                    nmatches++;
+                    if (check_ori) {
+                        float rot = kp1.angle - kp2.angle;
+                        if (rot < 0.0) rot += 360.0f;
+                        int bin = (int)std::round(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        hist[bin].push_back(idx1);
+                    }
+                }
+            }
+            ++a, ++b;
+        } else if (K1.node_id[a] < K2.node_id[b]) {
+            ++a;   // lower_bound(f2it->first)
+        } else {
+            ++b;
+        }
+    }
+    if (check_ori) {
+        int cnt[HISTO_LENGTH], ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HISTO_LENGTH; ++i) cnt[i] = (int)hist[i].size();
+        three_maxima(cnt, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int idx1 : hist[i]) P->match12[idx1] = -1, nmatches--;
+        }
+    }
+    return nmatches;
+}
+
+// Parity hooks for the camera-model pieces.
+void oracle_kb8_unproject(const float *cam, float x, float y, float *ray) { kb8_unproject_f(cam, x, y, ray); }
+void oracle_jacobi_svd4_v(const float *A, float *V) { jacobi_svd4_v(A, V); }
+float oracle_triangulate_matches(const float *cam1, const float *cam2, const omv_kp *kp1, const omv_kp *kp2,
+                                 const float *R12, const float *t12, float sigma, float unc) {
+    return triangulate_matches(cam1, cam2, *kp1, *kp2, R12, t12, sigma, unc);
+}
+
+}  // extern "C"
