@@ -1,0 +1,407 @@
+// MI355X-native ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1131-1456) for multi-camera
+// keyframe pairs, with KannalaBrandt8::epipolarConstrain / TriangulateMatches / unproject / Triangulate
+// (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429) and Eigen's
+// JacobiSVD<Matrix4f> restated in float.
+//
+// One wavefront per keyframe pair (pairs are independent: vbMatched2 is never set, :1204, :1261).  The
+// scan is the reference's: shared FeatureVector nodes in ascending id, for each keypoint idx1 of the
+// node (without a map point) the best candidate idx2 of the other keyframe's node by Hamming distance
+// (<= TH_LOW, later equal distances replace earlier ones) among those passing the epipolar test.  The
+// only sequential coupling is the camera-pair state (R12, t12, pCamera1, pCamera2) that persists from
+// one candidate to the next: pairs the reference lists assign it, the others reuse it.  So per node
+// chunk the wave first computes, in parallel, every (idx1, idx2) Hamming distance and — for listed
+// camera pairs, whose transform does not depend on the scan — the epipolar test; then lane 0 replays the
+// scan in order, running the epipolar test itself only for unlisted camera pairs (with the state the
+// replay has reached).  Float arithmetic without contraction; glibc's atan2f / tanf and correctly
+// rounded sqrtf are restated (omv_device.h), so the result is bit-exact to oracle/tri_oracle.cpp.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "../../include/omv.h"
+#include "omv_device.h"
+
+namespace {
+
+#define HIP_OK(x)                                                                    \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "omv: %s failed: %s\n", #x, hipGetErrorString(e_));      \
+            return OMV_ERR_HIP;                                                      \
+        }                                                                            \
+    } while (0)
+
+constexpr int kTriLow = 50;          // ORBmatcher::TH_LOW
+constexpr int kHisto = 30;           // HISTO_LENGTH
+constexpr int kCand = 8192;          // (idx1, idx2) candidates staged per node chunk (1 byte each)
+constexpr int kTriMaxKp = 16384;     // keypoints of keyframe 1 (orientation bins, 1 byte each)
+constexpr uint8_t kInvalid = 0xff, kListed = 0x40, kOk = 0x80;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// KannalaBrandt8::project(const Eigen::Vector3f&): cos / sin of the promoted float (C double functions)
+__device__ void kb8_project_f(const float *k, const float *X, float &u, float &v) {
+    const float x2y2 = X[0] * X[0] + X[1] * X[1];
+    const float theta = omv::glibc_atan2f(omv::sqrtf_cr(x2y2), X[2]);
+    const float psi = omv::glibc_atan2f(X[1], X[0]);
+    const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+    const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+    u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
+    v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
+}
+
+// KannalaBrandt8::unproject (precision 1e-6, <= 10 Newton steps, scale = std::tan(theta) / theta_d)
+__device__ void kb8_unproject_f(const float *k, float px, float py, float *ray) {
+    const float pwx = (px - k[2]) / k[0], pwy = (py - k[3]) / k[1];
+    float scale = 1.f;
+    float theta_d = omv::sqrtf_cr(pwx * pwx + pwy * pwy);
+    theta_d = fminf(fmaxf((float)(-3.14159265358979323846 / 2.f), theta_d), (float)(3.14159265358979323846 / 2.f));
+    if ((double)theta_d > 1e-8) {
+        float theta = theta_d;
+        for (int j = 0; j < 10; j++) {
+            const float theta2 = theta * theta, theta4 = theta2 * theta2, theta6 = theta4 * theta2,
+                        theta8 = theta4 * theta4;
+            const float k0_theta2 = k[4] * theta2, k1_theta4 = k[5] * theta4;
+            const float k2_theta6 = k[6] * theta6, k3_theta8 = k[7] * theta8;
+            const float theta_fix = (theta * (1 + k0_theta2 + k1_theta4 + k2_theta6 + k3_theta8) - theta_d) /
+                                    (1 + 3 * k0_theta2 + 5 * k1_theta4 + 7 * k2_theta6 + 9 * k3_theta8);
+            theta = theta - theta_fix;
+            if (fabsf(theta_fix) < 1e-6f) break;
+        }
+        scale = omv::glibc_tanf(theta) / theta_d;
+    }
+    ray[0] = pwx * scale, ray[1] = pwy * scale, ray[2] = 1.f;
+}
+
+// Eigen::JacobiSVD<Matrix4f>(A, ComputeFullV).matrixV() (row-major A, V): square, no QR preconditioner;
+// scale by max |a_ij|; cyclic two-sided Jacobi sweeps with threshold max(FLT_MIN, 2 eps maxDiagEntry);
+// singular values sorted descending (first max), V's columns with them.
+__device__ void jacobi_svd4_v(const float *A, float *V) {
+    float W[16];
+    float scale = 0.f;
+    for (int i = 0; i < 16; ++i) scale = fmaxf(scale, fabsf(A[i]));
+    if (scale == 0.f) scale = 1.f;
+    for (int i = 0; i < 16; ++i) W[i] = A[i] / scale, V[i] = (i % 5 == 0) ? 1.f : 0.f;
+    const float considerAsZero = 1.17549435e-38f, precision = 2.f * 1.1920928955078125e-07f;
+    float maxDiag = fabsf(W[0]);
+    for (int i = 1; i < 4; ++i) maxDiag = fmaxf(maxDiag, fabsf(W[5 * i]));
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        for (int p = 1; p < 4; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float threshold = fmaxf(considerAsZero, precision * maxDiag);
+                if (!(fabsf(W[4 * p + q]) > threshold || fabsf(W[4 * q + p]) > threshold)) continue;
+                finished = false;
+                const float m00 = W[4 * p + p], m01 = W[4 * p + q], m10 = W[4 * q + p], m11 = W[4 * q + q];
+                float c1, s1;
+                const float t = m00 + m11, d = m10 - m01;
+                if (fabsf(d) < considerAsZero) {
+                    s1 = 0.f, c1 = 1.f;
+                } else {
+                    const float u = t / d;
+                    const float tmp = omv::sqrtf_cr(1.f + u * u);
+                    s1 = 1.f / tmp, c1 = u / tmp;
+                }
+                float n00 = m00, n01 = m01, n11 = m11;
+                if (!(c1 == 1.f && s1 == 0.f)) {
+                    n00 = c1 * m00 + s1 * m10, n01 = c1 * m01 + s1 * m11;
+                    n11 = -s1 * m01 + c1 * m11;
+                }
+                float cr, sr;
+                const float deno = 2.f * fabsf(n01);
+                if (deno < considerAsZero) {
+                    cr = 1.f, sr = 0.f;
+                } else {
+                    const float tau = (n00 - n11) / deno;
+                    const float w = omv::sqrtf_cr(tau * tau + 1.f);
+                    const float tt = tau > 0.f ? 1.f / (tau + w) : 1.f / (tau - w);
+                    const float sign_t = tt > 0.f ? 1.f : -1.f;
+                    const float n = 1.f / omv::sqrtf_cr(tt * tt + 1.f);
+                    sr = -sign_t * (n01 / fabsf(n01)) * fabsf(tt) * n;
+                    cr = n;
+                }
+                const float cl = c1 * cr - s1 * -sr, sl = c1 * -sr + s1 * cr;
+                if (!(cl == 1.f && sl == 0.f))
+                    for (int k = 0; k < 4; ++k) {
+                        const float xi = W[4 * p + k], yi = W[4 * q + k];
+                        W[4 * p + k] = cl * xi + sl * yi;
+                        W[4 * q + k] = -sl * xi + cl * yi;
+                    }
+                if (!(cr == 1.f && -sr == 0.f))
+                    for (int k = 0; k < 4; ++k) {
+                        float xi = W[4 * k + p], yi = W[4 * k + q];
+                        W[4 * k + p] = cr * xi + -sr * yi;
+                        W[4 * k + q] = -(-sr) * xi + cr * yi;
+                        xi = V[4 * k + p], yi = V[4 * k + q];
+                        V[4 * k + p] = cr * xi + -sr * yi;
+                        V[4 * k + q] = -(-sr) * xi + cr * yi;
+                    }
+                maxDiag = fmaxf(maxDiag, fmaxf(fabsf(W[4 * p + p]), fabsf(W[4 * q + q])));
+            }
+    }
+    float sv[4];
+    for (int i = 0; i < 4; ++i) sv[i] = fabsf(W[5 * i]) * scale;
+    for (int i = 0; i < 4; ++i) {
+        int pos = i;
+        for (int j = i + 1; j < 4; ++j)
+            if (sv[j] > sv[pos]) pos = j;
+        if (sv[pos] == 0.f) break;
+        if (pos != i) {
+            const float t = sv[i];
+            sv[i] = sv[pos], sv[pos] = t;
+            for (int k = 0; k < 4; ++k) {
+                const float u = V[4 * k + i];
+                V[4 * k + i] = V[4 * k + pos], V[4 * k + pos] = u;
+            }
+        }
+    }
+}
+
+// KannalaBrandt8::TriangulateMatches (z1 > 0 on success, -1 .. -5 on the reference's rejections)
+__device__ float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2,
+                                     const float *R12, const float *t12, float sigmaLevel, float unc) {
+    float r1[3], r2[3], r21[3];
+    kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
+    kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
+    for (int i = 0; i < 3; ++i) r21[i] = R12[3 * i] * r2[0] + R12[3 * i + 1] * r2[1] + R12[3 * i + 2] * r2[2];
+    const float dot = r1[0] * r21[0] + r1[1] * r21[1] + r1[2] * r21[2];
+    const float n1 = omv::sqrtf_cr(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+    const float n21 = omv::sqrtf_cr(r21[0] * r21[0] + r21[1] * r21[1] + r21[2] * r21[2]);
+    const float cosParallaxRays = dot / (n1 * n21);
+    if ((double)cosParallaxRays > 0.9998) return -1;
+    float R21[9], t2[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R21[3 * i + j] = R12[3 * j + i];
+    for (int i = 0; i < 3; ++i) t2[i] = -R21[3 * i] * t12[0] + -R21[3 * i + 1] * t12[1] + -R21[3 * i + 2] * t12[2];
+    // Triangulate: A rows p.x T.row(2) - T.row(0), p.y T.row(2) - T.row(1); Tcw1 = [I | 0], Tcw2 = [R21 | t2]
+    const float T1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float T2[12] = {R21[0], R21[1], R21[2], t2[0], R21[3], R21[4], R21[5], t2[1], R21[6], R21[7], R21[8], t2[2]};
+    float A[16], V[16];
+    for (int j = 0; j < 4; ++j) {
+        A[j] = r1[0] * T1[8 + j] - T1[j];
+        A[4 + j] = r1[1] * T1[8 + j] - T1[4 + j];
+        A[8 + j] = r2[0] * T2[8 + j] - T2[j];
+        A[12 + j] = r2[1] * T2[8 + j] - T2[4 + j];
+    }
+    jacobi_svd4_v(A, V);
+    float x3D[3];
+    for (int i = 0; i < 3; ++i) x3D[i] = V[4 * i + 3] / V[15];
+    const float z1 = x3D[2];
+    if (z1 <= 0) return -2;
+    const float z2 = R21[6] * x3D[0] + R21[7] * x3D[1] + R21[8] * x3D[2] + t2[2];
+    if (z2 <= 0) return -3;
+    float u1, v1;
+    kb8_project_f(cam1, x3D, u1, v1);
+    const float ex1 = u1 - kp1.x, ey1 = v1 - kp1.y;
+    if ((double)(ex1 * ex1 + ey1 * ey1) > 5.991 * (double)sigmaLevel) return -4;
+    float x3D2[3];
+    for (int i = 0; i < 3; ++i) x3D2[i] = R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2] + t2[i];
+    float u2, v2;
+    kb8_project_f(cam2, x3D2, u2, v2);
+    const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
+    if ((double)(ex2 * ex2 + ey2 * ey2) > 5.991 * (double)unc) return -5;
+    return z1;
+}
+
+__device__ __forceinline__ int cam_of(const omv_kf_view &k, int idx) {
+    return idx < k.n_left ? 0 : idx < k.n_left + k.n_right ? 1 : idx < k.n_left + k.n_right + k.n_sideleft ? 2 : 3;
+}
+// (cameraId1, cameraId2) -> OMV_TRI_PAIRS index, or -1 where the reference keeps R12 / t12 (:1300-1392)
+__device__ __forceinline__ int pair_of(int c1, int c2) {
+    const int code = c1 * 4 + c2;
+    switch (code) {
+        case 0: return 0;    // LL
+        case 1: return 1;    // LR
+        case 4: return 2;    // RL
+        case 5: return 3;    // RR
+        case 2: return 4;    // L-SL
+        case 8: return 5;    // SL-L
+        case 10: return 6;   // SL-SL
+        case 7: return 7;    // R-SR
+        case 13: return 8;   // SR-R
+        case 15: return 9;   // SR-SR
+        default: return -1;
+    }
+}
+__device__ __constant__ int kPairCam1[10] = {0, 0, 1, 1, 0, 2, 2, 1, 3, 3};
+__device__ __constant__ int kPairCam2[10] = {0, 1, 0, 1, 2, 0, 2, 3, 1, 3};
+
+struct TriCams {
+    float cam[4][8];
+};
+
+__device__ bool epipolar_ok(const omv_tri_pair &P, const TriCams &C, int pr, const omv_kp &kp1, const omv_kp &kp2) {
+    return triangulate_matches(C.cam[kPairCam1[pr]], C.cam[kPairCam2[pr]], kp1, kp2, P.T[pr], P.T[pr] + 9,
+                               P.kf1.level_sigma2[kp1.octave], P.kf2.level_sigma2[kp2.octave]) > 0.0001f;
+}
+
+__global__ void __launch_bounds__(64) tri_kernel(const omv_tri_pair *pairs, TriCams C, int only_stereo, int coarse,
+                                                 int check_ori, int32_t *n_matches, int *err) {
+    __shared__ uint8_t cand[kCand];
+    __shared__ uint8_t bins[kTriMaxKp];
+    __shared__ int hist[kHisto];
+    __shared__ int s_keep[kHisto];
+    __shared__ int s_removed;
+    const omv_tri_pair &P = pairs[blockIdx.x];
+    const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < K1.n; i += 64) P.match12[i] = -1;
+    if (K1.n > kTriMaxKp) {
+        if (lane == 0) atomicExch(err, OMV_ERR_CAPACITY), n_matches[blockIdx.x] = 0;
+        return;
+    }
+    for (int i = lane; i < K1.n; i += 64) bins[i] = 0xff;
+    if (lane < kHisto) hist[lane] = 0;
+    wave_sync();
+    int state = 0;   // the persistent camera-pair state; LL before any assignment
+    int nmatch = 0;
+    int a = 0, b = 0;
+    while (a < K1.n_nodes && b < K2.n_nodes) {   // FeatureVector intersection in ascending node id
+        const uint32_t ia = K1.node_id[a], ib = K2.node_id[b];
+        if (ia < ib) {
+            ++a;
+            continue;
+        }
+        if (ib < ia) {
+            ++b;
+            continue;
+        }
+        const int s1 = K1.node_start[a], n1 = K1.node_start[a + 1] - s1;
+        const int s2 = K2.node_start[b], n2 = K2.node_start[b + 1] - s2;
+        ++a, ++b;
+        if (n2 == 0 || n1 == 0) continue;
+        if (n2 > kCand) {
+            if (lane == 0) atomicExch(err, OMV_ERR_CAPACITY);
+            continue;
+        }
+        const int chunk = kCand / n2;
+        for (int c0 = 0; c0 < n1; c0 += chunk) {
+            const int cn = min(chunk, n1 - c0);
+            // phase A: distances + epipolar tests of listed camera pairs, one candidate per lane
+            for (int q = lane; q < cn * n2; q += 64) {
+                const int i1 = q / n2, i2 = q - i1 * n2;
+                const int idx1 = K1.node_idx[s1 + c0 + i1], idx2 = K2.node_idx[s2 + i2];
+                uint8_t code = kInvalid;
+                if (!K1.has_mp[idx1] && !only_stereo && !K2.has_mp[idx2]) {
+                    const int dist = omv::hamming256((const uint64_t *)(K1.desc + 32 * (size_t)idx1),
+                                                     (const uint64_t *)(K2.desc + 32 * (size_t)idx2));
+                    if (dist <= kTriLow) {
+                        code = (uint8_t)dist;
+                        const int pr = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
+                        if (pr >= 0) {
+                            code |= kListed;
+                            if (coarse || epipolar_ok(P, C, pr, K1.kps[idx1], K2.kps[idx2])) code |= kOk;
+                        }
+                    }
+                }
+                cand[q] = code;
+            }
+            wave_sync();
+            // phase B: the reference's scan, in order
+            if (lane == 0) {
+                for (int i1 = 0; i1 < cn; ++i1) {
+                    const int idx1 = K1.node_idx[s1 + c0 + i1];
+                    if (K1.has_mp[idx1] || only_stereo) continue;
+                    int bestDist = kTriLow, bestIdx2 = -1;
+                    for (int i2 = 0; i2 < n2; ++i2) {
+                        const uint8_t code = cand[i1 * n2 + i2];
+                        if (code == kInvalid) continue;
+                        const int dist = code & 0x3f;
+                        if (dist > bestDist) continue;
+                        const int idx2 = K2.node_idx[s2 + i2];
+                        bool ok;
+                        if (code & kListed) {
+                            state = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
+                            ok = (code & kOk) != 0;
+                        } else {
+                            ok = coarse || epipolar_ok(P, C, state, K1.kps[idx1], K2.kps[idx2]);
+                        }
+                        if (ok) bestIdx2 = idx2, bestDist = dist;
+                    }
+                    if (bestIdx2 >= 0) {
+                        P.match12[idx1] = bestIdx2;
+                        ++nmatch;
+                        if (check_ori) {
+                            float rot = K1.kps[idx1].angle - K2.kps[bestIdx2].angle;
+                            if ((double)rot < 0.0) rot += 360.0f;
+                            int bin = (int)roundf(rot * (1.0f / kHisto));
+                            if (bin == kHisto) bin = 0;
+                            bins[idx1] = (uint8_t)bin;
+                        }
+                    }
+                }
+            }
+            wave_sync();
+        }
+    }
+    if (check_ori) {   // rotation histogram: keep the three largest bins (ComputeThreeMaxima, :2537-2573)
+        for (int i = lane; i < K1.n; i += 64)
+            if (bins[i] != 0xff) atomicAdd(&hist[bins[i]], 1);
+        if (lane == 0) s_removed = 0;
+        wave_sync();
+        if (lane == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < kHisto; i++) {
+                const int s = hist[i];
+                if (s > max1) {
+                    max3 = max2, max2 = max1, max1 = s;
+                    ind3 = ind2, ind2 = ind1, ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2, max2 = s;
+                    ind3 = ind2, ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+            else if (max3 < 0.1f * (float)max1) ind3 = -1;
+            for (int i = 0; i < kHisto; ++i) s_keep[i] = (i == ind1 || i == ind2 || i == ind3) ? 1 : 0;
+        }
+        wave_sync();
+        int removed = 0;
+        for (int i = lane; i < K1.n; i += 64)
+            if (bins[i] != 0xff && !s_keep[bins[i]]) P.match12[i] = -1, ++removed;
+        for (int d = 32; d >= 1; d >>= 1) removed += __shfl_xor(removed, d, 64);
+        if (lane == 0) nmatch -= removed;
+    }
+    if (lane == 0) n_matches[blockIdx.x] = nmatch;
+}
+
+}  // namespace
+
+extern "C" {
+
+omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
+                                                const float *cams, int only_stereo, int coarse, int check_ori,
+                                                int32_t *n_matches, void *stream) {
+    if (!m || n_pairs < 0 || (n_pairs > 0 && (!pairs || !cams || !n_matches))) return OMV_ERR_ARG;
+    if (n_pairs == 0) return OMV_OK;
+    for (int i = 0; i < n_pairs; ++i)
+        if (!pairs[i].match12 || pairs[i].kf1.n < 0 || pairs[i].kf2.n < 0) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    TriCams C;
+    for (int c = 0; c < 4; ++c)
+        for (int q = 0; q < 8; ++q) C.cam[c][q] = cams[8 * c + q];
+    omv_tri_pair *d_pairs = nullptr;
+    int *d_err = nullptr;
+    HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(omv_tri_pair) * n_pairs + sizeof(int), st));
+    d_err = (int *)(d_pairs + n_pairs);
+    HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(omv_tri_pair) * n_pairs, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
+    tri_kernel<<<n_pairs, 64, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err);
+    HIP_OK(hipGetLastError());
+    int h_err = 0;
+    HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipFreeAsync(d_pairs, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return h_err ? (omv_status)h_err : OMV_OK;
+}
+
+}  // extern "C"

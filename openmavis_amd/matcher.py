@@ -155,6 +155,45 @@ class ORBmatcher:
             "omv_matcher_search_last_frame")
         return frames.n_matches
 
+    def SearchForTriangulation(self, pairs, cams, bOnlyStereo=False, bCoarse=False, stream=None):
+        """ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1131-1456) for a batch of multi-camera
+        keyframe pairs.  pairs: list of dicts {kf1, kf2, T, match12}: kf* hold the omv_kf_view fields
+        (n, n_left, n_right, n_sideleft ints; kps / desc / has_mp / node_id / node_start / node_idx device
+        tensors; level_sigma2 host floats), T the 10 camera-pair transforms (float [10][12]), match12 a
+        device int32 [kf1.n] receiving vMatches12.  cams: host [4][8] KB8 parameters (L, R, SL, SR).
+        Returns the per-pair match counts (device int32 tensor); synchronous."""
+        import torch
+        from .synth_tri import kf_struct
+        if self._h is None:
+            h = ctypes.c_void_p()
+            _lib.check(self._lib.omv_matcher_create(1, 1, 1, 1, ctypes.byref(h)), "omv_matcher_create")
+            self._h, self._shape = h, (1, 1, 1, 1)
+        n = len(pairs)
+        arr = (_lib.TriPair * max(n, 1))()
+        keep = []
+
+        def ptr(_name, t):
+            keep.append(t)
+            return ctypes.c_void_p(t.data_ptr())
+
+        dev = None
+        for i, p in enumerate(pairs):
+            arr[i].kf1 = kf_struct(p["kf1"], _lib.KfView, p["kf1"]["level_sigma2"], ptr)
+            arr[i].kf2 = kf_struct(p["kf2"], _lib.KfView, p["kf2"]["level_sigma2"], ptr)
+            T = np.asarray(p["T"], np.float32).reshape(_lib.OMV_TRI_PAIRS, 12)
+            for r in range(_lib.OMV_TRI_PAIRS):
+                for c in range(12):
+                    arr[i].T[r][c] = float(T[r, c])
+            arr[i].match12 = ctypes.c_void_p(p["match12"].data_ptr())
+            dev = p["match12"].device
+        out = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        c = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(4, 8))
+        _lib.check(self._lib.omv_matcher_search_for_triangulation(
+            self._h, n, arr, _lib.ptr(c), int(bool(bOnlyStereo)), int(bool(bCoarse)), int(self.mbCheckOrientation),
+            _lib.ptr(out), self._stream(stream)), "omv_matcher_search_for_triangulation")
+        del keep
+        return out[:n]
+
     def StereoLapping(self, frames, ratio=0.8, stream=None):
         """Lowe-ratio knn candidates of ComputeMultiFishEyeMatches (before triangulation)."""
         h = self._handle(frames)

@@ -1,0 +1,53 @@
+"""GPU parity of SearchForTriangulation (openmavis_amd/csrc/tri.hip) against the CPU oracle
+(oracle/tri_oracle.cpp): vMatches12 and the match count bit-exact (integer / index output; the float
+triangulation is restated op-for-op on both sides, glibc tanf / atan2f included)."""
+import numpy as np
+import pytest
+
+from openmavis_amd import synth_tri
+from openmavis_amd.matcher import ORBmatcher
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_pairs(pairs):
+    import torch
+    out = []
+    for p in pairs:
+        q = dict(T=p["T"])
+        for k in ("kf1", "kf2"):
+            kf = p[k]
+            d = {f: kf[f] for f in ("n", "n_left", "n_right", "n_sideleft")}
+            d["kps"] = torch.from_numpy(kf["kps"].view(np.float32).reshape(-1, 6).copy()).cuda()
+            for f in ("desc", "has_mp", "node_start", "node_idx"):
+                d[f] = torch.from_numpy(np.ascontiguousarray(kf[f])).cuda()
+            d["node_id"] = torch.from_numpy(kf["node_id"].view(np.int32).copy()).cuda()
+            d["level_sigma2"] = p["level_sigma2"]
+            q[k] = d
+        q["match12"] = torch.full((p["kf1"]["n"],), -9, dtype=torch.int32, device="cuda")
+        out.append(q)
+    return out
+
+
+@pytest.mark.parametrize("check_ori,coarse", [(False, False), (True, False), (False, True)])
+def test_search_for_triangulation_matches_oracle(oracle, check_ori, coarse):
+    pairs = [synth_tri.make_tri_pair(seed=s, n_pts=400 + 50 * s) for s in range(1, 9)]
+    dp = _device_pairs(pairs)
+    m = ORBmatcher(0.6, check_ori)
+    n = m.SearchForTriangulation(dp, pairs[0]["cams"], bCoarse=coarse).cpu().numpy()
+    for i, p in enumerate(pairs):
+        n_o, m_o = oracle.search_for_triangulation(p, coarse=coarse, check_ori=check_ori)
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
+
+
+def test_search_for_triangulation_edge_cases(oracle):
+    """All keypoints already carry map points; bOnlyStereo on multi-camera keyframes; an empty pair."""
+    p = synth_tri.make_tri_pair(seed=11)
+    p_full = dict(p, kf1=dict(p["kf1"], has_mp=np.ones_like(p["kf1"]["has_mp"])))
+    dp = _device_pairs([p, p_full])
+    m = ORBmatcher(0.6, False)
+    assert m.SearchForTriangulation(dp[:1], p["cams"], bOnlyStereo=True).cpu().numpy()[0] == 0
+    n = m.SearchForTriangulation(dp, p["cams"]).cpu().numpy()
+    assert n[1] == 0 and (dp[1]["match12"].cpu().numpy() == -1).all()
+    assert n[0] == oracle.search_for_triangulation(p)[0]
