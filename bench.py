@@ -195,6 +195,100 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
     }
 
 
+def pose_leg(batch, cpu_batch, reps, dev):
+    """PoseInertialOptimizationLastKeyFrame (Optimizer.cc:5021-5578) on a batch of tracked frames: one call =
+    every frame's 4 rounds x 10 Gauss-Newton iterations + outlier passes + marginal Hessian; value = frames/s
+    (state reset by a device copy outside the timed region)."""
+    import torch
+    from openmavis_amd import synth_pose
+    from openmavis_amd.optimizer import PoseInertialOptimizer
+    F = int(batch["n_frames"])
+    init = {k: torch.tensor(np.asarray(batch[k], np.float64), device=dev) for k in synth_pose.STATE_KEYS}
+    arrays = {k: v.clone() for k, v in init.items()}
+    for k in synth_pose.INPUT_KEYS:
+        arrays[k] = torch.from_numpy(np.ascontiguousarray(batch[k])).to(dev)
+    kpo = torch.zeros((F, int(batch["kp_cap"])), dtype=torch.uint8, device=dev)
+    H = torch.zeros((F, 225), dtype=torch.float64, device=dev)
+    opt = PoseInertialOptimizer(max_frames=F, max_edges=max(len(batch["mono_cam"]), len(batch["stereo_cam"]), 1))
+    for _ in range(2):
+        opt.PoseInertialOptimizationLastKeyFrame(batch, arrays, kpo, H)
+    torch.cuda.synchronize(dev)
+    total = 0.0
+    for _ in range(reps):
+        for k in init:
+            arrays[k].copy_(init[k])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        opt.PoseInertialOptimizationLastKeyFrame(batch, arrays, kpo, H)
+        torch.cuda.synchronize(dev)
+        total += time.perf_counter() - t0
+    out = {"metric": "PoseInertialOptimizationLastKeyFrame frames/s", "value": round(F * reps / total, 1),
+           "unit": "frames/s", "ms_per_batch": round(total / reps * 1e3, 3), "frames_per_batch": F,
+           "edges_per_frame": round(len(batch["mono_cam"]) / F, 1), "dtype": "f64"}
+    if cpu_batch is not None:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        t0 = time.perf_counter()
+        done = 0
+        while done == 0 or time.perf_counter() - t0 < 2.0:   # a ~2 s sample
+            oracle.pose_last_kf(cpu_batch)
+            done += int(cpu_batch["n_frames"])
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / dt, 1), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{done} frame optimisations ({cpu_batch['n_frames']} distinct frames of the "
+                                         f"batch), oracle C++ restatement, 1 thread, {dt:.2f} s"}
+    return out
+
+
+def tri_leg(pairs, n_pairs, reps, dev):
+    """ORBmatcher::SearchForTriangulation (ORBmatcher.cc:1131-1456) over a batch of multi-camera keyframe pairs
+    (KannalaBrandt8 epipolar test with the 4x4 JacobiSVD triangulation); value = keyframe pairs/s."""
+    import torch
+    from openmavis_amd.matcher import ORBmatcher
+    dp = []
+    for i in range(n_pairs):
+        p = pairs[i % len(pairs)]
+        q = dict(T=p["T"])
+        for k in ("kf1", "kf2"):
+            kf = p[k]
+            d = {f: kf[f] for f in ("n", "n_left", "n_right", "n_sideleft")}
+            d["kps"] = torch.from_numpy(kf["kps"].view(np.float32).reshape(-1, 6).copy()).to(dev)
+            for f in ("desc", "has_mp", "node_start", "node_idx"):
+                d[f] = torch.from_numpy(np.ascontiguousarray(kf[f])).to(dev)
+            d["node_id"] = torch.from_numpy(kf["node_id"].view(np.int32).copy()).to(dev)
+            d["level_sigma2"] = p["level_sigma2"]
+            q[k] = d
+        q["match12"] = torch.empty(p["kf1"]["n"], dtype=torch.int32, device=dev)
+        dp.append(q)
+    m = ORBmatcher(0.6, False)   # LocalMapping::CreateNewMapPoints: ORBmatcher(0.6, false)
+    cams = pairs[0]["cams"]
+    for _ in range(2):
+        m.SearchForTriangulation(dp, cams)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        n = m.SearchForTriangulation(dp, cams)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    out = {"metric": "SearchForTriangulation keyframe pairs/s", "value": round(n_pairs * reps / dt, 1),
+           "unit": "keyframe pairs/s", "ms_per_batch": round(dt / reps * 1e3, 3), "pairs_per_batch": n_pairs,
+           "keypoints_per_keyframe": int(np.mean([p["kf1"]["n"] for p in pairs])),
+           "matches_per_pair": round(float(n.float().mean().item()), 1)}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    t0 = time.perf_counter()
+    done = 0
+    while done == 0 or time.perf_counter() - t0 < 2.0:   # a ~2 s sample
+        for p in pairs:
+            oracle.search_for_triangulation(p)
+        done += len(pairs)
+    dt = time.perf_counter() - t0
+    out["cpu_baseline"] = {"value": round(done / dt, 1), "unit": "keyframe pairs/s", "cores": 1, "kind": "port",
+                           "sample": f"{done} pair searches ({len(pairs)} distinct pairs), oracle C++ restatement, "
+                                     f"1 thread, {dt:.2f} s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -213,6 +307,8 @@ def main():
                          "instead of running a window replica per rank")
     ap.add_argument("--cpu-frames", type=int, default=120, help="frames in the CPU-baseline sample (~6 s)")
     ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
+    ap.add_argument("--pose-frames", type=int, default=1024, help="frames per PoseInertialOptimization batch (0: skip)")
+    ap.add_argument("--tri-pairs", type=int, default=256, help="keyframe pairs per SearchForTriangulation batch (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,6 +324,15 @@ def main():
     if args.lba_steps > 0:
         from openmavis_amd import synth_ba
         lba_prob = synth_ba.make_lba_problem(seed=5)   # configs[4] window (same on every rank)
+    pose_batch = pose_cpu = None
+    if args.pose_frames > 0:
+        from openmavis_amd import synth_pose
+        pose_cpu = synth_pose.make_pose_batch(n_frames=32, n_pts=1000, seed=1, outlier_frac=0.1)
+        pose_batch = synth_pose.tile_batch(pose_cpu, args.pose_frames)
+    tri_pairs = None
+    if args.tri_pairs > 0:
+        from openmavis_amd import synth_tri
+        tri_pairs = [synth_tri.make_tri_pair(seed=s, n_pts=1200, n_distract=600) for s in range(16)]
 
     import torch
     import torch.distributed as dist
@@ -339,6 +444,9 @@ def main():
             stages["frustum"] = stages.get("frustum", 0.0) + sum(a.elapsed_time(b) for a, b in gr["ev"]) / args.steps
 
     lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world, args.lba_shard) if lba_prob is not None else None
+    pose = pose_leg(pose_batch, pose_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev) \
+        if pose_batch is not None else None
+    tri = tri_leg(tri_pairs, args.tri_pairs, 10, dev) if tri_pairs is not None else None
 
     if rank != 0:
         if world > 1:
@@ -408,6 +516,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "local_ba": lba,
+        "pose_inertial": pose,
+        "triangulation": tri,
     }
     print(json.dumps(out))
     if world > 1:

@@ -129,3 +129,22 @@ def as_pose_struct(batch, struct_cls, arrays):
     s.kp_cap = int(batch["kp_cap"])
     s.n_mono, s.n_stereo = int(len(batch["mono_cam"])), int(len(batch["stereo_cam"]))
     return s, keep
+
+
+def tile_batch(b, F):
+    """Repeat a generated batch's frames (with their edges) up to F frames (cheap large batches)."""
+    n0 = int(b["n_frames"])
+    out = dict(b)
+    fr = [f % n0 for f in range(F)]
+    for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba", "preint",
+              "true_Rwb", "true_twb", "true_vel"):
+        out[k] = np.ascontiguousarray(np.asarray(b[k])[fr])
+    for kind in ("mono", "stereo"):
+        st = b[f"{kind}_start"]
+        idx = np.concatenate([np.arange(st[f], st[f + 1]) for f in fr]).astype(np.int64)
+        counts = np.array([st[f + 1] - st[f] for f in fr])
+        out[f"{kind}_start"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        for k in [k for k in b if k.startswith(kind + "_") and k != f"{kind}_start"]:
+            out[k] = np.ascontiguousarray(np.asarray(b[k])[idx])
+    out["n_frames"] = F
+    return out
