@@ -155,6 +155,17 @@ omv_status omv_matcher_search_projection(omv_matcher *m, int n_frames, const omv
 omv_status omv_matcher_stereo_lapping(omv_matcher *m, int n_frames, const uint8_t *desc, const int *n_kp,
                                       const int *mono, double ratio, int32_t *l2r, int32_t *r2l, void *stream);
 
+/* The depth check of Frame::ComputeMultiFishEyeMatches (src/Frame.cc:1488-1512) on the pairs
+ * omv_matcher_stereo_lapping left in l2r: KannalaBrandt8::TriangulateMatches(mpCamera2, kpL, kpR,
+ * mRlr, mtlr, sigma2[octL], sigma2[octR]) > 1e-4 keeps a pair (l2r / r2l [frame][kp_cap], the later
+ * left index wins on r2l), writes mvDepth of the left keypoints (depth [frame][kp_cap], -1 elsewhere)
+ * and mvStereo3Dpoints (p3d [frame][kp_cap][3]); failures clear l2r.  kps: [frame][n_cams][kp_cap]
+ * (block 0 = left, 1 = right).  cams: host [2][8] (L, R); Rlr / tlr / level_sigma2: host. */
+omv_status omv_matcher_stereo_triangulate(omv_matcher *m, int n_frames, int n_cams, int kp_cap, const omv_kp *kps,
+                                          const int *n_kp, const int *mono, const float *cams, const float *Rlr,
+                                          const float *tlr, const float *level_sigma2, int nlevels, int32_t *l2r,
+                                          int32_t *r2l, float *depth, float *p3d, void *stream);
+
 /* Device-side error word (OMV_ERR_CAPACITY if a bound was hit) since the last call; syncs. */
 omv_status omv_matcher_last_error(omv_matcher *m);
 
@@ -383,6 +394,13 @@ typedef struct omv_tri_pair {
  * cameras the reference does not list ((L,SR), (SR,L), (R,SL), (SL,R), (SL,SR), (SR,SL)) is whatever the
  * previous candidate of the scan assigned (the reference's R12/t12/pCamera1/pCamera2 persist across
  * iterations); before any assignment it is LL (the reference's R12/t12 are uninitialised there). */
+/* Parity hook: KannalaBrandt8::unproject of kp1 (cams2[0]) and kp2 (cams2[1]), JacobiSVD<Matrix4f> V of
+ * svd_in (row-major 4x4), TriangulateMatches(kp1, kp2, R12, t12, sigma, unc) on one device thread:
+ * out31 = ray1[3] ray2[3] V[16] z p3D[3] x3D[3] uv1[2] (x3D / uv1: the triangulated point and its
+ * projection into camera 1 even when a later check rejects it).  Host pointers; synchronous. */
+omv_status omv_tri_debug(const float *cams2, const omv_kp *kp1, const omv_kp *kp2, const float *R12, const float *t12,
+                         const float *svd_in, float sigma, float unc, float *out31);
+
 omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
                                                 const float *cams, int only_stereo, int coarse, int check_ori,
                                                 int32_t *n_matches, void *stream);

@@ -187,6 +187,9 @@ SIGNATURES = {
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
     "omv_lba_reset": (_I, [_VP]),
     "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),
+    "omv_tri_debug": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _F, _F, _VP]),
+    "omv_matcher_stereo_triangulate": (_I, [_VP, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _VP,
+                                            _VP, _VP]),
     "omv_matcher_search_for_triangulation": (_I, [_VP, _I, ctypes.POINTER(TriPair), _VP, _I, _I, _I, _VP, _VP]),
     "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),
     "omv_pose_destroy": (_I, [_VP]),
@@ -226,10 +229,15 @@ def load(path=LIB_PATH):
     return lib
 
 
+class _Ptr(ctypes.c_void_p):
+    """A c_void_p that keeps its tensor / array alive while the call it is passed to runs (so that
+    `ptr(np.ascontiguousarray(x))` on a temporary cannot dangle)."""
+
+
 def ptr(t):
-    """Device/host pointer of a torch tensor or numpy array as c_void_p."""
+    """Device/host pointer of a torch tensor or numpy array as c_void_p (keeps `t` alive)."""
     if t is None:
         return None
-    if hasattr(t, "data_ptr"):
-        return ctypes.c_void_p(t.data_ptr())
-    return ctypes.c_void_p(t.ctypes.data)
+    p = _Ptr(t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data)
+    p._keep = t
+    return p

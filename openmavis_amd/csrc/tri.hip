@@ -165,7 +165,8 @@ __device__ void jacobi_svd4_v(const float *A, float *V) {
 
 // KannalaBrandt8::TriangulateMatches (z1 > 0 on success, -1 .. -5 on the reference's rejections)
 __device__ float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2,
-                                     const float *R12, const float *t12, float sigmaLevel, float unc) {
+                                     const float *R12, const float *t12, float sigmaLevel, float unc,
+                                     float *p3D = nullptr) {
     float r1[3], r2[3], r21[3];
     kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
     kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
@@ -206,6 +207,7 @@ __device__ float triangulate_matches(const float *cam1, const float *cam2, const
     kb8_project_f(cam2, x3D2, u2, v2);
     const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
     if ((double)(ex2 * ex2 + ey2 * ey2) > 5.991 * (double)unc) return -5;
+    if (p3D) p3D[0] = x3D[0], p3D[1] = x3D[1], p3D[2] = x3D[2];
     return z1;
 }
 
@@ -374,9 +376,118 @@ __global__ void __launch_bounds__(64) tri_kernel(const omv_tri_pair *pairs, TriC
     if (lane == 0) n_matches[blockIdx.x] = nmatch;
 }
 
+// Frame::ComputeMultiFishEyeMatches' depth check (src/Frame.cc:1488-1512) on the Lowe-filtered
+// lapping knn pairs (omv_matcher_stereo_lapping's l2r): one thread per left keypoint.
+struct StereoTriArgs {
+    const omv_kp *kps;
+    const int *n_kp, *mono;
+    int n_cams, kp_cap;
+    float camL[8], camR[8], Rlr[9], tlr[3], sigma2[16];
+    int32_t *l2r, *r2l;
+    float *depth, *p3d;
+};
+__global__ void stereo_reset_kernel(StereoTriArgs A) {
+    const int frame = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.kp_cap) return;
+    A.r2l[(size_t)frame * A.kp_cap + i] = -1;
+    A.depth[(size_t)frame * A.kp_cap + i] = -1.0f;
+}
+__global__ void stereo_tri_kernel(StereoTriArgs A) {
+    const int frame = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nL = A.n_kp[frame * A.n_cams];
+    if (i >= nL) return;
+    const size_t slot = (size_t)frame * A.kp_cap + i;
+    int32_t *l2r = A.l2r + slot;
+    const int r = *l2r;
+    if (r < 0) return;
+    const size_t base = (size_t)frame * A.n_cams * A.kp_cap;   // keypoints [frame][cam][kp_cap]: L = 0, R = 1
+    const omv_kp &kl = A.kps[base + i], &kr = A.kps[base + A.kp_cap + r];
+    float p3D[3];
+    const float depth = triangulate_matches(A.camL, A.camR, kl, kr, A.Rlr, A.tlr, A.sigma2[kl.octave],
+                                            A.sigma2[kr.octave], p3D);
+    if (depth > 0.0001f) {
+        A.depth[slot] = depth;
+        for (int q = 0; q < 3; ++q) A.p3d[slot * 3 + q] = p3D[q];
+        atomicMax(&A.r2l[(size_t)frame * A.kp_cap + r], i);   // the later left index wins
+    } else {
+        *l2r = -1;
+    }
+}
+
+// Parity hook: the camera-model pieces for one input (out: ray1[3] ray2[3] V[16] z p3D[3]).
+__global__ void tri_debug_kernel(TriCams C, omv_kp kp1, omv_kp kp2, const float *Rt, float sigma, float unc, float *out) {
+    kb8_unproject_f(C.cam[0], kp1.x, kp1.y, out);
+    kb8_unproject_f(C.cam[1], kp2.x, kp2.y, out + 3);
+    float A[16];
+    for (int i = 0; i < 16; ++i) A[i] = Rt[12 + i];
+    jacobi_svd4_v(A, out + 6);
+    out[22] = triangulate_matches(C.cam[0], C.cam[1], kp1, kp2, Rt, Rt + 9, sigma, unc, out + 23);
+    // intermediates of the triangulation of (kp1, kp2): x3D[3] and its projection uv1[2] -> out[26..30]
+    float r1[3], r2[3], R21[9], t2[3], V[16];
+    kb8_unproject_f(C.cam[0], kp1.x, kp1.y, r1);
+    kb8_unproject_f(C.cam[1], kp2.x, kp2.y, r2);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R21[3 * i + j] = Rt[3 * j + i];
+    for (int i = 0; i < 3; ++i) t2[i] = -R21[3 * i] * Rt[9] + -R21[3 * i + 1] * Rt[10] + -R21[3 * i + 2] * Rt[11];
+    const float T1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float T2[12] = {R21[0], R21[1], R21[2], t2[0], R21[3], R21[4], R21[5], t2[1], R21[6], R21[7], R21[8], t2[2]};
+    for (int j = 0; j < 4; ++j) {
+        A[j] = r1[0] * T1[8 + j] - T1[j];
+        A[4 + j] = r1[1] * T1[8 + j] - T1[4 + j];
+        A[8 + j] = r2[0] * T2[8 + j] - T2[j];
+        A[12 + j] = r2[1] * T2[8 + j] - T2[4 + j];
+    }
+    jacobi_svd4_v(A, V);
+    float x3D[3];
+    for (int i = 0; i < 3; ++i) x3D[i] = V[4 * i + 3] / V[15];
+    float u1, v1;
+    kb8_project_f(C.cam[0], x3D, u1, v1);
+    out[26] = x3D[0], out[27] = x3D[1], out[28] = x3D[2], out[29] = u1, out[30] = v1;
+}
+
 }  // namespace
 
 extern "C" {
+
+omv_status omv_tri_debug(const float *cams2, const omv_kp *kp1, const omv_kp *kp2, const float *R12, const float *t12,
+                         const float *svd_in, float sigma, float unc, float *out31) {
+    if (!cams2 || !kp1 || !kp2 || !R12 || !t12 || !svd_in || !out31) return OMV_ERR_ARG;
+    TriCams C{};
+    for (int q = 0; q < 16; ++q) C.cam[q / 8][q % 8] = cams2[q];
+    float h[28];
+    for (int q = 0; q < 9; ++q) h[q] = R12[q];
+    for (int q = 0; q < 3; ++q) h[9 + q] = t12[q];
+    for (int q = 0; q < 16; ++q) h[12 + q] = svd_in[q];
+    float *d = nullptr;
+    HIP_OK(hipMalloc(&d, sizeof(float) * (28 + 31)));
+    HIP_OK(hipMemcpy(d, h, sizeof(float) * 28, hipMemcpyHostToDevice));
+    tri_debug_kernel<<<1, 1>>>(C, *kp1, *kp2, d, sigma, unc, d + 28);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpy(out31, d + 28, sizeof(float) * 31, hipMemcpyDeviceToHost));
+    HIP_OK(hipFree(d));
+    return OMV_OK;
+}
+
+omv_status omv_matcher_stereo_triangulate(omv_matcher *m, int n_frames, int n_cams, int kp_cap, const omv_kp *kps,
+                                          const int *n_kp, const int *mono, const float *cams, const float *Rlr,
+                                          const float *tlr, const float *level_sigma2, int nlevels, int32_t *l2r,
+                                          int32_t *r2l, float *depth, float *p3d, void *stream) {
+    if (!m || n_frames <= 0 || n_cams < 2 || kp_cap <= 0 || !kps || !n_kp || !mono || !cams || !Rlr || !tlr ||
+        !level_sigma2 || nlevels <= 0 || nlevels > 16 || !l2r || !r2l || !depth || !p3d)
+        return OMV_ERR_ARG;
+    StereoTriArgs A{kps, n_kp, mono, n_cams, kp_cap, {}, {}, {}, {}, {}, l2r, r2l, depth, p3d};
+    for (int q = 0; q < 8; ++q) A.camL[q] = cams[q], A.camR[q] = cams[8 + q];
+    for (int q = 0; q < 9; ++q) A.Rlr[q] = Rlr[q];
+    for (int q = 0; q < 3; ++q) A.tlr[q] = tlr[q];
+    for (int q = 0; q < nlevels; ++q) A.sigma2[q] = level_sigma2[q];
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g((kp_cap + 255) / 256, n_frames);
+    stereo_reset_kernel<<<g, 256, 0, st>>>(A);
+    stereo_tri_kernel<<<g, 256, 0, st>>>(A);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
 
 omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
                                                 const float *cams, int only_stereo, int coarse, int check_ori,

@@ -155,6 +155,27 @@ class ORBmatcher:
             "omv_matcher_search_last_frame")
         return frames.n_matches
 
+    def StereoTriangulate(self, frames, cams, Rlr, tlr, level_sigma2, stream=None):
+        """The depth check of Frame::ComputeMultiFishEyeMatches (src/Frame.cc:1488-1512) on the pairs
+        StereoLapping left in frames.l2r: KannalaBrandt8::TriangulateMatches with mRlr / mtlr.  Fills
+        frames.depth (mvDepth of the left keypoints) and frames.p3d (mvStereo3Dpoints), clears failed
+        pairs and rebuilds frames.r2l."""
+        import torch
+        if not hasattr(frames, "depth"):
+            frames.depth = torch.full((frames.n_frames, frames.kp_cap), -1.0, dtype=torch.float32,
+                                      device=frames.l2r.device)
+            frames.p3d = torch.zeros((frames.n_frames, frames.kp_cap, 3), dtype=torch.float32, device=frames.l2r.device)
+        h = self._handle(frames)
+        c = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(-1, 8)[:2])
+        R = np.ascontiguousarray(np.asarray(Rlr, np.float32).reshape(9))
+        t = np.ascontiguousarray(np.asarray(tlr, np.float32).reshape(3))
+        sg = np.ascontiguousarray(np.asarray(level_sigma2, np.float32))
+        _lib.check(self._lib.omv_matcher_stereo_triangulate(
+            h, frames.n_frames, frames.n_cams, frames.kp_cap, _lib.ptr(frames.kps), _lib.ptr(frames.n_kp),
+            _lib.ptr(frames.mono), _lib.ptr(c), _lib.ptr(R), _lib.ptr(t), _lib.ptr(sg), len(sg), _lib.ptr(frames.l2r),
+            _lib.ptr(frames.r2l), _lib.ptr(frames.depth), _lib.ptr(frames.p3d), self._stream(stream)),
+            "omv_matcher_stereo_triangulate")
+
     def SearchForTriangulation(self, pairs, cams, bOnlyStereo=False, bCoarse=False, stream=None):
         """ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1131-1456) for a batch of multi-camera
         keyframe pairs.  pairs: list of dicts {kf1, kf2, T, match12}: kf* hold the omv_kf_view fields

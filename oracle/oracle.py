@@ -27,8 +27,17 @@ def lib():
     return _lib
 
 
+class _Ptr(ctypes.c_void_p):
+    """A c_void_p that keeps its array alive for the duration of the call it is passed to (a temporary
+    like `_p(x.copy())` would otherwise be freed before the C function reads it)."""
+
+
 def _p(a):
-    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+    if a is None:
+        return None
+    p = _Ptr(a.ctypes.data)
+    p._keep = a
+    return p
 
 
 def orb_tables(nfeatures=1200, scale=1.2, nlevels=8):
@@ -337,3 +346,18 @@ def jacobi_svd4_v(A):
     V = np.zeros((4, 4), np.float32)
     lib().oracle_jacobi_svd4_v(_p(A), _p(V))
     return V
+
+
+def stereo_triangulate(kpsL, nL, kpsR, nR, cams, Rlr, tlr, sigma2, l2r):
+    """Frame::ComputeMultiFishEyeMatches' depth check on Lowe candidates l2r [nL] (right index or -1):
+    returns (l2r, r2l [nR], depth [nL], p3d [nL][3])."""
+    l2r = np.ascontiguousarray(l2r[:nL], np.int32).copy()
+    r2l = np.full(max(nR, 1), -1, np.int32)
+    depth = np.zeros(max(nL, 1), np.float32)
+    p3d = np.zeros((max(nL, 1), 3), np.float32)
+    c = np.ascontiguousarray(cams, np.float32).reshape(-1, 8)
+    lib().oracle_stereo_triangulate(_p(np.ascontiguousarray(kpsL)), int(nL), _p(np.ascontiguousarray(kpsR)), int(nR),
+                                    _p(c[0].copy()), _p(c[1].copy()), _p(np.ascontiguousarray(Rlr, np.float32)),
+                                    _p(np.ascontiguousarray(tlr, np.float32)), _p(np.ascontiguousarray(sigma2, np.float32)),
+                                    _p(l2r), _p(r2l), _p(depth), _p(p3d))
+    return l2r, r2l[:nR], depth[:nL], p3d[:nL]

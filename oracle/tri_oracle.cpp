@@ -161,7 +161,7 @@ void jacobi_svd4_v(const float *A, float *V) {
 
 // KannalaBrandt8::TriangulateMatches (returns z1, or -1 .. -5)
 float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2, const float *R12,
-                          const float *t12, float sigmaLevel, float unc) {
+                          const float *t12, float sigmaLevel, float unc, float *p3D = nullptr) {
     float r1[3], r2[3], r21[3];
     kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
     kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
@@ -202,6 +202,7 @@ float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp
     kb8_project_f(cam2, x3D2, u2, v2);
     const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
     if ((ex2 * ex2 + ey2 * ey2) > 5.991 * unc) return -5;
+    if (p3D) p3D[0] = x3D[0], p3D[1] = x3D[1], p3D[2] = x3D[2];
     return z1;
 }
 
@@ -319,6 +320,52 @@ int oracle_search_for_triangulation(const omv_tri_pair *P, const float *cams, in
         }
     }
     return nmatches;
+}
+
+// Frame::ComputeMultiFishEyeMatches' depth check (src/Frame.cc:1488-1512) for one frame: l2r holds the
+// Lowe-filtered candidates (right index or -1) of the nL left keypoints; on return the kept pairs, r2l
+// (right block, the later left index wins), depth (-1 where none) and p3d [nL][3].
+void oracle_stereo_triangulate(const omv_kp *kpsL, int nL, const omv_kp *kpsR, int nR, const float *camL,
+                               const float *camR, const float *Rlr, const float *tlr, const float *sigma2,
+                               int32_t *l2r, int32_t *r2l, float *depth, float *p3d) {
+    for (int j = 0; j < nR; ++j) r2l[j] = -1;
+    for (int i = 0; i < nL; ++i) {
+        depth[i] = -1.0f;
+        const int r = l2r[i];
+        if (r < 0) continue;
+        float p[3];
+        const float d = triangulate_matches(camL, camR, kpsL[i], kpsR[r], Rlr, tlr, sigma2[kpsL[i].octave],
+                                            sigma2[kpsR[r].octave], p);
+        if (d > 0.0001f) {
+            r2l[r] = i;
+            depth[i] = d;
+            for (int q = 0; q < 3; ++q) p3d[3 * i + q] = p[q];
+        } else {
+            l2r[i] = -1;
+        }
+    }
+}
+
+// The triangulated point and its projection into camera 1 (parity hook): out x3D[3] uv1[2].
+void oracle_tri_point(const float *cam1, const float *cam2, const omv_kp *kp1, const omv_kp *kp2, const float *R12,
+                      const float *t12, float *out) {
+    float r1[3], r2[3], R21[9], t2[3], A[16], V[16];
+    kb8_unproject_f(cam1, kp1->x, kp1->y, r1);
+    kb8_unproject_f(cam2, kp2->x, kp2->y, r2);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R21[3 * i + j] = R12[3 * j + i];
+    for (int i = 0; i < 3; ++i) t2[i] = -R21[3 * i] * t12[0] + -R21[3 * i + 1] * t12[1] + -R21[3 * i + 2] * t12[2];
+    const float T1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float T2[12] = {R21[0], R21[1], R21[2], t2[0], R21[3], R21[4], R21[5], t2[1], R21[6], R21[7], R21[8], t2[2]};
+    for (int j = 0; j < 4; ++j) {
+        A[j] = r1[0] * T1[8 + j] - T1[j];
+        A[4 + j] = r1[1] * T1[8 + j] - T1[4 + j];
+        A[8 + j] = r2[0] * T2[8 + j] - T2[j];
+        A[12 + j] = r2[1] * T2[8 + j] - T2[4 + j];
+    }
+    jacobi_svd4_v(A, V);
+    for (int i = 0; i < 3; ++i) out[i] = V[4 * i + 3] / V[15];
+    kb8_project_f(cam1, out, out[3], out[4]);
 }
 
 // Parity hooks for the camera-model pieces.

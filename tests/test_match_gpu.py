@@ -70,6 +70,49 @@ def test_stereo_lapping_matches_oracle(frames, oracle):
         assert (el2r >= 0).sum() > 5
 
 
+def test_stereo_triangulate_matches_oracle(frames, oracle):
+    """ComputeMultiFishEyeMatches' TriangulateMatches depth check (Frame.cc:1488-1512) on the lapping knn
+    pairs: kept pairs, r2l, mvDepth and mvStereo3Dpoints bit-exact vs the oracle."""
+    from openmavis_amd import synth_ba
+    kps, desc, n_kp, mono = host(frames, oracle)
+    cams, Rbc, tbc = synth_ba.rig()
+    Rlr = (Rbc[0].T @ Rbc[1]).astype(np.float32)
+    tlr = (Rbc[0].T @ (tbc[1] - tbc[0])).astype(np.float32)
+    sigma2 = np.array([frames.geom.scale_factors[i] for i in range(8)], np.float32) ** 2
+    m = ORBmatcher(0.8)
+    m.StereoLapping(frames, 0.8)
+    cand = frames.l2r.cpu().numpy().copy()
+    m.StereoTriangulate(frames, cams[:2], Rlr, tlr, sigma2)
+    l2r, r2l = frames.l2r.cpu().numpy(), frames.r2l.cpu().numpy()
+    depth, p3d = frames.depth.cpu().numpy(), frames.p3d.cpu().numpy()
+    kept = 0
+    for f in range(frames.n_frames):
+        nL, nR = n_kp[f, 0], n_kp[f, 1]
+        el2r, er2l, ed, ep = oracle.stereo_triangulate(kps[f, 0], nL, kps[f, 1], nR, cams[:2], Rlr, tlr, sigma2,
+                                                       cand[f])
+        assert np.array_equal(l2r[f, :nL], el2r), f"frame {f} l2r"
+        assert np.array_equal(r2l[f, :nR], er2l), f"frame {f} r2l"
+        assert np.array_equal(depth[f, :nL].view(np.uint32), ed.view(np.uint32)), f"frame {f} depth"
+        ok = el2r >= 0
+        assert np.array_equal(p3d[f, :nL][ok].view(np.uint32), ep[ok].view(np.uint32)), f"frame {f} p3D"
+        kept += int(ok.sum())
+    assert (cand >= 0).sum() > 0
+    # the tool's own hook: TriangulateMatches pieces on one device thread agree with the oracle's
+    import ctypes
+    from openmavis_amd import _lib
+    f = int(np.argmax((l2r >= 0).sum(1)))
+    i = int(np.nonzero(l2r[f] >= 0)[0][0]) if (l2r[f] >= 0).any() else int(np.nonzero(cand[f] >= 0)[0][0])
+    r = int(cand[f, i])
+    out = np.zeros(31, np.float32)
+    _lib.check(_lib.load().omv_tri_debug(_lib.ptr(np.ascontiguousarray(cams[:2], np.float32)),
+                                         _lib.ptr(np.ascontiguousarray(kps[f, 0, i:i + 1])),
+                                         _lib.ptr(np.ascontiguousarray(kps[f, 1, r:r + 1])), _lib.ptr(Rlr), _lib.ptr(tlr),
+                                         _lib.ptr(np.eye(4, dtype=np.float32)), ctypes.c_float(sigma2[kps[f, 0, i]["octave"]]),
+                                         ctypes.c_float(sigma2[kps[f, 1, r]["octave"]]), _lib.ptr(out)), "omv_tri_debug")
+    assert np.array_equal(out[:3].view(np.uint32), oracle.kb8_unproject(cams[0], kps[f, 0, i]["x"], kps[f, 0, i]["y"]).view(np.uint32))
+    assert np.array_equal(out[6:22].reshape(4, 4), np.eye(4, dtype=np.float32))   # the SVD of I is I
+
+
 def _mps_for(frames, oracle, M, seed, torch):
     kps, desc, n_kp, _ = host(frames, oracle)
     per = [synth.make_map_points(kps[f], desc[f], n_kp[f], M, seed + f, W, H) for f in range(frames.n_frames)]
