@@ -103,42 +103,55 @@ __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_
 }
 
 // K1 --------------------------------------------------------------------------------------------
-// One workgroup per (output row, image) of level l: the two source rows of level l-1 (y.sx0, y.sx1)
-// are staged in LDS with dword loads, each thread computes 4 adjacent output pixels and stores them
-// as one dword (level pitches are 16-byte aligned).
-constexpr int kPyrRowDw = 1024;   // staged source row capacity in dwords (levels up to 4096 px wide)
+// One workgroup per (block of kPyrBlock output rows, image) of level l: the source rows of level l-1
+// the block reads (y.sx0 of its first row .. y.sx1 of its last, ~1.2 kPyrBlock + 2) are staged in LDS
+// once with dword loads, together with the level's x table; each thread then computes 4 adjacent
+// output pixels per step and stores them as one dword (level pitches are 16-byte aligned).
+constexpr int kPyrBlock = 16;
 
 __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const uint8_t *images, size_t img_stride,
                                                          size_t pitch0, uint8_t *pyr, const XTab *xt,
                                                          const XTab *yt, int n_images) {
-    __shared__ __attribute__((aligned(16))) uint32_t rows[2][kPyrRowDw];
+    extern __shared__ __attribute__((aligned(16))) uint32_t pyr_lds[];
     const LevelGeom &L = g.lv[l];
-    const int dy = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+    const int img = blockIdx.y, tid = threadIdx.x;
+    const int dy0 = blockIdx.x * kPyrBlock, dy1 = min(dy0 + kPyrBlock, L.h);
     int sp;
     const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, l - 1, &sp);
     const int sw = g.lv[l - 1].w;
-    uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
-    const XTab y = yt[L.ytab_off + dy];
-    const uint8_t *r0 = src + (size_t)y.sx0 * sp, *r1 = src + (size_t)y.sx1 * sp;
     const int ndw = (sw + 3) >> 2;
+    XTab *xs = reinterpret_cast<XTab *>(pyr_lds);            // [L.w]
+    uint32_t *rows = pyr_lds + ((3 * L.w + 3) & ~3);         // [nr][ndw]
+    const int sy0 = yt[L.ytab_off + dy0].sx0, sy1 = yt[L.ytab_off + dy1 - 1].sx1;
+    const int nr = sy1 - sy0 + 1;
+    for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
     const bool dwords = (sp & 3) == 0 && ((((uintptr_t)src) & 3) == 0) && ndw * 4 <= sp;
     if (dwords) {
-        const uint32_t *w0 = (const uint32_t *)r0, *w1 = (const uint32_t *)r1;
-        for (int i = tid; i < ndw; i += 256) rows[0][i] = w0[i], rows[1][i] = w1[i];
+        for (int q = tid; q < nr * ndw; q += 256) {
+            const int r = q / ndw, i = q - r * ndw;
+            rows[q] = reinterpret_cast<const uint32_t *>(src + (size_t)(sy0 + r) * sp)[i];
+        }
     } else {
-        uint8_t *b0 = (uint8_t *)rows[0], *b1 = (uint8_t *)rows[1];
-        for (int i = tid; i < sw; i += 256) b0[i] = r0[i], b1[i] = r1[i];
+        uint8_t *b = reinterpret_cast<uint8_t *>(rows);
+        for (int q = tid; q < nr * sw; q += 256) {
+            const int r = q / sw, i = q - r * sw;
+            b[(size_t)r * ndw * 4 + i] = src[(size_t)(sy0 + r) * sp + i];
+        }
     }
     __syncthreads();
-    const uint8_t *R0 = (const uint8_t *)rows[0], *R1 = (const uint8_t *)rows[1];
-    const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
-    for (int dx0 = tid * 4; dx0 < L.w; dx0 += 1024) {
+    const int nq = (L.w + 3) >> 2;
+    for (int q = tid; q < (dy1 - dy0) * nq; q += 256) {
+        const int r = q / nq, dx0 = (q - r * nq) * 4, dy = dy0 + r;
+        const XTab y = yt[L.ytab_off + dy];
+        const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx0 - sy0) * ndw);
+        const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx1 - sy0) * ndw);
+        const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
         uint32_t packed = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int dx = dx0 + j;
             if (dx < L.w) {
-                const XTab x = xt[L.xtab_off + dx];
+                const XTab x = xs[dx];
                 const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
                 const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
                 const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
@@ -146,6 +159,7 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
                 packed |= (uint32_t)min(v, 255) << (8 * j);
             }
         }
+        uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
         if (dx0 + 3 < L.w) {
             *reinterpret_cast<uint32_t *>(dst + dx0) = packed;
         } else {
@@ -232,8 +246,9 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         const uint32_t *g0 = (const uint32_t *)(row0 - o);
         const int sw = sp >> 2;
         uint32_t *l0 = (uint32_t *)smem;
+        const uint32_t mnd = (1u << 20) / (uint32_t)nd + 1u;   // i / nd, exact while i * nd < 2^20
         for (int i = lane; i < nd * rh; i += 64) {
-            const int r = i / nd, w = i - r * nd;
+            const int r = (int)(((uint32_t)i * mnd) >> 20), w = i - r * nd;
             l0[i] = g0[(size_t)r * sw + w];
         }
     } else {
@@ -255,23 +270,75 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     const int t = min(g.ini_th, g.min_th);
     const uint64_t lt = (1ull << lane) - 1ull;
     int ncand = 0;
-    for (int i0 = 0; i0 < ndet; i0 += 64) {
-        const int i = i0 + lane;
-        bool pass = false;
-        if (i < ndet) {
-            int r, q;
-            rowcol(i, r, q);
-            const uint8_t *p = pix + r * rs + q;
-            const int v = p[0];
-            const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
-            const bool a0 = d0 > t, a4 = d4 > t, a8 = d8 > t, a12 = d12 > t;
-            const bool b0 = d0 < -t, b4 = d4 < -t, b8 = d8 < -t, b12 = d12 < -t;
-            pass = (a0 && a4) || (a4 && a8) || (a8 && a12) || (a12 && a0) || (b0 && b4) || (b4 && b8) ||
-                   (b8 && b12) || (b12 && b0);
+    if (dwords && ndet > 0) {
+        // 4 pixels per lane: the quad of LDS dword j (bytes 4j..4j+3 = columns 4j+k-o of its row) with its
+        // compass neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent
+        // dwords), the tests on packed int16 pairs: d > t  <=>  sign(d - (t+1)) = 0, d < -t  <=>  sign(d + t).
+        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
+        const int jq0 = (o + 3) >> 2, jq1 = (o + rw - 4) >> 2, nqr = jq1 - jq0 + 1, rsw = rs >> 2;
+        const int nq = nqr * dh;
+        const uint32_t mq = (1u << 20) / (uint32_t)nqr + 1u;   // t / nqr, exact while t * nqr < 2^20
+        const pk16 T1{(short)(t + 1), (short)(t + 1)}, T0{(short)t, (short)t};
+        auto lo = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c010c00u)); };
+        auto hi = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c030c02u)); };
+        auto test = [&](pk16 v, pk16 n0, pk16 n4, pk16 n8, pk16 n12) {   // bits 15 / 31: the pair passes
+            const pk16 d0 = v - n0, d4 = v - n4, d8 = v - n8, d12 = v - n12;
+            const uint32_t a0 = ~__builtin_bit_cast(uint32_t, pk16(d0 - T1)), a4 = ~__builtin_bit_cast(uint32_t, pk16(d4 - T1));
+            const uint32_t a8 = ~__builtin_bit_cast(uint32_t, pk16(d8 - T1)), a12 = ~__builtin_bit_cast(uint32_t, pk16(d12 - T1));
+            const uint32_t b0 = __builtin_bit_cast(uint32_t, pk16(d0 + T0)), b4 = __builtin_bit_cast(uint32_t, pk16(d4 + T0));
+            const uint32_t b8 = __builtin_bit_cast(uint32_t, pk16(d8 + T0)), b12 = __builtin_bit_cast(uint32_t, pk16(d12 + T0));
+            return ((a0 & a4) | (a4 & a8) | (a8 & a12) | (a12 & a0) | (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0)) &
+                   0x80008000u;
+        };
+        for (int t0 = 0; t0 < nq; t0 += 64) {
+            const int tq = t0 + lane;
+            uint32_t bits = 0;
+            int r = 0, jq = 0;
+            if (tq < nq) {
+                const int rr = (int)(((uint32_t)tq * mq) >> 20);
+                r = 3 + rr, jq = jq0 + tq - rr * nqr;
+                const int j = r * rsw + jq;
+                const uint32_t C = w32[j], Dn = w32[j + 3 * rsw], Up = w32[j - 3 * rsw];
+                const uint32_t Lf = __builtin_amdgcn_alignbyte(C, w32[j - 1], 1);
+                const uint32_t Rt = __builtin_amdgcn_alignbyte(w32[j + 1], C, 3);
+                const uint32_t pl = test(lo(C), lo(Dn), lo(Rt), lo(Up), lo(Lf));
+                const uint32_t ph = test(hi(C), hi(Dn), hi(Rt), hi(Up), hi(Lf));
+                bits = ((pl >> 15) & 1u) | ((pl >> 30) & 2u) | ((ph >> 13) & 4u) | ((ph >> 28) & 8u);
+                // columns of the quad outside the detection window [3, rw - 4]
+                const int q0 = 4 * jq - o;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (q0 + k < 3 || q0 + k > rw - 4) bits &= ~(1u << k);
+            }
+            // row-major order: lanes hold consecutive quads, bit k = column q0 + k
+            const uint64_t m0 = __ballot(bits & 1u), m1 = __ballot(bits & 2u), m2 = __ballot(bits & 4u),
+                           m3 = __ballot(bits & 8u);
+            int pos = ncand + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+            const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (bits & (1u << k)) cand[pos++] = (uint16_t)(ibase + k);
+            ncand += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
         }
-        const uint64_t m = __ballot(pass);
-        if (pass) cand[ncand + __popcll(m & lt)] = (uint16_t)i;
-        ncand += __popcll(m);
+    } else {
+        for (int i0 = 0; i0 < ndet; i0 += 64) {
+            const int i = i0 + lane;
+            bool pass = false;
+            if (i < ndet) {
+                int r, q;
+                rowcol(i, r, q);
+                const uint8_t *p = pix + r * rs + q;
+                const int v = p[0];
+                const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
+                const bool a0 = d0 > t, a4 = d4 > t, a8 = d8 > t, a12 = d12 > t;
+                const bool b0 = d0 < -t, b4 = d4 < -t, b8 = d8 < -t, b12 = d12 < -t;
+                pass = (a0 && a4) || (a4 && a8) || (a8 && a12) || (a12 && a0) || (b0 && b4) || (b4 && b8) ||
+                       (b8 && b12) || (b12 && b0);
+            }
+            const uint64_t m = __ballot(pass);
+            if (pass) cand[ncand + __popcll(m & lt)] = (uint16_t)i;
+            ncand += __popcll(m);
+        }
     }
     __syncthreads();
     for (int k = lane; k < ncand; k += 64) {
@@ -882,6 +949,7 @@ struct omv_orb {
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
     int rmax = 0;
     size_t oct_lds = 0;
+    size_t pyr_lds[kMaxLevels] = {};   // K1 dynamic LDS per level: x table + the widest row block
     // host staging for the synchronous path
     uint8_t *d_img1 = nullptr;
     omv_kp *d_kp1 = nullptr;
@@ -1082,6 +1150,22 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     const size_t n = (size_t)max_images;
     HIP_OK(hipMalloc(&o->d_cells, sizeof(Cell) * cells.size()));
     HIP_OK(hipMemcpy(o->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice));
+    for (int l = 1; l < g.nlevels; ++l) {   // K1 LDS: the level's x table + the most source rows a row block reads
+        const LevelGeom &L = g.lv[l];
+        int nr = 0;
+        for (int dy0 = 0; dy0 < L.h; dy0 += kPyrBlock) {
+            const int dy1 = std::min(dy0 + kPyrBlock, L.h);
+            nr = std::max(nr, yt[L.ytab_off + dy1 - 1].sx1 - yt[L.ytab_off + dy0].sx0 + 1);
+        }
+        o->pyr_lds[l] = sizeof(uint32_t) * (((3 * (size_t)L.w + 3) & ~(size_t)3) + (size_t)nr * ((g.lv[l - 1].w + 3) / 4));
+        if (o->pyr_lds[l] > 160 * 1024) {   // images wider than ~8000 px
+            delete o;
+            return OMV_ERR_ARG;
+        }
+        if (o->pyr_lds[l] > 64 * 1024)
+            (void)hipFuncSetAttribute((const void *)pyr_resize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)o->pyr_lds[l]);
+    }
     HIP_OK(hipMalloc(&o->d_xt, sizeof(XTab) * std::max<size_t>(1, xt.size())));
     HIP_OK(hipMalloc(&o->d_yt, sizeof(XTab) * std::max<size_t>(1, yt.size())));
     if (!xt.empty()) HIP_OK(hipMemcpy(o->d_xt, xt.data(), sizeof(XTab) * xt.size(), hipMemcpyHostToDevice));
@@ -1140,8 +1224,8 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K1: pyramid, level by level
     for (int l = 1; l < g.nlevels; ++l) {
-        pyr_resize_kernel<<<dim3(g.lv[l].h, n), 256, 0, st>>>(g, l, images, image_stride, pitch, o->d_pyr, o->d_xt,
-                                                               o->d_yt, n);
+        pyr_resize_kernel<<<dim3((g.lv[l].h + kPyrBlock - 1) / kPyrBlock, n), 256, o->pyr_lds[l], st>>>(
+            g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, n);
     }
     mark(o, st);
     // K2: FAST per cell
