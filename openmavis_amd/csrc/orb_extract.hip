@@ -267,148 +267,145 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         const int rr = (int)(((uint32_t)i * mdw) >> 20);
         r = 3 + rr, q = 3 + i - rr * dw;
     };
-    const int t = min(g.ini_th, g.min_th);
     const uint64_t lt = (1ull << lane) - 1ull;
-    int ncand = 0;
-    if (dwords && ndet > 0) {
-        // 4 pixels per lane: the quad of LDS dword j (bytes 4j..4j+3 = columns 4j+k-o of its row) with its
-        // compass neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent
-        // dwords), the tests on packed int16 pairs: d > t  <=>  sign(d - (t+1)) = 0, d < -t  <=>  sign(d + t).
-        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
-        const int jq0 = (o + 3) >> 2, jq1 = (o + rw - 4) >> 2, nqr = jq1 - jq0 + 1, rsw = rs >> 2;
-        const int nq = nqr * dh;
-        const uint32_t mq = (1u << 20) / (uint32_t)nqr + 1u;   // t / nqr, exact while t * nqr < 2^20
-        const pk16 T1{(short)(t + 1), (short)(t + 1)}, T0{(short)t, (short)t};
-        auto lo = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c010c00u)); };
-        auto hi = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c030c02u)); };
-        auto test = [&](pk16 v, pk16 n0, pk16 n4, pk16 n8, pk16 n12) {   // bits 15 / 31: the pair passes
-            const pk16 d0 = v - n0, d4 = v - n4, d8 = v - n8, d12 = v - n12;
-            const uint32_t a0 = ~__builtin_bit_cast(uint32_t, pk16(d0 - T1)), a4 = ~__builtin_bit_cast(uint32_t, pk16(d4 - T1));
-            const uint32_t a8 = ~__builtin_bit_cast(uint32_t, pk16(d8 - T1)), a12 = ~__builtin_bit_cast(uint32_t, pk16(d12 - T1));
-            const uint32_t b0 = __builtin_bit_cast(uint32_t, pk16(d0 + T0)), b4 = __builtin_bit_cast(uint32_t, pk16(d4 + T0));
-            const uint32_t b8 = __builtin_bit_cast(uint32_t, pk16(d8 + T0)), b12 = __builtin_bit_cast(uint32_t, pk16(d12 + T0));
-            return ((a0 & a4) | (a4 & a8) | (a8 & a12) | (a12 & a0) | (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0)) &
-                   0x80008000u;
-        };
-        for (int t0 = 0; t0 < nq; t0 += 64) {
-            const int tq = t0 + lane;
-            uint32_t bits = 0;
-            int r = 0, jq = 0;
-            if (tq < nq) {
-                const int rr = (int)(((uint32_t)tq * mq) >> 20);
-                r = 3 + rr, jq = jq0 + tq - rr * nqr;
-                const int j = r * rsw + jq;
-                const uint32_t C = w32[j], Dn = w32[j + 3 * rsw], Up = w32[j - 3 * rsw];
-                const uint32_t Lf = __builtin_amdgcn_alignbyte(C, w32[j - 1], 1);
-                const uint32_t Rt = __builtin_amdgcn_alignbyte(w32[j + 1], C, 3);
-                const uint32_t pl = test(lo(C), lo(Dn), lo(Rt), lo(Up), lo(Lf));
-                const uint32_t ph = test(hi(C), hi(Dn), hi(Rt), hi(Up), hi(Lf));
-                bits = ((pl >> 15) & 1u) | ((pl >> 30) & 2u) | ((ph >> 13) & 4u) | ((ph >> 28) & 8u);
-                // columns of the quad outside the detection window [3, rw - 4]
-                const int q0 = 4 * jq - o;
+    // compass prefilter at threshold t: the row-major candidate list cand[0..n) (returns n)
+    auto prefilter = [&](int t) {
+        int ncand = 0;
+        if (dwords && ndet > 0) {
+            // 4 pixels per lane: the quad of LDS dword j (bytes 4j..4j+3 = columns 4j+k-o of its row) with its
+            // compass neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent
+            // dwords), the tests on packed int16 pairs: d > t <=> sign(d - (t+1)) = 0, d < -t <=> sign(d + t).
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
+            const int jq0 = (o + 3) >> 2, jq1 = (o + rw - 4) >> 2, nqr = jq1 - jq0 + 1, rsw = rs >> 2;
+            const int nq = nqr * dh;
+            const uint32_t mq = (1u << 20) / (uint32_t)nqr + 1u;   // tq / nqr, exact while tq * nqr < 2^20
+            const pk16 T1{(short)(t + 1), (short)(t + 1)}, T0{(short)t, (short)t};
+            auto lo = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c010c00u)); };
+            auto hi = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c030c02u)); };
+            auto test = [&](pk16 v, pk16 n0, pk16 n4, pk16 n8, pk16 n12) {   // bits 15 / 31: the pair passes
+                const pk16 d0 = v - n0, d4 = v - n4, d8 = v - n8, d12 = v - n12;
+                const uint32_t a0 = ~__builtin_bit_cast(uint32_t, pk16(d0 - T1)),
+                               a4 = ~__builtin_bit_cast(uint32_t, pk16(d4 - T1));
+                const uint32_t a8 = ~__builtin_bit_cast(uint32_t, pk16(d8 - T1)),
+                               a12 = ~__builtin_bit_cast(uint32_t, pk16(d12 - T1));
+                const uint32_t b0 = __builtin_bit_cast(uint32_t, pk16(d0 + T0)), b4 = __builtin_bit_cast(uint32_t, pk16(d4 + T0));
+                const uint32_t b8 = __builtin_bit_cast(uint32_t, pk16(d8 + T0)),
+                               b12 = __builtin_bit_cast(uint32_t, pk16(d12 + T0));
+                return ((a0 & a4) | (a4 & a8) | (a8 & a12) | (a12 & a0) | (b0 & b4) | (b4 & b8) | (b8 & b12) |
+                        (b12 & b0)) &
+                       0x80008000u;
+            };
+            for (int t0 = 0; t0 < nq; t0 += 64) {
+                const int tq = t0 + lane;
+                uint32_t bits = 0;
+                int r = 0, jq = 0;
+                if (tq < nq) {
+                    const int rr = (int)(((uint32_t)tq * mq) >> 20);
+                    r = 3 + rr, jq = jq0 + tq - rr * nqr;
+                    const int j = r * rsw + jq;
+                    const uint32_t C = w32[j], Dn = w32[j + 3 * rsw], Up = w32[j - 3 * rsw];
+                    const uint32_t Lf = __builtin_amdgcn_alignbyte(C, w32[j - 1], 1);
+                    const uint32_t Rt = __builtin_amdgcn_alignbyte(w32[j + 1], C, 3);
+                    const uint32_t pl = test(lo(C), lo(Dn), lo(Rt), lo(Up), lo(Lf));
+                    const uint32_t ph = test(hi(C), hi(Dn), hi(Rt), hi(Up), hi(Lf));
+                    bits = ((pl >> 15) & 1u) | ((pl >> 30) & 2u) | ((ph >> 13) & 4u) | ((ph >> 28) & 8u);
+                    const int q0 = 4 * jq - o;   // columns of the quad outside [3, rw - 4]
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (q0 + k < 3 || q0 + k > rw - 4) bits &= ~(1u << k);
+                }
+                // row-major order: lanes hold consecutive quads, bit k = column q0 + k
+                const uint64_t m0 = __ballot(bits & 1u), m1 = __ballot(bits & 2u), m2 = __ballot(bits & 4u),
+                               m3 = __ballot(bits & 8u);
+                int pos = ncand + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+                const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (q0 + k < 3 || q0 + k > rw - 4) bits &= ~(1u << k);
+                    if (bits & (1u << k)) cand[pos++] = (uint16_t)(ibase + k);
+                ncand += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
             }
-            // row-major order: lanes hold consecutive quads, bit k = column q0 + k
-            const uint64_t m0 = __ballot(bits & 1u), m1 = __ballot(bits & 2u), m2 = __ballot(bits & 4u),
-                           m3 = __ballot(bits & 8u);
-            int pos = ncand + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-            const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (bits & (1u << k)) cand[pos++] = (uint16_t)(ibase + k);
-            ncand += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
-        }
-    } else {
-        for (int i0 = 0; i0 < ndet; i0 += 64) {
-            const int i = i0 + lane;
-            bool pass = false;
-            if (i < ndet) {
-                int r, q;
-                rowcol(i, r, q);
-                const uint8_t *p = pix + r * rs + q;
-                const int v = p[0];
-                const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
-                const bool a0 = d0 > t, a4 = d4 > t, a8 = d8 > t, a12 = d12 > t;
-                const bool b0 = d0 < -t, b4 = d4 < -t, b8 = d8 < -t, b12 = d12 < -t;
-                pass = (a0 && a4) || (a4 && a8) || (a8 && a12) || (a12 && a0) || (b0 && b4) || (b4 && b8) ||
-                       (b8 && b12) || (b12 && b0);
+        } else {
+            for (int i0 = 0; i0 < ndet; i0 += 64) {
+                const int i = i0 + lane;
+                bool pass = false;
+                if (i < ndet) {
+                    int r, q;
+                    rowcol(i, r, q);
+                    const uint8_t *p = pix + r * rs + q;
+                    const int v = p[0];
+                    const int d0 = v - p[3 * rs], d4 = v - p[3], d8 = v - p[-3 * rs], d12 = v - p[-3];
+                    const bool a0 = d0 > t, a4 = d4 > t, a8 = d8 > t, a12 = d12 > t;
+                    const bool b0 = d0 < -t, b4 = d4 < -t, b8 = d8 < -t, b12 = d12 < -t;
+                    pass = (a0 && a4) || (a4 && a8) || (a8 && a12) || (a12 && a0) || (b0 && b4) || (b4 && b8) ||
+                           (b8 && b12) || (b12 && b0);
+                }
+                const uint64_t m = __ballot(pass);
+                if (pass) cand[ncand + __popcll(m & lt)] = (uint16_t)i;
+                ncand += __popcll(m);
             }
-            const uint64_t m = __ballot(pass);
-            if (pass) cand[ncand + __popcll(m & lt)] = (uint16_t)i;
-            ncand += __popcll(m);
         }
-    }
-    __syncthreads();
-    for (int k = lane; k < ncand; k += 64) {
-        const int i = cand[k];
-        int r, q;
-        rowcol(i, r, q);
-        const int sv = fast_strength(pix + r * rs + q, rs);
-        S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
-    }
-    __syncthreads();
-    int tot_ini = 0, tot_min = 0;
-    for (int k0 = 0; k0 < ncand; k0 += 64) {
-        const int k = k0 + lane;
-        bool ki = false, km = false;
-        if (k < ncand) {
+        __syncthreads();
+        // FAST strength of the candidates (threshold-free; non-candidates keep S = 0)
+        for (int k = lane; k < ncand; k += 64) {
             const int i = cand[k];
             int r, q;
             rowcol(i, r, q);
-            const uint8_t *sp8 = S + r * rs + q;
-            const int v = sp8[0];
-            const int sc = v - 1;
-            ki = v > g.ini_th;
-            km = v > g.min_th;
-#pragma unroll
-            for (int n = 0; n < 9; ++n) {
-                if (n == 4) continue;
-                const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
-                ki = ki && (sc > (nv > g.ini_th ? nv - 1 : 0));
-                km = km && (sc > (nv > g.min_th ? nv - 1 : 0));
-            }
+            const int sv = fast_strength(pix + r * rs + q, rs);
+            S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
         }
-        tot_ini += __popcll(__ballot(ki));
-        tot_min += __popcll(__ballot(km));
+        __syncthreads();
+        return ncand;
+    };
+    // NMS at threshold th over the candidates: keypoint k survives iff S > th and S - 1 > every neighbour's
+    // cornerScore (S - 1 if S > th, else 0).  Returns the count; with `out`, emits row-major.
+    auto nms = [&](int ncand, int th, uint32_t *out) {
+        int base = 0;
+        for (int k0 = 0; k0 < ncand; k0 += 64) {
+            const int k = k0 + lane;
+            bool keep = false;
+            uint32_t packed = 0;
+            if (k < ncand) {
+                const int i = cand[k];
+                int r, q;
+                rowcol(i, r, q);
+                const uint8_t *sp8 = S + r * rs + q;
+                const int v = sp8[0];
+                if (v > th) {
+                    keep = true;
+                    const int sc = v - 1;
+#pragma unroll
+                    for (int n = 0; n < 9; ++n) {
+                        if (n == 4) continue;
+                        const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
+                        keep = keep && (sc > (nv > th ? nv - 1 : 0));
+                    }
+                    const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
+                    packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)sc << 24);
+                }
+            }
+            const uint64_t m = __ballot(keep);
+            if (out && keep) out[base + __popcll(m & lt)] = packed;
+            base += __popcll(m);
+        }
+        return base;
+    };
+    // iniThFAST first; minThFAST only for a cell without an iniTh keypoint (ORBextractor.cc:745-782).  Every
+    // pixel with S > th passes the compass prefilter at th, so the iniTh pass only needs those candidates:
+    // the NMS treats non-candidates (S = 0) as the reference treats scores <= th.
+    int th = g.ini_th;
+    int ncand = prefilter(th);
+    int total = nms(ncand, th, nullptr);
+    if (total == 0) {
+        th = g.min_th;
+        ncand = prefilter(th);
+        total = nms(ncand, th, nullptr);
     }
-    const int th = tot_ini > 0 ? g.ini_th : g.min_th;
-    const int total = tot_ini > 0 ? tot_ini : tot_min;
     if (total > g.cell_cap) {   // cannot happen by construction (cap = max NMS survivors)
         if (lane == 0) cell_cnt[blockIdx.x] = -1;
         return;
     }
     // emit row-major; coordinates relative to the FAST border (minBorder = 16)
-    uint32_t *out = cell_kp + (size_t)blockIdx.x * g.cell_cap;
-    int base = 0;
-    for (int k0 = 0; k0 < ncand; k0 += 64) {
-        const int k = k0 + lane;
-        bool keep = false;
-        uint32_t packed = 0;
-        if (k < ncand) {
-            const int i = cand[k];
-            int r, q;
-            rowcol(i, r, q);
-            const uint8_t *sp8 = S + r * rs + q;
-            const int v = sp8[0];
-            if (v > th) {
-                keep = true;
-                const int sc = v - 1;
-#pragma unroll
-                for (int n = 0; n < 9; ++n) {
-                    if (n == 4) continue;
-                    const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
-                    keep = keep && (sc > (nv > th ? nv - 1 : 0));
-                }
-                const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
-                packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)sc << 24);
-            }
-        }
-        const uint64_t m = __ballot(keep);
-        if (keep) out[base + __popcll(m & lt)] = packed;
-        base += __popcll(m);
-    }
+    nms(ncand, th, cell_kp + (size_t)blockIdx.x * g.cell_cap);
     if (lane == 0) cell_cnt[blockIdx.x] = total;
 }
 
