@@ -531,11 +531,15 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
         return;
     }
-    for (int i = 0; i < ncell; ++i) {
-        const int b = cellscan[i];
-        const int n = (i + 1 < ncell ? cellscan[i + 1] : K) - b;
-        const uint32_t *src = a.cell_kp + ((size_t)img * g.n_cells + L.cell_begin + i) * g.cell_cap;
-        for (int k = tid; k < n; k += T) cand[b + k] = src[k];
+    // one thread per key: its cell is the last one whose start <= k (empty cells share the next start)
+    for (int k = tid; k < K; k += T) {
+        int lo = 0, hi = ncell - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cellscan[mid] <= k) lo = mid;
+            else hi = mid - 1;
+        }
+        cand[k] = a.cell_kp[((size_t)img * g.n_cells + L.cell_begin + lo) * g.cell_cap + (k - cellscan[lo])];
     }
     __syncthreads();
 
