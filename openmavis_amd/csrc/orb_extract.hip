@@ -42,6 +42,7 @@ constexpr int kPatchW = 2 * kPatchR + 1;   // 43
 constexpr int kWinR = 18;
 constexpr int kWinW = 2 * kWinR + 1;       // 37
 constexpr int kPatchS = 48;                 // LDS row stride of the staged patch: 12 dwords cover 43 + 3
+constexpr int kHsS = 40;                    // LDS row stride of the horizontal blur sums (10 quads of columns)
 
 __constant__ int c_pattern[256 * 4] = {
 #define OMV_PATTERN_TABLE_BEGIN
@@ -786,7 +787,7 @@ struct DescArgs {
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
-    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kWinW];
+    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kHsS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + wave;
     int img = slot / g.out_per_img;
@@ -844,16 +845,26 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         }
     }
     __syncthreads();
-    // intensity centroid over the r = 15 disc (umax rows), exact integer sums
+    // intensity centroid over the r = 15 disc (umax rows), exact integer sums: per (row v, dword k of the
+    // row's columns u = 4k + b - 15) one v_dot4 of the pixels with the in-disc mask (row sum, for m01) and
+    // one with the weights u + 15 (m10 = sum (u + 15) I - 15 sum I)
+    const int pofs = (int)(P - patch[wave]);
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch[wave]);
     int m01 = 0, m10 = 0;
-    for (int i = lane; i < 31 * 31; i += 64) {
-        const int v = i / 31 - 15, u = i % 31 - 15;
-        const int av = v < 0 ? -v : v;
-        if ((u < 0 ? -u : u) <= c_umax[av]) {
-            const int I = P[(kPatchR + v) * kPatchS + kPatchR + u];
-            m10 += u * I;
-            m01 += v * I;
+    for (int i = lane; i < 31 * 8; i += 64) {
+        const int vr = i >> 3, k = i & 7, v = vr - 15;
+        const int av = v < 0 ? -v : v, um = c_umax[av];
+        const int off = pofs + (kPatchR + v) * kPatchS + 6 + 4 * k, dwi = off >> 2, sh = off & 3;
+        const uint32_t w = __builtin_amdgcn_alignbyte(pw[dwi + 1], pw[dwi], sh);
+        uint32_t msk = 0, wu = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int u = 4 * k + b - 15;
+            if (u <= 15 && (u < 0 ? -u : u) <= um) msk |= 1u << (8 * b), wu |= (uint32_t)(u + 15) << (8 * b);
         }
+        const int rs = (int)__builtin_amdgcn_udot4(w, msk, 0u, false);
+        m10 += (int)__builtin_amdgcn_udot4(w, wu, 0u, false) - 15 * rs;
+        m01 += v * rs;
     }
     for (int d = 32; d >= 1; d >>= 1) {
         m01 += __shfl_xor(m01, d, 64);
@@ -865,22 +876,29 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
     // vertical ((sum + 2^15) >> 16) evaluated only at the 512 steered sample points.
     uint16_t *Hs = hsum[wave];
     {
-        const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch[wave]);
-        const int pofs = (int)(P - patch[wave]);
+        // 4 adjacent window columns per lane from 4 dwords (one shared alignment sh = pofs & 3)
         constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-        for (int i = lane; i < kPatchW * kWinW; i += 64) {
-            const int r = i / kWinW, q = i - r * kWinW;
-            const int off = pofs + r * kPatchS + q, dw = off >> 2, sh = off & 3;
-            const uint32_t d0 = pw[dw], d1 = pw[dw + 1], d2 = pw[dw + 2];
-            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            Hs[i] = (uint16_t)__builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
+        const int sh = pofs & 3;
+        for (int i = lane; i < kPatchW * (kHsS / 4); i += 64) {
+            const int r = i / (kHsS / 4), jq = i - r * (kHsS / 4);
+            const int dw0 = (pofs + r * kPatchS) / 4 + jq;   // kPatchS and 4 jq are dword multiples
+            const uint32_t D[4] = {pw[dw0], pw[dw0 + 1], pw[dw0 + 2], pw[dw0 + 3]};
+            uint32_t h[4];
+#pragma unroll
+            for (int sc = 0; sc < 4; ++sc) {
+                const int b = sh + sc, j = b >> 2, a = b & 3;
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(D[j + 1], D[j], a);
+                const uint32_t w1 = __builtin_amdgcn_alignbyte(D[j + 2 < 4 ? j + 2 : 3], D[j + 1], a);
+                h[sc] = __builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
+            }
+            *reinterpret_cast<uint2 *>(Hs + r * kHsS + 4 * jq) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
         }
     }
     __syncthreads();
     auto blurred = [&](int r, int q) {   // window coordinates (0..36)
         uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * Hs[(r + k) * kWinW + q];
+        for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * Hs[(r + k) * kHsS + q];
         return (int)min((acc + 32768u) >> 16, 255u);
     };
     // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
