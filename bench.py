@@ -294,8 +294,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=256, help="multi-cam frames per step per GPU")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--frames", type=int, default=384, help="multi-cam frames per step per GPU")
+    ap.add_argument("--streams", type=int, default=3,
                     help="frame groups per GPU, each on its own HIP stream (latency-bound matcher stages of one "
                          "group overlap extraction of another)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -485,9 +485,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_step_bytes[dom] // launches}
         pmc = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch's images
             try:
-                roof["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                rec = json.load(open(pmc))
+                if "hbm_bytes_per_image" in rec and dom in ("pyr_resize", "fast_cells", "octree", "describe"):
+                    roof["traffic"] = rec["hbm_bytes_per_image"] * Bg * C
+                    roof["traffic_source"] = f"profiles/pmc_{dom}.json ({rec['tag']}), per image x {Bg * C} images"
             except Exception:
                 pass
     cpu = None

@@ -27,14 +27,14 @@ def short(name):
     return name
 
 
-def main(src, tag):
+def main(src, tag, images_per_launch=None, command=None):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
-             "Command: `rocprofv3 --kernel-trace --stats -T -- python3 bench.py --no-cpu-baseline "
-             "--steps 5 --warmup 1 --frames 64` (MI355X, one GPU).", "",
+             "Command: `" + (command or "rocprofv3 --kernel-trace --stats -T -- python3 bench.py --no-cpu-baseline "
+                             "--steps 5 --warmup 1 --frames 64") + "` (MI355X, one GPU).", "",
              "| kernel | calls | total ms | avg us | min us | max us | share |", "|---|---|---|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
@@ -56,12 +56,16 @@ def main(src, tag):
         b = (2 * f + w) * 1024
         lines.append(f"| {k} | {len(d['FETCH_SIZE'])} | {f:.1f} | {w:.1f} | {b:.0f} |")
         if k in SHORT.values():
-            json.dump({"kernel": k, "tag": tag, "fetch_kb_per_launch": f, "write_kb_per_launch": w,
-                       "hbm_bytes_per_launch": round(b), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024"},
-                      open(os.path.join(prof, f"pmc_{k}.json"), "w"), indent=1)
+            rec = {"kernel": k, "tag": tag, "fetch_kb_per_launch": f, "write_kb_per_launch": w,
+                   "hbm_bytes_per_launch": round(b), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024"}
+            if images_per_launch:   # extraction kernels: one launch covers images_per_launch images
+                rec["images_per_launch"] = images_per_launch
+                rec["hbm_bytes_per_image"] = round(b / images_per_launch)
+            json.dump(rec, open(os.path.join(prof, f"pmc_{k}.json"), "w"), indent=1)
     open(os.path.join(prof, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01",
+         int(sys.argv[3]) if len(sys.argv) > 3 else None, sys.argv[4] if len(sys.argv) > 4 else None)
