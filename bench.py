@@ -260,6 +260,8 @@ def tri_leg(pairs, n_pairs, reps, dev):
             q[k] = d
         q["match12"] = torch.empty(p["kf1"]["n"], dtype=torch.int32, device=dev)
         dp.append(q)
+    from openmavis_amd.matcher import TriPairBatch
+    dp = TriPairBatch(dp)   # keyframes resident: the omv_tri_pair array is built once
     m = ORBmatcher(0.6, False)   # LocalMapping::CreateNewMapPoints: ORBmatcher(0.6, false)
     cams = pairs[0]["cams"]
     for _ in range(2):

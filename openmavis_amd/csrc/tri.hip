@@ -3,17 +3,23 @@
 // (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429) and Eigen's
 // JacobiSVD<Matrix4f> restated in float.
 //
-// One wavefront per keyframe pair (pairs are independent: vbMatched2 is never set, :1204, :1261).  The
-// scan is the reference's: shared FeatureVector nodes in ascending id, for each keypoint idx1 of the
-// node (without a map point) the best candidate idx2 of the other keyframe's node by Hamming distance
-// (<= TH_LOW, later equal distances replace earlier ones) among those passing the epipolar test.  The
-// only sequential coupling is the camera-pair state (R12, t12, pCamera1, pCamera2) that persists from
-// one candidate to the next: pairs the reference lists assign it, the others reuse it.  So per node
-// chunk the wave first computes, in parallel, every (idx1, idx2) Hamming distance and — for listed
-// camera pairs, whose transform does not depend on the scan — the epipolar test; then lane 0 replays the
-// scan in order, running the epipolar test itself only for unlisted camera pairs (with the state the
-// replay has reached).  Float arithmetic without contraction; glibc's atan2f / tanf and correctly
-// rounded sqrtf are restated (omv_device.h), so the result is bit-exact to oracle/tri_oracle.cpp.
+// One 256-thread workgroup per keyframe pair (pairs are independent: vbMatched2 is never set, :1204,
+// :1261).  The scan is the reference's: shared FeatureVector nodes in ascending id, for each keypoint idx1
+// of the node (without a map point) the best candidate idx2 of the other keyframe's node by Hamming
+// distance (<= TH_LOW, later equal distances replace earlier ones) among those passing the epipolar test.
+// The only sequential coupling is the camera-pair state (R12, t12, pCamera1, pCamera2) that persists from
+// one candidate to the next: camera pairs the reference lists assign it, the others reuse it.
+//   1. The node intersection (each thread binary-searches one node of keyframe 1) and the candidate
+//      space of all (node, idx1, idx2) in scan order are laid out in LDS.
+//   2. All threads compute Hamming distances, 4 consecutive candidates each, and compact the few that
+//      can matter (no map point on either side, distance <= TH_LOW) in scan order.
+//   3. Epipolar tests run as a flat work list over all threads: a listed camera pair is tested with
+//      its own transform; an unlisted one with every state it can possibly meet — the state entering
+//      the batch plus each listed pair compacted before it (an OR-scan) — so the result the replay needs
+//      is always among them.
+//   4. Thread 0 replays the scan over the compacted candidates, looking the results up.
+// Float arithmetic without contraction; glibc's atan2f / tanf and correctly rounded sqrtf are restated
+// (omv_device.h), so the result is bit-exact to oracle/tri_oracle.cpp.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -34,15 +40,13 @@ namespace {
 
 constexpr int kTriLow = 50;          // ORBmatcher::TH_LOW
 constexpr int kHisto = 30;           // HISTO_LENGTH
-constexpr int kCand = 8192;          // (idx1, idx2) candidates staged per node chunk (1 byte each)
-constexpr int kTriMaxKp = 16384;     // keypoints of keyframe 1 (orientation bins, 1 byte each)
-constexpr uint8_t kInvalid = 0xff, kListed = 0x40, kOk = 0x80;
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+constexpr int kTriMaxKp = 16384;     // keypoints of keyframe 1 (orientation bins, 1 byte each; < 2^16)
+constexpr int kTriThreads = 512;
+constexpr int kTriWaves = kTriThreads / 64;
+constexpr int kSeg = kTriThreads;    // keyframe-1 nodes intersected per segment
+constexpr int kPerThread = 4;        // consecutive candidates per thread per tile
+constexpr int kTile = kTriThreads * kPerThread;
+constexpr int kVal = 4096;           // compacted candidates per replay batch
 
 // KannalaBrandt8::project(const Eigen::Vector3f&): cos / sin of the promoted float (C double functions)
 __device__ void kb8_project_f(const float *k, const float *X, float &u, float &v) {
@@ -243,111 +247,231 @@ __device__ bool epipolar_ok(const omv_tri_pair &P, const TriCams &C, int pr, con
                                P.kf1.level_sigma2[kp1.octave], P.kf2.level_sigma2[kp2.octave]) > 0.0001f;
 }
 
-__global__ void __launch_bounds__(64) tri_kernel(const omv_tri_pair *pairs, TriCams C, int only_stereo, int coarse,
-                                                 int check_ori, int32_t *n_matches, int *err) {
-    __shared__ uint8_t cand[kCand];
+// Exclusive block scan (kTriThreads threads, one value each) with associative `op`; `total` = op over all.
+template <typename T, typename Op>
+__device__ __forceinline__ T block_scan_excl(T v, T id, Op op, T *s_w, T &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc = op(o, inc);   // o covers the earlier lanes (op need not commute)
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    T pre = id;
+    for (int i = 0; i < w; ++i) pre = op(pre, s_w[i]);
+    total = pre;
+    for (int i = w; i < kTriWaves; ++i) total = op(total, s_w[i]);
+    T ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = id;
+    __syncthreads();
+    return op(pre, ex);
+}
+
+// compacted candidate code: distance bits 0-5, listed bit 6, camera pair bits 8-11
+constexpr uint16_t kCodeListed = 0x40;
+
+__global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pairs, TriCams C, int only_stereo,
+                                                          int coarse, int check_ori, int32_t *n_matches, int *err) {
     __shared__ uint8_t bins[kTriMaxKp];
+    __shared__ int seg_s1[kSeg], seg_n1[kSeg], seg_s2[kSeg], seg_n2[kSeg], seg_pref[kSeg + 1];
+    __shared__ uint32_t v_pk[kVal];      // idx1 << 16 | idx2
+    __shared__ uint16_t v_code[kVal], v_mask[kVal];
+    __shared__ uint32_t v_res[kVal];     // epipolar results, one bit per camera-pair state
+    __shared__ int v_item[kVal + 1];
+    __shared__ int s_wi[kTriWaves];
+    __shared__ unsigned s_wu[kTriWaves];
     __shared__ int hist[kHisto];
     __shared__ int s_keep[kHisto];
-    __shared__ int s_removed;
+    __shared__ int s_state, s_row, s_best;
     const omv_tri_pair &P = pairs[blockIdx.x];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < K1.n; i += 64) P.match12[i] = -1;
-    if (K1.n > kTriMaxKp) {
-        if (lane == 0) atomicExch(err, OMV_ERR_CAPACITY), n_matches[blockIdx.x] = 0;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < K1.n; i += kTriThreads) P.match12[i] = -1;
+    if (K1.n > kTriMaxKp || K2.n > 65535) {
+        if (tid == 0) atomicExch(err, OMV_ERR_CAPACITY), n_matches[blockIdx.x] = 0;
         return;
     }
-    for (int i = lane; i < K1.n; i += 64) bins[i] = 0xff;
-    if (lane < kHisto) hist[lane] = 0;
-    wave_sync();
-    int state = 0;   // the persistent camera-pair state; LL before any assignment
-    int nmatch = 0;
-    int a = 0, b = 0;
-    while (a < K1.n_nodes && b < K2.n_nodes) {   // FeatureVector intersection in ascending node id
-        const uint32_t ia = K1.node_id[a], ib = K2.node_id[b];
-        if (ia < ib) {
-            ++a;
-            continue;
+    for (int i = tid; i < K1.n; i += kTriThreads) bins[i] = 0xff;
+    if (tid < kHisto) hist[tid] = 0;
+    if (tid == 0) s_state = 0, s_row = -1, s_best = kTriLow;   // camera-pair state: LL before any assignment
+    __syncthreads();
+    auto add = [](int x, int y) { return x + y; };
+    // thread 0's replay state, carried across batches
+    int nmatch = 0, cur_row = -1, bestDist = kTriLow, bestIdx2 = -1;
+    auto finish_row = [&]() {
+        if (cur_row < 0 || bestIdx2 < 0) return;
+        P.match12[cur_row] = bestIdx2;
+        ++nmatch;
+        if (check_ori) {
+            float rot = K1.kps[cur_row].angle - K2.kps[bestIdx2].angle;
+            if ((double)rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / kHisto));
+            if (bin == kHisto) bin = 0;
+            bins[cur_row] = (uint8_t)bin;
         }
-        if (ib < ia) {
-            ++b;
-            continue;
+    };
+    int n_valid = 0;
+    // epipolar tests of the compacted batch (step 3) and the in-order replay (step 4)
+    auto flush = [&]() {
+        __syncthreads();   // the last tile's compacted entries
+        if (!coarse) {
+            // States entry k can meet: the last listed entry before it that is certain to pass the distance
+            // test (an anchor: its distance <= every earlier distance of its row, and <= the replay's
+            // bestDist when the row continues from the previous batch) fixes the state; listed entries
+            // after the anchor may change it.  Two segmented scans per tile: a min-scan of the distances
+            // (reset at row starts) finds the anchors, an OR-scan of the listed pairs (reset at anchors)
+            // gives the masks.  Bit 8 / bit 16 mark a segment start.
+            auto seg_min = [](unsigned x, unsigned y) {
+                return ((x | y) & 0x100u) | ((y & 0x100u) ? (y & 0xffu) : min(x & 0xffu, y & 0xffu));
+            };
+            auto seg_or = [](unsigned x, unsigned y) {
+                return ((x | y) & 0x10000u) | ((y & 0x10000u) ? (y & 0xffffu) : ((x | y) & 0xffffu));
+            };
+            unsigned cmin = (n_valid > 0 && (int)(v_pk[0] >> 16) == s_row) ? (unsigned)s_best : 0xffu;
+            unsigned cor = 1u << s_state;
+            int icarry = 0;
+            for (int t0 = 0; t0 < n_valid; t0 += kTriThreads) {
+                const int k = t0 + tid;
+                unsigned vmin = 0xffu, vor = 0;
+                bool listed = false;
+                int dist = 0, pr = 0;
+                if (k < n_valid) {
+                    const int code = v_code[k];
+                    listed = (code & kCodeListed) != 0;
+                    dist = code & 0x3f, pr = (code >> 8) & 15;
+                    const int row = (int)(v_pk[k] >> 16);
+                    const int prev = k > 0 ? (int)(v_pk[k - 1] >> 16) : s_row;
+                    vmin = (row != prev ? 0x100u : 0u) | (unsigned)dist;
+                }
+                unsigned tmin;
+                const unsigned bmin = seg_min(cmin, block_scan_excl(vmin, 0xffu, seg_min, s_wu, tmin));
+                const bool row_start = (vmin & 0x100u) != 0;
+                const bool anchor = listed && (row_start || (unsigned)dist <= (bmin & 0xffu));
+                if (listed) vor = (anchor ? 0x10000u : 0u) | (1u << pr);
+                unsigned tor;
+                const unsigned bor_ = seg_or(cor, block_scan_excl(vor, 0u, seg_or, s_wu, tor));
+                const unsigned m = listed ? (1u << pr) : (bor_ & 0x3ffu);
+                const int cnt = k < n_valid ? __popc(m) : 0;
+                int itot;
+                const int off = icarry + block_scan_excl(cnt, 0, add, s_wi, itot);
+                if (k < n_valid) v_mask[k] = (uint16_t)m, v_item[k] = off, v_res[k] = 0;
+                cmin = seg_min(cmin, tmin);
+                cor = seg_or(cor, tor);
+                icarry += itot;
+            }
+            if (tid == 0) v_item[n_valid] = icarry;
+            __syncthreads();
+            for (int j = tid; j < icarry; j += kTriThreads) {
+                int lo = 0, hi = n_valid;   // last k with v_item[k] <= j
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (v_item[mid] <= j) lo = mid;
+                    else hi = mid;
+                }
+                unsigned m = v_mask[lo];
+                for (int r = j - v_item[lo]; r > 0; --r) m &= m - 1;
+                const int state = __ffs(m) - 1;
+                const uint32_t pk = v_pk[lo];
+                if (epipolar_ok(P, C, state, K1.kps[pk >> 16], K2.kps[pk & 0xffff])) atomicOr(&v_res[lo], 1u << state);
+            }
+            __syncthreads();
         }
-        const int s1 = K1.node_start[a], n1 = K1.node_start[a + 1] - s1;
-        const int s2 = K2.node_start[b], n2 = K2.node_start[b + 1] - s2;
-        ++a, ++b;
-        if (n2 == 0 || n1 == 0) continue;
-        if (n2 > kCand) {
-            if (lane == 0) atomicExch(err, OMV_ERR_CAPACITY);
-            continue;
+        if (tid == 0) {
+            int state = s_state;
+            for (int k = 0; k < n_valid; ++k) {
+                const uint32_t pk = v_pk[k];
+                const int idx1 = (int)(pk >> 16);
+                if (idx1 != cur_row) {
+                    finish_row();
+                    cur_row = idx1, bestDist = kTriLow, bestIdx2 = -1;
+                }
+                const int code = v_code[k];
+                const int dist = code & 0x3f;
+                if (dist > bestDist) continue;
+                if (code & kCodeListed) state = (code >> 8) & 15;
+                const bool ok = coarse || ((v_res[k] >> state) & 1u);
+                if (ok) bestIdx2 = (int)(pk & 0xffff), bestDist = dist;
+            }
+            s_state = state, s_row = cur_row, s_best = bestDist;
         }
-        const int chunk = kCand / n2;
-        for (int c0 = 0; c0 < n1; c0 += chunk) {
-            const int cn = min(chunk, n1 - c0);
-            // phase A: distances + epipolar tests of listed camera pairs, one candidate per lane
-            for (int q = lane; q < cn * n2; q += 64) {
-                const int i1 = q / n2, i2 = q - i1 * n2;
-                const int idx1 = K1.node_idx[s1 + c0 + i1], idx2 = K2.node_idx[s2 + i2];
-                uint8_t code = kInvalid;
-                if (!K1.has_mp[idx1] && !only_stereo && !K2.has_mp[idx2]) {
-                    const int dist = omv::hamming256((const uint64_t *)(K1.desc + 32 * (size_t)idx1),
-                                                     (const uint64_t *)(K2.desc + 32 * (size_t)idx2));
-                    if (dist <= kTriLow) {
-                        code = (uint8_t)dist;
-                        const int pr = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
-                        if (pr >= 0) {
-                            code |= kListed;
-                            if (coarse || epipolar_ok(P, C, pr, K1.kps[idx1], K2.kps[idx2])) code |= kOk;
+        __syncthreads();
+        n_valid = 0;
+    };
+    for (int a0 = 0; a0 < K1.n_nodes && !only_stereo; a0 += kSeg) {
+        // step 1: this segment's node intersection, in ascending node id
+        int s1 = 0, n1 = 0, s2 = 0, n2 = 0;
+        const int a = a0 + tid;
+        if (a < K1.n_nodes) {
+            const uint32_t id = K1.node_id[a];
+            int lo = 0, hi = K2.n_nodes;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (K2.node_id[mid] < id) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < K2.n_nodes && K2.node_id[lo] == id) {
+                s1 = K1.node_start[a], n1 = K1.node_start[a + 1] - s1;
+                s2 = K2.node_start[lo], n2 = K2.node_start[lo + 1] - s2;
+            }
+        }
+        const int has = (n1 > 0 && n2 > 0) ? 1 : 0;
+        int n_seg;
+        const int pos = block_scan_excl(has, 0, add, s_wi, n_seg);
+        int q_seg;
+        const int qoff = block_scan_excl(has ? n1 * n2 : 0, 0, add, s_wi, q_seg);
+        if (has) seg_s1[pos] = s1, seg_n1[pos] = n1, seg_s2[pos] = s2, seg_n2[pos] = n2, seg_pref[pos] = qoff;
+        if (tid == 0) seg_pref[n_seg] = q_seg;
+        __syncthreads();
+        // step 2: distances and compaction, tile by tile
+        for (int t0 = 0; t0 < q_seg; t0 += kTile) {
+            if (n_valid + kTile > kVal) flush();
+            uint32_t pk[kPerThread];
+            uint16_t cd[kPerThread];
+            int cnt = 0;
+            const int qb = t0 + tid * kPerThread;
+            if (qb < q_seg) {
+                int lo = 0, hi = n_seg;   // last node with seg_pref <= qb
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (seg_pref[mid] <= qb) lo = mid;
+                    else hi = mid;
+                }
+                int nd = lo, loc = qb - seg_pref[lo];
+                int i1 = loc / seg_n2[nd], i2 = loc - i1 * seg_n2[nd];
+                for (int j = 0; j < kPerThread && qb + j < q_seg; ++j) {
+                    const int idx1 = K1.node_idx[seg_s1[nd] + i1], idx2 = K2.node_idx[seg_s2[nd] + i2];
+                    if (!K1.has_mp[idx1] && !K2.has_mp[idx2]) {
+                        const int dist = omv::hamming256((const uint64_t *)(K1.desc + 32 * (size_t)idx1),
+                                                         (const uint64_t *)(K2.desc + 32 * (size_t)idx2));
+                        if (dist <= kTriLow) {
+                            const int pr = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
+                            pk[cnt] = (uint32_t)idx1 << 16 | (uint32_t)idx2;
+                            cd[cnt] = (uint16_t)(dist | (pr >= 0 ? kCodeListed | (pr << 8) : 0));
+                            ++cnt;
                         }
+                    }
+                    if (++i2 == seg_n2[nd]) {
+                        i2 = 0;
+                        if (++i1 == seg_n1[nd]) i1 = 0, ++nd;
                     }
                 }
-                cand[q] = code;
             }
-            wave_sync();
-            // phase B: the reference's scan, in order
-            if (lane == 0) {
-                for (int i1 = 0; i1 < cn; ++i1) {
-                    const int idx1 = K1.node_idx[s1 + c0 + i1];
-                    if (K1.has_mp[idx1] || only_stereo) continue;
-                    int bestDist = kTriLow, bestIdx2 = -1;
-                    for (int i2 = 0; i2 < n2; ++i2) {
-                        const uint8_t code = cand[i1 * n2 + i2];
-                        if (code == kInvalid) continue;
-                        const int dist = code & 0x3f;
-                        if (dist > bestDist) continue;
-                        const int idx2 = K2.node_idx[s2 + i2];
-                        bool ok;
-                        if (code & kListed) {
-                            state = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
-                            ok = (code & kOk) != 0;
-                        } else {
-                            ok = coarse || epipolar_ok(P, C, state, K1.kps[idx1], K2.kps[idx2]);
-                        }
-                        if (ok) bestIdx2 = idx2, bestDist = dist;
-                    }
-                    if (bestIdx2 >= 0) {
-                        P.match12[idx1] = bestIdx2;
-                        ++nmatch;
-                        if (check_ori) {
-                            float rot = K1.kps[idx1].angle - K2.kps[bestIdx2].angle;
-                            if ((double)rot < 0.0) rot += 360.0f;
-                            int bin = (int)roundf(rot * (1.0f / kHisto));
-                            if (bin == kHisto) bin = 0;
-                            bins[idx1] = (uint8_t)bin;
-                        }
-                    }
-                }
-            }
-            wave_sync();
+            int tot;
+            const int off = n_valid + block_scan_excl(cnt, 0, add, s_wi, tot);
+            for (int j = 0; j < cnt; ++j) v_pk[off + j] = pk[j], v_code[off + j] = cd[j];
+            n_valid += tot;
         }
     }
+    flush();
+    if (tid == 0) finish_row();
+    __syncthreads();
     if (check_ori) {   // rotation histogram: keep the three largest bins (ComputeThreeMaxima, :2537-2573)
-        for (int i = lane; i < K1.n; i += 64)
+        for (int i = tid; i < K1.n; i += kTriThreads)
             if (bins[i] != 0xff) atomicAdd(&hist[bins[i]], 1);
-        if (lane == 0) s_removed = 0;
-        wave_sync();
-        if (lane == 0) {
+        __syncthreads();
+        if (tid == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < kHisto; i++) {
                 const int s = hist[i];
@@ -366,14 +490,15 @@ __global__ void __launch_bounds__(64) tri_kernel(const omv_tri_pair *pairs, TriC
             else if (max3 < 0.1f * (float)max1) ind3 = -1;
             for (int i = 0; i < kHisto; ++i) s_keep[i] = (i == ind1 || i == ind2 || i == ind3) ? 1 : 0;
         }
-        wave_sync();
+        __syncthreads();
         int removed = 0;
-        for (int i = lane; i < K1.n; i += 64)
+        for (int i = tid; i < K1.n; i += kTriThreads)
             if (bins[i] != 0xff && !s_keep[bins[i]]) P.match12[i] = -1, ++removed;
-        for (int d = 32; d >= 1; d >>= 1) removed += __shfl_xor(removed, d, 64);
-        if (lane == 0) nmatch -= removed;
+        int tot;
+        block_scan_excl(removed, 0, add, s_wi, tot);
+        if (tid == 0) nmatch -= tot;
     }
-    if (lane == 0) n_matches[blockIdx.x] = nmatch;
+    if (tid == 0) n_matches[blockIdx.x] = nmatch;
 }
 
 // Frame::ComputeMultiFishEyeMatches' depth check (src/Frame.cc:1488-1512) on the Lowe-filtered
@@ -506,7 +631,7 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
     d_err = (int *)(d_pairs + n_pairs);
     HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(omv_tri_pair) * n_pairs, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
-    tri_kernel<<<n_pairs, 64, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err);
+    tri_kernel<<<n_pairs, kTriThreads, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err);
     HIP_OK(hipGetLastError());
     int h_err = 0;
     HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));

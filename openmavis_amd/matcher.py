@@ -68,6 +68,31 @@ class MapPointBatch:
         return v
 
 
+class TriPairBatch:
+    """The omv_tri_pair array of a list of keyframe pairs (see ORBmatcher.SearchForTriangulation), built
+    once so repeated searches over resident keyframes pay no per-pair host marshalling."""
+
+    def __init__(self, pairs):
+        from .synth_tri import kf_struct
+        self.n = len(pairs)
+        self.arr = (_lib.TriPair * max(self.n, 1))()
+        self._keep = []
+        self.device = None
+
+        def ptr(_name, t):
+            self._keep.append(t)
+            return ctypes.c_void_p(t.data_ptr())
+
+        for i, p in enumerate(pairs):
+            self.arr[i].kf1 = kf_struct(p["kf1"], _lib.KfView, p["kf1"]["level_sigma2"], ptr)
+            self.arr[i].kf2 = kf_struct(p["kf2"], _lib.KfView, p["kf2"]["level_sigma2"], ptr)
+            T = np.ascontiguousarray(np.asarray(p["T"], np.float32).reshape(_lib.OMV_TRI_PAIRS, 12))
+            ctypes.memmove(ctypes.addressof(self.arr[i].T), T.ctypes.data, T.nbytes)
+            self.arr[i].match12 = ctypes.c_void_p(p["match12"].data_ptr())
+            self._keep.append(p["match12"])
+            self.device = p["match12"].device
+
+
 class ORBmatcher:
     def __init__(self, nnratio=0.6, checkOri=True):
         self.mfNNratio = float(nnratio)
@@ -182,37 +207,20 @@ class ORBmatcher:
         (n, n_left, n_right, n_sideleft ints; kps / desc / has_mp / node_id / node_start / node_idx device
         tensors; level_sigma2 host floats), T the 10 camera-pair transforms (float [10][12]), match12 a
         device int32 [kf1.n] receiving vMatches12.  cams: host [4][8] KB8 parameters (L, R, SL, SR).
-        Returns the per-pair match counts (device int32 tensor); synchronous."""
+        `pairs` may also be a prebuilt TriPairBatch.  Returns the per-pair match counts (device int32
+        tensor); synchronous."""
         import torch
-        from .synth_tri import kf_struct
         if self._h is None:
             h = ctypes.c_void_p()
             _lib.check(self._lib.omv_matcher_create(1, 1, 1, 1, ctypes.byref(h)), "omv_matcher_create")
             self._h, self._shape = h, (1, 1, 1, 1)
-        n = len(pairs)
-        arr = (_lib.TriPair * max(n, 1))()
-        keep = []
-
-        def ptr(_name, t):
-            keep.append(t)
-            return ctypes.c_void_p(t.data_ptr())
-
-        dev = None
-        for i, p in enumerate(pairs):
-            arr[i].kf1 = kf_struct(p["kf1"], _lib.KfView, p["kf1"]["level_sigma2"], ptr)
-            arr[i].kf2 = kf_struct(p["kf2"], _lib.KfView, p["kf2"]["level_sigma2"], ptr)
-            T = np.asarray(p["T"], np.float32).reshape(_lib.OMV_TRI_PAIRS, 12)
-            for r in range(_lib.OMV_TRI_PAIRS):
-                for c in range(12):
-                    arr[i].T[r][c] = float(T[r, c])
-            arr[i].match12 = ctypes.c_void_p(p["match12"].data_ptr())
-            dev = p["match12"].device
+        batch = pairs if isinstance(pairs, TriPairBatch) else TriPairBatch(pairs)
+        n, arr, dev = batch.n, batch.arr, batch.device
         out = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         c = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(4, 8))
         _lib.check(self._lib.omv_matcher_search_for_triangulation(
             self._h, n, arr, _lib.ptr(c), int(bool(bOnlyStereo)), int(bool(bCoarse)), int(self.mbCheckOrientation),
             _lib.ptr(out), self._stream(stream)), "omv_matcher_search_for_triangulation")
-        del keep
         return out[:n]
 
     def StereoLapping(self, frames, ratio=0.8, stream=None):

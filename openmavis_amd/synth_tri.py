@@ -110,12 +110,13 @@ def make_tri_pair(seed=1, n_pts=500, n_distract=200, n_nodes=100, baseline=(0.2,
 
 def kf_struct(kf, struct_cls, sigma2, arr):
     """omv_kf_view from a synth keyframe dict; `arr(name, array)` returns the pointer to use."""
+    import ctypes
     s = struct_cls()
     s.n, s.n_left, s.n_right, s.n_sideleft = int(kf["n"]), int(kf["n_left"]), int(kf["n_right"]), int(kf["n_sideleft"])
     s.kps, s.desc, s.has_mp = arr("kps", kf["kps"]), arr("desc", kf["desc"]), arr("has_mp", kf["has_mp"])
     s.n_nodes = int(len(kf["node_id"]))
     s.node_id, s.node_start, s.node_idx = (arr("node_id", kf["node_id"]), arr("node_start", kf["node_start"]),
                                            arr("node_idx", kf["node_idx"]))
-    for i in range(min(16, len(sigma2))):
-        s.level_sigma2[i] = float(sigma2[i])
+    sg = np.ascontiguousarray(np.asarray(sigma2, np.float32)[:16])
+    ctypes.memmove(ctypes.addressof(s.level_sigma2), sg.ctypes.data, sg.nbytes)
     return s

@@ -51,3 +51,19 @@ def test_search_for_triangulation_edge_cases(oracle):
     n = m.SearchForTriangulation(dp, p["cams"]).cpu().numpy()
     assert n[1] == 0 and (dp[1]["match12"].cpu().numpy() == -1).all()
     assert n[0] == oracle.search_for_triangulation(p)[0]
+
+
+@pytest.mark.parametrize("kw", [dict(n_pts=1500, n_distract=600),          # several replay batches
+                                dict(n_pts=600, n_distract=300, n_nodes=3),   # few huge nodes: tiles span rows
+                                dict(n_pts=900, n_distract=300, n_nodes=4000),  # many tiny nodes, > 1 segment
+                                dict(n_pts=500, cams_used=2)])                 # only listed L/R pairs
+def test_search_for_triangulation_shapes(oracle, kw):
+    """Bench-size and skewed FeatureVector layouts: batch / tile / segment boundaries of the device scan."""
+    pairs = [synth_tri.make_tri_pair(seed=30 + s, **kw) for s in range(3)]
+    dp = _device_pairs(pairs)
+    m = ORBmatcher(0.6, True)
+    n = m.SearchForTriangulation(dp, pairs[0]["cams"]).cpu().numpy()
+    for i, p in enumerate(pairs):
+        n_o, m_o = oracle.search_for_triangulation(p, check_ori=True)
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
