@@ -88,6 +88,13 @@ def cpu_baseline(n_frames=12, frames=None):
     for i, imgs in enumerate(frames):
         n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH)
         prep.append(_gen_map((kps, desc, n_out, 700 + i)))
+    from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
+    Rlr = R_cl[1].T.astype(np.float32)
+    tlr = (-R_cl[1].T @ t_cl[1]).astype(np.float32)
+    bf = float(cams[0][0] * np.linalg.norm(tlr))
+    sigma2 = (np.float32(SCALE) ** (2 * np.arange(NLEV))).astype(np.float32)
+    U = undist_params(BLOCK_CAM_ID)
+    depth = (np.random.default_rng(5).random((4, H, W)) * 25.0).astype(np.float32)
     t0 = time.perf_counter()
     for i, imgs in enumerate(frames):
         n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH)
@@ -101,6 +108,9 @@ def cpu_baseline(n_frames=12, frames=None):
         for qi in np.nonzero(ok)[0]:
             l2r[mono[0] + qi] = mono[1] + i2[qi, 0]
             r2l[mono[1] + i2[qi, 0]] = mono[0] + qi
+        l2r, r2l, _, _ = oracle.stereo_triangulate(kps[0], n_out[0], kps[1], n_out[1], cams[:2], Rlr, tlr, sigma2, l2r)
+        for c in range(4):   # mvuRight (GetDepthFromUndistortedPoints)
+            oracle.depth_from_undistorted(kps[c, :n_out[c]], depth[c], U[c], bf)
         pose, world, mp = prep[i]
         track, _ = oracle.frustum(rig, pose, world["pos"], world["normal"], world["min_dist"], world["max_dist"], 0.5,
                                   mp["view_cos"], mp["track_depth"])
@@ -392,6 +402,18 @@ def main():
 
     cams_r, R_cl, t_cl = synth.hilti_rig(C)
     rig = make_rig(cams_r, R_cl, t_cl, W, H, SCALE, NLEV)
+    # Frame ctor tail: the lapping pairs' TriangulateMatches (mRlr / mtlr = left-from-right) and mvuRight
+    # from the 4 reference blocks' undistorted depth images (synthetic, resident: 0-25 m, holes)
+    from openmavis_amd.frame import frame_uright
+    Rlr = R_cl[1].T.astype(np.float32)
+    tlr = (-R_cl[1].T @ t_cl[1]).astype(np.float32)
+    BF = float(cams_r[0][0] * np.linalg.norm(tlr))
+    sigma2 = (np.float32(SCALE) ** (2 * np.arange(NLEV))).astype(np.float32)
+    NB = min(4, C)
+    gdep = torch.Generator(device=dev).manual_seed(1234 + first)
+    for gr in groups:
+        gr["depth"] = torch.rand((Bg, NB, H, W), generator=gdep, device=dev, dtype=torch.float32) * 25.0
+        gr["uright"] = torch.empty((Bg, NB, gr["cap"]), dtype=torch.float32, device=dev)
     timing_on = [False]
 
     def step():
@@ -402,6 +424,8 @@ def main():
                 fb.kp_to_mp.fill_(-1)                   # Frame ctor: mvpMapPoints = vector(N, nullptr)
             gr["matcher"].AssignFeaturesToGrid(fb, stream=st)
             gr["matcher"].StereoLapping(fb, 0.8, stream=st)
+            gr["matcher"].StereoTriangulate(fb, cams_r[:2], Rlr, tlr, sigma2, stream=st)
+            frame_uright(fb, gr["depth"], BF, stream=st, out=gr["uright"])
             if timing_on[0]:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
@@ -514,7 +538,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded Hilti-like 5x720x540 frames; 5000-point local maps from the frames' own keypoints)",
         "config": {"workload": "Hilti-2022 exp04-like 5 cams 720x540, 1200 feat/cam, ORB extract + lapping knn + "
-                               "SearchByProjection(M=5000, th=6)",
+                               "stereo TriangulateMatches + mvuRight from depth + SearchByProjection(M=5000, th=6)",
                    "frames_per_step_per_gpu": B, "streams_per_gpu": G, "parallelism": f"frame-replicas x{world}"},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
         "matches_last_step": n_matches,

@@ -455,6 +455,43 @@ omv_status omv_pose_destroy(omv_pose *h);
 omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
                                      int32_t *n_good, double *H, void *stream);
 
+/* ---- Frame construction tail (src/Frame.cc:1913-1939) ---- */
+
+/* cv::fisheye::undistortPoints parameters of one camera block (GetDepthFromUndistortedPoints,
+ * src/Frame.cc:1659-1734): origK / newK as float (fx, fy, cx, cy; the reference's cv::Mat_<float>),
+ * dist_coeff as double (k1..k4). */
+typedef struct omv_fisheye_undist {
+    float K[4];
+    double D[4];
+    float newK[4];
+} omv_fisheye_undist;
+
+/* GetDepthFromUndistortedPoints for every keypoint of every camera block:
+ * cv::fisheye::undistortPoints(kp.pt, origK, D, noArray(), newK) (OpenCV >= 4.5 semantics: at most
+ * 10 Newton steps, eps 1e-8, theta clipped to pi/2, (-1e6, -1e6) for a flipped / unconverged theta),
+ * then d = depth[cam](round(y), round(x)) (0 outside the image) and
+ * u_right = kp.x - bf / d where 0 < d <= 20, else -1 (:1736-1763); the reference's mvuRight.
+ * The first n_blocks (<= n_cams, <= 8) camera blocks of each frame are processed.
+ *   kps / n_kp   device [frame][n_cams][kp_cap] / [frame][n_cams]
+ *   depth        device float [frame][n_blocks][depth_h][depth_w] (the undistorted depth images)
+ *   undist       host [n_blocks]: the block's parameters (the reference maps L, R, SL, SR to its
+ *                cam_id 1, 0, 4, 3, :1916-1922)
+ *   u_right      device float [frame][n_blocks][kp_cap]
+ *   undist_xy    device float [frame][n_blocks][kp_cap][2] (the undistorted points) or NULL */
+omv_status omv_frame_uright(int n_frames, int n_cams, int n_blocks, int kp_cap, const omv_kp *kps, const int *n_kp,
+                            const float *depth, int depth_w, int depth_h, const omv_fisheye_undist *undist, float bf,
+                            float *u_right, float *undist_xy, void *stream);
+
+/* The cv::vconcat of Frame's per-camera keypoints / descriptors / mvuRight into the dense frame
+ * arrays (mDescriptors = [L; R; SL; SR], :1936-1939; mvKeys order of the N-indexed vectors):
+ * frame f's keypoints of its first n_blocks (<= n_cams) blocks land at rows [offset[f], offset[f] + N_f),
+ * N_f = sum of n_kp[f][0..n_blocks).  uright_in: [frame][n_blocks][kp_cap] (omv_frame_uright's layout).
+ *   offset       device int [n_frames + 1] (output; exclusive prefix of N_f, offset[n_frames] = total)
+ *   kps_out / desc_out / uright_out   device [total] rows (uright_in / uright_out may be NULL) */
+omv_status omv_frame_pack(int n_frames, int n_cams, int n_blocks, int kp_cap, const omv_kp *kps, const uint8_t *desc,
+                          const float *uright_in, const int *n_kp, int *offset, omv_kp *kps_out, uint8_t *desc_out,
+                          float *uright_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,6 +125,11 @@ class TriPair(ctypes.Structure):
                 ("match12", ctypes.c_void_p)]
 
 
+class FisheyeUndist(ctypes.Structure):
+    """omv_fisheye_undist (include/omv.h)."""
+    _fields_ = [("K", ctypes.c_float * 4), ("D", ctypes.c_double * 4), ("newK", ctypes.c_float * 4)]
+
+
 class LbaOpts(ctypes.Structure):
     _fields_ = [("opt_it", ctypes.c_int), ("lambda_init", ctypes.c_double), ("max_trials", ctypes.c_int),
                 ("large", ctypes.c_int)]
@@ -195,6 +200,9 @@ SIGNATURES = {
     "omv_pose_destroy": (_I, [_VP]),
     "omv_pose_inertial_last_kf": (_I, [_VP, ctypes.POINTER(PoseBatch), _I, _VP, _VP, _VP, _VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
+    "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
+                              _VP]),
+    "omv_frame_pack": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
 }
 
 _lib = None

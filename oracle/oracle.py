@@ -361,3 +361,16 @@ def stereo_triangulate(kpsL, nL, kpsR, nR, cams, Rlr, tlr, sigma2, l2r):
                                     _p(np.ascontiguousarray(tlr, np.float32)), _p(np.ascontiguousarray(sigma2, np.float32)),
                                     _p(l2r), _p(r2l), _p(depth), _p(p3d))
     return l2r, r2l[:nR], depth[:nL], p3d[:nL]
+
+
+def depth_from_undistorted(keys, depth, undist, bf):
+    """GetDepthFromUndistortedPoints for one camera block: keys (KP_DTYPE [n]), depth float [h][w],
+    undist an omv_fisheye_undist (openmavis_amd._lib.FisheyeUndist).  Returns (u_right [n], xy [n][2])."""
+    keys = np.ascontiguousarray(keys)
+    n = len(keys)
+    d = np.ascontiguousarray(depth, np.float32)
+    ur = np.zeros(max(n, 1), np.float32)
+    xy = np.zeros((max(n, 1), 2), np.float32)
+    lib().oracle_depth_from_undistorted(_p(keys) if n else None, int(n), _p(d), int(d.shape[1]), int(d.shape[0]),
+                                        ctypes.byref(undist), ctypes.c_float(bf), _p(ur), _p(xy))
+    return ur[:n], xy[:n]
