@@ -455,6 +455,29 @@ omv_status omv_pose_destroy(omv_pose *h);
 omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
                                      int32_t *n_good, double *H, void *stream);
 
+/* Optimizer::PoseInertialOptimizationLastFrame (src/Optimizer.cc:5580-6170): as above, but the previous
+ * frame's four vertices are free (ids 4-7; the batch's kf_* fields hold Frame::mpPrevFrame's state and
+ * `preint` is Frame::mpImuPreintegratedFrame), one EdgeInertial over all six vertex blocks, EdgeGyroRW /
+ * EdgeAccRW between the two frames' biases with information from Frame::mpImuPreintegrated's C (the
+ * last keyframe's preintegration, :5960-5971), and an EdgePriorPoseImu (G2oTypes.cc:748-785, Huber 5)
+ * on the previous frame from its ConstraintPoseImu (pFp->mpcpi).  The mono chi2 threshold is 5.991 in all
+ * four rounds (:5992).  H receives the frame's 15x15 block after Optimizer::Marginalize(H, 0, 14)
+ * (:3388-3455, pseudo-inverse below 1e-6) — the matrix handed to the ConstraintPoseImu ctor (:6158-6164);
+ * run omv_pose_constraint on it to obtain the stored prior.  The previous frame's state is not written
+ * back (the reference discards it). */
+typedef struct omv_pose_prior {
+    const double *Rwb, *twb, *vel, *bg, *ba;   /* device [F][9] / [F][3]: ConstraintPoseImu Rwb, twb, vwb, bg, ba */
+    const double *H;                           /* device [F][225]: ConstraintPoseImu::H (after its ctor) */
+    const float *preint_kf;                    /* device [F][OMV_PREINT_FLOATS]: Frame::mpImuPreintegrated */
+} omv_pose_prior;
+omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, const omv_pose_prior *prior,
+                                        int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream);
+
+/* ConstraintPoseImu ctor (include/G2oTypes.h:639-659) on n matrices: H <- (H + H) / 2 (= H), then its
+ * symmetric eigen-decomposition with eigenvalues below 1e-12 zeroed, recomposed.  Device [n][225]
+ * (H_out may alias H_in).  Asynchronous. */
+omv_status omv_pose_constraint(int n, const double *H_in, double *H_out, void *stream);
+
 /* ---- Frame construction tail (src/Frame.cc:1913-1939) ---- */
 
 /* cv::fisheye::undistortPoints parameters of one camera block (GetDepthFromUndistortedPoints,

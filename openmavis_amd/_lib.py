@@ -108,6 +108,11 @@ class PoseBatch(ctypes.Structure):
                     "stereo_xw")] + [("kp_cap", ctypes.c_int), ("n_mono", ctypes.c_int), ("n_stereo", ctypes.c_int)]
 
 
+class PosePrior(ctypes.Structure):
+    """omv_pose_prior (include/omv.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("Rwb", "twb", "vel", "bg", "ba", "H", "preint_kf")]
+
+
 class KfView(ctypes.Structure):
     """omv_kf_view (include/omv.h)."""
     _fields_ = [("n", ctypes.c_int), ("n_left", ctypes.c_int), ("n_right", ctypes.c_int),
@@ -199,6 +204,9 @@ SIGNATURES = {
     "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),
     "omv_pose_destroy": (_I, [_VP]),
     "omv_pose_inertial_last_kf": (_I, [_VP, ctypes.POINTER(PoseBatch), _I, _VP, _VP, _VP, _VP]),
+    "omv_pose_inertial_last_frame": (_I, [_VP, ctypes.POINTER(PoseBatch), ctypes.POINTER(PosePrior), _I, _VP, _VP,
+                                          _VP, _VP]),
+    "omv_pose_constraint": (_I, [_I, _VP, _VP, _VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
     "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
                               _VP]),

@@ -411,6 +411,68 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Cyclic Jacobi eigen-decomposition of the symmetric N x N matrix A (row-major, LDS) over one wavefront:
+// A is driven to diag(w) in place, V (LDS, N x N) receives the eigenvectors (columns).  Per element the same
+// operations in the same order as the oracle's sym_eig (ba_oracle.cpp).  Every lane of the wave must call it.
+template <int N>
+__device__ inline void sym_eig_wave(double *A, double *V, int lane) {
+    static_assert(N <= 64, "one row per lane");
+    for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) off += A[p * N + q] * A[p * N + q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = A[p * N + q];
+                if (apq == 0) continue;
+                const double th = (A[q * N + q] - A[p * N + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+                const double c = 1 / sqrt(t * t + 1), s = t * c;
+                wave_lds_sync();
+                if (lane < N) {
+                    const double akp = A[lane * N + p], akq = A[lane * N + q];
+                    A[lane * N + p] = c * akp - s * akq, A[lane * N + q] = s * akp + c * akq;
+                }
+                wave_lds_sync();
+                if (lane < N) {
+                    const double apk = A[p * N + lane], aqk = A[q * N + lane];
+                    A[p * N + lane] = c * apk - s * aqk, A[q * N + lane] = s * apk + c * aqk;
+                    const double vkp = V[lane * N + p], vkq = V[lane * N + q];
+                    V[lane * N + p] = c * vkp - s * vkq, V[lane * N + q] = s * vkp + c * vkq;
+                }
+                wave_lds_sync();
+            }
+    }
+}
+
+// EdgePriorPoseImu::computeError / linearizeOplus (G2oTypes.cc:758-785) at the vertex state (R, t, v, bg, ba)
+// against the ConstraintPoseImu state pr = [Rwb 9 | twb 3 | vwb 3 | bg 3 | ba 3]; J (15x15 over pose 6,
+// v 3, bg 3, ba 3) may be null.
+__device__ inline void prior_error_jac(const double *pr, const double *R, const double *t, const double *v,
+                                       const double *bg, const double *ba, double *e, double *J) {
+    double RR[9], d[3], et[3];
+    mtm3(pr, R, RR);
+    log_so3(RR, e);
+    for (int q = 0; q < 3; ++q) d[q] = t[q] - pr[9 + q];
+    mtv3(pr, d, et);
+    for (int q = 0; q < 3; ++q) {
+        e[3 + q] = et[q];
+        e[6 + q] = v[q] - pr[12 + q];
+        e[9 + q] = bg[q] - pr[15 + q];
+        e[12 + q] = ba[q] - pr[18 + q];
+    }
+    if (!J) return;
+    double iJ[9];
+    inv_right_jac(e, iJ);
+    for (int q = 0; q < 225; ++q) J[q] = 0.0;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) J[r * 15 + c] = iJ[3 * r + c], J[(3 + r) * 15 + 3 + c] = RR[3 * r + c];
+    for (int q = 6; q < 15; ++q) J[q * 15 + q] = 1.0;
+}
+
 // EdgeInertial's information (ctor, G2oTypes.cc:486-495): Info = C[0:9,0:9]^-1, symmetrised, projected onto
 // its non-negative eigen-space (eigenvalues < 1e-12 zeroed) — Gauss-Jordan with partial pivoting and cyclic
 // Jacobi, per element the same operations in the same order as lba.hip's host path and the oracle, spread
@@ -451,33 +513,7 @@ __device__ inline void inertial_info9_wave(const float *C15, double *out, double
     wave_lds_sync();
     for (int q = lane; q < 81; q += 64) I[q] = A[q];
     wave_lds_sync();
-    for (int sweep = 0; sweep < 100; ++sweep) {   // cyclic Jacobi
-        double off = 0;
-        for (int p = 0; p < 9; ++p)
-            for (int q = p + 1; q < 9; ++q) off += I[p * 9 + q] * I[p * 9 + q];
-        if (off < 1e-300) break;
-        for (int p = 0; p < 9; ++p)
-            for (int q = p + 1; q < 9; ++q) {
-                const double apq = I[p * 9 + q];
-                if (apq == 0) continue;
-                const double th = (I[q * 9 + q] - I[p * 9 + p]) / (2 * apq);
-                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
-                const double c = 1 / sqrt(t * t + 1), s = t * c;
-                wave_lds_sync();
-                if (lane < 9) {
-                    const double akp = I[lane * 9 + p], akq = I[lane * 9 + q];
-                    I[lane * 9 + p] = c * akp - s * akq, I[lane * 9 + q] = s * akp + c * akq;
-                }
-                wave_lds_sync();
-                if (lane < 9) {
-                    const double apk = I[p * 9 + lane], aqk = I[q * 9 + lane];
-                    I[p * 9 + lane] = c * apk - s * aqk, I[q * 9 + lane] = s * apk + c * aqk;
-                    const double vkp = V[lane * 9 + p], vkq = V[lane * 9 + q];
-                    V[lane * 9 + p] = c * vkp - s * vkq, V[lane * 9 + q] = s * vkp + c * vkq;
-                }
-                wave_lds_sync();
-            }
-    }
+    sym_eig_wave<9>(I, V, lane);
     for (int q = lane; q < 81; q += 64) {
         const int r = q / 9, c = q % 9;
         double s = 0;

@@ -19,6 +19,15 @@
 // one-thread-per-frame kernel launched first.
 // Between rounds every thread classifies its edges (mono pass, then stereo pass: the keypoint flag is
 // shared and the stereo pass sees the mono pass's writes, as in the reference's two loops).
+//
+// Optimizer::PoseInertialOptimizationLastFrame (src/Optimizer.cc:5580-6170) is the same kernel with
+// kLF = true: the previous frame's four vertices are free (30 states), EdgeInertial contributes all
+// 24 Jacobian columns (thread 0) while thread 64 linearises the EdgePriorPoseImu (G2oTypes.cc:748-785,
+// Huber 5), the random walks couple the two frames' biases, the 30x30 LDLT runs on wavefront 0 and
+// lanes 0 / 1 update the two frames.  At the end the 30-state Hessian is marginalised onto the frame
+// (Optimizer::Marginalize, Optimizer.cc:3388-3455) with a wavefront Jacobi pseudo-inverse.
+// pose_constraint_kernel is the ConstraintPoseImu ctor (G2oTypes.h:639-659) that turns that matrix
+// into the next frame's prior.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -65,24 +74,49 @@ struct PoseArgs {
     double *H;
     int rec_init;
     const double *info;   // [F][99] EdgeInertial 9x9 | GyroRW 3x3 | AccRW 3x3 information (pose_info_kernel)
+    // PoseInertialOptimizationLastFrame: the previous frame's ConstraintPoseImu (EdgePriorPoseImu)
+    const double *pRwb, *ptwb, *pvel, *pbg, *pba, *pH;
 };
 
-// The edges' information matrices (EdgeInertial ctor :486-495, InfoG / InfoA :5397-5406), one wavefront
-// per frame: kept out of the optimisation kernel so its Jacobi sweeps do not size that kernel's registers.
-__global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, double *info) {
+// The edges' information matrices (EdgeInertial ctor :486-495 from `preint`, InfoG / InfoA :5397-5406 /
+// :5960-5971 from `preint_rw`), one wavefront per frame: kept out of the optimisation kernel so its
+// Jacobi sweeps do not size that kernel's registers.
+__global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, const float *preint_rw, double *info) {
     __shared__ double sm[243];
     const int f = blockIdx.x, lane = threadIdx.x;
-    const float *pre = preint + (size_t)f * kPF;
+    const float *pre = preint + (size_t)f * kPF, *prw = preint_rw + (size_t)f * kPF;
     double *o = info + (size_t)f * 99;
     inertial_info9_wave(pre + PreView::C, o, sm, lane);
     if (lane == 0) {
         double g[9], a[9];
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c)
-                g[3 * r + c] = pre[PreView::C + (9 + r) * 15 + 9 + c], a[3 * r + c] = pre[PreView::C + (12 + r) * 15 + 12 + c];
+                g[3 * r + c] = prw[PreView::C + (9 + r) * 15 + 9 + c], a[3 * r + c] = prw[PreView::C + (12 + r) * 15 + 12 + c];
         inv3(g, o + 81);
         inv3(a, o + 90);
     }
+}
+
+// ConstraintPoseImu ctor (G2oTypes.h:639-659), one wavefront per matrix: (H + H) / 2, eigenvalues < 1e-12
+// zeroed, V diag(w) V^T.
+__global__ void __launch_bounds__(64) pose_constraint_kernel(const double *Hin, double *Hout) {
+    __shared__ double A[225], V[225];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const double *hi = Hin + (size_t)f * 225;
+    for (int q = lane; q < 225; q += 64) A[q] = (hi[q] + hi[q]) / 2;
+    wave_lds_sync();
+    sym_eig_wave<15>(A, V, lane);
+    double out[4];
+    for (int q = lane, i = 0; q < 225; q += 64, ++i) {
+        const int r = q / 15, c = q % 15;
+        double s = 0;
+        for (int k = 0; k < 15; ++k) {
+            const double w = A[k * 16] < 1e-12 ? 0.0 : A[k * 16];
+            s += V[r * 15 + k] * w * V[c * 15 + k];
+        }
+        out[i] = s;
+    }
+    for (int q = lane, i = 0; q < 225; q += 64, ++i) Hout[(size_t)f * 225 + q] = out[i];
 }
 
 // One visual edge of the frame (EdgeMonoOnlyPose or EdgeStereoOnlyPose).
@@ -200,18 +234,40 @@ __device__ __forceinline__ int block_count(int v, int *sh) {
     return t;
 }
 
-__global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, PoseArgs A) {
+// State index (LastFrame's 30-vector: frame pose 0-5, v 6-8, bg 9-11, ba 12-14, previous frame 15-29) ->
+// column of EdgeInertial's 9x24 Jacobian [P1 V1 G1 A1 P2 V2]; -1 for the frame's biases.
+__device__ __forceinline__ int ei_col(int s) { return s < 9 ? 15 + s : (s < 15 ? -1 : s - 15); }
+
+// EdgeGyroRW (`acc` false) / EdgeAccRW Hessian entry between LastFrame states i and j: [[O, -O], [-O, O]]
+// over (frame bias, previous frame bias); 0 off the bias blocks.
+__device__ __forceinline__ double rw_entry(int i, int j, bool acc, const double *O) {
+    const int o = acc ? 12 : 9;
+    const int gi = (i >= o && i < o + 3) ? i - o : ((i >= o + 15 && i < o + 18) ? i - o - 15 : -1);
+    const int gj = (j >= o && j < o + 3) ? j - o : ((j >= o + 15 && j < o + 18) ? j - o - 15 : -1);
+    if (gi < 0 || gj < 0) return 0.0;
+    return ((i < 15) == (j < 15)) ? O[3 * gi + gj] : -O[3 * gi + gj];
+}
+
+// kLF = false: PoseInertialOptimizationLastKeyFrame (15 free states, the keyframe's vertices fixed);
+// kLF = true: PoseInertialOptimizationLastFrame (30 free states, EdgePriorPoseImu on the previous frame).
+template <bool kLF>
+__global__ void __launch_bounds__(kPoseThreads) pose_opt_kernel(Rig rig, PoseArgs A) {
+    constexpr int N = kLF ? 30 : 15;
+    constexpr int NP = kLF ? 225 : 1;
     const int f = blockIdx.x, tid = threadIdx.x;
     const int C = rig.n_cams;
-    // vertex states: index 0 = last keyframe (fixed), 1 = frame
+    // vertex states: index 0 = last keyframe (fixed) / previous frame (free), 1 = frame
     __shared__ double sRwb[18], stwb[6], svel[6], sbg[6], sba[6];
     __shared__ double sRcw[kMaxCams * 9], stcw[kMaxCams * 3];
     __shared__ double red[kPoseWaves][kNormal];
     __shared__ double nrm[kNormal];
     __shared__ double J[216], WJ[216], om9[9], info9[81], infoG[9], infoA[9], e9[9];
-    __shared__ double Hs[225], bs[15], xs[15], xt[15], lt[30];
-    __shared__ int s_ok, cnt[kPoseWaves], ltr[15];
+    __shared__ double Hs[N * N], bs[N], xs[N], xt[N], lt[2 * N];
+    __shared__ int s_ok, cnt[kPoseWaves], ltr[N];
     __shared__ int k1s, k2s;
+    // EdgePriorPoseImu: ConstraintPoseImu state / information, error, Jacobian, H_prior J, H_prior e
+    __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1];
+    __shared__ double Am[NP], Vm[NP];   // Marginalize's eigen-decomposition
     if (tid == 0) {
         for (int q = 0; q < 9; ++q) sRwb[q] = A.kRwb[9 * f + q], sRwb[9 + q] = A.Rwb[9 * f + q];
         for (int q = 0; q < 3; ++q) {
@@ -222,10 +278,22 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
         }
         k1s = 0, k2s = 1;
     }
+    if constexpr (kLF) {
+        for (int q = tid; q < 225; q += kPoseThreads) pH[q] = A.pH[(size_t)f * 225 + q];
+        if (tid < 21) {
+            double v;
+            if (tid < 9) v = A.pRwb[9 * f + tid];
+            else if (tid < 12) v = A.ptwb[3 * f + tid - 9];
+            else if (tid < 15) v = A.pvel[3 * f + tid - 12];
+            else if (tid < 18) v = A.pbg[3 * f + tid - 15];
+            else v = A.pba[3 * f + tid - 18];
+            sPr[tid] = v;
+        }
+    }
     for (int q = tid; q < C * 9; q += kPoseThreads) sRcw[q] = A.Rcw[(size_t)f * C * 9 + q];
     for (int q = tid; q < C * 3; q += kPoseThreads) stcw[q] = A.tcw[(size_t)f * C * 3 + q];
-    for (int q = tid; q < 15; q += kPoseThreads) xs[q] = 0.0;
-    for (int q = tid; q < 216; q += kPoseThreads) J[q] = 0.0;   // only the free columns 15-23 get written
+    for (int q = tid; q < N; q += kPoseThreads) xs[q] = 0.0;
+    for (int q = tid; q < 216; q += kPoseThreads) J[q] = 0.0;   // LastKeyFrame writes only the free columns 15-23
     const float *pre = A.preint + (size_t)f * kPF;
     for (int q = tid; q < 99; q += kPoseThreads) {
         const double v = A.info[(size_t)f * 99 + q];
@@ -246,7 +314,7 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
     Imu imu{};
     imu.n = 1, imu.kf1 = &k1s, imu.kf2 = &k2s, imu.pre = pre;
     const double dmono = (double)(float)sqrt(5.991), dst = (double)(float)sqrt(7.815);
-    const float chi2Mono[4] = {12.f, 7.5f, 5.991f, 5.991f};
+    const float chi2Mono[4] = {kLF ? 5.991f : 12.f, kLF ? 5.991f : 7.5f, 5.991f, 5.991f};   // :5992 / :5432
     const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
     int nBad = 0, nIn = 0;
     for (int it = 0; it < 4; ++it) {
@@ -273,14 +341,43 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
                 const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, stq ? -v.w * r[2] * w1 : 0.0};
                 edge_normal(JP, stq, v.w * w1, om, acc);
             }
-            if (tid == 0) imu_error_jac_p2v2(st, imu, 0, e9, J);   // EdgeInertial at the current state
-            reduce_normal(acc, red, nrm);   // (its barriers also publish J / e9)
-            // EdgeInertial: free columns 15-20 (frame pose) and 21-23 (frame velocity) -> state 0..8
-            for (int q = tid; q < 81; q += kPoseThreads) {
-                const int r = q / 9, c = q % 9;
-                double t = 0;
-                for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + 15 + c];
-                WJ[q] = t;
+            if constexpr (kLF) {   // EdgeInertial (all six vertex blocks) and EdgePriorPoseImu, in parallel
+                if (tid == 0) {
+                    imu_error(st, imu, 0, e9);
+                    imu_jacobian(st, imu, 0, J);
+                }
+                if (tid == 64) prior_error_jac(sPr, sRwb, stwb, svel, sbg, sba, eP, JPr);
+            } else {
+                if (tid == 0) imu_error_jac_p2v2(st, imu, 0, e9, J);   // EdgeInertial at the current state
+            }
+            reduce_normal(acc, red, nrm);   // (its barriers also publish J / e9 / eP / JPr)
+            if constexpr (kLF) {
+                for (int q = tid; q < 216; q += kPoseThreads) {   // Info J over all 24 columns
+                    const int r = q / 24, c = q % 24;
+                    double t = 0;
+                    for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + c];
+                    WJ[q] = t;
+                }
+                for (int q = tid; q < 225; q += kPoseThreads) {   // H_prior J
+                    const int k = q / 15, j = q % 15;
+                    double t = 0;
+                    for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * JPr[l * 15 + j];
+                    PJ[q] = t;
+                }
+                if (tid >= 64 && tid < 79) {   // H_prior e
+                    const int k = tid - 64;
+                    double t = 0;
+                    for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * eP[l];
+                    OeP[k] = t;
+                }
+            } else {
+                // EdgeInertial: free columns 15-20 (frame pose) and 21-23 (frame velocity) -> state 0..8
+                for (int q = tid; q < 81; q += kPoseThreads) {
+                    const int r = q / 9, c = q % 9;
+                    double t = 0;
+                    for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + 15 + c];
+                    WJ[q] = t;
+                }
             }
             if (tid < 9) {
                 double t = 0;
@@ -288,68 +385,133 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
                 om9[tid] = -t;
             }
             __syncthreads();
-            for (int q = tid; q < 225; q += kPoseThreads) {
-                const int i = q / 15, j = q % 15;
-                double h = 0;
-                if (i < 6 && j < 6) {   // visual 6x6 (symmetric from the upper triangle)
-                    const int a = min(i, j), b = max(i, j);
-                    h = nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+            if constexpr (kLF) {
+                // EdgePriorPoseImu's Huber weight: chi2 = e^T H_prior e (every thread, same order)
+                double chi2p = 0, r0, w1p;
+                for (int k = 0; k < 15; ++k) chi2p += eP[k] * OeP[k];
+                huber(chi2p, 5.0, 25.0, r0, w1p);
+                // lower triangle in the oracle's per-element order (visual, inertial, random walks, prior), mirrored
+                for (int q = tid; q < N * N; q += kPoseThreads) {
+                    const int i = q / N, j = q % N;
+                    if (j > i) continue;
+                    double h = 0;
+                    if (i < 6) h = nrm[j * 6 - j * (j - 1) / 2 + (i - j)];
+                    const int ci = ei_col(i), cj = ei_col(j);
+                    if (ci >= 0 && cj >= 0) {
+                        double t = 0;
+                        for (int k = 0; k < 9; ++k) t += J[k * 24 + ci] * WJ[k * 24 + cj];
+                        h += t;
+                    }
+                    h += rw_entry(i, j, false, infoG);
+                    h += rw_entry(i, j, true, infoA);
+                    if (i >= 15 && j >= 15) {
+                        double t = 0;
+                        for (int k = 0; k < 15; ++k) t += JPr[k * 15 + i - 15] * (w1p * PJ[k * 15 + j - 15]);
+                        h += t;
+                    }
+                    Hs[i * N + j] = h;
+                    Hs[j * N + i] = h;
                 }
-                if (i < 9 && j < 9) {
-                    double t = 0;
-                    for (int k = 0; k < 9; ++k) t += J[k * 24 + 15 + i] * WJ[k * 9 + j];
-                    h += t;
+                if (tid < N) {
+                    const int i = tid;
+                    double t = i < 6 ? nrm[21 + i] : 0.0;
+                    const int ci = ei_col(i);
+                    if (ci >= 0) {
+                        double u = 0;
+                        for (int k = 0; k < 9; ++k) u += J[k * 24 + ci] * om9[k];
+                        t += u;
+                    }
+                    // EdgeGyroRW / EdgeAccRW: e = b_frame - b_prev, J_frame = I, J_prev = -I
+                    const int bi = i % 15;
+                    if (bi >= 9) {
+                        const bool acc_rw = bi >= 12;
+                        const int r = (bi - 9) % 3;
+                        const double *Iw = acc_rw ? infoA : infoG;
+                        const double *bv = acc_rw ? sba : sbg;
+                        double ee[3];
+                        for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
+                        const double oe = Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                        t += i < 15 ? -oe : oe;
+                    }
+                    if (i >= 15) {   // b -= rho' J^T H_prior e
+                        double u = 0;
+                        for (int k = 0; k < 15; ++k) u += JPr[k * 15 + i - 15] * (-OeP[k] * w1p);
+                        t += u;
+                    }
+                    bs[i] = t;
                 }
-                if (i >= 9 && j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
-                Hs[q] = h;
-            }
-            if (tid < 15) {
-                double t = tid < 6 ? nrm[21 + tid] : 0.0;
-                if (tid < 9) {
-                    double u = 0;
-                    for (int k = 0; k < 9; ++k) u += J[k * 24 + 15 + tid] * om9[k];
-                    t += u;
+            } else {
+                for (int q = tid; q < 225; q += kPoseThreads) {
+                    const int i = q / 15, j = q % 15;
+                    double h = 0;
+                    if (i < 6 && j < 6) {   // visual 6x6 (symmetric from the upper triangle)
+                        const int a = min(i, j), b = max(i, j);
+                        h = nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+                    }
+                    if (i < 9 && j < 9) {
+                        double t = 0;
+                        for (int k = 0; k < 9; ++k) t += J[k * 24 + 15 + i] * WJ[k * 9 + j];
+                        h += t;
+                    }
+                    if (i >= 9 && j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+                    Hs[q] = h;
                 }
-                if (tid >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b - b_kf, J = I
-                    const bool acc_rw = tid >= 12;
-                    const int r = (tid - 9) % 3;
-                    const double *Iw = acc_rw ? infoA : infoG;
-                    const double *bv = acc_rw ? sba : sbg;
-                    double ee[3];
-                    for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
-                    t -= Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                if (tid < 15) {
+                    double t = tid < 6 ? nrm[21 + tid] : 0.0;
+                    if (tid < 9) {
+                        double u = 0;
+                        for (int k = 0; k < 9; ++k) u += J[k * 24 + 15 + tid] * om9[k];
+                        t += u;
+                    }
+                    if (tid >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b - b_kf, J = I
+                        const bool acc_rw = tid >= 12;
+                        const int r = (tid - 9) % 3;
+                        const double *Iw = acc_rw ? infoA : infoG;
+                        const double *bv = acc_rw ? sba : sbg;
+                        double ee[3];
+                        for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
+                        t -= Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                    }
+                    bs[tid] = t;
                 }
-                bs[tid] = t;
-            }
+            }   // LastKeyFrame system
             __syncthreads();
             if (tid < 64) {
-                const bool ok = ldlt_pivot_solve_wave<15>(Hs, bs, xt, lt, ltr, tid);
+                const bool ok = ldlt_pivot_solve_wave<N>(Hs, bs, xt, lt, ltr, tid);
                 if (tid == 0) {
                     if (ok)   // a failed solve leaves the solver's previous x in place
-                        for (int q = 0; q < 15; ++q) xs[q] = xt[q];
+                        for (int q = 0; q < N; ++q) xs[q] = xt[q];
                     s_ok = ok ? 1 : 0;
                 }
-            }
-            if (tid == 0) {
-                // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235)
-                double *Rw = sRwb + 9, *tw = stwb + 3;
-                double t[3], dR[9], Rn[9], Rbw[9], tbw[3];
-                mv3(Rw, xs + 3, t);
-                for (int q = 0; q < 3; ++q) tw[q] += t[q];
-                exp_so3(xs, dR);
-                mm3(Rw, dR, Rn);
-                for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
-                tr3(Rn, Rbw);
-                mv3(Rbw, tw, tbw);
-                for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
-                for (int c = 0; c < C; ++c) {
-                    double Rc[9], tc[3];
-                    mm3(rig.Rcb[c], Rbw, Rc);
-                    mv3(rig.Rcb[c], tbw, tc);
-                    for (int q = 0; q < 9; ++q) sRcw[9 * c + q] = Rc[q];
-                    for (int q = 0; q < 3; ++q) stcw[3 * c + q] = tc[q] + rig.tcb[c][q];
+                wave_lds_sync();
+                // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235): lane 0 the frame (with its
+                // cameras), lane 1 the previous frame (LastFrame; its cameras are not read)
+                if (tid == 0 || (kLF && tid == 1)) {
+                    const int v = tid == 0 ? 1 : 0;
+                    const double *xv = xs + (tid == 0 ? 0 : 15);
+                    double *Rw = sRwb + 9 * v, *tw = stwb + 3 * v;
+                    double t[3], dR[9], Rn[9];
+                    mv3(Rw, xv + 3, t);
+                    for (int q = 0; q < 3; ++q) tw[q] += t[q];
+                    exp_so3(xv, dR);
+                    mm3(Rw, dR, Rn);
+                    for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
+                    if (tid == 0) {
+                        double Rbw[9], tbw[3];
+                        tr3(Rn, Rbw);
+                        mv3(Rbw, tw, tbw);
+                        for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
+                        for (int c = 0; c < C; ++c) {
+                            double Rc[9], tc[3];
+                            mm3(rig.Rcb[c], Rbw, Rc);
+                            mv3(rig.Rcb[c], tbw, tc);
+                            for (int q = 0; q < 9; ++q) sRcw[9 * c + q] = Rc[q];
+                            for (int q = 0; q < 3; ++q) stcw[3 * c + q] = tc[q] + rig.tcb[c][q];
+                        }
+                    }
+                    for (int q = 0; q < 3; ++q)
+                        svel[3 * v + q] += xv[6 + q], sbg[3 * v + q] += xv[9 + q], sba[3 * v + q] += xv[12 + q];
                 }
-                for (int q = 0; q < 3; ++q) svel[3 + q] += xs[6 + q], sbg[3 + q] += xs[9 + q], sba[3 + q] += xs[12 + q];
             }
             __syncthreads();
             if (!s_ok) break;   // optimize() stops after a failed iteration
@@ -389,7 +551,7 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
         }
         nBad = block_count(bad, cnt);
         nIn = block_count(in, cnt);
-        if (ne + 3 < 10) break;   // optimizer.edges().size() < 10
+        if (ne + (kLF ? 4 : 3) < 10) break;   // optimizer.edges().size() < 10
     }
     if (nIn < 30 && !A.rec_init) {   // recover not too bad points (:5503-5526)
         int bad = 0;
@@ -407,8 +569,94 @@ __global__ void __launch_bounds__(kPoseThreads) pose_lastkf_kernel(Rig rig, Pose
     }
     __threadfence_block();
     __syncthreads();
-    // ConstraintPoseImu's Hessian (:5529-5571): information without robust weights, inlier edges only
-    if (A.H) {
+    if constexpr (kLF) {
+        // :6112-6156: the 30-state Hessian without robust weights (EdgeInertial, the random walks, the prior,
+        // inlier visual edges) at the final state, then Marginalize(H, 0, 14) of the previous frame
+        // (:3388-3455): H_ff - H_fp pinv(H_pp) H_pf, JacobiSVD's pseudo-inverse of the symmetric H_pp as
+        // V diag(1/w) V^T over |w| > 1e-6.  Hs in this kernel's state order (frame 0-14, previous 15-29).
+        if (A.H) {
+            double acc[kNormal];
+            for (int q = 0; q < kNormal; ++q) acc[q] = 0;
+            for (int q = tid; q < ne; q += kPoseThreads) {
+                const bool stq = q >= nm;
+                const int e = stq ? s0 + q - nm : m0 + q;
+                const VEdge v = load_edge(A, stq, e);
+                if (kpo[v.kp]) continue;
+                double r[3], Xc[3], JP[18];
+                edge_error(rig, sRcw, stcw, v, r, Xc);
+                edge_jac(rig, v, Xc, JP);
+                const double om[3] = {0, 0, 0};
+                edge_normal(JP, stq, v.w, om, acc);
+            }
+            if (tid == 0) imu_jacobian(st, imu, 0, J);
+            if (tid == 64) prior_error_jac(sPr, sRwb, stwb, svel, sbg, sba, eP, JPr);
+            reduce_normal(acc, red, nrm);
+            for (int q = tid; q < 216; q += kPoseThreads) {
+                const int r = q / 24, c = q % 24;
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * 24 + c];
+                WJ[q] = t;
+            }
+            for (int q = tid; q < 225; q += kPoseThreads) {
+                const int k = q / 15, j = q % 15;
+                double t = 0;
+                for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * JPr[l * 15 + j];
+                PJ[q] = t;
+            }
+            __syncthreads();
+            for (int q = tid; q < N * N; q += kPoseThreads) {   // the reference's order: ei, egr, ear, ep, visual
+                const int i = q / N, j = q % N;
+                double h = 0;
+                const int ci = ei_col(i), cj = ei_col(j);
+                if (ci >= 0 && cj >= 0) {
+                    double t = 0;
+                    for (int k = 0; k < 9; ++k) t += J[k * 24 + ci] * WJ[k * 24 + cj];
+                    h += t;
+                }
+                h += rw_entry(i, j, false, infoG);
+                h += rw_entry(i, j, true, infoA);
+                if (i >= 15 && j >= 15) {
+                    double t = 0;
+                    for (int k = 0; k < 15; ++k) t += JPr[k * 15 + i - 15] * PJ[k * 15 + j - 15];
+                    h += t;
+                }
+                if (i < 6 && j < 6) {
+                    const int a = min(i, j), b = max(i, j);
+                    h += nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+                }
+                Hs[q] = h;
+            }
+            __syncthreads();
+            for (int q = tid; q < 225; q += kPoseThreads) Am[q] = Hs[(15 + q / 15) * N + 15 + q % 15];
+            __syncthreads();
+            if (tid < 64) sym_eig_wave<15>(Am, Vm, tid);
+            __syncthreads();
+            for (int q = tid; q < 225; q += kPoseThreads) {   // pinv(H_pp) -> PJ
+                const int r = q / 15, c = q % 15;
+                double s = 0;
+                for (int k = 0; k < 15; ++k) {
+                    const double w = Am[k * 16];
+                    s += Vm[r * 15 + k] * (fabs(w) > 1e-6 ? 1.0 / w : 0.0) * Vm[c * 15 + k];
+                }
+                PJ[q] = s;
+            }
+            __syncthreads();
+            for (int q = tid; q < 225; q += kPoseThreads) {   // T = H_fp pinv(H_pp) -> JPr
+                const int i = q / 15, j = q % 15;
+                double s = 0;
+                for (int k = 0; k < 15; ++k) s += Hs[i * N + 15 + k] * PJ[k * 15 + j];
+                JPr[q] = s;
+            }
+            __syncthreads();
+            for (int q = tid; q < 225; q += kPoseThreads) {
+                const int i = q / 15, j = q % 15;
+                double s = 0;
+                for (int k = 0; k < 15; ++k) s += JPr[i * 15 + k] * Hs[(15 + k) * N + j];
+                A.H[(size_t)f * 225 + q] = Hs[i * N + j] - s;
+            }
+        }
+    } else if (A.H) {
+        // ConstraintPoseImu's Hessian (:5529-5571): information without robust weights, inlier edges only
         double acc[kNormal];
         for (int q = 0; q < kNormal; ++q) acc[q] = 0;
         for (int q = tid; q < ne; q += kPoseThreads) {
@@ -498,11 +746,20 @@ omv_status omv_pose_destroy(omv_pose *h) {
     return OMV_OK;
 }
 
-omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
-                                     int32_t *n_good, double *H, void *stream) {
+}  // extern "C"
+
+namespace {
+
+// Both optimisations: validate, fill the kernel arguments, launch the information kernel and the
+// one-workgroup-per-frame optimisation.  prior == nullptr: LastKeyFrame.
+omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prior *prior, int rec_init,
+                       uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream) {
     if (!h || !b || !kp_outlier || !n_good) return OMV_ERR_ARG;
     if (b->n_frames <= 0 || b->n_frames > h->max_frames || b->n_cams <= 0 || b->n_cams > kMaxCams ||
         b->n_mono < 0 || b->n_stereo < 0 || b->n_mono > h->max_edges || b->n_stereo > h->max_edges || b->kp_cap <= 0)
+        return OMV_ERR_ARG;
+    if (prior && (!prior->Rwb || !prior->twb || !prior->vel || !prior->bg || !prior->ba || !prior->H ||
+                  !prior->preint_kf))
         return OMV_ERR_ARG;
     Rig rig{};
     rig.n_cams = b->n_cams;
@@ -517,8 +774,39 @@ omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int r
                b->mono_xw, b->mono_close, b->stereo_start, b->stereo_cam, b->stereo_kp, b->stereo_obs,
                b->stereo_inv_sigma2, b->stereo_xw, b->kp_cap, h->chi2, h->chi2 + h->max_edges, h->act,
                h->act + h->max_edges, kp_outlier, n_good, H, rec_init, h->info};
-    pose_info_kernel<<<b->n_frames, 64, 0, (hipStream_t)stream>>>(b->preint, h->info);
-    pose_lastkf_kernel<<<b->n_frames, kPoseThreads, 0, (hipStream_t)stream>>>(rig, A);
+    hipStream_t st = (hipStream_t)stream;
+    if (prior) {
+        A.pRwb = prior->Rwb, A.ptwb = prior->twb, A.pvel = prior->vel, A.pbg = prior->bg, A.pba = prior->ba;
+        A.pH = prior->H;
+        pose_info_kernel<<<b->n_frames, 64, 0, st>>>(b->preint, prior->preint_kf, h->info);
+        pose_opt_kernel<true><<<b->n_frames, kPoseThreads, 0, st>>>(rig, A);
+    } else {
+        pose_info_kernel<<<b->n_frames, 64, 0, st>>>(b->preint, b->preint, h->info);
+        pose_opt_kernel<false><<<b->n_frames, kPoseThreads, 0, st>>>(rig, A);
+    }
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+omv_status omv_pose_inertial_last_kf(omv_pose *h, const omv_pose_batch *b, int rec_init, uint8_t *kp_outlier,
+                                     int32_t *n_good, double *H, void *stream) {
+    return launch_pose(h, b, nullptr, rec_init, kp_outlier, n_good, H, stream);
+}
+
+omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, const omv_pose_prior *prior,
+                                        int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream) {
+    if (!prior) return OMV_ERR_ARG;
+    return launch_pose(h, b, prior, rec_init, kp_outlier, n_good, H, stream);
+}
+
+omv_status omv_pose_constraint(int n, const double *H_in, double *H_out, void *stream) {
+    if (n < 0 || (n > 0 && (!H_in || !H_out))) return OMV_ERR_ARG;
+    if (n == 0) return OMV_OK;
+    pose_constraint_kernel<<<n, 64, 0, (hipStream_t)stream>>>(H_in, H_out);
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }

@@ -161,3 +161,35 @@ class PoseInertialOptimizer:
                    "omv_pose_inertial_last_kf")
         del keep
         return n_good
+
+    def PoseInertialOptimizationLastFrame(self, batch, arrays, kp_outlier, H=None, bRecInit=False, stream=None):
+        """Optimizer::PoseInertialOptimizationLastFrame (src/Optimizer.cc:5580-6170) on every frame of the
+        batch.  As PoseInertialOptimizationLastKeyFrame, but `arrays`' kf_* tensors hold the previous
+        frame's vertices (free here, not written back), `preint` is mpImuPreintegratedFrame, and `arrays`
+        also carries the previous frame's ConstraintPoseImu (prior_Rwb / prior_twb / prior_vel / prior_bg /
+        prior_ba, prior_H [F][225]) and preint_kf (mpImuPreintegrated).  H receives Marginalize's frame
+        block; ConstraintPoseImu() turns it into the next prior."""
+        import torch
+        from .synth_pose import as_pose_struct, as_prior_struct
+        s, keep = as_pose_struct(batch, _lib.PoseBatch, arrays)
+        pr = as_prior_struct(_lib.PosePrior, arrays)
+        n_good = torch.zeros(s.n_frames, dtype=torch.int32, device=kp_outlier.device)
+        st = stream if stream is not None else torch.cuda.current_stream(kp_outlier.device).cuda_stream
+        _lib.check(self._lib.omv_pose_inertial_last_frame(self._h, ctypes.byref(s), ctypes.byref(pr),
+                                                          int(bool(bRecInit)), _lib.ptr(kp_outlier), _lib.ptr(n_good),
+                                                          _lib.ptr(H), ctypes.c_void_p(st)),
+                   "omv_pose_inertial_last_frame")
+        del keep
+        return n_good
+
+    @staticmethod
+    def ConstraintPoseImu(H, out=None, stream=None):
+        """The ConstraintPoseImu ctor's projection (include/G2oTypes.h:639-659) of device float64 [n][225]
+        matrices; returns `out` (may be H itself)."""
+        import torch
+        lib = _lib.load()
+        out = torch.empty_like(H) if out is None else out
+        st = stream if stream is not None else torch.cuda.current_stream(H.device).cuda_stream
+        _lib.check(lib.omv_pose_constraint(int(H.shape[0]), _lib.ptr(H), _lib.ptr(out), ctypes.c_void_p(st)),
+                   "omv_pose_constraint")
+        return out

@@ -29,7 +29,7 @@ def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac
 
     F = n_frames
     out = {k: [] for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg",
-                           "kf_ba", "preint", "true_Rwb", "true_twb", "true_vel")}
+                           "kf_ba", "preint", "true_Rwb", "true_twb", "true_vel", "t")}
     mono = {k: [] for k in ("cam", "kp", "obs", "w", "xw", "close", "outlier")}
     st = {k: [] for k in ("cam", "kp", "obs", "w", "xw")}
     m_start, s_start = [0], [0]
@@ -43,6 +43,7 @@ def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac
         out["kf_bg"].append(np.zeros(3)), out["kf_ba"].append(np.zeros(3))
         out["preint"].append(synth_ba.preintegrate(t_kf, t_kf + dt))
         out["true_Rwb"].append(Rt), out["true_twb"].append(pt), out["true_vel"].append(vt)
+        out["t"].append(t_kf + dt)
         ax = rng.normal(0, 1, 3)
         ax /= np.linalg.norm(ax)
         R0 = Rt @ synth_ba._exp(ax * np.deg2rad(rot_noise_deg))
@@ -96,6 +97,51 @@ def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac
     return b
 
 
+PRIOR_KEYS = ("prior_Rwb", "prior_twb", "prior_vel", "prior_bg", "prior_ba", "prior_H", "preint_kf")
+
+
+def make_last_frame_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac=0.0, n_cams=5, bf=40.0,
+                          frame_dt=0.05, prior_rot_deg=0.1, prior_trans=0.01, prior_vel=0.02):
+    """Batches for Optimizer::PoseInertialOptimizationLastFrame (Optimizer.cc:5580-6170): make_pose_batch's
+    frames and edges, each with a previous frame `frame_dt` earlier.  The previous frame carries the
+    ConstraintPoseImu its own optimisation left (pFp->mpcpi: the true state perturbed by ~0.1 deg / 1 cm /
+    2 cm/s, and a dense SPD 15x15 information); its vertices start from that state cast to float, as
+    SetImuPoseVelocity(...cast<float>()) stored it (:6103-6109).  `preint` becomes the frame-to-frame
+    preintegration (mpImuPreintegratedFrame); the keyframe-to-frame one moves to `preint_kf`
+    (mpImuPreintegrated, whose covariance gives EdgeGyroRW / EdgeAccRW their information)."""
+    b = make_pose_batch(n_frames=n_frames, n_pts=n_pts, seed=seed, outlier_frac=outlier_frac,
+                        stereo_frac=stereo_frac, n_cams=n_cams, bf=bf)
+    rng = np.random.Generator(np.random.PCG64(seed + 7919))
+    F = int(b["n_frames"])
+    b["preint_kf"] = b["preint"]
+    pre, pr = [], {k: [] for k in PRIOR_KEYS[:6]}
+    scale = np.array([3e2] * 3 + [1e2] * 3 + [3e1] * 3 + [1e3] * 3 + [1e2] * 3)
+    for f in range(F):
+        t = float(b["t"][f])
+        tp = t - frame_dt
+        Rp, pp, vp = synth_ba._pose_at(tp)
+        ax = rng.normal(0, 1, 3)
+        ax /= np.linalg.norm(ax)
+        Rq = Rp @ synth_ba._exp(ax * np.deg2rad(prior_rot_deg))
+        u, _, vh = np.linalg.svd(Rq)
+        pr["prior_Rwb"].append(u @ vh)
+        pr["prior_twb"].append(pp + rng.normal(0, prior_trans, 3))
+        pr["prior_vel"].append(vp + rng.normal(0, prior_vel, 3))
+        pr["prior_bg"].append(rng.normal(0, 1e-4, 3))
+        pr["prior_ba"].append(rng.normal(0, 1e-3, 3))
+        M = rng.normal(0, 1, (15, 15))
+        H = scale[:, None] * (M.T @ M / 15 + np.eye(15)) * scale[None, :]
+        pr["prior_H"].append(((H + H.T) / 2).reshape(225))
+        pre.append(synth_ba.preintegrate(tp, t))
+    for k, v in pr.items():
+        b[k] = np.array(v, np.float64)
+    b["preint"] = np.stack(pre).astype(np.float32)
+    # Frame::mpPrevFrame's vertices: the prior's state through the float setters
+    for k in ("Rwb", "twb", "vel", "bg", "ba"):
+        b["kf_" + k] = b["prior_" + k].astype(np.float32).astype(np.float64)
+    return b
+
+
 STATE_KEYS = ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba")
 INPUT_KEYS = ("kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba", "preint", "mono_start", "mono_cam", "mono_kp",
               "mono_obs", "mono_inv_sigma2", "mono_xw", "mono_close", "stereo_start", "stereo_cam", "stereo_kp",
@@ -131,13 +177,24 @@ def as_pose_struct(batch, struct_cls, arrays):
     return s, keep
 
 
+def as_prior_struct(struct_cls, arrays):
+    """Fill an omv_pose_prior from `arrays` (PRIOR_KEYS -> numpy or torch device arrays)."""
+    import ctypes
+    s = struct_cls()
+    for k in PRIOR_KEYS:
+        a = arrays[k]
+        p = a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data
+        setattr(s, k[6:] if k.startswith("prior_") else k, ctypes.c_void_p(p))
+    return s
+
+
 def tile_batch(b, F):
     """Repeat a generated batch's frames (with their edges) up to F frames (cheap large batches)."""
     n0 = int(b["n_frames"])
     out = dict(b)
     fr = [f % n0 for f in range(F)]
     for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba", "preint",
-              "true_Rwb", "true_twb", "true_vel"):
+              "true_Rwb", "true_twb", "true_vel", "t") + tuple(k for k in PRIOR_KEYS if k in b):
         out[k] = np.ascontiguousarray(np.asarray(b[k])[fr])
     for kind in ("mono", "stereo"):
         st = b[f"{kind}_start"]

@@ -189,6 +189,7 @@ M3 rightJ(const V3 &v) {
 struct Preint {
     float dR[9], dV[3], dP[3], JRg[9], JVg[9], JVa[9], JPg[9], JPa[9], b[6], dT, C[225];
 };
+constexpr size_t kPreintC = offsetof(Preint, C) / sizeof(float);   // C's offset in an OMV_PREINT_FLOATS record
 void f33mul(const float *a, const float *b, float *r) {
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
@@ -1305,6 +1306,8 @@ struct PoseProblem {
     }
 };
 
+void load_pose_frame(const omv_pose_batch *b, int f, const float *C_rw, PoseProblem &P);
+
 }  // namespace
 
 extern "C" {
@@ -1314,56 +1317,8 @@ int oracle_pose_inertial_last_kf(const omv_pose_batch *b, int f, int rec_init, u
                                  double *Hout) {
     PoseProblem P;
     const int C = b->n_cams;
-    P.C = C, P.cam = b->cam, P.bf = (double)b->bf;
-    for (int c = 0; c < C; ++c) {
-        M3 a, r;
-        std::memcpy(a.m, b->Rcb + 9 * c, 72);
-        std::memcpy(r.m, b->Rbc + 9 * c, 72);
-        P.Rcb.push_back(a), P.Rbc.push_back(r);
-        P.tcb.push_back(V3{{b->tcb[3 * c], b->tcb[3 * c + 1], b->tcb[3 * c + 2]}});
-        P.tbc.push_back(V3{{b->tbc[3 * c], b->tbc[3 * c + 1], b->tbc[3 * c + 2]}});
-    }
-    auto v3 = [](const double *p) { return V3{{p[0], p[1], p[2]}}; };
-    std::memcpy(P.Rwb.m, b->Rwb + 9 * f, 72);
-    P.twb = v3(b->twb + 3 * f), P.v = v3(b->vel + 3 * f), P.bg = v3(b->bg + 3 * f), P.ba = v3(b->ba + 3 * f);
-    P.Rcw.resize(C), P.tcw.resize(C);
-    for (int c = 0; c < C; ++c) {
-        std::memcpy(P.Rcw[c].m, b->Rcw + 9 * ((size_t)f * C + c), 72);
-        P.tcw[c] = v3(b->tcw + 3 * ((size_t)f * C + c));
-    }
-    std::memcpy(P.kRwb.m, b->kf_Rwb + 9 * f, 72);
-    P.ktwb = v3(b->kf_twb + 3 * f), P.kv = v3(b->kf_vel + 3 * f), P.kbg = v3(b->kf_bg + 3 * f),
-    P.kba = v3(b->kf_ba + 3 * f);
-    std::memcpy(&P.pre, b->preint + (size_t)f * OMV_PREINT_FLOATS, sizeof(float) * OMV_PREINT_FLOATS);
-    P.info9 = inertial_info(P.pre);
-    {
-        M3 g, a;
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) {
-                g(r, c) = (double)P.pre.C[(9 + r) * 15 + 9 + c];
-                a(r, c) = (double)P.pre.C[(12 + r) * 15 + 12 + c];
-            }
-        P.infoG = inv3(g), P.infoA = inv3(a);
-    }
-    for (int e = b->mono_start[f]; e < b->mono_start[f + 1]; ++e) {
-        PoseEdge q;
-        q.cam = b->mono_cam[e], q.kp = b->mono_kp[e], q.stereo = false;
-        q.obs[0] = b->mono_obs[2 * e], q.obs[1] = b->mono_obs[2 * e + 1], q.obs[2] = 0;
-        q.w = (double)b->mono_inv_sigma2[e];
-        q.Xw = V3{{(double)b->mono_xw[3 * e], (double)b->mono_xw[3 * e + 1], (double)b->mono_xw[3 * e + 2]}};
-        q.close = b->mono_close[e] != 0;
-        P.E.push_back(q);
-    }
-    const int n_mono = (int)P.E.size();
-    for (int e = b->stereo_start[f]; e < b->stereo_start[f + 1]; ++e) {
-        PoseEdge q;
-        q.cam = b->stereo_cam[e], q.kp = b->stereo_kp[e], q.stereo = true;
-        for (int d = 0; d < 3; ++d) q.obs[d] = b->stereo_obs[3 * e + d];
-        q.w = (double)b->stereo_inv_sigma2[e];
-        q.Xw = V3{{(double)b->stereo_xw[3 * e], (double)b->stereo_xw[3 * e + 1], (double)b->stereo_xw[3 * e + 2]}};
-        q.close = false;
-        P.E.push_back(q);
-    }
+    // EdgeGyroRW / EdgeAccRW information from the same preintegration as the EdgeInertial
+    load_pose_frame(b, f, b->preint + (size_t)f * OMV_PREINT_FLOATS + kPreintC, P);
     const int n_edges = (int)P.E.size();
     for (const PoseEdge &e : P.E) kp_outlier[e.kp] = 0;   // mvbOutlier[i] = false at edge creation
     const float chi2Mono[4] = {12, 7.5, 5.991, 5.991};
@@ -1399,7 +1354,6 @@ int oracle_pose_inertial_last_kf(const omv_pose_batch *b, int f, int rec_init, u
             else ++nBad;
         }
     }
-    (void)n_mono;
     // state back
     std::memcpy(b->Rwb + 9 * f, P.Rwb.m, 72);
     std::memcpy(b->twb + 3 * f, P.twb.v, 24);
@@ -1444,6 +1398,404 @@ int oracle_pose_inertial_last_kf(const omv_pose_batch *b, int f, int rec_init, u
                 }
         }
         std::memcpy(Hout, H, sizeof H);
+    }
+    return 0;
+}
+
+}  // extern "C"
+
+// =============================================================================================
+// Optimizer::PoseInertialOptimizationLastFrame (src/Optimizer.cc:5580-6170), one frame, and the
+// ConstraintPoseImu ctor (include/G2oTypes.h:639-659).
+namespace {
+
+// Symmetric 15x15: V diag(g(w)) V^T from the cyclic-Jacobi eigen-decomposition (sym_eig).
+void sym_recompose(const std::vector<double> &w, const std::vector<double> &V, int n, double *out) {
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+            double s = 0;
+            for (int k = 0; k < n; ++k) s += V[r * n + k] * w[k] * V[c * n + k];
+            out[r * n + c] = s;
+        }
+}
+
+// ConstraintPoseImu ctor: H = (H + H) / 2 (exactly H), eigenvalues < 1e-12 zeroed.  Eigen's
+// SelfAdjointEigenSolver (tridiagonalisation + implicit QR) is restated by cyclic Jacobi.
+void constraint_pose_imu(const double *Hin, double *Hout) {
+    std::vector<double> A(225);
+    for (int q = 0; q < 225; ++q) A[q] = (Hin[q] + Hin[q]) / 2;
+    std::vector<double> w, V;
+    sym_eig(A, 15, w, V);
+    for (double &x : w)
+        if (x < 1e-12) x = 0;
+    sym_recompose(w, V, 15, Hout);
+}
+
+struct PoseLFProblem : PoseProblem {
+    // ConstraintPoseImu of the previous frame (pFp->mpcpi): EdgePriorPoseImu's measurement and information
+    M3 pRwb;
+    V3 ptwb, pv, pbg, pba;
+    std::vector<double> pH;   // 15x15
+    double dprior = 5.0;      // rkp->setDelta(5) (:5986)
+
+    // EdgePriorPoseImu::computeError (G2oTypes.cc:758-771) at the previous frame's vertices (k*)
+    void prior_error(double e[15]) const {
+        const V3 er = logSO3(mul(tr(pRwb), kRwb));
+        const V3 et = mul(tr(pRwb), sub(ktwb, ptwb));
+        const V3 ev = sub(kv, pv), eg = sub(kbg, pbg), ea = sub(kba, pba);
+        for (int q = 0; q < 3; ++q) e[q] = er[q], e[3 + q] = et[q], e[6 + q] = ev[q], e[9 + q] = eg[q], e[12 + q] = ea[q];
+    }
+    // EdgePriorPoseImu::linearizeOplus (:773-785): J 15x15 over (pose 6, v 3, bg 3, ba 3)
+    void prior_jac(double J[225]) const {
+        std::fill(J, J + 225, 0.0);
+        const M3 RR = mul(tr(pRwb), kRwb);
+        const M3 iJ = invRightJ(logSO3(RR));
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) J[r * 15 + c] = iJ(r, c), J[(3 + r) * 15 + 3 + c] = RR(r, c);
+        for (int q = 6; q < 15; ++q) J[q * 15 + q] = 1.0;
+    }
+    // EdgeInertial's 9x24 Jacobian [P1 V1 G1 A1 P2 V2] (GetHessian's column order, G2oTypes.h:445-455)
+    void inertial_j24(double Jc[9][24]) const {
+        std::vector<double> J[6];
+        inertial_jac(pre, verts(), J);
+        const int off[6] = {0, 6, 9, 12, 15, 21}, dim[6] = {6, 3, 3, 3, 6, 3};
+        for (int v = 0; v < 6; ++v)
+            for (int r = 0; r < 9; ++r)
+                for (int c = 0; c < dim[v]; ++c) Jc[r][off[v] + c] = J[v][r * dim[v] + c];
+    }
+
+    // One Gauss-Newton iteration over the 30 free states in g2o's hessian-index order (vertex ids
+    // 0-7): frame pose 0-5, v 6-8, bg 9-11, ba 12-14, previous frame pose 15-20, v 21-23, bg 24-26,
+    // ba 27-29.  Edges in creation order: visual, EdgeInertial, EdgeGyroRW, EdgeAccRW, EdgePriorPoseImu.
+    bool gn_iteration(std::vector<double> &x_prev) {
+        for (PoseEdge &e : E)
+            if (e.active) compute_error(e);
+        std::vector<double> H(900, 0.0);
+        double b[30] = {0}, rho[3];
+        auto h = [&](int i, int j) -> double & { return H[(size_t)i * 30 + j]; };
+        for (PoseEdge &e : E) {
+            if (!e.active) continue;
+            double r[3], JP[18];
+            error(e, r);
+            jac(e, JP);
+            const int nr = e.stereo ? 3 : 2;
+            double w1 = 1.0;
+            if (e.robust) {
+                Solver::huber(e.chi2, e.stereo ? dst : dmono, e.stereo ? dst * dst : dmono * dmono, rho);
+                w1 = rho[1];
+            }
+            const double w = e.w * w1;
+            double om[3];
+            for (int q = 0; q < nr; ++q) om[q] = -e.w * r[q] * w1;
+            for (int i = 0; i < 6; ++i) {
+                double t = JP[i] * om[0] + JP[6 + i] * om[1];
+                if (nr == 3) t += JP[12 + i] * om[2];
+                b[i] += t;
+                for (int j = 0; j < 6; ++j) {
+                    double hh = JP[i] * JP[j] + JP[6 + i] * JP[6 + j];
+                    if (nr == 3) hh += JP[12 + i] * JP[12 + j];
+                    h(i, j) += w * hh;
+                }
+            }
+        }
+        // EdgeInertial over all six vertex blocks: ei column c -> state index
+        {
+            double e9[9], Jc[9][24];
+            inertial_error(pre, verts(), e9);
+            inertial_j24(Jc);
+            int smap[24];
+            for (int c = 0; c < 15; ++c) smap[c] = 15 + c;    // P1 V1 G1 A1: the previous frame
+            for (int c = 15; c < 24; ++c) smap[c] = c - 15;   // P2 V2: the frame
+            double Oe[9];
+            for (int r = 0; r < 9; ++r) {
+                double t = 0;
+                for (int c = 0; c < 9; ++c) t += info9[r * 9 + c] * e9[c];
+                Oe[r] = t;
+            }
+            double OJ[9][24];
+            for (int r = 0; r < 9; ++r)
+                for (int j = 0; j < 24; ++j) {
+                    double t = 0;
+                    for (int c = 0; c < 9; ++c) t += info9[r * 9 + c] * Jc[c][j];
+                    OJ[r][j] = t;
+                }
+            for (int i = 0; i < 24; ++i) {
+                double t = 0;
+                for (int r = 0; r < 9; ++r) t += Jc[r][i] * Oe[r];
+                b[smap[i]] -= t;
+                for (int j = 0; j < 24; ++j) {
+                    double hh = 0;
+                    for (int r = 0; r < 9; ++r) hh += Jc[r][i] * OJ[r][j];
+                    h(smap[i], smap[j]) += hh;
+                }
+            }
+        }
+        // EdgeGyroRW / EdgeAccRW (G2oTypes.h:567-633): e = b_frame - b_prev, J_prev = -I, J_frame = I
+        for (int which = 0; which < 2; ++which) {
+            const V3 er = which ? sub(ba, kba) : sub(bg, kbg);
+            const M3 &Iw = which ? infoA : infoG;
+            const int of = which ? 12 : 9, op = which ? 27 : 24;
+            const V3 Oe = mul(Iw, er);
+            for (int i = 0; i < 3; ++i) {
+                b[op + i] += Oe[i];
+                b[of + i] -= Oe[i];
+                for (int j = 0; j < 3; ++j) {
+                    h(op + i, op + j) += Iw(i, j);
+                    h(op + i, of + j) -= Iw(i, j);
+                    h(of + i, op + j) -= Iw(i, j);
+                    h(of + i, of + j) += Iw(i, j);
+                }
+            }
+        }
+        // EdgePriorPoseImu, Huber(5) on chi2 = e^T H e (base_multi_edge.hpp: omega_r = -rho' H e,
+        // weighted information rho' H)
+        {
+            double e[15], J[225], Oe[15];
+            prior_error(e);
+            prior_jac(J);
+            double chi2 = 0;
+            for (int k = 0; k < 15; ++k) {
+                double t = 0;
+                for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * e[l];
+                Oe[k] = t;
+            }
+            for (int k = 0; k < 15; ++k) chi2 += e[k] * Oe[k];
+            Solver::huber(chi2, dprior, dprior * dprior, rho);
+            const double w1 = rho[1];
+            double WJ[225];
+            for (int k = 0; k < 15; ++k)
+                for (int j = 0; j < 15; ++j) {
+                    double t = 0;
+                    for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * J[l * 15 + j];
+                    WJ[k * 15 + j] = w1 * t;
+                }
+            for (int i = 0; i < 15; ++i) {
+                double t = 0;
+                for (int k = 0; k < 15; ++k) t += J[k * 15 + i] * (-Oe[k] * w1);
+                b[15 + i] += t;
+                for (int j = 0; j < 15; ++j) {
+                    double hh = 0;
+                    for (int k = 0; k < 15; ++k) hh += J[k * 15 + i] * WJ[k * 15 + j];
+                    h(15 + i, 15 + j) += hh;
+                }
+            }
+        }
+        double x[30];
+        const bool ok = ldlt_pivot_solve(H, 30, b, x);
+        if (!ok)
+            for (int i = 0; i < 30; ++i) x[i] = x_prev[i];
+        for (int i = 0; i < 30; ++i) x_prev[i] = x[i];
+        // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235) on both frames
+        twb = add(twb, mul(Rwb, V3{{x[3], x[4], x[5]}}));
+        Rwb = mul(Rwb, expSO3(x[0], x[1], x[2]));
+        const M3 Rbw = tr(Rwb);
+        const V3 tbw = scale(mul(Rbw, twb), -1.0);
+        for (int c = 0; c < C; ++c) {
+            Rcw[c] = mul(Rcb[c], Rbw);
+            tcw[c] = add(mul(Rcb[c], tbw), tcb[c]);
+        }
+        for (int q = 0; q < 3; ++q) v[q] += x[6 + q], bg[q] += x[9 + q], ba[q] += x[12 + q];
+        ktwb = add(ktwb, mul(kRwb, V3{{x[18], x[19], x[20]}}));
+        kRwb = mul(kRwb, expSO3(x[15], x[16], x[17]));
+        for (int q = 0; q < 3; ++q) kv[q] += x[21 + q], kbg[q] += x[24 + q], kba[q] += x[27 + q];
+        return ok;
+    }
+};
+
+// Load one frame of an omv_pose_batch (frame vertices, the k* vertices, rig, preintegration, visual edges
+// in creation order: EdgeMonoOnlyPose, then EdgeStereoOnlyPose).  InfoG / InfoA from `C_rw`.
+void load_pose_frame(const omv_pose_batch *b, int f, const float *C_rw, PoseProblem &P) {
+    const int C = b->n_cams;
+    P.C = C, P.cam = b->cam, P.bf = (double)b->bf;
+    for (int c = 0; c < C; ++c) {
+        M3 a, r;
+        std::memcpy(a.m, b->Rcb + 9 * c, 72);
+        std::memcpy(r.m, b->Rbc + 9 * c, 72);
+        P.Rcb.push_back(a), P.Rbc.push_back(r);
+        P.tcb.push_back(V3{{b->tcb[3 * c], b->tcb[3 * c + 1], b->tcb[3 * c + 2]}});
+        P.tbc.push_back(V3{{b->tbc[3 * c], b->tbc[3 * c + 1], b->tbc[3 * c + 2]}});
+    }
+    auto v3 = [](const double *p) { return V3{{p[0], p[1], p[2]}}; };
+    std::memcpy(P.Rwb.m, b->Rwb + 9 * f, 72);
+    P.twb = v3(b->twb + 3 * f), P.v = v3(b->vel + 3 * f), P.bg = v3(b->bg + 3 * f), P.ba = v3(b->ba + 3 * f);
+    P.Rcw.resize(C), P.tcw.resize(C);
+    for (int c = 0; c < C; ++c) {
+        std::memcpy(P.Rcw[c].m, b->Rcw + 9 * ((size_t)f * C + c), 72);
+        P.tcw[c] = v3(b->tcw + 3 * ((size_t)f * C + c));
+    }
+    std::memcpy(P.kRwb.m, b->kf_Rwb + 9 * f, 72);
+    P.ktwb = v3(b->kf_twb + 3 * f), P.kv = v3(b->kf_vel + 3 * f), P.kbg = v3(b->kf_bg + 3 * f),
+    P.kba = v3(b->kf_ba + 3 * f);
+    std::memcpy(&P.pre, b->preint + (size_t)f * OMV_PREINT_FLOATS, sizeof(float) * OMV_PREINT_FLOATS);
+    P.info9 = inertial_info(P.pre);
+    {
+        M3 g, a;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+                g(r, c) = (double)C_rw[(9 + r) * 15 + 9 + c];
+                a(r, c) = (double)C_rw[(12 + r) * 15 + 12 + c];
+            }
+        P.infoG = inv3(g), P.infoA = inv3(a);
+    }
+    for (int e = b->mono_start[f]; e < b->mono_start[f + 1]; ++e) {
+        PoseEdge q;
+        q.cam = b->mono_cam[e], q.kp = b->mono_kp[e], q.stereo = false;
+        q.obs[0] = b->mono_obs[2 * e], q.obs[1] = b->mono_obs[2 * e + 1], q.obs[2] = 0;
+        q.w = (double)b->mono_inv_sigma2[e];
+        q.Xw = V3{{(double)b->mono_xw[3 * e], (double)b->mono_xw[3 * e + 1], (double)b->mono_xw[3 * e + 2]}};
+        q.close = b->mono_close[e] != 0;
+        P.E.push_back(q);
+    }
+    for (int e = b->stereo_start[f]; e < b->stereo_start[f + 1]; ++e) {
+        PoseEdge q;
+        q.cam = b->stereo_cam[e], q.kp = b->stereo_kp[e], q.stereo = true;
+        for (int d = 0; d < 3; ++d) q.obs[d] = b->stereo_obs[3 * e + d];
+        q.w = (double)b->stereo_inv_sigma2[e];
+        q.Xw = V3{{(double)b->stereo_xw[3 * e], (double)b->stereo_xw[3 * e + 1], (double)b->stereo_xw[3 * e + 2]}};
+        q.close = false;
+        P.E.push_back(q);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_pose_constraint(const double *Hin, double *Hout) {
+    constraint_pose_imu(Hin, Hout);
+    return 0;
+}
+
+// One frame of the batch (host pointers in `b` / `pr`); kp_outlier [kp_cap], H [225] (may be NULL):
+// the frame's block of Marginalize(H, 0, 14), before the ConstraintPoseImu ctor.
+int oracle_pose_inertial_last_frame(const omv_pose_batch *b, const omv_pose_prior *pr, int f, int rec_init,
+                                    uint8_t *kp_outlier, int32_t *n_good, double *Hout) {
+    PoseLFProblem P;
+    load_pose_frame(b, f, pr->preint_kf + (size_t)f * OMV_PREINT_FLOATS + kPreintC, P);
+    std::memcpy(P.pRwb.m, pr->Rwb + 9 * f, 72);
+    for (int q = 0; q < 3; ++q) {
+        P.ptwb[q] = pr->twb[3 * f + q], P.pv[q] = pr->vel[3 * f + q];
+        P.pbg[q] = pr->bg[3 * f + q], P.pba[q] = pr->ba[3 * f + q];
+    }
+    P.pH.assign(pr->H + 225 * (size_t)f, pr->H + 225 * (size_t)f + 225);
+    const int n_edges = (int)P.E.size();
+    for (const PoseEdge &e : P.E) kp_outlier[e.kp] = 0;   // mvbOutlier[i] = false at edge creation
+    const float chi2Mono[4] = {5.991f, 5.991f, 5.991f, 5.991f};
+    const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
+    int nBad = 0, nInliers = 0;
+    std::vector<double> x_prev(30, 0.0);
+    for (int it = 0; it < 4; ++it) {
+        for (int i = 0; i < 10; ++i)   // optimize(its[it]): stops after a failed solve
+            if (!P.gn_iteration(x_prev)) break;
+        nBad = 0, nInliers = 0;
+        const float chi2close = 1.5f * chi2Mono[it];
+        for (int q = 0; q < n_edges; ++q) {   // mono loop, then stereo loop (:6014-6064)
+            PoseEdge &e = P.E[q];
+            if (kp_outlier[e.kp]) P.compute_error(e);
+            const float chi2 = (float)e.chi2;
+            bool out;
+            if (!e.stereo) out = (chi2 > chi2Mono[it] && !e.close) || (e.close && chi2 > chi2close) || !P.depth_positive(e);
+            else out = chi2 > chi2Stereo[it];
+            kp_outlier[e.kp] = out ? 1 : 0;
+            e.active = !out;
+            if (out) ++nBad;
+            else ++nInliers;
+            if (it == 2) e.robust = false;
+        }
+        if (n_edges + 4 < 10) break;   // optimizer.edges().size() < 10 (ei, egr, ear, ep)
+    }
+    if (nInliers < 30 && !rec_init) {   // :6074-6098
+        nBad = 0;
+        for (int q = 0; q < n_edges; ++q) {
+            PoseEdge &e = P.E[q];
+            P.compute_error(e);
+            if (e.chi2 < (e.stereo ? 24.f : 18.f)) kp_outlier[e.kp] = 0;
+            else ++nBad;
+        }
+    }
+    const int C = b->n_cams;
+    std::memcpy(b->Rwb + 9 * f, P.Rwb.m, 72);
+    std::memcpy(b->twb + 3 * f, P.twb.v, 24);
+    std::memcpy(b->vel + 3 * f, P.v.v, 24);
+    std::memcpy(b->bg + 3 * f, P.bg.v, 24);
+    std::memcpy(b->ba + 3 * f, P.ba.v, 24);
+    for (int c = 0; c < C; ++c) {
+        std::memcpy(b->Rcw + 9 * ((size_t)f * C + c), P.Rcw[c].m, 72);
+        std::memcpy(b->tcw + 3 * ((size_t)f * C + c), P.tcw[c].v, 24);
+    }
+    *n_good = n_edges - nBad;
+    if (Hout) {   // :6112-6156 in the reference's layout: previous frame 0-14, frame 15-29
+        std::vector<double> H(900, 0.0);
+        auto h = [&](int i, int j) -> double & { return H[(size_t)i * 30 + j]; };
+        double Jc[9][24];
+        P.inertial_j24(Jc);
+        for (int i = 0; i < 24; ++i)   // ei->GetHessian(): J^T Info J
+            for (int j = 0; j < 24; ++j) {
+                double s = 0;
+                for (int r = 0; r < 9; ++r) {
+                    double oj = 0;
+                    for (int c = 0; c < 9; ++c) oj += P.info9[r * 9 + c] * Jc[c][j];
+                    s += Jc[r][i] * oj;
+                }
+                h(i, j) += s;
+            }
+        for (int which = 0; which < 2; ++which) {   // egr / ear->GetHessian(): [[I, -I], [-I, I]] blocks
+            const M3 &Iw = which ? P.infoA : P.infoG;
+            const int o1 = which ? 12 : 9, o2 = which ? 27 : 24;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    h(o1 + i, o1 + j) += Iw(i, j);
+                    h(o1 + i, o2 + j) += -Iw(i, j);
+                    h(o2 + i, o1 + j) += -Iw(i, j);
+                    h(o2 + i, o2 + j) += Iw(i, j);
+                }
+        }
+        {   // ep->GetHessian(): J^T H_prior J (no robust weight)
+            double J[225];
+            P.prior_jac(J);
+            for (int i = 0; i < 15; ++i)
+                for (int j = 0; j < 15; ++j) {
+                    double s = 0;
+                    for (int k = 0; k < 15; ++k) {
+                        double oj = 0;
+                        for (int l = 0; l < 15; ++l) oj += P.pH[k * 15 + l] * J[l * 15 + j];
+                        s += J[k * 15 + i] * oj;
+                    }
+                    h(i, j) += s;
+                }
+        }
+        for (const PoseEdge &e : P.E) {   // inlier visual edges' GetHessian()
+            if (kp_outlier[e.kp]) continue;
+            double JP[18];
+            P.jac(e, JP);
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) {
+                    double s = JP[i] * JP[j] + JP[6 + i] * JP[6 + j];
+                    if (e.stereo) s += JP[12 + i] * JP[12 + j];
+                    h(15 + i, 15 + j) += e.w * s;
+                }
+        }
+        // Marginalize(H, 0, 14): Hff - Hfp pinv(Hpp) Hpf; JacobiSVD's pseudo-inverse of the symmetric Hpp
+        // (singular values = |eigenvalues|, U = V sign) is V diag(1/w) V^T over |w| > 1e-6
+        std::vector<double> A(225), w, V;
+        for (int i = 0; i < 15; ++i)
+            for (int j = 0; j < 15; ++j) A[i * 15 + j] = h(i, j);
+        sym_eig(A, 15, w, V);
+        for (double &x : w) x = std::fabs(x) > 1e-6 ? 1.0 / x : 0.0;
+        double inv[225], T[225];
+        sym_recompose(w, V, 15, inv);
+        for (int i = 0; i < 15; ++i)
+            for (int j = 0; j < 15; ++j) {
+                double s = 0;
+                for (int k = 0; k < 15; ++k) s += h(15 + i, k) * inv[k * 15 + j];
+                T[i * 15 + j] = s;
+            }
+        for (int i = 0; i < 15; ++i)
+            for (int j = 0; j < 15; ++j) {
+                double s = 0;
+                for (int k = 0; k < 15; ++k) s += T[i * 15 + k] * h(k, 15 + j);
+                Hout[i * 15 + j] = h(15 + i, 15 + j) - s;
+            }
     }
     return 0;
 }

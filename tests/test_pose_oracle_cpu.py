@@ -50,6 +50,68 @@ def test_few_inliers_recover_pass(oracle):
     assert (k_rec[:, :40].sum(1) <= k_no[:, :40].sum(1)).all()
 
 
+@pytest.fixture(scope="module")
+def lf_batch():
+    return synth_pose.make_last_frame_batch(n_frames=6, n_pts=300, seed=1, outlier_frac=0.1)
+
+
+def test_last_frame_recovers_state_and_flags_outliers(lf_batch, oracle):
+    """PoseInertialOptimizationLastFrame (Optimizer.cc:5580-6170): pose / velocity pulled to the truth,
+    planted outliers found, the return value nInitialCorrespondences - nBad."""
+    b = lf_batch
+    st, kpo, n_good, _ = oracle.pose_last_frame(b)
+    for f in range(b["n_frames"]):
+        assert _rot_deg(b["Rwb"][f], b["true_Rwb"][f]) > 0.4
+        assert _rot_deg(st["Rwb"][f], b["true_Rwb"][f]) < 0.05
+        assert np.linalg.norm(st["twb"][f] - b["true_twb"][f]) < 1e-2
+        m0, m1 = b["mono_start"][f], b["mono_start"][f + 1]
+        truth = b["mono_is_outlier"][m0:m1]
+        flags = kpo[f, b["mono_kp"][m0:m1]].astype(bool)
+        assert (flags & truth).sum() >= 0.9 * truth.sum()
+        assert (flags & ~truth).sum() <= 0.05 * (~truth).sum()
+        assert n_good[f] == (m1 - m0) - flags.sum()
+
+
+def test_last_frame_prior_pulls_previous_frame(oracle):
+    """A stiffer EdgePriorPoseImu makes the frame's estimate follow the prior more: with the prior
+    information scaled up 1e4 the result moves towards what the prior implies, and the marginal
+    Hessian (the next frame's prior) grows."""
+    b = synth_pose.make_last_frame_batch(n_frames=3, n_pts=60, seed=8, outlier_frac=0.0)
+    _, _, _, H1 = oracle.pose_last_frame(b)
+    b2 = dict(b)
+    b2["prior_H"] = b["prior_H"] * 1e4
+    _, _, _, H2 = oracle.pose_last_frame(b2)
+    for f in range(3):
+        assert np.trace(H2[f].reshape(15, 15)) > np.trace(H1[f].reshape(15, 15))
+
+
+def test_marginalised_hessian_and_constraint(lf_batch, oracle):
+    """Marginalize(H, 0, 14) is a Schur complement of a PSD matrix (PSD, symmetric to rounding); the
+    ConstraintPoseImu ctor leaves a PSD matrix unchanged to rounding and zeroes negative eigenvalues."""
+    _, _, _, H = oracle.pose_last_frame(lf_batch)
+    for f in range(lf_batch["n_frames"]):
+        h = H[f].reshape(15, 15)
+        assert np.abs(h - h.T).max() <= 1e-7 * np.abs(h).max()
+        assert np.linalg.eigvalsh((h + h.T) / 2).min() > 0
+    Hc = oracle.pose_constraint(H)
+    assert np.abs(Hc - H).max() <= 1e-7 * np.abs(H).max()
+    rng = np.random.default_rng(3)
+    M = rng.normal(0, 1, (15, 15))
+    S = M + M.T
+    P = oracle.pose_constraint(S.reshape(1, 225))[0].reshape(15, 15)
+    w, V = np.linalg.eigh(S)
+    ref = (V * np.where(w < 1e-12, 0, w)) @ V.T
+    assert np.abs(P - ref).max() < 1e-10
+
+
+def test_last_frame_few_edges_stop_after_first_round(oracle):
+    """optimizer.edges().size() < 10 (:6069): 5 visual edges + 4 break after the first round, so the
+    round-0 threshold decides (all rounds use 5.991 here; the recover pass then re-admits)."""
+    b = synth_pose.make_last_frame_batch(n_frames=2, n_pts=5, seed=5, outlier_frac=0.0)
+    st, kpo, n_good, _ = oracle.pose_last_frame(b)
+    assert (n_good <= 5).all() and (n_good >= 0).all()
+
+
 def test_stereo_edges_share_the_keypoint_flag(oracle):
     b = synth_pose.make_pose_batch(n_frames=3, n_pts=200, seed=4, outlier_frac=0.1, stereo_frac=0.5)
     assert len(b["stereo_cam"]) > 100
