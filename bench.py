@@ -205,23 +205,26 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
     }
 
 
-def pose_leg(batch, cpu_batch, reps, dev):
-    """PoseInertialOptimizationLastKeyFrame (Optimizer.cc:5021-5578) on a batch of tracked frames: one call =
-    every frame's 4 rounds x 10 Gauss-Newton iterations + outlier passes + marginal Hessian; value = frames/s
-    (state reset by a device copy outside the timed region)."""
+def pose_leg(batch, cpu_batch, reps, dev, last_frame=False):
+    """PoseInertialOptimizationLastKeyFrame (Optimizer.cc:5021-5578) or, with last_frame,
+    PoseInertialOptimizationLastFrame (:5580-6170, the previous frame's vertices free + EdgePriorPoseImu +
+    Marginalize) on a batch of tracked frames: one call = every frame's 4 rounds x 10 Gauss-Newton
+    iterations + outlier passes + marginal Hessian; value = frames/s (state reset by a device copy outside
+    the timed region)."""
     import torch
     from openmavis_amd import synth_pose
     from openmavis_amd.optimizer import PoseInertialOptimizer
     F = int(batch["n_frames"])
     init = {k: torch.tensor(np.asarray(batch[k], np.float64), device=dev) for k in synth_pose.STATE_KEYS}
     arrays = {k: v.clone() for k, v in init.items()}
-    for k in synth_pose.INPUT_KEYS:
+    for k in synth_pose.INPUT_KEYS + (synth_pose.PRIOR_KEYS if last_frame else ()):
         arrays[k] = torch.from_numpy(np.ascontiguousarray(batch[k])).to(dev)
     kpo = torch.zeros((F, int(batch["kp_cap"])), dtype=torch.uint8, device=dev)
     H = torch.zeros((F, 225), dtype=torch.float64, device=dev)
     opt = PoseInertialOptimizer(max_frames=F, max_edges=max(len(batch["mono_cam"]), len(batch["stereo_cam"]), 1))
+    run = opt.PoseInertialOptimizationLastFrame if last_frame else opt.PoseInertialOptimizationLastKeyFrame
     for _ in range(2):
-        opt.PoseInertialOptimizationLastKeyFrame(batch, arrays, kpo, H)
+        run(batch, arrays, kpo, H)
     torch.cuda.synchronize(dev)
     total = 0.0
     for _ in range(reps):
@@ -229,10 +232,11 @@ def pose_leg(batch, cpu_batch, reps, dev):
             arrays[k].copy_(init[k])
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        opt.PoseInertialOptimizationLastKeyFrame(batch, arrays, kpo, H)
+        run(batch, arrays, kpo, H)
         torch.cuda.synchronize(dev)
         total += time.perf_counter() - t0
-    out = {"metric": "PoseInertialOptimizationLastKeyFrame frames/s", "value": round(F * reps / total, 1),
+    name = "PoseInertialOptimizationLastFrame" if last_frame else "PoseInertialOptimizationLastKeyFrame"
+    out = {"metric": f"{name} frames/s", "value": round(F * reps / total, 1),
            "unit": "frames/s", "ms_per_batch": round(total / reps * 1e3, 3), "frames_per_batch": F,
            "edges_per_frame": round(len(batch["mono_cam"]) / F, 1), "dtype": "f64"}
     if cpu_batch is not None:
@@ -241,7 +245,7 @@ def pose_leg(batch, cpu_batch, reps, dev):
         t0 = time.perf_counter()
         done = 0
         while done == 0 or time.perf_counter() - t0 < 2.0:   # a ~2 s sample
-            oracle.pose_last_kf(cpu_batch)
+            (oracle.pose_last_frame if last_frame else oracle.pose_last_kf)(cpu_batch)
             done += int(cpu_batch["n_frames"])
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(done / dt, 1), "unit": "frames/s", "cores": 1, "kind": "port",
@@ -336,11 +340,13 @@ def main():
     if args.lba_steps > 0:
         from openmavis_amd import synth_ba
         lba_prob = synth_ba.make_lba_problem(seed=5)   # configs[4] window (same on every rank)
-    pose_batch = pose_cpu = None
+    pose_batch = pose_cpu = lf_batch = lf_cpu = None
     if args.pose_frames > 0:
         from openmavis_amd import synth_pose
         pose_cpu = synth_pose.make_pose_batch(n_frames=32, n_pts=1000, seed=1, outlier_frac=0.1)
         pose_batch = synth_pose.tile_batch(pose_cpu, args.pose_frames)
+        lf_cpu = synth_pose.make_last_frame_batch(n_frames=32, n_pts=1000, seed=1, outlier_frac=0.1)
+        lf_batch = synth_pose.tile_batch(lf_cpu, args.pose_frames)
     tri_pairs = None
     if args.tri_pairs > 0:
         from openmavis_amd import synth_tri
@@ -472,6 +478,8 @@ def main():
     lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world, args.lba_shard) if lba_prob is not None else None
     pose = pose_leg(pose_batch, pose_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev) \
         if pose_batch is not None else None
+    pose_lf = pose_leg(lf_batch, lf_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev, last_frame=True) \
+        if lf_batch is not None else None
     tri = tri_leg(tri_pairs, args.tri_pairs, 10, dev) if tri_pairs is not None else None
 
     if rank != 0:
@@ -546,6 +554,7 @@ def main():
         "cpu_baseline": cpu,
         "local_ba": lba,
         "pose_inertial": pose,
+        "pose_inertial_last_frame": pose_lf,
         "triangulation": tri,
     }
     print(json.dumps(out))
