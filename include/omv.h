@@ -209,6 +209,79 @@ omv_status omv_matcher_search_last_frame(omv_matcher *m, int n_frames, const omv
                                          int32_t *kp_to_mp, int32_t *n_matches, void *stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Keyframe-side projection searches: map points projected into one camera block of a
+ * keyframe (or frame) of the last omv_matcher_assign_grid batch and matched by Hamming distance in the
+ * GetFeaturesInArea window.  One call runs a list of jobs; a job = (keyframe, camera block, pose, a run
+ * of map points).  Modes:
+ *   OMV_KF_FUSE       ORBmatcher::Fuse(KF, vpMapPoints, th, cameraID) (src/ORBmatcher.cc:1458-1647):
+ *                     depth / IsInImage / distance-invariance / 60-degree viewing tests, PredictScale,
+ *                     KeyFrame::GetFeaturesInArea (src/KeyFrame.cc:771-834), levels [pred-1, pred], the
+ *                     chi2 reprojection gate (stereo 7.8 on block 0 where mvuRight >= 0, else 5.99), best
+ *                     by (distance, window order) from 256, accepted at <= TH_LOW.  The caller applies
+ *                     the Replace / AddObservation of each accepted (point, keypoint) in list order.
+ *   OMV_KF_FUSE_SIM3  ORBmatcher::Fuse(KF, Scw, vpPoints, th, vpReplacePoint) (:1649-1769), one job per
+ *                     camera block: no distance / viewing tests, no gate, best from INT_MAX.
+ *   OMV_KF_SBP_SIM3   ORBmatcher::SearchByProjection(KF, Siw, vpPoints[, vpPointsKFs], vpMatched, th,
+ *                     ratioHamming, cameraID) (:668-776, :778-893): keypoints matched before (kp_match
+ *                     >= 0, initially and by earlier points of the job) are skipped, accepted at
+ *                     <= TH_LOW * ratioHamming and claimed in kp_match.
+ *   OMV_KF_SBP_FRAME  ORBmatcher::SearchByProjection(Frame&, KF, sAlreadyFound, th, ORBdist)
+ *                     (:2415-2535): the "keyframe" of the job is the current frame (inclusive mnMinX..mnMaxX
+ *                     bounds, Frame::GetFeaturesInArea with levels [pred-1, pred+1]), no viewing test,
+ *                     claims in kp_match, accepted at <= ORBdist; with check_ori the rotation-histogram
+ *                     filter (ComputeThreeMaxima, :2537-2573) un-claims matches outside the three top bins.
+ * Jobs on the same keyframe / frame run in job order (claims carry over), others in parallel.  The
+ * caller leaves out of a job's list the points the reference skips before projecting (isBad(),
+ * IsInKeyFrame(pKF), spAlreadyFound / sAlreadyFound) and passes each job's camera pose as the
+ * reference composes it (GetPose / GetRightPose / ..., SE3f(Siw.rotationMatrix(), Siw.translation() /
+ * Siw.scale()), GetRelativePoseTrl() * Tlw, CurrentFrame.GetPose()).
+ * ---------------------------------------------------------------------------------------------- */
+enum { OMV_KF_FUSE = 0, OMV_KF_FUSE_SIM3 = 1, OMV_KF_SBP_SIM3 = 2, OMV_KF_SBP_FRAME = 3 };
+
+typedef struct omv_kf_search_job {
+    int kf;                /* keyframe / frame index in the assign_grid batch */
+    int cam;               /* cameraID: the camera block searched */
+    omv_se3f Tcw;          /* world -> camera block `cam` */
+    float Ow[3];           /* that camera's centre (the distance / viewing tests) */
+    int mp_start, mp_count;   /* the job's entries [mp_start, mp_start + mp_count) of mp_list; jobs tile
+                                 mp_list in order */
+} omv_kf_search_job;
+
+typedef struct omv_kf_mps {        /* device map-point table */
+    const float *pos;              /* [M][3] GetWorldPos()                                           */
+    const float *normal;           /* [M][3] GetNormal()                                             */
+    const float *min_dist;         /* [M] mfMinDistance (GetMinDistanceInvariance = 0.8f * it)      */
+    const float *max_dist;         /* [M] mfMaxDistance (GetMaxDistanceInvariance = 1.2f * it)      */
+    const uint8_t *desc;           /* [M][32] GetDescriptor()                                        */
+} omv_kf_mps;
+
+typedef struct omv_kf_search_params {
+    int mode;                      /* OMV_KF_*                                                       */
+    float th;                      /* window radius factor (th * mvScaleFactors[pred])                */
+    float max_dist;                /* acceptance: best <= max_dist (TH_LOW, TH_LOW * ratio, ORBdist) */
+    float bf;                      /* KeyFrame::mbf (OMV_KF_FUSE stereo gate)                         */
+    const float *uright;           /* device [n_kf][kp_cap] mvuRight of block 0 (OMV_KF_FUSE) or NULL */
+    float inv_level_sigma2[16];    /* mvInvLevelSigma2                                               */
+    float log_scale_factor;        /* mfLogScaleFactor                                               */
+    int n_levels;                  /* mnScaleLevels                                                  */
+    float cams[8][8];              /* KannalaBrandt8 parameters per camera block                     */
+    int check_ori;                 /* OMV_KF_SBP_FRAME: mbCheckOrientation                           */
+    const float *mp_angle;         /* device [n_entries]: pKF->mvKeysUn[i].angle per entry (check_ori) */
+} omv_kf_search_params;
+
+/* jobs: host [n_jobs] (validated, then copied to the handle); mp_list: device [n_entries] map-point table rows; kp_match: device
+ * [n_kf][n_cams * kp_cap] slot claims (-1 free, else the claiming table row; in/out, claim modes only,
+ * may be NULL otherwise); best_idx / best_dist: device [n_entries] — the chosen keypoint as the
+ * keyframe's N-index (camera offset + index in its block; -1 if the point was rejected or nothing
+ * qualified) and its distance (Fuse modes: the scan's best even above the threshold; claim modes: the
+ * accepted match only); n_matches: device [n_jobs] the reference's return value per job. */
+omv_status omv_matcher_search_kf(omv_matcher *m, int n_kf, const omv_frame_geom *geom, const omv_kp *kps,
+                                 const uint8_t *desc, const int *n_kp, int n_jobs, const omv_kf_search_job *jobs,
+                                 int n_entries, const int32_t *mp_list, const omv_kf_mps *mps,
+                                 const omv_kf_search_params *p, int32_t *kp_match, int32_t *best_idx,
+                                 int32_t *best_dist, int32_t *n_matches, void *stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Frame::isInFrustum (src/Frame.cc:736-826; the multi-camera isInFrustumChecks, :1529-1653) with
  * MapPoint::PredictScale (src/MapPoint.cc:624-637) and KannalaBrandt8::project(Vector3f)
  * (src/CameraModels/KannalaBrandt8.cpp:48-67), for every local map point of every frame — the loop

@@ -61,6 +61,28 @@ class SE3f(ctypes.Structure):
     _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3)]
 
 
+class KfSearchJob(ctypes.Structure):
+    """omv_kf_search_job (include/omv.h)."""
+    _fields_ = [("kf", ctypes.c_int), ("cam", ctypes.c_int), ("Tcw", SE3f), ("Ow", ctypes.c_float * 3),
+                ("mp_start", ctypes.c_int), ("mp_count", ctypes.c_int)]
+
+
+class KfMps(ctypes.Structure):
+    """omv_kf_mps (include/omv.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "normal", "min_dist", "max_dist", "desc")]
+
+
+class KfSearchParams(ctypes.Structure):
+    """omv_kf_search_params (include/omv.h)."""
+    _fields_ = [("mode", ctypes.c_int), ("th", ctypes.c_float), ("max_dist", ctypes.c_float), ("bf", ctypes.c_float),
+                ("uright", ctypes.c_void_p), ("inv_level_sigma2", ctypes.c_float * 16),
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int), ("cams", (ctypes.c_float * 8) * 8),
+                ("check_ori", ctypes.c_int), ("mp_angle", ctypes.c_void_p)]
+
+
+OMV_KF_FUSE, OMV_KF_FUSE_SIM3, OMV_KF_SBP_SIM3, OMV_KF_SBP_FRAME = 0, 1, 2, 3
+
+
 class LastFrame(ctypes.Structure):
     _fields_ = [("pos", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("valid", ctypes.c_void_p),
                 ("has_obs", ctypes.c_void_p), ("kps", ctypes.c_void_p), ("S", ctypes.c_int)]
@@ -207,6 +229,9 @@ SIGNATURES = {
     "omv_pose_inertial_last_frame": (_I, [_VP, ctypes.POINTER(PoseBatch), ctypes.POINTER(PosePrior), _I, _VP, _VP,
                                           _VP, _VP]),
     "omv_pose_constraint": (_I, [_I, _VP, _VP, _VP]),
+    "omv_matcher_search_kf": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(KfSearchJob),
+                                   _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,
+                                   _VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
     "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
                               _VP]),

@@ -1015,6 +1015,248 @@ __global__ void __launch_bounds__(256) lf_histo_kernel(const int2 *pushes, const
     if (threadIdx.x == 0) n_matches[frame] -= removed;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Keyframe-side projection searches (omv_matcher_search_kf): ORBmatcher::Fuse (both overloads,
+// ORBmatcher.cc:1458-1769), SearchByProjection(KF, Sim3, ...) (:668-893) and
+// SearchByProjection(Frame&, KF, ...) (:2415-2535).
+//   kf_cand_kernel     one thread per (job, map point): SE3f transform, float KB8 projection, the mode's
+//                      depth / bounds / distance / viewing tests, PredictScale, and the 16 best window
+//                      candidates by (distance, window order) passing the level filter, Fuse's
+//                      reprojection gate and the claims present at the call.  The Fuse modes read no
+//                      state the loop changes, so their answer is final here.
+//   kf_resolve_kernel  claim modes: one wavefront per keyframe walks its jobs and points in order; a
+//                      point takes the first of its candidates not claimed so far (ballot over the 16),
+//                      rescanning the window when all are taken and it held more; then
+//                      OMV_KF_SBP_FRAME's rotation histogram un-claims matches outside the top 3 bins.
+// Slots claimed at the call are never freed during it (the histogram only removes this call's claims),
+// so filtering them in the candidate pass is exact.
+struct KfArgs {
+    FrameArgs f;
+    const omv_kf_search_job *jobs;
+    int n_jobs, n_kf;
+    const int32_t *mp_list;
+    int n_entries;
+    omv_kf_mps mps;
+    int mode, check_ori;
+    float th, max_dist, bf;
+    const float *uright;
+    float invs2[16], log_scale;
+    int n_levels;
+    float cams[kMaxCams][8];
+    const float *mp_angle;
+    int32_t *kp_match, *best_idx, *best_dist, *n_matches;
+    Rec *recs;
+    int *counts;
+    float4 *geo;   // per entry: window centre x, y, radius, predicted level (bits) for rescans
+};
+
+__device__ __forceinline__ bool kf_claim_mode(int mode) { return mode == OMV_KF_SBP_SIM3 || mode == OMV_KF_SBP_FRAME; }
+
+// The job whose run of mp_list holds entry e (jobs tile mp_list in order; the last of equal starts).
+__device__ __forceinline__ int kf_job_of(const KfArgs &a, int e) {
+    int lo = 0, hi = a.n_jobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.jobs[mid].mp_start <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Level window: the KeyFrame modes filter [pred-1, pred] in their loop, OMV_KF_SBP_FRAME's
+// Frame::GetFeaturesInArea takes [pred-1, pred+1].
+__device__ __forceinline__ void kf_levels(int mode, int pred, int &minL, int &maxL) {
+    minL = pred - 1;
+    maxL = mode == OMV_KF_SBP_FRAME ? pred + 1 : pred;
+}
+
+__device__ __forceinline__ int kf_block_offset(const FrameArgs &f, int kf, int cam) {   // N-index of the block's kp 0
+    int off = 0;
+    for (int c = 0; c < cam; ++c) off += f.n_kp[(size_t)kf * f.n_cams + c];
+    return off;
+}
+
+__global__ void __launch_bounds__(256) kf_cand_kernel(KfArgs a) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.n_entries) return;
+    const int j = kf_job_of(a, e);
+    const omv_kf_search_job &J = a.jobs[j];
+    const int kf = J.kf, cam = J.cam, mode = a.mode, C = a.f.n_cams, cap = a.f.kp_cap;
+    const bool claim = kf_claim_mode(mode);
+    const int mp = a.mp_list[e];
+    Top t;
+    t.reset();
+    float4 g = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    do {
+        const float P[3] = {a.mps.pos[3 * (size_t)mp], a.mps.pos[3 * (size_t)mp + 1], a.mps.pos[3 * (size_t)mp + 2]};
+        float Pc[3];
+        se3_apply(J.Tcw, P, Pc);
+        if (mode != OMV_KF_SBP_FRAME && Pc[2] < 0.0f) break;   // depth must be positive
+        float u, v;
+        kb8_project_f(a.cams[cam], Pc, u, v);
+        if (mode == OMV_KF_SBP_FRAME) {   // CurrentFrame.mnMinX .. mnMaxX, inclusive
+            if (u < a.f.min_x || u > a.f.max_x || v < a.f.min_y || v > a.f.max_y) break;
+        } else if (!(u >= a.f.min_x && u < a.f.max_x && v >= a.f.min_y && v < a.f.max_y)) {   // KeyFrame::IsInImage
+            break;
+        }
+        const float invz = 1 / Pc[2];
+        const float ur = u - a.bf * invz;
+        const float maxd = a.mps.max_dist[mp];
+        const float maxDistance = 1.2f * maxd, minDistance = 0.8f * a.mps.min_dist[mp];
+        const float PO[3] = {P[0] - J.Ow[0], P[1] - J.Ow[1], P[2] - J.Ow[2]};
+        const float dist3D = omv::sqrtf_cr(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+        if (mode != OMV_KF_FUSE_SIM3 && (dist3D < minDistance || dist3D > maxDistance)) break;
+        if (mode == OMV_KF_FUSE || mode == OMV_KF_SBP_SIM3) {   // viewing angle < 60 deg
+            const float *Pn = a.mps.normal + 3 * (size_t)mp;
+            if ((double)(PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2]) < 0.5 * (double)dist3D) break;
+        }
+        int pred = (int)ceil(log((double)(maxd / dist3D)) / (double)a.log_scale);   // MapPoint::PredictScale
+        pred = pred < 0 ? 0 : (pred >= a.n_levels ? a.n_levels - 1 : pred);
+        const float radius = a.th * a.f.scale[pred];
+        int minL, maxL;
+        kf_levels(mode, pred, minL, maxL);
+        uint64_t dmp[4];
+        load_desc(a.mps.desc + (size_t)mp * 32, dmp);
+        const int32_t *cl = claim ? a.kp_match + (size_t)kf * C * cap : nullptr;
+        const omv_kp *kk = a.f.kps + (size_t)kf * C * cap;
+        const float *urow = a.uright ? a.uright + (size_t)kf * cap : nullptr;
+        scan_window(a.f, kf, cam, u, v, radius, minL, maxL, dmp,
+                    [&](int slot) {
+                        if (claim) return cl[slot] >= 0;
+                        if (mode != OMV_KF_FUSE) return false;
+                        const omv_kp k = kk[slot];   // reprojection gate (ORBmatcher.cc:1594-1615)
+                        const float ex = u - k.x, ey = v - k.y;
+                        const int i = slot - cam * cap;
+                        if (cam == 0 && urow[i] >= 0) {
+                            const float er = ur - urow[i];
+                            const float e2 = ex * ex + ey * ey + er * er;
+                            return (double)(e2 * a.invs2[k.octave]) > 7.8;
+                        }
+                        const float e2 = ex * ex + ey * ey;
+                        return (double)(e2 * a.invs2[k.octave]) > 5.99;
+                    },
+                    t);
+        g = make_float4(u, v, radius, __int_as_float(pred));
+    } while (false);
+    if (!claim) {
+        int bi = -1, bd = -1;
+        if (t.n > 0) bi = kf_block_offset(a.f, kf, cam) + t.idx(0), bd = t.dist(0);
+        a.best_idx[e] = bi, a.best_dist[e] = bd;
+        if (bi >= 0 && (float)bd <= a.max_dist) atomicAdd(a.n_matches + j, 1);
+        return;
+    }
+    uint4 *o4 = reinterpret_cast<uint4 *>(&a.recs[e]);
+#pragma unroll
+    for (int q = 0; q < kTop / 4; ++q)
+        o4[q] = make_uint4(4 * q < t.n ? t.rec(4 * q) : 0u, 4 * q + 1 < t.n ? t.rec(4 * q + 1) : 0u,
+                           4 * q + 2 < t.n ? t.rec(4 * q + 2) : 0u, 4 * q + 3 < t.n ? t.rec(4 * q + 3) : 0u);
+    a.counts[e] = t.count;
+    a.geo[e] = g;
+}
+
+// Rotation bin of a SearchByProjection(Frame&, KF, ...) match (:2502-2510).
+__device__ __forceinline__ int kf_rot_bin(float kf_angle, float frame_angle) {
+    float rot = kf_angle - frame_angle;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / 30));
+    return bin == 30 ? 0 : bin;
+}
+
+__global__ void __launch_bounds__(64) kf_resolve_kernel(KfArgs a) {
+    extern __shared__ uint32_t claimed[];
+    __shared__ int hist[30];
+    const int kf = blockIdx.x, lane = threadIdx.x;
+    const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap, W = (S + 31) / 32;
+    int32_t *cl = a.kp_match + (size_t)kf * S;
+    for (int w = lane; w < W; w += 64) {
+        uint32_t bits = 0;
+        for (int b = 0; b < 32; ++b) {
+            const int s = w * 32 + b;
+            if (s < S && cl[s] >= 0) bits |= 1u << b;
+        }
+        claimed[w] = bits;
+    }
+    wave_sync();
+    const bool ori = a.mode == OMV_KF_SBP_FRAME && a.check_ori;
+    for (int j = 0; j < a.n_jobs; ++j) {
+        const omv_kf_search_job &J = a.jobs[j];
+        if (J.kf != kf) continue;
+        const int cam = J.cam, off = kf_block_offset(a.f, kf, cam);
+        const omv_kp *kk = a.f.kps + (size_t)kf * S;
+        int nm = 0;
+        if (lane < 30) hist[lane] = 0;
+        wave_sync();
+        for (int e = J.mp_start; e < J.mp_start + J.mp_count; ++e) {
+            const int cnt = a.counts[e];
+            int idx = -1, dist = 0;
+            if (cnt > 0) {
+                const int nrec = min(cnt, kTop);
+                const uint32_t r = lane < nrec ? a.recs[e].e[lane] : 0u;
+                const bool free = lane < nrec && !bit_of(claimed, cam * cap + rec_idx(r));
+                const uint64_t m = __ballot(free);
+                if (m) {
+                    const uint32_t rf = __shfl(r, __ffsll((long long)m) - 1, 64);
+                    idx = rec_idx(rf), dist = rec_dist(rf);
+                } else if (cnt > kTop) {   // all 16 taken and the window held more: rescan (rare)
+                    if (lane == 0) {
+                        const float4 g = a.geo[e];
+                        int minL, maxL;
+                        kf_levels(a.mode, __float_as_int(g.w), minL, maxL);
+                        uint64_t dmp[4];
+                        load_desc(a.mps.desc + (size_t)a.mp_list[e] * 32, dmp);
+                        Top t;
+                        scan_window(a.f, kf, cam, g.x, g.y, g.z, minL, maxL, dmp,
+                                    [&](int slot) { return bit_of(claimed, slot); }, t);
+                        if (t.n > 0) idx = t.idx(0), dist = t.dist(0);
+                    }
+                    idx = __shfl(idx, 0, 64), dist = __shfl(dist, 0, 64);
+                }
+            }
+            const bool ok = idx >= 0 && (float)dist <= a.max_dist;
+            if (lane == 0) {
+                if (ok) {
+                    const int slot = cam * cap + idx;
+                    claimed[slot >> 5] |= 1u << (slot & 31);
+                    cl[slot] = a.mp_list[e];
+                    a.best_idx[e] = off + idx, a.best_dist[e] = dist;
+                    if (ori) ++hist[kf_rot_bin(a.mp_angle[e], kk[slot].angle)];
+                } else {
+                    a.best_idx[e] = -1, a.best_dist[e] = -1;
+                }
+            }
+            nm += ok ? 1 : 0;
+            wave_sync();
+        }
+        if (ori) {   // ComputeThreeMaxima (:2537-2573), then un-claim the matches outside the top bins
+            if (lane == 0) {
+                int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+                for (int i = 0; i < 30; i++) {
+                    const int sz = hist[i];
+                    if (sz > max1) max3 = max2, max2 = max1, max1 = sz, ind3 = ind2, ind2 = ind1, ind1 = i;
+                    else if (sz > max2) max3 = max2, max2 = sz, ind3 = ind2, ind2 = i;
+                    else if (sz > max3) max3 = sz, ind3 = i;
+                }
+                if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+                else if (max3 < 0.1f * (float)max1) ind3 = -1;
+                for (int e = J.mp_start; e < J.mp_start + J.mp_count; ++e) {
+                    const int bi = a.best_idx[e];
+                    if (bi < 0) continue;
+                    const int slot = cam * cap + (bi - off);
+                    const int bin = kf_rot_bin(a.mp_angle[e], kk[slot].angle);
+                    if (bin == ind1 || bin == ind2 || bin == ind3) continue;
+                    claimed[slot >> 5] &= ~(1u << (slot & 31));
+                    cl[slot] = -1;
+                    a.best_idx[e] = -1, a.best_dist[e] = -1;
+                    --nm;
+                }
+            }
+            nm = __shfl(nm, 0, 64);
+            wave_sync();
+        }
+        if (lane == 0) a.n_matches[j] = nm;
+    }
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -1025,6 +1267,10 @@ struct omv_matcher {
     int *d_counts = nullptr;
     int *d_flags = nullptr;   // per (frame, point): in_view bits | skip | has_obs (cand -> resolve)
     int2 *d_push = nullptr;   // SearchByProjection(last frame): (slot, rotation bin) per claim, in order
+    float4 *d_geo = nullptr;  // keyframe searches: per entry window geometry (claim-mode rescans)
+    size_t geo_cap = 0;
+    omv_kf_search_job *d_jobs = nullptr;
+    size_t jobs_cap = 0;
     int *d_npush = nullptr;
     size_t push_cap = 0;
     int32_t *d_knn_i = nullptr, *d_knn_d = nullptr;
@@ -1139,7 +1385,7 @@ omv_status omv_matcher_last_error(omv_matcher *h) {
 omv_status omv_matcher_destroy(omv_matcher *h) {
     if (!h) return OMV_ERR_ARG;
     void *p[] = {h->d_cell_start, h->d_cell_idx, h->d_recs, h->d_counts, h->d_flags, h->d_knn_i, h->d_knn_d, h->d_err,
-                 h->d_push, h->d_npush};
+                 h->d_push, h->d_npush, h->d_geo, h->d_jobs};
     for (void *q : p)
         if (q) (void)hipFree(q);
     delete h;
@@ -1245,6 +1491,70 @@ omv_status omv_matcher_search_last_frame(omv_matcher *h, int n_frames, const omv
     const size_t lds = sizeof(uint32_t) * ((S + 31) / 32) + 2 * sizeof(int) * S;
     lf_resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
     if (check_ori) lf_histo_kernel<<<n_frames, 256, 0, st>>>(h->d_push, h->d_npush, (int)per_frame, S, kp_to_mp, n_matches);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_matcher_search_kf(omv_matcher *h, int n_kf, const omv_frame_geom *g, const omv_kp *kps,
+                                 const uint8_t *desc, const int *n_kp, int n_jobs, const omv_kf_search_job *jobs,
+                                 int n_entries, const int32_t *mp_list, const omv_kf_mps *mps,
+                                 const omv_kf_search_params *p, int32_t *kp_match, int32_t *best_idx,
+                                 int32_t *best_dist, int32_t *n_matches, void *stream) {
+    if (!h || !g || !kps || !desc || !n_kp || !mps || !p || n_kf <= 0 || n_kf > h->max_frames ||
+        g->n_cams != h->n_cams || n_jobs < 0 || n_entries < 0 || (n_jobs > 0 && (!jobs || !n_matches)) ||
+        (n_entries > 0 && (!mp_list || !best_idx || !best_dist || !mps->pos || !mps->desc || !mps->min_dist ||
+                           !mps->max_dist || !mps->normal)))
+        return OMV_ERR_ARG;
+    if (p->mode < OMV_KF_FUSE || p->mode > OMV_KF_SBP_FRAME || p->n_levels <= 0 || p->n_levels > 16) return OMV_ERR_ARG;
+    const bool claim = p->mode == OMV_KF_SBP_SIM3 || p->mode == OMV_KF_SBP_FRAME;
+    if ((claim && !kp_match) || (p->mode == OMV_KF_FUSE && !p->uright) ||
+        (p->mode == OMV_KF_SBP_FRAME && p->check_ori && n_entries > 0 && !p->mp_angle))
+        return OMV_ERR_ARG;
+    int next = 0;   // jobs must tile mp_list in order, name a keyframe of the batch and one of its blocks
+    for (int j = 0; j < n_jobs; ++j) {
+        const omv_kf_search_job &J = jobs[j];
+        if (J.kf < 0 || J.kf >= n_kf || J.cam < 0 || J.cam >= h->n_cams || J.mp_start != next || J.mp_count < 0)
+            return OMV_ERR_ARG;
+        if (p->mode == OMV_KF_SBP_FRAME && J.cam != 0) return OMV_ERR_ARG;   // CurrentFrame.mpCamera, left grid
+        next += J.mp_count;
+    }
+    if (next != n_entries) return OMV_ERR_ARG;
+    if ((size_t)n_entries > (size_t)h->max_frames * h->n_cams * std::max(1, h->max_mps)) return OMV_ERR_CAPACITY;
+    if (n_jobs == 0) return OMV_OK;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    if (h->jobs_cap < (size_t)n_jobs) {
+        if (h->d_jobs) (void)hipFree(h->d_jobs);
+        h->d_jobs = nullptr, h->jobs_cap = 0;
+        HIP_OK(hipMalloc(&h->d_jobs, sizeof(omv_kf_search_job) * n_jobs));
+        h->jobs_cap = n_jobs;
+    }
+    if (claim && h->geo_cap < (size_t)std::max(1, n_entries)) {
+        if (h->d_geo) (void)hipFree(h->d_geo);
+        h->d_geo = nullptr, h->geo_cap = 0;
+        HIP_OK(hipMalloc(&h->d_geo, sizeof(float4) * std::max(1, n_entries)));
+        h->geo_cap = std::max(1, n_entries);
+    }
+    HIP_OK(hipMemcpyAsync(h->d_jobs, jobs, sizeof(omv_kf_search_job) * n_jobs, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(n_matches, 0, sizeof(int32_t) * n_jobs, st));
+    KfArgs a{};
+    fill_frame(h, g, kps, desc, n_kp, a.f);
+    a.jobs = h->d_jobs, a.n_jobs = n_jobs, a.n_kf = n_kf;
+    a.mp_list = mp_list, a.n_entries = n_entries, a.mps = *mps;
+    a.mode = p->mode, a.check_ori = p->check_ori;
+    a.th = p->th, a.max_dist = p->max_dist, a.bf = p->bf, a.uright = p->uright;
+    for (int l = 0; l < 16; ++l) a.invs2[l] = p->inv_level_sigma2[l];
+    a.log_scale = p->log_scale_factor, a.n_levels = p->n_levels;
+    for (int c = 0; c < h->n_cams; ++c)
+        for (int q = 0; q < 8; ++q) a.cams[c][q] = p->cams[c][q];
+    a.mp_angle = p->mp_angle;
+    a.kp_match = kp_match, a.best_idx = best_idx, a.best_dist = best_dist, a.n_matches = n_matches;
+    a.recs = h->d_recs, a.counts = h->d_counts, a.geo = h->d_geo;
+    if (n_entries > 0) kf_cand_kernel<<<(n_entries + 255) / 256, 256, 0, st>>>(a);
+    if (claim) {
+        const size_t lds = sizeof(uint32_t) * (((size_t)h->n_cams * h->kp_cap + 31) / 32);
+        kf_resolve_kernel<<<n_kf, 64, lds, st>>>(a);
+    }
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }

@@ -249,6 +249,85 @@ class ORBmatcher:
             _lib.ptr(frames.n_matches), self._stream(stream)), "omv_matcher_search_projection")
         return frames.n_matches
 
+    # ---- keyframe-side projection searches (omv_matcher_search_kf) -----------------------------------
+    def _search_kf(self, kfs, mode, jobs, mp_list, mps, params, kp_match, stream):
+        h = self._handle(kfs, max(1, -(-len(mp_list) // (kfs.n_frames * kfs.n_cams))))
+        self.AssignFeaturesToGrid(kfs, stream)
+        import torch
+        dev = kfs.kps.device
+        n_e = int(mp_list.shape[0])
+        best_idx = torch.empty(max(n_e, 1), dtype=torch.int32, device=dev)
+        best_dist = torch.empty(max(n_e, 1), dtype=torch.int32, device=dev)
+        n_matches = torch.empty(max(len(jobs), 1), dtype=torch.int32, device=dev)
+        arr = (_lib.KfSearchJob * max(len(jobs), 1))()
+        for i, jb in enumerate(jobs):
+            arr[i].kf, arr[i].cam = int(jb["kf"]), int(jb["cam"])
+            T = np.asarray(jb["Tcw"], np.float32).reshape(7)
+            for q in range(4):
+                arr[i].Tcw.q[q] = float(T[q])
+            for q in range(3):
+                arr[i].Tcw.t[q] = float(T[4 + q])
+                arr[i].Ow[q] = float(np.float32(jb["Ow"][q]))
+            arr[i].mp_start, arr[i].mp_count = int(jb["mp_start"]), int(jb["mp_count"])
+        m = _lib.KfMps(*[_lib.ptr(mps[k]) for k in ("pos", "normal", "min_dist", "max_dist", "desc")])
+        params.mode = mode
+        _lib.check(self._lib.omv_matcher_search_kf(
+            h, kfs.n_frames, ctypes.byref(kfs.geom), _lib.ptr(kfs.kps), _lib.ptr(kfs.desc), _lib.ptr(kfs.n_kp),
+            len(jobs), arr, n_e, _lib.ptr(mp_list), ctypes.byref(m), ctypes.byref(params), _lib.ptr(kp_match),
+            _lib.ptr(best_idx), _lib.ptr(best_dist), _lib.ptr(n_matches), self._stream(stream)), "omv_matcher_search_kf")
+        return best_idx[:n_e], best_dist[:n_e], n_matches[:len(jobs)]
+
+    def Fuse(self, kfs, jobs, mp_list, mps, params, stream=None):
+        """ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID) (src/ORBmatcher.cc:1458-1647) for a batch of
+        jobs (keyframe, cameraID, its pose Tcw [qx qy qz qw tx ty tz] and centre Ow, a run of mp_list).
+        `kfs`: a FrameBatch of the keyframes; mps: dict of device tensors pos / normal / min_dist /
+        max_dist / desc (omv_kf_mps); params: kf_search_params(...).  Returns (best_idx, best_dist,
+        n_fused): per entry the chosen keypoint (the keyframe's N-index, -1 none) and its distance —
+        accepted when <= TH_LOW; the caller applies Replace / AddObservation in entry order — and the
+        reference's return value per job."""
+        return self._search_kf(kfs, _lib.OMV_KF_FUSE, jobs, mp_list, mps, params, None, stream)
+
+    def FuseSim3(self, kfs, jobs, mp_list, mps, params, stream=None):
+        """ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1649-1769): one job per camera block,
+        each with Tiw = GetRelativePose*() * SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale())."""
+        return self._search_kf(kfs, _lib.OMV_KF_FUSE_SIM3, jobs, mp_list, mps, params, None, stream)
+
+    def SearchByProjectionSim3(self, kfs, jobs, mp_list, mps, vpMatched, params, stream=None):
+        """ORBmatcher::SearchByProjection(pKF, Siw, vpPoints, vpMatched, th, ratioHamming, cameraID)
+        (:668-776; the vpPointsKFs overload :778-893 matches identically).  vpMatched: device int32
+        [n_kf][n_cams * kp_cap] slot claims (-1 free), updated in place with the mp_list values."""
+        return self._search_kf(kfs, _lib.OMV_KF_SBP_SIM3, jobs, mp_list, mps, params, vpMatched, stream)
+
+    def SearchByProjectionKF(self, frames, jobs, mp_list, mps, params, stream=None):
+        """ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:2415-2535): each
+        job projects one keyframe's map points (its mvKeysUn angles in params.mp_angle) into a frame of
+        `frames` (camera block 0); claims go to frames.kp_to_mp (Frame::mvpMapPoints)."""
+        params.check_ori = int(self.mbCheckOrientation)
+        return self._search_kf(frames, _lib.OMV_KF_SBP_FRAME, jobs, mp_list, mps, params, frames.kp_to_mp, stream)
+
+
+def kf_search_params(th, max_dist, cams, scale_factor=1.2, nlevels=8, bf=0.0, uright=None, mp_angle=None):
+    """omv_kf_search_params: window factor th, acceptance max_dist (TH_LOW, TH_LOW * ratioHamming or
+    ORBdist), KB8 parameters per block, the extractor's scale tables, mbf and mvuRight (Fuse)."""
+    p = _lib.KfSearchParams()
+    p.th, p.max_dist, p.bf = float(th), float(max_dist), float(bf)
+    p.uright = _lib.ptr(uright) if uright is not None else None
+    sf = np.float32(scale_factor)
+    scales = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        scales.append(np.float32(scales[-1] * sf))
+    for i, s in enumerate(scales):
+        p.inv_level_sigma2[i] = float(np.float32(1.0) / np.float32(s * s))
+    p.log_scale_factor = float(np.float32(np.log(np.float64(sf))))
+    p.n_levels = nlevels
+    c = np.asarray(cams, np.float32).reshape(-1, 8)
+    for i in range(c.shape[0]):
+        for q in range(8):
+            p.cams[i][q] = float(c[i, q])
+    p.mp_angle = _lib.ptr(mp_angle) if mp_angle is not None else None
+    p._keep = (uright, mp_angle)
+    return p
+
 
 def make_rig(cams, R_cl, t_cl, width, height, scale_factor=1.2, nlevels=8):
     """omv_rig from per-camera KB8 parameters and the block-c-from-block-0 transforms (float32)."""

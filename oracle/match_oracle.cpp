@@ -462,3 +462,148 @@ int oracle_frustum(const RigF *rig, const PoseF *pose, const float *pos, const f
 }
 
 }  // extern "C"
+
+// ---- Keyframe-side projection searches -------------------------------------------------------------------
+//   ORBmatcher::Fuse(KF, vpMapPoints, th, cameraID)                    src/ORBmatcher.cc:1458-1647
+//   ORBmatcher::Fuse(KF, Scw, vpPoints, th, vpReplacePoint)            src/ORBmatcher.cc:1649-1769
+//   ORBmatcher::SearchByProjection(KF, Siw, vpPoints, vpMatched, ...)  src/ORBmatcher.cc:668-776, 778-893
+//   ORBmatcher::SearchByProjection(Frame&, KF, sAlreadyFound, th, ORBdist)  src/ORBmatcher.cc:2415-2535
+//   KeyFrame::GetFeaturesInArea / IsInImage                            src/KeyFrame.cc:771-838
+//   MapPoint::Get{Min,Max}DistanceInvariance / PredictScale(KF)       src/MapPoint.cc:598-622
+// Each job is the reference's loop over its map points, literally; the map mutations the reference makes
+// after a Fuse decision (Replace / AddObservation) are the caller's, so Fuse reports the decision per point.
+#include "../include/omv.h"
+
+extern "C" {
+
+int oracle_search_kf(const FrameGeom *g, const KP *kps, const uint8_t *desc, int kp_cap, const int *n_kp, int n_kf,
+                     int n_jobs, const omv_kf_search_job *jobs, const int32_t *mp_list, const float *pos,
+                     const float *normal, const float *min_d, const float *max_d, const uint8_t *mp_desc,
+                     const omv_kf_search_params *p, int32_t *kp_match, int32_t *best_idx, int32_t *best_dist,
+                     int32_t *n_matches) {
+    const int C = g->n_cams;
+    const int mode = p->mode;
+    const bool claim = mode == OMV_KF_SBP_SIM3 || mode == OMV_KF_SBP_FRAME;
+    std::vector<View> views(n_kf);
+    std::vector<bool> built(n_kf, false);
+    const int HISTO_LENGTH = 30;
+    const float factor = 1.0f / HISTO_LENGTH;
+    for (int j = 0; j < n_jobs; ++j) {
+        const omv_kf_search_job &J = jobs[j];
+        const int kf = J.kf, cam = J.cam;
+        if (!built[kf]) {
+            views[kf] = View{g, 0, 0, {}, kps + (size_t)kf * C * kp_cap, kp_cap, n_kp + (size_t)kf * C};
+            build_grids(views[kf]);
+            built[kf] = true;
+        }
+        const View &v = views[kf];
+        int32_t *claims = claim ? kp_match + (size_t)kf * C * kp_cap : nullptr;
+        const KP *kk = kps + (size_t)kf * C * kp_cap;
+        const uint8_t *dd = desc + (size_t)kf * C * kp_cap * 32;
+        int off = 0;   // the keyframe's N-index of the block's first keypoint
+        for (int c = 0; c < cam; ++c) off += n_kp[(size_t)kf * C + c];
+        SE3F T;
+        std::memcpy(T.q, J.Tcw.q, 16), std::memcpy(T.t, J.Tcw.t, 12);
+        std::vector<std::vector<int>> rotHist(HISTO_LENGTH);
+        int nm = 0;
+        for (int e = J.mp_start; e < J.mp_start + J.mp_count; ++e) {
+            best_idx[e] = -1, best_dist[e] = -1;
+            const int mp = mp_list[e];
+            const float *P = pos + 3 * (size_t)mp, *Pn = normal + 3 * (size_t)mp;
+            float Pc[3];
+            se3_apply(T, P, Pc);
+            if (mode != OMV_KF_SBP_FRAME && Pc[2] < 0.0f) continue;   // depth must be positive
+            float u, vv;
+            kb8_project_f(p->cams[cam], Pc, u, vv);
+            if (mode == OMV_KF_SBP_FRAME) {   // CurrentFrame.mnMinX .. mnMaxX, inclusive (:2445-2448)
+                if (u < g->min_x || u > g->max_x) continue;
+                if (vv < g->min_y || vv > g->max_y) continue;
+            } else if (!(u >= g->min_x && u < g->max_x && vv >= g->min_y && vv < g->max_y)) {   // IsInImage
+                continue;
+            }
+            const float invz = 1 / Pc[2];
+            const float ur = u - p->bf * invz;
+            const float maxDistance = 1.2f * max_d[mp], minDistance = 0.8f * min_d[mp];
+            const float PO[3] = {P[0] - J.Ow[0], P[1] - J.Ow[1], P[2] - J.Ow[2]};
+            const float dist3D = std::sqrt(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+            if (mode != OMV_KF_FUSE_SIM3 && (dist3D < minDistance || dist3D > maxDistance)) continue;
+            if ((mode == OMV_KF_FUSE || mode == OMV_KF_SBP_SIM3) &&
+                PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2] < 0.5 * dist3D)   // viewing angle < 60 deg
+                continue;
+            int pred = (int)std::ceil(std::log((double)(max_d[mp] / dist3D)) / (double)p->log_scale_factor);
+            if (pred < 0) pred = 0;
+            else if (pred >= p->n_levels) pred = p->n_levels - 1;
+            const float radius = p->th * g->scale_factors[pred];
+            const std::vector<int> win = mode == OMV_KF_SBP_FRAME
+                                             ? features_in_area(v, u, vv, radius, pred - 1, pred + 1, cam)
+                                             : features_in_area(v, u, vv, radius, 0, -1, cam);   // KeyFrame version
+            if (win.empty()) continue;
+            const uint8_t *dmp = mp_desc + (size_t)mp * 32;
+            int bestDist = mode == OMV_KF_FUSE_SIM3 ? INT32_MAX : 256, bestIdx = -1;
+            for (int i : win) {
+                const int slot = cam * kp_cap + i;
+                if (claim && claims[slot] >= 0) continue;   // vpMatched[idx] / CurrentFrame.mvpMapPoints[i2]
+                const KP &kp = kk[slot];
+                if (mode != OMV_KF_SBP_FRAME && (kp.octave < pred - 1 || kp.octave > pred)) continue;
+                if (mode == OMV_KF_FUSE) {   // reprojection gate (:1594-1615)
+                    const float ex = u - kp.x, ey = vv - kp.y;
+                    if (cam == 0 && p->uright[(size_t)kf * kp_cap + i] >= 0) {
+                        const float er = ur - p->uright[(size_t)kf * kp_cap + i];
+                        const float e2 = ex * ex + ey * ey + er * er;
+                        if (e2 * p->inv_level_sigma2[kp.octave] > 7.8) continue;
+                    } else {
+                        const float e2 = ex * ex + ey * ey;
+                        if (e2 * p->inv_level_sigma2[kp.octave] > 5.99) continue;
+                    }
+                }
+                const int d = descriptor_distance(dmp, dd + (size_t)slot * 32);
+                if (d < bestDist) bestDist = d, bestIdx = i;
+            }
+            // bestIdx >= 0: with the reference's thresholds (< 256) an empty scan is never accepted
+            const bool ok = bestIdx >= 0 && (float)bestDist <= p->max_dist;
+            if (!claim) {
+                if (bestIdx >= 0) best_idx[e] = off + bestIdx, best_dist[e] = bestDist;
+                if (ok) ++nm;
+                continue;
+            }
+            if (!ok) continue;
+            const int slot = cam * kp_cap + bestIdx;
+            claims[slot] = mp;
+            best_idx[e] = off + bestIdx, best_dist[e] = bestDist;
+            ++nm;
+            if (mode == OMV_KF_SBP_FRAME && p->check_ori) {
+                float rot = p->mp_angle[e] - kk[slot].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                rotHist[bin].push_back(e);
+            }
+        }
+        if (mode == OMV_KF_SBP_FRAME && p->check_ori) {   // ComputeThreeMaxima (:2537-2573) + removal
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int sz = (int)rotHist[i].size();
+                if (sz > max1) {
+                    max3 = max2, max2 = max1, max1 = sz, ind3 = ind2, ind2 = ind1, ind1 = i;
+                } else if (sz > max2) {
+                    max3 = max2, max2 = sz, ind3 = ind2, ind2 = i;
+                } else if (sz > max3) {
+                    max3 = sz, ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+            else if (max3 < 0.1f * (float)max1) ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++)
+                if (i != ind1 && i != ind2 && i != ind3)
+                    for (int e : rotHist[i]) {
+                        claims[cam * kp_cap + (best_idx[e] - off)] = -1;
+                        best_idx[e] = -1, best_dist[e] = -1;
+                        --nm;
+                    }
+        }
+        n_matches[j] = nm;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -408,3 +408,45 @@ def depth_from_undistorted(keys, depth, undist, bf):
     lib().oracle_depth_from_undistorted(_p(keys) if n else None, int(n), _p(d), int(d.shape[1]), int(d.shape[0]),
                                         ctypes.byref(undist), ctypes.c_float(bf), _p(ur), _p(xy))
     return ur[:n], xy[:n]
+
+
+# ---- keyframe-side projection searches -----------------------------------------------------------------
+def search_kf(b, th, max_dist, check_ori=True):
+    """Restated ORBmatcher::Fuse / Fuse(Sim3) / SearchByProjection(KF, Sim3) / SearchByProjection(Frame&, KF)
+    on a synth_kfmatch batch (mode b["mode"]).  Returns (best_idx, best_dist, n_matches, kp_match)."""
+    from openmavis_amd._lib import FrameGeom, KfSearchJob
+    from openmavis_amd.matcher import kf_search_params
+    g = FrameGeom()
+    g.n_cams, g.min_x, g.max_x, g.min_y, g.max_y, g.nlevels = b["n_cams"], 0.0, float(b["width"]), 0.0, \
+        float(b["height"]), b["nlevels"]
+    s = np.float32(1.0)
+    for i in range(b["nlevels"]):
+        g.scale_factors[i] = float(s)
+        s = np.float32(s * np.float32(1.2))
+    uright = np.ascontiguousarray(b["uright"], np.float32)
+    angle = np.ascontiguousarray(b["mp_angle"], np.float32)
+    p = kf_search_params(th, max_dist, b["cams"], bf=float(b["bf"]), nlevels=b["nlevels"])
+    p.uright, p.mp_angle = _p(uright), _p(angle)
+    p.mode, p.check_ori = int(b["mode"]), int(bool(check_ori))
+    jobs = (KfSearchJob * len(b["jobs"]))()
+    for i, jb in enumerate(b["jobs"]):
+        jobs[i].kf, jobs[i].cam = jb["kf"], jb["cam"]
+        T = np.asarray(jb["Tcw"], np.float32)
+        for q in range(4):
+            jobs[i].Tcw.q[q] = float(T[q])
+        for q in range(3):
+            jobs[i].Tcw.t[q] = float(T[4 + q])
+            jobs[i].Ow[q] = float(jb["Ow"][q])
+        jobs[i].mp_start, jobs[i].mp_count = jb["mp_start"], jb["mp_count"]
+    n_e = len(b["mp_list"])
+    best_idx = np.zeros(n_e, np.int32)
+    best_dist = np.zeros(n_e, np.int32)
+    n_m = np.zeros(len(b["jobs"]), np.int32)
+    kp_match = np.array(b["kp_match"], np.int32, copy=True)
+    m = b["mps"]
+    lib().oracle_search_kf(ctypes.byref(g), _p(np.ascontiguousarray(b["kps"])), _p(np.ascontiguousarray(b["desc"])),
+                           int(b["kp_cap"]), _p(np.ascontiguousarray(b["n_kp"], np.int32)), int(b["n_kf"]),
+                           len(b["jobs"]), jobs, _p(b["mp_list"]), _p(m["pos"]), _p(m["normal"]), _p(m["min_dist"]),
+                           _p(m["max_dist"]), _p(m["desc"]), ctypes.byref(p), _p(kp_match), _p(best_idx),
+                           _p(best_dist), _p(n_m))
+    return best_idx, best_dist, n_m, kp_match

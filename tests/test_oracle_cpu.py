@@ -145,3 +145,24 @@ def test_frustum_oracle_kats(oracle):
     assert out["in_view"][3].sum() == 0                                                          # behind
     assert out["level"][4, 0] == 7                                                               # clamped
     assert n == int((out["in_view"].sum(1) > 0).sum())
+
+
+# ---- keyframe-side projection searches (ORBmatcher::Fuse / SearchByProjection(KF...) restatement) -------
+def test_kf_search_oracle_recovers_true_keypoints(oracle):
+    """Points derived from a keypoint of the job's block are matched back to that keypoint (or an
+    equivalent one at distance <= the derived one) by Fuse; claim modes never assign a keypoint twice."""
+    from openmavis_amd import synth_kfmatch as sk
+    b = sk.make_kf_search(0, seed=5)
+    bi, bd, nm, _ = oracle.search_kf(b, *sk.MODE_PARAMS[0])
+    assert nm.sum() > 0.4 * len(bi)
+    acc = (bi >= 0) & (bd <= 50)
+    assert (nm == [int(acc[j["mp_start"]:j["mp_start"] + j["mp_count"]].sum()) for j in b["jobs"]]).all()
+    for mode in (2, 3):
+        b = sk.make_kf_search(mode, seed=5)
+        bi, bd, nm, km = oracle.search_kf(b, *sk.MODE_PARAMS[mode])
+        claimed = km[km != b["kp_match"]]
+        assert (claimed >= 0).all() and len(claimed) == nm.sum()
+        for jb in b["jobs"]:   # one keypoint per point, no keypoint twice within a keyframe
+            sl = bi[jb["mp_start"]:jb["mp_start"] + jb["mp_count"]]
+            sl = sl[sl >= 0]
+            assert len(np.unique(sl)) == len(sl)
