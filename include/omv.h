@@ -551,6 +551,20 @@ omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, co
  * (H_out may alias H_in).  Asynchronous. */
 omv_status omv_pose_constraint(int n, const double *H_in, double *H_out, void *stream);
 
+/* ---- IMU preintegration ----
+ * IMU::Preintegrated::IntegrateNewMeasurement (src/ImuTypes.cc:160-239) over n independent records, as
+ * Tracking::PreintegrateIMU drives it (src/Tracking.cc:1675-1712).  Record r integrates the measurements
+ * meas[start[r] .. start[r+1]) in order, each (ax ay az wx wy wz dt) with the interpolation of
+ * PreintegrateIMU already applied, starting from its current state:
+ *   preint  device [n][OMV_PREINT_FLOATS] in/out (dR dV dP JRg JVg JVa JPg JPa b dT C; Initialize() =
+ *           identity dR, zeros elsewhere, b = the bias)
+ *   avg     device [n][6] in/out avgA | avgW, or NULL
+ *   start   device [n+1]; meas device [start[n]][7]
+ *   Nga / NgaWalk  host [6]: the diagonals of IMU::Calib::Cov / CovWalk (Eigen::DiagonalMatrix<float, 6>,
+ *                  include/ImuTypes.h:126; Tracking.cc:601 builds them from Ng*sf, Na*sf, Ngw/sf, Naw/sf). */
+omv_status omv_imu_preintegrate(int n, float *preint, float *avg, const float *meas, const int32_t *start,
+                                const float *Nga, const float *NgaWalk, void *stream);
+
 /* ---- Frame construction tail (src/Frame.cc:1913-1939) ---- */
 
 /* cv::fisheye::undistortPoints parameters of one camera block (GetDepthFromUndistortedPoints,

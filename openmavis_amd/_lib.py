@@ -232,6 +232,7 @@ SIGNATURES = {
     "omv_matcher_search_kf": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(KfSearchJob),
                                    _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,
                                    _VP]),
+    "omv_imu_preintegrate": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
     "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
                               _VP]),

@@ -450,3 +450,21 @@ def search_kf(b, th, max_dist, check_ori=True):
                            _p(m["max_dist"]), _p(m["desc"]), ctypes.byref(p), _p(kp_match), _p(best_idx),
                            _p(best_dist), _p(n_m))
     return best_idx, best_dist, n_m, kp_match
+
+
+# ---- IMU preintegration ---------------------------------------------------------------------------------
+def preintegrate(b, Nga, NgaWalk):
+    """IMU::Preintegrated::IntegrateNewMeasurement restated on every record of a synth_imu batch from
+    Initialize(bias).  Returns (records [n][292] float32, avg [n][6])."""
+    n = len(b["start"]) - 1
+    rec = np.zeros((n, 292), np.float32)
+    rec[:, [0, 4, 8]] = 1.0
+    rec[:, 60:66] = b["bias"]
+    avg = np.zeros((n, 6), np.float32)
+    Nga = np.ascontiguousarray(Nga, np.float32)
+    NgaWalk = np.ascontiguousarray(NgaWalk, np.float32)
+    meas = np.ascontiguousarray(b["meas"], np.float32)
+    for r in range(n):
+        s0, s1 = int(b["start"][r]), int(b["start"][r + 1])
+        lib().oracle_preintegrate(_p(rec[r]), _p(avg[r]), _p(meas[s0:s1]), s1 - s0, _p(Nga), _p(NgaWalk))
+    return rec, avg
