@@ -565,6 +565,34 @@ omv_status omv_pose_constraint(int n, const double *H_in, double *H_out, void *s
 omv_status omv_imu_preintegrate(int n, float *preint, float *avg, const float *meas, const int32_t *start,
                                 const float *Nga, const float *NgaWalk, void *stream);
 
+/* ---- DBoW2 vocabulary transform ----
+ * TemplatedVocabulary<FORB::TDescriptor, FORB>::transform(features, BowVector&, FeatureVector&, levelsup)
+ * (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1194, per feature :1217-1259) as Frame::ComputeBoW /
+ * KeyFrame::ComputeBoW call it (src/KeyFrame.cc:207-214, levelsup 4), over a batch of descriptor sets.
+ * The vocabulary tree is flattened in loadFromTextFile's node order (node 0 = root, :1338-1424). */
+typedef struct omv_vocab {
+    int n_nodes, n_words;
+    int L;                         /* m_L (FeatureVector level = L - levelsup)                        */
+    int scoring;                   /* DBoW2::ScoringType: 0 L1, 1 L2, 2 chi-square, 3 KL, 4 Bhattacharyya, 5 dot product */
+    int weighting;                 /* DBoW2::WeightingType: 0 TF_IDF, 1 TF, 2 IDF, 3 BINARY            */
+    const int32_t *child_start;    /* device [n_nodes + 1]: m_nodes[i].children as a CSR, file order  */
+    const int32_t *child_ids;      /* device [child_start[n_nodes]]                                   */
+    const uint8_t *desc;           /* device [n_nodes][32] node descriptors                           */
+    const int32_t *word_id;        /* device [n_nodes] m_nodes[i].word_id (leaves)                    */
+    const double *weight;          /* device [n_nodes] m_nodes[i].weight (idf; 0 = stopped word)      */
+} omv_vocab;
+
+/* n_sets sets of desc [set][cap][32] with n_desc[set] <= cap <= 16384 rows (mDescriptors row order).
+ * Per feature (device [set][cap]): word, wval (the word's weight), node (FeatureVector node, -1 if the
+ * descent ended above that level).  BowVector (device [set][cap]): bow_word ascending, bow_value, count in
+ * bow_n [set].  FeatureVector (device): fv_node [set][cap] ascending, fv_start [set][cap + 1] (offsets
+ * into fv_idx [set][cap]), count in fv_n [set].  Stopped words (weight <= 0) are left out of both, as in
+ * the reference.  Asynchronous. */
+omv_status omv_bow_transform(const omv_vocab *voc, int n_sets, const uint8_t *desc, int cap, const int *n_desc,
+                             int levelsup, int32_t *word, double *wval, int32_t *node, int32_t *bow_word,
+                             double *bow_value, int32_t *bow_n, int32_t *fv_node, int32_t *fv_start, int32_t *fv_idx,
+                             int32_t *fv_n, void *stream);
+
 /* ---- Frame construction tail (src/Frame.cc:1913-1939) ---- */
 
 /* cv::fisheye::undistortPoints parameters of one camera block (GetDepthFromUndistortedPoints,

@@ -61,6 +61,13 @@ class SE3f(ctypes.Structure):
     _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3)]
 
 
+class Vocab(ctypes.Structure):
+    """omv_vocab (include/omv.h)."""
+    _fields_ = [("n_nodes", ctypes.c_int), ("n_words", ctypes.c_int), ("L", ctypes.c_int), ("scoring", ctypes.c_int),
+                ("weighting", ctypes.c_int)] + [(n, ctypes.c_void_p) for n in (
+                    "child_start", "child_ids", "desc", "word_id", "weight")]
+
+
 class KfSearchJob(ctypes.Structure):
     """omv_kf_search_job (include/omv.h)."""
     _fields_ = [("kf", ctypes.c_int), ("cam", ctypes.c_int), ("Tcw", SE3f), ("Ow", ctypes.c_float * 3),
@@ -233,6 +240,7 @@ SIGNATURES = {
                                    _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,
                                    _VP]),
     "omv_imu_preintegrate": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "omv_bow_transform": (_I, [ctypes.POINTER(Vocab), _I, _VP, _I, _VP, _I] + [_VP] * 10 + [_VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),
     "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
                               _VP]),

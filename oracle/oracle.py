@@ -468,3 +468,28 @@ def preintegrate(b, Nga, NgaWalk):
         s0, s1 = int(b["start"][r]), int(b["start"][r + 1])
         lib().oracle_preintegrate(_p(rec[r]), _p(avg[r]), _p(meas[s0:s1]), s1 - s0, _p(Nga), _p(NgaWalk))
     return rec, avg
+
+
+# ---- DBoW2 vocabulary transform ---------------------------------------------------------------------------
+def bow_transform(v, desc, n_desc, levelsup):
+    """TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup) restated per set of a
+    synth_bow vocabulary dict.  Returns a list of dicts (word, wval, node, bow_word, bow_value, fv_node,
+    fv_start, fv_idx) per set."""
+    from openmavis_amd._lib import Vocab
+    keep = {k: np.ascontiguousarray(v[k]) for k in ("child_start", "child_ids", "desc", "word_id", "weight")}
+    voc = Vocab(len(v["weight"]), v["n_words"], v["L"], v["scoring"], v["weighting"],
+                *[ctypes.c_void_p(keep[k].ctypes.data) for k in ("child_start", "child_ids", "desc", "word_id",
+                                                                 "weight")])
+    out = []
+    for s in range(desc.shape[0]):
+        n = int(n_desc[s])
+        d = np.ascontiguousarray(desc[s, :n])
+        word, node, bw, fvn, fvi = (np.zeros(max(n, 1), np.int32) for _ in range(5))
+        wval, bv = np.zeros(max(n, 1)), np.zeros(max(n, 1))
+        fvs = np.zeros(n + 1, np.int32)
+        nb, nf = ctypes.c_int32(), ctypes.c_int32()
+        lib().oracle_bow_transform(ctypes.byref(voc), _p(d), n, int(levelsup), _p(word), _p(wval), _p(node), _p(bw),
+                                   _p(bv), ctypes.byref(nb), _p(fvn), _p(fvs), _p(fvi), ctypes.byref(nf))
+        out.append(dict(word=word[:n], wval=wval[:n], node=node[:n], bow_word=bw[:nb.value], bow_value=bv[:nb.value],
+                        fv_node=fvn[:nf.value], fv_start=fvs[:nf.value + 1], fv_idx=fvi[:fvs[nf.value]]))
+    return out
