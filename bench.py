@@ -305,6 +305,97 @@ def tri_leg(pairs, n_pairs, reps, dev):
     return out
 
 
+def _timed(fn, reps, dev):
+    import torch
+    fn()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / reps
+
+
+def _cpu_rate(fn, units, budget=1.5):
+    t0 = time.perf_counter()
+    done = 0
+    while done == 0 or time.perf_counter() - t0 < budget:
+        fn()
+        done += units
+    return done, time.perf_counter() - t0
+
+
+def aux_legs(dev, cpu):
+    """The SURVEY §8f rows beside the two headline metrics, each on a batch already in HBM with its CPU oracle
+    timed on a bounded sample: ORBmatcher::Fuse (LocalMapping::SearchInNeighbors scale), DBoW2 transform
+    (ComputeBoW of whole multi-camera frames) and IMU preintegration (PreintegrateIMU records)."""
+    import torch
+    from openmavis_amd import synth_bow, synth_imu, synth_kfmatch
+    from openmavis_amd.bow import ORBVocabulary
+    from openmavis_amd.imu import Calib, PreintegratedBatch
+    from openmavis_amd.matcher import FrameBatch, ORBmatcher, kf_search_params
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+    out = {}
+    # ---- Fuse: 32 keyframes x 5 blocks, ~660 map points per (keyframe, block)
+    b = synth_kfmatch.make_kf_search(0, n_kf=32, kp_cap=1200, pts_per_job=600, seed=11)
+    K, Cc, cap = b["n_kf"], b["n_cams"], b["kp_cap"]
+    scale = [1.0]
+    for _ in range(1, b["nlevels"]):
+        scale.append(float(np.float32(scale[-1] * np.float32(1.2))))
+    kfs = FrameBatch(torch, K, Cc, cap, b["width"], b["height"], scale, device=dev)
+    kfs.kps.copy_(torch.from_numpy(np.ascontiguousarray(b["kps"]).view(np.int32).reshape(K, Cc, cap, 6)))
+    kfs.desc.copy_(torch.from_numpy(b["desc"]))
+    kfs.n_kp.copy_(torch.from_numpy(b["n_kp"]))
+    mps = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b["mps"].items()}
+    mp_list = torch.from_numpy(b["mp_list"]).to(dev)
+    p = kf_search_params(3.0, 50.0, b["cams"], bf=float(b["bf"]), uright=torch.from_numpy(b["uright"]).to(dev))
+    m = ORBmatcher(0.6)
+    dt = _timed(lambda: m.Fuse(kfs, b["jobs"], mp_list, mps, p), 10, dev)
+    n_e = len(b["mp_list"])
+    out["fuse"] = {"metric": "ORBmatcher::Fuse map-point projections/s", "value": round(n_e / dt, 1),
+                   "unit": "points/s", "ms_per_batch": round(dt * 1e3, 3), "points_per_batch": n_e,
+                   "jobs_per_batch": len(b["jobs"])}
+    if cpu:
+        done, t = _cpu_rate(lambda: oracle.search_kf(b, 3.0, 50.0), n_e)
+        out["fuse"]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "points/s", "cores": 1, "kind": "port",
+                                       "sample": f"{done} point fusions, oracle C++ restatement, 1 thread, {t:.2f} s"}
+    # ---- DBoW2 transform: 128 sets of 6000 descriptors (5 x 1200), k = 10, L = 5 vocabulary
+    v = synth_bow.make_vocab(k=10, L=5, seed=1)
+    d, n = synth_bow.make_sets(v, n_sets=128, cap=6000, seed=2)
+    voc = ORBVocabulary(v, device=dev)
+    dd, nn = torch.from_numpy(d).to(dev), torch.from_numpy(n).to(dev)
+    dt = _timed(lambda: voc.transform(dd, nn, 3), 10, dev)
+    nd = int(n.sum())
+    out["bow"] = {"metric": "DBoW2 transform descriptors/s (BowVector + FeatureVector)", "value": round(nd / dt, 1),
+                  "unit": "descriptors/s", "ms_per_batch": round(dt * 1e3, 3), "sets_per_batch": 128,
+                  "vocabulary": {"k": 10, "L": 5, "nodes": len(v["weight"])}}
+    if cpu:
+        done, t = _cpu_rate(lambda: oracle.bow_transform(v, d[:4], n[:4], 3), int(n[:4].sum()))
+        out["bow"]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "descriptors/s", "cores": 1,
+                                      "kind": "port", "sample": f"{done} descriptors, oracle, 1 thread, {t:.2f} s"}
+    # ---- IMU preintegration: 2048 records of 4-40 samples at 200 Hz
+    ib = synth_imu.make_imu_batch(n_rec=2048, seed=1)
+    cal = Calib(1.7e-4, 2.0e-3, 1.9e-5, 3.0e-3, freq=200.0)
+    pre = PreintegratedBatch(2048, cal, device=dev)
+    meas, st = torch.from_numpy(ib["meas"]).to(dev), torch.from_numpy(ib["start"]).to(dev)
+
+    def run():
+        pre.Initialize(ib["bias"])
+        pre.IntegrateNewMeasurements(meas, st)
+    dt = _timed(run, 10, dev)
+    nm = int(ib["start"][-1])
+    out["imu_preint"] = {"metric": "IMU IntegrateNewMeasurement steps/s", "value": round(nm / dt, 1),
+                         "unit": "measurements/s", "ms_per_batch": round(dt * 1e3, 3), "records_per_batch": 2048}
+    if cpu:
+        sub = dict(ib, start=ib["start"][:65], bias=ib["bias"][:64])
+        done, t = _cpu_rate(lambda: oracle.preintegrate(sub, cal.Cov, cal.CovWalk), int(sub["start"][-1]))
+        out["imu_preint"]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "measurements/s", "cores": 1,
+                                             "kind": "port", "sample": f"{done} measurements, oracle, 1 thread, {t:.2f} s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,6 +416,7 @@ def main():
     ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
     ap.add_argument("--pose-frames", type=int, default=1024, help="frames per PoseInertialOptimization batch (0: skip)")
     ap.add_argument("--tri-pairs", type=int, default=256, help="keyframe pairs per SearchForTriangulation batch (0: skip)")
+    ap.add_argument("--aux", type=int, default=1, help="Fuse / DBoW2 transform / IMU preintegration legs (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -481,6 +573,7 @@ def main():
     pose_lf = pose_leg(lf_batch, lf_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev, last_frame=True) \
         if lf_batch is not None else None
     tri = tri_leg(tri_pairs, args.tri_pairs, 10, dev) if tri_pairs is not None else None
+    aux = aux_legs(dev, rank == 0 and not args.no_cpu_baseline) if args.aux else {}
 
     if rank != 0:
         if world > 1:
@@ -555,6 +648,7 @@ def main():
         "local_ba": lba,
         "pose_inertial": pose,
         "pose_inertial_last_frame": pose_lf,
+        **aux,
         "triangulation": tri,
     }
     print(json.dumps(out))

@@ -12,42 +12,37 @@ from . import synth
 
 def make_vocab(k=10, L=4, seed=1, scoring=0, weighting=0, early_leaf=0.1, stop=0.05):
     rng = np.random.Generator(np.random.PCG64(seed))
-    desc = [np.zeros(32, np.uint8)]
-    parent, depth = [0], [0]
-    frontier = [0]
+    desc = [np.zeros((1, 32), np.uint8)]
+    parent = [np.zeros(1, np.int64)]
+    frontier = np.zeros(1, np.int64)
+    n = 1
     for lvl in range(1, L + 1):
-        nxt = []
-        for p in frontier:
-            for _ in range(k):
-                nxt.append(len(desc))
-                if p == 0:
-                    desc.append(rng.integers(0, 256, 32, dtype=np.uint8))
-                else:
-                    desc.append(synth.flip_bits(desc[p][None], rng, max(2, 64 >> lvl))[0])
-                parent.append(p)
-                depth.append(lvl)
-        if lvl == L - 1:   # some depth L-1 nodes stay leaves (an unbalanced tree)
-            nxt = [i for i in nxt if rng.random() >= early_leaf]
-        frontier = nxt
-    n = len(desc)
-    children = [[] for _ in range(n)]
-    for i in range(1, n):
-        children[parent[i]].append(i)
+        par = np.repeat(frontier, k)
+        if lvl == 1:
+            d = rng.integers(0, 256, (len(par), 32), dtype=np.uint8)
+        else:
+            d = synth.flip_bits(np.concatenate(desc)[par], rng, max(2, 64 >> lvl))
+        ids = np.arange(n, n + len(par))
+        n += len(par)
+        desc.append(d)
+        parent.append(par)
+        frontier = ids[rng.random(len(ids)) >= early_leaf] if lvl == L - 1 else ids   # some stay leaves
+    desc = np.concatenate(desc)
+    parent = np.concatenate(parent)
+    counts = np.bincount(parent[1:], minlength=n)
+    cs = np.zeros(n + 1, np.int32)
+    cs[1:] = np.cumsum(counts)
+    child_ids = np.argsort(parent[1:], kind="stable").astype(np.int32) + 1   # per parent, in line order
+    leaf = counts == 0
+    leaf[0] = False
     word = np.zeros(n, np.int32)
-    nw = 0
-    for i in range(1, n):
-        if not children[i]:
-            word[i] = nw
-            nw += 1
+    word[leaf] = np.arange(leaf.sum(), dtype=np.int32)
     weight = np.where(rng.random(n) < stop, 0.0, rng.uniform(0.5, 5.0, n))
     weight[0] = 0.0
     if weighting in (1, 3):   # TF / BINARY vocabularies store weight 1 per word (DBoW2 setNodeWeights)
         weight = np.where(weight > 0, 1.0, 0.0)
-    cs = np.zeros(n + 1, np.int32)
-    cs[1:] = np.cumsum([len(c) for c in children])
-    return dict(k=k, L=L, scoring=scoring, weighting=weighting, n_words=nw, child_start=cs,
-                child_ids=np.array([c for ch in children for c in ch], np.int32), desc=np.stack(desc),
-                word_id=word, weight=weight)
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, n_words=int(leaf.sum()), child_start=cs,
+                child_ids=child_ids, desc=desc, word_id=word, weight=weight)
 
 
 def make_sets(v, n_sets=4, cap=2000, seed=2):
