@@ -420,10 +420,12 @@ __device__ inline void sym_eig_wave(double *A, double *V, int lane) {
     for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
     wave_lds_sync();
     for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0;
-        for (int p = 0; p < N; ++p)
+        double off = 0, dg = 0;   // converged: off-diagonal mass below 1e-32 of the diagonal's
+        for (int p = 0; p < N; ++p) {
+            dg += A[p * N + p] * A[p * N + p];
             for (int q = p + 1; q < N; ++q) off += A[p * N + q] * A[p * N + q];
-        if (off < 1e-300) break;
+        }
+        if (off <= 1e-32 * dg || off < 1e-300) break;
         for (int p = 0; p < N; ++p)
             for (int q = p + 1; q < N; ++q) {
                 const double apq = A[p * N + q];

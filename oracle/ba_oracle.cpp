@@ -293,10 +293,12 @@ void sym_eig(std::vector<double> A, int n, std::vector<double> &w, std::vector<d
     V.assign(n * n, 0.0);
     for (int i = 0; i < n; ++i) V[i * n + i] = 1;
     for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0;
-        for (int p = 0; p < n; ++p)
+        double off = 0, dg = 0;   // converged: off-diagonal mass below 1e-32 of the diagonal's
+        for (int p = 0; p < n; ++p) {
+            dg += A[p * n + p] * A[p * n + p];
             for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
-        if (off < 1e-300) break;
+        }
+        if (off <= 1e-32 * dg || off < 1e-300) break;
         for (int p = 0; p < n; ++p)
             for (int q = p + 1; q < n; ++q) {
                 const double apq = A[p * n + q];
