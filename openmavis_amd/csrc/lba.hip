@@ -57,11 +57,10 @@ constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / bac
 
 
 
-__global__ void __launch_bounds__(256) mono_err_kernel(Rig rig, State s, Edges E, double delta, double dsqr,
-                                                       double delta_st, double dsqr_st, double *err, double *err3,
-                                                       double *chi2, double *partial) {
-    __shared__ double sh[8];
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void mono_err_block(int blk, double *sh, Rig rig, State s, Edges E, double delta,
+                                               double dsqr, double delta_st, double dsqr_st, double *err,
+                                               double *err3, double *chi2, double *partial) {
+    const int e = blk * blockDim.x + threadIdx.x;
     double r0 = 0;
     if (e < E.n) {
         const int k = E.kf[e], c = E.cam[e], C = rig.n_cams;
@@ -88,12 +87,12 @@ __global__ void __launch_bounds__(256) mono_err_kernel(Rig rig, State s, Edges E
         else huber(c2, delta, dsqr, r0, r1);
     }
     const double t = block_reduce_sum(r0, sh);
-    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    if (threadIdx.x == 0) partial[blk] = t;
 }
 
-
-__global__ void imu_err_kernel(State s, Imu I, double delta, double dsqr, double *err9, double *partial) {
-    __shared__ double sh[8];
+// EdgeInertial + random-walk errors, one block (threads >= I.n contribute 0 to the fixed-order sum).
+__device__ __forceinline__ void imu_err_block(double *sh, State s, Imu I, double delta, double dsqr, double *err9,
+                                              double *partial) {
     const int i = threadIdx.x;
     double r0 = 0;
     if (i < I.n) {
@@ -125,6 +124,19 @@ __global__ void imu_err_kernel(State s, Imu I, double delta, double dsqr, double
     }
     const double t = block_reduce_sum(r0, sh);
     if (threadIdx.x == 0) partial[0] = t;
+}
+
+// computeActiveErrors in one launch: blocks [0, n_mono_blocks) the visual edges (256 each), the block after
+// them (when has_imu) the inertial / random-walk edges.
+__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s, Edges E, double delta,
+                                                  double dsqr, double delta_st, double dsqr_st, double *err, double *err3,
+                                                  double *chi2, double *partial, Imu I, double delta_imu,
+                                                  double dsqr_imu, double *err9, double *imu_partial) {
+    __shared__ double sh[8];
+    if ((int)blockIdx.x < n_mono_blocks)
+        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, partial);
+    else if (has_imu)
+        imu_err_block(sh, s, I, delta_imu, dsqr_imu, err9, imu_partial);
 }
 
 // Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
@@ -166,12 +178,11 @@ struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lowe
 };
 
 // LDS accumulators of a workgroup: kSpan keyframes x (36 + 6)
-__global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, Edges E, Land L, Red R, double delta,
-                                                         double dsqr, double delta_st, double dsqr_st, const double *err,
-                                                         const double *err3, const double *chi2) {
-    __shared__ double acc[kSpan * 42];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const int kf0 = L.wg_kf0[blockIdx.x];
+__device__ __forceinline__ void build_land_block(int blk, double *acc, Rig rig, State s, Edges E, Land L, Red R,
+                                                 double delta, double dsqr, double delta_st, double dsqr_st,
+                                                 const double *err, const double *err3, const double *chi2) {
+    const int p = blk * blockDim.x + threadIdx.x;
+    const int kf0 = L.wg_kf0[blk];
     for (int q = threadIdx.x; q < kSpan * 42; q += blockDim.x) acc[q] = 0;
     __syncthreads();
     if (p < L.n) {
@@ -282,11 +293,10 @@ __global__ void __launch_bounds__(kLandWG) build_land_kernel(Rig rig, State s, E
 
 // ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
 
-__global__ void __launch_bounds__(64) build_imu_kernel(State s, Imu I, Red R, double delta, double dsqr, const double *err9) {
-    __shared__ double J[216];
-    __shared__ double WJ[216];   // Omega' J  (9 x 24)
-    __shared__ double om[9];
-    const int i = blockIdx.x, lane = threadIdx.x;
+__device__ __forceinline__ void build_imu_block(int i, double *sm, State s, Imu I, Red R, double delta, double dsqr,
+                                                const double *err9) {
+    double *J = sm, *WJ = sm + 216, *om = sm + 432;   // J (9 x 24), Omega' J (9 x 24), -Omega' e
+    const int lane = threadIdx.x;
     if (lane == 0) imu_jacobian(s, I, i, J);
     __syncthreads();
     const double *e = err9 + 9 * i;
@@ -354,6 +364,27 @@ __global__ void __launch_bounds__(64) build_imu_kernel(State s, Imu I, Red R, do
             if (o2 >= 0) unsafeAtomicAdd(R.b + o2 + r, -Oe);
         }
     }
+}
+
+// buildSystem in one launch (64-thread blocks): blocks [0, n_land) the landmark part, the next n_imu blocks
+// one inertial edge each.
+constexpr int kBuildLds = kSpan * 42 > 441 ? kSpan * 42 : 441;
+__global__ void __launch_bounds__(kLandWG) build_kernel(int n_land, Rig rig, State s, Edges E, Land L, Red R,
+                                                        double delta, double dsqr, double delta_st, double dsqr_st,
+                                                        const double *err, const double *err3, const double *chi2,
+                                                        Imu I, double delta_imu, double dsqr_imu, const double *err9) {
+    __shared__ double sm[kBuildLds];
+    if ((int)blockIdx.x < n_land)
+        build_land_block(blockIdx.x, sm, rig, s, E, L, R, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+    else
+        build_imu_block(blockIdx.x - n_land, sm, s, I, R, delta_imu, dsqr_imu, err9);
+}
+
+// H = 0, b = 0 before a build (one launch instead of two fills)
+__global__ void zero_kernel(double *H, size_t nH, double *b, int nb) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nH) H[q] = 0.0;
+    if (q < (size_t)nb) b[q] = 0.0;
 }
 
 // ---- trial: Schur complement into the packed block layout ------------------------------------------
@@ -899,8 +930,6 @@ struct omv_lba {
     int n_mono_all = 0, n_stereo_all = 0;   // caller edge counts (perm_edge >= n_mono_all: EdgeStereo)
     double *d_err3 = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;   // inertial edges run beside the visual kernels (fork / join events)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev[8];
     double stage_ms[4] = {0, 0, 0, 0};
     int last_trials = 0;
@@ -922,9 +951,6 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     omv_lba *h = new omv_lba();
     h->max_kf = max_kf, h->max_cams = max_cams, h->max_pts = max_pts, h->max_mono = max_mono, h->max_imu = max_imu;
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     for (auto &e : h->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipHostMalloc((void **)&h->h_out, 4 * sizeof(double), hipHostMallocDefault));
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
@@ -940,9 +966,6 @@ omv_status omv_lba_destroy(omv_lba *h) {
     free_problem(h);
     for (auto &e : h->ev) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
-    if (h->side) (void)hipStreamDestroy(h->side);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     if (h->h_out) (void)hipHostFree(h->h_out);
     delete h;
     return OMV_OK;
@@ -1251,31 +1274,14 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 }  // extern "C"
 
 // ---- the LM driver ---------------------------------------------------------------------------------
-// Fork the side stream off the main one / join it back (the inertial kernels are one workgroup each
-// and latency-bound, so they overlap the visual kernels instead of following them).
-static omv_status lba_fork(omv_lba *h) {
-    HIP_OK(hipEventRecord(h->ev_fork, h->stream));
-    HIP_OK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    return OMV_OK;
-}
-static omv_status lba_join(omv_lba *h) {
-    HIP_OK(hipEventRecord(h->ev_join, h->side));
-    HIP_OK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-    return OMV_OK;
-}
-
+// computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
 static omv_status lba_errors(omv_lba *h, const State &s) {
-    hipStream_t st = h->stream;
-    omv_status r;
-    if (h->imu_here) {
-        if ((r = lba_fork(h)) != OMV_OK) return r;
-        imu_err_kernel<<<1, 64, 0, h->side>>>(s, h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
-    }
-    if (h->n_mono > 0)
-        mono_err_kernel<<<h->n_wg_edge, 256, 0, st>>>(h->rig, s, h->E, h->delta_mono, h->dsqr_mono, h->delta_st,
-                                                       h->dsqr_st, h->d_err, h->d_err3, h->d_chi2,
-                                                       h->d_partial);
-    if (h->imu_here && (r = lba_join(h)) != OMV_OK) return r;
+    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
+    const int blocks = nmb + (h->imu_here ? 1 : 0);
+    if (blocks > 0)
+        err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s, h->E, h->delta_mono, h->dsqr_mono,
+                                                  h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, h->d_partial,
+                                                  h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
@@ -1389,18 +1395,16 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         const double iniChi = currentChi;
         // buildSystem
         HIP_OK(hipEventRecord(h->ev[0], st));
-        HIP_OK(hipMemsetAsync(h->R.H, 0, sizeof(double) * (size_t)nred * nred, st));
-        HIP_OK(hipMemsetAsync(h->R.b, 0, sizeof(double) * nred, st));
-        if (h->imu_here) {
-            if ((rs = lba_fork(h)) != OMV_OK) return rs;
-            build_imu_kernel<<<h->n_imu, 64, 0, h->side>>>(A, h->I, h->R, h->delta_imu, h->dsqr_imu, h->d_err9);
+        {
+            const size_t nH = (size_t)nred * nred;
+            zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred);
+            const int nl = h->n_pts > 0 ? gl : 0, ni_blk = h->imu_here ? h->n_imu : 0;
+            if (nl + ni_blk > 0)
+                build_kernel<<<nl + ni_blk, kLandWG, 0, st>>>(nl, h->rig, A, h->E, h->L, h->R, h->delta_mono,
+                                                              h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err,
+                                                              h->d_err3, h->d_chi2, h->I, h->delta_imu, h->dsqr_imu,
+                                                              h->d_err9);
         }
-        if (h->n_pts > 0)
-            build_land_kernel<<<gl, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono,
-                                                      h->delta_st, h->dsqr_st, h->d_err, h->d_err3,
-                                                  h->d_chi2);
-        if (h->imu_here && (rs = lba_join(h)) != OMV_OK) return rs;
-        if (h->imu_here) HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -1433,13 +1437,12 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
                 ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x, h->d_scratch,
                                                               h->d_fail);
             HIP_OK(hipEventRecord(h->ev[4], st));
-            // keyframe update beside the landmark back-substitution; both feed the trial's errors
-            if ((rs = lba_fork(h)) != OMV_OK) return rs;
-            update_kf_kernel<<<1, 256, 0, h->side>>>(h->rig, h->R, bsys, h->d_offV, h->d_offG, h->d_offA, h->n_opt,
+            // landmark back-substitution, then the keyframe update; both feed the trial's errors (one stream:
+            // a side stream's fork / join cost more than the ~10 us update)
+            update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, bsys, h->d_offV, h->d_offG, h->d_offA, h->n_opt,
                                                      lambda, h->d_x, A, B, h->d_scale_partial);
             if (h->n_pts > 0)
                 backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
-            if ((rs = lba_join(h)) != OMV_OK) return rs;
             if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
             if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc, true)) != OMV_OK) return rs;
             const int fail = sc[2] != 0.0;
