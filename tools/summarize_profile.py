@@ -34,7 +34,7 @@ def main(src, tag, images_per_launch=None, command=None):
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
              "Command: `" + (command or "rocprofv3 --kernel-trace --stats -T -- python3 bench.py --no-cpu-baseline "
-                             "--steps 5 --warmup 1 --frames 64") + "` (MI355X, one GPU).", "",
+                             "--steps 5 --warmup 1 --lba-steps 3 --pose-frames 256 --tri-pairs 64") + "` (MI355X, one GPU).", "",
              "| kernel | calls | total ms | avg us | min us | max us | share |", "|---|---|---|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
