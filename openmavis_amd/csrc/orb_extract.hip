@@ -50,6 +50,8 @@ __constant__ int c_pattern[256 * 4] = {
 #include "orb_pattern_31.inc"
 };
 __constant__ int c_umax[16];
+// intensity-centroid masks per (disc row v + 15, dword k): x = in-disc byte mask, y = byte weights u + 15
+__constant__ uint2 c_icmask[31 * 8];
 __constant__ int c_gauss7[7] = {18, 34, 48, 56, 48, 34, 18};
 
 struct LevelGeom {
@@ -773,6 +775,38 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
 }
 
 // K4 --------------------------------------------------------------------------------------------
+// LDS written by this wavefront and read back by its other lanes: LDS operations of one wave complete in
+// order, so the fence only has to stop the compiler from moving them (wavefront scope).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Horizontal 7-tap sums of the staged patch (patch byte (r, c) at dword 12 r, byte SH + c): per lane 4
+// adjacent window columns from 4 dwords, as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
+// items i = lane + 64 t, (row, quad) = (i / 10, i % 10) stepped incrementally.
+template <int SH>
+__device__ __forceinline__ void hsum_rows(const uint32_t *pw, uint16_t *Hs, int lane) {
+    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+    int r = lane / 10, jq = lane - 10 * r;
+    for (int i = lane; i < kPatchW * (kHsS / 4); i += 64) {
+        const int dw0 = r * (kPatchS / 4) + jq;
+        const uint32_t D[4] = {pw[dw0], pw[dw0 + 1], pw[dw0 + 2], pw[dw0 + 3]};
+        uint32_t h[4];
+#pragma unroll
+        for (int sc = 0; sc < 4; ++sc) {
+            const int bb = SH + sc, j = bb >> 2, al = bb & 3;
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(D[j + 1], D[j], al);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(D[j + 2 < 4 ? j + 2 : 3], D[j + 1], al);
+            h[sc] = __builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
+        }
+        *reinterpret_cast<uint2 *>(Hs + r * kHsS + 4 * jq) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        jq += 4, r += 6;
+        if (jq >= kHsS / 4) jq -= kHsS / 4, ++r;
+    }
+}
+
 struct DescArgs {
     const uint8_t *images;
     size_t img_stride, pitch0;
@@ -806,64 +840,59 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         a.n_out[img] = tot;
         a.mono[img] = mono;
     }
-    // Inactive waves (slot beyond this level's count) still take part in the block barriers.
+    // Each wave owns its LDS slices (patch[wave], hsum[wave]): wave-scope syncs only, so the four waves of a
+    // workgroup run independently and an inactive one leaves at once.
     const bool active = in_range && j < cnts[3 * l];
-    const uint32_t p = active ? a.lvl_out[(size_t)img * g.out_per_img + s] : 0u;
-    const uint32_t cl = active ? a.lvl_cls[(size_t)img * g.out_per_img + s] : 0u;
+    if (!active) return;
+    const uint32_t p = a.lvl_out[(size_t)img * g.out_per_img + s];
+    const uint32_t cl = a.lvl_cls[(size_t)img * g.out_per_img + s];
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
     const int score = (int)(p >> 24);
     int sp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
-    // stage the 43x43 patch (row stride kPatchS): interior patches as 12 aligned dwords per row, all
-    // loads issued before any LDS store; patches touching the level border take reflect101 byte loads
+    // stage the 43x43 patch (row stride kPatchS): interior patches as 12 aligned dwords per row (lane ->
+    // row lane / 12 + 5k, dword lane % 12 for lanes < 60), all loads issued before any LDS store; patches
+    // touching the level border take reflect101 byte loads
     uint8_t *P = patch[wave];
     const int x0 = cx - kPatchR, y0 = cy - kPatchR;
     const bool inner = x0 >= 0 && y0 >= 0 && x0 + kPatchW <= L.w && y0 + kPatchW <= L.h && (sp & 3) == 0 &&
                        (((uintptr_t)src) & 3) == 0;
-    if (active && inner) {
+    if (inner) {
         const uint8_t *r0 = src + (size_t)y0 * sp + x0;
         const int o = (int)(((uintptr_t)r0) & 3);
-        const uint32_t *g0 = (const uint32_t *)(r0 - o);
-        const int sw = sp >> 2;
+        const int lr = lane / 12, lc = lane - 12 * lr;
+        const uint32_t *g0 = (const uint32_t *)(r0 - o) + (size_t)lr * (sp >> 2) + lc;
+        const size_t step = (size_t)5 * (sp >> 2);
         uint32_t v[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int d = lane + 64 * k;
-            if (d < kPatchW * 12) v[k] = g0[(size_t)(d / 12) * sw + d % 12];
-        }
+        for (int k = 0; k < 9; ++k)
+            if (lane < 60 && lr + 5 * k < kPatchW) v[k] = g0[k * step];
+        uint32_t *l0 = reinterpret_cast<uint32_t *>(P) + lane;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int d = lane + 64 * k;
-            if (d < kPatchW * 12) reinterpret_cast<uint32_t *>(P)[d] = v[k];
-        }
+        for (int k = 0; k < 9; ++k)
+            if (lane < 60 && lr + 5 * k < kPatchW) l0[60 * k] = v[k];
         P += o;
-    } else if (active) {
+    } else {
         for (int i = lane; i < kPatchW * kPatchW; i += 64) {
             const int r = i / kPatchW, q = i - r * kPatchW;
             const int yy = omv::reflect101(y0 + r, L.h), xx = omv::reflect101(x0 + q, L.w);
             P[r * kPatchS + q] = src[(size_t)yy * sp + xx];
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     // intensity centroid over the r = 15 disc (umax rows), exact integer sums: per (row v, dword k of the
     // row's columns u = 4k + b - 15) one v_dot4 of the pixels with the in-disc mask (row sum, for m01) and
-    // one with the weights u + 15 (m10 = sum (u + 15) I - 15 sum I)
+    // one with the weights u + 15 (m10 = sum (u + 15) I - 15 sum I); masks from c_icmask
     const int pofs = (int)(P - patch[wave]);
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch[wave]);
     int m01 = 0, m10 = 0;
     for (int i = lane; i < 31 * 8; i += 64) {
         const int vr = i >> 3, k = i & 7, v = vr - 15;
-        const int av = v < 0 ? -v : v, um = c_umax[av];
+        const uint2 mk = c_icmask[i];
         const int off = pofs + (kPatchR + v) * kPatchS + 6 + 4 * k, dwi = off >> 2, sh = off & 3;
         const uint32_t w = __builtin_amdgcn_alignbyte(pw[dwi + 1], pw[dwi], sh);
-        uint32_t msk = 0, wu = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int u = 4 * k + b - 15;
-            if (u <= 15 && (u < 0 ? -u : u) <= um) msk |= 1u << (8 * b), wu |= (uint32_t)(u + 15) << (8 * b);
-        }
-        const int rs = (int)__builtin_amdgcn_udot4(w, msk, 0u, false);
-        m10 += (int)__builtin_amdgcn_udot4(w, wu, 0u, false) - 15 * rs;
+        const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
+        m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
         m01 += v * rs;
     }
     for (int d = 32; d >= 1; d >>= 1) {
@@ -875,26 +904,13 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
     // rows x 37 window columns, 7 taps as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
     // vertical ((sum + 2^15) >> 16) evaluated only at the 512 steered sample points.
     uint16_t *Hs = hsum[wave];
-    {
-        // 4 adjacent window columns per lane from 4 dwords (one shared alignment sh = pofs & 3)
-        constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-        const int sh = pofs & 3;
-        for (int i = lane; i < kPatchW * (kHsS / 4); i += 64) {
-            const int r = i / (kHsS / 4), jq = i - r * (kHsS / 4);
-            const int dw0 = (pofs + r * kPatchS) / 4 + jq;   // kPatchS and 4 jq are dword multiples
-            const uint32_t D[4] = {pw[dw0], pw[dw0 + 1], pw[dw0 + 2], pw[dw0 + 3]};
-            uint32_t h[4];
-#pragma unroll
-            for (int sc = 0; sc < 4; ++sc) {
-                const int b = sh + sc, j = b >> 2, a = b & 3;
-                const uint32_t w0 = __builtin_amdgcn_alignbyte(D[j + 1], D[j], a);
-                const uint32_t w1 = __builtin_amdgcn_alignbyte(D[j + 2 < 4 ? j + 2 : 3], D[j + 1], a);
-                h[sc] = __builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
-            }
-            *reinterpret_cast<uint2 *>(Hs + r * kHsS + 4 * jq) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        }
+    switch (pofs & 3) {   // the byte alignment of the patch is wave-uniform: one specialised loop each
+        case 0: hsum_rows<0>(pw, Hs, lane); break;
+        case 1: hsum_rows<1>(pw, Hs, lane); break;
+        case 2: hsum_rows<2>(pw, Hs, lane); break;
+        default: hsum_rows<3>(pw, Hs, lane); break;
     }
-    __syncthreads();
+    wave_lds_sync();
     auto blurred = [&](int r, int q) {   // window coordinates (0..36)
         uint32_t acc = 0;
 #pragma unroll
@@ -919,7 +935,6 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
         const int ib = blurred(kWinR + bdy, kWinR + bdx);
         words[rd] = __ballot(ia < ib);
     }
-    if (!active) return;   // after the last barrier
     // final row: monoIndex order (front) or lapping order (back, reversed)
     int mono_before = 0, lap_before = 0, total = 0;
     for (int q = 0; q < g.nlevels; ++q) {
@@ -1201,6 +1216,20 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     HIP_OK(hipMalloc(&o->d_err, sizeof(int)));
     HIP_OK(hipMemset(o->d_err, 0, sizeof(int)));
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), o->umax, sizeof(o->umax)));
+    {
+        uint2 icm[31 * 8];
+        for (int vr = 0; vr < 31; ++vr)
+            for (int k = 0; k < 8; ++k) {
+                const int av = vr < 15 ? 15 - vr : vr - 15, um = o->umax[av];
+                uint32_t msk = 0, wu = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int u = 4 * k + b - 15;
+                    if (u <= 15 && std::abs(u) <= um) msk |= 1u << (8 * b), wu |= (uint32_t)(u + 15) << (8 * b);
+                }
+                icm[vr * 8 + k] = make_uint2(msk, wu);
+            }
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icm, sizeof(icm)));
+    }
     *out = o;
     return OMV_OK;
 }
