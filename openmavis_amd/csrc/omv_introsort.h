@@ -174,4 +174,111 @@ OMV_HD inline void libstdcxx_sort(SortItem *arr, int n, int *stack) {
     }
 }
 
+
+#ifdef __HIPCC__
+// ---- the same sort, data-parallel on the device ----------------------------------------------------
+// wave_introsort_loop: __introsort_loop by one wavefront (all 64 lanes, uniform control flow).  The
+// sequential __unguarded_partition(first + 1, last, pivot = first) is computed from the original values:
+// with LS = ascending positions in [first+1, last) whose item is not < pivot ("left stoppers") and
+// RS = descending positions in [first, last) whose item is not > pivot (the pivot itself included), the
+// k-th iteration swaps LS[k-1] <-> RS[k-1] while LS[k-1] < RS[k-1]; at the first K with LS[K-1] >= RS[K-1]
+// the scan returns min(LS[K-1], RS[K-2]) (a missing LS entry or K = 1 drops that term).  Before the
+// crossing neither scan reaches a swapped position, so every stopper is an original one.  The median
+// and the (rare) heapsort fallback run on lane 0.
+// block_final_insertion_sort: __final_insertion_sort is a stable insertion sort of the whole range, i.e.
+// item i goes to rank #{j : (k1, k2, j) < (k1_i, k2_i, i)}; every thread of the block ranks its items.
+__device__ __forceinline__ void sort_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline int wave_unguarded_partition(SortItem *arr, int f, int l, int *LS, int *RS, int lane) {
+    const SortItem p = arr[f];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int nL = 0, nR = 0;
+    for (int base = f + 1; base < l; base += 64) {
+        const int x = base + lane;
+        const bool fl = x < l && !item_less(arr[x], p);
+        const unsigned long long m = __ballot(fl);
+        if (fl) LS[nL + __popcll(m & lt)] = x;
+        nL += __popcll(m);
+    }
+    for (int base = l - 1; base >= f; base -= 64) {
+        const int y = base - lane;
+        const bool fl = y >= f && !item_less(p, arr[y]);
+        const unsigned long long m = __ballot(fl);
+        if (fl) RS[nR + __popcll(m & lt)] = y;
+        nR += __popcll(m);
+    }
+    sort_wave_sync();
+    int K = 0;   // crossing iteration, 1-based
+    for (int k0 = 0;; k0 += 64) {
+        const int k = k0 + lane;
+        const int lsv = k < nL ? LS[k] : 0x7fffffff;
+        const int rsv = k < nR ? RS[k] : -0x7fffffff;
+        const unsigned long long m = __ballot(lsv >= rsv);
+        if (m) {
+            K = k0 + __ffsll((long long)m);
+            break;
+        }
+    }
+    const int cut = min(K - 1 < nL ? LS[K - 1] : 0x7fffffff, K >= 2 ? RS[K - 2] : 0x7fffffff);
+    for (int q = lane; q < K - 1; q += 64) {   // disjoint positions: LS[q] < RS[q], both monotone
+        const int i = LS[q], j = RS[q];
+        const SortItem u = arr[i], v = arr[j];
+        arr[i] = v;
+        arr[j] = u;
+    }
+    sort_wave_sync();
+    return cut;
+}
+
+// `stack`: 3*(2*lg(n)+2) ints; LS, RS: n ints each (LDS).
+__device__ inline void wave_introsort_loop(SortItem *arr, int n, int *stack, int *LS, int *RS, int lane) {
+    const int kThreshold = 16;
+    if (n <= 1) return;
+    int sp = 0;
+    int first = 0, last = n, depth = 2 * floor_log2(n);
+    for (;;) {
+        while (last - first > kThreshold) {
+            if (depth == 0) {
+                if (lane == 0) heap_sort(arr + first, last - first);
+                sort_wave_sync();
+                last = first;
+                break;
+            }
+            --depth;
+            const int mid = first + (last - first) / 2;
+            if (lane == 0) median_to_first(&arr[first], &arr[first + 1], &arr[mid], &arr[last - 1]);
+            sort_wave_sync();
+            const int cut = wave_unguarded_partition(arr, first, last, LS, RS, lane);
+            stack[sp] = first, stack[sp + 1] = cut, stack[sp + 2] = depth;   // every lane stores the same value
+            sp += 3;
+            first = cut;
+        }
+        if (sp == 0) break;
+        sort_wave_sync();
+        sp -= 3;
+        first = stack[sp], last = stack[sp + 1], depth = stack[sp + 2];
+    }
+}
+
+// All threads of the block; tmp: n items of scratch.  Requires k1 >= 0, 0 <= k2 < 2^20, n <= 4096.
+__device__ inline void block_final_insertion_sort(SortItem *arr, int n, SortItem *tmp, int tid, int T) {
+    auto key = [](const SortItem &a, int i) {
+        return ((unsigned long long)(unsigned)a.k1 << 32) | ((unsigned long long)(unsigned)a.k2 << 12) | (unsigned)i;
+    };
+    for (int i = tid; i < n; i += T) {
+        const unsigned long long c = key(arr[i], i);
+        int r = 0;
+        for (int j = 0; j < n; ++j) r += key(arr[j], j) < c ? 1 : 0;
+        tmp[r] = arr[i];
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += T) arr[i] = tmp[i];
+    __syncthreads();
+}
+#endif
+
 }  // namespace omv

@@ -517,6 +517,10 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     omv::SortItem *items = reinterpret_cast<omv::SortItem *>(buf + 20 * NC);   // NC items (3 ints)
     int *sstack = buf + 23 * NC;     // 192
 
+#ifdef OMV_OCT_PROFILE
+    long long pf_t0 = wall_clock64(), pf_sort = 0, pf_p1 = 0, pf_p2 = 0, pf_gather = 0;
+    int pf_r1 = 0, pf_r2 = 0;
+#endif
     const int ncell = L.cell_end - L.cell_begin;
     uint32_t *cand = a.cand + (size_t)img * g.cand_per_img + L.cand_off;
     uint32_t *nid = a.nid + (size_t)img * g.cand_per_img + L.cand_off;
@@ -590,6 +594,9 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     for (int k = tid; k < K; k += T) nid[k] = (uint32_t)scanA[nid[k]];
     __syncthreads();
 
+#ifdef OMV_OCT_PROFILE
+    pf_gather = wall_clock64() - pf_t0;
+#endif
     // ---- subdivision rounds ----
     // phase 1: every node with > 1 key splits (list walk :562-613)
     // phase 2: only the expandable list of the last round, largest (size, UL.x) first (:621-679)
@@ -597,6 +604,10 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     int nv = 0;   // phase 2: |V|, V stored in vlist (indices into A, creation order)
     for (int guard = 0; guard < 4096; ++guard) {
         const int prev = m;
+#ifdef OMV_OCT_PROFILE
+        const long long pf_r = wall_clock64();
+        const bool pf_ph2 = phase2;
+#endif
         // 1. mark which nodes split this round, zero child counts
         for (int i = tid; i < m; i += T) {
             map[i] = -1;
@@ -607,12 +618,17 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         if (!phase2) {
             for (int i = tid; i < m; i += T) vpos[i] = A.cnt[i] > 1 ? 0 : -1;
         } else {
-            // sort V by (size, UL.x) with the libstdc++ introsort replica (one lane)
-            if (tid == 0) {
-                for (int j = 0; j < nv; ++j) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
-                omv::libstdcxx_sort(items, nv, sstack);
-            }
+            // sort V by (size, UL.x) exactly as libstdc++'s std::sort moves the elements: the introsort
+            // partitions on wave 0, the final insertion sort as a stable rank over the block (B is free
+            // until step 4: its x0 / x1 / y0 rows hold the items' scratch)
+            for (int j = tid; j < nv; j += T) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
             __syncthreads();
+            if ((tid >> 6) == 0) omv::wave_introsort_loop(items, nv, sstack, scanA, scanB, tid & 63);
+            __syncthreads();
+            omv::block_final_insertion_sort(items, nv, reinterpret_cast<omv::SortItem *>(B.x0), tid, T);
+#ifdef OMV_OCT_PROFILE
+            pf_sort += wall_clock64() - pf_r;
+#endif
             for (int j = tid; j < nv; j += T) vpos[items[j].payload] = j;
         }
         __syncthreads();
@@ -645,20 +661,22 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
             n_proc_nodes = m;   // scan domain
         } else {
             // divide from the back of the sorted list until the list holds >= N nodes (:633-675)
-            if (tid == 0) {
-                int size = m, jstar = nv;
-                for (int j = nv - 1; j >= 0; --j) {
-                    const int n = items[j].payload;
-                    int nk = 0;
-                    for (int t = 0; t < 4; ++t) nk += ccnt[4 * n + t] > 0;
-                    size += nk - 1;
-                    jstar = j;
-                    if (size >= N) break;
-                }
-                shared_int[0] = jstar;
+            // the list size after dividing items[nv-1 .. j] is m + sum (children - 1) over them: a suffix
+            // sum (block scan over r = nv-1-j); the walk stops at the first r reaching N, else at j = 0
+            int *dv = B.cnt, *dv1 = B.y1;   // B is free until step 4
+            for (int r = tid; r < nv; r += T) {
+                const int n = items[nv - 1 - r].payload;
+                int nk = 0;
+                for (int t = 0; t < 4; ++t) nk += ccnt[4 * n + t] > 0;
+                dv[r] = dv1[r] = nk - 1;
             }
+            if (tid == 0) shared_int[0] = nv;
             __syncthreads();
-            const int jstar = shared_int[0];
+            block_excl_scan(dv, nv, tmp);
+            for (int r = tid; r < nv; r += T)
+                if (m + dv[r] + dv1[r] >= N) atomicMin(&shared_int[0], r);
+            __syncthreads();
+            const int jstar = shared_int[0] < nv ? nv - 1 - shared_int[0] : 0;
             n_proc_nodes = nv - jstar;
             // processing position p = 0.. corresponds to items[nv-1-p]
             for (int p = tid; p < n_proc_nodes; p += T) {
@@ -728,6 +746,10 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         }
         __syncthreads();
         m = newm;
+#ifdef OMV_OCT_PROFILE
+        if (pf_ph2) pf_p2 += wall_clock64() - pf_r, ++pf_r2;
+        else pf_p1 += wall_clock64() - pf_r, ++pf_r1;
+#endif
         if (m >= N || m == prev) break;
         if (!phase2) {
             if (m + nexp * 3 > N) phase2 = true;
@@ -772,6 +794,11 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         cnt_out[1] = m - nlap;
         cnt_out[2] = nlap;
     }
+#ifdef OMV_OCT_PROFILE
+    if (tid == 0 && img < 2)
+        printf("oct img %d level %d K %d N %d m %d ticks(100MHz) total %lld gather %lld p1 %lld (%d rounds) p2 %lld (%d rounds, sort %lld)\n",
+               img, l, K, N, m, wall_clock64() - pf_t0, pf_gather, pf_p1, pf_r1, pf_p2, pf_r2, pf_sort);
+#endif
 }
 
 // K4 --------------------------------------------------------------------------------------------

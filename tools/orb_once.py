@@ -5,6 +5,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("OMV_LIB"):   # e.g. a -DOMV_OCT_PROFILE build of the library
+    from openmavis_amd import _lib  # noqa: E402
+    _lib.load(os.environ["OMV_LIB"])
 
 
 def main():
