@@ -498,6 +498,16 @@ __device__ __forceinline__ void wave_sync() {
     }
 }
 
+// 1 / x by v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; the pivots are normal
+// numbers -- a zero / non-finite pivot is flagged by the caller)
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
 // One wavefront: D = L diag(d) L^T in place (unit L strictly below the diagonal, d on it) and W = L^-1
 // by the same eliminations, stored transposed in the strict upper triangle (W[j][i] at D[i][j], i < j).
 // Eight passes, each eliminating a 2x2 pivot block (c0, c0+1): with P = [p00 .; p10 p11],
@@ -515,6 +525,7 @@ __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
     double cur[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) cur[t] = D[lane + 64 * t];
+#pragma unroll
     for (int c0 = 0; c0 < 16; c0 += 2) {
         const double p00 = D[c0 * 17], p10 = D[(c0 + 1) * 16 + c0], p11 = D[(c0 + 1) * 17];
         double bi0[4], bi1[4];
@@ -524,31 +535,35 @@ __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
             bi1[t] = D[(q + 4 * t) * 16 + c0 + 1];
         }
         const double bj0 = D[j * 16 + c0], bj1 = D[j * 16 + c0 + 1];
-        const double i0 = 1.0 / p00;
+        // the two reciprocals are independent (d1 = det / p00, 1 / d1 = p00 / det): one latency, not two
+        const double det = p00 * p11 - p10 * p10;
+        const double i0 = rcp_nr(p00), idet = rcp_nr(det);
         const double l = p10 * i0;
-        const double d1 = p11 - l * p10;
-        const double i1 = 1.0 / d1;
+        const double d1 = det * i0;
+        const double i1 = p00 * idet;
         if (lane == 0 && !(p00 != 0.0 && isfinite(p00) && d1 != 0.0 && isfinite(d1))) *bad = 1;
         const double uj = bj1 - l * bj0;
         const double lb0 = bj0 * i0, lb1 = uj * i1;   // L_B row j (used when j is below the pivot)
+        // every candidate value computed, then selected (v_cndmask): the cases are mutually exclusive, and
+        // a branchy form costs more in exec-mask flow than the arithmetic it skips
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = q + 4 * t;
             const double x = cur[t];
             const double ui = bi1[t] - l * bi0[t];
+            const double trail = x - bi0[t] * bj0 * i0 - ui * uj * i1;
+            const double w0 = i == c0 ? 1.0 : (i == c0 + 1 ? 0.0 : bi0[t]);
+            const double w1 = i == c0 ? -l : (i == c0 + 1 ? 1.0 : ui);
+            const double base = i < c0 ? x : 0.0;
+            const double upv = j == c0 + 1 ? base - l * w0 : base - (lb0 * w0 + lb1 * w1);
+            const bool lower = i >= j;
             double r = x;
-            if (i >= j) {
-                if (j > c0 + 1) r = x - bi0[t] * bj0 * i0 - ui * uj * i1;
-                else if (j == c0 && i > c0 + 1) r = bi0[t] * i0;
-                else if (j == c0 + 1 && i > c0 + 1) r = ui * i1;
-                else if (i == c0 + 1 && j == c0) r = l;
-                else if (i == c0 + 1 && j == c0 + 1) r = d1;
-            } else if (j > c0 && i <= c0 + 1 && !(i == c0 + 1 && j == c0 + 1)) {
-                const double w0 = i == c0 ? 1.0 : (i == c0 + 1 ? 0.0 : bi0[t]);
-                const double w1 = i == c0 ? -l : (i == c0 + 1 ? 1.0 : ui);
-                const double base = i < c0 ? x : 0.0;
-                r = j == c0 + 1 ? base - l * w0 : base - (lb0 * w0 + lb1 * w1);
-            }
+            r = (lower && j > c0 + 1) ? trail : r;
+            r = (lower && j == c0 && i > c0 + 1) ? bi0[t] * i0 : r;
+            r = (lower && j == c0 + 1 && i > c0 + 1) ? ui * i1 : r;
+            r = (lower && i == c0 + 1 && j == c0) ? l : r;
+            r = (lower && i == c0 + 1 && j == c0 + 1) ? d1 : r;
+            r = (!lower && j > c0 && i <= c0 + 1 && !(i == c0 + 1 && j == c0 + 1)) ? upv : r;
             cur[t] = r;
         }
         if (j == c0 + 2 || j == c0 + 3) {
@@ -574,7 +589,7 @@ __device__ __forceinline__ void panel16(double *A, const double *Dk, int lane) {
         const double b = kk < rc ? Dk[kk * 16 + rc] : (kk == rc ? 1.0 : 0.0);   // (L^-T)[kk][col]
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
-    const double id = 1.0 / Dk[rc * 17];
+    const double id = rcp_nr(Dk[rc * 17]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) A[(kq + 4 * i) * 16 + rc] = acc[i] * id;
 }
