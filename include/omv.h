@@ -50,6 +50,12 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
                           omv_orb **out);
 omv_status omv_orb_destroy(omv_orb *orb);
 
+/* Test hook (no reference counterpart): the device replica of libstdc++'s std::sort that the octree
+ * uses for DistributeOctTree's compareNodes order (src/ORBextractor.cc:482-494, :629-632), on one
+ * array of n <= 2048 (k1, k2) pairs with k1 >= 0, 0 <= k2 < 2^20 (device memory); perm receives the
+ * original indices in sorted order. */
+omv_status omv_selftest_node_sort(const int *k1, const int *k2, int n, int *perm, void *stream);
+
 /* Upper bound on keypoints one image can produce (output row capacity N_max).  The reference can
  * return up to quota+2 keypoints per level (DistributeOctTree :673 stops at >= N). */
 int omv_orb_max_keypoints(const omv_orb *orb);

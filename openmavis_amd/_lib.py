@@ -192,6 +192,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 SIGNATURES = {
     "omv_orb_create": (_I, [ctypes.POINTER(OrbParams), _I, _I, _I, ctypes.POINTER(_VP)]),
     "omv_orb_destroy": (_I, [_VP]),
+    "omv_selftest_node_sort": (_I, [_VP, _VP, _I, _VP, _VP]),
     "omv_orb_max_keypoints": (_I, [_VP]),
     "omv_orb_scale_tables": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "omv_orb_extract_batch": (_I, [_VP, _I, _VP, _SZ, _SZ, _VP, _VP, _VP, _VP, _VP, _VP]),

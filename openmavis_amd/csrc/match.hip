@@ -227,46 +227,80 @@ __device__ __forceinline__ float window_radius(const FrameArgs &f, const MpArgs 
     return r * f.scale[m.level[bc]];
 }
 
-// One thread per (frame, map point, camera).
+// Candidates per (frame, map point, camera).
 // Per-point flag word for the resolve stage: bits 0..C-1 in_view per camera, bit 16 skipped
 // (mp_skipped), bit 17 has observations.
 constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
 
+// Work compaction: a point is in view in ~1-2 of the C cameras, so a wave over consecutive (point, camera)
+// slots would idle most lanes through the window scans.  Each wave takes kCandChunk consecutive slots,
+// writes the empty records of the inactive ones directly, compacts the active slots into an LDS queue
+// (ballot prefix, slot order kept) and scans them 64 at a time.
+constexpr int kCandChunk = 192;
+
 __global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
                                                    const uint8_t *occ_init, Rec *recs, int *counts, int *flags,
                                                    int far_points, float th_far) {
+    __shared__ int queue[4][kCandChunk];
     const int C = f.n_cams;
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long long)n_frames * m.M * C) return;
-    const int c = (int)(gid % C);
-    const long long fm = gid / C;
-    const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
-    const size_t bc = (size_t)fm * C + c;
-    if (c == 0) {
-        int fl = 0;
-        for (int q = 0; q < C; ++q) fl |= m.in_view[(size_t)fm * C + q] ? (1 << q) : 0;
-        if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
-        if (m.has_obs[fm]) fl |= kFlagObs;
-        flags[fm] = fl;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long total = (long long)n_frames * m.M * C;
+    const long long g0 = ((long long)blockIdx.x * 4 + wave) * kCandChunk;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int nq = 0;
+    for (int s0 = 0; s0 < kCandChunk; s0 += 64) {
+        const long long gid = g0 + s0 + lane;
+        bool act = false;
+        if (gid < total) {
+            const int c = (int)(gid % C);
+            const long long fm = gid / C;
+            const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
+            const size_t bc = (size_t)gid;
+            if (c == 0) {
+                int fl = 0;
+                for (int q = 0; q < C; ++q) fl |= m.in_view[(size_t)fm * C + q] ? (1 << q) : 0;
+                if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
+                if (m.has_obs[fm]) fl |= kFlagObs;
+                flags[fm] = fl;
+            }
+            const int lvl = m.level[bc];
+            act = m.in_view[bc] && lvl >= 0 && lvl < f.nlevels;
+            if (!act) {
+                uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
+#pragma unroll
+                for (int v = 0; v < kTop / 4; ++v) o4[v] = make_uint4(0u, 0u, 0u, 0u);
+                counts[bc] = 0;
+            }
+        }
+        const uint64_t am = __ballot(act);
+        if (act) queue[wave][nq + __popcll(am & lt)] = s0 + lane;
+        nq += __popcll(am);
     }
-    Rec &out = recs[bc];
-    Top t;
-    t.reset();
-    const int lvl = m.level[bc];
-    if (m.in_view[bc] && lvl >= 0 && lvl < f.nlevels) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int q0 = 0; q0 < nq; q0 += 64) {
+        if (q0 + lane >= nq) break;
+        const long long gid = g0 + queue[wave][q0 + lane];
+        const int c = (int)(gid % C);
+        const long long fm = gid / C;
+        const int frame = (int)(fm / m.M);
+        const size_t bc = (size_t)gid;
+        Top t;
+        t.reset();
         uint64_t dmp[4];
         load_desc(m.desc + (size_t)fm * 32, dmp);
         const float r = window_radius(f, m, bc, c, th, th != 1.0f);
         const uint8_t *occ = occ_init ? occ_init + (size_t)frame * C * f.kp_cap : nullptr;
-        scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, lvl - 1, lvl, dmp,
+        scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp,
                     [&](int slot) { return occ && occ[slot]; }, t);
-    }
-    uint4 *o4 = reinterpret_cast<uint4 *>(&out);   // 64-B record as four 16-B stores
+        uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);   // 64-B record as four 16-B stores
 #pragma unroll
-    for (int v = 0; v < kTop / 4; ++v)
-        o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
-                           4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
-    counts[bc] = t.count;
+        for (int v = 0; v < kTop / 4; ++v)
+            o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
+                               4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
+        counts[bc] = t.count;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1435,7 +1469,7 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
-        cand_kernel<<<(int)((tot + 255) / 256), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs,
+        cand_kernel<<<(int)((tot + 4 * kCandChunk - 1) / (4 * kCandChunk)), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs,
                                                               h->d_counts, h->d_flags, far_points, th_far);
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;

@@ -387,7 +387,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 }
             }
             const uint64_t m = __ballot(keep);
-            if (out && keep) out[base + __popcll(m & lt)] = packed;
+            const int pos = base + __popcll(m & lt);
+            if (out && keep && pos < g.cell_cap) out[pos] = packed;
             base += __popcll(m);
         }
         return base;
@@ -395,21 +396,19 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     // iniThFAST first; minThFAST only for a cell without an iniTh keypoint (ORBextractor.cc:745-782).  Every
     // pixel with S > th passes the compass prefilter at th, so the iniTh pass only needs those candidates:
     // the NMS treats non-candidates (S = 0) as the reference treats scores <= th.
+    // keypoints are emitted row-major by the counting pass itself (coordinates relative to the FAST border,
+    // minBorder = 16); a cell without an iniTh keypoint wrote nothing and is redone at minTh
+    uint32_t *out = cell_kp + (size_t)blockIdx.x * g.cell_cap;
     int th = g.ini_th;
     int ncand = prefilter(th);
-    int total = nms(ncand, th, nullptr);
+    int total = nms(ncand, th, out);
     if (total == 0) {
         th = g.min_th;
         ncand = prefilter(th);
-        total = nms(ncand, th, nullptr);
+        total = nms(ncand, th, out);
     }
-    if (total > g.cell_cap) {   // cannot happen by construction (cap = max NMS survivors)
-        if (lane == 0) cell_cnt[blockIdx.x] = -1;
-        return;
-    }
-    // emit row-major; coordinates relative to the FAST border (minBorder = 16)
-    nms(ncand, th, cell_kp + (size_t)blockIdx.x * g.cell_cap);
-    if (lane == 0) cell_cnt[blockIdx.x] = total;
+    // cap = max NMS survivors of the window, so this cannot trigger (writes past it were dropped)
+    if (lane == 0) cell_cnt[blockIdx.x] = total > g.cell_cap ? -1 : total;
 }
 
 // K3 --------------------------------------------------------------------------------------------
@@ -992,6 +991,20 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
 
 inline int host_round_even(float v) { return (int)std::nearbyint(v); }
 
+// Test hook: the octree's device sort (wave_introsort_loop + block_final_insertion_sort) on one array.
+__global__ void __launch_bounds__(256) node_sort_selftest_kernel(const int *k1, const int *k2, int n, int *perm) {
+    extern __shared__ __attribute__((aligned(16))) int ssm[];
+    omv::SortItem *items = reinterpret_cast<omv::SortItem *>(ssm);
+    omv::SortItem *tmp = items + n;
+    int *LS = reinterpret_cast<int *>(tmp + n), *RS = LS + n, *stk = RS + n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = omv::SortItem{k1[i], k2[i], i};
+    __syncthreads();
+    if (threadIdx.x < 64) omv::wave_introsort_loop(items, n, stk, LS, RS, threadIdx.x);
+    __syncthreads();
+    omv::block_final_insertion_sort(items, n, tmp, threadIdx.x, blockDim.x);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = items[i].payload;
+}
+
 }  // namespace
 
 struct omv_orb {
@@ -1009,6 +1022,7 @@ struct omv_orb {
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
     int rmax = 0;
+    size_t fast_lds = 0;   // K2 dynamic LDS: region + strength map (rmax each) + the candidate list (u16)
     size_t oct_lds = 0;
     size_t pyr_lds[kMaxLevels] = {};   // K1 dynamic LDS per level: x table + the widest row block
     // host staging for the synchronous path
@@ -1181,6 +1195,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.node_cap = std::max(max_nodes, max_cells_lvl);
     g.node_cap = (g.node_cap + 15) & ~15;
     o->rmax = ((max_rw + 6) & ~3) * max_rh;   // LDS row stride rounds (rw + misalignment) up to 4 bytes
+    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
     o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
     return OMV_OK;
 }
@@ -1304,7 +1319,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    fast_cells_kernel<<<g.n_cells * n, 64, 4 * o->rmax, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
+    fast_cells_kernel<<<g.n_cells * n, 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
                                                                o->d_cell_cnt, o->d_cell_kp, o->rmax);
     mark(o, st);
     // K3: octree per (image, level)
@@ -1383,6 +1398,17 @@ omv_status omv_orb_debug_level(omv_orb *o, int img, int level, uint8_t *out, int
     HIP_OK(hipMemcpy2D(out, L.w, o->d_pyr + (size_t)img * o->g.pyr_bytes + L.off, L.pitch, L.w, L.h,
                        hipMemcpyDeviceToHost));
     return OMV_OK;
+}
+
+omv_status omv_selftest_node_sort(const int *k1, const int *k2, int n, int *perm, void *stream) {
+    if (n < 0 || n > 2048 || (n > 0 && (!k1 || !k2 || !perm))) return OMV_ERR_ARG;
+    if (n == 0) return OMV_OK;
+    const size_t lds = (size_t)n * (2 * sizeof(omv::SortItem) + 2 * sizeof(int)) + 192 * sizeof(int);
+    if (hipFuncSetAttribute((const void *)node_sort_selftest_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+        return OMV_ERR_HIP;
+    node_sort_selftest_kernel<<<1, 256, lds, (hipStream_t)stream>>>(k1, k2, n, perm);
+    return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
 }  // extern "C"

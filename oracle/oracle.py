@@ -40,6 +40,15 @@ def _p(a):
     return p
 
 
+def std_sort_pairs(k1, k2):
+    """libstdc++ std::sort of (k1, k2) pairs (compareNodes order): the sorted original indices."""
+    k1 = np.ascontiguousarray(k1, np.int32)
+    k2 = np.ascontiguousarray(k2, np.int32)
+    perm = np.zeros(len(k1), np.int32)
+    lib().oracle_std_sort_pairs(_p(k1), _p(k2), ctypes.c_int(len(k1)), _p(perm))
+    return perm
+
+
 def orb_tables(nfeatures=1200, scale=1.2, nlevels=8):
     sc, isc, s2, is2 = (np.zeros(nlevels, np.float32) for _ in range(4))
     q = np.zeros(nlevels, np.int32)

@@ -498,6 +498,17 @@ struct oracle_kp {
     int32_t octave;
 };
 
+// libstdc++'s std::sort itself with compareNodes' order (src/ORBextractor.cc:482-494: size, then UL.x;
+// ties left to the algorithm): the expected permutation for omv_selftest_node_sort.
+int oracle_std_sort_pairs(const int *k1, const int *k2, int n, int *perm) {
+    struct E { int a, b, id; };
+    std::vector<E> v(n);
+    for (int i = 0; i < n; ++i) v[i] = E{k1[i], k2[i], i};
+    std::sort(v.begin(), v.end(), [](const E &x, const E &y) { return x.a < y.a || (x.a == y.a && x.b < y.b); });
+    for (int i = 0; i < n; ++i) perm[i] = v[i].id;
+    return 0;
+}
+
 static oracle::Img wrap(const uint8_t *img, int w, int h, int stride) {
     oracle::Img im;
     im.w = w, im.h = h;

@@ -86,3 +86,34 @@ def test_flat_image_has_no_keypoints():
     ex = ORBextractor(500, 1.2, 8, 20, 7)
     mono, kps, desc = ex(np.full((240, 320), 77, np.uint8), None, (0, 0))
     assert mono == 0 and len(kps) == 0
+
+
+def test_octree_device_sort_matches_std_sort(oracle, torch_cuda):
+    """The octree's data-parallel std::sort replica (omv_introsort.h) moves tie-equal nodes exactly like
+    libstdc++'s std::sort: adversarial arrays (few distinct keys, reversed input, a median-of-3 pattern
+    that reaches the heapsort fallback), compared permutation for permutation."""
+    torch = torch_cuda
+    from openmavis_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(1234)
+    for trial in range(400):
+        n = trial if trial < 40 else int(rng.integers(0, 2049))
+        kmax, xmax = int(rng.integers(1, 7)), int(rng.integers(1, 5))
+        k1 = rng.integers(0, kmax, n).astype(np.int32)
+        k2 = rng.integers(0, xmax, n).astype(np.int32)
+        if trial % 7 == 0:
+            k1, k2 = k1[::-1].copy(), k2[::-1].copy()
+        if trial % 11 == 0:
+            i = np.arange(n)
+            k1 = np.where(i % 2 == 1, i, n - i).astype(np.int32)
+            k2 = np.zeros(n, np.int32)
+        if trial % 13 == 0:
+            k1 = rng.integers(0, 3000, n).astype(np.int32)
+            k2 = rng.integers(0, 4096, n).astype(np.int32)
+        want = oracle.std_sort_pairs(k1, k2)
+        d1, d2 = torch.from_numpy(k1).cuda(), torch.from_numpy(k2).cuda()
+        perm = torch.full((max(n, 1),), -1, dtype=torch.int32, device="cuda")
+        assert lib.omv_selftest_node_sort(d1.data_ptr(), d2.data_ptr(), n, perm.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        got = perm.cpu().numpy()[:n]
+        assert np.array_equal(got, want), f"trial {trial} n {n}: first mismatch at {np.argmax(got != want)}"
