@@ -171,6 +171,17 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     }
 }
 
+// XCD-aware block order: the dispatcher deals workgroup b to XCD b % 8, so consecutive logical blocks
+// (neighbouring cells / keypoints of one image, which share pixels) are given to one XCD: physical b runs
+// logical (b % 8) * ceil(n / 8) + b / 8 and the image's bytes are fetched into one L2, not eight.  The
+// grid is padded to a multiple of 8; returns -1 for a padding block.
+__device__ __forceinline__ int xcd_block(int n_logical) {
+    const int chunk = (n_logical + 7) >> 3;
+    const int b = (int)(blockIdx.x & 7) * chunk + (int)(blockIdx.x >> 3);
+    return b < n_logical ? b : -1;
+}
+__host__ inline int xcd_grid(int n_logical) { return (n_logical + 7) & ~7; }
+
 // K2 --------------------------------------------------------------------------------------------
 // FAST-9 strength: max over the 16 circular 9-arcs of min(d) (darker) and of min(-d) (brighter),
 // d = centre - ring.  A pixel is a FAST corner at threshold t iff S > t, and OpenCV's
@@ -228,10 +239,12 @@ __device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
 //   4. emission at iniTh, or minTh if the cell had no iniTh keypoint (ORBextractor.cc:764-782).
 __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
-                                                        int *cell_cnt, uint32_t *cell_kp, int rmax) {
+                                                        int *cell_cnt, uint32_t *cell_kp, int rmax, int n_blocks) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int img = blockIdx.x / g.n_cells;
-    const int ci = blockIdx.x - img * g.n_cells;
+    const int blk = xcd_block(n_blocks);
+    if (blk < 0) return;
+    const int img = blk / g.n_cells;
+    const int ci = blk - img * g.n_cells;
     const Cell c = cells[ci];
     const int lane = threadIdx.x;
     const int rw = c.x1 - c.x0, rh = c.y1 - c.y0;
@@ -398,7 +411,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     // the NMS treats non-candidates (S = 0) as the reference treats scores <= th.
     // keypoints are emitted row-major by the counting pass itself (coordinates relative to the FAST border,
     // minBorder = 16); a cell without an iniTh keypoint wrote nothing and is redone at minTh
-    uint32_t *out = cell_kp + (size_t)blockIdx.x * g.cell_cap;
+    uint32_t *out = cell_kp + (size_t)blk * g.cell_cap;
     int th = g.ini_th;
     int ncand = prefilter(th);
     int total = nms(ncand, th, out);
@@ -408,7 +421,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         total = nms(ncand, th, out);
     }
     // cap = max NMS survivors of the window, so this cannot trigger (writes past it were dropped)
-    if (lane == 0) cell_cnt[blockIdx.x] = total > g.cell_cap ? -1 : total;
+    if (lane == 0) cell_cnt[blk] = total > g.cell_cap ? -1 : total;
 }
 
 // K3 --------------------------------------------------------------------------------------------
@@ -845,11 +858,13 @@ struct DescArgs {
     int n_images;
 };
 
-__global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a) {
+__global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
     __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kHsS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + wave;
+    const int blk = xcd_block(n_blocks);
+    if (blk < 0) return;
+    const int slot = blk * 4 + wave;
     int img = slot / g.out_per_img;
     const int s = slot - img * g.out_per_img;
     const bool in_range = img < a.n_images;
@@ -1319,8 +1334,8 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    fast_cells_kernel<<<g.n_cells * n, 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
-                                                               o->d_cell_cnt, o->d_cell_kp, o->rmax);
+    fast_cells_kernel<<<xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
+                                                               o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
     mark(o, st);
     // K3: octree per (image, level)
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
@@ -1329,7 +1344,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     // K4: orientation + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
     const int waves = g.out_per_img * n;
-    describe_kernel<<<(waves + 3) / 4, 256, 0, st>>>(g, da);
+    describe_kernel<<<xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
     HIP_OK(hipGetLastError());
     return OMV_OK;
