@@ -9,6 +9,10 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
+# heartbeat under gpurun_out/ (the traced bench prints only at its end); each step keeps its own timeout
+( while sleep 20; do date >> $OUT/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
     python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 1 --lba-steps 3 --pose-frames 256 --tri-pairs 64 \
     > $OUT/bench_trace.json 2> $OUT/bench_trace.err
