@@ -525,11 +525,21 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     wave_sync();
     int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
     int total = 0;
+#ifdef OMV_RESOLVE_PROFILE
+    long long pf0 = wall_clock64(), pf_eval = 0, pf_wait = 0;
+    int pf_rounds = 0, pf_fallback = 0;
+#endif
     for (int base = 0, buf = 0; base < M; base += 64, buf ^= 1) {
         const int nb = min(64, M - base);
         // block `base` has landed in LDS; start copying the next block into the other buffer
+#ifdef OMV_RESOLVE_PROFILE
+        const long long pw = wall_clock64();
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
+#ifdef OMV_RESOLVE_PROFILE
+        pf_wait += wall_clock64() - pw;
+#endif
         if (base + 64 < M) issue(buf ^ 1, base + 64);
         const uint8_t *sb = stage0 + buf * SL.bytes;
         const BlockStage bs{reinterpret_cast<const Rec *>(sb + SL.rec), reinterpret_cast<const int *>(sb + SL.count),
@@ -542,8 +552,16 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             e.claim = lane_claim + lane * kMaxClaims;
             e.rel = lane_rel + lane * kMaxClaims;
             const int nrev = nrevived;
+#ifdef OMV_RESOLVE_PROFILE
+            const long long pe = wall_clock64();
+            ++pf_rounds;
+#endif
             if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, l2r_s, r2l_s, e);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
+#ifdef OMV_RESOLVE_PROFILE
+            pf_eval += wall_clock64() - pe;
+            pf_fallback += __popcll(__ballot(active && e.fallback));
+#endif
             const bool obs = active && (bs.flags[lane] & kFlagObs);
             if (obs)
                 for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], lane);
@@ -595,6 +613,11 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
         }
     }
     if (lane == 0) a.n_matches[frame] = total;
+#ifdef OMV_RESOLVE_PROFILE
+    if (lane == 0 && frame < 3)
+        printf("resolve frame %d M %d matches %d ticks(100MHz) total %lld eval %lld wait %lld rounds %d fallback lanes %d revived %d occ %d\n",
+               frame, M, total, wall_clock64() - pf0, pf_eval, pf_wait, pf_rounds, pf_fallback, nrevived, occ ? 1 : 0);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
