@@ -44,11 +44,24 @@ constexpr int kWinW = 2 * kWinR + 1;       // 37
 constexpr int kPatchS = 48;                 // LDS row stride of the staged patch: 12 dwords cover 43 + 3
 constexpr int kHsS = 40;                    // LDS row stride of the horizontal blur sums (10 quads of columns)
 
-__constant__ int c_pattern[256 * 4] = {
 #define OMV_PATTERN_TABLE_BEGIN
 #define OMV_PATTERN_TABLE_END
+constexpr int kPattern[256 * 4] = {
 #include "orb_pattern_31.inc"
 };
+// the 256 point pairs (ax, ay, bx, by), |coordinate| <= 15, packed as signed bytes: one dword per pair,
+// loaded by each lane once per keypoint before the patch staging
+struct PackedPattern {
+    uint32_t v[256];
+};
+constexpr PackedPattern pack_pattern() {
+    PackedPattern p{};
+    for (int i = 0; i < 256; ++i)
+        p.v[i] = (uint32_t)(kPattern[4 * i] & 0xff) | ((uint32_t)(kPattern[4 * i + 1] & 0xff) << 8) |
+                 ((uint32_t)(kPattern[4 * i + 2] & 0xff) << 16) | ((uint32_t)(kPattern[4 * i + 3] & 0xff) << 24);
+    return p;
+}
+__constant__ PackedPattern c_pattern8 = pack_pattern();
 __constant__ int c_umax[16];
 // intensity-centroid masks per (disc row v + 15, dword k): x = in-disc byte mask, y = byte weights u + 15
 __constant__ uint2 c_icmask[31 * 8];
@@ -884,7 +897,13 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     // Each wave owns its LDS slices (patch[wave], hsum[wave]): wave-scope syncs only, so the four waves of a
     // workgroup run independently and an inactive one leaves at once.
     const bool active = in_range && j < cnts[3 * l];
+#ifdef OMV_DESC_PROFILE
+    const long long t0 = wall_clock64();
+#endif
     if (!active) return;
+    uint32_t pat[4];   // this lane's pattern pairs of the four ballot rounds (latency overlaps the staging)
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) pat[rd] = c_pattern8.v[rd * 64 + lane];
     const uint32_t p = a.lvl_out[(size_t)img * g.out_per_img + s];
     const uint32_t cl = a.lvl_cls[(size_t)img * g.out_per_img + s];
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
@@ -921,6 +940,9 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         }
     }
     wave_lds_sync();
+#ifdef OMV_DESC_PROFILE
+    const long long t1 = wall_clock64();
+#endif
     // intensity centroid over the r = 15 disc (umax rows), exact integer sums: per (row v, dword k of the
     // row's columns u = 4k + b - 15) one v_dot4 of the pixels with the in-disc mask (row sum, for m01) and
     // one with the weights u + 15 (m10 = sum (u + 15) I - 15 sum I); masks from c_icmask
@@ -941,6 +963,9 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         m10 += __shfl_xor(m10, d, 64);
     }
     const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
+#ifdef OMV_DESC_PROFILE
+    const long long t2 = wall_clock64();
+#endif
     // 7x7 sigma-2 blur (GaussianBlur's bit-exact 8U path): horizontal sums exact in u16 over the 43 patch
     // rows x 37 window columns, 7 taps as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
     // vertical ((sum + 2^15) >> 16) evaluated only at the 512 steered sample points.
@@ -952,6 +977,9 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         default: hsum_rows<3>(pw, Hs, lane); break;
     }
     wave_lds_sync();
+#ifdef OMV_DESC_PROFILE
+    const long long t3 = wall_clock64();
+#endif
     auto blurred = [&](int r, int q) {   // window coordinates (0..36)
         uint32_t acc = 0;
 #pragma unroll
@@ -961,13 +989,15 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
     float sn, cs;
     omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
+#ifdef OMV_DESC_PROFILE
+    const long long t4 = wall_clock64();
+#endif
     const float fa = cs, fb = sn;
     uint64_t words[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) {
-        const int i = rd * 64 + lane;
-        const int ax = c_pattern[4 * i], ay = c_pattern[4 * i + 1];
-        const int bx = c_pattern[4 * i + 2], by = c_pattern[4 * i + 3];
+        const int ax = (int)(int8_t)(pat[rd] & 0xff), ay = (int)(int8_t)((pat[rd] >> 8) & 0xff);
+        const int bx = (int)(int8_t)((pat[rd] >> 16) & 0xff), by = (int)(int8_t)(pat[rd] >> 24);
         const int ady = omv::round_even((float)ax * fb + (float)ay * fa);
         const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
         const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
@@ -987,6 +1017,12 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     omv_kp *kp = a.kps + (size_t)img * g.n_max + row;
     uint64_t *dst = reinterpret_cast<uint64_t *>(a.desc + ((size_t)img * g.n_max + row) * 32);
     if (lane < 4) dst[lane] = words[lane];
+#ifdef OMV_DESC_PROFILE
+    if (lane == 0 && img == 0 && (s & 127) == 0) {
+        const long long t6 = wall_clock64();
+        printf("desc slot %d ticks(100MHz) stage %lld centroid+atan %lld hsum %lld sincos %lld brief %lld\n", s, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t6 - t4);
+    }
+#endif
     if (lane == 0) {
         float x = (float)cx, y = (float)cy;
         if (l != 0) x *= L.scale, y *= L.scale;
