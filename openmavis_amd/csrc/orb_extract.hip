@@ -42,7 +42,8 @@ constexpr int kPatchW = 2 * kPatchR + 1;   // 43
 constexpr int kWinR = 18;
 constexpr int kWinW = 2 * kWinR + 1;       // 37
 constexpr int kPatchS = 48;                 // LDS row stride of the staged patch: 12 dwords cover 43 + 3
-constexpr int kHsS = 40;                    // LDS row stride of the horizontal blur sums (10 quads of columns)
+constexpr int kHsS = 40;                    // horizontal blur sums: 10 quads of columns per patch row
+constexpr int kHtS = 44;                    // ... stored column-major, 43 rows + pad per column (u16)
 
 #define OMV_PATTERN_TABLE_BEGIN
 #define OMV_PATTERN_TABLE_END
@@ -853,7 +854,8 @@ __device__ __forceinline__ void hsum_rows(const uint32_t *pw, uint16_t *Hs, int 
             const uint32_t w1 = __builtin_amdgcn_alignbyte(D[j + 2 < 4 ? j + 2 : 3], D[j + 1], al);
             h[sc] = __builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
         }
-        *reinterpret_cast<uint2 *>(Hs + r * kHsS + 4 * jq) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+#pragma unroll
+        for (int sc = 0; sc < 4; ++sc) Hs[(4 * jq + sc) * kHtS + r] = (uint16_t)h[sc];
         jq += 4, r += 6;
         if (jq >= kHsS / 4) jq -= kHsS / 4, ++r;
     }
@@ -873,7 +875,7 @@ struct DescArgs {
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
-    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kPatchW * kHsS];
+    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kHsS * kHtS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int blk = xcd_block(n_blocks);
     if (blk < 0) return;
@@ -980,10 +982,19 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
 #ifdef OMV_DESC_PROFILE
     const long long t3 = wall_clock64();
 #endif
+    // vertical 7-tap sum at window (r, q): the column's sums r..r+6 are contiguous u16, read as 4 dwords
+    // from the pair boundary at or below r and re-paired (v_alignbit by 16 when r is odd), then 4 v_dot2
+    // against the packed taps (18,34)(48,56)(48,34)(18,0) -- the same exact integer sum
+    const uint32_t *Hw = reinterpret_cast<const uint32_t *>(Hs);
     auto blurred = [&](int r, int q) {   // window coordinates (0..36)
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * Hs[(r + k) * kHsS + q];
+        const int d0 = (q * kHtS + r) >> 1, sh = (r & 1) << 4;
+        const uint32_t D0 = Hw[d0], D1 = Hw[d0 + 1], D2 = Hw[d0 + 2], D3 = Hw[d0 + 3];
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        auto u2 = [](uint32_t x) { return __builtin_bit_cast(us2, x); };
+        uint32_t acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D1, D0, sh)), u2(18u | (34u << 16)), 0u, false);
+        acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D2, D1, sh)), u2(48u | (56u << 16)), acc, false);
+        acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D3, D2, sh)), u2(48u | (34u << 16)), acc, false);
+        acc = __builtin_amdgcn_udot2(u2(D3 >> sh), u2(18u), acc, false);
         return (int)min((acc + 32768u) >> 16, 255u);
     };
     // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
