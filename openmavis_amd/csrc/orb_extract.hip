@@ -873,7 +873,7 @@ struct DescArgs {
     int n_images;
 };
 
-__global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
+__global__ void __launch_bounds__(256, 7) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
     __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kHsS * kHtS];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
