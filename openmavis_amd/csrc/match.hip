@@ -238,7 +238,7 @@ constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
 // (ballot prefix, slot order kept) and scans them 64 at a time.
 constexpr int kCandChunk = 192;
 
-__global__ void __launch_bounds__(256) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
+__global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
                                                    const uint8_t *occ_init, Rec *recs, int *counts, int *flags,
                                                    int far_points, float th_far) {
     __shared__ int queue[4][kCandChunk];
