@@ -598,8 +598,9 @@ def main():
         # isInFrustum: per point pos/normal/min/max in, per (point, cam) proj x/y, cos, level, flag out
         "frustum": B * M_MPS * (32 + C * 17 + 4),
         "stereo_knn": B * 2 * 1200 * 32,
-        # per (point, camera) candidate scan: descriptor + projection + ~window candidates' records
-        "proj_candidates": B * M_MPS * (32 + C * 16),
+        # per point: descriptor 32 B; per (point, camera) slot: projection x / y / cos / level / in-view
+        # 17 B read, the 64-B record + 4-B count written (window candidates' 60 B each not counted)
+        "proj_candidates": B * M_MPS * (32 + C * (17 + 68)),
         "proj_resolve": B * M_MPS * C * 32,
     }
     roof = None

@@ -194,9 +194,16 @@ __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, flo
     for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
         const int c0 = ix * kGridRows + nMinCellY, c1 = ix * kGridRows + nMaxCellY;
         const int e = cs[c1 + 1];
-        for (int p = cs[c0]; p < e; ++p) {   // cells iy = min..max of column ix are contiguous
-            const int i = ci[p];
+        // cells iy = min..max of column ix are contiguous.  Latency-bound gathers, so one step's loads go
+        // out together: the keypoint and its descriptor (speculatively) with the next index
+        int p = cs[c0];
+        int inext = p < e ? ci[p] : 0;
+        for (; p < e; ++p) {
+            const int i = inext;
+            if (p + 1 < e) inext = ci[p + 1];
             const omv_kp k = kp[i];
+            uint64_t d[4];
+            load_desc(dd + (size_t)i * 32, d);
             if (checkLevels) {
                 if (k.octave < minL) continue;
                 if (maxL >= 0 && k.octave > maxL) continue;
@@ -204,8 +211,6 @@ __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, flo
             if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
             if (blocked(cam * f.kp_cap + i)) continue;
             ++t.count;
-            uint64_t d[4];
-            load_desc(dd + (size_t)i * 32, d);
             t.insert(i, omv::hamming256(dmp, d), k.octave);
         }
     }
