@@ -293,6 +293,10 @@ omv_status omv_matcher_search_kf(omv_matcher *m, int n_kf, const omv_frame_geom 
  * (src/CameraModels/KannalaBrandt8.cpp:48-67), for every local map point of every frame — the loop
  * of Tracking::SearchLocalPoints.  Writes the projection fields SearchByProjection reads.
  * ---------------------------------------------------------------------------------------------- */
+/* GeometricCamera subclasses (src/CameraModels): KannalaBrandt8 (KannalaBrandt8.cpp) and Pinhole (Pinhole.cpp) */
+#define OMV_CAM_KB8 0
+#define OMV_CAM_PINHOLE 1
+
 typedef struct omv_rig {
     int n_cams;
     float cam[8][8];               /* KannalaBrandt8 mvParameters per camera block                 */
@@ -301,6 +305,8 @@ typedef struct omv_rig {
     float min_x, max_x, min_y, max_y;  /* mnMinX .. mnMaxY                                          */
     float log_scale_factor;        /* mfLogScaleFactor                                              */
     int n_levels;                  /* mnScaleLevels                                                 */
+    int model[8];                  /* camera model per block: OMV_CAM_KB8 (0, the default of a
+                                      zero-initialised rig) or OMV_CAM_PINHOLE (cam[c][0..3] = fx fy cx cy) */
 } omv_rig;
 
 typedef struct omv_frame_pose {   /* block-0 camera: mRcw, mtcw and the inverse mRwc, mOw */

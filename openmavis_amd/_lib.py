@@ -14,6 +14,8 @@ OMV_ERR_ARG = 1
 OMV_ERR_HIP = 2
 OMV_ERR_CAPACITY = 3
 OMV_ERR_NO_DEVICE = 4
+CAM_KB8 = 0       # OMV_CAM_KB8
+CAM_PINHOLE = 1   # OMV_CAM_PINHOLE
 _ERRS = {1: "bad argument", 2: "HIP runtime error", 3: "device capacity exceeded", 4: "no HIP device"}
 
 
@@ -53,7 +55,8 @@ class Rig(ctypes.Structure):
     _fields_ = [("n_cams", ctypes.c_int), ("cam", (ctypes.c_float * 8) * 8), ("R_cl", (ctypes.c_float * 9) * 8),
                 ("t_cl", (ctypes.c_float * 3) * 8), ("t_lc", (ctypes.c_float * 3) * 8), ("min_x", ctypes.c_float),
                 ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
-                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int)]
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int),
+                ("model", ctypes.c_int * 8)]
 
 
 class SE3f(ctypes.Structure):

@@ -17,8 +17,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OMV_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["orb_extract.hip", "match.hip", "lba.hip", "pose.hip", "tri.hip", "frame.hip", "imu.hip", "bow.hip"]
-HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
              f"--offload-arch={ARCH}", "-Wno-unused-result"]
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
 
 
 def _newer(target, deps):
@@ -29,12 +30,29 @@ def _newer(target, deps):
 
 
 def build_hip(force=False, verbose=True):
+    """One hipcc -c per translation unit (in parallel, only the stale ones), then one shared link."""
+    from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
-    deps.append(os.path.join(ROOT, "include", "omv.h"))
-    if not force and not _newer(LIB, deps):
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
+    hdrs.append(os.path.join(ROOT, "include", "omv.h"))
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    objs = [os.path.join(OBJ_DIR, os.path.basename(s) + ".o") for s in srcs]
+    stale = [(s, o) for s, o in zip(srcs, objs) if force or _newer(o, [s] + hdrs)]
+
+    def compile_one(so):
+        s, o = so
+        cmd = [HIPCC] + HIP_FLAGS + ["-I", os.path.join(ROOT, "include"), "-c", s, "-o", o + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(o + ".tmp", o)
+
+    if stale:
+        with ThreadPoolExecutor(max_workers=min(8, len(stale))) as ex:
+            list(ex.map(compile_one, stale))
+    if not stale and not _newer(LIB, objs):
         return LIB
-    cmd = [HIPCC] + HIP_FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + srcs
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

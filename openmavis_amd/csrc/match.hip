@@ -335,6 +335,7 @@ struct ResolveArgs {
     int *err;
     float th, th_far, nnratio;
     int far_points;
+    int staged;          // the 64-point blocks are double-buffered in LDS (else read from global)
 };
 
 // Shared per-block staging of the 64 points a wavefront evaluates.
@@ -396,7 +397,8 @@ __device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float 
 }
 
 __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
-                         const int *revived, int nrevived, const int32_t *l2r, const int32_t *r2l, Eval &e) {
+                         const uint32_t *occ0, const int *revived, int nrevived, const int32_t *l2r,
+                         const int32_t *r2l, Eval &e) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     const int C = f.n_cams, cap = f.kp_cap;
@@ -422,6 +424,10 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
         if (!obs && bit_of(bits, slot)) e.unblock = true;
         e.claim[e.nclaim++] = slot;
     };
+    // the left block's stereo partner claim (ORBmatcher.cc:125-131) by a point without observations frees
+    // an initially-occupied right keypoint for this point's own right-block search (:150-160); the
+    // right-block record was built without it (occupied at the call), so that window is rescanned
+    int self_rev = -1;
     for (int c = 0; c < C; ++c) {
         if (!((fl >> c) & 1)) continue;
         const int lvl = bs.level[l * C + c];
@@ -438,6 +444,9 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
                 if (s / cap == c) need_rescan = in_window(f, frame, c, s, m.proj_x[bc], m.proj_y[bc], rad, lvl);
             }
         }
+        if (c == 1 && self_rev >= 0 && !need_rescan)
+            need_rescan = in_window(f, frame, c, self_rev, m.proj_x[bc], m.proj_y[bc],
+                                    window_radius(f, m, bc, c, a.th, a.th != 1.0f), lvl);
         if (rcount == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
         int b1 = -1, b2 = -1, d1 = 256, d2 = 256, o1 = -1, o2 = -1;
         if (!need_rescan) {
@@ -468,7 +477,11 @@ __device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const Bl
             if (o1 == o2 && (float)d1 > a.nnratio * d2) return;   // `continue` to the next map point
             if (c == 0) {
                 add_claim(b1);
-                if (C > 1 && l2r[b1] != -1) add_claim(cap + l2r[b1]), e.nmatch++;
+                if (C > 1 && l2r[b1] != -1) {
+                    const int ps = cap + l2r[b1];
+                    if (!obs && bit_of(occ0, ps) && bit_of(bits, ps)) self_rev = ps;
+                    add_claim(ps), e.nmatch++;
+                }
                 e.nmatch++;
             } else if (c == 1) {
                 if (r2l[b1] != -1) add_claim(r2l[b1]), e.nmatch++;
@@ -493,15 +506,18 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     const int nwords = (S + 31) >> 5;
     uint32_t *bits = rsm;                                         // blocked: mvpMapPoints[s] has observations
     uint32_t *occ0 = rsm + nwords;                                // initially occupied (not in the records)
-    int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);       // first blocking claimer lane in a batch
-    int *lastw = owner + S;                                       // last writer lane among committing lanes
-    int32_t *l2r_s = lastw + S;                                   // this frame's mvLeftToRightMatch
+    // owner: per slot, in the conflict phase of a round the first lane (with observations) claiming it
+    // (atomicMin of lane), in the commit phase 63 - the last committing writer (atomicMin of 63 - lane);
+    // 64 = none between the phases
+    int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);
+    int32_t *l2r_s = owner + S;                                   // this frame's mvLeftToRightMatch
     int32_t *r2l_s = l2r_s + cap;                                 // and mvRightToLeftMatch
-    uint8_t *stage0 = reinterpret_cast<uint8_t *>(rsm) + ((8 * (size_t)nwords + 8 * (size_t)S + 8 * (size_t)cap + 15) & ~(size_t)15);
+    uint8_t *stage0 = reinterpret_cast<uint8_t *>(rsm) + ((8 * (size_t)nwords + 4 * (size_t)S + 8 * (size_t)cap + 15) & ~(size_t)15);
     const StageLayout SL(C);
     const int M = a.m.M;
     // issue the async copy of block `base` into stage buffer `buf`
     auto issue = [&](int buf, int base) {
+        if (!a.staged) return;   // large rigs: the records are read from global memory
         uint8_t *b = stage0 + buf * SL.bytes;
         const int nb = min(64, M - base);
         const size_t o = ((size_t)frame * M + base) * C, op = (size_t)frame * M + base;
@@ -521,7 +537,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
         bits[w] = v;
         occ0[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = 64, lastw[s] = -1;
+    for (int s = lane; s < S; s += 64) owner[s] = 64;
     for (int s = lane; s < cap; s += 64) {
         l2r_s[s] = a.l2r[(size_t)frame * cap + s];
         r2l_s[s] = a.r2l[(size_t)frame * cap + s];
@@ -547,8 +563,11 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
 #endif
         if (base + 64 < M) issue(buf ^ 1, base + 64);
         const uint8_t *sb = stage0 + buf * SL.bytes;
-        const BlockStage bs{reinterpret_cast<const Rec *>(sb + SL.rec), reinterpret_cast<const int *>(sb + SL.count),
-                            reinterpret_cast<const int *>(sb + SL.level), reinterpret_cast<const int *>(sb + SL.flags)};
+        const size_t go = ((size_t)frame * M + base) * C, gp = (size_t)frame * M + base;
+        const BlockStage bs = a.staged
+            ? BlockStage{reinterpret_cast<const Rec *>(sb + SL.rec), reinterpret_cast<const int *>(sb + SL.count),
+                         reinterpret_cast<const int *>(sb + SL.level), reinterpret_cast<const int *>(sb + SL.flags)}
+            : BlockStage{a.recs + go, a.counts + go, a.m.level + go, a.flags + gp};
         const int i = base + lane;
         int start = 0;
         while (start < nb) {
@@ -561,7 +580,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             const long long pe = wall_clock64();
             ++pf_rounds;
 #endif
-            if (active) evaluate(a, frame, i, lane, bs, bits, revived, nrev, l2r_s, r2l_s, e);
+            if (active) evaluate(a, frame, i, lane, bs, bits, occ0, revived, nrev, l2r_s, r2l_s, e);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
 #ifdef OMV_RESOLVE_PROFILE
             pf_eval += wall_clock64() - pe;
@@ -579,6 +598,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             wave_sync();
             if (obs)
                 for (int q = 0; q < e.nclaim; ++q) owner[e.claim[q]] = 64;
+            wave_sync();
             uint64_t cm = __ballot(conflict);
             const uint64_t um = __ballot(active && e.unblock);
             if (um) {
@@ -590,12 +610,12 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             // commit lanes [start, j0): the highest committing lane writes a shared slot last
             const bool committed = lane >= start && lane < j0;
             if (committed)
-                for (int t = 0; t < e.nclaim; ++t) atomicMax(&lastw[e.claim[t]], lane);
+                for (int t = 0; t < e.nclaim; ++t) atomicMin(&owner[e.claim[t]], 63 - lane);
             wave_sync();
             if (committed)
                 for (int t = 0; t < e.nclaim; ++t) {
                     const int s = e.claim[t];
-                    if (lastw[s] != lane) continue;
+                    if (owner[s] != 63 - lane) continue;
                     k2m[s] = i;
                     if (obs) {
                         atomicOr(&bits[s >> 5], 1u << (s & 31));
@@ -609,7 +629,7 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
                 }
             wave_sync();
             if (committed)
-                for (int t = 0; t < e.nclaim; ++t) lastw[e.claim[t]] = -1;
+                for (int t = 0; t < e.nclaim; ++t) owner[e.claim[t]] = 64;
             int nm = committed ? e.nmatch : 0;
             for (int d = 32; d >= 1; d >>= 1) nm += __shfl_xor(nm, d, 64);
             total += nm;
@@ -741,13 +761,19 @@ __global__ void __launch_bounds__(256) frustum_kernel(const omv_frame_pose *pose
         const float Pc_dist = omv::sqrtf_cr(Pc[0] * Pc[0] + Pc[1] * Pc[1] + Pc[2] * Pc[2]);
         if (Pc[2] >= 0.0f) {
             const float *k = rig.cam[c];
-            const float x2y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
-            const float theta = omv::glibc_atan2f(omv::sqrtf_cr(x2y2), Pc[2]);
-            const float psi = omv::glibc_atan2f(Pc[1], Pc[0]);
-            const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
-            const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
-            const float u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
-            const float v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
+            float u, v;
+            if (rig.model[c] == OMV_CAM_PINHOLE) {   // Pinhole::project(Vector3f) (Pinhole.cpp:26-32)
+                u = k[0] * Pc[0] / Pc[2] + k[2];
+                v = k[1] * Pc[1] / Pc[2] + k[3];
+            } else {                                 // KannalaBrandt8::project(Vector3f)
+                const float x2y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
+                const float theta = omv::glibc_atan2f(omv::sqrtf_cr(x2y2), Pc[2]);
+                const float psi = omv::glibc_atan2f(Pc[1], Pc[0]);
+                const float t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
+                const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
+                u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
+                v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
+            }
             if (!(u < rig.min_x || u > rig.max_x || v < rig.min_y || v > rig.max_y)) {
                 const float maxD = 1.2f * maxd, minD = 0.8f * mind;
                 const float PO[3] = {P[0] - twc[c][0], P[1] - twc[c][1], P[2] - twc[c][2]};
@@ -906,8 +932,8 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
     const int C = f.n_cams, cap = f.kp_cap, S = C * cap;
     const int nwords = (S + 31) >> 5;
     uint32_t *bits = lsm;                                        // blocked slots
-    int *owner = reinterpret_cast<int *>(lsm + nwords);          // first claiming lane (with obs) in a batch
-    int *lastw = owner + S;                                      // last committing writer
+    // first claiming lane (with obs) in the conflict phase, 63 - the last committing writer in the commit phase
+    int *owner = reinterpret_cast<int *>(lsm + nwords);
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
     for (int w = lane; w < nwords; w += 64) {
         uint32_t v = 0;
@@ -917,7 +943,7 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
         }
         bits[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = 64, lastw[s] = -1;
+    for (int s = lane; s < S; s += 64) owner[s] = 64;
     wave_sync();
     int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
     int2 *push = a.pushes + (size_t)frame * a.L.S * C;
@@ -984,6 +1010,7 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
             wave_sync();
             if (obs)
                 for (int q = 0; q < nclaim; ++q) owner[claim[q]] = 64;
+            wave_sync();
             uint64_t cm = __ballot(conflict);
             const uint64_t um = __ballot(active && unblock);
             if (um) {
@@ -1002,7 +1029,7 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
             const int ptot = __shfl(incl, 63, 64);
             if (committed) {
                 for (int q = 0; q < nclaim; ++q) {
-                    atomicMax(&lastw[claim[q]], lane);
+                    atomicMin(&owner[claim[q]], 63 - lane);
                     if (a.check_ori) push[npush + incl - np + q] = make_int2(claim[q], bin[q]);
                 }
             }
@@ -1012,14 +1039,14 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
             if (committed)
                 for (int q = 0; q < nclaim; ++q) {
                     const int slot = claim[q];
-                    if (lastw[slot] != lane) continue;
+                    if (owner[slot] != 63 - lane) continue;
                     k2m[slot] = s;
                     if (obs) atomicOr(&bits[slot >> 5], 1u << (slot & 31));
                     else atomicAnd(&bits[slot >> 5], ~(1u << (slot & 31)));
                 }
             wave_sync();
             if (committed)
-                for (int q = 0; q < nclaim; ++q) lastw[claim[q]] = -1;
+                for (int q = 0; q < nclaim; ++q) owner[claim[q]] = 64;
             start = j0;
             wave_sync();
             (void)lt;
@@ -1365,11 +1392,19 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
     f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
 }
 
-static size_t resolve_lds_bytes(int C, int cap) {
+// resolve workspace: blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l, and (when it
+// fits) the double-buffered 64-point stage; *staged = 0 when only the workspace fits
+static size_t resolve_lds_bytes(int C, int cap, int *staged = nullptr) {
     const size_t S = (size_t)C * cap;
-    size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + 2 * sizeof(int) * S + 2 * sizeof(int32_t) * cap;
+    size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + sizeof(int) * S + 2 * sizeof(int32_t) * cap;
     b = (b + 15) & ~(size_t)15;
-    return b + 2 * (size_t)StageLayout(C).bytes;
+    const size_t with_stage = b + 2 * (size_t)StageLayout(C).bytes;
+    if (staged) *staged = with_stage <= kResolveLds;
+    return with_stage <= kResolveLds ? with_stage : b;
+}
+static size_t lf_resolve_lds_bytes(int C, int cap) {
+    const size_t S = (size_t)C * cap;
+    return sizeof(uint32_t) * ((S + 31) / 32) + sizeof(int) * S;
 }
 
 extern "C" {
@@ -1390,11 +1425,14 @@ omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
     if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)
         return OMV_ERR_ARG;
-    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds) return OMV_ERR_ARG;   // resolve workspace must fit LDS
+    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds || lf_resolve_lds_bytes(n_cams, kp_cap) > kResolveLds)
+        return OMV_ERR_ARG;   // resolve workspaces must fit LDS
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
     if (hipFuncSetAttribute((const void *)resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds) !=
-        hipSuccess)
+            hipSuccess ||
+        hipFuncSetAttribute((const void *)lf_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kResolveLds) != hipSuccess)
         return OMV_ERR_HIP;
     omv_matcher *h = new omv_matcher();
     h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
@@ -1502,10 +1540,10 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
+    int staged = 1;
+    const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap, &staged);
     ResolveArgs ra{f, m, h->d_recs, h->d_counts, h->d_flags, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
-                   far_points};
-    const int S = h->n_cams * h->kp_cap;
-    const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap);
+                   far_points, staged};
     resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
     if (h->timing) {
         h->ev.push_back({2, {e0, e1}});
@@ -1550,8 +1588,7 @@ omv_status omv_matcher_search_last_frame(omv_matcher *h, int n_frames, const omv
     LfResolveArgs ra{f, L, G, Tcw, Tlw, h->d_recs, h->d_counts, kp_occ_init, kp_to_mp, n_matches, h->d_push, h->d_npush,
                      check_ori};
     const int S = C * h->kp_cap;
-    const size_t lds = sizeof(uint32_t) * ((S + 31) / 32) + 2 * sizeof(int) * S;
-    lf_resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
+    lf_resolve_kernel<<<n_frames, 64, lf_resolve_lds_bytes(C, h->kp_cap), st>>>(ra);
     if (check_ori) lf_histo_kernel<<<n_frames, 256, 0, st>>>(h->d_push, h->d_npush, (int)per_frame, S, kp_to_mp, n_matches);
     HIP_OK(hipGetLastError());
     return OMV_OK;

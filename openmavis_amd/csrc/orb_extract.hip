@@ -917,8 +917,10 @@ __global__ void __launch_bounds__(256, 7) describe_kernel(Geom g, DescArgs a, in
     // touching the level border take reflect101 byte loads
     uint8_t *P = patch[wave];
     const int x0 = cx - kPatchR, y0 = cy - kPatchR;
+    // the 12 dwords of a row reach byte (x0 & ~3) + 47: keep them inside the row's pitch (hence inside the
+    // image / level allocation even on its last row)
     const bool inner = x0 >= 0 && y0 >= 0 && x0 + kPatchW <= L.w && y0 + kPatchW <= L.h && (sp & 3) == 0 &&
-                       (((uintptr_t)src) & 3) == 0;
+                       (((uintptr_t)src) & 3) == 0 && (x0 & ~3) + 48 <= sp;
     if (inner) {
         const uint8_t *r0 = src + (size_t)y0 * sp + x0;
         const int o = (int)(((uintptr_t)r0) & 3);
@@ -1283,6 +1285,13 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     if (o->oct_lds > 160 * 1024) {
         delete o;
         return OMV_ERR_ARG;
+    }
+    // 1080p levels hold ~1,500 cells: the octree's node lists then exceed the default 64 KB dynamic LDS
+    if (o->oct_lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)octree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)o->oct_lds) !=
+            hipSuccess) {
+        delete o;
+        return OMV_ERR_HIP;
     }
     const Geom &g = o->g;
     const size_t n = (size_t)max_images;

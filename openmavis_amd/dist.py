@@ -61,6 +61,78 @@ def allgather_camera_slabs(kps, desc, n_kp, group=None):
     return g_kps, g_desc, g_n
 
 
+class CameraShard:
+    """One camera per rank (BASELINE configs[2] / [3]; the reference's unit of parallelism is the per-camera
+    extractor thread, src/Frame.cc:1841-1862): rank r extracts cameras r, r + world, ... of every frame and
+    the tracking rank needs all of them, so the ranks exchange fixed-size slabs in ONE all_gather_into_tensor
+    (RCCL ring over xGMI with mode "device"; staged through host memory with mode "host" for gloo).
+
+    The send buffer is sectioned so the extractor writes straight into it (no packing copy):
+        n_kp [k][F] | mono [k][F] | kps [k][F][kp_cap][6] (omv_kp rows) | desc [k][F][kp_cap][32 B]
+    with k = ceil(n_cams / world) camera slots per rank (cam-major: a rank with fewer cameras extracts only its
+    first len(cams) * F images).  `gather` scatters every rank's slab into a FrameBatch [F][n_cams] in camera
+    order, on every rank."""
+
+    def __init__(self, rank, world, n_cams, n_frames, kp_cap, device, mode="device", group=None):
+        import torch
+        self.rank, self.world, self.n_cams, self.F, self.cap = rank, world, n_cams, n_frames, kp_cap
+        self.k = (n_cams + world - 1) // world
+        self.cams = list(range(rank, n_cams, world))
+        self.mode, self.group, self.device = mode, group, device
+        k, F = self.k, n_frames
+        self.off_mono = k * F
+        self.off_kps = 2 * k * F
+        self.off_desc = self.off_kps + k * F * kp_cap * 6
+        self.words = self.off_desc + k * F * kp_cap * 8
+        self.send = torch.zeros(self.words, dtype=torch.int32, device=device)
+        self.recv = torch.empty(world * self.words, dtype=torch.int32, device=device)
+        if mode == "host":
+            self._send_h = torch.empty(self.words, dtype=torch.int32)
+            self._recv_h = torch.empty(world * self.words, dtype=torch.int32)
+
+    def camera_of(self, r, j):
+        return r + j * self.world
+
+    def outputs(self):
+        """This rank's extractor outputs as views of the send slab, for its len(cams) * F images (cam-major)."""
+        import torch
+        n = len(self.cams) * self.F
+        s, cap = self.send, self.cap
+        return (s[self.off_kps:self.off_kps + n * cap * 6].view(n, cap, 6),
+                s[self.off_desc:self.off_desc + n * cap * 8].view(torch.uint8).view(n, cap, 32),
+                s[:n], s[self.off_mono:self.off_mono + n])
+
+    def gather(self, fb, stream=None):
+        """All-gather the slabs and scatter them into FrameBatch fb ([F][n_cams][kp_cap] tensors on this rank)."""
+        import contextlib
+        import torch
+        import torch.distributed as dist
+        on_gpu = torch.device(self.device).type == "cuda"
+        ctx = torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device)) \
+            if on_gpu else contextlib.nullcontext()
+        with ctx:
+            if self.mode == "host" and on_gpu:
+                self._send_h.copy_(self.send)
+                dist.all_gather_into_tensor(self._recv_h, self._send_h, group=self.group)
+                self.recv.copy_(self._recv_h)
+            else:
+                dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+            F, cap, k = self.F, self.cap, self.k
+            rv = self.recv.view(self.world, self.words)
+            for r in range(self.world):
+                for j in range(k):
+                    c = self.camera_of(r, j)
+                    if c >= self.n_cams:
+                        continue
+                    b = j * F
+                    fb.n_kp[:, c].copy_(rv[r, b:b + F])
+                    fb.mono[:, c].copy_(rv[r, self.off_mono + b:self.off_mono + b + F])
+                    o = self.off_kps + b * cap * 6
+                    fb.kps[:, c].copy_(rv[r, o:o + F * cap * 6].view(F, cap, 6))
+                    o = self.off_desc + b * cap * 8
+                    fb.desc[:, c].copy_(rv[r, o:o + F * cap * 8].view(torch.uint8).view(F, cap, 32))
+
+
 class LbaAllReduce:
     """The omv_allreduce_fn of a landmark-sharded LocalInertialBA over torch.distributed.
 

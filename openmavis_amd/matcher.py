@@ -329,13 +329,16 @@ def kf_search_params(th, max_dist, cams, scale_factor=1.2, nlevels=8, bf=0.0, ur
     return p
 
 
-def make_rig(cams, R_cl, t_cl, width, height, scale_factor=1.2, nlevels=8):
-    """omv_rig from per-camera KB8 parameters and the block-c-from-block-0 transforms (float32)."""
+def make_rig(cams, R_cl, t_cl, width, height, scale_factor=1.2, nlevels=8, model="kb8"):
+    """omv_rig from per-camera parameters (KannalaBrandt8: fx fy cx cy k1..k4; Pinhole: fx fy cx cy) and the
+    block-c-from-block-0 transforms (float32).  model: "kb8" / "pinhole" for every block, or one per block."""
     r = _lib.Rig()
     C = len(cams)
     r.n_cams = C
+    models = [model] * C if isinstance(model, str) else list(model)
     for c in range(C):
-        for q in range(8):
+        r.model[c] = {"kb8": _lib.CAM_KB8, "pinhole": _lib.CAM_PINHOLE}[models[c]]
+        for q in range(len(cams[c])):
             r.cam[c][q] = float(cams[c][q])
         Rc = np.asarray(R_cl[c], np.float32).reshape(3, 3)
         tc = np.asarray(t_cl[c], np.float32).reshape(3)

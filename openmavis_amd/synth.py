@@ -122,6 +122,30 @@ def hilti_rig(n_cams=5):
     return cams[:n_cams].astype(np.float32), R_cl[:n_cams].astype(np.float32), t_cl[:n_cams].astype(np.float32)
 
 
+def p1080_rig(n_cams=8, width=1920, height=1080):
+    """BASELINE config 4's synthetic Pinhole rig: n_cams cameras on a 0.15 m ring, yawed 360/n_cams degrees
+    apart (block 0 = left, 1 = right, >= 2 side cameras), fx = fy = 700 px, principal point at the image
+    centre.  Returns (Pinhole parameters [C][4], R_cl [C][3][3], t_cl [C][3]) in float32."""
+    cams = np.tile(np.array([700.0, 700.0, width / 2.0, height / 2.0]), (n_cams, 1))
+    R_cl, t_cl = [], []
+    for c in range(n_cams):
+        a = 2 * np.pi * c / n_cams
+        # camera c's axes in block-0 coordinates: yaw a about the y (down) axis
+        Rlc = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        Ol = 0.15 * np.array([np.sin(a), 0.0, np.cos(a) - 1.0])   # centre on the ring through block 0's
+        R_cl.append(Rlc.T)
+        t_cl.append(-Rlc.T @ Ol)
+    return cams.astype(np.float32), np.array(R_cl, np.float32), np.array(t_cl, np.float32)
+
+
+def pinhole_unproject(k, u, v):
+    """Unit ray of pixel (u, v) through Pinhole k = (fx, fy, cx, cy)."""
+    k = np.asarray(k, np.float64)
+    ray = np.stack([(np.asarray(u, np.float64) - k[2]) / k[0], (np.asarray(v, np.float64) - k[3]) / k[1],
+                    np.ones(np.shape(u))], -1)
+    return ray / np.linalg.norm(ray, axis=-1, keepdims=True)
+
+
 def random_pose(rng):
     """omv_frame_pose as float32[24]: Rcw, tcw, Rwc, Ow of block 0."""
     q = rng.normal(0, 1, 4)
@@ -152,7 +176,7 @@ def kb8_unproject(k, u, v, iters=10):
 
 
 def make_world_map(kps, desc, n_kp, M, seed, cams, R_cl, t_cl, pose, width, height, nlevels=8, frac_true=0.6,
-                   scale=1.2):
+                   scale=1.2, model="kb8"):
     """Local map points in 3-D for one frame: `frac_true` are keypoints of a random camera block
     unprojected to a depth U(2, 20) m (descriptor with U{0..8} bit flips, mfMaxDistance chosen so
     PredictScale returns the keypoint's octave), the rest random pixels/depths/octaves.  Normals point
@@ -170,7 +194,7 @@ def make_world_map(kps, desc, n_kp, M, seed, cams, R_cl, t_cl, pose, width, heig
     ray = np.zeros((M, 3))
     for c in range(C):
         sel = cam == c
-        ray[sel] = kb8_unproject(cams[c], u[sel], v[sel])
+        ray[sel] = (pinhole_unproject if model == "pinhole" else kb8_unproject)(cams[c], u[sel], v[sel])
     depth = rng.uniform(2.0, 20.0, M)
     Xc = ray * depth[:, None]
     Rcl, tcl = R_cl[cam].astype(np.float64), t_cl[cam].astype(np.float64)

@@ -383,6 +383,7 @@ struct RigF {
     float min_x, max_x, min_y, max_y;
     float log_scale_factor;         // mfLogScaleFactor = (float)log(mfScaleFactor)
     int n_levels;
+    int model[8];                   // 0 KannalaBrandt8, 1 Pinhole
 };
 struct PoseF {
     float Rcw[9], tcw[3], Rwc[9], Ow[3];
@@ -405,6 +406,12 @@ static void kb8_project_f(const float *k, const float *X, float &u, float &v) {
     const float r = theta + k[4] * t3 + k[5] * t5 + k[6] * t7 + k[7] * t9;
     u = (float)(k[0] * r * std::cos((double)psi) + k[2]);
     v = (float)(k[1] * r * std::sin((double)psi) + k[3]);
+}
+
+// Pinhole::project(const Eigen::Vector3f&) (Pinhole.cpp:26-32): fx * x / z + cx, float, left to right
+static void pinhole_project_f(const float *k, const float *X, float &u, float &v) {
+    u = k[0] * X[0] / X[2] + k[2];
+    v = k[1] * X[1] / X[2] + k[3];
 }
 
 int oracle_frustum(const RigF *rig, const PoseF *pose, const float *pos, const float *normal, const float *min_d,
@@ -437,8 +444,9 @@ int oracle_frustum(const RigF *rig, const PoseF *pose, const float *pos, const f
             for (int q = 0; q < 3; ++q) Pc[q] = Pc[q] + tc[c][q];
             const float Pc_dist = std::sqrt(Pc[0] * Pc[0] + Pc[1] * Pc[1] + Pc[2] * Pc[2]);
             if (Pc[2] < 0.0f) continue;
-            float u, v;
-            kb8_project_f(rig->cam[c], Pc, u, v);
+            float u, v;   // mpCamera{,2,3,4}->project(Pc) (Frame.cc:1577-1592)
+            if (rig->model[c] == 1) pinhole_project_f(rig->cam[c], Pc, u, v);
+            else kb8_project_f(rig->cam[c], Pc, u, v);
             if (u < rig->min_x || u > rig->max_x) continue;
             if (v < rig->min_y || v > rig->max_y) continue;
             const float maxD = 1.2f * max_d[i], minD = 0.8f * min_d[i];

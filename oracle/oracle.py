@@ -199,7 +199,8 @@ class RigF(ctypes.Structure):
     _fields_ = [("n_cams", ctypes.c_int), ("cam", (ctypes.c_float * 8) * 8), ("R_cl", (ctypes.c_float * 9) * 8),
                 ("t_cl", (ctypes.c_float * 3) * 8), ("t_lc", (ctypes.c_float * 3) * 8), ("min_x", ctypes.c_float),
                 ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
-                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int)]
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int),
+                ("model", ctypes.c_int * 8)]
 
 
 def frustum(rig, pose, pos, normal, min_dist, max_dist, cos_limit=0.5, view_cos=None, track_depth=None):

@@ -184,7 +184,8 @@ def test_reoptimize_same_handle(small, oracle):
     _compare_state(small, s2, s1, oracle)
 
 
-def test_landmark_sharded_two_ranks(oracle, tmp_path):
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_landmark_sharded_two_ranks(oracle, tmp_path, backend):
     """landmarks sharded over 2 ranks (gloo, both on this box's GPU), one all-reduce of the
     partial Schur system per trial.  The merged outcome meets the same bar against the oracle, and
     every rank holds the identical keyframe state (asserted inside the worker)."""
@@ -192,14 +193,17 @@ def test_landmark_sharded_two_ranks(oracle, tmp_path):
     import socket
     import subprocess
     import sys
+    import torch
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL device all-reduce needs 2 visible GPUs (the gloo case covers a 1-GPU box)")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = tmp_path / "shard.npz"
+    out = tmp_path / f"shard_{backend}.npz"
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tools", "lba_shard_run.py"),
-           "--out", str(out), "--backend", "gloo", "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000"]
+           "--out", str(out), "--backend", backend, "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000"]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])

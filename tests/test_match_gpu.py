@@ -284,3 +284,69 @@ def test_search_by_projection_last_frame_matches_oracle(frames, oracle, torch_cu
         assert n > 200
     frames.occ_init = None
     frames.kp_to_mp.fill_(-1)
+
+
+def test_search_by_projection_stereo_partner_revives_right_keypoint(frames, oracle, torch_cuda):
+    """A left-block claim by a point without observations writes the stereo partner's slot
+    (ORBmatcher.cc:125-131); if that right keypoint was occupied at the call, it becomes free for the same
+    point's right-block search (:150-160).  Geometrically coherent l2r pairs: the right keypoint sits at the
+    point's right-camera projection, half of them initially occupied, most points without observations."""
+    torch = torch_cuda
+    M = 3000
+    per, mpb = _mps_for(frames, oracle, M, 77, torch)
+    kps, desc, n_kp, _ = host(frames, oracle)
+    rng = np.random.default_rng(99)
+    cap = frames.kp_cap
+    l2r = np.full((frames.n_frames, cap), -1, np.int32)
+    r2l = np.full((frames.n_frames, cap), -1, np.int32)
+    occ = np.zeros((frames.n_frames, C * cap), np.uint8)
+    for f, p in enumerate(per):
+        nl, nr = int(n_kp[f, 0]), int(n_kp[f, 1])
+        # points seen by block 0 at (near) a left keypoint: pair that keypoint with a right keypoint and let the
+        # point see block 1 exactly there
+        px, py = p["proj_x"][:, 0], p["proj_y"][:, 0]
+        seen = np.nonzero(p["in_view"][:, 0] > 0)[0]
+        right = rng.permutation(nr)
+        used_l = set()
+        k = 0
+        for pi in seen:
+            d = (kps[f, 0, :nl]["x"] - px[pi]) ** 2 + (kps[f, 0, :nl]["y"] - py[pi]) ** 2
+            li = int(np.argmin(d))
+            if d[li] > 4.0 or li in used_l or k >= nr:
+                continue
+            used_l.add(li)
+            ri = int(right[k])
+            k += 1
+            l2r[f, li], r2l[f, ri] = ri, li
+            p["proj_x"][pi, 1] = kps[f, 1, ri]["x"]
+            p["proj_y"][pi, 1] = kps[f, 1, ri]["y"]
+            p["level"][pi, 1] = kps[f, 1, ri]["octave"]
+            p["in_view"][pi, 1] = 1
+            p["view_cos"][pi, 1] = 0.999
+            if rng.random() < 0.5:
+                occ[f, cap + ri] = 1
+        p["has_obs"][:] = (rng.random(M) < 0.2).astype(np.uint8)
+        assert k > 100
+    for key in ("proj_x", "proj_y", "level", "in_view", "view_cos", "has_obs"):
+        getattr(mpb, key).copy_(torch.from_numpy(np.stack([p[key] for p in per])))
+    frames.l2r.copy_(torch.from_numpy(l2r))
+    frames.r2l.copy_(torch.from_numpy(r2l))
+    init = np.where(occ > 0, 123456, -1).astype(np.int32)
+    frames.occ_init = torch.from_numpy(occ).cuda()
+    frames.kp_to_mp.copy_(torch.from_numpy(init))
+    m = ORBmatcher(0.8)
+    m.SearchByProjection(frames, mpb, 6.0, False, 50.0)
+    torch.cuda.synchronize()
+    got, got_n = frames.kp_to_mp.cpu().numpy(), frames.n_matches.cpu().numpy()
+    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+    for f in range(frames.n_frames):
+        exp = init[f].copy()
+        n = oracle.search_by_projection(g, kps[f], desc[f], n_kp[f], per[f], 6.0, False, 50.0, 0.8, l2r[f], r2l[f],
+                                        occ[f], exp)
+        bad = np.nonzero(exp != got[f])[0]
+        assert n == got_n[f] and bad.size == 0, (f, n, int(got_n[f]), bad[:8])
+        # right keypoints freed by their own point's partner claim and then matched by it in block 1
+        assert ((exp[cap:2 * cap] >= 0) & (exp[cap:2 * cap] != 123456) & (occ[f, cap:2 * cap] > 0)).sum() > 10
+    assert m.last_error() == 0
+    frames.occ_init = None
+    frames.kp_to_mp.fill_(-1)
