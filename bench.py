@@ -7,13 +7,19 @@ images (and map points) are already resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B] [--no-cpu-baseline]
 
-For N > 1 launch with torch.distributed.run; every rank processes its own frames (frame-parallel
-replicas, no data-path collective: the path shards by frame) and rank 0 prints one JSON line with
-the whole-job throughput (max time over ranks).
+--gpus N > 1 without a torch.distributed environment: the script starts N ranks itself
+(torch.distributed.run, one process per GPU, before anything touches a GPU) and exits with their status.
+Every rank processes its own frames (frame-parallel replicas, no data-path collective: the path shards by
+frame) and rank 0 prints one JSON line with the whole-job throughput (max time over ranks).  At N > 1 the
+camera-sharded layouts run as extra legs: `cam_shard` (configs[2], 5 Hilti cameras over the ranks, one
+RCCL all-gather of the keypoint / descriptor slabs, matching on rank 0) and `p1080` (configs[3], 8 Pinhole
+cameras 1920x1080 over the ranks).  At N = 1 `p1080` is the 8-camera batch on one GPU.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,6 +46,12 @@ def _gen_frame(f):
     return synth.hilti_frame(f, C, W, H)
 
 
+def _gen_cam_image(item):
+    from openmavis_amd import synth
+    c, f = item
+    return synth.synth_image(synth.HILTI_SEED + 1000 * c + f, W, H)
+
+
 def _gen_map(args):
     """3-D local map of one frame (world points + map-point fields) and its block-0 pose."""
     from openmavis_amd import synth
@@ -50,77 +62,160 @@ def _gen_map(args):
     return pose, world, mp
 
 
+def _cpu_workers():
+    """Worker count for host pools: the CPUs this process may run on, at most 16 (the GPU box's CPU share;
+    os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+_POOL = None
+
+
+def _pool():
+    """One fork pool for the whole run, created before anything touches the GPU (forked children never
+    inherit a HIP context) and closed + joined at the end (no process outlives the bench)."""
+    global _POOL
+    if _POOL is None and _cpu_workers() > 1:
+        import multiprocessing as mp
+        _POOL = mp.get_context("fork").Pool(_cpu_workers())
+    return _POOL
+
+
+def _close_pool():
+    global _POOL
+    if _POOL is not None:
+        _POOL.close()
+        _POOL.join()
+        _POOL = None
+
+
 def _pool_map(fn, items):
-    n = min(16, os.cpu_count() or 1, len(items))
-    if n <= 1:
+    pool = _pool()
+    if pool is None or len(items) <= 1:
         return [fn(i) for i in items]
-    import multiprocessing as mp
-    with mp.get_context("fork").Pool(n) as pool:
-        return pool.map(fn, items)
+    return pool.map(fn, items)
 
 
-def level_pixels():
-    sizes = []
-    inv = 1.0
-    s = [1.0]
-    for _ in range(1, NLEV):
-        s.append(float(np.float32(s[-1] * np.float64(np.float32(SCALE)))))
-    for l in range(NLEV):
-        invs = np.float32(1.0) / np.float32(s[l])
-        sizes.append((int(np.rint(np.float32(W) * invs)), int(np.rint(np.float32(H) * invs))))
-    del inv
-    return [w * h for w, h in sizes]
+def host_info():
+    """The host the CPU baselines ran on (nproc, lscpu model, sockets, threads)."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["usable_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keys = {"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "CPU(s)": "cpus"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                v = v.strip()
+                info[keys[k.strip()]] = int(v) if v.isdigit() else v
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
 
 
-def cpu_baseline(n_frames=12, frames=None):
-    """Reference-faithful CPU path on this host: the oracle (scalar C++ restatement, one std::thread
-    per camera like src/Frame.cc:1841-1862, frames one at a time) timed on a bounded sample."""
+_CPU_CONST = None
+
+
+def _cpu_const():
+    """Per-process constants of the CPU pipeline (rig, stereo extrinsics, undistortion, depth images)."""
+    global _CPU_CONST
+    if _CPU_CONST is None:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        from openmavis_amd import synth
+        from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
+        from openmavis_amd.matcher import make_rig
+        tab = oracle.orb_tables(NFEAT, SCALE, NLEV)
+        cams, R_cl, t_cl = synth.hilti_rig(C)
+        Rlr = R_cl[1].T.astype(np.float32)
+        tlr = (-R_cl[1].T @ t_cl[1]).astype(np.float32)
+        _CPU_CONST = dict(
+            g=oracle.frame_geom(C, W, H, tab["scale"]), rig=make_rig(cams, R_cl, t_cl, W, H, SCALE, NLEV), cams=cams,
+            Rlr=Rlr, tlr=tlr, bf=float(cams[0][0] * np.linalg.norm(tlr)),
+            sigma2=(np.float32(SCALE) ** (2 * np.arange(NLEV))).astype(np.float32), U=undist_params(BLOCK_CAM_ID),
+            depth=(np.random.default_rng(5).random((4, H, W)) * 25.0).astype(np.float32))
+    return _CPU_CONST
+
+
+def _cpu_prep(item):
+    """Untimed: the 3-D local map of a frame, derived from a first extraction of its own keypoints."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from openmavis_amd import synth
-    tab = oracle.orb_tables(NFEAT, SCALE, NLEV)
-    g = oracle.frame_geom(C, W, H, tab["scale"])
-    from openmavis_amd.matcher import make_rig
-    cams, R_cl, t_cl = synth.hilti_rig(C)
-    rig = make_rig(cams, R_cl, t_cl, W, H, SCALE, NLEV)
-    # 3-D local maps from a first (untimed) extraction of each frame
-    prep = []
-    for i, imgs in enumerate(frames):
-        n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH)
-        prep.append(_gen_map((kps, desc, n_out, 700 + i)))
-    from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
-    Rlr = R_cl[1].T.astype(np.float32)
-    tlr = (-R_cl[1].T @ t_cl[1]).astype(np.float32)
-    bf = float(cams[0][0] * np.linalg.norm(tlr))
-    sigma2 = (np.float32(SCALE) ** (2 * np.arange(NLEV))).astype(np.float32)
-    U = undist_params(BLOCK_CAM_ID)
-    depth = (np.random.default_rng(5).random((4, H, W)) * 25.0).astype(np.float32)
+    i, imgs = item
+    n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH, threaded=False)
+    return _gen_map((kps, desc, n_out, 700 + i))
+
+
+def _cpu_frame(imgs, prep, threaded):
+    """The reference path of one multi-camera frame on the CPU oracle: extraction (one std::thread per camera
+    when threaded, like src/Frame.cc:1841-1862), lapping knn + Lowe, TriangulateMatches, mvuRight, isInFrustum,
+    SearchByProjection."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    k = _cpu_const()
+    n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH, threaded=threaded)
+    cap = kps.shape[1]
+    q = desc[0, mono[0]:n_out[0]]
+    t = desc[1, mono[1]:n_out[1]]
+    i2, d2 = oracle.bf_knn2(q, t)
+    l2r = np.full(cap, -1, np.int32)
+    r2l = np.full(cap, -1, np.int32)
+    ok = (i2[:, 1] >= 0) & (d2[:, 0].astype(np.float64) < d2[:, 1].astype(np.float64) * 0.8)
+    for qi in np.nonzero(ok)[0]:
+        l2r[mono[0] + qi] = mono[1] + i2[qi, 0]
+        r2l[mono[1] + i2[qi, 0]] = mono[0] + qi
+    l2r, r2l, _, _ = oracle.stereo_triangulate(kps[0], n_out[0], kps[1], n_out[1], k["cams"][:2], k["Rlr"], k["tlr"],
+                                               k["sigma2"], l2r)
+    for c in range(4):   # mvuRight (GetDepthFromUndistortedPoints)
+        oracle.depth_from_undistorted(kps[c, :n_out[c]], k["depth"][c], k["U"][c], k["bf"])
+    pose, world, mp = prep
+    track, _ = oracle.frustum(k["rig"], pose, world["pos"], world["normal"], world["min_dist"], world["max_dist"], 0.5,
+                              mp["view_cos"], mp["track_depth"])
+    k2m = np.full(C * cap, -1, np.int32)
+    return oracle.search_by_projection(k["g"], kps, desc, n_out, dict(mp, **track), TH, False, 50.0, NNRATIO, l2r, r2l,
+                                       None, k2m)
+
+
+def _cpu_frame_job(item):
+    imgs, prep = item
+    return _cpu_frame(imgs, prep, threaded=False)
+
+
+def cpu_baseline(frames, best_frames=0):
+    """The CPU reference path on this host, timed on a bounded sample of the same workload (the oracle: scalar
+    C++ restatement; the reference itself cannot be built here):
+      mode A, reference-faithful: one std::thread per camera (src/Frame.cc:1841-1862), frames one at a time;
+      mode B, CPU-best: whole frames in parallel over the usable cores (one worker per core, 1 thread each).
+    Runs before anything touches the GPU."""
+    preps = _pool_map(_cpu_prep, list(enumerate(frames)))
+    _cpu_const()
     t0 = time.perf_counter()
-    for i, imgs in enumerate(frames):
-        n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH)
-        cap = kps.shape[1]
-        q = desc[0, mono[0]:n_out[0]]
-        t = desc[1, mono[1]:n_out[1]]
-        i2, d2 = oracle.bf_knn2(q, t)
-        l2r = np.full(cap, -1, np.int32)
-        r2l = np.full(cap, -1, np.int32)
-        ok = (i2[:, 1] >= 0) & (d2[:, 0].astype(np.float64) < d2[:, 1].astype(np.float64) * 0.8)
-        for qi in np.nonzero(ok)[0]:
-            l2r[mono[0] + qi] = mono[1] + i2[qi, 0]
-            r2l[mono[1] + i2[qi, 0]] = mono[0] + qi
-        l2r, r2l, _, _ = oracle.stereo_triangulate(kps[0], n_out[0], kps[1], n_out[1], cams[:2], Rlr, tlr, sigma2, l2r)
-        for c in range(4):   # mvuRight (GetDepthFromUndistortedPoints)
-            oracle.depth_from_undistorted(kps[c, :n_out[c]], depth[c], U[c], bf)
-        pose, world, mp = prep[i]
-        track, _ = oracle.frustum(rig, pose, world["pos"], world["normal"], world["min_dist"], world["max_dist"], 0.5,
-                                  mp["view_cos"], mp["track_depth"])
-        k2m = np.full(C * cap, -1, np.int32)
-        oracle.search_by_projection(g, kps, desc, n_out, dict(mp, **track), TH, False, 50.0, NNRATIO, l2r, r2l, None,
-                                    k2m)
+    for imgs, prep in zip(frames, preps):
+        _cpu_frame(imgs, prep, threaded=True)
     dt = time.perf_counter() - t0
-    return dict(value=n_frames / dt, unit="multi-cam frames/s", cores=C, kind="port",
-                sample=f"{n_frames} Hilti-like frames (5x720x540, 1200 feat/cam, M={M_MPS} map points), "
-                       f"oracle C++ restatement, one thread per camera, {dt:.1f} s")
+    n = len(frames)
+    out = dict(value=round(n / dt, 3), unit="multi-cam frames/s", cores=C, kind="port",
+               sample=f"{n} Hilti-like frames (5x720x540, 1200 feat/cam, M={M_MPS} map points), oracle C++ "
+                      f"restatement, one thread per camera (mode A, reference-faithful), {dt:.1f} s",
+               host=host_info())
+    if best_frames > 0 and _pool() is not None:
+        items = [(frames[i % n], preps[i % n]) for i in range(best_frames)]
+        _pool_map(_cpu_frame_job, items[:_cpu_workers()])   # warm every worker (constants, oracle load)
+        t0 = time.perf_counter()
+        _pool_map(_cpu_frame_job, items)
+        dt = time.perf_counter() - t0
+        out["mode_b"] = dict(value=round(best_frames / dt, 3), unit="multi-cam frames/s", cores=_cpu_workers(),
+                             kind="port", sample=f"{best_frames} frames, whole frames in parallel over "
+                                                 f"{_cpu_workers()} worker processes (1 thread each), {dt:.1f} s")
+    return out
 
 
 def lba_bytes_per_trial(prob):
@@ -396,6 +491,313 @@ def aux_legs(dev, cpu):
     return out
 
 
+# ---- configs[3]: synthetic 8-camera Pinhole rig, 1920x1080, 2000 features/cam --------------------------------
+P_W, P_H, P_C, P_NF, P_INI, P_MIN, P_M, P_TH = 1920, 1080, 8, 2000, 20, 7, 8000, 3.0
+
+
+def level_sizes(w, h, nlevels=NLEV, scale=SCALE):
+    """Pyramid level sizes with the ORBextractor ctor's float arithmetic."""
+    s = [1.0]
+    for _ in range(1, nlevels):
+        s.append(float(np.float32(s[-1] * np.float64(np.float32(scale)))))
+    out = []
+    for l in range(nlevels):
+        invs = np.float32(1.0) / np.float32(s[l])
+        out.append((int(np.rint(np.float32(w) * invs)), int(np.rint(np.float32(h) * invs))))
+    return out
+
+
+def cam_bytes(w, h, n_kp):
+    """SURVEY §8(d) algorithmic bytes of one camera-frame's extraction: every level read once, every derived
+    level written once, 56 B per keypoint (24 B record + 32 B descriptor)."""
+    P = [a * b for a, b in level_sizes(w, h)]
+    return sum(P) + sum(P[1:]) + 56 * n_kp
+
+
+def _gen_p1080_image(item):
+    from openmavis_amd import synth
+    f, c = item
+    return synth.synth_image(synth.P1080_SEED + 1000 * c + f, P_W, P_H)
+
+
+def _gen_p1080_map(args):
+    from openmavis_amd import synth
+    kps, desc, n_kp, seed = args
+    cams, R_cl, t_cl = synth.p1080_rig(P_C, P_W, P_H)
+    pose = synth.random_pose(np.random.default_rng(seed))
+    world, mp = synth.make_world_map(kps, desc, n_kp, P_M, seed, cams, R_cl, t_cl, pose, P_W, P_H, NLEV,
+                                     model="pinhole")
+    return pose, world, mp
+
+
+def p1080_cpu_baseline(frames):
+    """Oracle on a bounded sample: extraction of the 8 cameras (one std::thread each), isInFrustum through
+    Pinhole::project and SearchByProjection over the 8 blocks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from openmavis_amd import synth
+    from openmavis_amd.matcher import make_rig
+    cams, R_cl, t_cl = synth.p1080_rig(P_C, P_W, P_H)
+    rig = make_rig(cams, R_cl, t_cl, P_W, P_H, model="pinhole")
+    g = oracle.frame_geom(P_C, P_W, P_H, oracle.orb_tables(P_NF, SCALE, NLEV)["scale"])
+    lap = np.zeros((P_C, 2), np.int32)
+    preps = []
+    for i, imgs in enumerate(frames):
+        n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, P_NF, lap, SCALE, NLEV, P_INI, P_MIN)
+        preps.append(_gen_p1080_map((kps, desc, n_out, 900 + i)))
+    t0 = time.perf_counter()
+    for imgs, (pose, world, mp) in zip(frames, preps):
+        n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, P_NF, lap, SCALE, NLEV, P_INI, P_MIN)
+        track, _ = oracle.frustum(rig, pose, world["pos"], world["normal"], world["min_dist"], world["max_dist"], 0.5,
+                                  mp["view_cos"], mp["track_depth"])
+        no = np.full(kps.shape[1], -1, np.int32)
+        oracle.search_by_projection(g, kps, desc, n_out, dict(mp, **track), P_TH, False, 50.0, NNRATIO, no, no, None,
+                                    np.full(P_C * kps.shape[1], -1, np.int32))
+    dt = time.perf_counter() - t0
+    return dict(value=round(len(frames) / dt, 3), unit="multi-cam frames/s", cores=P_C, kind="port",
+                sample=f"{len(frames)} frames of 8 x 1920x1080 (2000 feat/cam, M={P_M}), oracle C++ restatement, "
+                       f"one thread per camera, {dt:.1f} s")
+
+
+def p1080_leg(imgs, B, steps, warmup, dev, world, rank, cpu):
+    """BASELINE configs[3]: per frame, 8 Pinhole cameras 1920x1080 extracted (2000 features, iniTh 20, lapping
+    [0,0]) + grid + isInFrustum (Pinhole::project) + SearchByProjection of an 8,000-point 3-D local map.  One GPU:
+    the 8B images in one batch.  N GPUs: camera-sharded (rank r extracts cameras r, r+N, ...; one all-gather of
+    the slabs; matching on rank 0).  imgs: this rank's images, frame-major [B][8] on one GPU, cam-major [k][B]
+    (its k cameras) when sharded."""
+    import torch
+    import torch.distributed as tdist
+    from openmavis_amd import synth
+    from openmavis_amd.dist import CameraShard, job_seconds
+    from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher, isInFrustum, make_rig
+    from openmavis_amd.orb import ORBextractor
+    shard = world > 1
+    my_cams = list(range(rank, P_C, world)) if shard else list(range(P_C))
+    n_img = len(my_cams) * B
+    ex = ORBextractor(P_NF, SCALE, NLEV, P_INI, P_MIN, width=P_W, height=P_H, max_images=max(1, n_img))
+    cap = ex.max_keypoints()
+    fb = FrameBatch(torch, B, P_C, cap, P_W, P_H, ex.GetScaleFactors(), device=dev)
+    d_img = torch.from_numpy(imgs).to(dev) if n_img else None
+    lap = np.zeros((max(1, n_img), 2), np.int32)
+    sh = CameraShard(rank, world, P_C, B, cap, dev, mode=_slab_mode()) if shard else None
+    if shard:   # this rank's cameras, cam-major, straight into its slab
+        kps_o, desc_o, n_o, mono_o = sh.outputs()
+    else:       # frame-major images straight into the frame batch
+        kps_o, desc_o, n_o, mono_o = fb.kps.view(-1, cap, 6), fb.desc.view(-1, cap, 32), fb.n_kp.view(-1), \
+            fb.mono.view(-1)
+
+    def extract():
+        if n_img:
+            ex.extract_batch(d_img, lap[:n_img], kps_o, desc_o, n_o, mono_o)
+
+    def assemble():
+        if shard:
+            sh.gather(fb)
+
+    extract()
+    assemble()
+    torch.cuda.synchronize(dev)
+    assert ex.last_error() == 0, "p1080 extraction capacity error"
+    cams, R_cl, t_cl = synth.p1080_rig(P_C, P_W, P_H)
+    rig = make_rig(cams, R_cl, t_cl, P_W, P_H, model="pinhole")
+    m = ORBmatcher(NNRATIO)
+    if rank == 0:   # the tracking rank's 3-D local maps, from the frames' own keypoints (setup, untimed)
+        kv = fb.kps.cpu().numpy().view(np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                                 ("response", "<f4"), ("octave", "<i4")])).reshape(B, P_C, cap)
+        dh, nh = fb.desc.cpu().numpy(), fb.n_kp.cpu().numpy()
+        per = [_gen_p1080_map((kv[f], dh[f], nh[f], 900 + f)) for f in range(B)]
+        poses = torch.from_numpy(np.stack([p[0] for p in per])).to(dev)
+        wmap = {k: torch.from_numpy(np.stack([p[1][k] for p in per])).to(dev) for k in per[0][1]}
+        mps = MapPointBatch(**{k: torch.from_numpy(np.stack([p[2][k] for p in per])).to(dev) for k in per[0][2]})
+
+    def step():
+        extract()
+        assemble()
+        if rank == 0:
+            fb.kp_to_mp.fill_(-1)
+            m.AssignFeaturesToGrid(fb)
+            isInFrustum(poses, rig, wmap, mps, 0.5)
+            m.SearchByProjection(fb, mps, P_TH, False, 50.0, grid_ready=True)
+
+    for _ in range(warmup):
+        step()
+    if shard:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if shard:
+        tdist.barrier()
+    dt = job_seconds(time.perf_counter() - t0, dev)
+    # extraction alone (HIP events on the launch stream): the §8(d) roofline of this rank's extraction launch
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    ext_ms = None
+    if n_img:
+        ev0.record()
+        for _ in range(reps):
+            extract()
+        ev1.record()
+        torch.cuda.synchronize(dev)
+        ext_ms = ev0.elapsed_time(ev1) / reps
+    n_kp_img = int(n_o.sum().item()) if n_img else 0
+    if rank != 0:
+        return None
+    bytes_launch = sum(cam_bytes(P_W, P_H, 0) for _ in range(n_img)) + 56 * n_kp_img
+    out = {"metric": "multi-cam frames/s (8 x 1920x1080 Pinhole, ORB extract + isInFrustum + SearchByProjection)",
+           "value": round(B * steps / dt, 2), "unit": "multi-cam frames/s", "ms_per_step": round(dt / steps * 1e3, 3),
+           "frames_per_step": B, "n_gpus": world, "scaling": "strong" if shard else "weak",
+           "matches_last_step": int(fb.n_matches.sum().item()),
+           "config": {"workload": "synthetic 8-cam Pinhole rig 1920x1080, 2000 feat/cam, iniTh 20, lapping [0,0], "
+                                  f"M={P_M} map points, th {P_TH}",
+                      "parallelism": f"camera-sharded x{world} (RCCL all-gather of the slabs, matching on rank 0)"
+                      if shard else "8-camera batch on one GPU"}}
+    if ext_ms:
+        ach = bytes_launch / (ext_ms * 1e-3) / 1e9
+        out["extraction_roofline"] = {
+            "kernel": "ORB extraction (pyramid + FAST + octree + describe), rank 0's launch", "bound": "hbm",
+            "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+            "avg_launch_ms": round(ext_ms, 4), "images_per_launch": n_img,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "bytes_per_camera_at_2000_kp": cam_bytes(P_W, P_H, 2000)}
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    return out
+
+
+def cam_shard_leg(imgs, B, steps, warmup, dev, world, rank):
+    """BASELINE configs[2]: the Hilti 5-camera frame with its cameras sharded over the ranks (rank r extracts
+    cameras r, r+N, ...), ONE all-gather of the keypoint / descriptor slabs over RCCL, then the tracking rank's
+    matching (grid, lapping knn, SearchByProjection; SURVEY §8e: matching is replicas only).  imgs: this rank's
+    images, cam-major [k][B]."""
+    import torch
+    import torch.distributed as tdist
+    from openmavis_amd.dist import CameraShard, job_seconds
+    from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher
+    from openmavis_amd.orb import ORBextractor
+    from openmavis_amd import synth
+    my_cams = list(range(rank, C, world))
+    n_img = len(my_cams) * B
+    ex = ORBextractor(NFEAT, SCALE, NLEV, INI_TH, MIN_TH, width=W, height=H, max_images=max(1, n_img))
+    cap = ex.max_keypoints()
+    fb = FrameBatch(torch, B, C, cap, W, H, ex.GetScaleFactors(), device=dev)
+    sh = CameraShard(rank, world, C, B, cap, dev, mode=_slab_mode())
+    kps_o, desc_o, n_o, mono_o = sh.outputs()
+    d_img = torch.from_numpy(imgs).to(dev) if n_img else None
+    lap = np.array([LAP[c] for c in my_cams for _ in range(B)], np.int32).reshape(-1, 2)
+    m = ORBmatcher(NNRATIO)
+
+    def gather():
+        if n_img:
+            ex.extract_batch(d_img, lap, kps_o, desc_o, n_o, mono_o)
+        sh.gather(fb)
+
+    gather()
+    torch.cuda.synchronize(dev)
+    if rank == 0:
+        kv = fb.kps.cpu().numpy().view(np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                                 ("response", "<f4"), ("octave", "<i4")])).reshape(B, C, cap)
+        dh, nh = fb.desc.cpu().numpy(), fb.n_kp.cpu().numpy()
+        per = [synth.make_map_points(kv[f], dh[f], nh[f], M_MPS, 300 + f, W, H) for f in range(B)]
+        mps = MapPointBatch(**{k: torch.from_numpy(np.stack([p[k] for p in per])).to(dev) for k in per[0]})
+
+    def step():
+        gather()
+        if rank == 0:
+            fb.kp_to_mp.fill_(-1)
+            m.AssignFeaturesToGrid(fb)
+            m.StereoLapping(fb, 0.8)
+            m.SearchByProjection(fb, mps, TH, False, 50.0, grid_ready=True)
+
+    for _ in range(warmup):
+        step()
+    tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    tdist.barrier()
+    dt = job_seconds(time.perf_counter() - t0, dev)
+    if rank != 0:
+        return None
+    return {"metric": "multi-cam frames/s (5x720x540, cameras sharded over the GPUs)",
+            "value": round(B * steps / dt, 2), "unit": "multi-cam frames/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "frames_per_step": B, "n_gpus": world, "scaling": "strong",
+            "slab_bytes_per_rank": sh.words * 4, "matches_last_step": int(fb.n_matches.sum().item()),
+            "config": {"workload": "Hilti-like 5 cams 720x540, 1200 feat/cam: extraction sharded one camera per "
+                                   "GPU, RCCL all-gather of keypoints + descriptors, grid + lapping knn + "
+                                   f"SearchByProjection(M={M_MPS}) on rank 0",
+                       "parallelism": f"camera-sharded x{world}"}}
+
+
+def latency_leg(d_img, gr0, n_frames, dev, rig, stereo):
+    """Single-frame latency of the sequential tracker (frame t+1's search needs frame t's pose): one multi-camera
+    frame at a time on one stream (B = 1), extract + grid + lapping knn + TriangulateMatches + mvuRight +
+    isInFrustum + SearchByProjection, synchronised per frame; p50 / p99 of the per-frame wall time."""
+    import torch
+    from openmavis_amd.frame import frame_uright
+    from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher, isInFrustum
+    from openmavis_amd.orb import ORBextractor
+    ex = ORBextractor(NFEAT, SCALE, NLEV, INI_TH, MIN_TH, width=W, height=H, max_images=C)
+    cap = ex.max_keypoints()
+    fb = FrameBatch(torch, 1, C, cap, W, H, ex.GetScaleFactors(), device=dev)
+    m = ORBmatcher(NNRATIO)
+    n_avail = gr0["poses"].shape[0]
+    frames = []
+    for f in range(n_avail):
+        frames.append(dict(img=d_img[f * C:(f + 1) * C], pose=gr0["poses"][f:f + 1],
+                           world={k: v[f:f + 1] for k, v in gr0["world"].items()},
+                           mps=MapPointBatch(**{k: getattr(gr0["mps"], k)[f:f + 1].clone()
+                                                for k in MapPointBatch.FIELDS}),
+                           depth=gr0["depth"][f:f + 1].contiguous()))
+    ur = torch.empty((1, min(4, C), cap), dtype=torch.float32, device=dev)
+    Rlr, tlr, BF, sigma2, cams_r = stereo
+
+    def one(fr):
+        ex.extract_batch(fr["img"], LAP, fb.kps.view(-1, cap, 6), fb.desc.view(-1, cap, 32), fb.n_kp.view(-1),
+                         fb.mono.view(-1))
+        fb.kp_to_mp.fill_(-1)
+        m.AssignFeaturesToGrid(fb)
+        m.StereoLapping(fb, 0.8)
+        m.StereoTriangulate(fb, cams_r[:2], Rlr, tlr, sigma2)
+        frame_uright(fb, fr["depth"], BF, out=ur)
+        isInFrustum(fr["pose"], rig, fr["world"], fr["mps"], 0.5)
+        m.SearchByProjection(fb, fr["mps"], TH, False, 50.0, grid_ready=True)
+
+    for i in range(5):
+        one(frames[i % n_avail])
+    torch.cuda.synchronize(dev)
+    lat = []
+    for i in range(n_frames):
+        t0 = time.perf_counter()
+        one(frames[i % n_avail])
+        torch.cuda.synchronize(dev)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    lat = np.array(lat)
+    return {"metric": "single-frame latency (B=1, one stream, synchronised per frame)", "unit": "ms",
+            "p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
+            "mean_ms": round(float(lat.mean()), 4), "frames": n_frames,
+            "sequential_frames_per_s": round(1e3 / float(np.percentile(lat, 50)), 1)}
+
+
+def _slab_mode():
+    import torch.distributed as tdist
+    return "host" if tdist.get_backend() == "gloo" else "device"
+
+
+def _launch_ranks(n):
+    """--gpus N > 1 outside torch.distributed: start N ranks (one process per GPU) and return their status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -412,26 +814,54 @@ def main():
     ap.add_argument("--lba-shard", action="store_true",
                     help="N>1: shard one window's landmarks over the ranks (RCCL all-reduce per LM trial) "
                          "instead of running a window replica per rank")
-    ap.add_argument("--cpu-frames", type=int, default=120, help="frames in the CPU-baseline sample (~6 s)")
+    ap.add_argument("--cpu-frames", type=int, default=60, help="frames in the mode-A CPU sample (~10 s)")
+    ap.add_argument("--cpu-best-frames", type=int, default=64, help="frames in the mode-B (all-core) CPU sample")
     ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
     ap.add_argument("--pose-frames", type=int, default=1024, help="frames per PoseInertialOptimization batch (0: skip)")
     ap.add_argument("--tri-pairs", type=int, default=256, help="keyframe pairs per SearchForTriangulation batch (0: skip)")
     ap.add_argument("--aux", type=int, default=1, help="Fuse / DBoW2 transform / IMU preintegration legs (0: skip)")
+    ap.add_argument("--p1080-frames", type=int, default=16, help="configs[3] 8 x 1920x1080 frames per step (0: skip)")
+    ap.add_argument("--p1080-steps", type=int, default=10)
+    ap.add_argument("--p1080-cpu-frames", type=int, default=2)
+    ap.add_argument("--shard-frames", type=int, default=64, help="N>1: frames per step of the camera-sharded leg")
+    ap.add_argument("--latency-frames", type=int, default=200, help="B=1 sequential frames timed (0: skip)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))   # before anything touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     B = args.frames
     first = rank * B
-    # inputs are generated before anything touches the GPU (worker pool = plain fork, no HIP yet)
+    # inputs are generated before anything touches the GPU (host pool = plain fork, no HIP yet)
     imgs = np.concatenate(_pool_map(_gen_frame, list(range(first, first + B))))   # [B*C, H, W]
-    cpu_frames = [] if (args.no_cpu_baseline or world > 1) else _pool_map(
-        _gen_frame, list(range(10_000, 10_000 + args.cpu_frames)))
+    cpu = p1080_cpu = lba_cpu = None
     lba_prob = None
     if args.lba_steps > 0:
         from openmavis_amd import synth_ba
         lba_prob = synth_ba.make_lba_problem(seed=5)   # configs[4] window (same on every rank)
+    do_cpu = not args.no_cpu_baseline and world == 1
+    p_imgs = None
+    if args.p1080_frames > 0:
+        PB = args.p1080_frames
+        items = [(f, c) for f in range(PB) for c in range(P_C)] if world == 1 else \
+            [(f, c) for c in range(rank, P_C, world) for f in range(PB)]
+        p_imgs = np.stack(_pool_map(_gen_p1080_image, items)) if items else np.zeros((0, P_H, P_W), np.uint8)
+        if do_cpu and args.p1080_cpu_frames > 0:
+            p1080_cpu = p1080_cpu_baseline([np.stack([_gen_p1080_image((10_000 + f, c)) for c in range(P_C)])
+                                            for f in range(args.p1080_cpu_frames)])
+    s_imgs = None
+    if world > 1 and args.shard_frames > 0:
+        SB = args.shard_frames
+        s_imgs = np.stack([img for c in range(rank, C, world) for img in
+                           _pool_map(_gen_cam_image, [(c, 20_000 + f) for f in range(SB)])]) \
+            if rank < C else np.zeros((0, H, W), np.uint8)
+    if do_cpu:   # CPU baselines on this host, before the GPU work
+        cpu_frames = _pool_map(_gen_frame, list(range(10_000, 10_000 + args.cpu_frames)))
+        cpu = cpu_baseline(cpu_frames, args.cpu_best_frames)
+        if lba_prob is not None:
+            lba_cpu = lba_cpu_baseline(lba_prob, args.cpu_lba_runs)
     pose_batch = pose_cpu = lf_batch = lf_cpu = None
     if args.pose_frames > 0:
         from openmavis_amd import synth_pose
@@ -443,15 +873,21 @@ def main():
     if args.tri_pairs > 0:
         from openmavis_amd import synth_tri
         tri_pairs = [synth_tri.make_tri_pair(seed=s, n_pts=1200, n_distract=600) for s in range(16)]
+    _close_pool()   # no forked worker outlives the host phase
 
     import torch
     import torch.distributed as dist
 
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    # OMV_BENCH_REHEARSE=1: rehearse the N-rank path on a box with fewer GPUs (ranks share cards, gloo collectives,
+    # slabs staged through host memory); never used for a reported number
+    rehearse = os.environ.get("OMV_BENCH_REHEARSE") == "1"
+    dev = torch.device("cuda", (local % torch.cuda.device_count()) if rehearse else (local if world > 1 else 0))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from openmavis_amd.dist import job_seconds
     from openmavis_amd import synth
@@ -566,8 +1002,18 @@ def main():
             for k, v in {**es, **ms}.items():
                 stages[k] = stages.get(k, 0.0) + v / args.steps
             stages["frustum"] = stages.get("frustum", 0.0) + sum(a.elapsed_time(b) for a, b in gr["ev"]) / args.steps
+            gr["ex"].enable_timing(False)
+            gr["matcher"].enable_timing(False)
 
+    lat = latency_leg(d_img, groups[0], args.latency_frames, dev, rig, (Rlr, tlr, BF, sigma2, cams_r)) \
+        if args.latency_frames > 0 and rank == 0 else None
+    shard_leg = cam_shard_leg(s_imgs, args.shard_frames, 10, 2, dev, world, rank) \
+        if s_imgs is not None else None
+    p1080 = p1080_leg(p_imgs, args.p1080_frames, args.p1080_steps, 2, dev, world, rank, p1080_cpu) \
+        if p_imgs is not None else None
     lba = lba_leg(lba_prob, args.lba_steps, args.lba_warmup, dev, world, args.lba_shard) if lba_prob is not None else None
+    if lba is not None and lba_cpu is not None:
+        lba["cpu_baseline"] = lba_cpu
     pose = pose_leg(pose_batch, pose_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev) \
         if pose_batch is not None else None
     pose_lf = pose_leg(lf_batch, lf_cpu if rank == 0 and not args.no_cpu_baseline else None, 10, dev, last_frame=True) \
@@ -582,8 +1028,8 @@ def main():
 
     total_frames = B * world * args.steps
     value = total_frames / dt
-    # roofline of the dominant kernel: algorithmic bytes per launch / measured average duration
-    P = level_pixels()
+    # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes per launch / measured average duration
+    P = [a * b for a, b in level_sizes(W, H)]
     n_kp_step = int(nkp_h.sum())   # keypoints per step (same frames every step)
     per_step_bytes = {
         # pyramid: level l-1 read, level l written, l = 1..7
@@ -592,8 +1038,9 @@ def main():
         "fast_cells": B * C * sum(P),
         # octree: candidates are tiny; listed for completeness (latency-bound)
         "octree": B * C * 8 * 2500,
-        # describe: 43x43 window per keypoint + 56 B record
-        "describe": n_kp_step * (43 * 43 + 56),
+        # describe (§8(d)): every level read once (patches overlap; the level is the unit of traffic) + the
+        # 56-B keypoint record / descriptor written per keypoint
+        "describe": B * C * sum(P) + n_kp_step * 56,
         "grid": n_kp_step * 28,
         # isInFrustum: per point pos/normal/min/max in, per (point, cam) proj x/y, cos, level, flag out
         "frustum": B * M_MPS * (32 + C * 17 + 4),
@@ -611,7 +1058,8 @@ def main():
         achieved = per_step_bytes[dom] / launches / (avg_ms * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_step_bytes[dom] // launches}
+                "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_step_bytes[dom] // launches,
+                "bytes_formula": "SURVEY 8(d): describe = sum of level pixels + 56 B per keypoint, per image"}
         pmc = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
         if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch's images
             try:
@@ -621,11 +1069,10 @@ def main():
                     roof["traffic_source"] = f"profiles/pmc_{dom}.json ({rec['tag']}), per image x {Bg * C} images"
             except Exception:
                 pass
-    cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(len(cpu_frames), cpu_frames)
-        if lba is not None:
-            lba["cpu_baseline"] = lba_cpu_baseline(lba_prob, args.cpu_lba_runs)
+        # the whole path: SURVEY §8(d) bytes of a multi-camera frame (5 extractions + matching) x frames/s
+        frame_bytes = C * cam_bytes(W, H, 0) + 56 * n_kp_step / B + 968_000
+        roof["pipeline"] = {"bytes_per_frame": int(frame_bytes), "achieved": round(frame_bytes * value / 1e9, 2),
+                            "unit": "GB/s", "frac": round(frame_bytes * value / 1e9 / HBM_PEAK_GBS, 5)}
     out = {
         "metric": "multi-cam frames/sec (ORB extract+match) + LocalBA iters/sec, 5x720x540",
         "value": round(value, 2),
@@ -646,6 +1093,9 @@ def main():
         "matches_last_step": n_matches,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "latency_b1": lat,
+        "cam_shard": shard_leg,
+        "p1080": p1080,
         "local_ba": lba,
         "pose_inertial": pose,
         "pose_inertial_last_frame": pose_lf,
