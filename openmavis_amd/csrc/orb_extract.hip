@@ -1,5 +1,5 @@
 // MI355X-native ORB extractor: the path of ORBextractor::operator() (src/ORBextractor.cc:987-1071)
-// as four gfx950 kernels over a batch of device-resident images.
+// as five gfx950 kernels over a batch of device-resident images.
 //
 //   K1 pyr_resize   one launch per pyramid level l >= 1, level l from level l-1 (ComputePyramid
 //                   :1073-1104; cv::resize INTER_LINEAR 8U fixed point), coefficient tables
@@ -13,11 +13,13 @@
 //                   LDS for quadrant counts) plus the libstdc++ introsort replica for the
 //                   (size, UL.x) refinement ordering; picks max-response key per node; classifies
 //                   lapping/non-lapping for the output split (:1045-1067).
-//   K4 describe     one wavefront per keypoint: the 43x43 reflect-101 patch goes to LDS once;
-//                   intensity-centroid angle (IC_Angle :19-43, fastAtan2), the 7x7 sigma-2 blur of
-//                   the 37x37 sampling window (GaussianBlur 8U bit-exact path), steered rBRIEF via
-//                   4 ballots (computeOrbDescriptor :46-90); writes the keypoint and descriptor
-//                   straight into its final (mono-front / lapping-back) row.
+//   K4 blur         every level blurred once into a blurred pyramid (GaussianBlur 7x7 sigma 2,
+//                   :1035-1036, OpenCV's bit-exact 8U path, BORDER_REFLECT_101 on the level), one
+//                   workgroup per 32x128 tile staged in LDS.
+//   K5 describe     one wavefront per keypoint: intensity-centroid angle over the un-blurred level
+//                   (IC_Angle :19-43, fastAtan2) and steered rBRIEF by byte gathers from the blurred
+//                   level, 4 ballots (computeOrbDescriptor :46-90); writes the keypoint and
+//                   descriptor straight into its final (mono-front / lapping-back) row.
 //
 // All float code is compiled with -ffp-contract=off (see omv_device.h).
 #include <hip/hip_runtime.h>
@@ -35,16 +37,9 @@
 namespace {
 
 constexpr int kMaxLevels = 16;
+constexpr int kOrbStages = 5;   // pyramid, FAST cells, octree, blur, describe (omv_orb_stage_ms)
 constexpr int kEdge = 19;     // EDGE_THRESHOLD
 constexpr int kMinB = kEdge - 3;
-constexpr int kPatchR = 21;   // 18 (max steered pattern radius) + 3 (blur half-width)
-constexpr int kPatchW = 2 * kPatchR + 1;   // 43
-constexpr int kWinR = 18;
-constexpr int kWinW = 2 * kWinR + 1;       // 37
-constexpr int kPatchS = 48;                 // LDS row stride of the staged patch: 12 dwords cover 43 + 3
-constexpr int kHsS = 40;                    // horizontal blur sums: 10 quads of columns per patch row
-constexpr int kHtS = 44;                    // ... stored column-major, 43 rows + pad per column (u16)
-
 #define OMV_PATTERN_TABLE_BEGIN
 #define OMV_PATTERN_TABLE_END
 constexpr int kPattern[256 * 4] = {
@@ -100,6 +95,10 @@ struct Geom {
     int out_per_img;        // level-output slots per image
     int n_max;              // output rows per image
     int node_cap;           // octree LDS node capacity
+    // blurred pyramid (K4): level 0 at pitch blur_pitch0, levels >= 1 at the pyramid's offsets/pitches
+    int blur_pitch0;
+    long long blur0_bytes, blur_bytes;   // level-0 block, whole per-image block
+    int blur_tile_off[kMaxLevels + 1];   // first K4 tile of each level within an image (last = tiles/image)
     LevelGeom lv[kMaxLevels];
 };
 
@@ -828,43 +827,127 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
 }
 
 // K4 --------------------------------------------------------------------------------------------
-// LDS written by this wavefront and read back by its other lanes: LDS operations of one wave complete in
-// order, so the fence only has to stop the compiler from moving them (wavefront scope).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// GaussianBlur 7x7, sigma 2 (ORBextractor.cc:1035-1036; OpenCV's bit-exact 8U path): every pyramid level
+// blurred once, as the reference does, into a blurred pyramid with the same layout.  One workgroup per
+// 32-row x 128-column tile of a level: the 38 x 136 source bytes (BORDER_REFLECT_101 on the level's own
+// bounds) are staged in LDS as dwords, the horizontal 7-tap sums of 4 adjacent columns are two v_dot4_u32_u8
+// on byte-aligned dwords (u16 exact), the vertical taps a multiply-add chain (u24 operands), and each quad of blurred
+// pixels is stored as one dword: (sum_i k_i sum_j k_j p + 2^15) >> 16 with k = [18, 34, 48, 56, 48, 34, 18].
+constexpr int kBlurTH = 32, kBlurTW = 128;              // output tile
+constexpr int kBlurSR = kBlurTH + 6, kBlurSD = kBlurTW / 4 + 2;   // staged rows, staged dwords per row (136 B)
 
-// Horizontal 7-tap sums of the staged patch (patch byte (r, c) at dword 12 r, byte SH + c): per lane 4
-// adjacent window columns from 4 dwords, as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
-// items i = lane + 64 t, (row, quad) = (i / 10, i % 10) stepped incrementally.
-template <int SH>
-__device__ __forceinline__ void hsum_rows(const uint32_t *pw, uint16_t *Hs, int lane) {
-    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-    int r = lane / 10, jq = lane - 10 * r;
-    for (int i = lane; i < kPatchW * (kHsS / 4); i += 64) {
-        const int dw0 = r * (kPatchS / 4) + jq;
-        const uint32_t D[4] = {pw[dw0], pw[dw0 + 1], pw[dw0 + 2], pw[dw0 + 3]};
-        uint32_t h[4];
-#pragma unroll
-        for (int sc = 0; sc < 4; ++sc) {
-            const int bb = SH + sc, j = bb >> 2, al = bb & 3;
-            const uint32_t w0 = __builtin_amdgcn_alignbyte(D[j + 1], D[j], al);
-            const uint32_t w1 = __builtin_amdgcn_alignbyte(D[j + 2 < 4 ? j + 2 : 3], D[j + 1], al);
-            h[sc] = __builtin_amdgcn_udot4(w1, G1, __builtin_amdgcn_udot4(w0, G0, 0u, false), false);
-        }
-#pragma unroll
-        for (int sc = 0; sc < 4; ++sc) Hs[(4 * jq + sc) * kHtS + r] = (uint16_t)h[sc];
-        jq += 4, r += 6;
-        if (jq >= kHsS / 4) jq -= kHsS / 4, ++r;
-    }
-}
-
-struct DescArgs {
+struct BlurArgs {
     const uint8_t *images;
     size_t img_stride, pitch0;
     const uint8_t *pyr;
+    uint8_t *blur;
+};
+
+__device__ __forceinline__ uint8_t *blur_level(const Geom &g, uint8_t *blur, int img, int l, int *pitch) {
+    if (l == 0) {
+        *pitch = g.blur_pitch0;
+        return blur + (size_t)img * g.blur_bytes;
+    }
+    *pitch = g.lv[l].pitch;
+    return blur + (size_t)img * g.blur_bytes + g.blur0_bytes + g.lv[l].off;
+}
+
+__global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_blocks) {
+    __shared__ __attribute__((aligned(16))) uint32_t raw[kBlurSR * kBlurSD];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[kBlurSR * kBlurTW];
+    const int blk = xcd_block(n_blocks);
+    if (blk < 0) return;
+    const int tpi = g.blur_tile_off[g.nlevels];
+    const int img = blk / tpi;
+    const int t = blk - img * tpi;
+    int l = 0;
+    while (l + 1 < g.nlevels && t >= g.blur_tile_off[l + 1]) ++l;
+    const LevelGeom &L = g.lv[l];
+    const int tcols = (L.w + kBlurTW - 1) / kBlurTW;
+    const int tr = (t - g.blur_tile_off[l]) / tcols, tc = (t - g.blur_tile_off[l]) - tr * tcols;
+    const int y0 = tr * kBlurTH, x0 = tc * kBlurTW;
+    int sp;
+    const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
+    const int tid = threadIdx.x;
+    // stage rows y0-3 .. y0+34, bytes x0-4 .. x0+131 (reflect-101 outside the level)
+    const bool interior_x = x0 >= 4 && x0 + kBlurTW + 4 <= L.w;
+    for (int i = tid; i < kBlurSR * kBlurSD; i += 256) {
+        const int r = i / kBlurSD, d = i - r * kBlurSD;
+        const int yy = omv::reflect101(min(y0 - 3 + r, 2 * L.h - 2), L.h);
+        const uint8_t *row = src + (size_t)yy * sp;
+        const int c0 = x0 - 4 + 4 * d;
+        uint32_t v;
+        if (interior_x && ((((uintptr_t)row) & 3) == 0)) {
+            v = *reinterpret_cast<const uint32_t *>(row + c0);
+        } else {
+            v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int xx = c0 + b;
+                const uint32_t px = (xx >= -L.w + 1 && xx < 2 * L.w - 1) ? row[omv::reflect101(xx, L.w)] : 0u;
+                v |= px << (8 * b);
+            }
+        }
+        raw[i] = v;
+    }
+    __syncthreads();
+    // horizontal: staged byte 4 q + 1 + s .. 4 q + 7 + s -> output column x0 + 4 q + s
+    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+    for (int i = tid; i < kBlurSR * (kBlurTW / 4); i += 256) {
+        const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
+        const uint32_t *D = raw + r * kBlurSD + q;
+        const uint32_t d0 = D[0], d1 = D[1], d2 = D[2];
+        uint32_t h[4];
+        h[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), G1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), G0, 0u, false), false);
+        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), G1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), G0, 0u, false), false);
+        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), G1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), G0, 0u, false), false);
+        h[3] = __builtin_amdgcn_udot4(d2, G1, __builtin_amdgcn_udot4(d1, G0, 0u, false), false);
+        *reinterpret_cast<uint2 *>(hs + r * kBlurTW + 4 * q) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    }
+    __syncthreads();
+    // vertical at the tile's output quads
+    int bp;
+    uint8_t *dst = blur_level(g, a.blur, img, l, &bp);
+    const int rows = min(kBlurTH, L.h - y0), cols = min(kBlurTW, L.w - x0);
+    for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
+        const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
+        if (r >= rows || 4 * q >= cols) continue;
+        uint32_t s0 = 32768u, s1 = 32768u, s2 = 32768u, s3 = 32768u;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const uint2 hv = *reinterpret_cast<const uint2 *>(hs + (r + k) * kBlurTW + 4 * q);
+            const uint32_t kk = (uint32_t)c_gauss7[k];
+            s0 += (hv.x & 0xffffu) * kk;
+            s1 += (hv.x >> 16) * kk;
+            s2 += (hv.y & 0xffffu) * kk;
+            s3 += (hv.y >> 16) * kk;
+        }
+        const uint32_t packed = min(s0 >> 16, 255u) | (min(s1 >> 16, 255u) << 8) | (min(s2 >> 16, 255u) << 16) |
+                                (min(s3 >> 16, 255u) << 24);
+        uint8_t *o = dst + (size_t)(y0 + r) * bp + x0 + 4 * q;
+        if (4 * q + 3 < cols) {
+            *reinterpret_cast<uint32_t *>(o) = packed;
+        } else {
+            for (int b = 0; 4 * q + b < cols; ++b) o[b] = (uint8_t)(packed >> (8 * b));
+        }
+    }
+}
+
+// K5 --------------------------------------------------------------------------------------------
+// Orientation + rBRIEF, one wavefront per output slot (inactive slots leave at once):
+//   IC_Angle (:19-43) over the r = 15 disc of the UN-blurred level: per (disc row, dword) one v_dot4 with the
+//   in-disc byte mask (row sum -> m01) and one with the weights u + 15 (m10), from two aligned dword loads and
+//   a v_alignbyte; a wave reduction; fastAtan2 (degrees, float);
+//   computeOrbDescriptor (:46-90) on the BLURRED level: lane = pattern pair (4 rounds of 64), steering by
+//   (cos, sin) with cvRound, the two samples as byte gathers (L2-resident: the image's levels were just
+//   blurred), bit = I(a) < I(b) collected by 4 ballots = 32 bytes.
+struct DescArgs {
+    const uint8_t *images;
+    size_t img_stride, pitch0;
+    const uint8_t *pyr, *blur;
     const uint32_t *lvl_out, *lvl_cls;
     const int *lvl_cnt;
     omv_kp *kps;
@@ -873,152 +956,86 @@ struct DescArgs {
     int n_images;
 };
 
-__global__ void __launch_bounds__(256, 7) describe_kernel(Geom g, DescArgs a, int n_blocks) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kPatchS + 8];
-    __shared__ __attribute__((aligned(16))) uint16_t hsum[4][kHsS * kHtS];
+__global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int blk = xcd_block(n_blocks);
     if (blk < 0) return;
     const int slot = blk * 4 + wave;
-    int img = slot / g.out_per_img;
+    const int img = slot / g.out_per_img;
     const int s = slot - img * g.out_per_img;
-    const bool in_range = img < a.n_images;
-    if (!in_range) img = a.n_images - 1;   // tail waves of the last block: compute nothing
-    // which level does slot s belong to
+    if (img >= a.n_images) return;
     int l = 0;
     while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_off) ++l;
     const LevelGeom &L = g.lv[l];
     const int j = s - L.out_off;
     const int *cnts = a.lvl_cnt + (size_t)img * g.nlevels * 3;
-    if (in_range && s == 0 && lane == 0) {
+    if (s == 0 && lane == 0) {
         int tot = 0, mono = 0;
         for (int q = 0; q < g.nlevels; ++q) tot += cnts[3 * q], mono += cnts[3 * q + 1];
         a.n_out[img] = tot;
         a.mono[img] = mono;
     }
-    // Each wave owns its LDS slices (patch[wave], hsum[wave]): wave-scope syncs only, so the four waves of a
-    // workgroup run independently and an inactive one leaves at once.
-    const bool active = in_range && j < cnts[3 * l];
-#ifdef OMV_DESC_PROFILE
-    const long long t0 = wall_clock64();
-#endif
-    if (!active) return;
-    uint32_t pat[4];   // this lane's pattern pairs of the four ballot rounds (latency overlaps the staging)
-#pragma unroll
-    for (int rd = 0; rd < 4; ++rd) pat[rd] = c_pattern8.v[rd * 64 + lane];
+    if (j >= cnts[3 * l]) return;
     const uint32_t p = a.lvl_out[(size_t)img * g.out_per_img + s];
     const uint32_t cl = a.lvl_cls[(size_t)img * g.out_per_img + s];
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
     const int score = (int)(p >> 24);
     int sp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
-    // stage the 43x43 patch (row stride kPatchS): interior patches as 12 aligned dwords per row (lane ->
-    // row lane / 12 + 5k, dword lane % 12 for lanes < 60), all loads issued before any LDS store; patches
-    // touching the level border take reflect101 byte loads
-    uint8_t *P = patch[wave];
-    const int x0 = cx - kPatchR, y0 = cy - kPatchR;
-    // the 12 dwords of a row reach byte (x0 & ~3) + 47: keep them inside the row's pitch (hence inside the
-    // image / level allocation even on its last row)
-    const bool inner = x0 >= 0 && y0 >= 0 && x0 + kPatchW <= L.w && y0 + kPatchW <= L.h && (sp & 3) == 0 &&
-                       (((uintptr_t)src) & 3) == 0 && (x0 & ~3) + 48 <= sp;
-    if (inner) {
-        const uint8_t *r0 = src + (size_t)y0 * sp + x0;
-        const int o = (int)(((uintptr_t)r0) & 3);
-        const int lr = lane / 12, lc = lane - 12 * lr;
-        const uint32_t *g0 = (const uint32_t *)(r0 - o) + (size_t)lr * (sp >> 2) + lc;
-        const size_t step = (size_t)5 * (sp >> 2);
-        uint32_t v[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            if (lane < 60 && lr + 5 * k < kPatchW) v[k] = g0[k * step];
-        uint32_t *l0 = reinterpret_cast<uint32_t *>(P) + lane;
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            if (lane < 60 && lr + 5 * k < kPatchW) l0[60 * k] = v[k];
-        P += o;
-    } else {
-        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
-            const int r = i / kPatchW, q = i - r * kPatchW;
-            const int yy = omv::reflect101(y0 + r, L.h), xx = omv::reflect101(x0 + q, L.w);
-            P[r * kPatchS + q] = src[(size_t)yy * sp + xx];
-        }
-    }
-    wave_lds_sync();
-#ifdef OMV_DESC_PROFILE
-    const long long t1 = wall_clock64();
-#endif
-    // intensity centroid over the r = 15 disc (umax rows), exact integer sums: per (row v, dword k of the
-    // row's columns u = 4k + b - 15) one v_dot4 of the pixels with the in-disc mask (row sum, for m01) and
-    // one with the weights u + 15 (m10 = sum (u + 15) I - 15 sum I); masks from c_icmask
-    const int pofs = (int)(P - patch[wave]);
-    const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch[wave]);
+    // intensity centroid: items i = lane + 64 t over (disc row vr = i >> 3, dword k = i & 7), 248 items; the disc
+    // rows are >= 4 rows inside the level, so the second dword of a row never leaves the allocation
     int m01 = 0, m10 = 0;
-    for (int i = lane; i < 31 * 8; i += 64) {
-        const int vr = i >> 3, k = i & 7, v = vr - 15;
-        const uint2 mk = c_icmask[i];
-        const int off = pofs + (kPatchR + v) * kPatchS + 6 + 4 * k, dwi = off >> 2, sh = off & 3;
-        const uint32_t w = __builtin_amdgcn_alignbyte(pw[dwi + 1], pw[dwi], sh);
-        const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
-        m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
-        m01 += v * rs;
+    {
+        uint32_t lo[4], hi[4];
+        int sh[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = lane + 64 * t;
+            const int vr = min(i >> 3, 30), k = i & 7;
+            const uint8_t *ad = src + (size_t)(cy - 15 + vr) * sp + (cx - 15 + 4 * k);
+            const uint32_t *al = reinterpret_cast<const uint32_t *>((uintptr_t)ad & ~(uintptr_t)3);
+            sh[t] = (int)((uintptr_t)ad & 3);
+            lo[t] = al[0];
+            hi[t] = al[1];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = lane + 64 * t;
+            if (i < 31 * 8) {
+                const uint2 mk = c_icmask[i];
+                const uint32_t w = __builtin_amdgcn_alignbyte(hi[t], lo[t], sh[t]);
+                const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
+                m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
+                m01 += ((i >> 3) - 15) * rs;
+            }
+        }
     }
     for (int d = 32; d >= 1; d >>= 1) {
         m01 += __shfl_xor(m01, d, 64);
         m10 += __shfl_xor(m10, d, 64);
     }
     const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
-#ifdef OMV_DESC_PROFILE
-    const long long t2 = wall_clock64();
-#endif
-    // 7x7 sigma-2 blur (GaussianBlur's bit-exact 8U path): horizontal sums exact in u16 over the 43 patch
-    // rows x 37 window columns, 7 taps as two v_dot4_u32_u8 on byte-aligned dwords (v_alignbyte);
-    // vertical ((sum + 2^15) >> 16) evaluated only at the 512 steered sample points.
-    uint16_t *Hs = hsum[wave];
-    switch (pofs & 3) {   // the byte alignment of the patch is wave-uniform: one specialised loop each
-        case 0: hsum_rows<0>(pw, Hs, lane); break;
-        case 1: hsum_rows<1>(pw, Hs, lane); break;
-        case 2: hsum_rows<2>(pw, Hs, lane); break;
-        default: hsum_rows<3>(pw, Hs, lane); break;
-    }
-    wave_lds_sync();
-#ifdef OMV_DESC_PROFILE
-    const long long t3 = wall_clock64();
-#endif
-    // vertical 7-tap sum at window (r, q): the column's sums r..r+6 are contiguous u16, read as 4 dwords
-    // from the pair boundary at or below r and re-paired (v_alignbit by 16 when r is odd), then 4 v_dot2
-    // against the packed taps (18,34)(48,56)(48,34)(18,0) -- the same exact integer sum
-    const uint32_t *Hw = reinterpret_cast<const uint32_t *>(Hs);
-    auto blurred = [&](int r, int q) {   // window coordinates (0..36)
-        const int d0 = (q * kHtS + r) >> 1, sh = (r & 1) << 4;
-        const uint32_t D0 = Hw[d0], D1 = Hw[d0 + 1], D2 = Hw[d0 + 2], D3 = Hw[d0 + 3];
-        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-        auto u2 = [](uint32_t x) { return __builtin_bit_cast(us2, x); };
-        uint32_t acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D1, D0, sh)), u2(18u | (34u << 16)), 0u, false);
-        acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D2, D1, sh)), u2(48u | (56u << 16)), acc, false);
-        acc = __builtin_amdgcn_udot2(u2(__builtin_amdgcn_alignbit(D3, D2, sh)), u2(48u | (34u << 16)), acc, false);
-        acc = __builtin_amdgcn_udot2(u2(D3 >> sh), u2(18u), acc, false);
-        return (int)min((acc + 32768u) >> 16, 255u);
-    };
-    // steered BRIEF: pair i = 64*round + lane -> bit i of the descriptor; ballot = 8 bytes
     float sn, cs;
     omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
-#ifdef OMV_DESC_PROFILE
-    const long long t4 = wall_clock64();
-#endif
     const float fa = cs, fb = sn;
-    uint64_t words[4];
+    int bpitch;
+    const uint8_t *bl = blur_level(g, const_cast<uint8_t *>(a.blur), img, l, &bpitch) + (size_t)cy * bpitch + cx;
+    uint32_t ia[4], ib[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) {
-        const int ax = (int)(int8_t)(pat[rd] & 0xff), ay = (int)(int8_t)((pat[rd] >> 8) & 0xff);
-        const int bx = (int)(int8_t)((pat[rd] >> 16) & 0xff), by = (int)(int8_t)(pat[rd] >> 24);
+        const uint32_t pt = c_pattern8.v[rd * 64 + lane];
+        const int ax = (int)(int8_t)(pt & 0xff), ay = (int)(int8_t)((pt >> 8) & 0xff);
+        const int bx = (int)(int8_t)((pt >> 16) & 0xff), by = (int)(int8_t)(pt >> 24);
         const int ady = omv::round_even((float)ax * fb + (float)ay * fa);
         const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
         const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
         const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
-        const int ia = blurred(kWinR + ady, kWinR + adx);
-        const int ib = blurred(kWinR + bdy, kWinR + bdx);
-        words[rd] = __ballot(ia < ib);
+        ia[rd] = bl[(ptrdiff_t)ady * bpitch + adx];
+        ib[rd] = bl[(ptrdiff_t)bdy * bpitch + bdx];
     }
+    uint64_t words[4];
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) words[rd] = __ballot(ia[rd] < ib[rd]);
     // final row: monoIndex order (front) or lapping order (back, reversed)
     int mono_before = 0, lap_before = 0, total = 0;
     for (int q = 0; q < g.nlevels; ++q) {
@@ -1030,12 +1047,6 @@ __global__ void __launch_bounds__(256, 7) describe_kernel(Geom g, DescArgs a, in
     omv_kp *kp = a.kps + (size_t)img * g.n_max + row;
     uint64_t *dst = reinterpret_cast<uint64_t *>(a.desc + ((size_t)img * g.n_max + row) * 32);
     if (lane < 4) dst[lane] = words[lane];
-#ifdef OMV_DESC_PROFILE
-    if (lane == 0 && img == 0 && (s & 127) == 0) {
-        const long long t6 = wall_clock64();
-        printf("desc slot %d ticks(100MHz) stage %lld centroid+atan %lld hsum %lld sincos %lld brief %lld\n", s, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t6 - t4);
-    }
-#endif
     if (lane == 0) {
         float x = (float)cx, y = (float)cy;
         if (l != 0) x *= L.scale, y *= L.scale;
@@ -1081,7 +1092,7 @@ struct omv_orb {
     // device
     Cell *d_cells = nullptr;
     XTab *d_xt = nullptr, *d_yt = nullptr;
-    uint8_t *d_pyr = nullptr;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     int *d_cell_cnt = nullptr;
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
@@ -1099,14 +1110,14 @@ struct omv_orb {
     int device = 0;
     // optional per-stage HIP-event timing (bench.py): events recorded on the launch stream
     bool timing = false;
-    std::vector<hipEvent_t> ev;   // 5 events per batch: before K1, K2, K3, K4, after K4
-    double stage_ms[4] = {0, 0, 0, 0};
+    std::vector<hipEvent_t> ev;   // 6 events per batch: before K1, K2, K3, K4, K5, after K5
+    double stage_ms[kOrbStages] = {};
     long long stage_calls = 0;
 };
 
 static void flush_timing(omv_orb *o) {
-    for (size_t b = 0; b + 5 <= o->ev.size(); b += 5) {
-        for (int k = 0; k < 4; ++k) {
+    for (size_t b = 0; b + kOrbStages + 1 <= o->ev.size(); b += kOrbStages + 1) {
+        for (int k = 0; k < kOrbStages; ++k) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, o->ev[b + k], o->ev[b + k + 1]);
             o->stage_ms[k] += ms;
@@ -1253,6 +1264,12 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
         cand_off += L.cand_cap;
     }
     g.pyr_bytes = (pyr_off + 255) & ~255LL;
+    g.blur_pitch0 = (o->W + 15) & ~15;
+    g.blur0_bytes = ((long long)g.blur_pitch0 * o->H + 255) & ~255LL;
+    g.blur_bytes = g.blur0_bytes + g.pyr_bytes;
+    g.blur_tile_off[0] = 0;
+    for (int l = 0; l < nl; ++l)
+        g.blur_tile_off[l + 1] = g.blur_tile_off[l] + ((g.lv[l].h + kBlurTH - 1) / kBlurTH) * ((g.lv[l].w + kBlurTW - 1) / kBlurTW);
     g.cand_per_img = cand_off;
     g.out_per_img = out_off;
     g.n_max = out_off;
@@ -1318,6 +1335,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     if (!xt.empty()) HIP_OK(hipMemcpy(o->d_xt, xt.data(), sizeof(XTab) * xt.size(), hipMemcpyHostToDevice));
     if (!yt.empty()) HIP_OK(hipMemcpy(o->d_yt, yt.data(), sizeof(XTab) * yt.size(), hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&o->d_pyr, std::max<size_t>(256, (size_t)g.pyr_bytes * n)));
+    HIP_OK(hipMalloc(&o->d_blur, (size_t)g.blur_bytes * n));
     HIP_OK(hipMalloc(&o->d_cell_cnt, sizeof(int) * g.n_cells * n));
     HIP_OK(hipMalloc(&o->d_cell_kp, sizeof(uint32_t) * (size_t)g.n_cells * g.cell_cap * n));
     HIP_OK(hipMalloc(&o->d_cand, sizeof(uint32_t) * (size_t)g.cand_per_img * n));
@@ -1350,7 +1368,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
     for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
-    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_pyr, o->d_blur, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
     for (void *p : ptrs)
@@ -1397,8 +1415,13 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
     octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
     mark(o, st);
-    // K4: orientation + descriptors, one wave per output slot
-    DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
+    // K4: blurred pyramid, one workgroup per 32 x 128 tile
+    const int blur_blocks = g.blur_tile_off[g.nlevels] * n;
+    blur_kernel<<<xcd_grid(blur_blocks), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
+                                                       blur_blocks);
+    mark(o, st);
+    // K5: orientation + descriptors, one wave per output slot
+    DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_blur, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
     const int waves = g.out_per_img * n;
     describe_kernel<<<xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
@@ -1412,14 +1435,14 @@ omv_status omv_orb_enable_timing(omv_orb *o, int on) {
     return OMV_OK;
 }
 
-omv_status omv_orb_stage_ms(omv_orb *o, double *ms4, long long *calls, int reset) {
-    if (!o || !ms4) return OMV_ERR_ARG;
+omv_status omv_orb_stage_ms(omv_orb *o, double *ms5, long long *calls, int reset) {
+    if (!o || !ms5) return OMV_ERR_ARG;
     HIP_OK(hipStreamSynchronize(o->last_stream));
     flush_timing(o);
-    for (int k = 0; k < 4; ++k) ms4[k] = o->stage_ms[k];
+    for (int k = 0; k < kOrbStages; ++k) ms5[k] = o->stage_ms[k];
     if (calls) *calls = o->stage_calls;
     if (reset) {
-        for (int k = 0; k < 4; ++k) o->stage_ms[k] = 0;
+        for (int k = 0; k < kOrbStages; ++k) o->stage_ms[k] = 0;
         o->stage_calls = 0;
     }
     return OMV_OK;

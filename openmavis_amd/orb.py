@@ -130,13 +130,13 @@ class ORBextractor:
         return out
 
     # -- measurement ------------------------------------------------------------------------------
-    STAGES = ("pyr_resize", "fast_cells", "octree", "describe")
+    STAGES = ("pyr_resize", "fast_cells", "octree", "blur", "describe")
 
     def enable_timing(self, on=True):
         _lib.check(self._lib.omv_orb_enable_timing(self._h, int(bool(on))))
 
     def stage_ms(self, reset=True):
-        ms = np.zeros(4, np.float64)
+        ms = np.zeros(len(self.STAGES), np.float64)
         calls = ctypes.c_longlong()
         _lib.check(self._lib.omv_orb_stage_ms(self._h, _lib.ptr(ms), ctypes.byref(calls), int(bool(reset))))
         return dict(zip(self.STAGES, ms.tolist())), calls.value
