@@ -15,7 +15,7 @@
 //                   lapping/non-lapping for the output split (:1045-1067).
 //   K4 blur         every level blurred once into a blurred pyramid (GaussianBlur 7x7 sigma 2,
 //                   :1035-1036, OpenCV's bit-exact 8U path, BORDER_REFLECT_101 on the level), one
-//                   workgroup per 32x128 tile staged in LDS.
+//                   wavefront per 32x256 tile, horizontal sums in a sliding 7-row register window.
 //   K5 describe     one wavefront per keypoint: intensity-centroid angle over the un-blurred level
 //                   (IC_Angle :19-43, fastAtan2) and steered rBRIEF by byte gathers from the blurred
 //                   level, 4 ballots (computeOrbDescriptor :46-90); writes the keypoint and
@@ -828,13 +828,14 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
 
 // K4 --------------------------------------------------------------------------------------------
 // GaussianBlur 7x7, sigma 2 (ORBextractor.cc:1035-1036; OpenCV's bit-exact 8U path): every pyramid level
-// blurred once, as the reference does, into a blurred pyramid with the same layout.  One workgroup per
-// 32-row x 128-column tile of a level: the 38 x 136 source bytes (BORDER_REFLECT_101 on the level's own
-// bounds) are staged in LDS as dwords, the horizontal 7-tap sums of 4 adjacent columns are two v_dot4_u32_u8
-// on byte-aligned dwords (u16 exact), the vertical taps a multiply-add chain (u24 operands), and each quad of blurred
-// pixels is stored as one dword: (sum_i k_i sum_j k_j p + 2^15) >> 16 with k = [18, 34, 48, 56, 48, 34, 18].
-constexpr int kBlurTH = 32, kBlurTW = 128;              // output tile
-constexpr int kBlurSR = kBlurTH + 6, kBlurSD = kBlurTW / 4 + 2;   // staged rows, staged dwords per row (136 B)
+// blurred once, as the reference does, into a blurred pyramid with the same layout.  One wavefront per
+// 32-row x 256-column tile of a level, no LDS: lane = column quad x .. x+3, walking down the tile's 38 input
+// rows (BORDER_REFLECT_101 on the level's own bounds).  Per input row a lane loads its own dword and takes
+// its neighbours' (bytes x-4 .. x-1, x+4 .. x+7) by DPP wave shifts, the horizontal 7-tap sums of its four
+// columns are two v_dot4_u32_u8 each on byte-aligned dwords (u16 exact), kept in a 7-row register window;
+// each output row is the vertical 7-tap sum (sum_i k_i sum_j k_j p + 2^15) >> 16, k = [18, 34, 48, 56, 48,
+// 34, 18], packed by v_perm into one dword store.  The sums never exceed 255 * 2^16 + 2^15, so no clamp.
+constexpr int kBlurTH = 32, kBlurTW = 256;   // output rows / columns per wavefront tile
 
 struct BlurArgs {
     const uint8_t *images;
@@ -852,88 +853,159 @@ __device__ __forceinline__ uint8_t *blur_level(const Geom &g, uint8_t *blur, int
     return blur + (size_t)img * g.blur_bytes + g.blur0_bytes + g.lv[l].off;
 }
 
-__global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_blocks) {
-    __shared__ __attribute__((aligned(16))) uint32_t raw[kBlurSR * kBlurSD];
-    __shared__ __attribute__((aligned(16))) uint16_t hs[kBlurSR * kBlurTW];
-    const int blk = xcd_block(n_blocks);
+// bytes c .. c+3 of a level row, reflect-101 outside [0, w) (bytes more than one width outside read 0: no
+// output column uses them); `fast`: the row is dword aligned, c a multiple of 4
+__device__ __forceinline__ uint32_t row_dword(const uint8_t *row, int c, int w, bool fast) {
+    if (fast && c >= 0 && c + 3 < w) return *reinterpret_cast<const uint32_t *>(row + c);
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int xx = c + b;
+        const uint32_t px = (xx > -w && xx < 2 * w - 1) ? row[omv::reflect101(xx, w)] : 0u;
+        v |= px << (8 * b);
+    }
+    return v;
+}
+
+// Where a lane's dword (bytes p .. p+3 of a level row) comes from: the aligned dwords at a0 and a1 and the
+// v_perm selector picking its four bytes out of them -- row-independent, so computed once per tile.  Bytes
+// outside [0, w) reflect-101 (BORDER_REFLECT_101); positions that feed no output column read byte 0.
+struct DwordSrc {
+    int a0, a1;
+    uint32_t sel;
+};
+__device__ __forceinline__ DwordSrc dword_src(int p, int w) {
+    if (p >= 0 && p + 3 < w) return DwordSrc{p, p, 0x03020100u};
+    int idx[4], mn = 1 << 30, mx = -1;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int q = p + b;
+        idx[b] = (q > -w && q < 2 * w - 1 && p < w + 4) ? omv::reflect101(q, w) : 0;
+        mn = min(mn, idx[b]), mx = max(mx, idx[b]);
+    }
+    DwordSrc d;
+    d.a0 = mn & ~3;
+    d.a1 = (mx & ~3) == d.a0 ? d.a0 : d.a0 + 4;
+    d.sel = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) d.sel |= (uint32_t)(idx[b] - d.a0) << (8 * b);   // 0..7: bytes of {D1:D0}
+    return d;
+}
+
+// One wavefront tile, rows software-pipelined kBlurPF deep (the loads of row r + kBlurPF issue before row r
+// is summed).  EDGE: the tile's input columns x0-4 .. x0+259 leave the level, every dword is assembled by
+// v_perm from two aligned loads; otherwise two plain loads per row (own dword + the lane-0/63 outside one).
+constexpr int kBlurPF = 8;
+template <bool EDGE>
+__device__ __forceinline__ void blur_tile(const uint8_t *__restrict__ src, int sp, uint8_t *__restrict__ dst, int bp,
+                                          int w, int h, int y0, int x0, int lane) {
+    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+    constexpr int NR = kBlurTH + 6;
+    const int x = x0 + 4 * lane, rows = min(kBlurTH, h - y0);
+    const int pe = lane == 63 ? x0 + kBlurTW : x0 - 4;   // lane 0's left / lane 63's right outside dword
+    DwordSrc cs{x, x, 0x03020100u}, es{pe, pe, 0x03020100u};
+    if (EDGE) cs = dword_src(x, w), es = dword_src(pe, w);
+    uint32_t bc0[kBlurPF], bc1[kBlurPF], be0[kBlurPF], be1[kBlurPF];
+    auto fetch = [&](int r, int k) {
+        const int yy = omv::reflect101(min(y0 - 3 + r, 2 * h - 2), h);
+        const uint8_t *row = src + (size_t)yy * sp;
+        bc0[k] = *reinterpret_cast<const uint32_t *>(row + cs.a0);
+        be0[k] = *reinterpret_cast<const uint32_t *>(row + es.a0);
+        if (EDGE) {
+            bc1[k] = *reinterpret_cast<const uint32_t *>(row + cs.a1);
+            be1[k] = *reinterpret_cast<const uint32_t *>(row + es.a1);
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < kBlurPF; ++r) fetch(r, r);
+    uint32_t win[7][4];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int k = r % kBlurPF;
+        uint32_t C = bc0[k], E = be0[k];
+        if (EDGE) C = __builtin_amdgcn_perm(bc1[k], C, cs.sel), E = __builtin_amdgcn_perm(be1[k], E, es.sel);
+        if (r + kBlurPF < NR) fetch(r + kBlurPF, k);
+        // lane 0's left and lane 63's right neighbour dwords lie outside the tile: DPP keeps `old` (= E) there
+        const uint32_t Lw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const uint32_t Rw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x130, 0xf, 0xf, false);   // wave_shl:1
+        uint32_t *hs = win[r % 7];
+        hs[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 1), G1,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 1), G0, 0u, false), false);
+        hs[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 2), G1,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 2), G0, 0u, false), false);
+        hs[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 3), G1,
+                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 3), G0, 0u, false), false);
+        hs[3] = __builtin_amdgcn_udot4(Rw, G1, __builtin_amdgcn_udot4(C, G0, 0u, false), false);
+        if (r >= 6) {
+            uint32_t s4[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)   // u24 operands: v_mul_u32_u24 (full rate) instead of v_mul_lo_u32
+                s4[c] = __umul24(18u, win[(r - 6) % 7][c] + win[r % 7][c]) + __umul24(34u, win[(r - 5) % 7][c] + win[(r - 1) % 7][c]) +
+                        __umul24(48u, win[(r - 4) % 7][c] + win[(r - 2) % 7][c]) + __umul24(56u, win[(r - 3) % 7][c]) + 32768u;
+            // byte 2 of each sum is the blurred pixel
+            const uint32_t lo = __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u);   // [s0.b2, s1.b2, 0, 0]
+            const uint32_t hi = __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);   // [0, 0, s2.b2, s3.b2]
+            if (r - 6 < rows && x < w) *reinterpret_cast<uint32_t *>(dst + (size_t)(y0 + r - 6) * bp + x) = lo | hi;
+        }
+    }
+}
+
+// rows that are not dword aligned (a caller's level-0 pitch): byte loads, one row at a time
+__device__ void blur_tile_bytes(const uint8_t *src, int sp, uint8_t *dst, int bp, int w, int h, int y0, int x0, int lane) {
+    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+    const int x = x0 + 4 * lane, rows = min(kBlurTH, h - y0);
+    const int pe = lane == 63 ? x0 + kBlurTW : x0 - 4;
+    uint32_t win[7][4];
+#pragma unroll
+    for (int r = 0; r < kBlurTH + 6; ++r) {
+        const uint8_t *row = src + (size_t)omv::reflect101(min(y0 - 3 + r, 2 * h - 2), h) * sp;
+        const uint32_t C = row_dword(row, x, w, false), E = row_dword(row, pe, w, false);
+        const uint32_t Lw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x138, 0xf, 0xf, false);
+        const uint32_t Rw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x130, 0xf, 0xf, false);
+        uint32_t *hs = win[r % 7];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            hs[c] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, c + 1), G1,
+                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, c + 1), G0, 0u, false), false);
+        hs[3] = __builtin_amdgcn_udot4(Rw, G1, __builtin_amdgcn_udot4(C, G0, 0u, false), false);
+        if (r >= 6 && r - 6 < rows && x < w) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint32_t acc = 32768u;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * win[(r - 6 + k) % 7][c];
+                v |= (acc >> 16) << (8 * c);
+            }
+            *reinterpret_cast<uint32_t *>(dst + (size_t)(y0 + r - 6) * bp + x) = v;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_tiles) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int blk = xcd_block((n_tiles + 3) >> 2);
     if (blk < 0) return;
+    const int tile = __builtin_amdgcn_readfirstlane(blk * 4 + wave);   // wave-uniform: scalar address math
+    if (tile >= n_tiles) return;
     const int tpi = g.blur_tile_off[g.nlevels];
-    const int img = blk / tpi;
-    const int t = blk - img * tpi;
+    const int img = tile / tpi;
+    const int t = tile - img * tpi;
     int l = 0;
     while (l + 1 < g.nlevels && t >= g.blur_tile_off[l + 1]) ++l;
     const LevelGeom &L = g.lv[l];
     const int tcols = (L.w + kBlurTW - 1) / kBlurTW;
     const int tr = (t - g.blur_tile_off[l]) / tcols, tc = (t - g.blur_tile_off[l]) - tr * tcols;
     const int y0 = tr * kBlurTH, x0 = tc * kBlurTW;
-    int sp;
+    int sp, bp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
-    const int tid = threadIdx.x;
-    // stage rows y0-3 .. y0+34, bytes x0-4 .. x0+131 (reflect-101 outside the level)
-    const bool interior_x = x0 >= 4 && x0 + kBlurTW + 4 <= L.w;
-    for (int i = tid; i < kBlurSR * kBlurSD; i += 256) {
-        const int r = i / kBlurSD, d = i - r * kBlurSD;
-        const int yy = omv::reflect101(min(y0 - 3 + r, 2 * L.h - 2), L.h);
-        const uint8_t *row = src + (size_t)yy * sp;
-        const int c0 = x0 - 4 + 4 * d;
-        uint32_t v;
-        if (interior_x && ((((uintptr_t)row) & 3) == 0)) {
-            v = *reinterpret_cast<const uint32_t *>(row + c0);
-        } else {
-            v = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int xx = c0 + b;
-                const uint32_t px = (xx >= -L.w + 1 && xx < 2 * L.w - 1) ? row[omv::reflect101(xx, L.w)] : 0u;
-                v |= px << (8 * b);
-            }
-        }
-        raw[i] = v;
-    }
-    __syncthreads();
-    // horizontal: staged byte 4 q + 1 + s .. 4 q + 7 + s -> output column x0 + 4 q + s
-    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-    for (int i = tid; i < kBlurSR * (kBlurTW / 4); i += 256) {
-        const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
-        const uint32_t *D = raw + r * kBlurSD + q;
-        const uint32_t d0 = D[0], d1 = D[1], d2 = D[2];
-        uint32_t h[4];
-        h[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), G1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), G0, 0u, false), false);
-        h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), G1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), G0, 0u, false), false);
-        h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), G1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), G0, 0u, false), false);
-        h[3] = __builtin_amdgcn_udot4(d2, G1, __builtin_amdgcn_udot4(d1, G0, 0u, false), false);
-        *reinterpret_cast<uint2 *>(hs + r * kBlurTW + 4 * q) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-    }
-    __syncthreads();
-    // vertical at the tile's output quads
-    int bp;
     uint8_t *dst = blur_level(g, a.blur, img, l, &bp);
-    const int rows = min(kBlurTH, L.h - y0), cols = min(kBlurTW, L.w - x0);
-    for (int i = tid; i < kBlurTH * (kBlurTW / 4); i += 256) {
-        const int r = i / (kBlurTW / 4), q = i - r * (kBlurTW / 4);
-        if (r >= rows || 4 * q >= cols) continue;
-        uint32_t s0 = 32768u, s1 = 32768u, s2 = 32768u, s3 = 32768u;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const uint2 hv = *reinterpret_cast<const uint2 *>(hs + (r + k) * kBlurTW + 4 * q);
-            const uint32_t kk = (uint32_t)c_gauss7[k];
-            s0 += (hv.x & 0xffffu) * kk;
-            s1 += (hv.x >> 16) * kk;
-            s2 += (hv.y & 0xffffu) * kk;
-            s3 += (hv.y >> 16) * kk;
-        }
-        const uint32_t packed = min(s0 >> 16, 255u) | (min(s1 >> 16, 255u) << 8) | (min(s2 >> 16, 255u) << 16) |
-                                (min(s3 >> 16, 255u) << 24);
-        uint8_t *o = dst + (size_t)(y0 + r) * bp + x0 + 4 * q;
-        if (4 * q + 3 < cols) {
-            *reinterpret_cast<uint32_t *>(o) = packed;
-        } else {
-            for (int b = 0; 4 * q + b < cols; ++b) o[b] = (uint8_t)(packed >> (8 * b));
-        }
-    }
+    if (((((uintptr_t)src) | (uintptr_t)sp) & 3) != 0)
+        blur_tile_bytes(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
+    else if (x0 >= 4 && x0 + kBlurTW + 4 <= L.w)
+        blur_tile<false>(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
+    else
+        blur_tile<true>(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
 }
 
 // K5 --------------------------------------------------------------------------------------------
@@ -1415,10 +1487,10 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
     octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
     mark(o, st);
-    // K4: blurred pyramid, one workgroup per 32 x 128 tile
-    const int blur_blocks = g.blur_tile_off[g.nlevels] * n;
-    blur_kernel<<<xcd_grid(blur_blocks), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
-                                                       blur_blocks);
+    // K4: blurred pyramid, one wavefront per 32 x 256 tile
+    const int blur_tiles = g.blur_tile_off[g.nlevels] * n;
+    blur_kernel<<<xcd_grid((blur_tiles + 3) / 4), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
+                                                               blur_tiles);
     mark(o, st);
     // K5: orientation + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_blur, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
