@@ -29,19 +29,20 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force=False, verbose=True):
-    """One hipcc -c per translation unit (in parallel, only the stale ones), then one shared link."""
+def build_hip(force=False, verbose=True, defines=(), lib=LIB, obj_dir=OBJ_DIR):
+    """One hipcc -c per translation unit (in parallel, only the stale ones), then one shared link.
+    `defines` / `lib` / `obj_dir` build an instrumented variant (e.g. -DOMV_RESOLVE_PROFILE) beside the product."""
     from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES if os.path.exists(os.path.join(CSRC, s))]
     hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     hdrs.append(os.path.join(ROOT, "include", "omv.h"))
-    os.makedirs(OBJ_DIR, exist_ok=True)
-    objs = [os.path.join(OBJ_DIR, os.path.basename(s) + ".o") for s in srcs]
+    os.makedirs(obj_dir, exist_ok=True)
+    objs = [os.path.join(obj_dir, os.path.basename(s) + ".o") for s in srcs]
     stale = [(s, o) for s, o in zip(srcs, objs) if force or _newer(o, [s] + hdrs)]
 
     def compile_one(so):
         s, o = so
-        cmd = [HIPCC] + HIP_FLAGS + ["-I", os.path.join(ROOT, "include"), "-c", s, "-o", o + ".tmp"]
+        cmd = [HIPCC] + HIP_FLAGS + [f"-D{d}" for d in defines] + ["-I", os.path.join(ROOT, "include"), "-c", s, "-o", o + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
@@ -50,14 +51,22 @@ def build_hip(force=False, verbose=True):
     if stale:
         with ThreadPoolExecutor(max_workers=min(8, len(stale))) as ex:
             list(ex.map(compile_one, stale))
-    if not stale and not _newer(LIB, objs):
-        return LIB
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp"] + objs
+    if not stale and not _newer(lib, objs):
+        return lib
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
+def build_variant(name, defines, verbose=True):
+    """Instrumented library openmavis_amd/variants/libomv_<name>.so (timing printfs etc.; never the product)."""
+    vdir = os.path.join(PKG, "variants")
+    os.makedirs(vdir, exist_ok=True)
+    return build_hip(False, verbose, defines, os.path.join(vdir, f"libomv_{name}.so"),
+                     os.path.join(ROOT, "build", "obj_" + name))
 
 
 def build_oracle(verbose=True):
@@ -72,4 +81,7 @@ def build_all(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":   # python -m openmavis_amd.build variant NAME DEF...
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        build_all(force="--force" in sys.argv)

@@ -396,108 +396,180 @@ __device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float 
     return fabsf(k.x - x) < r && fabsf(k.y - y) < r;
 }
 
-__device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
-                         const uint32_t *occ0, const int *revived, int nrevived, const int32_t *l2r,
-                         const int32_t *r2l, Eval &e) {
+// Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window
+// and skips keypoints held by a point with observations (ORBmatcher.cc:77-79); the record holds the kTop
+// best candidates in (distance, window order), so the walk is: fetch the 16 entries and their blocked bits
+// together (two LDS round trips, no per-entry dependency chain), then take the first two unblocked entries
+// with mask arithmetic.  The only own earlier write of the point that can fall into a later camera's
+// block is camera 0's stereo-partner claim in block 1 (pa0, ORBmatcher.cc:125-131): it reads as blocked
+// iff the point itself has observations.
+struct Pick {
+    int b1, b2, d1, d2, o1, o2;
+    bool rescan;   // the 16 entries ran out with more candidates in the window
+};
+
+__device__ __forceinline__ Pick pick_record(const Rec &r, int rcount, int c, int cap, const uint32_t *bits, int pa0,
+                                            bool obs) {
+    const uint4 *r4 = reinterpret_cast<const uint4 *>(&r);
+    uint32_t e[kTop];
+#pragma unroll
+    for (int v = 0; v < kTop / 4; ++v) {
+        const uint4 q = r4[v];
+        e[4 * v] = q.x, e[4 * v + 1] = q.y, e[4 * v + 2] = q.z, e[4 * v + 3] = q.w;
+    }
+    const int avail = min(rcount, kTop);
+    uint32_t blocked = 0;
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) {
+        const int slot = c * cap + rec_idx(e[k]);
+        uint32_t b = (bits[slot >> 5] >> (slot & 31)) & 1u;
+        if (slot == pa0) b = obs ? 1u : 0u;
+        blocked |= b << k;
+    }
+    const uint32_t u = ~blocked & ((1u << avail) - 1u);   // avail <= 16
+    const uint32_t u2 = u & (u - 1u);
+    const int k1 = u ? __ffs(u) - 1 : -1, k2 = u2 ? __ffs(u2) - 1 : -1;
+    uint32_t v1 = 0, v2 = 0;
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) {
+        v1 = k == k1 ? e[k] : v1;
+        v2 = k == k2 ? e[k] : v2;
+    }
+    Pick p;
+    p.b1 = k1 >= 0 ? rec_idx(v1) : -1, p.d1 = k1 >= 0 ? rec_dist(v1) : 256, p.o1 = k1 >= 0 ? rec_oct(v1) : -1;
+    p.b2 = k2 >= 0 ? rec_idx(v2) : -1, p.d2 = k2 >= 0 ? rec_dist(v2) : 256, p.o2 = k2 >= 0 ? rec_oct(v2) : -1;
+    p.rescan = k2 < 0 && rcount > kTop;
+    return p;
+}
+
+// Full GetFeaturesInArea rescan of one window against the current claims (freed initially-occupied
+// keypoints, or more than kTop - 2 candidates claimed): rare.
+__device__ __forceinline__ Pick rescan_window(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
+                                           const uint32_t *bits, int pa0, bool obs) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
+    const size_t bc = fm * f.n_cams + c;
+    uint64_t dmp[4];
+    load_desc(m.desc + fm * 32, dmp);
+    Top t;
+    scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f), lvl - 1,
+                lvl, dmp, [&](int slot) { return slot == pa0 ? obs : bit_of(bits, slot); }, t);
+    Pick p;
+    p.b1 = p.b2 = -1, p.d1 = p.d2 = 256, p.o1 = p.o2 = -1, p.rescan = false;
+    if (t.n > 0) p.b1 = t.idx(0), p.d1 = t.dist(0), p.o1 = t.oct(0);
+    if (t.n > 1) p.b2 = t.idx(1), p.d2 = t.dist(1), p.o2 = t.oct(1);
+    return p;
+}
+
+// Does a freed initially-occupied keypoint fall into this (point, camera) window?  (rare)
+__device__ __forceinline__ bool revived_in_window(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
+                                               const int *revived, int nrevived, int self_rev) {
+    const FrameArgs &f = a.f;
+    const MpArgs &m = a.m;
+    if (nrevived > kMaxRevived) return true;   // list overflowed: rescan every window (exact, slow)
+    const int cap = f.kp_cap;
+    const size_t bc = fm * f.n_cams + c;
+    const float rad = window_radius(f, m, bc, c, a.th, a.th != 1.0f);
+    for (int q = 0; q < nrevived; ++q) {
+        const int s = revived[q];
+        if (s / cap == c && in_window(f, frame, c, s, m.proj_x[bc], m.proj_y[bc], rad, lvl)) return true;
+    }
+    return c == 1 && self_rev >= 0 && in_window(f, frame, c, self_rev, m.proj_x[bc], m.proj_y[bc], rad, lvl);
+}
+
+// One map point against the committed claims (ORBmatcher.cc:33-177 for one pMP).  Cameras are visited in
+// ascending order over the in-view bits only (the wave iterates the largest in-view count of its lanes,
+// not n_cams).  Claims and the slots that decided the result go to the lane's LDS rows.
+#ifdef OMV_RESOLVE_PROFILE
+struct EvalProf {
+    long long t[6], last;
+};
+#define OMV_EP(k) (ep.t[k] += wall_clock64() - ep.last, ep.last = wall_clock64())
+#else
+struct EvalProf {};
+#define OMV_EP(k) ((void)0)
+#endif
+__device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
+                         const uint32_t *occ0, const int *revived, int nrevived, const int32_t *l2r,
+                         const int32_t *r2l, Eval &e, EvalProf &ep) {
+    const FrameArgs &f = a.f;
     const int C = f.n_cams, cap = f.kp_cap;
     e.nclaim = e.nrel = e.nmatch = 0;
     e.fallback = e.unblock = false;
     const int fl = bs.flags[l];
+    OMV_EP(0);
     if (fl & kFlagSkip) return;
-    const size_t fm = (size_t)frame * m.M + i;
+    const size_t fm = (size_t)frame * a.m.M + i;
     const bool obs = (fl & kFlagObs) != 0;
-    auto is_blocked = [&](int slot) {
-        if (bit_of(bits, slot)) {
-            // an own earlier claim of a point without observations unblocks it
-            for (int q = 0; q < e.nclaim; ++q)
-                if (e.claim[q] == slot) return obs;
-            return true;
-        }
-        if (obs)
-            for (int q = 0; q < e.nclaim; ++q)
-                if (e.claim[q] == slot) return true;
-        return false;
-    };
     auto add_claim = [&](int slot) {
-        if (!obs && bit_of(bits, slot)) e.unblock = true;
+        if (!obs && bit_of(bits, slot)) e.unblock = true;   // overwrites a keypoint later points saw blocked
         e.claim[e.nclaim++] = slot;
     };
     // the left block's stereo partner claim (ORBmatcher.cc:125-131) by a point without observations frees
     // an initially-occupied right keypoint for this point's own right-block search (:150-160); the
     // right-block record was built without it (occupied at the call), so that window is rescanned
-    int self_rev = -1;
-    for (int c = 0; c < C; ++c) {
-        if (!((fl >> c) & 1)) continue;
+    int self_rev = -1, pa0 = -1;
+    for (uint32_t vm = (uint32_t)fl & ((1u << C) - 1u); vm; vm &= vm - 1u) {
+        const int c = __ffs(vm) - 1;
         const int lvl = bs.level[l * C + c];
-        if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
-        const Rec &r = bs.rec[l * C + c];
         const int rcount = bs.count[l * C + c];
-        const size_t bc = fm * C + c;
-        // a freed initially-occupied keypoint inside this window is missing from the record
-        bool need_rescan = nrevived > kMaxRevived;   // list overflowed: rescan every window (exact, slow)
-        if (nrevived > 0 && !need_rescan) {
-            const float rad = window_radius(f, m, bc, c, a.th, a.th != 1.0f);
-            for (int q = 0; q < nrevived && !need_rescan; ++q) {
-                const int s = revived[q];
-                if (s / cap == c) need_rescan = in_window(f, frame, c, s, m.proj_x[bc], m.proj_y[bc], rad, lvl);
-            }
-        }
-        if (c == 1 && self_rev >= 0 && !need_rescan)
-            need_rescan = in_window(f, frame, c, self_rev, m.proj_x[bc], m.proj_y[bc],
-                                    window_radius(f, m, bc, c, a.th, a.th != 1.0f), lvl);
+        OMV_EP(1);
+        if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
+        bool need_rescan = (nrevived > 0 || (c == 1 && self_rev >= 0)) &&
+                           revived_in_window(a, frame, fm, c, lvl, revived, nrevived, self_rev);
         if (rcount == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
-        int b1 = -1, b2 = -1, d1 = 256, d2 = 256, o1 = -1, o2 = -1;
+        Pick p;
+        OMV_EP(2);
         if (!need_rescan) {
-            const int avail = min(rcount, kTop);
-            for (int k = 0; k < avail && b2 < 0; ++k) {
-                const uint32_t v = r.e[k];
-                const int slot = c * cap + rec_idx(v);
-                if (is_blocked(slot)) continue;
-                if (b1 < 0) b1 = rec_idx(v), d1 = rec_dist(v), o1 = rec_oct(v);
-                else b2 = rec_idx(v), d2 = rec_dist(v), o2 = rec_oct(v);
-            }
-            if (b2 < 0 && rcount > kTop) need_rescan = true;
+            p = pick_record(bs.rec[l * C + c], rcount, c, cap, bits, c == 1 ? pa0 : -1, obs);
+            need_rescan = p.rescan;
         }
+        OMV_EP(3);
         if (need_rescan) {
             e.fallback = true;
-            uint64_t dmp[4];
-            load_desc(m.desc + fm * 32, dmp);
-            Top t;
-            scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f),
-                        lvl - 1, lvl, dmp, is_blocked, t);
-            b1 = b2 = -1, d1 = d2 = 256, o1 = o2 = -1;
-            if (t.n > 0) b1 = t.idx(0), d1 = t.dist(0), o1 = t.oct(0);
-            if (t.n > 1) b2 = t.idx(1), d2 = t.dist(1), o2 = t.oct(1);
+            p = rescan_window(a, frame, fm, c, lvl, bits, c == 1 ? pa0 : -1, obs);
         }
-        if (b1 >= 0) e.rel[e.nrel++] = c * cap + b1;
-        if (b2 >= 0) e.rel[e.nrel++] = c * cap + b2;
-        if (d1 <= kTH_HIGH) {
-            if (o1 == o2 && (float)d1 > a.nnratio * d2) return;   // `continue` to the next map point
+        OMV_EP(4);
+        if (p.b1 >= 0) e.rel[e.nrel++] = c * cap + p.b1;
+        if (p.b2 >= 0) e.rel[e.nrel++] = c * cap + p.b2;
+        if (p.d1 <= kTH_HIGH) {
+            if (p.o1 == p.o2 && (float)p.d1 > a.nnratio * p.d2) return;   // `continue` to the next map point
             if (c == 0) {
-                add_claim(b1);
-                if (C > 1 && l2r[b1] != -1) {
-                    const int ps = cap + l2r[b1];
+                add_claim(p.b1);
+                if (C > 1 && l2r[p.b1] != -1) {
+                    const int ps = cap + l2r[p.b1];
                     if (!obs && bit_of(occ0, ps) && bit_of(bits, ps)) self_rev = ps;
                     add_claim(ps), e.nmatch++;
+                    pa0 = ps;
                 }
                 e.nmatch++;
             } else if (c == 1) {
-                if (r2l[b1] != -1) add_claim(r2l[b1]), e.nmatch++;
-                add_claim(cap + b1);
+                if (r2l[p.b1] != -1) add_claim(r2l[p.b1]), e.nmatch++;
+                add_claim(cap + p.b1);
                 e.nmatch++;
             } else {
-                add_claim(c * cap + b1);
+                add_claim(c * cap + p.b1);
                 e.nmatch++;
             }
         }
+        OMV_EP(5);
     }
 }
 
+// One stage buffer (the current 64-point block) sized for kMaxCams; the claim state is in dynamic LDS.
+constexpr int kStageBytes = 64 * kMaxCams * (int)sizeof(Rec) + 2 * 64 * kMaxCams * 4 + 64 * 4;
+constexpr size_t kResolveStaticLds = (size_t)kStageBytes + 2 * 64 * kMaxClaims * 4 + 4 * (kMaxRevived + 1);
+
 // One wavefront (one 64-thread workgroup) per frame.
-__global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
+// The next 64-point block is prefetched into registers with ordinary global loads while the current block
+// resolves, and written to the LDS stage at the block boundary: the loads' only consumers are those writes,
+// so nothing in the rounds waits on them (an LDS-DMA prefetch would make the compiler drain it before LDS
+// accesses it cannot prove disjoint).  kLdsK2m: the frame's assignment (mvpMapPoints) also lives in LDS and
+// is written back once (no global store in the rounds); otherwise it is updated in global memory.
+template <bool kLdsK2m>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) resolve_kernel(ResolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
     __shared__ int revived[kMaxRevived];
     __shared__ int nrevived;
     __shared__ int lane_claim[64 * kMaxClaims], lane_rel[64 * kMaxClaims];
@@ -506,68 +578,92 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
     const int nwords = (S + 31) >> 5;
     uint32_t *bits = rsm;                                         // blocked: mvpMapPoints[s] has observations
     uint32_t *occ0 = rsm + nwords;                                // initially occupied (not in the records)
-    // owner: per slot, in the conflict phase of a round the first lane (with observations) claiming it
-    // (atomicMin of lane), in the commit phase 63 - the last committing writer (atomicMin of 63 - lane);
-    // 64 = none between the phases
+    // owner: per slot, a phase-stamped word (phase << 7 | x, phases count down, so the current phase's
+    // atomicMin always beats stale words and nothing is ever reset).  Conflict phase: x = the first lane
+    // (with observations) claiming the slot; commit phase: x = 63 - the last committing writer.
     int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);
     int32_t *l2r_s = owner + S;                                   // this frame's mvLeftToRightMatch
     int32_t *r2l_s = l2r_s + cap;                                 // and mvRightToLeftMatch
-    uint8_t *stage0 = reinterpret_cast<uint8_t *>(rsm) + ((8 * (size_t)nwords + 4 * (size_t)S + 8 * (size_t)cap + 15) & ~(size_t)15);
+    int32_t *const k2m_g = a.kp_to_mp + (size_t)frame * S;
+    int32_t *const k2m = kLdsK2m ? r2l_s + cap : k2m_g;          // this frame's mvpMapPoints
     const StageLayout SL(C);
     const int M = a.m.M;
-    // issue the async copy of block `base` into stage buffer `buf`
-    auto issue = [&](int buf, int base) {
-        if (!a.staged) return;   // large rigs: the records are read from global memory
-        uint8_t *b = stage0 + buf * SL.bytes;
-        const int nb = min(64, M - base);
-        const size_t o = ((size_t)frame * M + base) * C, op = (size_t)frame * M + base;
-        glds_copy16(a.recs + o, b + SL.rec, nb * C * (int)sizeof(Rec), lane);
-        glds_copy4(a.counts + o, b + SL.count, nb * C * 4, lane);
-        glds_copy4(a.m.level + o, b + SL.level, nb * C * 4, lane);
-        glds_copy4(a.flags + op, b + SL.flags, nb * 4, lane);
-    };
-    if (M > 0) issue(0, 0);
+    // register prefetch of one block: lane-linear 16-B chunks of the records, dwords of counts / levels, flags
+    // (macros, not lambdas: the arrays must stay in registers)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register vector (uint4 copies go by memcpy)
+    u32x4 pre_rec[kMaxCams * 4];
+    int pre_cnt[kMaxCams], pre_lvl[kMaxCams], pre_flag = 0;
+#define OMV_RESOLVE_PREFETCH(BASE)                                                                              \
+    {                                                                                                           \
+        const int nb_ = min(64, M - (BASE));                                                                    \
+        const size_t o_ = ((size_t)frame * M + (BASE)) * C;                                                     \
+        const u32x4 *rs_ = reinterpret_cast<const u32x4 *>(a.recs + o_);                                        \
+        const int lr_ = nb_ * C * 4 - 1, lc_ = nb_ * C - 1; /* clamped (branch-free) tail reads */           \
+        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams * 4; ++v)                               \
+            pre_rec[v] = rs_[min(lane + 64 * v, lr_)];                                                          \
+        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams; ++v) {                                 \
+            pre_cnt[v] = a.counts[o_ + min(lane + 64 * v, lc_)];                                                \
+            pre_lvl[v] = a.m.level[o_ + min(lane + 64 * v, lc_)];                                               \
+        }                                                                                                       \
+        pre_flag = a.flags[(size_t)frame * M + (BASE) + min(lane, nb_ - 1)];                                   \
+    }
+#define OMV_RESOLVE_TO_STAGE(BASE)                                                                              \
+    {                                                                                                           \
+        const int nb_ = min(64, M - (BASE));                                                                    \
+        u32x4 *rd_ = reinterpret_cast<u32x4 *>(stage + SL.rec);                                                 \
+        int *cd_ = reinterpret_cast<int *>(stage + SL.count), *ld_ = reinterpret_cast<int *>(stage + SL.level); \
+        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams * 4; ++v)                               \
+            if (lane + 64 * v < nb_ * C * 4) rd_[lane + 64 * v] = pre_rec[v];                                  \
+        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams; ++v) if (lane + 64 * v < nb_ * C) {    \
+            cd_[lane + 64 * v] = pre_cnt[v];                                                                    \
+            ld_[lane + 64 * v] = pre_lvl[v];                                                                    \
+        }                                                                                                       \
+        if (lane < nb_) reinterpret_cast<int *>(stage + SL.flags)[lane] = pre_flag;                            \
+    }
+    if (M > 0) OMV_RESOLVE_PREFETCH(0);
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
     for (int w = lane; w < nwords; w += 64) {
         uint32_t v = 0;
-        for (int b = 0; b < 32; ++b) {
-            const int s = w * 32 + b;
-            if (s < S && occ && occ[s]) v |= 1u << b;
+        if (occ) {
+            uint8_t o[32];   // all 32 byte loads in flight together
+#pragma unroll
+            for (int b = 0; b < 32; ++b) o[b] = occ[min(w * 32 + b, S - 1)];
+#pragma unroll
+            for (int b = 0; b < 32; ++b) v |= (w * 32 + b < S && o[b]) ? 1u << b : 0u;
         }
         bits[w] = v;
         occ0[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = 64;
+    for (int s = lane; s < S; s += 64) owner[s] = INT_MAX;
+    if (kLdsK2m)
+        for (int s = lane; s < S; s += 64) k2m[s] = k2m_g[s];
     for (int s = lane; s < cap; s += 64) {
         l2r_s[s] = a.l2r[(size_t)frame * cap + s];
         r2l_s[s] = a.r2l[(size_t)frame * cap + s];
     }
     if (lane == 0) nrevived = 0;
-    wave_sync();
-    int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
-    int total = 0;
+    int total = 0;              // this lane's committed matches (summed over the wave at the end)
+    int phase = 0x3fffff;       // owner stamp of the current conflict phase (commit phase = phase - 1)
+    EvalProf ep;
 #ifdef OMV_RESOLVE_PROFILE
     long long pf0 = wall_clock64(), pf_eval = 0, pf_wait = 0;
     int pf_rounds = 0, pf_fallback = 0;
+    for (int k = 0; k < 6; ++k) ep.t[k] = 0;
 #endif
-    for (int base = 0, buf = 0; base < M; base += 64, buf ^= 1) {
+    const BlockStage bs{reinterpret_cast<const Rec *>(stage + SL.rec), reinterpret_cast<const int *>(stage + SL.count),
+                        reinterpret_cast<const int *>(stage + SL.level), reinterpret_cast<const int *>(stage + SL.flags)};
+    for (int base = 0; base < M; base += 64) {
         const int nb = min(64, M - base);
-        // block `base` has landed in LDS; start copying the next block into the other buffer
 #ifdef OMV_RESOLVE_PROFILE
         const long long pw = wall_clock64();
 #endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_sync();          // the previous block's rounds are done with the stage
+        OMV_RESOLVE_TO_STAGE(base);   // (waits for this block's prefetch, issued a block earlier)
         wave_sync();
 #ifdef OMV_RESOLVE_PROFILE
         pf_wait += wall_clock64() - pw;
 #endif
-        if (base + 64 < M) issue(buf ^ 1, base + 64);
-        const uint8_t *sb = stage0 + buf * SL.bytes;
-        const size_t go = ((size_t)frame * M + base) * C, gp = (size_t)frame * M + base;
-        const BlockStage bs = a.staged
-            ? BlockStage{reinterpret_cast<const Rec *>(sb + SL.rec), reinterpret_cast<const int *>(sb + SL.count),
-                         reinterpret_cast<const int *>(sb + SL.level), reinterpret_cast<const int *>(sb + SL.flags)}
-            : BlockStage{a.recs + go, a.counts + go, a.m.level + go, a.flags + gp};
+        if (base + 64 < M) OMV_RESOLVE_PREFETCH(base + 64);
         const int i = base + lane;
         int start = 0;
         while (start < nb) {
@@ -578,27 +674,28 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             const int nrev = nrevived;
 #ifdef OMV_RESOLVE_PROFILE
             const long long pe = wall_clock64();
+            ep.last = pe;
             ++pf_rounds;
 #endif
-            if (active) evaluate(a, frame, i, lane, bs, bits, occ0, revived, nrev, l2r_s, r2l_s, e);
+            if (active) evaluate(a, frame, i, lane, bs, bits, occ0, revived, nrev, l2r_s, r2l_s, e, ep);
             else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
 #ifdef OMV_RESOLVE_PROFILE
             pf_eval += wall_clock64() - pe;
             pf_fallback += __popcll(__ballot(active && e.fallback));
 #endif
             const bool obs = active && (bs.flags[lane] & kFlagObs);
+            const int keyA = (phase << 7) | lane, keyB = ((phase - 1) << 7) | (63 - lane);
             if (obs)
-                for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], lane);
+                for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], keyA);
             wave_sync();
             bool conflict = false;
             if (active && lane > start) {
                 conflict = e.fallback;   // a full rescan saw the whole window: only safe at the batch head
-                for (int q = 0; q < e.nrel && !conflict; ++q) conflict = owner[e.rel[q]] < lane;
+                for (int q = 0; q < e.nrel && !conflict; ++q) {
+                    const int o = owner[e.rel[q]];
+                    conflict = (o >> 7) == phase && (o & 127) < lane;
+                }
             }
-            wave_sync();
-            if (obs)
-                for (int q = 0; q < e.nclaim; ++q) owner[e.claim[q]] = 64;
-            wave_sync();
             uint64_t cm = __ballot(conflict);
             const uint64_t um = __ballot(active && e.unblock);
             if (um) {
@@ -610,12 +707,12 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
             // commit lanes [start, j0): the highest committing lane writes a shared slot last
             const bool committed = lane >= start && lane < j0;
             if (committed)
-                for (int t = 0; t < e.nclaim; ++t) atomicMin(&owner[e.claim[t]], 63 - lane);
+                for (int t = 0; t < e.nclaim; ++t) atomicMin(&owner[e.claim[t]], keyB);
             wave_sync();
-            if (committed)
+            if (committed) {
                 for (int t = 0; t < e.nclaim; ++t) {
                     const int s = e.claim[t];
-                    if (owner[s] != 63 - lane) continue;
+                    if (owner[s] != keyB) continue;
                     k2m[s] = i;
                     if (obs) {
                         atomicOr(&bits[s >> 5], 1u << (s & 31));
@@ -627,22 +724,31 @@ __global__ void __launch_bounds__(64) resolve_kernel(ResolveArgs a) {
                         atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
                     }
                 }
-            wave_sync();
-            if (committed)
-                for (int t = 0; t < e.nclaim; ++t) owner[e.claim[t]] = 64;
-            int nm = committed ? e.nmatch : 0;
-            for (int d = 32; d >= 1; d >>= 1) nm += __shfl_xor(nm, d, 64);
-            total += nm;
+                total += e.nmatch;
+            }
+            phase -= 2;
             start = j0;
             wave_sync();
         }
     }
+    if (kLdsK2m) {
+        wave_sync();
+        for (int s = lane; s < S; s += 64) k2m_g[s] = k2m[s];
+    }
+    for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
     if (lane == 0) a.n_matches[frame] = total;
 #ifdef OMV_RESOLVE_PROFILE
+    for (int k = 0; k < 6; ++k)
+        for (int d = 32; d >= 1; d >>= 1) ep.t[k] = max(ep.t[k], (long long)__shfl_xor(ep.t[k], d, 64));
+    if (lane == 0 && frame < 3)
+        printf("resolve sections flags %lld lvl %lld pre %lld pick %lld rescan %lld claims %lld\n", ep.t[0], ep.t[1], ep.t[2],
+               ep.t[3], ep.t[4], ep.t[5]);
     if (lane == 0 && frame < 3)
         printf("resolve frame %d M %d matches %d ticks(100MHz) total %lld eval %lld wait %lld rounds %d fallback lanes %d revived %d occ %d\n",
                frame, M, total, wall_clock64() - pf0, pf_eval, pf_wait, pf_rounds, pf_fallback, nrevived, occ ? 1 : 0);
 #endif
+#undef OMV_RESOLVE_PREFETCH
+#undef OMV_RESOLVE_TO_STAGE
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -943,7 +1049,7 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
         }
         bits[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = 64;
+    for (int s = lane; s < S; s += 64) owner[s] = INT_MAX;
     wave_sync();
     int32_t *k2m = a.kp_to_mp + (size_t)frame * S;
     int2 *push = a.pushes + (size_t)frame * a.L.S * C;
@@ -1392,15 +1498,15 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
     f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
 }
 
-// resolve workspace: blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l, and (when it
-// fits) the double-buffered 64-point stage; *staged = 0 when only the workspace fits
-static size_t resolve_lds_bytes(int C, int cap, int *staged = nullptr) {
+// resolve workspace (dynamic LDS): blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l and,
+// when it fits beside the static stage, the frame's assignment (*lds_k2m = 1)
+static size_t resolve_lds_bytes(int C, int cap, int *lds_k2m = nullptr) {
     const size_t S = (size_t)C * cap;
     size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + sizeof(int) * S + 2 * sizeof(int32_t) * cap;
-    b = (b + 15) & ~(size_t)15;
-    const size_t with_stage = b + 2 * (size_t)StageLayout(C).bytes;
-    if (staged) *staged = with_stage <= kResolveLds;
-    return with_stage <= kResolveLds ? with_stage : b;
+    const size_t with_k2m = b + sizeof(int32_t) * S;
+    const bool fits = with_k2m + kResolveStaticLds <= kResolveLds;
+    if (lds_k2m) *lds_k2m = fits;
+    return fits ? with_k2m : b;
 }
 static size_t lf_resolve_lds_bytes(int C, int cap) {
     const size_t S = (size_t)C * cap;
@@ -1425,15 +1531,14 @@ omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
     if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)
         return OMV_ERR_ARG;
-    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds || lf_resolve_lds_bytes(n_cams, kp_cap) > kResolveLds)
+    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds - kResolveStaticLds || lf_resolve_lds_bytes(n_cams, kp_cap) > kResolveLds)
         return OMV_ERR_ARG;   // resolve workspaces must fit LDS
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
-    if (hipFuncSetAttribute((const void *)resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void *)lf_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kResolveLds) != hipSuccess)
-        return OMV_ERR_HIP;
+    const int resolve_dyn = (int)(kResolveLds - kResolveStaticLds);
+    HIP_OK(hipFuncSetAttribute((const void *)resolve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, resolve_dyn));
+    HIP_OK(hipFuncSetAttribute((const void *)resolve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, resolve_dyn));
+    HIP_OK(hipFuncSetAttribute((const void *)lf_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds));
     omv_matcher *h = new omv_matcher();
     h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
     const size_t fc = (size_t)max_frames * n_cams;
@@ -1540,11 +1645,14 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
-    int staged = 1;
+    int staged = 1;   // the assignment fits in LDS
     const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap, &staged);
     ResolveArgs ra{f, m, h->d_recs, h->d_counts, h->d_flags, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
                    far_points, staged};
-    resolve_kernel<<<n_frames, 64, lds, st>>>(ra);
+    if (staged)
+        resolve_kernel<true><<<n_frames, 64, lds, st>>>(ra);
+    else
+        resolve_kernel<false><<<n_frames, 64, lds, st>>>(ra);
     if (h->timing) {
         h->ev.push_back({2, {e0, e1}});
         h->ev.push_back({3, {e2, mk_event(st)}});
