@@ -309,18 +309,25 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
 }
 
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxClaims = 2 * kMaxCams;
-constexpr int kMaxRevived = 64;   // initially-occupied keypoints freed during the call (rare)
-
-struct Eval {                // claim / rel point at the lane's LDS rows (dynamic indexing stays out of scratch)
-    int nclaim;
-    int *claim;
-    int nrel;
-    int *rel;              // slots whose blocked status decided the result (best / second)
-    int nmatch;
-    bool fallback;         // needed a full window rescan
-    bool unblock;          // overwrote a blocked slot while having no observations
-};
+// Claim resolution (the order-dependent part of SearchByProjection).
+//
+// Decomposition: the keypoint slots of camera blocks >= 2 are only ever touched by searches in their own block,
+// blocks 0 and 1 are coupled by the stereo-partner writes (ORBmatcher.cc:125-131, :194-200).  So the claims form
+// independent domains D0 = {block 0, block 1} and Dc-1 = {block c} for c >= 2.  A point visits its cameras in
+// order and a failed ratio test ends its visit (the `continue` of :116 / :185 / ...), so domain w may evaluate a
+// point only once the domains of its earlier cameras have decided whether it stopped there.  One wavefront per
+// domain: each walks the points in view of its domain in map-point order, 64 at a time, with the prefix-commit
+// rounds below; per-point stop cameras and per-domain progress counters in LDS order the domains (a domain
+// waits until every earlier domain has finished the points of its current block; the order is acyclic, so the
+// workgroup always drains).
+//
+// Rounds (per domain wave): every lane evaluates its point against the committed claims; lanes whose best /
+// second candidate was claimed by an earlier lane of the same batch (or after a full rescan, or after an earlier
+// lane without observations overwrote a blocked keypoint) end the committed prefix; the prefix commits in
+// parallel (the highest lane writes a shared slot last) and the rest is re-evaluated.
+constexpr int kMaxRevived = 64;   // initially-occupied keypoints freed during the call, per domain (rare)
+constexpr int kMaxDomains = kMaxCams - 1;
+constexpr int kListCap = 128;     // per-domain ring of member point indices (the next block is built ahead)
 
 struct ResolveArgs {
     FrameArgs f;
@@ -335,45 +342,11 @@ struct ResolveArgs {
     int *err;
     float th, th_far, nnratio;
     int far_points;
-    int staged;          // the 64-point blocks are double-buffered in LDS (else read from global)
+    int lds_k2m;         // the frame's assignment is kept in LDS (else updated in global memory)
 };
 
-// Shared per-block staging of the 64 points a wavefront evaluates.
-// LDS image of one block of 64 points: raw copies of the global SoA rows [point][cam] (and [point]),
-// filled asynchronously by global_load_lds while the previous block is being resolved.
-struct BlockStage {
-    const Rec *rec;
-    const int *count, *level, *flags;
-};
-
-// Byte offsets of one stage buffer's arrays (16-byte aligned), for C cameras.
-struct StageLayout {
-    int rec, count, level, flags, bytes;
-    __host__ __device__ StageLayout(int C) {
-        rec = 0;
-        count = rec + 64 * C * (int)sizeof(Rec);
-        level = count + 64 * C * 4;
-        flags = level + 64 * C * 4;
-        bytes = flags + 64 * 4;
-    }
-};
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void gbl_void_t;
-
-// Async copy of n bytes global -> LDS (n a multiple of SZ; lane-linear image), SZ in {4, 16}.
-#define OMV_GLDS_COPY(NAME, SZ)                                                                                \
-    __device__ __forceinline__ void NAME(const void *g, void *l, int n, int lane) {                             \
-        for (int off = 0; off < n; off += 64 * SZ)                                                             \
-            if (off + lane * SZ < n)                                                                           \
-                __builtin_amdgcn_global_load_lds((gbl_void_t *)((const char *)g + off + lane * SZ),            \
-                                                 (lds_void_t *)((char *)l + off), SZ, 0, 0);                   \
-    }
-OMV_GLDS_COPY(glds_copy16, 16)
-OMV_GLDS_COPY(glds_copy4, 4)
-#undef OMV_GLDS_COPY
-// The resolve workgroup is ONE wavefront: its LDS operations complete in order, so a wavefront-scope
-// fence (compiler ordering only; no vmcnt drain of the in-flight global_load_lds) replaces barriers.
+// Each domain wave issues only wave-private LDS traffic on its own slots between its rounds; a wavefront-scope
+// fence orders the wave's own LDS operations (no barrier: the other waves run their own rounds).
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -396,28 +369,30 @@ __device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float 
     return fabsf(k.x - x) < r && fabsf(k.y - y) < r;
 }
 
-// Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window
-// and skips keypoints held by a point with observations (ORBmatcher.cc:77-79); the record holds the kTop
-// best candidates in (distance, window order), so the walk is: fetch the 16 entries and their blocked bits
-// together (two LDS round trips, no per-entry dependency chain), then take the first two unblocked entries
-// with mask arithmetic.  The only own earlier write of the point that can fall into a later camera's
-// block is camera 0's stereo-partner claim in block 1 (pa0, ORBmatcher.cc:125-131): it reads as blocked
-// iff the point itself has observations.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register vector (uint4 copies go by memcpy)
+
+// One (point, camera) record held in registers: the kTop candidates, the unblocked count, the predicted level.
+struct RegRec {
+    u32x4 e[kTop / 4];
+    int count, level;
+};
+
+// Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window and
+// skips keypoints held by a point with observations (ORBmatcher.cc:77-79); the record holds the kTop best
+// candidates in (distance, window order), so the walk is: fetch the 16 blocked bits together (one LDS round
+// trip), then take the first two unblocked entries with mask arithmetic.  The only own earlier write of the
+// point that can fall into a later camera's block is camera 0's stereo-partner claim in block 1 (pa0,
+// ORBmatcher.cc:125-131): it reads as blocked iff the point itself has observations.
 struct Pick {
     int b1, b2, d1, d2, o1, o2;
     bool rescan;   // the 16 entries ran out with more candidates in the window
 };
 
-__device__ __forceinline__ Pick pick_record(const Rec &r, int rcount, int c, int cap, const uint32_t *bits, int pa0,
-                                            bool obs) {
-    const uint4 *r4 = reinterpret_cast<const uint4 *>(&r);
+__device__ __forceinline__ Pick pick_record(const RegRec &r, int c, int cap, const uint32_t *bits, int pa0, bool obs) {
     uint32_t e[kTop];
 #pragma unroll
-    for (int v = 0; v < kTop / 4; ++v) {
-        const uint4 q = r4[v];
-        e[4 * v] = q.x, e[4 * v + 1] = q.y, e[4 * v + 2] = q.z, e[4 * v + 3] = q.w;
-    }
-    const int avail = min(rcount, kTop);
+    for (int v = 0; v < kTop / 4; ++v) e[4 * v] = r.e[v].x, e[4 * v + 1] = r.e[v].y, e[4 * v + 2] = r.e[v].z, e[4 * v + 3] = r.e[v].w;
+    const int avail = min(r.count, kTop);
     uint32_t blocked = 0;
 #pragma unroll
     for (int k = 0; k < kTop; ++k) {
@@ -438,14 +413,14 @@ __device__ __forceinline__ Pick pick_record(const Rec &r, int rcount, int c, int
     Pick p;
     p.b1 = k1 >= 0 ? rec_idx(v1) : -1, p.d1 = k1 >= 0 ? rec_dist(v1) : 256, p.o1 = k1 >= 0 ? rec_oct(v1) : -1;
     p.b2 = k2 >= 0 ? rec_idx(v2) : -1, p.d2 = k2 >= 0 ? rec_dist(v2) : 256, p.o2 = k2 >= 0 ? rec_oct(v2) : -1;
-    p.rescan = k2 < 0 && rcount > kTop;
+    p.rescan = k2 < 0 && r.count > kTop;
     return p;
 }
 
 // Full GetFeaturesInArea rescan of one window against the current claims (freed initially-occupied
 // keypoints, or more than kTop - 2 candidates claimed): rare.
 __device__ __forceinline__ Pick rescan_window(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
-                                           const uint32_t *bits, int pa0, bool obs) {
+                                              const uint32_t *bits, int pa0, bool obs) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     const size_t bc = fm * f.n_cams + c;
@@ -461,9 +436,9 @@ __device__ __forceinline__ Pick rescan_window(const ResolveArgs &a, int frame, s
     return p;
 }
 
-// Does a freed initially-occupied keypoint fall into this (point, camera) window?  (rare)
+// Does a freed initially-occupied keypoint of this domain fall into this (point, camera) window?  (rare)
 __device__ __forceinline__ bool revived_in_window(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
-                                               const int *revived, int nrevived, int self_rev) {
+                                                  const int *revived, int nrevived, int self_rev) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     if (nrevived > kMaxRevived) return true;   // list overflowed: rescan every window (exact, slow)
@@ -477,152 +452,269 @@ __device__ __forceinline__ bool revived_in_window(const ResolveArgs &a, int fram
     return c == 1 && self_rev >= 0 && in_window(f, frame, c, self_rev, m.proj_x[bc], m.proj_y[bc], rad, lvl);
 }
 
-// One map point against the committed claims (ORBmatcher.cc:33-177 for one pMP).  Cameras are visited in
-// ascending order over the in-view bits only (the wave iterates the largest in-view count of its lanes,
-// not n_cams).  Claims and the slots that decided the result go to the lane's LDS rows.
-#ifdef OMV_RESOLVE_PROFILE
-struct EvalProf {
-    long long t[6], last;
+// One point's visit of the NC cameras c0 .. c0+NC-1 of a domain (ORBmatcher.cc:45-330 for one pMP), against the
+// committed claims.  NC = 2 for D0 (blocks 0 and 1, stereo partners), 1 for the side domains.  Claims and the
+// slots that decided the result stay in registers (compile-time indices).
+template <int NC>
+struct Visit {
+    int claim[2 * NC];   // slots written (mvpMapPoints = pMP), -1 none
+    int rel[2 * NC];     // best / second slots per camera, -1 none
+    int nmatch;
+    int stop;            // camera whose ratio test failed (the visit ended there), 255 none
+    bool fallback;       // needed a full window rescan
+    bool unblock;        // overwrote a blocked slot while having no observations
 };
-#define OMV_EP(k) (ep.t[k] += wall_clock64() - ep.last, ep.last = wall_clock64())
-#else
-struct EvalProf {};
-#define OMV_EP(k) ((void)0)
-#endif
-__device__ void evaluate(const ResolveArgs &a, int frame, int i, int l, const BlockStage &bs, const uint32_t *bits,
-                         const uint32_t *occ0, const int *revived, int nrevived, const int32_t *l2r,
-                         const int32_t *r2l, Eval &e, EvalProf &ep) {
+
+template <int NC>
+__device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, int c0, int fl, const RegRec (&rr)[NC],
+                                      const uint32_t *bits, const uint32_t *occ0, const int *revived, int nrevived,
+                                      const int32_t *l2r, const int32_t *r2l, Visit<NC> &v) {
     const FrameArgs &f = a.f;
     const int C = f.n_cams, cap = f.kp_cap;
-    e.nclaim = e.nrel = e.nmatch = 0;
-    e.fallback = e.unblock = false;
-    const int fl = bs.flags[l];
-    OMV_EP(0);
-    if (fl & kFlagSkip) return;
+#pragma unroll
+    for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
+    v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
     const size_t fm = (size_t)frame * a.m.M + i;
     const bool obs = (fl & kFlagObs) != 0;
-    auto add_claim = [&](int slot) {
-        if (!obs && bit_of(bits, slot)) e.unblock = true;   // overwrites a keypoint later points saw blocked
-        e.claim[e.nclaim++] = slot;
+    auto claim = [&](int q, int slot) {
+        if (!obs && bit_of(bits, slot)) v.unblock = true;   // overwrites a keypoint later points saw blocked
+        v.claim[q] = slot;
     };
-    // the left block's stereo partner claim (ORBmatcher.cc:125-131) by a point without observations frees
-    // an initially-occupied right keypoint for this point's own right-block search (:150-160); the
-    // right-block record was built without it (occupied at the call), so that window is rescanned
+    // the left block's stereo partner claim (ORBmatcher.cc:125-131) by a point without observations frees an
+    // initially-occupied right keypoint for this point's own right-block search (:150-160); the right-block
+    // record was built without it (occupied at the call), so that window is rescanned
     int self_rev = -1, pa0 = -1;
-    for (uint32_t vm = (uint32_t)fl & ((1u << C) - 1u); vm; vm &= vm - 1u) {
-        const int c = __ffs(vm) - 1;
-        const int lvl = bs.level[l * C + c];
-        const int rcount = bs.count[l * C + c];
-        OMV_EP(1);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const int c = c0 + k;
+        if (!((fl >> c) & 1)) continue;
+        const int lvl = rr[k].level;
         if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
         bool need_rescan = (nrevived > 0 || (c == 1 && self_rev >= 0)) &&
                            revived_in_window(a, frame, fm, c, lvl, revived, nrevived, self_rev);
-        if (rcount == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
+        if (rr[k].count == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
         Pick p;
-        OMV_EP(2);
         if (!need_rescan) {
-            p = pick_record(bs.rec[l * C + c], rcount, c, cap, bits, c == 1 ? pa0 : -1, obs);
+            p = pick_record(rr[k], c, cap, bits, c == 1 ? pa0 : -1, obs);
             need_rescan = p.rescan;
         }
-        OMV_EP(3);
         if (need_rescan) {
-            e.fallback = true;
+            v.fallback = true;
             p = rescan_window(a, frame, fm, c, lvl, bits, c == 1 ? pa0 : -1, obs);
         }
-        OMV_EP(4);
-        if (p.b1 >= 0) e.rel[e.nrel++] = c * cap + p.b1;
-        if (p.b2 >= 0) e.rel[e.nrel++] = c * cap + p.b2;
+        v.rel[2 * k] = p.b1 >= 0 ? c * cap + p.b1 : -1;
+        v.rel[2 * k + 1] = p.b2 >= 0 ? c * cap + p.b2 : -1;
         if (p.d1 <= kTH_HIGH) {
-            if (p.o1 == p.o2 && (float)p.d1 > a.nnratio * p.d2) return;   // `continue` to the next map point
+            if (p.o1 == p.o2 && (float)p.d1 > a.nnratio * p.d2) {   // `continue` to the next map point
+                v.stop = c;
+                return;
+            }
             if (c == 0) {
-                add_claim(p.b1);
+                claim(0, p.b1);
                 if (C > 1 && l2r[p.b1] != -1) {
                     const int ps = cap + l2r[p.b1];
                     if (!obs && bit_of(occ0, ps) && bit_of(bits, ps)) self_rev = ps;
-                    add_claim(ps), e.nmatch++;
+                    claim(1, ps), v.nmatch++;
                     pa0 = ps;
                 }
-                e.nmatch++;
+                v.nmatch++;
             } else if (c == 1) {
-                if (r2l[p.b1] != -1) add_claim(r2l[p.b1]), e.nmatch++;
-                add_claim(cap + p.b1);
-                e.nmatch++;
+                if (r2l[p.b1] != -1) claim(2 * k, r2l[p.b1]), v.nmatch++;
+                claim(2 * k + 1, cap + p.b1);
+                v.nmatch++;
             } else {
-                add_claim(c * cap + p.b1);
-                e.nmatch++;
+                claim(2 * k, c * cap + p.b1);
+                v.nmatch++;
             }
         }
-        OMV_EP(5);
     }
 }
 
-// One stage buffer (the current 64-point block) sized for kMaxCams; the claim state is in dynamic LDS.
-constexpr int kStageBytes = 64 * kMaxCams * (int)sizeof(Rec) + 2 * 64 * kMaxCams * 4 + 64 * 4;
-constexpr size_t kResolveStaticLds = (size_t)kStageBytes + 2 * 64 * kMaxClaims * 4 + 4 * (kMaxRevived + 1);
+// Shared LDS state of one frame's resolve (all domains).
+struct ResolveShared {
+    uint32_t *bits;    // blocked: mvpMapPoints[s] has observations (atomics: a word may hold two domains' slots)
+    uint32_t *occ0;    // initially occupied (not in the records)
+    int *owner;        // per slot: phase-stamped claim word (see run_domain)
+    int32_t *l2r, *r2l;
+    int32_t *k2m;      // this frame's mvpMapPoints (LDS or global)
+    uint8_t *stop;     // per point: the camera whose ratio test ended its visit (255 none)
+    int *prog;         // per domain: points below this index are final in that domain
+    int *list;         // per domain ring of member point indices [kMaxDomains][kListCap]
+    int *revived;      // per domain [kMaxDomains][kMaxRevived]
+    int *nrevived;     // per domain
+    int *total;
+};
 
-// One wavefront (one 64-thread workgroup) per frame.
-// The next 64-point block is prefetched into registers with ordinary global loads while the current block
-// resolves, and written to the LDS stage at the block boundary: the loads' only consumers are those writes,
-// so nothing in the rounds waits on them (an LDS-DMA prefetch would make the compiler drain it before LDS
-// accesses it cannot prove disjoint).  kLdsK2m: the frame's assignment (mvpMapPoints) also lives in LDS and
-// is written back once (no global store in the rounds); otherwise it is updated in global memory.
+// The rounds of one domain (wave w) over its member points.
+template <int NC>
+__device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveShared &sh, int frame, int w, int c0,
+                                           int lane) {
+    const int C = a.f.n_cams, M = a.m.M;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int *list = sh.list + w * kListCap;
+    int *revived = sh.revived + w * kMaxRevived;
+    const int *flags_f = a.flags + (size_t)frame * M;
+    const size_t rec_base = (size_t)frame * M;
+    const uint32_t dom_mask = ((1u << NC) - 1u) << c0;
+    // member list: points [0, fscan) scanned; ring entries [head, tail)
+    int fscan = 0, head = 0, tail = 0;
+    // flags of the next 4 chunks of 64 points, prefetched
+    int fr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) fr[q] = q * 64 + lane < M ? flags_f[q * 64 + lane] : kFlagSkip;
+    // append members until the ring holds a full block past `from` (or the points run out)
+    auto fill = [&](int from) {
+        while (tail - from < 64 && fscan < M) {
+            const int fl = fr[0];
+            fr[0] = fr[1], fr[1] = fr[2], fr[2] = fr[3];
+            const int nxt = fscan + 4 * 64 + lane;
+            fr[3] = nxt < M ? flags_f[nxt] : kFlagSkip;
+            const bool mem = fscan + lane < M && !(fl & kFlagSkip) && (fl & dom_mask);
+            const uint64_t bm = __ballot(mem);
+            if (mem) list[(tail + __popcll(bm & lt)) & (kListCap - 1)] = fscan + lane;
+            tail += __popcll(bm);
+            fscan += 64;
+        }
+        wave_sync();
+    };
+    // register prefetch of a block's records (lane l: member point l of the block)
+    RegRec cur[NC], nxt[NC];
+    int cur_flag = 0, nxt_flag = 0;
+    auto load_block = [&](int h, RegRec (&rr)[NC], int &flag) {
+        const int nb = min(64, tail - h);
+        const int pt = list[(h + min(lane, max(nb - 1, 0))) & (kListCap - 1)];
+        flag = flags_f[pt];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            const size_t bc = (rec_base + pt) * C + c0 + k;
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(a.recs + bc);
+#pragma unroll
+            for (int q = 0; q < kTop / 4; ++q) rr[k].e[q] = src[q];
+            rr[k].count = a.counts[bc];
+            rr[k].level = a.m.level[bc];
+        }
+    };
+    fill(0);
+    if (tail > head) load_block(head, nxt, nxt_flag);
+    int total = 0;
+    int phase = 0x3fffff;   // owner stamp of the current conflict phase (commit phase = phase - 1)
+    while (tail > head) {
+        const int nb = min(64, tail - head);
+        const int pt = list[(head + min(lane, nb - 1)) & (kListCap - 1)];
+        const int pmax = list[(head + nb - 1) & (kListCap - 1)];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) cur[k] = nxt[k];
+        cur_flag = nxt_flag;
+        // build and prefetch the next block while this one resolves
+        const int head2 = head + nb;
+        fill(head2);
+        if (tail > head2) load_block(head2, nxt, nxt_flag);
+        // the earlier domains must have decided every point of this block
+        for (int q = 0; q < w; ++q)
+            while (__hip_atomic_load(&sh.prog[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= pmax)
+                __builtin_amdgcn_s_sleep(1);
+        const bool alive = lane < nb && (w == 0 || sh.stop[pt] > c0);
+        int start = 0;
+        while (start < nb) {
+            const bool active = alive && lane >= start;
+            Visit<NC> v;
+            const int nrev = min(sh.nrevived[w], kMaxRevived + 1);
+            if (active) visit<NC>(a, frame, pt, c0, cur_flag, cur, sh.bits, sh.occ0, revived, nrev, sh.l2r, sh.r2l, v);
+            else {
+#pragma unroll
+                for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
+                v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
+            }
+            const bool obs = active && (cur_flag & kFlagObs);
+            const int keyA = (phase << 7) | lane, keyB = ((phase - 1) << 7) | (63 - lane);
+            if (obs) {
+#pragma unroll
+                for (int q = 0; q < 2 * NC; ++q)
+                    if (v.claim[q] >= 0) atomicMin(&sh.owner[v.claim[q]], keyA);
+            }
+            wave_sync();
+            bool conflict = false;
+            if (active && lane > start) {
+                conflict = v.fallback;   // a full rescan saw the whole window: only safe at the batch head
+#pragma unroll
+                for (int q = 0; q < 2 * NC; ++q)
+                    if (v.rel[q] >= 0) {
+                        const int o = sh.owner[v.rel[q]];
+                        conflict = conflict || ((o >> 7) == phase && (o & 127) < lane);
+                    }
+            }
+            uint64_t cm = __ballot(conflict);
+            const uint64_t um = __ballot(active && v.unblock);
+            if (um) {
+                // a point without observations overwrote a blocked keypoint: later lanes saw it blocked
+                const int u = __ffsll((long long)um) - 1;
+                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));
+            }
+            const int j0 = cm ? min(nb, __ffsll((long long)cm) - 1) : nb;
+            // commit lanes [start, j0): the highest committing lane writes a shared slot last
+            const bool committed = active && lane < j0;
+            if (committed) {
+#pragma unroll
+                for (int q = 0; q < 2 * NC; ++q)
+                    if (v.claim[q] >= 0) atomicMin(&sh.owner[v.claim[q]], keyB);
+            }
+            wave_sync();
+            if (committed) {
+#pragma unroll
+                for (int q = 0; q < 2 * NC; ++q) {
+                    const int s = v.claim[q];
+                    if (s < 0 || sh.owner[s] != keyB) continue;
+                    sh.k2m[s] = pt;
+                    if (obs) {
+                        atomicOr(&sh.bits[s >> 5], 1u << (s & 31));
+                    } else {
+                        if (bit_of(sh.occ0, s) && bit_of(sh.bits, s)) {   // an initially occupied keypoint is freed
+                            const int r = atomicAdd(&sh.nrevived[w], 1);
+                            if (r < kMaxRevived) revived[r] = s;
+                        }
+                        atomicAnd(&sh.bits[s >> 5], ~(1u << (s & 31)));
+                    }
+                }
+                if (v.stop != 255) sh.stop[pt] = (uint8_t)v.stop;
+                total += v.nmatch;
+            }
+            phase -= 2;
+            start = j0;
+            wave_sync();
+        }
+        head = head2;
+        // every point below the next block's first member is final in this domain
+        if (lane == 0)
+            __hip_atomic_store(&sh.prog[w], tail > head ? list[head & (kListCap - 1)] : M, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (lane == 0) __hip_atomic_store(&sh.prog[w], M, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
+    if (lane == 0) atomicAdd(sh.total, total);
+}
+
+// One workgroup per frame, one wavefront per claim domain (1 + max(0, n_cams - 2) waves).
 template <bool kLdsK2m>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) resolve_kernel(ResolveArgs a) {
+__global__ void __launch_bounds__(64 * kMaxDomains) resolve_kernel(ResolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kStageBytes];
-    __shared__ int revived[kMaxRevived];
-    __shared__ int nrevived;
-    __shared__ int lane_claim[64 * kMaxClaims], lane_rel[64 * kMaxClaims];
-    const int frame = blockIdx.x, lane = threadIdx.x;
-    const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap;
+    __shared__ int list[kMaxDomains * kListCap];
+    __shared__ int revived[kMaxDomains * kMaxRevived];
+    __shared__ int nrevived[kMaxDomains], prog[kMaxDomains], total;
+    const int frame = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const int C = a.f.n_cams, cap = a.f.kp_cap, S = C * cap, M = a.m.M;
     const int nwords = (S + 31) >> 5;
-    uint32_t *bits = rsm;                                         // blocked: mvpMapPoints[s] has observations
-    uint32_t *occ0 = rsm + nwords;                                // initially occupied (not in the records)
-    // owner: per slot, a phase-stamped word (phase << 7 | x, phases count down, so the current phase's
-    // atomicMin always beats stale words and nothing is ever reset).  Conflict phase: x = the first lane
-    // (with observations) claiming the slot; commit phase: x = 63 - the last committing writer.
-    int *owner = reinterpret_cast<int *>(rsm + 2 * nwords);
-    int32_t *l2r_s = owner + S;                                   // this frame's mvLeftToRightMatch
-    int32_t *r2l_s = l2r_s + cap;                                 // and mvRightToLeftMatch
+    ResolveShared sh;
+    sh.bits = rsm;
+    sh.occ0 = rsm + nwords;
+    sh.owner = reinterpret_cast<int *>(rsm + 2 * nwords);
+    sh.l2r = sh.owner + S;
+    sh.r2l = sh.l2r + cap;
     int32_t *const k2m_g = a.kp_to_mp + (size_t)frame * S;
-    int32_t *const k2m = kLdsK2m ? r2l_s + cap : k2m_g;          // this frame's mvpMapPoints
-    const StageLayout SL(C);
-    const int M = a.m.M;
-    // register prefetch of one block: lane-linear 16-B chunks of the records, dwords of counts / levels, flags
-    // (macros, not lambdas: the arrays must stay in registers)
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register vector (uint4 copies go by memcpy)
-    u32x4 pre_rec[kMaxCams * 4];
-    int pre_cnt[kMaxCams], pre_lvl[kMaxCams], pre_flag = 0;
-#define OMV_RESOLVE_PREFETCH(BASE)                                                                              \
-    {                                                                                                           \
-        const int nb_ = min(64, M - (BASE));                                                                    \
-        const size_t o_ = ((size_t)frame * M + (BASE)) * C;                                                     \
-        const u32x4 *rs_ = reinterpret_cast<const u32x4 *>(a.recs + o_);                                        \
-        const int lr_ = nb_ * C * 4 - 1, lc_ = nb_ * C - 1; /* clamped (branch-free) tail reads */           \
-        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams * 4; ++v)                               \
-            pre_rec[v] = rs_[min(lane + 64 * v, lr_)];                                                          \
-        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams; ++v) {                                 \
-            pre_cnt[v] = a.counts[o_ + min(lane + 64 * v, lc_)];                                                \
-            pre_lvl[v] = a.m.level[o_ + min(lane + 64 * v, lc_)];                                               \
-        }                                                                                                       \
-        pre_flag = a.flags[(size_t)frame * M + (BASE) + min(lane, nb_ - 1)];                                   \
-    }
-#define OMV_RESOLVE_TO_STAGE(BASE)                                                                              \
-    {                                                                                                           \
-        const int nb_ = min(64, M - (BASE));                                                                    \
-        u32x4 *rd_ = reinterpret_cast<u32x4 *>(stage + SL.rec);                                                 \
-        int *cd_ = reinterpret_cast<int *>(stage + SL.count), *ld_ = reinterpret_cast<int *>(stage + SL.level); \
-        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams * 4; ++v)                               \
-            if (lane + 64 * v < nb_ * C * 4) rd_[lane + 64 * v] = pre_rec[v];                                  \
-        _Pragma("clang loop unroll(full)") for (int v = 0; v < kMaxCams; ++v) if (lane + 64 * v < nb_ * C) {    \
-            cd_[lane + 64 * v] = pre_cnt[v];                                                                    \
-            ld_[lane + 64 * v] = pre_lvl[v];                                                                    \
-        }                                                                                                       \
-        if (lane < nb_) reinterpret_cast<int *>(stage + SL.flags)[lane] = pre_flag;                            \
-    }
-    if (M > 0) OMV_RESOLVE_PREFETCH(0);
+    sh.k2m = kLdsK2m ? sh.r2l + cap : k2m_g;
+    sh.stop = reinterpret_cast<uint8_t *>(sh.r2l + cap + (kLdsK2m ? S : 0));
+    sh.prog = prog, sh.list = list, sh.revived = revived, sh.nrevived = nrevived, sh.total = &total;
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
-    for (int w = lane; w < nwords; w += 64) {
+    for (int w = tid; w < nwords; w += nt) {
         uint32_t v = 0;
         if (occ) {
             uint8_t o[32];   // all 32 byte loads in flight together
@@ -631,124 +723,31 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 #pragma unroll
             for (int b = 0; b < 32; ++b) v |= (w * 32 + b < S && o[b]) ? 1u << b : 0u;
         }
-        bits[w] = v;
-        occ0[w] = v;
+        sh.bits[w] = v;
+        sh.occ0[w] = v;
     }
-    for (int s = lane; s < S; s += 64) owner[s] = INT_MAX;
+    for (int s = tid; s < S; s += nt) sh.owner[s] = INT_MAX;
     if (kLdsK2m)
-        for (int s = lane; s < S; s += 64) k2m[s] = k2m_g[s];
-    for (int s = lane; s < cap; s += 64) {
-        l2r_s[s] = a.l2r[(size_t)frame * cap + s];
-        r2l_s[s] = a.r2l[(size_t)frame * cap + s];
+        for (int s = tid; s < S; s += nt) sh.k2m[s] = k2m_g[s];
+    for (int s = tid; s < cap; s += nt) {
+        sh.l2r[s] = a.l2r[(size_t)frame * cap + s];
+        sh.r2l[s] = a.r2l[(size_t)frame * cap + s];
     }
-    if (lane == 0) nrevived = 0;
-    int total = 0;              // this lane's committed matches (summed over the wave at the end)
-    int phase = 0x3fffff;       // owner stamp of the current conflict phase (commit phase = phase - 1)
-    EvalProf ep;
-#ifdef OMV_RESOLVE_PROFILE
-    long long pf0 = wall_clock64(), pf_eval = 0, pf_wait = 0;
-    int pf_rounds = 0, pf_fallback = 0;
-    for (int k = 0; k < 6; ++k) ep.t[k] = 0;
-#endif
-    const BlockStage bs{reinterpret_cast<const Rec *>(stage + SL.rec), reinterpret_cast<const int *>(stage + SL.count),
-                        reinterpret_cast<const int *>(stage + SL.level), reinterpret_cast<const int *>(stage + SL.flags)};
-    for (int base = 0; base < M; base += 64) {
-        const int nb = min(64, M - base);
-#ifdef OMV_RESOLVE_PROFILE
-        const long long pw = wall_clock64();
-#endif
-        wave_sync();          // the previous block's rounds are done with the stage
-        OMV_RESOLVE_TO_STAGE(base);   // (waits for this block's prefetch, issued a block earlier)
-        wave_sync();
-#ifdef OMV_RESOLVE_PROFILE
-        pf_wait += wall_clock64() - pw;
-#endif
-        if (base + 64 < M) OMV_RESOLVE_PREFETCH(base + 64);
-        const int i = base + lane;
-        int start = 0;
-        while (start < nb) {
-            const bool active = lane >= start && lane < nb;
-            Eval e;
-            e.claim = lane_claim + lane * kMaxClaims;
-            e.rel = lane_rel + lane * kMaxClaims;
-            const int nrev = nrevived;
-#ifdef OMV_RESOLVE_PROFILE
-            const long long pe = wall_clock64();
-            ep.last = pe;
-            ++pf_rounds;
-#endif
-            if (active) evaluate(a, frame, i, lane, bs, bits, occ0, revived, nrev, l2r_s, r2l_s, e, ep);
-            else e.nclaim = e.nrel = e.nmatch = 0, e.fallback = e.unblock = false;
-#ifdef OMV_RESOLVE_PROFILE
-            pf_eval += wall_clock64() - pe;
-            pf_fallback += __popcll(__ballot(active && e.fallback));
-#endif
-            const bool obs = active && (bs.flags[lane] & kFlagObs);
-            const int keyA = (phase << 7) | lane, keyB = ((phase - 1) << 7) | (63 - lane);
-            if (obs)
-                for (int q = 0; q < e.nclaim; ++q) atomicMin(&owner[e.claim[q]], keyA);
-            wave_sync();
-            bool conflict = false;
-            if (active && lane > start) {
-                conflict = e.fallback;   // a full rescan saw the whole window: only safe at the batch head
-                for (int q = 0; q < e.nrel && !conflict; ++q) {
-                    const int o = owner[e.rel[q]];
-                    conflict = (o >> 7) == phase && (o & 127) < lane;
-                }
-            }
-            uint64_t cm = __ballot(conflict);
-            const uint64_t um = __ballot(active && e.unblock);
-            if (um) {
-                // a point without observations overwrote a blocked keypoint: later lanes saw it blocked
-                const int u = __ffsll((long long)um) - 1;
-                cm |= (u >= 63) ? 0ull : (~0ull << (u + 1));
-            }
-            const int j0 = cm ? min(nb, __ffsll((long long)cm) - 1) : nb;
-            // commit lanes [start, j0): the highest committing lane writes a shared slot last
-            const bool committed = lane >= start && lane < j0;
-            if (committed)
-                for (int t = 0; t < e.nclaim; ++t) atomicMin(&owner[e.claim[t]], keyB);
-            wave_sync();
-            if (committed) {
-                for (int t = 0; t < e.nclaim; ++t) {
-                    const int s = e.claim[t];
-                    if (owner[s] != keyB) continue;
-                    k2m[s] = i;
-                    if (obs) {
-                        atomicOr(&bits[s >> 5], 1u << (s & 31));
-                    } else {
-                        if (bit_of(occ0, s) && bit_of(bits, s)) {   // an initially occupied keypoint is freed
-                            const int q = atomicAdd(&nrevived, 1);
-                            if (q < kMaxRevived) revived[q] = s;
-                        }
-                        atomicAnd(&bits[s >> 5], ~(1u << (s & 31)));
-                    }
-                }
-                total += e.nmatch;
-            }
-            phase -= 2;
-            start = j0;
-            wave_sync();
-        }
+    for (int p = tid; p < M; p += nt) sh.stop[p] = 255;
+    if (tid < kMaxDomains) nrevived[tid] = 0, prog[tid] = 0;
+    if (tid == 0) total = 0;
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+    if (w == 0) {
+        if (C >= 2) run_domain<2>(a, sh, frame, 0, 0, lane);
+        else run_domain<1>(a, sh, frame, 0, 0, lane);
+    } else {
+        run_domain<1>(a, sh, frame, w, w + 1, lane);
     }
-    if (kLdsK2m) {
-        wave_sync();
-        for (int s = lane; s < S; s += 64) k2m_g[s] = k2m[s];
-    }
-    for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
-    if (lane == 0) a.n_matches[frame] = total;
-#ifdef OMV_RESOLVE_PROFILE
-    for (int k = 0; k < 6; ++k)
-        for (int d = 32; d >= 1; d >>= 1) ep.t[k] = max(ep.t[k], (long long)__shfl_xor(ep.t[k], d, 64));
-    if (lane == 0 && frame < 3)
-        printf("resolve sections flags %lld lvl %lld pre %lld pick %lld rescan %lld claims %lld\n", ep.t[0], ep.t[1], ep.t[2],
-               ep.t[3], ep.t[4], ep.t[5]);
-    if (lane == 0 && frame < 3)
-        printf("resolve frame %d M %d matches %d ticks(100MHz) total %lld eval %lld wait %lld rounds %d fallback lanes %d revived %d occ %d\n",
-               frame, M, total, wall_clock64() - pf0, pf_eval, pf_wait, pf_rounds, pf_fallback, nrevived, occ ? 1 : 0);
-#endif
-#undef OMV_RESOLVE_PREFETCH
-#undef OMV_RESOLVE_TO_STAGE
+    __syncthreads();
+    if (kLdsK2m)
+        for (int s = tid; s < S; s += nt) k2m_g[s] = sh.k2m[s];
+    if (tid == 0) a.n_matches[frame] = total;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1498,11 +1497,12 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
     f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
 }
 
-// resolve workspace (dynamic LDS): blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l and,
-// when it fits beside the static stage, the frame's assignment (*lds_k2m = 1)
-static size_t resolve_lds_bytes(int C, int cap, int *lds_k2m = nullptr) {
+// resolve workspace (dynamic LDS): blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l, the
+// per-point stop camera and, when it fits, the frame's assignment (*lds_k2m = 1)
+constexpr size_t kResolveStaticLds = 4 * ((size_t)kMaxDomains * (kListCap + kMaxRevived + 2) + 1);
+static size_t resolve_lds_bytes(int C, int cap, int M, int *lds_k2m = nullptr) {
     const size_t S = (size_t)C * cap;
-    size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + sizeof(int) * S + 2 * sizeof(int32_t) * cap;
+    const size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + sizeof(int) * S + 2 * sizeof(int32_t) * cap + ((size_t)M + 3) / 4 * 4;
     const size_t with_k2m = b + sizeof(int32_t) * S;
     const bool fits = with_k2m + kResolveStaticLds <= kResolveLds;
     if (lds_k2m) *lds_k2m = fits;
@@ -1531,7 +1531,7 @@ omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig 
 omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mps, omv_matcher **out) {
     if (!out || max_frames <= 0 || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || kp_cap > 65535 || max_mps < 0)
         return OMV_ERR_ARG;
-    if (resolve_lds_bytes(n_cams, kp_cap) > kResolveLds - kResolveStaticLds || lf_resolve_lds_bytes(n_cams, kp_cap) > kResolveLds)
+    if (resolve_lds_bytes(n_cams, kp_cap, max_mps) > kResolveLds - kResolveStaticLds || lf_resolve_lds_bytes(n_cams, kp_cap) > kResolveLds)
         return OMV_ERR_ARG;   // resolve workspaces must fit LDS
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OMV_ERR_NO_DEVICE;
@@ -1646,13 +1646,14 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
     int staged = 1;   // the assignment fits in LDS
-    const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap, &staged);
+    const size_t lds = resolve_lds_bytes(h->n_cams, h->kp_cap, M, &staged);
     ResolveArgs ra{f, m, h->d_recs, h->d_counts, h->d_flags, l2r, r2l, kp_occ_init, kp_to_mp, n_matches, h->d_err, th, th_far, nnratio,
                    far_points, staged};
+    const int n_dom = 1 + max(0, h->n_cams - 2);   // one wavefront per claim domain
     if (staged)
-        resolve_kernel<true><<<n_frames, 64, lds, st>>>(ra);
+        resolve_kernel<true><<<n_frames, 64 * n_dom, lds, st>>>(ra);
     else
-        resolve_kernel<false><<<n_frames, 64, lds, st>>>(ra);
+        resolve_kernel<false><<<n_frames, 64 * n_dom, lds, st>>>(ra);
     if (h->timing) {
         h->ev.push_back({2, {e0, e1}});
         h->ev.push_back({3, {e2, mk_event(st)}});
