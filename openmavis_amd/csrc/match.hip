@@ -56,13 +56,18 @@ struct FrameArgs {
 };
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) grid_kernel(FrameArgs f, int32_t *cell_start, int32_t *cell_idx) {
+// One 256-thread workgroup per (frame, camera): per-cell counts by LDS atomics, a block scan of the 3,072
+// counts, an unordered scatter by per-cell cursors, then each cell's (short) run sorted by keypoint index —
+// the reference push_backs in index order, and GetFeaturesInArea's output order depends on it.
+__global__ void __launch_bounds__(256) grid_kernel(FrameArgs f, int32_t *cell_start, int32_t *cell_idx) {
     __shared__ int cnt[kCells];
+    __shared__ int cur[kCells];
+    __shared__ int wsum[4];
     const int fc = blockIdx.x;   // frame * n_cams + cam
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = f.n_kp[fc];
     const omv_kp *kp = f.kps + (size_t)fc * f.kp_cap;
-    for (int c = lane; c < kCells; c += 64) cnt[c] = 0;
+    for (int c = tid; c < kCells; c += 256) cnt[c] = 0;
     __syncthreads();
     auto cell_of = [&](int i) {
         const int px = (int)roundf((kp[i].x - f.min_x) * f.invW);
@@ -70,53 +75,51 @@ __global__ void __launch_bounds__(64) grid_kernel(FrameArgs f, int32_t *cell_sta
         if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
         return px * kGridRows + py;   // mGrid[ix][iy]
     };
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += 256) {
         const int c = cell_of(i);
         if (c >= 0) atomicAdd(&cnt[c], 1);
     }
     __syncthreads();
-    // exclusive scan of 3072 counts: 48 per lane
-    constexpr int per = kCells / 64;
-    int s = 0;
-    for (int k = 0; k < per; ++k) s += cnt[lane * per + k];
+    // exclusive scan of 3,072 counts: 12 per thread, wave scan, then the 4 wave totals
+    constexpr int per = kCells / 256;
+    int v[per], s = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) v[k] = cnt[tid * per + k], s += v[k];
     int incl = s;
     for (int d = 1; d < 64; d <<= 1) {
         const int t = __shfl_up(incl, d, 64);
         if (lane >= d) incl += t;
     }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
     int run = incl - s;
-    __syncthreads();
+    for (int q = 0; q < wv; ++q) run += wsum[q];
     int32_t *cs = cell_start + (size_t)fc * (kCells + 1);
+#pragma unroll
     for (int k = 0; k < per; ++k) {
-        const int c = lane * per + k;
-        const int v = cnt[c];
-        cnt[c] = run;
+        const int c = tid * per + k;
         cs[c] = run;
-        run += v;
+        cnt[c] = run;   // start of the cell's run
+        cur[c] = run;   // scatter cursor
+        run += v[k];
     }
-    if (lane == 63) cs[kCells] = run;
+    if (tid == 255) cs[kCells] = run;
     __syncthreads();
-    // order-preserving scatter, 64 keypoints at a time
     int32_t *out = cell_idx + (size_t)fc * f.kp_cap;
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
-        const int c = i < n ? cell_of(i) : -1;
-        int before = 0, after = 0;
-        for (int j = 0; j < 64; ++j) {
-            const int cj = __shfl(c, j, 64);
-            if (cj == c) {
-                before += j < lane;
-                after += j > lane;
-            }
+    for (int i = tid; i < n; i += 256) {
+        const int c = cell_of(i);
+        if (c >= 0) out[atomicAdd(&cur[c], 1)] = i;
+    }
+    __syncthreads();
+    // ascending index order inside each cell (runs are a few entries long)
+    for (int c = tid; c < kCells; c += 256) {
+        const int b0 = cnt[c], e0 = cur[c];
+        for (int p = b0 + 1; p < e0; ++p) {
+            const int x = out[p];
+            int q = p - 1;
+            while (q >= b0 && out[q] > x) out[q + 1] = out[q], --q;
+            out[q + 1] = x;
         }
-        int pos = 0;
-        if (c >= 0) {
-            pos = cnt[c] + before;
-            out[pos] = i;
-        }
-        __syncthreads();
-        if (c >= 0 && after == 0) cnt[c] = pos + 1;
-        __syncthreads();
     }
 }
 
@@ -598,6 +601,13 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
     if (tail > head) load_block(head, nxt, nxt_flag);
     int total = 0;
     int phase = 0x3fffff;   // owner stamp of the current conflict phase (commit phase = phase - 1)
+#ifdef OMV_RESOLVE_PROFILE
+    long long tp[5] = {0, 0, 0, 0, 0}, tl = wall_clock64();
+    int nblocks = 0, nrounds = 0;
+#define OMV_TP(k) (tp[k] += wall_clock64() - tl, tl = wall_clock64())
+#else
+#define OMV_TP(k) ((void)0)
+#endif
     while (tail > head) {
         const int nb = min(64, tail - head);
         const int pt = list[(head + min(lane, nb - 1)) & (kListCap - 1)];
@@ -613,18 +623,21 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
         for (int q = 0; q < w; ++q)
             while (__hip_atomic_load(&sh.prog[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= pmax)
                 __builtin_amdgcn_s_sleep(1);
+        OMV_TP(0);
         const bool alive = lane < nb && (w == 0 || sh.stop[pt] > c0);
         int start = 0;
         while (start < nb) {
             const bool active = alive && lane >= start;
             Visit<NC> v;
             const int nrev = min(sh.nrevived[w], kMaxRevived + 1);
+            OMV_TP(1);
             if (active) visit<NC>(a, frame, pt, c0, cur_flag, cur, sh.bits, sh.occ0, revived, nrev, sh.l2r, sh.r2l, v);
             else {
 #pragma unroll
                 for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
                 v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
             }
+            OMV_TP(2);
             const bool obs = active && (cur_flag & kFlagObs);
             const int keyA = (phase << 7) | lane, keyB = ((phase - 1) << 7) | (63 - lane);
             if (obs) {
@@ -681,7 +694,14 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
             phase -= 2;
             start = j0;
             wave_sync();
+            OMV_TP(3);
+#ifdef OMV_RESOLVE_PROFILE
+            ++nrounds;
+#endif
         }
+#ifdef OMV_RESOLVE_PROFILE
+        ++nblocks;
+#endif
         head = head2;
         // every point below the next block's first member is final in this domain
         if (lane == 0)
@@ -689,6 +709,12 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
                                __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (lane == 0) __hip_atomic_store(&sh.prog[w], M, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef OMV_RESOLVE_PROFILE
+    if (lane == 0 && frame < 2)
+        printf("resolve frame %d domain %d blocks %d rounds %d ticks(100MHz): block-start+deps %lld rounds-pre %lld visit %lld commit %lld\n",
+               frame, w, nblocks, nrounds, tp[0], tp[1], tp[2], tp[3]);
+#endif
+#undef OMV_TP
     for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
     if (lane == 0) atomicAdd(sh.total, total);
 }
@@ -762,17 +788,26 @@ struct KnnArgs {
     int out_cap;
 };
 
+// G lanes per query: lane g of a query's group scores train rows g, g+G, ... of every LDS tile (its own top-2 by
+// (distance, index), strict updates in index order), then the group merges its G top-2 lists with shuffles.  The
+// result is the two smallest (distance, index) pairs — exactly knnMatch's "first index wins ties".  G > 1 cuts
+// the per-query chain for small batches (one frame: 1,200 queries); G = 1 for large batches.
+template <int G>
 __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
     __shared__ __attribute__((aligned(16))) uint64_t tile[256][4];
+    constexpr int QB = 256 / G;   // queries per block
     const int pair = blockIdx.y;
     const int qo = a.q_off ? a.q_off[pair * a.pair_stride_off] : 0;
     const int to = a.t_off ? a.t_off[pair * a.pair_stride_off] : 0;
     const int nq = a.nq[pair * a.pair_stride_off] - qo;
     const int nt = a.nt[pair * a.pair_stride_off] - to;
-    const int qi = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= max(nq, 0)) return;   // block-uniform
+    const int g = threadIdx.x % G;
+    const int qi = blockIdx.x * QB + threadIdx.x / G;
+    if (blockIdx.x * QB >= max(nq, 0)) return;   // block-uniform
     uint64_t dq[4] = {0, 0, 0, 0};
     if (qi < nq) load_desc(a.q + pair * a.q_stride + (size_t)(qo + qi) * 32, dq);
+    // keys (distance << 32 | index): "none" = (INT_MAX, -1) sorts last
+    uint64_t k0 = ~0ull >> 1, k1 = ~0ull >> 1;
     int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
     for (int b = 0; b < nt; b += 256) {
         __syncthreads();
@@ -780,7 +815,7 @@ __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
         if (j < nt) load_desc(a.t + pair * a.t_stride + (size_t)(to + j) * 32, tile[threadIdx.x]);
         __syncthreads();
         const int e = min(256, nt - b);
-        for (int k = 0; k < e; ++k) {
+        for (int k = g; k < e; k += G) {
             const int d = omv::hamming256(dq, tile[k]);
             if (d < d1) {
                 if (d0 > d) d1 = d0, i1 = i0, d0 = d, i0 = b + k;
@@ -788,10 +823,30 @@ __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
             }
         }
     }
-    if (qi < nq) {
+    k0 = ((uint64_t)(uint32_t)d0 << 32) | (uint32_t)i0;
+    k1 = ((uint64_t)(uint32_t)d1 << 32) | (uint32_t)i1;
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) {   // merge with the partner group-lane's top-2
+        const uint64_t o0 = __shfl_xor(k0, m, 64), o1 = __shfl_xor(k1, m, 64);
+        const uint64_t r0 = k0 < o0 ? k0 : o0;
+        const uint64_t r1 = k0 < o0 ? (k1 < o0 ? k1 : o0) : (k0 < o1 ? k0 : o1);
+        k0 = r0, k1 = r1;
+    }
+    if (qi < nq && g == 0) {
         int32_t *oi = a.idx2 + ((size_t)pair * a.out_cap + qi) * 2;
         int32_t *od = a.dist2 + ((size_t)pair * a.out_cap + qi) * 2;
-        oi[0] = i0, oi[1] = i1, od[0] = d0, od[1] = d1;
+        oi[0] = (int32_t)(uint32_t)k0, oi[1] = (int32_t)(uint32_t)k1;
+        od[0] = (int32_t)(k0 >> 32), od[1] = (int32_t)(k1 >> 32);
+    }
+}
+
+// Lanes per query for a knn launch of n_pairs x q_cap queries: spread small batches over the whole chip.
+static void launch_knn2(const KnnArgs &a, int n_pairs, int q_cap, hipStream_t st) {
+    const long long queries = (long long)n_pairs * q_cap;
+    if (queries <= 32768) {
+        knn2_kernel<8><<<dim3((q_cap + 31) / 32, n_pairs), 256, 0, st>>>(a, n_pairs);
+    } else {
+        knn2_kernel<1><<<dim3((q_cap + 255) / 256, n_pairs), 256, 0, st>>>(a, n_pairs);
     }
 }
 
@@ -1606,7 +1661,7 @@ omv_status omv_matcher_assign_grid(omv_matcher *h, int n_frames, const omv_frame
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
-    grid_kernel<<<n_frames * h->n_cams, 64, 0, st>>>(f, h->d_cell_start, h->d_cell_idx);
+    grid_kernel<<<n_frames * h->n_cams, 256, 0, st>>>(f, h->d_cell_start, h->d_cell_idx);
     if (h->timing) h->ev.push_back({0, {e0, mk_event(st)}});
     HIP_OK(hipGetLastError());
     return OMV_OK;
@@ -1772,8 +1827,7 @@ omv_status omv_bf_knn2(int n_pairs, const uint8_t *query, int q_cap, const int *
     if (n_pairs <= 0 || !query || !train || !nq || !nt || !idx2 || !dist2 || q_cap <= 0 || t_cap <= 0)
         return OMV_ERR_ARG;
     KnnArgs a{query, train, (long long)q_cap * 32, (long long)t_cap * 32, nq, nt, nullptr, nullptr, 1, idx2, dist2, q_cap};
-    dim3 grid((q_cap + 255) / 256, n_pairs);
-    knn2_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a, n_pairs);
+    launch_knn2(a, n_pairs, q_cap, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }
@@ -1791,8 +1845,7 @@ omv_status omv_matcher_stereo_lapping(omv_matcher *h, int n_frames, const uint8_
     // query = camera 0 rows [mono0, n0), train = camera 1 rows [mono1, n1)
     KnnArgs a{desc, desc + (size_t)cap * 32, (long long)C * cap * 32, (long long)C * cap * 32, n_kp, n_kp + 1,
               mono, mono + 1, C, h->d_knn_i, h->d_knn_d, cap};
-    dim3 grid((cap + 255) / 256, n_frames);
-    knn2_kernel<<<grid, 256, 0, st>>>(a, n_frames);
+    launch_knn2(a, n_frames, cap, st);
     dim3 g2((cap + 255) / 256, n_frames);
     stereo_pairs_kernel<<<g2, 256, 0, st>>>(h->d_knn_i, h->d_knn_d, cap, n_kp, mono, C, cap, ratio, l2r, r2l, n_frames);
     if (h->timing) h->ev.push_back({1, {e0, mk_event(st)}});
