@@ -154,8 +154,10 @@ struct Top {
         for (int q = 0; q < kTop; ++q) key[q] = ~0ull;
         n = count = seq = 0;
     }
-    __device__ __forceinline__ void insert(int idx, int dist, int oct) {
-        const uint64_t k = ((uint64_t)dist << 40) | ((uint64_t)(seq++) << 20) | ((uint64_t)oct << 16) | (uint64_t)idx;
+    __device__ __forceinline__ void insert(int idx, int dist, int oct) { insert_at(idx, dist, oct, seq++); }
+    // q: the candidate's position in the window's iteration order (< 2^20)
+    __device__ __forceinline__ void insert_at(int idx, int dist, int oct, int q) {
+        const uint64_t k = ((uint64_t)dist << 40) | ((uint64_t)q << 20) | ((uint64_t)oct << 16) | (uint64_t)idx;
 #pragma unroll
         for (int q = kTop - 1; q > 0; --q) key[q] = k < key[q - 1] ? key[q - 1] : (k < key[q] ? k : key[q]);
         key[0] = k < key[0] ? k : key[0];
@@ -219,6 +221,81 @@ __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, flo
     }
 }
 
+// scan_window over G cooperating lanes (g = the lane's rank in its group): the window's candidates in the
+// reference's iteration order (columns ix ascending, each column's cells iy ascending = one contiguous CSR run)
+// are dealt round-robin, each lane keeps its own top kTop keyed by window position, then merge_top() selects the
+// group's kTop smallest keys — the same list scan_window builds on one lane.  For small batches, where one
+// lane's chain of dependent gathers through a large window is the kernel's critical path.
+template <int G, class Blocked>
+__device__ void scan_window_coop(const FrameArgs &f, int frame, int cam, float x, float y, float r, int minL, int maxL,
+                                 const uint64_t dmp[4], Blocked blocked, Top &t, int g) {
+    t.reset();
+    const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (nMaxCellY < 0) return;
+    const bool checkLevels = (minL > 0) || (maxL >= 0);
+    const size_t fc = (size_t)frame * f.n_cams + cam;
+    const int32_t *cs = f.cell_start + fc * (kCells + 1);
+    const int32_t *ci = f.cell_idx + fc * f.kp_cap;
+    const omv_kp *kp = f.kps + fc * f.kp_cap;
+    const uint8_t *dd = f.desc + fc * f.kp_cap * 32;
+    int pos = g, acc = 0;   // this lane's next window position; window positions before the current column
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int b = cs[ix * kGridRows + nMinCellY], e = cs[ix * kGridRows + nMaxCellY + 1];
+        for (; pos < acc + (e - b); pos += G) {
+            const int i = ci[b + pos - acc];
+            const omv_kp k = kp[i];
+            uint64_t d[4];
+            load_desc(dd + (size_t)i * 32, d);
+            if (checkLevels) {
+                if (k.octave < minL) continue;
+                if (maxL >= 0 && k.octave > maxL) continue;
+            }
+            if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+            if (blocked(cam * f.kp_cap + i)) continue;
+            ++t.count;
+            t.insert_at(i, omv::hamming256(dmp, d), k.octave, pos);
+        }
+        acc += e - b;
+    }
+}
+
+// The group's kTop smallest keys (unique: window positions differ) into every lane's t, counts summed.
+template <int G>
+__device__ __forceinline__ void merge_top(Top &t) {
+    uint64_t out[kTop];
+#pragma unroll
+    for (int r = 0; r < kTop; ++r) {
+        const uint64_t h = t.key[0];
+        uint64_t mn = h;
+#pragma unroll
+        for (int s = 1; s < G; s <<= 1) {
+            const uint64_t o = __shfl_xor(mn, s, 64);
+            mn = o < mn ? o : mn;
+        }
+        out[r] = mn;
+        const bool own = h == mn && h != ~0ull;
+#pragma unroll
+        for (int q = 0; q < kTop - 1; ++q) t.key[q] = own ? t.key[q + 1] : t.key[q];
+        t.key[kTop - 1] = own ? ~0ull : t.key[kTop - 1];
+    }
+    int cnt = t.count;
+#pragma unroll
+    for (int s = 1; s < G; s <<= 1) cnt += __shfl_xor(cnt, s, 64);
+    t.count = cnt;
+    t.n = 0;
+#pragma unroll
+    for (int r = 0; r < kTop; ++r) {
+        t.key[r] = out[r];
+        t.n += out[r] != ~0ull;
+    }
+}
+
 __device__ __forceinline__ bool mp_skipped(const MpArgs &m, int frame, int i, int C, int far_points, float th_far) {
     const size_t b = (size_t)frame * m.M + i;
     bool any = false;
@@ -246,20 +323,24 @@ constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
 // (ballot prefix, slot order kept) and scans them 64 at a time.
 constexpr int kCandChunk = 192;
 
+// G: lanes per window (1 for large batches; 8 when the batch is a frame or two and the windows' gather chains,
+// not the slot count, set the kernel's time).
+template <int G>
 __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
                                                    const uint8_t *occ_init, Rec *recs, int *counts, int *flags,
                                                    int far_points, float th_far) {
-    __shared__ int queue[4][kCandChunk];
+    constexpr int kChunk = kCandChunk / G;   // slots per wave: G lanes per active slot keep ~one pass per wave
+    __shared__ int queue[4][kChunk];
     const int C = f.n_cams;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long total = (long long)n_frames * m.M * C;
-    const long long g0 = ((long long)blockIdx.x * 4 + wave) * kCandChunk;
+    const long long g0 = ((long long)blockIdx.x * 4 + wave) * kChunk;
     const uint64_t lt = (1ull << lane) - 1ull;
     int nq = 0;
-    for (int s0 = 0; s0 < kCandChunk; s0 += 64) {
+    for (int s0 = 0; s0 < kChunk; s0 += 64) {
         const long long gid = g0 + s0 + lane;
         bool act = false;
-        if (gid < total) {
+        if (s0 + lane < kChunk && gid < total) {
             const int c = (int)(gid % C);
             const long long fm = gid / C;
             const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
@@ -287,9 +368,10 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q0 = 0; q0 < nq; q0 += 64) {
-        if (q0 + lane >= nq) break;
-        const long long gid = g0 + queue[wave][q0 + lane];
+    const int g = lane % G;
+    for (int q0 = 0; q0 < nq; q0 += 64 / G) {
+        if (q0 + lane / G >= nq) break;   // whole groups leave together
+        const long long gid = g0 + queue[wave][q0 + lane / G];
         const int c = (int)(gid % C);
         const long long fm = gid / C;
         const int frame = (int)(fm / m.M);
@@ -300,14 +382,22 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
         load_desc(m.desc + (size_t)fm * 32, dmp);
         const float r = window_radius(f, m, bc, c, th, th != 1.0f);
         const uint8_t *occ = occ_init ? occ_init + (size_t)frame * C * f.kp_cap : nullptr;
-        scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp,
-                    [&](int slot) { return occ && occ[slot]; }, t);
-        uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);   // 64-B record as four 16-B stores
+        if constexpr (G == 1) {
+            scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp,
+                        [&](int slot) { return occ && occ[slot]; }, t);
+        } else {
+            scan_window_coop<G>(f, frame, c, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp,
+                                [&](int slot) { return occ && occ[slot]; }, t, g);
+            merge_top<G>(t);
+        }
+        if (g == 0) {
+            uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);   // 64-B record as four 16-B stores
 #pragma unroll
-        for (int v = 0; v < kTop / 4; ++v)
-            o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
-                               4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
-        counts[bc] = t.count;
+            for (int v = 0; v < kTop / 4; ++v)
+                o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
+                                   4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
+            counts[bc] = t.count;
+        }
     }
 }
 
@@ -1695,8 +1785,12 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
-        cand_kernel<<<(int)((tot + 4 * kCandChunk - 1) / (4 * kCandChunk)), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs,
-                                                              h->d_counts, h->d_flags, far_points, th_far);
+        if (tot <= 262144)   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
+            cand_kernel<8><<<(int)((tot + 4 * (kCandChunk / 8) - 1) / (4 * (kCandChunk / 8))), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags,
+                                                 far_points, th_far);
+        else
+            cand_kernel<1><<<(int)((tot + 4 * kCandChunk - 1) / (4 * kCandChunk)), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags,
+                                                 far_points, th_far);
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once
