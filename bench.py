@@ -495,6 +495,20 @@ def aux_legs(dev, cpu):
 P_W, P_H, P_C, P_NF, P_INI, P_MIN, P_M, P_TH = 1920, 1080, 8, 2000, 20, 7, 8000, 3.0
 
 
+BYTES_FORMULA = {
+    "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image",
+    "fast_cells": "sum of level pixels read once, per image",
+    "octree": "8 B x 2,500 candidates, per image",
+    "blur": "sum of level pixels read + written, per image",
+    "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image",
+    "grid": "28 B per keypoint",
+    "frustum": "per map point 32 B in + 4 B out, per (point, camera) 17 B out",
+    "stereo_knn": "2 x 1,200 descriptors x 32 B per frame",
+    "proj_candidates": "per map point 32 B, per (point, camera) 17 B read + 68 B written",
+    "proj_resolve": "per map point 4 B + per (point, camera) 72 B (record, count, level) read",
+}
+
+
 def level_sizes(w, h, nlevels=NLEV, scale=SCALE):
     """Pyramid level sizes with the ORBextractor ctor's float arithmetic."""
     s = [1.0]
@@ -825,6 +839,8 @@ def main():
     ap.add_argument("--p1080-cpu-frames", type=int, default=2)
     ap.add_argument("--shard-frames", type=int, default=64, help="N>1: frames per step of the camera-sharded leg")
     ap.add_argument("--latency-frames", type=int, default=200, help="B=1 sequential frames timed (0: skip)")
+    ap.add_argument("--iso-reps", type=int, default=3,
+                    help="isolated single-stream passes of one group for the per-kernel roofline (0: skip)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -950,24 +966,34 @@ def main():
         gr["uright"] = torch.empty((Bg, NB, gr["cap"]), dtype=torch.float32, device=dev)
     timing_on = [False]
 
+    def group_step(gr, sync_frustum=False):
+        """One group's pass; sync_frustum: return isInFrustum's event time (synchronises that stream)."""
+        fb, st = gr["fb"], gr["stream"]
+        extract(gr)
+        with torch.cuda.stream(st):
+            fb.kp_to_mp.fill_(-1)                   # Frame ctor: mvpMapPoints = vector(N, nullptr)
+        gr["matcher"].AssignFeaturesToGrid(fb, stream=st)
+        gr["matcher"].StereoLapping(fb, 0.8, stream=st)
+        gr["matcher"].StereoTriangulate(fb, cams_r[:2], Rlr, tlr, sigma2, stream=st)
+        frame_uright(fb, gr["depth"], BF, stream=st, out=gr["uright"])
+        timed = timing_on[0] or sync_frustum
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+        isInFrustum(gr["poses"], rig, gr["world"], gr["mps"], 0.5, stream=st)   # Tracking::SearchLocalPoints
+        if timed:
+            e1.record(st)
+            if not sync_frustum:
+                gr["ev"].append((e0, e1))
+        gr["matcher"].SearchByProjection(fb, gr["mps"], TH, False, 50.0, stream=st, grid_ready=True)
+        if sync_frustum:
+            e1.synchronize()
+            return e0.elapsed_time(e1)
+        return 0.0
+
     def step():
         for gr in groups:
-            fb, st = gr["fb"], gr["stream"]
-            extract(gr)
-            with torch.cuda.stream(st):
-                fb.kp_to_mp.fill_(-1)                   # Frame ctor: mvpMapPoints = vector(N, nullptr)
-            gr["matcher"].AssignFeaturesToGrid(fb, stream=st)
-            gr["matcher"].StereoLapping(fb, 0.8, stream=st)
-            gr["matcher"].StereoTriangulate(fb, cams_r[:2], Rlr, tlr, sigma2, stream=st)
-            frame_uright(fb, gr["depth"], BF, stream=st, out=gr["uright"])
-            if timing_on[0]:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st)
-            isInFrustum(gr["poses"], rig, gr["world"], gr["mps"], 0.5, stream=st)   # Tracking::SearchLocalPoints
-            if timing_on[0]:
-                e1.record(st)
-                gr["ev"].append((e0, e1))
-            gr["matcher"].SearchByProjection(fb, gr["mps"], TH, False, 50.0, stream=st, grid_ready=True)
+            group_step(gr)
 
     for _ in range(args.warmup):
         step()
@@ -1005,6 +1031,29 @@ def main():
             gr["ex"].enable_timing(False)
             gr["matcher"].enable_timing(False)
 
+    # isolated per-stage device time: group 0's pipeline alone on its stream (no other group running), HIP events
+    # on that stream around each stage — the per-launch durations the roofline uses (rocprof's per-grid rows of
+    # the same launches agree; the overlapped stage times above include other streams' work)
+    iso = {}
+    if args.iso_reps > 0:
+        gr0 = groups[0]
+        for gr in groups:
+            gr["ex"].enable_timing(False)
+            gr["matcher"].enable_timing(False)
+        gr0["ex"].enable_timing(True)
+        gr0["matcher"].enable_timing(True)
+        gr0["ex"].stage_ms(reset=True)
+        gr0["matcher"].stage_ms(reset=True)
+        fr_ms = 0.0
+        for _ in range(args.iso_reps):
+            torch.cuda.synchronize(dev)
+            fr_ms += group_step(gr0, True)
+        torch.cuda.synchronize(dev)
+        es, calls = gr0["ex"].stage_ms(reset=True)
+        iso = {k: v / args.iso_reps for k, v in {**es, **gr0["matcher"].stage_ms(reset=True)}.items()}
+        iso["frustum"] = fr_ms / args.iso_reps
+        gr0["ex"].enable_timing(False)
+        gr0["matcher"].enable_timing(False)
     lat = latency_leg(d_img, groups[0], args.latency_frames, dev, rig, (Rlr, tlr, BF, sigma2, cams_r)) \
         if args.latency_frames > 0 and rank == 0 else None
     shard_leg = cam_shard_leg(s_imgs, args.shard_frames, 10, 2, dev, world, rank) \
@@ -1041,6 +1090,8 @@ def main():
         # describe (§8(d)): every level read once (patches overlap; the level is the unit of traffic) + the
         # 56-B keypoint record / descriptor written per keypoint
         "describe": B * C * sum(P) + n_kp_step * 56,
+        # GaussianBlur 7x7 of every level: level read, blurred level written
+        "blur": B * C * 2 * sum(P),
         "grid": n_kp_step * 28,
         # isInFrustum: per point pos/normal/min/max in, per (point, cam) proj x/y, cos, level, flag out
         "frustum": B * M_MPS * (32 + C * 17 + 4),
@@ -1048,27 +1099,44 @@ def main():
         # per point: descriptor 32 B; per (point, camera) slot: projection x / y / cos / level / in-view
         # 17 B read, the 64-B record + 4-B count written (window candidates' 60 B each not counted)
         "proj_candidates": B * M_MPS * (32 + C * (17 + 68)),
-        "proj_resolve": B * M_MPS * C * 32,
+        # per point its flag word, per (point, camera) the 64-B record + count + level (upper bound: only the
+        # in-view slots are read)
+        "proj_resolve": B * M_MPS * (4 + C * 72),
     }
     roof = None
-    if stages:
-        dom = max(stages, key=lambda k: stages[k])
-        launches = {"pyr_resize": NLEV - 1}.get(dom, 1) * G
-        avg_ms = stages[dom] / launches
-        achieved = per_step_bytes[dom] / launches / (avg_ms * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_step_bytes[dom] // launches,
-                "bytes_formula": "SURVEY 8(d): describe = sum of level pixels + 56 B per keypoint, per image"}
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
-        if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch's images
-            try:
-                rec = json.load(open(pmc))
-                if "hbm_bytes_per_image" in rec and dom in ("pyr_resize", "fast_cells", "octree", "describe"):
-                    roof["traffic"] = rec["hbm_bytes_per_image"] * Bg * C
-                    roof["traffic_source"] = f"profiles/pmc_{dom}.json ({rec['tag']}), per image x {Bg * C} images"
-            except Exception:
-                pass
+    kernels = {}
+    if iso:
+        # per stage: isolated duration of one launch (one group of Bg frames) vs its SURVEY 8(d) bytes
+        frames_pl = Bg
+        for k, ms in iso.items():
+            if k not in per_step_bytes or ms <= 0:
+                continue
+            alg = per_step_bytes[k] // G
+            ach = alg / (ms * 1e-3) / 1e9
+            rec = {"avg_launch_ms": round(ms, 4), "launches_per_step": G, "algorithmic_bytes_per_launch": int(alg),
+                   "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None}
+            pmc = os.path.join(ROOT, "profiles", f"pmc_{k}.json")
+            if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch
+                try:
+                    r = json.load(open(pmc))
+                    if "hbm_bytes_per_image" in r:
+                        rec["traffic"] = int(r["hbm_bytes_per_image"] * Bg * C)
+                    elif "hbm_bytes_per_frame" in r:
+                        rec["traffic"] = int(r["hbm_bytes_per_frame"] * Bg)
+                    if rec["traffic"] is not None:
+                        rec["traffic_source"] = f"profiles/pmc_{k}.json ({r['tag']}, program {r.get('program', 'orb')})"
+                except Exception:
+                    pass
+            kernels[k] = rec
+        dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+        d = kernels[dom]
+        roof = {"kernel": dom, "bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["frac"], "traffic": d["traffic"], "avg_launch_ms": d["avg_launch_ms"],
+                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"], "frames_per_launch": frames_pl,
+                "timing": "HIP events on the launch stream, group 0 alone (isolated passes after the timed steps)",
+                "bytes_formula": BYTES_FORMULA[dom]}
+        if d.get("traffic_source"):
+            roof["traffic_source"] = d["traffic_source"]
         # the whole path: SURVEY §8(d) bytes of a multi-camera frame (5 extractions + matching) x frames/s
         frame_bytes = C * cam_bytes(W, H, 0) + 56 * n_kp_step / B + 968_000
         roof["pipeline"] = {"bytes_per_frame": int(frame_bytes), "achieved": round(frame_bytes * value / 1e9, 2),
@@ -1090,6 +1158,9 @@ def main():
                                "stereo TriangulateMatches + mvuRight from depth + SearchByProjection(M=5000, th=6)",
                    "frames_per_step_per_gpu": B, "streams_per_gpu": G, "parallelism": f"frame-replicas x{world}"},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
+        "stage_ms_note": "stage_ms_per_step: HIP events per stream while the 3 groups overlap (includes other streams' "
+                         "kernels); kernels: isolated per-launch roofline of each stage",
+        "kernels": kernels,
         "matches_last_step": n_matches,
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -16,8 +16,13 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"pyr_resize": "pyr_resize", "fast_cells": "fast_cells", "octree": "octree", "describe": "describe",
-         "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs", "cand_kernel": "proj_candidates",
-         "resolve": "proj_resolve"}
+         "blur_kernel": "blur", "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
+         "stereo_tri_kernel": "stereo_tri", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
+         "frustum_kernel": "frustum", "uright_kernel": "uright", "err_kernel": "lba_err", "build_kernel": "lba_build",
+         "schur_kernel": "lba_schur", "ldlt_kernel": "lba_ldlt", "backsub_kernel": "lba_backsub",
+         "update_kf_kernel": "lba_update_kf", "finish_kernel": "lba_finish", "zero_kernel": "lba_zero"}
+# PMC programs (tools/profile_gpu.sh): units one launch covers
+PMC_SOURCES = {"orb": ("images", 160), "match": ("frames", 32), "lba": ("launches", 1)}
 
 
 def short(name):
@@ -27,7 +32,7 @@ def short(name):
     return name
 
 
-def main(src, tag, images_per_launch=None, command=None):
+def main(src, tag, command=None):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -40,32 +45,48 @@ def main(src, tag, images_per_launch=None, command=None):
         lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
                      f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
                      f"{float(r['MaxNs']) / 1e3:.1f} | {100 * float(r['TotalDurationNs']) / tot:.1f}% |")
+    # per (kernel, grid) from the dispatch trace: launches of one kernel at different batch sizes differ
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        by = defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            by[(short(r["Kernel_Name"]), "x".join(r.get(f"Grid_Size_{a}", "?") for a in "XYZ"))].append(
+                (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
+        lines += ["", "## Per kernel and grid size (dispatch trace)", "",
+                  "| kernel | grid (work-items) | calls | avg us | min us |", "|---|---|---|---|---|"]
+        for (k, g), v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+            if sum(v) < 50:   # skip sub-50-us totals
+                continue
+            lines.append(f"| {k} | {g} | {len(v)} | {sum(v) / len(v):.1f} | {min(v):.1f} |")
     pmc = defaultdict(lambda: defaultdict(list))
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        p = os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")
-        if not os.path.exists(p):
-            continue
-        for r in csv.DictReader(open(p)):
-            pmc[short(r["Kernel_Name"])][c].append(float(r["Counter_Value"]))
+    for srcname in PMC_SOURCES:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            p = os.path.join(src, f"pmc_{srcname}_{c}", "run_counter_collection.csv")
+            if not os.path.exists(p):
+                continue
+            for r in csv.DictReader(open(p)):
+                pmc[(srcname, short(r["Kernel_Name"]))][c].append(float(r["Counter_Value"]))
     lines += ["", "## HBM traffic per launch (separate --pmc passes; KB x 1024; FETCH doubled for gfx950)", "",
-              "| kernel | launches | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | corrected bytes/launch |",
-              "|---|---|---|---|---|"]
-    for k, d in sorted(pmc.items()):
+              "| program | kernel | launches | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | corrected bytes/launch | per unit |",
+              "|---|---|---|---|---|---|---|"]
+    for (srcname, k), d in sorted(pmc.items()):
         f = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
         w = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
         b = (2 * f + w) * 1024
-        lines.append(f"| {k} | {len(d['FETCH_SIZE'])} | {f:.1f} | {w:.1f} | {b:.0f} |")
+        unit, n = PMC_SOURCES[srcname]
+        lines.append(f"| {srcname} | {k} | {len(d['FETCH_SIZE'])} | {f:.1f} | {w:.1f} | {b:.0f} | "
+                     f"{b / n:.0f} B per {unit[:-1]} |")
         if k in SHORT.values():
-            rec = {"kernel": k, "tag": tag, "fetch_kb_per_launch": f, "write_kb_per_launch": w,
-                   "hbm_bytes_per_launch": round(b), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024"}
-            if images_per_launch:   # extraction kernels: one launch covers images_per_launch images
-                rec["images_per_launch"] = images_per_launch
-                rec["hbm_bytes_per_image"] = round(b / images_per_launch)
-            json.dump(rec, open(os.path.join(prof, f"pmc_{k}.json"), "w"), indent=1)
+            rec = {"kernel": k, "tag": tag, "program": srcname, "fetch_kb_per_launch": f, "write_kb_per_launch": w,
+                   "hbm_bytes_per_launch": round(b), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024",
+                   f"{unit}_per_launch": n, f"hbm_bytes_per_{unit[:-1]}": round(b / n)}
+            out = os.path.join(prof, f"pmc_{k}.json")
+            if srcname == "match" and os.path.exists(out) and json.load(open(out)).get("program") == "orb":
+                continue   # extraction kernels keep the extraction-only program's numbers
+            json.dump(rec, open(out, "w"), indent=1)
     open(os.path.join(prof, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01",
-         int(sys.argv[3]) if len(sys.argv) > 3 else None, sys.argv[4] if len(sys.argv) > 4 else None)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01", sys.argv[3] if len(sys.argv) > 3 else None)
