@@ -328,13 +328,15 @@ constexpr int kCandChunk = 192;
 template <int G>
 __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
                                                    const uint8_t *occ_init, Rec *recs, int *counts, int *flags,
-                                                   int far_points, float th_far) {
+                                                   int far_points, float th_far, int n_blocks) {
     constexpr int kChunk = kCandChunk / G;   // slots per wave: G lanes per active slot keep ~one pass per wave
     __shared__ int queue[4][kChunk];
     const int C = f.n_cams;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long total = (long long)n_frames * m.M * C;
-    const long long g0 = ((long long)blockIdx.x * 4 + wave) * kChunk;
+    const int blk = omv::xcd_block(n_blocks);   // consecutive slots (one frame's map points) on one XCD's L2
+    if (blk < 0) return;
+    const long long g0 = ((long long)blk * 4 + wave) * kChunk;
     const uint64_t lt = (1ull << lane) - 1ull;
     int nq = 0;
     for (int s0 = 0; s0 < kChunk; s0 += 64) {
@@ -1785,12 +1787,15 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
-        if (tot <= 262144)   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
-            cand_kernel<8><<<(int)((tot + 4 * (kCandChunk / 8) - 1) / (4 * (kCandChunk / 8))), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags,
-                                                 far_points, th_far);
-        else
-            cand_kernel<1><<<(int)((tot + 4 * kCandChunk - 1) / (4 * kCandChunk)), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags,
-                                                 far_points, th_far);
+        if (tot <= 262144) {   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
+            const int nb = (int)((tot + 4 * (kCandChunk / 8) - 1) / (4 * (kCandChunk / 8)));
+            cand_kernel<8><<<omv::xcd_grid(nb), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts,
+                                                              h->d_flags, far_points, th_far, nb);
+        } else {
+            const int nb = (int)((tot + 4 * kCandChunk - 1) / (4 * kCandChunk));
+            cand_kernel<1><<<omv::xcd_grid(nb), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts,
+                                                              h->d_flags, far_points, th_far, nb);
+        }
     }
     hipEvent_t e1 = h->timing ? mk_event(st) : nullptr;
     hipEvent_t e2 = h->timing ? mk_event(st) : nullptr;   // own start event: every event is destroyed once

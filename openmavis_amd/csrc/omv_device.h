@@ -233,4 +233,15 @@ __device__ inline float glibc_tanf(float x) {
     return glibc_kernel_tanf(y0, y1, 1 - ((n & 1) << 1));
 }
 
+// XCD-aware block order: the dispatcher deals workgroup b to XCD b % 8, so consecutive logical blocks
+// (neighbouring cells / keypoints / map points of one image or frame, which share bytes) are given to one XCD:
+// physical b runs logical (b % 8) * ceil(n / 8) + b / 8 and those bytes are fetched into one L2, not eight.
+// The grid is padded to a multiple of 8; returns -1 for a padding block.
+__device__ __forceinline__ int xcd_block(int n_logical) {
+    const int chunk = (n_logical + 7) >> 3;
+    const int b = (int)(blockIdx.x & 7) * chunk + (int)(blockIdx.x >> 3);
+    return b < n_logical ? b : -1;
+}
+__host__ inline int xcd_grid(int n_logical) { return (n_logical + 7) & ~7; }
+
 }  // namespace omv

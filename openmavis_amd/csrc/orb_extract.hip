@@ -184,16 +184,6 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     }
 }
 
-// XCD-aware block order: the dispatcher deals workgroup b to XCD b % 8, so consecutive logical blocks
-// (neighbouring cells / keypoints of one image, which share pixels) are given to one XCD: physical b runs
-// logical (b % 8) * ceil(n / 8) + b / 8 and the image's bytes are fetched into one L2, not eight.  The
-// grid is padded to a multiple of 8; returns -1 for a padding block.
-__device__ __forceinline__ int xcd_block(int n_logical) {
-    const int chunk = (n_logical + 7) >> 3;
-    const int b = (int)(blockIdx.x & 7) * chunk + (int)(blockIdx.x >> 3);
-    return b < n_logical ? b : -1;
-}
-__host__ inline int xcd_grid(int n_logical) { return (n_logical + 7) & ~7; }
 
 // K2 --------------------------------------------------------------------------------------------
 // FAST-9 strength: max over the 16 circular 9-arcs of min(d) (darker) and of min(-d) (brighter),
@@ -254,7 +244,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
                                                         int *cell_cnt, uint32_t *cell_kp, int rmax, int n_blocks) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int blk = xcd_block(n_blocks);
+    const int blk = omv::xcd_block(n_blocks);
     if (blk < 0) return;
     const int img = blk / g.n_cells;
     const int ci = blk - img * g.n_cells;
@@ -984,7 +974,7 @@ __device__ void blur_tile_bytes(const uint8_t *src, int sp, uint8_t *dst, int bp
 
 __global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_tiles) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int blk = xcd_block((n_tiles + 3) >> 2);
+    const int blk = omv::xcd_block((n_tiles + 3) >> 2);
     if (blk < 0) return;
     const int tile = __builtin_amdgcn_readfirstlane(blk * 4 + wave);   // wave-uniform: scalar address math
     if (tile >= n_tiles) return;
@@ -1030,7 +1020,7 @@ struct DescArgs {
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int blk = xcd_block(n_blocks);
+    const int blk = omv::xcd_block(n_blocks);
     if (blk < 0) return;
     const int slot = blk * 4 + wave;
     const int img = slot / g.out_per_img;
@@ -1480,7 +1470,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    fast_cells_kernel<<<xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
+    fast_cells_kernel<<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
                                                                o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
     mark(o, st);
     // K3: octree per (image, level)
@@ -1489,13 +1479,13 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K4: blurred pyramid, one wavefront per 32 x 256 tile
     const int blur_tiles = g.blur_tile_off[g.nlevels] * n;
-    blur_kernel<<<xcd_grid((blur_tiles + 3) / 4), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
+    blur_kernel<<<omv::xcd_grid((blur_tiles + 3) / 4), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
                                                                blur_tiles);
     mark(o, st);
     // K5: orientation + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_blur, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
     const int waves = g.out_per_img * n;
-    describe_kernel<<<xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
+    describe_kernel<<<omv::xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
     HIP_OK(hipGetLastError());
     return OMV_OK;

@@ -27,6 +27,18 @@ def lib():
     return _lib
 
 
+def use_library(path):
+    """Switch the restatement library (the contraction study loads oracle/liboracle_fma.so)."""
+    global _lib
+    _lib = ctypes.CDLL(path)
+    return _lib
+
+
+def set_contract(mode):
+    """0: no contraction (parity mode); 1: GCC's contraction of the reference's own steering products."""
+    lib().oracle_set_contract(int(mode))
+
+
 class _Ptr(ctypes.c_void_p):
     """A c_void_p that keeps its array alive for the duration of the call it is passed to (a temporary
     like `_p(x.copy())` would otherwise be freed before the C function reads it)."""

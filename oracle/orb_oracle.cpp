@@ -340,6 +340,15 @@ static void gauss7_u8(const Img &src, Img &dst) {
         }
 }
 
+// Floating-point contraction study (tools/fma_study.py): 0 = none (the parity mode: every restated float path
+// rounds each operation, as the device does); 1 = the contraction GCC applies to the reference's own
+// translation unit when built with its flags (-O3 -march=native on an FMA machine, CMakeLists.txt:12-15): the
+// steering products of GET_VALUE (ORBextractor.cc:56-57) fused as GCC's convert_mult_to_fma does (the first
+// product of `a*b + c*d` / `a*b - c*d` becomes the FMA, the second is rounded).  OpenCV's own code (fastAtan2,
+// resize, FAST, GaussianBlur) keeps mode 0: its contraction depends on how OpenCV was built (unpinned).
+static int g_contract = 0;
+extern "C" void oracle_set_contract(int mode) { g_contract = mode; }
+
 // ---- steered BRIEF (ORBextractor.cc:46-90) ---------------------------------------------------------
 static void rbrief(const Img &blur, const KP &k, uint8_t *desc) {
     const float rad = k.angle * (float)(M_PI / 180.f);
@@ -347,8 +356,14 @@ static void rbrief(const Img &blur, const KP &k, uint8_t *desc) {
     const int cy = round_even(k.y), cx = round_even(k.x);
     auto sample = [&](int idx) {
         const int px = kPattern[2 * idx], py = kPattern[2 * idx + 1];
-        const int dy = round_even((float)px * b + (float)py * a);
-        const int dx = round_even((float)px * a - (float)py * b);
+        int dy, dx;
+        if (g_contract == 1) {
+            dy = round_even(std::fma((float)px, b, (float)py * a));
+            dx = round_even(std::fma((float)px, a, -((float)py * b)));
+        } else {
+            dy = round_even((float)px * b + (float)py * a);
+            dx = round_even((float)px * a - (float)py * b);
+        }
         return (int)blur.at(cy + dy, cx + dx);
     };
     for (int byte = 0; byte < 32; ++byte) {
