@@ -271,14 +271,18 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
         res, _ = ba.optimize(**LBA_CFG)
         total += time.perf_counter() - t0
         trials += res["trials"]
-        for k, v in ba.stage_ms().items():
-            st_sum[k] = st_sum.get(k, 0) + v
     torch.cuda.synchronize(dev)
     dt = job_seconds(total, dev)
+    # per-stage device times: one extra optimize() with direct launches and events (the timed loop runs the
+    # captured LM step, which carries no per-stage events)
+    ba.enable_timing(True)
+    ba.reset().optimize(**LBA_CFG)
+    st_sum = {k: v for k, v in ba.stage_ms().items()}
+    ba.enable_timing(False)
     trial_ms = dt / trials * 1e3
     bpt = lba_bytes_per_trial(prob)
     achieved = bpt / (trial_ms * 1e-3) / 1e9
-    stages = {k: round(v / trials, 4) for k, v in st_sum.items() if k != "trials"}
+    stages = {k: round(v / max(st_sum.get("trials", 1), 1), 4) for k, v in st_sum.items() if k != "trials"}
     return {
         "metric": "LocalBA iters/sec (LM trials/s)",
         "value": round(trials * (1 if shard else world) / dt, 2),

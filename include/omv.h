@@ -422,8 +422,14 @@ omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stere
 /* Restore the state uploaded by the last set_problem (device-side copy; for re-runs and benchmarks). */
 omv_status omv_lba_reset(omv_lba *h);
 /* Per-stage device time of the last optimize: 0 linearise+build, 1 Schur, 2 reduced solve,
- * 3 back-substitution+update+errors; plus the number of trials. */
+ * 3 back-substitution+update+errors; plus the number of trials.  On one rank the stages are timed only
+ * with omv_lba_enable_timing(h, 1) (direct launches with events instead of the captured LM step). */
 omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials);
+omv_status omv_lba_enable_timing(omv_lba *h, int on);
+/* LM driver on one rank: 0 (default) keeps g2o's accept / reject / lambda / stop logic on the device (one
+ * captured hipGraph per trial, one read-back per optimize); 1 runs it on the host with a read-back per trial
+ * (the driver the sharded solve uses).  Both make the same decisions (tests/test_lba_gpu.py). */
+omv_status omv_lba_set_driver(omv_lba *h, int host_driven);
 
 /* Landmark sharding across ranks: one exchange per LM trial.
  * Call before omv_lba_set_problem.  Every rank then passes the SAME full problem; the handle keeps

@@ -228,6 +228,8 @@ SIGNATURES = {
     "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "omv_lba_evaluate_stereo": (_I, [_VP, _VP, _VP, _VP]),
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
+    "omv_lba_enable_timing": (_I, [_VP, _I]),
+    "omv_lba_set_driver": (_I, [_VP, _I]),
     "omv_lba_reset": (_I, [_VP]),
     "omv_lba_set_comm": (_I, [_VP, _I, _I, _VP, _VP]),
     "omv_tri_debug": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _F, _F, _VP]),

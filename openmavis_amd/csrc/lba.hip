@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -56,6 +58,28 @@ constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / bac
 
 
 
+
+// Device-resident Levenberg-Marquardt control (optimization_algorithm_levenberg.cpp:61-169), for the
+// single-rank path: the accept / reject decision, the lambda schedule and the iteration / stop logic run in
+// finish_trial_kernel, so one LM trial is a fixed kernel sequence (captured once as a hipGraph) whose kernels
+// read lambda and their gate from here, and the host reads the outcome back once per optimize().
+struct LmCtl {
+    double lambda, ni, currentChi, iniChi, errors_chi, err0, rho, lambda_init;
+    int it, qmax, nBad, trials, its, opt_it, max_trials;
+    int done;                // the optimisation has ended
+    int errors_of_current;   // the last computed errors belong to the current state (A)
+    int need_build;          // the next step starts a new iteration (buildSystem)
+    int accepted;            // the last trial was accepted: the trial state B becomes A
+    int g_active, g_errA, g_build;   // gates of the next step (set by ctl_init / finish_trial)
+};
+enum { kGateAlways = 0, kGateErrA = 1, kGateBuild = 2, kGateTrial = 3 };
+__device__ __forceinline__ bool gate_open(const LmCtl *c, int g) {
+    if (!c || g == kGateAlways) return true;
+    if (g == kGateErrA) return c->g_errA != 0;
+    if (g == kGateBuild) return c->g_build != 0;
+    return c->g_active != 0;
+}
+__device__ __forceinline__ double lm_lambda(const LmCtl *c, double lambda) { return c ? c->lambda : lambda; }
 
 __device__ __forceinline__ void mono_err_block(int blk, double *sh, Rig rig, State s, Edges E, double delta,
                                                double dsqr, double delta_st, double dsqr_st, double *err,
@@ -131,12 +155,127 @@ __device__ __forceinline__ void imu_err_block(double *sh, State s, Imu I, double
 __global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s, Edges E, double delta,
                                                   double dsqr, double delta_st, double dsqr_st, double *err, double *err3,
                                                   double *chi2, double *partial, Imu I, double delta_imu,
-                                                  double dsqr_imu, double *err9, double *imu_partial) {
+                                                  double dsqr_imu, double *err9, double *imu_partial, const LmCtl *ctl,
+                                                  int gate) {
     __shared__ double sh[8];
+    if (!gate_open(ctl, gate)) return;
     if ((int)blockIdx.x < n_mono_blocks)
         mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, partial);
     else if (has_imu)
         imu_err_block(sh, s, I, delta_imu, dsqr_imu, err9, imu_partial);
+}
+
+// activeRobustChi2: inertial partial + visual partials in a fixed order (one block of 256).
+__device__ __forceinline__ double sum_chi(const double *mono_partial, int n_mono_blocks, const double *imu_partial,
+                                          double *sh) {
+    double v = 0;
+    for (int i = threadIdx.x; i < n_mono_blocks; i += blockDim.x) v += mono_partial[i];
+    const double t = block_reduce_sum(v, sh);
+    return imu_partial[0] + t;
+}
+
+// The next step's gates from the LM state: a trial runs unless the optimisation ended; it starts a new
+// iteration (buildSystem) after an iteration ended, and first recomputes the current state's errors when the
+// last computed errors were a rejected trial's.
+__device__ __forceinline__ void set_gates(LmCtl *c) {
+    c->g_active = !c->done;
+    c->g_build = !c->done && c->need_build;
+    c->g_errA = c->g_build && !c->errors_of_current;
+}
+
+// optimize()'s start: err = activeRobustChi2 of the initial state (Optimizer.cc:3273-3274), LM state reset
+// (iteration 0's lambda = lambda_init, ni = 2, nBad = 0, optimization_algorithm_levenberg.cpp:103-108).
+__global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
+                                                       const double *imu_partial, int opt_it, int max_trials,
+                                                       double lambda_init) {
+    __shared__ double sh[8];
+    const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
+    if (threadIdx.x == 0) {
+        c->err0 = c->errors_chi = chi;
+        c->errors_of_current = 1;
+        c->need_build = 1;
+        c->it = c->qmax = c->nBad = c->trials = c->its = 0;
+        c->opt_it = opt_it, c->max_trials = max_trials, c->lambda_init = lambda_init;
+        c->lambda = lambda_init, c->ni = 2, c->rho = 0, c->accepted = 0;
+        c->done = opt_it <= 0;
+        set_gates(c);
+    }
+}
+
+// One step's LM bookkeeping (optimization_algorithm_levenberg.cpp:61-169), after the trial's errors:
+//   a step that started an iteration: ++its, currentChi = iniChi = activeRobustChi2 of the current state (its
+//   errors recomputed this step when the last ones were a rejected trial's), qmax = 0;
+//   the trial: rho, accept (the trial state becomes current) or reject (lambda *= ni), then the do-while /
+//   iteration / nBad stop tests in the reference's order, and the next step's gates.
+__global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
+                                                           const double *imu_partial, const double *mono_partial_a,
+                                                           const double *imu_partial_a, const double *scale_partial,
+                                                           int n_scale, const int *fail) {
+    __shared__ double sh[8];
+    if (!c->g_active) return;
+    const bool errA = c->g_errA != 0;
+    double chiA = 0;
+    if (errA) {
+        chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
+        __syncthreads();
+    }
+    const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
+    double sc = 0;
+    for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
+    __syncthreads();
+    const double ssum = block_reduce_sum(sc, sh);
+    if (threadIdx.x != 0) return;
+    if (c->g_build) {   // iteration start
+        ++c->its;
+        if (errA) c->errors_chi = chiA, c->errors_of_current = 1;
+        c->currentChi = c->iniChi = c->errors_chi;
+        c->qmax = 0;
+    }
+    const bool ok = *fail == 0;
+    double tempChi = chi;
+    c->errors_chi = chi;
+    c->errors_of_current = 0;   // the last computed errors belong to the trial state
+    if (!ok) tempChi = DBL_MAX;
+    double scale = ok ? ssum : 0.0;
+    scale += 1e-3;
+    const double rho = (c->currentChi - tempChi) / scale;
+    c->rho = rho;
+    ++c->trials;
+    c->accepted = 0;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3.0);
+        alpha = fmin(alpha, 2. / 3.);
+        c->lambda *= fmax(1. / 3., alpha);
+        c->ni = 2;
+        c->currentChi = tempChi;
+        c->accepted = 1;
+        c->errors_of_current = 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+    }
+    ++c->qmax;
+    if (rho < 0 && c->qmax < c->max_trials) {
+        c->need_build = 0;   // another trial of this iteration
+    } else {
+        c->need_build = 1;
+        if (c->qmax == c->max_trials || rho == 0) {
+            c->done = 1;
+        } else {
+            if ((c->iniChi - c->currentChi) * 1e3 < c->iniChi) ++c->nBad;
+            else c->nBad = 0;
+            if (c->nBad >= 3) c->done = 1;
+        }
+        if (++c->it >= c->opt_it) c->done = 1;
+    }
+    set_gates(c);
+}
+
+// An accepted trial's state B becomes the current state A (one contiguous copy of the state block; after the
+// optimisation ended the flag of its last trial stays set and the copy repeats idempotently).
+__global__ void accept_copy_kernel(const LmCtl *c, const double *B, double *A, size_t n) {
+    if (!c->accepted) return;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (size_t)gridDim.x * blockDim.x) A[q] = B[q];
 }
 
 // Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
@@ -372,8 +511,10 @@ constexpr int kBuildLds = kSpan * 42 > 441 ? kSpan * 42 : 441;
 __global__ void __launch_bounds__(kLandWG) build_kernel(int n_land, Rig rig, State s, Edges E, Land L, Red R,
                                                         double delta, double dsqr, double delta_st, double dsqr_st,
                                                         const double *err, const double *err3, const double *chi2,
-                                                        Imu I, double delta_imu, double dsqr_imu, const double *err9) {
+                                                        Imu I, double delta_imu, double dsqr_imu, const double *err9,
+                                                        const LmCtl *ctl) {
     __shared__ double sm[kBuildLds];
+    if (!gate_open(ctl, kGateBuild)) return;
     if ((int)blockIdx.x < n_land)
         build_land_block(blockIdx.x, sm, rig, s, E, L, R, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
     else
@@ -381,7 +522,8 @@ __global__ void __launch_bounds__(kLandWG) build_kernel(int n_land, Rig rig, Sta
 }
 
 // H = 0, b = 0 before a build (one launch instead of two fills)
-__global__ void zero_kernel(double *H, size_t nH, double *b, int nb) {
+__global__ void zero_kernel(double *H, size_t nH, double *b, int nb, const LmCtl *ctl) {
+    if (!gate_open(ctl, kGateBuild)) return;
     const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q < nH) H[q] = 0.0;
     if (q < (size_t)nb) b[q] = 0.0;
@@ -401,7 +543,10 @@ struct BlockPat {
     const int4 *pair;                // (slot(i,j), slot(i,k), slot(j,k), 0)
 };
 
-__global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, double *Sp, double *coef) {
+__global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, double *Sp, double *coef,
+                            const LmCtl *ctl) {
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q < n) coef[q] = 0;
     if (q >= P.n_slots * 256) return;
@@ -410,8 +555,11 @@ __global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, d
     Sp[q] = gc <= gr ? H[(size_t)gr * n + gc] + (gr == gc ? lambda : 0.0) : 0.0;
 }
 
-__global__ void __launch_bounds__(kLandWG) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef) {
+__global__ void __launch_bounds__(kLandWG) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef,
+                                                        const LmCtl *ctl) {
     __shared__ double acc[kSpan * kSpan * 36 / 2 + kSpan * 36 / 2 + kSpan * 6];   // lower block triangle + coef
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
     // block (a, b), a >= b, stored at ((a * (a + 1)) / 2 + b) * 36
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int kf0 = L.wg_kf0[blockIdx.x];
@@ -617,9 +765,10 @@ constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (th
 template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
 __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat P, const double *b,
                                                             const double *coef, double *x, double *gscratch,
-                                                            int *fail) {
+                                                            int *fail, const LmCtl *ctl) {
     extern __shared__ __attribute__((aligned(16))) double lsm[];
     __shared__ int bad;
+    if (!gate_open(ctl, kGateTrial)) return;
     const int nb = P.nb, nv = 16 * nb;
     double *pk = G ? gscratch : lsm;
     double *y = pk + (size_t)P.n_slots * 256;
@@ -741,8 +890,10 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 
 // ---- trial: back-substitution + updates + scale ----------------------------------------------------
 __global__ void __launch_bounds__(kLandWG) backsub_kernel(Land L, Red R, double lambda, const double *xp, State a, State bst,
-                                                      double *scale_partial) {
+                                                      double *scale_partial, const LmCtl *ctl) {
     __shared__ double sh[8];
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     double sc = 0;
     if (p < L.n) {
@@ -773,8 +924,11 @@ __global__ void __launch_bounds__(kLandWG) backsub_kernel(Land L, Red R, double 
 
 // ImuCamPose::Update (G2oTypes.cc:211-235) + vertex adds; the pose part of computeScale.
 __global__ void update_kf_kernel(Rig rig, Red R, const double *b, const int *offV, const int *offG, const int *offA,
-                                 int n_opt, double lambda, const double *xp, State a, State bst, double *scale_partial) {
+                                 int n_opt, double lambda, const double *xp, State a, State bst, double *scale_partial,
+                                 const LmCtl *ctl) {
     __shared__ double sh[8];
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
     const int C = rig.n_cams;
     for (int k = threadIdx.x; k < n_opt; k += blockDim.x) {
         const double *u = xp + R.offP[k];
@@ -927,7 +1081,14 @@ struct omv_lba {
     int *d_offP = nullptr, *d_offV = nullptr, *d_offG = nullptr, *d_offA = nullptr;
     double *d_err = nullptr, *d_chi2 = nullptr, *d_err9 = nullptr;
     double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
+    double *d_partial_a = nullptr, *d_imu_partial_a = nullptr;   // the current state's errors recomputed in a step
     double *h_out = nullptr;   // pinned host copy of d_out: the per-trial 24-byte read-back
+    LmCtl *d_ctl = nullptr;    // device-resident LM control (single-rank path)
+    LmCtl *h_ctl = nullptr;    // pinned copy: the one read-back per optimize()
+    hipGraph_t step_graph = nullptr;
+    hipGraphExec_t step_exec = nullptr;   // one LM step (trial, and buildSystem when an iteration starts)
+    bool timing = false;       // direct launches with per-stage events instead of the captured step
+    bool host_lm = false;      // force the host-driven LM loop (parity checks of the device control)
     double *d_S = nullptr, *d_coef = nullptr, *d_x = nullptr, *d_scratch = nullptr;
     int *d_fail = nullptr;
     double *d_bb = nullptr;    // the trial's copy of b (all-reduced with the packed system when sharded)
@@ -954,6 +1115,9 @@ struct omv_lba {
 static void free_problem(omv_lba *h) {
     for (void *p : h->owned) (void)hipFree(p);
     h->owned.clear();
+    if (h->step_exec) (void)hipGraphExecDestroy(h->step_exec);
+    if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
+    h->step_exec = nullptr, h->step_graph = nullptr;   // the captured step holds the old problem's pointers
 }
 
 extern "C" {
@@ -968,6 +1132,8 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     for (auto &e : h->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipHostMalloc((void **)&h->h_out, 4 * sizeof(double), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void **)&h->h_ctl, sizeof(LmCtl), hipHostMallocDefault));
+    HIP_OK(hipMalloc((void **)&h->d_ctl, sizeof(LmCtl)));
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
     h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdltLds) == hipSuccess;
@@ -982,6 +1148,10 @@ omv_status omv_lba_destroy(omv_lba *h) {
     for (auto &e : h->ev) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->h_out) (void)hipHostFree(h->h_out);
+    if (h->h_ctl) (void)hipHostFree(h->h_ctl);
+    if (h->d_ctl) (void)hipFree(h->d_ctl);
+    if (h->step_exec) (void)hipGraphExecDestroy(h->step_exec);
+    if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
     delete h;
     return OMV_OK;
 }
@@ -1271,6 +1441,8 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_err9 = dalloc<double>(ow, 10 * (size_t)NI);
     h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
     h->d_imu_partial = dalloc<double>(ow, 1);
+    h->d_partial_a = dalloc<double>(ow, std::max(1, h->n_wg_edge));
+    h->d_imu_partial_a = dalloc<double>(ow, 1);
     h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
     h->d_out = dalloc<double>(ow, 4);
     // [packed blocks | b | coef]: contiguous, the one buffer a sharded solve all-reduces per trial
@@ -1283,6 +1455,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_fail = dalloc<int>(ow, 1);
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
+    HIP_OK(hipMemset(h->d_imu_partial_a, 0, sizeof(double)));
     return OMV_OK;
 }
 
@@ -1290,13 +1463,16 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 
 // ---- the LM driver ---------------------------------------------------------------------------------
 // computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
-static omv_status lba_errors(omv_lba *h, const State &s) {
+static omv_status lba_errors(omv_lba *h, const State &s, const LmCtl *ctl = nullptr, int gate = kGateAlways,
+                             bool partial_a = false) {
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
     const int blocks = nmb + (h->imu_here ? 1 : 0);
     if (blocks > 0)
         err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s, h->E, h->delta_mono, h->dsqr_mono,
-                                                  h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, h->d_partial,
-                                                  h->I, h->delta_imu, h->dsqr_imu, h->d_err9, h->d_imu_partial);
+                                                  h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2,
+                                                  partial_a ? h->d_partial_a : h->d_partial, h->I, h->delta_imu,
+                                                  h->dsqr_imu, h->d_err9, partial_a ? h->d_imu_partial_a : h->d_imu_partial,
+                                                  ctl, gate);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
@@ -1380,6 +1556,122 @@ omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stere
     return lba_eval(h, nullptr, nullptr, nullptr, nullptr, stereo_err, stereo_jx, stereo_jp);
 }
 
+static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res);
+
+// One LM step of the single-rank path: the gated kernel sequence (see LmCtl).  A = st[0] is always the
+// current state and B = st[1] the trial; an accepted trial is copied back into A on the device.  With `ev`,
+// events bracket the stages (build, Schur, solve, update + errors) for omv_lba_stage_ms.
+static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
+    hipStream_t st = h->stream;
+    LmCtl *c = h->d_ctl;
+    const int nred = h->n_red, gl = std::max(1, h->n_wg_land);
+    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
+    State &A = h->st[0], &B = h->st[1];
+    omv_status rs;
+    if ((rs = lba_errors(h, A, c, kGateErrA, true)) != OMV_OK) return rs;   // after a rejected trial
+    if (ev) HIP_OK(hipEventRecord(ev[0], st));
+    {
+        const size_t nH = (size_t)nred * nred;
+        zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, c);
+        const int nl = h->n_pts > 0 ? gl : 0, ni_blk = h->imu_here ? h->n_imu : 0;
+        if (nl + ni_blk > 0)
+            build_kernel<<<nl + ni_blk, kLandWG, 0, st>>>(nl, h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono,
+                                                          h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, h->I,
+                                                          h->delta_imu, h->dsqr_imu, h->d_err9, c);
+    }
+    if (ev) HIP_OK(hipEventRecord(ev[1], st));
+    const int npk = std::max(h->BP.n_slots * 256, nred);
+    pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, 0.0, h->d_S, h->d_coef, c);
+    if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, 0.0, h->d_S, h->d_coef, c);
+    if (ev) HIP_OK(hipEventRecord(ev[2], st));
+    if (h->use_lds)
+        ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
+                                                                 h->d_fail, c);
+    else
+        ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch, h->d_fail,
+                                                      c);
+    if (ev) HIP_OK(hipEventRecord(ev[3], st));
+    update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, h->R.b, h->d_offV, h->d_offG, h->d_offA, h->n_opt, 0.0, h->d_x, A, B,
+                                        h->d_scale_partial, c);
+    if (h->n_pts > 0) backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, 0.0, h->d_x, A, B, h->d_scale_partial + 1, c);
+    if ((rs = lba_errors(h, B, c, kGateTrial)) != OMV_OK) return rs;
+    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a, h->d_imu_partial_a,
+                                           h->d_scale_partial, h->n_pts > 0 ? gl + 1 : 1, h->d_fail);
+    accept_copy_kernel<<<256, 256, 0, st>>>(c, B.Rwb, A.Rwb, h->state_doubles());
+    if (ev) HIP_OK(hipEventRecord(ev[4], st));
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+// optimize() on one rank with the LM control on the device: the initial errors, then LM steps in batches
+// (opt_it first: every iteration takes at least one trial) until the device reports the end; one read-back
+// per batch.  Identical decisions to the host-driven loop below (which the sharded solve keeps, its per-trial
+// all-reduce being a host call).
+static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba_result *res) {
+    hipStream_t st = h->stream;
+    if (h->cur != 0) {   // the device path keeps the current state in st[0]
+        HIP_OK(hipMemcpyAsync(h->st[0].Rwb, h->st[1].Rwb, h->state_doubles() * sizeof(double), hipMemcpyDeviceToDevice,
+                              st));
+        h->cur = 0;
+    }
+    omv_status rs;
+    if ((rs = lba_errors(h, h->st[0])) != OMV_OK) return rs;
+    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
+    ctl_init_kernel<<<1, 256, 0, st>>>(h->d_ctl, h->d_partial, nmb, h->d_imu_partial, o->opt_it, o->max_trials,
+                                       o->lambda_init);
+    HIP_OK(hipGetLastError());
+    if (!h->timing && !h->step_exec) {   // capture one step (the problem's pointers are fixed until set_problem)
+        HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        rs = lba_step(h, nullptr);
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(st, &g);
+        if (rs != OMV_OK) return rs;
+        if (ce != hipSuccess) {
+            fprintf(stderr, "omv: LM step capture failed: %s\n", hipGetErrorString(ce));
+            return OMV_ERR_HIP;
+        }
+        h->step_graph = g;
+        HIP_OK(hipGraphInstantiate(&h->step_exec, g, nullptr, nullptr, 0));
+    }
+    const int max_steps = std::max(0, o->opt_it) * std::max(1, o->max_trials);
+    std::vector<std::array<hipEvent_t, 5>> evs;
+    int launched = 0, batch = std::min(std::max(0, o->opt_it), max_steps);
+    while (true) {
+        for (int i = 0; i < batch; ++i) {
+            if (h->timing) {
+                std::array<hipEvent_t, 5> e{};
+                for (auto &x : e) HIP_OK(hipEventCreate(&x));
+                evs.push_back(e);
+                if ((rs = lba_step(h, evs.back().data())) != OMV_OK) return rs;
+            } else {
+                HIP_OK(hipGraphLaunch(h->step_exec, st));
+            }
+        }
+        launched += batch;
+        HIP_OK(hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (h->h_ctl->done || launched >= max_steps) break;
+        batch = std::min(4, max_steps - launched);
+    }
+    const LmCtl &c = *h->h_ctl;
+    for (double &m : h->stage_ms) m = 0;
+    for (auto &e : evs) {
+        float ms;
+        for (int k = 0; k < 4; ++k) {
+            HIP_OK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+            h->stage_ms[k] += ms;
+        }
+        for (auto &x : e) (void)hipEventDestroy(x);
+    }
+    h->last_trials = c.trials;
+    res->err = (float)c.err0;
+    res->err_end = (float)c.errors_chi;
+    res->iterations = c.its;
+    res->trials = c.trials;
+    res->lambda = c.lambda;
+    return OMV_OK;
+}
+
 omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
     if (!h || !o || !p || !res) return OMV_ERR_ARG;
     hipStream_t st = h->stream;
@@ -1387,6 +1679,10 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     double sc[3];
     omv_status rs;
     for (double &m : h->stage_ms) m = 0;
+    if (h->world == 1 && !h->host_lm) {
+        if ((rs = lba_optimize_device(h, o, res)) != OMV_OK) return rs;
+        return lba_finish_result(h, o, p, res);
+    }
     // err = activeRobustChi2 at the initial state (Optimizer.cc:3273-3274)
     if ((rs = lba_errors(h, h->st[h->cur])) != OMV_OK) return rs;
     if ((rs = lba_read_scalars(h, 0, sc, false)) != OMV_OK) return rs;
@@ -1412,13 +1708,13 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         HIP_OK(hipEventRecord(h->ev[0], st));
         {
             const size_t nH = (size_t)nred * nred;
-            zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred);
+            zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, nullptr);
             const int nl = h->n_pts > 0 ? gl : 0, ni_blk = h->imu_here ? h->n_imu : 0;
             if (nl + ni_blk > 0)
                 build_kernel<<<nl + ni_blk, kLandWG, 0, st>>>(nl, h->rig, A, h->E, h->L, h->R, h->delta_mono,
                                                               h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err,
                                                               h->d_err3, h->d_chi2, h->I, h->delta_imu, h->dsqr_imu,
-                                                              h->d_err9);
+                                                              h->d_err9, nullptr);
         }
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
@@ -1436,8 +1732,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             const int npk = std::max(h->BP.n_slots * 256, nred);
             // lambda on the pose diagonal once (rank 0 of a sharded solve)
             pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, h->rank == 0 ? lambda : 0.0, h->d_S,
-                                                           h->d_coef);
-            if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef);
+                                                           h->d_coef, nullptr);
+            if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef, nullptr);
             const double *bsys = h->R.b;
             if (h->world > 1) {   // one exchange: sum the partial Schur systems of the landmark shards
                 HIP_OK(hipMemcpyAsync(h->d_bb, h->R.b, sizeof(double) * nred, hipMemcpyDeviceToDevice, st));
@@ -1447,17 +1743,17 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             HIP_OK(hipEventRecord(h->ev[3], st));
             if (h->use_lds)
                 ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x,
-                                                                         h->d_scratch, h->d_fail);
+                                                                         h->d_scratch, h->d_fail, nullptr);
             else
                 ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x, h->d_scratch,
-                                                              h->d_fail);
+                                                              h->d_fail, nullptr);
             HIP_OK(hipEventRecord(h->ev[4], st));
             // landmark back-substitution, then the keyframe update; both feed the trial's errors (one stream:
             // a side stream's fork / join cost more than the ~10 us update)
             update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, bsys, h->d_offV, h->d_offG, h->d_offA, h->n_opt,
-                                                     lambda, h->d_x, A, B, h->d_scale_partial);
+                                                     lambda, h->d_x, A, B, h->d_scale_partial, nullptr);
             if (h->n_pts > 0)
-                backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1);
+                backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1, nullptr);
             if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
             if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc, true)) != OMV_OK) return rs;
             const int fail = sc[2] != 0.0;
@@ -1509,6 +1805,13 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     res->iterations = its;
     res->trials = trials;
     res->lambda = lambda;
+    return lba_finish_result(h, o, p, res);
+}
+
+// The epilogue shared by both LM drivers: state write-back in the caller's order, per-edge chi2 and the
+// reference's outlier / FAIL tests (Optimizer.cc:3282-3321).
+static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
+    hipStream_t st = h->stream;
     // write back the state (caller order)
     const State &s = h->st[h->cur];
     const int K = h->n_kf, C = h->rig.n_cams, P = h->n_pts, E = h->n_mono;
@@ -1572,6 +1875,18 @@ omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *p
     if (n_pts) *n_pts = h->n_pts;
     if (n_mono) *n_mono = h->n_mono;
     if (pt_index) std::copy(h->perm_pt.begin(), h->perm_pt.end(), pt_index);
+    return OMV_OK;
+}
+
+omv_status omv_lba_enable_timing(omv_lba *h, int on) {
+    if (!h) return OMV_ERR_ARG;
+    h->timing = on != 0;
+    return OMV_OK;
+}
+
+omv_status omv_lba_set_driver(omv_lba *h, int host_driven) {
+    if (!h) return OMV_ERR_ARG;
+    h->host_lm = host_driven != 0;
     return OMV_OK;
 }
 

@@ -116,6 +116,16 @@ class LocalInertialBA:
         _lib.check(self._lib.omv_lba_shard(self._h, None, None, _lib.ptr(idx)), "omv_lba_shard")
         return idx, n_e.value
 
+    def enable_timing(self, on=True):
+        """Per-stage events on the next optimize() calls (direct launches instead of the captured LM step)."""
+        _lib.check(self._lib.omv_lba_enable_timing(self._h, int(bool(on))), "omv_lba_enable_timing")
+        return self
+
+    def set_driver(self, host_driven):
+        """True: g2o's LM decisions on the host (read-back per trial); False (default): on the device."""
+        _lib.check(self._lib.omv_lba_set_driver(self._h, int(bool(host_driven))), "omv_lba_set_driver")
+        return self
+
     def stage_ms(self):
         """Device ms of the last optimize: build, schur, solve, update+errors; and the trial count."""
         ms = np.zeros(4)

@@ -173,6 +173,27 @@ def test_optimize_full_window(full, oracle):
     assert t["trials"] == rg["trials"]
 
 
+@pytest.mark.parametrize("large", [True, False])
+def test_device_lm_driver_matches_host_driver(small, oracle, large):
+    """The device-resident LM control (one captured hipGraph per trial, one read-back per optimize) makes the
+    host loop's decisions: same iterations / trials / status, err / err_end and state at the parity bar; the
+    per-stage timing mode (direct launches) as well."""
+    kw = dict(opt_it=10 if not large else 4, lambda_init=1e0 if not large else 1e-2, max_trials=10, large=large)
+    ba = _solver(small).set_problem(small)
+    rh, sh = ba.set_driver(True).optimize(**kw)
+    rd, sd = ba.set_problem(small).set_driver(False).optimize(**kw)
+    rt, st = ba.set_problem(small).enable_timing(True).optimize(**kw)
+    ro, so, _ = oracle.lba_optimize(small, **kw)
+    for r, s in ((rd, sd), (rt, st)):
+        assert (r["iterations"], r["trials"], r["status"]) == (rh["iterations"], rh["trials"], rh["status"])
+        for k in ("err", "err_end"):
+            assert abs(r[k] - rh[k]) <= 1e-6 * abs(rh[k]), (k, r[k], rh[k])
+        _compare_result(small, r, ro)
+        _compare_state(small, s, so, oracle)
+    t = ba.stage_ms()
+    assert t["trials"] == rt["trials"] and t["solve"] > 0
+
+
 def test_reoptimize_same_handle(small, oracle):
     """set_problem twice on one handle (workspace reuse) gives the same answer."""
     ba = _solver(small)
