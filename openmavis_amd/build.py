@@ -75,9 +75,34 @@ def build_oracle(verbose=True):
     return os.path.join(odir, "liboracle.so")
 
 
+CONSUMER_SRC = os.path.join(ROOT, "tests", "cpp", "omv_consumer.cpp")
+CONSUMER_BIN = os.path.join(PKG, "bin", "omv_consumer")
+
+
+def build_consumer(verbose=True):
+    """tests/cpp/omv_consumer.cpp: a plain C++ (g++) consumer of include/omv.h + include/omv_adapters.hpp, linked
+    against libomv_hip.so and the HIP runtime only (test infrastructure for the C++ integration path)."""
+    deps = [CONSUMER_SRC, os.path.join(ROOT, "include", "omv.h"), os.path.join(ROOT, "include", "omv_adapters.hpp"), LIB]
+    if not os.path.exists(CONSUMER_SRC) or not _newer(CONSUMER_BIN, deps):
+        return CONSUMER_BIN
+    os.makedirs(os.path.dirname(CONSUMER_BIN), exist_ok=True)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(rocm, "include"), CONSUMER_SRC,
+           "-o", CONSUMER_BIN + ".tmp", "-L", PKG, "-lomv_hip", "-Wl,-rpath,$ORIGIN/..",
+           "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath," + os.path.join(rocm, "lib")]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(CONSUMER_BIN + ".tmp", CONSUMER_BIN)
+    return CONSUMER_BIN
+
+
 def build_all(force=False, verbose=True):
     build_oracle(verbose)
-    return build_hip(force, verbose)
+    lib = build_hip(force, verbose)
+    build_consumer(verbose)
+    return lib
 
 
 if __name__ == "__main__":

@@ -1,0 +1,197 @@
+// A C++ consumer of include/omv.h through the adapters of include/omv_adapters.hpp — what the reference's
+// C++ would link.  Built with g++ against the header and libomv_hip.so only (no torch, no
+// Python); driven by tests/test_cpp_consumer_gpu.py, which writes the inputs as raw arrays into a directory
+// and checks the outputs against the CPU oracle (ORB / SearchByProjection bit-exact) and the Python path
+// (LocalInertialBA, parity bar).
+//
+//   omv_consumer orb   DIR   per image: ORBextractor::operator() (one image per call, host memory)
+//   omv_consumer frame DIR   MultiCameraFrame (batched extraction + grid + lapping knn) + SearchByProjection
+//   omv_consumer lba   DIR   LocalInertialBAWindow: keyframes added in a mixed fixed / optimisable order,
+//                            flattened optimisable-first, optimised, written back
+//
+// DIR/meta.txt holds "key value" lines; arrays are DIR/<name>.bin in the dtype the test wrote.
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "omv_adapters.hpp"
+
+namespace {
+
+std::map<std::string, double> read_meta(const std::string &dir) {
+    std::map<std::string, double> m;
+    std::ifstream f(dir + "/meta.txt");
+    std::string k;
+    double v;
+    while (f >> k >> v) m[k] = v;
+    if (m.empty()) throw omv_adapt::Error("no " + dir + "/meta.txt");
+    return m;
+}
+
+template <class T>
+std::vector<T> read_bin(const std::string &dir, const std::string &name) {
+    std::ifstream f(dir + "/" + name + ".bin", std::ios::binary | std::ios::ate);
+    if (!f) throw omv_adapt::Error("missing " + name + ".bin");
+    const size_t bytes = (size_t)f.tellg();
+    std::vector<T> v(bytes / sizeof(T));
+    f.seekg(0);
+    f.read(reinterpret_cast<char *>(v.data()), (std::streamsize)bytes);
+    return v;
+}
+
+template <class T>
+void write_bin(const std::string &dir, const std::string &name, const T *p, size_t n) {
+    std::ofstream f(dir + "/" + name + ".bin", std::ios::binary);
+    f.write(reinterpret_cast<const char *>(p), (std::streamsize)(n * sizeof(T)));
+}
+template <class T>
+void write_bin(const std::string &dir, const std::string &name, const std::vector<T> &v) {
+    write_bin(dir, name, v.data(), v.size());
+}
+
+int run_orb(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int n = (int)m["n"], W = (int)m["W"], H = (int)m["H"];
+    const auto img = read_bin<uint8_t>(dir, "images");
+    const auto lap = read_bin<int32_t>(dir, "lapping");
+    omv_adapt::ORBextractor ex((int)m["nfeatures"], 1.2f, 8, (int)m["ini"], (int)m["min"]);
+    std::vector<int32_t> mono(n);
+    for (int i = 0; i < n; ++i) {
+        std::vector<omv_kp> k;
+        std::vector<uint8_t> d;
+        const int l[2] = {lap[2 * i], lap[2 * i + 1]};
+        mono[i] = ex(img.data() + (size_t)i * W * H, W, H, W, k, d, l);
+        write_bin(dir, "kps_" + std::to_string(i), k);
+        write_bin(dir, "desc_" + std::to_string(i), d);
+    }
+    write_bin(dir, "mono", mono);
+    return 0;
+}
+
+int run_frame(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["C"], W = (int)m["W"], H = (int)m["H"], M = (int)m["M"];
+    const auto img = read_bin<uint8_t>(dir, "images");
+    const auto lap = read_bin<int32_t>(dir, "lapping");
+    std::vector<std::array<int, 2>> lapping(C);
+    for (int c = 0; c < C; ++c) lapping[c] = {lap[2 * c], lap[2 * c + 1]};
+    const omv_orb_params p{(int)m["nfeatures"], 1.2f, 8, (int)m["ini"], (int)m["min"]};
+    omv_adapt::MultiCameraFrame F(C, W, H, p, lapping, M);
+    std::vector<const uint8_t *> ims(C);
+    for (int c = 0; c < C; ++c) ims[c] = img.data() + (size_t)c * W * H;
+    F.build(ims);
+    for (int c = 0; c < C; ++c) {
+        std::vector<omv_kp> k;
+        std::vector<uint8_t> d;
+        F.keypoints(c, k, d);
+        write_bin(dir, "kps_" + std::to_string(c), k);
+        write_bin(dir, "desc_" + std::to_string(c), d);
+    }
+    std::vector<int32_t> l2r, r2l;
+    F.stereo(l2r, r2l);
+    write_bin(dir, "l2r", l2r);
+    write_bin(dir, "r2l", r2l);
+    if (M == 0) return 0;
+    omv_adapt::LocalMapView v;
+    v.desc = read_bin<uint8_t>(dir, "mp_desc"), v.proj_x = read_bin<float>(dir, "mp_proj_x");
+    v.proj_y = read_bin<float>(dir, "mp_proj_y"), v.view_cos = read_bin<float>(dir, "mp_view_cos");
+    v.level = read_bin<int32_t>(dir, "mp_level"), v.in_view = read_bin<uint8_t>(dir, "mp_in_view");
+    v.track_depth = read_bin<float>(dir, "mp_track_depth"), v.is_bad = read_bin<uint8_t>(dir, "mp_is_bad");
+    v.has_obs = read_bin<uint8_t>(dir, "mp_has_obs");
+    std::vector<int32_t> k2m((size_t)C * F.kp_cap(), -1);
+    omv_adapt::SearchByProjection sbp((float)m["nnratio"]);
+    const int nm = sbp(F, v, (float)m["th"], m["far"] != 0, (float)m["th_far"], k2m);
+    write_bin(dir, "kp_to_mp", k2m);
+    write_bin(dir, "n_matches", &nm, 1);
+    std::ofstream(dir + "/kp_cap.txt") << F.kp_cap() << "\n";
+    return 0;
+}
+
+int run_lba(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["n_cams"], K = (int)m["n_kf"], n_opt = (int)m["n_opt"], P = (int)m["n_pts"];
+    const auto order = read_bin<int32_t>(dir, "kf_order");   // window insertion order of the original keyframes
+    const auto Rwb = read_bin<double>(dir, "Rwb"), twb = read_bin<double>(dir, "twb"), Rcw = read_bin<double>(dir, "Rcw");
+    const auto tcw = read_bin<double>(dir, "tcw"), vel = read_bin<double>(dir, "vel"), bg = read_bin<double>(dir, "bg");
+    const auto ba = read_bin<double>(dir, "ba");
+    const auto kf_imu = read_bin<uint8_t>(dir, "kf_imu");
+    const auto pts = read_bin<double>(dir, "pts");
+    const auto depth = read_bin<float>(dir, "pt_track_depth");
+    const auto mpt = read_bin<int32_t>(dir, "mono_pt"), mkf = read_bin<int32_t>(dir, "mono_kf"), mcam = read_bin<int32_t>(dir, "mono_cam");
+    const auto mobs = read_bin<double>(dir, "mono_obs");
+    const auto mw = read_bin<float>(dir, "mono_inv_sigma2");
+    const auto ik1 = read_bin<int32_t>(dir, "imu_kf1"), ik2 = read_bin<int32_t>(dir, "imu_kf2");
+    const auto pre = read_bin<float>(dir, "preint");
+    const auto irob = read_bin<uint8_t>(dir, "imu_robust");
+    const auto isc = read_bin<float>(dir, "imu_info_scale");
+    omv_adapt::LocalInertialBAWindow win(C, read_bin<float>(dir, "cam"), read_bin<double>(dir, "Rcb"), read_bin<double>(dir, "tcb"),
+                                         read_bin<double>(dir, "Rbc"), read_bin<double>(dir, "tbc"));
+    std::vector<int> slot(K);   // original keyframe -> window index
+    for (int w = 0; w < K; ++w) {
+        const int k = order[w];
+        omv_adapt::LocalInertialBAWindow::KeyFrame f;
+        std::copy_n(&Rwb[9 * k], 9, f.Rwb.begin()), std::copy_n(&twb[3 * k], 3, f.twb.begin());
+        std::copy_n(&vel[3 * k], 3, f.vel.begin()), std::copy_n(&bg[3 * k], 3, f.bg.begin()), std::copy_n(&ba[3 * k], 3, f.ba.begin());
+        f.Rcw.resize(C), f.tcw.resize(C);
+        for (int c = 0; c < C; ++c) {
+            std::copy_n(&Rcw[((size_t)k * C + c) * 9], 9, f.Rcw[c].begin());
+            std::copy_n(&tcw[((size_t)k * C + c) * 3], 3, f.tcw[c].begin());
+        }
+        f.imu = kf_imu[k] != 0, f.fixed = k >= n_opt;
+        slot[k] = win.add_keyframe(f);
+    }
+    for (int i = 0; i < P; ++i) win.add_point({pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}, depth[i]);
+    for (size_t e = 0; e < mpt.size(); ++e) win.add_mono(mpt[e], slot[mkf[e]], mcam[e], mobs[2 * e], mobs[2 * e + 1], mw[e]);
+    for (size_t i = 0; i < ik1.size(); ++i)
+        win.add_inertial({slot[ik1[i]], slot[ik2[i]],
+                          std::vector<float>(pre.begin() + i * OMV_PREINT_FLOATS, pre.begin() + (i + 1) * OMV_PREINT_FLOATS),
+                          irob[i] != 0, isc[i]});
+    std::vector<double> chi2;
+    std::vector<uint8_t> outl;
+    const omv_lba_result r = win.optimize(m["large"] != 0, &chi2, &outl);
+    // state back in the original keyframe order
+    std::vector<double> oRwb(9 * K), otwb(3 * K), oRcw((size_t)9 * K * C), otcw((size_t)3 * K * C), ovel(3 * K), obg(3 * K), oba(3 * K);
+    for (int k = 0; k < K; ++k) {
+        const auto &f = win.keyframes()[slot[k]];
+        std::copy(f.Rwb.begin(), f.Rwb.end(), &oRwb[9 * k]), std::copy(f.twb.begin(), f.twb.end(), &otwb[3 * k]);
+        std::copy(f.vel.begin(), f.vel.end(), &ovel[3 * k]), std::copy(f.bg.begin(), f.bg.end(), &obg[3 * k]);
+        std::copy(f.ba.begin(), f.ba.end(), &oba[3 * k]);
+        for (int c = 0; c < C; ++c) {
+            std::copy(f.Rcw[c].begin(), f.Rcw[c].end(), &oRcw[((size_t)k * C + c) * 9]);
+            std::copy(f.tcw[c].begin(), f.tcw[c].end(), &otcw[((size_t)k * C + c) * 3]);
+        }
+    }
+    write_bin(dir, "out_Rwb", oRwb), write_bin(dir, "out_twb", otwb), write_bin(dir, "out_Rcw", oRcw);
+    write_bin(dir, "out_tcw", otcw), write_bin(dir, "out_vel", ovel), write_bin(dir, "out_bg", obg), write_bin(dir, "out_ba", oba);
+    write_bin(dir, "out_pts", win.points());
+    write_bin(dir, "out_chi2", chi2), write_bin(dir, "out_outlier", outl);
+    std::ofstream o(dir + "/result.txt");
+    o.precision(17);
+    o << "err " << r.err << "\nerr_end " << r.err_end << "\nstatus " << r.status << "\niterations " << r.iterations
+      << "\ntrials " << r.trials << "\nlambda " << r.lambda << "\n";
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc != 3) {
+        std::fprintf(stderr, "usage: %s orb|frame|lba DIR\n", argv[0]);
+        return 2;
+    }
+    try {
+        const std::string mode = argv[1], dir = argv[2];
+        if (mode == "orb") return run_orb(dir);
+        if (mode == "frame") return run_frame(dir);
+        if (mode == "lba") return run_lba(dir);
+        std::fprintf(stderr, "unknown mode %s\n", argv[1]);
+        return 2;
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "omv_consumer: %s\n", e.what());
+        return 1;
+    }
+}

@@ -1,0 +1,143 @@
+"""The C++ integration path: tests/cpp/omv_consumer.cpp (g++, include/omv.h + include/omv_adapters.hpp, linked
+against libomv_hip.so only — no torch, no Python binding) runs the adapters INTEGRATION.md describes on the GPU.
+
+- ORBextractor::operator() adapter, one image per call: bit-exact vs the CPU oracle;
+- MultiCameraFrame (batched extraction + AssignFeaturesToGrid + lapping knn) and the SearchByProjection
+  adapter: keypoints, descriptors, stereo pairs, assignments and match count bit-exact vs the oracle;
+- LocalInertialBAWindow (keyframes added in mixed fixed / optimisable order, flattened optimisable-first like
+  the reference's vertex creation): identical LM trials / iterations / status to the Python path on the same
+  window, state and chi2 within the LocalInertialBA parity bar of tests/test_lba_gpu.py.
+The binary runs as a child process (no exec from this process)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from openmavis_amd import build as omv_build, synth, synth_ba
+
+pytestmark = pytest.mark.gpu
+
+W, H, C = 720, 540, 5
+LAP = np.array([[0, 720], [0, 720], [0, 0], [0, 0], [0, 0]], np.int32)
+
+
+def _consumer():
+    if not os.path.exists(omv_build.CONSUMER_BIN):
+        pytest.fail(f"{omv_build.CONSUMER_BIN} not built (python -m openmavis_amd.build)")
+    return omv_build.CONSUMER_BIN
+
+
+def _run(mode, d):
+    r = subprocess.run([_consumer(), mode, str(d)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def _meta(d, **kv):
+    with open(os.path.join(d, "meta.txt"), "w") as f:
+        for k, v in kv.items():
+            f.write(f"{k} {v}\n")
+
+
+def _w(d, name, a):
+    np.ascontiguousarray(a).tofile(os.path.join(d, name + ".bin"))
+
+
+def _r(d, name, dtype):
+    return np.fromfile(os.path.join(d, name + ".bin"), dtype)
+
+
+def test_orb_extractor_adapter(tmp_path, oracle):
+    imgs = np.stack([synth.hilti_frame(40)[0], synth.hilti_frame(41)[1], synth.synth_image(77, W, H)])
+    laps = np.array([[0, 720], [0, 720], [0, 0]], np.int32)
+    _meta(tmp_path, n=len(imgs), W=W, H=H, nfeatures=1200, ini=15, min=7)
+    _w(tmp_path, "images", imgs)
+    _w(tmp_path, "lapping", laps)
+    _run("orb", tmp_path)
+    mono = _r(tmp_path, "mono", np.int32)
+    for i, img in enumerate(imgs):
+        om, ok, od = oracle.orb_extract(img, 1200, 1.2, 8, 15, 7, tuple(laps[i]))
+        k = _r(tmp_path, f"kps_{i}", oracle.KP_DTYPE)
+        d = _r(tmp_path, f"desc_{i}", np.uint8).reshape(-1, 32)
+        assert mono[i] == om and len(k) == len(ok)
+        assert np.array_equal(k.view(np.uint32), ok.view(np.uint32)), f"image {i} keypoints"
+        assert np.array_equal(d, od), f"image {i} descriptors"
+
+
+def test_multicamera_frame_and_search_by_projection(tmp_path, oracle):
+    imgs = synth.hilti_frame(42)
+    M = 3000
+    # oracle first: the keypoints the map points are derived from (identical on the device, checked below)
+    cap = 1200 + 64 * 8
+    kps = np.zeros((C, cap), oracle.KP_DTYPE)
+    desc = np.zeros((C, cap, 32), np.uint8)
+    n_kp, mono = np.zeros(C, np.int32), np.zeros(C, np.int32)
+    for c in range(C):
+        mono[c], k, d = oracle.orb_extract(imgs[c], 1200, 1.2, 8, 15, 7, tuple(LAP[c]))
+        n_kp[c] = len(k)
+        kps[c, :len(k)], desc[c, :len(k)] = k, d
+    mp = synth.make_map_points(kps, desc, n_kp, M, 9, W, H)
+    _meta(tmp_path, C=C, W=W, H=H, nfeatures=1200, ini=15, min=7, M=M, th=6.0, far=0, th_far=20.0, nnratio=0.8)
+    _w(tmp_path, "images", imgs)
+    _w(tmp_path, "lapping", LAP)
+    for k in ("desc", "proj_x", "proj_y", "view_cos", "level", "in_view", "track_depth", "is_bad", "has_obs"):
+        _w(tmp_path, "mp_" + k, mp[k])
+    _run("frame", tmp_path)
+    dcap = int(open(os.path.join(tmp_path, "kp_cap.txt")).read())
+    for c in range(C):
+        k = _r(tmp_path, f"kps_{c}", oracle.KP_DTYPE)
+        d = _r(tmp_path, f"desc_{c}", np.uint8).reshape(-1, 32)
+        assert len(k) == n_kp[c] and np.array_equal(k.view(np.uint32), kps[c, :n_kp[c]].view(np.uint32)), f"cam {c}"
+        assert np.array_equal(d, desc[c, :n_kp[c]]), f"cam {c} descriptors"
+    l2r, r2l = _r(tmp_path, "l2r", np.int32), _r(tmp_path, "r2l", np.int32)
+    # the lapping knn + Lowe pairs (Frame.cc:1461-1491)
+    q, t = desc[0, mono[0]:n_kp[0]], desc[1, mono[1]:n_kp[1]]
+    i2, d2 = oracle.bf_knn2(q, t)
+    el2r = np.full(dcap, -1, np.int32)
+    for qi in range(len(q)):
+        if i2[qi, 1] >= 0 and float(d2[qi, 0]) < float(d2[qi, 1]) * 0.8:
+            el2r[mono[0] + qi] = mono[1] + i2[qi, 0]
+    assert np.array_equal(l2r, el2r)
+    # SearchByProjection on the device frame: the oracle on the same frame (padded to the device's row capacity)
+    kp_d = np.zeros((C, dcap), oracle.KP_DTYPE)
+    de_d = np.zeros((C, dcap, 32), np.uint8)
+    for c in range(C):
+        kp_d[c, :n_kp[c]], de_d[c, :n_kp[c]] = kps[c, :n_kp[c]], desc[c, :n_kp[c]]
+    sf = [1.0]
+    for _ in range(7):
+        sf.append(float(np.float32(sf[-1] * 1.2)))   # mvScaleFactor: (float)(previous * scaleFactor)
+    g = oracle.frame_geom(C, W, H, sf)
+    exp = np.full(C * dcap, -1, np.int32)
+    n = oracle.search_by_projection(g, kp_d, de_d, n_kp, mp, 6.0, False, 20.0, 0.8, l2r, r2l,
+                                    np.zeros(C * dcap, np.uint8), exp)
+    got = _r(tmp_path, "kp_to_mp", np.int32)
+    assert int(_r(tmp_path, "n_matches", np.int32)[0]) == n and n > 300
+    assert np.array_equal(got, exp)
+
+
+def test_local_inertial_ba_window(tmp_path, oracle):
+    from test_lba_gpu import _compare_state, _solver
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11)
+    K, n_opt = prob["n_kf"], prob["n_opt"]
+    # window insertion order: fixed and optimisable keyframes interleaved (relative order kept in each group,
+    # so the flattened vertex order equals the problem's)
+    fixed, opt = list(range(n_opt, K)), list(range(n_opt))
+    order = np.array([x for pair in zip(fixed, opt) for x in pair] + fixed[len(opt):] + opt[len(fixed):], np.int32)
+    _meta(tmp_path, n_cams=prob["n_cams"], n_kf=K, n_opt=n_opt, n_pts=len(prob["pts"]), large=1)
+    _w(tmp_path, "kf_order", order)
+    for k in ("cam", "Rcb", "tcb", "Rbc", "tbc", "kf_imu", "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts",
+              "pt_track_depth", "mono_pt", "mono_kf", "mono_cam", "mono_obs", "mono_inv_sigma2", "imu_kf1", "imu_kf2",
+              "preint", "imu_robust", "imu_info_scale"):
+        _w(tmp_path, k, prob[k])
+    _run("lba", tmp_path)
+    res = dict(line.split() for line in open(os.path.join(tmp_path, "result.txt")))
+    rp, sp = _solver(prob).set_problem(prob).optimize(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    assert (int(res["iterations"]), int(res["trials"]), int(res["status"])) == (rp["iterations"], rp["trials"], rp["status"])
+    for k in ("err", "err_end"):
+        assert abs(float(res[k]) - rp[k]) <= 1e-5 * abs(rp[k]), (k, res[k], rp[k])
+    ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    sc = {k: _r(tmp_path, "out_" + k, np.float64).reshape(so[k].shape)
+          for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts")}
+    _compare_state(prob, sc, so, oracle)
+    chi2 = _r(tmp_path, "out_chi2", np.float64)
+    assert np.allclose(chi2, rp["mono_chi2"], rtol=1e-6, atol=1e-3)
