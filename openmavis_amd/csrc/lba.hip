@@ -5,14 +5,16 @@
 // Per LM iteration (optimization_algorithm_levenberg.cpp:61-169):
 //   errors   1 thread / visual edge (+1 thread / inertial edge): residual, chi2, Huber rho; deterministic
 //            two-level chi2 reduction (computeActiveErrors + activeRobustChi2)
-//   build    1 thread / landmark (edges sorted landmark-major): EdgeMono Jacobians, the landmark's
-//            Hll / bl and per-keyframe Hpl blocks in registers; the pose-diagonal JpT W Jp terms are
-//            reduced in LDS per workgroup (landmarks are ordered by keyframe window, so a workgroup
-//            touches a few keyframes) and flushed with f64 atomics into the dense reduced matrix;
-//            1 wavefront / inertial edge for the 9x24 Jacobian and its 24x24 quadratic form
+//   build    1 thread / landmark (edges sorted landmark-major): EdgeMono / EdgeStereo Jacobians, the
+//            landmark's Hll / bl and per-keyframe Hpl blocks in registers; 1 workgroup / optimisable
+//            keyframe gathers its edges for the pose-diagonal JpT W Jp and JpT W e (fixed-order reduction);
+//            1 wavefront / inertial edge writes its 30x30 quadratic form (EdgeInertial + random walks),
+//            added into the reduced system colour by colour (no two edges of a colour share a keyframe)
 //   per trial (lambda):
-//     schur    1 thread / landmark: Dinv = (Hll + lambda I)^-1, Hpl Dinv Hpl^T into the reduced
-//              system (LDS pre-reduction again), coefficients Hpl Dinv bl
+//     schur    1 thread / landmark: Dinv = (Hll + lambda I)^-1, BD = Hpl Dinv and Hpl Dinv bl per slot;
+//              1 workgroup / reduced-system block gathers its (slot a, slot b) terms BD_a Hpl_b^T and, on the
+//              diagonal, the keyframe's coefficients — fixed-order sums throughout, no float atomics, so a
+//              solve is bitwise identical run to run
 //     ldlt     1 workgroup: block LDL^T of the reduced system (keyframe blocks of 15 / 6) on the
 //              symbolic block pattern (host-computed fill-in), the nonzero blocks staged in LDS,
 //              then block forward / backward substitution (SimplicialLDLT semantics: no pivoting,
@@ -20,8 +22,9 @@
 //     update   1 thread / landmark: back-substitution xl = Dinv (bl - Hpl^T xp) and the point update;
 //              1 thread / keyframe: ImuCamPose::Update (body-frame SE3 with ExpSO3) + v, bg, ba;
 //              the step's computeScale term; errors of the trial state
-//   The accept / reject decision (rho, lambda schedule, push/pop) runs on the host from two scalars
-//   per trial, exactly as the reference; push/pop is a double-buffered state.
+//   The accept / reject decision (rho, lambda schedule, push/pop) runs on the device (finish_trial_kernel,
+//   LmCtl) with one read-back per optimize(); a host-driven loop with the same decisions is kept for
+//   sharded solves and parity checks.  Push/pop is a double-buffered state.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,7 +47,6 @@ namespace {
 
 using namespace omv_g2o;
 
-constexpr int kSpan = 8;
 constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / back-substitution)          // keyframes a workgroup may touch for LDS pre-reduction
 
 #define HIP_OK(x)                                                                    \
@@ -302,11 +304,20 @@ struct Land {
     const int *edge_start;   // [P+1]
     const int *slot_start;   // [P+1]
     const int *slot_kf;      // [nslots]
-    const int *wg_kf0;       // [n_wg] first keyframe of the workgroup's span, or -1 (span too wide)
     double *Hll;             // [P][9]
     double *bl;              // [P][3]
     double *Hpl;             // [nslots][18] pose rows x point cols
+    double *BD;              // [nslots][18] Hpl Dinv (the trial's Schur operand)
+    double *cs;              // [nslots][6]  Hpl Dinv bl
     int n;
+};
+
+// Gather lists for the deterministic reductions (host-built once per problem, each in ascending order):
+struct Gather {
+    const int *kf_edge_start, *kf_edge;     // per optimisable keyframe: its visual edges
+    const int *kf_slot_start, *kf_slot;     // per optimisable keyframe: its landmark slots
+    const int *tr_start;                    // per reduced-system block (BlockPat slot): its Schur terms
+    const int2 *tr;                         //   (landmark slot a, landmark slot b), a's keyframe >= b's
 };
 
 struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lower triangle used
@@ -316,124 +327,172 @@ struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lowe
     int n_kf;
 };
 
-// LDS accumulators of a workgroup: kSpan keyframes x (36 + 6)
-__device__ __forceinline__ void build_land_block(int blk, double *acc, Rig rig, State s, Edges E, Land L, Red R,
-                                                 double delta, double dsqr, double delta_st, double dsqr_st,
-                                                 const double *err, const double *err3, const double *chi2) {
+// One visual edge at the current errors (EdgeMono, or EdgeStereo when ur >= 0): the point Jacobian JX (nr x 3),
+// the pose Jacobian JP (nr x 6, ImuCamPose order), the robust weight w = invSigma2 * rho' and the weighted
+// residual om = -invSigma2 * rho' * e (constructQuadraticForm, base_binary_edge.hpp:55-116).
+__device__ __forceinline__ int edge_jacobians(const Rig &rig, const State &s, const Edges &E, int e, double delta,
+                                              double dsqr, double delta_st, double dsqr_st, const double *err,
+                                              const double *err3, const double *chi2, double JX[9], double JP[18],
+                                              double &w, double om[3]) {
+    const int k = E.kf[e], c = E.cam[e], C = rig.n_cams;
+    const double *Rcw = s.Rcw + ((size_t)k * C + c) * 9, *tcw = s.tcw + ((size_t)k * C + c) * 3;
+    const double *X = s.pts + (size_t)E.pt[e] * 3;
+    double Xc[3], Xb[3];
+    mv3(Rcw, X, Xc);
+    for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
+    mv3(rig.Rbc[c], Xc, Xb);
+    for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
+    const bool st = E.ur[e] >= 0.f;   // EdgeStereo: proj_jac row 2 = row 0, (2,2) += bf / z^2
+    double pj[9];
+    kb8_jac(rig.cam[c], Xc, pj);
+    const int nr = st ? 3 : 2;
+    // all three rows are formed (zero for a mono edge) so the arrays stay in registers; the sums skip row 2
+    if (st) {
+        const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
+        pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
+    } else {
+        pj[6] = pj[7] = pj[8] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            JX[3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
+    {
+        double pr[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
+        const double x = Xb[0], y = Xb[1], z = Xb[2];
+        const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+                JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    }
+    double r0, r1;
+    if (st) huber(chi2[e], delta_st, dsqr_st, r0, r1);
+    else huber(chi2[e], delta, dsqr, r0, r1);
+    const double wi = (double)E.w[e];
+    w = wi * r1;
+    om[0] = -wi * err[2 * e] * r1, om[1] = -wi * err[2 * e + 1] * r1;
+    om[2] = st ? -wi * err3[e] * r1 : 0.0;
+    return nr;
+}
+
+// sums over the residual rows: the EdgeStereo row is added last (mono edges: 2 rows)
+__device__ __forceinline__ double rows2(const double *A, int ia, const double *B, int ib, int lda, int ldb, int nr) {
+    double t = A[ia] * B[ib] + A[lda + ia] * B[ldb + ib];
+    if (nr == 3) t += A[2 * lda + ia] * B[2 * ldb + ib];
+    return t;
+}
+__device__ __forceinline__ double rows_om(const double *A, int ia, int lda, const double *om, int nr) {
+    double t = A[ia] * om[0] + A[lda + ia] * om[1];
+    if (nr == 3) t += A[2 * lda + ia] * om[2];
+    return t;
+}
+
+// Landmark part of buildSystem: one thread per landmark (edges in landmark-major order): Hll, bl and the
+// per-(landmark, keyframe) Hpl blocks, each summed in edge order.  The keyframe-diagonal terms are gathered per
+// keyframe by build_pose_kernel (fixed order, no atomics).
+__device__ __forceinline__ void build_land_block(int blk, Rig rig, State s, Edges E, Land L, double delta,
+                                                 double dsqr, double delta_st, double dsqr_st, const double *err,
+                                                 const double *err3, const double *chi2) {
     const int p = blk * blockDim.x + threadIdx.x;
-    const int kf0 = L.wg_kf0[blk];
-    for (int q = threadIdx.x; q < kSpan * 42; q += blockDim.x) acc[q] = 0;
-    __syncthreads();
-    if (p < L.n) {
-        double Hll[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
-        double Hpl[18];
-        int cur_slot = -1;
-        const int C = rig.n_cams;
-        const double *X = s.pts + (size_t)p * 3;
-        for (int e = L.edge_start[p]; e < L.edge_start[p + 1]; ++e) {
-            const int k = E.kf[e], c = E.cam[e];
-            const double *Rcw = s.Rcw + ((size_t)k * C + c) * 9, *tcw = s.tcw + ((size_t)k * C + c) * 3;
-            double Xc[3], Xb[3];
-            mv3(Rcw, X, Xc);
-            for (int q = 0; q < 3; ++q) Xc[q] += tcw[q];
-            mv3(rig.Rbc[c], Xc, Xb);
-            for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
-            const bool st = E.ur[e] >= 0.f;   // EdgeStereo: proj_jac row 2 = row 0, (2,2) += bf / z^2
-            double pj[9];
-            kb8_jac(rig.cam[c], Xc, pj);
-            const int nr = st ? 3 : 2;
-            if (st) {
-                const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
-                pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
-            }
-            double JX[9], JP[18];
-            for (int r = 0; r < nr; ++r)
-                for (int q = 0; q < 3; ++q)
-                    JX[3 * r + q] = -(pj[3 * r] * Rcw[q] + pj[3 * r + 1] * Rcw[3 + q] + pj[3 * r + 2] * Rcw[6 + q]);
-            {
-                double pr[9];
-                for (int r = 0; r < nr; ++r)
-                    for (int q = 0; q < 3; ++q)
-                        pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] +
-                                        pj[3 * r + 2] * rig.Rcb[c][6 + q];
-                const double x = Xb[0], y = Xb[1], z = Xb[2];
-                const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-                for (int r = 0; r < nr; ++r)
-                    for (int q = 0; q < 6; ++q)
-                        JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
-            }
-            double r0, r1;
-            if (st) huber(chi2[e], delta_st, dsqr_st, r0, r1);
-            else huber(chi2[e], delta, dsqr, r0, r1);
-            const double wi = (double)E.w[e];
-            const double w = wi * r1;
-            const double om0 = -wi * err[2 * e] * r1, om1 = -wi * err[2 * e + 1] * r1;
-            const double om2 = st ? -wi * err3[e] * r1 : 0.0;
-            // sums over the residual rows: the EdgeStereo row is added last (mono edges: 2 rows as before)
-            auto rows = [&](const double *A, int ia, const double *B, int ib, int lda, int ldb) {
-                double t = A[ia] * B[ib] + A[lda + ia] * B[ldb + ib];
-                if (st) t += A[2 * lda + ia] * B[2 * ldb + ib];
-                return t;
-            };
-            auto rows_om = [&](const double *A, int ia, int lda) {
-                double t = A[ia] * om0 + A[lda + ia] * om1;
-                if (st) t += A[2 * lda + ia] * om2;
-                return t;
-            };
-            for (int r = 0; r < 3; ++r) {
-                bl[r] += rows_om(JX, r, 3);
-                for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * rows(JX, r, JX, q, 3, 3);
-            }
-            const int slot = E.slot[e];
-            if (slot != cur_slot) {
-                if (cur_slot >= 0)
-                    for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
-                for (int q = 0; q < 18; ++q) Hpl[q] = 0;
-                cur_slot = slot;
-            }
-            for (int r = 0; r < 6; ++r)
-                for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * rows(JP, r, JX, q, 6, 3);
-            const int o = R.offP[k];
-            if (o < 0) continue;   // fixed keyframe: no pose terms
-            if (kf0 >= 0 && k - kf0 >= 0 && k - kf0 < kSpan) {
-                double *a = acc + (k - kf0) * 42;
-                for (int r = 0; r < 6; ++r) {
-                    unsafeAtomicAdd(a + 36 + r, rows_om(JP, r, 6));
-                    for (int q = 0; q <= r; ++q) unsafeAtomicAdd(a + 6 * r + q, w * rows(JP, r, JP, q, 6, 6));
-                }
-            } else {
-                for (int r = 0; r < 6; ++r) {
-                    unsafeAtomicAdd(R.b + o + r, rows_om(JP, r, 6));
-                    for (int q = 0; q <= r; ++q)
-                        unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + q, w * rows(JP, r, JP, q, 6, 6));
-                }
-            }
+    if (p >= L.n) return;
+    double Hll[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+    double Hpl[18];
+    int cur_slot = -1;
+    for (int e = L.edge_start[p]; e < L.edge_start[p + 1]; ++e) {
+        double JX[9], JP[18], w, om[3];
+        const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            bl[r] += rows_om(JX, r, 3, om, nr);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * rows2(JX, r, JX, q, 3, 3, nr);
         }
-        if (cur_slot >= 0)
-            for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
-        for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = Hll[q];
-        for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = bl[q];
+        const int slot = E.slot[e];
+        if (slot != cur_slot) {
+            if (cur_slot >= 0)
+                for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
+            for (int q = 0; q < 18; ++q) Hpl[q] = 0;
+            cur_slot = slot;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * rows2(JP, r, JX, q, 6, 3, nr);
+    }
+    if (cur_slot >= 0)
+        for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
+    for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = Hll[q];
+    for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = bl[q];
+}
+
+// Fixed-order wavefront sum (xor tree): the wave total in every lane; callers combine the waves in order.
+__device__ __forceinline__ double wave_sum_fixed(double v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Keyframe-diagonal visual terms of buildSystem: one workgroup per optimisable keyframe gathers its edges
+// (ascending edge order, strided over the threads), 21 + 6 sums per thread, then a fixed-order reduction.
+__global__ void __launch_bounds__(256) build_pose_kernel(Rig rig, State s, Edges E, Gather G, Red R, double delta,
+                                                         double dsqr, double delta_st, double dsqr_st,
+                                                         const double *err, const double *err3, const double *chi2,
+                                                         const LmCtl *ctl) {
+    __shared__ double wsum[4][27];
+    if (!gate_open(ctl, kGateBuild)) return;
+    const int k = blockIdx.x, o = R.offP[k];
+    double acc[27];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) acc[q] = 0;
+    for (int i = G.kf_edge_start[k] + threadIdx.x; i < G.kf_edge_start[k + 1]; i += blockDim.x) {
+        const int e = G.kf_edge[i];
+        double JX[9], JP[18], w, om[3];
+        const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
+        int q = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c <= r; ++c) acc[q++] += w * rows2(JP, r, JP, c, 6, 6, nr);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) acc[21 + r] += rows_om(JP, r, 6, om, nr);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 27; ++q) {
+        const double t = wave_sum_fixed(acc[q]);
+        if (lane == 0) wsum[wave][q] = t;
     }
     __syncthreads();
-    if (kf0 >= 0)
-        for (int q = threadIdx.x; q < kSpan * 42; q += blockDim.x) {
-            const int k = kf0 + q / 42, j = q % 42;
-            if (acc[q] == 0.0 || k >= R.n_kf) continue;
-            const int o = R.offP[k];
-            if (o < 0) continue;
-            if (j < 36) {
-                const int r = j / 6, c = j % 6;
-                if (c <= r) unsafeAtomicAdd(R.H + (size_t)(o + r) * R.n + o + c, acc[q]);
-            } else {
-                unsafeAtomicAdd(R.b + o + (j - 36), acc[q]);
-            }
+    if (threadIdx.x < 27 && o >= 0) {
+        const int q = threadIdx.x;
+        double t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += wsum[w][q];
+        if (q < 21) {
+            int r = 0;
+            while ((r + 1) * (r + 2) / 2 <= q) ++r;
+            const int c = q - r * (r + 1) / 2;
+            R.H[(size_t)(o + r) * R.n + o + c] = t;   // the first contribution after the zeroing
+        } else {
+            R.b[o + q - 21] = t;
         }
+    }
 }
 
 // ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
 
-__device__ __forceinline__ void build_imu_block(int i, double *sm, State s, Imu I, Red R, double delta, double dsqr,
-                                                const double *err9) {
+// Inertial + random-walk edges of one EdgeInertial i (one wavefront): the 30 x 30 quadratic form and 30 gradient
+// over the edge's local variables [P1 V1 G1 A1 P2 V2 G2 A2] (EdgeInertial over the first 24, EdgeGyroRW on
+// G1 / G2, EdgeAccRW on A1 / A2), written to its own slot; imu_add_kernel adds the slots into the reduced system.
+constexpr int kImuLoc = 30, kImuContrib = kImuLoc * kImuLoc + kImuLoc;
+__device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Imu I, double delta, double dsqr,
+                                                  const double *err9, double *contrib) {
     double *J = sm, *WJ = sm + 216, *om = sm + 432;   // J (9 x 24), Omega' J (9 x 24), -Omega' e
     const int lane = threadIdx.x;
     if (lane == 0) imu_jacobian(s, I, i, J);
@@ -456,69 +515,86 @@ __device__ __forceinline__ void build_imu_block(int i, double *sm, State s, Imu 
     }
     __syncthreads();
     const int k1 = I.kf1[i], k2 = I.kf2[i];
-    const int off[6] = {I.offP[k1], I.offV[k1], I.offG[k1], I.offA[k1], I.offP[k2], I.offV[k2]};
-    const int col0[6] = {0, 6, 9, 12, 15, 21};
-    const int dim[6] = {6, 3, 3, 3, 6, 3};
-    // map a J column to its reduced-system index (-1 fixed)
-    auto red = [&](int c) {
-        int v = 0;
-        while (v < 5 && c >= col0[v + 1]) ++v;
-        return off[v] < 0 ? -1 : off[v] + (c - col0[v]);
-    };
-    for (int q = lane; q < 24 * 24; q += 64) {
-        const int a = q / 24, b = q % 24;
-        const int ra = red(a), rb = red(b);
-        if (ra < 0 || rb < 0 || rb > ra) continue;   // lower triangle of the reduced matrix
+    double *Hc = contrib + (size_t)i * kImuContrib, *bc = Hc + kImuLoc * kImuLoc;
+    const double *Ig = I.infoG + 9 * i, *Ia = I.infoA + 9 * i;
+    for (int q = lane; q < kImuLoc * kImuLoc; q += 64) {
+        const int a = q / kImuLoc, b = q % kImuLoc;
         double t = 0;
-        for (int k = 0; k < 9; ++k) t += J[k * 24 + a] * WJ[k * 24 + b];
-        unsafeAtomicAdd(R.H + (size_t)ra * R.n + rb, t);
+        if (a < 24 && b < 24)
+            for (int k = 0; k < 9; ++k) t += J[k * 24 + a] * WJ[k * 24 + b];
+        // random walks: H += J^T Info J with J1 = -I (G1 / A1), J2 = I (G2 / A2)
+        const int ga = a >= 9 && a < 12 ? 0 : (a >= 24 && a < 27 ? 1 : -1), gb = b >= 9 && b < 12 ? 0 : (b >= 24 && b < 27 ? 1 : -1);
+        const int aa = a >= 12 && a < 15 ? 0 : (a >= 27 ? 1 : -1), ab = b >= 12 && b < 15 ? 0 : (b >= 27 ? 1 : -1);
+        if (ga >= 0 && gb >= 0) {
+            const int r = a - (ga ? 24 : 9), c = b - (gb ? 24 : 9);
+            t += (ga == gb ? 1.0 : -1.0) * Ig[3 * r + c];
+        }
+        if (aa >= 0 && ab >= 0) {
+            const int r = a - (aa ? 27 : 12), c = b - (ab ? 27 : 12);
+            t += (aa == ab ? 1.0 : -1.0) * Ia[3 * r + c];
+        }
+        Hc[q] = t;
     }
-    if (lane < 24) {
-        const int ra = red(lane);
-        if (ra >= 0) {
-            double t = 0;
+    if (lane < kImuLoc) {
+        double t = 0;
+        if (lane < 24)
             for (int k = 0; k < 9; ++k) t += J[k * 24 + lane] * om[k];
-            unsafeAtomicAdd(R.b + ra, t);
-        }
-    }
-    // EdgeGyroRW / EdgeAccRW (J1 = -I, J2 = I): lanes 0..17 -> (which, r, c) blocks
-    (void)dim;
-    if (lane < 18) {
-        const int which = lane / 9, rc = lane % 9, r = rc / 3, c = rc % 3;
-        const double *Iw = which ? I.infoA + 9 * i : I.infoG + 9 * i;
-        const int o1 = which ? I.offA[k1] : I.offG[k1], o2 = which ? I.offA[k2] : I.offG[k2];
-        const double *b1v = which ? s.ba : s.bg;
-        if (o1 >= 0) unsafeAtomicAdd(R.H + (size_t)(o1 + r) * R.n + o1 + c, Iw[rc]);
-        if (o2 >= 0) unsafeAtomicAdd(R.H + (size_t)(o2 + r) * R.n + o2 + c, Iw[rc]);
-        if (o1 >= 0 && o2 >= 0) {
-            // block (o2, o1) lies in the lower triangle when o2 > o1: -Iw^T
-            if (o2 > o1) unsafeAtomicAdd(R.H + (size_t)(o2 + r) * R.n + o1 + c, -Iw[3 * c + r]);
-            else unsafeAtomicAdd(R.H + (size_t)(o1 + r) * R.n + o2 + c, -Iw[rc]);
-        }
-        if (c == 0) {
+        // random walks: b -= J^T Info e, e = b2 - b1 (+ on the first keyframe's bias, - on the second's)
+        int which = -1, r = 0;   // 0 gyro, 1 acc
+        if (lane >= 9 && lane < 15) which = lane >= 12, r = lane - (lane >= 12 ? 12 : 9);
+        else if (lane >= 24) which = lane >= 27, r = lane - (lane >= 27 ? 27 : 24);
+        if (which >= 0) {
+            const double *bv = which ? s.ba : s.bg, *Iw = which ? Ia : Ig;
             double ee[3];
-            for (int q = 0; q < 3; ++q) ee[q] = b1v[3 * k2 + q] - b1v[3 * k1 + q];
+            for (int q = 0; q < 3; ++q) ee[q] = bv[3 * k2 + q] - bv[3 * k1 + q];
             const double Oe = Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
-            if (o1 >= 0) unsafeAtomicAdd(R.b + o1 + r, Oe);
-            if (o2 >= 0) unsafeAtomicAdd(R.b + o2 + r, -Oe);
+            t += lane < 24 ? Oe : -Oe;
         }
+        bc[lane] = t;
     }
 }
 
-// buildSystem in one launch (64-thread blocks): blocks [0, n_land) the landmark part, the next n_imu blocks
-// one inertial edge each.
-constexpr int kBuildLds = kSpan * 42 > 441 ? kSpan * 42 : 441;
-__global__ void __launch_bounds__(kLandWG) build_kernel(int n_land, Rig rig, State s, Edges E, Land L, Red R,
-                                                        double delta, double dsqr, double delta_st, double dsqr_st,
-                                                        const double *err, const double *err3, const double *chi2,
-                                                        Imu I, double delta_imu, double dsqr_imu, const double *err9,
-                                                        const LmCtl *ctl) {
-    __shared__ double sm[kBuildLds];
+__global__ void __launch_bounds__(kLandWG) imu_contrib_kernel(State s, Imu I, double delta, double dsqr,
+                                                              const double *err9, double *contrib, const LmCtl *ctl) {
+    __shared__ double sm[441];
     if (!gate_open(ctl, kGateBuild)) return;
-    if ((int)blockIdx.x < n_land)
-        build_land_block(blockIdx.x, sm, rig, s, E, L, R, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-    else
-        build_imu_block(blockIdx.x - n_land, sm, s, I, R, delta_imu, dsqr_imu, err9);
+    imu_contrib_block(blockIdx.x, sm, s, I, delta, dsqr, err9, contrib);
+}
+
+// Adds the inertial slots of one colour class (no two of its edges share a keyframe, so every reduced-system
+// entry receives at most one term per launch; the classes run in a fixed order after build_pose_kernel).
+__global__ void __launch_bounds__(kLandWG) imu_add_kernel(Imu I, Red R, const double *contrib, const int *edges, int n,
+                                                          const LmCtl *ctl) {
+    if (!gate_open(ctl, kGateBuild)) return;
+    if ((int)blockIdx.x >= n) return;
+    const int i = edges[blockIdx.x];
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const int off[8] = {I.offP[k1], I.offV[k1], I.offG[k1], I.offA[k1], I.offP[k2], I.offV[k2], I.offG[k2], I.offA[k2]};
+    const int col0[9] = {0, 6, 9, 12, 15, 21, 24, 27, 30};
+    auto red = [&](int c) {
+        int v = 0;
+        while (v < 7 && c >= col0[v + 1]) ++v;
+        return off[v] < 0 ? -1 : off[v] + (c - col0[v]);
+    };
+    const double *Hc = contrib + (size_t)i * kImuContrib, *bc = Hc + kImuLoc * kImuLoc;
+    for (int q = threadIdx.x; q < kImuLoc * kImuLoc; q += blockDim.x) {
+        const int a = q / kImuLoc, b = q % kImuLoc;
+        const int ra = red(a), rb = red(b);
+        if (ra < 0 || rb < 0 || rb > ra) continue;   // lower triangle of the reduced matrix
+        R.H[(size_t)ra * R.n + rb] += Hc[q];
+    }
+    if ((int)threadIdx.x < kImuLoc) {
+        const int ra = red(threadIdx.x);
+        if (ra >= 0) R.b[ra] += bc[threadIdx.x];
+    }
+}
+
+// Landmark part of buildSystem (64 landmarks per block).
+__global__ void __launch_bounds__(kLandWG) build_kernel(Rig rig, State s, Edges E, Land L, double delta, double dsqr,
+                                                        double delta_st, double dsqr_st, const double *err,
+                                                        const double *err3, const double *chi2, const LmCtl *ctl) {
+    if (!gate_open(ctl, kGateBuild)) return;
+    build_land_block(blockIdx.x, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
 }
 
 // H = 0, b = 0 before a build (one launch instead of two fills)
@@ -555,75 +631,77 @@ __global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, d
     Sp[q] = gc <= gr ? H[(size_t)gr * n + gc] + (gr == gc ? lambda : 0.0) : 0.0;
 }
 
-__global__ void __launch_bounds__(kLandWG) schur_kernel(Land L, Red R, BlockPat P, double lambda, double *S, double *coef,
-                                                        const LmCtl *ctl) {
-    __shared__ double acc[kSpan * kSpan * 36 / 2 + kSpan * 36 / 2 + kSpan * 6];   // lower block triangle + coef
+// Schur complement (block_solver.hpp:353-486), deterministic:
+//   schur_point_kernel  per landmark: Dinv = (Hll + lambda I)^-1, and per optimisable landmark slot a:
+//                       BD_a = Hpl_a Dinv, cs_a = Hpl_a Dinv bl
+//   schur_block_kernel  per reduced-system block (i, j): S_ij -= sum over its (a, b) terms of BD_a Hpl_b^T, and on
+//                       the diagonal coef_i = sum over keyframe i's slots of cs_a — gathered in ascending order,
+//                       fixed-order reductions, no atomics (results identical run to run)
+__global__ void __launch_bounds__(kLandWG) schur_point_kernel(Land L, Red R, double lambda, const LmCtl *ctl) {
     if (!gate_open(ctl, kGateTrial)) return;
     lambda = lm_lambda(ctl, lambda);
-    // block (a, b), a >= b, stored at ((a * (a + 1)) / 2 + b) * 36
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const int kf0 = L.wg_kf0[blockIdx.x];
-    const int nblk = kSpan * (kSpan + 1) / 2;
-    double *cacc = acc + nblk * 36;
-    for (int q = threadIdx.x; q < nblk * 36 + kSpan * 6; q += blockDim.x) acc[q] = 0;
-    __syncthreads();
-    if (p < L.n) {
-        double D[9], Dinv[9];
-        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
-        D[0] += lambda, D[4] += lambda, D[8] += lambda;
-        inv3(D, Dinv);
-        const double *bl = L.bl + (size_t)p * 3;
-        double db[3];
-        mv3(Dinv, bl, db);
-        const int s0 = L.slot_start[p], s1 = L.slot_start[p + 1];
-        for (int a = s0; a < s1; ++a) {
-            const int ka = L.slot_kf[a];
-            const int oa = R.offP[ka];
-            if (oa < 0) continue;
-            const double *Ba = L.Hpl + (size_t)a * 18;
-            double BD[18];
-            for (int r = 0; r < 6; ++r)
-                for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ba[3 * r] * Dinv[c] + Ba[3 * r + 1] * Dinv[3 + c] + Ba[3 * r + 2] * Dinv[6 + c];
-            const bool local_a = kf0 >= 0 && ka - kf0 >= 0 && ka - kf0 < kSpan;
-            for (int r = 0; r < 6; ++r) {
-                const double cv = Ba[3 * r] * db[0] + Ba[3 * r + 1] * db[1] + Ba[3 * r + 2] * db[2];
-                if (local_a) unsafeAtomicAdd(cacc + (ka - kf0) * 6 + r, cv);
-                else unsafeAtomicAdd(coef + oa + r, cv);
-            }
-            for (int b = s0; b < s1; ++b) {
-                const int kb = L.slot_kf[b];
-                const int ob = R.offP[kb];
-                if (ob < 0 || ob > oa) continue;   // lower triangle: row block oa >= col block ob
-                const double *Bb = L.Hpl + (size_t)b * 18;
-                const bool local = local_a && kb - kf0 >= 0 && kb - kf0 < kSpan;
-                const int la = ka - kf0, lb = kb - kf0;
-                // keyframe order == reduced order (offsets increase with keyframe index)
-                double *blk = local ? acc + ((la * (la + 1)) / 2 + lb) * 36 : nullptr;
-                for (int r = 0; r < 6; ++r)
-                    for (int c = 0; c < 6; ++c) {
-                        if (ob == oa && c > r) continue;
-                        const double v = BD[3 * r] * Bb[3 * c] + BD[3 * r + 1] * Bb[3 * c + 1] + BD[3 * r + 2] * Bb[3 * c + 2];
-                        if (local) unsafeAtomicAdd(blk + 6 * r + c, -v);
-                        else unsafeAtomicAdd(S + (size_t)P.slot[ka * P.nb + kb] * 256 + 16 * r + c, -v);
-                    }
-            }
+    if (p >= L.n) return;
+    double D[9], Dinv[9];
+    for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+    D[0] += lambda, D[4] += lambda, D[8] += lambda;
+    inv3(D, Dinv);
+    const double *bl = L.bl + (size_t)p * 3;
+    double db[3];
+    mv3(Dinv, bl, db);
+    for (int a = L.slot_start[p]; a < L.slot_start[p + 1]; ++a) {
+        if (R.offP[L.slot_kf[a]] < 0) continue;
+        const double *Ba = L.Hpl + (size_t)a * 18;
+        double *BD = L.BD + (size_t)a * 18, *cs = L.cs + (size_t)a * 6;
+        for (int r = 0; r < 6; ++r) {
+            for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ba[3 * r] * Dinv[c] + Ba[3 * r + 1] * Dinv[3 + c] + Ba[3 * r + 2] * Dinv[6 + c];
+            cs[r] = Ba[3 * r] * db[0] + Ba[3 * r + 1] * db[1] + Ba[3 * r + 2] * db[2];
         }
     }
-    __syncthreads();
-    if (kf0 >= 0) {
-        for (int q = threadIdx.x; q < nblk * 36; q += blockDim.x) {
-            if (acc[q] == 0.0) continue;
-            const int blk = q / 36, e = q % 36;
-            int la = 0;
-            while ((la + 1) * (la + 2) / 2 <= blk) ++la;
-            const int lb = blk - la * (la + 1) / 2;
-            const int ka = kf0 + la, kb = kf0 + lb;
-            unsafeAtomicAdd(S + (size_t)P.slot[ka * P.nb + kb] * 256 + 16 * (e / 6) + e % 6, acc[q]);
+}
+
+__global__ void __launch_bounds__(256) schur_block_kernel(Land L, Red R, BlockPat P, Gather G, double *S, double *coef,
+                                                          const LmCtl *ctl) {
+    __shared__ double wsum[4][42];
+    if (!gate_open(ctl, kGateTrial)) return;
+    const int t = blockIdx.x, bi = P.slot_i[t], bj = P.slot_j[t];
+    const int t0 = G.tr_start[t], t1 = G.tr_start[t + 1];
+    const bool diag = bi == bj;
+    if (t0 == t1 && !diag) return;   // fill-in block: no landmark term
+    double acc[42];
+#pragma unroll
+    for (int q = 0; q < 42; ++q) acc[q] = 0;
+    for (int i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+        const int2 ab = G.tr[i];
+        const double *BD = L.BD + (size_t)ab.x * 18, *Hb = L.Hpl + (size_t)ab.y * 18;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                acc[6 * r + c] += BD[3 * r] * Hb[3 * c] + BD[3 * r + 1] * Hb[3 * c + 1] + BD[3 * r + 2] * Hb[3 * c + 2];
+    }
+    if (diag)   // coef of this keyframe: its landmark slots' Hpl Dinv bl
+        for (int i = G.kf_slot_start[bi] + threadIdx.x; i < G.kf_slot_start[bi + 1]; i += blockDim.x) {
+            const double *cs = L.cs + (size_t)G.kf_slot[i] * 6;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) acc[36 + r] += cs[r];
         }
-        for (int q = threadIdx.x; q < kSpan * 6; q += blockDim.x) {
-            if (cacc[q] == 0.0) continue;
-            const int ka = kf0 + q / 6;
-            unsafeAtomicAdd(coef + R.offP[ka] + q % 6, cacc[q]);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 42; ++q) {
+        const double v = wave_sum_fixed(acc[q]);
+        if (lane == 0) wsum[wave][q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 42) {
+        const int q = threadIdx.x;
+        double v = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += wsum[w][q];
+        if (q < 36) {
+            const int r = q / 6, c = q % 6;
+            if (!diag || c <= r) S[(size_t)t * 256 + 16 * r + c] -= v;
+        } else if (diag) {
+            coef[R.offP[bi] + q - 36] = v;
         }
     }
 }
@@ -1077,6 +1155,10 @@ struct omv_lba {
     Red R{};
     Imu I{};
     BlockPat BP{};
+    Gather G{};
+    double *d_imu_contrib = nullptr;   // [n_imu][30 x 30 + 30] per-edge inertial contributions
+    int *d_imu_colour = nullptr;       // inertial edges grouped by colour (no shared keyframe within a colour)
+    std::vector<int> imu_colour_start;
     int n_wg_land = 0, n_wg_edge = 0;
     int *d_offP = nullptr, *d_offV = nullptr, *d_offG = nullptr, *d_offA = nullptr;
     double *d_err = nullptr, *d_chi2 = nullptr, *d_err9 = nullptr;
@@ -1259,15 +1341,22 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     pt_edge[P] = (int)e_pt.size();
     pt_slot[P] = (int)slot_kf.size();
     h->n_slots = (int)slot_kf.size();
-    // workgroup keyframe spans (kLandWG landmarks per workgroup)
     h->n_wg_land = (P + kLandWG - 1) / kLandWG;
-    std::vector<int> wg_kf0(std::max(1, h->n_wg_land), -1);
-    for (int g = 0; g < h->n_wg_land; ++g) {
-        int lo = 1 << 30, hi = -1;
-        for (int q = g * kLandWG; q < std::min(P, (g + 1) * kLandWG); ++q)
-            for (int s = pt_slot[q]; s < pt_slot[q + 1]; ++s)
-                if (slot_kf[s] < p->n_opt) lo = std::min(lo, slot_kf[s]), hi = std::max(hi, slot_kf[s]);
-        wg_kf0[g] = (hi >= 0 && hi - lo < kSpan) ? lo : (hi < 0 ? 0 : -1);
+    // per optimisable keyframe: its edges and its landmark slots, ascending (build_pose_kernel, schur_block_kernel)
+    std::vector<int> kf_edge_start(nb + 1, 0), kf_edge, kf_slot_start(nb + 1, 0), kf_slot;
+    for (int e = 0; e < E; ++e)
+        if (e_kf[e] < nb) ++kf_edge_start[e_kf[e] + 1];
+    for (int s2 = 0; s2 < h->n_slots; ++s2)
+        if (slot_kf[s2] < nb) ++kf_slot_start[slot_kf[s2] + 1];
+    for (int k = 0; k < nb; ++k)
+        kf_edge_start[k + 1] += kf_edge_start[k], kf_slot_start[k + 1] += kf_slot_start[k];
+    kf_edge.resize(kf_edge_start[nb]), kf_slot.resize(kf_slot_start[nb]);
+    {
+        std::vector<int> fe(kf_edge_start.begin(), kf_edge_start.end() - 1), fs(kf_slot_start.begin(), kf_slot_start.end() - 1);
+        for (int e = 0; e < E; ++e)
+            if (e_kf[e] < nb) kf_edge[fe[e_kf[e]]++] = e;
+        for (int s2 = 0; s2 < h->n_slots; ++s2)
+            if (slot_kf[s2] < nb) kf_slot[fs[slot_kf[s2]]++] = s2;
     }
     // inertial blocks + symbolic LDL^T fill-in
     for (int i = 0; i < NI; ++i) {
@@ -1291,6 +1380,24 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
                 slot_i.push_back(i), slot_j.push_back(j);
             }
     const int n_slots = (int)slot_i.size();
+    // Schur terms per block: landmark slots (a, b) of one landmark, keyframe(a) >= keyframe(b), both optimisable;
+    // grouped by block, each group in (landmark, a, b) order
+    std::vector<int> tr_start(n_slots + 1, 0);
+    std::vector<int2> tr;
+    {
+        auto each = [&](auto &&f) {
+            for (int q = 0; q < P; ++q)
+                for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
+                    if (slot_kf[a] < nb)
+                        for (int b = pt_slot[q]; b <= a; ++b)   // slots of a landmark ascend with the keyframe
+                            if (slot_kf[b] < nb) f(slot[slot_kf[a] * nb + slot_kf[b]], a, b);
+        };
+        each([&](int t, int, int) { ++tr_start[t + 1]; });
+        for (int t = 0; t < n_slots; ++t) tr_start[t + 1] += tr_start[t];
+        tr.resize(tr_start[n_slots]);
+        std::vector<int> fill(tr_start.begin(), tr_start.end() - 1);
+        each([&](int t, int a, int b) { tr[fill[t]++] = make_int2(a, b); });
+    }
     std::vector<int> pan_start(nb + 1, 0), pan, pair_start(nb + 1, 0);
     std::vector<int4> pair;
     for (int k = 0; k < nb; ++k) {
@@ -1382,16 +1489,28 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     if (!d_e_ur) return OMV_ERR_HIP;
     HIP_OK(up(d_e_ur, e_ur.data(), E));
     h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, d_e_ur, E};
-    int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots),
-        *d_wg = dalloc<int>(ow, wg_kf0.size());
+    int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots);
     double *d_Hll = dalloc<double>(ow, 9 * (size_t)P), *d_bl = dalloc<double>(ow, 3 * (size_t)P),
-           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots);
-    if (!d_Hpl) return OMV_ERR_HIP;
+           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots), *d_BD = dalloc<double>(ow, 18 * (size_t)h->n_slots),
+           *d_cs = dalloc<double>(ow, 6 * (size_t)h->n_slots);
+    if (!d_cs) return OMV_ERR_HIP;
     HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
     HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
     HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
-    HIP_OK(up(d_wg, wg_kf0.data(), wg_kf0.size()));
-    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_wg, d_Hll, d_bl, d_Hpl, P};
+    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_Hll, d_bl, d_Hpl, d_BD, d_cs, P};
+    {
+        int *d_kes = dalloc<int>(ow, nb + 1), *d_ke = dalloc<int>(ow, kf_edge.size()), *d_kss = dalloc<int>(ow, nb + 1),
+            *d_ks = dalloc<int>(ow, kf_slot.size()), *d_trs = dalloc<int>(ow, n_slots + 1);
+        int2 *d_tr = dalloc<int2>(ow, tr.size());
+        if (!d_tr) return OMV_ERR_HIP;
+        HIP_OK(up(d_kes, kf_edge_start.data(), nb + 1));
+        if (!kf_edge.empty()) HIP_OK(up(d_ke, kf_edge.data(), kf_edge.size()));
+        HIP_OK(up(d_kss, kf_slot_start.data(), nb + 1));
+        if (!kf_slot.empty()) HIP_OK(up(d_ks, kf_slot.data(), kf_slot.size()));
+        HIP_OK(up(d_trs, tr_start.data(), n_slots + 1));
+        if (!tr.empty()) HIP_OK(up(d_tr, tr.data(), tr.size()));
+        h->G = Gather{d_kes, d_ke, d_kss, d_ks, d_trs, d_tr};
+    }
     h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
     h->d_offA = dalloc<int>(ow, K);
     HIP_OK(up(h->d_offP, offP.data(), K));
@@ -1419,6 +1538,28 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         HIP_OK(up(d_rob, rob.data(), NI));
     }
     h->I = Imu{NI, d_k1, d_k2, d_pre, d_i9, d_iG, d_iA, d_rob, h->d_offP, h->d_offV, h->d_offG, h->d_offA};
+    {   // greedy edge colouring: an inertial edge takes the first colour neither of its keyframes holds yet
+        std::vector<int> colour(NI), n_col;
+        std::vector<std::vector<char>> used(K);
+        for (int i = 0; i < NI; ++i) {
+            auto &u1 = used[p->imu_kf1[i]], &u2 = used[p->imu_kf2[i]];
+            int c = 0;
+            while ((c < (int)u1.size() && u1[c]) || (c < (int)u2.size() && u2[c])) ++c;
+            u1.resize(std::max(u1.size(), (size_t)c + 1), 0), u2.resize(std::max(u2.size(), (size_t)c + 1), 0);
+            u1[c] = u2[c] = 1;
+            colour[i] = c;
+            if (c >= (int)n_col.size()) n_col.resize(c + 1, 0);
+            ++n_col[c];
+        }
+        h->imu_colour_start.assign(n_col.size() + 1, 0);
+        for (size_t c = 0; c < n_col.size(); ++c) h->imu_colour_start[c + 1] = h->imu_colour_start[c] + n_col[c];
+        std::vector<int> by(NI), fill(h->imu_colour_start.begin(), h->imu_colour_start.end() - 1);
+        for (int i = 0; i < NI; ++i) by[fill[colour[i]]++] = i;
+        h->d_imu_colour = dalloc<int>(ow, NI);
+        h->d_imu_contrib = dalloc<double>(ow, (size_t)NI * kImuContrib);
+        if (!h->d_imu_contrib) return OMV_ERR_HIP;
+        if (NI > 0) HIP_OK(up(h->d_imu_colour, by.data(), NI));
+    }
     // block pattern
     int *d_slot = dalloc<int>(ow, (size_t)nb * nb), *d_slot_i = dalloc<int>(ow, n_slots),
         *d_slot_j = dalloc<int>(ow, n_slots), *d_pan_start = dalloc<int>(ow, nb + 1), *d_pan = dalloc<int>(ow, pan.size()),
@@ -1558,6 +1699,43 @@ omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stere
 
 static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res);
 
+// buildSystem at state A: H = 0, the landmark blocks, the keyframe-diagonal visual terms, the inertial edges
+// colour by colour.  Every entry is a fixed-order sum: the system is identical run to run.
+static void launch_build(omv_lba *h, const State &A, const LmCtl *c) {
+    hipStream_t st = h->stream;
+    const int nred = h->n_red;
+    const size_t nH = (size_t)nred * nred;
+    zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, c);
+    if (h->n_pts > 0)
+        build_kernel<<<h->n_wg_land, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->delta_mono, h->dsqr_mono, h->delta_st,
+                                                       h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, c);
+    if (h->n_mono > 0 && h->n_opt > 0)
+        build_pose_kernel<<<h->n_opt, 256, 0, st>>>(h->rig, A, h->E, h->G, h->R, h->delta_mono, h->dsqr_mono,
+                                                    h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, c);
+    if (h->imu_here && h->n_imu > 0) {
+        imu_contrib_kernel<<<h->n_imu, kLandWG, 0, st>>>(A, h->I, h->delta_imu, h->dsqr_imu, h->d_err9,
+                                                         h->d_imu_contrib, c);
+        for (size_t k = 0; k + 1 < h->imu_colour_start.size(); ++k) {
+            const int n = h->imu_colour_start[k + 1] - h->imu_colour_start[k];
+            imu_add_kernel<<<n, kLandWG, 0, st>>>(h->I, h->R, h->d_imu_contrib, h->d_imu_colour + h->imu_colour_start[k],
+                                                  n, c);
+        }
+    }
+}
+
+// The trial's reduced system: pack H + lambda I into the block layout, then the Schur complement.
+static void launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
+    hipStream_t st = h->stream;
+    const int npk = std::max(h->BP.n_slots * 256, h->n_red);
+    // lambda on the pose diagonal once (rank 0 of a sharded solve); every rank damps its own landmarks
+    pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, h->n_red, h->BP, h->rank == 0 ? lambda : 0.0, h->d_S,
+                                                   h->d_coef, c);
+    if (h->n_pts > 0) {
+        schur_point_kernel<<<h->n_wg_land, kLandWG, 0, st>>>(h->L, h->R, lambda, c);
+        schur_block_kernel<<<h->BP.n_slots, 256, 0, st>>>(h->L, h->R, h->BP, h->G, h->d_S, h->d_coef, c);
+    }
+}
+
 // One LM step of the single-rank path: the gated kernel sequence (see LmCtl).  A = st[0] is always the
 // current state and B = st[1] the trial; an accepted trial is copied back into A on the device.  With `ev`,
 // events bracket the stages (build, Schur, solve, update + errors) for omv_lba_stage_ms.
@@ -1570,19 +1748,9 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     omv_status rs;
     if ((rs = lba_errors(h, A, c, kGateErrA, true)) != OMV_OK) return rs;   // after a rejected trial
     if (ev) HIP_OK(hipEventRecord(ev[0], st));
-    {
-        const size_t nH = (size_t)nred * nred;
-        zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, c);
-        const int nl = h->n_pts > 0 ? gl : 0, ni_blk = h->imu_here ? h->n_imu : 0;
-        if (nl + ni_blk > 0)
-            build_kernel<<<nl + ni_blk, kLandWG, 0, st>>>(nl, h->rig, A, h->E, h->L, h->R, h->delta_mono, h->dsqr_mono,
-                                                          h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, h->I,
-                                                          h->delta_imu, h->dsqr_imu, h->d_err9, c);
-    }
+    launch_build(h, A, c);
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
-    const int npk = std::max(h->BP.n_slots * 256, nred);
-    pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, 0.0, h->d_S, h->d_coef, c);
-    if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, 0.0, h->d_S, h->d_coef, c);
+    launch_schur(h, 0.0, c);
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
     if (h->use_lds)
         ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
@@ -1706,16 +1874,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         const double iniChi = currentChi;
         // buildSystem
         HIP_OK(hipEventRecord(h->ev[0], st));
-        {
-            const size_t nH = (size_t)nred * nred;
-            zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, nullptr);
-            const int nl = h->n_pts > 0 ? gl : 0, ni_blk = h->imu_here ? h->n_imu : 0;
-            if (nl + ni_blk > 0)
-                build_kernel<<<nl + ni_blk, kLandWG, 0, st>>>(nl, h->rig, A, h->E, h->L, h->R, h->delta_mono,
-                                                              h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err,
-                                                              h->d_err3, h->d_chi2, h->I, h->delta_imu, h->dsqr_imu,
-                                                              h->d_err9, nullptr);
-        }
+        launch_build(h, A, nullptr);
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -1729,11 +1888,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         bool build_timed = false;   // the build's events complete before the first trial's read-back
         do {
             HIP_OK(hipEventRecord(h->ev[2], st));
-            const int npk = std::max(h->BP.n_slots * 256, nred);
-            // lambda on the pose diagonal once (rank 0 of a sharded solve)
-            pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, nred, h->BP, h->rank == 0 ? lambda : 0.0, h->d_S,
-                                                           h->d_coef, nullptr);
-            if (h->n_pts > 0) schur_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, h->BP, lambda, h->d_S, h->d_coef, nullptr);
+            launch_schur(h, lambda, nullptr);
             const double *bsys = h->R.b;
             if (h->world > 1) {   // one exchange: sum the partial Schur systems of the landmark shards
                 HIP_OK(hipMemcpyAsync(h->d_bb, h->R.b, sizeof(double) * nred, hipMemcpyDeviceToDevice, st));

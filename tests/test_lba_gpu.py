@@ -200,9 +200,26 @@ def test_reoptimize_same_handle(small, oracle):
     r1, s1 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
     r2, s2 = ba.set_problem(small).optimize(opt_it=4, lambda_init=1e-2, large=True)
     assert r1["trials"] == r2["trials"]
-    # the device sums use float atomics (order varies run to run), so "the same answer" is the parity
-    # bar, not bit equality
     _compare_state(small, s2, s1, oracle)
+
+
+@pytest.mark.parametrize("driver", ["device", "host"])
+def test_bitwise_identical_run_to_run(full, driver):
+    """Every device reduction is a fixed-order sum (no float atomics): two solves of the bench window — on
+    fresh handles and on one reused handle — give bit-identical state, chi2, err / err_end and lambda."""
+    kw = dict(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    runs = []
+    ba = _solver(full).set_driver(driver == "host")
+    for h in (ba, ba, _solver(full).set_driver(driver == "host")):
+        r, s = h.set_problem(full).optimize(**kw)
+        runs.append((r, s))
+    r0, s0 = runs[0]
+    for r, s in runs[1:]:
+        for k in ("err", "err_end", "lambda_", "iterations", "trials", "status"):
+            assert r[k] == r0[k], (k, r[k], r0[k])
+        assert np.array_equal(r["mono_chi2"].view(np.uint64), r0["mono_chi2"].view(np.uint64))
+        for k in STATE:
+            assert np.array_equal(np.asarray(s[k]).view(np.uint64), np.asarray(s0[k]).view(np.uint64)), k
 
 
 @pytest.mark.parametrize("backend", ["gloo", "nccl"])
