@@ -268,7 +268,7 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
     for _ in range(steps):
         ba.reset()
         t0 = time.perf_counter()
-        res, _ = ba.optimize(**LBA_CFG)
+        res, _ = ba.optimize(**LBA_CFG, chi2=False)
         total += time.perf_counter() - t0
         trials += res["trials"]
     torch.cuda.synchronize(dev)

@@ -37,6 +37,7 @@
 #include <map>
 #include <numeric>
 #include <set>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/omv.h"
@@ -152,21 +153,6 @@ __device__ __forceinline__ void imu_err_block(double *sh, State s, Imu I, double
     if (threadIdx.x == 0) partial[0] = t;
 }
 
-// computeActiveErrors in one launch: blocks [0, n_mono_blocks) the visual edges (256 each), the block after
-// them (when has_imu) the inertial / random-walk edges.
-__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s, Edges E, double delta,
-                                                  double dsqr, double delta_st, double dsqr_st, double *err, double *err3,
-                                                  double *chi2, double *partial, Imu I, double delta_imu,
-                                                  double dsqr_imu, double *err9, double *imu_partial, const LmCtl *ctl,
-                                                  int gate) {
-    __shared__ double sh[8];
-    if (!gate_open(ctl, gate)) return;
-    if ((int)blockIdx.x < n_mono_blocks)
-        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, partial);
-    else if (has_imu)
-        imu_err_block(sh, s, I, delta_imu, dsqr_imu, err9, imu_partial);
-}
-
 // activeRobustChi2: inertial partial + visual partials in a fixed order (one block of 256).
 __device__ __forceinline__ double sum_chi(const double *mono_partial, int n_mono_blocks, const double *imu_partial,
                                           double *sh) {
@@ -209,11 +195,9 @@ __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *m
 //   errors recomputed this step when the last ones were a rejected trial's), qmax = 0;
 //   the trial: rho, accept (the trial state becomes current) or reject (lambda *= ni), then the do-while /
 //   iteration / nBad stop tests in the reference's order, and the next step's gates.
-__global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
-                                                           const double *imu_partial, const double *mono_partial_a,
-                                                           const double *imu_partial_a, const double *scale_partial,
-                                                           int n_scale, const int *fail) {
-    __shared__ double sh[8];
+__device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_partial, int n_mono_blocks,
+                                  const double *imu_partial, const double *mono_partial_a, const double *imu_partial_a,
+                                  const double *scale_partial, int n_scale, const int *fail) {
     if (!c->g_active) return;
     const bool errA = c->g_errA != 0;
     double chiA = 0;
@@ -280,6 +264,44 @@ __global__ void accept_copy_kernel(const LmCtl *c, const double *B, double *A, s
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (size_t)gridDim.x * blockDim.x) A[q] = B[q];
 }
 
+// A step's opening error launch also carries the copy B -> A of an accepted last trial (instead of the errors of
+// A, which are only recomputed after a rejected trial).
+struct ErrAux {
+    const double *copy_src;   // non-null: copy copy_n doubles to copy_dst when the last trial was accepted
+    double *copy_dst;
+    size_t copy_n;
+};
+
+// computeActiveErrors in one launch: blocks [0, n_mono_blocks) the visual edges (256 each), the block after
+// them (when has_imu) the inertial / random-walk edges.
+__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s, Edges E, double delta,
+                                                  double dsqr, double delta_st, double dsqr_st, double *err, double *err3,
+                                                  double *chi2, double *partial, Imu I, double delta_imu,
+                                                  double dsqr_imu, double *err9, double *imu_partial, const LmCtl *ctl,
+                                                  int gate, ErrAux aux) {
+    __shared__ double sh[8];
+    if (aux.copy_dst && ctl->accepted) {
+        for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < aux.copy_n; q += (size_t)gridDim.x * blockDim.x)
+            aux.copy_dst[q] = aux.copy_src[q];
+        return;
+    }
+    if (!gate_open(ctl, gate)) return;
+    if ((int)blockIdx.x < n_mono_blocks)
+        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, partial);
+    else if (has_imu)
+        imu_err_block(sh, s, I, delta_imu, dsqr_imu, err9, imu_partial);
+}
+
+// One LM step's bookkeeping after the trial's errors (one block of 256).
+__global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
+                                                           const double *imu_partial, const double *mono_partial_a,
+                                                           const double *imu_partial_a, const double *scale_partial,
+                                                           int n_scale, const int *fail) {
+    __shared__ double sh[8];
+    finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, mono_partial_a, imu_partial_a, scale_partial,
+                      n_scale, fail);
+}
+
 // Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
 __global__ void __launch_bounds__(256) finish_kernel(const double *mono_partial, int n_mono_blocks, const double *imu_partial,
                                                      const double *scale_partial, int n_scale, const int *fail,
@@ -304,24 +326,34 @@ struct Land {
     const int *edge_start;   // [P+1]
     const int *slot_start;   // [P+1]
     const int *slot_kf;      // [nslots]
+    const int *slot_pt;      // [nslots] the landmark of a slot
     double *Hll;             // [P][9]
     double *bl;              // [P][3]
     double *Hpl;             // [nslots][18] pose rows x point cols
-    double *BD;              // [nslots][18] Hpl Dinv (the trial's Schur operand)
-    double *cs;              // [nslots][6]  Hpl Dinv bl
     int n;
 };
 
-// Gather lists for the deterministic reductions (host-built once per problem, each in ascending order):
+// Work lists of the deterministic reductions (host-built once per problem, every list in ascending order).
+// Each reduction is split in chunks of at most 256 items; a chunk writes its fixed-order partial sum, and the
+// reduced-system block's assembly (the next launch) sums the chunk partials in chunk order, so every value is
+// identical run to run whatever the scheduling.
 struct Gather {
-    const int *kf_edge_start, *kf_edge;     // per optimisable keyframe: its visual edges
-    const int *kf_slot_start, *kf_slot;     // per optimisable keyframe: its landmark slots
-    const int *tr_start;                    // per reduced-system block (BlockPat slot): its Schur terms
-    const int2 *tr;                         //   (landmark slot a, landmark slot b), a's keyframe >= b's
+    const int4 *pchunk;      // pose chunks: (keyframe, first, end) over kf_edge
+    const int *kf_edge;      // per optimisable keyframe, its visual edges
+    const int *pc_start;     // [nb+1] per keyframe: its pose chunks
+    double *pose_part;       // [n_pchunk][27]: 21 lower-triangle JpT W Jp sums + 6 JpT W e
+    const int4 *schunk;      // Schur chunks: (block slot, first term, end term)
+    const int2 *tr;          // Schur terms (landmark slot a, landmark slot b) oriented to their block
+    const int *sc_start;     // [n_slots+1] per block: its Schur chunks
+    double *schur_part;      // [n_schunk][42]: 36 Hpl_a Dinv Hpl_b^T + 6 Hpl_a Dinv bl
+    const int4 *imu_blk;     // per block: inertial edges (edge, side of the block row, side of the column)
+    const int *ib_start;     // [n_slots+1]
+    const int2 *imu_vec;     // per keyframe: inertial edges (edge, side)
+    const int *iv_start;     // [nb+1]
+    const double *contrib;   // [n_imu][30 x 30 + 30] per-edge inertial quadratic forms
 };
 
-struct Red {   // reduced (non-marginalised) system, dense row-major n x n, lower triangle used
-    double *H, *b;
+struct Red {   // reduced (non-marginalised) system: 16 rows per optimisable keyframe
     int n;
     const int *offP;   // per keyframe, -1 for fixed
     int n_kf;
@@ -439,19 +471,17 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
     return v;
 }
 
-// Keyframe-diagonal visual terms of buildSystem: one workgroup per optimisable keyframe gathers its edges
-// (ascending edge order, strided over the threads), 21 + 6 sums per thread, then a fixed-order reduction.
-__global__ void __launch_bounds__(256) build_pose_kernel(Rig rig, State s, Edges E, Gather G, Red R, double delta,
-                                                         double dsqr, double delta_st, double dsqr_st,
-                                                         const double *err, const double *err3, const double *chi2,
-                                                         const LmCtl *ctl) {
-    __shared__ double wsum[4][27];
-    if (!gate_open(ctl, kGateBuild)) return;
-    const int k = blockIdx.x, o = R.offP[k];
+// Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= 256 edges of one keyframe, ascending) per
+// 64-thread block: lane l takes edges l, l+64, ...; 21 + 6 sums, a fixed-order wave reduction, one partial row.
+// The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled (schur_kernel).
+__device__ __forceinline__ void pose_chunk_block(int ch, Rig rig, State s, Edges E, Gather G, double delta, double dsqr,
+                                                 double delta_st, double dsqr_st, const double *err,
+                                                 const double *err3, const double *chi2) {
+    const int4 pc = G.pchunk[ch];
     double acc[27];
 #pragma unroll
     for (int q = 0; q < 27; ++q) acc[q] = 0;
-    for (int i = G.kf_edge_start[k] + threadIdx.x; i < G.kf_edge_start[k + 1]; i += blockDim.x) {
+    for (int i = pc.y + (int)threadIdx.x; i < pc.z; i += blockDim.x) {
         const int e = G.kf_edge[i];
         double JX[9], JP[18], w, om[3];
         const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
@@ -463,26 +493,14 @@ __global__ void __launch_bounds__(256) build_pose_kernel(Rig rig, State s, Edges
 #pragma unroll
         for (int r = 0; r < 6; ++r) acc[21 + r] += rows_om(JP, r, 6, om, nr);
     }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63;
+    double mine = 0;
 #pragma unroll
     for (int q = 0; q < 27; ++q) {
         const double t = wave_sum_fixed(acc[q]);
-        if (lane == 0) wsum[wave][q] = t;
+        mine = lane == q ? t : mine;
     }
-    __syncthreads();
-    if (threadIdx.x < 27 && o >= 0) {
-        const int q = threadIdx.x;
-        double t = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += wsum[w][q];
-        if (q < 21) {
-            int r = 0;
-            while ((r + 1) * (r + 2) / 2 <= q) ++r;
-            const int c = q - r * (r + 1) / 2;
-            R.H[(size_t)(o + r) * R.n + o + c] = t;   // the first contribution after the zeroing
-        } else {
-            R.b[o + q - 21] = t;
-        }
-    }
+    if (lane < 27) G.pose_part[(size_t)ch * 27 + lane] = mine;
 }
 
 // ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
@@ -554,155 +572,164 @@ __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Im
     }
 }
 
-__global__ void __launch_bounds__(kLandWG) imu_contrib_kernel(State s, Imu I, double delta, double dsqr,
-                                                              const double *err9, double *contrib, const LmCtl *ctl) {
+// buildSystem in one launch of 64-thread blocks: [0, n_land) the landmark blocks (Hll, bl, Hpl per slot),
+// [n_land, n_land + n_pchunk) the keyframe-diagonal pose chunks, then one block per inertial edge (its 30 x 30
+// quadratic form).  Nothing is accumulated across blocks: the reduced system is assembled per trial by
+// schur_kernel from these per-landmark, per-chunk and per-edge parts.
+__global__ void __launch_bounds__(kLandWG) build_kernel(Rig rig, State s, Edges E, Land L, Gather G, Imu I, int n_land,
+                                                        int n_pchunk, double delta, double dsqr, double delta_st,
+                                                        double dsqr_st, double delta_imu, double dsqr_imu,
+                                                        const double *err, const double *err3, const double *chi2,
+                                                        const double *err9, double *contrib, const LmCtl *ctl) {
     __shared__ double sm[441];
     if (!gate_open(ctl, kGateBuild)) return;
-    imu_contrib_block(blockIdx.x, sm, s, I, delta, dsqr, err9, contrib);
+    const int blk = blockIdx.x;
+    if (blk < n_land) build_land_block(blk, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+    else if (blk < n_land + n_pchunk)
+        pose_chunk_block(blk - n_land, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+    else imu_contrib_block(blk - n_land - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
 }
 
-// Adds the inertial slots of one colour class (no two of its edges share a keyframe, so every reduced-system
-// entry receives at most one term per launch; the classes run in a fixed order after build_pose_kernel).
-__global__ void __launch_bounds__(kLandWG) imu_add_kernel(Imu I, Red R, const double *contrib, const int *edges, int n,
-                                                          const LmCtl *ctl) {
-    if (!gate_open(ctl, kGateBuild)) return;
-    if ((int)blockIdx.x >= n) return;
-    const int i = edges[blockIdx.x];
-    const int k1 = I.kf1[i], k2 = I.kf2[i];
-    const int off[8] = {I.offP[k1], I.offV[k1], I.offG[k1], I.offA[k1], I.offP[k2], I.offV[k2], I.offG[k2], I.offA[k2]};
-    const int col0[9] = {0, 6, 9, 12, 15, 21, 24, 27, 30};
-    auto red = [&](int c) {
-        int v = 0;
-        while (v < 7 && c >= col0[v + 1]) ++v;
-        return off[v] < 0 ? -1 : off[v] + (c - col0[v]);
-    };
-    const double *Hc = contrib + (size_t)i * kImuContrib, *bc = Hc + kImuLoc * kImuLoc;
-    for (int q = threadIdx.x; q < kImuLoc * kImuLoc; q += blockDim.x) {
-        const int a = q / kImuLoc, b = q % kImuLoc;
-        const int ra = red(a), rb = red(b);
-        if (ra < 0 || rb < 0 || rb > ra) continue;   // lower triangle of the reduced matrix
-        R.H[(size_t)ra * R.n + rb] += Hc[q];
-    }
-    if ((int)threadIdx.x < kImuLoc) {
-        const int ra = red(threadIdx.x);
-        if (ra >= 0) R.b[ra] += bc[threadIdx.x];
-    }
-}
-
-// Landmark part of buildSystem (64 landmarks per block).
-__global__ void __launch_bounds__(kLandWG) build_kernel(Rig rig, State s, Edges E, Land L, double delta, double dsqr,
-                                                        double delta_st, double dsqr_st, const double *err,
-                                                        const double *err3, const double *chi2, const LmCtl *ctl) {
-    if (!gate_open(ctl, kGateBuild)) return;
-    build_land_block(blockIdx.x, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-}
-
-// H = 0, b = 0 before a build (one launch instead of two fills)
-__global__ void zero_kernel(double *H, size_t nH, double *b, int nb, const LmCtl *ctl) {
-    if (!gate_open(ctl, kGateBuild)) return;
-    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nH) H[q] = 0.0;
-    if (q < (size_t)nb) b[q] = 0.0;
-}
-
-// ---- trial: Schur complement into the packed block layout ------------------------------------------
+// ---- trial: the reduced system, assembled and Schur-complemented per block -----------------------------
 // The reduced system is stored as 16x16 blocks (keyframe block = pose 6 | v 3 | bg 3 | ba 3 | pad 1,
-// padded to one f64 MFMA tile): slot(i, j) for block row i >= block column j on the symbolic LDL^T
-// pattern (fill-in included), row-major 16x16 each.  Padding rows have zero gradient and lambda on
-// the diagonal, so they solve to exactly zero and add nothing to computeScale.
+// padded to one f64 MFMA tile) on the symbolic LDL^T pattern (fill-in included) of the elimination order
+// `perm` (position -> keyframe, host-chosen, see plan_order): slot(pi, pj) for block row pi >= block column
+// pj, row-major 16x16 each, holding H's block (perm[pi], perm[pj]).  Padding rows have zero gradient and
+// lambda on the diagonal, so they solve to exactly zero and add nothing to computeScale.  b and the Schur
+// right-hand side stay in keyframe order (16 k + r).
 struct BlockPat {
-    int nb, n_slots;
-    const int *slot;                 // [nb*nb] slot of block (i, j), i >= j; -1 structurally zero
-    const int *slot_i, *slot_j;      // [n_slots]
-    const int *pan_start, *pan;      // step k's panel: blocks i > k with slot(i, k) >= 0
-    const int *pair_start;           // step k's trailing updates (i >= j > k, both in the panel)
-    const int4 *pair;                // (slot(i,j), slot(i,k), slot(j,k), 0)
+    int nb, n_slots, n_lev;
+    const int *perm;                 // [nb] position -> keyframe
+    const int *slot_kr, *slot_kc;    // [n_slots] keyframes of the block's row / column
+    const int *dslot;                // [nb] diagonal slot per position
+    const int *lev_start, *lev_col;  // elimination-tree levels: the positions of level l
+    const int *pt_start;             // [n_lev+1] panel tasks of a level
+    const int2 *pt;                  //   (slot(i, k), dslot(k))
+    const int *ug_start;             // [n_lev+1] update groups of a level (one target block each)
+    const int *ug_task_start;        // [n_groups+1]
+    const int4 *ug;                  //   (slot(i, j), slot(i, k), slot(j, k), dslot(k)), ascending k
+    const int *rs_start;             // [nb+1] row structure of position i: (slot(i, k), k), k < i
+    const int2 *rs;
+    const int *cs_start;             // [nb+1] column structure of position k: (slot(i, k), i), i > k
+    const int2 *cs;
 };
 
-__global__ void pack_kernel(const double *H, int n, BlockPat P, double lambda, double *Sp, double *coef,
-                            const LmCtl *ctl) {
-    if (!gate_open(ctl, kGateTrial)) return;
-    lambda = lm_lambda(ctl, lambda);
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < n) coef[q] = 0;
-    if (q >= P.n_slots * 256) return;
-    const int sl = q >> 8, e = q & 255, r = e >> 4, c = e & 15;
-    const int gr = 16 * P.slot_i[sl] + r, gc = 16 * P.slot_j[sl] + c;
-    Sp[q] = gc <= gr ? H[(size_t)gr * n + gc] + (gr == gc ? lambda : 0.0) : 0.0;
-}
-
-// Schur complement (block_solver.hpp:353-486), deterministic:
-//   schur_point_kernel  per landmark: Dinv = (Hll + lambda I)^-1, and per optimisable landmark slot a:
-//                       BD_a = Hpl_a Dinv, cs_a = Hpl_a Dinv bl
-//   schur_block_kernel  per reduced-system block (i, j): S_ij -= sum over its (a, b) terms of BD_a Hpl_b^T, and on
-//                       the diagonal coef_i = sum over keyframe i's slots of cs_a — gathered in ascending order,
-//                       fixed-order reductions, no atomics (results identical run to run)
-__global__ void __launch_bounds__(kLandWG) schur_point_kernel(Land L, Red R, double lambda, const LmCtl *ctl) {
-    if (!gate_open(ctl, kGateTrial)) return;
-    lambda = lm_lambda(ctl, lambda);
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= L.n) return;
-    double D[9], Dinv[9];
-    for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
-    D[0] += lambda, D[4] += lambda, D[8] += lambda;
-    inv3(D, Dinv);
-    const double *bl = L.bl + (size_t)p * 3;
-    double db[3];
-    mv3(Dinv, bl, db);
-    for (int a = L.slot_start[p]; a < L.slot_start[p + 1]; ++a) {
-        if (R.offP[L.slot_kf[a]] < 0) continue;
-        const double *Ba = L.Hpl + (size_t)a * 18;
-        double *BD = L.BD + (size_t)a * 18, *cs = L.cs + (size_t)a * 6;
-        for (int r = 0; r < 6; ++r) {
-            for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ba[3 * r] * Dinv[c] + Ba[3 * r + 1] * Dinv[3 + c] + Ba[3 * r + 2] * Dinv[6 + c];
-            cs[r] = Ba[3 * r] * db[0] + Ba[3 * r + 1] * db[1] + Ba[3 * r + 2] * db[2];
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) schur_block_kernel(Land L, Red R, BlockPat P, Gather G, double *S, double *coef,
-                                                          const LmCtl *ctl) {
+// Per chunk of one block's Schur terms (<= 256 landmark slot pairs (a, b), one per thread): Dinv = (Hll +
+// lambda I)^-1 of the landmark, BD = Hpl_a Dinv, the 6x6 term BD Hpl_b^T and, on a diagonal block (a == b),
+// Hpl_a Dinv bl (block_solver.hpp:353-486); a fixed-order reduction into the chunk's partial.
+__global__ void __launch_bounds__(256) schur_kernel(Land L, Gather G, BlockPat P, double lambda, const LmCtl *ctl) {
     __shared__ double wsum[4][42];
     if (!gate_open(ctl, kGateTrial)) return;
-    const int t = blockIdx.x, bi = P.slot_i[t], bj = P.slot_j[t];
-    const int t0 = G.tr_start[t], t1 = G.tr_start[t + 1];
-    const bool diag = bi == bj;
-    if (t0 == t1 && !diag) return;   // fill-in block: no landmark term
+    lambda = lm_lambda(ctl, lambda);
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const int4 sc = G.schunk[ch];
+    const int t = sc.x;
+    const int kr = P.slot_kr[t], kc = P.slot_kc[t];
+    const bool diag = kr == kc;
     double acc[42];
 #pragma unroll
     for (int q = 0; q < 42; ++q) acc[q] = 0;
-    for (int i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    const int i = sc.y + tid;
+    if (i < sc.z) {
         const int2 ab = G.tr[i];
-        const double *BD = L.BD + (size_t)ab.x * 18, *Hb = L.Hpl + (size_t)ab.y * 18;
+        const int p = L.slot_pt[ab.x];
+        double D[9], Dinv[9];
+        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+        D[0] += lambda, D[4] += lambda, D[8] += lambda;
+        inv3(D, Dinv);
+        const double *Ha = L.Hpl + (size_t)ab.x * 18, *Hb = L.Hpl + (size_t)ab.y * 18;
+        double BD[18];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ha[3 * r] * Dinv[c] + Ha[3 * r + 1] * Dinv[3 + c] + Ha[3 * r + 2] * Dinv[6 + c];
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-                acc[6 * r + c] += BD[3 * r] * Hb[3 * c] + BD[3 * r + 1] * Hb[3 * c + 1] + BD[3 * r + 2] * Hb[3 * c + 2];
-    }
-    if (diag)   // coef of this keyframe: its landmark slots' Hpl Dinv bl
-        for (int i = G.kf_slot_start[bi] + threadIdx.x; i < G.kf_slot_start[bi + 1]; i += blockDim.x) {
-            const double *cs = L.cs + (size_t)G.kf_slot[i] * 6;
+                acc[6 * r + c] = BD[3 * r] * Hb[3 * c] + BD[3 * r + 1] * Hb[3 * c + 1] + BD[3 * r + 2] * Hb[3 * c + 2];
+        if (diag) {
+            const double *bl = L.bl + (size_t)p * 3;
+            double db[3];
+            mv3(Dinv, bl, db);
 #pragma unroll
-            for (int r = 0; r < 6; ++r) acc[36 + r] += cs[r];
+            for (int r = 0; r < 6; ++r) acc[36 + r] = Ha[3 * r] * db[0] + Ha[3 * r + 1] * db[1] + Ha[3 * r + 2] * db[2];
         }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    }
+    const int wave = tid >> 6, lane = tid & 63;
+    {
+        double mine = 0;
 #pragma unroll
-    for (int q = 0; q < 42; ++q) {
-        const double v = wave_sum_fixed(acc[q]);
-        if (lane == 0) wsum[wave][q] = v;
+        for (int q = 0; q < 42; ++q) {
+            const double v = wave_sum_fixed(acc[q]);
+            mine = lane == q ? v : mine;
+        }
+        if (lane < 42) wsum[wave][lane] = mine;
     }
     __syncthreads();
-    if (threadIdx.x < 42) {
-        const int q = threadIdx.x;
-        double v = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += wsum[w][q];
-        if (q < 36) {
-            const int r = q / 6, c = q % 6;
-            if (!diag || c <= r) S[(size_t)t * 256 + 16 * r + c] -= v;
-        } else if (diag) {
-            coef[R.offP[bi] + q - 36] = v;
+    if (tid < 42) G.schur_part[(size_t)ch * 42 + tid] = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+}
+
+// sum_{i = from}^{to - 1} base[i * stride] in index order, loads issued four at a time (same order of the adds)
+__device__ __forceinline__ double ordered_sum(const double *base, int from, int to, int stride) {
+    double s = 0;
+    int i = from;
+    for (; i + 4 <= to; i += 4) {
+        const double a0 = base[(size_t)i * stride], a1 = base[(size_t)(i + 1) * stride],
+                     a2 = base[(size_t)(i + 2) * stride], a3 = base[(size_t)(i + 3) * stride];
+        s += a0;
+        s += a1;
+        s += a2;
+        s += a3;
+    }
+    for (; i < to; ++i) s += base[(size_t)i * stride];
+    return s;
+}
+
+// One block per reduced-system block: H's block (the keyframe-diagonal pose chunks, the inertial edges touching
+// it) + lambda on the diagonal - the Schur chunk partials in chunk order, and on a diagonal block the keyframe's
+// b and Schur right-hand side.  `pose_lambda` is 0 on the ranks > 0 of a sharded solve (lambda enters once).
+__global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat P, double lambda, int pose_lambda,
+                                                       double *S, double *bvec, double *coef, const LmCtl *ctl) {
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int kr = P.slot_kr[t], kc = P.slot_kc[t];
+    const bool diag = kr == kc;
+    const int c0 = G.sc_start[t], c1 = G.sc_start[t + 1];
+    const int r = tid >> 4, c = tid & 15;
+    double v = 0;
+    if (!diag || c <= r) {
+        if (diag && r < 6) {   // keyframe-diagonal visual terms
+            v += ordered_sum(G.pose_part + r * (r + 1) / 2 + c, G.pc_start[kr], G.pc_start[kr + 1], 27);
         }
+        if (r < 15 && c < 15) {   // inertial edges touching the block (variable groups present in the system)
+            const bool rows_ok = r < 6 || I.offV[kr] >= 0, cols_ok = c < 6 || I.offV[kc] >= 0;
+            if (rows_ok && cols_ok)
+                for (int q = G.ib_start[t]; q < G.ib_start[t + 1]; ++q) {
+                    const int4 e = G.imu_blk[q];
+                    v += G.contrib[(size_t)e.x * kImuContrib + (15 * e.y + r) * kImuLoc + 15 * e.z + c];
+                }
+        }
+        if (diag && r == c && pose_lambda) v += lambda;
+        if (r < 6 && c < 6) {
+            v -= ordered_sum(G.schur_part + 6 * r + c, c0, c1, 42);
+        }
+    }
+    S[(size_t)t * 256 + tid] = v;
+    if (diag && tid < 16) {   // b and the Schur right-hand side of keyframe kr
+        double bv = 0, cf = 0;
+        if (tid < 6) {
+            bv = ordered_sum(G.pose_part + 21 + tid, G.pc_start[kr], G.pc_start[kr + 1], 27);
+            cf = ordered_sum(G.schur_part + 36 + tid, c0, c1, 42);
+        }
+        if (tid < 15 && (tid < 6 || I.offV[kr] >= 0))
+            for (int q = G.iv_start[kr]; q < G.iv_start[kr + 1]; ++q) {
+                const int2 e = G.imu_vec[q];
+                bv += G.contrib[(size_t)e.x * kImuContrib + kImuLoc * kImuLoc + 15 * e.y + tid];
+            }
+        bvec[16 * kr + tid] = bv;
+        coef[16 * kr + tid] = cf;
     }
 }
 
@@ -840,6 +867,37 @@ __device__ __forceinline__ void update16(double *Sij, const double *Lik, const d
 constexpr int kLdltThreads = 512;
 constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (the static part is one int)
 
+// Forward substitution of one column (one wavefront): y_i <- L_ii^-1 (y_i - sum_k L_ik y_k) over the row
+// structure, four blocks at a time (lane groups), then the unit lower inverse stored above the diagonal.
+__device__ __forceinline__ void forward_col(const double *pk, double *y, const BlockPat &P, int i, int lane) {
+    const int r16 = lane & 15, grp = lane >> 4;
+    double acc = 0;
+    for (int q = P.rs_start[i] + grp; q < P.rs_start[i + 1]; q += 4) {
+        const int2 e = P.rs[q];
+        const double *Lik = pk + (size_t)e.x * 256 + r16 * 16;
+        const double *yk = y + 16 * e.y;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc += Lik[m] * yk[m];
+    }
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    const double v = y[16 * i + r16] - acc;
+    const double *Di = pk + (size_t)P.dslot[i] * 256;
+    double out = v;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const double vm = __shfl(v, m, 16);
+        out += (m < r16 ? Di[m * 16 + r16] : 0.0) * vm;
+    }
+    if (lane < 16) y[16 * i + lane] = out;
+}
+
+// Block LDL^T on the host-planned elimination order, level by level of its elimination tree: the columns of
+// one level are independent (their trailing updates only reach ancestors, at higher levels), so a level's
+// diagonal factors run on separate wavefronts, then its panels, then its trailing updates -- grouped by
+// target block, each group on one wavefront in ascending column order (no two wavefronts write a block).
+// Forward substitution runs beside the panels of each column's level (gathering its row structure: descendants,
+// final by then), backward substitution gathers each column's structure (ancestors) level by level downwards.
 template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
 __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat P, const double *b,
                                                             const double *coef, double *x, double *gscratch,
@@ -855,158 +913,114 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     if (tid == 0) bad = 0;
 #ifdef OMV_LDLT_PROFILE
     const long long t_0 = wall_clock64();
-    long long t_1 = 0, t_2 = 0, t_3 = 0, pf_fac = 0, pf_pan = 0, pf_upd = 0;
+    long long t_1 = 0, t_2 = 0, t_3 = 0;
 #endif
     {
         const double2 *src = (const double2 *)Sp;
         double2 *dst = (double2 *)pk;
         for (int q = tid; q < P.n_slots * 128; q += blockDim.x) dst[q] = src[q];
-        for (int q = tid; q < nv; q += blockDim.x) y[q] = b[q] - coef[q];
+        for (int q = tid; q < nv; q += blockDim.x) {
+            const int g = 16 * P.perm[q >> 4] + (q & 15);
+            y[q] = b[g] - coef[g];
+        }
     }
     __syncthreads();
-    for (int k = 0; k < nb; ++k) {
-        double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
 #ifdef OMV_LDLT_PROFILE
-        long long ta = wall_clock64();
+    long long pf_fac = 0, pf_pan = 0, pf_upd = 0, tp = wall_clock64();
+#define OMV_LDLT_TICK(acc)                       \
+    {                                            \
+        const long long tn = wall_clock64();     \
+        acc += tn - tp;                          \
+        tp = tn;                                 \
+    }
+#else
+#define OMV_LDLT_TICK(acc)
 #endif
-        if (wave == 0) factor16<G>(Dk, lane, &bad);
+    for (int lev = 0; lev < P.n_lev; ++lev) {
+        for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw)
+            factor16<G>(pk + (size_t)P.dslot[P.lev_col[c]] * 256, lane, &bad);
         __syncthreads();
-#ifdef OMV_LDLT_PROFILE
-        long long tb = wall_clock64();
-        pf_fac += tb - ta;
-#endif
-        const int p0 = P.pan_start[k], p1 = P.pan_start[k + 1];
-        for (int p = p0 + wave; p < p1; p += nw) panel16(pk + (size_t)P.slot[P.pan[p] * nb + k] * 256, Dk, lane);
-        __syncthreads();
-#ifdef OMV_LDLT_PROFILE
-        long long tc = wall_clock64();
-        pf_pan += tc - tb;
-#endif
-        const int q0 = P.pair_start[k], q1 = P.pair_start[k + 1];
-        for (int q = q0 + wave; q < q1; q += nw) {
-            const int4 pr = P.pair[q];
-            update16(pk + (size_t)pr.x * 256, pk + (size_t)pr.y * 256, pk + (size_t)pr.z * 256, Dk, lane);
+        OMV_LDLT_TICK(pf_fac)
+        // panels of the level's columns, and beside them each column's forward substitution (its row structure
+        // holds descendants only, final since their levels): y_i <- L_ii^-1 (y_i - sum_k L_ik y_k), with
+        // W = L_ii^-1 stored transposed above the diagonal
+        const int p0 = P.pt_start[lev], p1 = P.pt_start[lev + 1], c0 = P.lev_start[lev];
+        const int nt = p1 - p0 + P.lev_start[lev + 1] - c0;
+        for (int q = wave; q < nt; q += nw) {
+            if (q < p1 - p0) {
+                const int2 pt = P.pt[p0 + q];
+                panel16(pk + (size_t)pt.x * 256, pk + (size_t)pt.y * 256, lane);
+            } else {
+                forward_col(pk, y, P, P.lev_col[c0 + q - (p1 - p0)], lane);
+            }
         }
         __syncthreads();
-#ifdef OMV_LDLT_PROFILE
-        pf_upd += wall_clock64() - tc;
-#endif
+        OMV_LDLT_TICK(pf_pan)
+        const int g0 = P.ug_start[lev], g1 = P.ug_start[lev + 1];
+        if (g1 > g0) {
+            for (int g = g0 + wave; g < g1; g += nw)
+                for (int q = P.ug_task_start[g]; q < P.ug_task_start[g + 1]; ++q) {
+                    const int4 u = P.ug[q];
+                    update16(pk + (size_t)u.x * 256, pk + (size_t)u.y * 256, pk + (size_t)u.z * 256,
+                             pk + (size_t)u.w * 256, lane);
+                }
+            __syncthreads();
+        }
+        OMV_LDLT_TICK(pf_upd)
     }
+#undef OMV_LDLT_TICK
 #ifdef OMV_LDLT_PROFILE
     t_1 = wall_clock64();
 #endif
-    if (wave == 0) {
-        // forward: y_k <- L_kk^-1 y_k, then y_i -= L_ik y_k for the panel (four blocks per pass)
-        for (int k = 0; k < nb; ++k) {
-            const double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
-            const int r16 = lane & 15;
-            double v = y[16 * k + r16];
+    const int r16 = lane & 15, grp = lane >> 4;
+#ifdef OMV_LDLT_PROFILE
+    t_2 = wall_clock64();
+#endif
+    for (int q = tid; q < nv; q += blockDim.x) y[q] /= pk[(size_t)P.dslot[q >> 4] * 256 + (q & 15) * 17];
+    __syncthreads();
+    // backward: x_k = L_kk^-T (z_k - sum_i L_ik^T x_i)
+    for (int lev = P.n_lev - 1; lev >= 0; --lev) {
+        for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw) {
+            const int k = P.lev_col[c];
+            double acc = 0;
+            for (int q = P.cs_start[k] + grp; q < P.cs_start[k + 1]; q += 4) {
+                const int2 e = P.cs[q];
+                const double *Lik = pk + (size_t)e.x * 256 + r16;
+                const double *xi = xs + 16 * e.y;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc += Lik[r * 16] * xi[r];
+            }
+            acc += __shfl_xor(acc, 16, 64);
+            acc += __shfl_xor(acc, 32, 64);
+            const double v = y[16 * k + r16] - acc;
+            const double *row = pk + (size_t)P.dslot[k] * 256 + r16 * 16;
+            double out = v;
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
-                const double w = Dk[m * 16 + r16];
-                v += (m < r16 ? w : 0.0) * y[16 * k + m];
+                const double vm = __shfl(v, m, 16);
+                out += (m > r16 ? row[m] : 0.0) * vm;
             }
-            wave_sync<G>();
-            if (lane < 16) y[16 * k + lane] = v;
-            wave_sync<G>();
-            for (int p = P.pan_start[k]; p < P.pan_start[k + 1]; p += 4) {
-                const int pp = p + (lane >> 4);
-                if (pp < P.pan_start[k + 1]) {
-                    const int i = P.pan[pp];
-                    const double *Lik = pk + (size_t)P.slot[i * nb + k] * 256 + r16 * 16;
-                    double acc = 0;
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) acc += Lik[m] * y[16 * k + m];
-                    y[16 * i + r16] -= acc;
-                }
-            }
-            wave_sync<G>();
+            if (lane < 16) xs[16 * k + lane] = out;
         }
-#ifdef OMV_LDLT_PROFILE
-        t_2 = wall_clock64();
-#endif
-        for (int q = lane; q < nv; q += 64) y[q] /= pk[(size_t)P.slot[(q >> 4) * nb + (q >> 4)] * 256 + (q & 15) * 17];
-        wave_sync<G>();
-        // backward: r_k = z_k - sum_i L_ik^T x_i, x_k = L_kk^-T r_k
-        for (int k = nb - 1; k >= 0; --k) {
-            const double *Dk = pk + (size_t)P.slot[k * nb + k] * 256;
-            const int c16 = lane & 15;
-            {
-                // lanes 16p + c: panel block p's contribution to entry c, summed over the four groups
-                double v = 0;
-                for (int p = P.pan_start[k] + (lane >> 4); p < P.pan_start[k + 1]; p += 4) {
-                    const int i = P.pan[p];
-                    const double *Lik = pk + (size_t)P.slot[i * nb + k] * 256 + c16;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v += Lik[r * 16] * xs[16 * i + r];
-                }
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
-                if (lane < 16) y[16 * k + lane] -= v;
-            }
-            wave_sync<G>();
-            {
-                double v = y[16 * k + c16];
-                const double *row = Dk + c16 * 16;
-#pragma unroll
-                for (int m = 0; m < 16; ++m) v += (m > c16 ? row[m] : 0.0) * y[16 * k + m];
-                if (lane < 16) xs[16 * k + lane] = v;
-            }
-            wave_sync<G>();
-        }
+        __syncthreads();
     }
 #ifdef OMV_LDLT_PROFILE
     t_3 = wall_clock64();
     if (tid == 0)
-        printf("ldlt ticks(100MHz): factor %lld (diag %lld panel %lld update %lld) fwd %lld bwd %lld slots %d\n",
-               t_1 - t_0, pf_fac, pf_pan, pf_upd, t_2 - t_1, t_3 - t_2, P.n_slots);
+        printf("ldlt ticks(100MHz): factor+fwd %lld (diag %lld panel+fwd %lld update %lld) scale %lld bwd %lld slots %d "
+               "levels %d\n", t_1 - t_0, pf_fac, pf_pan, pf_upd, t_2 - t_1, t_3 - t_2, P.n_slots, P.n_lev);
 #endif
-    __syncthreads();
-    for (int q = tid; q < nv; q += blockDim.x) x[q] = xs[q];
+    for (int q = tid; q < nv; q += blockDim.x) x[16 * P.perm[q >> 4] + (q & 15)] = xs[q];
     if (tid == 0) *fail = bad;
 }
 
-// ---- trial: back-substitution + updates + scale ----------------------------------------------------
-__global__ void __launch_bounds__(kLandWG) backsub_kernel(Land L, Red R, double lambda, const double *xp, State a, State bst,
-                                                      double *scale_partial, const LmCtl *ctl) {
-    __shared__ double sh[8];
-    if (!gate_open(ctl, kGateTrial)) return;
-    lambda = lm_lambda(ctl, lambda);
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    double sc = 0;
-    if (p < L.n) {
-        double D[9], Dinv[9];
-        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
-        D[0] += lambda, D[4] += lambda, D[8] += lambda;
-        inv3(D, Dinv);
-        const double *bl = L.bl + (size_t)p * 3;
-        double c[3] = {bl[0], bl[1], bl[2]};
-        for (int s = L.slot_start[p]; s < L.slot_start[p + 1]; ++s) {
-            const int o = R.offP[L.slot_kf[s]];
-            if (o < 0) continue;
-            const double *B = L.Hpl + (size_t)s * 18;
-            for (int q = 0; q < 3; ++q)
-                for (int r = 0; r < 6; ++r) c[q] -= B[3 * r + q] * xp[o + r];
-        }
-        double xl[3];
-        mv3(Dinv, c, xl);
-        for (int q = 0; q < 3; ++q) {
-            bst.pts[(size_t)p * 3 + q] = a.pts[(size_t)p * 3 + q] + xl[q];
-            sc += xl[q] * (lambda * xl[q] + bl[q]);
-        }
-    }
-    const double t = block_reduce_sum(sc, sh);
-    if (threadIdx.x == 0) scale_partial[blockIdx.x] = t;
-}
-
-
-// ImuCamPose::Update (G2oTypes.cc:211-235) + vertex adds; the pose part of computeScale.
-__global__ void update_kf_kernel(Rig rig, Red R, const double *b, const int *offV, const int *offG, const int *offA,
-                                 int n_opt, double lambda, const double *xp, State a, State bst, double *scale_partial,
-                                 const LmCtl *ctl) {
-    __shared__ double sh[8];
-    if (!gate_open(ctl, kGateTrial)) return;
-    lambda = lm_lambda(ctl, lambda);
+// ---- trial: keyframe update + landmark back-substitution + computeScale terms, one launch ----------------
+// Block 0: ImuCamPose::Update (G2oTypes.cc:211-235) + the velocity / bias vertex adds for every optimisable
+// keyframe and the pose part of computeScale (scale_partial[0]); blocks 1..: one thread per landmark, the
+// back-substitution xl = Dinv (bl - Hpl^T xp), the point update and the landmark part (scale_partial[blk]).
+__device__ __forceinline__ void update_kf_block(double *sh, Rig rig, Red R, const double *b, const int *offV,
+                                                const int *offG, const int *offA, int n_opt, double lambda,
+                                                const double *xp, State a, State bst, double *scale_partial) {
     const int C = rig.n_cams;
     for (int k = threadIdx.x; k < n_opt; k += blockDim.x) {
         const double *u = xp + R.offP[k];
@@ -1041,6 +1055,78 @@ __global__ void update_kf_kernel(Rig rig, Red R, const double *b, const int *off
     for (int q = threadIdx.x; q < R.n; q += blockDim.x) sc += xp[q] * (lambda * xp[q] + b[q]);
     const double tt = block_reduce_sum(sc, sh);
     if (threadIdx.x == 0) scale_partial[0] = tt;
+}
+
+__device__ __forceinline__ void backsub_block(int blk, double *sh, Land L, Red R, double lambda, const double *xp,
+                                              State a, State bst, double *scale_partial) {
+    const int p = blk * blockDim.x + threadIdx.x;
+    double sc = 0;
+    if (p < L.n) {
+        double D[9], Dinv[9];
+        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+        D[0] += lambda, D[4] += lambda, D[8] += lambda;
+        inv3(D, Dinv);
+        const double *bl = L.bl + (size_t)p * 3;
+        double c[3] = {bl[0], bl[1], bl[2]};
+        for (int s = L.slot_start[p]; s < L.slot_start[p + 1]; ++s) {
+            const int o = R.offP[L.slot_kf[s]];
+            if (o < 0) continue;
+            const double *B = L.Hpl + (size_t)s * 18;
+            for (int q = 0; q < 3; ++q)
+                for (int r = 0; r < 6; ++r) c[q] -= B[3 * r + q] * xp[o + r];
+        }
+        double xl[3];
+        mv3(Dinv, c, xl);
+        for (int q = 0; q < 3; ++q) {
+            bst.pts[(size_t)p * 3 + q] = a.pts[(size_t)p * 3 + q] + xl[q];
+            sc += xl[q] * (lambda * xl[q] + bl[q]);
+        }
+    }
+    const double t = block_reduce_sum(sc, sh);
+    if (threadIdx.x == 0) scale_partial[1 + blk] = t;
+}
+
+// kf_block: this rank updates the keyframes (every rank of a sharded solve updates them identically; the
+// pose part of computeScale is counted once by the caller's choice of scale partials).
+__global__ void __launch_bounds__(kLandWG) update_kernel(Rig rig, Land L, Red R, const double *b, const int *offV,
+                                                         const int *offG, const int *offA, int n_opt, double lambda,
+                                                         const double *xp, State a, State bst, double *scale_partial,
+                                                         const LmCtl *ctl) {
+    __shared__ double sh[8];
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
+    if (blockIdx.x == 0) update_kf_block(sh, rig, R, b, offV, offG, offA, n_opt, lambda, xp, a, bst, scale_partial);
+    else backsub_block(blockIdx.x - 1, sh, L, R, lambda, xp, a, bst, scale_partial);
+}
+
+// The optimisation's epilogue on the device (single rank): per visual edge the reference's outlier test
+// (Optimizer.cc:3282-3311: EdgeMono chi2 > 5.991, or > 1.5 * 5.991 when the point's trackDepth < 10, or a
+// non-positive depth; EdgeStereo chi2 > 7.815) at the final state, written in the caller's edge order with
+// the chi2, and the points in the caller's order; the host reads one staging block.
+__global__ void epilogue_kernel(Rig rig, State s, Edges E, const int *perm_edge, int n_mono_all,
+                                const float *track_depth, const int *perm_pt, int n_pts, uint8_t *flags,
+                                double *chi2_out, double *pts_out, const double *chi2, double *head, int n_head) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n_head) head[q] = s.Rwb[q];   // the keyframe part of the state (it precedes the points)
+    if (q < E.n) {
+        const int e = q, o = perm_edge[e];
+        const double c2 = chi2[e];
+        uint8_t f;
+        if (o >= n_mono_all) {
+            f = c2 > 7.815f ? 1 : 0;
+        } else {
+            const int k = E.kf[e], c = E.cam[e], p = E.pt[e], C = rig.n_cams;
+            const double *R = s.Rcw + ((size_t)k * C + c) * 9, *t = s.tcw + ((size_t)k * C + c) * 3;
+            const double *X = s.pts + 3 * (size_t)p;
+            const bool depth_pos = (R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2]) > 0.0;
+            const bool close = track_depth[p] < 10.f;
+            f = ((c2 > 5.991f && !close) || (c2 > 1.5f * 5.991f && close) || !depth_pos) ? 1 : 0;
+        }
+        flags[o] = f;
+        if (chi2_out) chi2_out[o] = c2;
+    }
+    if (q < n_pts)
+        for (int d = 0; d < 3; ++d) pts_out[3 * (size_t)perm_pt[q] + d] = s.pts[3 * (size_t)q + d];
 }
 
 // ---- evaluation helpers for parity ---------------------------------------------------------------
@@ -1131,6 +1217,67 @@ void host_sym_eig(std::vector<double> A, int n, std::vector<double> &w, std::vec
     for (int i = 0; i < n; ++i) w[i] = A[i * n + i];
 }
 
+// Symbolic block LDL^T of the keyframe adjacency `adj` (nb x nb, symmetric) in the elimination order `perm`
+// (position -> keyframe): the filled lower pattern in positions and each position's elimination-tree level
+// (leaves 0, a parent above all its children).  Returns the number of levels (the factorisation's critical
+// path in diagonal-block steps) and the number of stored blocks.
+int symbolic_ldlt(int nb, const std::vector<uint8_t> &adj, const std::vector<int> &perm, std::vector<uint8_t> &pat,
+                  std::vector<int> &level, int &n_slots) {
+    pat.assign((size_t)nb * nb, 0);
+    for (int i = 0; i < nb; ++i)
+        for (int j = 0; j <= i; ++j) pat[(size_t)i * nb + j] = i == j || adj[(size_t)perm[i] * nb + perm[j]];
+    for (int k = 0; k < nb; ++k)
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[(size_t)i * nb + k])
+                for (int j = k + 1; j <= i; ++j)
+                    if (pat[(size_t)j * nb + k]) pat[(size_t)i * nb + j] = 1;
+    level.assign(nb, 0);
+    n_slots = 0;
+    int top = 0;
+    for (int k = 0; k < nb; ++k) {
+        for (int i = k; i < nb; ++i) n_slots += pat[(size_t)i * nb + k];
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[(size_t)i * nb + k]) {   // the parent: the first block below the diagonal
+                level[i] = std::max(level[i], level[k] + 1);
+                break;
+            }
+        top = std::max(top, level[k]);
+    }
+    return nb > 0 ? top + 1 : 0;
+}
+
+// The elimination order of the reduced system's keyframe blocks.  Candidates: the keyframe order, and every
+// two-way dissection of it -- a cut c, the separator S = the keyframes before c adjacent to one at or after c,
+// then [before c minus S, in order] [from c, reversed] [S]: the two sides share no block, so their columns
+// factor concurrently, and each side is eliminated away from the separator (no fill beyond it).  The one with
+// the fewest elimination-tree levels whose blocks fit `max_slots` wins (ties: fewer blocks, then earlier).
+// The solution of the damped system does not depend on the order beyond rounding (SimplicialLDLT's own AMD
+// ordering is a different one again, linear_solver_eigen.h:60).
+std::vector<int> plan_order(int nb, const std::vector<uint8_t> &adj, int max_slots) {
+    std::vector<int> best(nb);
+    std::iota(best.begin(), best.end(), 0);
+    std::vector<uint8_t> pat;
+    std::vector<int> lev;
+    int best_slots = 0;
+    int best_h = symbolic_ldlt(nb, adj, best, pat, lev, best_slots);
+    for (int cut = 1; cut < nb; ++cut) {
+        std::vector<int> order, sep;
+        for (int v = 0; v < cut; ++v) {
+            bool s = false;
+            for (int w = cut; w < nb && !s; ++w) s = adj[(size_t)v * nb + w] != 0;
+            (s ? sep : order).push_back(v);
+        }
+        if (sep.size() * 2 > (size_t)nb) continue;
+        for (int w = nb - 1; w >= cut; --w) order.push_back(w);
+        order.insert(order.end(), sep.begin(), sep.end());
+        int ns = 0;
+        const int h = symbolic_ldlt(nb, adj, order, pat, lev, ns);
+        if (ns > max_slots) continue;
+        if (h < best_h || (h == best_h && ns < best_slots)) best = order, best_h = h, best_slots = ns;
+    }
+    return best;
+}
+
 template <typename T>
 T *dalloc(std::vector<void *> &owned, size_t n) {
     void *p = nullptr;
@@ -1157,9 +1304,15 @@ struct omv_lba {
     BlockPat BP{};
     Gather G{};
     double *d_imu_contrib = nullptr;   // [n_imu][30 x 30 + 30] per-edge inertial contributions
-    int *d_imu_colour = nullptr;       // inertial edges grouped by colour (no shared keyframe within a colour)
-    std::vector<int> imu_colour_start;
-    int n_wg_land = 0, n_wg_edge = 0;
+    int n_wg_land = 0, n_wg_edge = 0, n_pchunk = 0, n_schunk = 0;
+    // device epilogue (single rank): perm_edge / perm_pt / trackDepth in device order, one staging block
+    // [state without points | points in caller order | chi2 in caller order | outlier flags in caller order]
+    int *d_perm_edge = nullptr, *d_perm_pt = nullptr;
+    float *d_track_depth = nullptr;
+    double *d_stage = nullptr, *h_stage = nullptr;
+    size_t stage_bytes = 0;
+    bool epi_ready = false;    // the staging block holds this optimize()'s final result
+    bool epi_chi2 = false;     //   including the chi2
     int *d_offP = nullptr, *d_offV = nullptr, *d_offG = nullptr, *d_offA = nullptr;
     double *d_err = nullptr, *d_chi2 = nullptr, *d_err9 = nullptr;
     double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
@@ -1197,6 +1350,8 @@ struct omv_lba {
 static void free_problem(omv_lba *h) {
     for (void *p : h->owned) (void)hipFree(p);
     h->owned.clear();
+    if (h->h_stage) (void)hipHostFree(h->h_stage);
+    h->h_stage = nullptr, h->stage_bytes = 0;
     if (h->step_exec) (void)hipGraphExecDestroy(h->step_exec);
     if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
     h->step_exec = nullptr, h->step_graph = nullptr;   // the captured step holds the old problem's pointers
@@ -1290,13 +1445,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     // block pattern of the reduced system (keyframe blocks) from ALL landmarks: every rank of a
     // sharded solve lays out the identical packed system
     const int nb = p->n_opt;
-    std::vector<uint8_t> pat((size_t)nb * nb, 0);
-    for (int k = 0; k < nb; ++k) pat[k * nb + k] = 1;
+    std::vector<uint8_t> adj((size_t)nb * nb, 0);   // keyframe adjacency (symmetric)
     for (int q = 0; q < P_all; ++q)
         for (int a : pe[q])
             for (int b : pe[q]) {
                 const int i = e_kf_of(a), j = e_kf_of(b);
-                if (i < nb && j < nb && j <= i) pat[i * nb + j] = 1;
+                if (i < nb && j < nb && i != j) adj[(size_t)i * nb + j] = 1;
             }
     // this rank's landmarks: a contiguous share of the landmark order
     if (h->world > 1) {
@@ -1342,55 +1496,90 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     pt_slot[P] = (int)slot_kf.size();
     h->n_slots = (int)slot_kf.size();
     h->n_wg_land = (P + kLandWG - 1) / kLandWG;
-    // per optimisable keyframe: its edges and its landmark slots, ascending (build_pose_kernel, schur_block_kernel)
-    std::vector<int> kf_edge_start(nb + 1, 0), kf_edge, kf_slot_start(nb + 1, 0), kf_slot;
-    for (int e = 0; e < E; ++e)
-        if (e_kf[e] < nb) ++kf_edge_start[e_kf[e] + 1];
-    for (int s2 = 0; s2 < h->n_slots; ++s2)
-        if (slot_kf[s2] < nb) ++kf_slot_start[slot_kf[s2] + 1];
-    for (int k = 0; k < nb; ++k)
-        kf_edge_start[k + 1] += kf_edge_start[k], kf_slot_start[k + 1] += kf_slot_start[k];
-    kf_edge.resize(kf_edge_start[nb]), kf_slot.resize(kf_slot_start[nb]);
-    {
-        std::vector<int> fe(kf_edge_start.begin(), kf_edge_start.end() - 1), fs(kf_slot_start.begin(), kf_slot_start.end() - 1);
-        for (int e = 0; e < E; ++e)
-            if (e_kf[e] < nb) kf_edge[fe[e_kf[e]]++] = e;
-        for (int s2 = 0; s2 < h->n_slots; ++s2)
-            if (slot_kf[s2] < nb) kf_slot[fs[slot_kf[s2]]++] = s2;
-    }
-    // inertial blocks + symbolic LDL^T fill-in
+    // inertial edges: ids checked, and their blocks in the keyframe adjacency
     for (int i = 0; i < NI; ++i) {
         if (p->imu_kf1[i] < 0 || p->imu_kf1[i] >= K || p->imu_kf2[i] < 0 || p->imu_kf2[i] >= K ||
             p->imu_kf1[i] == p->imu_kf2[i])
             return OMV_ERR_ARG;
-        const int a = std::max(p->imu_kf1[i], p->imu_kf2[i]), b = std::min(p->imu_kf1[i], p->imu_kf2[i]);
-        if (a < nb && b < nb) pat[a * nb + b] = 1;
+        const int a = p->imu_kf1[i], b = p->imu_kf2[i];
+        if (a < nb && b < nb) adj[(size_t)a * nb + b] = adj[(size_t)b * nb + a] = 1;
     }
-    // reduced order follows keyframe index: block i sits after block j for i > j (offP increasing)
-    for (int k = 0; k < nb; ++k)
-        for (int i = k + 1; i < nb; ++i)
-            if (pat[i * nb + k])
-                for (int j = k + 1; j <= i; ++j)
-                    if (pat[j * nb + k]) pat[i * nb + j] = 1;
-    std::vector<int> slot((size_t)nb * nb, -1), slot_i, slot_j;
-    for (int j = 0; j < nb; ++j)   // column-major slot order: a step's panel blocks sit together
+    // elimination order (every rank of a sharded solve plans from the same full pattern) and its symbolic LDL^T
+    const size_t vec_bytes = 2 * (size_t)nred * sizeof(double);
+    const int lds_slots = h->lds_ok && kLdltLds > vec_bytes ? (int)((kLdltLds - vec_bytes) / (256 * sizeof(double))) : 0;
+    const std::vector<int> perm = plan_order(nb, adj, std::max(lds_slots, 1));
+    std::vector<int> ipos(nb);
+    for (int q = 0; q < nb; ++q) ipos[perm[q]] = q;
+    std::vector<uint8_t> pat;
+    std::vector<int> level;
+    int n_slots = 0;
+    const int n_lev = symbolic_ldlt(nb, adj, perm, pat, level, n_slots);
+    std::vector<int> slot((size_t)nb * nb, -1), slot_kr, slot_kc, dslot(nb);
+    for (int j = 0; j < nb; ++j)   // column-major in positions: a column's panel blocks sit together
         for (int i = j; i < nb; ++i)
-            if (pat[i * nb + j]) {
-                slot[i * nb + j] = (int)slot_i.size();
-                slot_i.push_back(i), slot_j.push_back(j);
+            if (pat[(size_t)i * nb + j]) {
+                slot[(size_t)i * nb + j] = (int)slot_kr.size();
+                slot_kr.push_back(perm[i]), slot_kc.push_back(perm[j]);
             }
-    const int n_slots = (int)slot_i.size();
-    // Schur terms per block: landmark slots (a, b) of one landmark, keyframe(a) >= keyframe(b), both optimisable;
-    // grouped by block, each group in (landmark, a, b) order
+    for (int k = 0; k < nb; ++k) dslot[k] = slot[(size_t)k * nb + k];
+    // level schedule: columns per level; panel tasks; trailing updates grouped by target block (ascending k)
+    std::vector<int> lev_start(n_lev + 1, 0), lev_col, pt_start(n_lev + 1, 0), ug_start(n_lev + 1, 0), ug_task_start(1, 0);
+    std::vector<int2> pt;
+    std::vector<int4> ug;
+    for (int l = 0; l < n_lev; ++l) {
+        lev_start[l] = (int)lev_col.size();
+        pt_start[l] = (int)pt.size();
+        ug_start[l] = (int)ug_task_start.size() - 1;
+        std::map<int, std::vector<int4>> by_target;   // target slot -> updates in ascending k
+        for (int k = 0; k < nb; ++k) {
+            if (level[k] != l) continue;
+            lev_col.push_back(k);
+            std::vector<int> col;
+            for (int i = k + 1; i < nb; ++i)
+                if (pat[(size_t)i * nb + k]) col.push_back(i), pt.push_back(make_int2(slot[(size_t)i * nb + k], dslot[k]));
+            for (size_t a = 0; a < col.size(); ++a)
+                for (size_t c = 0; c <= a; ++c) {
+                    const int i = col[a], j = col[c];
+                    by_target[slot[(size_t)i * nb + j]].push_back(
+                        make_int4(slot[(size_t)i * nb + j], slot[(size_t)i * nb + k], slot[(size_t)j * nb + k], dslot[k]));
+                }
+        }
+        for (auto &kv : by_target) {
+            ug.insert(ug.end(), kv.second.begin(), kv.second.end());
+            ug_task_start.push_back((int)ug.size());
+        }
+    }
+    lev_start[n_lev] = (int)lev_col.size();
+    pt_start[n_lev] = (int)pt.size();
+    ug_start[n_lev] = (int)ug_task_start.size() - 1;
+    std::vector<int> rs_start(nb + 1, 0), cs_start(nb + 1, 0);
+    std::vector<int2> rs, cs;
+    for (int i = 0; i < nb; ++i) {
+        rs_start[i] = (int)rs.size();
+        for (int k = 0; k < i; ++k)
+            if (pat[(size_t)i * nb + k]) rs.push_back(make_int2(slot[(size_t)i * nb + k], k));
+    }
+    rs_start[nb] = (int)rs.size();
+    for (int k = 0; k < nb; ++k) {
+        cs_start[k] = (int)cs.size();
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[(size_t)i * nb + k]) cs.push_back(make_int2(slot[(size_t)i * nb + k], i));
+    }
+    cs_start[nb] = (int)cs.size();
+    // Schur terms per block: landmark slots (a, b) of one landmark oriented to the block (a on the block's row
+    // keyframe, b on its column keyframe; on a diagonal block a == b), grouped by block in (landmark, a, b) order,
+    // then split into chunks of <= 256 (at least one per block: the chunk that assembles it)
     std::vector<int> tr_start(n_slots + 1, 0);
     std::vector<int2> tr;
     {
         auto each = [&](auto &&f) {
             for (int q = 0; q < P; ++q)
                 for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
-                    if (slot_kf[a] < nb)
-                        for (int b = pt_slot[q]; b <= a; ++b)   // slots of a landmark ascend with the keyframe
-                            if (slot_kf[b] < nb) f(slot[slot_kf[a] * nb + slot_kf[b]], a, b);
+                    for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
+                        const int ka = slot_kf[a], kb = slot_kf[b];
+                        if (ka >= nb || kb >= nb || ipos[ka] < ipos[kb] || (ka == kb && a != b)) continue;
+                        f(slot[(size_t)ipos[ka] * nb + ipos[kb]], a, b);
+                    }
         };
         each([&](int t, int, int) { ++tr_start[t + 1]; });
         for (int t = 0; t < n_slots; ++t) tr_start[t + 1] += tr_start[t];
@@ -1398,21 +1587,69 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         std::vector<int> fill(tr_start.begin(), tr_start.end() - 1);
         each([&](int t, int a, int b) { tr[fill[t]++] = make_int2(a, b); });
     }
-    std::vector<int> pan_start(nb + 1, 0), pan, pair_start(nb + 1, 0);
-    std::vector<int4> pair;
-    for (int k = 0; k < nb; ++k) {
-        pan_start[k] = (int)pan.size();
-        pair_start[k] = (int)pair.size();
-        for (int i = k + 1; i < nb; ++i)
-            if (pat[i * nb + k]) pan.push_back(i);
-        for (int a = pan_start[k]; a < (int)pan.size(); ++a)
-            for (int c = pan_start[k]; c <= a; ++c) {
-                const int i = pan[a], j = pan[c];
-                pair.push_back(make_int4(slot[i * nb + j], slot[i * nb + k], slot[j * nb + k], 0));
-            }
+    std::vector<int4> schunk;
+    std::vector<int> sc_start(n_slots + 1, 0);
+    for (int t = 0; t < n_slots; ++t) {
+        sc_start[t] = (int)schunk.size();
+        int q = tr_start[t];
+        do {
+            const int e = std::min(q + 256, tr_start[t + 1]);
+            schunk.push_back(make_int4(t, q, e, 0));
+            q = e;
+        } while (q < tr_start[t + 1]);
     }
-    pan_start[nb] = (int)pan.size();
-    pair_start[nb] = (int)pair.size();
+    sc_start[n_slots] = (int)schunk.size();
+    h->n_schunk = (int)schunk.size();
+    // pose chunks: per optimisable keyframe its visual edges (ascending), <= 256 per chunk
+    std::vector<int> kf_edge_start(nb + 1, 0), kf_edge, pc_start(nb + 1, 0);
+    std::vector<int4> pchunk;
+    for (int e = 0; e < E; ++e)
+        if (e_kf[e] < nb) ++kf_edge_start[e_kf[e] + 1];
+    for (int k = 0; k < nb; ++k) kf_edge_start[k + 1] += kf_edge_start[k];
+    kf_edge.resize(kf_edge_start[nb]);
+    {
+        std::vector<int> fe(kf_edge_start.begin(), kf_edge_start.end() - 1);
+        for (int e = 0; e < E; ++e)
+            if (e_kf[e] < nb) kf_edge[fe[e_kf[e]]++] = e;
+    }
+    for (int k = 0; k < nb; ++k) {
+        pc_start[k] = (int)pchunk.size();
+        for (int q = kf_edge_start[k]; q < kf_edge_start[k + 1]; q += 256)
+            pchunk.push_back(make_int4(k, q, std::min(q + 256, kf_edge_start[k + 1]), 0));
+    }
+    pc_start[nb] = (int)pchunk.size();
+    h->n_pchunk = (int)pchunk.size();
+    // inertial edges per block (edge, side of the row keyframe, side of the column keyframe; side 0 = kf1) and per
+    // keyframe (edge, side), in edge order; only the rank that evaluates them
+    std::vector<int> ib_start(n_slots + 1, 0), iv_start(nb + 1, 0);
+    std::vector<int4> imu_blk;
+    std::vector<int2> imu_vec;
+    {
+        std::vector<std::vector<int4>> bl(n_slots);
+        std::vector<std::vector<int2>> vl(nb);
+        if (h->imu_here)
+            for (int i = 0; i < NI; ++i) {
+                const int kk[2] = {p->imu_kf1[i], p->imu_kf2[i]};
+                for (int sr = 0; sr < 2; ++sr) {
+                    if (kk[sr] >= nb) continue;
+                    vl[kk[sr]].push_back(make_int2(i, sr));
+                    for (int sc = 0; sc < 2; ++sc) {
+                        if (kk[sc] >= nb || ipos[kk[sr]] < ipos[kk[sc]]) continue;
+                        bl[slot[(size_t)ipos[kk[sr]] * nb + ipos[kk[sc]]]].push_back(make_int4(i, sr, sc, 0));
+                    }
+                }
+            }
+        for (int t = 0; t < n_slots; ++t) {
+            ib_start[t] = (int)imu_blk.size();
+            imu_blk.insert(imu_blk.end(), bl[t].begin(), bl[t].end());
+        }
+        ib_start[n_slots] = (int)imu_blk.size();
+        for (int k = 0; k < nb; ++k) {
+            iv_start[k] = (int)imu_vec.size();
+            imu_vec.insert(imu_vec.end(), vl[k].begin(), vl[k].end());
+        }
+        iv_start[nb] = (int)imu_vec.size();
+    }
     const size_t ldlt_bytes = ((size_t)n_slots * 256 + 2 * (size_t)nred) * sizeof(double);
     h->use_lds = h->lds_ok && ldlt_bytes <= kLdltLds ? 1 : 0;
     h->ldlt_lds = h->use_lds ? ldlt_bytes : 0;
@@ -1489,43 +1726,36 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     if (!d_e_ur) return OMV_ERR_HIP;
     HIP_OK(up(d_e_ur, e_ur.data(), E));
     h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, d_e_ur, E};
-    int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots);
+    int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots),
+        *d_slot_pt = dalloc<int>(ow, h->n_slots);
     double *d_Hll = dalloc<double>(ow, 9 * (size_t)P), *d_bl = dalloc<double>(ow, 3 * (size_t)P),
-           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots), *d_BD = dalloc<double>(ow, 18 * (size_t)h->n_slots),
-           *d_cs = dalloc<double>(ow, 6 * (size_t)h->n_slots);
-    if (!d_cs) return OMV_ERR_HIP;
-    HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
-    HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
-    HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
-    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_Hll, d_bl, d_Hpl, d_BD, d_cs, P};
+           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots);
+    if (!d_Hpl || !d_slot_pt) return OMV_ERR_HIP;
     {
-        int *d_kes = dalloc<int>(ow, nb + 1), *d_ke = dalloc<int>(ow, kf_edge.size()), *d_kss = dalloc<int>(ow, nb + 1),
-            *d_ks = dalloc<int>(ow, kf_slot.size()), *d_trs = dalloc<int>(ow, n_slots + 1);
-        int2 *d_tr = dalloc<int2>(ow, tr.size());
-        if (!d_tr) return OMV_ERR_HIP;
-        HIP_OK(up(d_kes, kf_edge_start.data(), nb + 1));
-        if (!kf_edge.empty()) HIP_OK(up(d_ke, kf_edge.data(), kf_edge.size()));
-        HIP_OK(up(d_kss, kf_slot_start.data(), nb + 1));
-        if (!kf_slot.empty()) HIP_OK(up(d_ks, kf_slot.data(), kf_slot.size()));
-        HIP_OK(up(d_trs, tr_start.data(), n_slots + 1));
-        if (!tr.empty()) HIP_OK(up(d_tr, tr.data(), tr.size()));
-        h->G = Gather{d_kes, d_ke, d_kss, d_ks, d_trs, d_tr};
+        std::vector<int> slot_pt(h->n_slots);
+        for (int q = 0; q < P; ++q)
+            for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a) slot_pt[a] = q;
+        HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
+        HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
+        if (h->n_slots > 0) HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
+        if (h->n_slots > 0) HIP_OK(up(d_slot_pt, slot_pt.data(), h->n_slots));
     }
+    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_slot_pt, d_Hll, d_bl, d_Hpl, P};
     h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
     h->d_offA = dalloc<int>(ow, K);
     HIP_OK(up(h->d_offP, offP.data(), K));
     HIP_OK(up(h->d_offV, offV.data(), K));
     HIP_OK(up(h->d_offG, offG.data(), K));
     HIP_OK(up(h->d_offA, offA.data(), K));
-    double *d_H = dalloc<double>(ow, (size_t)nred * nred), *d_b = dalloc<double>(ow, nred);
-    h->R = Red{d_H, d_b, nred, h->d_offP, K};
+    h->R = Red{nred, h->d_offP, K};
     // inertial
     int *d_k1 = dalloc<int>(ow, NI), *d_k2 = dalloc<int>(ow, NI);
     float *d_pre = dalloc<float>(ow, (size_t)NI * kPF);
     double *d_i9 = dalloc<double>(ow, (size_t)NI * 81), *d_iG = dalloc<double>(ow, (size_t)NI * 9),
            *d_iA = dalloc<double>(ow, (size_t)NI * 9);
     uint8_t *d_rob = dalloc<uint8_t>(ow, NI);
-    if (!d_rob) return OMV_ERR_HIP;
+    h->d_imu_contrib = dalloc<double>(ow, (size_t)NI * kImuContrib);
+    if (!d_rob || !h->d_imu_contrib) return OMV_ERR_HIP;
     if (NI > 0) {
         HIP_OK(up(d_k1, p->imu_kf1, NI));
         HIP_OK(up(d_k2, p->imu_kf2, NI));
@@ -1538,42 +1768,37 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         HIP_OK(up(d_rob, rob.data(), NI));
     }
     h->I = Imu{NI, d_k1, d_k2, d_pre, d_i9, d_iG, d_iA, d_rob, h->d_offP, h->d_offV, h->d_offG, h->d_offA};
-    {   // greedy edge colouring: an inertial edge takes the first colour neither of its keyframes holds yet
-        std::vector<int> colour(NI), n_col;
-        std::vector<std::vector<char>> used(K);
-        for (int i = 0; i < NI; ++i) {
-            auto &u1 = used[p->imu_kf1[i]], &u2 = used[p->imu_kf2[i]];
-            int c = 0;
-            while ((c < (int)u1.size() && u1[c]) || (c < (int)u2.size() && u2[c])) ++c;
-            u1.resize(std::max(u1.size(), (size_t)c + 1), 0), u2.resize(std::max(u2.size(), (size_t)c + 1), 0);
-            u1[c] = u2[c] = 1;
-            colour[i] = c;
-            if (c >= (int)n_col.size()) n_col.resize(c + 1, 0);
-            ++n_col[c];
-        }
-        h->imu_colour_start.assign(n_col.size() + 1, 0);
-        for (size_t c = 0; c < n_col.size(); ++c) h->imu_colour_start[c + 1] = h->imu_colour_start[c] + n_col[c];
-        std::vector<int> by(NI), fill(h->imu_colour_start.begin(), h->imu_colour_start.end() - 1);
-        for (int i = 0; i < NI; ++i) by[fill[colour[i]]++] = i;
-        h->d_imu_colour = dalloc<int>(ow, NI);
-        h->d_imu_contrib = dalloc<double>(ow, (size_t)NI * kImuContrib);
-        if (!h->d_imu_contrib) return OMV_ERR_HIP;
-        if (NI > 0) HIP_OK(up(h->d_imu_colour, by.data(), NI));
+    // reduction work lists
+    auto upv = [&](const auto &v) {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        T *d = dalloc<T>(ow, v.size());
+        if (d && !v.empty() && up(d, v.data(), v.size()) != hipSuccess) d = nullptr;
+        return (const T *)d;
+    };
+    {
+        Gather &g = h->G;
+        g.pchunk = upv(pchunk), g.kf_edge = upv(kf_edge), g.pc_start = upv(pc_start);
+        g.schunk = upv(schunk), g.tr = upv(tr), g.sc_start = upv(sc_start);
+        g.imu_blk = upv(imu_blk), g.ib_start = upv(ib_start), g.imu_vec = upv(imu_vec), g.iv_start = upv(iv_start);
+        g.pose_part = dalloc<double>(ow, (size_t)std::max(1, h->n_pchunk) * 27);
+        g.schur_part = dalloc<double>(ow, (size_t)h->n_schunk * 42);
+        g.contrib = h->d_imu_contrib;
+        if (!g.pchunk || !g.kf_edge || !g.pc_start || !g.schunk || !g.tr || !g.sc_start || !g.imu_blk || !g.ib_start ||
+            !g.imu_vec || !g.iv_start || !g.pose_part || !g.schur_part)
+            return OMV_ERR_HIP;
     }
-    // block pattern
-    int *d_slot = dalloc<int>(ow, (size_t)nb * nb), *d_slot_i = dalloc<int>(ow, n_slots),
-        *d_slot_j = dalloc<int>(ow, n_slots), *d_pan_start = dalloc<int>(ow, nb + 1), *d_pan = dalloc<int>(ow, pan.size()),
-        *d_pair_start = dalloc<int>(ow, nb + 1);
-    int4 *d_pair = dalloc<int4>(ow, pair.size());
-    if (!d_pair) return OMV_ERR_HIP;
-    HIP_OK(up(d_slot, slot.data(), (size_t)nb * nb));
-    HIP_OK(up(d_slot_i, slot_i.data(), n_slots));
-    HIP_OK(up(d_slot_j, slot_j.data(), n_slots));
-    HIP_OK(up(d_pan_start, pan_start.data(), nb + 1));
-    if (!pan.empty()) HIP_OK(up(d_pan, pan.data(), pan.size()));
-    HIP_OK(up(d_pair_start, pair_start.data(), nb + 1));
-    if (!pair.empty()) HIP_OK(up(d_pair, pair.data(), pair.size()));
-    h->BP = BlockPat{nb, n_slots, d_slot, d_slot_i, d_slot_j, d_pan_start, d_pan, d_pair_start, d_pair};
+    // block pattern + level schedule
+    {
+        BlockPat &B = h->BP;
+        B.nb = nb, B.n_slots = n_slots, B.n_lev = n_lev;
+        B.perm = upv(perm), B.slot_kr = upv(slot_kr), B.slot_kc = upv(slot_kc), B.dslot = upv(dslot);
+        B.lev_start = upv(lev_start), B.lev_col = upv(lev_col), B.pt_start = upv(pt_start), B.pt = upv(pt);
+        B.ug_start = upv(ug_start), B.ug_task_start = upv(ug_task_start), B.ug = upv(ug);
+        B.rs_start = upv(rs_start), B.rs = upv(rs), B.cs_start = upv(cs_start), B.cs = upv(cs);
+        if (!B.perm || !B.slot_kr || !B.slot_kc || !B.dslot || !B.lev_start || !B.lev_col || !B.pt_start || !B.pt ||
+            !B.ug_start || !B.ug_task_start || !B.ug || !B.rs_start || !B.rs || !B.cs_start || !B.cs)
+            return OMV_ERR_HIP;
+    }
     // work buffers
     h->n_wg_edge = (E + 255) / 256;
     h->d_err = dalloc<double>(ow, 2 * (size_t)E);
@@ -1597,6 +1822,21 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
     HIP_OK(hipMemset(h->d_imu_partial_a, 0, sizeof(double)));
+    // device epilogue (single rank): caller-order permutations, trackDepth in device order, the staging block
+    if (h->world == 1) {
+        std::vector<float> td(P, 1e30f);
+        if (p->pt_track_depth)
+            for (int q = 0; q < P; ++q) td[q] = p->pt_track_depth[order[q]];
+        h->d_perm_edge = dalloc<int>(ow, E), h->d_perm_pt = dalloc<int>(ow, P), h->d_track_depth = dalloc<float>(ow, P);
+        const size_t head = (size_t)(h->st[0].pts - h->st[0].Rwb);
+        h->stage_bytes = (head + 3 * (size_t)P + ((size_t)E + 7) / 8 + (size_t)E) * sizeof(double);
+        h->d_stage = dalloc<double>(ow, (h->stage_bytes + 7) / 8);
+        if (!h->d_perm_edge || !h->d_perm_pt || !h->d_track_depth || !h->d_stage) return OMV_ERR_HIP;
+        if (E > 0) HIP_OK(up(h->d_perm_edge, h->perm_edge.data(), E));
+        if (P > 0) HIP_OK(up(h->d_perm_pt, order.data(), P));
+        if (P > 0) HIP_OK(up(h->d_track_depth, td.data(), P));
+        HIP_OK(hipHostMalloc((void **)&h->h_stage, h->stage_bytes, hipHostMallocDefault));
+    }
     return OMV_OK;
 }
 
@@ -1605,15 +1845,16 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 // ---- the LM driver ---------------------------------------------------------------------------------
 // computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
 static omv_status lba_errors(omv_lba *h, const State &s, const LmCtl *ctl = nullptr, int gate = kGateAlways,
-                             bool partial_a = false) {
+                             bool partial_a = false, ErrAux aux = ErrAux{}) {
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
-    const int blocks = nmb + (h->imu_here ? 1 : 0);
+    int blocks = nmb + (h->imu_here ? 1 : 0);
+    if (aux.copy_dst) blocks = std::max(blocks, 1);   // the copy runs even without edges
     if (blocks > 0)
         err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s, h->E, h->delta_mono, h->dsqr_mono,
                                                   h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2,
                                                   partial_a ? h->d_partial_a : h->d_partial, h->I, h->delta_imu,
                                                   h->dsqr_imu, h->d_err9, partial_a ? h->d_imu_partial_a : h->d_imu_partial,
-                                                  ctl, gate);
+                                                  ctl, gate, aux);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 
@@ -1698,74 +1939,68 @@ omv_status omv_lba_evaluate_stereo(omv_lba *h, double *stereo_err, double *stere
 }
 
 static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res);
+static bool lba_epilogue_ok(const omv_lba *h);
+static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2);
 
-// buildSystem at state A: H = 0, the landmark blocks, the keyframe-diagonal visual terms, the inertial edges
-// colour by colour.  Every entry is a fixed-order sum: the system is identical run to run.
+// buildSystem at state A: the landmark blocks, the keyframe-diagonal pose chunks and the inertial edges' quadratic
+// forms in one launch (every part a fixed-order sum: the system is identical run to run).
 static void launch_build(omv_lba *h, const State &A, const LmCtl *c) {
-    hipStream_t st = h->stream;
-    const int nred = h->n_red;
-    const size_t nH = (size_t)nred * nred;
-    zero_kernel<<<(int)((nH + 255) / 256), 256, 0, st>>>(h->R.H, nH, h->R.b, nred, c);
-    if (h->n_pts > 0)
-        build_kernel<<<h->n_wg_land, kLandWG, 0, st>>>(h->rig, A, h->E, h->L, h->delta_mono, h->dsqr_mono, h->delta_st,
-                                                       h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, c);
-    if (h->n_mono > 0 && h->n_opt > 0)
-        build_pose_kernel<<<h->n_opt, 256, 0, st>>>(h->rig, A, h->E, h->G, h->R, h->delta_mono, h->dsqr_mono,
-                                                    h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2, c);
-    if (h->imu_here && h->n_imu > 0) {
-        imu_contrib_kernel<<<h->n_imu, kLandWG, 0, st>>>(A, h->I, h->delta_imu, h->dsqr_imu, h->d_err9,
-                                                         h->d_imu_contrib, c);
-        for (size_t k = 0; k + 1 < h->imu_colour_start.size(); ++k) {
-            const int n = h->imu_colour_start[k + 1] - h->imu_colour_start[k];
-            imu_add_kernel<<<n, kLandWG, 0, st>>>(h->I, h->R, h->d_imu_contrib, h->d_imu_colour + h->imu_colour_start[k],
-                                                  n, c);
-        }
-    }
+    const int n_imu_blk = h->imu_here ? h->n_imu : 0;
+    const int blocks = h->n_wg_land + h->n_pchunk + n_imu_blk;
+    if (blocks > 0)
+        build_kernel<<<blocks, kLandWG, 0, h->stream>>>(h->rig, A, h->E, h->L, h->G, h->I, h->n_wg_land, h->n_pchunk,
+                                                        h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu,
+                                                        h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2, h->d_err9,
+                                                        h->d_imu_contrib, c);
 }
 
-// The trial's reduced system: pack H + lambda I into the block layout, then the Schur complement.
+// The trial's reduced system (H + lambda I minus the landmark Schur terms, b, the Schur right-hand side) in one
+// launch; lambda on the pose diagonal once (rank 0 of a sharded solve), every rank damps its own landmarks.
 static void launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
-    hipStream_t st = h->stream;
-    const int npk = std::max(h->BP.n_slots * 256, h->n_red);
-    // lambda on the pose diagonal once (rank 0 of a sharded solve); every rank damps its own landmarks
-    pack_kernel<<<(npk + 255) / 256, 256, 0, st>>>(h->R.H, h->n_red, h->BP, h->rank == 0 ? lambda : 0.0, h->d_S,
-                                                   h->d_coef, c);
-    if (h->n_pts > 0) {
-        schur_point_kernel<<<h->n_wg_land, kLandWG, 0, st>>>(h->L, h->R, lambda, c);
-        schur_block_kernel<<<h->BP.n_slots, 256, 0, st>>>(h->L, h->R, h->BP, h->G, h->d_S, h->d_coef, c);
-    }
+    schur_kernel<<<h->n_schunk, 256, 0, h->stream>>>(h->L, h->G, h->BP, lambda, c);
+    assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, lambda, h->rank == 0 ? 1 : 0, h->d_S,
+                                                          h->d_bb, h->d_coef, c);
+}
+
+static void launch_ldlt(omv_lba *h, const LmCtl *c) {
+    if (h->use_lds)
+        ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x,
+                                                                        h->d_scratch, h->d_fail, c);
+    else
+        ldlt_kernel<true><<<1, kLdltThreads, 0, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x, h->d_scratch,
+                                                             h->d_fail, c);
+}
+
+static void launch_update(omv_lba *h, double lambda, const State &A, const State &B, const LmCtl *c) {
+    update_kernel<<<1 + h->n_wg_land, kLandWG, 0, h->stream>>>(h->rig, h->L, h->R, h->d_bb, h->d_offV, h->d_offG,
+                                                               h->d_offA, h->n_opt, lambda, h->d_x, A, B,
+                                                               h->d_scale_partial, c);
 }
 
 // One LM step of the single-rank path: the gated kernel sequence (see LmCtl).  A = st[0] is always the
-// current state and B = st[1] the trial; an accepted trial is copied back into A on the device.  With `ev`,
-// events bracket the stages (build, Schur, solve, update + errors) for omv_lba_stage_ms.
+// current state and B = st[1] the trial.  The step opens with the copy B -> A of an accepted last trial (or, after
+// a rejected one, the errors of A when an iteration starts) and closes with the trial's errors and the LM
+// bookkeeping.  With `ev`, events bracket the stages (build, Schur, solve, update + errors).
 static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     hipStream_t st = h->stream;
     LmCtl *c = h->d_ctl;
-    const int nred = h->n_red, gl = std::max(1, h->n_wg_land);
-    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
-    State &A = h->st[0], &B = h->st[1];
+    const State &A = h->st[0], &B = h->st[1];
     omv_status rs;
-    if ((rs = lba_errors(h, A, c, kGateErrA, true)) != OMV_OK) return rs;   // after a rejected trial
+    ErrAux start{};
+    start.copy_src = B.Rwb, start.copy_dst = A.Rwb, start.copy_n = h->state_doubles();
+    if ((rs = lba_errors(h, A, c, kGateErrA, true, start)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[0], st));
     launch_build(h, A, c);
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
     launch_schur(h, 0.0, c);
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
-    if (h->use_lds)
-        ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch,
-                                                                 h->d_fail, c);
-    else
-        ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, h->R.b, h->d_coef, h->d_x, h->d_scratch, h->d_fail,
-                                                      c);
+    launch_ldlt(h, c);
     if (ev) HIP_OK(hipEventRecord(ev[3], st));
-    update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, h->R.b, h->d_offV, h->d_offG, h->d_offA, h->n_opt, 0.0, h->d_x, A, B,
-                                        h->d_scale_partial, c);
-    if (h->n_pts > 0) backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, 0.0, h->d_x, A, B, h->d_scale_partial + 1, c);
+    launch_update(h, 0.0, A, B, c);
     if ((rs = lba_errors(h, B, c, kGateTrial)) != OMV_OK) return rs;
-    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a, h->d_imu_partial_a,
-                                           h->d_scale_partial, h->n_pts > 0 ? gl + 1 : 1, h->d_fail);
-    accept_copy_kernel<<<256, 256, 0, st>>>(c, B.Rwb, A.Rwb, h->state_doubles());
+    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
+                                           h->d_partial_a, h->d_imu_partial_a, h->d_scale_partial,
+                                           h->n_pts > 0 ? h->n_wg_land + 1 : 1, h->d_fail);
     if (ev) HIP_OK(hipEventRecord(ev[4], st));
     HIP_OK(hipGetLastError());
     return OMV_OK;
@@ -1773,9 +2008,11 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
 
 // optimize() on one rank with the LM control on the device: the initial errors, then LM steps in batches
 // (opt_it first: every iteration takes at least one trial) until the device reports the end; one read-back
-// per batch.  Identical decisions to the host-driven loop below (which the sharded solve keeps, its per-trial
-// all-reduce being a host call).
+// per batch; the last accepted trial's state copied into A.  Identical decisions to the host-driven loop below
+// (which the sharded solve keeps, its per-trial all-reduce being a host call).
 static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba_result *res) {
+    const bool want_chi2 = res->mono_chi2 || res->stereo_chi2;
+    h->epi_ready = false;
     hipStream_t st = h->stream;
     if (h->cur != 0) {   // the device path keeps the current state in st[0]
         HIP_OK(hipMemcpyAsync(h->st[0].Rwb, h->st[1].Rwb, h->state_doubles() * sizeof(double), hipMemcpyDeviceToDevice,
@@ -1816,10 +2053,18 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
             }
         }
         launched += batch;
+        // the epilogue rides along with the control read-back (kept when the device reports the end)
+        const bool spec = lba_epilogue_ok(h);
+        if (spec && (rs = lba_enqueue_epilogue(h, want_chi2)) != OMV_OK) return rs;
         HIP_OK(hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         if (h->h_ctl->done || launched >= max_steps) break;
+        h->epi_ready = false;
         batch = std::min(4, max_steps - launched);
+    }
+    if (!h->epi_ready) {   // the last accepted trial's state into A
+        accept_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
+        HIP_OK(hipGetLastError());
     }
     const LmCtl &c = *h->h_ctl;
     for (double &m : h->stage_ms) m = 0;
@@ -1843,7 +2088,6 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
 omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
     if (!h || !o || !p || !res) return OMV_ERR_ARG;
     hipStream_t st = h->stream;
-    const int nred = h->n_red;
     double sc[3];
     omv_status rs;
     for (double &m : h->stage_ms) m = 0;
@@ -1889,26 +2133,13 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         do {
             HIP_OK(hipEventRecord(h->ev[2], st));
             launch_schur(h, lambda, nullptr);
-            const double *bsys = h->R.b;
-            if (h->world > 1) {   // one exchange: sum the partial Schur systems of the landmark shards
-                HIP_OK(hipMemcpyAsync(h->d_bb, h->R.b, sizeof(double) * nred, hipMemcpyDeviceToDevice, st));
-                if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
-                bsys = h->d_bb;
-            }
+            // one exchange: sum the partial reduced systems [blocks | b | Schur rhs] of the landmark shards
+            if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
             HIP_OK(hipEventRecord(h->ev[3], st));
-            if (h->use_lds)
-                ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x,
-                                                                         h->d_scratch, h->d_fail, nullptr);
-            else
-                ldlt_kernel<true><<<1, kLdltThreads, 0, st>>>(h->d_S, h->BP, bsys, h->d_coef, h->d_x, h->d_scratch,
-                                                              h->d_fail, nullptr);
+            launch_ldlt(h, nullptr);
             HIP_OK(hipEventRecord(h->ev[4], st));
-            // landmark back-substitution, then the keyframe update; both feed the trial's errors (one stream:
-            // a side stream's fork / join cost more than the ~10 us update)
-            update_kf_kernel<<<1, 256, 0, st>>>(h->rig, h->R, bsys, h->d_offV, h->d_offG, h->d_offA, h->n_opt,
-                                                     lambda, h->d_x, A, B, h->d_scale_partial, nullptr);
-            if (h->n_pts > 0)
-                backsub_kernel<<<gl, kLandWG, 0, st>>>(h->L, h->R, lambda, h->d_x, A, B, h->d_scale_partial + 1, nullptr);
+            // keyframe update + landmark back-substitution (one launch), then the trial's errors
+            launch_update(h, lambda, A, B, nullptr);
             if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
             if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc, true)) != OMV_OK) return rs;
             const int fail = sc[2] != 0.0;
@@ -1965,23 +2196,76 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
 
 // The epilogue shared by both LM drivers: state write-back in the caller's order, per-edge chi2 and the
 // reference's outlier / FAIL tests (Optimizer.cc:3282-3321).
+// The single-rank device epilogue: state of A (an accepted last trial copied in first), outlier flags, chi2 when
+// asked for and the points in the caller's order into the staging block [head | points | flags | chi2], then
+// its read-back into pinned memory (not synchronised here).
+static bool lba_epilogue_ok(const omv_lba *h) {
+    return h->world == 1 && h->d_stage && h->cur == 0 && h->n_mono_all + h->n_stereo_all == h->n_mono;
+}
+static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2) {
+    hipStream_t st = h->stream;
+    const State &s = h->st[0];
+    const int P = h->n_pts, E = h->n_mono;
+    const size_t head = (size_t)(s.pts - s.Rwb), fl = ((size_t)E + 7) / 8;
+    double *d_pts = h->d_stage + head;
+    uint8_t *d_flags = (uint8_t *)(d_pts + 3 * (size_t)P);
+    double *d_chi2 = d_pts + 3 * (size_t)P + fl;
+    if (!h->host_lm) accept_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
+    const int n = std::max(std::max(E, P), (int)head);
+    epilogue_kernel<<<(n + 255) / 256, 256, 0, st>>>(h->rig, s, h->E, h->d_perm_edge, h->n_mono_all, h->d_track_depth,
+                                                     h->d_perm_pt, P, d_flags, want_chi2 ? d_chi2 : nullptr, d_pts,
+                                                     h->d_chi2, h->d_stage, (int)head);
+    HIP_OK(hipGetLastError());
+    const size_t bytes = (head + 3 * (size_t)P + fl + (want_chi2 ? (size_t)E : 0)) * sizeof(double);
+    HIP_OK(hipMemcpyAsync(h->h_stage, h->d_stage, bytes, hipMemcpyDeviceToHost, st));
+    h->epi_ready = true, h->epi_chi2 = want_chi2;
+    return OMV_OK;
+}
+
 static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *p, omv_lba_result *res) {
     hipStream_t st = h->stream;
-    // write back the state (caller order)
     const State &s = h->st[h->cur];
     const int K = h->n_kf, C = h->rig.n_cams, P = h->n_pts, E = h->n_mono;
-    std::vector<double> stg(h->state_doubles()), chi2(E);
-    HIP_OK(hipMemcpyAsync(stg.data(), s.Rwb, stg.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-    if (E > 0) HIP_OK(hipMemcpyAsync(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    {
-        const double *q = stg.data();
+    const bool fail = (2 * res->err < res->err_end || std::isnan(res->err) || std::isnan(res->err_end)) && !o->large;
+    res->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
+    auto take_head = [&](const double *q) {
         auto take = [&](double *dst, size_t n) {
             std::memcpy(dst, q, n * sizeof(double));
             q += n;
         };
         take(p->Rwb, 9 * (size_t)K), take(p->twb, 3 * (size_t)K), take(p->Rcw, 9 * (size_t)K * C);
         take(p->tcw, 3 * (size_t)K * C), take(p->vel, 3 * (size_t)K), take(p->bg, 3 * (size_t)K), take(p->ba, 3 * (size_t)K);
+    };
+    if (lba_epilogue_ok(h)) {
+        // device epilogue: outlier flags / chi2 / points in the caller's order, one staging read-back (already in
+        // flight with the LM control's last read-back when the device driver ran)
+        const bool want_chi2 = res->mono_chi2 || res->stereo_chi2;
+        if (!h->epi_ready || (want_chi2 && !h->epi_chi2)) {
+            omv_status rs = lba_enqueue_epilogue(h, want_chi2);
+            if (rs != OMV_OK) return rs;
+            HIP_OK(hipStreamSynchronize(st));
+        }
+        h->epi_ready = false;
+        const size_t head = (size_t)(s.pts - s.Rwb);
+        take_head(h->h_stage);
+        std::memcpy(p->pts, h->h_stage + head, 3 * sizeof(double) * (size_t)P);
+        const uint8_t *hf = (const uint8_t *)(h->h_stage + head + 3 * (size_t)P);
+        const double *hc = h->h_stage + head + 3 * (size_t)P + ((size_t)E + 7) / 8;
+        const int EM = h->n_mono_all, ES = h->n_stereo_all;
+        if (res->mono_chi2) std::memcpy(res->mono_chi2, hc, sizeof(double) * EM);
+        if (res->stereo_chi2) std::memcpy(res->stereo_chi2, hc + EM, sizeof(double) * ES);
+        if (res->mono_outlier) std::memcpy(res->mono_outlier, hf, EM);
+        if (res->stereo_outlier) std::memcpy(res->stereo_outlier, hf + EM, ES);
+        return OMV_OK;
+    }
+    // sharded rank: this rank's landmarks and edges only, on the host
+    std::vector<double> stg(h->state_doubles()), chi2(E);
+    HIP_OK(hipMemcpyAsync(stg.data(), s.Rwb, stg.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (E > 0) HIP_OK(hipMemcpyAsync(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    take_head(stg.data());
+    {
+        const double *q = stg.data() + (s.pts - s.Rwb);
         for (int i = 0; i < P; ++i)
             for (int d = 0; d < 3; ++d) p->pts[3 * (size_t)h->perm_pt[i] + d] = q[3 * (size_t)i + d];
     }
@@ -2004,8 +2288,6 @@ static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_p
             res->mono_outlier[oe] = ((c2 > 5.991f && !close) || (c2 > 1.5f * 5.991f && close) || !depth_pos) ? 1 : 0;
         }
     }
-    const bool fail = (2 * res->err < res->err_end || std::isnan(res->err) || std::isnan(res->err_end)) && !o->large;
-    res->status = fail ? OMV_LBA_FAIL : OMV_LBA_OK;
     return OMV_OK;
 }
 

@@ -73,18 +73,20 @@ class LocalInertialBA:
         self._s, self._keep = s, keep
         return self
 
-    def optimize(self, opt_it=10, lambda_init=1e0, max_trials=10, large=False):
+    def optimize(self, opt_it=10, lambda_init=1e0, max_trials=10, large=False, chi2=True):
+        """chi2=False: only the outlier flags (what the reference's culling uses), no per-edge chi2 read-back."""
         if self._s is None:
             raise _lib.OmvError("LocalInertialBA.optimize: no problem set")
         o = _lib.LbaOpts(int(opt_it), float(lambda_init), int(max_trials), int(bool(large)))
         E, S = self._s.n_mono, self._s.n_stereo
-        chi2 = np.zeros(E)
+        want = bool(chi2)
+        chi2 = np.zeros(E) if want else None
         outl = np.zeros(E, np.uint8)
-        s_chi2 = np.zeros(S)
+        s_chi2 = np.zeros(S) if want else None
         s_outl = np.zeros(S, np.uint8)
         r = _lib.LbaResult()
-        r.mono_chi2, r.mono_outlier = _lib.ptr(chi2), _lib.ptr(outl)
-        r.stereo_chi2, r.stereo_outlier = _lib.ptr(s_chi2), _lib.ptr(s_outl)
+        r.mono_chi2, r.mono_outlier = (_lib.ptr(chi2) if want else None), _lib.ptr(outl)
+        r.stereo_chi2, r.stereo_outlier = (_lib.ptr(s_chi2) if want else None), _lib.ptr(s_outl)
         _lib.check(self._lib.omv_lba_optimize(self._h, ctypes.byref(o), ctypes.byref(self._s), ctypes.byref(r)),
                    "omv_lba_optimize")
         res = dict(err=r.err, err_end=r.err_end, status=r.status, iterations=r.iterations, trials=r.trials,

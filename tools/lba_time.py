@@ -18,7 +18,7 @@ ba.set_problem(prob)
 for i in range(runs):
     ba.reset()
     t = time.time()
-    r, s = ba.optimize(opt_it=4, lambda_init=1e-2, large=True)
+    r, s = ba.optimize(opt_it=4, lambda_init=1e-2, large=True, chi2=False)
     dt = time.time() - t
     print(json.dumps(dict(wall_ms=round(dt * 1e3, 3), err=r["err"], err_end=r["err_end"],
                           **{k: round(float(v), 4) for k, v in ba.stage_ms().items()})))
