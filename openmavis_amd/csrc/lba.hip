@@ -597,6 +597,10 @@ __global__ void __launch_bounds__(kLandWG) build_kernel(Rig rig, State s, Edges 
 // pj, row-major 16x16 each, holding H's block (perm[pi], perm[pj]).  Padding rows have zero gradient and
 // lambda on the diagonal, so they solve to exactly zero and add nothing to computeScale.  b and the Schur
 // right-hand side stay in keyframe order (16 k + r).
+// Entry (r, c) of a 16x16 block sits at 16 r + (c ^ r): a column read by 16 lanes (one per row), as the MFMA
+// A operands and the pivot columns are, touches 16 distinct LDS banks instead of two (rows are 32 banks apart).
+__host__ __device__ __forceinline__ int sw16(int r, int c) { return 16 * r + (c ^ r); }
+
 struct BlockPat {
     int nb, n_slots, n_lev;
     const int *perm;                 // [nb] position -> keyframe
@@ -716,7 +720,7 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
             v -= ordered_sum(G.schur_part + 6 * r + c, c0, c1, 42);
         }
     }
-    S[(size_t)t * 256 + tid] = v;
+    S[(size_t)t * 256 + sw16(r, c)] = v;
     if (diag && tid < 16) {   // b and the Schur right-hand side of keyframe kr
         double bv = 0, cf = 0;
         if (tid < 6) {
@@ -777,17 +781,17 @@ __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
     double cur[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) cur[t] = D[lane + 64 * t];
+    for (int t = 0; t < 4; ++t) cur[t] = D[sw16(q + 4 * t, j)];
 #pragma unroll
     for (int c0 = 0; c0 < 16; c0 += 2) {
-        const double p00 = D[c0 * 17], p10 = D[(c0 + 1) * 16 + c0], p11 = D[(c0 + 1) * 17];
+        const double p00 = D[sw16(c0, c0)], p10 = D[sw16(c0 + 1, c0)], p11 = D[sw16(c0 + 1, c0 + 1)];
         double bi0[4], bi1[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            bi0[t] = D[(q + 4 * t) * 16 + c0];
-            bi1[t] = D[(q + 4 * t) * 16 + c0 + 1];
+            bi0[t] = D[sw16(q + 4 * t, c0)];
+            bi1[t] = D[sw16(q + 4 * t, c0 + 1)];
         }
-        const double bj0 = D[j * 16 + c0], bj1 = D[j * 16 + c0 + 1];
+        const double bj0 = D[sw16(j, c0)], bj1 = D[sw16(j, c0 + 1)];
         // the two reciprocals are independent (d1 = det / p00, 1 / d1 = p00 / det): one latency, not two
         const double det = p00 * p11 - p10 * p10;
         const double i0 = rcp_nr(p00), idet = rcp_nr(det);
@@ -821,12 +825,12 @@ __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
         }
         if (j == c0 + 2 || j == c0 + 3) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) D[lane + 64 * t] = cur[t];
+            for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];
         }
         wave_sync<G>();
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) D[lane + 64 * t] = cur[t];
+    for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];
     wave_sync<G>();
 }
 
@@ -838,13 +842,13 @@ __device__ __forceinline__ void panel16(double *A, const double *Dk, int lane) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int kk = 4 * s + kq;
-        const double a = A[rc * 16 + kk];
-        const double b = kk < rc ? Dk[kk * 16 + rc] : (kk == rc ? 1.0 : 0.0);   // (L^-T)[kk][col]
+        const double a = A[sw16(rc, kk)];
+        const double b = kk < rc ? Dk[sw16(kk, rc)] : (kk == rc ? 1.0 : 0.0);   // (L^-T)[kk][col]
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
-    const double id = rcp_nr(Dk[rc * 17]);
+    const double id = rcp_nr(Dk[sw16(rc, rc)]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) A[(kq + 4 * i) * 16 + rc] = acc[i] * id;
+    for (int i = 0; i < 4; ++i) A[sw16(kq + 4 * i, rc)] = acc[i] * id;
 }
 
 // One wavefront: S_ij -= L_ik diag(d) L_jk^T.
@@ -852,16 +856,16 @@ __device__ __forceinline__ void update16(double *Sij, const double *Lik, const d
     const int rc = lane & 15, kq = lane >> 4;
     v4d acc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = Sij[(kq + 4 * i) * 16 + rc];
+    for (int i = 0; i < 4; ++i) acc[i] = Sij[sw16(kq + 4 * i, rc)];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int kk = 4 * s + kq;
-        const double a = -Lik[rc * 16 + kk] * Dk[kk * 17];
-        const double b = Ljk[rc * 16 + kk];
+        const double a = -Lik[sw16(rc, kk)] * Dk[sw16(kk, kk)];
+        const double b = Ljk[sw16(rc, kk)];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Sij[(kq + 4 * i) * 16 + rc] = acc[i];
+    for (int i = 0; i < 4; ++i) Sij[sw16(kq + 4 * i, rc)] = acc[i];
 }
 
 constexpr int kLdltThreads = 512;
@@ -874,10 +878,10 @@ __device__ __forceinline__ void forward_col(const double *pk, double *y, const B
     double acc = 0;
     for (int q = P.rs_start[i] + grp; q < P.rs_start[i + 1]; q += 4) {
         const int2 e = P.rs[q];
-        const double *Lik = pk + (size_t)e.x * 256 + r16 * 16;
+        const double *Lik = pk + (size_t)e.x * 256;
         const double *yk = y + 16 * e.y;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc += Lik[m] * yk[m];
+        for (int m = 0; m < 16; ++m) acc += Lik[sw16(r16, m)] * yk[m];
     }
     acc += __shfl_xor(acc, 16, 64);
     acc += __shfl_xor(acc, 32, 64);
@@ -887,7 +891,7 @@ __device__ __forceinline__ void forward_col(const double *pk, double *y, const B
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const double vm = __shfl(v, m, 16);
-        out += (m < r16 ? Di[m * 16 + r16] : 0.0) * vm;
+        out += (m < r16 ? Di[sw16(m, r16)] : 0.0) * vm;
     }
     if (lane < 16) y[16 * i + lane] = out;
 }
@@ -976,7 +980,7 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 #ifdef OMV_LDLT_PROFILE
     t_2 = wall_clock64();
 #endif
-    for (int q = tid; q < nv; q += blockDim.x) y[q] /= pk[(size_t)P.dslot[q >> 4] * 256 + (q & 15) * 17];
+    for (int q = tid; q < nv; q += blockDim.x) y[q] /= pk[(size_t)P.dslot[q >> 4] * 256 + sw16(q & 15, q & 15)];
     __syncthreads();
     // backward: x_k = L_kk^-T (z_k - sum_i L_ik^T x_i)
     for (int lev = P.n_lev - 1; lev >= 0; --lev) {
@@ -985,20 +989,20 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
             double acc = 0;
             for (int q = P.cs_start[k] + grp; q < P.cs_start[k + 1]; q += 4) {
                 const int2 e = P.cs[q];
-                const double *Lik = pk + (size_t)e.x * 256 + r16;
+                const double *Lik = pk + (size_t)e.x * 256;
                 const double *xi = xs + 16 * e.y;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc += Lik[r * 16] * xi[r];
+                for (int r = 0; r < 16; ++r) acc += Lik[sw16(r, r16)] * xi[r];
             }
             acc += __shfl_xor(acc, 16, 64);
             acc += __shfl_xor(acc, 32, 64);
             const double v = y[16 * k + r16] - acc;
-            const double *row = pk + (size_t)P.dslot[k] * 256 + r16 * 16;
+            const double *Dk = pk + (size_t)P.dslot[k] * 256;
             double out = v;
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
                 const double vm = __shfl(v, m, 16);
-                out += (m > r16 ? row[m] : 0.0) * vm;
+                out += (m > r16 ? Dk[sw16(r16, m)] : 0.0) * vm;
             }
             if (lane < 16) xs[16 * k + lane] = out;
         }
