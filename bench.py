@@ -300,8 +300,18 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
         "dtype": "f64",
         "roofline": {"kernel": "whole LM trial", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None, "algorithmic_bytes_per_trial": bpt},
+                     "traffic": lba_traffic(), "algorithmic_bytes_per_trial": bpt,
+                     "traffic_source": "profiles/pmc_lba_trial.json (FETCH_SIZE / WRITE_SIZE passes over tools/lba_time.py)"},
     }
+
+
+def lba_traffic():
+    """HBM bytes per LM trial from the last profile's PMC passes (profiles/pmc_lba_trial.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_lba_trial.json")
+    try:
+        return int(json.load(open(p))["hbm_bytes_per_trial"])
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def pose_leg(batch, cpu_batch, reps, dev, last_frame=False):

@@ -19,8 +19,9 @@ SHORT = {"pyr_resize": "pyr_resize", "fast_cells": "fast_cells", "octree": "octr
          "blur_kernel": "blur", "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
          "stereo_tri_kernel": "stereo_tri", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
          "frustum_kernel": "frustum", "uright_kernel": "uright", "err_kernel": "lba_err", "build_kernel": "lba_build",
-         "schur_kernel": "lba_schur", "ldlt_kernel": "lba_ldlt", "backsub_kernel": "lba_backsub",
-         "update_kf_kernel": "lba_update_kf", "finish_kernel": "lba_finish", "zero_kernel": "lba_zero"}
+         "schur_kernel": "lba_schur", "assemble_kernel": "lba_assemble", "ldlt_kernel": "lba_ldlt",
+         "update_kernel": "lba_update", "finish_trial_kernel": "lba_finish_trial", "accept_copy_kernel": "lba_accept",
+         "epilogue_kernel": "lba_epilogue", "ctl_init_kernel": "lba_ctl_init"}
 # PMC programs (tools/profile_gpu.sh): units one launch covers
 PMC_SOURCES = {"orb": ("images", 160), "match": ("frames", 32), "lba": ("launches", 1)}
 
@@ -84,6 +85,21 @@ def main(src, tag, command=None):
             if srcname == "match" and os.path.exists(out) and json.load(open(out)).get("program") == "orb":
                 continue   # extraction kernels keep the extraction-only program's numbers
             json.dump(rec, open(out, "w"), indent=1)
+    # LocalInertialBA: every kernel of the lba program (tools/lba_time.py), per LM trial
+    lba = [(k, d) for (s, k), d in pmc.items() if s == "lba" and k.startswith("lba_")]
+    trials = 0
+    tf = os.path.join(src, "lba_FETCH_SIZE.txt")
+    if os.path.exists(tf):
+        for line in open(tf):
+            if line.startswith("{"):
+                trials += int(json.loads(line).get("trials", 0))
+    if lba and trials:
+        tot = sum(2 * sum(d["FETCH_SIZE"]) + sum(d["WRITE_SIZE"]) for _, d in lba) * 1024
+        rec = {"kernel": "lba_trial", "tag": tag, "program": "lba", "trials": trials, "hbm_bytes_per_trial": round(tot / trials),
+               "kernels": sorted(k for k, _ in lba), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024, summed over the "
+               "LocalInertialBA kernels of tools/lba_time.py (set-up uploads excluded), per LM trial"}
+        json.dump(rec, open(os.path.join(prof, "pmc_lba_trial.json"), "w"), indent=1)
+        lines += ["", f"LocalInertialBA per LM trial: {rec['hbm_bytes_per_trial']} B of HBM traffic ({trials} trials)"]
     open(os.path.join(prof, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
