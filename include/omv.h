@@ -497,6 +497,48 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
                                                 int32_t *n_matches, void *stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * ORBmatcher::SearchByBoW — Hamming matching of the keypoints that share a vocabulary node (DBoW2
+ * FeatureVector, node ids ascending), with the rotation-consistency filter (ComputeThreeMaxima):
+ *   OMV_BOW_KF_FRAME  SearchByBoW(KeyFrame *pKF, Frame &F, vpMapPointMatches) (src/ORBmatcher.cc:349-666):
+ *                     per keyframe keypoint with a map point, the best unmatched frame keypoint of each
+ *                     camera block (L [0, Nleft), R, SL, SR by the frame's ranges; F.n_left = -1: one block),
+ *                     left accepted at <= TH_LOW with the nnratio test, right / side blocks accepted at
+ *                     <= TH_LOW (their ratio test is `|| true`) and only when the left best passed TH_LOW.
+ *                     Called by Tracking::TrackReferenceKeyFrame / Relocalization.
+ *   OMV_BOW_KF_KF     SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, vpMatches12) (:1006-1129): per pKF1
+ *                     keypoint with a map point the best unclaimed pKF2 keypoint with a map point (vbMatched2),
+ *                     accepted at < TH_LOW with the nnratio test.  Called by LoopClosing's place recognition.
+ * One wavefront per job; jobs are independent.  `kf.has_mp` / `other.has_mp` = GetMapPoint(idx) && !isBad().
+ * ---------------------------------------------------------------------------------------------- */
+enum { OMV_BOW_KF_FRAME = 0, OMV_BOW_KF_KF = 1 };
+
+typedef struct omv_bow_job {
+    omv_kf_view kf;         /* pKF / pKF1 (its kps give the keyframe keypoint angles, mvKeysUn order) */
+    omv_kf_view other;      /* F (n_sideleft = -1: no side cameras) / pKF2 */
+    int32_t *match;         /* device: OMV_BOW_KF_FRAME [other.n] vpMapPointMatches as the keyframe keypoint
+                               index whose map point the frame keypoint received (-1 none);
+                               OMV_BOW_KF_KF [kf.n] vpMatches12 as the pKF2 keypoint index (-1 none) */
+} omv_bow_job;
+
+/* jobs: host [n_jobs]; n_matches: device [n_jobs] (the reference's return value).  Up to 16384 keypoints
+ * per view (OMV_ERR_CAPACITY beyond). */
+omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_job *jobs, int mode, float nnratio,
+                                     int check_ori, int32_t *n_matches, void *stream);
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (src/ORBmatcher.cc:
+ * 895-1004): for every level-0 keypoint of F1 in order, Frame::GetFeaturesInArea(vbPrevMatched[i1], windowSize,
+ * 0, 0) on F2's grid (the last omv_matcher_assign_grid batch, camera block 0: F2.mvKeysUn), the best candidate
+ * whose previous match (vMatchedDistance) is strictly worse, accepted at <= TH_LOW with the nnratio test; a
+ * better later F1 keypoint takes the F2 keypoint over; rotation-consistency filter; vbPrevMatched updated to the
+ * matched F2 keypoints.  pairs: host [n_pairs][2] (F1, F2) frame indices of the batch; prev_matched: device
+ * [n_pairs][kp_cap][2] in/out; matches12: device [n_pairs][kp_cap] (vnMatches12, -1 none); n_matches: device
+ * [n_pairs].  F1's keypoints are frame pairs[i][0]'s block 0 (mvKeysUn). */
+omv_status omv_matcher_search_for_initialization(omv_matcher *m, int n_pairs, const int32_t *pairs,
+                                                 const omv_frame_geom *geom, const omv_kp *kps, const uint8_t *desc,
+                                                 const int *n_kp, float *prev_matched, int window, float nnratio,
+                                                 int check_ori, int32_t *matches12, int32_t *n_matches, void *stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Pose-inertial optimisation of tracked frames — replaces Optimizer::PoseInertialOptimizationLastKeyFrame
  * (src/Optimizer.cc:5021-5578): Gauss-Newton (4 rounds x 10 iterations, dense LDLT) over the frame's
  * VertexPose / VertexVelocity / VertexGyroBias / VertexAccBias with the last keyframe's vertices fixed;

@@ -162,6 +162,14 @@ class TriPair(ctypes.Structure):
                 ("match12", ctypes.c_void_p)]
 
 
+class BowJob(ctypes.Structure):
+    """omv_bow_job (include/omv.h)."""
+    _fields_ = [("kf", KfView), ("other", KfView), ("match", ctypes.c_void_p)]
+
+
+OMV_BOW_KF_FRAME, OMV_BOW_KF_KF = 0, 1
+
+
 class FisheyeUndist(ctypes.Structure):
     """omv_fisheye_undist (include/omv.h)."""
     _fields_ = [("K", ctypes.c_float * 4), ("D", ctypes.c_double * 4), ("newK", ctypes.c_float * 4)]
@@ -236,6 +244,9 @@ SIGNATURES = {
     "omv_matcher_stereo_triangulate": (_I, [_VP, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _VP,
                                             _VP, _VP]),
     "omv_matcher_search_for_triangulation": (_I, [_VP, _I, ctypes.POINTER(TriPair), _VP, _I, _I, _I, _VP, _VP]),
+    "omv_matcher_search_by_bow": (_I, [_VP, _I, ctypes.POINTER(BowJob), _I, _F, _I, _VP, _VP]),
+    "omv_matcher_search_for_initialization": (_I, [_VP, _I, _VP, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _VP, _I,
+                                                   _F, _I, _VP, _VP, _VP]),
     "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),
     "omv_pose_destroy": (_I, [_VP]),
     "omv_pose_inertial_last_kf": (_I, [_VP, ctypes.POINTER(PoseBatch), _I, _VP, _VP, _VP, _VP]),

@@ -1598,6 +1598,157 @@ __global__ void __launch_bounds__(64) kf_resolve_kernel(KfArgs a) {
     }
 }
 
+// ---- ORBmatcher::SearchForInitialization (ORBmatcher.cc:895-1004) ---------------------------------------
+// One wavefront per frame pair, F1's level-0 keypoints in order (the claims are sequential: vMatchedDistance /
+// vnMatches21 of F2 change with every accepted match).  For one F1 keypoint the lanes take the window's
+// candidates of each grid column (GetFeaturesInArea order: columns ix, the column's cells iy contiguous in the
+// CSR, keypoints ascending), each keeping its best (distance, window position) key and second distance; one
+// min-reduction gives the reference's best (first minimal distance) and second.  The F2 claim state, F1's
+// matches and rotation bins live in LDS.
+struct InitArgs {
+    FrameArgs f;
+    const int32_t *pairs;   // [n][2] (F1, F2) frame indices
+    float *prev;            // [n][kp_cap][2] vbPrevMatched in/out
+    int window;
+    float nnratio;
+    int check_ori;
+    int32_t *m12;           // [n][kp_cap]
+    int32_t *n_matches;     // [n]
+};
+
+__host__ __device__ inline size_t init_lds_bytes(int cap) { return (size_t)cap * 13 + 4 * 36 + 16; }
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
+__global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int ism[];
+    const FrameArgs &f = a.f;
+    const int cap = f.kp_cap, lane = threadIdx.x, pr = blockIdx.x;
+    int *mdist = ism, *m21 = ism + cap, *m12 = ism + 2 * cap;
+    int *cnt = ism + 3 * cap, *ind = cnt + 30;
+    uint8_t *bins = reinterpret_cast<uint8_t *>(ind + 4);
+    const size_t fc1 = (size_t)a.pairs[2 * pr] * f.n_cams, fc2 = (size_t)a.pairs[2 * pr + 1] * f.n_cams;   // block 0
+    const int n1 = f.n_kp[fc1], n2 = f.n_kp[fc2];
+    const omv_kp *kp1 = f.kps + fc1 * cap, *kp2 = f.kps + fc2 * cap;
+    const uint8_t *ds1 = f.desc + fc1 * cap * 32, *ds2 = f.desc + fc2 * cap * 32;
+    const int32_t *cs = f.cell_start + fc2 * (kCells + 1), *ci = f.cell_idx + fc2 * cap;
+    float *prev = a.prev + (size_t)pr * cap * 2;
+    for (int i = lane; i < n1; i += 64) m12[i] = -1, bins[i] = 0xff;
+    for (int i = lane; i < n2; i += 64) mdist[i] = INT_MAX, m21[i] = -1;
+    if (lane < 30) cnt[lane] = 0;
+    __syncthreads();
+    const float r = (float)a.window;
+    int nm = 0;
+    for (int i1 = 0; i1 < n1; ++i1) {
+        const omv_kp k1 = kp1[i1];
+        if (k1.octave > 0) continue;
+        const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+        // Frame::GetFeaturesInArea(x, y, windowSize, 0, 0) window (Frame.cc:890-967)
+        const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+        if (nMinCellX >= kGridCols) continue;
+        const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+        if (nMaxCellX < 0) continue;
+        const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+        if (nMinCellY >= kGridRows) continue;
+        const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+        if (nMaxCellY < 0) continue;
+        uint64_t d1[4];
+        load_desc(ds1 + (size_t)i1 * 32, d1);
+        uint32_t bk = 0xffffffffu;
+        int sec = INT_MAX, bidx = -1, ord = 0;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+            const int p0 = cs[ix * kGridRows + nMinCellY], p1 = cs[ix * kGridRows + nMaxCellY + 1];
+            for (int p = p0 + lane; p < p1; p += 64) {
+                const int i2 = ci[p];
+                const omv_kp k = kp2[i2];
+                if (k.octave != 0) continue;   // levels [0, 0]
+                if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+                uint64_t d2[4];
+                load_desc(ds2 + (size_t)i2 * 32, d2);
+                const int dist = omv::hamming256(d1, d2);
+                if (mdist[i2] <= dist) continue;
+                const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)(ord + p - p0);
+                if (key < bk) {   // this lane's candidates arrive in window order
+                    if (bk != 0xffffffffu) sec = min(sec, (int)(bk >> 16));
+                    bk = key, bidx = i2;
+                } else {
+                    sec = min(sec, dist);
+                }
+            }
+            ord += p1 - p0;
+        }
+        const uint32_t g = wave_min_u32(bk);
+        if (g == 0xffffffffu) continue;   // no candidate (vIndices2 empty, or all skipped)
+        const uint32_t other = bk == g ? (uint32_t)sec : (bk == 0xffffffffu ? (uint32_t)INT_MAX : bk >> 16);
+        const int bestDist2 = (int)wave_min_u32(other), bestDist = (int)(g >> 16);
+        const int src = __ffsll((long long)__ballot(bk == g)) - 1;
+        const int bestIdx2 = __shfl(bidx, src, 64);
+        if (bestDist <= 50 && (float)bestDist < (float)bestDist2 * a.nnratio) {
+            const int old = m21[bestIdx2];
+            if (old >= 0) --nm;
+            ++nm;
+            if (lane == 0) {
+                if (old >= 0) m12[old] = -1;
+                m12[i1] = bestIdx2, m21[bestIdx2] = i1, mdist[bestIdx2] = bestDist;
+                if (a.check_ori) {   // rot = angle1 - angle2, +360 if negative, bin = round(rot / 30), 30 -> 0
+                    float rot = k1.angle - kp2[bestIdx2].angle;
+                    if (rot < 0.0f) rot += 360.0f;
+                    int bin = (int)roundf(rot * (1.0f / 30));
+                    if (bin == 30) bin = 0;
+                    bins[i1] = (uint8_t)bin;
+                    ++cnt[bin];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (a.check_ori) {   // ComputeThreeMaxima, then every push outside the top bins that is still matched
+        if (lane == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < 30; i++) {
+                const int s = cnt[i];
+                if (s > max1) {
+                    max3 = max2, max2 = max1, max1 = s;
+                    ind3 = ind2, ind2 = ind1, ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2, max2 = s;
+                    ind3 = ind2, ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1, ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            ind[0] = ind1, ind[1] = ind2, ind[2] = ind3;
+        }
+        __syncthreads();
+        int removed = 0;
+        for (int i = lane; i < n1; i += 64) {
+            const int bn = bins[i];
+            if (bn != 0xff && bn != ind[0] && bn != ind[1] && bn != ind[2] && m12[i] >= 0) m12[i] = -1, ++removed;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) removed += __shfl_xor(removed, d, 64);
+        nm -= removed;
+        __syncthreads();
+    }
+    int32_t *out = a.m12 + (size_t)pr * cap;
+    for (int i = lane; i < n1; i += 64) {
+        const int m = m12[i];
+        out[i] = m;
+        if (m >= 0) prev[2 * i] = kp2[m].x, prev[2 * i + 1] = kp2[m].y;   // vbPrevMatched update
+    }
+    if (lane == 0) a.n_matches[pr] = nm;
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -1949,6 +2100,35 @@ omv_status omv_matcher_stereo_lapping(omv_matcher *h, int n_frames, const uint8_
     stereo_pairs_kernel<<<g2, 256, 0, st>>>(h->d_knn_i, h->d_knn_d, cap, n_kp, mono, C, cap, ratio, l2r, r2l, n_frames);
     if (h->timing) h->ev.push_back({1, {e0, mk_event(st)}});
     HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+
+omv_status omv_matcher_search_for_initialization(omv_matcher *h, int n_pairs, const int32_t *pairs,
+                                                 const omv_frame_geom *g, const omv_kp *kps, const uint8_t *desc,
+                                                 const int *n_kp, float *prev_matched, int window, float nnratio,
+                                                 int check_ori, int32_t *matches12, int32_t *n_matches, void *stream) {
+    if (!h || n_pairs < 0 || (n_pairs > 0 && (!pairs || !g || !kps || !desc || !n_kp || !prev_matched || !matches12 ||
+                                              !n_matches)) ||
+        g->n_cams != h->n_cams || window < 0)
+        return OMV_ERR_ARG;
+    if (n_pairs == 0) return OMV_OK;
+    for (int i = 0; i < 2 * n_pairs; ++i)
+        if (pairs[i] < 0 || pairs[i] >= h->max_frames) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    FrameArgs f;
+    fill_frame(h, g, kps, desc, n_kp, f);
+    const size_t lds = init_lds_bytes(h->kp_cap);
+    if (lds > 160 * 1024) return OMV_ERR_CAPACITY;
+    HIP_OK(hipFuncSetAttribute((const void *)init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int32_t *d_pairs = nullptr;
+    HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(int32_t) * 2 * n_pairs, st));
+    HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(int32_t) * 2 * n_pairs, hipMemcpyHostToDevice, st));
+    InitArgs ia{f, d_pairs, prev_matched, window, nnratio, check_ori, matches12, n_matches};
+    init_kernel<<<n_pairs, 64, lds, st>>>(ia);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipFreeAsync(d_pairs, st));
     return OMV_OK;
 }
 

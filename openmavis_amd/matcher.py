@@ -93,6 +93,28 @@ class TriPairBatch:
             self.device = p["match12"].device
 
 
+class BowJobBatch:
+    """The omv_bow_job array of a list of SearchByBoW jobs (see ORBmatcher.SearchByBoW), built once."""
+
+    def __init__(self, jobs):
+        from .synth_tri import kf_struct
+        self.n = len(jobs)
+        self.arr = (_lib.BowJob * max(self.n, 1))()
+        self._keep = []
+        self.device = None
+
+        def ptr(_name, t):
+            self._keep.append(t)
+            return ctypes.c_void_p(t.data_ptr())
+
+        for i, j in enumerate(jobs):
+            self.arr[i].kf = kf_struct(j["kf"], _lib.KfView, j["kf"].get("level_sigma2", np.ones(16)), ptr)
+            self.arr[i].other = kf_struct(j["other"], _lib.KfView, j["other"].get("level_sigma2", np.ones(16)), ptr)
+            self.arr[i].match = ctypes.c_void_p(j["match"].data_ptr())
+            self._keep.append(j["match"])
+            self.device = j["match"].device
+
+
 class ORBmatcher:
     def __init__(self, nnratio=0.6, checkOri=True):
         self.mfNNratio = float(nnratio)
@@ -222,6 +244,51 @@ class ORBmatcher:
             self._h, n, arr, _lib.ptr(c), int(bool(bOnlyStereo)), int(bool(bCoarse)), int(self.mbCheckOrientation),
             _lib.ptr(out), self._stream(stream)), "omv_matcher_search_for_triangulation")
         return out[:n]
+
+    def _scratch_handle(self):
+        if self._h is None:
+            h = ctypes.c_void_p()
+            _lib.check(self._lib.omv_matcher_create(1, 1, 1, 1, ctypes.byref(h)), "omv_matcher_create")
+            self._h, self._shape = h, (1, 1, 1, 1)
+        return self._h
+
+    def SearchByBoW(self, jobs, kf_kf=False, stream=None):
+        """ORBmatcher::SearchByBoW (src/ORBmatcher.cc:349-666, (KeyFrame, Frame); with kf_kf the (KeyFrame,
+        KeyFrame) overload :1006-1129) for a batch of jobs.  jobs: list of dicts {kf, other, match}: kf / other
+        hold the omv_kf_view fields (n, n_left, n_right, n_sideleft ints; kps / desc / has_mp / node_id /
+        node_start / node_idx device tensors; n_left = -1 for a single-camera frame, n_sideleft = -1 without side
+        cameras), match a device int32 tensor: (KF, F) [other.n] the keyframe keypoint whose map point each frame
+        keypoint received, (KF1, KF2) [kf.n] the pKF2 keypoint of each pKF1 keypoint (-1 none).  `jobs` may be a
+        prebuilt BowJobBatch.  Returns the per-job match counts (device int32 tensor); synchronous."""
+        import torch
+        h = self._scratch_handle()
+        batch = jobs if isinstance(jobs, BowJobBatch) else BowJobBatch(jobs)
+        out = torch.zeros(max(batch.n, 1), dtype=torch.int32, device=batch.device)
+        _lib.check(self._lib.omv_matcher_search_by_bow(
+            h, batch.n, batch.arr, _lib.OMV_BOW_KF_KF if kf_kf else _lib.OMV_BOW_KF_FRAME, ctypes.c_float(self.mfNNratio),
+            int(self.mbCheckOrientation), _lib.ptr(out), self._stream(stream)), "omv_matcher_search_by_bow")
+        return out[:batch.n]
+
+    def SearchForInitialization(self, frames, pairs, prev_matched, windowSize=100, stream=None, grid_ready=False):
+        """ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+        (src/ORBmatcher.cc:895-1004) for frame pairs of a single-camera FrameBatch (block 0 = mvKeysUn).  pairs:
+        [(f1, f2), ...] frame indices; prev_matched: device float32 [n_pairs, kp_cap, 2] (vbPrevMatched, updated
+        in place).  Returns (vnMatches12 device int32 [n_pairs, kp_cap], per-pair counts device int32)."""
+        import torch
+        h = self._handle(frames)
+        if not grid_ready:
+            self.AssignFeaturesToGrid(frames, stream)
+        pr = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+        n = len(pr)
+        dev = frames.kps.device
+        m12 = torch.full((max(n, 1), frames.kp_cap), -1, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        _lib.check(self._lib.omv_matcher_search_for_initialization(
+            h, n, _lib.ptr(pr), ctypes.byref(frames.geom), _lib.ptr(frames.kps), _lib.ptr(frames.desc),
+            _lib.ptr(frames.n_kp), _lib.ptr(prev_matched), int(windowSize), ctypes.c_float(self.mfNNratio),
+            int(self.mbCheckOrientation), _lib.ptr(m12), _lib.ptr(cnt), self._stream(stream)),
+            "omv_matcher_search_for_initialization")
+        return m12[:n], cnt[:n]
 
     def StereoLapping(self, frames, ratio=0.8, stream=None):
         """Lowe-ratio knn candidates of ComputeMultiFishEyeMatches (before triangulation)."""

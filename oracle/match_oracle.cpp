@@ -615,3 +615,110 @@ int oracle_search_kf(const FrameGeom *g, const KP *kps, const uint8_t *desc, int
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------
+// ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+//                                                    src/ORBmatcher.cc:895-1004 (+ ComputeThreeMaxima :2537-2573)
+// Single-camera frames (F.Nleft == -1): GetFeaturesInArea on F2's mGrid of mvKeysUn with levels [0, 0].
+// The rotation histogram keeps every push, including F1 keypoints whose F2 keypoint a later, better F1
+// keypoint took over (their removal then finds vnMatches12 < 0 and changes nothing), as the reference.
+namespace {
+const int TH_LOW_INIT = 50, HISTO_INIT = 30;
+void three_maxima_init(const int *cnt, int &ind1, int &ind2, int &ind3) {   // ComputeThreeMaxima
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < HISTO_INIT; i++) {
+        const int s = cnt[i];
+        if (s > max1) {
+            max3 = max2, max2 = max1, max1 = s;
+            ind3 = ind2, ind2 = ind1, ind1 = i;
+        } else if (s > max2) {
+            max3 = max2, max2 = s;
+            ind3 = ind2, ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1, ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+// F1: n1 keypoints / descriptors; F2: n2 keypoints / descriptors with geometry g (n_cams ignored: one block);
+// prev [n1][2] in/out (vbPrevMatched); m12 [n1] out.  Returns nmatches.
+int oracle_search_for_initialization(const FrameGeom *g, const KP *kps1, const uint8_t *desc1, int n1, const KP *kps2,
+                                     const uint8_t *desc2, int n2, float *prev, int window, float nnratio,
+                                     int check_ori, int32_t *m12) {
+    FrameGeom g1 = *g;
+    g1.n_cams = 1;
+    View v{&g1, 0, 0, {}, kps2, n2, &n2};
+    build_grids(v);
+    int nmatches = 0;
+    for (int i = 0; i < n1; ++i) m12[i] = -1;
+    std::vector<int> rotHist[HISTO_INIT];
+    const float factor = 1.0f / HISTO_INIT;
+    std::vector<int> vMatchedDistance(n2, INT32_MAX), vnMatches21(n2, -1);
+    for (int i1 = 0; i1 < n1; i1++) {
+        const KP kp1 = kps1[i1];
+        const int level1 = kp1.octave;
+        if (level1 > 0) continue;
+        const std::vector<int> vIndices2 =
+            features_in_area(v, prev[2 * i1], prev[2 * i1 + 1], (float)window, level1, level1, 0);
+        if (vIndices2.empty()) continue;
+        const uint8_t *d1 = desc1 + 32 * (size_t)i1;
+        int bestDist = INT32_MAX, bestDist2 = INT32_MAX, bestIdx2 = -1;
+        for (int i2 : vIndices2) {
+            const int dist = descriptor_distance(d1, desc2 + 32 * (size_t)i2);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_LOW_INIT) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    m12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                m12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (check_ori) {
+                    float rot = kps1[i1].angle - kps2[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)std::round(rot * factor);
+                    if (bin == HISTO_INIT) bin = 0;
+                    rotHist[bin].push_back(i1);
+                }
+            }
+        }
+    }
+    if (check_ori) {
+        int cnt[HISTO_INIT], ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HISTO_INIT; ++i) cnt[i] = (int)rotHist[i].size();
+        three_maxima_init(cnt, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_INIT; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int idx1 : rotHist[i])
+                if (m12[idx1] >= 0) {
+                    m12[idx1] = -1;
+                    nmatches--;
+                }
+        }
+    }
+    for (int i1 = 0; i1 < n1; i1++)
+        if (m12[i1] >= 0) prev[2 * i1] = kps2[m12[i1]].x, prev[2 * i1 + 1] = kps2[m12[i1]].y;
+    return nmatches;
+}
+
+}  // extern "C"

@@ -515,3 +515,45 @@ def bow_transform(v, desc, n_desc, levelsup):
         out.append(dict(word=word[:n], wval=wval[:n], node=node[:n], bow_word=bw[:nb.value], bow_value=bv[:nb.value],
                         fv_node=fvn[:nf.value], fv_start=fvs[:nf.value + 1], fv_idx=fvi[:fvs[nf.value]]))
     return out
+
+
+# ---- SearchByBoW / SearchForInitialization ---------------------------------------------------------
+def search_by_bow(job, kf_kf=False, nnratio=0.75, check_ori=True):
+    """Restated ORBmatcher::SearchByBoW on a job {kf, other} of synth keyframe dicts (numpy):
+    (nmatches, match) with match [other.n] ((KF, F)) or [kf.n] ((KF1, KF2))."""
+    from openmavis_amd._lib import BowJob, KfView, OMV_BOW_KF_FRAME, OMV_BOW_KF_KF
+    from openmavis_amd.synth_tri import kf_struct
+    keep = []
+
+    def arr(_name, a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    j = BowJob()
+    j.kf = kf_struct(job["kf"], KfView, np.ones(16), arr)
+    j.other = kf_struct(job["other"], KfView, np.ones(16), arr)
+    m = np.full(job["kf"]["n"] if kf_kf else job["other"]["n"], -7, np.int32)
+    j.match = ctypes.c_void_p(m.ctypes.data)
+    f = lib().oracle_search_by_bow
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int]
+    n = f(ctypes.cast(ctypes.byref(j), ctypes.c_void_p), OMV_BOW_KF_KF if kf_kf else OMV_BOW_KF_FRAME, nnratio,
+          int(check_ori))
+    return n, m
+
+
+def search_for_initialization(geom, kps1, desc1, kps2, desc2, prev, window=100, nnratio=0.9, check_ori=True):
+    """Restated ORBmatcher::SearchForInitialization: (nmatches, vnMatches12 [n1], vbPrevMatched [n1][2]).
+    kps*: structured (KP_DTYPE) arrays of mvKeysUn; geom: F2's frame geometry."""
+    kps1, kps2 = np.ascontiguousarray(kps1), np.ascontiguousarray(kps2)
+    desc1, desc2 = np.ascontiguousarray(desc1, np.uint8), np.ascontiguousarray(desc2, np.uint8)
+    prev = np.array(prev, np.float32, copy=True).reshape(-1, 2)
+    m12 = np.full(len(kps1), -7, np.int32)
+    f = lib().oracle_search_for_initialization
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+    n = f(ctypes.cast(ctypes.byref(geom), ctypes.c_void_p), _p(kps1), _p(desc1), len(kps1), _p(kps2), _p(desc2),
+          len(kps2), _p(prev), int(window), nnratio, int(check_ori), _p(m12))
+    return n, m12, prev
