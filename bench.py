@@ -502,6 +502,77 @@ def aux_legs(dev, cpu):
         done, t = _cpu_rate(lambda: oracle.preintegrate(sub, cal.Cov, cal.CovWalk), int(sub["start"][-1]))
         out["imu_preint"]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "measurements/s", "cores": 1,
                                              "kind": "port", "sample": f"{done} measurements, oracle, 1 thread, {t:.2f} s"}
+    # ---- SearchByBoW(KF, F): 256 (reference keyframe, multi-camera frame) jobs of ~2,570 keypoints each
+    #      (Tracking::TrackReferenceKeyFrame: ORBmatcher(0.7, true)); (KF1, KF2) on the same pairs
+    from openmavis_amd import synth_init, synth_tri
+    from openmavis_amd.matcher import BowJobBatch
+    pairs = [synth_tri.make_tri_pair(seed=s, n_pts=1200, n_distract=600, mp_frac=0.8) for s in range(16)]
+
+    def view(kf):
+        d = {f: kf[f] for f in ("n", "n_left", "n_right", "n_sideleft")}
+        d["kps"] = torch.from_numpy(kf["kps"].view(np.float32).reshape(-1, 6).copy()).to(dev)
+        for f in ("desc", "has_mp", "node_start", "node_idx"):
+            d[f] = torch.from_numpy(np.ascontiguousarray(kf[f])).to(dev)
+        d["node_id"] = torch.from_numpy(kf["node_id"].view(np.int32).copy()).to(dev)
+        return d
+    views = [(view(p["kf1"]), view(p["kf2"])) for p in pairs]
+    for name, kf_kf, nn in (("search_by_bow", False, 0.7), ("search_by_bow_kf_kf", True, 0.75)):
+        jobs = []
+        for i in range(256):
+            a, o = views[i % len(views)]
+            p = pairs[i % len(pairs)]
+            jobs.append(dict(kf=a, other=o, match=torch.empty(p["kf1"]["n"] if kf_kf else p["kf2"]["n"],
+                                                              dtype=torch.int32, device=dev)))
+        batch = BowJobBatch(jobs)
+        mb = ORBmatcher(nn, True)
+        dt = _timed(lambda: mb.SearchByBoW(batch, kf_kf=kf_kf), 10, dev)
+        nres = mb.SearchByBoW(batch, kf_kf=kf_kf)
+        out[name] = {"metric": f"ORBmatcher::SearchByBoW ({'KeyFrame, KeyFrame' if kf_kf else 'KeyFrame, Frame'}) "
+                               "searches/s", "value": round(256 / dt, 1), "unit": "searches/s",
+                     "ms_per_batch": round(dt * 1e3, 3), "jobs_per_batch": 256,
+                     "keypoints_per_view": int(np.mean([p["kf1"]["n"] for p in pairs])),
+                     "matches_per_search": round(float(nres.float().mean().item()), 1)}
+        if cpu:
+            done, t = _cpu_rate(lambda: [oracle.search_by_bow(dict(kf=p["kf1"], other=p["kf2"]), kf_kf, nn, True)
+                                         for p in pairs[:4]], 4)
+            out[name]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "searches/s", "cores": 1,
+                                         "kind": "port", "sample": f"{done} searches, oracle, 1 thread, {t:.2f} s"}
+    # ---- SearchForInitialization: 64 monocular frame pairs (1,000 keypoints, EuRoC-sized), window 100
+    ip = [synth_init.make_init_pair(seed=s, n=1000) for s in range(8)]
+    cap = max(max(len(p["f1"]["kps"]), len(p["f2"]["kps"])) for p in ip)
+    NP = 64
+    fb = FrameBatch(torch, 2 * NP, 1, cap, synth_init.W, synth_init.H, synth_init.scale_factors(), device=dev)
+    prev0 = torch.zeros((NP, cap, 2), dtype=torch.float32, device=dev)
+    for i in range(NP):
+        p = ip[i % len(ip)]
+        for k, f in enumerate(("f1", "f2")):
+            kp = p[f]["kps"]
+            fb.kps[2 * i + k, 0, :len(kp)] = torch.from_numpy(kp.view(np.int32).reshape(-1, 6).copy())
+            fb.desc[2 * i + k, 0, :len(kp)] = torch.from_numpy(p[f]["desc"])
+            fb.n_kp[2 * i + k, 0] = len(kp)
+        prev0[i, :len(p["prev"])] = torch.from_numpy(p["prev"])
+    mi = ORBmatcher(0.9, True)   # Tracking::MonocularInitialization: ORBmatcher(0.9, true), windowSize 100
+    mi.AssignFeaturesToGrid(fb)
+    prs = [(2 * i, 2 * i + 1) for i in range(NP)]
+    prev = prev0.clone()
+
+    def run_init():
+        prev.copy_(prev0)
+        return mi.SearchForInitialization(fb, prs, prev, 100, grid_ready=True)
+    dt = _timed(run_init, 10, dev)
+    _, ni = run_init()
+    out["search_for_initialization"] = {"metric": "ORBmatcher::SearchForInitialization frame pairs/s",
+                                        "value": round(NP / dt, 1), "unit": "frame pairs/s",
+                                        "ms_per_batch": round(dt * 1e3, 3), "pairs_per_batch": NP,
+                                        "matches_per_pair": round(float(ni.float().mean().item()), 1)}
+    if cpu:
+        g = oracle.frame_geom(1, synth_init.W, synth_init.H, synth_init.scale_factors())
+        done, t = _cpu_rate(lambda: [oracle.search_for_initialization(g, p["f1"]["kps"], p["f1"]["desc"],
+                                                                      p["f2"]["kps"], p["f2"]["desc"], p["prev"])
+                                     for p in ip[:4]], 4)
+        out["search_for_initialization"]["cpu_baseline"] = {
+            "value": round(done / t, 1), "unit": "frame pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} pair searches, oracle, 1 thread, {t:.2f} s"}
     return out
 
 
