@@ -4,15 +4,19 @@
 // claims of earlier keyframe keypoints, the per-camera-block best / second and the rotation-consistency
 // filter (ComputeThreeMaxima, :2537-2573).
 //
-// One wavefront per job.  The node merge and the walk over keyframe keypoints are wave-uniform; for one
-// keyframe keypoint the lanes take the other view's keypoints of the node (64 at a time), each keeping its
-// own best (distance, node position) key and second distance per camera block, and one min-reduction per
-// block combines them: the best is the first minimal distance in node order (the reference's strict `<`
-// update), the second the smallest distance of the others.  Claims live in an LDS bitmap, the matches'
-// rotation bins in LDS bytes; the top-3 filter runs over them at the end.
+// Two launches.  bow_cand_kernel, one thread per keyframe keypoint (position in its FeatureVector CSR): the
+// node's candidates in the other view under the static filters (block ranges, map points, idx < N), their
+// distances, and per camera block the kTop best by (distance, node position) -- the order the reference's
+// strict `<` update ranks them.  bow_resolve_kernel, one wavefront per job: the reference's sequential walk
+// (common nodes ascending = the keyframe CSR order), where only the claims of earlier keyframe keypoints can
+// change a pick: the first two unclaimed entries of each block are its best and second, and a block whose
+// short list runs out while it holds more candidates is rescanned on the wave.  Claims live in an LDS bitmap,
+// the matches' rotation bins in LDS bytes; the top-3 filter runs over them at the end.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <vector>
 
 #include "../../include/omv.h"
 #include "omv_device.h"
@@ -91,11 +95,141 @@ __device__ __forceinline__ int frame_block(const omv_kf_view &F, int idx) {
     return -1;
 }
 
+// Candidate records, one per position q of the keyframe's FeatureVector CSR (the resolve's walk order):
+// [0] o0 (-1: no search) [1] o1 [2] idx1 [3] counts of blocks 0|1 (u16 each) [4] counts 2|3 [5..7] pad,
+// [8 + kTop c + k] the k-th best static candidate of block c as (distance << 23 | rotation bin << 16 | keypoint
+// index), ascending by (distance, node position); 0xffffffff past the end.  Claims are the only dynamic filter, so the first two
+// unclaimed entries are the reference's best and second whenever the block holds <= kTop candidates or two
+// of them are unclaimed; otherwise the resolve rescans the node.
+constexpr int kTop = 8, kRecWords = 8 + 4 * kTop, kChunk = 32;   // kChunk * kRecWords: a multiple of 64
+
+// Static filters + camera block of candidate idx2 (-1: not a candidate whatever the claims)
 template <int MODE>
-__global__ void __launch_bounds__(64) bow_kernel(const omv_bow_job *jobs, float nnratio, int check_ori,
-                                                 int32_t *n_matches, int *err) {
+__device__ __forceinline__ int cand_block(const omv_kf_view &O, int idx2) {
+    if (MODE == OMV_BOW_KF_FRAME) return frame_block(O, idx2);
+    if (O.n_left != -1 && idx2 >= O.n) return -1;
+    return O.has_mp[idx2] ? 0 : -1;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bow_cand_kernel(const omv_bow_job *jobs, const int *rec_off, uint32_t *recs) {
+    constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1;
+    const omv_bow_job &J = jobs[blockIdx.y];
+    const omv_kf_view &K = J.kf, &O = J.other;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= K.n) return;
+    uint32_t *R = recs + ((size_t)rec_off[blockIdx.y] + q) * kRecWords;
+    const int idx1 = K.node_idx[q];
+    int o0 = -1, o1 = -1;
+    if (K.has_mp[idx1] && !(MODE == OMV_BOW_KF_KF && K.n_left != -1 && idx1 >= K.n)) {
+        int lo = 0, hi = K.n_nodes - 1;   // the node holding position q: the last a with node_start[a] <= q
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (K.node_start[mid] <= q) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t id = K.node_id[lo];
+        int l = 0, h = O.n_nodes;   // the same node id in the other view
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (O.node_id[mid] < id) l = mid + 1;
+            else h = mid;
+        }
+        if (l < O.n_nodes && O.node_id[l] == id) o0 = O.node_start[l], o1 = O.node_start[l + 1];
+    }
+    uint32_t key[NB][kTop], ent[NB][kTop];
+    int cnt[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        cnt[c] = 0;
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) key[c][k] = kNone, ent[c][k] = kNone;
+    }
+    if (o0 >= 0) {
+        const uint64_t *dq = reinterpret_cast<const uint64_t *>(K.desc + 32 * (size_t)idx1);
+        const uint64_t d1[4] = {dq[0], dq[1], dq[2], dq[3]};
+        for (int p = o0; p < o1; ++p) {
+            const int idx2 = O.node_idx[p];
+            const int blk = cand_block<MODE>(O, idx2);
+            if (blk < 0) continue;
+            const uint64_t *q2 = reinterpret_cast<const uint64_t *>(O.desc + 32 * (size_t)idx2);
+            const uint64_t d2[4] = {q2[0], q2[1], q2[2], q2[3]};
+            const int dist = omv::hamming256(d1, d2);
+            const int bin = rot_bin(K.kps[idx1].angle, O.kps[idx2].angle);   // static: both angles are fixed
+            uint32_t kk = ((uint32_t)dist << 16) | (uint32_t)(p - o0),
+                     ee = ((uint32_t)dist << 23) | ((uint32_t)bin << 16) | (uint32_t)idx2;
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                if (c != blk) continue;
+                ++cnt[c];
+#pragma unroll
+                for (int k = 0; k < kTop; ++k) {   // insertion into the sorted top list
+                    if (kk < key[c][k]) {
+                        const uint32_t tk = key[c][k], te = ent[c][k];
+                        key[c][k] = kk, ent[c][k] = ee;
+                        kk = tk, ee = te;
+                    }
+                }
+            }
+        }
+    }
+    R[0] = (uint32_t)o0, R[1] = (uint32_t)o1, R[2] = (uint32_t)idx1;
+    R[3] = (uint32_t)min(cnt[0], 0xffff) | (NB > 1 ? (uint32_t)min(cnt[NB > 1 ? 1 : 0], 0xffff) << 16 : 0u);
+    R[4] = NB > 2 ? ((uint32_t)min(cnt[NB > 2 ? 2 : 0], 0xffff) | (uint32_t)min(cnt[NB > 3 ? 3 : 0], 0xffff) << 16) : 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) R[8 + kTop * c + k] = c < NB ? ent[c < NB ? c : 0][k] : kNone;
+}
+
+// The full scan of one keyframe keypoint's node with the current claims (the rare fallback): per block the
+// best (distance, node position) key and second distance over the wave.
+template <int MODE, int NB>
+__device__ void scan_node(const omv_kf_view &O, const uint32_t *claimed, const uint64_t d1[4], int o0, int o1,
+                          int lane, int *bd, int *bi, int *bs) {
+    uint32_t bk[NB];
+    int sec[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) bk[c] = kNone, sec[c] = 256;
+    for (int p = o0 + lane; p < o1; p += 64) {
+        const int idx2 = O.node_idx[p];
+        const int blk = cand_block<MODE>(O, idx2);
+        if (blk < 0 || ((claimed[idx2 >> 5] >> (idx2 & 31)) & 1u)) continue;
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(O.desc + 32 * (size_t)idx2);
+        const uint64_t d2[4] = {q[0], q[1], q[2], q[3]};
+        const int dist = omv::hamming256(d1, d2);
+        const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)(p - o0);
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+            if (c != blk) continue;
+            if (key < bk[c]) {   // this lane's candidates arrive in node order
+                if (bk[c] != kNone) sec[c] = min(sec[c], (int)(bk[c] >> 16));
+                bk[c] = key;
+            } else {
+                sec[c] = min(sec[c], dist);
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        const uint32_t g = wave_min_u32(bk[c]);
+        const uint32_t other = bk[c] == g ? (uint32_t)sec[c] : (bk[c] == kNone ? 256u : bk[c] >> 16);
+        bs[c] = (int)wave_min_u32(other);
+        bd[c] = g == kNone ? 256 : (int)(g >> 16);
+        bi[c] = g == kNone ? -1 : O.node_idx[o0 + (int)(g & 0xffffu)];
+    }
+}
+
+// One wavefront per job: the reference's sequential walk over the records (common nodes ascending, keyframe
+// keypoints in node order), claims in an LDS bitmap, then the rotation filter.
+template <int MODE>
+__global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs, const int *rec_off,
+                                                         const uint32_t *recs, float nnratio, int check_ori,
+                                                         int32_t *n_matches, int *err) {
     __shared__ uint32_t claimed[kMaxKp / 32];
     __shared__ uint8_t bins[kMaxKp];
+    __shared__ int16_t match[kMaxKp];   // the output, written to memory once at the end (no stores in the walk)
+    __shared__ uint32_t recbuf[2][kChunk * kRecWords];
     __shared__ int cnt[kHisto];
     __shared__ int ind[3];
     constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1;
@@ -107,118 +241,126 @@ __global__ void __launch_bounds__(64) bow_kernel(const omv_bow_job *jobs, float 
         if (lane == 0) *err = OMV_ERR_CAPACITY;
         return;
     }
-    for (int i = lane; i < n_out; i += 64) J.match[i] = -1, bins[i] = 0xff;
+    for (int i = lane; i < n_out; i += 64) match[i] = -1, bins[i] = 0xff;
     for (int i = lane; i < (O.n + 31) / 32; i += 64) claimed[i] = 0;
     if (lane < kHisto) cnt[lane] = 0;
     __syncthreads();
-    int nm = 0;
-    int a = 0, b = 0;
-    while (a < K.n_nodes && b < O.n_nodes) {
-        const uint32_t na = K.node_id[a], nb = O.node_id[b];
-        if (na < nb) {   // lower_bound on the smaller side
-            ++a;
-            continue;
+    // records staged through LDS a chunk at a time (one coalesced load per chunk, the next chunk in flight while
+    // the current one is walked): the walk itself then only waits on LDS
+    const uint32_t *R = recs + (size_t)rec_off[blockIdx.x] * kRecWords;
+    const int n_words = K.n * kRecWords;
+    constexpr int kPer = kChunk * kRecWords / 64;
+    uint32_t nxt[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) nxt[k] = 64 * k + lane < n_words ? R[64 * k + lane] : 0u;
+    int nm = 0, buf = 0;
+    for (int base = 0; base < K.n; base += kChunk) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) recbuf[buf][64 * k + lane] = nxt[k];
+        const int nb = base + kChunk;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int w = nb * kRecWords + 64 * k + lane;
+            nxt[k] = w < n_words ? R[w] : 0u;
         }
-        if (nb < na) {
-            ++b;
-            continue;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int q = base; q < min(nb, K.n); ++q) {
+        const uint32_t *cr = recbuf[buf] + (q - base) * kRecWords;
+        const int o0 = (int)cr[0];
+        if (o0 < 0) continue;
+        const int o1 = (int)cr[1], idx1 = (int)cr[2];
+        const uint32_t c01 = cr[3], c23 = cr[4];
+        // lane c < NB: the block's first two unclaimed entries
+        const int c = lane < NB ? lane : 0;
+        uint32_t e[kTop];
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) e[k] = cr[8 + kTop * c + k];
+        const int total = (int)(((c < 2 ? c01 : c23) >> (16 * (c & 1))) & 0xffffu);
+        // all claim words first (independent LDS reads, one latency), then a branch-free pick
+        uint32_t cw[kTop];
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) cw[k] = claimed[(e[k] == kNone ? 0u : e[k] & 0xffffu) >> 5];
+        uint32_t best = kNone;
+        int d2 = 256, found = 0;
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) {
+            const uint32_t x = e[k];
+            const bool ok = x != kNone && !((cw[k] >> (x & 31u)) & 1u);
+            best = ok && found == 0 ? x : best;
+            d2 = ok && found == 1 ? (int)(x >> 23) : d2;
+            found += ok && found < 2 ? 1 : 0;
         }
-        const int o0 = O.node_start[b], o1 = O.node_start[b + 1];
-        for (int i1 = K.node_start[a]; i1 < K.node_start[a + 1]; ++i1) {
-            const int idx1 = K.node_idx[i1];
-            if (MODE == OMV_BOW_KF_KF && K.n_left != -1 && idx1 >= K.n) continue;
-            if (!K.has_mp[idx1]) continue;
-            uint64_t d1[4];
-            {
-                const uint64_t *q = reinterpret_cast<const uint64_t *>(K.desc + 32 * (size_t)idx1);
-                d1[0] = q[0], d1[1] = q[1], d1[2] = q[2], d1[3] = q[3];
+        const bool rescan = lane < NB && found < 2 && total > kTop;
+        int bd[NB], bi[NB], bs[NB], bb[NB];
+        if (__ballot(rescan)) {
+            const uint64_t *dq = reinterpret_cast<const uint64_t *>(K.desc + 32 * (size_t)idx1);
+            const uint64_t d1[4] = {dq[0], dq[1], dq[2], dq[3]};
+            scan_node<MODE, NB>(O, claimed, d1, o0, o1, lane, bd, bi, bs);
+#pragma unroll
+            for (int cc = 0; cc < NB; ++cc)
+                bb[cc] = check_ori && bd[cc] <= TH_LOW ? rot_bin(K.kps[idx1].angle, O.kps[bi[cc]].angle) : 0;
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < NB; ++cc) {   // lane cc's pick, read into scalar registers
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)best, cc);
+                bd[cc] = b == kNone ? 256 : (int)(b >> 23);
+                bi[cc] = b == kNone ? -1 : (int)(b & 0xffffu);
+                bb[cc] = (int)((b >> 16) & 31u);
+                bs[cc] = __builtin_amdgcn_readlane(d2, cc);
             }
-            uint32_t bk[NB];
-            int sec[NB];
+        }
+        if (MODE == OMV_BOW_KF_FRAME) {
+            if (bd[0] <= TH_LOW) {
 #pragma unroll
-            for (int c = 0; c < NB; ++c) bk[c] = kNone, sec[c] = 256;
-            for (int p = o0 + lane; p < o1; p += 64) {
-                const int idx2 = O.node_idx[p];
-                int blk = 0;
-                bool ok = !((claimed[idx2 >> 5] >> (idx2 & 31)) & 1u);
-                if (MODE == OMV_BOW_KF_FRAME) {
-                    blk = frame_block(O, idx2);
-                    ok = ok && blk >= 0;
-                } else {
-                    ok = ok && !(O.n_left != -1 && idx2 >= O.n) && O.has_mp[idx2];
-                }
-                if (!ok) continue;
-                const uint64_t *q = reinterpret_cast<const uint64_t *>(O.desc + 32 * (size_t)idx2);
-                const uint64_t d2[4] = {q[0], q[1], q[2], q[3]};
-                const int dist = omv::hamming256(d1, d2);
-                const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)(p - o0);
-#pragma unroll
-                for (int c = 0; c < NB; ++c) {
-                    if (c != blk) continue;
-                    if (key < bk[c]) {   // this lane's candidates arrive in node order
-                        if (bk[c] != kNone) sec[c] = min(sec[c], (int)(bk[c] >> 16));
-                        bk[c] = key;
-                    } else {
-                        sec[c] = min(sec[c], dist);
-                    }
-                }
-            }
-            int bd[NB], bi[NB], bs[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                const uint32_t g = wave_min_u32(bk[c]);
-                const uint32_t other = bk[c] == g ? (uint32_t)sec[c] : (bk[c] == kNone ? 256u : bk[c] >> 16);
-                bs[c] = (int)wave_min_u32(other);
-                bd[c] = g == kNone ? 256 : (int)(g >> 16);
-                bi[c] = g == kNone ? -1 : O.node_idx[o0 + (int)(g & 0xffffu)];
-            }
-            if (MODE == OMV_BOW_KF_FRAME) {
-                if (bd[0] <= TH_LOW) {
-#pragma unroll
-                    for (int c = 0; c < NB; ++c) {
-                        if (bd[c] > TH_LOW) continue;
-                        // left: the nnratio test; right / side: `... || true` (ORBmatcher.cc:520-521, ...)
-                        if (c == 0 && !((float)bd[0] < nnratio * (float)bs[0])) continue;
-                        const int idxF = bi[c];
-                        if (lane == 0) {
-                            J.match[idxF] = idx1;
-                            claimed[idxF >> 5] |= 1u << (idxF & 31);
-                            if (check_ori) {
-                                const int bin = rot_bin(K.kps[idx1].angle, O.kps[idxF].angle);
-                                bins[idxF] = (uint8_t)bin;
-                                ++cnt[bin];
-                            }
+                for (int cc = 0; cc < NB; ++cc) {
+                    if (bd[cc] > TH_LOW) continue;
+                    // left: the nnratio test; right / side: `... || true` (ORBmatcher.cc:520-521, ...)
+                    if (cc == 0 && !((float)bd[0] < nnratio * (float)bs[0])) continue;
+                    const int idxF = bi[cc];
+                    if (lane == 0) {
+                        match[idxF] = (int16_t)idx1;
+                        claimed[idxF >> 5] |= 1u << (idxF & 31);
+                        if (check_ori) {
+                            bins[idxF] = (uint8_t)bb[cc];
+                            ++cnt[bb[cc]];
                         }
-                        ++nm;
                     }
+                    ++nm;
                 }
-            } else if (bd[0] < TH_LOW && (float)bd[0] < nnratio * (float)bs[0]) {
-                const int idx2 = bi[0];
-                if (lane == 0) {
-                    J.match[idx1] = idx2;
-                    claimed[idx2 >> 5] |= 1u << (idx2 & 31);   // vbMatched2
-                    if (check_ori) {
-                        const int bin = rot_bin(K.kps[idx1].angle, O.kps[idx2].angle);
-                        bins[idx1] = (uint8_t)bin;
-                        ++cnt[bin];
-                    }
-                }
-                ++nm;
             }
-            __syncthreads();   // the claims before the next keyframe keypoint's scan
+        } else if (bd[0] < TH_LOW && (float)bd[0] < nnratio * (float)bs[0]) {
+            const int idx2 = bi[0];
+            if (lane == 0) {
+                match[idx1] = (int16_t)idx2;
+                claimed[idx2 >> 5] |= 1u << (idx2 & 31);   // vbMatched2
+                if (check_ori) {
+                    bins[idx1] = (uint8_t)bb[0];
+                    ++cnt[bb[0]];
+                }
+            }
+            ++nm;
         }
-        ++a, ++b;
+        // the claims before the next keyframe keypoint's pick: one wavefront, LDS only -- a wave-scope fence
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+        buf ^= 1;
     }
     if (check_ori) {
         if (lane == 0) three_maxima(cnt, ind);
         __syncthreads();
-        int removed = 0;
-        for (int i = lane; i < n_out; i += 64) {
-            const int bn = bins[i];
-            if (bn != 0xff && bn != ind[0] && bn != ind[1] && bn != ind[2]) J.match[i] = -1, ++removed;
-        }
-        nm -= wave_sum_i32(removed);
     }
+    int removed = 0;
+    for (int i = lane; i < n_out; i += 64) {
+        const int bn = bins[i];
+        const bool drop = check_ori && bn != 0xff && bn != ind[0] && bn != ind[1] && bn != ind[2];
+        removed += drop ? 1 : 0;
+        J.match[i] = drop ? -1 : (int32_t)match[i];
+    }
+    nm -= wave_sum_i32(removed);
     if (lane == 0) n_matches[blockIdx.x] = nm;
 }
 
@@ -239,19 +381,34 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
         if (j.kf.n > kMaxKp || j.other.n > kMaxKp) return OMV_ERR_CAPACITY;
     }
     hipStream_t st = (hipStream_t)stream;
-    omv_bow_job *d_jobs = nullptr;
-    HIP_OK(hipMallocAsync((void **)&d_jobs, sizeof(omv_bow_job) * n_jobs + sizeof(int), st));
-    int *d_err = (int *)(d_jobs + n_jobs);
+    std::vector<int> off(n_jobs + 1, 0);
+    int max_n = 1;
+    for (int i = 0; i < n_jobs; ++i) off[i + 1] = off[i] + jobs[i].kf.n, max_n = std::max(max_n, jobs[i].kf.n);
+    const size_t job_bytes = (sizeof(omv_bow_job) * n_jobs + 15) & ~(size_t)15;
+    const size_t off_bytes = (sizeof(int) * (n_jobs + 1) + 15) & ~(size_t)15;
+    char *d_buf = nullptr;
+    HIP_OK(hipMallocAsync((void **)&d_buf, job_bytes + off_bytes + 16 + (size_t)off[n_jobs] * kRecWords * 4, st));
+    omv_bow_job *d_jobs = (omv_bow_job *)d_buf;
+    int *d_off = (int *)(d_buf + job_bytes);
+    int *d_err = (int *)(d_buf + job_bytes + off_bytes);
+    uint32_t *d_recs = (uint32_t *)(d_buf + job_bytes + off_bytes + 16);
     HIP_OK(hipMemcpyAsync(d_jobs, jobs, sizeof(omv_bow_job) * n_jobs, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_off, off.data(), sizeof(int) * (n_jobs + 1), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
-    if (mode == OMV_BOW_KF_FRAME)
-        bow_kernel<OMV_BOW_KF_FRAME><<<n_jobs, 64, 0, st>>>(d_jobs, nnratio, check_ori, n_matches, d_err);
-    else
-        bow_kernel<OMV_BOW_KF_KF><<<n_jobs, 64, 0, st>>>(d_jobs, nnratio, check_ori, n_matches, d_err);
+    const dim3 cg((max_n + 255) / 256, n_jobs);
+    if (mode == OMV_BOW_KF_FRAME) {
+        bow_cand_kernel<OMV_BOW_KF_FRAME><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
+        bow_resolve_kernel<OMV_BOW_KF_FRAME><<<n_jobs, 64, 0, st>>>(d_jobs, d_off, d_recs, nnratio, check_ori,
+                                                                   n_matches, d_err);
+    } else {
+        bow_cand_kernel<OMV_BOW_KF_KF><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
+        bow_resolve_kernel<OMV_BOW_KF_KF><<<n_jobs, 64, 0, st>>>(d_jobs, d_off, d_recs, nnratio, check_ori, n_matches,
+                                                                d_err);
+    }
     HIP_OK(hipGetLastError());
     int h_err = 0;
     HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipFreeAsync(d_jobs, st));
+    HIP_OK(hipFreeAsync(d_buf, st));
     HIP_OK(hipStreamSynchronize(st));
     return h_err ? (omv_status)h_err : OMV_OK;
 }

@@ -1643,10 +1643,18 @@ __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
     __syncthreads();
     const float r = (float)a.window;
     int nm = 0;
+    // the next F1 keypoint's fields are loaded one iteration ahead (the walk is a chain of dependent steps)
+    omv_kp kn{};
+    float xn = 0.f, yn = 0.f;
+    uint64_t dn[4] = {0, 0, 0, 0};
+    if (n1 > 0) kn = kp1[0], xn = prev[0], yn = prev[1], load_desc(ds1, dn);
     for (int i1 = 0; i1 < n1; ++i1) {
-        const omv_kp k1 = kp1[i1];
+        const omv_kp k1 = kn;
+        const float x = xn, y = yn;
+        const uint64_t d1[4] = {dn[0], dn[1], dn[2], dn[3]};
+        if (i1 + 1 < n1)
+            kn = kp1[i1 + 1], xn = prev[2 * i1 + 2], yn = prev[2 * i1 + 3], load_desc(ds1 + (size_t)(i1 + 1) * 32, dn);
         if (k1.octave > 0) continue;
-        const float x = prev[2 * i1], y = prev[2 * i1 + 1];
         // Frame::GetFeaturesInArea(x, y, windowSize, 0, 0) window (Frame.cc:890-967)
         const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
         if (nMinCellX >= kGridCols) continue;
@@ -1656,30 +1664,46 @@ __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
         if (nMinCellY >= kGridRows) continue;
         const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
         if (nMaxCellY < 0) continue;
-        uint64_t d1[4];
-        load_desc(ds1 + (size_t)i1 * 32, d1);
         uint32_t bk = 0xffffffffu;
-        int sec = INT_MAX, bidx = -1, ord = 0;
-        for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
-            const int p0 = cs[ix * kGridRows + nMinCellY], p1 = cs[ix * kGridRows + nMaxCellY + 1];
-            for (int p = p0 + lane; p < p1; p += 64) {
-                const int i2 = ci[p];
-                const omv_kp k = kp2[i2];
-                if (k.octave != 0) continue;   // levels [0, 0]
-                if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
-                uint64_t d2[4];
-                load_desc(ds2 + (size_t)i2 * 32, d2);
-                const int dist = omv::hamming256(d1, d2);
-                if (mdist[i2] <= dist) continue;
-                const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)(ord + p - p0);
-                if (key < bk) {   // this lane's candidates arrive in window order
-                    if (bk != 0xffffffffu) sec = min(sec, (int)(bk >> 16));
-                    bk = key, bidx = i2;
-                } else {
-                    sec = min(sec, dist);
-                }
+        int sec = INT_MAX, bidx = -1;
+        // the window's columns are contiguous CSR runs; lane j < ncol holds column j's run, an inclusive scan
+        // flattens them in GetFeaturesInArea order, and the lanes walk the flattened list 64 at a time (one
+        // gather chain per 64 candidates instead of one per column)
+        const int ncol = nMaxCellX - nMinCellX + 1;
+        int cp0 = 0, clen = 0;
+        if (lane < ncol) {
+            const int ix = nMinCellX + lane;
+            cp0 = cs[ix * kGridRows + nMinCellY];
+            clen = cs[ix * kGridRows + nMaxCellY + 1] - cp0;
+        }
+        int incl = clen;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        const int excl = incl - clen, total = __shfl(incl, 63, 64);
+        for (int base = 0; base < total; base += 64) {
+            const int pos = base + lane;   // the shuffles run on the whole wavefront (uniform loop)
+            int j = 0;
+            for (int t = 1; t < ncol; ++t) j = __shfl(excl, t, 64) <= pos ? t : j;
+            const int p = __shfl(cp0, j, 64) + pos - __shfl(excl, j, 64);
+            if (pos >= total) continue;
+            const int i2 = ci[p];
+            const omv_kp k = kp2[i2];
+            if (k.octave != 0) continue;   // levels [0, 0]
+            if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+            uint64_t d2[4];
+            load_desc(ds2 + (size_t)i2 * 32, d2);
+            const int dist = omv::hamming256(d1, d2);
+            if (mdist[i2] <= dist) continue;
+            const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)pos;
+            if (key < bk) {   // this lane's candidates arrive in window order
+                if (bk != 0xffffffffu) sec = min(sec, (int)(bk >> 16));
+                bk = key, bidx = i2;
+            } else {
+                sec = min(sec, dist);
             }
-            ord += p1 - p0;
         }
         const uint32_t g = wave_min_u32(bk);
         if (g == 0xffffffffu) continue;   // no candidate (vIndices2 empty, or all skipped)
@@ -1704,7 +1728,7 @@ __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
                 }
             }
         }
-        __syncthreads();
+        wave_sync();   // the claim state before the next F1 keypoint (one wavefront, LDS only)
     }
     if (a.check_ori) {   // ComputeThreeMaxima, then every push outside the top bins that is still matched
         if (lane == 0) {
