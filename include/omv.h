@@ -381,6 +381,10 @@ typedef struct omv_lba_problem {
     const double *stereo_obs;  /* [n_stereo][3] (kpUn.pt.x, kpUn.pt.y, mvuRight); mvuRight >= 0 */
     const float *stereo_inv_sigma2;   /* [n_stereo] */
     float bf;                  /* KeyFrame::mbf (ImuCamPose::bf) */
+    /* GeometricCamera type per camera: OMV_CAM_KB8 (cam = KannalaBrandt8 fx fy cx cy k1..k4) or
+     * OMV_CAM_PINHOLE (cam = Pinhole fx fy cx cy, the rest ignored: Pinhole::project / projectJac,
+     * src/CameraModels/Pinhole.cpp:18-24, :55-65).  NULL: every camera KannalaBrandt8. */
+    const int32_t *cam_model;  /* [n_cams] */
 } omv_lba_problem;
 
 typedef struct omv_lba_opts {
@@ -576,6 +580,7 @@ typedef struct omv_pose_batch {
     const float *stereo_inv_sigma2, *stereo_xw;
     int kp_cap;                         /* per-frame stride of kp_outlier */
     int n_mono, n_stereo;               /* edge totals of the batch (mono_start[F], stereo_start[F]) */
+    const int32_t *cam_model;           /* host [n_cams] OMV_CAM_KB8 / OMV_CAM_PINHOLE (as omv_lba_problem); NULL: KB8 */
 } omv_pose_batch;
 
 typedef struct omv_pose omv_pose;

@@ -126,7 +126,7 @@ class LbaProblem(ctypes.Structure):
                 ("imu_kf2", ctypes.c_void_p), ("preint", ctypes.c_void_p), ("imu_robust", ctypes.c_void_p),
                 ("imu_info_scale", ctypes.c_void_p), ("n_stereo", ctypes.c_int), ("stereo_pt", ctypes.c_void_p),
                 ("stereo_kf", ctypes.c_void_p), ("stereo_obs", ctypes.c_void_p),
-                ("stereo_inv_sigma2", ctypes.c_void_p), ("bf", ctypes.c_float)]
+                ("stereo_inv_sigma2", ctypes.c_void_p), ("bf", ctypes.c_float), ("cam_model", ctypes.c_void_p)]
 
 
 class PoseBatch(ctypes.Structure):
@@ -137,7 +137,8 @@ class PoseBatch(ctypes.Structure):
                     "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba",
                     "preint", "mono_start", "mono_cam", "mono_kp", "mono_obs", "mono_inv_sigma2", "mono_xw",
                     "mono_close", "stereo_start", "stereo_cam", "stereo_kp", "stereo_obs", "stereo_inv_sigma2",
-                    "stereo_xw")] + [("kp_cap", ctypes.c_int), ("n_mono", ctypes.c_int), ("n_stereo", ctypes.c_int)]
+                    "stereo_xw")] + [("kp_cap", ctypes.c_int), ("n_mono", ctypes.c_int), ("n_stereo", ctypes.c_int),
+                                   ("cam_model", ctypes.c_void_p)]
 
 
 class PosePrior(ctypes.Structure):

@@ -92,6 +92,7 @@ struct Rig {
     float cam[kMaxCams][8];
     double Rcb[kMaxCams][9], tcb[kMaxCams][3], Rbc[kMaxCams][9], tbc[kMaxCams][3];
     double bf;   // ImuCamPose::bf = KeyFrame::mbf (EdgeStereo)
+    int model[kMaxCams];   // OMV_CAM_KB8 / OMV_CAM_PINHOLE (GeometricCamera::mnType)
 };
 
 // KannalaBrandt8::project(const Eigen::Vector3d&) (KannalaBrandt8.cpp:28-46)
@@ -123,6 +124,30 @@ __device__ __forceinline__ void kb8_jac(const float *k, const double *X, double 
     J[4] = (double)k[1] * (fd * X[2] * y2 / q + f * x2 / r3);
     J[2] = -(double)k[0] * fd * X[0] / (r2 + z2);
     J[5] = -(double)k[1] * fd * X[1] / (r2 + z2);
+}
+
+// Pinhole::project(const Eigen::Vector3d&) (Pinhole.cpp:18-24): float parameters, double arithmetic
+__device__ __forceinline__ void pinhole_project(const float *k, const double *X, double &u, double &v) {
+    u = (double)k[0] * X[0] / X[2] + (double)k[2];
+    v = (double)k[1] * X[1] / X[2] + (double)k[3];
+}
+// Pinhole::projectJac (Pinhole.cpp:55-65), 2x3 row-major
+__device__ __forceinline__ void pinhole_jac(const float *k, const double *X, double *J) {
+    J[0] = (double)k[0] / X[2];
+    J[1] = 0.0;
+    J[2] = (double)(-k[0]) * X[0] / (X[2] * X[2]);
+    J[3] = 0.0;
+    J[4] = (double)k[1] / X[2];
+    J[5] = (double)(-k[1]) * X[1] / (X[2] * X[2]);
+}
+// pCamera[c]->project / projectJac by the camera's type
+__device__ __forceinline__ void cam_project(const Rig &rig, int c, const double *X, double &u, double &v) {
+    if (rig.model[c] == OMV_CAM_PINHOLE) pinhole_project(rig.cam[c], X, u, v);
+    else kb8_project(rig.cam[c], X, u, v);
+}
+__device__ __forceinline__ void cam_jac(const Rig &rig, int c, const double *X, double *J) {
+    if (rig.model[c] == OMV_CAM_PINHOLE) pinhole_jac(rig.cam[c], X, J);
+    else kb8_jac(rig.cam[c], X, J);
 }
 
 struct State {   // one of the two state buffers

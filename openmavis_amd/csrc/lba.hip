@@ -97,7 +97,7 @@ __device__ __forceinline__ void mono_err_block(int blk, double *sh, Rig rig, Sta
         mv3(R, X, Xc);
         Xc[0] += t[0], Xc[1] += t[1], Xc[2] += t[2];
         double u, v;
-        kb8_project(rig.cam[c], Xc, u, v);
+        cam_project(rig, c, Xc, u, v);
         const double e0 = E.obs[2 * e] - u, e1 = E.obs[2 * e + 1] - v;
         const double w = (double)E.w[e];
         double c2 = e0 * w * e0 + e1 * w * e1;
@@ -376,7 +376,7 @@ __device__ __forceinline__ int edge_jacobians(const Rig &rig, const State &s, co
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
     const bool st = E.ur[e] >= 0.f;   // EdgeStereo: proj_jac row 2 = row 0, (2,2) += bf / z^2
     double pj[9];
-    kb8_jac(rig.cam[c], Xc, pj);
+    cam_jac(rig, c, Xc, pj);
     const int nr = st ? 3 : 2;
     // all three rows are formed (zero for a mono edge) so the arrays stay in registers; the sums skip row 2
     if (st) {
@@ -1147,7 +1147,7 @@ __global__ void mono_jac_kernel(Rig rig, State s, Edges E, double *jx, double *j
     mv3(rig.Rbc[c], Xc, Xb);
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
     double pj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    kb8_jac(rig.cam[c], Xc, pj);
+    cam_jac(rig, c, Xc, pj);
     if (E.ur[e] >= 0.f) {
         const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
         pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
@@ -1420,6 +1420,8 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     rig.n_cams = C;
     for (int c = 0; c < C; ++c) {
         for (int q = 0; q < 8; ++q) rig.cam[c][q] = p->cam[8 * c + q];
+        rig.model[c] = p->cam_model ? p->cam_model[c] : OMV_CAM_KB8;
+        if (rig.model[c] != OMV_CAM_KB8 && rig.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
         for (int q = 0; q < 9; ++q) rig.Rcb[c][q] = p->Rcb[9 * c + q], rig.Rbc[c][q] = p->Rbc[9 * c + q];
         for (int q = 0; q < 3; ++q) rig.tcb[c][q] = p->tcb[3 * c + q], rig.tbc[c][q] = p->tbc[3 * c + q];
     }

@@ -152,7 +152,7 @@ __device__ __forceinline__ double edge_error(const Rig &rig, const double *Rcw, 
     mv3(R, v.X, Xc);
     for (int q = 0; q < 3; ++q) Xc[q] += t[q];
     double u, vv;
-    kb8_project(rig.cam[v.cam], Xc, u, vv);
+    cam_project(rig, v.cam, Xc, u, vv);
     r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv, r[2] = 0;
     double c = r[0] * v.w * r[0] + r[1] * v.w * r[1];
     if (v.stereo) {
@@ -170,7 +170,7 @@ __device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const d
     mv3(rig.Rbc[c], Xc, Xb);
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
     double pj[9];
-    kb8_jac(rig.cam[c], Xc, pj);
+    cam_jac(rig, c, Xc, pj);
     const int nr = v.stereo ? 3 : 2;
     if (v.stereo) {
         const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
@@ -765,6 +765,8 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     rig.n_cams = b->n_cams;
     for (int c = 0; c < b->n_cams; ++c) {
         for (int q = 0; q < 8; ++q) rig.cam[c][q] = b->cam[8 * c + q];
+        rig.model[c] = b->cam_model ? b->cam_model[c] : OMV_CAM_KB8;
+        if (rig.model[c] != OMV_CAM_KB8 && rig.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
         for (int q = 0; q < 9; ++q) rig.Rcb[c][q] = b->Rcb[9 * c + q], rig.Rbc[c][q] = b->Rbc[9 * c + q];
         for (int q = 0; q < 3; ++q) rig.tcb[c][q] = b->tcb[3 * c + q], rig.tbc[c][q] = b->tbc[3 * c + q];
     }

@@ -48,6 +48,15 @@ def kb8_project(k, X):
     return np.stack([k[0] * rr * np.cos(psi) + k[2], k[1] * rr * np.sin(psi) + k[3]], -1)
 
 
+def pinhole_project(k, X):
+    """Pinhole::project in double (vectorised; generation only)."""
+    return np.stack([k[0] * X[..., 0] / X[..., 2] + k[2], k[1] * X[..., 1] / X[..., 2] + k[3]], -1)
+
+
+def cam_project(k, X, pinhole=False):
+    return pinhole_project(k, X) if pinhole else kb8_project(k, X)
+
+
 def rig():
     """(cam params [5][8] float32, Rbc [5][3][3], tbc [5][3]) — camera -> body."""
     Tbc = [T_B_C1, T_B_C1 @ T_C1_C2, T_B_C3, T_B_C4]
@@ -152,11 +161,12 @@ def _log(R):
 
 
 def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_noise=0.05, rot_noise_deg=0.5,
-                     trans_noise=0.02, n_cams=5, stereo_frac=0.0, bf=40.0):
+                     trans_noise=0.02, n_cams=5, stereo_frac=0.0, bf=40.0, pinhole=False):
     """stereo_frac > 0: that fraction of the camera-0 observations become EdgeStereo observations
     (u, v, u_R = u - bf / z + noise), as LocalInertialBA creates them for keypoints with a right
     coordinate / depth (Optimizer.cc:3108-3143); drawn from a separate stream, so the rest of the
-    window is the same as with stereo_frac = 0."""
+    window is the same as with stereo_frac = 0.  pinhole: every camera a Pinhole (fx fy cx cy of the Hilti
+    cameras, Pinhole.cpp), problem["cam_model"] = OMV_CAM_PINHOLE per camera."""
     rng = np.random.Generator(np.random.PCG64(seed))
     cams, Rbc, tbc = rig()
     cams, Rbc, tbc = cams[:n_cams], Rbc[:n_cams], tbc[:n_cams]
@@ -204,7 +214,7 @@ def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_n
                     if X[2] < 0.3:
                         ok = False
                         break
-                    uv = kb8_project(cams[c].astype(np.float64), X)
+                    uv = cam_project(cams[c].astype(np.float64), X, pinhole)
                     if not (5 <= uv[0] <= 715 and 5 <= uv[1] <= 535):
                         ok = False
                         break
@@ -220,7 +230,7 @@ def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_n
         for k in trip:
             Rcw, tcw = cam_pose(*true[k][:2])
             for c in (c1, chosen):
-                uv = kb8_project(cams[c].astype(np.float64), Rcw[c] @ Xw + tcw[c]) + rng.normal(0, obs_noise, 2)
+                uv = cam_project(cams[c].astype(np.float64), Rcw[c] @ Xw + tcw[c], pinhole) + rng.normal(0, obs_noise, 2)
                 obs_pt.append(p)
                 obs_kf.append(slot[k])
                 obs_cam.append(c)
@@ -275,6 +285,8 @@ def make_lba_problem(n_kf=50, n_opt=25, n_pts=20000, seed=5, obs_noise=0.7, pt_n
                  stereo_inv_sigma2=inv_sig[st], bf=np.float32(bf)) if stereo_frac > 0 else {}
     keep_m = ~st
     obs_pt, obs_kf, obs_cam, obs_uv, inv_sig = obs_pt[keep_m], obs_kf[keep_m], obs_cam[keep_m], obs_uv[keep_m], inv_sig[keep_m]
+    if pinhole:
+        extra["cam_model"] = np.full(n_cams, 1, np.int32)   # OMV_CAM_PINHOLE
     return dict(**extra,
         n_cams=n_cams, cam=cams, Rcb=Rcb, tcb=tcb, Rbc=Rbc, tbc=tbc, n_kf=n_kf, n_opt=n_opt,
         kf_imu=np.ones(n_kf, np.uint8), Rwb=Rwb, twb=twb, Rcw=Rcw, tcw=tcw, vel=vel, bg=bg, ba=ba,
@@ -324,6 +336,8 @@ def as_struct(prob, struct_cls):
         s.stereo_obs = arr("stereo_obs", np.float64)
         s.stereo_inv_sigma2 = arr("stereo_inv_sigma2", np.float32)
     s.bf = float(prob.get("bf", 0.0))
+    if "cam_model" in prob:
+        s.cam_model = arr("cam_model", np.int32)
     return s, keep
 
 

@@ -15,7 +15,7 @@ from . import synth_ba
 
 
 def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac=0.0, n_cams=5, bf=40.0,
-                    rot_noise_deg=0.5, trans_noise=0.03, vel_noise=0.05):
+                    rot_noise_deg=0.5, trans_noise=0.03, vel_noise=0.05, pinhole=False):
     rng = np.random.Generator(np.random.PCG64(seed))
     cams, Rbc, tbc = synth_ba.rig()
     cams, Rbc, tbc = cams[:n_cams], Rbc[:n_cams], tbc[:n_cams]
@@ -63,7 +63,7 @@ def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac
             d[2] = abs(d[2]) * 1.5 + 0.6
             d /= np.linalg.norm(d)
             Xc = d * rng.uniform(2.0, 25.0)
-            uv = synth_ba.kb8_project(cams[c].astype(np.float64), Xc)
+            uv = synth_ba.cam_project(cams[c].astype(np.float64), Xc, pinhole)
             if not (5 <= uv[0] <= 715 and 5 <= uv[1] <= 535):
                 continue
             Xw = (Rct[c].T @ (Xc - tct[c])).astype(np.float32)   # MapPoint::GetWorldPos is float
@@ -94,6 +94,8 @@ def make_pose_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac
              stereo_start=np.array(s_start, np.int32), stereo_cam=np.array(st["cam"], np.int32),
              stereo_kp=np.array(st["kp"], np.int32), stereo_obs=np.array(st["obs"], np.float64).reshape(-1, 3),
              stereo_inv_sigma2=np.array(st["w"], np.float32), stereo_xw=np.array(st["xw"], np.float32).reshape(-1, 3))
+    if pinhole:
+        b["cam_model"] = np.full(n_cams, 1, np.int32)   # OMV_CAM_PINHOLE
     return b
 
 
@@ -101,7 +103,7 @@ PRIOR_KEYS = ("prior_Rwb", "prior_twb", "prior_vel", "prior_bg", "prior_ba", "pr
 
 
 def make_last_frame_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stereo_frac=0.0, n_cams=5, bf=40.0,
-                          frame_dt=0.05, prior_rot_deg=0.1, prior_trans=0.01, prior_vel=0.02):
+                          frame_dt=0.05, prior_rot_deg=0.1, prior_trans=0.01, prior_vel=0.02, pinhole=False):
     """Batches for Optimizer::PoseInertialOptimizationLastFrame (Optimizer.cc:5580-6170): make_pose_batch's
     frames and edges, each with a previous frame `frame_dt` earlier.  The previous frame carries the
     ConstraintPoseImu its own optimisation left (pFp->mpcpi: the true state perturbed by ~0.1 deg / 1 cm /
@@ -110,7 +112,7 @@ def make_last_frame_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, stere
     preintegration (mpImuPreintegratedFrame); the keyframe-to-frame one moves to `preint_kf`
     (mpImuPreintegrated, whose covariance gives EdgeGyroRW / EdgeAccRW their information)."""
     b = make_pose_batch(n_frames=n_frames, n_pts=n_pts, seed=seed, outlier_frac=outlier_frac,
-                        stereo_frac=stereo_frac, n_cams=n_cams, bf=bf)
+                        stereo_frac=stereo_frac, n_cams=n_cams, bf=bf, pinhole=pinhole)
     rng = np.random.Generator(np.random.PCG64(seed + 7919))
     F = int(b["n_frames"])
     b["preint_kf"] = b["preint"]
@@ -174,6 +176,8 @@ def as_pose_struct(batch, struct_cls, arrays):
         setattr(s, k, anyptr(arrays[k]))
     s.kp_cap = int(batch["kp_cap"])
     s.n_mono, s.n_stereo = int(len(batch["mono_cam"])), int(len(batch["stereo_cam"]))
+    if "cam_model" in batch:
+        s.cam_model = hptr(batch["cam_model"], np.int32)
     return s, keep
 
 

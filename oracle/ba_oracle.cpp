@@ -265,6 +265,29 @@ void kb8_jac(const float *k, const V3 &X, double J[6]) {   // 2x3 row-major
     J[5] = -k[1] * fd * X[1] / (r2 + z2);
 }
 
+// ---- Pinhole (src/CameraModels/Pinhole.cpp:18-24, :55-65) ------------------------------------------------
+void pinhole_project(const float *k, const V3 &X, double &u, double &v) {
+    u = k[0] * X[0] / X[2] + k[2];
+    v = k[1] * X[1] / X[2] + k[3];
+}
+void pinhole_jac(const float *k, const V3 &X, double J[6]) {
+    J[0] = k[0] / X[2];
+    J[1] = 0.f;
+    J[2] = -k[0] * X[0] / (X[2] * X[2]);
+    J[3] = 0.f;
+    J[4] = k[1] / X[2];
+    J[5] = -k[1] * X[1] / (X[2] * X[2]);
+}
+// pCamera[c]->project / projectJac by GeometricCamera type (model NULL: KannalaBrandt8)
+void cam_project(const int32_t *model, int c, const float *k, const V3 &X, double &u, double &v) {
+    if (model && model[c] == OMV_CAM_PINHOLE) pinhole_project(k, X, u, v);
+    else kb8_project(k, X, u, v);
+}
+void cam_jac(const int32_t *model, int c, const float *k, const V3 &X, double J[6]) {
+    if (model && model[c] == OMV_CAM_PINHOLE) pinhole_jac(k, X, J);
+    else kb8_jac(k, X, J);
+}
+
 // ---- dense helpers ---------------------------------------------------------------------------------
 bool invert_gj(std::vector<double> &A, int n) {   // in place, partial pivoting
     std::vector<double> I(n * n, 0.0);
@@ -514,7 +537,7 @@ struct Solver {
         const int k = P.mono_kf[e], c = P.mono_cam[e];
         const V3 Xc = add(mul(pose[k].Rcw[c], pts[P.mono_pt[e]]), pose[k].tcw[c]);
         double u, v;
-        kb8_project(camk(c), Xc, u, v);
+        cam_project(P.cam_model, c, camk(c), Xc, u, v);
         out[0] = P.mono_obs[2 * e] - u;
         out[1] = P.mono_obs[2 * e + 1] - v;
     }
@@ -523,7 +546,7 @@ struct Solver {
         const int k = P.stereo_kf[e];
         const V3 Xc = add(mul(pose[k].Rcw[0], pts[P.stereo_pt[e]]), pose[k].tcw[0]);
         double u, v;
-        kb8_project(camk(0), Xc, u, v);
+        cam_project(P.cam_model, 0, camk(0), Xc, u, v);
         const double invZ = 1 / Xc[2];
         const double ur = u - (double)P.bf * invZ;
         out[0] = P.stereo_obs[3 * e] - u;
@@ -609,7 +632,7 @@ struct Solver {
         const V3 Xc = add(mul(Rcw, pts[P.mono_pt[e]]), pose[k].tcw[c]);
         const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
         double pj[6];
-        kb8_jac(camk(c), Xc, pj);
+        cam_jac(P.cam_model, c, camk(c), Xc, pj);
         for (int r = 0; r < 2; ++r)
             for (int q = 0; q < 3; ++q)
                 JX[3 * r + q] = -(pj[3 * r] * Rcw(0, q) + pj[3 * r + 1] * Rcw(1, q) + pj[3 * r + 2] * Rcw(2, q));
@@ -630,7 +653,7 @@ struct Solver {
         const V3 Xc = add(mul(Rcw, pts[P.stereo_pt[e]]), pose[k].tcw[c]);
         const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
         double pj[9];
-        kb8_jac(camk(c), Xc, pj);
+        cam_jac(P.cam_model, c, camk(c), Xc, pj);
         const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
         pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + (double)P.bf * inv_z2;
         for (int r = 0; r < 3; ++r)
@@ -1146,6 +1169,7 @@ struct PoseEdge {
 struct PoseProblem {
     int C;
     const float *cam;
+    const int32_t *model = nullptr;   // omv_pose_batch::cam_model (NULL: KannalaBrandt8)
     std::vector<M3> Rcb, Rbc;
     std::vector<V3> tcb, tbc;
     double bf;
@@ -1167,7 +1191,7 @@ struct PoseProblem {
     void error(const PoseEdge &e, double r[3]) const {
         const V3 Xc = add(mul(Rcw[e.cam], e.Xw), tcw[e.cam]);
         double u, vv;
-        kb8_project(cam + 8 * e.cam, Xc, u, vv);
+        cam_project(model, e.cam, cam + 8 * e.cam, Xc, u, vv);
         r[0] = e.obs[0] - u;
         r[1] = e.obs[1] - vv;
         r[2] = 0;
@@ -1196,7 +1220,7 @@ struct PoseProblem {
         const V3 Xc = add(mul(Rcw[c], e.Xw), tcw[c]);
         const V3 Xb = add(mul(Rbc[c], Xc), tbc[c]);
         double pj[9];
-        kb8_jac(cam + 8 * c, Xc, pj);
+        cam_jac(model, c, cam + 8 * c, Xc, pj);
         const int nr = e.stereo ? 3 : 2;
         if (e.stereo) {
             const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
@@ -1608,7 +1632,7 @@ struct PoseLFProblem : PoseProblem {
 // in creation order: EdgeMonoOnlyPose, then EdgeStereoOnlyPose).  InfoG / InfoA from `C_rw`.
 void load_pose_frame(const omv_pose_batch *b, int f, const float *C_rw, PoseProblem &P) {
     const int C = b->n_cams;
-    P.C = C, P.cam = b->cam, P.bf = (double)b->bf;
+    P.C = C, P.cam = b->cam, P.model = b->cam_model, P.bf = (double)b->bf;
     for (int c = 0; c < C; ++c) {
         M3 a, r;
         std::memcpy(a.m, b->Rcb + 9 * c, 72);

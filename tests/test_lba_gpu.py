@@ -119,6 +119,21 @@ def test_optimize_small(small, oracle, large):
 
 
 @pytest.fixture(scope="module")
+def small_pinhole():
+    return synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=12, pinhole=True)
+
+
+def test_pinhole_residuals_and_jacobians(small_pinhole, oracle):
+    """A Pinhole rig (configs[3]'s camera model): Pinhole::project / projectJac in EdgeMono."""
+    test_residuals_and_jacobians(small_pinhole, oracle)
+
+
+@pytest.mark.parametrize("large", [True, False])
+def test_optimize_small_pinhole(small_pinhole, oracle, large):
+    test_optimize_small(small_pinhole, oracle, large)
+
+
+@pytest.fixture(scope="module")
 def small_st():
     return synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11, stereo_frac=0.5)
 

@@ -48,9 +48,13 @@ def _compare(b, g, o):
     assert np.abs(H_g - H_o).max() <= 1e-6 * np.abs(H_o).max()
 
 
-@pytest.mark.parametrize("seed,outliers,stereo", [(1, 0.1, 0.0), (2, 0.25, 0.0), (4, 0.1, 0.5)])
-def test_pose_inertial_last_kf_matches_oracle(oracle, seed, outliers, stereo):
-    b = synth_pose.make_pose_batch(n_frames=12, n_pts=300, seed=seed, outlier_frac=outliers, stereo_frac=stereo)
+@pytest.mark.parametrize("seed,outliers,stereo,pinhole",
+                         [(1, 0.1, 0.0, False), (2, 0.25, 0.0, False), (4, 0.1, 0.5, False), (5, 0.1, 0.0, True),
+                          (6, 0.1, 0.5, True)])
+def test_pose_inertial_last_kf_matches_oracle(oracle, seed, outliers, stereo, pinhole):
+    """pinhole: a Pinhole rig (configs[3]'s camera model, Pinhole::project / projectJac in the edges)."""
+    b = synth_pose.make_pose_batch(n_frames=12, n_pts=300, seed=seed, outlier_frac=outliers, stereo_frac=stereo,
+                                   pinhole=pinhole)
     _compare(b, _run_gpu(b), oracle.pose_last_kf(b))
 
 

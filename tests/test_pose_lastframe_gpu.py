@@ -49,10 +49,11 @@ def _compare(b, g, o):
         assert np.abs(H_g[f] - H_o[f]).max() <= 1e-6 * np.abs(H_o[f]).max(), f
 
 
-@pytest.mark.parametrize("seed,outliers,stereo", [(1, 0.1, 0.0), (2, 0.25, 0.0), (4, 0.1, 0.5)])
-def test_pose_inertial_last_frame_matches_oracle(oracle, seed, outliers, stereo):
+@pytest.mark.parametrize("seed,outliers,stereo,pinhole",
+                         [(1, 0.1, 0.0, False), (2, 0.25, 0.0, False), (4, 0.1, 0.5, False), (5, 0.1, 0.0, True)])
+def test_pose_inertial_last_frame_matches_oracle(oracle, seed, outliers, stereo, pinhole):
     b = synth_pose.make_last_frame_batch(n_frames=12, n_pts=300, seed=seed, outlier_frac=outliers,
-                                         stereo_frac=stereo)
+                                         stereo_frac=stereo, pinhole=pinhole)
     _compare(b, _run_gpu(b), oracle.pose_last_frame(b))
 
 
