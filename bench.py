@@ -573,6 +573,35 @@ def aux_legs(dev, cpu):
         out["search_for_initialization"]["cpu_baseline"] = {
             "value": round(done / t, 1), "unit": "frame pairs/s", "cores": 1, "kind": "port",
             "sample": f"{done} pair searches, oracle, 1 thread, {t:.2f} s"}
+    # ---- SearchBySim3: 32 keyframe pairs (5 blocks, ~900 projected map points per side), th 7.5
+    from openmavis_amd import synth_sim3
+    sb = synth_sim3.make_sim3_batch(n_pairs=32, seed=5)
+    K, Cc, cap = sb["n_kf"], sb["n_cams"], sb["kp_cap"]
+    skf = FrameBatch(torch, K, Cc, cap, sb["width"], sb["height"], scale, device=dev)
+    skf.kps.copy_(torch.from_numpy(np.ascontiguousarray(sb["kps"]).view(np.int32).reshape(K, Cc, cap, 6)))
+    skf.desc.copy_(torch.from_numpy(sb["desc"]))
+    skf.n_kp.copy_(torch.from_numpy(sb["n_kp"]))
+    smps = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in sb["mps"].items()}
+    sl = [torch.from_numpy(np.ascontiguousarray(sb[k], np.int32)).to(dev) for k in ("kp1", "mp1", "kp2", "mp2")]
+    from openmavis_amd.matcher import sim3_job_array
+    sjobs = sim3_job_array(sb["jobs"])
+    ms = ORBmatcher(0.75, True)
+    ns = len(sb["jobs"])
+
+    def run_sim3():
+        return ms.SearchBySim3(skf, sjobs, *sl, smps, th=7.5)
+    dt = _timed(run_sim3, 10, dev)
+    _, nf = run_sim3()
+    out["search_by_sim3"] = {"metric": "ORBmatcher::SearchBySim3 keyframe pairs/s (grid build included)",
+                             "value": round(ns / dt, 1), "unit": "keyframe pairs/s", "ms_per_batch": round(dt * 1e3, 3),
+                             "pairs_per_batch": ns, "points_per_pair": round((len(sb["kp1"]) + len(sb["kp2"])) / ns, 1),
+                             "matches_per_pair": round(float(nf.float().mean().item()), 1)}
+    if cpu:
+        small = synth_sim3.make_sim3_batch(n_pairs=4, seed=5)
+        done, t = _cpu_rate(lambda: oracle.search_by_sim3(small), 4)
+        out["search_by_sim3"]["cpu_baseline"] = {
+            "value": round(done / t, 1), "unit": "keyframe pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} pair searches (grid build included), oracle, 1 thread, {t:.2f} s"}
     return out
 
 

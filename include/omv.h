@@ -287,6 +287,39 @@ omv_status omv_matcher_search_kf(omv_matcher *m, int n_kf, const omv_frame_geom 
                                  const omv_kf_search_params *p, int32_t *kp_match, int32_t *best_idx,
                                  int32_t *best_dist, int32_t *n_matches, void *stream);
 
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (src/ORBmatcher.cc:1771-1983) for a list of
+ * keyframe pairs of the last omv_matcher_assign_grid batch.  Side 1 of a job = the pKF1 keypoints i1 whose
+ * map point the reference projects (GetMapPointMatches()[i1] set, !vbAlreadyMatched1[i1], !isBad()), as
+ * (kp1 = i1, the N-index, mp1 = its map-point table row); side 2 likewise for pKF2.  Each side-1 point goes
+ * through T1w then S21 into pKF2, each side-2 point through T2w then S12 into pKF1; both use the pinhole
+ * formula with pKF1's fx fy cx cy (as the reference), IsInImage, the distance invariance on |p3Dc|,
+ * PredictScale, KeyFrame::GetFeaturesInArea (camera block 0) at levels [pred-1, pred], the strict-< best,
+ * kept at <= TH_HIGH; then the agreement check vnMatch2[vnMatch1[i1]] == i1.  A side's kp entries must be
+ * distinct within a job. */
+typedef struct omv_sim3f {         /* Sophus::Sim3f: RxSO3 quaternion (x, y, z, w; |q|^2 = scale), translation */
+    float q[4];
+    float t[3];
+    float scale;                   /* S.scale() as the caller's Sophus computes it (q.squaredNorm())          */
+} omv_sim3f;
+
+typedef struct omv_sim3_job {
+    int kf1, kf2;                  /* keyframes of the assign_grid batch                                       */
+    omv_se3f T1w, T2w;             /* pKF1->GetPose(), pKF2->GetPose()                                         */
+    omv_sim3f S12, S21;            /* S12 and S12.inverse()                                                    */
+    float fx, fy, cx, cy;          /* pKF1->fx, fy, cx, cy                                                     */
+    int start1, count1;            /* the job's run of the side-1 list (runs tile the list in order)          */
+    int start2, count2;            /* the job's run of the side-2 list                                         */
+} omv_sim3_job;
+
+/* jobs: host [n_jobs]; kp1 / mp1: device [n1]; kp2 / mp2: device [n2]; mps: pos, min_dist, max_dist, desc
+ * (normal unused); th: the radius factor; match12: device [n1] the pKF2 keypoint (N-index) matched to each
+ * side-1 entry (vpMatches12[i1] = vpMapPoints2[match12]) or -1; n_found: device [n_jobs] the return value. */
+omv_status omv_matcher_search_by_sim3(omv_matcher *m, int n_kf, const omv_frame_geom *geom, const omv_kp *kps,
+                                      const uint8_t *desc, const int *n_kp, int n_jobs, const omv_sim3_job *jobs,
+                                      int n1, const int32_t *kp1, const int32_t *mp1, int n2, const int32_t *kp2,
+                                      const int32_t *mp2, const omv_kf_mps *mps, float th, float log_scale_factor,
+                                      int n_levels, int32_t *match12, int32_t *n_found, void *stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Frame::isInFrustum (src/Frame.cc:736-826; the multi-camera isInFrustumChecks, :1529-1653) with
  * MapPoint::PredictScale (src/MapPoint.cc:624-637) and KannalaBrandt8::project(Vector3f)

@@ -77,6 +77,19 @@ class KfSearchJob(ctypes.Structure):
                 ("mp_start", ctypes.c_int), ("mp_count", ctypes.c_int)]
 
 
+class Sim3f(ctypes.Structure):
+    """omv_sim3f (include/omv.h)."""
+    _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3), ("scale", ctypes.c_float)]
+
+
+class Sim3Job(ctypes.Structure):
+    """omv_sim3_job (include/omv.h)."""
+    _fields_ = [("kf1", ctypes.c_int), ("kf2", ctypes.c_int), ("T1w", SE3f), ("T2w", SE3f), ("S12", Sim3f),
+                ("S21", Sim3f), ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("start1", ctypes.c_int), ("count1", ctypes.c_int), ("start2", ctypes.c_int),
+                ("count2", ctypes.c_int)]
+
+
 class KfMps(ctypes.Structure):
     """omv_kf_mps (include/omv.h)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("pos", "normal", "min_dist", "max_dist", "desc")]
@@ -257,6 +270,8 @@ SIGNATURES = {
     "omv_matcher_search_kf": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(KfSearchJob),
                                    _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,
                                    _VP]),
+    "omv_matcher_search_by_sim3": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(Sim3Job),
+                                        _I, _VP, _VP, _I, _VP, _VP, ctypes.POINTER(KfMps), _F, _F, _I, _VP, _VP, _VP]),
     "omv_imu_preintegrate": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_bow_transform": (_I, [ctypes.POINTER(Vocab), _I, _VP, _I, _VP, _I] + [_VP] * 10 + [_VP]),
     "omv_lba_shard": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _VP]),

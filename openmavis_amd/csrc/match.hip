@@ -1598,6 +1598,99 @@ __global__ void __launch_bounds__(64) kf_resolve_kernel(KfArgs a) {
     }
 }
 
+// ---- ORBmatcher::SearchBySim3 (ORBmatcher.cc:1771-1983) ------------------------------------------------
+//   sbs3_cand_kernel   one thread per entry of either side: side 1 (:1812-1885) T1w then S21 into pKF2,
+//                      side 2 (:1888-1961) T2w then S12 into pKF1; pinhole with pKF1's intrinsics in both
+//                      directions, IsInImage, distance invariance on |p3Dc|, PredictScale, the window's best
+//                      at levels [pred-1, pred] (strict <, so the first of equal distances), kept at <= TH_HIGH.
+//                      vnMatch1 per side-1 entry; vnMatch2 scattered into a dense [job][N] table.
+//   sbs3_agree_kernel  the agreement check (:1964-1979) per side-1 entry.
+// No state changes between the points of a pass, so every entry is independent.
+struct Sim3Args {
+    FrameArgs f;
+    const omv_sim3_job *jobs;
+    int n_jobs, n1, n2, N;             // N = n_cams * kp_cap: the keyframe N-index bound
+    const int32_t *kp1, *mp1, *kp2, *mp2;
+    omv_kf_mps mps;
+    float th, log_scale;
+    int n_levels;
+    int32_t *vn1;                      // [n1] vnMatch1 per side-1 entry
+    int32_t *vn2;                      // [n_jobs][N] vnMatch2 (-1 initially)
+    int32_t *match12, *n_found;
+};
+
+// Sophus RxSO3 * p + t (rxso3.hpp:265-272, sim3.hpp:226-229): s p + (w 2(v x p) + v x 2(v x p)) + t
+__device__ __forceinline__ void sim3_apply(const omv_sim3f &S, const float *p, float *r) {
+    float two[3], c[3];
+    cross3f(S.q, p, two);
+    for (int i = 0; i < 3; ++i) two[i] = two[i] + two[i];
+    cross3f(S.q, two, c);
+    for (int i = 0; i < 3; ++i) r[i] = (S.scale * p[i] + (S.q[3] * two[i] + c[i])) + S.t[i];
+}
+
+// The job whose run of the side's list holds entry k (runs tile the list in order; the last of equal starts).
+__device__ __forceinline__ int sbs3_job_of(const Sim3Args &a, bool one, int k) {
+    int lo = 0, hi = a.n_jobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((one ? a.jobs[mid].start1 : a.jobs[mid].start2) <= k) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) sbs3_cand_kernel(Sim3Args a) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.n1 + a.n2) return;
+    const bool one = e < a.n1;
+    const int k = one ? e : e - a.n1;
+    const int j = sbs3_job_of(a, one, k);
+    const omv_sim3_job &J = a.jobs[j];
+    const int mp = one ? a.mp1[k] : a.mp2[k];
+    const int tgt = one ? J.kf2 : J.kf1;
+    int best = -1;
+    do {
+        const float P[3] = {a.mps.pos[3 * (size_t)mp], a.mps.pos[3 * (size_t)mp + 1], a.mps.pos[3 * (size_t)mp + 2]};
+        float Pc[3], Pt[3];
+        se3_apply(one ? J.T1w : J.T2w, P, Pc);
+        sim3_apply(one ? J.S21 : J.S12, Pc, Pt);
+        if (Pt[2] < 0.0f) break;   // depth must be positive
+        // invz = 1.0 / z in double, stored as float: equal to the float quotient (53 >= 2 * 24 + 2)
+        const float invz = 1.0f / Pt[2];
+        const float x = Pt[0] * invz, y = Pt[1] * invz;
+        const float u = J.fx * x + J.cx, v = J.fy * y + J.cy;
+        if (!(u >= a.f.min_x && u < a.f.max_x && v >= a.f.min_y && v < a.f.max_y)) break;   // IsInImage
+        const float maxd = a.mps.max_dist[mp];
+        const float maxDistance = 1.2f * maxd, minDistance = 0.8f * a.mps.min_dist[mp];
+        const float dist3D = omv::sqrtf_cr(Pt[0] * Pt[0] + Pt[1] * Pt[1] + Pt[2] * Pt[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) break;
+        int pred = (int)ceil(log((double)(maxd / dist3D)) / (double)a.log_scale);   // MapPoint::PredictScale
+        pred = pred < 0 ? 0 : (pred >= a.n_levels ? a.n_levels - 1 : pred);
+        const float radius = a.th * a.f.scale[pred];
+        uint64_t dmp[4];
+        load_desc(a.mps.desc + (size_t)mp * 32, dmp);
+        Top t;
+        scan_window(a.f, tgt, 0, u, v, radius, pred - 1, pred, dmp, [](int) { return false; }, t);
+        if (t.n > 0 && t.dist(0) <= kTH_HIGH) best = t.idx(0);   // block 0: the N-index is the block index
+    } while (false);
+    if (one) {
+        a.vn1[k] = best;
+    } else if (best >= 0) {
+        const int i2 = a.kp2[k];
+        if ((unsigned)i2 < (unsigned)a.N) a.vn2[(size_t)j * a.N + i2] = best;
+    }
+}
+
+__global__ void __launch_bounds__(256) sbs3_agree_kernel(Sim3Args a) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n1) return;
+    const int j = sbs3_job_of(a, true, k);
+    const int i2 = a.vn1[k];
+    const bool ok = i2 >= 0 && a.vn2[(size_t)j * a.N + i2] == a.kp1[k];
+    a.match12[k] = ok ? i2 : -1;
+    if (ok) atomicAdd(a.n_found + j, 1);
+}
+
 // ---- ORBmatcher::SearchForInitialization (ORBmatcher.cc:895-1004) ---------------------------------------
 // One wavefront per frame pair, F1's level-0 keypoints in order (the claims are sequential: vMatchedDistance /
 // vnMatches21 of F2 change with every accepted match).  For one F1 keypoint the lanes take the window's
@@ -2093,6 +2186,53 @@ omv_status omv_matcher_search_kf(omv_matcher *h, int n_kf, const omv_frame_geom 
         kf_resolve_kernel<<<n_kf, 64, lds, st>>>(a);
     }
     HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_matcher_search_by_sim3(omv_matcher *h, int n_kf, const omv_frame_geom *g, const omv_kp *kps,
+                                      const uint8_t *desc, const int *n_kp, int n_jobs, const omv_sim3_job *jobs,
+                                      int n1, const int32_t *kp1, const int32_t *mp1, int n2, const int32_t *kp2,
+                                      const int32_t *mp2, const omv_kf_mps *mps, float th, float log_scale_factor,
+                                      int n_levels, int32_t *match12, int32_t *n_found, void *stream) {
+    if (!h || !g || !kps || !desc || !n_kp || !mps || n_kf <= 0 || n_kf > h->max_frames || g->n_cams != h->n_cams ||
+        n_jobs < 0 || n1 < 0 || n2 < 0 || (n_jobs > 0 && (!jobs || !n_found)) || (n1 > 0 && (!kp1 || !mp1 || !match12)) ||
+        (n2 > 0 && (!kp2 || !mp2)) || ((n1 + n2) > 0 && (!mps->pos || !mps->desc || !mps->min_dist || !mps->max_dist)) ||
+        n_levels <= 0 || n_levels > 16)
+        return OMV_ERR_ARG;
+    int next1 = 0, next2 = 0;   // runs tile both lists in order; keyframes of the batch
+    for (int j = 0; j < n_jobs; ++j) {
+        const omv_sim3_job &J = jobs[j];
+        if (J.kf1 < 0 || J.kf1 >= n_kf || J.kf2 < 0 || J.kf2 >= n_kf || J.start1 != next1 || J.count1 < 0 ||
+            J.start2 != next2 || J.count2 < 0)
+            return OMV_ERR_ARG;
+        next1 += J.count1, next2 += J.count2;
+    }
+    if (next1 != n1 || next2 != n2) return OMV_ERR_ARG;
+    if (n_jobs == 0) return OMV_OK;
+    hipStream_t st = (hipStream_t)stream;
+    h->last = st;
+    const int N = h->n_cams * h->kp_cap;
+    const size_t job_b = ((sizeof(omv_sim3_job) * n_jobs + 255) / 256) * 256;
+    const size_t vn1_b = ((sizeof(int32_t) * std::max(1, n1) + 255) / 256) * 256;
+    const size_t vn2_b = sizeof(int32_t) * (size_t)n_jobs * N;
+    uint8_t *buf = nullptr;
+    HIP_OK(hipMallocAsync((void **)&buf, job_b + vn1_b + vn2_b, st));
+    Sim3Args a{};
+    fill_frame(h, g, kps, desc, n_kp, a.f);
+    a.jobs = reinterpret_cast<const omv_sim3_job *>(buf);
+    a.n_jobs = n_jobs, a.n1 = n1, a.n2 = n2, a.N = N;
+    a.kp1 = kp1, a.mp1 = mp1, a.kp2 = kp2, a.mp2 = mp2, a.mps = *mps;
+    a.th = th, a.log_scale = log_scale_factor, a.n_levels = n_levels;
+    a.vn1 = reinterpret_cast<int32_t *>(buf + job_b);
+    a.vn2 = reinterpret_cast<int32_t *>(buf + job_b + vn1_b);
+    a.match12 = match12, a.n_found = n_found;
+    HIP_OK(hipMemcpyAsync(buf, jobs, sizeof(omv_sim3_job) * n_jobs, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(a.vn2, 0xff, vn2_b, st));
+    HIP_OK(hipMemsetAsync(n_found, 0, sizeof(int32_t) * n_jobs, st));
+    if (n1 + n2 > 0) sbs3_cand_kernel<<<(n1 + n2 + 255) / 256, 256, 0, st>>>(a);
+    if (n1 > 0) sbs3_agree_kernel<<<(n1 + 255) / 256, 256, 0, st>>>(a);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipFreeAsync(buf, st));
     return OMV_OK;
 }
 

@@ -372,6 +372,57 @@ class ORBmatcher:
         params.check_ori = int(self.mbCheckOrientation)
         return self._search_kf(frames, _lib.OMV_KF_SBP_FRAME, jobs, mp_list, mps, params, frames.kp_to_mp, stream)
 
+    def SearchBySim3(self, kfs, jobs, kp1, mp1, kp2, mp2, mps, th=7.5, stream=None):
+        """ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (src/ORBmatcher.cc:1771-1983) for keyframe
+        pairs of the FrameBatch `kfs`.  jobs: dicts (see sim3_job_array) or a prebuilt omv_sim3_job array; kp1 /
+        mp1: device int32, per pair in job order, the pKF1 keypoints (N-index) whose map point is projected and
+        its table row (kp2 / mp2 likewise for pKF2); mps: dict of device tensors pos / min_dist / max_dist / desc.
+        Returns (match12 [len(kp1)]: the pKF2 keypoint each side-1 entry is matched to, -1 none; n_found per
+        pair), device int32."""
+        import torch
+        h = self._handle(kfs)
+        self.AssignFeaturesToGrid(kfs, stream)
+        arr = jobs if not isinstance(jobs, (list, tuple)) else sim3_job_array(jobs)
+        n_jobs = len(jobs)
+        dev = kfs.kps.device
+        n1, n2 = int(kp1.shape[0]), int(kp2.shape[0])
+        match12 = torch.empty(max(n1, 1), dtype=torch.int32, device=dev)
+        n_found = torch.empty(max(n_jobs, 1), dtype=torch.int32, device=dev)
+        m = _lib.KfMps(_lib.ptr(mps["pos"]), None, _lib.ptr(mps["min_dist"]), _lib.ptr(mps["max_dist"]),
+                       _lib.ptr(mps["desc"]))
+        g = kfs.geom
+        log_sf = float(np.float32(np.log(np.float64(np.float32(g.scale_factors[1])))))
+        _lib.check(self._lib.omv_matcher_search_by_sim3(
+            h, kfs.n_frames, ctypes.byref(g), _lib.ptr(kfs.kps), _lib.ptr(kfs.desc), _lib.ptr(kfs.n_kp), n_jobs, arr,
+            n1, _lib.ptr(kp1), _lib.ptr(mp1), n2, _lib.ptr(kp2), _lib.ptr(mp2), ctypes.byref(m), ctypes.c_float(th),
+            ctypes.c_float(log_sf), int(g.nlevels), _lib.ptr(match12), _lib.ptr(n_found), self._stream(stream)),
+            "omv_matcher_search_by_sim3")
+        return match12[:n1], n_found[:n_jobs]
+
+
+def sim3_job_array(jobs):
+    """omv_sim3_job array of dict jobs {kf1, kf2, T1w, T2w ([qx qy qz qw tx ty tz]), S12, S21 ({q, t, scale}),
+    fx, fy, cx, cy, start1, count1, start2, count2}."""
+    arr = (_lib.Sim3Job * max(len(jobs), 1))()
+    for i, jb in enumerate(jobs):
+        a = arr[i]
+        a.kf1, a.kf2 = int(jb["kf1"]), int(jb["kf2"])
+        for dst, T in ((a.T1w, jb["T1w"]), (a.T2w, jb["T2w"])):
+            T = np.asarray(T, np.float32).reshape(7)
+            for q in range(4):
+                dst.q[q] = float(T[q])
+            for q in range(3):
+                dst.t[q] = float(T[4 + q])
+        for dst, S in ((a.S12, jb["S12"]), (a.S21, jb["S21"])):
+            for q in range(4):
+                dst.q[q] = float(S["q"][q])
+            for q in range(3):
+                dst.t[q] = float(S["t"][q])
+            dst.scale = float(S["scale"])
+        a.fx, a.fy, a.cx, a.cy = (float(np.float32(jb[k])) for k in ("fx", "fy", "cx", "cy"))
+        a.start1, a.count1, a.start2, a.count2 = (int(jb[k]) for k in ("start1", "count1", "start2", "count2"))
+    return arr
+
 
 def kf_search_params(th, max_dist, cams, scale_factor=1.2, nlevels=8, bf=0.0, uright=None, mp_angle=None):
     """omv_kf_search_params: window factor th, acceptance max_dist (TH_LOW, TH_LOW * ratioHamming or

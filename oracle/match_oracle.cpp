@@ -12,6 +12,8 @@
 //     + KannalaBrandt8::project(Eigen::Vector3f)     src/CameraModels/KannalaBrandt8.cpp:48-67
 //   ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
 //                                                    src/ORBmatcher.cc:1985-2413 (+ ComputeThreeMaxima :2537-2573)
+//   ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, S12, th)
+//                                                    src/ORBmatcher.cc:1771-1983
 //   cv::BFMatcher(NORM_HAMMING).knnMatch(k = 2)      as called by Frame::ComputeMultiFishEyeMatches,
 //                                                    src/Frame.cc:1483 (OpenCV batchDistance K = 2:
 //                                                    strict '<' insertion, first train index wins ties)
@@ -610,6 +612,92 @@ int oracle_search_kf(const FrameGeom *g, const KP *kps, const uint8_t *desc, int
                     }
         }
         n_matches[j] = nm;
+    }
+    return 0;
+}
+
+// ---- ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, S12, th)            src/ORBmatcher.cc:1771-1983
+// Sophus Sim3f * p = RxSO3 * p + t (sim3.hpp:226-229) with RxSO3 * p = s p + (w 2(v x p) + v x 2(v x p))
+// (rxso3.hpp:265-272, s = the caller's S.scale()).  Side lists: the keypoints whose map point the reference
+// projects (mapped, not vbAlreadyMatched, not bad), in index order; vnMatch1 / vnMatch2 are the reference's
+// per-keypoint arrays.
+static void sim3_apply(const omv_sim3f &S, const float *p, float *r) {
+    float two[3], c[3];
+    cross3f(S.q, p, two);
+    for (int i = 0; i < 3; ++i) two[i] = two[i] + two[i];
+    cross3f(S.q, two, c);
+    for (int i = 0; i < 3; ++i) r[i] = (S.scale * p[i] + (S.q[3] * two[i] + c[i])) + S.t[i];
+}
+
+int oracle_search_by_sim3(const FrameGeom *g, const KP *kps, const uint8_t *desc, int kp_cap, const int *n_kp,
+                          int n_kf, int n_jobs, const omv_sim3_job *jobs, const int32_t *kp1, const int32_t *mp1,
+                          const int32_t *kp2, const int32_t *mp2, const float *pos, const float *min_d,
+                          const float *max_d, const uint8_t *mp_desc, float th, float log_scale_factor, int n_levels,
+                          int32_t *match12, int32_t *n_found) {
+    const int C = g->n_cams;
+    std::vector<View> views(n_kf);
+    for (int kf = 0; kf < n_kf; ++kf) {
+        views[kf] = View{g, 0, 0, {}, kps + (size_t)kf * C * kp_cap, kp_cap, n_kp + (size_t)kf * C};
+        build_grids(views[kf]);
+    }
+    const int N = C * kp_cap;   // N-index bound (GetMapPointMatches().size() <= N)
+    for (int j = 0; j < n_jobs; ++j) {
+        const omv_sim3_job &J = jobs[j];
+        // one direction: the points of a side projected through T then S into keyframe `tgt`
+        auto pass = [&](const int32_t *kpl, const int32_t *mpl, int start, int count, const omv_se3f &Tw,
+                        const omv_sim3f &S, int tgt, std::vector<int> &vnMatch) {
+            SE3F T;
+            std::memcpy(T.q, Tw.q, 16), std::memcpy(T.t, Tw.t, 12);
+            const View &v = views[tgt];
+            const KP *kk = kps + (size_t)tgt * C * kp_cap;
+            const uint8_t *dd = desc + (size_t)tgt * C * kp_cap * 32;
+            for (int e = start; e < start + count; ++e) {
+                const int mp = mpl[e];
+                const float *P = pos + 3 * (size_t)mp;
+                float p3Dc1[3], p3Dc2[3];
+                se3_apply(T, P, p3Dc1);
+                sim3_apply(S, p3Dc1, p3Dc2);
+                if (p3Dc2[2] < 0.0) continue;   // depth must be positive
+                const float invz = 1.0 / p3Dc2[2];
+                const float x = p3Dc2[0] * invz;
+                const float y = p3Dc2[1] * invz;
+                const float u = J.fx * x + J.cx;
+                const float vv = J.fy * y + J.cy;
+                if (!(u >= g->min_x && u < g->max_x && vv >= g->min_y && vv < g->max_y)) continue;   // IsInImage
+                const float maxDistance = 1.2f * max_d[mp], minDistance = 0.8f * min_d[mp];
+                const float dist3D = std::sqrt(p3Dc2[0] * p3Dc2[0] + p3Dc2[1] * p3Dc2[1] + p3Dc2[2] * p3Dc2[2]);
+                if (dist3D < minDistance || dist3D > maxDistance) continue;
+                int pred = (int)std::ceil(std::log((double)(max_d[mp] / dist3D)) / (double)log_scale_factor);
+                if (pred < 0) pred = 0;
+                else if (pred >= n_levels) pred = n_levels - 1;
+                const float radius = th * g->scale_factors[pred];
+                const std::vector<int> win = features_in_area(v, u, vv, radius, 0, -1, 0);   // KeyFrame version
+                if (win.empty()) continue;
+                const uint8_t *dMP = mp_desc + (size_t)mp * 32;
+                int bestDist = INT32_MAX, bestIdx = -1;
+                for (int idx : win) {
+                    const KP &kp = kk[idx];
+                    if (kp.octave < pred - 1 || kp.octave > pred) continue;
+                    const int dist = descriptor_distance(dMP, dd + (size_t)idx * 32);
+                    if (dist < bestDist) bestDist = dist, bestIdx = idx;
+                }
+                if (bestDist <= TH_HIGH) vnMatch[kpl[e]] = bestIdx;
+            }
+        };
+        std::vector<int> vnMatch1(N, -1), vnMatch2(N, -1);
+        pass(kp1, mp1, J.start1, J.count1, J.T1w, J.S21, J.kf2, vnMatch1);
+        pass(kp2, mp2, J.start2, J.count2, J.T2w, J.S12, J.kf1, vnMatch2);
+        int nFound = 0;   // check agreement
+        for (int e = J.start1; e < J.start1 + J.count1; ++e) {
+            const int i1 = kp1[e];
+            const int idx2 = vnMatch1[i1];
+            match12[e] = -1;
+            if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+                match12[e] = idx2;
+                nFound++;
+            }
+        }
+        n_found[j] = nFound;
     }
     return 0;
 }

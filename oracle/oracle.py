@@ -557,3 +557,38 @@ def search_for_initialization(geom, kps1, desc1, kps2, desc2, prev, window=100, 
     n = f(ctypes.cast(ctypes.byref(geom), ctypes.c_void_p), _p(kps1), _p(desc1), len(kps1), _p(kps2), _p(desc2),
           len(kps2), _p(prev), int(window), nnratio, int(check_ori), _p(m12))
     return n, m12, prev
+
+
+# ---- SearchBySim3 ------------------------------------------------------------------------------------
+def _kf_geom(b):
+    from openmavis_amd._lib import FrameGeom
+    g = FrameGeom()
+    g.n_cams, g.min_x, g.max_x, g.min_y, g.max_y, g.nlevels = b["n_cams"], 0.0, float(b["width"]), 0.0, \
+        float(b["height"]), b["nlevels"]
+    s = np.float32(1.0)
+    for i in range(b["nlevels"]):
+        g.scale_factors[i] = float(s)
+        s = np.float32(s * np.float32(1.2))
+    return g
+
+
+def search_by_sim3(b, th=7.5):
+    """Restated ORBmatcher::SearchBySim3 on a synth_sim3 batch: (match12 [n1] per side-1 entry, n_found [jobs])."""
+    from openmavis_amd.matcher import sim3_job_array
+    g = _kf_geom(b)
+    jobs = sim3_job_array(b["jobs"])
+    m = b["mps"]
+    kp1, mp1 = np.ascontiguousarray(b["kp1"], np.int32), np.ascontiguousarray(b["mp1"], np.int32)
+    kp2, mp2 = np.ascontiguousarray(b["kp2"], np.int32), np.ascontiguousarray(b["mp2"], np.int32)
+    match12 = np.full(max(len(kp1), 1), -7, np.int32)
+    n_found = np.zeros(max(len(b["jobs"]), 1), np.int32)
+    f = lib().oracle_search_by_sim3
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + \
+        [ctypes.c_void_p] * 9 + [ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f(ctypes.cast(ctypes.byref(g), ctypes.c_void_p), _p(np.ascontiguousarray(b["kps"])),
+      _p(np.ascontiguousarray(b["desc"])), int(b["kp_cap"]), _p(np.ascontiguousarray(b["n_kp"], np.int32)),
+      int(b["n_kf"]), len(b["jobs"]), ctypes.cast(jobs, ctypes.c_void_p), _p(kp1), _p(mp1), _p(kp2), _p(mp2),
+      _p(m["pos"]), _p(m["min_dist"]), _p(m["max_dist"]), _p(m["desc"]), float(th), float(np.float32(np.log(np.float64(np.float32(1.2))))),
+      int(b["nlevels"]), _p(match12), _p(n_found))
+    return match12[:len(kp1)], n_found[:len(b["jobs"])]
