@@ -230,6 +230,18 @@ __device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
     return max(A, -B);
 }
 
+// Inclusive wave64 prefix sum by DPP (row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31);
+// every lane of the wave must be active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // One wavefront (= one workgroup of 64) per cell.  The cell's region is staged into LDS with dword
 // loads (row stride rs, 4-byte aligned; pixel (r, q) at pix[r * rs + q]); then
 //   1. prefilter at min(iniTh, minTh): a 9-arc of the 16-ring always holds two adjacent compass points
@@ -291,13 +303,17 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     auto prefilter = [&](int t) {
         int ncand = 0;
         if (dwords && ndet > 0) {
-            // 4 pixels per lane: the quad of LDS dword j (bytes 4j..4j+3 = columns 4j+k-o of its row) with its
-            // compass neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent
-            // dwords), the tests on packed int16 pairs: d > t <=> sign(d - (t+1)) = 0, d < -t <=> sign(d + t).
+            // 8 pixels per lane: LDS dwords j, j+1 of a row (bytes = columns 4j+k-o) with their compass
+            // neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent dwords),
+            // the tests on packed int16 pairs: d > t <=> sign(d - (t+1)) = 0, d < -t <=> sign(d + t).  The
+            // adjacent-pair test (a0&a4)|(a4&a8)|(a8&a12)|(a12&a0) is (a0|a8)&(a4|a12).  Survivors go to the
+            // list by a DPP wave scan of the per-lane counts; the writes are branch-free (a lane's unused
+            // writes go to its own slot past the list).
             const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
             const int jq0 = (o + 3) >> 2, jq1 = (o + rw - 4) >> 2, nqr = jq1 - jq0 + 1, rsw = rs >> 2;
-            const int nq = nqr * dh;
-            const uint32_t mq = (1u << 20) / (uint32_t)nqr + 1u;   // tq / nqr, exact while tq * nqr < 2^20
+            const int npr = (nqr + 1) >> 1;   // dword pairs per row
+            const int np = npr * dh;
+            const uint32_t mp = (1u << 20) / (uint32_t)npr + 1u;   // tp / npr, exact while tp * npr < 2^20
             const pk16 T1{(short)(t + 1), (short)(t + 1)}, T0{(short)t, (short)t};
             auto lo = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c010c00u)); };
             auto hi = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c030c02u)); };
@@ -310,38 +326,45 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const uint32_t b0 = __builtin_bit_cast(uint32_t, pk16(d0 + T0)), b4 = __builtin_bit_cast(uint32_t, pk16(d4 + T0));
                 const uint32_t b8 = __builtin_bit_cast(uint32_t, pk16(d8 + T0)),
                                b12 = __builtin_bit_cast(uint32_t, pk16(d12 + T0));
-                return ((a0 & a4) | (a4 & a8) | (a8 & a12) | (a12 & a0) | (b0 & b4) | (b4 & b8) | (b8 & b12) |
-                        (b12 & b0)) &
-                       0x80008000u;
+                return (((a0 | a8) & (a4 | a12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
             };
-            for (int t0 = 0; t0 < nq; t0 += 64) {
-                const int tq = t0 + lane;
+            uint16_t *dummy = cand + ndet + lane;
+            for (int t0 = 0; t0 < np; t0 += 64) {
+                const int tp = t0 + lane;
                 uint32_t bits = 0;
-                int r = 0, jq = 0;
-                if (tq < nq) {
-                    const int rr = (int)(((uint32_t)tq * mq) >> 20);
-                    r = 3 + rr, jq = jq0 + tq - rr * nqr;
+                int r = 3, jq = jq0;
+                if (tp < np) {
+                    const int rr = (int)(((uint32_t)tp * mp) >> 20);
+                    r = 3 + rr, jq = jq0 + 2 * (tp - rr * npr);
                     const int j = r * rsw + jq;
-                    const uint32_t C = w32[j], Dn = w32[j + 3 * rsw], Up = w32[j - 3 * rsw];
-                    const uint32_t Lf = __builtin_amdgcn_alignbyte(C, w32[j - 1], 1);
-                    const uint32_t Rt = __builtin_amdgcn_alignbyte(w32[j + 1], C, 3);
-                    const uint32_t pl = test(lo(C), lo(Dn), lo(Rt), lo(Up), lo(Lf));
-                    const uint32_t ph = test(hi(C), hi(Dn), hi(Rt), hi(Up), hi(Lf));
-                    bits = ((pl >> 15) & 1u) | ((pl >> 30) & 2u) | ((ph >> 13) & 4u) | ((ph >> 28) & 8u);
-                    const int q0 = 4 * jq - o;   // columns of the quad outside [3, rw - 4]
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (q0 + k < 3 || q0 + k > rw - 4) bits &= ~(1u << k);
+                    const uint32_t Wm = w32[j - 1], C0 = w32[j], C1 = w32[j + 1], Wp = w32[j + 2];
+                    const uint32_t D0 = w32[j + 3 * rsw], D1 = w32[j + 3 * rsw + 1];
+                    const uint32_t U0 = w32[j - 3 * rsw], U1 = w32[j - 3 * rsw + 1];
+                    const uint32_t L0 = __builtin_amdgcn_alignbyte(C0, Wm, 1), L1 = __builtin_amdgcn_alignbyte(C1, C0, 1);
+                    const uint32_t R0 = __builtin_amdgcn_alignbyte(C1, C0, 3), R1 = __builtin_amdgcn_alignbyte(Wp, C1, 3);
+                    const uint32_t p0 = test(lo(C0), lo(D0), lo(R0), lo(U0), lo(L0));
+                    const uint32_t p1 = test(hi(C0), hi(D0), hi(R0), hi(U0), hi(L0));
+                    const uint32_t p2 = test(lo(C1), lo(D1), lo(R1), lo(U1), lo(L1));
+                    const uint32_t p3 = test(hi(C1), hi(D1), hi(R1), hi(U1), hi(L1));
+                    bits = ((p0 >> 15) & 1u) | ((p0 >> 30) & 2u) | ((p1 >> 13) & 4u) | ((p1 >> 28) & 8u) |
+                           ((p2 >> 11) & 16u) | ((p2 >> 26) & 32u) | ((p3 >> 9) & 64u) | ((p3 >> 24) & 128u);
+                    // columns q0 + k of the pair outside [3, rw - 4] (the second dword of a row's last pair
+                    // may lie wholly past it)
+                    const int q0 = 4 * jq - o;
+                    const int klo = min(max(3 - q0, 0), 8), khi = min(max(rw - 3 - q0, 0), 8);
+                    bits &= ((1u << khi) - 1u) & ~((1u << klo) - 1u);
                 }
-                // row-major order: lanes hold consecutive quads, bit k = column q0 + k
-                const uint64_t m0 = __ballot(bits & 1u), m1 = __ballot(bits & 2u), m2 = __ballot(bits & 4u),
-                               m3 = __ballot(bits & 8u);
-                int pos = ncand + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+                const int cnt = __popc(bits);
+                const int incl = wave_incl_scan_dpp(cnt);
+                int pos = ncand + incl - cnt;
                 const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (bits & (1u << k)) cand[pos++] = (uint16_t)(ibase + k);
-                ncand += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+                for (int k = 0; k < 8; ++k) {   // row-major: lanes hold consecutive pairs, bit k = column q0 + k
+                    const uint32_t b = (bits >> k) & 1u;
+                    *(b ? cand + pos : dummy) = (uint16_t)(ibase + k);
+                    pos += (int)b;
+                }
+                ncand += __builtin_amdgcn_readlane(incl, 63);
             }
         } else {
             for (int i0 = 0; i0 < ndet; i0 += 64) {
@@ -1338,7 +1361,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.node_cap = std::max(max_nodes, max_cells_lvl);
     g.node_cap = (g.node_cap + 15) & ~15;
     o->rmax = ((max_rw + 6) & ~3) * max_rh;   // LDS row stride rounds (rw + misalignment) up to 4 bytes
-    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
+    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6)) + 2 * 64;   // + per-lane dummy slots
     o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
     return OMV_OK;
 }
