@@ -191,42 +191,43 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
 // cornerScore<16>(t) then returns S - 1 (the threshold floor max(t, .) never binds for a corner).
 typedef short pk16 __attribute__((ext_vector_type(2)));   // packed int16 pair (v_pk_* ops)
 
-// (x, y) -> (y, x)
-__device__ __forceinline__ pk16 pk_swap(pk16 x) { return pk16{x.y, x.x}; }
+// The strength on packed f16 pairs (k, k+8): 1024 + n is the f16 bit pattern 0x6400 | n (n < 1024), so the
+// differences d = v - ring are exact, and every min / max of integers in [-255, 255] is exact.  gfx950's
+// v_pk_minimum3_f16 / v_pk_maximum3_f16 take three operands: the 9-arc is min3 of three 3-runs.
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 h2_swap(h2 x) { return h2{x.y, x.x}; }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 h2_biased(const uint8_t *lo, const uint8_t *hi) {   // (1024 + *lo, 1024 + *hi)
+    const u16x2 v{(unsigned short)*lo, (unsigned short)*hi};   // ds_read_u8_d16 / _d16_hi
+    return __builtin_bit_cast(h2, __builtin_bit_cast(uint32_t, v) | 0x64006400u);
+}
 
-// Ring values are handled as pairs (k, k+8), so each min/max below is one v_pk_min/max_i16 for two
-// arcs; Q(k) for k >= 8 is the swapped pair of k-8.
-__device__ __forceinline__ int fast_strength(const uint8_t *p, int stride) {
-    const short v = p[0];
+template <int RS>
+__device__ __forceinline__ int fast_strength_h(const uint8_t *p, int stride_rt) {
+    const int stride = RS > 0 ? RS : stride_rt;
     const int o[16] = {3 * stride, 3 * stride + 1, 2 * stride + 2, stride + 3, 3, -stride + 3, -2 * stride + 2,
                        -3 * stride + 1, -3 * stride, -3 * stride - 1, -2 * stride - 2, -stride - 3, -3, stride - 3,
                        2 * stride - 2, 3 * stride - 1};
-    pk16 d[8];
-    const pk16 vv{v, v};
+    const h2 vv = h2_biased(p, p);
+    h2 d[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = vv - pk16{(short)p[o[k]], (short)p[o[k + 8]]};
-    auto Q = [&](const pk16 *a, int k) { return k < 8 ? a[k] : pk_swap(a[k - 8]); };
-    pk16 mn2[8], mx2[8], mn4[8], mx4[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        mn2[k] = __builtin_elementwise_min(d[k], Q(d, k + 1));
-        mx2[k] = __builtin_elementwise_max(d[k], Q(d, k + 1));
-    }
+    for (int k = 0; k < 8; ++k) d[k] = vv - h2_biased(p + o[k], p + o[k + 8]);
+    auto Q = [&](const h2 *a, int k) { return k < 8 ? a[k] : h2_swap(a[k - 8]); };
+    h2 t3n[8], t3x[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        mn4[k] = __builtin_elementwise_min(mn2[k], Q(mn2, k + 2));
-        mx4[k] = __builtin_elementwise_max(mx2[k], Q(mx2, k + 2));
+        t3n[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[k], Q(d, k + 1)), Q(d, k + 2));
+        t3x[k] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(d[k], Q(d, k + 1)), Q(d, k + 2));
     }
-    pk16 a{-1000, -1000}, b{1000, 1000};
+    h2 a{(_Float16)-1000, (_Float16)-1000}, b{(_Float16)1000, (_Float16)1000};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const pk16 opp = pk_swap(d[k]);   // d[k + 8] paired with d[k]
-        const pk16 m9 = __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], Q(mn4, k + 4)), opp);
-        const pk16 M9 = __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], Q(mx4, k + 4)), opp);
-        a = __builtin_elementwise_max(a, m9);
-        b = __builtin_elementwise_min(b, M9);
+        const h2 m9 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(t3n[k], Q(t3n, k + 3)), Q(t3n, k + 6));
+        const h2 M9 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(t3x[k], Q(t3x, k + 3)), Q(t3x, k + 6));
+        a = __builtin_elementwise_maximum(a, m9);
+        b = __builtin_elementwise_minimum(b, M9);
     }
-    const int A = max((int)a.x, (int)a.y), B = min((int)b.x, (int)b.y);
+    const int A = (int)__builtin_elementwise_maximum(a.x, a.y), B = (int)__builtin_elementwise_minimum(b.x, b.y);
     return max(A, -B);
 }
 
@@ -252,6 +253,7 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int v) {
 //      what the NMS of any threshold >= t sees for non-corners);
 //   3. NMS (3x3, strict >) at iniTh and minTh in one pass over the survivors;
 //   4. emission at iniTh, or minTh if the cell had no iniTh keypoint (ORBextractor.cc:764-782).
+template <int RS>   // LDS row stride in bytes (0: per cell, rounded up to 4)
 __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
                                                         int *cell_cnt, uint32_t *cell_kp, int rmax, int n_blocks) {
@@ -268,19 +270,24 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     const uint8_t *row0 = src + (size_t)c.y0 * sp + c.x0;
     const bool dwords = ((sp & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
     const int o = dwords ? (int)(((uintptr_t)row0) & 3) : 0;
-    const int rs = (rw + o + 3) & ~3;
+    const int rs = RS > 0 ? RS : ((rw + o + 3) & ~3);
     uint8_t *pix = smem + o;
     uint8_t *S = smem + rmax;
     uint16_t *cand = (uint16_t *)(smem + 2 * rmax);
     if (dwords) {
-        const int nd = rs >> 2;
+        const int nd = (rw + o + 3) >> 2;   // dwords of a row read (the LDS row holds rs / 4)
         const uint32_t *g0 = (const uint32_t *)(row0 - o);
         const int sw = sp >> 2;
         uint32_t *l0 = (uint32_t *)smem;
-        const uint32_t mnd = (1u << 20) / (uint32_t)nd + 1u;   // i / nd, exact while i * nd < 2^20
-        for (int i = lane; i < nd * rh; i += 64) {
-            const int r = (int)(((uint32_t)i * mnd) >> 20), w = i - r * nd;
-            l0[i] = g0[(size_t)r * sw + w];
+        // lane -> (row lr of a band of rpi rows, dword w); the band steps down the region by pointer increments
+        const int rpi = 64 / nd, lr = lane / nd, w = lane - lr * nd;
+        if (lr < rpi) {
+            const uint32_t *gs = g0 + (size_t)lr * sw + w;
+            uint32_t *ld = l0 + lr * (rs >> 2) + w;
+            const size_t gstep = (size_t)rpi * sw;
+            const int lstep = rpi * (rs >> 2);
+#pragma unroll 4
+            for (int r = lr; r < rh; r += rpi, gs += gstep, ld += lstep) *ld = *gs;
         }
     } else {
         for (int i = lane; i < rw * rh; i += 64) {
@@ -288,7 +295,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             pix[r * rs + q] = row0[(size_t)r * sp + q];
         }
     }
-    for (int i = lane; i < (rs * rh) >> 2; i += 64) ((uint32_t *)S)[i] = 0;
+    for (int i = lane; i < (rs * rh + 15) >> 4; i += 64) ((uint4 *)S)[i] = make_uint4(0, 0, 0, 0);   // rmax % 16 == 0
     __syncthreads();
     const int dw = rw - 6, dh = rh - 6;   // detection window [3, rw-4] x [3, rh-4]
     const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
@@ -304,9 +311,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         int ncand = 0;
         if (dwords && ndet > 0) {
             // 8 pixels per lane: LDS dwords j, j+1 of a row (bytes = columns 4j+k-o) with their compass
-            // neighbours as whole dwords (up / down rows; left / right by v_alignbyte of the adjacent dwords),
-            // the tests on packed int16 pairs: d > t <=> sign(d - (t+1)) = 0, d < -t <=> sign(d + t).  The
-            // adjacent-pair test (a0&a4)|(a4&a8)|(a8&a12)|(a12&a0) is (a0|a8)&(a4|a12).  Survivors go to the
+            // neighbours as whole dwords (up / down rows; left / right as byte windows of the adjacent dwords, one
+            // v_perm each), the tests on packed int16 pairs.  The adjacent-pair test (a0&a4)|(a4&a8)|(a8&a12)|(a12&a0) is (a0|a8)&(a4|a12).  Survivors go to the
             // list by a DPP wave scan of the per-lane counts; the writes are branch-free (a lane's unused
             // writes go to its own slot past the list).
             const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
@@ -314,18 +320,20 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             const int npr = (nqr + 1) >> 1;   // dword pairs per row
             const int np = npr * dh;
             const uint32_t mp = (1u << 20) / (uint32_t)npr + 1u;   // tp / npr, exact while tp * npr < 2^20
-            const pk16 T1{(short)(t + 1), (short)(t + 1)}, T0{(short)t, (short)t};
-            auto lo = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c010c00u)); };
-            auto hi = [](uint32_t w) { return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(w, w, 0x0c030c02u)); };
+            const pk16 T0{(short)t, (short)t};
+            // bytes s, s+1 (lo) / s+2, s+3 (hi) of the 8-byte {a:b} as a packed int16 pair
+            auto lo = [](uint32_t a, uint32_t b, uint32_t s) {
+                return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(a, b, 0x0c000c00u | ((s + 1) << 16) | s));
+            };
+            auto hi = [](uint32_t a, uint32_t b, uint32_t s) {
+                return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(a, b, 0x0c000c00u | ((s + 3) << 16) | (s + 2)));
+            };
             auto test = [&](pk16 v, pk16 n0, pk16 n4, pk16 n8, pk16 n12) {   // bits 15 / 31: the pair passes
-                const pk16 d0 = v - n0, d4 = v - n4, d8 = v - n8, d12 = v - n12;
-                const uint32_t a0 = ~__builtin_bit_cast(uint32_t, pk16(d0 - T1)),
-                               a4 = ~__builtin_bit_cast(uint32_t, pk16(d4 - T1));
-                const uint32_t a8 = ~__builtin_bit_cast(uint32_t, pk16(d8 - T1)),
-                               a12 = ~__builtin_bit_cast(uint32_t, pk16(d12 - T1));
-                const uint32_t b0 = __builtin_bit_cast(uint32_t, pk16(d0 + T0)), b4 = __builtin_bit_cast(uint32_t, pk16(d4 + T0));
-                const uint32_t b8 = __builtin_bit_cast(uint32_t, pk16(d8 + T0)),
-                               b12 = __builtin_bit_cast(uint32_t, pk16(d12 + T0));
+                // brighter n > v + t <=> sign((v + t) - n); darker n < v - t <=> sign(n - (v - t))
+                const pk16 vp = v + T0, vm = v - T0;
+                auto sg = [](pk16 x) { return __builtin_bit_cast(uint32_t, x); };
+                const uint32_t a0 = sg(vp - n0), a4 = sg(vp - n4), a8 = sg(vp - n8), a12 = sg(vp - n12);
+                const uint32_t b0 = sg(n0 - vm), b4 = sg(n4 - vm), b8 = sg(n8 - vm), b12 = sg(n12 - vm);
                 return (((a0 | a8) & (a4 | a12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
             };
             uint16_t *dummy = cand + ndet + lane;
@@ -340,12 +348,11 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                     const uint32_t Wm = w32[j - 1], C0 = w32[j], C1 = w32[j + 1], Wp = w32[j + 2];
                     const uint32_t D0 = w32[j + 3 * rsw], D1 = w32[j + 3 * rsw + 1];
                     const uint32_t U0 = w32[j - 3 * rsw], U1 = w32[j - 3 * rsw + 1];
-                    const uint32_t L0 = __builtin_amdgcn_alignbyte(C0, Wm, 1), L1 = __builtin_amdgcn_alignbyte(C1, C0, 1);
-                    const uint32_t R0 = __builtin_amdgcn_alignbyte(C1, C0, 3), R1 = __builtin_amdgcn_alignbyte(Wp, C1, 3);
-                    const uint32_t p0 = test(lo(C0), lo(D0), lo(R0), lo(U0), lo(L0));
-                    const uint32_t p1 = test(hi(C0), hi(D0), hi(R0), hi(U0), hi(L0));
-                    const uint32_t p2 = test(lo(C1), lo(D1), lo(R1), lo(U1), lo(L1));
-                    const uint32_t p3 = test(hi(C1), hi(D1), hi(R1), hi(U1), hi(L1));
+                    // left neighbours: {C:prev} from byte 1; right: {next:C} from byte 3
+                    const uint32_t p0 = test(lo(C0, C0, 0), lo(D0, D0, 0), lo(C1, C0, 3), lo(U0, U0, 0), lo(C0, Wm, 1));
+                    const uint32_t p1 = test(hi(C0, C0, 0), hi(D0, D0, 0), hi(C1, C0, 3), hi(U0, U0, 0), hi(C0, Wm, 1));
+                    const uint32_t p2 = test(lo(C1, C1, 0), lo(D1, D1, 0), lo(Wp, C1, 3), lo(U1, U1, 0), lo(C1, C0, 1));
+                    const uint32_t p3 = test(hi(C1, C1, 0), hi(D1, D1, 0), hi(Wp, C1, 3), hi(U1, U1, 0), hi(C1, C0, 1));
                     bits = ((p0 >> 15) & 1u) | ((p0 >> 30) & 2u) | ((p1 >> 13) & 4u) | ((p1 >> 28) & 8u) |
                            ((p2 >> 11) & 16u) | ((p2 >> 26) & 32u) | ((p3 >> 9) & 64u) | ((p3 >> 24) & 128u);
                     // columns q0 + k of the pair outside [3, rw - 4] (the second dword of a row's last pair
@@ -392,7 +399,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             const int i = cand[k];
             int r, q;
             rowcol(i, r, q);
-            const int sv = fast_strength(pix + r * rs + q, rs);
+            const int sv = fast_strength_h<RS>(pix + r * rs + q, rs);
             S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
         }
         __syncthreads();
@@ -1182,6 +1189,7 @@ struct omv_orb {
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
     int rmax = 0;
+    int fast_rs = 0;       // K2 LDS row stride: 68 (17 dwords, odd: rows spread over the banks) when every cell row (plus misalignment) fits, else per cell
     size_t fast_lds = 0;   // K2 dynamic LDS: region + strength map (rmax each) + the candidate list (u16)
     size_t oct_lds = 0;
     size_t pyr_lds[kMaxLevels] = {};   // K1 dynamic LDS per level: x table + the widest row block
@@ -1340,6 +1348,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
         prev_w = L.w, prev_h = L.h;
     }
     g.n_cells = (int)cells.size();
+    if (max_rw > 80 || max_rh > 80) return OMV_ERR_ARG;   // K2's index arithmetic (cells are ~35-45 px)
     const int dw = max_rw - 6, dh = max_rh - 6;
     g.cell_cap = ((dw + 1) / 2) * ((dh + 1) / 2);
     for (int l = 0; l < nl; ++l) {
@@ -1360,7 +1369,8 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.n_max = out_off;
     g.node_cap = std::max(max_nodes, max_cells_lvl);
     g.node_cap = (g.node_cap + 15) & ~15;
-    o->rmax = ((max_rw + 6) & ~3) * max_rh;   // LDS row stride rounds (rw + misalignment) up to 4 bytes
+    o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
+    o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
     o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6)) + 2 * 64;   // + per-lane dummy slots
     o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
     return OMV_OK;
@@ -1493,8 +1503,12 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    fast_cells_kernel<<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(g, o->d_cells, images, image_stride, pitch, o->d_pyr,
-                                                               o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
+    if (o->fast_rs == 68)
+        fast_cells_kernel<68><<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(
+            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
+    else
+        fast_cells_kernel<0><<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(
+            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
     mark(o, st);
     // K3: octree per (image, level)
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
