@@ -406,7 +406,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
         return ncand;
     };
     // NMS at threshold th over the candidates: keypoint k survives iff S > th and S - 1 > every neighbour's
-    // cornerScore (S - 1 if S > th, else 0).  Returns the count; with `out`, emits row-major.
+    // cornerScore (S - 1 if S > th, else 0) -- i.e. S > max(th, 1, every neighbour's S).  Returns the count;
+    // with `out`, emits row-major.
     auto nms = [&](int ncand, int th, uint32_t *out) {
         int base = 0;
         for (int k0 = 0; k0 < ncand; k0 += 64) {
@@ -419,18 +420,14 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 rowcol(i, r, q);
                 const uint8_t *sp8 = S + r * rs + q;
                 const int v = sp8[0];
-                if (v > th) {
-                    keep = true;
-                    const int sc = v - 1;
+                // v > th and v - 1 > (nv > th ? nv - 1 : 0) for all 8 neighbours <=> v > max(nv..., th, 1)
+                int m = max(th, 1);
 #pragma unroll
-                    for (int n = 0; n < 9; ++n) {
-                        if (n == 4) continue;
-                        const int nv = sp8[(n / 3 - 1) * rs + (n % 3 - 1)];
-                        keep = keep && (sc > (nv > th ? nv - 1 : 0));
-                    }
-                    const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
-                    packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)sc << 24);
-                }
+                for (int n = 0; n < 9; ++n)
+                    if (n != 4) m = max(m, (int)sp8[(n / 3 - 1) * rs + (n % 3 - 1)]);
+                keep = v > m;
+                const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
+                packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)(v - 1) << 24);
             }
             const uint64_t m = __ballot(keep);
             const int pos = base + __popcll(m & lt);
