@@ -313,8 +313,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             // 8 pixels per lane: LDS dwords j, j+1 of a row (bytes = columns 4j+k-o) with their compass
             // neighbours as whole dwords (up / down rows; left / right as byte windows of the adjacent dwords, one
             // v_perm each), the tests on packed int16 pairs.  The adjacent-pair test (a0&a4)|(a4&a8)|(a8&a12)|(a12&a0) is (a0|a8)&(a4|a12).  Survivors go to the
-            // list by a DPP wave scan of the per-lane counts; the writes are branch-free (a lane's unused
-            // writes go to its own slot past the list).
+            // list by a DPP wave scan of the per-lane counts, each lane then writing its set bits.
             const uint32_t *w32 = reinterpret_cast<const uint32_t *>(smem);
             const int jq0 = (o + 3) >> 2, jq1 = (o + rw - 4) >> 2, nqr = jq1 - jq0 + 1, rsw = rs >> 2;
             const int npr = (nqr + 1) >> 1;   // dword pairs per row
@@ -336,7 +335,6 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const uint32_t b0 = sg(n0 - vm), b4 = sg(n4 - vm), b8 = sg(n8 - vm), b12 = sg(n12 - vm);
                 return (((a0 | a8) & (a4 | a12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
             };
-            uint16_t *dummy = cand + ndet + lane;
             for (int t0 = 0; t0 < np; t0 += 64) {
                 const int tp = t0 + lane;
                 uint32_t bits = 0;
@@ -365,12 +363,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const int incl = wave_incl_scan_dpp(cnt);
                 int pos = ncand + incl - cnt;
                 const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {   // row-major: lanes hold consecutive pairs, bit k = column q0 + k
-                    const uint32_t b = (bits >> k) & 1u;
-                    *(b ? cand + pos : dummy) = (uint16_t)(ibase + k);
-                    pos += (int)b;
-                }
+                // row-major: lanes hold consecutive pairs, bit k = column q0 + k (a few set bits per lane)
+                for (uint32_t b = bits; b; b &= b - 1u) cand[pos++] = (uint16_t)(ibase + __builtin_ctz(b));
                 ncand += __builtin_amdgcn_readlane(incl, 63);
             }
         } else {
@@ -1045,6 +1039,8 @@ struct DescArgs {
     int n_images;
 };
 
+constexpr int kPatchRows = 37, kPatchDw = 11;   // K5's staged blurred patch: rows cy-18..cy+18, 44 bytes each
+
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int blk = omv::xcd_block(n_blocks);
@@ -1071,6 +1067,27 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     const int score = (int)(p >> 24);
     int sp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
+    int bpitch;
+    const uint8_t *bl = blur_level(g, const_cast<uint8_t *>(a.blur), img, l, &bpitch) + (size_t)cy * bpitch + cx;
+    // The rotated samples lie within radius 18.4 of the keypoint, so the blurred 37 x 37 patch is staged into
+    // this wave's LDS (rows cy-18 .. cy+18, 11 aligned dwords each) while the centroid loads are in flight;
+    // the sampling then reads LDS.  Keypoints lie >= 19 px inside the level, so the dwords stay inside it.
+    __shared__ uint32_t patch[4][kPatchRows * kPatchDw];
+    uint32_t *pw = patch[wave];
+    const uint8_t *prow = bl - (ptrdiff_t)18 * bpitch - 18;
+    const int po = (int)((uintptr_t)prow & 3);
+    const bool staged = (bpitch & 3) == 0;
+    uint32_t pv[7];
+    if (staged) {
+        const uint32_t *pa = reinterpret_cast<const uint32_t *>(prow - po);
+        const int sw = bpitch >> 2;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int i = min(lane + 64 * t, kPatchRows * kPatchDw - 1);
+            const int r = i / kPatchDw, w = i - r * kPatchDw;
+            pv[t] = pa[r * sw + w];
+        }
+    }
     // intensity centroid: items i = lane + 64 t over (disc row vr = i >> 3, dword k = i & 7), 248 items; the disc
     // rows are >= 4 rows inside the level, so the second dword of a row never leaves the allocation
     int m01 = 0, m10 = 0;
@@ -1099,6 +1116,15 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
             }
         }
     }
+    if (staged) {
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+            if (lane + 64 * t < kPatchRows * kPatchDw) pw[lane + 64 * t] = pv[t];
+        // other lanes read these bytes below: a wave's LDS operations complete in order; keep the compiler's too
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     for (int d = 32; d >= 1; d >>= 1) {
         m01 += __shfl_xor(m01, d, 64);
         m10 += __shfl_xor(m10, d, 64);
@@ -1107,8 +1133,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     float sn, cs;
     omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
     const float fa = cs, fb = sn;
-    int bpitch;
-    const uint8_t *bl = blur_level(g, const_cast<uint8_t *>(a.blur), img, l, &bpitch) + (size_t)cy * bpitch + cx;
+    const uint8_t *pb = reinterpret_cast<const uint8_t *>(pw) + 18 * kPatchDw * 4 + 18 + po;   // the keypoint
     uint32_t ia[4], ib[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) {
@@ -1119,8 +1144,13 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
         const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
         const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
-        ia[rd] = bl[(ptrdiff_t)ady * bpitch + adx];
-        ib[rd] = bl[(ptrdiff_t)bdy * bpitch + bdx];
+        if (staged) {
+            ia[rd] = pb[ady * (kPatchDw * 4) + adx];
+            ib[rd] = pb[bdy * (kPatchDw * 4) + bdx];
+        } else {
+            ia[rd] = bl[(ptrdiff_t)ady * bpitch + adx];
+            ib[rd] = bl[(ptrdiff_t)bdy * bpitch + bdx];
+        }
     }
     uint64_t words[4];
 #pragma unroll
@@ -1368,7 +1398,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.node_cap = (g.node_cap + 15) & ~15;
     o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
     o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
-    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6)) + 2 * 64;   // + per-lane dummy slots
+    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
     o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
     return OMV_OK;
 }
