@@ -95,6 +95,7 @@ struct Geom {
     int out_per_img;        // level-output slots per image
     int n_max;              // output rows per image
     int node_cap;           // octree LDS node capacity
+    int ccnt_cap;           // octree child-count region (>= 4 node_cap; also holds the level's cell scan)
     // blurred pyramid (K4): level 0 at pitch blur_pitch0, levels >= 1 at the pyramid's offsets/pitches
     int blur_pitch0;
     long long blur0_bytes, blur_bytes;   // level-0 block, whole per-image block
@@ -543,15 +544,16 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     int *buf = osm + 32;
     NodeSoA A{buf, buf + NC, buf + 2 * NC, buf + 3 * NC, buf + 4 * NC};
     NodeSoA B{buf + 5 * NC, buf + 6 * NC, buf + 7 * NC, buf + 8 * NC, buf + 9 * NC};
-    int *ccnt = buf + 10 * NC;       // 4 * NC
-    int *scanA = buf + 14 * NC;      // NC
-    int *scanB = buf + 15 * NC;      // NC
-    int *map = buf + 16 * NC;        // NC: new index of an unsplit/unprocessed node, or -1
-    int *vlist = buf + 17 * NC;      // NC
-    int *vpos = buf + 18 * NC;       // NC: position in the sorted V list, or -1
-    int *cellscan = buf + 19 * NC;   // cells of this level (<= NC by host check)
-    omv::SortItem *items = reinterpret_cast<omv::SortItem *>(buf + 20 * NC);   // NC items (3 ints)
-    int *sstack = buf + 23 * NC;     // 192
+    int *ccnt = buf + 10 * NC;       // ccnt_cap (>= 4 * NC)
+    int *cellscan = ccnt;            // the level's cells (<= ccnt_cap by host check), gather phase only
+    int *rest = ccnt + g.ccnt_cap;
+    int *scanA = rest;               // NC
+    int *scanB = rest + NC;          // NC
+    int *map = rest + 2 * NC;        // NC: new index of an unsplit/unprocessed node, or -1
+    int *vlist = rest + 3 * NC;      // NC
+    int *vpos = rest + 4 * NC;       // NC: position in the sorted V list, or -1
+    omv::SortItem *items = reinterpret_cast<omv::SortItem *>(rest + 5 * NC);   // NC items (3 ints)
+    int *sstack = rest + 8 * NC;     // 192
 
 #ifdef OMV_OCT_PROFILE
     long long pf_t0 = wall_clock64(), pf_sort = 0, pf_p1 = 0, pf_p2 = 0, pf_gather = 0;
@@ -1060,9 +1062,10 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         a.n_out[img] = tot;
         a.mono[img] = mono;
     }
-    if (j >= cnts[3 * l]) return;
+    // the slot's record is loaded with the level count (one round trip; slots past the count are in bounds)
     const uint32_t p = a.lvl_out[(size_t)img * g.out_per_img + s];
     const uint32_t cl = a.lvl_cls[(size_t)img * g.out_per_img + s];
+    if (j >= cnts[3 * l]) return;
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
     const int score = (int)(p >> 24);
     int sp;
@@ -1394,12 +1397,12 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.cand_per_img = cand_off;
     g.out_per_img = out_off;
     g.n_max = out_off;
-    g.node_cap = std::max(max_nodes, max_cells_lvl);
-    g.node_cap = (g.node_cap + 15) & ~15;
+    g.node_cap = (max_nodes + 15) & ~15;   // <= quota + 3 nodes exist at once (DistributeOctTree's stop rules)
+    g.ccnt_cap = (std::max(4 * g.node_cap, max_cells_lvl) + 15) & ~15;
     o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
     o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
     o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
-    o->oct_lds = (size_t)(32 + 23 * g.node_cap + 192) * sizeof(int);
+    o->oct_lds = (size_t)(32 + 18 * g.node_cap + g.ccnt_cap + 192) * sizeof(int);
     return OMV_OK;
 }
 
