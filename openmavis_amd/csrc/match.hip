@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <vector>
@@ -171,6 +172,34 @@ struct Top {
     }
 };
 
+// The same list for one lane inserting in window order: 32-bit keys dist << 23 | oct << 16 | idx compared by
+// distance alone (k | 0x7fffff < key <=> dist(k) < dist(key)), so a new key moves past strictly larger
+// distances only and equal distances keep window order -- the strict `<` scans' tie rule, at half the
+// compare / select work of the 64-bit keys.
+struct TopSeq {
+    uint32_t key[kTop];
+    int n, count;
+    __device__ __forceinline__ void reset() {
+#pragma unroll
+        for (int q = 0; q < kTop; ++q) key[q] = ~0u;
+        n = count = 0;
+    }
+    __device__ __forceinline__ void insert(int idx, int dist, int oct) {
+        const uint32_t k = ((uint32_t)dist << 23) | ((uint32_t)oct << 16) | (uint32_t)idx;
+        const uint32_t kk = k | 0x7fffffu;
+#pragma unroll
+        for (int q = kTop - 1; q > 0; --q) key[q] = kk < key[q - 1] ? key[q - 1] : (kk < key[q] ? k : key[q]);
+        key[0] = kk < key[0] ? k : key[0];
+        n = min(n + 1, kTop);
+    }
+    __device__ __forceinline__ int idx(int q) const { return (int)(key[q] & 0xffff); }
+    __device__ __forceinline__ int oct(int q) const { return (int)((key[q] >> 16) & 0x7f); }
+    __device__ __forceinline__ int dist(int q) const { return (int)(key[q] >> 23); }
+    __device__ __forceinline__ uint32_t rec(int q) const {   // Rec entry: idx | dist << 16 | oct << 25
+        return (uint32_t)idx(q) | ((uint32_t)dist(q) << 16) | ((uint32_t)oct(q) << 25);
+    }
+};
+
 __device__ __forceinline__ void load_desc(const uint8_t *p, uint64_t d[4]) {
     const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
     d[0] = q[0], d[1] = q[1], d[2] = q[2], d[3] = q[3];
@@ -178,9 +207,9 @@ __device__ __forceinline__ void load_desc(const uint8_t *p, uint64_t d[4]) {
 
 // Window of GetFeaturesInArea(x, y, r, level-1, level, cam), in the reference's iteration order;
 // keeps the kTop best unblocked candidates by (dist, order).
-template <class Blocked>
+template <class Blocked, class TopT>
 __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, float y, float r, int minL, int maxL,
-                            const uint64_t dmp[4], Blocked blocked, Top &t) {
+                            const uint64_t dmp[4], Blocked blocked, TopT &t) {
     t.reset();
     const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
     if (nMinCellX >= kGridCols) return;
@@ -378,7 +407,7 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
         const long long fm = gid / C;
         const int frame = (int)(fm / m.M);
         const size_t bc = (size_t)gid;
-        Top t;
+        std::conditional_t<G == 1, TopSeq, Top> t;
         t.reset();
         uint64_t dmp[4];
         load_desc(m.desc + (size_t)fm * 32, dmp);
@@ -521,7 +550,7 @@ __device__ __forceinline__ Pick rescan_window(const ResolveArgs &a, int frame, s
     const size_t bc = fm * f.n_cams + c;
     uint64_t dmp[4];
     load_desc(m.desc + fm * 32, dmp);
-    Top t;
+    TopSeq t;
     scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f), lvl - 1,
                 lvl, dmp, [&](int slot) { return slot == pa0 ? obs : bit_of(bits, slot); }, t);
     Pick p;
@@ -1141,7 +1170,7 @@ __global__ void __launch_bounds__(256) lf_cand_kernel(FrameArgs f, LastArgs L, L
     const int c = (int)(gid % C);
     const long long fs = gid / C;
     const int frame = (int)(fs / L.S), s = (int)(fs % L.S);
-    Top t;
+    TopSeq t;
     t.reset();
     float x, y, r;
     int minL, maxL;
@@ -1233,7 +1262,7 @@ __global__ void __launch_bounds__(64) lf_resolve_kernel(LfResolveArgs a) {
                             lf_window(f, a.L, a.G, a.Tcw[frame], a.Tlw[frame], frame, s, c, x, y, rr, minL, maxL);
                             uint64_t dmp[4];
                             load_desc(a.L.desc + fs * 32, dmp);
-                            Top t;
+                            TopSeq t;
                             scan_window(f, frame, c, x, y, rr, minL, maxL, dmp,
                                         [&](int slot) { return bit_of(bits, slot); }, t);
                             if (t.n > 0) best = t.idx(0), bd = t.dist(0);
@@ -1425,7 +1454,7 @@ __global__ void __launch_bounds__(256) kf_cand_kernel(KfArgs a) {
     const int kf = J.kf, cam = J.cam, mode = a.mode, C = a.f.n_cams, cap = a.f.kp_cap;
     const bool claim = kf_claim_mode(mode);
     const int mp = a.mp_list[e];
-    Top t;
+    TopSeq t;
     t.reset();
     float4 g = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
     do {
@@ -1545,7 +1574,7 @@ __global__ void __launch_bounds__(64) kf_resolve_kernel(KfArgs a) {
                         kf_levels(a.mode, __float_as_int(g.w), minL, maxL);
                         uint64_t dmp[4];
                         load_desc(a.mps.desc + (size_t)a.mp_list[e] * 32, dmp);
-                        Top t;
+                        TopSeq t;
                         scan_window(a.f, kf, cam, g.x, g.y, g.z, minL, maxL, dmp,
                                     [&](int slot) { return bit_of(claimed, slot); }, t);
                         if (t.n > 0) idx = t.idx(0), dist = t.dist(0);
@@ -1669,7 +1698,7 @@ __global__ void __launch_bounds__(256) sbs3_cand_kernel(Sim3Args a) {
         const float radius = a.th * a.f.scale[pred];
         uint64_t dmp[4];
         load_desc(a.mps.desc + (size_t)mp * 32, dmp);
-        Top t;
+        TopSeq t;
         scan_window(a.f, tgt, 0, u, v, radius, pred - 1, pred, dmp, [](int) { return false; }, t);
         if (t.n > 0 && t.dist(0) <= kTH_HIGH) best = t.idx(0);   // block 0: the N-index is the block index
     } while (false);
