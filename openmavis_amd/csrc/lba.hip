@@ -799,29 +799,31 @@ __device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
         const double d1 = det * i0;
         const double i1 = p00 * idet;
         if (lane == 0 && !(p00 != 0.0 && isfinite(p00) && d1 != 0.0 && isfinite(d1))) *bad = 1;
-        const double uj = bj1 - l * bj0;
+        const double uj = __builtin_fma(-l, bj0, bj1);
         const double lb0 = bj0 * i0, lb1 = uj * i1;   // L_B row j (used when j is below the pivot)
-        // every candidate value computed, then selected (v_cndmask): the cases are mutually exclusive, and
-        // a branchy form costs more in exec-mask flow than the arithmetic it skips
+        // Lower part (i >= j) as one fused form x' = bi0 C0 + ui C1 + (j trailing ? x : 0) with per-column
+        // coefficients: trailing j > c0+1: (-lb0, -lb1) (the Schur update); j = c0: (i0, 0) (L column c0, and
+        // L[c0+1][c0] = p10 i0 = l); j = c0+1: (0, i1) (L column c0+1).  Upper part (i < j): the W = L^-1 rows.
+        // Every candidate is computed, then selected (v_cndmask): the cases are mutually exclusive, and a
+        // branchy form costs more in exec-mask flow than the arithmetic it skips.
+        const bool jA = j > c0 + 1, jC = j == c0 + 1;
+        const double C0 = jA ? -lb0 : (j == c0 ? i0 : 0.0);
+        const double C1 = jA ? -lb1 : (jC ? i1 : 0.0);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int i = q + 4 * t;
             const double x = cur[t];
-            const double ui = bi1[t] - l * bi0[t];
-            const double trail = x - bi0[t] * bj0 * i0 - ui * uj * i1;
+            const double ui = __builtin_fma(-l, bi0[t], bi1[t]);
+            const double lowv = __builtin_fma(bi0[t], C0, __builtin_fma(ui, C1, jA ? x : 0.0));
             const double w0 = i == c0 ? 1.0 : (i == c0 + 1 ? 0.0 : bi0[t]);
             const double w1 = i == c0 ? -l : (i == c0 + 1 ? 1.0 : ui);
             const double base = i < c0 ? x : 0.0;
-            const double upv = j == c0 + 1 ? base - l * w0 : base - (lb0 * w0 + lb1 * w1);
+            const double upv = jC ? __builtin_fma(-l, w0, base) : __builtin_fma(-lb0, w0, __builtin_fma(-lb1, w1, base));
             const bool lower = i >= j;
-            double r = x;
-            r = (lower && j > c0 + 1) ? trail : r;
-            r = (lower && j == c0 && i > c0 + 1) ? bi0[t] * i0 : r;
-            r = (lower && j == c0 + 1 && i > c0 + 1) ? ui * i1 : r;
-            r = (lower && i == c0 + 1 && j == c0) ? l : r;
-            r = (lower && i == c0 + 1 && j == c0 + 1) ? d1 : r;
-            r = (!lower && j > c0 && i <= c0 + 1 && !(i == c0 + 1 && j == c0 + 1)) ? upv : r;
-            cur[t] = r;
+            const bool keep_lo = j < c0 || (i == c0 && j == c0);
+            const double lo_r = keep_lo ? x : ((i == c0 + 1 && jC) ? d1 : lowv);
+            const bool up_set = j > c0 && i <= c0 + 1 && !(i == c0 + 1 && jC);
+            cur[t] = lower ? lo_r : (up_set ? upv : x);
         }
         if (j == c0 + 2 || j == c0 + 3) {
 #pragma unroll
