@@ -1023,12 +1023,12 @@ __global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_til
 
 // K5 --------------------------------------------------------------------------------------------
 // Orientation + rBRIEF, one wavefront per output slot (inactive slots leave at once):
-//   IC_Angle (:19-43) over the r = 15 disc of the UN-blurred level: per (disc row, dword) one v_dot4 with the
-//   in-disc byte mask (row sum -> m01) and one with the weights u + 15 (m10), from two aligned dword loads and
-//   a v_alignbyte; a wave reduction; fastAtan2 (degrees, float);
-//   computeOrbDescriptor (:46-90) on the BLURRED level: lane = pattern pair (4 rounds of 64), steering by
-//   (cos, sin) with cvRound, the two samples as byte gathers (L2-resident: the image's levels were just
-//   blurred), bit = I(a) < I(b) collected by 4 ballots = 32 bytes.
+//   IC_Angle (:19-43) over the r = 15 disc of the UN-blurred level: lane = (disc row, 16-byte half), one 16-byte
+//   and one dword load, four v_dot4 items each with the in-disc byte mask (row sum -> m01) and the weights
+//   u + 15 (m10); a wave reduction; fastAtan2 (degrees, float);
+//   computeOrbDescriptor (:46-90) on the BLURRED level: the 37 x 37 patch around the keypoint is staged into LDS
+//   (two 16-byte loads per lane, issued with the centroid loads), lane = pattern pair (4 rounds of 64), steering
+//   by (cos, sin) with cvRound, the two samples read from LDS, bit = I(a) < I(b) collected by 4 ballots = 32 bytes.
 struct DescArgs {
     const uint8_t *images;
     size_t img_stride, pitch0;
@@ -1041,7 +1041,8 @@ struct DescArgs {
     int n_images;
 };
 
-constexpr int kPatchRows = 37, kPatchDw = 11;   // K5's staged blurred patch: rows cy-18..cy+18, 44 bytes each
+constexpr int kPatchRows = 37, kPatchDw = 12;   // K5's staged blurred patch: rows cy-18..cy+18, 48 bytes each
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, dword-aligned
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1073,56 +1074,51 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     int bpitch;
     const uint8_t *bl = blur_level(g, const_cast<uint8_t *>(a.blur), img, l, &bpitch) + (size_t)cy * bpitch + cx;
     // The rotated samples lie within radius 18.4 of the keypoint, so the blurred 37 x 37 patch is staged into
-    // this wave's LDS (rows cy-18 .. cy+18, 11 aligned dwords each) while the centroid loads are in flight;
-    // the sampling then reads LDS.  Keypoints lie >= 19 px inside the level, so the dwords stay inside it.
-    __shared__ uint32_t patch[4][kPatchRows * kPatchDw];
+    // this wave's LDS (rows cy-18 .. cy+18, three 16-byte loads each) while the centroid loads are in flight;
+    // the sampling then reads LDS.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so every load
+    // below stays inside the level (at most 8 bytes into the next row).
+    __shared__ __attribute__((aligned(16))) uint32_t patch[4][kPatchRows * kPatchDw];
     uint32_t *pw = patch[wave];
     const uint8_t *prow = bl - (ptrdiff_t)18 * bpitch - 18;
     const int po = (int)((uintptr_t)prow & 3);
     const bool staged = (bpitch & 3) == 0;
-    uint32_t pv[7];
+    u32x4a pv[2];
     if (staged) {
         const uint32_t *pa = reinterpret_cast<const uint32_t *>(prow - po);
         const int sw = bpitch >> 2;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            const int i = min(lane + 64 * t, kPatchRows * kPatchDw - 1);
-            const int r = i / kPatchDw, w = i - r * kPatchDw;
-            pv[t] = pa[r * sw + w];
+        for (int t = 0; t < 2; ++t) {
+            const int i = min(lane + 64 * t, kPatchRows * 3 - 1);
+            const int r = i / 3, w = i - 3 * r;
+            pv[t] = *reinterpret_cast<const u32x4a *>(pa + r * sw + 4 * w);
         }
     }
-    // intensity centroid: items i = lane + 64 t over (disc row vr = i >> 3, dword k = i & 7), 248 items; the disc
-    // rows are >= 4 rows inside the level, so the second dword of a row never leaves the allocation
+    // intensity centroid: lane = (disc row vr = lane >> 1, half h = lane & 1) = bytes cx-15+16h .. +15 of row
+    // cy-15+vr as four dot4 items (one 16-byte and one dword load, byte-aligned by v_alignbyte)
     int m01 = 0, m10 = 0;
     {
-        uint32_t lo[4], hi[4];
-        int sh[4];
+        const int vr = min(lane >> 1, 30), h = lane & 1;
+        const uint8_t *ad = src + (size_t)(cy - 15 + vr) * sp + (cx - 15 + 16 * h);
+        const uint32_t *al = reinterpret_cast<const uint32_t *>((uintptr_t)ad & ~(uintptr_t)3);
+        const int sh = (int)((uintptr_t)ad & 3);
+        const u32x4a q4 = *reinterpret_cast<const u32x4a *>(al);
+        const uint32_t q5 = al[4];
+        const uint32_t qq[5] = {q4.x, q4.y, q4.z, q4.w, q5};
+        if (lane < 62) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i = lane + 64 * t;
-            const int vr = min(i >> 3, 30), k = i & 7;
-            const uint8_t *ad = src + (size_t)(cy - 15 + vr) * sp + (cx - 15 + 4 * k);
-            const uint32_t *al = reinterpret_cast<const uint32_t *>((uintptr_t)ad & ~(uintptr_t)3);
-            sh[t] = (int)((uintptr_t)ad & 3);
-            lo[t] = al[0];
-            hi[t] = al[1];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i = lane + 64 * t;
-            if (i < 31 * 8) {
-                const uint2 mk = c_icmask[i];
-                const uint32_t w = __builtin_amdgcn_alignbyte(hi[t], lo[t], sh[t]);
+            for (int k = 0; k < 4; ++k) {
+                const uint2 mk = c_icmask[vr * 8 + 4 * h + k];
+                const uint32_t w = __builtin_amdgcn_alignbyte(qq[k + 1], qq[k], sh);
                 const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
                 m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
-                m01 += ((i >> 3) - 15) * rs;
+                m01 += (vr - 15) * rs;
             }
         }
     }
     if (staged) {
 #pragma unroll
-        for (int t = 0; t < 7; ++t)
-            if (lane + 64 * t < kPatchRows * kPatchDw) pw[lane + 64 * t] = pv[t];
+        for (int t = 0; t < 2; ++t)
+            if (lane + 64 * t < kPatchRows * 3) reinterpret_cast<u32x4a *>(pw)[lane + 64 * t] = pv[t];
         // other lanes read these bytes below: a wave's LDS operations complete in order; keep the compiler's too
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
