@@ -122,7 +122,7 @@ __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_
 // K1 --------------------------------------------------------------------------------------------
 // One workgroup per (block of kPyrBlock output rows, image) of level l: the source rows of level l-1
 // the block reads (y.sx0 of its first row .. y.sx1 of its last, ~1.2 kPyrBlock + 2) are staged in LDS
-// once with dword loads, together with the level's x table; each thread then computes 4 adjacent
+// once with 16-byte loads, together with the level's x table; each thread then computes 4 adjacent
 // output pixels per step and stores them as one dword (level pitches are 16-byte aligned).
 constexpr int kPyrBlock = 16;
 
@@ -136,29 +136,34 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     int sp;
     const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, l - 1, &sp);
     const int sw = g.lv[l - 1].w;
-    const int ndw = (sw + 3) >> 2;
+    const int ndw = ((sw + 15) >> 4) << 2;   // LDS row: whole 16-byte groups
     XTab *xs = reinterpret_cast<XTab *>(pyr_lds);            // [L.w]
     uint32_t *rows = pyr_lds + ((3 * L.w + 3) & ~3);         // [nr][ndw]
     const int sy0 = yt[L.ytab_off + dy0].sx0, sy1 = yt[L.ytab_off + dy1 - 1].sx1;
     const int nr = sy1 - sy0 + 1;
     for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
-    const bool dwords = (sp & 3) == 0 && ((((uintptr_t)src) & 3) == 0) && ndw * 4 <= sp;
-    if (dwords) {
-        for (int q = tid; q < nr * ndw; q += 256) {
-            const int r = q / ndw, i = q - r * ndw;
-            rows[q] = reinterpret_cast<const uint32_t *>(src + (size_t)(sy0 + r) * sp)[i];
+    // q / d as __umulhi(q, ceil(2^32 / d)): exact for q < 2^32 / d (q < 2^16 here)
+    auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
+    if ((sp & 15) == 0 && (((uintptr_t)src) & 15) == 0) {   // 16-byte loads (the groups stay inside the pitch)
+        const int n4 = ndw >> 2;
+        const uint32_t m4 = divm(n4);
+        for (int q = tid; q < nr * n4; q += 256) {
+            const int r = (int)__umulhi((uint32_t)q, m4), i = q - r * n4;
+            reinterpret_cast<uint4 *>(rows)[q] = reinterpret_cast<const uint4 *>(src + (size_t)(sy0 + r) * sp)[i];
         }
     } else {
         uint8_t *b = reinterpret_cast<uint8_t *>(rows);
+        const uint32_t mw = divm(sw);
         for (int q = tid; q < nr * sw; q += 256) {
-            const int r = q / sw, i = q - r * sw;
+            const int r = (int)__umulhi((uint32_t)q, mw), i = q - r * sw;
             b[(size_t)r * ndw * 4 + i] = src[(size_t)(sy0 + r) * sp + i];
         }
     }
     __syncthreads();
     const int nq = (L.w + 3) >> 2;
+    const uint32_t mq = divm(nq);
     for (int q = tid; q < (dy1 - dy0) * nq; q += 256) {
-        const int r = q / nq, dx0 = (q - r * nq) * 4, dy = dy0 + r;
+        const int r = (int)__umulhi((uint32_t)q, mq), dx0 = (q - r * nq) * 4, dy = dy0 + r;
         const XTab y = yt[L.ytab_off + dy];
         const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx0 - sy0) * ndw);
         const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx1 - sy0) * ndw);
@@ -1442,7 +1447,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
             const int dy1 = std::min(dy0 + kPyrBlock, L.h);
             nr = std::max(nr, yt[L.ytab_off + dy1 - 1].sx1 - yt[L.ytab_off + dy0].sx0 + 1);
         }
-        o->pyr_lds[l] = sizeof(uint32_t) * (((3 * (size_t)L.w + 3) & ~(size_t)3) + (size_t)nr * ((g.lv[l - 1].w + 3) / 4));
+        o->pyr_lds[l] = sizeof(uint32_t) * (((3 * (size_t)L.w + 3) & ~(size_t)3) + (size_t)nr * (((g.lv[l - 1].w + 15) / 16) * 4));
         if (o->pyr_lds[l] > 160 * 1024) {   // images wider than ~8000 px
             delete o;
             return OMV_ERR_ARG;
