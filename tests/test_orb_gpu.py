@@ -30,6 +30,10 @@ CASES = [
     (720, 540, 500, 15, 7, (200, 400), 20222002),
     (320, 240, 300, 20, 7, (0, 0), 7),
     (400, 300, 400, 20, 7, (50, 90), 8),
+    # odd pitch: byte staging in the FAST cells, the pyramid and the blur (level 0 rows not dword aligned)
+    (333, 250, 300, 20, 7, (0, 0), 9),
+    # level 5 is one 68-px-wide cell column: FAST cells with the per-cell LDS row stride (cells > 65 px)
+    (248, 250, 150, 20, 7, (0, 0), 12),
 ]
 
 
