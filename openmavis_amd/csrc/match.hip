@@ -832,8 +832,8 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
     if (lane == 0) __hip_atomic_store(&sh.prog[w], M, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef OMV_RESOLVE_PROFILE
     if (lane == 0 && frame < 2)
-        printf("resolve frame %d domain %d blocks %d rounds %d ticks(100MHz): block-start+deps %lld rounds-pre %lld visit %lld commit %lld\n",
-               frame, w, nblocks, nrounds, tp[0], tp[1], tp[2], tp[3]);
+        printf("resolve frame %d domain %d blocks %d rounds %d revived %d ticks(100MHz): block-start+deps %lld rounds-pre %lld visit %lld commit %lld\n",
+               frame, w, nblocks, nrounds, sh.nrevived[w], tp[0], tp[1], tp[2], tp[3]);
 #endif
 #undef OMV_TP
     for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
