@@ -724,7 +724,8 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
     int phase = 0x3fffff;   // owner stamp of the current conflict phase (commit phase = phase - 1)
 #ifdef OMV_RESOLVE_PROFILE
     long long tp[5] = {0, 0, 0, 0, 0}, tl = wall_clock64();
-    int nblocks = 0, nrounds = 0;
+    int nblocks = 0, nrounds = 0, nfall = 0;
+    long long tp4 = 0;   // visit ticks of each block's first round
 #define OMV_TP(k) (tp[k] += wall_clock64() - tl, tl = wall_clock64())
 #else
 #define OMV_TP(k) ((void)0)
@@ -758,6 +759,9 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
                 for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
                 v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
             }
+#ifdef OMV_RESOLVE_PROFILE
+            if (start == 0) tp4 += wall_clock64() - tl;
+#endif
             OMV_TP(2);
             const bool obs = active && (cur_flag & kFlagObs);
             const int keyA = (phase << 7) | lane, keyB = ((phase - 1) << 7) | (63 - lane);
@@ -818,6 +822,7 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
             OMV_TP(3);
 #ifdef OMV_RESOLVE_PROFILE
             ++nrounds;
+            nfall += __popcll(__ballot(active && v.fallback));
 #endif
         }
 #ifdef OMV_RESOLVE_PROFILE
@@ -832,8 +837,9 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
     if (lane == 0) __hip_atomic_store(&sh.prog[w], M, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef OMV_RESOLVE_PROFILE
     if (lane == 0 && frame < 2)
-        printf("resolve frame %d domain %d blocks %d rounds %d revived %d ticks(100MHz): block-start+deps %lld rounds-pre %lld visit %lld commit %lld\n",
-               frame, w, nblocks, nrounds, sh.nrevived[w], tp[0], tp[1], tp[2], tp[3]);
+        printf("resolve frame %d domain %d blocks %d rounds %d revived %d rescans %d ticks(100MHz): block-start+deps %lld rounds-pre %lld visit %lld commit %lld\n",
+               frame, w, nblocks, nrounds, sh.nrevived[w], nfall, tp[0], tp[1], tp[2], tp[3]);
+    if (lane == 0 && frame < 2) printf("resolve frame %d domain %d first-round visit ticks %lld\n", frame, w, tp4);
 #endif
 #undef OMV_TP
     for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
