@@ -78,6 +78,7 @@ struct LevelGeom {
     float scale;            // mvScaleFactor[l]
     float size;             // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
     int xtab_off, ytab_off; // resize tables (l >= 1)
+    int xq_off, use_xq;     // quad table (l >= 1; use_xq: every pixel pair's sources fit two dwords)
 };
 
 struct Cell {
@@ -107,6 +108,15 @@ struct XTab {
     int sx0, sx1, coef;   // coef = a0 | (a1 << 16)
 };
 
+// One output quad (dx = 4q .. 4q+3) of a resize row: pixel pair p = j >> 1 reads the two source dwords at dword
+// index a[p] of the staged row; sel[j] is the v_perm selector that lays (src[sx0], src[sx1]) of pixel j out as a
+// u16 pair, cf[j] = (a0, a1) as a u16 pair, so h = v_dot2_u32_u16(perm, cf) = src[sx0] a0 + src[sx1] a1 exactly.
+struct __attribute__((aligned(16))) XQuad {
+    int a[2];
+    uint32_t sel[4], cf[4];
+    int pad[2];
+};
+
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_t *images, size_t img_stride,
                                                      size_t pitch0, const uint8_t *pyr, int img, int l,
@@ -128,7 +138,7 @@ constexpr int kPyrBlock = 16;
 
 __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const uint8_t *images, size_t img_stride,
                                                          size_t pitch0, uint8_t *pyr, const XTab *xt,
-                                                         const XTab *yt, int n_images) {
+                                                         const XTab *yt, const XQuad *xq, int n_images) {
     extern __shared__ __attribute__((aligned(16))) uint32_t pyr_lds[];
     const LevelGeom &L = g.lv[l];
     const int img = blockIdx.y, tid = threadIdx.x;
@@ -137,11 +147,17 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     const uint8_t *src = level_base(g, images, img_stride, pitch0, pyr, img, l - 1, &sp);
     const int sw = g.lv[l - 1].w;
     const int ndw = ((sw + 15) >> 4) << 2;   // LDS row: whole 16-byte groups
-    XTab *xs = reinterpret_cast<XTab *>(pyr_lds);            // [L.w]
-    uint32_t *rows = pyr_lds + ((3 * L.w + 3) & ~3);         // [nr][ndw]
+    const int nq = (L.w + 3) >> 2;
+    XTab *xs = reinterpret_cast<XTab *>(pyr_lds);            // [L.w]  (generic path)
+    XQuad *xqs = reinterpret_cast<XQuad *>(pyr_lds);         // [nq]   (quad path)
+    uint32_t *rows = pyr_lds + 12 * nq;                      // [nr][ndw] (+1 dword of slack)
     const int sy0 = yt[L.ytab_off + dy0].sx0, sy1 = yt[L.ytab_off + dy1 - 1].sx1;
     const int nr = sy1 - sy0 + 1;
-    for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
+    const bool quad = L.use_xq != 0;
+    if (quad)
+        for (int i = tid; i < nq; i += 256) xqs[i] = xq[L.xq_off + i];
+    else
+        for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
     // q / d as __umulhi(q, ceil(2^32 / d)): exact for q < 2^32 / d (q < 2^16 here)
     auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
     if ((sp & 15) == 0 && (((uintptr_t)src) & 15) == 0) {   // 16-byte loads (the groups stay inside the pitch)
@@ -160,25 +176,43 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
         }
     }
     __syncthreads();
-    const int nq = (L.w + 3) >> 2;
     const uint32_t mq = divm(nq);
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     for (int q = tid; q < (dy1 - dy0) * nq; q += 256) {
-        const int r = (int)__umulhi((uint32_t)q, mq), dx0 = (q - r * nq) * 4, dy = dy0 + r;
+        const int r = (int)__umulhi((uint32_t)q, mq), qd = q - r * nq, dx0 = qd * 4, dy = dy0 + r;
         const XTab y = yt[L.ytab_off + dy];
-        const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx0 - sy0) * ndw);
-        const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx1 - sy0) * ndw);
         const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
         uint32_t packed = 0;
+        if (quad) {
+            const XQuad X = xqs[qd];
+            const uint32_t *R0 = rows + (size_t)(y.sx0 - sy0) * ndw, *R1 = rows + (size_t)(y.sx1 - sy0) * ndw;
+            const uint32_t u0[4] = {R0[X.a[0]], R0[X.a[0] + 1], R0[X.a[1]], R0[X.a[1] + 1]};
+            const uint32_t u1[4] = {R1[X.a[0]], R1[X.a[0] + 1], R1[X.a[1]], R1[X.a[1] + 1]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int dx = dx0 + j;
-            if (dx < L.w) {
-                const XTab x = xs[dx];
-                const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
-                const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
-                const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
+            for (int j = 0; j < 4; ++j) {
+                const int pp = 2 * (j >> 1);
+                const u16x2 cf = __builtin_bit_cast(u16x2, X.cf[j]);
+                const int h0 = (int)__builtin_amdgcn_udot2(
+                    __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u0[pp + 1], u0[pp], X.sel[j])), cf, 0u, false);
+                const int h1 = (int)__builtin_amdgcn_udot2(
+                    __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u1[pp + 1], u1[pp], X.sel[j])), cf, 0u, false);
                 const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
                 packed |= (uint32_t)min(v, 255) << (8 * j);
+            }
+        } else {
+            const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx0 - sy0) * ndw);
+            const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx1 - sy0) * ndw);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int dx = dx0 + j;
+                if (dx < L.w) {
+                    const XTab x = xs[dx];
+                    const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
+                    const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
+                    const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
+                    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                    packed |= (uint32_t)min(v, 255) << (8 * j);
+                }
             }
         }
         uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
@@ -1215,6 +1249,7 @@ struct omv_orb {
     // device
     Cell *d_cells = nullptr;
     XTab *d_xt = nullptr, *d_yt = nullptr;
+    XQuad *d_xq = nullptr;
     uint8_t *d_pyr = nullptr, *d_blur = nullptr;
     int *d_cell_cnt = nullptr;
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
@@ -1260,7 +1295,7 @@ static void mark(omv_orb *o, hipStream_t st) {
     o->ev.push_back(e);
 }
 
-static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vector<XTab> &xt, std::vector<XTab> &yt) {
+static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vector<XTab> &xt, std::vector<XTab> &yt, std::vector<XQuad> &xq) {
     const omv_orb_params &p = o->p;
     const int nl = p.nlevels;
     // ORBextractor ctor tables (:362-391): scaleFactor is a double member
@@ -1367,6 +1402,26 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
             }
             for (int dx = xmax; dx < dw; ++dx) row[dx].coef = 2048, row[dx].sx1 = row[dx].sx0;
             xt.insert(xt.end(), row.begin(), row.end());
+            // quad table: each pixel pair's two source bytes within two dwords of its first pixel's sx0
+            L.xq_off = (int)xq.size();
+            L.use_xq = 1;
+            for (int q = 0; q < (dw + 3) / 4; ++q) {
+                XQuad X{};
+                for (int p = 0; p < 2; ++p) X.a[p] = (row[std::min(4 * q + 2 * p, dw - 1)].sx0) >> 2;
+                for (int j = 0; j < 4; ++j) {
+                    const int dx = 4 * q + j;
+                    if (dx >= dw) {
+                        X.sel[j] = 0x0c0c0c0cu, X.cf[j] = 0;
+                        continue;
+                    }
+                    const int base = 4 * X.a[j >> 1], o0 = row[dx].sx0 - base, o1 = row[dx].sx1 - base;
+                    const int a0 = (short)(row[dx].coef & 0xffff), a1 = (short)(row[dx].coef >> 16);
+                    if (o0 < 0 || o0 > 7 || o1 < 0 || o1 > 7 || a0 < 0 || a1 < 0) L.use_xq = 0;
+                    X.sel[j] = (uint32_t)(o0 & 7) | 0x0c00u | ((uint32_t)(o1 & 7) << 16) | 0x0c000000u;
+                    X.cf[j] = (uint32_t)(a0 & 0xffff) | ((uint32_t)(a1 & 0xffff) << 16);
+                }
+                xq.push_back(X);
+            }
             for (int dy = 0; dy < dh; ++dy) {
                 float fy = (float)((dy + 0.5) * sy_scale - 0.5);
                 int sy = (int)std::floor(fy);
@@ -1420,7 +1475,8 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     (void)hipGetDevice(&o->device);
     std::vector<Cell> cells;
     std::vector<XTab> xt, yt;
-    omv_status st = build_geometry(o, cells, xt, yt);
+    std::vector<XQuad> xq;
+    omv_status st = build_geometry(o, cells, xt, yt, xq);
     if (st != OMV_OK) {
         delete o;
         return st;
@@ -1447,7 +1503,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
             const int dy1 = std::min(dy0 + kPyrBlock, L.h);
             nr = std::max(nr, yt[L.ytab_off + dy1 - 1].sx1 - yt[L.ytab_off + dy0].sx0 + 1);
         }
-        o->pyr_lds[l] = sizeof(uint32_t) * (((3 * (size_t)L.w + 3) & ~(size_t)3) + (size_t)nr * (((g.lv[l - 1].w + 15) / 16) * 4));
+        o->pyr_lds[l] = sizeof(uint32_t) * (12 * (size_t)((L.w + 3) / 4) + (size_t)nr * (((g.lv[l - 1].w + 15) / 16) * 4) + 4);
         if (o->pyr_lds[l] > 160 * 1024) {   // images wider than ~8000 px
             delete o;
             return OMV_ERR_ARG;
@@ -1460,6 +1516,8 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     HIP_OK(hipMalloc(&o->d_yt, sizeof(XTab) * std::max<size_t>(1, yt.size())));
     if (!xt.empty()) HIP_OK(hipMemcpy(o->d_xt, xt.data(), sizeof(XTab) * xt.size(), hipMemcpyHostToDevice));
     if (!yt.empty()) HIP_OK(hipMemcpy(o->d_yt, yt.data(), sizeof(XTab) * yt.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&o->d_xq, sizeof(XQuad) * std::max<size_t>(1, xq.size())));
+    if (!xq.empty()) HIP_OK(hipMemcpy(o->d_xq, xq.data(), sizeof(XQuad) * xq.size(), hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&o->d_pyr, std::max<size_t>(256, (size_t)g.pyr_bytes * n)));
     HIP_OK(hipMalloc(&o->d_blur, (size_t)g.blur_bytes * n));
     HIP_OK(hipMalloc(&o->d_cell_cnt, sizeof(int) * g.n_cells * n));
@@ -1494,7 +1552,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
     for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
-    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_pyr, o->d_blur, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_pyr, o->d_blur, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
     for (void *p : ptrs)
@@ -1530,7 +1588,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     // K1: pyramid, level by level
     for (int l = 1; l < g.nlevels; ++l) {
         pyr_resize_kernel<<<dim3((g.lv[l].h + kPyrBlock - 1) / kPyrBlock, n), 256, o->pyr_lds[l], st>>>(
-            g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, n);
+            g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, o->d_xq, n);
     }
     mark(o, st);
     // K2: FAST per cell
