@@ -121,3 +121,13 @@ def test_octree_device_sort_matches_std_sort(oracle, torch_cuda):
         torch.cuda.synchronize()
         got = perm.cpu().numpy()[:n]
         assert np.array_equal(got, want), f"trial {trial} n {n}: first mismatch at {np.argmax(got != want)}"
+
+
+@pytest.mark.parametrize("scale,nlevels", [(1.5, 5), (2.0, 3)])
+def test_extract_other_scale_factors(oracle, scale, nlevels):
+    # other ORBextractor scale factors: the resize tables (and the pyramid's per-quad source windows) change
+    img = synth.synth_image(31, 640, 480)
+    o_mono, o_kps, o_desc = oracle.orb_extract(img, 1000, scale, nlevels, 20, 7, (0, 0))
+    ex = ORBextractor(1000, scale, nlevels, 20, 7)
+    g_mono, g_kps, g_desc = ex(img, None, (0, 0))
+    _compare(o_mono, o_kps, o_desc, g_mono, g_kps, g_desc, f"scale {scale} x {nlevels}")
