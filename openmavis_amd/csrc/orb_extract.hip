@@ -970,7 +970,8 @@ __device__ __forceinline__ void blur_tile(const uint8_t *__restrict__ src, int s
     };
 #pragma unroll
     for (int r = 0; r < kBlurPF; ++r) fetch(r, r);
-    uint32_t win[7][4];
+    uint32_t win[7][4];   // win[k % 7] = P(k - 1) = (h_{k-1}, h_k), the row pair ending at window row k
+    uint32_t hprev[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const int k = r % kBlurPF;
@@ -980,7 +981,7 @@ __device__ __forceinline__ void blur_tile(const uint8_t *__restrict__ src, int s
         // lane 0's left and lane 63's right neighbour dwords lie outside the tile: DPP keeps `old` (= E) there
         const uint32_t Lw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x138, 0xf, 0xf, false);   // wave_shr:1
         const uint32_t Rw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x130, 0xf, 0xf, false);   // wave_shl:1
-        uint32_t *hs = win[r % 7];
+        uint32_t hs[4];
         hs[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 1), G1,
                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 1), G0, 0u, false), false);
         hs[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 2), G1,
@@ -988,12 +989,23 @@ __device__ __forceinline__ void blur_tile(const uint8_t *__restrict__ src, int s
         hs[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 3), G1,
                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 3), G0, 0u, false), false);
         hs[3] = __builtin_amdgcn_udot4(Rw, G1, __builtin_amdgcn_udot4(C, G0, 0u, false), false);
+        // vertical pass on row pairs: P(k) = (h_k, h_{k+1}) as u16 halves (h < 2^16), so an output row is
+        // dot2(P(r-6), (18,34)) + dot2(P(r-4), (48,56)) + dot2(P(r-2), (48,34)) + 18 h_r + 32768, every pair
+        // packed once and used by three output rows
+        uint32_t *pw = win[r % 7];   // P(r-1) = (h_{r-1}, h_r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pw[c] = (hprev[c] & 0xffffu) | (hs[c] << 16), hprev[c] = hs[c];
         if (r >= 6) {
             uint32_t s4[4];
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            const u16x2 W01{18, 34}, W23{48, 56}, W45{48, 34};
 #pragma unroll
-            for (int c = 0; c < 4; ++c)   // u24 operands: v_mul_u32_u24 (full rate) instead of v_mul_lo_u32
-                s4[c] = __umul24(18u, win[(r - 6) % 7][c] + win[r % 7][c]) + __umul24(34u, win[(r - 5) % 7][c] + win[(r - 1) % 7][c]) +
-                        __umul24(48u, win[(r - 4) % 7][c] + win[(r - 2) % 7][c]) + __umul24(56u, win[(r - 3) % 7][c]) + 32768u;
+            for (int c = 0; c < 4; ++c) {
+                uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 5) % 7][c]), W01, 32768u, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 3) % 7][c]), W23, acc, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 1) % 7][c]), W45, acc, false);
+                s4[c] = __umul24(18u, hs[c]) + acc;
+            }
             // byte 2 of each sum is the blurred pixel
             const uint32_t lo = __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u);   // [s0.b2, s1.b2, 0, 0]
             const uint32_t hi = __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);   // [0, 0, s2.b2, s3.b2]
