@@ -58,9 +58,6 @@ constexpr PackedPattern pack_pattern() {
     return p;
 }
 __constant__ PackedPattern c_pattern8 = pack_pattern();
-__constant__ int c_umax[16];
-// intensity-centroid masks per (disc row v + 15, dword k): x = in-disc byte mask, y = byte weights u + 15
-__constant__ uint2 c_icmask[31 * 8];
 __constant__ int c_gauss7[7] = {18, 34, 48, 56, 48, 34, 18};
 
 struct LevelGeom {
@@ -99,6 +96,7 @@ struct Geom {
     int ccnt_cap;           // octree child-count region (>= 4 node_cap; also holds the level's cell scan)
     // blurred pyramid (K4): level 0 at pitch blur_pitch0, levels >= 1 at the pyramid's offsets/pitches
     int blur_pitch0;
+    unsigned long long umax_pk;          // IC_Angle's umax[0..15], 4 bits each (the disc half-widths)
     long long blur0_bytes, blur_bytes;   // level-0 block, whole per-image block
     int blur_tile_off[kMaxLevels + 1];   // first K4 tile of each level within an image (last = tiles/image)
     LevelGeom lv[kMaxLevels];
@@ -1156,9 +1154,15 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         const uint32_t q5 = al[4];
         const uint32_t qq[5] = {q4.x, q4.y, q4.z, q4.w, q5};
         if (lane < 62) {
+            // the disc row's bytes: u = 4 kd + b - 15 with |u| <= umax[|vr - 15|] (u <= 15 then holds too), the
+            // row-sum mask (1 per byte) and the weights u + 15, formed instead of loaded
+            const int um = (int)((g.umax_pk >> (4 * (vr < 15 ? 15 - vr : vr - 15))) & 15ull);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint2 mk = c_icmask[vr * 8 + 4 * h + k];
+                const int kd = 4 * h + k;
+                const int blo = min(max(15 - um - 4 * kd, 0), 4), bhi = min(max(15 + um - 4 * kd, -1), 3);
+                const uint32_t keep = (blo >= 4 ? 0u : (0xffffffffu << (8 * blo))) & (bhi < 0 ? 0u : (0xffffffffu >> (8 * (3 - bhi))));
+                const uint2 mk = make_uint2(0x01010101u & keep, (0x03020100u + 0x04040404u * (uint32_t)kd) & keep);
                 const uint32_t w = __builtin_amdgcn_alignbyte(qq[k + 1], qq[k], sh);
                 const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
                 m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
@@ -1339,6 +1343,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
 
     Geom &g = o->g;
     memset(&g, 0, sizeof(g));
+    for (int v = 0; v < 16; ++v) g.umax_pk |= (unsigned long long)(o->umax[v] & 15) << (4 * v);
     g.nlevels = nl, g.W = o->W, g.H = o->H, g.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
     g.min_th = std::min(std::max(p.min_th_fast, 0), 255);
     long long pyr_off = 0, cand_off = 0;
@@ -1542,21 +1547,6 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     HIP_OK(hipMalloc(&o->d_lap, sizeof(int) * 2 * n));
     HIP_OK(hipMalloc(&o->d_err, sizeof(int)));
     HIP_OK(hipMemset(o->d_err, 0, sizeof(int)));
-    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), o->umax, sizeof(o->umax)));
-    {
-        uint2 icm[31 * 8];
-        for (int vr = 0; vr < 31; ++vr)
-            for (int k = 0; k < 8; ++k) {
-                const int av = vr < 15 ? 15 - vr : vr - 15, um = o->umax[av];
-                uint32_t msk = 0, wu = 0;
-                for (int b = 0; b < 4; ++b) {
-                    const int u = 4 * k + b - 15;
-                    if (u <= 15 && std::abs(u) <= um) msk |= 1u << (8 * b), wu |= (uint32_t)(u + 15) << (8 * b);
-                }
-                icm[vr * 8 + k] = make_uint2(msk, wu);
-            }
-        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icm, sizeof(icm)));
-    }
     *out = o;
     return OMV_OK;
 }
