@@ -189,6 +189,69 @@ def _cpu_frame_job(item):
     return _cpu_frame(imgs, prep, threaded=False)
 
 
+def parity_post_run(checks, groups, rig, cams, Rlr, tlr, sigma2, bf):
+    """Untimed, after the timed steps: the CPU oracle as CHECKER (never the measured path) on frames of the LAST
+    timed step, read back from the measured run's own device buffers (the 3-stream, Bg-frame-per-launch shape).
+    checks: [(group, frame_in_group, images [C,H,W], (pose, world, mp_initial))].  Compares bit for bit:
+    extraction (keypoints as raw bits, descriptors, counts, monoIndex), the lapping pairs after TriangulateMatches
+    (l2r / r2l), mvuRight, isInFrustum's track and SearchByProjection's assignment + count."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
+    U = undist_params(BLOCK_CAM_ID)
+    g = oracle.frame_geom(C, W, H, oracle.orb_tables(NFEAT, SCALE, NLEV)["scale"])
+    bad = []
+    for gi, f, imgs, (pose, world, mp0) in checks:
+        gr = groups[gi]
+        fb = gr["fb"]
+        cap = fb.kp_cap
+        kps = fb.kps[f].cpu().numpy().view(oracle.KP_DTYPE).reshape(C, cap)
+        desc = fb.desc[f].cpu().numpy()
+        n_kp, mono = fb.n_kp[f].cpu().numpy(), fb.mono[f].cpu().numpy()
+        tag = f"group {gi} frame {f}"
+        for c in range(C):
+            om, ok, od = oracle.orb_extract(imgs[c], NFEAT, SCALE, NLEV, INI_TH, MIN_TH, tuple(LAP[c]))
+            n = int(n_kp[c])
+            if not (n == len(ok) and mono[c] == om and np.array_equal(kps[c, :n].view(np.uint32), ok.view(np.uint32))
+                    and np.array_equal(desc[c, :n], od)):
+                bad.append(f"{tag} cam {c}: extraction")
+        q, t = desc[0, mono[0]:n_kp[0]], desc[1, mono[1]:n_kp[1]]
+        i2, d2 = oracle.bf_knn2(q, t)
+        l2r = np.full(cap, -1, np.int32)
+        okm = (i2[:, 1] >= 0) & (d2[:, 0].astype(np.float64) < d2[:, 1].astype(np.float64) * 0.8)
+        for qi in np.nonzero(okm)[0]:
+            l2r[mono[0] + qi] = mono[1] + i2[qi, 0]
+        el2r, er2l, _, _ = oracle.stereo_triangulate(kps[0], n_kp[0], kps[1], n_kp[1], cams[:2], Rlr, tlr, sigma2, l2r)
+        gl2r, gr2l = fb.l2r[f].cpu().numpy(), fb.r2l[f].cpu().numpy()
+        if not (np.array_equal(gl2r[:n_kp[0]], el2r) and np.array_equal(gr2l[:n_kp[1]], er2l)):
+            bad.append(f"{tag}: stereo pairs")
+        dep, gur = gr["depth"][f].cpu().numpy(), gr["uright"][f].cpu().numpy()
+        for c in range(dep.shape[0]):
+            eur, _ = oracle.depth_from_undistorted(kps[c, :n_kp[c]], dep[c], U[c], bf)
+            if not np.array_equal(gur[c, :n_kp[c]].view(np.uint32), eur.view(np.uint32)):
+                bad.append(f"{tag} cam {c}: mvuRight")
+        track, _ = oracle.frustum(rig, pose, world["pos"], world["normal"], world["min_dist"], world["max_dist"], 0.5,
+                                  mp0["view_cos"], mp0["track_depth"])
+        gm = gr["mps"]
+        for k, v in track.items():
+            gv = getattr(gm, k)[f].cpu().numpy()
+            if not np.array_equal(np.ascontiguousarray(gv).view(np.uint8), np.ascontiguousarray(v.astype(gv.dtype)).view(np.uint8)):
+                bad.append(f"{tag}: isInFrustum {k}")
+        exp = np.full(C * cap, -1, np.int32)
+        n = oracle.search_by_projection(g, kps, desc, n_kp, dict(mp0, **track), TH, False, 50.0, NNRATIO,
+                                        _pad(el2r, cap), _pad(er2l, cap), None, exp)
+        if not (n == int(fb.n_matches[f].item()) and np.array_equal(exp, fb.kp_to_mp[f].cpu().numpy())):
+            bad.append(f"{tag}: SearchByProjection")
+    return {"frames": [f"group {gi} frame {f}" for gi, f, _, _ in checks], "bit_exact": not bad, "mismatches": bad,
+            "checked": "extraction, lapping pairs after TriangulateMatches, mvuRight, isInFrustum, SearchByProjection"}
+
+
+def _pad(a, cap):
+    out = np.full(cap, -1, np.int32)
+    out[:len(a)] = a
+    return out
+
+
 def cpu_baseline(frames, best_frames=0):
     """The CPU reference path on this host, timed on a bounded sample of the same workload (the oracle: scalar
     C++ restatement; the reference itself cannot be built here):
@@ -937,6 +1000,11 @@ def main():
                          "group overlap extraction of another)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-timing", type=int, default=1)
+    ap.add_argument("--parity-check", type=int, default=1,
+                    help="untimed oracle check of frames of the last timed step (--parity-frames)")
+    ap.add_argument("--parity-frames", default="0:0,-1:-1",
+                    help="group:frame list ('*' = every group, negative = from the end); default group 0's first "
+                         "frame and the last group's last frame")
     ap.add_argument("--lba-steps", type=int, default=10, help="LocalInertialBA optimize() calls timed (0: skip)")
     ap.add_argument("--lba-warmup", type=int, default=2)
     ap.add_argument("--lba-shard", action="store_true",
@@ -1047,6 +1115,9 @@ def main():
     kp_dtype = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
                          ("octave", "<i4")])
     nkp_h = []
+    parity_frames = []
+    parity_sel = [tuple(x.split(":")) for x in args.parity_frames.split(",")] if args.parity_check else []
+    parity_sel = [(g_, int(f)) for g_, f in parity_sel]
     for gi, gr in enumerate(groups):
         extract(gr)
         torch.cuda.synchronize(dev)
@@ -1058,6 +1129,9 @@ def main():
         nk = fb.n_kp.cpu().numpy()
         nkp_h.append(nk)
         per = [_gen_map((kps_h[f], desc_h[f], nk[f], 7000 + first + gi * Bg + f)) for f in range(Bg)]
+        # the post-run parity check's frames: host copies of their images and maps
+        for f in sorted({f % Bg for g_, f in parity_sel if g_ == "*" or int(g_) % G == gi}):
+            parity_frames.append((gi, f, imgs[(gi * Bg + f) * C:(gi * Bg + f + 1) * C], per[f]))
         gr["poses"] = torch.from_numpy(np.stack([p[0] for p in per])).to(dev)
         gr["world"] = {k: torch.from_numpy(np.stack([p[1][k] for p in per])).to(dev) for k in per[0][1]}
         gr["mps"] = MapPointBatch(**{k: torch.from_numpy(np.stack([p[2][k] for p in per])).to(dev) for k in per[0][2]})
@@ -1132,6 +1206,9 @@ def main():
     dt = job_seconds(time.perf_counter() - t0, dev)   # max over ranks
     assert all(gr["ex"].last_error() == 0 for gr in groups)
     n_matches = int(sum(gr["fb"].n_matches.sum().item() for gr in groups))
+    # untimed: the last timed step's outputs of two frames against the CPU oracle (checker only)
+    parity = parity_post_run(parity_frames, groups, rig, cams_r, Rlr, tlr, sigma2, BF) \
+        if args.parity_check and rank == 0 else None
 
     # per-stage device time per step, summed over the stream groups (groups overlap in time)
     stages = {}
@@ -1276,6 +1353,8 @@ def main():
                          "kernels); kernels: isolated per-launch roofline of each stage",
         "kernels": kernels,
         "matches_last_step": n_matches,
+        "parity_post_run": parity,
+        "parity_checked_frames": len(parity["frames"]) if parity and parity["bit_exact"] else 0,
         "roofline": roof,
         "cpu_baseline": cpu,
         "latency_b1": lat,

@@ -109,6 +109,11 @@ typedef struct omv_frame_geom {
     float min_y, max_y;
     int nlevels;
     float scale_factors[16]; /* Frame::mvScaleFactors                                              */
+    /* GeometricCamera type per camera block (Frame::mpCamera, mpCamera2, ...): OMV_CAM_KB8 (0, the
+     * zero-initialised default) or OMV_CAM_PINHOLE.  The projection searches project with it:
+     * SearchByProjection(F, LastF) block 0 (ORBmatcher.cc:2022, :2134), Fuse / SearchByProjection(KF, Sim3) /
+     * SearchByProjection(F, KF) the job's block (:1536, :1710, :710, :2443). */
+    int cam_model[8];
 } omv_frame_geom;
 
 /* Local map points projected into a frame (the MapPoint fields SearchByProjection reads after
@@ -205,7 +210,8 @@ typedef struct omv_last_frame {    /* device SoA per LastFrame keypoint slot s =
     int S;                         /* slots per last frame (n_cams * last_cap), <= the matcher's max_mps */
 } omv_last_frame;
 
-/* cams: host [n_cams][8] KB8 parameters (block 0 is used for every projection, as the reference);
+/* cams: host [n_cams][8] camera parameters (block 0's, of type geom->cam_model[0], are used for every
+ * projection, as the reference's CurrentFrame.mpCamera);
  * Tcw / Tlw: device [n_frames] current / last block-0 poses; Trl: host, block 1 from block 0;
  * kp_to_mp [frame][n_cams*kp_cap] in/out receives last-frame slots; n_matches [frame] (device). */
 omv_status omv_matcher_search_last_frame(omv_matcher *m, int n_frames, const omv_frame_geom *geom, const omv_kp *kps,
@@ -270,7 +276,8 @@ typedef struct omv_kf_search_params {
     float inv_level_sigma2[16];    /* mvInvLevelSigma2                                               */
     float log_scale_factor;        /* mfLogScaleFactor                                               */
     int n_levels;                  /* mnScaleLevels                                                  */
-    float cams[8][8];              /* KannalaBrandt8 parameters per camera block                     */
+    float cams[8][8];              /* camera parameters per block (KB8 fx fy cx cy k1..k4 / Pinhole fx fy cx cy;
+                                      the type is geom->cam_model[block])                             */
     int check_ori;                 /* OMV_KF_SBP_FRAME: mbCheckOrientation                           */
     const float *mp_angle;         /* device [n_entries]: pKF->mvKeysUn[i].angle per entry (check_ori) */
 } omv_kf_search_params;
@@ -488,10 +495,11 @@ omv_status omv_lba_shard(omv_lba *h, int32_t *n_pts, int32_t *n_mono, int32_t *p
 
 /* ------------------------------------------------------------------------------------------------
  * ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, vector<pair<size_t,size_t>>&, bOnlyStereo,
- * bCoarse) (src/ORBmatcher.cc:1131-1456) for multi-camera keyframes, with
- * KannalaBrandt8::epipolarConstrain / TriangulateMatches / unproject / Triangulate
- * (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429; Eigen::JacobiSVD<Matrix4f>
- * restated).  One workgroup per keyframe pair; pairs are independent (vbMatched2 is never set).
+ * bCoarse) (src/ORBmatcher.cc:1131-1456) for multi-camera keyframes, with pCamera1->epipolarConstrain
+ * dispatched on camera 1's type (:1380-1387): KannalaBrandt8::epipolarConstrain / TriangulateMatches /
+ * unproject / Triangulate (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429;
+ * Eigen::JacobiSVD<Matrix4f> restated; pCamera2's unprojectEig / project by its own type) or
+ * Pinhole::epipolarConstrain (src/CameraModels/Pinhole.cpp:103-132: F12 = K1^-T [t12]x R12 K2^-1).  One workgroup per keyframe pair; pairs are independent (vbMatched2 is never set).
  * ---------------------------------------------------------------------------------------------- */
 #define OMV_TRI_PAIRS 10   /* LL, LR, RL, RR, L-SL, SL-L, SL-SL, R-SR, SR-R, SR-SR (ORBmatcher.cc:1300-1392) */
 
@@ -517,8 +525,9 @@ typedef struct omv_tri_pair {
     int32_t *match12;                   /* device [kf1.n]: vMatches12 (-1 = none); vMatchedPairs = (i, match12[i] >= 0) */
 } omv_tri_pair;
 
-/* cams: host [4][8] KannalaBrandt8 parameters of the rig's L, R, SL, SR cameras (both keyframes share
- * the rig).  n_matches: device [n_pairs] (the return value).  The camera-pair transform of a pair of
+/* cams: host [4][8] parameters of the rig's L, R, SL, SR cameras (both keyframes share the rig):
+ * KannalaBrandt8 fx fy cx cy k1..k4 or Pinhole fx fy cx cy; cam_model: host [4] OMV_CAM_KB8 /
+ * OMV_CAM_PINHOLE per camera, NULL = all KannalaBrandt8.  n_matches: device [n_pairs] (the return value).  The camera-pair transform of a pair of
  * cameras the reference does not list ((L,SR), (SR,L), (R,SL), (SL,R), (SL,SR), (SR,SL)) is whatever the
  * previous candidate of the scan assigned (the reference's R12/t12/pCamera1/pCamera2 persist across
  * iterations); before any assignment it is LL (the reference's R12/t12 are uninitialised there). */
@@ -530,8 +539,8 @@ omv_status omv_tri_debug(const float *cams2, const omv_kp *kp1, const omv_kp *kp
                          const float *svd_in, float sigma, float unc, float *out31);
 
 omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
-                                                const float *cams, int only_stereo, int coarse, int check_ori,
-                                                int32_t *n_matches, void *stream);
+                                                const float *cams, const int32_t *cam_model, int only_stereo,
+                                                int coarse, int check_ori, int32_t *n_matches, void *stream);
 
 /* ------------------------------------------------------------------------------------------------
  * ORBmatcher::SearchByBoW — Hamming matching of the keypoints that share a vocabulary node (DBoW2
@@ -561,6 +570,9 @@ typedef struct omv_bow_job {
  * per view (OMV_ERR_CAPACITY beyond). */
 omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_job *jobs, int mode, float nnratio,
                                      int check_ori, int32_t *n_matches, void *stream);
+/* Diagnostic: the number of keyframe keypoints whose short candidate list ran out during the sequential walk
+ * (the node was rescanned under the current claims), summed over every SearchByBoW call of the process. */
+omv_status omv_matcher_bow_rescans(int64_t *total, int reset);
 
 /* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (src/ORBmatcher.cc:
  * 895-1004): for every level-0 keypoint of F1 in order, Frame::GetFeaturesInArea(vbPrevMatched[i1], windowSize,

@@ -253,9 +253,10 @@ class SearchByProjection {
 
 // ---- Optimizer::LocalInertialBA -----------------------------------------------------------------------------
 // The window as the reference builds its graph: keyframes (each with its body pose, per-camera poses, velocity,
-// biases, bImu, and whether it is fixed), map points, EdgeMono observations and inertial edges in creation
-// order.  flatten() renumbers keyframes optimisable-first (the vertex order of Optimizer.cc:2800-2860) and
-// produces the omv_lba_problem; optimize() runs it and writes the state back into the window unless FAIL.
+// biases, bImu, and whether it is fixed), map points, EdgeMono / EdgeStereo observations and inertial edges in
+// creation order.  flatten() renumbers keyframes optimisable-first (the vertex order of Optimizer.cc:2800-2860) and
+// produces the omv_lba_problem; optimize() runs it and writes keyframes AND points back into the window only when
+// the result is not OMV_LBA_FAIL (the reference returns before any SetWorldPos / SetPose, Optimizer.cc:3317-3321).
 class LocalInertialBAWindow {
   public:
     struct KeyFrame {
@@ -270,15 +271,24 @@ class LocalInertialBAWindow {
         std::vector<float> preint;   // OMV_PREINT_FLOATS
         bool robust;
         float info_scale;
+        // The reference's rule for the i-th of N inertial edges (Optimizer.cc:2972-2981): Huber sqrt(16.92) on
+        // the last edge (the one reaching the first fixed keyframe) or on every edge when bRecInit; the last
+        // edge's information scaled by 1e-2.
+        static Inertial make(int kf1, int kf2, std::vector<float> preint, bool is_last, bool bRecInit) {
+            return Inertial{kf1, kf2, std::move(preint), is_last || bRecInit, is_last ? 1e-2f : 1.0f};
+        }
     };
 
     LocalInertialBAWindow(int n_cams, std::vector<float> cams, std::vector<double> Rcb, std::vector<double> tcb,
-                          std::vector<double> Rbc, std::vector<double> tbc)
+                          std::vector<double> Rbc, std::vector<double> tbc, float bf = 0.f,
+                          std::vector<int32_t> cam_model = {})
         : C_(n_cams), cam_(std::move(cams)), Rcb_(std::move(Rcb)), tcb_(std::move(tcb)), Rbc_(std::move(Rbc)),
-          tbc_(std::move(tbc)) {}
+          tbc_(std::move(tbc)), bf_(bf), model_(std::move(cam_model)) {}
     ~LocalInertialBAWindow() {
         if (h_) (void)omv_lba_destroy(h_);
     }
+    LocalInertialBAWindow(const LocalInertialBAWindow &) = delete;
+    LocalInertialBAWindow &operator=(const LocalInertialBAWindow &) = delete;
 
     int add_keyframe(const KeyFrame &kf) {
         kfs_.push_back(kf);
@@ -289,27 +299,38 @@ class LocalInertialBAWindow {
         depth_.push_back(track_depth);
         return (int)depth_.size() - 1;
     }
+    // EdgeMono (Optimizer.cc:3080-3106): camera `cam` of keyframe `kf` observes point `pt` at (u, v)
     void add_mono(int pt, int kf, int cam, double u, double v, float inv_sigma2) {
         mono_.push_back({pt, kf, cam, u, v, inv_sigma2});
     }
+    // EdgeStereo (Optimizer.cc:3108-3143): a left-camera observation with mvuRight >= 0, obs (kpUn.x, kpUn.y, u_R),
+    // information I3 * invSigma2 (already divided by uncertainty2), Huber sqrt(7.815)
+    void add_stereo(int pt, int kf, double u, double v, double u_right, float inv_sigma2) {
+        stereo_.push_back({pt, kf, u, v, u_right, inv_sigma2});
+    }
     void add_inertial(const Inertial &e) { imu_.push_back(e); }
+    // Drop every keyframe, point and edge (the handle and its capacity are kept for the next window).
+    void clear() { kfs_.clear(), pts_.clear(), depth_.clear(), mono_.clear(), stereo_.clear(), imu_.clear(); }
 
-    // optimizer.optimize(opt_it) of the window (bLarge settings when `large`); returns the result, the window
-    // state updated in place unless status == OMV_LBA_FAIL (the reference's FAIL guard, :3317-3321)
-    omv_lba_result optimize(bool large, std::vector<double> *mono_chi2 = nullptr, std::vector<uint8_t> *outlier = nullptr) {
+    // optimizer.optimize(opt_it) of the window (bLarge settings when `large`); returns the result.  The window
+    // state is updated only when status == OMV_LBA_OK (the reference's FAIL guard, :3317-3321); the per-edge
+    // chi2 / outlier flags (:3282-3311) are reported either way.
+    omv_lba_result optimize(bool large, std::vector<double> *mono_chi2 = nullptr, std::vector<uint8_t> *outlier = nullptr,
+                            std::vector<double> *stereo_chi2 = nullptr, std::vector<uint8_t> *stereo_outlier = nullptr) {
         flatten();
-        if (!h_)
-            check(omv_lba_create((int)kfs_.size(), C_, (int)depth_.size(), (int)mono_.size(), std::max<int>(1, (int)imu_.size()),
-                                 &h_),
-                  "omv_lba_create");
+        ensure_capacity();
         check(omv_lba_set_problem(h_, &p_), "omv_lba_set_problem");
         const omv_lba_opts o{large ? 4 : 10, large ? 1e-2 : 1e0, 10, large ? 1 : 0};
         chi2_.assign(mono_.size(), 0.0), outl_.assign(mono_.size(), 0);
+        schi2_.assign(stereo_.size(), 0.0), soutl_.assign(stereo_.size(), 0);
         omv_lba_result r{};
         r.mono_chi2 = chi2_.data(), r.mono_outlier = outl_.data();
+        r.stereo_chi2 = schi2_.data(), r.stereo_outlier = soutl_.data();
         check(omv_lba_optimize(h_, &o, &p_, &r), "omv_lba_optimize");
         if (mono_chi2) *mono_chi2 = chi2_;
         if (outlier) *outlier = outl_;
+        if (stereo_chi2) *stereo_chi2 = schi2_;
+        if (stereo_outlier) *stereo_outlier = soutl_;
         if (r.status == OMV_LBA_OK) write_back();
         return r;
     }
@@ -322,6 +343,22 @@ class LocalInertialBAWindow {
         double u, v;
         float w;
     };
+    struct Stereo {
+        int pt, kf;
+        double u, v, ur;
+        float w;
+    };
+    // (Re)create the handle when this window exceeds the capacity it was created with (sliding windows vary)
+    void ensure_capacity() {
+        const int need[5] = {(int)kfs_.size(), C_, (int)depth_.size(), (int)(mono_.size() + stereo_.size()),
+                             std::max<int>(1, (int)imu_.size())};
+        bool fits = h_ != nullptr;
+        for (int i = 0; i < 5 && fits; ++i) fits = need[i] <= cap_[i];
+        if (fits) return;
+        if (h_) (void)omv_lba_destroy(h_), h_ = nullptr;
+        for (int i = 0; i < 5; ++i) cap_[i] = std::max(cap_[i], need[i]);
+        check(omv_lba_create(cap_[0], cap_[1], cap_[2], cap_[3], cap_[4], &h_), "omv_lba_create");
+    }
     void flatten() {
         const int K = (int)kfs_.size();
         order_.clear();
@@ -344,10 +381,16 @@ class LocalInertialBAWindow {
             ba_.insert(ba_.end(), f.ba.begin(), f.ba.end());
             kimu_.push_back(f.imu ? 1 : 0);
         }
+        ptsw_ = pts_;   // the solver's copy: pts_ changes only on write_back
         mpt_.clear(), mkf_.clear(), mcam_.clear(), mobs_.clear(), mw_.clear();
         for (const Mono &m : mono_) {
             mpt_.push_back(m.pt), mkf_.push_back(vid[m.kf]), mcam_.push_back(m.cam);
             mobs_.push_back(m.u), mobs_.push_back(m.v), mw_.push_back(m.w);
+        }
+        spt_.clear(), skf_.clear(), sobs_.clear(), sw_.clear();
+        for (const Stereo &e : stereo_) {
+            spt_.push_back(e.pt), skf_.push_back(vid[e.kf]);
+            sobs_.push_back(e.u), sobs_.push_back(e.v), sobs_.push_back(e.ur), sw_.push_back(e.w);
         }
         ik1_.clear(), ik2_.clear(), pre_.clear(), irob_.clear(), isc_.clear();
         for (const Inertial &e : imu_) {
@@ -360,13 +403,16 @@ class LocalInertialBAWindow {
         p_.n_kf = K, p_.n_opt = n_opt_, p_.kf_imu = kimu_.data();
         p_.Rwb = Rwb_.data(), p_.twb = twb_.data(), p_.Rcw = Rcw_.data(), p_.tcw = tcw_.data();
         p_.vel = vel_.data(), p_.bg = bg_.data(), p_.ba = ba_.data();
-        p_.n_pts = (int)depth_.size(), p_.pts = pts_.data(), p_.pt_track_depth = depth_.data();
+        p_.n_pts = (int)depth_.size(), p_.pts = ptsw_.data(), p_.pt_track_depth = depth_.data();
         p_.n_mono = (int)mono_.size(), p_.mono_pt = mpt_.data(), p_.mono_kf = mkf_.data(), p_.mono_cam = mcam_.data();
         p_.mono_obs = mobs_.data(), p_.mono_inv_sigma2 = mw_.data();
         p_.n_imu = (int)imu_.size(), p_.imu_kf1 = ik1_.data(), p_.imu_kf2 = ik2_.data(), p_.preint = pre_.data();
         p_.imu_robust = irob_.data(), p_.imu_info_scale = isc_.data();
+        p_.n_stereo = (int)stereo_.size(), p_.stereo_pt = spt_.data(), p_.stereo_kf = skf_.data();
+        p_.stereo_obs = sobs_.data(), p_.stereo_inv_sigma2 = sw_.data(), p_.bf = bf_;
+        p_.cam_model = model_.empty() ? nullptr : model_.data();
     }
-    void write_back() {   // vertex estimates back to the keyframes (points were updated in place)
+    void write_back() {   // vertex estimates back to the keyframes and points
         for (int i = 0; i < (int)order_.size(); ++i) {
             KeyFrame &f = kfs_[order_[i]];
             std::memcpy(f.Rwb.data(), &Rwb_[9 * i], 9 * sizeof(double));
@@ -379,25 +425,30 @@ class LocalInertialBAWindow {
             std::memcpy(f.bg.data(), &bg_[3 * i], 3 * sizeof(double));
             std::memcpy(f.ba.data(), &ba_[3 * i], 3 * sizeof(double));
         }
+        pts_ = ptsw_;
     }
 
     int C_;
     std::vector<float> cam_;
     std::vector<double> Rcb_, tcb_, Rbc_, tbc_;
+    float bf_;
+    std::vector<int32_t> model_;
     std::vector<KeyFrame> kfs_;
     std::vector<double> pts_;
     std::vector<float> depth_;
     std::vector<Mono> mono_;
+    std::vector<Stereo> stereo_;
     std::vector<Inertial> imu_;
     // flattened arrays (alive for the problem's lifetime)
     std::vector<int> order_;
     int n_opt_ = 0;
-    std::vector<double> Rwb_, twb_, Rcw_, tcw_, vel_, bg_, ba_, mobs_, chi2_;
-    std::vector<uint8_t> kimu_, irob_, outl_;
-    std::vector<int32_t> mpt_, mkf_, mcam_, ik1_, ik2_;
-    std::vector<float> mw_, pre_, isc_;
+    std::vector<double> Rwb_, twb_, Rcw_, tcw_, vel_, bg_, ba_, ptsw_, mobs_, sobs_, chi2_, schi2_;
+    std::vector<uint8_t> kimu_, irob_, outl_, soutl_;
+    std::vector<int32_t> mpt_, mkf_, mcam_, spt_, skf_, ik1_, ik2_;
+    std::vector<float> mw_, sw_, pre_, isc_;
     omv_lba_problem p_{};
     omv_lba *h_ = nullptr;
+    int cap_[5] = {0, 0, 0, 0, 0};   // max_kf, max_cams, max_pts, max visual edges, max_imu of h_
 };
 
 }  // namespace omv_adapt

@@ -41,7 +41,7 @@ class KeyPoint(ctypes.Structure):
 class FrameGeom(ctypes.Structure):
     _fields_ = [("n_cams", ctypes.c_int), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int),
-                ("scale_factors", ctypes.c_float * 16)]
+                ("scale_factors", ctypes.c_float * 16), ("cam_model", ctypes.c_int * 8)]
 
 
 class MpView(ctypes.Structure):
@@ -257,8 +257,9 @@ SIGNATURES = {
     "omv_tri_debug": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _F, _F, _VP]),
     "omv_matcher_stereo_triangulate": (_I, [_VP, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _VP,
                                             _VP, _VP]),
-    "omv_matcher_search_for_triangulation": (_I, [_VP, _I, ctypes.POINTER(TriPair), _VP, _I, _I, _I, _VP, _VP]),
+    "omv_matcher_search_for_triangulation": (_I, [_VP, _I, ctypes.POINTER(TriPair), _VP, _VP, _I, _I, _I, _VP, _VP]),
     "omv_matcher_search_by_bow": (_I, [_VP, _I, ctypes.POINTER(BowJob), _I, _F, _I, _VP, _VP]),
+    "omv_matcher_bow_rescans": (_I, [ctypes.POINTER(ctypes.c_int64), _I]),
     "omv_matcher_search_for_initialization": (_I, [_VP, _I, _VP, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _VP, _I,
                                                    _F, _I, _VP, _VP, _VP]),
     "omv_pose_create": (_I, [_I, _I, ctypes.POINTER(_VP)]),

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <vector>
 
@@ -35,6 +36,7 @@ namespace {
 constexpr int TH_LOW = 50, kHisto = 30;
 constexpr int kMaxKp = 16384;      // keypoints per view (LDS claim bitmap + rotation bins)
 constexpr uint32_t kNone = 0xffffffffu;
+std::atomic<int64_t> g_bow_rescans{0};   // walk rescans over all SearchByBoW calls (diagnostic)
 
 // rot = angle1 - angle2 (float), +360 if negative, bin = round(rot / 30) with 30 -> 0 (ORBmatcher.cc:475-481)
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
@@ -119,9 +121,12 @@ __global__ void __launch_bounds__(256) bow_cand_kernel(const omv_bow_job *jobs, 
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= K.n) return;
     uint32_t *R = recs + ((size_t)rec_off[blockIdx.y] + q) * kRecWords;
-    const int idx1 = K.node_idx[q];
+    // the FeatureVector lists only the keypoints of non-stopped words (TemplatedVocabulary.h:1157 `if (w > 0)`):
+    // positions past its end carry no search
+    const int n_list = K.n_nodes > 0 ? K.node_start[K.n_nodes] : 0;
+    const int idx1 = q < n_list ? K.node_idx[q] : 0;
     int o0 = -1, o1 = -1;
-    if (K.has_mp[idx1] && !(MODE == OMV_BOW_KF_KF && K.n_left != -1 && idx1 >= K.n)) {
+    if (q < n_list && K.has_mp[idx1] && !(MODE == OMV_BOW_KF_KF && K.n_left != -1 && idx1 >= K.n)) {
         int lo = 0, hi = K.n_nodes - 1;   // the node holding position q: the last a with node_start[a] <= q
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -226,6 +231,7 @@ template <int MODE>
 __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs, const int *rec_off,
                                                          const uint32_t *recs, float nnratio, int check_ori,
                                                          int32_t *n_matches, int *err) {
+    // err[0]: status; err[1]: rescans of the walk (diagnostic, omv_matcher_bow_rescans)
     __shared__ uint32_t claimed[kMaxKp / 32];
     __shared__ uint8_t bins[kMaxKp];
     __shared__ int16_t match[kMaxKp];   // the output, written to memory once at the end (no stores in the walk)
@@ -295,6 +301,7 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
         const bool rescan = lane < NB && found < 2 && total > kTop;
         int bd[NB], bi[NB], bs[NB], bb[NB];
         if (__ballot(rescan)) {
+            if (lane == 0) atomicAdd(err + 1, 1);
             const uint64_t *dq = reinterpret_cast<const uint64_t *>(K.desc + 32 * (size_t)idx1);
             const uint64_t d1[4] = {dq[0], dq[1], dq[2], dq[3]};
             scan_node<MODE, NB>(O, claimed, d1, o0, o1, lane, bd, bi, bs);
@@ -375,8 +382,9 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     if (n_jobs == 0) return OMV_OK;
     for (int i = 0; i < n_jobs; ++i) {
         const omv_bow_job &j = jobs[i];
-        if (!j.match || j.kf.n < 0 || j.other.n < 0 || (j.kf.n_nodes > 0 && (!j.kf.node_id || !j.kf.node_start)) ||
-            (j.other.n_nodes > 0 && (!j.other.node_id || !j.other.node_start)))
+        if (!j.match || j.kf.n < 0 || j.other.n < 0 || j.kf.n_nodes < 0 || j.other.n_nodes < 0 ||
+            (j.kf.n_nodes > 0 && (!j.kf.node_id || !j.kf.node_start || !j.kf.node_idx)) ||
+            (j.other.n_nodes > 0 && (!j.other.node_id || !j.other.node_start || !j.other.node_idx)))
             return OMV_ERR_ARG;
         if (j.kf.n > kMaxKp || j.other.n > kMaxKp) return OMV_ERR_CAPACITY;
     }
@@ -394,7 +402,7 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     uint32_t *d_recs = (uint32_t *)(d_buf + job_bytes + off_bytes + 16);
     HIP_OK(hipMemcpyAsync(d_jobs, jobs, sizeof(omv_bow_job) * n_jobs, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_off, off.data(), sizeof(int) * (n_jobs + 1), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
+    HIP_OK(hipMemsetAsync(d_err, 0, 2 * sizeof(int), st));
     const dim3 cg((max_n + 255) / 256, n_jobs);
     if (mode == OMV_BOW_KF_FRAME) {
         bow_cand_kernel<OMV_BOW_KF_FRAME><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
@@ -406,11 +414,19 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
                                                                 d_err);
     }
     HIP_OK(hipGetLastError());
-    int h_err = 0;
-    HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    int h_err[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(h_err, d_err, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_OK(hipFreeAsync(d_buf, st));
     HIP_OK(hipStreamSynchronize(st));
-    return h_err ? (omv_status)h_err : OMV_OK;
+    g_bow_rescans += h_err[1];
+    return h_err[0] ? (omv_status)h_err[0] : OMV_OK;
+}
+
+omv_status omv_matcher_bow_rescans(int64_t *total, int reset) {
+    if (!total) return OMV_ERR_ARG;
+    *total = g_bow_rescans.load();
+    if (reset) g_bow_rescans = 0;
+    return OMV_OK;
 }
 
 }  // extern "C"

@@ -49,6 +49,7 @@ struct FrameArgs {
     int n_cams, kp_cap, nlevels;
     float min_x, max_x, min_y, max_y, invW, invH;
     float scale[16];
+    int model[8];             // camera type per block (omv_frame_geom::cam_model)
     const omv_kp *kps;        // [frame][cam][kp_cap]
     const uint8_t *desc;      // [frame][cam][kp_cap][32]
     const int *n_kp;          // [frame][cam]
@@ -1132,6 +1133,16 @@ __device__ __forceinline__ void kb8_project_f(const float *k, const float *X, fl
     u = (float)((double)(k[0] * r) * cos((double)psi) + (double)k[2]);
     v = (float)((double)(k[1] * r) * sin((double)psi) + (double)k[3]);
 }
+// GeometricCamera::project(const Eigen::Vector3f&) by the block's camera type: KannalaBrandt8, or
+// Pinhole::project (Pinhole.cpp:26-32: fx * x / z + cx in float, left to right)
+__device__ __forceinline__ void cam_project_f(int model, const float *k, const float *X, float &u, float &v) {
+    if (model == OMV_CAM_PINHOLE) {
+        u = k[0] * X[0] / X[2] + k[2];
+        v = k[1] * X[1] / X[2] + k[3];
+    } else {
+        kb8_project_f(k, X, u, v);
+    }
+}
 
 // Window of last slot s in block c of frame `frame`: false if the point is skipped entirely.
 __device__ bool lf_window(const FrameArgs &f, const LastArgs &L, const LfGeo &G, const omv_se3f &Tcw,
@@ -1144,13 +1155,13 @@ __device__ bool lf_window(const FrameArgs &f, const LastArgs &L, const LfGeo &G,
     const float invzc = (float)(1.0 / (double)x3[2]);
     if (invzc < 0) return false;
     float u, v;
-    kb8_project_f(G.cam0, x3, u, v);
+    cam_project_f(f.model[0], G.cam0, x3, u, v);   // CurrentFrame.mpCamera->project (ORBmatcher.cc:2022)
     if (u < f.min_x || u > f.max_x || v < f.min_y || v > f.max_y) return false;
     x = u, y = v;
     if (c == 1) {
         float xr[3];
         se3_apply(G.Trl, x3, xr);
-        kb8_project_f(G.cam0, xr, x, y);
+        cam_project_f(f.model[0], G.cam0, xr, x, y);   // the same camera on Trl * x3Dc (:2134)
     }
     // bForward / bBackward from tlc = Tlw * twc, twc = -(q^-1 t)
     const omv_se3f inv{{-Tcw.q[0], -Tcw.q[1], -Tcw.q[2], Tcw.q[3]}, {0, 0, 0}};
@@ -1469,7 +1480,7 @@ __global__ void __launch_bounds__(256) kf_cand_kernel(KfArgs a) {
         se3_apply(J.Tcw, P, Pc);
         if (mode != OMV_KF_SBP_FRAME && Pc[2] < 0.0f) break;   // depth must be positive
         float u, v;
-        kb8_project_f(a.cams[cam], Pc, u, v);
+        cam_project_f(a.f.model[cam], a.cams[cam], Pc, u, v);   // pCamera / GetCamera(camId) (:1536, :1710, :2443)
         if (mode == OMV_KF_SBP_FRAME) {   // CurrentFrame.mnMinX .. mnMaxX, inclusive
             if (u < a.f.min_x || u > a.f.max_x || v < a.f.min_y || v > a.f.max_y) break;
         } else if (!(u >= a.f.min_x && u < a.f.max_x && v >= a.f.min_y && v < a.f.max_y)) {   // KeyFrame::IsInImage
@@ -1943,6 +1954,7 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
     f.invW = (float)kGridCols / (g->max_x - g->min_x);   // Frame.cc:1878-1879
     f.invH = (float)kGridRows / (g->max_y - g->min_y);
     for (int l = 0; l < 16; ++l) f.scale[l] = g->scale_factors[l];
+    for (int c = 0; c < 8; ++c) f.model[c] = g->cam_model[c];
     f.kps = kps, f.desc = desc, f.n_kp = n_kp;
     f.cell_start = h->d_cell_start, f.cell_idx = h->d_cell_idx;
 }

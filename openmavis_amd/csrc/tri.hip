@@ -1,7 +1,8 @@
 // MI355X-native ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1131-1456) for multi-camera
-// keyframe pairs, with KannalaBrandt8::epipolarConstrain / TriangulateMatches / unproject / Triangulate
-// (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429) and Eigen's
-// JacobiSVD<Matrix4f> restated in float.
+// keyframe pairs, with the camera models' epipolarConstrain dispatched on camera 1's type (:1380-1387):
+// KannalaBrandt8::epipolarConstrain / TriangulateMatches / unproject / Triangulate
+// (src/CameraModels/KannalaBrandt8.cpp:219-229, 319-395, 96-126, 414-429; Eigen's JacobiSVD<Matrix4f> restated
+// in float) or Pinhole::epipolarConstrain (src/CameraModels/Pinhole.cpp:103-132; Eigen's 3x3 inverse restated).
 //
 // One 256-thread workgroup per keyframe pair (pairs are independent: vbMatched2 is never set, :1204,
 // :1261).  The scan is the reference's: shared FeatureVector nodes in ascending id, for each keypoint idx1
@@ -80,6 +81,68 @@ __device__ void kb8_unproject_f(const float *k, float px, float py, float *ray) 
         scale = omv::glibc_tanf(theta) / theta_d;
     }
     ray[0] = pwx * scale, ray[1] = pwy * scale, ray[2] = 1.f;
+}
+
+// Pinhole::unprojectEig / project(const Eigen::Vector3f&) (Pinhole.cpp:26-32, :40-45): float, left to right
+__device__ __forceinline__ void pinhole_unproject_f(const float *k, float px, float py, float *ray) {
+    ray[0] = (px - k[2]) / k[0], ray[1] = (py - k[3]) / k[1], ray[2] = 1.f;
+}
+__device__ __forceinline__ void pinhole_project_f(const float *k, const float *X, float &u, float &v) {
+    u = k[0] * X[0] / X[2] + k[2];
+    v = k[1] * X[1] / X[2] + k[3];
+}
+// GeometricCamera::unprojectEig / project, dispatched on the camera type (the virtual calls of
+// KannalaBrandt8::TriangulateMatches on pCamera2, KannalaBrandt8.cpp:330, :382)
+__device__ __forceinline__ void cam_unproject_f(int model, const float *k, float px, float py, float *ray) {
+    if (model == OMV_CAM_PINHOLE) pinhole_unproject_f(k, px, py, ray);
+    else kb8_unproject_f(k, px, py, ray);
+}
+__device__ __forceinline__ void cam_project_f(int model, const float *k, const float *X, float &u, float &v) {
+    if (model == OMV_CAM_PINHOLE) pinhole_project_f(k, X, u, v);
+    else kb8_project_f(k, X, u, v);
+}
+
+// Eigen Matrix3f::inverse() (Eigen/src/LU/InverseImpl.h, compute_inverse<..., 3>): the cofactors of column 0,
+// det = their dot product with column 0, result(i, j) = cofactor(j, i) * (1 / det).  Row-major m / r.
+__device__ __forceinline__ float cofactor3(const float *m, int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
+}
+__device__ void eigen_inverse3(const float *m, float *r) {
+    const float c0 = cofactor3(m, 0, 0), c1 = cofactor3(m, 1, 0), c2 = cofactor3(m, 2, 0);
+    const float det = c0 * m[0] + c1 * m[3] + c2 * m[6];
+    const float invdet = 1.f / det;
+    r[0] = c0 * invdet, r[1] = c1 * invdet, r[2] = c2 * invdet;
+    for (int i = 1; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = cofactor3(m, j, i) * invdet;
+}
+// C = A B (3x3 row-major), each entry a left-to-right 3-term sum
+__device__ __forceinline__ void mat3_mul(const float *A, const float *B, float *C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+// Pinhole::epipolarConstrain (Pinhole.cpp:103-132): F12 = K1^-T [t12]x R12 K2^-1 (Eigen's products
+// evaluated left to right), the epipolar line of kp1 in image 2, dsqr = num^2 / den < 3.84 unc (double).
+// K2 = pCamera2->toK_() -- the same fx 0 cx / 0 fy cy / 0 0 1 form for both camera types.
+__device__ bool pinhole_epipolar(const float *k1, const float *k2, const omv_kp &kp1, const omv_kp &kp2,
+                                 const float *R12, const float *t12, float unc) {
+    const float K1t[9] = {k1[0], 0.f, 0.f, 0.f, k1[1], 0.f, k1[2], k1[3], 1.f};   // K1.transpose()
+    const float K2[9] = {k2[0], 0.f, k2[2], 0.f, k2[1], k2[3], 0.f, 0.f, 1.f};
+    const float tx[9] = {0.f, -t12[2], t12[1], t12[2], 0.f, -t12[0], -t12[1], t12[0], 0.f};   // Sophus::SO3f::hat
+    float K1ti[9], K2i[9], A[9], B[9], F[9];
+    eigen_inverse3(K1t, K1ti);
+    eigen_inverse3(K2, K2i);
+    mat3_mul(K1ti, tx, A);
+    mat3_mul(A, R12, B);
+    mat3_mul(B, K2i, F);
+    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
+    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
+    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * (double)unc;
 }
 
 // Eigen::JacobiSVD<Matrix4f>(A, ComputeFullV).matrixV() (row-major A, V): square, no QR preconditioner;
@@ -167,13 +230,14 @@ __device__ void jacobi_svd4_v(const float *A, float *V) {
     }
 }
 
-// KannalaBrandt8::TriangulateMatches (z1 > 0 on success, -1 .. -5 on the reference's rejections)
+// KannalaBrandt8::TriangulateMatches (z1 > 0 on success, -1 .. -5 on the reference's rejections); camera 1 is
+// the KannalaBrandt8 `this`, camera 2 of type model2 (its unprojectEig / project are virtual calls)
 __device__ float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2,
                                      const float *R12, const float *t12, float sigmaLevel, float unc,
-                                     float *p3D = nullptr) {
+                                     float *p3D = nullptr, int model2 = OMV_CAM_KB8) {
     float r1[3], r2[3], r21[3];
     kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
-    kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
+    cam_unproject_f(model2, cam2, kp2.x, kp2.y, r2);
     for (int i = 0; i < 3; ++i) r21[i] = R12[3 * i] * r2[0] + R12[3 * i + 1] * r2[1] + R12[3 * i + 2] * r2[2];
     const float dot = r1[0] * r21[0] + r1[1] * r21[1] + r1[2] * r21[2];
     const float n1 = omv::sqrtf_cr(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
@@ -208,7 +272,7 @@ __device__ float triangulate_matches(const float *cam1, const float *cam2, const
     float x3D2[3];
     for (int i = 0; i < 3; ++i) x3D2[i] = R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2] + t2[i];
     float u2, v2;
-    kb8_project_f(cam2, x3D2, u2, v2);
+    cam_project_f(model2, cam2, x3D2, u2, v2);
     const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
     if ((double)(ex2 * ex2 + ey2 * ey2) > 5.991 * (double)unc) return -5;
     if (p3D) p3D[0] = x3D[0], p3D[1] = x3D[1], p3D[2] = x3D[2];
@@ -240,11 +304,17 @@ __device__ __constant__ int kPairCam2[10] = {0, 1, 0, 1, 2, 0, 2, 3, 1, 3};
 
 struct TriCams {
     float cam[4][8];
+    int model[4];   // OMV_CAM_KB8 / OMV_CAM_PINHOLE per camera (L, R, SL, SR)
 };
 
+// pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, sigma2[kp1.octave], sigma2[kp2.octave]) (ORBmatcher.cc:
+// 1380-1387), a virtual call on camera 1's type
 __device__ bool epipolar_ok(const omv_tri_pair &P, const TriCams &C, int pr, const omv_kp &kp1, const omv_kp &kp2) {
-    return triangulate_matches(C.cam[kPairCam1[pr]], C.cam[kPairCam2[pr]], kp1, kp2, P.T[pr], P.T[pr] + 9,
-                               P.kf1.level_sigma2[kp1.octave], P.kf2.level_sigma2[kp2.octave]) > 0.0001f;
+    const int c1 = kPairCam1[pr], c2 = kPairCam2[pr];
+    if (C.model[c1] == OMV_CAM_PINHOLE)
+        return pinhole_epipolar(C.cam[c1], C.cam[c2], kp1, kp2, P.T[pr], P.T[pr] + 9, P.kf2.level_sigma2[kp2.octave]);
+    return triangulate_matches(C.cam[c1], C.cam[c2], kp1, kp2, P.T[pr], P.T[pr] + 9, P.kf1.level_sigma2[kp1.octave],
+                               P.kf2.level_sigma2[kp2.octave], nullptr, C.model[c2]) > 0.0001f;
 }
 
 // Exclusive block scan (kTriThreads threads, one value each) with associative `op`; `total` = op over all.
@@ -615,16 +685,19 @@ omv_status omv_matcher_stereo_triangulate(omv_matcher *m, int n_frames, int n_ca
 
 
 omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
-                                                const float *cams, int only_stereo, int coarse, int check_ori,
-                                                int32_t *n_matches, void *stream) {
+                                                const float *cams, const int32_t *cam_model, int only_stereo,
+                                                int coarse, int check_ori, int32_t *n_matches, void *stream) {
     if (!m || n_pairs < 0 || (n_pairs > 0 && (!pairs || !cams || !n_matches))) return OMV_ERR_ARG;
     if (n_pairs == 0) return OMV_OK;
     for (int i = 0; i < n_pairs; ++i)
         if (!pairs[i].match12 || pairs[i].kf1.n < 0 || pairs[i].kf2.n < 0) return OMV_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     TriCams C;
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < 4; ++c) {
         for (int q = 0; q < 8; ++q) C.cam[c][q] = cams[8 * c + q];
+        C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
+        if (C.model[c] != OMV_CAM_KB8 && C.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
+    }
     omv_tri_pair *d_pairs = nullptr;
     int *d_err = nullptr;
     HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(omv_tri_pair) * n_pairs + sizeof(int), st));

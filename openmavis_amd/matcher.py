@@ -22,23 +22,26 @@ TH_LOW = 50
 HISTO_LENGTH = 30
 
 
-def frame_geom(n_cams, width, height, scale_factors):
+def frame_geom(n_cams, width, height, scale_factors, cam_model=None):
+    """omv_frame_geom.  cam_model: per camera block "kb8" / "pinhole" (or 0 / 1); default every block KB8."""
     g = _lib.FrameGeom()
     g.n_cams = n_cams
-    g.min_x, g.max_x, g.min_y, g.max_y = 0.0, float(width), 0.0, float(height)   # KB8: no undistortion
+    g.min_x, g.max_x, g.min_y, g.max_y = 0.0, float(width), 0.0, float(height)   # image bounds (no undistortion)
     g.nlevels = len(scale_factors)
     for i, s in enumerate(scale_factors):
         g.scale_factors[i] = float(s)
+    for i, m in enumerate(cam_model if cam_model is not None else ()):
+        g.cam_model[i] = {"kb8": _lib.CAM_KB8, "pinhole": _lib.CAM_PINHOLE}.get(m, m) if isinstance(m, str) else int(m)
     return g
 
 
 class FrameBatch:
     """n_frames multi-camera frames resident on the GPU (torch tensors, padded per camera)."""
 
-    def __init__(self, torch, n_frames, n_cams, kp_cap, width, height, scale_factors, device="cuda"):
+    def __init__(self, torch, n_frames, n_cams, kp_cap, width, height, scale_factors, device="cuda", cam_model=None):
         self.torch = torch
         self.n_frames, self.n_cams, self.kp_cap = n_frames, n_cams, kp_cap
-        self.geom = frame_geom(n_cams, width, height, scale_factors)
+        self.geom = frame_geom(n_cams, width, height, scale_factors, cam_model)
         z = dict(device=device)
         self.kps = torch.zeros((n_frames, n_cams, kp_cap, 6), dtype=torch.int32, **z)
         self.desc = torch.zeros((n_frames, n_cams, kp_cap, 32), dtype=torch.uint8, **z)
@@ -223,14 +226,14 @@ class ORBmatcher:
             _lib.ptr(frames.r2l), _lib.ptr(frames.depth), _lib.ptr(frames.p3d), self._stream(stream)),
             "omv_matcher_stereo_triangulate")
 
-    def SearchForTriangulation(self, pairs, cams, bOnlyStereo=False, bCoarse=False, stream=None):
+    def SearchForTriangulation(self, pairs, cams, bOnlyStereo=False, bCoarse=False, stream=None, cam_model=None):
         """ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1131-1456) for a batch of multi-camera
         keyframe pairs.  pairs: list of dicts {kf1, kf2, T, match12}: kf* hold the omv_kf_view fields
         (n, n_left, n_right, n_sideleft ints; kps / desc / has_mp / node_id / node_start / node_idx device
         tensors; level_sigma2 host floats), T the 10 camera-pair transforms (float [10][12]), match12 a
         device int32 [kf1.n] receiving vMatches12.  cams: host [4][8] KB8 parameters (L, R, SL, SR).
         `pairs` may also be a prebuilt TriPairBatch.  Returns the per-pair match counts (device int32
-        tensor); synchronous."""
+        tensor); synchronous.  cam_model: per camera 0 (KannalaBrandt8) / 1 (Pinhole), default all KB8."""
         import torch
         if self._h is None:
             h = ctypes.c_void_p()
@@ -240,8 +243,9 @@ class ORBmatcher:
         n, arr, dev = batch.n, batch.arr, batch.device
         out = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         c = np.ascontiguousarray(np.asarray(cams, np.float32).reshape(4, 8))
+        cm = None if cam_model is None else np.ascontiguousarray(np.asarray(cam_model, np.int32).reshape(4))
         _lib.check(self._lib.omv_matcher_search_for_triangulation(
-            self._h, n, arr, _lib.ptr(c), int(bool(bOnlyStereo)), int(bool(bCoarse)), int(self.mbCheckOrientation),
+            self._h, n, arr, _lib.ptr(c), _lib.ptr(cm), int(bool(bOnlyStereo)), int(bool(bCoarse)), int(self.mbCheckOrientation),
             _lib.ptr(out), self._stream(stream)), "omv_matcher_search_for_triangulation")
         return out[:n]
 
@@ -268,6 +272,12 @@ class ORBmatcher:
             h, batch.n, batch.arr, _lib.OMV_BOW_KF_KF if kf_kf else _lib.OMV_BOW_KF_FRAME, ctypes.c_float(self.mfNNratio),
             int(self.mbCheckOrientation), _lib.ptr(out), self._stream(stream)), "omv_matcher_search_by_bow")
         return out[:batch.n]
+
+    def bow_rescans(self, reset=True):
+        """Diagnostic: keyframe keypoints whose SearchByBoW short list ran out (node rescanned), all calls."""
+        v = ctypes.c_int64()
+        _lib.check(self._lib.omv_matcher_bow_rescans(ctypes.byref(v), int(bool(reset))), "omv_matcher_bow_rescans")
+        return int(v.value)
 
     def SearchForInitialization(self, frames, pairs, prev_matched, windowSize=100, stream=None, grid_ready=False):
         """ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)

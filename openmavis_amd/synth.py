@@ -231,7 +231,7 @@ def quat_from_R(R):
     return q / np.linalg.norm(q)
 
 
-def make_last_frame(kps, desc, n_kp, seed, cams, Tcw7, frac_valid=0.7, rand_angle=0.2):
+def make_last_frame(kps, desc, n_kp, seed, cams, Tcw7, frac_valid=0.7, rand_angle=0.2, pinhole=False):
     """LastFrame for SearchByProjection(Frame&, const Frame&): the current frame's keypoints as the last
     frame's tracked points (unprojected through block 0's camera at depth U(2, 20) and moved to world
     with Tcw), descriptors with U{0..8} bit flips, `frac_valid` valid, angles perturbed (a `rand_angle`
@@ -243,7 +243,11 @@ def make_last_frame(kps, desc, n_kp, seed, cams, Tcw7, frac_valid=0.7, rand_angl
     ar = np.arange(S)
     exists = (ar % cap) < np.repeat(np.asarray(n_kp), cap)
     valid = exists & (rng.random(S) < frac_valid)
-    ray = kb8_unproject(cams[0], flat["x"], flat["y"])
+    if pinhole:   # Pinhole::unprojectEig of block 0's camera
+        k = np.asarray(cams[0], np.float64)
+        ray = np.stack([(flat["x"] - k[2]) / k[0], (flat["y"] - k[3]) / k[1], np.ones(S)], -1)
+    else:
+        ray = kb8_unproject(cams[0], flat["x"], flat["y"])
     Xc = ray * rng.uniform(2.0, 20.0, S)[:, None]
     q = np.asarray(Tcw7[:4], np.float64)
     t = np.asarray(Tcw7[4:], np.float64)

@@ -28,10 +28,13 @@ def _R_of(q):
 
 
 def make_kf_search(mode, n_kf=3, n_cams=5, kp_cap=600, pts_per_job=300, seed=1, width=720, height=540, nlevels=8,
-                   bf=40.0):
+                   bf=40.0, model="kb8"):
+    """model: "kb8", "pinhole" or one per block: the camera type of each block (omv_frame_geom::cam_model)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     cams = synth.hilti_rig(n_cams)[0]
     C = n_cams
+    models = [model] * C if isinstance(model, str) else list(model)
+    cam_model = np.array([1 if m == "pinhole" else 0 for m in models], np.int32)
     pw = np.float64(1.2) ** (-2.0 * np.arange(nlevels))
     kps = np.zeros((n_kf, C, kp_cap), KP_DTYPE)
     n_kp = rng.integers(int(kp_cap * 0.7), kp_cap + 1, (n_kf, C)).astype(np.int32)
@@ -63,7 +66,11 @@ def make_kf_search(mode, n_kf=3, n_cams=5, kp_cap=600, pts_per_job=300, seed=1, 
             v = np.where(true, src["y"] + rng.normal(0, 0.6, n), rng.uniform(0, height, n))
             octv = np.where(true, src["octave"], rng.integers(0, nlevels, n))
             depth = rng.uniform(2.0, 20.0, n)
-            Xc = synth.kb8_unproject(cams[cam], u, v) * depth[:, None]
+            if cam_model[cam]:   # Pinhole::unprojectEig
+                kc = np.asarray(cams[cam], np.float64)
+                Xc = np.stack([(u - kc[2]) / kc[0], (v - kc[3]) / kc[1], np.ones(n)], -1) * depth[:, None]
+            else:
+                Xc = synth.kb8_unproject(cams[cam], u, v) * depth[:, None]
             Xw = (Xc - t) @ R
             d = Xw - Ow.astype(np.float64)
             dist = np.linalg.norm(d, axis=1)
@@ -114,7 +121,7 @@ def make_kf_search(mode, n_kf=3, n_cams=5, kp_cap=600, pts_per_job=300, seed=1, 
     return dict(mode=mode, n_kf=n_kf, n_cams=C, kp_cap=kp_cap, width=width, height=height, nlevels=nlevels,
                 cams=cams, kps=kps, desc=desc, n_kp=n_kp, uright=uright, bf=np.float32(bf), jobs=jobs,
                 mp_list=np.concatenate(mp_list).astype(np.int32), mp_angle=np.concatenate(mp_angle).astype(np.float32),
-                mps=mps, kp_match=kp_match)
+                mps=mps, kp_match=kp_match, cam_model=cam_model)
 
 
 # reference parameters per mode: (th, max_dist) — Fuse th 3 / TH_LOW; Fuse(Sim3) th 4 / TH_LOW;

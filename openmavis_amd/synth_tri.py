@@ -19,7 +19,11 @@ def _se3_inv(R, t):
 
 
 def make_tri_pair(seed=1, n_pts=500, n_distract=200, n_nodes=100, baseline=(0.2, 0.6), mp_frac=0.3,
-                  cams_used=4):
+                  cams_used=4, model="kb8"):
+    """model: "kb8", "pinhole" (every camera a Pinhole with the Hilti fx fy cx cy: the configs[3] rig type) or a
+    list of 4 per camera ("kb8" / "pinhole", a mixed rig); pair["cam_model"] holds OMV_CAM_* per camera."""
+    models = [model] * 4 if isinstance(model, str) else list(model)
+    pin = [m == "pinhole" for m in models]
     rng = np.random.Generator(np.random.PCG64(seed))
     cams, Rbc, tbc = synth_ba.rig()
     cams, Rbc, tbc = cams[:4].copy(), Rbc[:4], tbc[:4]
@@ -56,7 +60,7 @@ def make_tri_pair(seed=1, n_pts=500, n_distract=200, n_nodes=100, baseline=(0.2,
                 X = Rcw[c] @ pts[p] + tcw[c]
                 if X[2] < 0.3:
                     continue
-                uv = synth_ba.kb8_project(cams[c].astype(np.float64), X)
+                uv = synth_ba.cam_project(cams[c].astype(np.float64), X, pin[c])
                 if not (5 <= uv[0] <= 715 and 5 <= uv[1] <= 535):
                     continue
                 uv = uv + rng.normal(0, 0.5, 2)
@@ -105,7 +109,12 @@ def make_tri_pair(seed=1, n_pts=500, n_distract=200, n_nodes=100, baseline=(0.2,
         T[i, :9] = (R1[c1] @ Rw2).ravel()
         T[i, 9:] = R1[c1] @ tw2 + t1[c1]
     sigma2 = (np.float32(1.2) ** (2 * np.arange(8))).astype(np.float32)
-    return dict(kf1=out[0], kf2=out[1], T=T, cams=cams.astype(np.float32), level_sigma2=sigma2)
+    cams = cams.astype(np.float32)
+    for c in range(4):
+        if pin[c]:
+            cams[c, 4:] = 0.0   # Pinhole: fx fy cx cy only
+    return dict(kf1=out[0], kf2=out[1], T=T, cams=cams, level_sigma2=sigma2,
+                cam_model=np.array([1 if p else 0 for p in pin], np.int32))
 
 
 def kf_struct(kf, struct_cls, sigma2, arr):

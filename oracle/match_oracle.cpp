@@ -40,11 +40,12 @@ struct KP {
     int32_t octave;
 };
 
-struct FrameGeom {
+struct FrameGeom {   // omv_frame_geom
     int n_cams;
     float min_x, max_x, min_y, max_y;
     int nlevels;
     float scale_factors[16];
+    int cam_model[8];   // 0 KannalaBrandt8, 1 Pinhole per camera block
 };
 
 int descriptor_distance(const uint8_t *a, const uint8_t *b) {
@@ -269,6 +270,12 @@ static void se3_apply(const SE3F &T, const float *p, float *r) {
     for (int i = 0; i < 3; ++i) r[i] = r[i] + T.t[i];
 }
 static void kb8_project_f(const float *k, const float *X, float &u, float &v);
+static void pinhole_project_f(const float *k, const float *X, float &u, float &v);
+// GeometricCamera::project(const Eigen::Vector3f&), dispatched on the block's camera type
+static void cam_project_f(int model, const float *k, const float *X, float &u, float &v) {
+    if (model == 1) pinhole_project_f(k, X, u, v);   // OMV_CAM_PINHOLE
+    else kb8_project_f(k, X, u, v);
+}
 
 }  // extern "C"
 
@@ -306,7 +313,7 @@ int oracle_search_last_frame(const FrameGeom *g, const KP *kps, const uint8_t *d
         const float invzc = (float)(1.0 / (double)x3Dc[2]);
         if (invzc < 0) continue;
         float u, vv;
-        kb8_project_f(cams, x3Dc, u, vv);
+        cam_project_f(g->cam_model[0], cams, x3Dc, u, vv);   // CurrentFrame.mpCamera->project (:2022)
         if (u < g->min_x || u > g->max_x) continue;
         if (vv < g->min_y || vv > g->max_y) continue;
         const int oct = last_kps[s].octave;
@@ -343,7 +350,7 @@ int oracle_search_last_frame(const FrameGeom *g, const KP *kps, const uint8_t *d
         if (C > 1) {   // right block: Trl * x3Dc projected with the LEFT camera model, no bounds check
             float x3Dr[3], ur, vr;
             se3_apply(*Trl, x3Dc, x3Dr);
-            kb8_project_f(cams, x3Dr, ur, vr);
+            cam_project_f(g->cam_model[0], cams, x3Dr, ur, vr);   // CurrentFrame.mpCamera->project (:2134)
             search(ur, vr, 1);
         }
         for (int cam = 2; cam < C; ++cam) search(u, vv, cam);   // side blocks search at the LEFT projection
@@ -524,7 +531,7 @@ int oracle_search_kf(const FrameGeom *g, const KP *kps, const uint8_t *desc, int
             se3_apply(T, P, Pc);
             if (mode != OMV_KF_SBP_FRAME && Pc[2] < 0.0f) continue;   // depth must be positive
             float u, vv;
-            kb8_project_f(p->cams[cam], Pc, u, vv);
+            cam_project_f(g->cam_model[cam], p->cams[cam], Pc, u, vv);   // pCamera / GetCamera(camId) (:1536, :1710)
             if (mode == OMV_KF_SBP_FRAME) {   // CurrentFrame.mnMinX .. mnMaxX, inclusive (:2445-2448)
                 if (u < g->min_x || u > g->max_x) continue;
                 if (vv < g->min_y || vv > g->max_y) continue;

@@ -136,15 +136,18 @@ def fast_atan2(y, x):
 class FrameGeom(ctypes.Structure):
     _fields_ = [("n_cams", ctypes.c_int), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int),
-                ("scale_factors", ctypes.c_float * 16)]
+                ("scale_factors", ctypes.c_float * 16), ("cam_model", ctypes.c_int * 8)]
 
 
-def frame_geom(n_cams, width, height, scale_factors):
+def frame_geom(n_cams, width, height, scale_factors, cam_model=None):
+    """omv_frame_geom; cam_model: per block 0 (KannalaBrandt8) / 1 (Pinhole), default all KB8."""
     g = FrameGeom()
     g.n_cams, g.min_x, g.max_x, g.min_y, g.max_y = n_cams, 0.0, float(width), 0.0, float(height)
     g.nlevels = len(scale_factors)
     for i, s in enumerate(scale_factors):
         g.scale_factors[i] = float(s)
+    for i, m in enumerate(cam_model if cam_model is not None else ()):
+        g.cam_model[i] = int(m)
     return g
 
 
@@ -386,9 +389,29 @@ def search_for_triangulation(pair, only_stereo=False, coarse=False, check_ori=Fa
     m12 = np.full(pair["kf1"]["n"], -7, np.int32)
     p.match12 = ctypes.c_void_p(m12.ctypes.data)
     cams = np.ascontiguousarray(pair["cams"], np.float32)
+    cm = pair.get("cam_model")
+    cm = None if cm is None else np.ascontiguousarray(cm, np.int32)
     lib().oracle_search_for_triangulation.restype = ctypes.c_int
-    n = lib().oracle_search_for_triangulation(ctypes.byref(p), _p(cams), int(only_stereo), int(coarse), int(check_ori))
+    n = lib().oracle_search_for_triangulation(ctypes.byref(p), _p(cams), _p(cm), int(only_stereo), int(coarse),
+                                              int(check_ori))
     return n, m12
+
+
+def eigen_inverse3(m):
+    """Eigen Matrix3f::inverse() restated (cofactor formula), float32 [3][3]."""
+    m = np.ascontiguousarray(m, np.float32).reshape(3, 3)
+    r = np.zeros((3, 3), np.float32)
+    lib().oracle_eigen_inverse3(_p(m), _p(r))
+    return r
+
+
+def pinhole_epipolar(k1, k2, kp1, kp2, R12, t12, unc):
+    """Pinhole::epipolarConstrain restated: bool.  kp1 / kp2: one-element KP_DTYPE arrays."""
+    f = lib().oracle_pinhole_epipolar
+    f.restype = ctypes.c_int
+    a = [np.ascontiguousarray(x, np.float32) for x in (k1, k2, R12, t12)]
+    return bool(f(_p(a[0]), _p(a[1]), _p(np.ascontiguousarray(kp1)), _p(np.ascontiguousarray(kp2)), _p(a[2]), _p(a[3]),
+                  ctypes.c_float(unc)))
 
 
 def kb8_unproject(cam, x, y):
@@ -445,6 +468,8 @@ def search_kf(b, th, max_dist, check_ori=True):
     for i in range(b["nlevels"]):
         g.scale_factors[i] = float(s)
         s = np.float32(s * np.float32(1.2))
+    for c, mdl in enumerate(b.get("cam_model", ())):
+        g.cam_model[c] = int(mdl)
     uright = np.ascontiguousarray(b["uright"], np.float32)
     angle = np.ascontiguousarray(b["mp_angle"], np.float32)
     p = kf_search_params(th, max_dist, b["cams"], bf=float(b["bf"]), nlevels=b["nlevels"])

@@ -9,6 +9,13 @@
 //   KannalaBrandt8::unproject / unprojectEig         src/CameraModels/KannalaBrandt8.cpp:96-126, 91-94
 //   KannalaBrandt8::project(const Eigen::Vector3f&)  src/CameraModels/KannalaBrandt8.cpp:48-67
 //   KannalaBrandt8::Triangulate                      src/CameraModels/KannalaBrandt8.cpp:414-429
+//   Pinhole::epipolarConstrain                       src/CameraModels/Pinhole.cpp:103-132
+//   Pinhole::unprojectEig / project(Vector3f)        src/CameraModels/Pinhole.cpp:26-32, :40-45
+//   Eigen::Matrix3f::inverse()                       Eigen/src/LU/InverseImpl.h compute_inverse<.., 3>
+//       (third-party; the cofactor formula: cofactors of column 0, det = their dot with column 0,
+//       result(i, j) = cofactor(j, i) * (1 / det))
+// pCamera1->epipolarConstrain is a virtual call (ORBmatcher.cc:1380-1387): dispatched on camera 1's type;
+// inside KannalaBrandt8::TriangulateMatches pCamera2->unprojectEig / project are camera 2's own.
 //   Eigen::JacobiSVD<Eigen::Matrix4f>(A, ComputeFullV)  Eigen 3.3.5+ / 3.4 two-sided Jacobi SVD
 //       (third-party, not under /root/reference; restated from its published algorithm: square input, so
 //       no QR preconditioner; scale by max|a_ij|; sweeps over (p, q) with threshold
@@ -75,6 +82,64 @@ void kb8_unproject_f(const float *k, float px, float py, float *ray) {
         scale = std::tan(theta) / theta_d;
     }
     ray[0] = pwx * scale, ray[1] = pwy * scale, ray[2] = 1.f;
+}
+
+// Pinhole::unprojectEig / project(const Eigen::Vector3f&): float, left to right
+void pinhole_unproject_f(const float *k, float px, float py, float *ray) {
+    ray[0] = (px - k[2]) / k[0], ray[1] = (py - k[3]) / k[1], ray[2] = 1.f;
+}
+void pinhole_project_f(const float *k, const float *X, float &u, float &v) {
+    u = k[0] * X[0] / X[2] + k[2];
+    v = k[1] * X[1] / X[2] + k[3];
+}
+void cam_unproject_f(int model, const float *k, float px, float py, float *ray) {
+    if (model == OMV_CAM_PINHOLE) pinhole_unproject_f(k, px, py, ray);
+    else kb8_unproject_f(k, px, py, ray);
+}
+void cam_project_f(int model, const float *k, const float *X, float &u, float &v) {
+    if (model == OMV_CAM_PINHOLE) pinhole_project_f(k, X, u, v);
+    else kb8_project_f(k, X, u, v);
+}
+
+// Eigen Matrix3f::inverse() (row-major in / out)
+float cofactor3(const float *m, int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
+}
+void eigen_inverse3(const float *m, float *r) {
+    const float c0 = cofactor3(m, 0, 0), c1 = cofactor3(m, 1, 0), c2 = cofactor3(m, 2, 0);
+    const float det = c0 * m[0] + c1 * m[3] + c2 * m[6];
+    const float invdet = 1.f / det;
+    r[0] = c0 * invdet, r[1] = c1 * invdet, r[2] = c2 * invdet;
+    for (int i = 1; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = cofactor3(m, j, i) * invdet;
+}
+void mat3_mul(const float *A, const float *B, float *C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// Pinhole::epipolarConstrain(pCamera2, kp1, kp2, R12, t12, sigmaLevel, unc): F12 = K1.transpose().inverse() *
+// SO3f::hat(t12) * R12 * K2.inverse(); a b c the epipolar line of kp1; dsqr < 3.84 * unc in double
+bool pinhole_epipolar(const float *k1, const float *k2, const omv_kp &kp1, const omv_kp &kp2, const float *R12,
+                      const float *t12, float unc) {
+    const float K1t[9] = {k1[0], 0.f, 0.f, 0.f, k1[1], 0.f, k1[2], k1[3], 1.f};
+    const float K2[9] = {k2[0], 0.f, k2[2], 0.f, k2[1], k2[3], 0.f, 0.f, 1.f};
+    const float tx[9] = {0.f, -t12[2], t12[1], t12[2], 0.f, -t12[0], -t12[1], t12[0], 0.f};
+    float K1ti[9], K2i[9], A[9], B[9], F[9];
+    eigen_inverse3(K1t, K1ti);
+    eigen_inverse3(K2, K2i);
+    mat3_mul(K1ti, tx, A);
+    mat3_mul(A, R12, B);
+    mat3_mul(B, K2i, F);
+    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
+    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
+    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * unc;
 }
 
 // Eigen::JacobiSVD<Matrix4f>(A, ComputeFullV).matrixV(), A and V row-major.
@@ -161,10 +226,10 @@ void jacobi_svd4_v(const float *A, float *V) {
 
 // KannalaBrandt8::TriangulateMatches (returns z1, or -1 .. -5)
 float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp1, const omv_kp &kp2, const float *R12,
-                          const float *t12, float sigmaLevel, float unc, float *p3D = nullptr) {
+                          const float *t12, float sigmaLevel, float unc, float *p3D = nullptr, int model2 = OMV_CAM_KB8) {
     float r1[3], r2[3], r21[3];
     kb8_unproject_f(cam1, kp1.x, kp1.y, r1);
-    kb8_unproject_f(cam2, kp2.x, kp2.y, r2);
+    cam_unproject_f(model2, cam2, kp2.x, kp2.y, r2);
     for (int i = 0; i < 3; ++i) r21[i] = R12[3 * i] * r2[0] + R12[3 * i + 1] * r2[1] + R12[3 * i + 2] * r2[2];
     const float dot = r1[0] * r21[0] + r1[1] * r21[1] + r1[2] * r21[2];
     const float n1 = sqrtf(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
@@ -199,7 +264,7 @@ float triangulate_matches(const float *cam1, const float *cam2, const omv_kp &kp
     float x3D2[3];
     for (int i = 0; i < 3; ++i) x3D2[i] = R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2] + t2[i];
     float u2, v2;
-    kb8_project_f(cam2, x3D2, u2, v2);
+    cam_project_f(model2, cam2, x3D2, u2, v2);
     const float ex2 = u2 - kp2.x, ey2 = v2 - kp2.y;
     if ((ex2 * ex2 + ey2 * ey2) > 5.991 * unc) return -5;
     if (p3D) p3D[0] = x3D[0], p3D[1] = x3D[1], p3D[2] = x3D[2];
@@ -254,8 +319,8 @@ void three_maxima(const int *cnt, int &ind1, int &ind2, int &ind3) {
 extern "C" {
 
 // One keyframe pair (host pointers in the views); writes match12 [kf1.n]; returns nmatches.
-int oracle_search_for_triangulation(const omv_tri_pair *P, const float *cams, int only_stereo, int coarse,
-                                    int check_ori) {
+int oracle_search_for_triangulation(const omv_tri_pair *P, const float *cams, const int32_t *cam_model,
+                                    int only_stereo, int coarse, int check_ori) {
     const omv_kf_view &K1 = P->kf1, &K2 = P->kf2;
     for (int i = 0; i < K1.n; ++i) P->match12[i] = -1;
     int nmatches = 0;
@@ -284,10 +349,15 @@ int oracle_search_for_triangulation(const omv_tri_pair *P, const float *cams, in
                     if (pr >= 0) state = pr;
                     static const int pc1[10] = {0, 0, 1, 1, 0, 2, 2, 1, 3, 3}, pc2[10] = {0, 1, 0, 1, 2, 0, 2, 3, 1, 3};
                     bool ok = coarse != 0;
-                    if (!ok)
+                    const int m1 = cam_model ? cam_model[pc1[state]] : OMV_CAM_KB8;
+                    const int m2 = cam_model ? cam_model[pc2[state]] : OMV_CAM_KB8;
+                    if (!ok && m1 == OMV_CAM_PINHOLE)   // pCamera1->epipolarConstrain: Pinhole
+                        ok = pinhole_epipolar(cams + 8 * pc1[state], cams + 8 * pc2[state], kp1, kp2, P->T[state],
+                                              P->T[state] + 9, K2.level_sigma2[kp2.octave]);
+                    else if (!ok)                       // KannalaBrandt8: TriangulateMatches(...) > 0.0001
                         ok = triangulate_matches(cams + 8 * pc1[state], cams + 8 * pc2[state], kp1, kp2, P->T[state],
                                                  P->T[state] + 9, K1.level_sigma2[kp1.octave],
-                                                 K2.level_sigma2[kp2.octave]) > 0.0001f;
+                                                 K2.level_sigma2[kp2.octave], nullptr, m2) > 0.0001f;
                     if (ok) bestIdx2 = idx2, bestDist = dist;
                 }
                 if (bestIdx2 >= 0) {
@@ -371,6 +441,11 @@ void oracle_tri_point(const float *cam1, const float *cam2, const omv_kp *kp1, c
 // Parity hooks for the camera-model pieces.
 void oracle_kb8_unproject(const float *cam, float x, float y, float *ray) { kb8_unproject_f(cam, x, y, ray); }
 void oracle_jacobi_svd4_v(const float *A, float *V) { jacobi_svd4_v(A, V); }
+void oracle_eigen_inverse3(const float *m, float *r) { eigen_inverse3(m, r); }
+int oracle_pinhole_epipolar(const float *k1, const float *k2, const omv_kp *kp1, const omv_kp *kp2, const float *R12,
+                            const float *t12, float unc) {
+    return pinhole_epipolar(k1, k2, *kp1, *kp2, R12, t12, unc) ? 1 : 0;
+}
 float oracle_triangulate_matches(const float *cam1, const float *cam2, const omv_kp *kp1, const omv_kp *kp2,
                                  const float *R12, const float *t12, float sigma, float unc) {
     return triangulate_matches(cam1, cam2, *kp1, *kp2, R12, t12, sigma, unc);

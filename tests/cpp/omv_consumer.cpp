@@ -7,7 +7,9 @@
 //   omv_consumer orb   DIR   per image: ORBextractor::operator() (one image per call, host memory)
 //   omv_consumer frame DIR   MultiCameraFrame (batched extraction + grid + lapping knn) + SearchByProjection
 //   omv_consumer lba   DIR   LocalInertialBAWindow: keyframes added in a mixed fixed / optimisable order,
-//                            flattened optimisable-first, optimised, written back
+//                            EdgeMono + EdgeStereo observations, inertial edges under the reference's robust
+//                            rule (last edge / bRecInit), flattened optimisable-first, optimised, written back
+//                            (not on FAIL); optionally a smaller window first on the same adapter
 //
 // DIR/meta.txt holds "key value" lines; arrays are DIR/<name>.bin in the dtype the test wrote.
 #include <cstdio>
@@ -111,9 +113,17 @@ int run_frame(const std::string &dir) {
     return 0;
 }
 
+// optional arrays (absent file: empty)
+template <class T>
+std::vector<T> read_opt(const std::string &dir, const std::string &name) {
+    std::ifstream f(dir + "/" + name + ".bin");
+    return f ? read_bin<T>(dir, name) : std::vector<T>();
+}
+
 int run_lba(const std::string &dir) {
     auto m = read_meta(dir);
     const int C = (int)m["n_cams"], K = (int)m["n_kf"], n_opt = (int)m["n_opt"], P = (int)m["n_pts"];
+    const bool rec_init = m["rec_init"] != 0;
     const auto order = read_bin<int32_t>(dir, "kf_order");   // window insertion order of the original keyframes
     const auto Rwb = read_bin<double>(dir, "Rwb"), twb = read_bin<double>(dir, "twb"), Rcw = read_bin<double>(dir, "Rcw");
     const auto tcw = read_bin<double>(dir, "tcw"), vel = read_bin<double>(dir, "vel"), bg = read_bin<double>(dir, "bg");
@@ -124,35 +134,52 @@ int run_lba(const std::string &dir) {
     const auto mpt = read_bin<int32_t>(dir, "mono_pt"), mkf = read_bin<int32_t>(dir, "mono_kf"), mcam = read_bin<int32_t>(dir, "mono_cam");
     const auto mobs = read_bin<double>(dir, "mono_obs");
     const auto mw = read_bin<float>(dir, "mono_inv_sigma2");
+    const auto spt = read_opt<int32_t>(dir, "stereo_pt"), skf = read_opt<int32_t>(dir, "stereo_kf");
+    const auto sobs = read_opt<double>(dir, "stereo_obs");
+    const auto sw = read_opt<float>(dir, "stereo_inv_sigma2");
     const auto ik1 = read_bin<int32_t>(dir, "imu_kf1"), ik2 = read_bin<int32_t>(dir, "imu_kf2");
     const auto pre = read_bin<float>(dir, "preint");
-    const auto irob = read_bin<uint8_t>(dir, "imu_robust");
-    const auto isc = read_bin<float>(dir, "imu_info_scale");
+    const auto model = read_opt<int32_t>(dir, "cam_model");
     omv_adapt::LocalInertialBAWindow win(C, read_bin<float>(dir, "cam"), read_bin<double>(dir, "Rcb"), read_bin<double>(dir, "tcb"),
-                                         read_bin<double>(dir, "Rbc"), read_bin<double>(dir, "tbc"));
+                                         read_bin<double>(dir, "Rbc"), read_bin<double>(dir, "tbc"), (float)m["bf"], model);
     std::vector<int> slot(K);   // original keyframe -> window index
-    for (int w = 0; w < K; ++w) {
-        const int k = order[w];
-        omv_adapt::LocalInertialBAWindow::KeyFrame f;
-        std::copy_n(&Rwb[9 * k], 9, f.Rwb.begin()), std::copy_n(&twb[3 * k], 3, f.twb.begin());
-        std::copy_n(&vel[3 * k], 3, f.vel.begin()), std::copy_n(&bg[3 * k], 3, f.bg.begin()), std::copy_n(&ba[3 * k], 3, f.ba.begin());
-        f.Rcw.resize(C), f.tcw.resize(C);
-        for (int c = 0; c < C; ++c) {
-            std::copy_n(&Rcw[((size_t)k * C + c) * 9], 9, f.Rcw[c].begin());
-            std::copy_n(&tcw[((size_t)k * C + c) * 3], 3, f.tcw[c].begin());
+    // the window with its first n_pts_use points and their edges (a smaller window first exercises the handle's
+    // re-creation when the next window is larger)
+    auto build = [&](int n_pts_use) {
+        win.clear();
+        for (int w = 0; w < K; ++w) {
+            const int k = order[w];
+            omv_adapt::LocalInertialBAWindow::KeyFrame f;
+            std::copy_n(&Rwb[9 * k], 9, f.Rwb.begin()), std::copy_n(&twb[3 * k], 3, f.twb.begin());
+            std::copy_n(&vel[3 * k], 3, f.vel.begin()), std::copy_n(&bg[3 * k], 3, f.bg.begin()), std::copy_n(&ba[3 * k], 3, f.ba.begin());
+            f.Rcw.resize(C), f.tcw.resize(C);
+            for (int c = 0; c < C; ++c) {
+                std::copy_n(&Rcw[((size_t)k * C + c) * 9], 9, f.Rcw[c].begin());
+                std::copy_n(&tcw[((size_t)k * C + c) * 3], 3, f.tcw[c].begin());
+            }
+            f.imu = kf_imu[k] != 0, f.fixed = k >= n_opt;
+            slot[k] = win.add_keyframe(f);
         }
-        f.imu = kf_imu[k] != 0, f.fixed = k >= n_opt;
-        slot[k] = win.add_keyframe(f);
+        for (int i = 0; i < n_pts_use; ++i) win.add_point({pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}, depth[i]);
+        for (size_t e = 0; e < mpt.size(); ++e)
+            if (mpt[e] < n_pts_use) win.add_mono(mpt[e], slot[mkf[e]], mcam[e], mobs[2 * e], mobs[2 * e + 1], mw[e]);
+        for (size_t e = 0; e < spt.size(); ++e)
+            if (spt[e] < n_pts_use) win.add_stereo(spt[e], slot[skf[e]], sobs[3 * e], sobs[3 * e + 1], sobs[3 * e + 2], sw[e]);
+        const int N = (int)ik1.size();
+        for (int i = 0; i < N; ++i)   // the reference's robust / information rule (Optimizer.cc:2972-2981)
+            win.add_inertial(omv_adapt::LocalInertialBAWindow::Inertial::make(
+                slot[ik1[i]], slot[ik2[i]],
+                std::vector<float>(pre.begin() + (size_t)i * OMV_PREINT_FLOATS, pre.begin() + (size_t)(i + 1) * OMV_PREINT_FLOATS),
+                i == N - 1, rec_init));
+    };
+    if (m["warm_small"] != 0) {
+        build(P / 4);
+        (void)win.optimize(m["large"] != 0);
     }
-    for (int i = 0; i < P; ++i) win.add_point({pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]}, depth[i]);
-    for (size_t e = 0; e < mpt.size(); ++e) win.add_mono(mpt[e], slot[mkf[e]], mcam[e], mobs[2 * e], mobs[2 * e + 1], mw[e]);
-    for (size_t i = 0; i < ik1.size(); ++i)
-        win.add_inertial({slot[ik1[i]], slot[ik2[i]],
-                          std::vector<float>(pre.begin() + i * OMV_PREINT_FLOATS, pre.begin() + (i + 1) * OMV_PREINT_FLOATS),
-                          irob[i] != 0, isc[i]});
-    std::vector<double> chi2;
-    std::vector<uint8_t> outl;
-    const omv_lba_result r = win.optimize(m["large"] != 0, &chi2, &outl);
+    build(P);
+    std::vector<double> chi2, schi2;
+    std::vector<uint8_t> outl, soutl;
+    const omv_lba_result r = win.optimize(m["large"] != 0, &chi2, &outl, &schi2, &soutl);
     // state back in the original keyframe order
     std::vector<double> oRwb(9 * K), otwb(3 * K), oRcw((size_t)9 * K * C), otcw((size_t)3 * K * C), ovel(3 * K), obg(3 * K), oba(3 * K);
     for (int k = 0; k < K; ++k) {
@@ -169,6 +196,7 @@ int run_lba(const std::string &dir) {
     write_bin(dir, "out_tcw", otcw), write_bin(dir, "out_vel", ovel), write_bin(dir, "out_bg", obg), write_bin(dir, "out_ba", oba);
     write_bin(dir, "out_pts", win.points());
     write_bin(dir, "out_chi2", chi2), write_bin(dir, "out_outlier", outl);
+    write_bin(dir, "out_stereo_chi2", schi2), write_bin(dir, "out_stereo_outlier", soutl);
     std::ofstream o(dir + "/result.txt");
     o.precision(17);
     o << "err " << r.err << "\nerr_end " << r.err_end << "\nstatus " << r.status << "\niterations " << r.iterations

@@ -34,6 +34,21 @@ def _host_view(kf, n_left=None, n_sideleft=None):
     return d
 
 
+def _stop_words(kf, seed, frac=0.25):
+    """Drop a fraction of the FeatureVector's nodes, as DBoW2 leaves stopped words (weight 0) out of it
+    (TemplatedVocabulary.h:1157): the CSR then lists fewer than n keypoints (node_start[n_nodes] < n)."""
+    rng = np.random.default_rng(seed)
+    keep = rng.random(len(kf["node_id"])) >= frac
+    starts, idx = kf["node_start"], kf["node_idx"]
+    runs = [idx[starts[a]:starts[a + 1]] for a in range(len(keep)) if keep[a]]
+    out = dict(kf)
+    out["node_id"] = kf["node_id"][keep].copy()
+    out["node_start"] = np.concatenate([[0], np.cumsum([len(r) for r in runs])]).astype(np.int32)
+    out["node_idx"] = (np.concatenate(runs) if runs else np.zeros(0, np.int32)).astype(np.int32)
+    assert out["node_start"][-1] < kf["n"]
+    return out
+
+
 CASES = [  # (kf_kf, check_ori, frame n_left override, frame n_sideleft override)
     (False, True, None, None),     # multi-camera frame, four blocks
     (False, False, None, None),
@@ -66,6 +81,49 @@ def test_search_by_bow_matches_oracle(oracle, kf_kf, check_ori, n_left, n_sidele
         assert n_o == int((m_o >= 0).sum())
         total += n_o
     assert total > 200   # the cases exercise real matching
+
+
+def _run_bow(oracle, pairs, kf_kf, check_ori, nnratio=0.75):
+    import torch
+    jobs, host_jobs = [], []
+    for p in pairs:
+        n_out = p["kf1"]["n"] if kf_kf else p["kf2"]["n"]
+        jobs.append(dict(kf=_dev_view(p["kf1"]), other=_dev_view(p["kf2"]),
+                         match=torch.full((n_out,), -9, dtype=torch.int32, device="cuda")))
+        host_jobs.append(dict(kf=p["kf1"], other=p["kf2"]))
+    m = ORBmatcher(nnratio, check_ori)
+    m.bow_rescans(reset=True)
+    n = m.SearchByBoW(jobs, kf_kf=kf_kf).cpu().numpy()
+    rescans = m.bow_rescans(reset=True)
+    total = 0
+    for i, hj in enumerate(host_jobs):
+        n_o, m_o = oracle.search_by_bow(hj, kf_kf=kf_kf, nnratio=nnratio, check_ori=check_ori)
+        g = jobs[i]["match"].cpu().numpy()
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(g, m_o), (i, np.nonzero(g != m_o)[0][:10])
+        total += n_o
+    return total, rescans
+
+
+@pytest.mark.parametrize("kf_kf", [False, True])
+def test_search_by_bow_stopped_words(oracle, kf_kf):
+    """FeatureVectors that leave keypoints out (stopped words): the walk must end at the list's end."""
+    pairs = []
+    for s in range(1, 7):
+        p = synth_tri.make_tri_pair(seed=20 + s, n_pts=300 + 50 * s, mp_frac=0.7, n_nodes=40 + 10 * s)
+        pairs.append(dict(p, kf1=_stop_words(p["kf1"], 100 + s), kf2=_stop_words(p["kf2"], 200 + s)))
+    total, _ = _run_bow(oracle, pairs, kf_kf, True)
+    assert total > 50
+
+
+@pytest.mark.parametrize("kf_kf", [False, True])
+def test_search_by_bow_crowded_nodes(oracle, kf_kf):
+    """Few vocabulary nodes (30+ candidates per node and camera block, as a real vocabulary at levelsup 4 gives):
+    the short lists overflow and the walk's rescan under the current claims runs; its result stays bit-exact."""
+    pairs = [synth_tri.make_tri_pair(seed=40 + s, n_pts=500 + 50 * s, mp_frac=0.9, n_nodes=5 + s) for s in range(1, 7)]
+    total, rescans = _run_bow(oracle, pairs, kf_kf, True, nnratio=0.9)
+    assert total > 50
+    assert rescans > 0, "the crowded-node case did not exercise the rescan path"
 
 
 def _init_frames(pairs):

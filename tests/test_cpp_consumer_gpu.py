@@ -115,29 +115,71 @@ def test_multicamera_frame_and_search_by_projection(tmp_path, oracle):
     assert np.array_equal(got, exp)
 
 
-def test_local_inertial_ba_window(tmp_path, oracle):
-    from test_lba_gpu import _compare_state, _solver
-    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11)
+LBA_ARRAYS = ("cam", "Rcb", "tcb", "Rbc", "tbc", "kf_imu", "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts",
+              "pt_track_depth", "mono_pt", "mono_kf", "mono_cam", "mono_obs", "mono_inv_sigma2", "imu_kf1", "imu_kf2",
+              "preint")
+STEREO_ARRAYS = ("stereo_pt", "stereo_kf", "stereo_obs", "stereo_inv_sigma2")
+
+
+def _run_lba_window(d, prob, large=True, rec_init=False, warm_small=False):
     K, n_opt = prob["n_kf"], prob["n_opt"]
     # window insertion order: fixed and optimisable keyframes interleaved (relative order kept in each group,
     # so the flattened vertex order equals the problem's)
     fixed, opt = list(range(n_opt, K)), list(range(n_opt))
     order = np.array([x for pair in zip(fixed, opt) for x in pair] + fixed[len(opt):] + opt[len(fixed):], np.int32)
-    _meta(tmp_path, n_cams=prob["n_cams"], n_kf=K, n_opt=n_opt, n_pts=len(prob["pts"]), large=1)
-    _w(tmp_path, "kf_order", order)
-    for k in ("cam", "Rcb", "tcb", "Rbc", "tbc", "kf_imu", "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts",
-              "pt_track_depth", "mono_pt", "mono_kf", "mono_cam", "mono_obs", "mono_inv_sigma2", "imu_kf1", "imu_kf2",
-              "preint", "imu_robust", "imu_info_scale"):
-        _w(tmp_path, k, prob[k])
-    _run("lba", tmp_path)
-    res = dict(line.split() for line in open(os.path.join(tmp_path, "result.txt")))
-    rp, sp = _solver(prob).set_problem(prob).optimize(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    _meta(d, n_cams=prob["n_cams"], n_kf=K, n_opt=n_opt, n_pts=len(prob["pts"]), large=int(large),
+          rec_init=int(rec_init), warm_small=int(warm_small), bf=float(prob.get("bf", 0.0)))
+    _w(d, "kf_order", order)
+    for k in LBA_ARRAYS + (STEREO_ARRAYS if prob.get("n_stereo", 0) else ()) + (("cam_model",) if "cam_model" in prob else ()):
+        _w(d, k, prob[k])
+    _run("lba", d)
+    res = dict(line.split() for line in open(os.path.join(d, "result.txt")))
+    st = {k: _r(d, "out_" + k, np.float64) for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts")}
+    return res, st
+
+
+def _check_against_python(d, prob, res, st, oracle, large=True):
+    from test_lba_gpu import _compare_state, _solver
+    opts = dict(opt_it=4, lambda_init=1e-2, max_trials=10, large=True) if large else \
+        dict(opt_it=10, lambda_init=1e0, max_trials=10, large=False)
+    rp, sp = _solver(prob).set_problem(prob).optimize(**opts)
     assert (int(res["iterations"]), int(res["trials"]), int(res["status"])) == (rp["iterations"], rp["trials"], rp["status"])
     for k in ("err", "err_end"):
         assert abs(float(res[k]) - rp[k]) <= 1e-5 * abs(rp[k]), (k, res[k], rp[k])
-    ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
-    sc = {k: _r(tmp_path, "out_" + k, np.float64).reshape(so[k].shape)
-          for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts")}
-    _compare_state(prob, sc, so, oracle)
-    chi2 = _r(tmp_path, "out_chi2", np.float64)
+    ro, so, _ = oracle.lba_optimize(prob, **opts)
+    _compare_state(prob, {k: v.reshape(so[k].shape) for k, v in st.items()}, so, oracle)
+    chi2 = _r(d, "out_chi2", np.float64)
     assert np.allclose(chi2, rp["mono_chi2"], rtol=1e-6, atol=1e-3)
+    if prob.get("n_stereo", 0):
+        schi2 = _r(d, "out_stereo_chi2", np.float64)
+        assert len(schi2) == prob["n_stereo"]
+        assert np.allclose(schi2, rp["stereo_chi2"], rtol=1e-6, atol=1e-3)
+        assert np.array_equal(_r(d, "out_stereo_outlier", np.uint8), rp["stereo_outlier"])
+
+
+def test_local_inertial_ba_window(tmp_path, oracle):
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11)
+    res, st = _run_lba_window(tmp_path, prob)
+    _check_against_python(tmp_path, prob, res, st, oracle)
+
+
+def test_local_inertial_ba_window_stereo_recinit_regrow(tmp_path, oracle):
+    """EdgeStereo observations through add_stereo (Optimizer.cc:3108-3143), every inertial edge robust under bRecInit
+    (:2972), and a smaller window optimised first on the same adapter (the handle is re-created for the larger one)."""
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=12, stereo_frac=0.5)
+    prob["imu_robust"] = np.ones_like(prob["imu_robust"])   # bRecInit: i == N-1 || bRecInit
+    assert prob["n_stereo"] > 300
+    res, st = _run_lba_window(tmp_path, prob, rec_init=True, warm_small=True)
+    _check_against_python(tmp_path, prob, res, st, oracle)
+
+
+def test_local_inertial_ba_window_fail_keeps_state(tmp_path):
+    """The FAIL guard (Optimizer.cc:3317-3321, !bLarge): a NaN observation makes err NaN, the reference returns
+    before writing anything back -- keyframes AND points keep their input values."""
+    prob = synth_ba.make_lba_problem(n_kf=12, n_opt=6, n_pts=600, seed=13)
+    prob["mono_obs"] = prob["mono_obs"].copy()
+    prob["mono_obs"][5, 0] = np.nan
+    res, st = _run_lba_window(tmp_path, prob, large=False)
+    assert int(res["status"]) == 1   # OMV_LBA_FAIL
+    for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts"):
+        assert np.array_equal(st[k], np.asarray(prob[k], np.float64).ravel()), k

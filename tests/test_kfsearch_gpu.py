@@ -19,7 +19,7 @@ def _run_gpu(b, th, max_dist, check_ori=True):
     scale = [1.0]
     for _ in range(1, b["nlevels"]):
         scale.append(float(np.float32(scale[-1] * np.float32(1.2))))
-    kfs = FrameBatch(torch, K, C, cap, b["width"], b["height"], scale, device=dev)
+    kfs = FrameBatch(torch, K, C, cap, b["width"], b["height"], scale, device=dev, cam_model=b.get("cam_model"))
     kfs.kps.copy_(torch.from_numpy(np.ascontiguousarray(b["kps"]).view(np.int32).reshape(K, C, cap, 6)))
     kfs.desc.copy_(torch.from_numpy(b["desc"]))
     kfs.n_kp.copy_(torch.from_numpy(b["n_kp"]))
@@ -76,3 +76,21 @@ def test_sbp_sim3_crowded_claims_rescan(oracle):
     o = oracle.search_kf(b, 40.0, 200.0)
     for x, y in zip(g, o):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("model", ["pinhole", ["pinhole", "kb8", "pinhole", "kb8", "kb8"]])
+def test_kf_search_pinhole_rig(oracle, mode, model):
+    """Fuse / Fuse(Sim3) / SearchByProjection(KF, Sim3) / SearchByProjection(F, KF) on Pinhole (and mixed) rigs:
+    pCamera / GetCamera(camId) / CurrentFrame.mpCamera->project by the block's type (ORBmatcher.cc:1536, :1710,
+    :710, :2443).  Bit-exact."""
+    b = sk.make_kf_search(mode, seed=7, model=model)
+    th, md = sk.MODE_PARAMS[mode]
+    g = _run_gpu(b, th, md)
+    o = oracle.search_kf(b, th, md)
+    for x, y in zip(g, o):
+        assert np.array_equal(x, y)
+    assert o[2].sum() > 100
+    # the camera type matters: the same data read as KB8 gives other answers
+    okb = oracle.search_kf(dict(b, cam_model=np.zeros_like(b["cam_model"])), th, md)
+    assert not np.array_equal(okb[0], o[0])

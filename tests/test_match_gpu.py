@@ -245,17 +245,23 @@ def test_frustum_then_search_by_projection_matches_oracle(frames, oracle, torch_
     frames.kp_to_mp.fill_(-1)
 
 
-@pytest.mark.parametrize("motion,check_ori", [("none", True), ("forward", True), ("backward", False)])
-def test_search_by_projection_last_frame_matches_oracle(frames, oracle, torch_cuda, motion, check_ori):
+@pytest.mark.parametrize("motion,check_ori,model", [("none", True, "kb8"), ("forward", True, "kb8"),
+                                                   ("backward", False, "kb8"), ("none", True, "pinhole"),
+                                                   ("forward", False, "pinhole")])
+def test_search_by_projection_last_frame_matches_oracle(frames, oracle, torch_cuda, motion, check_ori, model):
     """SearchByProjection(Frame&, const Frame& LastFrame, th, bMono) on device vs the oracle: assignments
-    (last-frame slots), counts, the rotation-histogram removals; forward / backward / neither window."""
+    (last-frame slots), counts, the rotation-histogram removals; forward / backward / neither window.  model
+    "pinhole": CurrentFrame.mpCamera is a Pinhole (configs[3]'s rig type; ORBmatcher.cc:2022, :2134)."""
     torch = torch_cuda
+    pin = model == "pinhole"
+    for c in range(C):
+        frames.geom.cam_model[c] = 1 if pin else 0
     kps, desc, n_kp, _ = host(frames, oracle)
     cams, R_cl, t_cl = synth.hilti_rig(C)
     rng = np.random.default_rng({"none": 1, "forward": 2, "backward": 3}[motion])
     F, cap = frames.n_frames, frames.kp_cap
     Tcw = np.stack([synth.random_se3(rng) for _ in range(F)])
-    lasts = [synth.make_last_frame(kps[f], desc[f], n_kp[f], 90 + f, cams, Tcw[f]) for f in range(F)]
+    lasts = [synth.make_last_frame(kps[f], desc[f], n_kp[f], 90 + f, cams, Tcw[f], pinhole=pin) for f in range(F)]
     # last pose: the current one moved along the optical axis (tlc.z vs mb decides the level window)
     dz = {"none": 0.0, "forward": 0.5, "backward": -0.5}[motion]
     Tlw = Tcw.copy()
@@ -269,11 +275,15 @@ def test_search_by_projection_last_frame_matches_oracle(frames, oracle, torch_cu
     frames.occ_init = torch.from_numpy(occ).cuda()
     frames.kp_to_mp.fill_(-1)
     m = ORBmatcher(0.9, checkOri=check_ori)
-    m.SearchByProjectionLastFrame(frames, last, torch.from_numpy(Tcw).cuda(), torch.from_numpy(Tlw).cuda(), cams, Trl,
-                                  th=7.0, bMono=False, mb=mb)
-    torch.cuda.synchronize()
+    try:
+        m.SearchByProjectionLastFrame(frames, last, torch.from_numpy(Tcw).cuda(), torch.from_numpy(Tlw).cuda(), cams,
+                                      Trl, th=7.0, bMono=False, mb=mb)
+        torch.cuda.synchronize()
+    finally:
+        for c in range(C):
+            frames.geom.cam_model[c] = 0
     got, got_n = frames.kp_to_mp.cpu().numpy(), frames.n_matches.cpu().numpy()
-    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)])
+    g = oracle.frame_geom(C, W, H, [frames.geom.scale_factors[i] for i in range(8)], [1 if pin else 0] * C)
     for f in range(F):
         exp = np.full(C * cap, -1, np.int32)
         n = oracle.search_last_frame(g, kps[f], desc[f], n_kp[f], cams, Tcw[f], Tlw[f], Trl, lasts[f]["pos"],

@@ -67,3 +67,26 @@ def test_search_for_triangulation_shapes(oracle, kw):
         n_o, m_o = oracle.search_for_triangulation(p, check_ori=True)
         assert n[i] == n_o, (i, n[i], n_o)
         assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
+
+
+@pytest.mark.parametrize("model", ["pinhole", ["pinhole", "kb8", "kb8", "pinhole"], ["kb8", "pinhole", "pinhole", "kb8"]])
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_search_for_triangulation_pinhole_rig(oracle, model, check_ori):
+    """configs[3]'s camera type: pCamera1->epipolarConstrain dispatches to Pinhole::epipolarConstrain (F12 = K1^-T
+    [t12]x R12 K2^-1, dsqr < 3.84 sigma2[kp2.octave]; Pinhole.cpp:103-132) -- and on mixed rigs KannalaBrandt8's
+    TriangulateMatches unprojects / projects camera 2 with its own type.  vMatches12 and counts bit-exact."""
+    pairs = [synth_tri.make_tri_pair(seed=60 + s, n_pts=400 + 60 * s, model=model) for s in range(6)]
+    dp = _device_pairs(pairs)
+    m = ORBmatcher(0.6, check_ori)
+    n = m.SearchForTriangulation(dp, pairs[0]["cams"], cam_model=pairs[0]["cam_model"]).cpu().numpy()
+    total = 0
+    for i, p in enumerate(pairs):
+        n_o, m_o = oracle.search_for_triangulation(p, check_ori=check_ori)
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
+        total += n_o
+    assert total > 300
+    # the camera type changes the result (a KB8 run of the same Pinhole data differs)
+    if model == "pinhole":
+        kb = [dict(p, cam_model=None) for p in pairs]
+        assert sum(oracle.search_for_triangulation(p, check_ori=check_ori)[0] for p in kb) != total
