@@ -104,6 +104,15 @@ def host_info():
     """The host the CPU baselines ran on (nproc, lscpu model, sockets, threads)."""
     info = {"nproc": os.cpu_count()}
     try:
+        info["rocm_version"] = open("/opt/rocm/.info/version").read().strip()
+    except OSError:
+        pass
+    try:   # device_count() does not initialise the GPU on this image
+        import torch
+        info["gpu_count"] = torch.cuda.device_count()
+    except Exception:
+        pass
+    try:
         info["usable_cpus"] = len(os.sched_getaffinity(0))
     except AttributeError:
         pass
@@ -121,6 +130,37 @@ def host_info():
     return info
 
 
+NATIVE_LIB = None   # oracle/liboracle_native.so once `make native` built it on this host (timing legs only)
+
+
+def _build_native_oracle():
+    """the CPU baseline is the restatement built -O3 -march=native ON THE TIMED HOST (the
+    container's CPU differs from the GPU box's, so it is never shipped prebuilt).  Falls back to the parity build."""
+    global NATIVE_LIB
+    try:
+        subprocess.run(["make", "-s", f"-j{_cpu_workers()}", "-C", os.path.join(ROOT, "oracle"), "native"],
+                       check=True, timeout=300, capture_output=True)
+        NATIVE_LIB = os.path.join(ROOT, "oracle", "liboracle_native.so")
+    except (OSError, subprocess.SubprocessError):
+        NATIVE_LIB = None
+
+
+def _oracle_build():
+    return "g++ -O3 -march=native, built on this host" if NATIVE_LIB else \
+        "g++ -O3 -march=x86-64-v2 -ffp-contract=off (native build unavailable)"
+
+
+def _oracle(timing):
+    """The oracle module with the timing build (timing=True: CPU baselines) or the parity build (the checker)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    want = NATIVE_LIB if timing and NATIVE_LIB else oracle.LIB
+    if getattr(oracle, "_active_path", None) != want:
+        oracle.use_library(want)
+        oracle._active_path = want
+    return oracle
+
+
 _CPU_CONST = None
 
 
@@ -128,8 +168,7 @@ def _cpu_const():
     """Per-process constants of the CPU pipeline (rig, stereo extrinsics, undistortion, depth images)."""
     global _CPU_CONST
     if _CPU_CONST is None:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
+        oracle = _oracle(timing=True)
         from openmavis_amd import synth
         from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
         from openmavis_amd.matcher import make_rig
@@ -147,8 +186,7 @@ def _cpu_const():
 
 def _cpu_prep(item):
     """Untimed: the 3-D local map of a frame, derived from a first extraction of its own keypoints."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle(timing=True)
     i, imgs = item
     n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH, threaded=False)
     return _gen_map((kps, desc, n_out, 700 + i))
@@ -158,8 +196,7 @@ def _cpu_frame(imgs, prep, threaded):
     """The reference path of one multi-camera frame on the CPU oracle: extraction (one std::thread per camera
     when threaded, like src/Frame.cc:1841-1862), lapping knn + Lowe, TriangulateMatches, mvuRight, isInFrustum,
     SearchByProjection."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle(timing=True)
     k = _cpu_const()
     n_out, mono, kps, desc = oracle.orb_extract_frame(imgs, NFEAT, LAP, SCALE, NLEV, INI_TH, MIN_TH, threaded=threaded)
     cap = kps.shape[1]
@@ -195,8 +232,7 @@ def parity_post_run(checks, groups, rig, cams, Rlr, tlr, sigma2, bf):
     checks: [(group, frame_in_group, images [C,H,W], (pose, world, mp_initial))].  Compares bit for bit:
     extraction (keypoints as raw bits, descriptors, counts, monoIndex), the lapping pairs after TriangulateMatches
     (l2r / r2l), mvuRight, isInFrustum's track and SearchByProjection's assignment + count."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle(timing=False)
     from openmavis_amd.frame import BLOCK_CAM_ID, undist_params
     U = undist_params(BLOCK_CAM_ID)
     g = oracle.frame_geom(C, W, H, oracle.orb_tables(NFEAT, SCALE, NLEV)["scale"])
@@ -252,32 +288,61 @@ def _pad(a, cap):
     return out
 
 
-def cpu_baseline(frames, best_frames=0):
-    """The CPU reference path on this host, timed on a bounded sample of the same workload (the oracle: scalar
-    C++ restatement; the reference itself cannot be built here):
-      mode A, reference-faithful: one std::thread per camera (src/Frame.cc:1841-1862), frames one at a time;
-      mode B, CPU-best: whole frames in parallel over the usable cores (one worker per core, 1 thread each).
-    Runs before anything touches the GPU."""
+def _cpu_frame_timed(item):
+    """Mode-B worker: one frame through the CPU reference path; returns its wall time (s)."""
+    imgs, prep = item
+    t0 = time.perf_counter()
+    _cpu_frame(imgs, prep, threaded=False)
+    return time.perf_counter() - t0
+
+
+def _lat_stats(ts):
+    a = np.asarray(ts) * 1e3
+    return {"median_ms": round(float(np.median(a)), 3), "p95_ms": round(float(np.percentile(a, 95)), 3)}
+
+
+def cpu_baseline(frames, timed_frames=500, warmup_frames=50, best_frames=500):
+    """The CPU reference path on this host, BASELINE.md §2's protocol, timed on the oracle (scalar C++ restatement
+    built -O3 -march=native on this host, `make native`; the reference itself cannot be built here):
+      mode A, reference-faithful: one std::thread per camera (src/Frame.cc:1841-1862), frames one at a time:
+              `warmup_frames` untimed, then `timed_frames` timed one by one (median / p95 per frame);
+      mode B, CPU-best: whole frames in parallel over the worker pool (one process per core of this job's CPU share,
+              1 thread each), `best_frames` frames.
+    The distinct frames (`frames`) are cycled.  Runs before anything touches the GPU."""
     preps = _pool_map(_cpu_prep, list(enumerate(frames)))
     _cpu_const()
-    t0 = time.perf_counter()
-    for imgs, prep in zip(frames, preps):
-        _cpu_frame(imgs, prep, threaded=True)
-    dt = time.perf_counter() - t0
     n = len(frames)
-    out = dict(value=round(n / dt, 3), unit="multi-cam frames/s", cores=C, kind="port",
-               sample=f"{n} Hilti-like frames (5x720x540, 1200 feat/cam, M={M_MPS} map points), oracle C++ "
-                      f"restatement, one thread per camera (mode A, reference-faithful), {dt:.1f} s",
-               host=host_info())
+    for i in range(warmup_frames):
+        _cpu_frame(frames[i % n], preps[i % n], threaded=True)
+    ts = []
+    t0 = time.perf_counter()
+    for i in range(timed_frames):
+        t1 = time.perf_counter()
+        _cpu_frame(frames[i % n], preps[i % n], threaded=True)
+        ts.append(time.perf_counter() - t1)
+    dt = time.perf_counter() - t0
+    out = dict(value=round(timed_frames / dt, 3), unit="multi-cam frames/s", cores=C, kind="port",
+               sample=f"{timed_frames} timed frames ({n} distinct Hilti-like 5x720x540 frames cycled, 1200 feat/cam, "
+                      f"M={M_MPS} map points) after {warmup_frames} warm-up frames; oracle C++ restatement "
+                      f"({_oracle_build()}), one thread per camera (mode A, reference-faithful), {dt:.1f} s",
+               **_lat_stats(ts), host=host_info())
     if best_frames > 0 and _pool() is not None:
         items = [(frames[i % n], preps[i % n]) for i in range(best_frames)]
-        _pool_map(_cpu_frame_job, items[:_cpu_workers()])   # warm every worker (constants, oracle load)
+        _pool_map(_cpu_frame_timed, items[:2 * _cpu_workers()])   # warm every worker (constants, oracle load)
         t0 = time.perf_counter()
-        _pool_map(_cpu_frame_job, items)
+        tb = _pool_map(_cpu_frame_timed, items)
         dt = time.perf_counter() - t0
-        out["mode_b"] = dict(value=round(best_frames / dt, 3), unit="multi-cam frames/s", cores=_cpu_workers(),
-                             kind="port", sample=f"{best_frames} frames, whole frames in parallel over "
-                                                 f"{_cpu_workers()} worker processes (1 thread each), {dt:.1f} s")
+        w = _cpu_workers()
+        hi = host_info()
+        out["mode_b"] = dict(value=round(best_frames / dt, 3), unit="multi-cam frames/s", cores=w, kind="port",
+                             sample=f"{best_frames} frames, whole frames in parallel over {w} worker processes "
+                                    f"(1 thread each: this job's CPU share of the host), {dt:.1f} s", **_lat_stats(tb),
+                             per_core=round(best_frames / dt / w, 3))
+        if hi.get("usable_cpus"):
+            out["mode_b"]["projected_all_usable_cpus"] = dict(
+                value=round(best_frames / dt / w * hi["usable_cpus"], 1), cpus=hi["usable_cpus"],
+                note="per-core rate x usable CPUs (a projection, not measured: the harness gives one GPU job "
+                     f"{w} of the host's CPUs)")
     return out
 
 
@@ -289,19 +354,23 @@ def lba_bytes_per_trial(prob):
     return 2 * E * 40 + 3 * P * 24 + S * (S + 1) // 2 * 8
 
 
-def lba_cpu_baseline(prob, runs=8):
-    """Oracle LocalInertialBA (scalar C++, single thread like g2o with OpenMP off) on the same window."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    trials = 0
+def lba_cpu_baseline(prob, min_trials=200, warmup_trials=10):
+    """Oracle LocalInertialBA (scalar C++, single thread like g2o with OpenMP off) on the same window, BASELINE.md
+    §2: >= `warmup_trials` LM trials untimed, then whole optimize() calls until >= `min_trials` timed trials."""
+    oracle = _oracle(timing=True)
+    w = 0
+    while w < warmup_trials:
+        w += oracle.lba_optimize(prob, **LBA_CFG)[0]["trials"]
+    trials, runs = 0, 0
     t0 = time.perf_counter()
-    for _ in range(runs):
+    while trials < min_trials:
         r, _, _ = oracle.lba_optimize(prob, **LBA_CFG)
         trials += r["trials"]
+        runs += 1
     dt = time.perf_counter() - t0
-    return dict(value=trials / dt, unit="LM trials/s", cores=1, kind="port",
-                sample=f"{runs} LocalInertialBA optimize() calls on the config-5 window ({trials} trials), "
-                       f"oracle C++ restatement, 1 thread, {dt:.1f} s")
+    return dict(value=trials / dt, unit="LM trials/s", cores=1, kind="port", ms_per_trial=round(dt / trials * 1e3, 3),
+                sample=f"{trials} timed LM trials ({runs} LocalInertialBA optimize() calls on the config-5 window) "
+                       f"after {w} warm-up trials, oracle C++ restatement ({_oracle_build()}), 1 thread, {dt:.1f} s")
 
 
 def lba_leg(prob, steps, warmup, dev, world, shard=False):
@@ -412,8 +481,7 @@ def pose_leg(batch, cpu_batch, reps, dev, last_frame=False):
            "unit": "frames/s", "ms_per_batch": round(total / reps * 1e3, 3), "frames_per_batch": F,
            "edges_per_frame": round(len(batch["mono_cam"]) / F, 1), "dtype": "f64"}
     if cpu_batch is not None:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
+        oracle = _oracle(timing=True)
         t0 = time.perf_counter()
         done = 0
         while done == 0 or time.perf_counter() - t0 < 2.0:   # a ~2 s sample
@@ -462,8 +530,7 @@ def tri_leg(pairs, n_pairs, reps, dev):
            "unit": "keyframe pairs/s", "ms_per_batch": round(dt / reps * 1e3, 3), "pairs_per_batch": n_pairs,
            "keypoints_per_keyframe": int(np.mean([p["kf1"]["n"] for p in pairs])),
            "matches_per_pair": round(float(n.float().mean().item()), 1)}
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle(timing=True)
     t0 = time.perf_counter()
     done = 0
     while done == 0 or time.perf_counter() - t0 < 2.0:   # a ~2 s sample
@@ -507,8 +574,7 @@ def aux_legs(dev, cpu):
     from openmavis_amd.imu import Calib, PreintegratedBatch
     from openmavis_amd.matcher import FrameBatch, ORBmatcher, kf_search_params
     if cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
+        oracle = _oracle(timing=True)
     out = {}
     # ---- Fuse: 32 keyframes x 5 blocks, ~660 map points per (keyframe, block)
     b = synth_kfmatch.make_kf_search(0, n_kf=32, kp_cap=1200, pts_per_job=600, seed=11)
@@ -675,15 +741,33 @@ P_W, P_H, P_C, P_NF, P_INI, P_MIN, P_M, P_TH = 1920, 1080, 8, 2000, 20, 7, 8000,
 BYTES_FORMULA = {
     "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image",
     "fast_cells": "sum of level pixels read once, per image",
-    "octree": "8 B x 2,500 candidates, per image",
+    "octree": "4 B per FAST candidate read (its input list) + 8 B per distributed keypoint written",
     "blur": "sum of level pixels read + written, per image",
     "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image",
-    "grid": "28 B per keypoint",
-    "frustum": "per map point 32 B in + 4 B out, per (point, camera) 17 B out",
-    "stereo_knn": "2 x 1,200 descriptors x 32 B per frame",
-    "proj_candidates": "per map point 32 B, per (point, camera) 17 B read + 68 B written",
-    "proj_resolve": "per map point 4 B + per (point, camera) 72 B (record, count, level) read",
+    "grid": "SURVEY 8(d) frame keypoints: 16 B per keypoint",
+    "frustum": "per map point 32 B world data in + per (point, camera) 16 B track out (the SearchByProjection input)",
+    "stereo_knn": "SURVEY 8(d) knn inputs: 2 x 1,200 descriptors x 32 B per frame",
+    "proj_candidates": "SURVEY 8(d) map points 5,000 x (32 + 5 x 16) B + frame descriptors 32 B per keypoint",
+    "proj_resolve": "SURVEY 8(d) outputs: 43,200 B per frame",
 }
+
+
+def per_step_algorithmic_bytes(B, P, n_kp, n_cand):
+    """Algorithmic bytes of one step (B frames) per kernel.  The matching kernels split SURVEY §8(d)'s 968,000 B per
+    frame (frame keypoints 96,000 -> grid, map points 560,000 + frame descriptors 192,000 -> candidates, knn inputs
+    76,800 -> knn, outputs 43,200 -> resolve); the design's own candidate records are not counted."""
+    return {
+        "pyr_resize": B * C * (sum(P[:-1]) + sum(P[1:])),
+        "fast_cells": B * C * sum(P),
+        "octree": 4 * n_cand + 8 * n_kp,
+        "blur": B * C * 2 * sum(P),
+        "describe": B * C * sum(P) + n_kp * 56,
+        "grid": n_kp * 16,
+        "frustum": B * M_MPS * (32 + C * 16),
+        "stereo_knn": B * 2 * 1200 * 32,
+        "proj_candidates": B * M_MPS * (32 + C * 16) + n_kp * 32,
+        "proj_resolve": B * 43_200,
+    }
 
 
 def level_sizes(w, h, nlevels=NLEV, scale=SCALE):
@@ -724,8 +808,7 @@ def _gen_p1080_map(args):
 def p1080_cpu_baseline(frames):
     """Oracle on a bounded sample: extraction of the 8 cameras (one std::thread each), isInFrustum through
     Pinhole::project and SearchByProjection over the 8 blocks."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle(timing=True)
     from openmavis_amd import synth
     from openmavis_amd.matcher import make_rig
     cams, R_cl, t_cl = synth.p1080_rig(P_C, P_W, P_H)
@@ -1010,9 +1093,11 @@ def main():
     ap.add_argument("--lba-shard", action="store_true",
                     help="N>1: shard one window's landmarks over the ranks (RCCL all-reduce per LM trial) "
                          "instead of running a window replica per rank")
-    ap.add_argument("--cpu-frames", type=int, default=60, help="frames in the mode-A CPU sample (~10 s)")
-    ap.add_argument("--cpu-best-frames", type=int, default=64, help="frames in the mode-B (all-core) CPU sample")
-    ap.add_argument("--cpu-lba-runs", type=int, default=40, help="optimize() calls in the CPU BA sample (~6 s)")
+    ap.add_argument("--cpu-frames", type=int, default=500, help="timed frames of the mode-A CPU sample (BASELINE.md §2)")
+    ap.add_argument("--cpu-warmup-frames", type=int, default=50)
+    ap.add_argument("--cpu-distinct-frames", type=int, default=100, help="distinct frames cycled by the CPU samples")
+    ap.add_argument("--cpu-best-frames", type=int, default=500, help="frames in the mode-B (whole CPU share) sample")
+    ap.add_argument("--cpu-lba-trials", type=int, default=200, help="timed LM trials of the CPU BA sample (+10 warm-up)")
     ap.add_argument("--pose-frames", type=int, default=1024, help="frames per PoseInertialOptimization batch (0: skip)")
     ap.add_argument("--tri-pairs", type=int, default=256, help="keyframe pairs per SearchForTriangulation batch (0: skip)")
     ap.add_argument("--aux", type=int, default=1, help="Fuse / DBoW2 transform / IMU preintegration legs (0: skip)")
@@ -1032,6 +1117,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     B = args.frames
     first = rank * B
+    do_cpu = not args.no_cpu_baseline and world == 1
+    if do_cpu:
+        _build_native_oracle()   # before the worker pool forks (the workers inherit NATIVE_LIB)
     # inputs are generated before anything touches the GPU (host pool = plain fork, no HIP yet)
     imgs = np.concatenate(_pool_map(_gen_frame, list(range(first, first + B))))   # [B*C, H, W]
     cpu = p1080_cpu = lba_cpu = None
@@ -1039,7 +1127,6 @@ def main():
     if args.lba_steps > 0:
         from openmavis_amd import synth_ba
         lba_prob = synth_ba.make_lba_problem(seed=5)   # configs[4] window (same on every rank)
-    do_cpu = not args.no_cpu_baseline and world == 1
     p_imgs = None
     if args.p1080_frames > 0:
         PB = args.p1080_frames
@@ -1056,10 +1143,10 @@ def main():
                            _pool_map(_gen_cam_image, [(c, 20_000 + f) for f in range(SB)])]) \
             if rank < C else np.zeros((0, H, W), np.uint8)
     if do_cpu:   # CPU baselines on this host, before the GPU work
-        cpu_frames = _pool_map(_gen_frame, list(range(10_000, 10_000 + args.cpu_frames)))
-        cpu = cpu_baseline(cpu_frames, args.cpu_best_frames)
+        cpu_frames = _pool_map(_gen_frame, list(range(10_000, 10_000 + args.cpu_distinct_frames)))
+        cpu = cpu_baseline(cpu_frames, args.cpu_frames, args.cpu_warmup_frames, args.cpu_best_frames)
         if lba_prob is not None:
-            lba_cpu = lba_cpu_baseline(lba_prob, args.cpu_lba_runs)
+            lba_cpu = lba_cpu_baseline(lba_prob, args.cpu_lba_trials)
     pose_batch = pose_cpu = lf_batch = lf_cpu = None
     if args.pose_frames > 0:
         from openmavis_amd import synth_pose
@@ -1137,6 +1224,7 @@ def main():
         gr["mps"] = MapPointBatch(**{k: torch.from_numpy(np.stack([p[2][k] for p in per])).to(dev) for k in per[0][2]})
         gr["ev"] = []
     nkp_h = np.concatenate(nkp_h)
+    n_cand_step = sum(gr["ex"].last_counts()[0] for gr in groups)   # FAST candidates of one step (octree input)
 
     cams_r, R_cl, t_cl = synth.hilti_rig(C)
     rig = make_rig(cams_r, R_cl, t_cl, W, H, SCALE, NLEV)
@@ -1268,66 +1356,71 @@ def main():
 
     total_frames = B * world * args.steps
     value = total_frames / dt
-    # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes per launch / measured average duration
+    # roofline per kernel: algorithmic bytes per launch (SURVEY §8(d) split over the kernels) / the
+    # kernel's average launch duration, two views: "overlapped" = HIP events on the launch stream during the timed
+    # steps (3 groups overlapping, what rocprof's kernel-trace average of the bench run shows) and "isolated" =
+    # group 0 alone after the timed steps
     P = [a * b for a, b in level_sizes(W, H)]
     n_kp_step = int(nkp_h.sum())   # keypoints per step (same frames every step)
-    per_step_bytes = {
-        # pyramid: level l-1 read, level l written, l = 1..7
-        "pyr_resize": B * C * (sum(P[:-1]) + sum(P[1:])),
-        # FAST: every level read once (the 6-px cell overlap re-reads are not algorithmic)
-        "fast_cells": B * C * sum(P),
-        # octree: candidates are tiny; listed for completeness (latency-bound)
-        "octree": B * C * 8 * 2500,
-        # describe (§8(d)): every level read once (patches overlap; the level is the unit of traffic) + the
-        # 56-B keypoint record / descriptor written per keypoint
-        "describe": B * C * sum(P) + n_kp_step * 56,
-        # GaussianBlur 7x7 of every level: level read, blurred level written
-        "blur": B * C * 2 * sum(P),
-        "grid": n_kp_step * 28,
-        # isInFrustum: per point pos/normal/min/max in, per (point, cam) proj x/y, cos, level, flag out
-        "frustum": B * M_MPS * (32 + C * 17 + 4),
-        "stereo_knn": B * 2 * 1200 * 32,
-        # per point: descriptor 32 B; per (point, camera) slot: projection x / y / cos / level / in-view
-        # 17 B read, the 64-B record + 4-B count written (window candidates' 60 B each not counted)
-        "proj_candidates": B * M_MPS * (32 + C * (17 + 68)),
-        # per point its flag word, per (point, camera) the 64-B record + count + level (upper bound: only the
-        # in-view slots are read)
-        "proj_resolve": B * M_MPS * (4 + C * 72),
-    }
+    per_step_bytes = per_step_algorithmic_bytes(B, P, n_kp_step, n_cand_step)
     roof = None
     kernels = {}
-    if iso:
-        # per stage: isolated duration of one launch (one group of Bg frames) vs its SURVEY 8(d) bytes
-        frames_pl = Bg
-        for k, ms in iso.items():
-            if k not in per_step_bytes or ms <= 0:
-                continue
-            alg = per_step_bytes[k] // G
-            ach = alg / (ms * 1e-3) / 1e9
-            rec = {"avg_launch_ms": round(ms, 4), "launches_per_step": G, "algorithmic_bytes_per_launch": int(alg),
-                   "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None}
-            pmc = os.path.join(ROOT, "profiles", f"pmc_{k}.json")
-            if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch
-                try:
-                    r = json.load(open(pmc))
-                    if "hbm_bytes_per_image" in r:
-                        rec["traffic"] = int(r["hbm_bytes_per_image"] * Bg * C)
-                    elif "hbm_bytes_per_frame" in r:
-                        rec["traffic"] = int(r["hbm_bytes_per_frame"] * Bg)
-                    if rec["traffic"] is not None:
-                        rec["traffic_source"] = f"profiles/pmc_{k}.json ({r['tag']}, program {r.get('program', 'orb')})"
-                except Exception:
-                    pass
-            kernels[k] = rec
-        dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+    ov = {k: v / G for k, v in stages.items()}   # ms per launch in the overlapped timed run
+    for k in per_step_bytes:
+        t_ov, t_iso = ov.get(k, 0.0), iso.get(k, 0.0)
+        if t_ov <= 0 and t_iso <= 0:
+            continue
+        alg = per_step_bytes[k] // G
+        rec = {"algorithmic_bytes_per_launch": int(alg), "launches_per_step": G, "bytes_formula": BYTES_FORMULA[k],
+               "traffic": None}
+        for view, t in (("overlapped", t_ov), ("isolated", t_iso)):
+            if t > 0:
+                ach = alg / (t * 1e-3) / 1e9
+                rec[view] = {"avg_launch_ms": round(t, 4), "ms_per_step": round(t * G, 4), "achieved": round(ach, 2),
+                             "frac": round(ach / HBM_PEAK_GBS, 5)}
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{k}.json")
+        if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch
+            try:
+                r = json.load(open(pmc))
+                if "hbm_bytes_per_image" in r:
+                    rec["traffic"] = int(r["hbm_bytes_per_image"] * Bg * C)
+                elif "hbm_bytes_per_frame" in r:
+                    rec["traffic"] = int(r["hbm_bytes_per_frame"] * Bg)
+                if rec["traffic"] is not None:
+                    rec["traffic_source"] = f"profiles/pmc_{k}.json ({r['tag']}, program {r.get('program', 'orb')})"
+                    rec["traffic_ratio"] = round(rec["traffic"] / alg, 3)
+            except Exception:
+                pass
+        kernels[k] = rec
+    if kernels:
+        view = "overlapped" if any("overlapped" in r for r in kernels.values()) else "isolated"
+        dom = max((k for k in kernels if view in kernels[k]), key=lambda k: kernels[k][view]["ms_per_step"])
         d = kernels[dom]
-        roof = {"kernel": dom, "bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": d["frac"], "traffic": d["traffic"], "avg_launch_ms": d["avg_launch_ms"],
-                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"], "frames_per_launch": frames_pl,
-                "timing": "HIP events on the launch stream, group 0 alone (isolated passes after the timed steps)",
-                "bytes_formula": BYTES_FORMULA[dom]}
+        roof = {"kernel": dom, "bound": "hbm", "achieved": d[view]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d[view]["frac"], "traffic": d["traffic"], "avg_launch_ms": d[view]["avg_launch_ms"],
+                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"], "frames_per_launch": Bg,
+                "timing": ("HIP events on the launch stream over the timed steps (3 stream groups overlapping); dominant = "
+                           "largest ms per step") if view == "overlapped" else
+                          "HIP events on the launch stream, group 0 alone (isolated passes after the timed steps)",
+                "bytes_formula": d["bytes_formula"]}
         if d.get("traffic_source"):
             roof["traffic_source"] = d["traffic_source"]
+        iso_k = [k for k in kernels if "isolated" in kernels[k]]
+        if iso_k:
+            di = max(iso_k, key=lambda k: kernels[k]["isolated"]["avg_launch_ms"])
+            roof["isolated"] = dict(kernel=di, **kernels[di]["isolated"])
+        if dom in iso and "isolated" in d:
+            roof["dominant_isolated_view"] = d["isolated"]
+        # PMC-measured extraction bytes per image vs SURVEY §8(d)'s 2,085,018 B per image
+        ext = ("pyr_resize", "fast_cells", "octree", "blur", "describe")
+        pm = [json.load(open(os.path.join(ROOT, "profiles", f"pmc_{k}.json")))
+              for k in ext if os.path.exists(os.path.join(ROOT, "profiles", f"pmc_{k}.json"))]
+        per_img = sum(r.get("hbm_bytes_per_image", 0) for r in pm)
+        if per_img:
+            ref_img = cam_bytes(W, H, n_kp_step / (B * C))
+            roof["extraction_traffic_ratio"] = round(per_img / ref_img, 3)
+            roof["extraction_traffic_bytes_per_image"] = int(per_img)
+            roof["extraction_algorithmic_bytes_per_image"] = int(ref_img)
         # the whole path: SURVEY §8(d) bytes of a multi-camera frame (5 extractions + matching) x frames/s
         frame_bytes = C * cam_bytes(W, H, 0) + 56 * n_kp_step / B + 968_000
         roof["pipeline"] = {"bytes_per_frame": int(frame_bytes), "achieved": round(frame_bytes * value / 1e9, 2),

@@ -91,6 +91,10 @@ omv_status omv_orb_last_error(omv_orb *orb);
 omv_status omv_orb_enable_timing(omv_orb *orb, int on);
 omv_status omv_orb_stage_ms(omv_orb *orb, double *ms5, long long *calls, int reset);
 
+/* Measurement: FAST candidates (the octree's input) and distributed keypoints of the last batch, summed over its
+ * images (synchronous read-back). */
+omv_status omv_orb_last_counts(omv_orb *orb, long long *n_candidates, long long *n_keypoints);
+
 /* Debug/parity hooks: copy pyramid level `level` of image `img` of the last batch to host. */
 omv_status omv_orb_debug_level(omv_orb *orb, int img, int level, uint8_t *out, int *w, int *h);
 

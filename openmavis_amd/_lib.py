@@ -225,6 +225,7 @@ SIGNATURES = {
     "omv_orb_last_error": (_I, [_VP]),
     "omv_orb_enable_timing": (_I, [_VP, _I]),
     "omv_orb_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(ctypes.c_longlong), _I]),
+    "omv_orb_last_counts": (_I, [_VP, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     "omv_orb_debug_level": (_I, [_VP, _I, _I, _VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "omv_matcher_create": (_I, [_I, _I, _I, _I, ctypes.POINTER(_VP)]),
     "omv_matcher_destroy": (_I, [_VP]),

@@ -1280,8 +1280,9 @@ struct omv_orb {
     omv_kp *d_kp1 = nullptr;
     uint8_t *d_desc1 = nullptr;
     int *d_n1 = nullptr;
-    std::vector<int> h_lap;
+    std::vector<int> h_lap;   // the lapping array last uploaded to d_lap (re-uploaded only when it changes)
     hipStream_t last_stream = nullptr;
+    int last_n = 0;
     int device = 0;
     // optional per-stage HIP-event timing (bench.py): events recorded on the launch stream
     bool timing = false;
@@ -1584,8 +1585,14 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     if (pitch < (size_t)o->W || image_stride < pitch * o->H) return OMV_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     o->last_stream = st;
+    o->last_n = n;
     const Geom &g = o->g;
-    HIP_OK(hipMemcpyAsync(o->d_lap, lapping, sizeof(int) * 2 * n, hipMemcpyHostToDevice, st));
+    // the lapping areas are constant per camera: a pageable host->device copy only when they change, so a
+    // steady stream of batches enqueues kernels only (no host stall between launches)
+    if (o->h_lap.size() < (size_t)2 * n || std::memcmp(o->h_lap.data(), lapping, sizeof(int) * 2 * n) != 0) {
+        HIP_OK(hipMemcpyAsync(o->d_lap, lapping, sizeof(int) * 2 * n, hipMemcpyHostToDevice, st));
+        o->h_lap.assign(lapping, lapping + 2 * n);
+    }
     mark(o, st);
     // K1: pyramid, level by level
     for (int l = 1; l < g.nlevels; ++l) {
@@ -1670,6 +1677,22 @@ omv_status omv_orb_extract_host(omv_orb *o, const uint8_t *image, size_t pitch, 
     *mono_index = hn[1];
     HIP_OK(hipMemcpy(kps, o->d_kp1, sizeof(omv_kp) * hn[0], hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(desc, o->d_desc1, 32 * (size_t)hn[0], hipMemcpyDeviceToHost));
+    return OMV_OK;
+}
+
+omv_status omv_orb_last_counts(omv_orb *o, long long *n_candidates, long long *n_keypoints) {
+    if (!o || !n_candidates || !n_keypoints) return OMV_ERR_ARG;
+    HIP_OK(hipStreamSynchronize(o->last_stream));
+    const int n = o->last_n;
+    std::vector<int> cc((size_t)n * o->g.n_cells), lc((size_t)n * o->g.nlevels * 3);
+    if (n > 0) {
+        HIP_OK(hipMemcpy(cc.data(), o->d_cell_cnt, sizeof(int) * cc.size(), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(lc.data(), o->d_lvl_cnt, sizeof(int) * lc.size(), hipMemcpyDeviceToHost));
+    }
+    long long c = 0, k = 0;
+    for (int v : cc) c += v > 0 ? v : 0;
+    for (size_t i = 0; i < lc.size(); i += 3) k += lc[i];
+    *n_candidates = c, *n_keypoints = k;
     return OMV_OK;
 }
 

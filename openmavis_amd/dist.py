@@ -71,7 +71,9 @@ class CameraShard:
         n_kp [k][F] | mono [k][F] | kps [k][F][kp_cap][6] (omv_kp rows) | desc [k][F][kp_cap][32 B]
     with k = ceil(n_cams / world) camera slots per rank (cam-major: a rank with fewer cameras extracts only its
     first len(cams) * F images).  `gather` scatters every rank's slab into a FrameBatch [F][n_cams] in camera
-    order, on every rank."""
+    order, on every rank: one indexed gather per field (count, monoIndex, keypoint rows, descriptor rows) over the
+    received slabs, with the (rank, row) index of every (frame, camera) built once -- 4 launches whatever the camera
+    and rank counts.  Ranks with no camera (configs[2]: 5 cameras on 8 GPUs) send an empty slab section."""
 
     def __init__(self, rank, world, n_cams, n_frames, kp_cap, device, mode="device", group=None):
         import torch
@@ -89,6 +91,10 @@ class CameraShard:
         if mode == "host":
             self._send_h = torch.empty(self.words, dtype=torch.int32)
             self._recv_h = torch.empty(world * self.words, dtype=torch.int32)
+        # gather index: output (frame f, camera c) <- rank c % world, slab row (c // world) * F + f
+        src_r = torch.tensor([c % world for f in range(F) for c in range(n_cams)], dtype=torch.long)
+        src_j = torch.tensor([(c // world) * F + f for f in range(F) for c in range(n_cams)], dtype=torch.long)
+        self._src = (src_r.to(device), src_j.to(device))
 
     def camera_of(self, r, j):
         return r + j * self.world
@@ -117,20 +123,18 @@ class CameraShard:
                 self.recv.copy_(self._recv_h)
             else:
                 dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
-            F, cap, k = self.F, self.cap, self.k
+            F, cap, k, C = self.F, self.cap, self.k, self.n_cams
             rv = self.recv.view(self.world, self.words)
-            for r in range(self.world):
-                for j in range(k):
-                    c = self.camera_of(r, j)
-                    if c >= self.n_cams:
-                        continue
-                    b = j * F
-                    fb.n_kp[:, c].copy_(rv[r, b:b + F])
-                    fb.mono[:, c].copy_(rv[r, self.off_mono + b:self.off_mono + b + F])
-                    o = self.off_kps + b * cap * 6
-                    fb.kps[:, c].copy_(rv[r, o:o + F * cap * 6].view(F, cap, 6))
-                    o = self.off_desc + b * cap * 8
-                    fb.desc[:, c].copy_(rv[r, o:o + F * cap * 8].view(torch.uint8).view(F, cap, 32))
+            r, j = self._src
+            # strided views [world][k * F][row] of each section of the received slabs (no copy), one gather each
+            n_v = rv[:, :k * F]
+            m_v = rv[:, self.off_mono:self.off_mono + k * F]
+            k_v = rv[:, self.off_kps:self.off_desc].view(self.world, k * F, cap * 6)
+            d_v = rv[:, self.off_desc:].view(self.world, k * F, cap * 8)
+            fb.n_kp.view(F * C).copy_(n_v[r, j])
+            fb.mono.view(F * C).copy_(m_v[r, j])
+            fb.kps.view(F * C, cap * 6).copy_(k_v[r, j])
+            fb.desc.view(F * C, cap * 32).copy_(d_v[r, j].view(torch.uint8))
 
 
 class LbaAllReduce:

@@ -130,6 +130,12 @@ class ORBextractor:
         return out
 
     # -- measurement ------------------------------------------------------------------------------
+    def last_counts(self):
+        """(FAST candidates, distributed keypoints) of the last batch, summed over its images."""
+        c, k = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.check(self._lib.omv_orb_last_counts(self._h, ctypes.byref(c), ctypes.byref(k)), "omv_orb_last_counts")
+        return c.value, k.value
+
     STAGES = ("pyr_resize", "fast_cells", "octree", "blur", "describe")
 
     def enable_timing(self, on=True):

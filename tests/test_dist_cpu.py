@@ -91,11 +91,12 @@ def _shard_worker(rank, world, port, q, n_cams, F, cap):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_cams", [5, 2])
-def test_camera_shard_gather_gloo(n_cams):
-    """configs[2]: one camera per rank (5 cameras on 2 ranks: 3 + 2 slots, or fewer cameras than
-    slots), one all-gather, every rank holds every camera's keypoints / descriptors in camera order."""
-    world, F, cap = 2, 3, 17
+@pytest.mark.parametrize("world,n_cams", [(2, 5), (2, 2), (5, 5), (8, 5)])
+def test_camera_shard_gather_gloo(world, n_cams):
+    """configs[2]: one camera per rank (5 cameras on 2 ranks: 3 + 2 slots; on 5 ranks one each; on 8 ranks --
+    the real 5-of-8 layout -- ranks 5-7 hold no camera and send empty sections), one all-gather, every rank holds
+    every camera's keypoints / descriptors in camera order."""
+    F, cap = 3, 17
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
