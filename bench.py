@@ -742,8 +742,8 @@ BYTES_FORMULA = {
     "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image",
     "fast_cells": "sum of level pixels read once, per image",
     "octree": "4 B per FAST candidate read (its input list) + 8 B per distributed keypoint written",
-    "blur": "sum of level pixels read + written, per image",
-    "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image",
+    "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image (the blur is evaluated in LDS at "
+                "the samples: no blurred pyramid)",
     "grid": "SURVEY 8(d) frame keypoints: 16 B per keypoint",
     "frustum": "per map point 32 B world data in + per (point, camera) 16 B track out (the SearchByProjection input)",
     "stereo_knn": "SURVEY 8(d) knn inputs: 2 x 1,200 descriptors x 32 B per frame",
@@ -760,7 +760,6 @@ def per_step_algorithmic_bytes(B, P, n_kp, n_cand):
         "pyr_resize": B * C * (sum(P[:-1]) + sum(P[1:])),
         "fast_cells": B * C * sum(P),
         "octree": 4 * n_cand + 8 * n_kp,
-        "blur": B * C * 2 * sum(P),
         "describe": B * C * sum(P) + n_kp * 56,
         "grid": n_kp * 16,
         "frustum": B * M_MPS * (32 + C * 16),
@@ -1412,7 +1411,7 @@ def main():
         if dom in iso and "isolated" in d:
             roof["dominant_isolated_view"] = d["isolated"]
         # PMC-measured extraction bytes per image vs SURVEY §8(d)'s 2,085,018 B per image
-        ext = ("pyr_resize", "fast_cells", "octree", "blur", "describe")
+        ext = ("pyr_resize", "fast_cells", "octree", "describe")
         pm = [json.load(open(os.path.join(ROOT, "profiles", f"pmc_{k}.json")))
               for k in ext if os.path.exists(os.path.join(ROOT, "profiles", f"pmc_{k}.json"))]
         per_img = sum(r.get("hbm_bytes_per_image", 0) for r in pm)

@@ -86,10 +86,10 @@ omv_status omv_orb_extract_host(omv_orb *orb, const uint8_t *image, size_t pitch
 omv_status omv_orb_last_error(omv_orb *orb);
 
 /* Per-stage device time (HIP events on the launch stream) for measurement: stages are
- * 0 pyramid, 1 FAST cells, 2 octree, 3 blurred pyramid (GaussianBlur 7x7), 4 orientation+descriptor.  omv_orb_stage_ms syncs, returns the
- * accumulated milliseconds since the last reset and the number of timed batches. */
+ * 0 pyramid, 1 FAST cells, 2 octree, 3 orientation + GaussianBlur 7x7 at the samples + descriptor.  omv_orb_stage_ms
+ * syncs, returns the accumulated milliseconds since the last reset and the number of timed batches. */
 omv_status omv_orb_enable_timing(omv_orb *orb, int on);
-omv_status omv_orb_stage_ms(omv_orb *orb, double *ms5, long long *calls, int reset);
+omv_status omv_orb_stage_ms(omv_orb *orb, double *ms4, long long *calls, int reset);
 
 /* Measurement: FAST candidates (the octree's input) and distributed keypoints of the last batch, summed over its
  * images (synchronous read-back). */

@@ -342,8 +342,9 @@ struct Gather {
     const int *kf_edge;      // per optimisable keyframe, its visual edges
     const int *pc_start;     // [nb+1] per keyframe: its pose chunks
     double *pose_part;       // [n_pchunk][27]: 21 lower-triangle JpT W Jp sums + 6 JpT W e
-    const int4 *schunk;      // Schur chunks: (block slot, first term, end term)
-    const int2 *tr;          // Schur terms (landmark slot a, landmark slot b) oriented to their block
+    const int *schunk_order; // launch order of the Schur chunks (XCD-contiguous runs of neighbouring blocks)
+    const int4 *tr;          // Schur terms (landmark slot a, landmark slot b, landmark, diagonal) oriented to their
+                             // block, each block's list padded to whole 256-term chunks (landmark -1: no term)
     const int *sc_start;     // [n_slots+1] per block: its Schur chunks
     double *schur_part;      // [n_schunk][42]: 36 Hpl_a Dinv Hpl_b^T + 6 Hpl_a Dinv bl
     const int4 *imu_blk;     // per block: inertial edges (edge, side of the block row, side of the column)
@@ -471,6 +472,32 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
     return v;
 }
 
+// Fixed-order wavefront sum of N <= 64 per-lane values at once (a transposing butterfly): at distance d = 32 .. 1
+// each lane keeps one half of its current values -- the lower half when (lane & d) == 0 -- adds the partner's
+// copy of that half, and sends the other; after six steps lane l holds the wave total of value l (l < N), in an
+// order fixed by the lane numbering.  63 shuffles instead of the 6 N of N separate xor trees.
+template <int N>
+__device__ __forceinline__ double wave_transpose_sum(const double (&v)[N], int lane) {
+    static_assert(N <= 64, "at most one value per lane");
+    double a[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {   // d = 32: values j and 32 + j
+        const double lo = j < N ? v[j] : 0.0, hi = j + 32 < N ? v[j + 32] : 0.0;
+        const bool up = (lane & 32) != 0;
+        a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, 64);
+    }
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) {
+        const bool up = (lane & d) != 0;
+#pragma unroll
+        for (int j = 0; j < d; ++j) {
+            const double lo = a[j], hi = a[j + d];
+            a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, d, 64);
+        }
+    }
+    return a[0];
+}
+
 // Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= 256 edges of one keyframe, ascending) per
 // 64-thread block: lane l takes edges l, l+64, ...; 21 + 6 sums, a fixed-order wave reduction, one partial row.
 // The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled (schur_kernel).
@@ -494,12 +521,7 @@ __device__ __forceinline__ void pose_chunk_block(int ch, Rig rig, State s, Edges
         for (int r = 0; r < 6; ++r) acc[21 + r] += rows_om(JP, r, 6, om, nr);
     }
     const int lane = threadIdx.x & 63;
-    double mine = 0;
-#pragma unroll
-    for (int q = 0; q < 27; ++q) {
-        const double t = wave_sum_fixed(acc[q]);
-        mine = lane == q ? t : mine;
-    }
+    const double mine = wave_transpose_sum(acc, lane);
     if (lane < 27) G.pose_part[(size_t)ch * 27 + lane] = mine;
 }
 
@@ -618,58 +640,54 @@ struct BlockPat {
     const int2 *cs;
 };
 
-// Per chunk of one block's Schur terms (<= 256 landmark slot pairs (a, b), one per thread): Dinv = (Hll +
-// lambda I)^-1 of the landmark, BD = Hpl_a Dinv, the 6x6 term BD Hpl_b^T and, on a diagonal block (a == b),
-// Hpl_a Dinv bl (block_solver.hpp:353-486); a fixed-order reduction into the chunk's partial.
-__global__ void __launch_bounds__(256) schur_kernel(Land L, Gather G, BlockPat P, double lambda, const LmCtl *ctl) {
+// Per chunk of one block's Schur terms (256 landmark slot pairs (a, b), one per thread; a block's last chunk padded):
+// Dinv = (Hll + lambda I)^-1 of the landmark, BD = Hpl_a Dinv, the 6x6 term BD Hpl_b^T and, on a diagonal block
+// (a == b), Hpl_a Dinv bl (block_solver.hpp:353-486); a fixed-order reduction into the chunk's partial.  The term
+// record carries its landmark, so a thread's loads are one dependent step behind its record; chunks run in
+// `schunk_order` with XCD-contiguous logical blocks (neighbouring blocks share landmarks: one XCD's L2 holds them).
+__global__ void __launch_bounds__(256) schur_kernel(Land L, Gather G, int n_chunks, double lambda, const LmCtl *ctl) {
     __shared__ double wsum[4][42];
     if (!gate_open(ctl, kGateTrial)) return;
+    const int lb = omv::xcd_block(n_chunks);
+    if (lb < 0) return;
     lambda = lm_lambda(ctl, lambda);
-    const int ch = blockIdx.x, tid = threadIdx.x;
-    const int4 sc = G.schunk[ch];
-    const int t = sc.x;
-    const int kr = P.slot_kr[t], kc = P.slot_kc[t];
-    const bool diag = kr == kc;
+    const int ch = G.schunk_order[lb], tid = threadIdx.x;
     double acc[42];
 #pragma unroll
     for (int q = 0; q < 42; ++q) acc[q] = 0;
-    const int i = sc.y + tid;
-    if (i < sc.z) {
-        const int2 ab = G.tr[i];
-        const int p = L.slot_pt[ab.x];
+    const int4 e = G.tr[(size_t)ch * 256 + tid];
+    if (e.z >= 0) {
+        const int p = e.z;
         double D[9], Dinv[9];
         for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
+        const double *Ha = L.Hpl + (size_t)e.x * 18, *Hb = L.Hpl + (size_t)e.y * 18;
+        double ha[18], hb[18], bl[3];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) ha[q] = Ha[q], hb[q] = Hb[q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bl[q] = L.bl[(size_t)p * 3 + q];
         D[0] += lambda, D[4] += lambda, D[8] += lambda;
         inv3(D, Dinv);
-        const double *Ha = L.Hpl + (size_t)ab.x * 18, *Hb = L.Hpl + (size_t)ab.y * 18;
         double BD[18];
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) BD[3 * r + c] = Ha[3 * r] * Dinv[c] + Ha[3 * r + 1] * Dinv[3 + c] + Ha[3 * r + 2] * Dinv[6 + c];
+            for (int c = 0; c < 3; ++c) BD[3 * r + c] = ha[3 * r] * Dinv[c] + ha[3 * r + 1] * Dinv[3 + c] + ha[3 * r + 2] * Dinv[6 + c];
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-                acc[6 * r + c] = BD[3 * r] * Hb[3 * c] + BD[3 * r + 1] * Hb[3 * c + 1] + BD[3 * r + 2] * Hb[3 * c + 2];
-        if (diag) {
-            const double *bl = L.bl + (size_t)p * 3;
+                acc[6 * r + c] = BD[3 * r] * hb[3 * c] + BD[3 * r + 1] * hb[3 * c + 1] + BD[3 * r + 2] * hb[3 * c + 2];
+        if (e.w) {
             double db[3];
             mv3(Dinv, bl, db);
 #pragma unroll
-            for (int r = 0; r < 6; ++r) acc[36 + r] = Ha[3 * r] * db[0] + Ha[3 * r + 1] * db[1] + Ha[3 * r + 2] * db[2];
+            for (int r = 0; r < 6; ++r) acc[36 + r] = ha[3 * r] * db[0] + ha[3 * r + 1] * db[1] + ha[3 * r + 2] * db[2];
         }
     }
     const int wave = tid >> 6, lane = tid & 63;
-    {
-        double mine = 0;
-#pragma unroll
-        for (int q = 0; q < 42; ++q) {
-            const double v = wave_sum_fixed(acc[q]);
-            mine = lane == q ? v : mine;
-        }
-        if (lane < 42) wsum[wave][lane] = mine;
-    }
+    const double mine = wave_transpose_sum(acc, lane);
+    if (lane < 42) wsum[wave][lane] = mine;
     __syncthreads();
     if (tid < 42) G.schur_part[(size_t)ch * 42 + tid] = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
 }
@@ -1576,38 +1594,39 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     cs_start[nb] = (int)cs.size();
     // Schur terms per block: landmark slots (a, b) of one landmark oriented to the block (a on the block's row
     // keyframe, b on its column keyframe; on a diagonal block a == b), grouped by block in (landmark, a, b) order,
-    // then split into chunks of <= 256 (at least one per block: the chunk that assembles it)
-    std::vector<int> tr_start(n_slots + 1, 0);
-    std::vector<int2> tr;
-    {
-        auto each = [&](auto &&f) {
-            for (int q = 0; q < P; ++q)
-                for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
-                    for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
-                        const int ka = slot_kf[a], kb = slot_kf[b];
-                        if (ka >= nb || kb >= nb || ipos[ka] < ipos[kb] || (ka == kb && a != b)) continue;
-                        f(slot[(size_t)ipos[ka] * nb + ipos[kb]], a, b);
-                    }
-        };
-        each([&](int t, int, int) { ++tr_start[t + 1]; });
-        for (int t = 0; t < n_slots; ++t) tr_start[t + 1] += tr_start[t];
-        tr.resize(tr_start[n_slots]);
-        std::vector<int> fill(tr_start.begin(), tr_start.end() - 1);
-        each([&](int t, int a, int b) { tr[fill[t]++] = make_int2(a, b); });
-    }
-    std::vector<int4> schunk;
+    // each block's list padded to whole chunks of 256 (at least one chunk per block: the chunk that assembles it)
     std::vector<int> sc_start(n_slots + 1, 0);
-    for (int t = 0; t < n_slots; ++t) {
-        sc_start[t] = (int)schunk.size();
-        int q = tr_start[t];
-        do {
-            const int e = std::min(q + 256, tr_start[t + 1]);
-            schunk.push_back(make_int4(t, q, e, 0));
-            q = e;
-        } while (q < tr_start[t + 1]);
+    std::vector<int4> tr;
+    {
+        std::vector<std::vector<int4>> by_blk(n_slots);
+        for (int q = 0; q < P; ++q)
+            for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
+                for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
+                    const int ka = slot_kf[a], kb = slot_kf[b];
+                    if (ka >= nb || kb >= nb || ipos[ka] < ipos[kb] || (ka == kb && a != b)) continue;
+                    by_blk[slot[(size_t)ipos[ka] * nb + ipos[kb]]].push_back(make_int4(a, b, q, a == b ? 1 : 0));
+                }
+        for (int t = 0; t < n_slots; ++t) {
+            sc_start[t] = (int)(tr.size() / 256);
+            tr.insert(tr.end(), by_blk[t].begin(), by_blk[t].end());
+            const size_t padded = std::max<size_t>(256, (tr.size() - (size_t)sc_start[t] * 256 + 255) / 256 * 256);
+            tr.resize((size_t)sc_start[t] * 256 + padded, make_int4(0, 0, -1, 0));
+        }
+        sc_start[n_slots] = (int)(tr.size() / 256);
     }
-    sc_start[n_slots] = (int)schunk.size();
-    h->n_schunk = (int)schunk.size();
+    h->n_schunk = sc_start[n_slots];
+    // launch order: chunks of blocks by the smaller keyframe of the block (blocks that share landmarks together)
+    std::vector<int> schunk_order(h->n_schunk);
+    {
+        std::vector<int> blk_order(n_slots);
+        std::iota(blk_order.begin(), blk_order.end(), 0);
+        std::stable_sort(blk_order.begin(), blk_order.end(), [&](int x, int y) {
+            return std::min(slot_kr[x], slot_kc[x]) < std::min(slot_kr[y], slot_kc[y]);
+        });
+        int w = 0;
+        for (int t : blk_order)
+            for (int c = sc_start[t]; c < sc_start[t + 1]; ++c) schunk_order[w++] = c;
+    }
     // pose chunks: per optimisable keyframe its visual edges (ascending), <= 256 per chunk
     std::vector<int> kf_edge_start(nb + 1, 0), kf_edge, pc_start(nb + 1, 0);
     std::vector<int4> pchunk;
@@ -1786,12 +1805,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     {
         Gather &g = h->G;
         g.pchunk = upv(pchunk), g.kf_edge = upv(kf_edge), g.pc_start = upv(pc_start);
-        g.schunk = upv(schunk), g.tr = upv(tr), g.sc_start = upv(sc_start);
+        g.schunk_order = upv(schunk_order), g.tr = upv(tr), g.sc_start = upv(sc_start);
         g.imu_blk = upv(imu_blk), g.ib_start = upv(ib_start), g.imu_vec = upv(imu_vec), g.iv_start = upv(iv_start);
         g.pose_part = dalloc<double>(ow, (size_t)std::max(1, h->n_pchunk) * 27);
         g.schur_part = dalloc<double>(ow, (size_t)h->n_schunk * 42);
         g.contrib = h->d_imu_contrib;
-        if (!g.pchunk || !g.kf_edge || !g.pc_start || !g.schunk || !g.tr || !g.sc_start || !g.imu_blk || !g.ib_start ||
+        if (!g.pchunk || !g.kf_edge || !g.pc_start || !g.schunk_order || !g.tr || !g.sc_start || !g.imu_blk || !g.ib_start ||
             !g.imu_vec || !g.iv_start || !g.pose_part || !g.schur_part)
             return OMV_ERR_HIP;
     }
@@ -1965,7 +1984,7 @@ static void launch_build(omv_lba *h, const State &A, const LmCtl *c) {
 // The trial's reduced system (H + lambda I minus the landmark Schur terms, b, the Schur right-hand side) in one
 // launch; lambda on the pose diagonal once (rank 0 of a sharded solve), every rank damps its own landmarks.
 static void launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
-    schur_kernel<<<h->n_schunk, 256, 0, h->stream>>>(h->L, h->G, h->BP, lambda, c);
+    schur_kernel<<<omv::xcd_grid(h->n_schunk), 256, 0, h->stream>>>(h->L, h->G, h->n_schunk, lambda, c);
     assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, lambda, h->rank == 0 ? 1 : 0, h->d_S,
                                                           h->d_bb, h->d_coef, c);
 }

@@ -13,13 +13,11 @@
 //                   LDS for quadrant counts) plus the libstdc++ introsort replica for the
 //                   (size, UL.x) refinement ordering; picks max-response key per node; classifies
 //                   lapping/non-lapping for the output split (:1045-1067).
-//   K4 blur         every level blurred once into a blurred pyramid (GaussianBlur 7x7 sigma 2,
-//                   :1035-1036, OpenCV's bit-exact 8U path, BORDER_REFLECT_101 on the level), one
-//                   wavefront per 32x256 tile, horizontal sums in a sliding 7-row register window.
-//   K5 describe     one wavefront per keypoint: intensity-centroid angle over the un-blurred level
-//                   (IC_Angle :19-43, fastAtan2) and steered rBRIEF by byte gathers from the blurred
-//                   level, 4 ballots (computeOrbDescriptor :46-90); writes the keypoint and
-//                   descriptor straight into its final (mono-front / lapping-back) row.
+//   K4 describe     one wavefront per keypoint: intensity-centroid angle over the un-blurred level
+//                   (IC_Angle :19-43, fastAtan2), the GaussianBlur 7x7 (:1035-1036, OpenCV's bit-exact
+//                   8U path) evaluated in LDS at the 512 rBRIEF sample points only, 4 ballots
+//                   (computeOrbDescriptor :46-90); writes the keypoint and descriptor straight into
+//                   its final (mono-front / lapping-back) row.  No blurred pyramid exists.
 //
 // All float code is compiled with -ffp-contract=off (see omv_device.h).
 #include <hip/hip_runtime.h>
@@ -28,6 +26,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <set>
 #include <vector>
 
 #include "../../include/omv.h"
@@ -37,7 +36,7 @@
 namespace {
 
 constexpr int kMaxLevels = 16;
-constexpr int kOrbStages = 5;   // pyramid, FAST cells, octree, blur, describe (omv_orb_stage_ms)
+constexpr int kOrbStages = 4;   // pyramid, FAST cells, octree, describe (omv_orb_stage_ms)
 constexpr int kEdge = 19;     // EDGE_THRESHOLD
 constexpr int kMinB = kEdge - 3;
 #define OMV_PATTERN_TABLE_BEGIN
@@ -94,11 +93,7 @@ struct Geom {
     int n_max;              // output rows per image
     int node_cap;           // octree LDS node capacity
     int ccnt_cap;           // octree child-count region (>= 4 node_cap; also holds the level's cell scan)
-    // blurred pyramid (K4): level 0 at pitch blur_pitch0, levels >= 1 at the pyramid's offsets/pitches
-    int blur_pitch0;
     unsigned long long umax_pk;          // IC_Angle's umax[0..15], 4 bits each (the disc half-widths)
-    long long blur0_bytes, blur_bytes;   // level-0 block, whole per-image block
-    int blur_tile_off[kMaxLevels + 1];   // first K4 tile of each level within an image (last = tiles/image)
     LevelGeom lv[kMaxLevels];
 };
 
@@ -877,224 +872,68 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
 }
 
 // K4 --------------------------------------------------------------------------------------------
-// GaussianBlur 7x7, sigma 2 (ORBextractor.cc:1035-1036; OpenCV's bit-exact 8U path): every pyramid level
-// blurred once, as the reference does, into a blurred pyramid with the same layout.  One wavefront per
-// 32-row x 256-column tile of a level, no LDS: lane = column quad x .. x+3, walking down the tile's 38 input
-// rows (BORDER_REFLECT_101 on the level's own bounds).  Per input row a lane loads its own dword and takes
-// its neighbours' (bytes x-4 .. x-1, x+4 .. x+7) by DPP wave shifts, the horizontal 7-tap sums of its four
-// columns are two v_dot4_u32_u8 each on byte-aligned dwords (u16 exact), kept in a 7-row register window;
-// each output row is the vertical 7-tap sum (sum_i k_i sum_j k_j p + 2^15) >> 16, k = [18, 34, 48, 56, 48,
-// 34, 18], packed by v_perm into one dword store.  The sums never exceed 255 * 2^16 + 2^15, so no clamp.
-constexpr int kBlurTH = 32, kBlurTW = 256;   // output rows / columns per wavefront tile
-
-struct BlurArgs {
-    const uint8_t *images;
-    size_t img_stride, pitch0;
-    const uint8_t *pyr;
-    uint8_t *blur;
-};
-
-__device__ __forceinline__ uint8_t *blur_level(const Geom &g, uint8_t *blur, int img, int l, int *pitch) {
-    if (l == 0) {
-        *pitch = g.blur_pitch0;
-        return blur + (size_t)img * g.blur_bytes;
-    }
-    *pitch = g.lv[l].pitch;
-    return blur + (size_t)img * g.blur_bytes + g.blur0_bytes + g.lv[l].off;
-}
-
-// bytes c .. c+3 of a level row, reflect-101 outside [0, w) (bytes more than one width outside read 0: no
-// output column uses them); `fast`: the row is dword aligned, c a multiple of 4
-__device__ __forceinline__ uint32_t row_dword(const uint8_t *row, int c, int w, bool fast) {
-    if (fast && c >= 0 && c + 3 < w) return *reinterpret_cast<const uint32_t *>(row + c);
-    uint32_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int xx = c + b;
-        const uint32_t px = (xx > -w && xx < 2 * w - 1) ? row[omv::reflect101(xx, w)] : 0u;
-        v |= px << (8 * b);
-    }
-    return v;
-}
-
-// Where a lane's dword (bytes p .. p+3 of a level row) comes from: the aligned dwords at a0 and a1 and the
-// v_perm selector picking its four bytes out of them -- row-independent, so computed once per tile.  Bytes
-// outside [0, w) reflect-101 (BORDER_REFLECT_101); positions that feed no output column read byte 0.
-struct DwordSrc {
-    int a0, a1;
-    uint32_t sel;
-};
-__device__ __forceinline__ DwordSrc dword_src(int p, int w) {
-    if (p >= 0 && p + 3 < w) return DwordSrc{p, p, 0x03020100u};
-    int idx[4], mn = 1 << 30, mx = -1;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int q = p + b;
-        idx[b] = (q > -w && q < 2 * w - 1 && p < w + 4) ? omv::reflect101(q, w) : 0;
-        mn = min(mn, idx[b]), mx = max(mx, idx[b]);
-    }
-    DwordSrc d;
-    d.a0 = mn & ~3;
-    d.a1 = (mx & ~3) == d.a0 ? d.a0 : d.a0 + 4;
-    d.sel = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) d.sel |= (uint32_t)(idx[b] - d.a0) << (8 * b);   // 0..7: bytes of {D1:D0}
-    return d;
-}
-
-// One wavefront tile, rows software-pipelined kBlurPF deep (the loads of row r + kBlurPF issue before row r
-// is summed).  EDGE: the tile's input columns x0-4 .. x0+259 leave the level, every dword is assembled by
-// v_perm from two aligned loads; otherwise two plain loads per row (own dword + the lane-0/63 outside one).
-constexpr int kBlurPF = 8;
-template <bool EDGE>
-__device__ __forceinline__ void blur_tile(const uint8_t *__restrict__ src, int sp, uint8_t *__restrict__ dst, int bp,
-                                          int w, int h, int y0, int x0, int lane) {
-    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-    constexpr int NR = kBlurTH + 6;
-    const int x = x0 + 4 * lane, rows = min(kBlurTH, h - y0);
-    const int pe = lane == 63 ? x0 + kBlurTW : x0 - 4;   // lane 0's left / lane 63's right outside dword
-    DwordSrc cs{x, x, 0x03020100u}, es{pe, pe, 0x03020100u};
-    if (EDGE) cs = dword_src(x, w), es = dword_src(pe, w);
-    uint32_t bc0[kBlurPF], bc1[kBlurPF], be0[kBlurPF], be1[kBlurPF];
-    auto fetch = [&](int r, int k) {
-        const int yy = omv::reflect101(min(y0 - 3 + r, 2 * h - 2), h);
-        const uint8_t *row = src + (size_t)yy * sp;
-        bc0[k] = *reinterpret_cast<const uint32_t *>(row + cs.a0);
-        be0[k] = *reinterpret_cast<const uint32_t *>(row + es.a0);
-        if (EDGE) {
-            bc1[k] = *reinterpret_cast<const uint32_t *>(row + cs.a1);
-            be1[k] = *reinterpret_cast<const uint32_t *>(row + es.a1);
-        }
-    };
-#pragma unroll
-    for (int r = 0; r < kBlurPF; ++r) fetch(r, r);
-    uint32_t win[7][4];   // win[k % 7] = P(k - 1) = (h_{k-1}, h_k), the row pair ending at window row k
-    uint32_t hprev[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        const int k = r % kBlurPF;
-        uint32_t C = bc0[k], E = be0[k];
-        if (EDGE) C = __builtin_amdgcn_perm(bc1[k], C, cs.sel), E = __builtin_amdgcn_perm(be1[k], E, es.sel);
-        if (r + kBlurPF < NR) fetch(r + kBlurPF, k);
-        // lane 0's left and lane 63's right neighbour dwords lie outside the tile: DPP keeps `old` (= E) there
-        const uint32_t Lw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x138, 0xf, 0xf, false);   // wave_shr:1
-        const uint32_t Rw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x130, 0xf, 0xf, false);   // wave_shl:1
-        uint32_t hs[4];
-        hs[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 1), G1,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 1), G0, 0u, false), false);
-        hs[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 2), G1,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 2), G0, 0u, false), false);
-        hs[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, 3), G1,
-                                       __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, 3), G0, 0u, false), false);
-        hs[3] = __builtin_amdgcn_udot4(Rw, G1, __builtin_amdgcn_udot4(C, G0, 0u, false), false);
-        // vertical pass on row pairs: P(k) = (h_k, h_{k+1}) as u16 halves (h < 2^16), so an output row is
-        // dot2(P(r-6), (18,34)) + dot2(P(r-4), (48,56)) + dot2(P(r-2), (48,34)) + 18 h_r + 32768, every pair
-        // packed once and used by three output rows
-        uint32_t *pw = win[r % 7];   // P(r-1) = (h_{r-1}, h_r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pw[c] = (hprev[c] & 0xffffu) | (hs[c] << 16), hprev[c] = hs[c];
-        if (r >= 6) {
-            uint32_t s4[4];
-            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-            const u16x2 W01{18, 34}, W23{48, 56}, W45{48, 34};
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 5) % 7][c]), W01, 32768u, false);
-                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 3) % 7][c]), W23, acc, false);
-                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, win[(r - 1) % 7][c]), W45, acc, false);
-                s4[c] = __umul24(18u, hs[c]) + acc;
-            }
-            // byte 2 of each sum is the blurred pixel
-            const uint32_t lo = __builtin_amdgcn_perm(s4[1], s4[0], 0x0c0c0602u);   // [s0.b2, s1.b2, 0, 0]
-            const uint32_t hi = __builtin_amdgcn_perm(s4[3], s4[2], 0x06020c0cu);   // [0, 0, s2.b2, s3.b2]
-            if (r - 6 < rows && x < w) *reinterpret_cast<uint32_t *>(dst + (size_t)(y0 + r - 6) * bp + x) = lo | hi;
-        }
-    }
-}
-
-// rows that are not dword aligned (a caller's level-0 pitch): byte loads, one row at a time
-__device__ void blur_tile_bytes(const uint8_t *src, int sp, uint8_t *dst, int bp, int w, int h, int y0, int x0, int lane) {
-    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-    const int x = x0 + 4 * lane, rows = min(kBlurTH, h - y0);
-    const int pe = lane == 63 ? x0 + kBlurTW : x0 - 4;
-    uint32_t win[7][4];
-#pragma unroll
-    for (int r = 0; r < kBlurTH + 6; ++r) {
-        const uint8_t *row = src + (size_t)omv::reflect101(min(y0 - 3 + r, 2 * h - 2), h) * sp;
-        const uint32_t C = row_dword(row, x, w, false), E = row_dword(row, pe, w, false);
-        const uint32_t Lw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x138, 0xf, 0xf, false);
-        const uint32_t Rw = (uint32_t)__builtin_amdgcn_update_dpp((int)E, (int)C, 0x130, 0xf, 0xf, false);
-        uint32_t *hs = win[r % 7];
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            hs[c] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(Rw, C, c + 1), G1,
-                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, Lw, c + 1), G0, 0u, false), false);
-        hs[3] = __builtin_amdgcn_udot4(Rw, G1, __builtin_amdgcn_udot4(C, G0, 0u, false), false);
-        if (r >= 6 && r - 6 < rows && x < w) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                uint32_t acc = 32768u;
-#pragma unroll
-                for (int k = 0; k < 7; ++k) acc += (uint32_t)c_gauss7[k] * win[(r - 6 + k) % 7][c];
-                v |= (acc >> 16) << (8 * c);
-            }
-            *reinterpret_cast<uint32_t *>(dst + (size_t)(y0 + r - 6) * bp + x) = v;
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) blur_kernel(Geom g, BlurArgs a, int n_tiles) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int blk = omv::xcd_block((n_tiles + 3) >> 2);
-    if (blk < 0) return;
-    const int tile = __builtin_amdgcn_readfirstlane(blk * 4 + wave);   // wave-uniform: scalar address math
-    if (tile >= n_tiles) return;
-    const int tpi = g.blur_tile_off[g.nlevels];
-    const int img = tile / tpi;
-    const int t = tile - img * tpi;
-    int l = 0;
-    while (l + 1 < g.nlevels && t >= g.blur_tile_off[l + 1]) ++l;
-    const LevelGeom &L = g.lv[l];
-    const int tcols = (L.w + kBlurTW - 1) / kBlurTW;
-    const int tr = (t - g.blur_tile_off[l]) / tcols, tc = (t - g.blur_tile_off[l]) - tr * tcols;
-    const int y0 = tr * kBlurTH, x0 = tc * kBlurTW;
-    int sp, bp;
-    const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
-    uint8_t *dst = blur_level(g, a.blur, img, l, &bp);
-    if (((((uintptr_t)src) | (uintptr_t)sp) & 3) != 0)
-        blur_tile_bytes(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
-    else if (x0 >= 4 && x0 + kBlurTW + 4 <= L.w)
-        blur_tile<false>(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
-    else
-        blur_tile<true>(src, sp, dst, bp, L.w, L.h, y0, x0, lane);
-}
-
-// K5 --------------------------------------------------------------------------------------------
-// Orientation + rBRIEF, one wavefront per output slot (inactive slots leave at once):
-//   IC_Angle (:19-43) over the r = 15 disc of the UN-blurred level: lane = (disc row, 16-byte half), one 16-byte
-//   and one dword load, four v_dot4 items each with the in-disc byte mask (row sum -> m01) and the weights
-//   u + 15 (m10); a wave reduction; fastAtan2 (degrees, float);
-//   computeOrbDescriptor (:46-90) on the BLURRED level: the 37 x 37 patch around the keypoint is staged into LDS
-//   (two 16-byte loads per lane, issued with the centroid loads), lane = pattern pair (4 rounds of 64), steering
-//   by (cos, sin) with cvRound, the two samples read from LDS, bit = I(a) < I(b) collected by 4 ballots = 32 bytes.
+// Orientation + blur + rBRIEF, one wavefront per output slot (inactive slots leave at once).  The reference
+// blurs every level whole (GaussianBlur 7x7 sigma 2, ORBextractor.cc:1035-1036, OpenCV's bit-exact 8U path,
+// BORDER_REFLECT_101 on the level) and then samples 512 pixels of it per keypoint; only the blurred values
+// within radius 18.4 of a keypoint are ever read, so the blur is evaluated here, per keypoint, from the
+// un-blurred level -- no blurred pyramid is written or re-read:
+//   stage   the raw 43 x 43 patch (rows cy-21 .. cy+21, cols cx-21 .. cx+21, reflect-101 outside the level)
+//           into this wave's LDS, three 16-byte loads per lane (byte loads near the level's left / right edge);
+//   IC_Angle (:19-43) over the r = 15 disc of that raw patch: lane = (disc row, 16-byte half), five LDS dwords,
+//           four v_dot4 items with the lane's in-disc byte masks (row sum -> m01) and weights u + 15 (m10) from a
+//           per-lane table; a wave reduction; fastAtan2 (degrees, float);
+//   blur    horizontal 7-tap sums (two v_dot4_u32_u8 per sum on byte-aligned dwords, exact in u16) of the
+//           (row pair, column quad) items any rotation of the pattern can reach (a host table, 189 of 220),
+//           stored column-major with the two rows of a pair in one dword; the vertical 7 taps only at the 512
+//           sample points: two ds_read2 + three v_dot2_u32_u16 + one mad, (sum_i k_i h_i + 2^15) >> 16,
+//           k = [18, 34, 48, 56, 48, 34, 18] -- OpenCV's separable fixed-point integers, so every sampled value
+//           equals the reference's blurred pixel;
+//   rBRIEF (computeOrbDescriptor :46-90): lane = pattern pair (4 rounds of 64), steering by (cos, sin) with
+//           cvRound, bit = I(a) < I(b) collected by 4 ballots = 32 bytes.
 struct DescArgs {
     const uint8_t *images;
     size_t img_stride, pitch0;
-    const uint8_t *pyr, *blur;
+    const uint8_t *pyr;
     const uint32_t *lvl_out, *lvl_cls;
     const int *lvl_cnt;
     omv_kp *kps;
     uint8_t *desc;
     int *n_out, *mono;
     int n_images;
+    const uint32_t *disc;    // [64][8] per lane: (row-sum mask, weight mask) of its four centroid dot4 items
+    const uint32_t *hitem;   // [kHItemIt * 64] horizontal items: raw dword offset | column-major offset << 16
 };
 
-constexpr int kPatchRows = 37, kPatchDw = 12;   // K5's staged blurred patch: rows cy-18..cy+18, 48 bytes each
+constexpr int kRawRows = 43, kRawDw = 12;   // raw patch: rows cy-21 .. cy+21, 48 bytes each (43 used + alignment)
+constexpr int kHCols = 40, kHStride = 23;   // horizontal sums: 40 columns x 22 row pairs (stride 23 dwords)
+constexpr int kDescDw = kRawRows * kRawDw + kHCols * kHStride;   // LDS dwords per wave (5,744 B)
+constexpr int kHItemIt = 4;                 // horizontal items per lane (<= 256 per keypoint)
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, dword-aligned
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // other lanes read what this wave just wrote: a wave's LDS operations complete in order; keep the compiler's too
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the 7-tap sums of output columns 4q .. 4q+3 of one raw row whose dwords q .. q+3 are d0..d3 (byte offset po)
+__device__ __forceinline__ void hsum4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, int po, uint32_t h[4]) {
+    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
+    const uint32_t A = __builtin_amdgcn_alignbyte(d1, d0, po), B = __builtin_amdgcn_alignbyte(d2, d1, po),
+                   C = __builtin_amdgcn_alignbyte(d3, d2, po);
+    h[0] = __builtin_amdgcn_udot4(B, G1, __builtin_amdgcn_udot4(A, G0, 0u, false), false);
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+        h[k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, B, k), G1,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(B, A, k), G0, 0u, false), false);
+}
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is wave-uniform: everything derived from the slot (record, level, counts, patch origin) is
+    // scalar work and scalar loads
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int blk = omv::xcd_block(n_blocks);
     if (blk < 0) return;
     const int slot = blk * 4 + wave;
@@ -1116,68 +955,87 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     const uint32_t p = a.lvl_out[(size_t)img * g.out_per_img + s];
     const uint32_t cl = a.lvl_cls[(size_t)img * g.out_per_img + s];
     if (j >= cnts[3 * l]) return;
+    // the lane's constant tables (independent of the record: in flight together)
+    const uint4 dm0 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane], dm1 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane + 1];
+    uint32_t hit[kHItemIt], pat[4];
+#pragma unroll
+    for (int it = 0; it < kHItemIt; ++it) hit[it] = a.hitem[lane + 64 * it];
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) pat[rd] = c_pattern8.v[rd * 64 + lane];
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
     const int score = (int)(p >> 24);
     int sp;
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
-    int bpitch;
-    const uint8_t *bl = blur_level(g, const_cast<uint8_t *>(a.blur), img, l, &bpitch) + (size_t)cy * bpitch + cx;
-    // The rotated samples lie within radius 18.4 of the keypoint, so the blurred 37 x 37 patch is staged into
-    // this wave's LDS (rows cy-18 .. cy+18, three 16-byte loads each) while the centroid loads are in flight;
-    // the sampling then reads LDS.  Keypoints lie in [19, w-20] x [19, h-20] of their level, so every load
-    // below stays inside the level (at most 8 bytes into the next row).
-    __shared__ __attribute__((aligned(16))) uint32_t patch[4][kPatchRows * kPatchDw];
-    uint32_t *pw = patch[wave];
-    const uint8_t *prow = bl - (ptrdiff_t)18 * bpitch - 18;
-    const int po = (int)((uintptr_t)prow & 3);
-    const bool staged = (bpitch & 3) == 0;
-    u32x4a pv[2];
-    if (staged) {
-        const uint32_t *pa = reinterpret_cast<const uint32_t *>(prow - po);
-        const int sw = bpitch >> 2;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4][kDescDw];
+    uint32_t *raw = lds[wave];
+    uint32_t *H = raw + kRawRows * kRawDw;   // H[c * kHStride + m] = h[2m][c] | h[2m+1][c] << 16
+    // Keypoints lie in [19, w-20] x [19, h-20] of their level, so the patch reaches at most 2 pixels past an
+    // edge (reflected).  Fast path: the level's rows are dword aligned and the 48 bytes from the aligned start
+    // stay inside [0, w): three 16-byte loads per lane; raw byte po + c is column cx - 21 + c.
+    const int x0 = cx - 21;
+    const bool dw_rows = ((((uintptr_t)src) | (uintptr_t)sp) & 3) == 0;
+    int po = dw_rows ? (x0 & 3) : 0;
+    if (dw_rows && x0 - po >= 0 && x0 - po + 4 * kRawDw <= L.w) {
+        const uint8_t *base = src + (x0 - po);
+        u32x4a pv[3];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int i = min(lane + 64 * t, kPatchRows * 3 - 1);
+        for (int t = 0; t < 3; ++t) {
+            const int i = min(lane + 64 * t, kRawRows * 3 - 1);
             const int r = i / 3, w = i - 3 * r;
-            pv[t] = *reinterpret_cast<const u32x4a *>(pa + r * sw + 4 * w);
+            const int yy = omv::reflect101(cy - 21 + r, L.h);
+            pv[t] = *reinterpret_cast<const u32x4a *>(base + (size_t)yy * sp + 16 * w);
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            if (lane + 64 * t < kRawRows * 3) reinterpret_cast<u32x4a *>(raw)[lane + 64 * t] = pv[t];
+    } else {
+        po = 0;   // byte loads, columns reflected (near the level's left / right edge, or rows not dword aligned)
+        for (int i = lane; i < kRawRows * kRawDw; i += 64) {
+            const int r = i / kRawDw, d = i - kRawDw * r;
+            const uint8_t *row = src + (size_t)omv::reflect101(cy - 21 + r, L.h) * sp;
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (4 * d + b < 43) v |= (uint32_t)row[omv::reflect101(x0 + 4 * d + b, L.w)] << (8 * b);
+            raw[i] = v;
         }
     }
+    wave_lds_sync();
+    // horizontal 7-tap sums of the table's (row pair m, column quad q) items: rows 2m, 2m+1 (raw dwords q .. q+3
+    // of each; the pair m = 21 reads one row past the patch for its unused second row), columns 4q .. 4q+3
+    // (column c is level column cx - 18 + c, taps raw bytes po + c .. po + c + 6)
+#pragma unroll
+    for (int it = 0; it < kHItemIt; ++it) {
+        const uint32_t e = hit[it];
+        if (e == 0xffffffffu) continue;
+        const uint32_t *ra = raw + (e & 0xffff);
+        uint32_t *hp = H + (e >> 16);
+        uint32_t ha[4], hb[4];
+        hsum4(ra[0], ra[1], ra[2], ra[3], po, ha);
+        hsum4(ra[kRawDw], ra[kRawDw + 1], ra[kRawDw + 2], ra[kRawDw + 3], po, hb);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hp[k * kHStride] = ha[k] | (hb[k] << 16);
+    }
     // intensity centroid: lane = (disc row vr = lane >> 1, half h = lane & 1) = bytes cx-15+16h .. +15 of row
-    // cy-15+vr as four dot4 items (one 16-byte and one dword load, byte-aligned by v_alignbyte)
+    // cy-15+vr (raw row 6 + vr, raw byte po + 6 + 16h) as four dot4 items over five LDS dwords; lanes 62, 63 and
+    // the bytes outside the disc have zero masks
     int m01 = 0, m10 = 0;
     {
         const int vr = min(lane >> 1, 30), h = lane & 1;
-        const uint8_t *ad = src + (size_t)(cy - 15 + vr) * sp + (cx - 15 + 16 * h);
-        const uint32_t *al = reinterpret_cast<const uint32_t *>((uintptr_t)ad & ~(uintptr_t)3);
-        const int sh = (int)((uintptr_t)ad & 3);
-        const u32x4a q4 = *reinterpret_cast<const u32x4a *>(al);
-        const uint32_t q5 = al[4];
-        const uint32_t qq[5] = {q4.x, q4.y, q4.z, q4.w, q5};
-        if (lane < 62) {
-            // the disc row's bytes: u = 4 kd + b - 15 with |u| <= umax[|vr - 15|] (u <= 15 then holds too), the
-            // row-sum mask (1 per byte) and the weights u + 15, formed instead of loaded
-            const int um = (int)((g.umax_pk >> (4 * (vr < 15 ? 15 - vr : vr - 15))) & 15ull);
+        const int b = po + 6 + 16 * h;
+        const uint32_t *al = raw + (6 + vr) * kRawDw + (b >> 2);
+        const int sh = b & 3;
+        const uint32_t qq[5] = {al[0], al[1], al[2], al[3], al[4]};
+        const uint32_t mk[8] = {dm0.x, dm0.y, dm0.z, dm0.w, dm1.x, dm1.y, dm1.z, dm1.w};
+        int rs = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int kd = 4 * h + k;
-                const int blo = min(max(15 - um - 4 * kd, 0), 4), bhi = min(max(15 + um - 4 * kd, -1), 3);
-                const uint32_t keep = (blo >= 4 ? 0u : (0xffffffffu << (8 * blo))) & (bhi < 0 ? 0u : (0xffffffffu >> (8 * (3 - bhi))));
-                const uint2 mk = make_uint2(0x01010101u & keep, (0x03020100u + 0x04040404u * (uint32_t)kd) & keep);
-                const uint32_t w = __builtin_amdgcn_alignbyte(qq[k + 1], qq[k], sh);
-                const int rs = (int)__builtin_amdgcn_udot4(w, mk.x, 0u, false);
-                m10 += (int)__builtin_amdgcn_udot4(w, mk.y, 0u, false) - 15 * rs;
-                m01 += (vr - 15) * rs;
-            }
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(qq[k + 1], qq[k], sh);
+            rs = (int)__builtin_amdgcn_udot4(w, mk[2 * k], (uint32_t)rs, false);
+            m10 += (int)__builtin_amdgcn_udot4(w, mk[2 * k + 1], 0u, false);
         }
-    }
-    if (staged) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-            if (lane + 64 * t < kPatchRows * 3) reinterpret_cast<u32x4a *>(pw)[lane + 64 * t] = pv[t];
-        // other lanes read these bytes below: a wave's LDS operations complete in order; keep the compiler's too
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        m10 -= 15 * rs;
+        m01 = (vr - 15) * rs;
     }
     for (int d = 32; d >= 1; d >>= 1) {
         m01 += __shfl_xor(m01, d, 64);
@@ -1187,28 +1045,33 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     float sn, cs;
     omv::glibc_sincosf(angle * (float)(3.14159265358979323846 / 180.f), &sn, &cs);
     const float fa = cs, fb = sn;
-    const uint8_t *pb = reinterpret_cast<const uint8_t *>(pw) + 18 * kPatchDw * 4 + 18 + po;   // the keypoint
-    uint32_t ia[4], ib[4];
+    wave_lds_sync();   // the horizontal sums of every lane are in LDS
+    // the blurred pixel at (cx + dx, cy + dy), |dx|, |dy| <= 18: column dx + 18, sum rows R0 = dy + 18 .. R0 + 6
+    // = the four pair dwords from R0 >> 1, realigned by a half when R0 is odd
+    auto blurred = [&](int dx, int dy) -> uint32_t {
+        const int R0 = dy + 18;
+        const uint32_t *q = H + (dx + 18) * kHStride + (R0 >> 1);
+        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+        const uint32_t sh = (uint32_t)(R0 & 1) << 4;
+        const uint32_t w0 = __builtin_amdgcn_alignbit(d1, d0, sh), w1 = __builtin_amdgcn_alignbit(d2, d1, sh),
+                       w2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+        uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w0), u16x2{18, 34}, 32768u, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w1), u16x2{48, 56}, acc, false);
+        acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w2), u16x2{48, 34}, acc, false);
+        return (acc + 18u * ((d3 >> sh) & 0xffffu)) >> 16;
+    };
+    uint64_t words[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) {
-        const uint32_t pt = c_pattern8.v[rd * 64 + lane];
+        const uint32_t pt = pat[rd];
         const int ax = (int)(int8_t)(pt & 0xff), ay = (int)(int8_t)((pt >> 8) & 0xff);
         const int bx = (int)(int8_t)((pt >> 16) & 0xff), by = (int)(int8_t)(pt >> 24);
         const int ady = omv::round_even((float)ax * fb + (float)ay * fa);
         const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
         const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
         const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
-        if (staged) {
-            ia[rd] = pb[ady * (kPatchDw * 4) + adx];
-            ib[rd] = pb[bdy * (kPatchDw * 4) + bdx];
-        } else {
-            ia[rd] = bl[(ptrdiff_t)ady * bpitch + adx];
-            ib[rd] = bl[(ptrdiff_t)bdy * bpitch + bdx];
-        }
+        words[rd] = __ballot(blurred(adx, ady) < blurred(bdx, bdy));
     }
-    uint64_t words[4];
-#pragma unroll
-    for (int rd = 0; rd < 4; ++rd) words[rd] = __ballot(ia[rd] < ib[rd]);
     // final row: monoIndex order (front) or lapping order (back, reversed)
     int mono_before = 0, lap_before = 0, total = 0;
     for (int q = 0; q < g.nlevels; ++q) {
@@ -1266,7 +1129,8 @@ struct omv_orb {
     Cell *d_cells = nullptr;
     XTab *d_xt = nullptr, *d_yt = nullptr;
     XQuad *d_xq = nullptr;
-    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+    uint32_t *d_disc = nullptr, *d_hitem = nullptr;   // K4's per-lane centroid masks and horizontal-sum items
+    uint8_t *d_pyr = nullptr;
     int *d_cell_cnt = nullptr;
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
@@ -1286,7 +1150,7 @@ struct omv_orb {
     int device = 0;
     // optional per-stage HIP-event timing (bench.py): events recorded on the launch stream
     bool timing = false;
-    std::vector<hipEvent_t> ev;   // 6 events per batch: before K1, K2, K3, K4, K5, after K5
+    std::vector<hipEvent_t> ev;   // 5 events per batch: before K1, K2, K3, K4, after K4
     double stage_ms[kOrbStages] = {};
     long long stage_calls = 0;
 };
@@ -1462,12 +1326,6 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
         cand_off += L.cand_cap;
     }
     g.pyr_bytes = (pyr_off + 255) & ~255LL;
-    g.blur_pitch0 = (o->W + 15) & ~15;
-    g.blur0_bytes = ((long long)g.blur_pitch0 * o->H + 255) & ~255LL;
-    g.blur_bytes = g.blur0_bytes + g.pyr_bytes;
-    g.blur_tile_off[0] = 0;
-    for (int l = 0; l < nl; ++l)
-        g.blur_tile_off[l + 1] = g.blur_tile_off[l] + ((g.lv[l].h + kBlurTH - 1) / kBlurTH) * ((g.lv[l].w + kBlurTW - 1) / kBlurTW);
     g.cand_per_img = cand_off;
     g.out_per_img = out_off;
     g.n_max = out_off;
@@ -1478,6 +1336,49 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
     o->oct_lds = (size_t)(32 + 18 * g.node_cap + g.ccnt_cap + 192) * sizeof(int);
     return OMV_OK;
+}
+
+// K4's per-lane constant tables.  disc[lane][2k], disc[lane][2k+1]: the row-sum and the weight (u + 15) byte masks of
+// the lane's centroid item k (disc row vr = min(lane >> 1, 30), bytes 16 (lane & 1) + 4k .. +3 of cx-15 ..; zero
+// outside the r = 15 disc, IC_Angle's umax rows, and for lanes 62, 63).  hitem: the (row pair, column quad) items of
+// the horizontal sums that any rotation of the pattern can sample: a steered point round(R(theta) p) lies in the
+// unit square around a point of the circle of radius |p|, so every integer (X, Y) whose square meets one of those
+// circles is kept, and with it rows Y + 18 .. Y + 24 of column X + 18.
+static std::vector<uint32_t> disc_table(const int umax[16]) {
+    std::vector<uint32_t> t(64 * 8, 0u);
+    for (int lane = 0; lane < 62; ++lane) {
+        const int vr = std::min(lane >> 1, 30), h = lane & 1;
+        const int um = umax[vr < 15 ? 15 - vr : vr - 15];
+        for (int k = 0; k < 4; ++k) {
+            const int kd = 4 * h + k;
+            const int blo = std::min(std::max(15 - um - 4 * kd, 0), 4), bhi = std::min(std::max(15 + um - 4 * kd, -1), 3);
+            const uint32_t keep = (blo >= 4 ? 0u : (0xffffffffu << (8 * blo))) & (bhi < 0 ? 0u : (0xffffffffu >> (8 * (3 - bhi))));
+            t[8 * lane + 2 * k] = 0x01010101u & keep;
+            t[8 * lane + 2 * k + 1] = (0x03020100u + 0x04040404u * (uint32_t)kd) & keep;
+        }
+    }
+    return t;
+}
+
+static bool hitem_table(std::vector<uint32_t> &t) {
+    std::vector<double> radii;
+    for (int i = 0; i < 512; ++i) radii.push_back(std::hypot((double)kPattern[2 * i], (double)kPattern[2 * i + 1]));
+    std::set<std::pair<int, int>> items;   // (row pair, column quad)
+    for (int X = -18; X <= 18; ++X)
+        for (int Y = -18; Y <= 18; ++Y) {
+            const double dmin = std::hypot(std::max(0.0, std::abs(X) - 0.5), std::max(0.0, std::abs(Y) - 0.5));
+            const double dmax = std::hypot(std::abs(X) + 0.5, std::abs(Y) + 0.5);
+            bool hit = false;
+            for (double r : radii) hit = hit || (dmin <= r && r <= dmax);
+            if (!hit) continue;
+            for (int R = Y + 18; R <= Y + 24; ++R) items.insert({R >> 1, (X + 18) >> 2});
+        }
+    if (items.size() > (size_t)kHItemIt * 64) return false;
+    t.assign((size_t)kHItemIt * 64, 0xffffffffu);
+    size_t i = 0;
+    for (const auto &mq : items)
+        t[i++] = (uint32_t)(2 * mq.first * kRawDw + mq.second) | ((uint32_t)(4 * mq.second * kHStride + mq.first) << 16);
+    return true;
 }
 
 extern "C" {
@@ -1536,8 +1437,19 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     if (!yt.empty()) HIP_OK(hipMemcpy(o->d_yt, yt.data(), sizeof(XTab) * yt.size(), hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&o->d_xq, sizeof(XQuad) * std::max<size_t>(1, xq.size())));
     if (!xq.empty()) HIP_OK(hipMemcpy(o->d_xq, xq.data(), sizeof(XQuad) * xq.size(), hipMemcpyHostToDevice));
+    {
+        const std::vector<uint32_t> dt = disc_table(o->umax);
+        std::vector<uint32_t> ht;
+        if (!hitem_table(ht)) {
+            delete o;
+            return OMV_ERR_ARG;
+        }
+        HIP_OK(hipMalloc(&o->d_disc, sizeof(uint32_t) * dt.size()));
+        HIP_OK(hipMemcpy(o->d_disc, dt.data(), sizeof(uint32_t) * dt.size(), hipMemcpyHostToDevice));
+        HIP_OK(hipMalloc(&o->d_hitem, sizeof(uint32_t) * ht.size()));
+        HIP_OK(hipMemcpy(o->d_hitem, ht.data(), sizeof(uint32_t) * ht.size(), hipMemcpyHostToDevice));
+    }
     HIP_OK(hipMalloc(&o->d_pyr, std::max<size_t>(256, (size_t)g.pyr_bytes * n)));
-    HIP_OK(hipMalloc(&o->d_blur, (size_t)g.blur_bytes * n));
     HIP_OK(hipMalloc(&o->d_cell_cnt, sizeof(int) * g.n_cells * n));
     HIP_OK(hipMalloc(&o->d_cell_kp, sizeof(uint32_t) * (size_t)g.n_cells * g.cell_cap * n));
     HIP_OK(hipMalloc(&o->d_cand, sizeof(uint32_t) * (size_t)g.cand_per_img * n));
@@ -1555,7 +1467,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
     for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
-    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_pyr, o->d_blur, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_disc, o->d_hitem, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
     for (void *p : ptrs)
@@ -1612,13 +1524,9 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
     octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
     mark(o, st);
-    // K4: blurred pyramid, one wavefront per 32 x 256 tile
-    const int blur_tiles = g.blur_tile_off[g.nlevels] * n;
-    blur_kernel<<<omv::xcd_grid((blur_tiles + 3) / 4), 256, 0, st>>>(g, BlurArgs{images, image_stride, pitch, o->d_pyr, o->d_blur},
-                                                               blur_tiles);
-    mark(o, st);
-    // K5: orientation + descriptors, one wave per output slot
-    DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_blur, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n};
+    // K4: orientation + blur at the samples + descriptors, one wave per output slot
+    DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n,
+                o->d_disc, o->d_hitem};
     const int waves = g.out_per_img * n;
     describe_kernel<<<omv::xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
@@ -1632,11 +1540,11 @@ omv_status omv_orb_enable_timing(omv_orb *o, int on) {
     return OMV_OK;
 }
 
-omv_status omv_orb_stage_ms(omv_orb *o, double *ms5, long long *calls, int reset) {
-    if (!o || !ms5) return OMV_ERR_ARG;
+omv_status omv_orb_stage_ms(omv_orb *o, double *ms4, long long *calls, int reset) {
+    if (!o || !ms4) return OMV_ERR_ARG;
     HIP_OK(hipStreamSynchronize(o->last_stream));
     flush_timing(o);
-    for (int k = 0; k < kOrbStages; ++k) ms5[k] = o->stage_ms[k];
+    for (int k = 0; k < kOrbStages; ++k) ms4[k] = o->stage_ms[k];
     if (calls) *calls = o->stage_calls;
     if (reset) {
         for (int k = 0; k < kOrbStages; ++k) o->stage_ms[k] = 0;

@@ -136,7 +136,7 @@ class ORBextractor:
         _lib.check(self._lib.omv_orb_last_counts(self._h, ctypes.byref(c), ctypes.byref(k)), "omv_orb_last_counts")
         return c.value, k.value
 
-    STAGES = ("pyr_resize", "fast_cells", "octree", "blur", "describe")
+    STAGES = ("pyr_resize", "fast_cells", "octree", "describe")
 
     def enable_timing(self, on=True):
         _lib.check(self._lib.omv_orb_enable_timing(self._h, int(bool(on))))

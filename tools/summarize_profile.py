@@ -16,7 +16,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"pyr_resize": "pyr_resize", "fast_cells": "fast_cells", "octree": "octree", "describe": "describe",
-         "blur_kernel": "blur", "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
+         "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
          "stereo_tri_kernel": "stereo_tri", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
          "frustum_kernel": "frustum", "uright_kernel": "uright", "err_kernel": "lba_err", "build_kernel": "lba_build",
          "schur_kernel": "lba_schur", "assemble_kernel": "lba_assemble", "ldlt_kernel": "lba_ldlt",
