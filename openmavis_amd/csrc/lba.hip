@@ -629,8 +629,6 @@ struct BlockPat {
     const int *slot_kr, *slot_kc;    // [n_slots] keyframes of the block's row / column
     const int *dslot;                // [nb] diagonal slot per position
     const int *lev_start, *lev_col;  // elimination-tree levels: the positions of level l
-    const int *pt_start;             // [n_lev+1] panel tasks of a level
-    const int2 *pt;                  //   (slot(i, k), dslot(k))
     const int *ug_start;             // [n_lev+1] update groups of a level (one target block each)
     const int *ug_task_start;        // [n_groups+1]
     const int4 *ug;                  //   (slot(i, j), slot(i, k), slot(j, k), dslot(k)), ascending k
@@ -783,107 +781,119 @@ __device__ __forceinline__ double rcp_nr(double x) {
     return fma(r, e, r);
 }
 
-// One wavefront: D = L diag(d) L^T in place (unit L strictly below the diagonal, d on it) and W = L^-1
-// by the same eliminations, stored transposed in the strict upper triangle (W[j][i] at D[i][j], i < j).
-// Eight passes, each eliminating a 2x2 pivot block (c0, c0+1): with P = [p00 .; p10 p11],
-// l = p10/p00, d1 = p11 - l p10, and for a row x its pivot-column values b_x0, b_x1, u_x = b_x1 - l b_x0:
-//   lower trailing (i, j > c0+1) : A_ij -= b_i0 b_j0 / p00 + u_i u_j / d1
-//   lower pivot columns           : L_i,c0 = b_i0 / p00, L_i,c0+1 = u_i / d1, L_c0+1,c0 = l, d = (p00, d1)
-//   upper, column j >= c0+1        : W[j][i] <- W[j][i] - L_B[j] . (new W rows c0, c0+1)[i]
-//                                     (W[c0+1][.] = W[c0+1][.] - l W[c0][.]; entries first touched here,
-//                                     i in {c0, c0+1}, start from 0 -- the upper triangle holds stale values)
-// Lane l owns entries e = l + 64t, (i, j) = (e>>4, e&15), kept in registers; a pass reads only the tile's
-// columns c0, c0+1, which their owners store at the end of the previous pass.
+// The reduced system is factored as a block LDL^T with 16x16 block pivots: A = L D L^T, L_ik = S_ik D_k^-1, D_k = S_kk
+// (each S the block as it stands when column k is eliminated).  Nothing but the blocks themselves and D_k^-1 is kept:
+// the diagonal slot of column k is overwritten by D_k^-1, the panels S_ik stay unscaled in place, and
+//   trailing update   S_ij -= S_ik D_k^-1 S_jk^T             (two f64 MFMA products, the inner one in registers)
+//   forward           z_k = D_k^-1 (y_k - sum_{j < k} S_kj z_j)
+//   backward          x_k = z_k - D_k^-1 sum_{i > k} S_ik^T x_i
+// so a level is one diagonal-inverse phase and one phase of updates + forward columns.  The solution is that of the
+// damped system (SimplicialLDLT's scalar LDL^T on its own AMD order, linear_solver_eigen.h:94-120, differs only in
+// rounding).
+
+// One wavefront: D (16x16 symmetric, lower triangle read) -> D^-1 in place (full), by four 4x4-pivot sweeps (the
+// sweep operator, block form): with pivot block P = {c0 .. c0+3}, Pi = M_PP^-1, b_x = M_xP,
+//   i, j not in P : M_ij - b_i Pi b_j^T      i in P, j not : (Pi b_j)_i      j in P, i not : (b_i Pi)_j
+//   i, j in P     : -Pi
+// after all four M = -D^-1.  Lane l owns column j = l & 15, rows q + 4t (q = l >> 4) in registers.  With
+// w = (j in P ? e_{j - c0} : b_j) and u = +-Pi w, every entry off the pivot rows is (j in P ? 0 : x) + b_i . u, and
+// the pivot rows (entry t = pass, all q) are -u_q.  Pi by 2x2 blocks: A^-1, the Schur complement S = C - B^T A^-1 B,
+// S^-1.  A zero / non-finite pivot determinant flags the solve.
 template <bool G>
-__device__ __forceinline__ void factor16(double *D, int lane, int *bad) {
+__device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
     double cur[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) cur[t] = D[sw16(q + 4 * t, j)];
+    for (int t = 0; t < 4; ++t) {
+        const int i = q + 4 * t;
+        cur[t] = D[i >= j ? sw16(i, j) : sw16(j, i)];
+    }
+    wave_sync<G>();
 #pragma unroll
-    for (int c0 = 0; c0 < 16; c0 += 2) {
-        const double p00 = D[sw16(c0, c0)], p10 = D[sw16(c0 + 1, c0)], p11 = D[sw16(c0 + 1, c0 + 1)];
-        double bi0[4], bi1[4];
+    for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];   // the full symmetric block: columns readable
+    wave_sync<G>();
+#pragma unroll
+    for (int pv = 0; pv < 4; ++pv) {
+        const int c0 = 4 * pv;
+        double pm[4][4], bi[4][4], bj[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y2 = 0; y2 < 4; ++y2) pm[x][y2] = D[sw16(c0 + x, c0 + y2)];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t != pv)
+#pragma unroll
+                for (int x = 0; x < 4; ++x) bi[t][x] = D[sw16(q + 4 * t, c0 + x)];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) bj[x] = D[sw16(j, c0 + x)];
+        // Pi = [[A^-1 + E S^-1 E^T, -E S^-1], [-S^-1 E^T, S^-1]], E = A^-1 B
+        const double da = pm[0][0] * pm[1][1] - pm[1][0] * pm[1][0];
+        const double ida = rcp_nr(da);
+        const double ai00 = pm[1][1] * ida, ai01 = -pm[1][0] * ida, ai11 = pm[0][0] * ida;
+        const double b00 = pm[0][2], b01 = pm[0][3], b10 = pm[1][2], b11 = pm[1][3];
+        const double e00 = ai00 * b00 + ai01 * b10, e01 = ai00 * b01 + ai01 * b11;
+        const double e10 = ai01 * b00 + ai11 * b10, e11 = ai01 * b01 + ai11 * b11;
+        const double s00 = pm[2][2] - (b00 * e00 + b10 * e10), s01 = pm[2][3] - (b00 * e01 + b10 * e11);
+        const double s11 = pm[3][3] - (b01 * e01 + b11 * e11);
+        const double ds = s00 * s11 - s01 * s01;
+        if (lane == 0 && !(da != 0.0 && isfinite(da) && ds != 0.0 && isfinite(ds) && pm[0][0] != 0.0)) *bad = 1;
+        const double ids = rcp_nr(ds);
+        const double si00 = s11 * ids, si01 = -s01 * ids, si11 = s00 * ids;
+        const double f00 = e00 * si00 + e01 * si01, f01 = e00 * si01 + e01 * si11;
+        const double f10 = e10 * si00 + e11 * si01, f11 = e10 * si01 + e11 * si11;
+        const double Pi[4][4] = {{ai00 + (f00 * e00 + f01 * e01), ai01 + (f00 * e10 + f01 * e11), -f00, -f01},
+                                 {ai01 + (f00 * e10 + f01 * e11), ai11 + (f10 * e10 + f11 * e11), -f10, -f11},
+                                 {-f00, -f10, si00, si01},
+                                 {-f01, -f11, si01, si11}};
+        const bool jP = (j >> 2) == pv;
+        const int jr = j & 3;
+        double w[4], u[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) w[x] = jP ? (x == jr ? 1.0 : 0.0) : bj[x];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const double c = ((Pi[x][0] * w[0] + Pi[x][1] * w[1]) + Pi[x][2] * w[2]) + Pi[x][3] * w[3];
+            u[x] = jP ? c : -c;
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            bi0[t] = D[sw16(q + 4 * t, c0)];
-            bi1[t] = D[sw16(q + 4 * t, c0 + 1)];
-        }
-        const double bj0 = D[sw16(j, c0)], bj1 = D[sw16(j, c0 + 1)];
-        // the two reciprocals are independent (d1 = det / p00, 1 / d1 = p00 / det): one latency, not two
-        const double det = p00 * p11 - p10 * p10;
-        const double i0 = rcp_nr(p00), idet = rcp_nr(det);
-        const double l = p10 * i0;
-        const double d1 = det * i0;
-        const double i1 = p00 * idet;
-        if (lane == 0 && !(p00 != 0.0 && isfinite(p00) && d1 != 0.0 && isfinite(d1))) *bad = 1;
-        const double uj = __builtin_fma(-l, bj0, bj1);
-        const double lb0 = bj0 * i0, lb1 = uj * i1;   // L_B row j (used when j is below the pivot)
-        // Lower part (i >= j) as one fused form x' = bi0 C0 + ui C1 + (j trailing ? x : 0) with per-column
-        // coefficients: trailing j > c0+1: (-lb0, -lb1) (the Schur update); j = c0: (i0, 0) (L column c0, and
-        // L[c0+1][c0] = p10 i0 = l); j = c0+1: (0, i1) (L column c0+1).  Upper part (i < j): the W = L^-1 rows.
-        // Every candidate is computed, then selected (v_cndmask): the cases are mutually exclusive, and a
-        // branchy form costs more in exec-mask flow than the arithmetic it skips.
-        const bool jA = j > c0 + 1, jC = j == c0 + 1;
-        const double C0 = jA ? -lb0 : (j == c0 ? i0 : 0.0);
-        const double C1 = jA ? -lb1 : (jC ? i1 : 0.0);
+            if (t == pv) {
+                cur[t] = -(q == 0 ? u[0] : q == 1 ? u[1] : q == 2 ? u[2] : u[3]);
+            } else {
+                double v = jP ? 0.0 : cur[t];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i = q + 4 * t;
-            const double x = cur[t];
-            const double ui = __builtin_fma(-l, bi0[t], bi1[t]);
-            const double lowv = __builtin_fma(bi0[t], C0, __builtin_fma(ui, C1, jA ? x : 0.0));
-            const double w0 = i == c0 ? 1.0 : (i == c0 + 1 ? 0.0 : bi0[t]);
-            const double w1 = i == c0 ? -l : (i == c0 + 1 ? 1.0 : ui);
-            const double base = i < c0 ? x : 0.0;
-            const double upv = jC ? __builtin_fma(-l, w0, base) : __builtin_fma(-lb0, w0, __builtin_fma(-lb1, w1, base));
-            const bool lower = i >= j;
-            const bool keep_lo = j < c0 || (i == c0 && j == c0);
-            const double lo_r = keep_lo ? x : ((i == c0 + 1 && jC) ? d1 : lowv);
-            const bool up_set = j > c0 && i <= c0 + 1 && !(i == c0 + 1 && jC);
-            cur[t] = lower ? lo_r : (up_set ? upv : x);
+                for (int x = 3; x >= 0; --x) v = __builtin_fma(bi[t][x], u[x], v);
+                cur[t] = v;
+            }
         }
-        if (j == c0 + 2 || j == c0 + 3) {
+        if ((j >> 2) == pv + 1) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];
         }
         wave_sync<G>();
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];
+    for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = -cur[t];
     wave_sync<G>();
 }
 
-// One wavefront: L_ik = S_ik L_kk^-T diag(d)^-1 (f64 MFMA 16x16x4, four k-steps), in place.
-// A/B operand lane maps: A[l&15][4s + (l>>4)], B[4s + (l>>4)][l&15]; D: col l&15, row (l>>4) + 4i.
-__device__ __forceinline__ void panel16(double *A, const double *Dk, int lane) {
-    v4d acc = {0, 0, 0, 0};
+// One wavefront: S_ij -= S_ik Dinv_k S_jk^T.  Q = Dinv_k S_jk^T by four 16x16x4 f64 MFMAs leaves Q[kq + 4s][rc] in
+// accumulator s of lane (rc, kq) -- exactly the B operand of step s of the second product -- so Q never leaves the
+// registers.  A/B operand lane maps: A[l&15][4s + (l>>4)], B[4s + (l>>4)][l&15]; D: col l&15, row (l>>4) + 4i.
+__device__ __forceinline__ void update16(double *Sij, const double *Sik, const double *Sjk, const double *Dinv, int lane) {
     const int rc = lane & 15, kq = lane >> 4;
+    v4d Q = {0, 0, 0, 0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int kk = 4 * s + kq;
-        const double a = A[sw16(rc, kk)];
-        const double b = kk < rc ? Dk[sw16(kk, rc)] : (kk == rc ? 1.0 : 0.0);   // (L^-T)[kk][col]
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        Q = __builtin_amdgcn_mfma_f64_16x16x4f64(Dinv[sw16(rc, kk)], Sjk[sw16(rc, kk)], Q, 0, 0, 0);
     }
-    const double id = rcp_nr(Dk[sw16(rc, rc)]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) A[sw16(kq + 4 * i, rc)] = acc[i] * id;
-}
-
-// One wavefront: S_ij -= L_ik diag(d) L_jk^T.
-__device__ __forceinline__ void update16(double *Sij, const double *Lik, const double *Ljk, const double *Dk, int lane) {
-    const int rc = lane & 15, kq = lane >> 4;
     v4d acc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = Sij[sw16(kq + 4 * i, rc)];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int kk = 4 * s + kq;
-        const double a = -Lik[sw16(rc, kk)] * Dk[sw16(kk, kk)];
-        const double b = Ljk[sw16(rc, kk)];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Sik[sw16(rc, 4 * s + kq)], Q[s], acc, 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) Sij[sw16(kq + 4 * i, rc)] = acc[i];
 }
@@ -891,37 +901,33 @@ __device__ __forceinline__ void update16(double *Sij, const double *Lik, const d
 constexpr int kLdltThreads = 512;
 constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (the static part is one int)
 
-// Forward substitution of one column (one wavefront): y_i <- L_ii^-1 (y_i - sum_k L_ik y_k) over the row
-// structure, four blocks at a time (lane groups), then the unit lower inverse stored above the diagonal.
+// Forward substitution of one column (one wavefront): z_i = Dinv_i (y_i - sum_k S_ik z_k) over the row structure
+// (descendants, final by then), four blocks at a time (lane groups).
 __device__ __forceinline__ void forward_col(const double *pk, double *y, const BlockPat &P, int i, int lane) {
     const int r16 = lane & 15, grp = lane >> 4;
     double acc = 0;
     for (int q = P.rs_start[i] + grp; q < P.rs_start[i + 1]; q += 4) {
         const int2 e = P.rs[q];
-        const double *Lik = pk + (size_t)e.x * 256;
-        const double *yk = y + 16 * e.y;
+        const double *Sik = pk + (size_t)e.x * 256;
+        const double *zk = y + 16 * e.y;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc += Lik[sw16(r16, m)] * yk[m];
+        for (int m = 0; m < 16; ++m) acc += Sik[sw16(r16, m)] * zk[m];
     }
     acc += __shfl_xor(acc, 16, 64);
     acc += __shfl_xor(acc, 32, 64);
     const double v = y[16 * i + r16] - acc;
     const double *Di = pk + (size_t)P.dslot[i] * 256;
-    double out = v;
+    double out = 0;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const double vm = __shfl(v, m, 16);
-        out += (m < r16 ? Di[sw16(m, r16)] : 0.0) * vm;
-    }
+    for (int m = 0; m < 16; ++m) out += Di[sw16(r16, m)] * __shfl(v, m, 16);
     if (lane < 16) y[16 * i + lane] = out;
 }
 
-// Block LDL^T on the host-planned elimination order, level by level of its elimination tree: the columns of
-// one level are independent (their trailing updates only reach ancestors, at higher levels), so a level's
-// diagonal factors run on separate wavefronts, then its panels, then its trailing updates -- grouped by
-// target block, each group on one wavefront in ascending column order (no two wavefronts write a block).
-// Forward substitution runs beside the panels of each column's level (gathering its row structure: descendants,
-// final by then), backward substitution gathers each column's structure (ancestors) level by level downwards.
+// Block LDL^T on the host-planned elimination order, level by level of its elimination tree: the columns of one level
+// are independent (their trailing updates only reach ancestors, at higher levels), so a level's diagonal inverses run
+// on separate wavefronts, then its trailing updates -- grouped by target block, each group on one wavefront in
+// ascending column order (no two wavefronts write a block) -- beside its columns' forward substitutions.  Backward
+// substitution gathers each column's structure (ancestors) level by level downwards.
 template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
 __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat P, const double *b,
                                                             const double *coef, double *x, double *gscratch,
@@ -937,7 +943,9 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     if (tid == 0) bad = 0;
 #ifdef OMV_LDLT_PROFILE
     const long long t_0 = wall_clock64();
-    long long t_1 = 0, t_2 = 0, t_3 = 0;
+    long long t_1 = 0, t_3 = 0;
+    __shared__ int pf_task[4];   // inverse ticks, forward ticks, inverse count, forward count
+    if (tid < 4) pf_task[tid] = 0;
 #endif
     {
         const double2 *src = (const double2 *)Sp;
@@ -950,7 +958,7 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     }
     __syncthreads();
 #ifdef OMV_LDLT_PROFILE
-    long long pf_fac = 0, pf_pan = 0, pf_upd = 0, tp = wall_clock64();
+    long long pf_fac = 0, pf_upd = 0, tp = wall_clock64();
 #define OMV_LDLT_TICK(acc)                       \
     {                                            \
         const long long tn = wall_clock64();     \
@@ -960,33 +968,35 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 #else
 #define OMV_LDLT_TICK(acc)
 #endif
-    for (int lev = 0; lev < P.n_lev; ++lev) {
-        for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw)
-            factor16<G>(pk + (size_t)P.dslot[P.lev_col[c]] * 256, lane, &bad);
-        __syncthreads();
-        OMV_LDLT_TICK(pf_fac)
-        // panels of the level's columns, and beside them each column's forward substitution (its row structure
-        // holds descendants only, final since their levels): y_i <- L_ii^-1 (y_i - sum_k L_ik y_k), with
-        // W = L_ii^-1 stored transposed above the diagonal
-        const int p0 = P.pt_start[lev], p1 = P.pt_start[lev + 1], c0 = P.lev_start[lev];
-        const int nt = p1 - p0 + P.lev_start[lev + 1] - c0;
-        for (int q = wave; q < nt; q += nw) {
-            if (q < p1 - p0) {
-                const int2 pt = P.pt[p0 + q];
-                panel16(pk + (size_t)pt.x * 256, pk + (size_t)pt.y * 256, lane);
-            } else {
-                forward_col(pk, y, P, P.lev_col[c0 + q - (p1 - p0)], lane);
-            }
+    // Level l: phase A inverts level l's diagonal blocks and, on the other wavefronts, forward-substitutes the columns
+    // of level l - 1 (their inverses and all their descendants' z are final; it is off the factorisation's critical
+    // path); phase B applies level l's trailing updates.  The last level's forward columns follow the loop.
+    for (int lev = 0; lev <= P.n_lev; ++lev) {
+        const int c0 = P.lev_start[min(lev, P.n_lev)], c1 = lev < P.n_lev ? P.lev_start[lev + 1] : c0;
+        const int f0 = lev > 0 ? P.lev_start[lev - 1] : 0, f1 = lev > 0 ? P.lev_start[lev] : 0;
+        const int na = c1 - c0 + f1 - f0;
+        for (int q = wave; q < na; q += nw) {
+#ifdef OMV_LDLT_PROFILE
+            const long long tq = wall_clock64();
+#endif
+            if (q < c1 - c0) inv16<G>(pk + (size_t)P.dslot[P.lev_col[c0 + q]] * 256, lane, &bad);
+            else forward_col(pk, y, P, P.lev_col[f0 + q - (c1 - c0)], lane);
+#ifdef OMV_LDLT_PROFILE
+            if (lane == 0) atomicAdd(q < c1 - c0 ? &pf_task[0] : &pf_task[1], (int)(wall_clock64() - tq));
+            if (lane == 0) atomicAdd(q < c1 - c0 ? &pf_task[2] : &pf_task[3], 1);
+#endif
         }
         __syncthreads();
-        OMV_LDLT_TICK(pf_pan)
+        OMV_LDLT_TICK(pf_fac)
+        if (lev == P.n_lev) break;
+        // the level's trailing updates, grouped by target
         const int g0 = P.ug_start[lev], g1 = P.ug_start[lev + 1];
         if (g1 > g0) {
-            for (int g = g0 + wave; g < g1; g += nw)
-                for (int q = P.ug_task_start[g]; q < P.ug_task_start[g + 1]; ++q) {
-                    const int4 u = P.ug[q];
-                    update16(pk + (size_t)u.x * 256, pk + (size_t)u.y * 256, pk + (size_t)u.z * 256,
-                             pk + (size_t)u.w * 256, lane);
+            for (int q = g0 + wave; q < g1; q += nw)
+                for (int u = P.ug_task_start[q]; u < P.ug_task_start[q + 1]; ++u) {
+                    const int4 t = P.ug[u];
+                    update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
+                             pk + (size_t)t.w * 256, lane);
                 }
             __syncthreads();
         }
@@ -997,42 +1007,35 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     t_1 = wall_clock64();
 #endif
     const int r16 = lane & 15, grp = lane >> 4;
-#ifdef OMV_LDLT_PROFILE
-    t_2 = wall_clock64();
-#endif
-    for (int q = tid; q < nv; q += blockDim.x) y[q] /= pk[(size_t)P.dslot[q >> 4] * 256 + sw16(q & 15, q & 15)];
-    __syncthreads();
-    // backward: x_k = L_kk^-T (z_k - sum_i L_ik^T x_i)
+    // backward: x_k = z_k - Dinv_k sum_i S_ik^T x_i
     for (int lev = P.n_lev - 1; lev >= 0; --lev) {
         for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw) {
             const int k = P.lev_col[c];
             double acc = 0;
             for (int q = P.cs_start[k] + grp; q < P.cs_start[k + 1]; q += 4) {
                 const int2 e = P.cs[q];
-                const double *Lik = pk + (size_t)e.x * 256;
+                const double *Sik = pk + (size_t)e.x * 256;
                 const double *xi = xs + 16 * e.y;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc += Lik[sw16(r, r16)] * xi[r];
+                for (int r = 0; r < 16; ++r) acc += Sik[sw16(r, r16)] * xi[r];
             }
             acc += __shfl_xor(acc, 16, 64);
             acc += __shfl_xor(acc, 32, 64);
-            const double v = y[16 * k + r16] - acc;
             const double *Dk = pk + (size_t)P.dslot[k] * 256;
-            double out = v;
+            double out = 0;
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                const double vm = __shfl(v, m, 16);
-                out += (m > r16 ? Dk[sw16(r16, m)] : 0.0) * vm;
-            }
-            if (lane < 16) xs[16 * k + lane] = out;
+            for (int m = 0; m < 16; ++m) out += Dk[sw16(r16, m)] * __shfl(acc, m, 16);
+            if (lane < 16) xs[16 * k + lane] = y[16 * k + r16] - out;
         }
         __syncthreads();
     }
 #ifdef OMV_LDLT_PROFILE
     t_3 = wall_clock64();
     if (tid == 0)
-        printf("ldlt ticks(100MHz): factor+fwd %lld (diag %lld panel+fwd %lld update %lld) scale %lld bwd %lld slots %d "
-               "levels %d\n", t_1 - t_0, pf_fac, pf_pan, pf_upd, t_2 - t_1, t_3 - t_2, P.n_slots, P.n_lev);
+        printf("ldlt ticks(100MHz): factor+fwd %lld (diag inverse+fwd %lld updates %lld) bwd %lld slots %d levels %d; "
+               "per inverse %.1f per forward col %.1f\n",
+               t_1 - t_0, pf_fac, pf_upd, t_3 - t_1, P.n_slots, P.n_lev, (double)pf_task[0] / max(pf_task[2], 1),
+               (double)pf_task[1] / max(pf_task[3], 1));
 #endif
     for (int q = tid; q < nv; q += blockDim.x) x[16 * P.perm[q >> 4] + (q & 15)] = xs[q];
     if (tid == 0) *fail = bad;
@@ -1548,13 +1551,11 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
                 slot_kr.push_back(perm[i]), slot_kc.push_back(perm[j]);
             }
     for (int k = 0; k < nb; ++k) dslot[k] = slot[(size_t)k * nb + k];
-    // level schedule: columns per level; panel tasks; trailing updates grouped by target block (ascending k)
-    std::vector<int> lev_start(n_lev + 1, 0), lev_col, pt_start(n_lev + 1, 0), ug_start(n_lev + 1, 0), ug_task_start(1, 0);
-    std::vector<int2> pt;
+    // level schedule: columns per level; trailing updates grouped by target block (ascending k)
+    std::vector<int> lev_start(n_lev + 1, 0), lev_col, ug_start(n_lev + 1, 0), ug_task_start(1, 0);
     std::vector<int4> ug;
     for (int l = 0; l < n_lev; ++l) {
         lev_start[l] = (int)lev_col.size();
-        pt_start[l] = (int)pt.size();
         ug_start[l] = (int)ug_task_start.size() - 1;
         std::map<int, std::vector<int4>> by_target;   // target slot -> updates in ascending k
         for (int k = 0; k < nb; ++k) {
@@ -1562,7 +1563,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             lev_col.push_back(k);
             std::vector<int> col;
             for (int i = k + 1; i < nb; ++i)
-                if (pat[(size_t)i * nb + k]) col.push_back(i), pt.push_back(make_int2(slot[(size_t)i * nb + k], dslot[k]));
+                if (pat[(size_t)i * nb + k]) col.push_back(i);
             for (size_t a = 0; a < col.size(); ++a)
                 for (size_t c = 0; c <= a; ++c) {
                     const int i = col[a], j = col[c];
@@ -1576,7 +1577,6 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         }
     }
     lev_start[n_lev] = (int)lev_col.size();
-    pt_start[n_lev] = (int)pt.size();
     ug_start[n_lev] = (int)ug_task_start.size() - 1;
     std::vector<int> rs_start(nb + 1, 0), cs_start(nb + 1, 0);
     std::vector<int2> rs, cs;
@@ -1819,10 +1819,10 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         BlockPat &B = h->BP;
         B.nb = nb, B.n_slots = n_slots, B.n_lev = n_lev;
         B.perm = upv(perm), B.slot_kr = upv(slot_kr), B.slot_kc = upv(slot_kc), B.dslot = upv(dslot);
-        B.lev_start = upv(lev_start), B.lev_col = upv(lev_col), B.pt_start = upv(pt_start), B.pt = upv(pt);
+        B.lev_start = upv(lev_start), B.lev_col = upv(lev_col);
         B.ug_start = upv(ug_start), B.ug_task_start = upv(ug_task_start), B.ug = upv(ug);
         B.rs_start = upv(rs_start), B.rs = upv(rs), B.cs_start = upv(cs_start), B.cs = upv(cs);
-        if (!B.perm || !B.slot_kr || !B.slot_kc || !B.dslot || !B.lev_start || !B.lev_col || !B.pt_start || !B.pt ||
+        if (!B.perm || !B.slot_kr || !B.slot_kc || !B.dslot || !B.lev_start || !B.lev_col ||
             !B.ug_start || !B.ug_task_start || !B.ug || !B.rs_start || !B.rs || !B.cs_start || !B.cs)
             return OMV_ERR_HIP;
     }
