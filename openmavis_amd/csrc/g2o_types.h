@@ -264,7 +264,7 @@ __device__ void log_so3(const double *R, double *w) {
 }
 
 // EdgeInertial::computeError (G2oTypes.cc:502-531)
-__device__ void imu_error(const State &s, const Imu &I, int i, double *e) {
+__device__ void imu_error(const State &s, const Imu &I, int i, double *e, double *eR_out = nullptr) {
     const int k1 = I.kf1[i], k2 = I.kf2[i];
     const float *p = I.pre + (size_t)i * kPF;
     float b1[6];
@@ -283,6 +283,8 @@ __device__ void imu_error(const State &s, const Imu &I, int i, double *e) {
     tr3(dR, dRt);
     mm3(dRt, R1t, A);
     mm3(A, R2, B);
+    if (eR_out)
+        for (int q = 0; q < 9; ++q) eR_out[q] = B[q];
     log_so3(B, e);
     double t[3];
     for (int q = 0; q < 3; ++q) t[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
@@ -385,6 +387,92 @@ __device__ void imu_jacobian(const State &s, const Imu &I, int i, double *J) {
     mm3(Rbw1, Rwb2, A);
     put(6, 18, A, 1.0);
     put(3, 21, Rbw1, 1.0);
+}
+
+// EdgeInertial::linearizeOplus (G2oTypes.cc:533-599) from the rotation error the error pass cached (eR = dR^T Rbw1
+// Rwb2, er = LogSO3(eR): the same values imu_jacobian recomputes), spread over a block's threads: thread 0 forms
+// invJr = InverseRightJacobianSO3(er) and the blocks that use it, thread 1 RightJacobianSO3(JRg dbg), threads 2..9
+// the blocks of the velocity / position rows; J [9][24] in shared memory, zeroed by the caller.  Same arithmetic,
+// entry for entry, as imu_jacobian.
+__device__ void imu_jacobian_par(const State &s, const Imu &I, int i, const double *eR, const double *er, double *J,
+                                 double *RJ) {
+    const int tid = threadIdx.x;
+    const int k1 = I.kf1[i], k2 = I.kf2[i];
+    const float *p = I.pre + (size_t)i * kPF;
+    const double *Rwb1 = s.Rwb + 9 * k1, *Rwb2 = s.Rwb + 9 * k2;
+    auto put = [&](int r0, int c0, const double *B, double sgn) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) J[(r0 + r) * 24 + c0 + c] = sgn * B[3 * r + c];
+    };
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    double Rbw1[9];
+    tr3(Rwb1, Rbw1);
+    if (tid == 1) {
+        float b1[6];
+        for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+        const float dbgf[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+        const double dbg[3] = {(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]};
+        double JRg[9], w3[3];
+        for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q];
+        mv3(JRg, dbg, w3);
+        right_jac(w3, RJ);
+    } else if (tid == 2) {
+        double v[3], w[3], W[9];
+        for (int q = 0; q < 3; ++q) v[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+        mv3(Rbw1, v, w);
+        hat3(w, W);
+        put(3, 0, W, 1.0);
+    } else if (tid == 3) {
+        double v[3], w[3], W[9];
+        for (int q = 0; q < 3; ++q)
+            v[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - 0.5 * g[q] * dt * dt;
+        mv3(Rbw1, v, w);
+        hat3(w, W);
+        put(6, 0, W, 1.0);
+    } else if (tid == 4) {
+        for (int q = 0; q < 3; ++q) J[(6 + q) * 24 + 3 + q] = -1.0;
+        put(3, 6, Rbw1, -1.0);
+        put(3, 21, Rbw1, 1.0);
+    } else if (tid == 5) {
+        put(6, 6, Rbw1, -dt);
+    } else if (tid == 6) {
+        double B[9];
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JVg + q];
+        put(3, 9, B, -1.0);
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JVa + q];
+        put(3, 12, B, -1.0);
+    } else if (tid == 7) {
+        double B[9];
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JPg + q];
+        put(6, 9, B, -1.0);
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JPa + q];
+        put(6, 12, B, -1.0);
+    } else if (tid == 8) {
+        double A[9];
+        mm3(Rbw1, Rwb2, A);
+        put(6, 18, A, 1.0);
+    }
+    double invJr[9];
+    if (tid == 0) {
+        inv_right_jac(er, invJr);
+        double R2t[9], A[9], B[9];
+        tr3(Rwb2, R2t);
+        mm3(invJr, R2t, A);
+        mm3(A, Rwb1, B);
+        put(0, 0, B, -1.0);
+        put(0, 15, invJr, 1.0);
+    }
+    __syncthreads();   // RJ
+    if (tid == 0) {
+        double eRt[9], A[9], B[9], Jg[9], JRg[9];
+        for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q];
+        tr3(eR, eRt);
+        mm3(invJr, eRt, A);
+        mm3(A, RJ, B);
+        mm3(B, JRg, Jg);
+        put(0, 9, Jg, -1.0);
+    }
 }
 
 __device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:802-815)

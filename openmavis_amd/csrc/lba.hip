@@ -48,6 +48,7 @@ namespace {
 
 using namespace omv_g2o;
 
+constexpr int kGrpEdges = 256;   // edges per buildSystem landmark group / pose chunk (one per thread)
 constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / back-substitution)          // keyframes a workgroup may touch for LDS pre-reduction
 
 #define HIP_OK(x)                                                                    \
@@ -124,7 +125,7 @@ __device__ __forceinline__ void imu_err_block(double *sh, State s, Imu I, double
     double r0 = 0;
     if (i < I.n) {
         double e[9];
-        imu_error(s, I, i, e);
+        imu_error(s, I, i, e, err9 + (size_t)10 * I.n + 9 * (size_t)i);   // + the rotation error for buildSystem
         const double *W = I.info9 + (size_t)i * 81;
         double c2 = 0;
         for (int r = 0; r < 9; ++r) {
@@ -331,6 +332,7 @@ struct Land {
     double *bl;              // [P][3]
     double *Hpl;             // [nslots][18] pose rows x point cols
     int n;
+    const int *grp_pt;       // [n_grp+1] buildSystem landmark groups: whole landmarks, <= kGrpEdges edges each
 };
 
 // Work lists of the deterministic reductions (host-built once per problem, every list in ascending order).
@@ -338,8 +340,8 @@ struct Land {
 // reduced-system block's assembly (the next launch) sums the chunk partials in chunk order, so every value is
 // identical run to run whatever the scheduling.
 struct Gather {
-    const int4 *pchunk;      // pose chunks: (keyframe, first, end) over kf_edge
-    const int *kf_edge;      // per optimisable keyframe, its visual edges
+    const int4 *pchunk;      // pose chunks: (keyframe, first, end) over the keyframe's edges
+    const int *kf_edge;      // [n_pchunk][kGrpEdges] each pose chunk's visual edges (ascending; -1 pads)
     const int *pc_start;     // [nb+1] per keyframe: its pose chunks
     double *pose_part;       // [n_pchunk][27]: 21 lower-triangle JpT W Jp sums + 6 JpT W e
     const int *schunk_order; // launch order of the Schur chunks (XCD-contiguous runs of neighbouring blocks)
@@ -428,44 +430,6 @@ __device__ __forceinline__ double rows_om(const double *A, int ia, int lda, cons
     return t;
 }
 
-// Landmark part of buildSystem: one thread per landmark (edges in landmark-major order): Hll, bl and the
-// per-(landmark, keyframe) Hpl blocks, each summed in edge order.  The keyframe-diagonal terms are gathered per
-// keyframe by build_pose_kernel (fixed order, no atomics).
-__device__ __forceinline__ void build_land_block(int blk, Rig rig, State s, Edges E, Land L, double delta,
-                                                 double dsqr, double delta_st, double dsqr_st, const double *err,
-                                                 const double *err3, const double *chi2) {
-    const int p = blk * blockDim.x + threadIdx.x;
-    if (p >= L.n) return;
-    double Hll[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
-    double Hpl[18];
-    int cur_slot = -1;
-    for (int e = L.edge_start[p]; e < L.edge_start[p + 1]; ++e) {
-        double JX[9], JP[18], w, om[3];
-        const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            bl[r] += rows_om(JX, r, 3, om, nr);
-#pragma unroll
-            for (int q = 0; q < 3; ++q) Hll[3 * r + q] += w * rows2(JX, r, JX, q, 3, 3, nr);
-        }
-        const int slot = E.slot[e];
-        if (slot != cur_slot) {
-            if (cur_slot >= 0)
-                for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
-            for (int q = 0; q < 18; ++q) Hpl[q] = 0;
-            cur_slot = slot;
-        }
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += w * rows2(JP, r, JX, q, 6, 3, nr);
-    }
-    if (cur_slot >= 0)
-        for (int q = 0; q < 18; ++q) L.Hpl[(size_t)cur_slot * 18 + q] = Hpl[q];
-    for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = Hll[q];
-    for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = bl[q];
-}
-
 // Fixed-order wavefront sum (xor tree): the wave total in every lane; callers combine the waves in order.
 __device__ __forceinline__ double wave_sum_fixed(double v) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -498,31 +462,125 @@ __device__ __forceinline__ double wave_transpose_sum(const double (&v)[N], int l
     return a[0];
 }
 
-// Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= 256 edges of one keyframe, ascending) per
-// 64-thread block: lane l takes edges l, l+64, ...; 21 + 6 sums, a fixed-order wave reduction, one partial row.
-// The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled (schur_kernel).
-__device__ __forceinline__ void pose_chunk_block(int ch, Rig rig, State s, Edges E, Gather G, double delta, double dsqr,
-                                                 double delta_st, double dsqr_st, const double *err,
-                                                 const double *err3, const double *chi2) {
-    const int4 pc = G.pchunk[ch];
+// Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= kGrpEdges edges of one keyframe, ascending) per
+// block, one edge per thread: 21 + 6 terms, a fixed-order reduction (transposing wave sums, then the waves in order),
+// one partial row.  The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled.
+__device__ __forceinline__ void pose_chunk_block(int ch, double *wsum, Rig rig, State s, Edges E, Gather G,
+                                                 double delta, double dsqr, double delta_st, double dsqr_st,
+                                                 const double *err, const double *err3, const double *chi2) {
     double acc[27];
 #pragma unroll
     for (int q = 0; q < 27; ++q) acc[q] = 0;
-    for (int i = pc.y + (int)threadIdx.x; i < pc.z; i += blockDim.x) {
-        const int e = G.kf_edge[i];
+    const int e = G.kf_edge[(size_t)ch * kGrpEdges + threadIdx.x];
+    if (e >= 0) {
         double JX[9], JP[18], w, om[3];
         const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
         int q = 0;
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
-            for (int c = 0; c <= r; ++c) acc[q++] += w * rows2(JP, r, JP, c, 6, 6, nr);
+            for (int c = 0; c <= r; ++c) acc[q++] = w * rows2(JP, r, JP, c, 6, 6, nr);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) acc[21 + r] += rows_om(JP, r, 6, om, nr);
+        for (int r = 0; r < 6; ++r) acc[21 + r] = rows_om(JP, r, 6, om, nr);
     }
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double mine = wave_transpose_sum(acc, lane);
-    if (lane < 27) G.pose_part[(size_t)ch * 27 + lane] = mine;
+    if (lane < 27) wsum[27 * wave + lane] = mine;
+    __syncthreads();
+    if (threadIdx.x < 27) {
+        double t = wsum[threadIdx.x];
+        for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) t += wsum[27 * w2 + threadIdx.x];
+        G.pose_part[(size_t)ch * 27 + threadIdx.x] = t;
+    }
+}
+
+// Landmark part of buildSystem for one group of whole landmarks (<= kGrpEdges edges, landmark-major): thread t forms
+// the Jacobians of the group's edge t and its 30 landmark terms (Hll 9, bl 3, Hpl 18) in LDS, then thread p sums the
+// terms of landmark p's edges in edge order (Hpl per keyframe slot) -- the sums and their order of one thread per
+// landmark walking its edges, with the edge chains run in parallel.  A group of one landmark with more edges than the
+// group holds is walked by its first thread alone.
+constexpr int kLandTerms = 30;
+struct LandAcc {
+    double Hll[9], bl[3], Hpl[18];
+    int slot;
+};
+// thread tid's terms of edge e into the group's LDS table (value-major: conflict-free)
+__device__ __forceinline__ void land_terms(int e, int tid, double *T, const Rig &rig, const State &s, const Edges &E,
+                                           double delta, double dsqr, double delta_st, double dsqr_st,
+                                           const double *err, const double *err3, const double *chi2) {
+    double JX[9], JP[18], w, om[3];
+    const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        T[(9 + r) * kGrpEdges + tid] = rows_om(JX, r, 3, om, nr);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) T[(3 * r + q) * kGrpEdges + tid] = w * rows2(JX, r, JX, q, 3, 3, nr);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) T[(12 + 3 * r + q) * kGrpEdges + tid] = w * rows2(JP, r, JX, q, 6, 3, nr);
+}
+// edges [f0, f1) of one landmark (table rows f - base) added to its sums in edge order; a finished slot's Hpl stored
+__device__ __forceinline__ void land_accumulate(LandAcc &a, const double *T, int base, int f0, int f1, const Edges &E,
+                                                const Land &L) {
+    for (int f = f0; f < f1; ++f) {
+        const int le = f - base;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a.bl[q] += T[(9 + q) * kGrpEdges + le];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) a.Hll[q] += T[q * kGrpEdges + le];
+        const int slot = E.slot[f];
+        if (slot != a.slot) {
+            if (a.slot >= 0)
+                for (int q = 0; q < 18; ++q) L.Hpl[(size_t)a.slot * 18 + q] = a.Hpl[q];
+            for (int q = 0; q < 18; ++q) a.Hpl[q] = 0;
+            a.slot = slot;
+        }
+#pragma unroll
+        for (int q = 0; q < 18; ++q) a.Hpl[q] += T[(12 + q) * kGrpEdges + le];
+    }
+}
+__device__ __forceinline__ void land_store(const LandAcc &a, int p, const Land &L) {
+    if (a.slot >= 0)
+        for (int q = 0; q < 18; ++q) L.Hpl[(size_t)a.slot * 18 + q] = a.Hpl[q];
+    for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = a.Hll[q];
+    for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = a.bl[q];
+}
+
+__device__ __forceinline__ void land_group(int g, double *T, LandAcc *big_acc, Rig rig, State s, Edges E, Land L,
+                                           double delta, double dsqr, double delta_st, double dsqr_st,
+                                           const double *err, const double *err3, const double *chi2) {
+    const int p0 = L.grp_pt[g], p1 = L.grp_pt[g + 1];
+    const int e0 = L.edge_start[p0], e1 = L.edge_start[p1];
+    const int tid = threadIdx.x;
+    if (e1 - e0 <= kGrpEdges) {
+        if (e0 + tid < e1) land_terms(e0 + tid, tid, T, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+        __syncthreads();
+        const int p = p0 + tid;
+        if (p >= p1) return;
+        LandAcc a{};
+        a.slot = -1;
+        land_accumulate(a, T, e0, L.edge_start[p], L.edge_start[p + 1], E, L);
+        land_store(a, p, L);
+        return;
+    }
+    // one landmark with more edges than a group holds: windows of kGrpEdges, thread 0 carries the sums in LDS
+    if (tid == 0) {
+        *big_acc = LandAcc{};
+        big_acc->slot = -1;
+    }
+    for (int base = e0; base < e1; base += kGrpEdges) {
+        if (base + tid < e1) land_terms(base + tid, tid, T, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+        __syncthreads();
+        if (tid == 0) {
+            LandAcc a = *big_acc;
+            land_accumulate(a, T, base, base, min(base + kGrpEdges, e1), E, L);
+            *big_acc = a;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) land_store(*big_acc, p0, L);
 }
 
 // ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
@@ -534,15 +592,17 @@ constexpr int kImuLoc = 30, kImuContrib = kImuLoc * kImuLoc + kImuLoc;
 __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Imu I, double delta, double dsqr,
                                                   const double *err9, double *contrib) {
     double *J = sm, *WJ = sm + 216, *om = sm + 432;   // J (9 x 24), Omega' J (9 x 24), -Omega' e
-    const int lane = threadIdx.x;
-    if (lane == 0) imu_jacobian(s, I, i, J);
+    const int lane = threadIdx.x, nt = blockDim.x;
+    for (int q = lane; q < 216; q += nt) J[q] = 0;
+    __syncthreads();
+    imu_jacobian_par(s, I, i, err9 + (size_t)10 * I.n + 9 * (size_t)i, err9 + 9 * (size_t)i, J, WJ);   // WJ: RJ scratch
     __syncthreads();
     const double *e = err9 + 9 * i;
     const double c2 = err9[(size_t)9 * I.n + i];
     double r0, r1 = 1.0;
     if (I.robust[i]) huber(c2, delta, dsqr, r0, r1);
     const double *W = I.info9 + (size_t)i * 81;
-    for (int q = lane; q < 216; q += 64) {
+    for (int q = lane; q < 216; q += nt) {
         const int r = q / 24, c = q % 24;
         double t = 0;
         for (int k = 0; k < 9; ++k) t += W[r * 9 + k] * J[k * 24 + c];
@@ -557,7 +617,7 @@ __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Im
     const int k1 = I.kf1[i], k2 = I.kf2[i];
     double *Hc = contrib + (size_t)i * kImuContrib, *bc = Hc + kImuLoc * kImuLoc;
     const double *Ig = I.infoG + 9 * i, *Ia = I.infoA + 9 * i;
-    for (int q = lane; q < kImuLoc * kImuLoc; q += 64) {
+    for (int q = lane; q < kImuLoc * kImuLoc; q += nt) {
         const int a = q / kImuLoc, b = q % kImuLoc;
         double t = 0;
         if (a < 24 && b < 24)
@@ -594,22 +654,32 @@ __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Im
     }
 }
 
-// buildSystem in one launch of 64-thread blocks: [0, n_land) the landmark blocks (Hll, bl, Hpl per slot),
-// [n_land, n_land + n_pchunk) the keyframe-diagonal pose chunks, then one block per inertial edge (its 30 x 30
-// quadratic form).  Nothing is accumulated across blocks: the reduced system is assembled per trial by
-// schur_kernel from these per-landmark, per-chunk and per-edge parts.
-__global__ void __launch_bounds__(kLandWG) build_kernel(Rig rig, State s, Edges E, Land L, Gather G, Imu I, int n_land,
-                                                        int n_pchunk, double delta, double dsqr, double delta_st,
-                                                        double dsqr_st, double delta_imu, double dsqr_imu,
-                                                        const double *err, const double *err3, const double *chi2,
-                                                        const double *err9, double *contrib, const LmCtl *ctl) {
+// buildSystem in two launches of 256-thread blocks, nothing accumulated across blocks (the reduced system is assembled
+// per trial from these per-landmark, per-chunk and per-edge parts): build_land_kernel, one block per landmark group
+// (Hll, bl, Hpl per slot); build_kernel, blocks [0, n_pchunk) the keyframe-diagonal pose chunks, then one block per
+// inertial edge (its 30 x 30 quadratic form).
+__global__ void __launch_bounds__(kGrpEdges) build_land_kernel(Rig rig, State s, Edges E, Land L, int n_grp, double delta,
+                                                               double dsqr, double delta_st, double dsqr_st,
+                                                               const double *err, const double *err3, const double *chi2,
+                                                               const LmCtl *ctl) {
+    __shared__ double T[kLandTerms * kGrpEdges];
+    __shared__ LandAcc big_acc;
+    if (!gate_open(ctl, kGateBuild)) return;
+    const int g = omv::xcd_block(n_grp);
+    if (g < 0) return;
+    land_group(g, T, &big_acc, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+}
+
+__global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s, Edges E, Gather G, Imu I, int n_pchunk,
+                                                          double delta, double dsqr, double delta_st, double dsqr_st,
+                                                          double delta_imu, double dsqr_imu, const double *err,
+                                                          const double *err3, const double *chi2, const double *err9,
+                                                          double *contrib, const LmCtl *ctl, int blk0) {
     __shared__ double sm[441];
     if (!gate_open(ctl, kGateBuild)) return;
-    const int blk = blockIdx.x;
-    if (blk < n_land) build_land_block(blk, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-    else if (blk < n_land + n_pchunk)
-        pose_chunk_block(blk - n_land, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-    else imu_contrib_block(blk - n_land - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
+    const int blk = blockIdx.x + blk0;
+    if (blk < n_pchunk) pose_chunk_block(blk, sm, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+    else imu_contrib_block(blk - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
 }
 
 // ---- trial: the reduced system, assembled and Schur-complemented per block -----------------------------
@@ -1331,7 +1401,7 @@ struct omv_lba {
     BlockPat BP{};
     Gather G{};
     double *d_imu_contrib = nullptr;   // [n_imu][30 x 30 + 30] per-edge inertial contributions
-    int n_wg_land = 0, n_wg_edge = 0, n_pchunk = 0, n_schunk = 0;
+    int n_wg_land = 0, n_wg_edge = 0, n_pchunk = 0, n_schunk = 0, n_lgrp = 0;
     // device epilogue (single rank): perm_edge / perm_pt / trackDepth in device order, one staging block
     // [state without points | points in caller order | chi2 in caller order | outlier flags in caller order]
     int *d_perm_edge = nullptr, *d_perm_pt = nullptr;
@@ -1349,6 +1419,8 @@ struct omv_lba {
     LmCtl *h_ctl = nullptr;    // pinned copy: the one read-back per optimize()
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;   // one LM step (trial, and buildSystem when an iteration starts)
+    hipGraph_t step4_graph = nullptr;
+    hipGraphExec_t step4_exec = nullptr;  // four LM steps in one launch (no launch gap between them)
     bool timing = false;       // direct launches with per-stage events instead of the captured step
     bool host_lm = false;      // force the host-driven LM loop (parity checks of the device control)
     double *d_S = nullptr, *d_coef = nullptr, *d_x = nullptr, *d_scratch = nullptr;
@@ -1381,7 +1453,10 @@ static void free_problem(omv_lba *h) {
     h->h_stage = nullptr, h->stage_bytes = 0;
     if (h->step_exec) (void)hipGraphExecDestroy(h->step_exec);
     if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
+    if (h->step4_exec) (void)hipGraphExecDestroy(h->step4_exec);
+    if (h->step4_graph) (void)hipGraphDestroy(h->step4_graph);
     h->step_exec = nullptr, h->step_graph = nullptr;   // the captured step holds the old problem's pointers
+    h->step4_exec = nullptr, h->step4_graph = nullptr;
 }
 
 extern "C" {
@@ -1416,6 +1491,8 @@ omv_status omv_lba_destroy(omv_lba *h) {
     if (h->d_ctl) (void)hipFree(h->d_ctl);
     if (h->step_exec) (void)hipGraphExecDestroy(h->step_exec);
     if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
+    if (h->step4_exec) (void)hipGraphExecDestroy(h->step4_exec);
+    if (h->step4_graph) (void)hipGraphDestroy(h->step4_graph);
     delete h;
     return OMV_OK;
 }
@@ -1639,10 +1716,14 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         for (int e = 0; e < E; ++e)
             if (e_kf[e] < nb) kf_edge[fe[e_kf[e]]++] = e;
     }
+    std::vector<int> kf_edge_pad;   // per chunk its edges, padded to kGrpEdges (one per thread)
     for (int k = 0; k < nb; ++k) {
         pc_start[k] = (int)pchunk.size();
-        for (int q = kf_edge_start[k]; q < kf_edge_start[k + 1]; q += 256)
-            pchunk.push_back(make_int4(k, q, std::min(q + 256, kf_edge_start[k + 1]), 0));
+        for (int q = kf_edge_start[k]; q < kf_edge_start[k + 1]; q += kGrpEdges) {
+            const int qe = std::min(q + kGrpEdges, kf_edge_start[k + 1]);
+            pchunk.push_back(make_int4(k, q, qe, 0));
+            for (int r = 0; r < kGrpEdges; ++r) kf_edge_pad.push_back(q + r < qe ? kf_edge[q + r] : -1);
+        }
     }
     pc_start[nb] = (int)pchunk.size();
     h->n_pchunk = (int)pchunk.size();
@@ -1767,7 +1848,20 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         if (h->n_slots > 0) HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
         if (h->n_slots > 0) HIP_OK(up(d_slot_pt, slot_pt.data(), h->n_slots));
     }
-    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_slot_pt, d_Hll, d_bl, d_Hpl, P};
+    // buildSystem landmark groups: whole landmarks in landmark order, at most kGrpEdges edges per group (a landmark
+    // with more edges forms a group of its own)
+    std::vector<int> grp_pt(1, 0);
+    for (int q = 0; q < P;) {
+        int r = q + 1;
+        while (r < P && pt_edge[r + 1] - pt_edge[q] <= kGrpEdges) ++r;
+        grp_pt.push_back(r);
+        q = r;
+    }
+    h->n_lgrp = (int)grp_pt.size() - 1;
+    const int *d_grp_pt = dalloc<int>(ow, grp_pt.size());
+    if (!d_grp_pt) return OMV_ERR_HIP;
+    HIP_OK(up(const_cast<int *>(d_grp_pt), grp_pt.data(), grp_pt.size()));
+    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_slot_pt, d_Hll, d_bl, d_Hpl, P, d_grp_pt};
     h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
     h->d_offA = dalloc<int>(ow, K);
     HIP_OK(up(h->d_offP, offP.data(), K));
@@ -1804,7 +1898,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     };
     {
         Gather &g = h->G;
-        g.pchunk = upv(pchunk), g.kf_edge = upv(kf_edge), g.pc_start = upv(pc_start);
+        g.pchunk = upv(pchunk), g.kf_edge = upv(kf_edge_pad), g.pc_start = upv(pc_start);
         g.schunk_order = upv(schunk_order), g.tr = upv(tr), g.sc_start = upv(sc_start);
         g.imu_blk = upv(imu_blk), g.ib_start = upv(ib_start), g.imu_vec = upv(imu_vec), g.iv_start = upv(iv_start);
         g.pose_part = dalloc<double>(ow, (size_t)std::max(1, h->n_pchunk) * 27);
@@ -1831,7 +1925,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_err = dalloc<double>(ow, 2 * (size_t)E);
     h->d_chi2 = dalloc<double>(ow, E);
     h->d_err3 = dalloc<double>(ow, E);
-    h->d_err9 = dalloc<double>(ow, 10 * (size_t)NI);
+    h->d_err9 = dalloc<double>(ow, 19 * (size_t)NI);   // [9n errors | n chi2 | 9n rotation errors eR]
     h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
     h->d_imu_partial = dalloc<double>(ow, 1);
     h->d_partial_a = dalloc<double>(ow, std::max(1, h->n_wg_edge));
@@ -1971,22 +2065,39 @@ static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2);
 
 // buildSystem at state A: the landmark blocks, the keyframe-diagonal pose chunks and the inertial edges' quadratic
 // forms in one launch (every part a fixed-order sum: the system is identical run to run).
-static void launch_build(omv_lba *h, const State &A, const LmCtl *c) {
+// buildSystem at state A: the landmark groups, then the keyframe-diagonal pose chunks and the inertial quadratic
+// forms (every part a fixed-order sum: the system is identical run to run).  A forked graph branch for the second
+// launch was measured slower (its fork / join cost more than the overlap gained).
+static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
     const int n_imu_blk = h->imu_here ? h->n_imu : 0;
-    const int blocks = h->n_wg_land + h->n_pchunk + n_imu_blk;
-    if (blocks > 0)
-        build_kernel<<<blocks, kLandWG, 0, h->stream>>>(h->rig, A, h->E, h->L, h->G, h->I, h->n_wg_land, h->n_pchunk,
-                                                        h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu,
-                                                        h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2, h->d_err9,
-                                                        h->d_imu_contrib, c);
+    if (h->n_lgrp > 0)
+        build_land_kernel<<<omv::xcd_grid(h->n_lgrp), kGrpEdges, 0, h->stream>>>(
+            h->rig, A, h->E, h->L, h->n_lgrp, h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err, h->d_err3,
+            h->d_chi2, c);
+    auto go = [&](int b0, int nblk) {
+        if (nblk > 0)
+            build_kernel<<<nblk, kGrpEdges, 0, h->stream>>>(h->rig, A, h->E, h->G, h->I, h->n_pchunk, h->delta_mono,
+                                                            h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu,
+                                                            h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2, h->d_err9,
+                                                            h->d_imu_contrib, c, b0);
+    };
+#ifdef OMV_BUILD_SPLIT   // profiling variant: the pose-chunk and inertial parts as two launches
+    go(0, h->n_pchunk);
+    go(h->n_pchunk, n_imu_blk);
+#else
+    go(0, h->n_pchunk + n_imu_blk);
+#endif
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
 }
 
 // The trial's reduced system (H + lambda I minus the landmark Schur terms, b, the Schur right-hand side) in one
 // launch; lambda on the pose diagonal once (rank 0 of a sharded solve), every rank damps its own landmarks.
-static void launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
+static omv_status launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
     schur_kernel<<<omv::xcd_grid(h->n_schunk), 256, 0, h->stream>>>(h->L, h->G, h->n_schunk, lambda, c);
     assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, lambda, h->rank == 0 ? 1 : 0, h->d_S,
                                                           h->d_bb, h->d_coef, c);
+    return OMV_OK;
 }
 
 static void launch_ldlt(omv_lba *h, const LmCtl *c) {
@@ -2017,9 +2128,9 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     start.copy_src = B.Rwb, start.copy_dst = A.Rwb, start.copy_n = h->state_doubles();
     if ((rs = lba_errors(h, A, c, kGateErrA, true, start)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[0], st));
-    launch_build(h, A, c);
+    if ((rs = launch_build(h, A, c)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
-    launch_schur(h, 0.0, c);
+    if ((rs = launch_schur(h, 0.0, c)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
     launch_ldlt(h, c);
     if (ev) HIP_OK(hipEventRecord(ev[3], st));
@@ -2052,31 +2163,39 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
     ctl_init_kernel<<<1, 256, 0, st>>>(h->d_ctl, h->d_partial, nmb, h->d_imu_partial, o->opt_it, o->max_trials,
                                        o->lambda_init);
     HIP_OK(hipGetLastError());
-    if (!h->timing && !h->step_exec) {   // capture one step (the problem's pointers are fixed until set_problem)
-        HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        rs = lba_step(h, nullptr);
-        hipGraph_t g = nullptr;
-        const hipError_t ce = hipStreamEndCapture(st, &g);
-        if (rs != OMV_OK) return rs;
-        if (ce != hipSuccess) {
-            fprintf(stderr, "omv: LM step capture failed: %s\n", hipGetErrorString(ce));
-            return OMV_ERR_HIP;
+    if (!h->timing && !h->step_exec) {   // capture one step and four steps (the problem's pointers are fixed
+                                         // until set_problem); a batch is launched as 4-step graphs + single steps
+        for (int n : {1, 4}) {
+            HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            for (int q = 0; q < n && rs == OMV_OK; ++q) rs = lba_step(h, nullptr);
+            hipGraph_t g = nullptr;
+            const hipError_t ce = hipStreamEndCapture(st, &g);
+            if (rs != OMV_OK) return rs;
+            if (ce != hipSuccess) {
+                fprintf(stderr, "omv: LM step capture failed: %s\n", hipGetErrorString(ce));
+                return OMV_ERR_HIP;
+            }
+            (n == 1 ? h->step_graph : h->step4_graph) = g;
+            HIP_OK(hipGraphInstantiate(n == 1 ? &h->step_exec : &h->step4_exec, g, nullptr, nullptr, 0));
         }
-        h->step_graph = g;
-        HIP_OK(hipGraphInstantiate(&h->step_exec, g, nullptr, nullptr, 0));
     }
     const int max_steps = std::max(0, o->opt_it) * std::max(1, o->max_trials);
     std::vector<std::array<hipEvent_t, 5>> evs;
     int launched = 0, batch = std::min(std::max(0, o->opt_it), max_steps);
     while (true) {
-        for (int i = 0; i < batch; ++i) {
+        for (int i = 0; i < batch;) {
             if (h->timing) {
                 std::array<hipEvent_t, 5> e{};
                 for (auto &x : e) HIP_OK(hipEventCreate(&x));
                 evs.push_back(e);
                 if ((rs = lba_step(h, evs.back().data())) != OMV_OK) return rs;
+                ++i;
+            } else if (i + 4 <= batch) {
+                HIP_OK(hipGraphLaunch(h->step4_exec, st));
+                i += 4;
             } else {
                 HIP_OK(hipGraphLaunch(h->step_exec, st));
+                ++i;
             }
         }
         launched += batch;
@@ -2145,7 +2264,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         const double iniChi = currentChi;
         // buildSystem
         HIP_OK(hipEventRecord(h->ev[0], st));
-        launch_build(h, A, nullptr);
+        if ((rs = launch_build(h, A, nullptr)) != OMV_OK) return rs;
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -2159,7 +2278,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         bool build_timed = false;   // the build's events complete before the first trial's read-back
         do {
             HIP_OK(hipEventRecord(h->ev[2], st));
-            launch_schur(h, lambda, nullptr);
+            if ((rs = launch_schur(h, lambda, nullptr)) != OMV_OK) return rs;
             // one exchange: sum the partial reduced systems [blocks | b | Schur rhs] of the landmark shards
             if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
             HIP_OK(hipEventRecord(h->ev[3], st));
