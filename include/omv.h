@@ -474,19 +474,24 @@ omv_status omv_lba_reset(omv_lba *h);
  * with omv_lba_enable_timing(h, 1) (direct launches with events instead of the captured LM step). */
 omv_status omv_lba_stage_ms(omv_lba *h, double *ms4, int *trials);
 omv_status omv_lba_enable_timing(omv_lba *h, int on);
-/* LM driver on one rank: 0 (default) keeps g2o's accept / reject / lambda / stop logic on the device (one
- * captured hipGraph per trial, one read-back per optimize); 1 runs it on the host with a read-back per trial
- * (the driver the sharded solve uses).  Both make the same decisions (tests/test_lba_gpu.py). */
+/* LM driver: 0 (default) keeps g2o's accept / reject / lambda / stop logic on the device (on one rank the steps
+ * are captured hipGraphs of four; a sharded solve launches the same gated steps directly, its collectives called
+ * in stream order), one control read-back per batch of steps; 1 runs it on the host with a read-back per trial.
+ * Both make the same decisions (tests/test_lba_gpu.py). */
 omv_status omv_lba_set_driver(omv_lba *h, int host_driven);
+/* Host waits (stream synchronisations) of the last omv_lba_optimize's LM loop and its trial count: the device
+ * driver waits once per batch of steps, never per trial. */
+omv_status omv_lba_host_syncs(omv_lba *h, int *host_syncs, int *trials);
 
-/* Landmark sharding across ranks: one exchange per LM trial.
+/* Landmark sharding across ranks: two exchanges per LM step, no host wait per step.
  * Call before omv_lba_set_problem.  Every rank then passes the SAME full problem; the handle keeps
  * the rank's contiguous share of the landmarks (in its landmark order) with their edges, and rank 0
  * alone evaluates the inertial / random-walk edges, adds lambda to the pose diagonal and the pose
  * part of computeScale.  Per trial the handle calls
  *     allreduce(ctx, buf, count, stream)   — in-place SUM of `count` doubles of device memory,
- * once on the partial Schur system [packed blocks | b | coef] and once on [chi2, scale] (the
- * initial / per-iteration chi2 too).  The call must be enqueued on (or ordered after) `stream`;
+ * once on the partial Schur system [packed blocks | b | coef] and once on [chi2 of the current state (when
+ * recomputed), chi2 of the trial, scale] (and once on optimize()'s initial chi2).  The call must be enqueued on
+ * (or ordered after) `stream`;
  * it returns 0 on success.  ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream)
  * is exactly that.  Every rank solves the identical reduced system; after omv_lba_optimize each
  * rank has written its own landmarks / edges (chi2, outlier) and all keyframes; err / err_end are

@@ -251,6 +251,7 @@ SIGNATURES = {
     "omv_lba_evaluate": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "omv_lba_evaluate_stereo": (_I, [_VP, _VP, _VP, _VP]),
     "omv_lba_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(_I)]),
+    "omv_lba_host_syncs": (_I, [_VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "omv_lba_enable_timing": (_I, [_VP, _I]),
     "omv_lba_set_driver": (_I, [_VP, _I]),
     "omv_lba_reset": (_I, [_VP]),

@@ -176,9 +176,9 @@ __device__ __forceinline__ void set_gates(LmCtl *c) {
 // (iteration 0's lambda = lambda_init, ni = 2, nBad = 0, optimization_algorithm_levenberg.cpp:103-108).
 __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                                        const double *imu_partial, int opt_it, int max_trials,
-                                                       double lambda_init) {
+                                                       double lambda_init, const double *pre) {
     __shared__ double sh[8];
-    const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
+    const double chi = pre ? pre[1] : sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
     if (threadIdx.x == 0) {
         c->err0 = c->errors_chi = chi;
         c->errors_of_current = 1;
@@ -198,19 +198,23 @@ __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *m
 //   iteration / nBad stop tests in the reference's order, and the next step's gates.
 __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                   const double *imu_partial, const double *mono_partial_a, const double *imu_partial_a,
-                                  const double *scale_partial, int n_scale, const int *fail) {
+                                  const double *scale_partial, int n_scale, const int *fail, const double *pre) {
     if (!c->g_active) return;
     const bool errA = c->g_errA != 0;
-    double chiA = 0;
-    if (errA) {
-        chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
+    double chiA = 0, chi, ssum;
+    if (pre) {   // a sharded solve: [chi(A), chi, computeScale] summed over the ranks (trial_scalars_kernel)
+        chiA = pre[0], chi = pre[1], ssum = pre[2];
+    } else {
+        if (errA) {
+            chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
+            __syncthreads();
+        }
+        chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
+        double sc = 0;
+        for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
         __syncthreads();
+        ssum = block_reduce_sum(sc, sh);
     }
-    const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
-    double sc = 0;
-    for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
-    __syncthreads();
-    const double ssum = block_reduce_sum(sc, sh);
     if (threadIdx.x != 0) return;
     if (c->g_build) {   // iteration start
         ++c->its;
@@ -297,10 +301,33 @@ __global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu
 __global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                                            const double *imu_partial, const double *mono_partial_a,
                                                            const double *imu_partial_a, const double *scale_partial,
-                                                           int n_scale, const int *fail) {
+                                                           int n_scale, const int *fail, const double *pre) {
     __shared__ double sh[8];
     finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, mono_partial_a, imu_partial_a, scale_partial,
-                      n_scale, fail);
+                      n_scale, fail, pre);
+}
+
+// A sharded solve's per-rank scalars, all-reduced before the LM bookkeeping: out = [chi(A) when this step recomputed
+// the current state's errors, chi of the trial, this rank's computeScale terms] (ctl == nullptr: out[1] = chi of
+// the errors just computed, optimize()'s initial err).  Gated like the trial.
+__global__ void __launch_bounds__(256) trial_scalars_kernel(const LmCtl *c, const double *mono_partial, int n_mono_blocks,
+                                                            const double *imu_partial, const double *mono_partial_a,
+                                                            const double *imu_partial_a, const double *scale_partial,
+                                                            int n_scale, double *out) {
+    __shared__ double sh[8];
+    if (c && !c->g_active) return;
+    double chiA = 0;
+    if (c && c->g_errA) {
+        chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
+        __syncthreads();
+    }
+    const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
+    double sc = 0;
+    if (c)
+        for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
+    __syncthreads();
+    const double ssum = block_reduce_sum(sc, sh);
+    if (threadIdx.x == 0) out[0] = chiA, out[1] = chi, out[2] = ssum;
 }
 
 // Final chi2 = imu partial + visual partials (fixed order); also finishes the computeScale sums.
@@ -1443,6 +1470,7 @@ struct omv_lba {
     hipEvent_t ev[8];
     double stage_ms[4] = {0, 0, 0, 0};
     int last_trials = 0;
+    int host_syncs = 0;        // host waits of the last optimize()'s LM loop (the device driver: one per batch)
     size_t state_doubles() const { return (size_t)n_kf * (24 + 12 * rig.n_cams) + 3 * (size_t)n_pts; }
 };
 
@@ -1996,6 +2024,7 @@ static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[3], bool 
     if (rs != OMV_OK) return rs;
     HIP_OK(hipMemcpyAsync(h->h_out, h->d_out, 3 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
+    ++h->host_syncs;
     for (int q = 0; q < 3; ++q) out[q] = h->h_out[q];
     return OMV_OK;
 }
@@ -2131,23 +2160,35 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     if ((rs = launch_build(h, A, c)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
     if ((rs = launch_schur(h, 0.0, c)) != OMV_OK) return rs;
+    // sharded: one in-place SUM of this rank's partial reduced system [blocks | b | Schur rhs], ordered on the stream
+    if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
     launch_ldlt(h, c);
     if (ev) HIP_OK(hipEventRecord(ev[3], st));
     launch_update(h, 0.0, A, B, c);
     if ((rs = lba_errors(h, B, c, kGateTrial)) != OMV_OK) return rs;
-    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
-                                           h->d_partial_a, h->d_imu_partial_a, h->d_scale_partial,
-                                           h->n_pts > 0 ? h->n_wg_land + 1 : 1, h->d_fail);
+    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0, nsc = h->n_pts > 0 ? h->n_wg_land + 1 : 1;
+    const double *pre = nullptr;
+    if (h->world > 1) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
+        const int s0 = h->rank > 0 ? 1 : 0;   // the keyframe part of computeScale enters once (rank 0)
+        trial_scalars_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a,
+                                                h->d_imu_partial_a, h->d_scale_partial + s0, nsc - s0, h->d_out);
+        if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
+        pre = h->d_out;
+    }
+    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a, h->d_imu_partial_a,
+                                           h->d_scale_partial, nsc, h->d_fail, pre);
     if (ev) HIP_OK(hipEventRecord(ev[4], st));
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }
 
-// optimize() on one rank with the LM control on the device: the initial errors, then LM steps in batches
-// (opt_it first: every iteration takes at least one trial) until the device reports the end; one read-back
-// per batch; the last accepted trial's state copied into A.  Identical decisions to the host-driven loop below
-// (which the sharded solve keeps, its per-trial all-reduce being a host call).
+// optimize() with the LM control on the device: the initial errors, then LM steps in batches (opt_it first: every
+// iteration takes at least one trial) until the device reports the end; one read-back per batch (host_syncs counts
+// them); the last accepted trial's state copied into A.  Identical decisions to the host-driven loop below.  A
+// sharded solve (world > 1) runs the same gated steps launched directly (its two all-reduces per step are calls into
+// the caller's collective, ordered on the handle's stream): every rank reaches identical decisions from the
+// all-reduced system and scalars, so every rank launches the same steps and collectives.
 static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba_result *res) {
     const bool want_chi2 = res->mono_chi2 || res->stereo_chi2;
     h->epi_ready = false;
@@ -2158,12 +2199,20 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
         h->cur = 0;
     }
     omv_status rs;
+    h->host_syncs = 0;
     if ((rs = lba_errors(h, h->st[0])) != OMV_OK) return rs;
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
+    const bool sharded = h->world > 1;
+    if (sharded) {
+        trial_scalars_kernel<<<1, 256, 0, st>>>(nullptr, h->d_partial, nmb, h->d_imu_partial, nullptr, nullptr, nullptr,
+                                                0, h->d_out);
+        if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
+    }
     ctl_init_kernel<<<1, 256, 0, st>>>(h->d_ctl, h->d_partial, nmb, h->d_imu_partial, o->opt_it, o->max_trials,
-                                       o->lambda_init);
+                                       o->lambda_init, sharded ? h->d_out : nullptr);
     HIP_OK(hipGetLastError());
-    if (!h->timing && !h->step_exec) {   // capture one step and four steps (the problem's pointers are fixed
+    const bool direct = h->timing || sharded;   // a collective call cannot be captured
+    if (!direct && !h->step_exec) {   // capture one step and four steps (the problem's pointers are fixed
                                          // until set_problem); a batch is launched as 4-step graphs + single steps
         for (int n : {1, 4}) {
             HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
@@ -2190,6 +2239,9 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
                 evs.push_back(e);
                 if ((rs = lba_step(h, evs.back().data())) != OMV_OK) return rs;
                 ++i;
+            } else if (direct) {
+                if ((rs = lba_step(h, nullptr)) != OMV_OK) return rs;
+                ++i;
             } else if (i + 4 <= batch) {
                 HIP_OK(hipGraphLaunch(h->step4_exec, st));
                 i += 4;
@@ -2204,6 +2256,7 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
         if (spec && (rs = lba_enqueue_epilogue(h, want_chi2)) != OMV_OK) return rs;
         HIP_OK(hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
+        ++h->host_syncs;
         if (h->h_ctl->done || launched >= max_steps) break;
         h->epi_ready = false;
         batch = std::min(4, max_steps - launched);
@@ -2237,7 +2290,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     double sc[3];
     omv_status rs;
     for (double &m : h->stage_ms) m = 0;
-    if (h->world == 1 && !h->host_lm) {
+    h->host_syncs = 0;
+    if (!h->host_lm) {
         if ((rs = lba_optimize_device(h, o, res)) != OMV_OK) return rs;
         return lba_finish_result(h, o, p, res);
     }
@@ -2470,6 +2524,13 @@ omv_status omv_lba_enable_timing(omv_lba *h, int on) {
 omv_status omv_lba_set_driver(omv_lba *h, int host_driven) {
     if (!h) return OMV_ERR_ARG;
     h->host_lm = host_driven != 0;
+    return OMV_OK;
+}
+
+omv_status omv_lba_host_syncs(omv_lba *h, int *host_syncs, int *trials) {
+    if (!h) return OMV_ERR_ARG;
+    if (host_syncs) *host_syncs = h->host_syncs;
+    if (trials) *trials = h->last_trials;
     return OMV_OK;
 }
 

@@ -128,6 +128,12 @@ class LocalInertialBA:
         _lib.check(self._lib.omv_lba_set_driver(self._h, int(bool(host_driven))), "omv_lba_set_driver")
         return self
 
+    def host_syncs(self):
+        """(host waits of the last optimize()'s LM loop, its trials): the device driver waits once per batch."""
+        n, t = ctypes.c_int(0), ctypes.c_int(0)
+        _lib.check(self._lib.omv_lba_host_syncs(self._h, ctypes.byref(n), ctypes.byref(t)), "omv_lba_host_syncs")
+        return n.value, t.value
+
     def stage_ms(self):
         """Device ms of the last optimize: build, schur, solve, update+errors; and the trial count."""
         ms = np.zeros(4)

@@ -237,11 +237,12 @@ def test_bitwise_identical_run_to_run(full, driver):
             assert np.array_equal(np.asarray(s[k]).view(np.uint64), np.asarray(s0[k]).view(np.uint64)), k
 
 
-@pytest.mark.parametrize("backend", ["gloo", "nccl"])
-def test_landmark_sharded_two_ranks(oracle, tmp_path, backend):
+@pytest.mark.parametrize("backend,driver", [("gloo", "device"), ("gloo", "host"), ("nccl", "device")])
+def test_landmark_sharded_two_ranks(oracle, tmp_path, backend, driver):
     """landmarks sharded over 2 ranks (gloo, both on this box's GPU), one all-reduce of the
-    partial Schur system per trial.  The merged outcome meets the same bar against the oracle, and
-    every rank holds the identical keyframe state (asserted inside the worker)."""
+    partial Schur system and one of the LM scalars per step.  The merged outcome meets the same bar against the
+    oracle, and every rank holds the identical keyframe state (asserted inside the worker).  The device LM driver
+    waits on the host once per batch of steps, never per trial (omv_lba_host_syncs)."""
     import os
     import socket
     import subprocess
@@ -256,7 +257,8 @@ def test_landmark_sharded_two_ranks(oracle, tmp_path, backend):
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tools", "lba_shard_run.py"),
-           "--out", str(out), "--backend", backend, "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000"]
+           "--out", str(out), "--backend", backend, "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000",
+           "--host-driver", "1" if driver == "host" else "0"]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
@@ -268,3 +270,8 @@ def test_landmark_sharded_two_ranks(oracle, tmp_path, backend):
           ("err", "err_end", "status", "iterations", "trials", "mono_chi2", "mono_outlier")}
     _compare_result(prob, rg, ro)
     _compare_state(prob, {k: g[k] for k in STATE}, so, oracle)
+    trials, syncs = int(g["trials"]), int(g["host_syncs"])
+    if driver == "device":
+        assert syncs <= (trials + 3) // 4 + 1 and (trials < 2 or syncs < trials), (syncs, trials)
+    else:
+        assert syncs >= trials, (syncs, trials)

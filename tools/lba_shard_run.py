@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--n-pts", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--large", type=int, default=1)
+    ap.add_argument("--host-driver", type=int, default=0, help="1: the host-driven LM loop (read-back per trial)")
     args = ap.parse_args()
 
     import numpy as np
@@ -48,15 +49,17 @@ def main():
     ba = LocalInertialBA(max_kf=prob["n_kf"], max_cams=prob["n_cams"], max_pts=len(prob["pts"]),
                          max_mono=len(prob["mono_pt"]), max_imu=max(1, len(prob["imu_kf1"])), rank=rank, world=world,
                          allreduce=ar)
+    ba.set_driver(bool(args.host_driver))
     ba.set_problem(prob)
     idx, n_e = ba.shard()
     res, st = ba.optimize(max_trials=10, large=bool(args.large), **lba_options(bool(args.large)))
+    syncs, trials = ba.host_syncs()
     mine = np.isin(prob["mono_pt"], idx)
     assert int(mine.sum()) == n_e
     part = dict(rank=rank, idx=idx, pts=st["pts"][idx], edges=np.nonzero(mine)[0],
                 chi2=res["mono_chi2"][mine], outl=res["mono_outlier"][mine],
                 kf={k: st[k] for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba")},
-                scal={k: res[k] for k in ("err", "err_end", "status", "iterations", "trials")})
+                scal={k: res[k] for k in ("err", "err_end", "status", "iterations", "trials")}, syncs=syncs)
     parts = [None] * world
     dist.all_gather_object(parts, part)
     if rank == 0:
@@ -75,6 +78,7 @@ def main():
                 assert np.array_equal(v, parts[0]["kf"][k]), ("keyframe state differs across ranks", k)
             assert q["scal"] == parts[0]["scal"], "LM outcome differs across ranks"
         out = dict(pts=pts, mono_chi2=chi2, mono_outlier=outl, owner=owner, world=world,
+                   host_syncs=max(q["syncs"] for q in parts),
                    **{k: v for k, v in parts[0]["kf"].items()}, **parts[0]["scal"])
         np.savez(args.out, **out)
         print(f"lba shard ok: world {world}, trials {out['trials']}, err {out['err']:.6g} -> {out['err_end']:.6g}")
