@@ -193,10 +193,12 @@ __device__ __forceinline__ void sort_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LS / RS: scratch of the range's own positions (entries f .. l-1), so disjoint ranges partition concurrently.
 __device__ inline int wave_unguarded_partition(SortItem *arr, int f, int l, int *LS, int *RS, int lane) {
     const SortItem p = arr[f];
     const unsigned long long lt = (1ull << lane) - 1ull;
     int nL = 0, nR = 0;
+    LS += f, RS += f;
     for (int base = f + 1; base < l; base += 64) {
         const int x = base + lane;
         const bool fl = x < l && !item_less(arr[x], p);
@@ -261,6 +263,54 @@ __device__ inline void wave_introsort_loop(SortItem *arr, int n, int *stack, int
         sort_wave_sync();
         sp -= 3;
         first = stack[sp], last = stack[sp + 1], depth = stack[sp + 2];
+    }
+}
+
+// __introsort_loop by all wavefronts of the block: the loop only ever splits a range into two disjoint ranges that it
+// then treats independently (each with the depth limit of the split), so the ranges of one recursion depth are
+// partitioned concurrently, one range per wavefront, level by level -- the same element moves as the sequential
+// loop.  q: 2 * (3 * (n / 17 + 1)) + 2 ints of scratch (two range queues + their counts); LS, RS: n ints each.
+__device__ inline int introsort_queue_ints(int n) { return 6 * (n / 17 + 1) + 2; }
+__device__ inline void block_introsort_loop(SortItem *arr, int n, int *q, int *LS, int *RS, int tid, int T) {
+    const int kThreshold = 16, cap = n / 17 + 1;
+    int *cnt = q, *qa = q + 2, *qb = qa + 3 * cap;
+    const int lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+    if (tid == 0) {
+        cnt[0] = n > kThreshold ? 1 : 0, cnt[1] = 0;
+        qa[0] = 0, qa[1] = n, qa[2] = 2 * floor_log2(max(n, 1));
+    }
+    __syncthreads();
+    for (int side = 0;; side ^= 1) {
+        int *cur = side ? qb : qa, *nxt = side ? qa : qb;
+        const int nq = cnt[side];
+        if (nq == 0) break;
+        for (int r = wave; r < nq; r += nw) {
+            const int f = cur[3 * r], l = cur[3 * r + 1];
+            int depth = cur[3 * r + 2];
+            if (depth == 0) {
+                if (lane == 0) heap_sort(arr + f, l - f);
+                sort_wave_sync();
+                continue;
+            }
+            --depth;
+            const int mid = f + (l - f) / 2;
+            if (lane == 0) median_to_first(&arr[f], &arr[f + 1], &arr[mid], &arr[l - 1]);
+            sort_wave_sync();
+            const int cut = wave_unguarded_partition(arr, f, l, LS, RS, lane);
+            if (lane == 0) {
+                if (l - cut > kThreshold) {
+                    const int k = atomicAdd(&cnt[side ^ 1], 1);
+                    nxt[3 * k] = cut, nxt[3 * k + 1] = l, nxt[3 * k + 2] = depth;
+                }
+                if (cut - f > kThreshold) {
+                    const int k = atomicAdd(&cnt[side ^ 1], 1);
+                    nxt[3 * k] = f, nxt[3 * k + 1] = cut, nxt[3 * k + 2] = depth;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) cnt[side] = 0;
+        __syncthreads();
     }
 }
 

@@ -585,7 +585,7 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     int *vlist = rest + 3 * NC;      // NC
     int *vpos = rest + 4 * NC;       // NC: position in the sorted V list, or -1
     omv::SortItem *items = reinterpret_cast<omv::SortItem *>(rest + 5 * NC);   // NC items (3 ints)
-    int *sstack = rest + 8 * NC;     // 192
+    int *sstack = rest + 8 * NC;     // the sort's range queues: introsort_queue_ints(NC) (<= oct_queue(NC))
 
 #ifdef OMV_OCT_PROFILE
     long long pf_t0 = wall_clock64(), pf_sort = 0, pf_p1 = 0, pf_p2 = 0, pf_gather = 0;
@@ -608,15 +608,11 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
         return;
     }
-    // one thread per key: its cell is the last one whose start <= k (empty cells share the next start)
-    for (int k = tid; k < K; k += T) {
-        int lo = 0, hi = ncell - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cellscan[mid] <= k) lo = mid;
-            else hi = mid - 1;
-        }
-        cand[k] = a.cell_kp[((size_t)img * g.n_cells + L.cell_begin + lo) * g.cell_cap + (k - cellscan[lo])];
+    // one thread per cell: its keys to [start, next start) (the cells' loads all in flight at once)
+    for (int i = tid; i < ncell; i += T) {
+        const int k0 = cellscan[i], k1 = i + 1 < ncell ? cellscan[i + 1] : K;
+        const uint32_t *src = a.cell_kp + ((size_t)img * g.n_cells + L.cell_begin + i) * g.cell_cap;
+        for (int k = k0; k < k1; ++k) cand[k] = src[k - k0];
     }
     __syncthreads();
 
@@ -689,12 +685,11 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
             for (int i = tid; i < m; i += T) vpos[i] = A.cnt[i] > 1 ? 0 : -1;
         } else {
             // sort V by (size, UL.x) exactly as libstdc++'s std::sort moves the elements: the introsort
-            // partitions on wave 0, the final insertion sort as a stable rank over the block (B is free
-            // until step 4: its x0 / x1 / y0 rows hold the items' scratch)
+            // partitions one recursion depth at a time, a range per wavefront, the final insertion sort as a
+            // stable rank over the block (B is free until step 4: its x0 / x1 / y0 rows hold the items' scratch)
             for (int j = tid; j < nv; j += T) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
             __syncthreads();
-            if ((tid >> 6) == 0) omv::wave_introsort_loop(items, nv, sstack, scanA, scanB, tid & 63);
-            __syncthreads();
+            omv::block_introsort_loop(items, nv, sstack, scanA, scanB, tid, T);
             omv::block_final_insertion_sort(items, nv, reinterpret_cast<omv::SortItem *>(B.x0), tid, T);
 #ifdef OMV_OCT_PROFILE
             pf_sort += wall_clock64() - pf_r;
@@ -1110,8 +1105,7 @@ __global__ void __launch_bounds__(256) node_sort_selftest_kernel(const int *k1, 
     int *LS = reinterpret_cast<int *>(tmp + n), *RS = LS + n, *stk = RS + n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = omv::SortItem{k1[i], k2[i], i};
     __syncthreads();
-    if (threadIdx.x < 64) omv::wave_introsort_loop(items, n, stk, LS, RS, threadIdx.x);
-    __syncthreads();
+    omv::block_introsort_loop(items, n, stk, LS, RS, threadIdx.x, blockDim.x);
     omv::block_final_insertion_sort(items, n, tmp, threadIdx.x, blockDim.x);
     for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = items[i].payload;
 }
@@ -1334,7 +1328,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
     o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
     o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
-    o->oct_lds = (size_t)(32 + 18 * g.node_cap + g.ccnt_cap + 192) * sizeof(int);
+    o->oct_lds = (size_t)(32 + 18 * g.node_cap + g.ccnt_cap + 6 * (g.node_cap / 17 + 1) + 2) * sizeof(int);
     return OMV_OK;
 }
 
@@ -1618,7 +1612,7 @@ omv_status omv_orb_debug_level(omv_orb *o, int img, int level, uint8_t *out, int
 omv_status omv_selftest_node_sort(const int *k1, const int *k2, int n, int *perm, void *stream) {
     if (n < 0 || n > 2048 || (n > 0 && (!k1 || !k2 || !perm))) return OMV_ERR_ARG;
     if (n == 0) return OMV_OK;
-    const size_t lds = (size_t)n * (2 * sizeof(omv::SortItem) + 2 * sizeof(int)) + 192 * sizeof(int);
+    const size_t lds = (size_t)n * (2 * sizeof(omv::SortItem) + 2 * sizeof(int)) + (6 * (n / 17 + 1) + 2) * sizeof(int);
     if (hipFuncSetAttribute((const void *)node_sort_selftest_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
         return OMV_ERR_HIP;
