@@ -82,6 +82,12 @@ omv_status omv_orb_extract_batch(omv_orb *orb, int n_images, const uint8_t *imag
 omv_status omv_orb_extract_host(omv_orb *orb, const uint8_t *image, size_t pitch, int lap0, int lap1,
                                 omv_kp *kps, uint8_t *desc, int *n_out, int *mono_index);
 
+/* Optional extra output of the following omv_orb_extract_batch calls: per output row (the omv_kp layout
+ * [image][N_max]) OpenCV ORB's Harris response (orb.cpp HarrisResponses, blockSize 7, k 0.04) at the keypoint's
+ * level position -- the north star's "Harris score".  The reference never computes it (its HARRIS_SCORE is a dead
+ * enum, include/ORBextractor.h:24; KeyPoint::response stays FAST's cornerScore).  NULL (default) disables it. */
+omv_status omv_orb_set_harris(omv_orb *orb, float *harris);
+
 /* Device-side error word of the last batch (OMV_ERR_CAPACITY if a bound was hit); syncs the stream. */
 omv_status omv_orb_last_error(omv_orb *orb);
 

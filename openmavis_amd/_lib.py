@@ -224,6 +224,7 @@ SIGNATURES = {
     "omv_orb_extract_host": (_I, [_VP, _VP, _SZ, _I, _I, _VP, _VP, _VP, _VP]),
     "omv_orb_last_error": (_I, [_VP]),
     "omv_orb_enable_timing": (_I, [_VP, _I]),
+    "omv_orb_set_harris": (_I, [_VP, _VP]),
     "omv_orb_stage_ms": (_I, [_VP, _VP, ctypes.POINTER(ctypes.c_longlong), _I]),
     "omv_orb_last_counts": (_I, [_VP, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     "omv_orb_debug_level": (_I, [_VP, _I, _I, _VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),

@@ -897,6 +897,7 @@ struct DescArgs {
     int n_images;
     const uint32_t *disc;    // [64][8] per lane: (row-sum mask, weight mask) of its four centroid dot4 items
     const uint32_t *hitem;   // [kHItemIt * 64] horizontal items: raw dword offset | column-major offset << 16
+    float *harris;           // optional [n_images][n_max]: OpenCV ORB's Harris response per output row
 };
 
 constexpr int kRawRows = 43, kRawDw = 12;   // raw patch: rows cy-21 .. cy+21, 48 bytes each (43 used + alignment)
@@ -1029,12 +1030,34 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
             rs = (int)__builtin_amdgcn_udot4(w, mk[2 * k], (uint32_t)rs, false);
             m10 += (int)__builtin_amdgcn_udot4(w, mk[2 * k + 1], 0u, false);
         }
-        m10 -= 15 * rs;
-        m01 = (vr - 15) * rs;
+        m10 -= __mul24(15, rs);
+        m01 = __mul24(vr - 15, rs);
     }
     for (int d = 32; d >= 1; d >>= 1) {
         m01 += __shfl_xor(m01, d, 64);
         m10 += __shfl_xor(m10, d, 64);
+    }
+    // optional Harris response (OpenCV ORB's HarrisResponses, blockSize 7, k 0.04 -- the north star's "Harris score";
+    // the reference's response is FAST's): lane k < 49 = block pixel (cy - 3 + k / 7, cx - 3 + k % 7) of the raw patch
+    float harris = 0.f;
+    if (a.harris) {
+        int ha = 0, hb = 0, hc = 0;
+        if (lane < 49) {
+            const int i = lane / 7, jj = lane - 7 * i;
+            const uint8_t *rb = reinterpret_cast<const uint8_t *>(raw) + (18 + i) * (4 * kRawDw) + po + 18 + jj;
+            const int st = 4 * kRawDw;
+            const int Ix = (rb[1] - rb[-1]) * 2 + (rb[-st + 1] - rb[-st - 1]) + (rb[st + 1] - rb[st - 1]);
+            const int Iy = (rb[st] - rb[-st]) * 2 + (rb[st - 1] - rb[-st - 1]) + (rb[st + 1] - rb[-st + 1]);
+            ha = Ix * Ix, hb = Iy * Iy, hc = Ix * Iy;
+        }
+        for (int d = 32; d >= 1; d >>= 1) {
+            ha += __shfl_xor(ha, d, 64);
+            hb += __shfl_xor(hb, d, 64);
+            hc += __shfl_xor(hc, d, 64);
+        }
+        const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+        const float scale_sq_sq = scale * scale * scale * scale;
+        harris = ((float)ha * hb - (float)hc * hc - 0.04f * ((float)ha + hb) * ((float)ha + hb)) * scale_sq_sq;
     }
     const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
     float sn, cs;
@@ -1044,8 +1067,8 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     // the blurred pixel at (cx + dx, cy + dy), |dx|, |dy| <= 18: column dx + 18, sum rows R0 = dy + 18 .. R0 + 6
     // = the four pair dwords from R0 >> 1, realigned by a half when R0 is odd
     auto blurred = [&](int dx, int dy) -> uint32_t {
-        const int R0 = dy + 18;
-        const uint32_t *q = H + (dx + 18) * kHStride + (R0 >> 1);
+        const int R0 = dy + 18;   // 0 .. 36, and dx + 18 too: 24-bit multiplies (full rate)
+        const uint32_t *q = H + __umul24((uint32_t)(dx + 18), (uint32_t)kHStride) + (R0 >> 1);
         const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
         const uint32_t sh = (uint32_t)(R0 & 1) << 4;
         const uint32_t w0 = __builtin_amdgcn_alignbit(d1, d0, sh), w1 = __builtin_amdgcn_alignbit(d2, d1, sh),
@@ -1078,6 +1101,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     omv_kp *kp = a.kps + (size_t)img * g.n_max + row;
     uint64_t *dst = reinterpret_cast<uint64_t *>(a.desc + ((size_t)img * g.n_max + row) * 32);
     if (lane < 4) dst[lane] = words[lane];
+    if (a.harris && lane == 0) a.harris[(size_t)img * g.n_max + row] = harris;
     if (lane == 0) {
         float x = (float)cx, y = (float)cy;
         if (l != 0) x *= L.scale, y *= L.scale;
@@ -1124,6 +1148,7 @@ struct omv_orb {
     XTab *d_xt = nullptr, *d_yt = nullptr;
     XQuad *d_xq = nullptr;
     uint32_t *d_disc = nullptr, *d_hitem = nullptr;   // K4's per-lane centroid masks and horizontal-sum items
+    float *harris = nullptr;   // optional Harris output of the next batches (omv_orb_set_harris)
     uint8_t *d_pyr = nullptr;
     int *d_cell_cnt = nullptr;
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
@@ -1520,11 +1545,17 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K4: orientation + blur at the samples + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n,
-                o->d_disc, o->d_hitem};
+                o->d_disc, o->d_hitem, o->harris};
     const int waves = g.out_per_img * n;
     describe_kernel<<<omv::xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
     HIP_OK(hipGetLastError());
+    return OMV_OK;
+}
+
+omv_status omv_orb_set_harris(omv_orb *o, float *harris) {
+    if (!o) return OMV_ERR_ARG;
+    o->harris = harris;
     return OMV_OK;
 }
 

@@ -105,12 +105,15 @@ class ORBextractor:
         return mono.value, kps[:n.value].copy(), desc[:n.value].copy()
 
     # -- batched device path ------------------------------------------------------------------------
-    def extract_batch(self, images, lapping, kps, desc, n_out, mono, stream=None):
+    def extract_batch(self, images, lapping, kps, desc, n_out, mono, stream=None, harris=None):
         """images: torch uint8 cuda tensor [n, H, W] (contiguous rows); lapping: host int array [n, 2];
         kps: torch [n, N_max, 6] 32-bit (omv_kp rows); desc: torch uint8 [n, N_max, 32];
-        n_out / mono: torch int32 [n].  Asynchronous on `stream` (torch stream or None)."""
+        n_out / mono: torch int32 [n]; harris: optional torch float32 [n, N_max], OpenCV ORB's Harris response
+        per row (an extra: the reference's response is FAST's).  Asynchronous on `stream` (torch stream or None)."""
         n, h, w = images.shape
         self._ensure(w, h, n)
+        _lib.check(self._lib.omv_orb_set_harris(self._h, _lib.ptr(harris) if harris is not None else None),
+                   "omv_orb_set_harris")
         lap = np.ascontiguousarray(np.asarray(lapping, dtype=np.int32).reshape(n, 2))
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
         pitch = images.stride(1)

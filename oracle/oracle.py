@@ -81,6 +81,17 @@ def pyramid_level(img, level, nfeatures=1200, scale=1.2, nlevels=8):
     return out
 
 
+def harris_responses(level_img, xs, ys):
+    """OpenCV ORB's HarrisResponses (blockSize 7, k 0.04) at integer level positions (an extra the reference lacks)."""
+    L = np.ascontiguousarray(level_img)
+    h, w = L.shape
+    xs = np.ascontiguousarray(xs, dtype=np.int32)
+    ys = np.ascontiguousarray(ys, dtype=np.int32)
+    out = np.zeros(len(xs), np.float32)
+    lib().oracle_harris_responses(_p(L), w, h, w, _p(xs), _p(ys), len(xs), _p(out))
+    return out
+
+
 def level_candidates(level_img, ini_th, min_th):
     L = np.ascontiguousarray(level_img)
     h, w = L.shape

@@ -554,6 +554,33 @@ int oracle_orb_pyramid_level(const uint8_t *img, int w, int h, int stride, int n
     return 0;
 }
 
+// Harris response at integer level positions (x, y): OpenCV ORB's HarrisResponses (modules/features2d/src/orb.cpp,
+// blockSize 7, harris_k 0.04) restated -- the north star's "Harris score"; the reference itself never computes it
+// (HARRIS_SCORE is a dead enum, include/ORBextractor.h:24; its response is FAST's).  Sobel-like Ix / Iy over the 7x7
+// block, integer sums a, b, c, then ((float)a * b - (float)c * c - k ((float)a + b)^2) * scale^4 in float.
+// Parity unpinned (no OpenCV build here): the restatement is checked against an independent numpy form in tests.
+void oracle_harris_responses(const uint8_t *lvl, int w, int h, int stride, const int *xs, const int *ys, int n,
+                             float *out) {
+    (void)w, (void)h;
+    const int bs = 7, r = bs / 2;
+    const float scale = 1.f / ((1 << 2) * bs * 255.f);
+    const float scale_sq_sq = scale * scale * scale * scale;
+    const float harris_k = 0.04f;
+    for (int q = 0; q < n; ++q) {
+        int a = 0, b = 0, c = 0;
+        for (int i = 0; i < bs; ++i)
+            for (int j = 0; j < bs; ++j) {
+                const uint8_t *p = lvl + (size_t)(ys[q] - r + i) * stride + (xs[q] - r + j);
+                const int Ix = (p[1] - p[-1]) * 2 + (p[-stride + 1] - p[-stride - 1]) + (p[stride + 1] - p[stride - 1]);
+                const int Iy = (p[stride] - p[-stride]) * 2 + (p[stride - 1] - p[-stride - 1]) + (p[stride + 1] - p[-stride + 1]);
+                a += Ix * Ix;
+                b += Iy * Iy;
+                c += Ix * Iy;
+            }
+        out[q] = ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+    }
+}
+
 // FAST candidates (vToDistributeKeys order) of one level given the level image. Returns count.
 int oracle_orb_level_candidates(const uint8_t *lvl, int w, int h, int iniTh, int minTh, float *xs,
                                 float *ys, float *resp, int cap) {

@@ -166,3 +166,26 @@ def test_kf_search_oracle_recovers_true_keypoints(oracle):
             sl = bi[jb["mp_start"]:jb["mp_start"] + jb["mp_count"]]
             sl = sl[sl >= 0]
             assert len(np.unique(sl)) == len(sl)
+
+
+def test_harris_oracle_matches_numpy(oracle):
+    """The oracle's OpenCV ORB HarrisResponses restatement (C, float32 at the end) against an independent numpy form of
+    the published formula (Sobel-like 3x3 gradients, 7x7 sums in int64, response in float64): the integer sums agree
+    exactly, so the float32 responses agree to float32 rounding of a few operations."""
+    img = synth.synth_image(31, 200, 160)
+    rng = np.random.default_rng(3)
+    xs = rng.integers(5, 195, 300).astype(np.int32)
+    ys = rng.integers(5, 155, 300).astype(np.int32)
+    got = oracle.harris_responses(img, xs, ys)
+    I = img.astype(np.int64)
+    Ix = (I[1:-1, 2:] - I[1:-1, :-2]) * 2 + (I[:-2, 2:] - I[:-2, :-2]) + (I[2:, 2:] - I[2:, :-2])
+    Iy = (I[2:, 1:-1] - I[:-2, 1:-1]) * 2 + (I[2:, :-2] - I[:-2, :-2]) + (I[2:, 2:] - I[:-2, 2:])
+    ref = np.zeros(len(xs))
+    scale = 1.0 / (4 * 7 * 255.0)
+    for q, (x, y) in enumerate(zip(xs, ys)):
+        gx = Ix[y - 4:y + 3, x - 4:x + 3]   # interior index = pixel - 1
+        gy = Iy[y - 4:y + 3, x - 4:x + 3]
+        a, b, c = int((gx * gx).sum()), int((gy * gy).sum()), int((gx * gy).sum())
+        ref[q] = (float(a) * b - float(c) * c - 0.04 * (float(a) + b) ** 2) * scale ** 4
+    assert np.allclose(got, ref, rtol=2e-6, atol=1e-12), np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-12))
+    assert (np.abs(ref) > 0).mean() > 0.9

@@ -131,3 +131,52 @@ def test_extract_other_scale_factors(oracle, scale, nlevels):
     ex = ORBextractor(1000, scale, nlevels, 20, 7)
     g_mono, g_kps, g_desc = ex(img, None, (0, 0))
     _compare(o_mono, o_kps, o_desc, g_mono, g_kps, g_desc, f"scale {scale} x {nlevels}")
+
+
+def test_harris_extra_matches_oracle(oracle, torch_cuda):
+    """The optional Harris output (OpenCV ORB's HarrisResponses, blockSize 7, k 0.04; north star "Harris response
+    within 1e-5"): per output row, at the keypoint's level position on the un-blurred level.  The reference computes
+    no Harris score (its response is FAST's, include/ORBextractor.h:24), so the oracle is OpenCV's published formula,
+    pinned by tests/test_oracle_cpu.py::test_harris_oracle_matches_numpy.  Same float expression on both sides:
+    required within 1e-5 relative (observed bit-exact); the keypoints and descriptors stay bit-exact with it on."""
+    torch = torch_cuda
+    imgs = synth.hilti_frame(5)
+    lap = np.array([[0, 720], [0, 720], [0, 0], [0, 0], [0, 0]], np.int32)
+    ex = ORBextractor(1200, 1.2, 8, 15, 7, width=720, height=540, max_images=5)
+    cap = ex.max_keypoints()
+    d_img = torch.from_numpy(imgs).cuda()
+    kps = torch.zeros((5, cap, 6), dtype=torch.int32, device="cuda")
+    desc = torch.zeros((5, cap, 32), dtype=torch.uint8, device="cuda")
+    n_out = torch.zeros(5, dtype=torch.int32, device="cuda")
+    mono = torch.zeros(5, dtype=torch.int32, device="cuda")
+    harris = torch.full((5, cap), float("nan"), dtype=torch.float32, device="cuda")
+    ex.extract_batch(d_img, lap, kps, desc, n_out, mono, harris=harris)
+    torch.cuda.synchronize()
+    assert ex.last_error() == 0
+    kps_h = kps.cpu().numpy().view(oracle.KP_DTYPE).reshape(5, cap)
+    desc_h, n_h, m_h, hr = desc.cpu().numpy(), n_out.cpu().numpy(), mono.cpu().numpy(), harris.cpu().numpy()
+    scale = oracle.orb_tables(1200, 1.2, 8)["scale"]
+    checked = 0
+    for c in range(5):
+        n = int(n_h[c])
+        o_mono, o_kps, o_desc = oracle.orb_extract(imgs[c], 1200, 1.2, 8, 15, 7, tuple(lap[c]))
+        _compare(o_mono, o_kps, o_desc, int(m_h[c]), kps_h[c, :n], desc_h[c, :n], f"cam {c} (harris on)")
+        for lvl in range(8):
+            rows = np.nonzero(kps_h[c, :n]["octave"] == lvl)[0]
+            if rows.size == 0:
+                continue
+            L = imgs[c] if lvl == 0 else oracle.pyramid_level(imgs[c], lvl, 1200)
+            k = kps_h[c, rows]
+            xs = np.rint(k["x"].astype(np.float64) / scale[lvl]).astype(np.int32)
+            ys = np.rint(k["y"].astype(np.float64) / scale[lvl]).astype(np.int32)
+            ref = oracle.harris_responses(L, xs, ys)
+            got = hr[c, rows]
+            tol = 1e-5 * np.maximum(np.abs(ref), 1e-30)
+            assert (np.abs(got - ref) <= tol).all(), (c, lvl, got[:4], ref[:4])
+            checked += rows.size
+    assert checked > 4000
+    # off by default: the next batch without the output leaves the buffer alone
+    harris.fill_(7.0)
+    ex.extract_batch(d_img, lap, kps, desc, n_out, mono)
+    torch.cuda.synchronize()
+    assert bool((harris == 7.0).all())
