@@ -727,12 +727,19 @@ struct BlockPat {
     const int *dslot;                // [nb] diagonal slot per position
     const int *lev_start, *lev_col;  // elimination-tree levels: the positions of level l
     const int *ug_start;             // [n_lev+1] update groups of a level (one target block each)
+    const int *ug_split;             // [n_lev] groups ug_start[l] .. ug_split[l]: the diagonal blocks of level l + 1
+    const int *crit_grp;             // [nb] per position: the group updating its diagonal from the level below, or -1
     const int *ug_task_start;        // [n_groups+1]
     const int4 *ug;                  //   (slot(i, j), slot(i, k), slot(j, k), dslot(k)), ascending k
     const int *rs_start;             // [nb+1] row structure of position i: (slot(i, k), k), k < i
     const int2 *rs;
     const int *cs_start;             // [nb+1] column structure of position k: (slot(i, k), i), i > k
     const int2 *cs;
+    // every array above but slot_kr / slot_kc lives in one contiguous device blob; when blob_ints > 0 the solver stages
+    // it into LDS after the blocks, so the per-level schedule reads on its critical path are LDS reads, not dependent
+    // global loads
+    const int *blob;
+    int blob_ints;
 };
 
 // Per chunk of one block's Schur terms (256 landmark slot pairs (a, b), one per thread; a block's last chunk padded):
@@ -888,14 +895,48 @@ __device__ __forceinline__ double rcp_nr(double x) {
 // damped system (SimplicialLDLT's scalar LDL^T on its own AMD order, linear_solver_eigen.h:94-120, differs only in
 // rounding).
 
-// One wavefront: D (16x16 symmetric, lower triangle read) -> D^-1 in place (full), by four 4x4-pivot sweeps (the
-// sweep operator, block form): with pivot block P = {c0 .. c0+3}, Pi = M_PP^-1, b_x = M_xP,
-//   i, j not in P : M_ij - b_i Pi b_j^T      i in P, j not : (Pi b_j)_i      j in P, i not : (b_i Pi)_j
-//   i, j in P     : -Pi
-// after all four M = -D^-1.  Lane l owns column j = l & 15, rows q + 4t (q = l >> 4) in registers.  With
-// w = (j in P ? e_{j - c0} : b_j) and u = +-Pi w, every entry off the pivot rows is (j in P ? 0 : x) + b_i . u, and
-// the pivot rows (entry t = pass, all q) are -u_q.  Pi by 2x2 blocks: A^-1, the Schur complement S = C - B^T A^-1 B,
-// S^-1.  A zero / non-finite pivot determinant flags the solve.
+// One wavefront: D (16x16 symmetric, lower triangle read) -> D^-1 in place (full), by sixteen 1x1 sweeps held in
+// registers (the sweep operator): with pivot p = M_kk, r = 1 / p,
+//   i, j != k : M_ij - M_ik (M_kj r)      row k : M_kj r      column k : M_ik r      M_kk : -r
+// after all sixteen M = -D^-1 (no pivoting: D is the damped, positive definite Hessian block).  Lane l owns column
+// j = l & 15, rows q + 4t (q = l >> 4).  Per pass the pivot is a uniform read (v_readlane), the row M_k. a cross-row
+// ds_bpermute issued ahead of the reciprocal, and the column M_.k a DPP row broadcast of lane k of each 16-lane row --
+// no LDS store / load round trip between passes (a v_permlane16/32_swap row broadcast measured slower: more
+// instructions on an issue-bound pass).  A zero / non-finite pivot flags the solve.
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int K>
+__device__ __forceinline__ double row_bcast_f64(double x) {   // lane K of each 16-lane row, to the whole row
+    const long long b = __builtin_bit_cast(long long, x);
+    const long long r = __builtin_amdgcn_update_dpp(b, b, 0x150 + K, 0xf, 0xf, false);   // all lanes written
+    return __builtin_bit_cast(double, r);
+}
+template <int K>
+__device__ __forceinline__ void sweep_pass(double cur[4], int q, int j, bool &ok) {
+    constexpr int tk = K >> 2, qk = K & 3;
+    const double p = readlane_f64(cur[tk], 16 * qk + K);
+    const double mkj = __shfl(cur[tk], 16 * qk + j, 64);   // issued early: its latency hides behind the reciprocal
+    ok = ok && p != 0.0 && isfinite(p);
+    const double r = rcp_nr(p);
+    const double f = mkj * r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double mik = row_bcast_f64<K>(cur[t]);
+        double v = j == K ? mik * r : __builtin_fma(-mik, f, cur[t]);
+        if (t == tk) v = q == qk ? (j == K ? -r : f) : v;
+        cur[t] = v;
+    }
+}
+template <int K>
+__device__ __forceinline__ void sweep_all(double cur[4], int q, int j, bool &ok) {
+    if constexpr (K < 16) {
+        sweep_pass<K>(cur, q, j, ok);
+        sweep_all<K + 1>(cur, q, j, ok);
+    }
+}
 template <bool G>
 __device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
@@ -905,73 +946,11 @@ __device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
         const int i = q + 4 * t;
         cur[t] = D[i >= j ? sw16(i, j) : sw16(j, i)];
     }
-    wave_sync<G>();
-#pragma unroll
-    for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];   // the full symmetric block: columns readable
-    wave_sync<G>();
-#pragma unroll
-    for (int pv = 0; pv < 4; ++pv) {
-        const int c0 = 4 * pv;
-        double pm[4][4], bi[4][4], bj[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y2 = 0; y2 < 4; ++y2) pm[x][y2] = D[sw16(c0 + x, c0 + y2)];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (t != pv)
-#pragma unroll
-                for (int x = 0; x < 4; ++x) bi[t][x] = D[sw16(q + 4 * t, c0 + x)];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) bj[x] = D[sw16(j, c0 + x)];
-        // Pi = [[A^-1 + E S^-1 E^T, -E S^-1], [-S^-1 E^T, S^-1]], E = A^-1 B
-        const double da = pm[0][0] * pm[1][1] - pm[1][0] * pm[1][0];
-        const double ida = rcp_nr(da);
-        const double ai00 = pm[1][1] * ida, ai01 = -pm[1][0] * ida, ai11 = pm[0][0] * ida;
-        const double b00 = pm[0][2], b01 = pm[0][3], b10 = pm[1][2], b11 = pm[1][3];
-        const double e00 = ai00 * b00 + ai01 * b10, e01 = ai00 * b01 + ai01 * b11;
-        const double e10 = ai01 * b00 + ai11 * b10, e11 = ai01 * b01 + ai11 * b11;
-        const double s00 = pm[2][2] - (b00 * e00 + b10 * e10), s01 = pm[2][3] - (b00 * e01 + b10 * e11);
-        const double s11 = pm[3][3] - (b01 * e01 + b11 * e11);
-        const double ds = s00 * s11 - s01 * s01;
-        if (lane == 0 && !(da != 0.0 && isfinite(da) && ds != 0.0 && isfinite(ds) && pm[0][0] != 0.0)) *bad = 1;
-        const double ids = rcp_nr(ds);
-        const double si00 = s11 * ids, si01 = -s01 * ids, si11 = s00 * ids;
-        const double f00 = e00 * si00 + e01 * si01, f01 = e00 * si01 + e01 * si11;
-        const double f10 = e10 * si00 + e11 * si01, f11 = e10 * si01 + e11 * si11;
-        const double Pi[4][4] = {{ai00 + (f00 * e00 + f01 * e01), ai01 + (f00 * e10 + f01 * e11), -f00, -f01},
-                                 {ai01 + (f00 * e10 + f01 * e11), ai11 + (f10 * e10 + f11 * e11), -f10, -f11},
-                                 {-f00, -f10, si00, si01},
-                                 {-f01, -f11, si01, si11}};
-        const bool jP = (j >> 2) == pv;
-        const int jr = j & 3;
-        double w[4], u[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) w[x] = jP ? (x == jr ? 1.0 : 0.0) : bj[x];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            const double c = ((Pi[x][0] * w[0] + Pi[x][1] * w[1]) + Pi[x][2] * w[2]) + Pi[x][3] * w[3];
-            u[x] = jP ? c : -c;
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (t == pv) {
-                cur[t] = -(q == 0 ? u[0] : q == 1 ? u[1] : q == 2 ? u[2] : u[3]);
-            } else {
-                double v = jP ? 0.0 : cur[t];
-#pragma unroll
-                for (int x = 3; x >= 0; --x) v = __builtin_fma(bi[t][x], u[x], v);
-                cur[t] = v;
-            }
-        }
-        if ((j >> 2) == pv + 1) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = cur[t];
-        }
-        wave_sync<G>();
-    }
+    bool ok = true;
+    sweep_all<0>(cur, q, j, ok);
 #pragma unroll
     for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = -cur[t];
+    if (lane == 0 && !ok) *bad = 1;
     wave_sync<G>();
 }
 
@@ -1002,21 +981,25 @@ constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (th
 // (descendants, final by then), four blocks at a time (lane groups).
 __device__ __forceinline__ void forward_col(const double *pk, double *y, const BlockPat &P, int i, int lane) {
     const int r16 = lane & 15, grp = lane >> 4;
-    double acc = 0;
+    double acc[4] = {0, 0, 0, 0};   // four chains (the sum is latency-bound)
     for (int q = P.rs_start[i] + grp; q < P.rs_start[i + 1]; q += 4) {
         const int2 e = P.rs[q];
         const double *Sik = pk + (size_t)e.x * 256;
         const double *zk = y + 16 * e.y;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc += Sik[sw16(r16, m)] * zk[m];
+        for (int m = 0; m < 16; ++m) acc[m & 3] = __builtin_fma(Sik[sw16(r16, m)], zk[m], acc[m & 3]);
     }
-    acc += __shfl_xor(acc, 16, 64);
-    acc += __shfl_xor(acc, 32, 64);
-    const double v = y[16 * i + r16] - acc;
+    double a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    a += __shfl_xor(a, 16, 64);
+    a += __shfl_xor(a, 32, 64);
+    const double v = y[16 * i + r16] - a;
+    // Dinv_i v: lane group grp takes columns 4 grp .. 4 grp + 3, then the four partial sums
     const double *Di = pk + (size_t)P.dslot[i] * 256;
     double out = 0;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) out += Di[sw16(r16, m)] * __shfl(v, m, 16);
+    for (int m = 0; m < 4; ++m) out = __builtin_fma(Di[sw16(r16, 4 * grp + m)], __shfl(v, 4 * grp + m, 16), out);
+    out += __shfl_xor(out, 16, 64);
+    out += __shfl_xor(out, 32, 64);
     if (lane < 16) y[16 * i + lane] = out;
 }
 
@@ -1026,30 +1009,51 @@ __device__ __forceinline__ void forward_col(const double *pk, double *y, const B
 // ascending column order (no two wavefronts write a block) -- beside its columns' forward substitutions.  Backward
 // substitution gathers each column's structure (ancestors) level by level downwards.
 template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
-__global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat P, const double *b,
+__global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat Pg, const double *b,
                                                             const double *coef, double *x, double *gscratch,
                                                             int *fail, const LmCtl *ctl) {
     extern __shared__ __attribute__((aligned(16))) double lsm[];
     __shared__ int bad;
     if (!gate_open(ctl, kGateTrial)) return;
-    const int nb = P.nb, nv = 16 * nb;
+    const int nb = Pg.nb, nv = 16 * nb;
     double *pk = G ? gscratch : lsm;
-    double *y = pk + (size_t)P.n_slots * 256;
+    double *y = pk + (size_t)Pg.n_slots * 256;
     double *xs = y + nv;
+    BlockPat P = Pg;   // the schedule, rebased onto its LDS copy when staged
+    if (!G && Pg.blob_ints > 0) {
+        int *sched = reinterpret_cast<int *>(xs + nv);
+        for (int q = threadIdx.x; q < Pg.blob_ints; q += blockDim.x) sched[q] = Pg.blob[q];
+        auto rb = [&](auto *p) { return reinterpret_cast<decltype(p)>(sched + (reinterpret_cast<const int *>(p) - Pg.blob)); };
+        P.perm = rb(Pg.perm), P.dslot = rb(Pg.dslot), P.lev_start = rb(Pg.lev_start), P.lev_col = rb(Pg.lev_col);
+        P.ug_start = rb(Pg.ug_start), P.ug_split = rb(Pg.ug_split), P.crit_grp = rb(Pg.crit_grp);
+        P.ug_task_start = rb(Pg.ug_task_start), P.ug = rb(Pg.ug), P.rs_start = rb(Pg.rs_start), P.rs = rb(Pg.rs);
+        P.cs_start = rb(Pg.cs_start), P.cs = rb(Pg.cs);
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     if (tid == 0) bad = 0;
 #ifdef OMV_LDLT_PROFILE
     const long long t_0 = wall_clock64();
     long long t_1 = 0, t_3 = 0;
     __shared__ int pf_task[4];   // inverse ticks, forward ticks, inverse count, forward count
+    __shared__ int pf_lev[16][4];   // per level: phase ticks, max inverse task ticks, inverses, other tasks (the
+                                    // static LDS must stay under the 512 B beside kLdltLds, or the plan changes)
     if (tid < 4) pf_task[tid] = 0;
+    if (tid < 64) pf_lev[tid >> 2][tid & 3] = 0;
 #endif
     {
         const double2 *src = (const double2 *)Sp;
         double2 *dst = (double2 *)pk;
-        for (int q = tid; q < P.n_slots * 128; q += blockDim.x) dst[q] = src[q];
+        // eight loads in flight per thread (a dependent load-store loop waits one memory latency per 8 KB)
+        const int n2 = P.n_slots * 128, T = blockDim.x;
+        for (int q0 = tid; q0 < n2; q0 += 8 * T) {
+            double2 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = src[min(q0 + k * T, n2 - 1)];   // unconditional: all eight in flight
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[min(q0 + k * T, n2 - 1)] = v[k];   // past the end: the last entry again
+        }
         for (int q = tid; q < nv; q += blockDim.x) {
-            const int g = 16 * P.perm[q >> 4] + (q & 15);
+            const int g = 16 * Pg.perm[q >> 4] + (q & 15);   // (the LDS copy is not complete before the barrier)
             y[q] = b[g] - coef[g];
         }
     }
@@ -1065,39 +1069,75 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 #else
 #define OMV_LDLT_TICK(acc)
 #endif
-    // Level l: phase A inverts level l's diagonal blocks and, on the other wavefronts, forward-substitutes the columns
-    // of level l - 1 (their inverses and all their descendants' z are final; it is off the factorisation's critical
-    // path); phase B applies level l's trailing updates.  The last level's forward columns follow the loop.
+    // One phase per level l: level l's diagonal inverses -- each preceded, on its wavefront, by the updates of its
+    // diagonal block from level l - 1 (the only trailing updates an inverse of level l waits for) -- beside level
+    // l - 1's forward columns (their inverses and all their descendants' z are final) and level l - 1's other trailing
+    // updates (no block of these is touched by an inverse of level l), so the bulk of each level's updates runs beside
+    // the next level's inverses.  Each target block's updates come in ascending column order on one wavefront.
+    // Wavefronts 0 .. ni-1 start on the inverses; with fewer than four inverses the wavefronts sharing their SIMDs
+    // (w + 4) stay idle so the inverses -- the critical path -- issue alone; every other wavefront (and an inverse
+    // wavefront once done) claims tasks from an LDS counter.  A phase advances the counter by its claimed tasks plus
+    // one final failed claim per participating wavefront, so phase bases need no reset.
+    __shared__ int claim;
+    if (tid == 0) claim = 0;
+    __syncthreads();
+    int base = 0;
     for (int lev = 0; lev <= P.n_lev; ++lev) {
         const int c0 = P.lev_start[min(lev, P.n_lev)], c1 = lev < P.n_lev ? P.lev_start[lev + 1] : c0;
         const int f0 = lev > 0 ? P.lev_start[lev - 1] : 0, f1 = lev > 0 ? P.lev_start[lev] : 0;
-        const int na = c1 - c0 + f1 - f0;
-        for (int q = wave; q < na; q += nw) {
-#ifdef OMV_LDLT_PROFILE
-            const long long tq = wall_clock64();
-#endif
-            if (q < c1 - c0) inv16<G>(pk + (size_t)P.dslot[P.lev_col[c0 + q]] * 256, lane, &bad);
-            else forward_col(pk, y, P, P.lev_col[f0 + q - (c1 - c0)], lane);
-#ifdef OMV_LDLT_PROFILE
-            if (lane == 0) atomicAdd(q < c1 - c0 ? &pf_task[0] : &pf_task[1], (int)(wall_clock64() - tq));
-            if (lane == 0) atomicAdd(q < c1 - c0 ? &pf_task[2] : &pf_task[3], 1);
-#endif
-        }
-        __syncthreads();
-        OMV_LDLT_TICK(pf_fac)
-        if (lev == P.n_lev) break;
-        // the level's trailing updates, grouped by target
-        const int g0 = P.ug_start[lev], g1 = P.ug_start[lev + 1];
-        if (g1 > g0) {
-            for (int q = g0 + wave; q < g1; q += nw)
-                for (int u = P.ug_task_start[q]; u < P.ug_task_start[q + 1]; ++u) {
-                    const int4 t = P.ug[u];
-                    update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
-                             pk + (size_t)t.w * 256, lane);
+        const int r0 = lev > 0 ? P.ug_split[lev - 1] : 0, r1 = lev > 0 ? P.ug_start[lev] : 0;
+        const int ni = c1 - c0, nf = f1 - f0, na = ni + nf + (r1 - r0);
+        const int ns = min(ni, nw);   // statically placed inverses
+        const int n_idle = ni < 4 ? max(0, min(ni, nw - 4)) : 0;
+        const bool idle = ni < 4 && wave >= 4 && wave - 4 < ni;
+        if (!idle) {
+            int q = wave < ns ? wave : -1;
+            for (;;) {
+                if (q < 0) {
+                    int qn = 0;
+                    if (lane == 0) qn = atomicAdd(&claim, 1);
+                    q = ns + __shfl(qn, 0, 64) - base;
+                    if (q >= na) break;
                 }
-            __syncthreads();
+#ifdef OMV_LDLT_PROFILE
+                const long long tq = wall_clock64();
+#endif
+                if (q < ni) {
+                    const int col = P.lev_col[c0 + q];
+                    const int g = P.crit_grp[col];
+                    if (g >= 0) {
+                        for (int u = P.ug_task_start[g]; u < P.ug_task_start[g + 1]; ++u) {
+                            const int4 t = P.ug[u];
+                            update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
+                                     pk + (size_t)t.w * 256, lane);
+                        }
+                        wave_sync<G>();
+                    }
+                    inv16<G>(pk + (size_t)P.dslot[col] * 256, lane, &bad);
+                } else if (q < ni + nf) {
+                    forward_col(pk, y, P, P.lev_col[f0 + q - ni], lane);
+                } else {
+                    const int g = r0 + q - ni - nf;
+                    for (int u = P.ug_task_start[g]; u < P.ug_task_start[g + 1]; ++u) {
+                        const int4 t = P.ug[u];
+                        update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
+                                 pk + (size_t)t.w * 256, lane);
+                    }
+                }
+#ifdef OMV_LDLT_PROFILE
+                if (lane == 0 && q < ni + nf) atomicAdd(q < ni ? &pf_task[0] : &pf_task[1], (int)(wall_clock64() - tq));
+                if (lane == 0 && q < ni + nf) atomicAdd(q < ni ? &pf_task[2] : &pf_task[3], 1);
+                if (lane == 0 && lev < 16 && q < ni) atomicMax(&pf_lev[lev][1], (int)(wall_clock64() - tq));
+#endif
+                q = -1;
+            }
         }
-        OMV_LDLT_TICK(pf_upd)
+        base += (na - ns) + (nw - n_idle);
+        __syncthreads();
+#ifdef OMV_LDLT_PROFILE
+        if (tid == 0 && lev < 16) pf_lev[lev][0] = (int)(wall_clock64() - tp), pf_lev[lev][2] = ni, pf_lev[lev][3] = na - ni;
+#endif
+        OMV_LDLT_TICK(pf_fac)
     }
 #undef OMV_LDLT_TICK
 #ifdef OMV_LDLT_PROFILE
@@ -1108,20 +1148,23 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     for (int lev = P.n_lev - 1; lev >= 0; --lev) {
         for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw) {
             const int k = P.lev_col[c];
-            double acc = 0;
+            double acc4[4] = {0, 0, 0, 0};
             for (int q = P.cs_start[k] + grp; q < P.cs_start[k + 1]; q += 4) {
                 const int2 e = P.cs[q];
                 const double *Sik = pk + (size_t)e.x * 256;
                 const double *xi = xs + 16 * e.y;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc += Sik[sw16(r, r16)] * xi[r];
+                for (int r = 0; r < 16; ++r) acc4[r & 3] = __builtin_fma(Sik[sw16(r, r16)], xi[r], acc4[r & 3]);
             }
+            double acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
             acc += __shfl_xor(acc, 16, 64);
             acc += __shfl_xor(acc, 32, 64);
             const double *Dk = pk + (size_t)P.dslot[k] * 256;
             double out = 0;
 #pragma unroll
-            for (int m = 0; m < 16; ++m) out += Dk[sw16(r16, m)] * __shfl(acc, m, 16);
+            for (int m = 0; m < 4; ++m) out = __builtin_fma(Dk[sw16(r16, 4 * grp + m)], __shfl(acc, 4 * grp + m, 16), out);
+            out += __shfl_xor(out, 16, 64);
+            out += __shfl_xor(out, 32, 64);
             if (lane < 16) xs[16 * k + lane] = y[16 * k + r16] - out;
         }
         __syncthreads();
@@ -1133,6 +1176,10 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
                "per inverse %.1f per forward col %.1f\n",
                t_1 - t_0, pf_fac, pf_upd, t_3 - t_1, P.n_slots, P.n_lev, (double)pf_task[0] / max(pf_task[2], 1),
                (double)pf_task[1] / max(pf_task[3], 1));
+    if (tid == 0)
+        for (int l = 0; l <= min(P.n_lev, 15); ++l)
+            printf("  level %d: phase %d max-inverse %d inverses %d other %d\n", l, pf_lev[l][0], pf_lev[l][1],
+                   pf_lev[l][2], pf_lev[l][3]);
 #endif
     for (int q = tid; q < nv; q += blockDim.x) x[16 * P.perm[q >> 4] + (q & 15)] = xs[q];
     if (tid == 0) *fail = bad;
@@ -1657,7 +1704,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             }
     for (int k = 0; k < nb; ++k) dslot[k] = slot[(size_t)k * nb + k];
     // level schedule: columns per level; trailing updates grouped by target block (ascending k)
-    std::vector<int> lev_start(n_lev + 1, 0), lev_col, ug_start(n_lev + 1, 0), ug_task_start(1, 0);
+    std::vector<int> lev_start(n_lev + 1, 0), lev_col, ug_start(n_lev + 1, 0), ug_split(std::max(n_lev, 1), 0),
+        ug_task_start(1, 0), crit_grp(nb, -1);
+    std::vector<int> slot_kr_pos(n_slots), slot_kc_pos(n_slots);   // block positions of each slot
+    for (int j = 0; j < nb; ++j)
+        for (int i = j; i < nb; ++i)
+            if (slot[(size_t)i * nb + j] >= 0) slot_kr_pos[slot[(size_t)i * nb + j]] = i, slot_kc_pos[slot[(size_t)i * nb + j]] = j;
     std::vector<int4> ug;
     for (int l = 0; l < n_lev; ++l) {
         lev_start[l] = (int)lev_col.size();
@@ -1676,9 +1728,18 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
                         make_int4(slot[(size_t)i * nb + j], slot[(size_t)i * nb + k], slot[(size_t)j * nb + k], dslot[k]));
                 }
         }
-        for (auto &kv : by_target) {
-            ug.insert(ug.end(), kv.second.begin(), kv.second.end());
-            ug_task_start.push_back((int)ug.size());
+        // the diagonal blocks of level l + 1 first: their inverses wait only for these groups, the rest of the level's
+        // updates run beside those inverses
+        for (int pass = 0; pass < 2; ++pass) {
+            for (auto &kv : by_target) {
+                const int kr = slot_kr_pos[kv.first], kc = slot_kc_pos[kv.first];
+                const bool crit = kr == kc && level[kr] == l + 1;
+                if (crit != (pass == 0)) continue;
+                if (crit) crit_grp[kr] = (int)ug_task_start.size() - 1;
+                ug.insert(ug.end(), kv.second.begin(), kv.second.end());
+                ug_task_start.push_back((int)ug.size());
+            }
+            if (pass == 0) ug_split[l] = (int)ug_task_start.size() - 1;
         }
     }
     lev_start[n_lev] = (int)lev_col.size();
@@ -1940,13 +2001,32 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     {
         BlockPat &B = h->BP;
         B.nb = nb, B.n_slots = n_slots, B.n_lev = n_lev;
-        B.perm = upv(perm), B.slot_kr = upv(slot_kr), B.slot_kc = upv(slot_kc), B.dslot = upv(dslot);
-        B.lev_start = upv(lev_start), B.lev_col = upv(lev_col);
-        B.ug_start = upv(ug_start), B.ug_task_start = upv(ug_task_start), B.ug = upv(ug);
-        B.rs_start = upv(rs_start), B.rs = upv(rs), B.cs_start = upv(cs_start), B.cs = upv(cs);
-        if (!B.perm || !B.slot_kr || !B.slot_kc || !B.dslot || !B.lev_start || !B.lev_col ||
-            !B.ug_start || !B.ug_task_start || !B.ug || !B.rs_start || !B.rs || !B.cs_start || !B.cs)
-            return OMV_ERR_HIP;
+        B.slot_kr = upv(slot_kr), B.slot_kc = upv(slot_kc);
+        std::vector<int> blob;
+        auto put = [&](const auto &v) {   // 16-byte aligned sub-array
+            const size_t off = blob.size(), n = v.size() * sizeof(v[0]) / sizeof(int);
+            blob.resize(off + ((n + 3) & ~(size_t)3));
+            if (n) std::memcpy(blob.data() + off, v.data(), n * sizeof(int));
+            return off;
+        };
+        const size_t o_perm = put(perm), o_dslot = put(dslot), o_ls = put(lev_start), o_lc = put(lev_col);
+        const size_t o_us = put(ug_start), o_usp = put(ug_split), o_cg = put(crit_grp), o_uts = put(ug_task_start);
+        const size_t o_ug = put(ug), o_rss = put(rs_start), o_rs = put(rs), o_css = put(cs_start), o_cs = put(cs);
+        const int *d_blob = upv(blob);
+        if (!B.slot_kr || !B.slot_kc || !d_blob) return OMV_ERR_HIP;
+        B.blob = d_blob;
+        B.perm = d_blob + o_perm, B.dslot = d_blob + o_dslot, B.lev_start = d_blob + o_ls, B.lev_col = d_blob + o_lc;
+        B.ug_start = d_blob + o_us, B.ug_split = d_blob + o_usp, B.crit_grp = d_blob + o_cg;
+        B.ug_task_start = d_blob + o_uts, B.ug = (const int4 *)(d_blob + o_ug);
+        B.rs_start = d_blob + o_rss, B.rs = (const int2 *)(d_blob + o_rs);
+        B.cs_start = d_blob + o_css, B.cs = (const int2 *)(d_blob + o_cs);
+        // stage the schedule in LDS when it fits beside the blocks and vectors
+        const size_t sched_bytes = blob.size() * sizeof(int);
+        B.blob_ints = 0;
+        if (h->use_lds && h->ldlt_lds + sched_bytes <= kLdltLds) {
+            h->ldlt_lds += sched_bytes;
+            B.blob_ints = (int)blob.size();
+        }
     }
     // work buffers
     h->n_wg_edge = (E + 255) / 256;

@@ -286,6 +286,9 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int v) {
 //      what the NMS of any threshold >= t sees for non-corners);
 //   3. NMS (3x3, strict >) at iniTh and minTh in one pass over the survivors;
 //   4. emission at iniTh, or minTh if the cell had no iniTh keypoint (ORBextractor.cc:764-782).
+#ifdef OMV_FAST_PROFILE
+__device__ unsigned long long g_fast_stats[8];
+#endif
 template <int RS>   // LDS row stride in bytes (0: per cell, rounded up to 4)
 __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
@@ -471,6 +474,9 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     uint32_t *out = cell_kp + (size_t)blk * g.cell_cap;
     int th = g.ini_th;
     int ncand = prefilter(th);
+#ifdef OMV_FAST_PROFILE
+    const int ncand0 = ncand;
+#endif
     int total = nms(ncand, th, out);
     if (total == 0) {
         th = g.min_th;
@@ -479,6 +485,28 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     }
     // cap = max NMS survivors of the window, so this cannot trigger (writes past it were dropped)
     if (lane == 0) cell_cnt[blk] = total > g.cell_cap ? -1 : total;
+#ifdef OMV_FAST_PROFILE
+    // totals over the launch: cells, detection-window pixels, prefilter candidates (both passes), minTh retries,
+    // keypoints; the last cell prints them
+    {
+        __shared__ int dummy;
+        (void)dummy;
+        if (lane == 0) {
+            atomicAdd(&g_fast_stats[0], 1ull);
+            atomicAdd(&g_fast_stats[1], (unsigned long long)ndet);
+            atomicAdd(&g_fast_stats[2], (unsigned long long)ncand0);
+            atomicAdd(&g_fast_stats[3], th == g.min_th && g.min_th != g.ini_th ? 1ull : 0ull);
+            atomicAdd(&g_fast_stats[4], (unsigned long long)ncand);
+            atomicAdd(&g_fast_stats[5], (unsigned long long)total);
+            __threadfence();
+            const unsigned long long done = atomicAdd(&g_fast_stats[7], 1ull) + 1;
+            if (done == (unsigned long long)n_blocks)
+                printf("fast: cells %llu pixels %llu cand(iniTh) %llu retries %llu cand(last pass) %llu keypoints %llu\n",
+                       g_fast_stats[0], g_fast_stats[1], g_fast_stats[2], g_fast_stats[3], g_fast_stats[4],
+                       g_fast_stats[5]);
+        }
+    }
+#endif
 }
 
 // K3 --------------------------------------------------------------------------------------------
