@@ -709,6 +709,32 @@ __global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s, Edge
     else imu_contrib_block(blk - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
 }
 
+// The whole build in one launch: blocks [0, n_other) the pose chunks then the inertial edges (build_kernel's work),
+// blocks from n_other_pad (n_other rounded up to 8, so the landmark groups keep their XCD-aware order) the landmark
+// groups (build_land_kernel's work).  The two halves are independent and each is latency-bound with few blocks, so
+// side by side they take about the longer one's time instead of the sum.
+__global__ void __launch_bounds__(kGrpEdges) build_all_kernel(Rig rig, State s, Edges E, Land L, int n_grp, Gather G,
+                                                              Imu I, int n_pchunk, int n_other, int n_other_pad,
+                                                              double delta, double dsqr, double delta_st, double dsqr_st,
+                                                              double delta_imu, double dsqr_imu, const double *err,
+                                                              const double *err3, const double *chi2, const double *err9,
+                                                              double *contrib, const LmCtl *ctl) {
+    __shared__ double T[kLandTerms * kGrpEdges];
+    __shared__ LandAcc big_acc;
+    if (!gate_open(ctl, kGateBuild)) return;
+    const int b = blockIdx.x;
+    if (b < n_other_pad) {
+        if (b >= n_other) return;
+        if (b < n_pchunk) pose_chunk_block(b, T, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+        else imu_contrib_block(b - n_pchunk, T, s, I, delta_imu, dsqr_imu, err9, contrib);
+        return;
+    }
+    const int bl = b - n_other_pad, chunk = (n_grp + 7) >> 3;
+    const int g = (bl & 7) * chunk + (bl >> 3);
+    if (g >= n_grp) return;
+    land_group(g, T, &big_acc, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+}
+
 // ---- trial: the reduced system, assembled and Schur-complemented per block -----------------------------
 // The reduced system is stored as 16x16 blocks (keyframe block = pose 6 | v 3 | bg 3 | ba 3 | pad 1,
 // padded to one f64 MFMA tile) on the symbolic LDL^T pattern (fill-in included) of the elimination order
@@ -2172,13 +2198,25 @@ static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_p
 static bool lba_epilogue_ok(const omv_lba *h);
 static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2);
 
-// buildSystem at state A: the landmark blocks, the keyframe-diagonal pose chunks and the inertial edges' quadratic
-// forms in one launch (every part a fixed-order sum: the system is identical run to run).
-// buildSystem at state A: the landmark groups, then the keyframe-diagonal pose chunks and the inertial quadratic
-// forms (every part a fixed-order sum: the system is identical run to run).  A forked graph branch for the second
-// launch was measured slower (its fork / join cost more than the overlap gained).
+// buildSystem at state A: the landmark groups, the keyframe-diagonal pose chunks and the inertial edges' quadratic
+// forms in one launch, side by side (build_all_kernel; every part a fixed-order sum: the system is identical run to
+// run).  Measured 29.6 -> 20.8 us per step against the two launches in sequence; a forked graph branch for the second
+// launch had been slower still (its fork / join cost more than the overlap gained).
 static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
     const int n_imu_blk = h->imu_here ? h->n_imu : 0;
+#ifndef OMV_BUILD_SPLIT
+    {
+        const int n_other = h->n_pchunk + n_imu_blk, n_other_pad = (n_other + 7) & ~7;
+        const int grid = n_other_pad + (h->n_lgrp > 0 ? omv::xcd_grid(h->n_lgrp) : 0);
+        if (grid > 0)
+            build_all_kernel<<<grid, kGrpEdges, 0, h->stream>>>(
+                h->rig, A, h->E, h->L, h->n_lgrp, h->G, h->I, h->n_pchunk, n_other, n_other_pad, h->delta_mono,
+                h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu, h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2,
+                h->d_err9, h->d_imu_contrib, c);
+        HIP_OK(hipGetLastError());
+        return OMV_OK;
+    }
+#endif
     if (h->n_lgrp > 0)
         build_land_kernel<<<omv::xcd_grid(h->n_lgrp), kGrpEdges, 0, h->stream>>>(
             h->rig, A, h->E, h->L, h->n_lgrp, h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err, h->d_err3,
@@ -2190,12 +2228,9 @@ static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
                                                             h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2, h->d_err9,
                                                             h->d_imu_contrib, c, b0);
     };
-#ifdef OMV_BUILD_SPLIT   // profiling variant: the pose-chunk and inertial parts as two launches
+    // profiling variant (OMV_BUILD_SPLIT): landmark groups, pose chunks and inertial edges as three launches
     go(0, h->n_pchunk);
     go(h->n_pchunk, n_imu_blk);
-#else
-    go(0, h->n_pchunk + n_imu_blk);
-#endif
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }
@@ -2203,6 +2238,8 @@ static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
 // The trial's reduced system (H + lambda I minus the landmark Schur terms, b, the Schur right-hand side) in one
 // launch; lambda on the pose diagonal once (rank 0 of a sharded solve), every rank damps its own landmarks.
 static omv_status launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
+    // (a last-chunk-assembles fusion of the two measured 4.5x slower: the device-scope fences it needs write back
+    // and invalidate the XCD's L2 per block)
     schur_kernel<<<omv::xcd_grid(h->n_schunk), 256, 0, h->stream>>>(h->L, h->G, h->n_schunk, lambda, c);
     assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, lambda, h->rank == 0 ? 1 : 0, h->d_S,
                                                           h->d_bb, h->d_coef, c);
