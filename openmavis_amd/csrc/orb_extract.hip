@@ -668,11 +668,23 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         B.cnt[i] = 0;
     }
     __syncthreads();
-    for (int k = tid; k < K; k += T) {
-        const float x = (float)(cand[k] & 0xfff);
-        const int n = (int)(x / hX);
-        nid[k] = (uint32_t)n;
-        atomicAdd(&B.cnt[n], 1);
+    // the passes over the keys below keep four global loads in flight per thread (clamped indices: unconditional
+    // loads, so the compiler does not serialise them behind their guards); nid / cand live in global scratch
+    constexpr int kKB = 4;
+    for (int k0 = tid; k0 < K; k0 += kKB * T) {
+        uint32_t cv[kKB];
+#pragma unroll
+        for (int i = 0; i < kKB; ++i) cv[i] = cand[min(k0 + i * T, K - 1)];
+#pragma unroll
+        for (int i = 0; i < kKB; ++i) {
+            const int k = k0 + i * T;
+            if (k < K) {
+                const float x = (float)(cv[i] & 0xfff);
+                const int n = (int)(x / hX);
+                nid[k] = (uint32_t)n;
+                atomicAdd(&B.cnt[n], 1);
+            }
+        }
     }
     __syncthreads();
     // drop empty strips, keep order
@@ -685,7 +697,14 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
             A.x0[j] = B.x0[i], A.x1[j] = B.x1[i], A.y0[j] = B.y0[i], A.y1[j] = B.y1[i], A.cnt[j] = B.cnt[i];
         }
     __syncthreads();
-    for (int k = tid; k < K; k += T) nid[k] = (uint32_t)scanA[nid[k]];
+    for (int k0 = tid; k0 < K; k0 += kKB * T) {
+        uint32_t nv4[kKB];
+#pragma unroll
+        for (int i = 0; i < kKB; ++i) nv4[i] = nid[min(k0 + i * T, K - 1)];
+#pragma unroll
+        for (int i = 0; i < kKB; ++i)
+            if (k0 + i * T < K) nid[k0 + i * T] = (uint32_t)scanA[nv4[i]];
+    }
     __syncthreads();
 
 #ifdef OMV_OCT_PROFILE
@@ -715,6 +734,8 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
             // sort V by (size, UL.x) exactly as libstdc++'s std::sort moves the elements: the introsort
             // partitions one recursion depth at a time, a range per wavefront, the final insertion sort as a
             // stable rank over the block (B is free until step 4: its x0 / x1 / y0 rows hold the items' scratch)
+            // (std::sort's exact element moves are needed: equal (size, UL.x) keys occur in every phase-2 list of
+            // the bench images -- siblings share UL.x -- so a rank sort of distinct keys never applies)
             for (int j = tid; j < nv; j += T) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
             __syncthreads();
             omv::block_introsort_loop(items, nv, sstack, scanA, scanB, tid, T);
@@ -726,16 +747,27 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         }
         __syncthreads();
         // 2. quadrant counts for the candidate nodes
-        for (int k = tid; k < K; k += T) {
-            const uint32_t n = nid[k] & ~kSplitFlag;
-            if (vpos[n] >= 0) {
-                const uint32_t p = cand[k];
-                const int x = p & 0xfff, y = (p >> 12) & 0xfff;
-                const int t = (x < node_mid_x(A, n) ? 0 : 1) + (y < node_mid_y(A, n) ? 0 : 2);
-                atomicAdd(&ccnt[4 * n + t], 1);
-                nid[k] = kSplitFlag | (n << 2) | t;
-            } else {
-                nid[k] = n;
+        for (int k0 = tid; k0 < K; k0 += kKB * T) {
+            uint32_t nv4[kKB], pv4[kKB];
+#pragma unroll
+            for (int i = 0; i < kKB; ++i) {
+                const int kc = min(k0 + i * T, K - 1);
+                nv4[i] = nid[kc], pv4[i] = cand[kc];
+            }
+#pragma unroll
+            for (int i = 0; i < kKB; ++i) {
+                const int k = k0 + i * T;
+                if (k >= K) continue;
+                const uint32_t n = nv4[i] & ~kSplitFlag;
+                if (vpos[n] >= 0) {
+                    const uint32_t p = pv4[i];
+                    const int x = p & 0xfff, y = (p >> 12) & 0xfff;
+                    const int t = (x < node_mid_x(A, n) ? 0 : 1) + (y < node_mid_y(A, n) ? 0 : 2);
+                    atomicAdd(&ccnt[4 * n + t], 1);
+                    nid[k] = kSplitFlag | (n << 2) | t;
+                } else {
+                    nid[k] = n;
+                }
             }
         }
         __syncthreads();
@@ -817,14 +849,22 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         }
         __syncthreads();
         // 5. relabel keys
-        for (int k = tid; k < K; k += T) {
-            const uint32_t v = nid[k];
-            if (v & kSplitFlag) {
-                const int n = (v & ~kSplitFlag) >> 2, t = v & 3;
-                const bool divided = phase2 ? vpos[n] >= 0 : true;
-                nid[k] = divided ? (uint32_t)(-ccnt[4 * n + t] - 1) : (uint32_t)map[n];
-            } else {
-                nid[k] = (uint32_t)map[v];
+        for (int k0 = tid; k0 < K; k0 += kKB * T) {
+            uint32_t nv4[kKB];
+#pragma unroll
+            for (int i = 0; i < kKB; ++i) nv4[i] = nid[min(k0 + i * T, K - 1)];
+#pragma unroll
+            for (int i = 0; i < kKB; ++i) {
+                const int k = k0 + i * T;
+                if (k >= K) continue;
+                const uint32_t v = nv4[i];
+                if (v & kSplitFlag) {
+                    const int n = (v & ~kSplitFlag) >> 2, t = v & 3;
+                    const bool divided = phase2 ? vpos[n] >= 0 : true;
+                    nid[k] = divided ? (uint32_t)(-ccnt[4 * n + t] - 1) : (uint32_t)map[n];
+                } else {
+                    nid[k] = (uint32_t)map[v];
+                }
             }
         }
         // 6. expandable children (> 1 key) in creation order = new indices Q-1 down to 0
@@ -858,10 +898,18 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
     int *best = scanA;
     for (int i = tid; i < m; i += T) best[i] = -1;
     __syncthreads();
-    for (int k = tid; k < K; k += T) {
-        const int n = (int)nid[k];
-        const int key = (int)((cand[k] >> 24) << 23) | (0x7fffff - k);
-        atomicMax(&best[n], key);
+    for (int k0 = tid; k0 < K; k0 += kKB * T) {
+        uint32_t nv4[kKB], pv4[kKB];
+#pragma unroll
+        for (int i = 0; i < kKB; ++i) {
+            const int kc = min(k0 + i * T, K - 1);
+            nv4[i] = nid[kc], pv4[i] = cand[kc];
+        }
+#pragma unroll
+        for (int i = 0; i < kKB; ++i) {
+            const int k = k0 + i * T;
+            if (k < K) atomicMax(&best[(int)nv4[i]], (int)((pv4[i] >> 24) << 23) | (0x7fffff - k));
+        }
     }
     __syncthreads();
     const int lap0 = a.lapping[2 * img], lap1 = a.lapping[2 * img + 1];
