@@ -364,12 +364,14 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 return __builtin_bit_cast(pk16, __builtin_amdgcn_perm(a, b, 0x0c000c00u | ((s + 3) << 16) | (s + 2)));
             };
             auto test = [&](pk16 v, pk16 n0, pk16 n4, pk16 n8, pk16 n12) {   // bits 15 / 31: the pair passes
-                // brighter n > v + t <=> sign((v + t) - n); darker n < v - t <=> sign(n - (v - t))
+                // brighter pair (n0 | n8 > v + t) & (n4 | n12 > v + t) <=> min(max(n0, n8), max(n4, n12)) > v + t,
+                // darker pair <=> max(min(n0, n8), min(n4, n12)) < v - t; each test is the sign of one difference
+                // (v_pk_max_i16 / v_pk_min_i16: 11 packed ops per pixel pair instead of 17)
                 const pk16 vp = v + T0, vm = v - T0;
                 auto sg = [](pk16 x) { return __builtin_bit_cast(uint32_t, x); };
-                const uint32_t a0 = sg(vp - n0), a4 = sg(vp - n4), a8 = sg(vp - n8), a12 = sg(vp - n12);
-                const uint32_t b0 = sg(n0 - vm), b4 = sg(n4 - vm), b8 = sg(n8 - vm), b12 = sg(n12 - vm);
-                return (((a0 | a8) & (a4 | a12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
+                const pk16 hi = __builtin_elementwise_min(__builtin_elementwise_max(n0, n8), __builtin_elementwise_max(n4, n12));
+                const pk16 lo = __builtin_elementwise_max(__builtin_elementwise_min(n0, n8), __builtin_elementwise_min(n4, n12));
+                return (sg(vp - hi) | sg(lo - vm)) & 0x80008000u;
             };
             for (int t0 = 0; t0 < np; t0 += 64) {
                 const int tp = t0 + lane;
@@ -387,8 +389,10 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                     const uint32_t p1 = test(hi(C0, C0, 0), hi(D0, D0, 0), hi(C1, C0, 3), hi(U0, U0, 0), hi(C0, Wm, 1));
                     const uint32_t p2 = test(lo(C1, C1, 0), lo(D1, D1, 0), lo(Wp, C1, 3), lo(U1, U1, 0), lo(C1, C0, 1));
                     const uint32_t p3 = test(hi(C1, C1, 0), hi(D1, D1, 0), hi(Wp, C1, 3), hi(U1, U1, 0), hi(C1, C0, 1));
-                    bits = ((p0 >> 15) & 1u) | ((p0 >> 30) & 2u) | ((p1 >> 13) & 4u) | ((p1 >> 28) & 8u) |
-                           ((p2 >> 11) & 16u) | ((p2 >> 26) & 32u) | ((p3 >> 9) & 64u) | ((p3 >> 24) & 128u);
+                    // bit 2k = p_k bit 15, bit 2k + 1 = p_k bit 31: the shifts land the bit-15s on 0, 2, 4, 6 and the
+                    // bit-31s on 16, 18, 20, 22
+                    const uint32_t xb = (p0 >> 15) | (p1 >> 13) | (p2 >> 11) | (p3 >> 9);
+                    bits = (xb & 0x55u) | ((xb >> 15) & 0xaau);
                     // columns q0 + k of the pair outside [3, rw - 4] (the second dword of a row's last pair
                     // may lie wholly past it)
                     const int q0 = 4 * jq - o;
