@@ -928,7 +928,8 @@ __device__ __forceinline__ double rcp_nr(double x) {
 // j = l & 15, rows q + 4t (q = l >> 4).  Per pass the pivot is a uniform read (v_readlane), the row M_k. a cross-row
 // ds_bpermute issued ahead of the reciprocal, and the column M_.k a DPP row broadcast of lane k of each 16-lane row --
 // no LDS store / load round trip between passes (a v_permlane16/32_swap row broadcast measured slower: more
-// instructions on an issue-bound pass).  A zero / non-finite pivot flags the solve.
+// instructions on an issue-bound pass; so did 2x2 pivot blocks, 4,200 vs 3,760 cycles).  A zero / non-finite
+// pivot flags the solve (through the non-finite entries it leaves).
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     const uint64_t b = __builtin_bit_cast(uint64_t, x);
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
@@ -941,11 +942,10 @@ __device__ __forceinline__ double row_bcast_f64(double x) {   // lane K of each 
     return __builtin_bit_cast(double, r);
 }
 template <int K>
-__device__ __forceinline__ void sweep_pass(double cur[4], int q, int j, bool &ok) {
+__device__ __forceinline__ void sweep_pass(double cur[4], int q, int j) {
     constexpr int tk = K >> 2, qk = K & 3;
     const double p = readlane_f64(cur[tk], 16 * qk + K);
     const double mkj = __shfl(cur[tk], 16 * qk + j, 64);   // issued early: its latency hides behind the reciprocal
-    ok = ok && p != 0.0 && isfinite(p);
     const double r = rcp_nr(p);
     const double f = mkj * r;
 #pragma unroll
@@ -957,12 +957,13 @@ __device__ __forceinline__ void sweep_pass(double cur[4], int q, int j, bool &ok
     }
 }
 template <int K>
-__device__ __forceinline__ void sweep_all(double cur[4], int q, int j, bool &ok) {
+__device__ __forceinline__ void sweep_all(double cur[4], int q, int j) {
     if constexpr (K < 16) {
-        sweep_pass<K>(cur, q, j, ok);
-        sweep_all<K + 1>(cur, q, j, ok);
+        sweep_pass<K>(cur, q, j);
+        sweep_all<K + 1>(cur, q, j);
     }
 }
+
 template <bool G>
 __device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
@@ -972,11 +973,13 @@ __device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
         const int i = q + 4 * t;
         cur[t] = D[i >= j ? sw16(i, j) : sw16(j, i)];
     }
-    bool ok = true;
-    sweep_all<0>(cur, q, j, ok);
+    sweep_all<0>(cur, q, j);
 #pragma unroll
     for (int t = 0; t < 4; ++t) D[sw16(q + 4 * t, j)] = -cur[t];
-    if (lane == 0 && !ok) *bad = 1;
+    // a zero or non-finite pivot leaves an infinite or NaN entry (1 / 0 = inf spreads through its row and column):
+    // one check of the result instead of one per pass
+    const bool fin = isfinite(cur[0]) && isfinite(cur[1]) && isfinite(cur[2]) && isfinite(cur[3]);
+    if (__ballot(!fin) && lane == 0) *bad = 1;
     wave_sync<G>();
 }
 
