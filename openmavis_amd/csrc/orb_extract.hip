@@ -640,11 +640,20 @@ __global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
         if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
         return;
     }
-    // one thread per cell: its keys to [start, next start) (the cells' loads all in flight at once)
+    // one thread per cell: its keys to [start, next start), eight loads in flight before their stores (the store
+    // to cand could alias the next load as far as the compiler knows, which serialised load -> store pairs)
     for (int i = tid; i < ncell; i += T) {
         const int k0 = cellscan[i], k1 = i + 1 < ncell ? cellscan[i + 1] : K;
         const uint32_t *src = a.cell_kp + ((size_t)img * g.n_cells + L.cell_begin + i) * g.cell_cap;
-        for (int k = k0; k < k1; ++k) cand[k] = src[k - k0];
+        for (int b = k0; b < k1; b += 8) {
+            const int nb = min(8, k1 - b);
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[b - k0 + min(u, nb - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < nb) cand[b + u] = v[u];
+        }
     }
     __syncthreads();
 
