@@ -595,7 +595,7 @@ struct OctArgs {
     int *err;
 };
 
-__global__ void __launch_bounds__(256) octree_kernel(Geom g, OctArgs a) {
+__global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   // 6 workgroups per CU (VGPRs <= 80)
     extern __shared__ __attribute__((aligned(16))) int osm[];
     const int img = blockIdx.x / g.nlevels;
     const int l = blockIdx.x - img * g.nlevels;
