@@ -562,23 +562,32 @@ __device__ int block_sum(int v, int *tmp) {
     return t;
 }
 
+// Node rectangles as packed 16-bit pairs (x0 | x1 << 16, y0 | y1 << 16; level coordinates < 2^15): 3 ints per node
+// instead of 5, so the workgroup's LDS stays under 20 KB (eight workgroups per CU)
 struct NodeSoA {
-    int *x0, *x1, *y0, *y1, *cnt;
+    int *xx, *yy, *cnt;
+    __device__ __forceinline__ int x0(int i) const { return xx[i] & 0xffff; }
+    __device__ __forceinline__ int x1(int i) const { return (int)((uint32_t)xx[i] >> 16); }
+    __device__ __forceinline__ int y0(int i) const { return yy[i] & 0xffff; }
+    __device__ __forceinline__ int y1(int i) const { return (int)((uint32_t)yy[i] >> 16); }
+    __device__ __forceinline__ void set(int i, int ax0, int ax1, int ay0, int ay1) const {
+        xx[i] = ax0 | (ax1 << 16), yy[i] = ay0 | (ay1 << 16);
+    }
+    __device__ __forceinline__ void copy_from(int i, const NodeSoA &o, int k) const {
+        xx[i] = o.xx[k], yy[i] = o.yy[k], cnt[i] = o.cnt[k];
+    }
 };
 
 // Quadrant of key (x, y) in node i: 0 = n1 (UL), 1 = n2 (UR), 2 = n3 (BL), 3 = n4 (BR)  (DivideNode)
 __device__ __forceinline__ int node_mid_x(const NodeSoA &A, int i) {
-    return A.x0[i] + (int)ceilf((float)(A.x1[i] - A.x0[i]) / 2);
+    return A.x0(i) + (int)ceilf((float)(A.x1(i) - A.x0(i)) / 2);
 }
 __device__ __forceinline__ int node_mid_y(const NodeSoA &A, int i) {
-    return A.y0[i] + (int)ceilf((float)(A.y1[i] - A.y0[i]) / 2);
+    return A.y0(i) + (int)ceilf((float)(A.y1(i) - A.y0(i)) / 2);
 }
-__device__ __forceinline__ void child_rect(const NodeSoA &A, int i, int t, int &x0, int &x1, int &y0, int &y1) {
+__device__ __forceinline__ void child_rect(const NodeSoA &A, int i, int t, const NodeSoA &Bo, int j) {
     const int xm = node_mid_x(A, i), ym = node_mid_y(A, i);
-    x0 = (t & 1) ? xm : A.x0[i];
-    x1 = (t & 1) ? A.x1[i] : xm;
-    y0 = (t & 2) ? ym : A.y0[i];
-    y1 = (t & 2) ? A.y1[i] : ym;
+    Bo.set(j, (t & 1) ? xm : A.x0(i), (t & 1) ? A.x1(i) : xm, (t & 2) ? ym : A.y0(i), (t & 2) ? A.y1(i) : ym);
 }
 
 constexpr uint32_t kSplitFlag = 0x80000000u;
@@ -595,7 +604,11 @@ struct OctArgs {
     int *err;
 };
 
-__global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   // 6 workgroups per CU (VGPRs <= 80)
+#ifndef OMV_OCT_WGS
+#define OMV_OCT_WGS 7   // workgroups per CU the register budget targets (LDS: 20 KB each; measured 6 / 7 / 8:
+                        // 0.527 / 0.495 / 0.518 ms per 128-frame launch, 8 spills registers)
+#endif
+__global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) int osm[];
     const int img = blockIdx.x / g.nlevels;
     const int l = blockIdx.x - img * g.nlevels;
@@ -606,9 +619,9 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
     int *tmp = osm;                  // 16
     int *shared_int = osm + 16;      // 16 scalars
     int *buf = osm + 32;
-    NodeSoA A{buf, buf + NC, buf + 2 * NC, buf + 3 * NC, buf + 4 * NC};
-    NodeSoA B{buf + 5 * NC, buf + 6 * NC, buf + 7 * NC, buf + 8 * NC, buf + 9 * NC};
-    int *ccnt = buf + 10 * NC;       // ccnt_cap (>= 4 * NC)
+    NodeSoA A{buf, buf + NC, buf + 2 * NC};
+    NodeSoA B{buf + 3 * NC, buf + 4 * NC, buf + 5 * NC};
+    int *ccnt = buf + 6 * NC;        // ccnt_cap (>= 4 * NC)
     int *cellscan = ccnt;            // the level's cells (<= ccnt_cap by host check), gather phase only
     int *rest = ccnt + g.ccnt_cap;
     int *scanA = rest;               // NC
@@ -674,10 +687,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
         return;
     }
     for (int i = tid; i < nIni; i += T) {
-        B.x0[i] = (int)(hX * (float)i);
-        B.x1[i] = (int)(hX * (float)(i + 1));
-        B.y0[i] = 0;
-        B.y1[i] = Hn;
+        B.set(i, (int)(hX * (float)i), (int)(hX * (float)(i + 1)), 0, Hn);
         B.cnt[i] = 0;
     }
     __syncthreads();
@@ -707,7 +717,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
     for (int i = tid; i < nIni; i += T)
         if (B.cnt[i] > 0) {
             const int j = scanA[i];
-            A.x0[j] = B.x0[i], A.x1[j] = B.x1[i], A.y0[j] = B.y0[i], A.y1[j] = B.y1[i], A.cnt[j] = B.cnt[i];
+            A.copy_from(j, B, i);
         }
     __syncthreads();
     for (int k0 = tid; k0 < K; k0 += kKB * T) {
@@ -749,10 +759,10 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
             // stable rank over the block (B is free until step 4: its x0 / x1 / y0 rows hold the items' scratch)
             // (std::sort's exact element moves are needed: equal (size, UL.x) keys occur in every phase-2 list of
             // the bench images -- siblings share UL.x -- so a rank sort of distinct keys never applies)
-            for (int j = tid; j < nv; j += T) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0[vlist[j]], vlist[j]};
+            for (int j = tid; j < nv; j += T) items[j] = omv::SortItem{A.cnt[vlist[j]], A.x0(vlist[j]), vlist[j]};
             __syncthreads();
             omv::block_introsort_loop(items, nv, sstack, scanA, scanB, tid, T);
-            omv::block_final_insertion_sort(items, nv, reinterpret_cast<omv::SortItem *>(B.x0), tid, T);
+            omv::block_final_insertion_sort(items, nv, reinterpret_cast<omv::SortItem *>(B.xx), tid, T);   // B: 3 NC ints
 #ifdef OMV_OCT_PROFILE
             pf_sort += wall_clock64() - pf_r;
 #endif
@@ -801,7 +811,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
             // divide from the back of the sorted list until the list holds >= N nodes (:633-675)
             // the list size after dividing items[nv-1 .. j] is m + sum (children - 1) over them: a suffix
             // sum (block scan over r = nv-1-j); the walk stops at the first r reaching N, else at j = 0
-            int *dv = B.cnt, *dv1 = B.y1;   // B is free until step 4
+            int *dv = B.cnt, *dv1 = B.yy;   // B is free until step 4
             for (int r = tid; r < nv; r += T) {
                 const int n = items[nv - 1 - r].payload;
                 int nk = 0;
@@ -848,7 +858,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
                     const int c = ccnt[4 * i + t];
                     if (c > 0) {
                         const int j = Q - 1 - r;
-                        child_rect(A, i, t, B.x0[j], B.x1[j], B.y0[j], B.y1[j]);
+                        child_rect(A, i, t, B, j);
                         B.cnt[j] = c;
                         ccnt[4 * i + t] = -(j + 1);   // remember the child's new index
                         ++r;
@@ -856,7 +866,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
                 }
             } else {
                 const int j = Q + scanB[i];
-                B.x0[j] = A.x0[i], B.x1[j] = A.x1[i], B.y0[j] = A.y0[i], B.y1[j] = A.y1[i], B.cnt[j] = A.cnt[i];
+                B.copy_from(j, A, i);
                 map[i] = j;
             }
         }
@@ -888,7 +898,7 @@ __global__ void __launch_bounds__(256, 6) octree_kernel(Geom g, OctArgs a) {   /
             if (B.cnt[Q - 1 - j] > 1) vlist[scanA[j]] = Q - 1 - j;
         // swap A <-> B
         for (int i = tid; i < newm; i += T) {
-            A.x0[i] = B.x0[i], A.x1[i] = B.x1[i], A.y0[i] = B.y0[i], A.y1[i] = B.y1[i], A.cnt[i] = B.cnt[i];
+            A.copy_from(i, B, i);
         }
         __syncthreads();
         m = newm;
@@ -1442,7 +1452,7 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
     o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
     o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
-    o->oct_lds = (size_t)(32 + 18 * g.node_cap + g.ccnt_cap + 6 * (g.node_cap / 17 + 1) + 2) * sizeof(int);
+    o->oct_lds = (size_t)(32 + 14 * g.node_cap + g.ccnt_cap + 6 * (g.node_cap / 17 + 1) + 2) * sizeof(int);
     return OMV_OK;
 }
 
