@@ -514,15 +514,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
 }
 
 // K3 --------------------------------------------------------------------------------------------
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
+// (every lane active: the DPP form, six VALU ops instead of six LDS-latency permutes)
+__device__ __forceinline__ int wave_incl_scan(int v) { return wave_incl_scan_dpp(v); }
 
 // In-place exclusive scan of a[0..n) in LDS by the whole (256-thread) block; returns the total.
 __device__ int block_excl_scan(int *a, int n, int *tmp) {
