@@ -73,7 +73,13 @@ struct LmCtl {
     int done;                // the optimisation has ended
     int errors_of_current;   // the last computed errors belong to the current state (A)
     int need_build;          // the next step starts a new iteration (buildSystem)
-    int accepted;            // the last trial was accepted: the trial state B becomes A
+    int accepted;            // the last trial was accepted: the trial state becomes current
+    // double-buffered state and errors (device driver): buffer `cur` holds the current state and its errors, the
+    // trial writes buffer cur ^ 1 and an accepted trial flips `cur` -- no copy, and no recomputation of the
+    // current errors after a rejected trial (they are still in their buffer); `last` = the buffer of the last
+    // computed errors (the reference reports those: g2o keeps a rejected trial's errors after the pop)
+    int cur, last;
+    double cur_chi;          // activeRobustChi2 of the current state
     int g_active, g_errA, g_build;   // gates of the next step (set by ctl_init / finish_trial)
 };
 enum { kGateAlways = 0, kGateErrA = 1, kGateBuild = 2, kGateTrial = 3 };
@@ -84,6 +90,13 @@ __device__ __forceinline__ bool gate_open(const LmCtl *c, int g) {
     return c->g_active != 0;
 }
 __device__ __forceinline__ double lm_lambda(const LmCtl *c, double lambda) { return c ? c->lambda : lambda; }
+
+struct ErrBufs {   // per-edge errors of one state: visual [2E], stereo row [E], chi2 [E], inertial [19 NI]
+    double *err, *err3, *chi2, *err9;
+};
+// Buffer of a role (0 = current, 1 = trial): by the control block's `cur` on the device driver, the role itself
+// without one (the host driver passes the state it means as the first of the pair).
+__device__ __forceinline__ int role_buf(const LmCtl *c, int role) { return c ? ((c->cur ^ role) & 1) : role; }
 
 __device__ __forceinline__ void mono_err_block(int blk, double *sh, Rig rig, State s, Edges E, double delta,
                                                double dsqr, double delta_st, double dsqr_st, double *err,
@@ -169,7 +182,7 @@ __device__ __forceinline__ double sum_chi(const double *mono_partial, int n_mono
 __device__ __forceinline__ void set_gates(LmCtl *c) {
     c->g_active = !c->done;
     c->g_build = !c->done && c->need_build;
-    c->g_errA = c->g_build && !c->errors_of_current;
+    c->g_errA = 0;   // the current errors stay in their buffer (double-buffered): never recomputed
 }
 
 // optimize()'s start: err = activeRobustChi2 of the initial state (Optimizer.cc:3273-3274), LM state reset
@@ -180,8 +193,9 @@ __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *m
     __shared__ double sh[8];
     const double chi = pre ? pre[1] : sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
     if (threadIdx.x == 0) {
-        c->err0 = c->errors_chi = chi;
+        c->err0 = c->errors_chi = c->cur_chi = chi;
         c->errors_of_current = 1;
+        c->cur = c->last = 0;
         c->need_build = 1;
         c->it = c->qmax = c->nBad = c->trials = c->its = 0;
         c->opt_it = opt_it, c->max_trials = max_trials, c->lambda_init = lambda_init;
@@ -192,23 +206,18 @@ __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *m
 }
 
 // One step's LM bookkeeping (optimization_algorithm_levenberg.cpp:61-169), after the trial's errors:
-//   a step that started an iteration: ++its, currentChi = iniChi = activeRobustChi2 of the current state (its
-//   errors recomputed this step when the last ones were a rejected trial's), qmax = 0;
+//   a step that started an iteration: ++its, currentChi = iniChi = activeRobustChi2 of the current state (kept with
+//   its buffer: after a rejected trial the reference recomputes the same errors and gets the same sum), qmax = 0;
 //   the trial: rho, accept (the trial state becomes current) or reject (lambda *= ni), then the do-while /
 //   iteration / nBad stop tests in the reference's order, and the next step's gates.
 __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_partial, int n_mono_blocks,
-                                  const double *imu_partial, const double *mono_partial_a, const double *imu_partial_a,
-                                  const double *scale_partial, int n_scale, const int *fail, const double *pre) {
+                                  const double *imu_partial, const double *scale_partial, int n_scale, const int *fail,
+                                  const double *pre) {
     if (!c->g_active) return;
-    const bool errA = c->g_errA != 0;
-    double chiA = 0, chi, ssum;
-    if (pre) {   // a sharded solve: [chi(A), chi, computeScale] summed over the ranks (trial_scalars_kernel)
-        chiA = pre[0], chi = pre[1], ssum = pre[2];
+    double chi, ssum;
+    if (pre) {   // a sharded solve: [-, chi, computeScale] summed over the ranks (trial_scalars_kernel)
+        chi = pre[1], ssum = pre[2];
     } else {
-        if (errA) {
-            chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
-            __syncthreads();
-        }
         chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
         double sc = 0;
         for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
@@ -216,12 +225,13 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
         ssum = block_reduce_sum(sc, sh);
     }
     if (threadIdx.x != 0) return;
-    if (c->g_build) {   // iteration start
+    if (c->g_build) {   // iteration start: the current state's activeRobustChi2 (its errors are in buffer cur)
         ++c->its;
-        if (errA) c->errors_chi = chiA, c->errors_of_current = 1;
-        c->currentChi = c->iniChi = c->errors_chi;
+        c->currentChi = c->iniChi = c->cur_chi;
         c->qmax = 0;
     }
+    const int trial_buf = c->cur ^ 1;
+    c->last = trial_buf;
     const bool ok = *fail == 0;
     double tempChi = chi;
     c->errors_chi = chi;
@@ -241,6 +251,7 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
         c->currentChi = tempChi;
         c->accepted = 1;
         c->errors_of_current = 1;
+        c->cur = trial_buf, c->cur_chi = chi;   // the trial's buffers become current
     } else {
         c->lambda *= c->ni;
         c->ni *= 2;
@@ -262,65 +273,48 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
     set_gates(c);
 }
 
-// An accepted trial's state B becomes the current state A (one contiguous copy of the state block; after the
-// optimisation ended the flag of its last trial stays set and the copy repeats idempotently).
-__global__ void accept_copy_kernel(const LmCtl *c, const double *B, double *A, size_t n) {
-    if (!c->accepted) return;
+// The current state into buffer 0 at optimize()'s end, when the last accepted trial left it in buffer 1 (one
+// contiguous copy of the state block; idempotent).
+__global__ void cur_copy_kernel(const LmCtl *c, const double *B, double *A, size_t n) {
+    if (!c->cur) return;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (size_t)gridDim.x * blockDim.x) A[q] = B[q];
 }
 
-// A step's opening error launch also carries the copy B -> A of an accepted last trial (instead of the errors of
-// A, which are only recomputed after a rejected trial).
-struct ErrAux {
-    const double *copy_src;   // non-null: copy copy_n doubles to copy_dst when the last trial was accepted
-    double *copy_dst;
-    size_t copy_n;
-};
-
 // computeActiveErrors in one launch: blocks [0, n_mono_blocks) the visual edges (256 each), the block after
-// them (when has_imu) the inertial / random-walk edges.
-__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s, Edges E, double delta,
-                                                  double dsqr, double delta_st, double dsqr_st, double *err, double *err3,
-                                                  double *chi2, double *partial, Imu I, double delta_imu,
-                                                  double dsqr_imu, double *err9, double *imu_partial, const LmCtl *ctl,
-                                                  int gate, ErrAux aux) {
+// them (when has_imu) the inertial / random-walk edges; state and error buffers of the role (role_buf).
+__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s0, State s1, Edges E,
+                                                  double delta, double dsqr, double delta_st, double dsqr_st,
+                                                  ErrBufs e0, ErrBufs e1, double *partial, Imu I, double delta_imu,
+                                                  double dsqr_imu, double *imu_partial, const LmCtl *ctl, int gate,
+                                                  int role) {
     __shared__ double sh[8];
-    if (aux.copy_dst && ctl->accepted) {
-        for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < aux.copy_n; q += (size_t)gridDim.x * blockDim.x)
-            aux.copy_dst[q] = aux.copy_src[q];
-        return;
-    }
     if (!gate_open(ctl, gate)) return;
+    const int bi = role_buf(ctl, role);
+    const State s = bi ? s1 : s0;
+    const ErrBufs e = bi ? e1 : e0;
     if ((int)blockIdx.x < n_mono_blocks)
-        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, partial);
+        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, e.err, e.err3, e.chi2, partial);
     else if (has_imu)
-        imu_err_block(sh, s, I, delta_imu, dsqr_imu, err9, imu_partial);
+        imu_err_block(sh, s, I, delta_imu, dsqr_imu, e.err9, imu_partial);
 }
 
 // One LM step's bookkeeping after the trial's errors (one block of 256).
 __global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
-                                                           const double *imu_partial, const double *mono_partial_a,
-                                                           const double *imu_partial_a, const double *scale_partial,
+                                                           const double *imu_partial, const double *scale_partial,
                                                            int n_scale, const int *fail, const double *pre) {
     __shared__ double sh[8];
-    finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, mono_partial_a, imu_partial_a, scale_partial,
-                      n_scale, fail, pre);
+    finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, scale_partial, n_scale, fail, pre);
 }
 
-// A sharded solve's per-rank scalars, all-reduced before the LM bookkeeping: out = [chi(A) when this step recomputed
-// the current state's errors, chi of the trial, this rank's computeScale terms] (ctl == nullptr: out[1] = chi of
-// the errors just computed, optimize()'s initial err).  Gated like the trial.
+// A sharded solve's per-rank scalars, all-reduced before the LM bookkeeping: out = [0 (unused), chi of the trial,
+// this rank's computeScale terms] (ctl == nullptr: out[1] = chi of the errors just computed, optimize()'s initial
+// err).  Gated like the trial.
 __global__ void __launch_bounds__(256) trial_scalars_kernel(const LmCtl *c, const double *mono_partial, int n_mono_blocks,
-                                                            const double *imu_partial, const double *mono_partial_a,
-                                                            const double *imu_partial_a, const double *scale_partial,
+                                                            const double *imu_partial, const double *scale_partial,
                                                             int n_scale, double *out) {
     __shared__ double sh[8];
     if (c && !c->g_active) return;
-    double chiA = 0;
-    if (c && c->g_errA) {
-        chiA = sum_chi(mono_partial_a, n_mono_blocks, imu_partial_a, sh);
-        __syncthreads();
-    }
+    const double chiA = 0;   // (unused: the current errors are kept, double-buffered)
     const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
     double sc = 0;
     if (c)
@@ -685,25 +679,32 @@ __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Im
 // per trial from these per-landmark, per-chunk and per-edge parts): build_land_kernel, one block per landmark group
 // (Hll, bl, Hpl per slot); build_kernel, blocks [0, n_pchunk) the keyframe-diagonal pose chunks, then one block per
 // inertial edge (its 30 x 30 quadratic form).
-__global__ void __launch_bounds__(kGrpEdges) build_land_kernel(Rig rig, State s, Edges E, Land L, int n_grp, double delta,
-                                                               double dsqr, double delta_st, double dsqr_st,
-                                                               const double *err, const double *err3, const double *chi2,
+__global__ void __launch_bounds__(kGrpEdges) build_land_kernel(Rig rig, State s0, State s1, Edges E, Land L, int n_grp,
+                                                               double delta, double dsqr, double delta_st,
+                                                               double dsqr_st, ErrBufs e0, ErrBufs e1,
                                                                const LmCtl *ctl) {
     __shared__ double T[kLandTerms * kGrpEdges];
     __shared__ LandAcc big_acc;
     if (!gate_open(ctl, kGateBuild)) return;
+    const int bi = role_buf(ctl, 0);
+    const State s = bi ? s1 : s0;
+    const double *err = bi ? e1.err : e0.err, *err3 = bi ? e1.err3 : e0.err3, *chi2 = bi ? e1.chi2 : e0.chi2;
     const int g = omv::xcd_block(n_grp);
     if (g < 0) return;
     land_group(g, T, &big_acc, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
 }
 
-__global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s, Edges E, Gather G, Imu I, int n_pchunk,
-                                                          double delta, double dsqr, double delta_st, double dsqr_st,
-                                                          double delta_imu, double dsqr_imu, const double *err,
-                                                          const double *err3, const double *chi2, const double *err9,
-                                                          double *contrib, const LmCtl *ctl, int blk0) {
+__global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s0, State s1, Edges E, Gather G, Imu I,
+                                                          int n_pchunk, double delta, double dsqr, double delta_st,
+                                                          double dsqr_st, double delta_imu, double dsqr_imu,
+                                                          ErrBufs e0, ErrBufs e1, double *contrib, const LmCtl *ctl,
+                                                          int blk0) {
     __shared__ double sm[441];
     if (!gate_open(ctl, kGateBuild)) return;
+    const int bi = role_buf(ctl, 0);
+    const State s = bi ? s1 : s0;
+    const ErrBufs eb = bi ? e1 : e0;
+    const double *err = eb.err, *err3 = eb.err3, *chi2 = eb.chi2, *err9 = eb.err9;
     const int blk = blockIdx.x + blk0;
     if (blk < n_pchunk) pose_chunk_block(blk, sm, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
     else imu_contrib_block(blk - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
@@ -713,15 +714,18 @@ __global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s, Edge
 // blocks from n_other_pad (n_other rounded up to 8, so the landmark groups keep their XCD-aware order) the landmark
 // groups (build_land_kernel's work).  The two halves are independent and each is latency-bound with few blocks, so
 // side by side they take about the longer one's time instead of the sum.
-__global__ void __launch_bounds__(kGrpEdges) build_all_kernel(Rig rig, State s, Edges E, Land L, int n_grp, Gather G,
-                                                              Imu I, int n_pchunk, int n_other, int n_other_pad,
+__global__ void __launch_bounds__(kGrpEdges) build_all_kernel(Rig rig, State s0, State s1, Edges E, Land L, int n_grp,
+                                                              Gather G, Imu I, int n_pchunk, int n_other, int n_other_pad,
                                                               double delta, double dsqr, double delta_st, double dsqr_st,
-                                                              double delta_imu, double dsqr_imu, const double *err,
-                                                              const double *err3, const double *chi2, const double *err9,
+                                                              double delta_imu, double dsqr_imu, ErrBufs e0, ErrBufs e1,
                                                               double *contrib, const LmCtl *ctl) {
     __shared__ double T[kLandTerms * kGrpEdges];
     __shared__ LandAcc big_acc;
     if (!gate_open(ctl, kGateBuild)) return;
+    const int bi = role_buf(ctl, 0);   // the current state and its errors
+    const State s = bi ? s1 : s0;
+    const ErrBufs eb = bi ? e1 : e0;
+    const double *err = eb.err, *err3 = eb.err3, *chi2 = eb.chi2, *err9 = eb.err9;
     const int b = blockIdx.x;
     if (b < n_other_pad) {
         if (b >= n_other) return;
@@ -1290,11 +1294,13 @@ __device__ __forceinline__ void backsub_block(int blk, double *sh, Land L, Red R
 // pose part of computeScale is counted once by the caller's choice of scale partials).
 __global__ void __launch_bounds__(kLandWG) update_kernel(Rig rig, Land L, Red R, const double *b, const int *offV,
                                                          const int *offG, const int *offA, int n_opt, double lambda,
-                                                         const double *xp, State a, State bst, double *scale_partial,
+                                                         const double *xp, State s0, State s1, double *scale_partial,
                                                          const LmCtl *ctl) {
     __shared__ double sh[8];
     if (!gate_open(ctl, kGateTrial)) return;
     lambda = lm_lambda(ctl, lambda);
+    const int ba = role_buf(ctl, 0);   // current -> trial
+    const State a = ba ? s1 : s0, bst = ba ? s0 : s1;
     if (blockIdx.x == 0) update_kf_block(sh, rig, R, b, offV, offG, offA, n_opt, lambda, xp, a, bst, scale_partial);
     else backsub_block(blockIdx.x - 1, sh, L, R, lambda, xp, a, bst, scale_partial);
 }
@@ -1305,8 +1311,10 @@ __global__ void __launch_bounds__(kLandWG) update_kernel(Rig rig, Land L, Red R,
 // the chi2, and the points in the caller's order; the host reads one staging block.
 __global__ void epilogue_kernel(Rig rig, State s, Edges E, const int *perm_edge, int n_mono_all,
                                 const float *track_depth, const int *perm_pt, int n_pts, uint8_t *flags,
-                                double *chi2_out, double *pts_out, const double *chi2, double *head, int n_head) {
+                                double *chi2_out, double *pts_out, const double *chi2_0, const double *chi2_1,
+                                const LmCtl *ctl, double *head, int n_head) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const double *chi2 = ctl && ctl->last ? chi2_1 : chi2_0;   // the last computed errors (a rejected trial's too)
     if (q < n_head) head[q] = s.Rwb[q];   // the keyframe part of the state (it precedes the points)
     if (q < E.n) {
         const int e = q, o = perm_edge[e];
@@ -1515,8 +1523,9 @@ struct omv_lba {
     bool epi_chi2 = false;     //   including the chi2
     int *d_offP = nullptr, *d_offV = nullptr, *d_offG = nullptr, *d_offA = nullptr;
     double *d_err = nullptr, *d_chi2 = nullptr, *d_err9 = nullptr;
+    double *d_err_b = nullptr, *d_chi2_b = nullptr, *d_err9_b = nullptr, *d_err3_b = nullptr;   // the second error buffer
+    ErrBufs eb(int i) const { return i ? ErrBufs{d_err_b, d_err3_b, d_chi2_b, d_err9_b} : ErrBufs{d_err, d_err3, d_chi2, d_err9}; }
     double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
-    double *d_partial_a = nullptr, *d_imu_partial_a = nullptr;   // the current state's errors recomputed in a step
     double *h_out = nullptr;   // pinned host copy of d_out: the per-trial 24-byte read-back
     LmCtl *d_ctl = nullptr;    // device-resident LM control (single-rank path)
     LmCtl *h_ctl = nullptr;    // pinned copy: the one read-back per optimize()
@@ -2063,10 +2072,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_chi2 = dalloc<double>(ow, E);
     h->d_err3 = dalloc<double>(ow, E);
     h->d_err9 = dalloc<double>(ow, 19 * (size_t)NI);   // [9n errors | n chi2 | 9n rotation errors eR]
+    h->d_err_b = dalloc<double>(ow, 2 * (size_t)E);       // the device driver's second (double-buffered) set
+    h->d_chi2_b = dalloc<double>(ow, E);
+    h->d_err3_b = dalloc<double>(ow, E);
+    h->d_err9_b = dalloc<double>(ow, 19 * (size_t)NI);
     h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
     h->d_imu_partial = dalloc<double>(ow, 1);
-    h->d_partial_a = dalloc<double>(ow, std::max(1, h->n_wg_edge));
-    h->d_imu_partial_a = dalloc<double>(ow, 1);
     h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
     h->d_out = dalloc<double>(ow, 4);
     // [packed blocks | b | coef]: contiguous, the one buffer a sharded solve all-reduces per trial
@@ -2079,7 +2090,6 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_fail = dalloc<int>(ow, 1);
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
-    HIP_OK(hipMemset(h->d_imu_partial_a, 0, sizeof(double)));
     // device epilogue (single rank): caller-order permutations, trackDepth in device order, the staging block
     if (h->world == 1) {
         std::vector<float> td(P, 1e30f);
@@ -2102,18 +2112,20 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 
 // ---- the LM driver ---------------------------------------------------------------------------------
 // computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
-static omv_status lba_errors(omv_lba *h, const State &s, const LmCtl *ctl = nullptr, int gate = kGateAlways,
-                             bool partial_a = false, ErrAux aux = ErrAux{}) {
+// lba_errors: the errors of state s into the first error buffer (host driver, optimize()'s start, evaluation);
+// lba_trial_errors: the device driver's trial state and buffer (role 1 of the control block's `cur`).
+static omv_status launch_errors(omv_lba *h, const State &s0, const State &s1, const LmCtl *ctl, int gate, int role) {
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
-    int blocks = nmb + (h->imu_here ? 1 : 0);
-    if (aux.copy_dst) blocks = std::max(blocks, 1);   // the copy runs even without edges
+    const int blocks = nmb + (h->imu_here ? 1 : 0);
     if (blocks > 0)
-        err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s, h->E, h->delta_mono, h->dsqr_mono,
-                                                  h->delta_st, h->dsqr_st, h->d_err, h->d_err3, h->d_chi2,
-                                                  partial_a ? h->d_partial_a : h->d_partial, h->I, h->delta_imu,
-                                                  h->dsqr_imu, h->d_err9, partial_a ? h->d_imu_partial_a : h->d_imu_partial,
-                                                  ctl, gate, aux);
+        err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s0, s1, h->E, h->delta_mono,
+                                                  h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0), h->eb(1), h->d_partial,
+                                                  h->I, h->delta_imu, h->dsqr_imu, h->d_imu_partial, ctl, gate, role);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
+}
+static omv_status lba_errors(omv_lba *h, const State &s) { return launch_errors(h, s, s, nullptr, kGateAlways, 0); }
+static omv_status lba_trial_errors(omv_lba *h, const LmCtl *c) {
+    return launch_errors(h, h->st[0], h->st[1], c, kGateTrial, 1);
 }
 
 // In-place SUM over the ranks of a sharded solve (no-op on one rank).
@@ -2205,7 +2217,7 @@ static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2);
 // forms in one launch, side by side (build_all_kernel; every part a fixed-order sum: the system is identical run to
 // run).  Measured 29.6 -> 20.8 us per step against the two launches in sequence; a forked graph branch for the second
 // launch had been slower still (its fork / join cost more than the overlap gained).
-static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
+static omv_status launch_build(omv_lba *h, const State &A, const State &B, const LmCtl *c) {
     const int n_imu_blk = h->imu_here ? h->n_imu : 0;
 #ifndef OMV_BUILD_SPLIT
     {
@@ -2213,23 +2225,21 @@ static omv_status launch_build(omv_lba *h, const State &A, const LmCtl *c) {
         const int grid = n_other_pad + (h->n_lgrp > 0 ? omv::xcd_grid(h->n_lgrp) : 0);
         if (grid > 0)
             build_all_kernel<<<grid, kGrpEdges, 0, h->stream>>>(
-                h->rig, A, h->E, h->L, h->n_lgrp, h->G, h->I, h->n_pchunk, n_other, n_other_pad, h->delta_mono,
-                h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu, h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2,
-                h->d_err9, h->d_imu_contrib, c);
+                h->rig, A, B, h->E, h->L, h->n_lgrp, h->G, h->I, h->n_pchunk, n_other, n_other_pad, h->delta_mono,
+                h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu, h->dsqr_imu, h->eb(0), h->eb(1), h->d_imu_contrib, c);
         HIP_OK(hipGetLastError());
         return OMV_OK;
     }
 #endif
     if (h->n_lgrp > 0)
         build_land_kernel<<<omv::xcd_grid(h->n_lgrp), kGrpEdges, 0, h->stream>>>(
-            h->rig, A, h->E, h->L, h->n_lgrp, h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->d_err, h->d_err3,
-            h->d_chi2, c);
+            h->rig, A, B, h->E, h->L, h->n_lgrp, h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0),
+            h->eb(1), c);
     auto go = [&](int b0, int nblk) {
         if (nblk > 0)
-            build_kernel<<<nblk, kGrpEdges, 0, h->stream>>>(h->rig, A, h->E, h->G, h->I, h->n_pchunk, h->delta_mono,
+            build_kernel<<<nblk, kGrpEdges, 0, h->stream>>>(h->rig, A, B, h->E, h->G, h->I, h->n_pchunk, h->delta_mono,
                                                             h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu,
-                                                            h->dsqr_imu, h->d_err, h->d_err3, h->d_chi2, h->d_err9,
-                                                            h->d_imu_contrib, c, b0);
+                                                            h->dsqr_imu, h->eb(0), h->eb(1), h->d_imu_contrib, c, b0);
     };
     // profiling variant (OMV_BUILD_SPLIT): landmark groups, pose chunks and inertial edges as three launches
     go(0, h->n_pchunk);
@@ -2264,20 +2274,17 @@ static void launch_update(omv_lba *h, double lambda, const State &A, const State
                                                                h->d_scale_partial, c);
 }
 
-// One LM step of the single-rank path: the gated kernel sequence (see LmCtl).  A = st[0] is always the
-// current state and B = st[1] the trial.  The step opens with the copy B -> A of an accepted last trial (or, after
-// a rejected one, the errors of A when an iteration starts) and closes with the trial's errors and the LM
-// bookkeeping.  With `ev`, events bracket the stages (build, Schur, solve, update + errors).
+// One LM step of the device driver: the gated kernel sequence (see LmCtl).  The state and error buffers are
+// double-buffered: the kernels take both (st[0], st[1]) and pick the current / trial one by the control block's
+// `cur`, an accepted trial flips it -- no copy launch, and no recomputation of the current errors after a rejected
+// trial.  With `ev`, events bracket the stages (build, Schur, solve, update + errors).
 static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     hipStream_t st = h->stream;
     LmCtl *c = h->d_ctl;
     const State &A = h->st[0], &B = h->st[1];
     omv_status rs;
-    ErrAux start{};
-    start.copy_src = B.Rwb, start.copy_dst = A.Rwb, start.copy_n = h->state_doubles();
-    if ((rs = lba_errors(h, A, c, kGateErrA, true, start)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[0], st));
-    if ((rs = launch_build(h, A, c)) != OMV_OK) return rs;
+    if ((rs = launch_build(h, A, B, c)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
     if ((rs = launch_schur(h, 0.0, c)) != OMV_OK) return rs;
     // sharded: one in-place SUM of this rank's partial reduced system [blocks | b | Schur rhs], ordered on the stream
@@ -2286,18 +2293,18 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     launch_ldlt(h, c);
     if (ev) HIP_OK(hipEventRecord(ev[3], st));
     launch_update(h, 0.0, A, B, c);
-    if ((rs = lba_errors(h, B, c, kGateTrial)) != OMV_OK) return rs;
+    if ((rs = lba_trial_errors(h, c)) != OMV_OK) return rs;
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0, nsc = h->n_pts > 0 ? h->n_wg_land + 1 : 1;
     const double *pre = nullptr;
     if (h->world > 1) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
         const int s0 = h->rank > 0 ? 1 : 0;   // the keyframe part of computeScale enters once (rank 0)
-        trial_scalars_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a,
-                                                h->d_imu_partial_a, h->d_scale_partial + s0, nsc - s0, h->d_out);
+        trial_scalars_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_scale_partial + s0,
+                                                nsc - s0, h->d_out);
         if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
         pre = h->d_out;
     }
-    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_partial_a, h->d_imu_partial_a,
-                                           h->d_scale_partial, nsc, h->d_fail, pre);
+    finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_scale_partial, nsc, h->d_fail,
+                                           pre);
     if (ev) HIP_OK(hipEventRecord(ev[4], st));
     HIP_OK(hipGetLastError());
     return OMV_OK;
@@ -2324,7 +2331,7 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
     const bool sharded = h->world > 1;
     if (sharded) {
-        trial_scalars_kernel<<<1, 256, 0, st>>>(nullptr, h->d_partial, nmb, h->d_imu_partial, nullptr, nullptr, nullptr,
+        trial_scalars_kernel<<<1, 256, 0, st>>>(nullptr, h->d_partial, nmb, h->d_imu_partial, nullptr,
                                                 0, h->d_out);
         if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
     }
@@ -2382,7 +2389,7 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
         batch = std::min(4, max_steps - launched);
     }
     if (!h->epi_ready) {   // the last accepted trial's state into A
-        accept_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
+        cur_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
         HIP_OK(hipGetLastError());
     }
     const LmCtl &c = *h->h_ctl;
@@ -2438,7 +2445,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         const double iniChi = currentChi;
         // buildSystem
         HIP_OK(hipEventRecord(h->ev[0], st));
-        if ((rs = launch_build(h, A, nullptr)) != OMV_OK) return rs;
+        if ((rs = launch_build(h, A, A, nullptr)) != OMV_OK) return rs;
         HIP_OK(hipEventRecord(h->ev[1], st));
         HIP_OK(hipGetLastError());
         if (it == 0) {
@@ -2530,11 +2537,12 @@ static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2) {
     double *d_pts = h->d_stage + head;
     uint8_t *d_flags = (uint8_t *)(d_pts + 3 * (size_t)P);
     double *d_chi2 = d_pts + 3 * (size_t)P + fl;
-    if (!h->host_lm) accept_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
+    if (!h->host_lm) cur_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
     const int n = std::max(std::max(E, P), (int)head);
     epilogue_kernel<<<(n + 255) / 256, 256, 0, st>>>(h->rig, s, h->E, h->d_perm_edge, h->n_mono_all, h->d_track_depth,
                                                      h->d_perm_pt, P, d_flags, want_chi2 ? d_chi2 : nullptr, d_pts,
-                                                     h->d_chi2, h->d_stage, (int)head);
+                                                     h->d_chi2, h->d_chi2_b, h->host_lm ? nullptr : h->d_ctl,
+                                                     h->d_stage, (int)head);
     HIP_OK(hipGetLastError());
     const size_t bytes = (head + 3 * (size_t)P + fl + (want_chi2 ? (size_t)E : 0)) * sizeof(double);
     HIP_OK(hipMemcpyAsync(h->h_stage, h->d_stage, bytes, hipMemcpyDeviceToHost, st));
@@ -2581,7 +2589,9 @@ static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_p
     // sharded rank: this rank's landmarks and edges only, on the host
     std::vector<double> stg(h->state_doubles()), chi2(E);
     HIP_OK(hipMemcpyAsync(stg.data(), s.Rwb, stg.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-    if (E > 0) HIP_OK(hipMemcpyAsync(chi2.data(), h->d_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
+    // the last computed errors: buffer `last` of the device driver's control block (the host driver uses the first)
+    const double *d_last_chi2 = (!h->host_lm && h->h_ctl && h->h_ctl->last) ? h->d_chi2_b : h->d_chi2;
+    if (E > 0) HIP_OK(hipMemcpyAsync(chi2.data(), d_last_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     take_head(stg.data());
     {
