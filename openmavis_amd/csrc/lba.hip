@@ -79,6 +79,7 @@ struct LmCtl {
     // current errors after a rejected trial (they are still in their buffer); `last` = the buffer of the last
     // computed errors (the reference reports those: g2o keeps a rejected trial's errors after the pop)
     int cur, last;
+    int init_pending;        // optimize()'s initial chi not summed yet (the first step's bookkeeping does it)
     double cur_chi;          // activeRobustChi2 of the current state
     int g_active, g_errA, g_build;   // gates of the next step (set by ctl_init / finish_trial)
 };
@@ -185,23 +186,37 @@ __device__ __forceinline__ void set_gates(LmCtl *c) {
     c->g_errA = 0;   // the current errors stay in their buffer (double-buffered): never recomputed
 }
 
+// The LM state reset of optimize()'s start (iteration 0's lambda = lambda_init, ni = 2, nBad = 0,
+// optimization_algorithm_levenberg.cpp:103-108), without the initial chi.
+struct LmReset {
+    LmCtl *c;   // null: no reset
+    int opt_it, max_trials;
+    double lambda_init;
+};
+__device__ __forceinline__ void ctl_reset(const LmReset &r) {
+    LmCtl *c = r.c;
+    c->errors_of_current = 1;
+    c->cur = c->last = 0;
+    c->need_build = 1;
+    c->it = c->qmax = c->nBad = c->trials = c->its = 0;
+    c->opt_it = r.opt_it, c->max_trials = r.max_trials, c->lambda_init = r.lambda_init;
+    c->lambda = r.lambda_init, c->ni = 2, c->rho = 0, c->accepted = 0;
+    c->done = r.opt_it <= 0;
+    set_gates(c);
+}
+
 // optimize()'s start: err = activeRobustChi2 of the initial state (Optimizer.cc:3273-3274), LM state reset
-// (iteration 0's lambda = lambda_init, ni = 2, nBad = 0, optimization_algorithm_levenberg.cpp:103-108).
+// (used when no step follows, opt_it <= 0; otherwise the initial error launch resets the control block and the
+// first step's bookkeeping sums the initial chi -- one launch less per optimize()).
 __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                                        const double *imu_partial, int opt_it, int max_trials,
                                                        double lambda_init, const double *pre) {
     __shared__ double sh[8];
     const double chi = pre ? pre[1] : sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
     if (threadIdx.x == 0) {
+        ctl_reset(LmReset{c, opt_it, max_trials, lambda_init});
         c->err0 = c->errors_chi = c->cur_chi = chi;
-        c->errors_of_current = 1;
-        c->cur = c->last = 0;
-        c->need_build = 1;
-        c->it = c->qmax = c->nBad = c->trials = c->its = 0;
-        c->opt_it = opt_it, c->max_trials = max_trials, c->lambda_init = lambda_init;
-        c->lambda = lambda_init, c->ni = 2, c->rho = 0, c->accepted = 0;
-        c->done = opt_it <= 0;
-        set_gates(c);
+        c->init_pending = 0;
     }
 }
 
@@ -212,12 +227,17 @@ __global__ void __launch_bounds__(256) ctl_init_kernel(LmCtl *c, const double *m
 //   iteration / nBad stop tests in the reference's order, and the next step's gates.
 __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                   const double *imu_partial, const double *scale_partial, int n_scale, const int *fail,
-                                  const double *pre) {
+                                  const double *pre, const double *mono_partial0, const double *imu_partial0) {
     if (!c->g_active) return;
-    double chi, ssum;
-    if (pre) {   // a sharded solve: [-, chi, computeScale] summed over the ranks (trial_scalars_kernel)
-        chi = pre[1], ssum = pre[2];
+    const bool initp = c->init_pending != 0;
+    double chi, ssum, chi0 = 0;
+    if (pre) {   // a sharded solve: [initial chi (first step), chi, computeScale] summed over the ranks
+        chi0 = pre[0], chi = pre[1], ssum = pre[2];
     } else {
+        if (initp) {   // optimize()'s initial errors (their own partial buffers)
+            chi0 = sum_chi(mono_partial0, n_mono_blocks, imu_partial0, sh);
+            __syncthreads();
+        }
         chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
         double sc = 0;
         for (int i = threadIdx.x; i < n_scale; i += blockDim.x) sc += scale_partial[i];
@@ -225,6 +245,7 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
         ssum = block_reduce_sum(sc, sh);
     }
     if (threadIdx.x != 0) return;
+    if (initp) c->err0 = c->errors_chi = c->cur_chi = chi0, c->init_pending = 0;
     if (c->g_build) {   // iteration start: the current state's activeRobustChi2 (its errors are in buffer cur)
         ++c->its;
         c->currentChi = c->iniChi = c->cur_chi;
@@ -286,8 +307,9 @@ __global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu
                                                   double delta, double dsqr, double delta_st, double dsqr_st,
                                                   ErrBufs e0, ErrBufs e1, double *partial, Imu I, double delta_imu,
                                                   double dsqr_imu, double *imu_partial, const LmCtl *ctl, int gate,
-                                                  int role) {
+                                                  int role, LmReset reset) {
     __shared__ double sh[8];
+    if (reset.c && blockIdx.x == 0 && threadIdx.x == 0) ctl_reset(reset), reset.c->init_pending = 1;
     if (!gate_open(ctl, gate)) return;
     const int bi = role_buf(ctl, role);
     const State s = bi ? s1 : s0;
@@ -301,9 +323,11 @@ __global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu
 // One LM step's bookkeeping after the trial's errors (one block of 256).
 __global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                                            const double *imu_partial, const double *scale_partial,
-                                                           int n_scale, const int *fail, const double *pre) {
+                                                           int n_scale, const int *fail, const double *pre,
+                                                           const double *mono_partial0, const double *imu_partial0) {
     __shared__ double sh[8];
-    finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, scale_partial, n_scale, fail, pre);
+    finish_trial_body(sh, c, mono_partial, n_mono_blocks, imu_partial, scale_partial, n_scale, fail, pre,
+                      mono_partial0, imu_partial0);
 }
 
 // A sharded solve's per-rank scalars, all-reduced before the LM bookkeeping: out = [0 (unused), chi of the trial,
@@ -311,10 +335,15 @@ __global__ void __launch_bounds__(256) finish_trial_kernel(LmCtl *c, const doubl
 // err).  Gated like the trial.
 __global__ void __launch_bounds__(256) trial_scalars_kernel(const LmCtl *c, const double *mono_partial, int n_mono_blocks,
                                                             const double *imu_partial, const double *scale_partial,
-                                                            int n_scale, double *out) {
+                                                            int n_scale, double *out, const double *mono_partial0,
+                                                            const double *imu_partial0) {
     __shared__ double sh[8];
     if (c && !c->g_active) return;
-    const double chiA = 0;   // (unused: the current errors are kept, double-buffered)
+    double chiA = 0;   // the initial chi while the first step's bookkeeping still has to take it
+    if (c && c->init_pending) {
+        chiA = sum_chi(mono_partial0, n_mono_blocks, imu_partial0, sh);
+        __syncthreads();
+    }
     const double chi = sum_chi(mono_partial, n_mono_blocks, imu_partial, sh);
     double sc = 0;
     if (c)
@@ -1309,12 +1338,18 @@ __global__ void __launch_bounds__(kLandWG) update_kernel(Rig rig, Land L, Red R,
 // (Optimizer.cc:3282-3311: EdgeMono chi2 > 5.991, or > 1.5 * 5.991 when the point's trackDepth < 10, or a
 // non-positive depth; EdgeStereo chi2 > 7.815) at the final state, written in the caller's edge order with
 // the chi2, and the points in the caller's order; the host reads one staging block.
-__global__ void epilogue_kernel(Rig rig, State s, Edges E, const int *perm_edge, int n_mono_all,
-                                const float *track_depth, const int *perm_pt, int n_pts, uint8_t *flags,
+__global__ void epilogue_kernel(Rig rig, State s0, State s1, size_t n_state, Edges E, const int *perm_edge,
+                                int n_mono_all, const float *track_depth, const int *perm_pt, int n_pts, uint8_t *flags,
                                 double *chi2_out, double *pts_out, const double *chi2_0, const double *chi2_1,
                                 const LmCtl *ctl, double *head, int n_head) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     const double *chi2 = ctl && ctl->last ? chi2_1 : chi2_0;   // the last computed errors (a rejected trial's too)
+    // the device driver's current state (double-buffered); buffer 1 is also copied into buffer 0, where the next
+    // optimize() starts
+    const bool in1 = ctl && ctl->cur;
+    const State s = in1 ? s1 : s0;
+    if (in1)
+        for (size_t k = q; k < n_state; k += (size_t)gridDim.x * blockDim.x) s0.Rwb[k] = s1.Rwb[k];
     if (q < n_head) head[q] = s.Rwb[q];   // the keyframe part of the state (it precedes the points)
     if (q < E.n) {
         const int e = q, o = perm_edge[e];
@@ -1526,6 +1561,7 @@ struct omv_lba {
     double *d_err_b = nullptr, *d_chi2_b = nullptr, *d_err9_b = nullptr, *d_err3_b = nullptr;   // the second error buffer
     ErrBufs eb(int i) const { return i ? ErrBufs{d_err_b, d_err3_b, d_chi2_b, d_err9_b} : ErrBufs{d_err, d_err3, d_chi2, d_err9}; }
     double *d_partial = nullptr, *d_imu_partial = nullptr, *d_scale_partial = nullptr, *d_out = nullptr;
+    double *d_partial0 = nullptr, *d_imu_partial0 = nullptr;   // optimize()'s initial errors (device driver)
     double *h_out = nullptr;   // pinned host copy of d_out: the per-trial 24-byte read-back
     LmCtl *d_ctl = nullptr;    // device-resident LM control (single-rank path)
     LmCtl *h_ctl = nullptr;    // pinned copy: the one read-back per optimize()
@@ -2078,6 +2114,8 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_err9_b = dalloc<double>(ow, 19 * (size_t)NI);
     h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
     h->d_imu_partial = dalloc<double>(ow, 1);
+    h->d_partial0 = dalloc<double>(ow, std::max(1, h->n_wg_edge));
+    h->d_imu_partial0 = dalloc<double>(ow, 1);
     h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
     h->d_out = dalloc<double>(ow, 4);
     // [packed blocks | b | coef]: contiguous, the one buffer a sharded solve all-reduces per trial
@@ -2090,6 +2128,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_fail = dalloc<int>(ow, 1);
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
+    HIP_OK(hipMemset(h->d_imu_partial0, 0, sizeof(double)));
     // device epilogue (single rank): caller-order permutations, trackDepth in device order, the staging block
     if (h->world == 1) {
         std::vector<float> td(P, 1e30f);
@@ -2114,13 +2153,16 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 // computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
 // lba_errors: the errors of state s into the first error buffer (host driver, optimize()'s start, evaluation);
 // lba_trial_errors: the device driver's trial state and buffer (role 1 of the control block's `cur`).
-static omv_status launch_errors(omv_lba *h, const State &s0, const State &s1, const LmCtl *ctl, int gate, int role) {
+static omv_status launch_errors(omv_lba *h, const State &s0, const State &s1, const LmCtl *ctl, int gate, int role,
+                                LmReset reset = LmReset{}, bool init_partials = false) {
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
     const int blocks = nmb + (h->imu_here ? 1 : 0);
     if (blocks > 0)
         err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s0, s1, h->E, h->delta_mono,
-                                                  h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0), h->eb(1), h->d_partial,
-                                                  h->I, h->delta_imu, h->dsqr_imu, h->d_imu_partial, ctl, gate, role);
+                                                  h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0), h->eb(1),
+                                                  init_partials ? h->d_partial0 : h->d_partial, h->I, h->delta_imu,
+                                                  h->dsqr_imu, init_partials ? h->d_imu_partial0 : h->d_imu_partial,
+                                                  ctl, gate, role, reset);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
 static omv_status lba_errors(omv_lba *h, const State &s) { return launch_errors(h, s, s, nullptr, kGateAlways, 0); }
@@ -2299,12 +2341,12 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     if (h->world > 1) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
         const int s0 = h->rank > 0 ? 1 : 0;   // the keyframe part of computeScale enters once (rank 0)
         trial_scalars_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_scale_partial + s0,
-                                                nsc - s0, h->d_out);
+                                                nsc - s0, h->d_out, h->d_partial0, h->d_imu_partial0);
         if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
         pre = h->d_out;
     }
     finish_trial_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_scale_partial, nsc, h->d_fail,
-                                           pre);
+                                           pre, h->d_partial0, h->d_imu_partial0);
     if (ev) HIP_OK(hipEventRecord(ev[4], st));
     HIP_OK(hipGetLastError());
     return OMV_OK;
@@ -2327,16 +2369,24 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
     }
     omv_status rs;
     h->host_syncs = 0;
-    if ((rs = lba_errors(h, h->st[0])) != OMV_OK) return rs;
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
     const bool sharded = h->world > 1;
-    if (sharded) {
-        trial_scalars_kernel<<<1, 256, 0, st>>>(nullptr, h->d_partial, nmb, h->d_imu_partial, nullptr,
-                                                0, h->d_out);
-        if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
+    if (o->opt_it > 0 && nmb + (h->imu_here ? 1 : 0) > 0) {
+        // the initial errors into their own partials, the control block reset by the same launch; the first step's
+        // bookkeeping sums the initial chi (through the first all-reduce on a sharded solve)
+        if ((rs = launch_errors(h, h->st[0], h->st[0], nullptr, kGateAlways, 0,
+                                LmReset{h->d_ctl, o->opt_it, o->max_trials, o->lambda_init}, true)) != OMV_OK)
+            return rs;
+    } else {
+        if ((rs = lba_errors(h, h->st[0])) != OMV_OK) return rs;
+        if (sharded) {
+            trial_scalars_kernel<<<1, 256, 0, st>>>(nullptr, h->d_partial, nmb, h->d_imu_partial, nullptr, 0, h->d_out,
+                                                    nullptr, nullptr);
+            if ((rs = lba_allreduce(h, h->d_out, 3)) != OMV_OK) return rs;
+        }
+        ctl_init_kernel<<<1, 256, 0, st>>>(h->d_ctl, h->d_partial, nmb, h->d_imu_partial, o->opt_it, o->max_trials,
+                                           o->lambda_init, sharded ? h->d_out : nullptr);
     }
-    ctl_init_kernel<<<1, 256, 0, st>>>(h->d_ctl, h->d_partial, nmb, h->d_imu_partial, o->opt_it, o->max_trials,
-                                       o->lambda_init, sharded ? h->d_out : nullptr);
     HIP_OK(hipGetLastError());
     const bool direct = h->timing || sharded;   // a collective call cannot be captured
     if (!direct && !h->step_exec) {   // capture one step and four steps (the problem's pointers are fixed
@@ -2537,9 +2587,9 @@ static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2) {
     double *d_pts = h->d_stage + head;
     uint8_t *d_flags = (uint8_t *)(d_pts + 3 * (size_t)P);
     double *d_chi2 = d_pts + 3 * (size_t)P + fl;
-    if (!h->host_lm) cur_copy_kernel<<<64, 256, 0, st>>>(h->d_ctl, h->st[1].Rwb, h->st[0].Rwb, h->state_doubles());
     const int n = std::max(std::max(E, P), (int)head);
-    epilogue_kernel<<<(n + 255) / 256, 256, 0, st>>>(h->rig, s, h->E, h->d_perm_edge, h->n_mono_all, h->d_track_depth,
+    epilogue_kernel<<<(n + 255) / 256, 256, 0, st>>>(h->rig, s, h->st[1], h->state_doubles(), h->E, h->d_perm_edge,
+                                                     h->n_mono_all, h->d_track_depth,
                                                      h->d_perm_pt, P, d_flags, want_chi2 ? d_chi2 : nullptr, d_pts,
                                                      h->d_chi2, h->d_chi2_b, h->host_lm ? nullptr : h->d_ctl,
                                                      h->d_stage, (int)head);

@@ -5,8 +5,15 @@ import sys
 
 tr = list(csv.DictReader(open(sys.argv[1])))
 tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+# the last optimize() starts at its initial error launch: the first err_kernel after the previous optimize()'s
+# epilogue (the control block reset rides on that launch; older traces have a separate ctl_init launch)
+epi = [i for i, r in enumerate(tr) if "epilogue_kernel" in r["Kernel_Name"]]
 idx = [i for i, r in enumerate(tr) if "ctl_init" in r["Kernel_Name"]]
-s = idx[-1]
+if idx:
+    s = idx[-1]
+else:
+    s0 = epi[-2] + 1 if len(epi) >= 2 else 0
+    s = next(i for i in range(s0, len(tr)) if "err_kernel" in tr[i]["Kernel_Name"]) + 1
 t0 = int(tr[s]["Start_Timestamp"])
 prev = None
 tot = {}
