@@ -737,16 +737,15 @@ __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArg
         const long long pf_r = wall_clock64();
         const bool pf_ph2 = phase2;
 #endif
-        // 1. mark which nodes split this round, zero child counts
+        // 1. mark which nodes split this round (phase 1: every node with > 1 key), zero child counts.  No barrier
+        // here: each node's entries are written by one thread, and the phase-2 sort reads only A and the V list
+        // (both final since the previous round's last barrier) before its own first barrier.
         for (int i = tid; i < m; i += T) {
             map[i] = -1;
-            vpos[i] = -1;
+            vpos[i] = !phase2 && A.cnt[i] > 1 ? 0 : -1;
             ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
         }
-        __syncthreads();
-        if (!phase2) {
-            for (int i = tid; i < m; i += T) vpos[i] = A.cnt[i] > 1 ? 0 : -1;
-        } else {
+        if (phase2) {
             // sort V by (size, UL.x) exactly as libstdc++'s std::sort moves the elements: the introsort
             // partitions one recursion depth at a time, a range per wavefront, the final insertion sort as a
             // stable rank over the block (B is free until step 4: its x0 / x1 / y0 rows hold the items' scratch)

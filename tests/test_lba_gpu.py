@@ -209,6 +209,27 @@ def test_device_lm_driver_matches_host_driver(small, oracle, large):
     assert t["trials"] == rt["trials"] and t["solve"] > 0
 
 
+@pytest.mark.parametrize("large", [True, False])
+def test_device_driver_with_rejected_trials(small, oracle, large):
+    """lambda_init 1e-9 makes half the trials fail (oracle: 6 iterations, 12 trials): the device driver's
+    double-buffered state keeps the current state and its errors through each rejected trial, reports the last
+    computed errors' chi (a rejected trial's, as g2o does) and matches the host driver and the oracle -- decisions
+    exactly, err / err_end and the state at the parity bar -- in the graph and in the direct-launch mode."""
+    kw = dict(opt_it=6, lambda_init=1e-9, max_trials=10, large=large)
+    ro, so, _ = oracle.lba_optimize(small, **kw)
+    assert ro["trials"] > ro["iterations"], ro   # the case exercises rejections
+    ba = _solver(small).set_problem(small)
+    rh, sh = ba.set_driver(True).optimize(**kw)
+    rd, sd = ba.set_problem(small).set_driver(False).optimize(**kw)
+    rt, st = ba.set_problem(small).enable_timing(True).optimize(**kw)
+    for r, s in ((rd, sd), (rt, st)):
+        assert (r["iterations"], r["trials"], r["status"]) == (rh["iterations"], rh["trials"], rh["status"])
+        for k in ("err", "err_end"):
+            assert abs(r[k] - rh[k]) <= 1e-6 * abs(rh[k]), (k, r[k], rh[k])
+        _compare_result(small, r, ro)
+        _compare_state(small, s, so, oracle)
+
+
 def test_reoptimize_same_handle(small, oracle):
     """set_problem twice on one handle (workspace reuse) gives the same answer."""
     ba = _solver(small)
