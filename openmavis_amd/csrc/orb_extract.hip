@@ -544,6 +544,42 @@ __device__ int block_excl_scan(int *a, int n, int *tmp) {
     return tot;
 }
 
+// Two independent in-place exclusive scans (a[0..na), b[0..nb)) with one set of barriers; tmp holds 16 ints.
+// Thread t scans the same chunks as block_excl_scan, so a caller that wrote exactly those entries itself needs no
+// barrier before the call.
+__device__ int2 block_excl_scan2(int *a, int na, int *b, int nb, int *tmp) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int ca = (na + T - 1) / T, a0 = min(na, tid * ca), a1 = min(na, a0 + ca);
+    const int cb = (nb + T - 1) / T, b0 = min(nb, tid * cb), b1 = min(nb, b0 + cb);
+    int sa = 0, sb = 0;
+    for (int i = a0; i < a1; ++i) sa += a[i];
+    for (int i = b0; i < b1; ++i) sb += b[i];
+    const int ia = wave_incl_scan(sa), ib = wave_incl_scan(sb);
+    const int wave = tid >> 6, nw = T >> 6;
+    __syncthreads();
+    if ((tid & 63) == 63) tmp[wave] = ia, tmp[8 + wave] = ib;
+    __syncthreads();
+    int oa = 0, ta = 0, ob = 0, tb = 0;
+    for (int w = 0; w < nw; ++w) {
+        if (w < wave) oa += tmp[w], ob += tmp[8 + w];
+        ta += tmp[w], tb += tmp[8 + w];
+    }
+    int run = oa + ia - sa;
+    for (int i = a0; i < a1; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    run = ob + ib - sb;
+    for (int i = b0; i < b1; ++i) {
+        const int v = b[i];
+        b[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return make_int2(ta, tb);
+}
+
 __device__ int block_sum(int v, int *tmp) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     __syncthreads();
@@ -603,8 +639,11 @@ struct OctArgs {
 #endif
 __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) int osm[];
-    const int img = blockIdx.x / g.nlevels;
-    const int l = blockIdx.x - img * g.nlevels;
+    // level-major block order: the finest levels (most keys, the longest workgroups) of every image are dispatched
+    // first and the short coarse levels fill the launch's tail (longest-job-first)
+    const int n_img = gridDim.x / g.nlevels;
+    const int l = blockIdx.x / n_img;
+    const int img = blockIdx.x - l * n_img;
     const LevelGeom &L = g.lv[l];
     const int tid = threadIdx.x, T = blockDim.x;
     const int NC = g.node_cap;
@@ -790,8 +829,10 @@ __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArg
         //    processed[i]: scanA holds #non-empty children in creation order position
         int n_proc_nodes;   // number of divided nodes
         if (!phase2) {
-            // creation order = list order; every candidate node is divided
-            for (int i = tid; i < m; i += T) {
+            // creation order = list order; every candidate node is divided.  Each thread writes the chunk of
+            // entries the scans below give it, so no barrier separates the two
+            const int chunk = (m + T - 1) / T, i0 = min(m, tid * chunk), i1 = min(m, i0 + chunk);
+            for (int i = i0; i < i1; ++i) {
                 int nk = 0;
                 if (vpos[i] >= 0)
                     for (int t = 0; t < 4; ++t) nk += ccnt[4 * i + t] > 0;
@@ -832,16 +873,17 @@ __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArg
             for (int p = tid; p < n_proc_nodes; p += T) vpos[items[nv - 1 - p].payload] = p;
             __syncthreads();
             for (int i = tid; i < m; i += T) scanB[i] = vpos[i] >= 0 ? 0 : 1;
+            __syncthreads();
         }
-        __syncthreads();
-        const int Q = block_excl_scan(scanA, n_proc_nodes, tmp);
-        const int U = block_excl_scan(scanB, m, tmp);
-        const int newm = Q + U;
+        const int2 QU = block_excl_scan2(scanA, n_proc_nodes, scanB, m, tmp);
+        const int Q = QU.x, newm = QU.x + QU.y;
         if (newm > NC) {
             if (tid == 0) atomicOr(a.err, OMV_ERR_CAPACITY);
             return;
         }
-        // 4. build the new list: children (reverse creation order) then survivors (old order)
+        // 4. build the new list: children (reverse creation order) then survivors (old order); xf[r]: the child
+        //    created r-th has > 1 key (the next round's V list, step 6).  xf aliases the sort items, dead by now
+        int *xf = reinterpret_cast<int *>(items);
         for (int i = tid; i < m; i += T) {
             const int p = phase2 ? vpos[i] : (vpos[i] >= 0 ? i : -1);
             if (p >= 0) {
@@ -852,6 +894,7 @@ __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArg
                         const int j = Q - 1 - r;
                         child_rect(A, i, t, B, j);
                         B.cnt[j] = c;
+                        xf[r] = c > 1 ? 1 : 0;
                         ccnt[4 * i + t] = -(j + 1);   // remember the child's new index
                         ++r;
                     }
@@ -883,14 +926,14 @@ __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArg
             }
         }
         // 6. expandable children (> 1 key) in creation order = new indices Q-1 down to 0
-        for (int j = tid; j < Q; j += T) scanA[j] = B.cnt[Q - 1 - j] > 1 ? 1 : 0;
-        __syncthreads();
-        const int nexp = block_excl_scan(scanA, Q, tmp);
+        const int nexp = block_excl_scan(xf, Q, tmp);
         for (int j = tid; j < Q; j += T)
-            if (B.cnt[Q - 1 - j] > 1) vlist[scanA[j]] = Q - 1 - j;
-        // swap A <-> B
-        for (int i = tid; i < newm; i += T) {
-            A.copy_from(i, B, i);
+            if (B.cnt[Q - 1 - j] > 1) vlist[xf[j]] = Q - 1 - j;
+        // the new list becomes A (the roles of the two node arrays swap; no copy)
+        {
+            const NodeSoA t = A;
+            A = B;
+            B = t;
         }
         __syncthreads();
         m = newm;
