@@ -634,8 +634,9 @@ struct OctArgs {
 };
 
 #ifndef OMV_OCT_WGS
-#define OMV_OCT_WGS 7   // workgroups per CU the register budget targets (LDS: 20 KB each; measured 6 / 7 / 8:
-                        // 0.527 / 0.495 / 0.518 ms per 128-frame launch, 8 spills registers)
+#define OMV_OCT_WGS 8   // workgroups per CU the register budget targets (LDS: 20 KB each; measured 6 / 7 / 8 with
+                        // the level-major order: 0.232 / 0.221 / 0.213 ms per 128-frame launch; 8 spills a few
+                        // registers but wins since the long level-0 workgroups overlap more of each other)
 #endif
 __global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) int osm[];
