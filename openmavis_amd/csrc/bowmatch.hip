@@ -10,8 +10,11 @@
 // strict `<` update ranks them.  bow_resolve_kernel, one wavefront per job: the reference's sequential walk
 // (common nodes ascending = the keyframe CSR order), where only the claims of earlier keyframe keypoints can
 // change a pick: the first two unclaimed entries of each block are its best and second, and a block whose
-// short list runs out while it holds more candidates is rescanned on the wave.  Claims live in an LDS bitmap,
-// the matches' rotation bins in LDS bytes; the top-3 filter runs over them at the end.
+// short list runs out while it holds more candidates is rescanned on the wave.  The walk runs in batches of
+// 64 / NB keypoints picked in parallel against the batch-start claims; the prefix before the first keypoint
+// whose examined entries an earlier batch keypoint claims commits at once (that keypoint is then walked alone):
+// 1.5x (KF, F) / 2.4x (KF, KF) over the keypoint-at-a-time walk.  Claims live in an LDS bitmap, the matches'
+// rotation bins in LDS bytes; the top-3 filter runs over them at the end.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +39,7 @@ namespace {
 constexpr int TH_LOW = 50, kHisto = 30;
 constexpr int kMaxKp = 16384;      // keypoints per view (LDS claim bitmap + rotation bins)
 constexpr uint32_t kNone = 0xffffffffu;
+constexpr int kFree = 0x7fffffff;
 std::atomic<int64_t> g_bow_rescans{0};   // walk rescans over all SearchByBoW calls (diagnostic)
 
 // rot = angle1 - angle2 (float), +360 if negative, bin = round(rot / 30) with 30 -> 0 (ORBmatcher.cc:475-481)
@@ -236,9 +240,10 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
     __shared__ uint8_t bins[kMaxKp];
     __shared__ int16_t match[kMaxKp];   // the output, written to memory once at the end (no stores in the walk)
     __shared__ uint32_t recbuf[2][kChunk * kRecWords];
+    __shared__ int owner[kMaxKp];   // batch claims: the first batch keypoint claiming an other-view keypoint, or kFree
     __shared__ int cnt[kHisto];
     __shared__ int ind[3];
-    constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1;
+    constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1, S = 64 / NB;
     const omv_bow_job &J = jobs[blockIdx.x];
     const omv_kf_view &K = J.kf, &O = J.other;
     const int lane = threadIdx.x;
@@ -249,6 +254,7 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
     }
     for (int i = lane; i < n_out; i += 64) match[i] = -1, bins[i] = 0xff;
     for (int i = lane; i < (O.n + 31) / 32; i += 64) claimed[i] = 0;
+    for (int i = lane; i < O.n; i += 64) owner[i] = kFree;
     if (lane < kHisto) cnt[lane] = 0;
     __syncthreads();
     // records staged through LDS a chunk at a time (one coalesced load per chunk, the next chunk in flight while
@@ -272,10 +278,10 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int q = base; q < min(nb, K.n); ++q) {
-        const uint32_t *cr = recbuf[buf] + (q - base) * kRecWords;
+        // one keyframe keypoint with the live claims (the batch's conflict / rescan case)
+        auto walk_one = [&](const uint32_t *cr) {
         const int o0 = (int)cr[0];
-        if (o0 < 0) continue;
+        if (o0 < 0) return;
         const int o1 = (int)cr[1], idx1 = (int)cr[2];
         const uint32_t c01 = cr[3], c23 = cr[4];
         // lane c < NB: the block's first two unclaimed entries
@@ -353,7 +359,81 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
+        };
+        // Batches of S = 64 / NB consecutive keyframe keypoints, lane (s, c) = keypoint q + s, camera block c: every
+        // pick against the claims at the batch start, then the conflict-free prefix commits at once.  A keypoint's
+        // pick stays the reference's iff no entry it examined (its unclaimed short-list entries up to the second)
+        // was claimed by an earlier keypoint of the batch: batch claims go to `owner` (the first claimer), each
+        // lane checks its examined entries against it, and the first keypoint with a conflict (or a rescan) is
+        // walked alone with the claims of the committed prefix.
+        const int qend = min(nb, K.n);
+        for (int q = base; q < qend;) {
+            const int nbatch = min(S, qend - q);
+            const int s = lane / NB, c = lane % NB;
+            const bool act = s < nbatch;
+            const uint32_t *cr = recbuf[buf] + (act ? q + s - base : 0) * kRecWords;
+            const int o0 = act ? (int)cr[0] : -1, idx1 = (int)cr[2];
+            const uint32_t c01 = cr[3], c23 = cr[4];
+            uint32_t e[kTop];
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) e[k] = cr[8 + kTop * c + k];
+            const int total = (int)(((c < 2 ? c01 : c23) >> (16 * (c & 1))) & 0xffffu);
+            uint32_t cw[kTop];
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) cw[k] = claimed[(e[k] == kNone ? 0u : e[k] & 0xffffu) >> 5];
+            uint32_t best = kNone, exm = 0;
+            int d2 = 256, found = 0;
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) {
+                const uint32_t x = e[k];
+                const bool ok = x != kNone && !((cw[k] >> (x & 31u)) & 1u);
+                exm |= ok && found < 2 ? 1u << k : 0u;
+                best = ok && found == 0 ? x : best;
+                d2 = ok && found == 1 ? (int)(x >> 23) : d2;
+                found += ok && found < 2 ? 1 : 0;
+            }
+            const bool search = o0 >= 0;
+            const bool rescan = search && found < 2 && total > kTop;
+            const int bd = best == kNone ? 256 : (int)(best >> 23), bi = (int)(best & 0xffffu);
+            const int bd0 = __shfl(bd, s * NB, 64), bs0 = __shfl(d2, s * NB, 64);
+            bool claim;
+            if (MODE == OMV_BOW_KF_FRAME)
+                claim = search && bd0 <= TH_LOW && bd <= TH_LOW && (c != 0 || (float)bd0 < nnratio * (float)bs0);
+            else
+                claim = search && bd < TH_LOW && (float)bd < nnratio * (float)d2;
+            if (claim) atomicMin(&owner[bi], s);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            bool bad = rescan;
+#pragma unroll
+            for (int k = 0; k < kTop; ++k)
+                if ((exm >> k) & 1u) bad |= owner[e[k] & 0xffffu] < s;
+            const uint64_t badm = __ballot(act && bad);
+            const int sstar = badm ? (int)(__builtin_ctzll(badm) / NB) : nbatch;   // first keypoint to walk alone
+            const bool commit = claim && s < sstar;
+            if (commit) {
+                atomicOr(&claimed[bi >> 5], 1u << (bi & 31));
+                const int at = MODE == OMV_BOW_KF_FRAME ? bi : idx1;
+                match[at] = (int16_t)(MODE == OMV_BOW_KF_FRAME ? idx1 : bi);
+                if (check_ori) {
+                    const int bb = (int)((best >> 16) & 31u);
+                    bins[at] = (uint8_t)bb;
+                    atomicAdd(&cnt[bb], 1);
+                }
+            }
+            nm += __popcll(__ballot(commit));
+            if (claim) owner[bi] = kFree;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (sstar < nbatch) {
+                walk_one(recbuf[buf] + (q + sstar - base) * kRecWords);
+                q += sstar + 1;
+            } else {
+                q += nbatch;
+            }
+        }
         buf ^= 1;
     }
     if (check_ori) {
