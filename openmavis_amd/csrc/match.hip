@@ -1738,11 +1738,18 @@ __global__ void __launch_bounds__(256) sbs3_agree_kernel(Sim3Args a) {
 }
 
 // ---- ORBmatcher::SearchForInitialization (ORBmatcher.cc:895-1004) ---------------------------------------
-// One wavefront per frame pair, F1's level-0 keypoints in order (the claims are sequential: vMatchedDistance /
-// vnMatches21 of F2 change with every accepted match).  For one F1 keypoint the lanes take the window's
-// candidates of each grid column (GetFeaturesInArea order: columns ix, the column's cells iy contiguous in the
-// CSR, keypoints ascending), each keeping its best (distance, window position) key and second distance; one
-// min-reduction gives the reference's best (first minimal distance) and second.  The F2 claim state, F1's
+// The claims are sequential (vMatchedDistance / vnMatches21 of F2 change with every accepted match), but a claim
+// only ever EXCLUDES window candidates: the scan skips F2 keypoints whose claimed distance is <= the new one
+// (`vMatchedDistance[i2] <= dist`, :937), and a claimed distance only decreases.  So the launch is two kernels:
+//  1. init_spec_kernel, one wavefront per F1 keypoint of every pair (the whole chip): the window scan with NO
+//     claim filter, keeping the four smallest (distance, window position) keys and their F2 indices;
+//  2. init_kernel, one wavefront per pair walking F1 in order: exclusion only removes candidates, so the
+//     filtered best and second are the first two of those keys the current claims leave -- known whenever two
+//     of them survive (or the window held fewer than four).  Otherwise the wavefront rescans the window with
+//     the filter, as the reference's loop does.
+// For one window scan the lanes take the candidates of each grid column (GetFeaturesInArea order: columns ix,
+// the column's cells iy contiguous in the CSR, keypoints ascending), each keeping its K smallest keys; K wave
+// reductions give the reference's best (first minimal distance) and second.  The F2 claim state, F1's
 // matches and rotation bins live in LDS.
 struct InitArgs {
     FrameArgs f;
@@ -1753,9 +1760,10 @@ struct InitArgs {
     int check_ori;
     int32_t *m12;           // [n][kp_cap]
     int32_t *n_matches;     // [n]
+    uint4 *spec;            // [n][kp_cap][2] {4 smallest keys}, {their F2 indices}, without the claim filter
 };
 
-__host__ __device__ inline size_t init_lds_bytes(int cap) { return (size_t)cap * 13 + 4 * 36 + 16; }
+__host__ __device__ inline size_t init_lds_bytes(int cap) { return (size_t)cap * 17 + 4 * 36 + 16; }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -1763,12 +1771,115 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 
+constexpr uint32_t kNoKey = 0xffffffffu;
+constexpr int kInitSpec = 4;   // speculative keys kept per F1 keypoint
+
+// Frame::GetFeaturesInArea(x, y, windowSize, 0, 0) window (Frame.cc:890-967) scanned by one wavefront.  Returns
+// the wave-uniform K smallest keys ((dist << 16) | window position, ascending) and their F2 indices (kNoKey / -1
+// past the candidates); mdist == nullptr scans without the claim filter.
+template <int K>
+__device__ __forceinline__ void init_window_scan(const FrameArgs &f, const int32_t *cs, const int32_t *ci,
+                                                 const omv_kp *kp2, const uint8_t *ds2, const uint64_t d1[4],
+                                                 float x, float y, float r, const int *mdist, int lane,
+                                                 uint32_t (&ok)[K], int (&oi)[K]) {
+    uint32_t kk[K];
+    int ii[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) ok[t] = kk[t] = kNoKey, oi[t] = ii[t] = -1;
+    const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (nMaxCellY < 0) return;
+    // the window's columns are contiguous CSR runs; lane j < ncol holds column j's run, an inclusive scan
+    // flattens them in GetFeaturesInArea order, and the lanes walk the flattened list 64 at a time (one
+    // gather chain per 64 candidates instead of one per column)
+    const int ncol = nMaxCellX - nMinCellX + 1;
+    int cp0 = 0, clen = 0;
+    if (lane < ncol) {
+        const int ix = nMinCellX + lane;
+        cp0 = cs[ix * kGridRows + nMinCellY];
+        clen = cs[ix * kGridRows + nMaxCellY + 1] - cp0;
+    }
+    int incl = clen;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+    }
+    const int excl = incl - clen, total = __shfl(incl, 63, 64);
+    for (int base = 0; base < total; base += 64) {
+        const int pos = base + lane;   // the shuffles run on the whole wavefront (uniform loop)
+        int j = 0;
+        for (int t = 1; t < ncol; ++t) j = __shfl(excl, t, 64) <= pos ? t : j;
+        const int p = __shfl(cp0, j, 64) + pos - __shfl(excl, j, 64);
+        if (pos >= total) continue;
+        const int i2 = ci[p];
+        const omv_kp k = kp2[i2];
+        if (k.octave != 0) continue;   // levels [0, 0]
+        if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+        uint64_t d2[4];
+        load_desc(ds2 + (size_t)i2 * 32, d2);
+        const int dist = omv::hamming256(d1, d2);
+        if (mdist && mdist[i2] <= dist) continue;
+        const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)pos;   // unique: distinct window positions
+#pragma unroll
+        for (int t = K - 1; t >= 0; --t)   // sorted insert (reads kk[t - 1] before step t - 1 writes it)
+            if (kk[t] > key) {
+                if (t > 0 && kk[t - 1] > key) kk[t] = kk[t - 1], ii[t] = ii[t - 1];
+                else kk[t] = key, ii[t] = i2;
+            }
+    }
+#pragma unroll
+    for (int t = 0; t < K; ++t) {   // K rounds of wave minimum over the lanes' heads, the winner pops its head
+        const uint32_t m = wave_min_u32(kk[0]);
+        if (m == kNoKey) return;
+        const int src = __ffsll((long long)__ballot(kk[0] == m)) - 1;
+        ok[t] = m, oi[t] = __shfl(ii[0], src, 64);
+        if (lane == src) {
+#pragma unroll
+            for (int u = 0; u + 1 < K; ++u) kk[u] = kk[u + 1], ii[u] = ii[u + 1];
+            kk[K - 1] = kNoKey;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) init_spec_kernel(InitArgs a) {
+    const FrameArgs &f = a.f;
+    const int cap = f.kp_cap, lane = threadIdx.x & 63, pr = blockIdx.y;
+    const int i1 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const size_t fc1 = (size_t)a.pairs[2 * pr] * f.n_cams, fc2 = (size_t)a.pairs[2 * pr + 1] * f.n_cams;   // block 0
+    const int n1 = f.n_kp[fc1];
+    if (i1 >= n1) return;   // wave-uniform
+    uint32_t k[kInitSpec];
+    int id[kInitSpec];
+#pragma unroll
+    for (int t = 0; t < kInitSpec; ++t) k[t] = kNoKey, id[t] = -1;
+    const omv_kp k1 = f.kps[fc1 * cap + i1];
+    if (k1.octave == 0) {
+        const float *prev = a.prev + ((size_t)pr * cap + i1) * 2;
+        uint64_t d1[4];
+        load_desc(f.desc + (fc1 * cap + i1) * 32, d1);
+        init_window_scan<kInitSpec>(f, f.cell_start + fc2 * (kCells + 1), f.cell_idx + fc2 * cap, f.kps + fc2 * cap,
+                                    f.desc + fc2 * cap * 32, d1, prev[0], prev[1], (float)a.window, nullptr, lane, k, id);
+    }
+    if (lane == 0) {
+        uint4 *o = a.spec + ((size_t)pr * cap + i1) * 2;
+        o[0] = uint4{k[0], k[1], k[2], k[3]};
+        o[1] = uint4{(uint32_t)id[0], (uint32_t)id[1], (uint32_t)id[2], (uint32_t)id[3]};
+    }
+}
+
 __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
     extern __shared__ __attribute__((aligned(16))) int ism[];
     const FrameArgs &f = a.f;
     const int cap = f.kp_cap, lane = threadIdx.x, pr = blockIdx.x;
     int *mdist = ism, *m21 = ism + cap, *m12 = ism + 2 * cap;
-    int *cnt = ism + 3 * cap, *ind = cnt + 30;
+    int *acc2 = ism + 3 * cap;   // [n1] the F2 keypoint F1 keypoint i1 was accepted with (rotHist push), or -1
+    int *cnt = ism + 4 * cap, *ind = cnt + 30;
     uint8_t *bins = reinterpret_cast<uint8_t *>(ind + 4);
     const size_t fc1 = (size_t)a.pairs[2 * pr] * f.n_cams, fc2 = (size_t)a.pairs[2 * pr + 1] * f.n_cams;   // block 0
     const int n1 = f.n_kp[fc1], n2 = f.n_kp[fc2];
@@ -1776,100 +1887,64 @@ __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
     const uint8_t *ds1 = f.desc + fc1 * cap * 32, *ds2 = f.desc + fc2 * cap * 32;
     const int32_t *cs = f.cell_start + fc2 * (kCells + 1), *ci = f.cell_idx + fc2 * cap;
     float *prev = a.prev + (size_t)pr * cap * 2;
-    for (int i = lane; i < n1; i += 64) m12[i] = -1, bins[i] = 0xff;
+    const uint4 *spec = a.spec + (size_t)pr * cap * 2;
+    for (int i = lane; i < n1; i += 64) m12[i] = -1, acc2[i] = -1, bins[i] = 0xff;
     for (int i = lane; i < n2; i += 64) mdist[i] = INT_MAX, m21[i] = -1;
     if (lane < 30) cnt[lane] = 0;
     __syncthreads();
     const float r = (float)a.window;
     int nm = 0;
-    // the next F1 keypoint's fields are loaded one iteration ahead (the walk is a chain of dependent steps)
-    omv_kp kn{};
-    float xn = 0.f, yn = 0.f;
-    uint64_t dn[4] = {0, 0, 0, 0};
-    if (n1 > 0) kn = kp1[0], xn = prev[0], yn = prev[1], load_desc(ds1, dn);
+    // the next F1 keypoint's speculative keys are loaded one iteration ahead (the walk is a chain of steps)
+    uint4 skn{}, sidn{};
+    if (n1 > 0) skn = spec[0], sidn = spec[1];
     for (int i1 = 0; i1 < n1; ++i1) {
-        const omv_kp k1 = kn;
-        const float x = xn, y = yn;
-        const uint64_t d1[4] = {dn[0], dn[1], dn[2], dn[3]};
-        if (i1 + 1 < n1)
-            kn = kp1[i1 + 1], xn = prev[2 * i1 + 2], yn = prev[2 * i1 + 3], load_desc(ds1 + (size_t)(i1 + 1) * 32, dn);
-        if (k1.octave > 0) continue;
-        // Frame::GetFeaturesInArea(x, y, windowSize, 0, 0) window (Frame.cc:890-967)
-        const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
-        if (nMinCellX >= kGridCols) continue;
-        const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
-        if (nMaxCellX < 0) continue;
-        const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
-        if (nMinCellY >= kGridRows) continue;
-        const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
-        if (nMaxCellY < 0) continue;
-        uint32_t bk = 0xffffffffu;
-        int sec = INT_MAX, bidx = -1;
-        // the window's columns are contiguous CSR runs; lane j < ncol holds column j's run, an inclusive scan
-        // flattens them in GetFeaturesInArea order, and the lanes walk the flattened list 64 at a time (one
-        // gather chain per 64 candidates instead of one per column)
-        const int ncol = nMaxCellX - nMinCellX + 1;
-        int cp0 = 0, clen = 0;
-        if (lane < ncol) {
-            const int ix = nMinCellX + lane;
-            cp0 = cs[ix * kGridRows + nMinCellY];
-            clen = cs[ix * kGridRows + nMaxCellY + 1] - cp0;
-        }
-        int incl = clen;
+        const uint32_t sk[4] = {skn.x, skn.y, skn.z, skn.w};
+        const int si[4] = {(int)sidn.x, (int)sidn.y, (int)sidn.z, (int)sidn.w};
+        if (i1 + 1 < n1) skn = spec[2 * i1 + 2], sidn = spec[2 * i1 + 3];
+        if (sk[0] == kNoKey) continue;   // no candidate without the filter: none with it (or not level 0 / off-grid)
+        // the filtered best and second are the two smallest keys the claims leave; known unless fewer than two of
+        // the kept keys survive while more candidates may lie beyond them
+        uint32_t g[2] = {kNoKey, kNoKey};
+        int bi[2] = {-1, -1}, found = 0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += t;
-        }
-        const int excl = incl - clen, total = __shfl(incl, 63, 64);
-        for (int base = 0; base < total; base += 64) {
-            const int pos = base + lane;   // the shuffles run on the whole wavefront (uniform loop)
-            int j = 0;
-            for (int t = 1; t < ncol; ++t) j = __shfl(excl, t, 64) <= pos ? t : j;
-            const int p = __shfl(cp0, j, 64) + pos - __shfl(excl, j, 64);
-            if (pos >= total) continue;
-            const int i2 = ci[p];
-            const omv_kp k = kp2[i2];
-            if (k.octave != 0) continue;   // levels [0, 0]
-            if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
-            uint64_t d2[4];
-            load_desc(ds2 + (size_t)i2 * 32, d2);
-            const int dist = omv::hamming256(d1, d2);
-            if (mdist[i2] <= dist) continue;
-            const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)pos;
-            if (key < bk) {   // this lane's candidates arrive in window order
-                if (bk != 0xffffffffu) sec = min(sec, (int)(bk >> 16));
-                bk = key, bidx = i2;
-            } else {
-                sec = min(sec, dist);
+        for (int t = 0; t < 4; ++t)
+            if (found < 2 && sk[t] != kNoKey && mdist[si[t]] > (int)(sk[t] >> 16)) {
+                if (found == 0) g[0] = sk[t], bi[0] = si[t];
+                else g[1] = sk[t];
+                ++found;
             }
+        if (found < 2 && sk[3] != kNoKey) {   // the reference's filtered scan
+            uint64_t d1[4];
+            load_desc(ds1 + (size_t)i1 * 32, d1);
+            init_window_scan<2>(f, cs, ci, kp2, ds2, d1, prev[2 * i1], prev[2 * i1 + 1], r, mdist, lane, g, bi);
         }
-        const uint32_t g = wave_min_u32(bk);
-        if (g == 0xffffffffu) continue;   // no candidate (vIndices2 empty, or all skipped)
-        const uint32_t other = bk == g ? (uint32_t)sec : (bk == 0xffffffffu ? (uint32_t)INT_MAX : bk >> 16);
-        const int bestDist2 = (int)wave_min_u32(other), bestDist = (int)(g >> 16);
-        const int src = __ffsll((long long)__ballot(bk == g)) - 1;
-        const int bestIdx2 = __shfl(bidx, src, 64);
+        if (g[0] == kNoKey) continue;
+        const int bestIdx2 = bi[0], bestDist = (int)(g[0] >> 16), bestDist2 = g[1] == kNoKey ? INT_MAX : (int)(g[1] >> 16);
         if (bestDist <= 50 && (float)bestDist < (float)bestDist2 * a.nnratio) {
             const int old = m21[bestIdx2];
             if (old >= 0) --nm;
             ++nm;
             if (lane == 0) {
                 if (old >= 0) m12[old] = -1;
-                m12[i1] = bestIdx2, m21[bestIdx2] = i1, mdist[bestIdx2] = bestDist;
-                if (a.check_ori) {   // rot = angle1 - angle2, +360 if negative, bin = round(rot / 30), 30 -> 0
-                    float rot = k1.angle - kp2[bestIdx2].angle;
-                    if (rot < 0.0f) rot += 360.0f;
-                    int bin = (int)roundf(rot * (1.0f / 30));
-                    if (bin == 30) bin = 0;
-                    bins[i1] = (uint8_t)bin;
-                    ++cnt[bin];
-                }
+                m12[i1] = bestIdx2, m21[bestIdx2] = i1, mdist[bestIdx2] = bestDist, acc2[i1] = bestIdx2;
             }
         }
         wave_sync();   // the claim state before the next F1 keypoint (one wavefront, LDS only)
     }
     if (a.check_ori) {   // ComputeThreeMaxima, then every push outside the top bins that is still matched
+        // the rotation histogram of every accept (each F1 keypoint is accepted at most once, so its bin is a
+        // function of (i1, acc2[i1]); the counts do not depend on the push order): off the walk's chain
+        for (int i = lane; i < n1; i += 64) {
+            const int j = acc2[i];
+            if (j < 0) continue;
+            float rot = kp1[i].angle - kp2[j].angle;   // rot = angle1 - angle2, +360 if negative
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / 30));   // bin = round(rot / 30), 30 -> 0
+            if (bin == 30) bin = 0;
+            bins[i] = (uint8_t)bin;
+            atomicAdd(cnt + bin, 1);
+        }
+        __syncthreads();
         if (lane == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < 30; i++) {
@@ -2336,9 +2411,13 @@ omv_status omv_matcher_search_for_initialization(omv_matcher *h, int n_pairs, co
     int32_t *d_pairs = nullptr;
     HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(int32_t) * 2 * n_pairs, st));
     HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(int32_t) * 2 * n_pairs, hipMemcpyHostToDevice, st));
-    InitArgs ia{f, d_pairs, prev_matched, window, nnratio, check_ori, matches12, n_matches};
+    uint4 *d_spec = nullptr;
+    HIP_OK(hipMallocAsync((void **)&d_spec, sizeof(uint4) * 2 * (size_t)n_pairs * h->kp_cap, st));
+    InitArgs ia{f, d_pairs, prev_matched, window, nnratio, check_ori, matches12, n_matches, d_spec};
+    init_spec_kernel<<<dim3((h->kp_cap + 3) / 4, n_pairs), 256, 0, st>>>(ia);
     init_kernel<<<n_pairs, 64, lds, st>>>(ia);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipFreeAsync(d_spec, st));
     HIP_OK(hipFreeAsync(d_pairs, st));
     return OMV_OK;
 }

@@ -160,3 +160,51 @@ def test_search_for_initialization_matches_oracle(oracle, window, check_ori, nnr
         assert np.array_equal(m12[i, :n1], m_o), (i, np.nonzero(m12[i, :n1] != m_o)[0][:10])
         assert np.array_equal(prev[i, :n1], prev_o)
         assert n_o > 50
+
+
+def _contest(p, rng, n_clusters=12, copies=6):
+    """Append clusters of identical F1 keypoints (same position, descriptor) and, next to them, F2 keypoints at
+    0, 5, 10, ... flipped bits: each copy claims the next-closest F2 keypoint once the earlier copies hold the
+    closer ones, so the walk's speculative four smallest keys run out (the filtered rescan runs)."""
+    f1k, f1d, f2k, f2d, prev = [p["f1"]["kps"]], [p["f1"]["desc"]], [p["f2"]["kps"]], [p["f2"]["desc"]], [p["prev"]]
+    for _ in range(n_clusters):
+        xy = np.array([[rng.uniform(40, synth_init.W - 40), rng.uniform(40, synth_init.H - 40)]], np.float32)
+        d = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+        f1k.append(synth_init._kps(np.repeat(xy, copies, 0), np.zeros(copies, np.int32), np.full(copies, 10, np.float32)))
+        f1d.append(np.repeat(d, copies, 0))
+        prev.append(np.repeat(xy, copies, 0))
+        dd = np.repeat(d, copies, 0)
+        for c in range(copies):
+            for b in rng.choice(256, 5 * c, replace=False):
+                dd[c, b // 8] ^= np.uint8(1 << (b % 8))
+        off = rng.normal(0, 2.0, (copies, 2)).astype(np.float32)
+        f2k.append(synth_init._kps(xy + off, np.zeros(copies, np.int32), np.full(copies, 15, np.float32)))
+        f2d.append(dd)
+    return dict(f1=dict(kps=np.concatenate(f1k), desc=np.concatenate(f1d)),
+                f2=dict(kps=np.concatenate(f2k), desc=np.concatenate(f2d)), prev=np.concatenate(prev))
+
+
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_for_initialization_contested_claims(oracle, check_ori):
+    """Claims that exclude the speculative best / second (and all four kept keys) match the oracle bit-exactly."""
+    import torch
+    rng = np.random.Generator(np.random.PCG64(77))
+    pairs = [_contest(synth_init.make_init_pair(seed=s, n=500, motion=(2.0, 1.0), rot=3.0), rng) for s in (11, 12, 13)]
+    fb, cap = _init_frames(pairs)
+    prev = torch.zeros((len(pairs), cap, 2), dtype=torch.float32, device="cuda")
+    for i, p in enumerate(pairs):
+        prev[i, :len(p["prev"])] = torch.from_numpy(p["prev"])
+    m = ORBmatcher(0.9, check_ori)
+    m12, n = m.SearchForInitialization(fb, [(2 * i, 2 * i + 1) for i in range(len(pairs))], prev, windowSize=100)
+    m12, n, prev = m12.cpu().numpy(), n.cpu().numpy(), prev.cpu().numpy()
+    g = oracle.frame_geom(1, synth_init.W, synth_init.H, synth_init.scale_factors())
+    for i, p in enumerate(pairs):
+        n_o, m_o, prev_o = oracle.search_for_initialization(g, p["f1"]["kps"], p["f1"]["desc"], p["f2"]["kps"],
+                                                            p["f2"]["desc"], p["prev"], 100, 0.9, check_ori)
+        n1 = len(p["f1"]["kps"])
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(m12[i, :n1], m_o), (i, np.nonzero(m12[i, :n1] != m_o)[0][:10])
+        assert np.array_equal(prev[i, :n1], prev_o)
+        # the clusters' later copies matched past the first four keys (the rescan ran)
+        f2n = len(p["f2"]["kps"]) - 12 * 6
+        assert (m_o[n1 - 12 * 6:] >= f2n).sum() >= 12 * 5, m_o[n1 - 12 * 6:]
