@@ -1742,10 +1742,10 @@ __global__ void __launch_bounds__(256) sbs3_agree_kernel(Sim3Args a) {
 // only ever EXCLUDES window candidates: the scan skips F2 keypoints whose claimed distance is <= the new one
 // (`vMatchedDistance[i2] <= dist`, :937), and a claimed distance only decreases.  So the launch is two kernels:
 //  1. init_spec_kernel, one wavefront per F1 keypoint of every pair (the whole chip): the window scan with NO
-//     claim filter, keeping the four smallest (distance, window position) keys and their F2 indices;
+//     claim filter, keeping the eight smallest (distance, window position) keys and their F2 indices;
 //  2. init_kernel, one wavefront per pair walking F1 in order: exclusion only removes candidates, so the
 //     filtered best and second are the first two of those keys the current claims leave -- known whenever two
-//     of them survive (or the window held fewer than four).  Otherwise the wavefront rescans the window with
+//     of them survive (or the window held fewer than eight).  Otherwise the wavefront rescans the window with
 //     the filter, as the reference's loop does.
 // For one window scan the lanes take the candidates of each grid column (GetFeaturesInArea order: columns ix,
 // the column's cells iy contiguous in the CSR, keypoints ascending), each keeping its K smallest keys; K wave
@@ -1760,10 +1760,11 @@ struct InitArgs {
     int check_ori;
     int32_t *m12;           // [n][kp_cap]
     int32_t *n_matches;     // [n]
-    uint4 *spec;            // [n][kp_cap][2] {4 smallest keys}, {their F2 indices}, without the claim filter
+    uint4 *spec;            // [n][kp_cap][4] {8 smallest keys}, {their F2 indices}, without the claim filter
 };
 
-__host__ __device__ inline size_t init_lds_bytes(int cap) { return (size_t)cap * 17 + 4 * 36 + 16; }
+constexpr int kInitChunk = 256;   // F1 keypoints whose speculative keys are staged in LDS at a time
+__host__ __device__ inline size_t init_lds_bytes(int cap) { return kInitChunk * 64 + (size_t)cap * 17 + 4 * 36 + 16; }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -1772,7 +1773,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 }
 
 constexpr uint32_t kNoKey = 0xffffffffu;
-constexpr int kInitSpec = 4;   // speculative keys kept per F1 keypoint
+constexpr int kInitSpec = 8;   // speculative keys kept per F1 keypoint (two uint4 of keys, two of F2 indices)
 
 // Frame::GetFeaturesInArea(x, y, windowSize, 0, 0) window (Frame.cc:890-967) scanned by one wavefront.  Returns
 // the wave-uniform K smallest keys ((dist << 16) | window position, ascending) and their F2 indices (kNoKey / -1
@@ -1867,16 +1868,20 @@ __global__ void __launch_bounds__(256) init_spec_kernel(InitArgs a) {
                                     f.desc + fc2 * cap * 32, d1, prev[0], prev[1], (float)a.window, nullptr, lane, k, id);
     }
     if (lane == 0) {
-        uint4 *o = a.spec + ((size_t)pr * cap + i1) * 2;
+        uint4 *o = a.spec + ((size_t)pr * cap + i1) * 4;
         o[0] = uint4{k[0], k[1], k[2], k[3]};
-        o[1] = uint4{(uint32_t)id[0], (uint32_t)id[1], (uint32_t)id[2], (uint32_t)id[3]};
+        o[1] = uint4{k[4], k[5], k[6], k[7]};
+        o[2] = uint4{(uint32_t)id[0], (uint32_t)id[1], (uint32_t)id[2], (uint32_t)id[3]};
+        o[3] = uint4{(uint32_t)id[4], (uint32_t)id[5], (uint32_t)id[6], (uint32_t)id[7]};
     }
 }
 
 __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int ism[];
+    extern __shared__ __attribute__((aligned(16))) int ism_raw[];
     const FrameArgs &f = a.f;
     const int cap = f.kp_cap, lane = threadIdx.x, pr = blockIdx.x;
+    uint4 *sbuf = reinterpret_cast<uint4 *>(ism_raw);   // [kInitChunk][4] speculative keys of the current chunk
+    int *ism = ism_raw + kInitChunk * 16;
     int *mdist = ism, *m21 = ism + cap, *m12 = ism + 2 * cap;
     int *acc2 = ism + 3 * cap;   // [n1] the F2 keypoint F1 keypoint i1 was accepted with (rotHist push), or -1
     int *cnt = ism + 4 * cap, *ind = cnt + 30;
@@ -1887,41 +1892,63 @@ __global__ void __launch_bounds__(64) init_kernel(InitArgs a) {
     const uint8_t *ds1 = f.desc + fc1 * cap * 32, *ds2 = f.desc + fc2 * cap * 32;
     const int32_t *cs = f.cell_start + fc2 * (kCells + 1), *ci = f.cell_idx + fc2 * cap;
     float *prev = a.prev + (size_t)pr * cap * 2;
-    const uint4 *spec = a.spec + (size_t)pr * cap * 2;
+    const uint4 *spec = a.spec + (size_t)pr * cap * 4;
     for (int i = lane; i < n1; i += 64) m12[i] = -1, acc2[i] = -1, bins[i] = 0xff;
     for (int i = lane; i < n2; i += 64) mdist[i] = INT_MAX, m21[i] = -1;
     if (lane < 30) cnt[lane] = 0;
     __syncthreads();
     const float r = (float)a.window;
     int nm = 0;
-    // the next F1 keypoint's speculative keys are loaded one iteration ahead (the walk is a chain of steps)
-    uint4 skn{}, sidn{};
-    if (n1 > 0) skn = spec[0], sidn = spec[1];
+    // the speculative keys are staged in LDS kInitChunk keypoints at a time (one global round trip per chunk,
+    // not one per step of the walk's chain); the next keypoint's entry is read one step ahead
+    auto stage = [&](int i0) {
+        const int m = min(kInitChunk, n1 - i0) * 4;
+        for (int q = lane; q < m; q += 64) sbuf[q] = spec[4 * i0 + q];
+        wave_sync();
+    };
+    // lane t < kInitSpec holds key t and its F2 index; the checks against the claims are one LDS load per lane
+    const uint32_t *sb = reinterpret_cast<const uint32_t *>(sbuf);
+    const bool kl = lane < kInitSpec;
+    uint32_t nkey = kNoKey;
+    int nidx = -1;
+    if (n1 > 0) {
+        stage(0);
+        if (kl) nkey = sb[lane], nidx = (int)sb[kInitSpec + lane];
+    }
     for (int i1 = 0; i1 < n1; ++i1) {
-        const uint32_t sk[4] = {skn.x, skn.y, skn.z, skn.w};
-        const int si[4] = {(int)sidn.x, (int)sidn.y, (int)sidn.z, (int)sidn.w};
-        if (i1 + 1 < n1) skn = spec[2 * i1 + 2], sidn = spec[2 * i1 + 3];
-        if (sk[0] == kNoKey) continue;   // no candidate without the filter: none with it (or not level 0 / off-grid)
+        const uint32_t mykey = nkey;
+        const int myidx = nidx;
+        if (i1 + 1 < n1) {
+            const int c = (i1 + 1) & (kInitChunk - 1);
+            if (c == 0) stage(i1 + 1);
+            if (kl) nkey = sb[16 * c + lane], nidx = (int)sb[16 * c + kInitSpec + lane];
+        }
+        // no candidate without the filter: none with it (or not level 0 / off-grid)
+        if ((uint32_t)__builtin_amdgcn_readfirstlane(mykey) == kNoKey) continue;
         // the filtered best and second are the two smallest keys the claims leave; known unless fewer than two of
         // the kept keys survive while more candidates may lie beyond them
+        int md = 0, mo = -1;
+        if (kl && mykey != kNoKey) md = mdist[myidx], mo = m21[myidx];
+        const uint64_t ok = __ballot(kl && mykey != kNoKey && md > (int)(mykey >> 16));
         uint32_t g[2] = {kNoKey, kNoKey};
-        int bi[2] = {-1, -1}, found = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (found < 2 && sk[t] != kNoKey && mdist[si[t]] > (int)(sk[t] >> 16)) {
-                if (found == 0) g[0] = sk[t], bi[0] = si[t];
-                else g[1] = sk[t];
-                ++found;
-            }
-        if (found < 2 && sk[3] != kNoKey) {   // the reference's filtered scan
+        int bi[2] = {-1, -1}, old = -1;
+        if (ok) {
+            const int t0 = __ffsll((long long)ok) - 1;
+            g[0] = (uint32_t)__builtin_amdgcn_readlane((int)mykey, t0);
+            bi[0] = __builtin_amdgcn_readlane(myidx, t0), old = __builtin_amdgcn_readlane(mo, t0);
+            const uint64_t rest = ok & (ok - 1);
+            if (rest) g[1] = (uint32_t)__builtin_amdgcn_readlane((int)mykey, __ffsll((long long)rest) - 1);
+        }
+        const int found = __popcll(ok);
+        if (found < 2 && (uint32_t)__builtin_amdgcn_readlane((int)mykey, kInitSpec - 1) != kNoKey) {   // filtered scan
             uint64_t d1[4];
             load_desc(ds1 + (size_t)i1 * 32, d1);
             init_window_scan<2>(f, cs, ci, kp2, ds2, d1, prev[2 * i1], prev[2 * i1 + 1], r, mdist, lane, g, bi);
+            if (g[0] != kNoKey) old = m21[bi[0]];
         }
         if (g[0] == kNoKey) continue;
         const int bestIdx2 = bi[0], bestDist = (int)(g[0] >> 16), bestDist2 = g[1] == kNoKey ? INT_MAX : (int)(g[1] >> 16);
         if (bestDist <= 50 && (float)bestDist < (float)bestDist2 * a.nnratio) {
-            const int old = m21[bestIdx2];
             if (old >= 0) --nm;
             ++nm;
             if (lane == 0) {
@@ -2412,7 +2439,7 @@ omv_status omv_matcher_search_for_initialization(omv_matcher *h, int n_pairs, co
     HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(int32_t) * 2 * n_pairs, st));
     HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(int32_t) * 2 * n_pairs, hipMemcpyHostToDevice, st));
     uint4 *d_spec = nullptr;
-    HIP_OK(hipMallocAsync((void **)&d_spec, sizeof(uint4) * 2 * (size_t)n_pairs * h->kp_cap, st));
+    HIP_OK(hipMallocAsync((void **)&d_spec, sizeof(uint4) * 4 * (size_t)n_pairs * h->kp_cap, st));
     InitArgs ia{f, d_pairs, prev_matched, window, nnratio, check_ori, matches12, n_matches, d_spec};
     init_spec_kernel<<<dim3((h->kp_cap + 3) / 4, n_pairs), 256, 0, st>>>(ia);
     init_kernel<<<n_pairs, 64, lds, st>>>(ia);

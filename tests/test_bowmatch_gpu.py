@@ -162,10 +162,10 @@ def test_search_for_initialization_matches_oracle(oracle, window, check_ori, nnr
         assert n_o > 50
 
 
-def _contest(p, rng, n_clusters=12, copies=6):
+def _contest(p, rng, n_clusters=12, copies=10):
     """Append clusters of identical F1 keypoints (same position, descriptor) and, next to them, F2 keypoints at
     0, 5, 10, ... flipped bits: each copy claims the next-closest F2 keypoint once the earlier copies hold the
-    closer ones, so the walk's speculative four smallest keys run out (the filtered rescan runs)."""
+    closer ones, so the walk's speculative eight smallest keys run out (the filtered rescan runs)."""
     f1k, f1d, f2k, f2d, prev = [p["f1"]["kps"]], [p["f1"]["desc"]], [p["f2"]["kps"]], [p["f2"]["desc"]], [p["prev"]]
     for _ in range(n_clusters):
         xy = np.array([[rng.uniform(40, synth_init.W - 40), rng.uniform(40, synth_init.H - 40)]], np.float32)
@@ -186,7 +186,7 @@ def _contest(p, rng, n_clusters=12, copies=6):
 
 @pytest.mark.parametrize("check_ori", [True, False])
 def test_search_for_initialization_contested_claims(oracle, check_ori):
-    """Claims that exclude the speculative best / second (and all four kept keys) match the oracle bit-exactly."""
+    """Claims that exclude the speculative best / second (and all eight kept keys) match the oracle bit-exactly."""
     import torch
     rng = np.random.Generator(np.random.PCG64(77))
     pairs = [_contest(synth_init.make_init_pair(seed=s, n=500, motion=(2.0, 1.0), rot=3.0), rng) for s in (11, 12, 13)]
@@ -206,5 +206,5 @@ def test_search_for_initialization_contested_claims(oracle, check_ori):
         assert np.array_equal(m12[i, :n1], m_o), (i, np.nonzero(m12[i, :n1] != m_o)[0][:10])
         assert np.array_equal(prev[i, :n1], prev_o)
         # the clusters' later copies matched past the first four keys (the rescan ran)
-        f2n = len(p["f2"]["kps"]) - 12 * 6
-        assert (m_o[n1 - 12 * 6:] >= f2n).sum() >= 12 * 5, m_o[n1 - 12 * 6:]
+        f2n = len(p["f2"]["kps"]) - 12 * 10
+        assert (m_o[n1 - 12 * 10:] >= f2n).sum() >= 12 * 9, m_o[n1 - 12 * 10:]
