@@ -251,7 +251,9 @@ __device__ __forceinline__ double rw_entry(int i, int j, bool acc, const double 
 // kLF = false: PoseInertialOptimizationLastKeyFrame (15 free states, the keyframe's vertices fixed);
 // kLF = true: PoseInertialOptimizationLastFrame (30 free states, EdgePriorPoseImu on the previous frame).
 template <bool kLF>
-__global__ void __launch_bounds__(kPoseThreads) pose_opt_kernel(Rig rig, PoseArgs A) {
+// Two waves per SIMD (<= 256 VGPRs + AGPRs per lane, a few spills): at one wave per SIMD (318 registers) only one
+// frame's workgroup fits a CU and a 1024-frame batch ran in four rounds; two halve that (1.6x per batch, r03i).
+__global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, PoseArgs A) {
     constexpr int N = kLF ? 30 : 15;
     constexpr int NP = kLF ? 225 : 1;
     const int f = blockIdx.x, tid = threadIdx.x;
