@@ -2011,12 +2011,13 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         if (h->n_slots > 0) HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
         if (h->n_slots > 0) HIP_OK(up(d_slot_pt, slot_pt.data(), h->n_slots));
     }
-    // buildSystem landmark groups: whole landmarks in landmark order, at most kGrpEdges edges per group (a landmark
-    // with more edges forms a group of its own)
+    // buildSystem landmark groups: whole landmarks in landmark order, at most kGrpEdges edges AND at most kGrpEdges
+    // landmarks per group (land_group sums one landmark per thread; edge-less landmarks add no edges, so the edge
+    // bound alone would let a group outgrow its threads); a landmark with more edges forms a group of its own
     std::vector<int> grp_pt(1, 0);
     for (int q = 0; q < P;) {
         int r = q + 1;
-        while (r < P && pt_edge[r + 1] - pt_edge[q] <= kGrpEdges) ++r;
+        while (r < P && r - q < kGrpEdges && pt_edge[r + 1] - pt_edge[q] <= kGrpEdges) ++r;
         grp_pt.push_back(r);
         q = r;
     }

@@ -2047,6 +2047,13 @@ static hipEvent_t mk_event(hipStream_t st) {
     return e;
 }
 
+// Camera types of the first n entries: KB8 or Pinhole only (tri / lba / pose reject anything else the same way).
+static bool cam_models_ok(const int *models, int n) {
+    for (int c = 0; c < n; ++c)
+        if (models[c] != OMV_CAM_KB8 && models[c] != OMV_CAM_PINHOLE) return false;
+    return true;
+}
+
 static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kps, const uint8_t *desc, const int *n_kp,
                        FrameArgs &f) {
     f.n_cams = h->n_cams;
@@ -2082,7 +2089,7 @@ extern "C" {
 omv_status omv_frustum(int n_frames, const omv_frame_pose *poses, const omv_rig *rig, const omv_mp_world *mp, int M,
                        float viewing_cos_limit, const omv_mp_track *out, int32_t *n_in_view, void *stream) {
     if (n_frames <= 0 || !poses || !rig || !mp || !out || M < 0 || rig->n_cams <= 0 || rig->n_cams > kMaxCams ||
-        rig->n_levels <= 0)
+        rig->n_levels <= 0 || !cam_models_ok(rig->model, rig->n_cams))
         return OMV_ERR_ARG;
     if (M == 0) return OMV_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -2166,6 +2173,7 @@ omv_status omv_matcher_assign_grid(omv_matcher *h, int n_frames, const omv_frame
     if (!h || !g || !kps || !n_kp || n_frames <= 0 || n_frames > h->max_frames || g->n_cams != h->n_cams)
         return OMV_ERR_ARG;
     FrameArgs f;
+    if (!cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     fill_frame(h, g, kps, nullptr, n_kp, f);
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
@@ -2198,6 +2206,7 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
     FrameArgs f;
+    if (!cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     fill_frame(h, g, kps, desc, n_kp, f);
     MpArgs m{mps->desc, mps->proj_x, mps->proj_y, mps->view_cos, mps->level, mps->in_view, mps->track_depth,
              mps->is_bad, mps->has_obs, M};
@@ -2245,6 +2254,7 @@ omv_status omv_matcher_search_last_frame(omv_matcher *h, int n_frames, const omv
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
     FrameArgs f;
+    if (!cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     fill_frame(h, g, kps, desc, n_kp, f);
     LastArgs L{last->pos, last->desc, last->valid, last->has_obs, last->kps, last->S};
     LfGeo G{};
@@ -2297,7 +2307,7 @@ omv_status omv_matcher_search_kf(omv_matcher *h, int n_kf, const omv_frame_geom 
         if (p->mode == OMV_KF_SBP_FRAME && J.cam != 0) return OMV_ERR_ARG;   // CurrentFrame.mpCamera, left grid
         next += J.mp_count;
     }
-    if (next != n_entries) return OMV_ERR_ARG;
+    if (next != n_entries || !cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     if ((size_t)n_entries > (size_t)h->max_frames * h->n_cams * std::max(1, h->max_mps)) return OMV_ERR_CAPACITY;
     if (n_jobs == 0) return OMV_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -2357,6 +2367,7 @@ omv_status omv_matcher_search_by_sim3(omv_matcher *h, int n_kf, const omv_frame_
         next1 += J.count1, next2 += J.count2;
     }
     if (next1 != n1 || next2 != n2) return OMV_ERR_ARG;
+    if (!cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     if (n_jobs == 0) return OMV_OK;
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
@@ -2431,6 +2442,7 @@ omv_status omv_matcher_search_for_initialization(omv_matcher *h, int n_pairs, co
     hipStream_t st = (hipStream_t)stream;
     h->last = st;
     FrameArgs f;
+    if (!cam_models_ok(g->cam_model, h->n_cams)) return OMV_ERR_ARG;
     fill_frame(h, g, kps, desc, n_kp, f);
     const size_t lds = init_lds_bytes(h->kp_cap);
     if (lds > 160 * 1024) return OMV_ERR_CAPACITY;

@@ -176,6 +176,24 @@ def test_optimize_visual_only_with_fixed_only_points(oracle):
     _compare_state(prob, sg, so, oracle)
 
 
+def test_optimize_with_edgeless_points(small, oracle):
+    """More than one build group's worth (> 256) of landmarks without edges, interleaved with observed ones: each
+    still gets its (zero) Hll / bl, so the back-substitution and computeScale see no stale values."""
+    prob = dict(small)
+    rng = np.random.default_rng(21)
+    n0, extra = len(prob["pts"]), 700
+    new = np.asarray(prob["pts"])[rng.integers(0, n0, extra)] + rng.normal(0, 0.5, (extra, 3))
+    prob["pts"] = np.concatenate([prob["pts"], new])
+    prob["pt_track_depth"] = np.concatenate([prob["pt_track_depth"], rng.uniform(1, 60, extra).astype(np.float32)])
+    for large in (True, False):
+        kw = dict(opt_it=4, lambda_init=1e-2) if large else dict(opt_it=10, lambda_init=1e0)
+        ro, so, _ = oracle.lba_optimize(prob, max_trials=10, large=large, **kw)
+        rg, sg = _solver(prob).set_problem(prob).optimize(max_trials=10, large=large, **kw)
+        _compare_result(prob, rg, ro)
+        _compare_state(prob, sg, so, oracle)
+        assert np.array_equal(sg["pts"][n0:], np.asarray(prob["pts"], np.float64)[n0:])
+
+
 def test_optimize_full_window(full, oracle):
     """The bench configuration: 25 optimisable + 25 fixed keyframes, 5 cameras, 20k points, 120k edges."""
     ro, so, _ = oracle.lba_optimize(full, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)

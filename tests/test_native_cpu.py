@@ -103,3 +103,28 @@ def test_no_device_means_loud_failure():
     from openmavis_amd.orb import ORBextractor
     with pytest.raises(_lib.OmvError):
         ORBextractor(500, 1.2, 8, 20, 7, width=640, height=480)
+
+
+def test_unknown_camera_model_is_rejected():
+    """Every projecting entry point rejects a camera type other than KB8 / Pinhole before touching the device
+    (a stray cam_model used to mean KB8 silently): omv_frustum through omv_rig.model."""
+    import ctypes
+    from openmavis_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from openmavis_amd import build
+        build.build_hip()
+    lib = _lib.load()
+    rig = _lib.Rig()
+    rig.n_cams, rig.n_levels, rig.log_scale_factor = 2, 8, 0.18232156
+    rig.min_x, rig.max_x, rig.min_y, rig.max_y = 0.0, 720.0, 0.0, 540.0
+    dummy = (ctypes.c_byte * 4096)()
+    poses, world, track = ctypes.cast(dummy, ctypes.c_void_p), _lib.MpWorld(), _lib.MpTrack()
+    for bad in (2, -1, 7):
+        rig.model[1] = bad
+        st = lib.omv_frustum(1, poses, ctypes.byref(rig), ctypes.byref(world), 0, ctypes.c_float(0.5),
+                             ctypes.byref(track), None, None)
+        assert st == _lib.OMV_ERR_ARG, (bad, st)
+    rig.model[1] = 1   # Pinhole: accepted (M = 0 returns before any launch)
+    st = lib.omv_frustum(1, poses, ctypes.byref(rig), ctypes.byref(world), 0, ctypes.c_float(0.5),
+                         ctypes.byref(track), None, None)
+    assert st == 0
