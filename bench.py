@@ -739,7 +739,8 @@ P_W, P_H, P_C, P_NF, P_INI, P_MIN, P_M, P_TH = 1920, 1080, 8, 2000, 20, 7, 8000,
 
 
 BYTES_FORMULA = {
-    "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image",
+    "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image (one launch per level: the 7 level "
+                  "launches of a stream group are timed and counted together as one 'launch')",
     "fast_cells": "sum of level pixels read once, per image",
     "octree": "4 B per FAST candidate read (its input list) + 8 B per distributed keypoint written",
     "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image (the blur is evaluated in LDS at "
@@ -750,6 +751,25 @@ BYTES_FORMULA = {
     "proj_candidates": "SURVEY 8(d) map points 5,000 x (32 + 5 x 16) B + frame descriptors 32 B per keypoint",
     "proj_resolve": "SURVEY 8(d) outputs: 43,200 B per frame",
 }
+
+
+def rocprof_launch_avg(kernel):
+    """Dispatch-trace average of `kernel` at its most-used grid in the newest committed
+    profiles/<tag>_kernel_grid.json (tools/summarize_profile.py); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_kernel_grid.json")))
+    if not files:
+        return None
+    try:
+        r = json.load(open(files[-1]))
+        rows = [x for x in r["rows"] if x["kernel"] == kernel]
+        if not rows:
+            return None
+        best = max(rows, key=lambda x: x["total_us"])
+        return {"avg_launch_ms": round(best["avg_us"] / 1e3, 4), "avg_us": best["avg_us"], "grid": best["grid"],
+                "calls": best["calls"], "source": os.path.relpath(files[-1], ROOT)}
+    except Exception:
+        return None
 
 
 def per_step_algorithmic_bytes(B, P, n_kp, n_cand):
@@ -1404,6 +1424,13 @@ def main():
                 "bytes_formula": d["bytes_formula"]}
         if d.get("traffic_source"):
             roof["traffic_source"] = d["traffic_source"]
+        rp = rocprof_launch_avg(dom)
+        if rp is not None:   # the committed rocprofv3 dispatch trace of the same bench launches, beside the events
+            ach = d["algorithmic_bytes_per_launch"] / (rp["avg_us"] * 1e-6) / 1e9
+            roof["rocprof"] = dict(rp, achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
+                                   note="rocprofv3 --kernel-trace average of the dominant kernel's bench-grid launches "
+                                        "(device time only; the HIP events above also hold queueing behind the other "
+                                        "streams' kernels)")
         iso_k = [k for k in kernels if "isolated" in kernels[k]]
         if iso_k:
             di = max(iso_k, key=lambda k: kernels[k]["isolated"]["avg_launch_ms"])

@@ -57,10 +57,16 @@ def main(src, tag, command=None):
                 (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
         lines += ["", "## Per kernel and grid size (dispatch trace)", "",
                   "| kernel | grid (work-items) | calls | avg us | min us |", "|---|---|---|---|---|"]
+        grid_rows = []
         for (k, g), v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
             if sum(v) < 50:   # skip sub-50-us totals
                 continue
             lines.append(f"| {k} | {g} | {len(v)} | {sum(v) / len(v):.1f} | {min(v):.1f} |")
+            grid_rows.append({"kernel": k, "grid": g, "calls": len(v), "avg_us": round(sum(v) / len(v), 2),
+                              "min_us": round(min(v), 2), "total_us": round(sum(v), 1)})
+        # read by bench.py (roofline.rocprof): the dominant kernel's dispatch-trace average beside its HIP-event time
+        json.dump({"tag": tag, "command": command, "rows": grid_rows},
+                  open(os.path.join(prof, f"{tag}_kernel_grid.json"), "w"), indent=1)
     pmc = defaultdict(lambda: defaultdict(list))
     for srcname in PMC_SOURCES:
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -70,19 +76,26 @@ def main(src, tag, command=None):
             for r in csv.DictReader(open(p)):
                 pmc[(srcname, short(r["Kernel_Name"]))][c].append(float(r["Counter_Value"]))
     lines += ["", "## HBM traffic per launch (separate --pmc passes; KB x 1024; FETCH doubled for gfx950)", "",
-              "| program | kernel | launches | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | corrected bytes/launch | per unit |",
+              "| program | kernel | launches | FETCH_SIZE KB/launch | WRITE_SIZE KB/launch | corrected bytes/launch | per unit (all launches of a pass) |",
               "|---|---|---|---|---|---|---|"]
+    # passes of a program = launches of its once-per-pass kernel; a kernel launched several times per pass (pyr_resize:
+    # one launch per pyramid level, 7 per extraction) has its per-unit bytes summed over all its launches of a pass
+    per_pass = {"orb": "describe", "match": "proj_resolve", "lba": None}
+    passes = {src: len(pmc[(src, k)]["FETCH_SIZE"]) for src, k in per_pass.items() if k and (src, k) in pmc}
     for (srcname, k), d in sorted(pmc.items()):
         f = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
         w = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
         b = (2 * f + w) * 1024
         unit, n = PMC_SOURCES[srcname]
+        lpp = len(d["FETCH_SIZE"]) / passes[srcname] if passes.get(srcname) else 1.0
         lines.append(f"| {srcname} | {k} | {len(d['FETCH_SIZE'])} | {f:.1f} | {w:.1f} | {b:.0f} | "
-                     f"{b / n:.0f} B per {unit[:-1]} |")
+                     f"{b * lpp / n:.0f} B per {unit[:-1]} ({lpp:g} launches per pass) |")
         if k in SHORT.values():
             rec = {"kernel": k, "tag": tag, "program": srcname, "fetch_kb_per_launch": f, "write_kb_per_launch": w,
                    "hbm_bytes_per_launch": round(b), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024",
-                   f"{unit}_per_launch": n, f"hbm_bytes_per_{unit[:-1]}": round(b / n)}
+                   f"{unit}_per_launch": n, "launches_per_pass": lpp,
+                   f"hbm_bytes_per_{unit[:-1]}": round(b * lpp / n),
+                   "per_unit_note": f"all launches of one pass (one batched call over {n} {unit}) summed, / {n}"}
             out = os.path.join(prof, f"pmc_{k}.json")
             if srcname == "match" and os.path.exists(out) and json.load(open(out)).get("program") == "orb":
                 continue   # extraction kernels keep the extraction-only program's numbers
