@@ -671,6 +671,20 @@ typedef struct omv_pose_prior {
 omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, const omv_pose_prior *prior,
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream);
 
+/* Kernel choice of the two calls above.  OMV_POSE_AUTO (default): up to 16 frames per call run on the grouped
+ * kernel — one frame over `parts` workgroups (0: one per 256 visual edges, at most 8) that exchange their
+ * normal-equation sums every Gauss-Newton iteration, the latency path of Tracking's one-frame call — and larger batches
+ * on one workgroup per frame.  OMV_POSE_BATCH / OMV_POSE_GROUPED force one of them (GROUPED needs kp_cap <= 16384).
+ * The grouped kernel reports a frame it could not run (more than 1024 visual edges in one workgroup's keypoint
+ * range) with n_good = -1 and OMV_ERR_CAPACITY in omv_pose_last_error. */
+#define OMV_POSE_AUTO 0
+#define OMV_POSE_BATCH 1
+#define OMV_POSE_GROUPED 2
+omv_status omv_pose_set_mode(omv_pose *h, int mode, int parts);
+/* Device error word of the calls since the last read (0, or OMV_ERR_CAPACITY / OMV_ERR_HIP from the grouped kernel);
+ * resets it and synchronises `stream`. */
+omv_status omv_pose_last_error(omv_pose *h, int32_t *err, void *stream);
+
 /* ConstraintPoseImu ctor (include/G2oTypes.h:639-659) on n matrices: H <- (H + H) / 2 (= H), then its
  * symmetric eigen-decomposition with eigenvalues below 1e-12 zeroed, recomposed.  Device [n][225]
  * (H_out may alias H_in).  Asynchronous. */

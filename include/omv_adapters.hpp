@@ -26,6 +26,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "omv.h"
@@ -309,6 +310,20 @@ class LocalInertialBAWindow {
         stereo_.push_back({pt, kf, u, v, u_right, inv_sigma2});
     }
     void add_inertial(const Inertial &e) { imu_.push_back(e); }
+    // Landmark sharding: this window's `rank` of `world` and the caller's in-place SUM
+    // collective (e.g. ncclAllReduce on the handle's stream).  Every rank adds the same full window; each optimises
+    // its share of the landmarks.  Kept across handle re-creation; a communicator of one rank runs the same collective
+    // call sequence.
+    void set_comm(int rank, int world, omv_allreduce_fn fn, void *ctx) {
+        rank_ = rank, world_ = world, ar_ = fn, ar_ctx_ = ctx;
+        if (h_) check(omv_lba_set_comm(h_, rank_, world_, ar_, ar_ctx_), "omv_lba_set_comm");
+    }
+    // Host waits of the last optimize()'s LM loop and its trials (omv_lba_host_syncs).
+    std::pair<int, int> host_syncs() const {
+        int n = 0, t = 0;
+        if (h_) check(omv_lba_host_syncs(h_, &n, &t), "omv_lba_host_syncs");
+        return {n, t};
+    }
     // Drop every keyframe, point and edge (the handle and its capacity are kept for the next window).
     void clear() { kfs_.clear(), pts_.clear(), depth_.clear(), mono_.clear(), stereo_.clear(), imu_.clear(); }
 
@@ -358,6 +373,7 @@ class LocalInertialBAWindow {
         if (h_) (void)omv_lba_destroy(h_), h_ = nullptr;
         for (int i = 0; i < 5; ++i) cap_[i] = std::max(cap_[i], need[i]);
         check(omv_lba_create(cap_[0], cap_[1], cap_[2], cap_[3], cap_[4], &h_), "omv_lba_create");
+        if (ar_ || world_ > 1) check(omv_lba_set_comm(h_, rank_, world_, ar_, ar_ctx_), "omv_lba_set_comm");
     }
     void flatten() {
         const int K = (int)kfs_.size();
@@ -449,6 +465,9 @@ class LocalInertialBAWindow {
     omv_lba_problem p_{};
     omv_lba *h_ = nullptr;
     int cap_[5] = {0, 0, 0, 0, 0};   // max_kf, max_cams, max_pts, max visual edges, max_imu of h_
+    int rank_ = 0, world_ = 1;
+    omv_allreduce_fn ar_ = nullptr;
+    void *ar_ctx_ = nullptr;
 };
 
 }  // namespace omv_adapt

@@ -90,7 +90,7 @@ def build_consumer(verbose=True):
     cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(rocm, "include"), CONSUMER_SRC,
            "-o", CONSUMER_BIN + ".tmp", "-L", PKG, "-lomv_hip", "-Wl,-rpath,$ORIGIN/..",
-           "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath," + os.path.join(rocm, "lib")]
+           "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-lrccl", "-Wl,-rpath," + os.path.join(rocm, "lib")]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -518,6 +518,39 @@ __device__ inline void imu_error_jac_p2v2(const State &s, const Imu &I, int i, d
         }
 }
 
+// Fixed-order wavefront sum of N <= 64 per-lane values at once (a transposing butterfly): at distance d = 32 .. 1
+// each lane keeps one half of its current values -- the lower half when (lane & d) == 0 -- adds the partner's
+// copy of that half, and sends the other; after six steps lane l holds the wave total of value l (l < N), in an
+// order fixed by the lane numbering.  63 shuffles instead of the 6 N of N separate xor trees.
+template <int N>
+__device__ __forceinline__ double wave_transpose_sum(const double (&v)[N], int lane) {
+    static_assert(N <= 64, "at most one value per lane");
+    double a[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {   // d = 32: values j and 32 + j
+        const double lo = j < N ? v[j] : 0.0, hi = j + 32 < N ? v[j + 32] : 0.0;
+        const bool up = (lane & 32) != 0;
+        a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, 64);
+    }
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) {
+        const bool up = (lane & d) != 0;
+#pragma unroll
+        for (int j = 0; j < d; ++j) {
+            const double lo = a[j], hi = a[j + d];
+            a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, d, 64);
+        }
+    }
+    return a[0];
+}
+
+// Lane l's value of x to every lane (v_readlane on both halves; l wave-uniform).
+__device__ __forceinline__ double lane_f64(double x, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

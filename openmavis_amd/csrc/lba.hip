@@ -486,32 +486,6 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
     return v;
 }
 
-// Fixed-order wavefront sum of N <= 64 per-lane values at once (a transposing butterfly): at distance d = 32 .. 1
-// each lane keeps one half of its current values -- the lower half when (lane & d) == 0 -- adds the partner's
-// copy of that half, and sends the other; after six steps lane l holds the wave total of value l (l < N), in an
-// order fixed by the lane numbering.  63 shuffles instead of the 6 N of N separate xor trees.
-template <int N>
-__device__ __forceinline__ double wave_transpose_sum(const double (&v)[N], int lane) {
-    static_assert(N <= 64, "at most one value per lane");
-    double a[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {   // d = 32: values j and 32 + j
-        const double lo = j < N ? v[j] : 0.0, hi = j + 32 < N ? v[j + 32] : 0.0;
-        const bool up = (lane & 32) != 0;
-        a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, 64);
-    }
-#pragma unroll
-    for (int d = 16; d >= 1; d >>= 1) {
-        const bool up = (lane & d) != 0;
-#pragma unroll
-        for (int j = 0; j < d; ++j) {
-            const double lo = a[j], hi = a[j + d];
-            a[j] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, d, 64);
-        }
-    }
-    return a[0];
-}
-
 // Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= kGrpEdges edges of one keyframe, ascending) per
 // block, one edge per thread: 21 + 6 terms, a fixed-order reduction (transposing wave sums, then the waves in order),
 // one partial row.  The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled.
@@ -2172,8 +2146,11 @@ static omv_status lba_trial_errors(omv_lba *h, const LmCtl *c) {
 }
 
 // In-place SUM over the ranks of a sharded solve (no-op on one rank).
+// The collective path runs whenever a communicator was given (omv_lba_set_comm), a single rank included: one RCCL
+// rank exercises exactly the multi-rank call sequence (stream order, in-place buffers, host-sync count).
+static bool lba_collective(const omv_lba *h) { return h->allreduce != nullptr; }
 static omv_status lba_allreduce(omv_lba *h, double *buf, size_t n) {
-    if (h->world <= 1) return OMV_OK;
+    if (!lba_collective(h)) return OMV_OK;
     HIP_OK(hipGetLastError());
     return h->allreduce(h->ar_ctx, buf, n, (void *)h->stream) == 0 ? OMV_OK : OMV_ERR_HIP;
 }
@@ -2339,7 +2316,7 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     if ((rs = lba_trial_errors(h, c)) != OMV_OK) return rs;
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0, nsc = h->n_pts > 0 ? h->n_wg_land + 1 : 1;
     const double *pre = nullptr;
-    if (h->world > 1) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
+    if (lba_collective(h)) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
         const int s0 = h->rank > 0 ? 1 : 0;   // the keyframe part of computeScale enters once (rank 0)
         trial_scalars_kernel<<<1, 256, 0, st>>>(c, h->d_partial, nmb, h->d_imu_partial, h->d_scale_partial + s0,
                                                 nsc - s0, h->d_out, h->d_partial0, h->d_imu_partial0);
@@ -2371,7 +2348,7 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
     omv_status rs;
     h->host_syncs = 0;
     const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
-    const bool sharded = h->world > 1;
+    const bool sharded = lba_collective(h);
     if (o->opt_it > 0 && nmb + (h->imu_here ? 1 : 0) > 0) {
         // the initial errors into their own partials, the control block reset by the same launch; the first step's
         // bookkeeping sums the initial chi (through the first all-reduce on a sharded solve)

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <vector>
 
@@ -710,6 +711,896 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
     for (int q = tid; q < C * 3; q += kPoseThreads) A.tcw[(size_t)f * C * 3 + q] = stcw[q];
 }
 
+
+// =====================================================================================================================
+// Latency path: one frame over G workgroups (Tracking's call pattern is ONE frame whose pose the next frame waits for,
+// Tracking.cc:2904-2942).  The frame's visual edges are split by keypoint range over the G workgroups (both edges of a
+// keypoint that carries a mono and a stereo edge land in one workgroup, so mvbOutlier stays workgroup-local) and held
+// in LDS for the whole call.  Per Gauss-Newton iteration every workgroup evaluates its edges (waves 0-3, one edge per
+// thread at <= 256 edges per workgroup), while wave 4 linearises EdgeInertial and wave 5 (LastFrame) EdgePriorPoseImu at
+// the same state; the 27 visual normal-equation sums of the G workgroups are exchanged as 8-byte {tag, word} granules
+// (write-through `sc1` stores, polled `sc1` loads: no fence, MI355X_MICROARCH.md hand-off R2) and summed in part order,
+// so every workgroup holds the identical system and runs the identical solve and update -- no second hop to broadcast
+// the state.  The 15x15 / 30x30 system is solved by one wavefront with the rows in registers (pivot order first,
+// Eigen's transpositions replayed on the original diagonal; right-looking LDL^T with v_readlane row broadcasts).
+// =====================================================================================================================
+constexpr int kLatThreads = 384;        // waves 0-3: visual edges; 4: EdgeInertial; 5: EdgePriorPoseImu (LastFrame)
+constexpr int kLatEdgeThreads = 256;
+constexpr int kLatMaxParts = 8;         // workgroups per frame
+constexpr int kLatCap = 1024;           // visual edges per workgroup (LDS)
+constexpr int kLatFlagCap = 16384;      // keypoints per frame (mvbOutlier staged in LDS)
+constexpr int kGran = 64;               // 8-byte granules per (frame, slot, part)
+constexpr int kLatAutoFrames = 16;      // OMV_POSE_AUTO: the grouped kernel up to this many frames per call
+constexpr size_t kLatFrameGran = 2 * kLatMaxParts * kGran;   // granules per frame (two slots by phase parity)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q): publish this part's values as
+// 2n granules of slot (phase & 1), sweep all G x 2n granules until every tag equals salt | phase, add the parts in part
+// order into out[0..n) (LDS).  One wavefront; false on a bounded-spin timeout (a missing sibling workgroup).
+__device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n, uint32_t *sc,
+                             double *out, int lane) {
+    const uint32_t tag = salt | (uint32_t)phase;
+    gu64 *slot = fb + (size_t)(phase & 1) * kLatMaxParts * kGran;
+    if (lane < n) {
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        __hip_atomic_store(slot + g * kGran + 2 * lane, ((unsigned long long)tag << 32) | (uint32_t)b, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(slot + g * kGran + 2 * lane + 1, ((unsigned long long)tag << 32) | (uint32_t)(b >> 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int per = 2 * n, M = G * per;
+    uint32_t val[8];
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int i = lane + 64 * m;
+            if (i < M) {
+                const int p = i / per, w = i - p * per;
+                const unsigned long long x = __hip_atomic_load(slot + p * kGran + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                val[m] = (uint32_t)x;
+                ok &= (uint32_t)(x >> 32) == tag;
+            }
+        }
+        if (__all(ok)) break;
+        if (spins > (1u << 22)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int i = lane + 64 * m;
+        if (i < M) {
+            const int p = i / per, w = i - p * per;
+            sc[p * kGran + w] = val[m];
+        }
+    }
+    wave_lds_sync();
+    if (lane < n) {
+        double s = 0;
+        for (int p = 0; p < G; ++p)
+            s += __builtin_bit_cast(double, ((uint64_t)sc[p * kGran + 2 * lane + 1] << 32) | sc[p * kGran + 2 * lane]);
+        out[lane] = s;
+    }
+    wave_lds_sync();
+    return true;
+}
+
+// Eigen::LDLT<MatrixXd> (ldlt_inplace::unblocked's pivot order, isPositive(), _solve_impl's D pseudo-inverse below
+// DBL_MIN) of the N x N symmetric H (LDS, row-major) on one wavefront, lane i = pivot position i:
+//   pick order  Eigen swaps the largest |diagonal| of the trailing corner to position k, first position on ties; that
+//               diagonal is never updated before it is picked, so the order follows from the original diagonal alone:
+//               by rank when the magnitudes are distinct, else replayed step by step (one ballot per step)
+//   factor      rows of P H P^T in registers; step k: D_k by v_readlane, column k below scaled by 1 / D_k, trailing
+//               update from row k (v_readlane broadcasts, FMA); a zero pivot leaves its column unscaled and no update
+//               (its terms D_k l l^T vanish in Eigen's left-looking form)
+//   solve       y = P b, L y' = y, y'' = D^+ y', L^T x = y'', x = P^T (same per-element subtraction order as Eigen's
+//               triangular solves; the factor differs from Eigen's by rounding: right-looking, fused multiply-adds)
+// x: LDS out (written only on success); pick / Lm: LDS scratch [N] / [N * N].  Returns isPositive().
+template <int N>
+__device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b, double *x, int *pick, double *Lm, int lane) {
+    static_assert(N <= 32, "rows on lanes 0..31");
+    const bool in = lane < N;
+    const double dv = in ? fabs(H[lane * (N + 1)]) : 0.0;
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double o = fabs(H[j * (N + 1)]);
+        gt += o > dv ? 1 : 0;
+        eq += o == dv ? 1 : 0;
+    }
+    if (__ballot(in && !(dv == dv))) return false;   // a NaN diagonal: no factorisation
+    if (!__ballot(in && eq > 1)) {
+        if (in) pick[gt] = lane;
+    } else {   // selection with positional swaps, lanes = elements (pos = current position)
+        int pos = lane;
+        bool picked = false;
+        for (int k = 0; k < N; ++k) {
+            uint64_t cand = __ballot(in && !picked && gt <= k && k < gt + eq);
+            int e = __builtin_ctzll(cand);
+            if (cand & (cand - 1)) {   // several equal magnitudes: the lowest current position
+                int bp = __builtin_amdgcn_readlane(pos, e);
+                for (uint64_t m = cand & (cand - 1); m; m &= m - 1) {
+                    const int c = __builtin_ctzll(m), pc = __builtin_amdgcn_readlane(pos, c);
+                    if (pc < bp) bp = pc, e = c;
+                }
+            }
+            const int xk = __builtin_ctzll(__ballot(in && pos == k));
+            const int pe = __builtin_amdgcn_readlane(pos, e);
+            if (lane == xk) pos = pe;
+            if (lane == e) pos = k, picked = true;
+            if (lane == 0) pick[k] = e;
+        }
+    }
+    wave_lds_sync();
+    const int pi = in ? pick[lane] : 0;
+    double r[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) r[j] = in ? H[pi * N + pick[j]] : 0.0;
+    if (!(lane_f64(r[0], 0) != 0.0)) {   // largest |diagonal| zero: Eigen stops with ZeroSign; the solve gives x = 0
+        if (in) x[lane] = 0.0;
+        wave_lds_sync();
+        return true;
+    }
+    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
+    double dmine = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const double d = lane_f64(r[k], k);
+        if (lane == k) dmine = d;
+        if (fabs(d) > 0.0) {
+            const double l = r[k] / d;
+#pragma unroll
+            for (int j = k + 1; j < N; ++j) {
+                const double c = lane_f64(r[j], k);
+                if (lane > k) r[j] = __builtin_fma(-l, c, r[j]);
+            }
+            if (lane > k) r[k] = l;
+        }
+        if (sign == 1) {
+            if (d < 0) sign = 3;
+        } else if (sign == 2) {
+            if (d > 0) sign = 3;
+        } else if (sign == 0) {
+            if (d > 0) sign = 1;
+            else if (d < 0) sign = 2;
+        }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    double y = in ? b[pi] : 0.0;
+#pragma unroll
+    for (int k = 0; k + 1 < N; ++k) {
+        const double yk = lane_f64(y, k);
+        if (lane > k) y = __builtin_fma(-r[k], yk, y);
+    }
+    y = fabs(dmine) > 2.2250738585072014e-308 ? y / dmine : 0.0;
+    if (in)
+#pragma unroll
+        for (int j = 0; j < N; ++j) Lm[lane * N + j] = r[j];
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < N; ++j) r[j] = in ? Lm[j * N + lane] : 0.0;   // r[j] = L_j,lane
+#pragma unroll
+    for (int j = N - 1; j >= 1; --j) {
+        const double xj = lane_f64(y, j);
+        if (lane < j) y = __builtin_fma(-r[j], xj, y);
+    }
+    if (in) x[pi] = y;
+    wave_lds_sync();
+    return true;
+}
+
+// EdgeInertial::linearizeOplus (G2oTypes.cc:533-599) on one wavefront from the cached rotation error (eR, er): the
+// lane roles of imu_jacobian_par, synchronised by wave barriers; entry for entry the arithmetic of imu_jacobian.
+// J [9][24] (LDS) must be zeroed by the caller; RJ, iJ: LDS scratch [9].
+__device__ void imu_jacobian_wave(const State &s, const Imu &I, const double *eR, const double *er, double *J,
+                                  double *RJ, double *iJ, int lane) {
+    const int k1 = I.kf1[0], k2 = I.kf2[0];
+    const float *p = I.pre;
+    const double *Rwb1 = s.Rwb + 9 * k1, *Rwb2 = s.Rwb + 9 * k2;
+    auto put = [&](int r0, int c0, const double *B, double sgn) {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) J[(r0 + r) * 24 + c0 + c] = sgn * B[3 * r + c];
+    };
+    const double dt = (double)p[PreView::dT];
+    const double g[3] = {0, 0, -(double)9.81f};
+    double Rbw1[9];
+    tr3(Rwb1, Rbw1);
+    if (lane == 0) {
+        double invJr[9], R2t[9], A[9], B[9];
+        inv_right_jac(er, invJr);
+        tr3(Rwb2, R2t);
+        mm3(invJr, R2t, A);
+        mm3(A, Rwb1, B);
+        put(0, 0, B, -1.0);
+        put(0, 15, invJr, 1.0);
+        for (int q = 0; q < 9; ++q) iJ[q] = invJr[q];
+    } else if (lane == 1) {
+        float b1[6];
+        for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
+        const float dbgf[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
+        const double dbg[3] = {(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]};
+        double JRg[9], w3[3], R[9];
+        for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q];
+        mv3(JRg, dbg, w3);
+        right_jac(w3, R);
+        for (int q = 0; q < 9; ++q) RJ[q] = R[q];
+    } else if (lane == 2) {
+        double v[3], w[3], W[9];
+        for (int q = 0; q < 3; ++q) v[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
+        mv3(Rbw1, v, w);
+        hat3(w, W);
+        put(3, 0, W, 1.0);
+    } else if (lane == 3) {
+        double v[3], w[3], W[9];
+        for (int q = 0; q < 3; ++q)
+            v[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - 0.5 * g[q] * dt * dt;
+        mv3(Rbw1, v, w);
+        hat3(w, W);
+        put(6, 0, W, 1.0);
+    } else if (lane == 4) {
+        for (int q = 0; q < 3; ++q) J[(6 + q) * 24 + 3 + q] = -1.0;
+        put(3, 6, Rbw1, -1.0);
+        put(3, 21, Rbw1, 1.0);
+    } else if (lane == 5) {
+        put(6, 6, Rbw1, -dt);
+    } else if (lane == 6) {
+        double B[9];
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JVg + q];
+        put(3, 9, B, -1.0);
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JVa + q];
+        put(3, 12, B, -1.0);
+    } else if (lane == 7) {
+        double B[9];
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JPg + q];
+        put(6, 9, B, -1.0);
+        for (int q = 0; q < 9; ++q) B[q] = p[PreView::JPa + q];
+        put(6, 12, B, -1.0);
+    } else if (lane == 8) {
+        double A[9];
+        mm3(Rbw1, Rwb2, A);
+        put(6, 18, A, 1.0);
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+        double eRt[9], A[9], B[9], Jg[9], JRg[9], invJr[9], R[9];
+        for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q], invJr[q] = iJ[q], R[q] = RJ[q];
+        tr3(eR, eRt);
+        mm3(invJr, eRt, A);
+        mm3(A, R, B);
+        mm3(B, JRg, Jg);
+        put(0, 9, Jg, -1.0);
+    }
+    wave_lds_sync();
+}
+
+// LDS of the grouped kernel beyond its static arrays: the workgroup's visual edges (SoA) and the frame's mvbOutlier.
+struct LatEdges {
+    double *ob0, *ob1, *ob2, *c2;   // observation (u, v, u_R), e->chi2() of the last computeError
+    float *x0, *x1, *x2, *w;        // MapPoint world position, invSigma2
+    int32_t *kp;
+    uint8_t *cam, *fl;              // camera; flags: 1 stereo, 2 bClose, 4 active (level 0)
+    uint8_t *kpo;                   // [kp_cap] mvbOutlier of the keypoints this workgroup owns
+};
+__host__ __device__ inline size_t lat_lds_bytes(int kp_cap) {
+    return (size_t)kLatCap * (4 * 8 + 4 * 4 + 4 + 2) + (((size_t)kp_cap + 15) / 16) * 16;
+}
+__device__ __forceinline__ LatEdges lat_carve(char *base) {
+    LatEdges E;
+    E.ob0 = (double *)base, E.ob1 = E.ob0 + kLatCap, E.ob2 = E.ob1 + kLatCap, E.c2 = E.ob2 + kLatCap;
+    E.x0 = (float *)(E.c2 + kLatCap), E.x1 = E.x0 + kLatCap, E.x2 = E.x1 + kLatCap, E.w = E.x2 + kLatCap;
+    E.kp = (int32_t *)(E.w + kLatCap);
+    E.cam = (uint8_t *)(E.kp + kLatCap), E.fl = E.cam + kLatCap, E.kpo = E.fl + kLatCap;
+    return E;
+}
+__device__ __forceinline__ VEdge lat_edge(const LatEdges &E, int q) {
+    VEdge v;
+    v.cam = E.cam[q], v.kp = E.kp[q], v.stereo = (E.fl[q] & 1) != 0;
+    v.obs[0] = E.ob0[q], v.obs[1] = E.ob1[q], v.obs[2] = v.stereo ? E.ob2[q] : 0.0;
+    v.w = (double)E.w[q];
+    v.X[0] = (double)E.x0[q], v.X[1] = (double)E.x1[q], v.X[2] = (double)E.x2[q];
+    return v;
+}
+
+// Workgroup-ordered compaction of this part's edges of one list (mono or stereo): edges whose keypoint lies in
+// [lo, hi), in list order, appended at *count.  Returns false (uniformly) past kLatCap.
+__device__ bool lat_select(const PoseArgs &A, bool stereo, int e0, int n, int lo, int hi, const LatEdges &E, int *count,
+                           int *wcnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = kLatThreads / 64;
+    for (int base = 0; base < n; base += kLatThreads) {
+        const int q = base + tid;
+        int kp = -1;
+        if (q < n) kp = stereo ? A.s_kp[e0 + q] : A.m_kp[e0 + q];
+        const bool take = q < n && kp >= lo && kp < hi;
+        const uint64_t bal = __ballot(take);
+        if (lane == 0) wcnt[wave] = __builtin_popcountll(bal);
+        __syncthreads();
+        int off = *count;
+        for (int w2 = 0; w2 < wave; ++w2) off += wcnt[w2];
+        int tot = *count;
+        for (int w2 = 0; w2 < kW; ++w2) tot += wcnt[w2];
+        if (tot > kLatCap) return false;
+        if (take) {
+            const int d = off + __builtin_popcountll(bal & ((1ull << lane) - 1));
+            const int e = e0 + q;
+            E.kp[d] = kp;
+            if (!stereo) {
+                E.cam[d] = (uint8_t)A.m_cam[e];
+                E.ob0[d] = A.m_obs[2 * e], E.ob1[d] = A.m_obs[2 * e + 1], E.ob2[d] = 0.0;
+                E.w[d] = A.m_w[e];
+                E.x0[d] = A.m_xw[3 * e], E.x1[d] = A.m_xw[3 * e + 1], E.x2[d] = A.m_xw[3 * e + 2];
+                E.fl[d] = (uint8_t)(4 | (A.m_close[e] ? 2 : 0));
+            } else {
+                E.cam[d] = (uint8_t)A.s_cam[e];
+                E.ob0[d] = A.s_obs[3 * e], E.ob1[d] = A.s_obs[3 * e + 1], E.ob2[d] = A.s_obs[3 * e + 2];
+                E.w[d] = A.s_w[e];
+                E.x0[d] = A.s_xw[3 * e], E.x1[d] = A.s_xw[3 * e + 1], E.x2[d] = A.s_xw[3 * e + 2];
+                E.fl[d] = 4 | 1;
+            }
+            E.kpo[kp] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) *count = tot;
+        __syncthreads();
+    }
+    return true;
+}
+
+// Keypoint-range boundary p of G: the mono list's (else the stereo list's) keypoint at its p/G quantile, made monotone
+// over p (the reference creates edges in keypoint order, so the parts balance; any order partitions correctly).
+__device__ int lat_bound(const PoseArgs &A, int p, int G, int m0, int nm, int s0, int ns) {
+    if (p <= 0) return INT_MIN;
+    if (p >= G) return INT_MAX;
+    const int32_t *key = nm > 0 ? A.m_kp + m0 : A.s_kp + s0;
+    const int n = nm > 0 ? nm : ns;
+    if (n == 0) return INT_MIN;
+    int b = INT_MIN;
+    for (int q = 1; q <= p; ++q) b = max(b, (int)key[(int64_t)n * q / G]);
+    return b;
+}
+
+template <bool kLF>
+__global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseArgs A, int G, gu64 *xbuf, uint32_t salt,
+                                                              int32_t *err_word) {
+    constexpr int N = kLF ? 30 : 15;
+    constexpr int NJ = kLF ? 216 : 81;   // EdgeInertial Jacobian entries kept: 9 x 24 (LastFrame), 9 x 9 (columns 15-23)
+    constexpr int NI = kLF ? 24 : 9;
+    constexpr int NP = kLF ? 225 : 1;
+    const int f = blockIdx.x / G, g = blockIdx.x - f * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    gu64 *fb = xbuf + (size_t)f * kLatFrameGran;
+    extern __shared__ __attribute__((aligned(16))) char lat_dyn[];
+    const LatEdges E = lat_carve(lat_dyn);
+    __shared__ Rig rig;
+    __shared__ double sRwb[18], stwb[6], svel[6], sbg[6], sba[6];
+    __shared__ double sRcw[kMaxCams * 9], stcw[kMaxCams * 3];
+    __shared__ double red[4][kNormal], nrm[32];
+    __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N];
+    __shared__ double info9[81], infoG[9], infoA[9];
+    __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], HI[NI * NI], bI[NI];
+    __shared__ double cA1[9], cdV[3], cdP[3], eRc[9], erc[3], RJs[9], iJs[9];
+    __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1], HP[NP],
+        bP[kLF ? 15 : 1];
+    __shared__ double Am[NP], Vm[NP];
+    __shared__ uint32_t xsc[kLatMaxParts * kGran];
+    __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N];
+    __shared__ int k1s, k2s;
+    __shared__ double s_cnt[2];
+    const int C = rig_in.n_cams;
+    for (int q = tid; q < (int)(sizeof(Rig) / 4); q += kLatThreads)
+        reinterpret_cast<uint32_t *>(&rig)[q] = reinterpret_cast<const uint32_t *>(&rig_in)[q];
+    if (tid == 0) {
+        for (int q = 0; q < 9; ++q) sRwb[q] = A.kRwb[9 * f + q], sRwb[9 + q] = A.Rwb[9 * f + q];
+        for (int q = 0; q < 3; ++q) {
+            stwb[q] = A.ktwb[3 * f + q], stwb[3 + q] = A.twb[3 * f + q];
+            svel[q] = A.kvel[3 * f + q], svel[3 + q] = A.vel[3 * f + q];
+            sbg[q] = A.kbg[3 * f + q], sbg[3 + q] = A.bg[3 * f + q];
+            sba[q] = A.kba[3 * f + q], sba[3 + q] = A.ba[3 * f + q];
+        }
+        k1s = 0, k2s = 1;
+        s_count = 0, s_abort = 0;
+    }
+    if constexpr (kLF) {
+        for (int q = tid; q < 225; q += kLatThreads) pH[q] = A.pH[(size_t)f * 225 + q];
+        if (tid < 21) {
+            double v;
+            if (tid < 9) v = A.pRwb[9 * f + tid];
+            else if (tid < 12) v = A.ptwb[3 * f + tid - 9];
+            else if (tid < 15) v = A.pvel[3 * f + tid - 12];
+            else if (tid < 18) v = A.pbg[3 * f + tid - 15];
+            else v = A.pba[3 * f + tid - 18];
+            sPr[tid] = v;
+        }
+    }
+    for (int q = tid; q < C * 9; q += kLatThreads) sRcw[q] = A.Rcw[(size_t)f * C * 9 + q];
+    for (int q = tid; q < C * 3; q += kLatThreads) stcw[q] = A.tcw[(size_t)f * C * 3 + q];
+    for (int q = tid; q < N; q += kLatThreads) xs[q] = 0.0;
+    for (int q = tid; q < NJ; q += kLatThreads) J[q] = 0.0;
+    for (int q = tid; q < 99; q += kLatThreads) {
+        const double v = A.info[(size_t)f * 99 + q];
+        if (q < 81) info9[q] = v;
+        else if (q < 90) infoG[q - 81] = v;
+        else infoA[q - 90] = v;
+    }
+    const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0;
+    const int s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
+    const int ne = nm + ns;
+    const int lo = lat_bound(A, g, G, m0, nm, s0, ns), hi = lat_bound(A, g + 1, G, m0, nm, s0, ns);
+    __syncthreads();
+    bool fit = lat_select(A, false, m0, nm, lo, hi, E, &s_count, wcnt);
+    const int nm_loc = s_count;
+    if (fit) fit = lat_select(A, true, s0, ns, lo, hi, E, &s_count, wcnt);
+    const int nloc = s_count;
+    int phase = 1;
+    // setup exchange: every part learns whether some part overflowed its LDS edge capacity
+    if (wave == 0) {
+        if (!lat_exchange(fb, phase, salt, g, G, fit ? 0.0 : 1.0, 1, xsc, s_cnt, lane)) s_abort = 1;
+        else if (lane == 0 && s_cnt[0] != 0.0) s_abort = 2;
+    }
+    State st{sRwb, stwb, nullptr, nullptr, svel, sbg, sba, nullptr};
+    Imu imu{};
+    imu.n = 1, imu.kf1 = &k1s, imu.kf2 = &k2s, imu.pre = A.preint + (size_t)f * kPF;
+    // LastKeyFrame: the keyframe's vertices are fixed, so IMU::Preintegrated's bias-corrected deltas and dR^T Rbw1
+    // are constants of the call (imu_error computes them the same way at every iteration)
+    if (!kLF && wave == 4 && lane == 0) {
+        const float *p = imu.pre;
+        float b1[6];
+        for (int q = 0; q < 3; ++q) b1[q] = (float)sba[q], b1[3 + q] = (float)sbg[q];
+        double dR[9], dRt[9], R1t[9];
+        delta_rot(p, b1, dR);
+        delta_vp(p, PreView::dV, PreView::JVg, PreView::JVa, b1, cdV);
+        delta_vp(p, PreView::dP, PreView::JPg, PreView::JPa, b1, cdP);
+        tr3(sRwb, R1t);
+        tr3(dR, dRt);
+        mm3(dRt, R1t, cA1);
+        for (int r = 0; r < 3; ++r)   // EdgeInertial d(e_v)/d(v2) = Rbw1, constant here
+            for (int c = 0; c < 3; ++c) J[(3 + r) * 9 + 6 + c] = R1t[3 * r + c];
+    }
+    // EdgeInertial's Jacobian / error at the current state on wave 4 (J, e9, WJ = Info J; with `sys` also om9 and
+    // HI = J^T Info J, bI = J^T om9), the arithmetic of imu_error + imu_jacobian / imu_error_jac_p2v2
+    auto inertial_wave = [&](bool sys) __attribute__((always_inline)) {
+        if constexpr (!kLF) {
+            const double *R1 = sRwb, *R2 = sRwb + 9;
+            const double dt = (double)imu.pre[PreView::dT];
+            const double gz[3] = {0, 0, -(double)9.81f};
+            if (lane == 0) {   // LogSO3(dR^T Rbw1 Rwb2), InverseRightJacobianSO3 of it
+                double B[9], er[3], iJ[9];
+                mm3(cA1, R2, B);
+                log_so3(B, er);
+                for (int q = 0; q < 3; ++q) e9[q] = er[q];
+                inv_right_jac(er, iJ);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) J[r * 9 + c] = iJ[3 * r + c];
+            } else if (lane == 1) {
+                double t[3], ev[3];
+                for (int q = 0; q < 3; ++q) t[q] = svel[3 + q] - svel[q] - gz[q] * dt;
+                mtv3(R1, t, ev);
+                for (int q = 0; q < 3; ++q) e9[3 + q] = ev[q] - cdV[q];
+            } else if (lane == 2) {
+                double t[3], ev[3];
+                for (int q = 0; q < 3; ++q) t[q] = stwb[3 + q] - stwb[q] - svel[q] * dt - gz[q] * dt * dt / 2;
+                mtv3(R1, t, ev);
+                for (int q = 0; q < 3; ++q) e9[6 + q] = ev[q] - cdP[q];
+            } else if (lane == 3) {   // Rbw1 Rwb2
+                double R1t[9], Aq[9];
+                tr3(R1, R1t);
+                mm3(R1t, R2, Aq);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) J[(6 + r) * 9 + 3 + c] = Aq[3 * r + c];
+            }
+        } else {
+            if (lane == 0) {   // imu_error, keeping dR^T Rbw1 Rwb2 and its log for the Jacobian
+                double e[9], eR[9];
+                imu_error(st, imu, 0, e, eR);
+                for (int q = 0; q < 9; ++q) e9[q] = e[q], eRc[q] = eR[q];
+                for (int q = 0; q < 3; ++q) erc[q] = e[q];
+            }
+            for (int q = lane; q < 216; q += 64) J[q] = 0.0;
+            wave_lds_sync();
+            imu_jacobian_wave(st, imu, eRc, erc, J, RJs, iJs, lane);
+        }
+        wave_lds_sync();
+        for (int q = lane; q < NJ + 9; q += 64) {
+            if (q < NJ) {
+                const int r = q / NI, c = q - (q / NI) * NI;
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * J[k * NI + c];
+                WJ[q] = t;
+            } else if (sys) {
+                const int r = q - NJ;
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += info9[r * 9 + k] * e9[k];
+                om9[r] = -t;
+            }
+        }
+        if (!sys) return;
+        wave_lds_sync();
+        for (int q = lane; q < NI * NI + NI; q += 64) {
+            if (q < NI * NI) {
+                const int i = q / NI, j = q - (q / NI) * NI;
+                double t = 0;
+                for (int k = 0; k < 9; ++k) t += J[k * NI + i] * WJ[k * NI + j];
+                HI[q] = t;
+            } else {
+                const int i = q - NI * NI;
+                double u = 0;
+                for (int k = 0; k < 9; ++k) u += J[k * NI + i] * om9[k];
+                bI[i] = u;
+            }
+        }
+    };
+    // EdgePriorPoseImu (LastFrame) on wave 5: eP, JPr, PJ = H_prior JPr; with `sys` OeP, the Huber weight and
+    // HP = JPr^T w PJ, bP = -JPr^T w H_prior eP
+    auto prior_wave = [&](bool sys) __attribute__((always_inline)) {
+        if constexpr (kLF) {
+            if (lane == 0) prior_error_jac(sPr, sRwb, stwb, svel, sbg, sba, eP, JPr);
+            wave_lds_sync();
+            for (int q = lane; q < 240; q += 64) {
+                if (q < 225) {
+                    const int k = q / 15, j = q % 15;
+                    double t = 0;
+                    for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * JPr[l * 15 + j];
+                    PJ[q] = t;
+                } else if (sys) {
+                    const int k = q - 225;
+                    double t = 0;
+                    for (int l = 0; l < 15; ++l) t += pH[k * 15 + l] * eP[l];
+                    OeP[k] = t;
+                }
+            }
+            if (!sys) return;
+            wave_lds_sync();
+            double chi2p = 0, r0, w1p;
+            for (int k = 0; k < 15; ++k) chi2p += eP[k] * OeP[k];
+            huber(chi2p, 5.0, 25.0, r0, w1p);
+            for (int q = lane; q < 240; q += 64) {
+                if (q < 225) {
+                    const int i = q / 15, j = q % 15;
+                    double t = 0;
+                    for (int k = 0; k < 15; ++k) t += JPr[k * 15 + i] * (w1p * PJ[k * 15 + j]);
+                    HP[q] = t;
+                } else {
+                    const int i = q - 225;
+                    double u = 0;
+                    for (int k = 0; k < 15; ++k) u += JPr[k * 15 + i] * (-OeP[k] * w1p);
+                    bP[i] = u;
+                }
+            }
+        }
+    };
+    __syncthreads();
+    if (s_abort) goto fail;
+    {
+        const double dmono = (double)(float)sqrt(5.991), dst = (double)(float)sqrt(7.815);
+        const float chi2Mono[4] = {kLF ? 5.991f : 12.f, kLF ? 5.991f : 7.5f, 5.991f, 5.991f};   // :5992 / :5432
+        const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
+        double nBad = 0, nIn = 0;
+        for (int it = 0; it < 4; ++it) {
+            const bool robust = it < 3;   // setRobustKernel(0) after the third classification
+            for (int gi = 0; gi < 10; ++gi) {
+                ++phase;
+                if (wave < 4) {   // computeActiveErrors + the visual part of buildSystem
+                    double acc[kNormal];
+#pragma unroll
+                    for (int q = 0; q < kNormal; ++q) acc[q] = 0;
+                    for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+                        if (!(E.fl[q] & 4)) continue;
+                        const VEdge v = lat_edge(E, q);
+                        double r[3], Xc[3], JP[18];
+                        const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+                        E.c2[q] = c2;
+                        double w1 = 1.0;
+                        if (robust) {
+                            double r0;
+                            if (v.stereo) huber(c2, dst, dst * dst, r0, w1);
+                            else huber(c2, dmono, dmono * dmono, r0, w1);
+                        }
+                        edge_jac(rig, v, Xc, JP);
+                        const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, v.stereo ? -v.w * r[2] * w1 : 0.0};
+                        edge_normal(JP, v.stereo, v.w * w1, om, acc);
+                    }
+                    const double mine = wave_transpose_sum(acc, lane);
+                    if (lane < kNormal) red[wave][lane] = mine;
+                } else if (wave == 4) {   // EdgeInertial at the iteration's state
+                    inertial_wave(true);
+                } else if (kLF && wave == 5) {   // EdgePriorPoseImu on the previous frame (vertex 0)
+                    prior_wave(true);
+                }
+                __syncthreads();
+                if (wave == 0) {
+                    const double v = lane < kNormal ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                    if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
+                }
+                __syncthreads();
+                if (s_abort) goto fail;
+                // the system in the oracle's per-element order (visual, inertial, random walks, prior)
+                for (int q = tid; q < N * N; q += kLatThreads) {
+                    const int i = q / N, j = q - (q / N) * N;
+                    if (j > i) continue;
+                    double h = 0;
+                    if constexpr (kLF) {
+                        if (i < 6) h = nrm[j * 6 - j * (j - 1) / 2 + (i - j)];
+                        const int ci = ei_col(i), cj = ei_col(j);
+                        if (ci >= 0 && cj >= 0) h += HI[ci * 24 + cj];
+                        h += rw_entry(i, j, false, infoG);
+                        h += rw_entry(i, j, true, infoA);
+                        if (i >= 15 && j >= 15) h += HP[(i - 15) * 15 + j - 15];
+                    } else {
+                        if (i < 6) h = nrm[j * 6 - j * (j - 1) / 2 + (i - j)];
+                        if (i < 9) h += HI[i * 9 + j];
+                        if (j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+                    }
+                    Hs[i * N + j] = h;
+                    Hs[j * N + i] = h;
+                }
+                if (tid < N) {
+                    const int i = tid;
+                    double t = i < 6 ? nrm[21 + i] : 0.0;
+                    if constexpr (kLF) {
+                        const int ci = ei_col(i);
+                        if (ci >= 0) t += bI[ci];
+                        const int bi = i % 15;
+                        if (bi >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b_frame - b_prev, J_frame = I, J_prev = -I
+                            const bool acc_rw = bi >= 12;
+                            const int r = (bi - 9) % 3;
+                            const double *Iw = acc_rw ? infoA : infoG;
+                            const double *bv = acc_rw ? sba : sbg;
+                            double ee[3];
+                            for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
+                            const double oe = Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                            t += i < 15 ? -oe : oe;
+                        }
+                        if (i >= 15) t += bP[i - 15];
+                    } else {
+                        if (i < 9) t += bI[i];
+                        if (i >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b - b_kf, J = I
+                            const bool acc_rw = i >= 12;
+                            const int r = (i - 9) % 3;
+                            const double *Iw = acc_rw ? infoA : infoG;
+                            const double *bv = acc_rw ? sba : sbg;
+                            double ee[3];
+                            for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
+                            t -= Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
+                        }
+                    }
+                    bs[i] = t;
+                }
+                __syncthreads();
+                if (wave == 0) {
+                    const bool ok = ldlt_pick_solve<N>(Hs, bs, xt, pick, Lm, lane);
+                    if (ok && lane < N) xs[lane] = xt[lane];   // a failed solve leaves the previous x in place
+                    if (lane == 0) s_ok = ok ? 1 : 0;
+                    wave_lds_sync();
+                    // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235): lane 0 the frame, lane 1 the
+                    // previous frame (LastFrame); then lane c the frame's camera c
+                    if (lane == 0 || (kLF && lane == 1)) {
+                        const int v = lane == 0 ? 1 : 0;
+                        const double *xv = xs + (lane == 0 ? 0 : 15);
+                        double *Rw = sRwb + 9 * v, *tw = stwb + 3 * v;
+                        double t[3], dR[9], Rn[9];
+                        mv3(Rw, xv + 3, t);
+                        for (int q = 0; q < 3; ++q) tw[q] += t[q];
+                        exp_so3(xv, dR);
+                        mm3(Rw, dR, Rn);
+                        for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
+                        for (int q = 0; q < 3; ++q)
+                            svel[3 * v + q] += xv[6 + q], sbg[3 * v + q] += xv[9 + q], sba[3 * v + q] += xv[12 + q];
+                    }
+                    wave_lds_sync();
+                    if (lane < C) {
+                        const int c = lane;
+                        double Rbw[9], tbw[3], Rc[9], tc[3];
+                        tr3(sRwb + 9, Rbw);
+                        mv3(Rbw, stwb + 3, tbw);
+                        for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
+                        mm3(rig.Rcb[c], Rbw, Rc);
+                        mv3(rig.Rcb[c], tbw, tc);
+                        for (int q = 0; q < 9; ++q) sRcw[9 * c + q] = Rc[q];
+                        for (int q = 0; q < 3; ++q) stcw[3 * c + q] = tc[q] + rig.tcb[c][q];
+                    }
+                }
+                __syncthreads();
+                if (!s_ok) break;   // optimize() stops after a failed iteration
+            }
+            // classification (:5436-5490): the mono pass, then the stereo pass; counts summed over the parts
+            double bad = 0, in = 0;
+            const float chi2close = 1.5f * chi2Mono[it];
+            for (int pass = 0; pass < 2; ++pass) {
+                if (wave < 4)
+                    for (int q = (pass ? nm_loc : 0) + tid; q < (pass ? nloc : nm_loc); q += kLatEdgeThreads) {
+                        const VEdge v = lat_edge(E, q);
+                        double Xc[3];
+                        if (E.kpo[v.kp]) {   // outliers of the last round: computeError at the current state
+                            double r[3];
+                            E.c2[q] = edge_error(rig, sRcw, stcw, v, r, Xc);
+                        }
+                        const float chi2 = (float)E.c2[q];
+                        bool out;
+                        if (!v.stereo) {
+                            const bool close = (E.fl[q] & 2) != 0;
+                            const double *R = sRcw + 9 * v.cam;
+                            const bool depth_pos =
+                                (R[6] * v.X[0] + R[7] * v.X[1] + R[8] * v.X[2] + stcw[3 * v.cam + 2]) > 0.0;
+                            out = (chi2 > chi2Mono[it] && !close) || (close && chi2 > chi2close) || !depth_pos;
+                        } else {
+                            out = chi2 > chi2Stereo[it];
+                        }
+                        E.kpo[v.kp] = out ? 1 : 0;
+                        E.fl[q] = (uint8_t)((E.fl[q] & 3) | (out ? 0 : 4));
+                        bad += out ? 1 : 0;
+                        in += out ? 0 : 1;
+                    }
+                __syncthreads();
+            }
+            {
+                double cnt2[2] = {bad, in};
+                const double sb = wave < 4 ? wave_transpose_sum(cnt2, lane) : 0.0;
+                if (wave < 4 && lane < 2) red[wave][lane] = sb;
+                __syncthreads();
+                ++phase;
+                if (wave == 0) {
+                    const double v = lane < 2 ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                    if (!lat_exchange(fb, phase, salt, g, G, v, 2, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
+                }
+                __syncthreads();
+                if (s_abort) goto fail;
+                nBad = s_cnt[0], nIn = s_cnt[1];
+            }
+            if (ne + (kLF ? 4 : 3) < 10) break;   // optimizer.edges().size() < 10
+        }
+        if (nIn < 30 && !A.rec_init) {   // recover not too bad points (:5503-5526)
+            double bad = 0;
+            if (wave < 4)
+                for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+                    const VEdge v = lat_edge(E, q);
+                    double r[3], Xc[3];
+                    const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+                    E.c2[q] = c2;
+                    if (c2 < (v.stereo ? 24.f : 18.f)) E.kpo[v.kp] = 0;
+                    else bad += 1;
+                }
+            double cnt1[1] = {bad};
+            const double sb = wave < 4 ? wave_transpose_sum(cnt1, lane) : 0.0;
+            if (wave < 4 && lane == 0) red[wave][0] = sb;
+            __syncthreads();
+            ++phase;
+            if (wave == 0) {
+                const double v = lane < 1 ? ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0] : 0.0;
+                if (!lat_exchange(fb, phase, salt, g, G, v, 1, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
+            }
+            __syncthreads();
+            if (s_abort) goto fail;
+            nBad = s_cnt[0];
+        }
+        // mvbOutlier of this part's keypoints
+        if (wave < 4)
+            for (int q = tid; q < nloc; q += kLatEdgeThreads) A.kp_out[(size_t)f * A.kp_cap + E.kp[q]] = E.kpo[E.kp[q]];
+        if (A.H) {
+            // the Hessian without robust weights at the final state (inlier visual edges): visual sums exchanged,
+            // EdgeInertial / EdgePriorPoseImu linearised by waves 4 / 5, the matrix formed by part 0
+            if (wave < 4) {
+                double acc[kNormal];
+#pragma unroll
+                for (int q = 0; q < kNormal; ++q) acc[q] = 0;
+                for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+                    const VEdge v = lat_edge(E, q);
+                    if (E.kpo[v.kp]) continue;
+                    double r[3], Xc[3], JP[18];
+                    edge_error(rig, sRcw, stcw, v, r, Xc);
+                    edge_jac(rig, v, Xc, JP);
+                    const double om[3] = {0, 0, 0};
+                    edge_normal(JP, v.stereo, v.w, om, acc);
+                }
+                const double mine = wave_transpose_sum(acc, lane);
+                if (lane < kNormal) red[wave][lane] = mine;
+            } else if (wave == 4) {
+                inertial_wave(false);
+            } else if (kLF && wave == 5) {
+                prior_wave(false);
+            }
+            __syncthreads();
+            ++phase;
+            if (wave == 0) {
+                const double v = lane < kNormal ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
+            }
+            __syncthreads();
+            if (s_abort) goto fail;
+            if (g == 0) {
+                if constexpr (kLF) {
+                    for (int q = tid; q < N * N; q += kLatThreads) {   // the reference's order: ei, egr, ear, ep, visual
+                        const int i = q / N, j = q % N;
+                        double h = 0;
+                        const int ci = ei_col(i), cj = ei_col(j);
+                        if (ci >= 0 && cj >= 0) {
+                            double t = 0;
+                            for (int k = 0; k < 9; ++k) t += J[k * 24 + ci] * WJ[k * 24 + cj];
+                            h += t;
+                        }
+                        h += rw_entry(i, j, false, infoG);
+                        h += rw_entry(i, j, true, infoA);
+                        if (i >= 15 && j >= 15) {
+                            double t = 0;
+                            for (int k = 0; k < 15; ++k) t += JPr[k * 15 + i - 15] * PJ[k * 15 + j - 15];
+                            h += t;
+                        }
+                        if (i < 6 && j < 6) {
+                            const int a = min(i, j), b = max(i, j);
+                            h += nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+                        }
+                        Hs[q] = h;
+                    }
+                    __syncthreads();
+                    // Marginalize(H, 0, 14) (:3388-3455) of the previous frame: H_ff - H_fp pinv(H_pp) H_pf
+                    for (int q = tid; q < 225; q += kLatThreads) Am[q] = Hs[(15 + q / 15) * N + 15 + q % 15];
+                    __syncthreads();
+                    if (wave == 0) sym_eig_wave<15>(Am, Vm, lane);
+                    __syncthreads();
+                    for (int q = tid; q < 225; q += kLatThreads) {   // pinv(H_pp) -> PJ
+                        const int r = q / 15, c = q % 15;
+                        double s = 0;
+                        for (int k = 0; k < 15; ++k) {
+                            const double w = Am[k * 16];
+                            s += Vm[r * 15 + k] * (fabs(w) > 1e-6 ? 1.0 / w : 0.0) * Vm[c * 15 + k];
+                        }
+                        PJ[q] = s;
+                    }
+                    __syncthreads();
+                    for (int q = tid; q < 225; q += kLatThreads) {   // T = H_fp pinv(H_pp) -> JPr
+                        const int i = q / 15, j = q % 15;
+                        double s = 0;
+                        for (int k = 0; k < 15; ++k) s += Hs[i * N + 15 + k] * PJ[k * 15 + j];
+                        JPr[q] = s;
+                    }
+                    __syncthreads();
+                    for (int q = tid; q < 225; q += kLatThreads) {
+                        const int i = q / 15, j = q % 15;
+                        double s = 0;
+                        for (int k = 0; k < 15; ++k) s += JPr[i * 15 + k] * Hs[(15 + k) * N + j];
+                        A.H[(size_t)f * 225 + q] = Hs[i * N + j] - s;
+                    }
+                } else {
+                    for (int q = tid; q < 225; q += kLatThreads) {
+                        const int i = q / 15, j = q % 15;
+                        double h = 0;
+                        if (i < 6 && j < 6) {
+                            const int a = min(i, j), b = max(i, j);
+                            h = nrm[a * 6 - a * (a - 1) / 2 + (b - a)];
+                        }
+                        if (i < 9 && j < 9) {
+                            double t = 0;
+                            for (int k = 0; k < 9; ++k) t += J[k * 9 + i] * WJ[k * 9 + j];
+                            h += t;
+                        }
+                        if (i >= 9 && j >= 9 && (i < 12) == (j < 12))
+                            h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+                        A.H[(size_t)f * 225 + q] = h;
+                    }
+                }
+            }
+        }
+        if (g == 0) {   // state back
+            if (tid == 0) {
+                for (int q = 0; q < 9; ++q) A.Rwb[9 * f + q] = sRwb[9 + q];
+                for (int q = 0; q < 3; ++q) {
+                    A.twb[3 * f + q] = stwb[3 + q], A.vel[3 * f + q] = svel[3 + q];
+                    A.bg[3 * f + q] = sbg[3 + q], A.ba[3 * f + q] = sba[3 + q];
+                }
+                A.n_good[f] = ne - (int)nBad;
+            }
+            for (int q = tid; q < C * 9; q += kLatThreads) A.Rcw[(size_t)f * C * 9 + q] = sRcw[q];
+            for (int q = tid; q < C * 3; q += kLatThreads) A.tcw[(size_t)f * C * 3 + q] = stcw[q];
+        }
+        return;
+    }
+fail:
+    // a part overflowed its LDS edge capacity (s_abort 2) or a sibling workgroup never arrived (1): the frame is
+    // reported (n_good -1, OMV_ERR_CAPACITY in the handle's error word) and left unoptimised
+    if (tid == 0) {
+        if (g == 0) A.n_good[f] = -1;
+        atomicOr(err_word, s_abort == 2 ? OMV_ERR_CAPACITY : OMV_ERR_HIP);
+    }
+}
+
 }  // namespace
 
 struct omv_pose {
@@ -717,6 +1608,12 @@ struct omv_pose {
     double *chi2 = nullptr;   // [2][max_edges]
     uint8_t *act = nullptr;   // [2][max_edges]
     double *info = nullptr;   // [max_frames][99]
+    // grouped (latency) path: per frame two slots x kLatMaxParts x kGran exchange granules, the call's tag salt,
+    // the device error word, the path policy (OMV_POSE_AUTO / _BATCH / _GROUPED) and the parts per frame (0: auto)
+    unsigned long long *xbuf = nullptr;
+    uint32_t call = 0;
+    int32_t *err = nullptr;
+    int mode = OMV_POSE_AUTO, parts = 0;
 };
 
 extern "C" {
@@ -728,10 +1625,16 @@ omv_status omv_pose_create(int max_frames, int max_edges, omv_pose **out) {
     omv_pose *h = new omv_pose();
     h->max_frames = max_frames, h->max_edges = max_edges;
     const size_t n = 2 * (size_t)std::max(1, max_edges);
+    const size_t xb = (size_t)max_frames * kLatFrameGran * sizeof(unsigned long long);
     if (hipMalloc(&h->chi2, n * sizeof(double)) != hipSuccess || hipMalloc(&h->act, n) != hipSuccess ||
-        hipMalloc(&h->info, (size_t)max_frames * 99 * sizeof(double)) != hipSuccess) {
+        hipMalloc(&h->info, (size_t)max_frames * 99 * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->xbuf, xb) != hipSuccess || hipMemset(h->xbuf, 0, xb) != hipSuccess ||
+        hipMalloc(&h->err, sizeof(int32_t)) != hipSuccess || hipMemset(h->err, 0, sizeof(int32_t)) != hipSuccess) {
         (void)hipFree(h->chi2);
         (void)hipFree(h->act);
+        (void)hipFree(h->info);
+        (void)hipFree(h->xbuf);
+        (void)hipFree(h->err);
         delete h;
         return OMV_ERR_HIP;
     }
@@ -744,7 +1647,24 @@ omv_status omv_pose_destroy(omv_pose *h) {
     (void)hipFree(h->chi2);
     (void)hipFree(h->act);
     (void)hipFree(h->info);
+    (void)hipFree(h->xbuf);
+    (void)hipFree(h->err);
     delete h;
+    return OMV_OK;
+}
+
+omv_status omv_pose_set_mode(omv_pose *h, int mode, int parts) {
+    if (!h || mode < OMV_POSE_AUTO || mode > OMV_POSE_GROUPED || parts < 0 || parts > kLatMaxParts) return OMV_ERR_ARG;
+    h->mode = mode, h->parts = parts;
+    return OMV_OK;
+}
+
+omv_status omv_pose_last_error(omv_pose *h, int32_t *err, void *stream) {
+    if (!h || !err) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    HIP_OK(hipMemcpyAsync(err, h->err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemsetAsync(h->err, 0, sizeof(int32_t), st));
+    HIP_OK(hipStreamSynchronize(st));
     return OMV_OK;
 }
 
@@ -782,11 +1702,37 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     if (prior) {
         A.pRwb = prior->Rwb, A.ptwb = prior->twb, A.pvel = prior->vel, A.pbg = prior->bg, A.pba = prior->ba;
         A.pH = prior->H;
-        pose_info_kernel<<<b->n_frames, 64, 0, st>>>(b->preint, prior->preint_kf, h->info);
-        pose_opt_kernel<true><<<b->n_frames, kPoseThreads, 0, st>>>(rig, A);
+    }
+    // Path: the grouped kernel (G workgroups per frame, latency) for a few frames, the one-workgroup-per-frame kernel
+    // for batches.  G from the mean edge count: one visual edge per edge-wave thread.
+    const int F = b->n_frames;
+    const long long ne_tot = (long long)b->n_mono + b->n_stereo;
+    const bool grouped_ok = b->kp_cap <= kLatFlagCap;
+    bool grouped = h->mode == OMV_POSE_GROUPED || (h->mode == OMV_POSE_AUTO && F <= kLatAutoFrames && grouped_ok);
+    if (h->mode == OMV_POSE_GROUPED && !grouped_ok) return OMV_ERR_ARG;
+    int G = h->parts;
+    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + kLatEdgeThreads - 1) / kLatEdgeThreads));
+    pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
+    if (grouped) {
+        h->call = (h->call + 1) & 0xFFFFFu;
+        if (h->call == 0) {   // tags repeat after 2^20 calls: clear the granules once
+            HIP_OK(hipMemsetAsync(h->xbuf, 0, (size_t)h->max_frames * kLatFrameGran * sizeof(unsigned long long), st));
+            h->call = 1;
+        }
+        const uint32_t salt = h->call << 12;
+        const size_t lds = lat_lds_bytes(b->kp_cap);
+        gu64 *xb = (gu64 *)h->xbuf;
+        if (prior) {
+            HIP_OK(hipFuncSetAttribute((const void *)pose_lat_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            pose_lat_kernel<true><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
+        } else {
+            HIP_OK(hipFuncSetAttribute((const void *)pose_lat_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            pose_lat_kernel<false><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
+        }
+    } else if (prior) {
+        pose_opt_kernel<true><<<F, kPoseThreads, 0, st>>>(rig, A);
     } else {
-        pose_info_kernel<<<b->n_frames, 64, 0, st>>>(b->preint, b->preint, h->info);
-        pose_opt_kernel<false><<<b->n_frames, kPoseThreads, 0, st>>>(rig, A);
+        pose_opt_kernel<false><<<F, kPoseThreads, 0, st>>>(rig, A);
     }
     HIP_OK(hipGetLastError());
     return OMV_OK;

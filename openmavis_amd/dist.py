@@ -140,12 +140,18 @@ class CameraShard:
 class LbaAllReduce:
     """The omv_allreduce_fn of a landmark-sharded LocalInertialBA over torch.distributed.
 
-    mode "device" (backend nccl = RCCL): the handle's device buffer is staged through a torch tensor
-    on the handle's own HIP stream (torch.cuda.ExternalStream), so the copy, the ring all-reduce over
-    xGMI and the copy back stay ordered with the LM kernels and the host never waits.
-    mode "host" (backend gloo): the stream is drained and the buffer goes through host memory — the
+    mode "device" (backend nccl = RCCL): the handle's device buffer itself is all-reduced IN PLACE on the
+    handle's own HIP stream (torch.cuda.ExternalStream; the buffer is wrapped as a tensor through the CUDA array
+    interface, no copy), so the ring all-reduce over xGMI stays ordered with the LM kernels and the host never
+    waits.  mode "host" (backend gloo): the stream is drained and the buffer goes through host memory — the
     CPU-collective rehearsal of the same exchange (tests, a GPU box with one card).
+    `calls` counts the collectives issued.
     """
+
+    class _Dev:   # a device buffer seen through __cuda_array_interface__ (float64, contiguous)
+        def __init__(self, ptr, count):
+            self.__cuda_array_interface__ = {"shape": (int(count),), "typestr": "<f8", "data": (int(ptr), False),
+                                             "version": 2}
 
     def __init__(self, mode="device", group=None, device=None):
         import ctypes
@@ -159,6 +165,7 @@ class LbaAllReduce:
         self._hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
         self._buf = None
         self._torch = torch
+        self.calls = 0
 
     def _staging(self, n, device):
         t = self._torch
@@ -169,6 +176,7 @@ class LbaAllReduce:
     def __call__(self, ptr, count, stream):
         import torch.distributed as dist
         t = self._torch
+        self.calls += 1
         nbytes = int(count) * 8
         if self.mode == "host":
             buf = self._staging(count, "cpu")
@@ -183,10 +191,6 @@ class LbaAllReduce:
             self._hip.hipStreamSynchronize(stream)   # buf is reused by the next call
             return
         ext = t.cuda.ExternalStream(stream, device=self.device)
-        with t.cuda.stream(ext):
-            buf = self._staging(count, self.device or t.cuda.current_device())
-            if self._hip.hipMemcpyAsync(buf.data_ptr(), ptr, nbytes, 3, stream) != 0:   # D2D
-                raise RuntimeError("hipMemcpyAsync D2D")
-            dist.all_reduce(buf, group=self.group)   # ordered after the copy (current stream = ext)
-            if self._hip.hipMemcpyAsync(ptr, buf.data_ptr(), nbytes, 3, stream) != 0:
-                raise RuntimeError("hipMemcpyAsync D2D")
+        with t.cuda.device(self.device if self.device is not None else t.cuda.current_device()), t.cuda.stream(ext):
+            view = t.as_tensor(self._Dev(ptr, count), device="cuda")
+            dist.all_reduce(view, group=self.group)   # in place on the handle's buffer, ordered on its stream

@@ -47,9 +47,9 @@ class LocalInertialBA:
         self._s = None
         self._keep = None
         self._cb = None
-        if world > 1:
-            if allreduce is None:
-                raise ValueError("LocalInertialBA: world > 1 needs an allreduce")
+        if world > 1 and allreduce is None:
+            raise ValueError("LocalInertialBA: world > 1 needs an allreduce")
+        if allreduce is not None:   # a collective given: the sharded call sequence, also on one rank
 
             def _cb(_ctx, buf, count, stream):
                 try:
@@ -166,6 +166,22 @@ class PoseInertialOptimizer:
         if getattr(self, "_h", None):
             self._lib.omv_pose_destroy(self._h)
             self._h = None
+
+    AUTO, BATCH, GROUPED = 0, 1, 2
+
+    def set_mode(self, mode, parts=0):
+        """Kernel choice (omv_pose_set_mode): AUTO (grouped kernel up to 16 frames per call, else one workgroup per
+        frame), BATCH or GROUPED (`parts` workgroups per frame, 0 = one per 256 visual edges)."""
+        _lib.check(self._lib.omv_pose_set_mode(self._h, int(mode), int(parts)), "omv_pose_set_mode")
+        return self
+
+    def last_error(self, stream=None):
+        """Device error word since the last read (0, or OMV_ERR_CAPACITY / OMV_ERR_HIP from the grouped kernel)."""
+        import torch
+        e = ctypes.c_int32(0)
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(self._lib.omv_pose_last_error(self._h, ctypes.byref(e), ctypes.c_void_p(st)), "omv_pose_last_error")
+        return e.value
 
     def PoseInertialOptimizationLastKeyFrame(self, batch, arrays, kp_outlier, H=None, bRecInit=False, stream=None):
         import torch

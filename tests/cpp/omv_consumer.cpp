@@ -9,7 +9,8 @@
 //   omv_consumer lba   DIR   LocalInertialBAWindow: keyframes added in a mixed fixed / optimisable order,
 //                            EdgeMono + EdgeStereo observations, inertial edges under the reference's robust
 //                            rule (last edge / bRecInit), flattened optimisable-first, optimised, written back
-//                            (not on FAIL); optionally a smaller window first on the same adapter
+//                            (not on FAIL); optionally a smaller window first on the same adapter; with meta
+//                            rccl 1 on a one-rank RCCL communicator (omv_lba_set_comm + ncclAllReduce, §4b)
 //
 // DIR/meta.txt holds "key value" lines; arrays are DIR/<name>.bin in the dtype the test wrote.
 #include <cstdio>
@@ -20,9 +21,18 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "omv_adapters.hpp"
 
 namespace {
+
+// INTEGRATION.md §4b's collective: RCCL's in-place all-reduce on the handle's stream (counted)
+int g_allreduce_calls = 0;
+int nccl_sum(void *comm, double *buf, size_t n, void *stream) {
+    ++g_allreduce_calls;
+    return ncclAllReduce(buf, buf, n, ncclFloat64, ncclSum, (ncclComm_t)comm, (hipStream_t)stream) == ncclSuccess ? 0 : 1;
+}
 
 std::map<std::string, double> read_meta(const std::string &dir) {
     std::map<std::string, double> m;
@@ -142,6 +152,13 @@ int run_lba(const std::string &dir) {
     const auto model = read_opt<int32_t>(dir, "cam_model");
     omv_adapt::LocalInertialBAWindow win(C, read_bin<float>(dir, "cam"), read_bin<double>(dir, "Rcb"), read_bin<double>(dir, "tcb"),
                                          read_bin<double>(dir, "Rbc"), read_bin<double>(dir, "tbc"), (float)m["bf"], model);
+    ncclComm_t comm = nullptr;
+    if (m["rccl"] != 0) {   // a one-rank RCCL communicator: the landmark-sharded call sequence on this GPU
+        ncclUniqueId id;
+        if (ncclGetUniqueId(&id) != ncclSuccess || ncclCommInitRank(&comm, 1, id, 0) != ncclSuccess)
+            throw omv_adapt::Error("RCCL communicator");
+        win.set_comm(0, 1, nccl_sum, comm);
+    }
     std::vector<int> slot(K);   // original keyframe -> window index
     // the window with its first n_pts_use points and their edges (a smaller window first exercises the handle's
     // re-creation when the next window is larger)
@@ -199,8 +216,11 @@ int run_lba(const std::string &dir) {
     write_bin(dir, "out_stereo_chi2", schi2), write_bin(dir, "out_stereo_outlier", soutl);
     std::ofstream o(dir + "/result.txt");
     o.precision(17);
+    const auto hs = win.host_syncs();
     o << "err " << r.err << "\nerr_end " << r.err_end << "\nstatus " << r.status << "\niterations " << r.iterations
-      << "\ntrials " << r.trials << "\nlambda " << r.lambda << "\n";
+      << "\ntrials " << r.trials << "\nlambda " << r.lambda << "\nallreduce_calls " << g_allreduce_calls
+      << "\nhost_syncs " << hs.first << "\n";
+    if (comm) ncclCommDestroy(comm);
     return 0;
 }
 

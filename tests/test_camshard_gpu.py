@@ -41,6 +41,18 @@ def test_camera_sharded_frame_equals_batched(oracle, torch_cuda, tmp_path):
     backend = "nccl" if torch.cuda.device_count() >= 2 else "gloo"
     g = _run_ranks(tmp_path, backend)
     assert int(g["world"]) == 2
+    _check_against_batched(g, oracle, torch)
+
+
+def test_camera_shard_rccl_one_rank(oracle, torch_cuda, tmp_path):
+    """CameraShard(mode="device") under torch's nccl backend (RCCL) with one rank: the slab all-gather runs through
+    RCCL on the device (all five cameras on rank 0) and the gathered frame equals the batched path bit for bit."""
+    g = _run_ranks(tmp_path, "nccl", world=1)
+    assert int(g["world"]) == 1
+    _check_against_batched(g, oracle, torch_cuda)
+
+
+def _check_against_batched(g, oracle, torch):
     # the single-GPU batched path on the same frames
     imgs = np.concatenate([synth.hilti_frame(f) for f in range(F)])
     ex = ORBextractor(NF, 1.2, 8, 15, 7, width=W, height=H, max_images=F * C)

@@ -121,14 +121,14 @@ LBA_ARRAYS = ("cam", "Rcb", "tcb", "Rbc", "tbc", "kf_imu", "Rwb", "twb", "Rcw", 
 STEREO_ARRAYS = ("stereo_pt", "stereo_kf", "stereo_obs", "stereo_inv_sigma2")
 
 
-def _run_lba_window(d, prob, large=True, rec_init=False, warm_small=False):
+def _run_lba_window(d, prob, large=True, rec_init=False, warm_small=False, rccl=False):
     K, n_opt = prob["n_kf"], prob["n_opt"]
     # window insertion order: fixed and optimisable keyframes interleaved (relative order kept in each group,
     # so the flattened vertex order equals the problem's)
     fixed, opt = list(range(n_opt, K)), list(range(n_opt))
     order = np.array([x for pair in zip(fixed, opt) for x in pair] + fixed[len(opt):] + opt[len(fixed):], np.int32)
     _meta(d, n_cams=prob["n_cams"], n_kf=K, n_opt=n_opt, n_pts=len(prob["pts"]), large=int(large),
-          rec_init=int(rec_init), warm_small=int(warm_small), bf=float(prob.get("bf", 0.0)))
+          rec_init=int(rec_init), warm_small=int(warm_small), bf=float(prob.get("bf", 0.0)), rccl=int(rccl))
     _w(d, "kf_order", order)
     for k in LBA_ARRAYS + (STEREO_ARRAYS if prob.get("n_stereo", 0) else ()) + (("cam_model",) if "cam_model" in prob else ()):
         _w(d, k, prob[k])
@@ -183,3 +183,16 @@ def test_local_inertial_ba_window_fail_keeps_state(tmp_path):
     assert int(res["status"]) == 1   # OMV_LBA_FAIL
     for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts"):
         assert np.array_equal(st[k], np.asarray(prob[k], np.float64).ravel()), k
+
+
+def test_local_inertial_ba_window_rccl_single_rank(tmp_path, oracle):
+    """INTEGRATION.md §4b compiled: the window on a one-rank RCCL communicator (ncclGetUniqueId / ncclCommInitRank,
+    omv_lba_set_comm with an ncclAllReduce callback).  The landmark-sharded call sequence runs for real -- two in-place
+    all-reduces per LM step on the handle's stream, directly launched gated steps, one host wait per batch of steps --
+    and the outcome meets the same bar as the unsharded window."""
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=1500, seed=11)
+    res, st = _run_lba_window(tmp_path, prob, rccl=True)
+    _check_against_python(tmp_path, prob, res, st, oracle)
+    trials, calls, syncs = int(res["trials"]), int(res["allreduce_calls"]), int(res["host_syncs"])
+    assert calls >= 2 * trials, (calls, trials)   # [blocks | b | rhs] and [chi(A), chi, computeScale] per step
+    assert syncs <= (trials + 3) // 4 + 1 and (trials < 2 or syncs < trials), (syncs, trials)

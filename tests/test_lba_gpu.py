@@ -276,25 +276,28 @@ def test_bitwise_identical_run_to_run(full, driver):
             assert np.array_equal(np.asarray(s[k]).view(np.uint64), np.asarray(s0[k]).view(np.uint64)), k
 
 
-@pytest.mark.parametrize("backend,driver", [("gloo", "device"), ("gloo", "host"), ("nccl", "device")])
-def test_landmark_sharded_two_ranks(oracle, tmp_path, backend, driver):
-    """landmarks sharded over 2 ranks (gloo, both on this box's GPU), one all-reduce of the
-    partial Schur system and one of the LM scalars per step.  The merged outcome meets the same bar against the
-    oracle, and every rank holds the identical keyframe state (asserted inside the worker).  The device LM driver
-    waits on the host once per batch of steps, never per trial (omv_lba_host_syncs)."""
+@pytest.mark.parametrize("backend,driver,world", [("gloo", "device", 2), ("gloo", "host", 2), ("gloo", "device", 4),
+                                                  ("nccl", "device", 1), ("nccl", "device", 2)])
+def test_landmark_sharded_ranks(oracle, tmp_path, backend, driver, world):
+    """landmarks sharded over `world` ranks, one all-reduce of the partial Schur system and one of the LM
+    scalars per step.  gloo: the ranks share this box's GPU, collectives through host memory (2 and 4 ranks).  nccl:
+    RCCL on the handle's device buffer in place (LbaAllReduce "device") -- one rank on a one-GPU box runs the same
+    call sequence, more ranks need as many GPUs.  The merged outcome meets the same bar against the oracle, and every
+    rank holds the identical keyframe state (asserted inside the worker).  The device LM driver waits on the host
+    once per batch of steps, never per trial (omv_lba_host_syncs)."""
     import os
     import socket
     import subprocess
     import sys
     import torch
-    if backend == "nccl" and torch.cuda.device_count() < 2:
-        pytest.skip("RCCL device all-reduce needs 2 visible GPUs (the gloo case covers a 1-GPU box)")
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        pytest.skip(f"RCCL over {world} ranks needs {world} visible GPUs (one rank and the gloo cases run on one)")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = tmp_path / f"shard_{backend}.npz"
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tools", "lba_shard_run.py"),
            "--out", str(out), "--backend", backend, "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000",
            "--host-driver", "1" if driver == "host" else "0"]
@@ -303,13 +306,14 @@ def test_landmark_sharded_two_ranks(oracle, tmp_path, backend, driver):
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     g = dict(np.load(out))
     prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=3000, seed=11)
-    assert int(g["world"]) == 2 and (g["owner"] >= 0).all() and len(set(g["owner"].tolist())) == 2
+    assert int(g["world"]) == world and (g["owner"] >= 0).all() and len(set(g["owner"].tolist())) == world
     ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
     rg = {k: (g[k].item() if g[k].ndim == 0 else g[k]) for k in
           ("err", "err_end", "status", "iterations", "trials", "mono_chi2", "mono_outlier")}
     _compare_result(prob, rg, ro)
     _compare_state(prob, {k: g[k] for k in STATE}, so, oracle)
     trials, syncs = int(g["trials"]), int(g["host_syncs"])
+    assert int(g["ar_calls"]) >= 2 * trials, (int(g["ar_calls"]), trials)   # the collectives really ran
     if driver == "device":
         assert syncs <= (trials + 3) // 4 + 1 and (trials < 2 or syncs < trials), (syncs, trials)
     else:

@@ -16,7 +16,13 @@ from openmavis_amd.optimizer import PoseInertialOptimizer
 pytestmark = pytest.mark.gpu
 
 
-def _run_gpu(b, rec_init=False):
+# kernel paths: one workgroup per frame; the grouped (latency) kernel with its automatic part count, 3 parts, and 8
+# parts (parts with few or no edges)
+MODES = [(PoseInertialOptimizer.BATCH, 0), (PoseInertialOptimizer.GROUPED, 0), (PoseInertialOptimizer.GROUPED, 3),
+         (PoseInertialOptimizer.GROUPED, 8)]
+
+
+def _run_gpu(b, rec_init=False, mode=(PoseInertialOptimizer.AUTO, 0)):
     import torch
     dev = "cuda:0"
     arrays = {}
@@ -28,8 +34,10 @@ def _run_gpu(b, rec_init=False):
     kpo = torch.full((F, cap), 255, dtype=torch.uint8, device=dev)
     H = torch.zeros((F, 225), dtype=torch.float64, device=dev)
     opt = PoseInertialOptimizer(max_frames=F, max_edges=max(len(b["mono_cam"]), len(b["stereo_cam"]), 1))
+    opt.set_mode(*mode)
     n_good = opt.PoseInertialOptimizationLastKeyFrame(b, arrays, kpo, H, bRecInit=rec_init)
     torch.cuda.synchronize()
+    assert opt.last_error() == 0
     st = {k: arrays[k].cpu().numpy() for k in synth_pose.STATE_KEYS}
     return st, kpo.cpu().numpy(), n_good.cpu().numpy(), H.cpu().numpy()
 
@@ -48,6 +56,11 @@ def _compare(b, g, o):
     assert np.abs(H_g - H_o).max() <= 1e-6 * np.abs(H_o).max()
 
 
+def _check(b, o, rec_init=False):
+    for mode in MODES:
+        _compare(b, _run_gpu(b, rec_init, mode), o)
+
+
 @pytest.mark.parametrize("seed,outliers,stereo,pinhole",
                          [(1, 0.1, 0.0, False), (2, 0.25, 0.0, False), (4, 0.1, 0.5, False), (5, 0.1, 0.0, True),
                           (6, 0.1, 0.5, True)])
@@ -55,17 +68,42 @@ def test_pose_inertial_last_kf_matches_oracle(oracle, seed, outliers, stereo, pi
     """pinhole: a Pinhole rig (configs[3]'s camera model, Pinhole::project / projectJac in the edges)."""
     b = synth_pose.make_pose_batch(n_frames=12, n_pts=300, seed=seed, outlier_frac=outliers, stereo_frac=stereo,
                                    pinhole=pinhole)
-    _compare(b, _run_gpu(b), oracle.pose_last_kf(b))
+    _check(b, oracle.pose_last_kf(b))
 
 
 @pytest.mark.parametrize("rec_init", [False, True])
 def test_pose_few_inliers(oracle, rec_init):
     """< 30 inliers: the recover pass (or not, with bRecInit)."""
     b = synth_pose.make_pose_batch(n_frames=4, n_pts=40, seed=3, outlier_frac=0.5)
-    _compare(b, _run_gpu(b, rec_init), oracle.pose_last_kf(b, rec_init))
+    _check(b, oracle.pose_last_kf(b, rec_init), rec_init)
 
 
 def test_pose_tiny_frame(oracle):
     """Fewer than 10 edges in the graph: the reference stops after the first round."""
     b = synth_pose.make_pose_batch(n_frames=3, n_pts=5, seed=5, outlier_frac=0.0)
-    _compare(b, _run_gpu(b), oracle.pose_last_kf(b))
+    _check(b, oracle.pose_last_kf(b))
+
+
+def test_pose_single_frame(oracle):
+    """Tracking's call: ONE frame (1,000 matched keypoints, 30 % with a stereo edge on the same keypoint), every path."""
+    b = synth_pose.make_pose_batch(n_frames=1, n_pts=1000, seed=7, stereo_frac=0.3)
+    _check(b, oracle.pose_last_kf(b))
+
+
+def test_grouped_capacity_is_reported():
+    """More visual edges in one workgroup's keypoint range than its LDS holds: the frame is reported (n_good -1,
+    OMV_ERR_CAPACITY), never silently truncated."""
+    import torch
+    from openmavis_amd import _lib
+    b = synth_pose.make_pose_batch(n_frames=1, n_pts=1100, seed=8)
+    dev = "cuda:0"
+    arrays = {k: torch.tensor(np.asarray(b[k], np.float64), device=dev).contiguous() for k in synth_pose.STATE_KEYS}
+    for k in synth_pose.INPUT_KEYS:
+        arrays[k] = torch.from_numpy(np.ascontiguousarray(b[k])).to(dev)
+    kpo = torch.zeros((1, int(b["kp_cap"])), dtype=torch.uint8, device=dev)
+    opt = PoseInertialOptimizer(max_frames=1, max_edges=len(b["mono_cam"])).set_mode(PoseInertialOptimizer.GROUPED, 1)
+    n_good = opt.PoseInertialOptimizationLastKeyFrame(b, arrays, kpo)
+    torch.cuda.synchronize()
+    assert int(n_good.cpu()[0]) == -1
+    assert opt.last_error() == _lib.OMV_ERR_CAPACITY
+    assert opt.last_error() == 0   # read resets it

@@ -17,7 +17,13 @@ from openmavis_amd.optimizer import PoseInertialOptimizer
 pytestmark = pytest.mark.gpu
 
 
-def _run_gpu(b, rec_init=False):
+# kernel paths: one workgroup per frame; the grouped (latency) kernel with its automatic part count, 3 parts, and 8
+# parts (parts with few or no edges)
+MODES = [(PoseInertialOptimizer.BATCH, 0), (PoseInertialOptimizer.GROUPED, 0), (PoseInertialOptimizer.GROUPED, 3),
+         (PoseInertialOptimizer.GROUPED, 8)]
+
+
+def _run_gpu(b, rec_init=False, mode=(PoseInertialOptimizer.AUTO, 0)):
     import torch
     dev = "cuda:0"
     arrays = {}
@@ -29,8 +35,10 @@ def _run_gpu(b, rec_init=False):
     kpo = torch.full((F, cap), 255, dtype=torch.uint8, device=dev)
     H = torch.zeros((F, 225), dtype=torch.float64, device=dev)
     opt = PoseInertialOptimizer(max_frames=F, max_edges=max(len(b["mono_cam"]), len(b["stereo_cam"]), 1))
+    opt.set_mode(*mode)
     n_good = opt.PoseInertialOptimizationLastFrame(b, arrays, kpo, H, bRecInit=rec_init)
     torch.cuda.synchronize()
+    assert opt.last_error() == 0
     st = {k: arrays[k].cpu().numpy() for k in synth_pose.STATE_KEYS}
     return st, kpo.cpu().numpy(), n_good.cpu().numpy(), H.cpu().numpy()
 
@@ -49,25 +57,30 @@ def _compare(b, g, o):
         assert np.abs(H_g[f] - H_o[f]).max() <= 1e-6 * np.abs(H_o[f]).max(), f
 
 
+def _check(b, o, rec_init=False):
+    for mode in MODES:
+        _compare(b, _run_gpu(b, rec_init, mode), o)
+
+
 @pytest.mark.parametrize("seed,outliers,stereo,pinhole",
                          [(1, 0.1, 0.0, False), (2, 0.25, 0.0, False), (4, 0.1, 0.5, False), (5, 0.1, 0.0, True)])
 def test_pose_inertial_last_frame_matches_oracle(oracle, seed, outliers, stereo, pinhole):
     b = synth_pose.make_last_frame_batch(n_frames=12, n_pts=300, seed=seed, outlier_frac=outliers,
                                          stereo_frac=stereo, pinhole=pinhole)
-    _compare(b, _run_gpu(b), oracle.pose_last_frame(b))
+    _check(b, oracle.pose_last_frame(b))
 
 
 @pytest.mark.parametrize("rec_init", [False, True])
 def test_pose_last_frame_few_inliers(oracle, rec_init):
     """< 30 inliers: the recover pass (:6074-6098), or not with bRecInit."""
     b = synth_pose.make_last_frame_batch(n_frames=4, n_pts=40, seed=3, outlier_frac=0.5)
-    _compare(b, _run_gpu(b, rec_init), oracle.pose_last_frame(b, rec_init))
+    _check(b, oracle.pose_last_frame(b, rec_init), rec_init)
 
 
 def test_pose_last_frame_tiny_frame(oracle):
     """Fewer than 10 edges in the graph (5 visual + 4): the reference stops after the first round."""
     b = synth_pose.make_last_frame_batch(n_frames=3, n_pts=5, seed=5, outlier_frac=0.0)
-    _compare(b, _run_gpu(b), oracle.pose_last_frame(b))
+    _check(b, oracle.pose_last_frame(b))
 
 
 def test_constraint_pose_imu_matches_oracle(oracle):
@@ -90,3 +103,9 @@ def test_constraint_pose_imu_matches_oracle(oracle):
     PoseInertialOptimizer.ConstraintPoseImu(t, out=t)
     torch.cuda.synchronize()
     assert np.abs(t.cpu().numpy() - g).max() == 0
+
+
+def test_pose_last_frame_single_frame(oracle):
+    """Tracking's call: ONE frame (1,000 matched keypoints, 30 % with a stereo edge on the same keypoint), every path."""
+    b = synth_pose.make_last_frame_batch(n_frames=1, n_pts=1000, seed=7, stereo_frac=0.3)
+    _check(b, oracle.pose_last_frame(b))

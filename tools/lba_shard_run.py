@@ -59,7 +59,8 @@ def main():
     part = dict(rank=rank, idx=idx, pts=st["pts"][idx], edges=np.nonzero(mine)[0],
                 chi2=res["mono_chi2"][mine], outl=res["mono_outlier"][mine],
                 kf={k: st[k] for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba")},
-                scal={k: res[k] for k in ("err", "err_end", "status", "iterations", "trials")}, syncs=syncs)
+                scal={k: res[k] for k in ("err", "err_end", "status", "iterations", "trials")}, syncs=syncs,
+                ar_calls=ar.calls)
     parts = [None] * world
     dist.all_gather_object(parts, part)
     if rank == 0:
@@ -78,7 +79,7 @@ def main():
                 assert np.array_equal(v, parts[0]["kf"][k]), ("keyframe state differs across ranks", k)
             assert q["scal"] == parts[0]["scal"], "LM outcome differs across ranks"
         out = dict(pts=pts, mono_chi2=chi2, mono_outlier=outl, owner=owner, world=world,
-                   host_syncs=max(q["syncs"] for q in parts),
+                   host_syncs=max(q["syncs"] for q in parts), ar_calls=min(q["ar_calls"] for q in parts),
                    **{k: v for k, v in parts[0]["kf"].items()}, **parts[0]["scal"])
         np.savez(args.out, **out)
         print(f"lba shard ok: world {world}, trials {out['trials']}, err {out['err']:.6g} -> {out['err_end']:.6g}")
