@@ -13,6 +13,15 @@
 //   LocalInertialBAWindow   Optimizer::LocalInertialBA's graph flattening (src/Optimizer.cc:2740-3267): key
 //                           frames (optimisable first, as the reference creates its vertices), points, EdgeMono
 //                           and inertial edges in creation order -> omv_lba_problem -> optimize -> write-back
+//   SearchByProjectionLastFrame  ORBmatcher::SearchByProjection(Frame&, const Frame& LastFrame, th, bMono)
+//                           (src/ORBmatcher.cc:1985-2413) on a MultiCameraFrame
+//   SearchForTriangulation  ORBmatcher::SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse)
+//                           (src/ORBmatcher.cc:1131-1456, called at LocalMapping.cc:468)
+//   PoseInertialOptimizer   Optimizer::PoseInertialOptimizationLastKeyFrame / LastFrame (src/Optimizer.cc:5021,
+//                           :5580) on ONE frame (Tracking's call): state, mvbOutlier, return value, the Hessian
+//                           of the ConstraintPoseImu
+//   Fuse                    ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID) (src/ORBmatcher.cc:1458-1647,
+//                           called 4x per camera at LocalMapping.cc:845-888): the chosen keypoint per point
 //
 // Errors: every omv_status != OMV_OK throws omv_adapt::Error (the adapters' callers are C++).
 #ifndef OMV_ADAPTERS_HPP
@@ -22,6 +31,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -187,8 +197,14 @@ class MultiCameraFrame {
     int n_cams() const { return C_; }
     int kp_cap() const { return cap_; }
 
+    // GeometricCamera type per camera block (OMV_CAM_KB8 default / OMV_CAM_PINHOLE)
+    void set_camera_models(const std::vector<int32_t> &models) {
+        for (int c = 0; c < C_ && c < 8; ++c) geom_.cam_model[c] = c < (int)models.size() ? models[c] : OMV_CAM_KB8;
+    }
+
   private:
     friend class SearchByProjection;
+    friend class SearchByProjectionLastFrame;
     int C_, W_, H_, cap_ = 0;
     std::vector<int> lap_;
     std::vector<float> scale_;
@@ -253,6 +269,413 @@ class SearchByProjection {
 };
 
 // ---- Optimizer::LocalInertialBA -----------------------------------------------------------------------------
+// ---- ORBmatcher::SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, th, bMono) --------------------
+// The LastFrame fields the reference reads, one slot per LastFrame keypoint s = cam * last_cap + i.
+struct LastFrameView {
+    int last_cap = 0;                                // keypoint slots per camera block
+    std::vector<float> pos;                          // [S][3] mvpMapPoints[s]->GetWorldPos()
+    std::vector<uint8_t> desc;                       // [S][32] GetDescriptor()
+    std::vector<uint8_t> valid;                      // [S] mvpMapPoints[s] && !mvbOutlier[s]
+    std::vector<uint8_t> has_obs;                    // [S] Observations() > 0
+    std::vector<omv_kp> keys;                        // [S] LastFrame keypoint s (octave, angle)
+    omv_se3f Tcw{};                                  // LastFrame.GetPose() (block 0)
+};
+
+class SearchByProjectionLastFrame {
+  public:
+    SearchByProjectionLastFrame(float nnratio, bool checkOri) : nnratio_(nnratio), check_ori_(checkOri) {}
+    // Returns nmatches; kp_to_mp [n_cams * kp_cap] in/out (CurrentFrame.mvpMapPoints as LastFrame slots, -1 NULL).
+    // cams [n_cams][8] (block 0's model = CurrentFrame.mpCamera), Tcw the current pose, Trl block 1 from block 0,
+    // mb = CurrentFrame.mb; occupied_init: keypoints already holding a point with observations.
+    int operator()(MultiCameraFrame &F, const LastFrameView &last, const omv_se3f &Tcw, const omv_se3f &Trl,
+                   const std::vector<float> &cams, float th, bool bMono, float mb, std::vector<int32_t> &kp_to_mp,
+                   const std::vector<uint8_t> *occupied_init = nullptr) {
+        hipStream_t st = F.st_;
+        const int S = (int)last.valid.size();
+        if ((int)last.pos.size() != 3 * S || (int)last.desc.size() != 32 * S || (int)last.keys.size() != S ||
+            (int)last.has_obs.size() != S)
+            throw Error("SearchByProjectionLastFrame: inconsistent LastFrameView");
+        pos_.upload(last.pos.data(), last.pos.size(), st), desc_.upload(last.desc.data(), last.desc.size(), st);
+        val_.upload(last.valid.data(), last.valid.size(), st), obs_.upload(last.has_obs.data(), last.has_obs.size(), st);
+        kps_.upload(last.keys.data(), last.keys.size(), st);
+        tcw_.upload(&Tcw, 1, st), tlw_.upload(&last.Tcw, 1, st);
+        k2m_.upload(kp_to_mp.data(), kp_to_mp.size(), st);
+        if (occupied_init) occ_.upload(occupied_init->data(), occupied_init->size(), st);
+        nm_.resize(1);
+        const omv_last_frame lf{pos_.p, desc_.p, val_.p, obs_.p, kps_.p, S};
+        check(omv_matcher_search_last_frame(F.m_, 1, &F.geom_, F.kps_.p, F.desc_.p, F.n_.p, cams.data(), tcw_.p, tlw_.p, &Trl,
+                                            &lf, th, bMono ? 1 : 0, mb, check_ori_ ? 1 : 0,
+                                            occupied_init ? occ_.p : nullptr, k2m_.p, nm_.p, st),
+              "omv_matcher_search_last_frame");
+        int n = 0;
+        k2m_.download(kp_to_mp.data(), kp_to_mp.size(), st);
+        nm_.download(&n, 1, st);
+        hip_check(hipStreamSynchronize(st), "SearchByProjectionLastFrame");
+        check(omv_matcher_last_error(F.m_), "matcher capacity");
+        return n;
+    }
+
+  private:
+    float nnratio_;
+    bool check_ori_;
+    DeviceArray<float> pos_;
+    DeviceArray<uint8_t> desc_, val_, obs_, occ_;
+    DeviceArray<omv_kp> kps_;
+    DeviceArray<omv_se3f> tcw_, tlw_;
+    DeviceArray<int32_t> k2m_;
+    DeviceArray<int> nm_;
+};
+
+// ---- ORBmatcher::SearchForTriangulation ------------------------------------------------------------------------
+// The KeyFrame fields SearchForTriangulation reads, keypoints in the reference's [L | R | SL | SR] index order.
+struct KeyFrameView {
+    int N = 0, NLeft = -1, NRight = 0, NSideLeft = 0;
+    std::vector<omv_kp> keys;                        // [N] mvKeys / mvKeysRight / mvKeysSideLeft / mvKeysSideRight
+    std::vector<uint8_t> descriptors;                // [N][32] mDescriptors
+    std::vector<uint8_t> has_map_point;              // [N] GetMapPoint(idx) != NULL
+    std::vector<uint32_t> feat_node;                 // mFeatVec: node ids ascending ...
+    std::vector<int32_t> feat_start, feat_idx;       // ... with their keypoint indices (CSR, [nodes + 1] / [..])
+    std::array<float, 16> level_sigma2{};            // mvLevelSigma2
+};
+
+class SearchForTriangulation {
+  public:
+    SearchForTriangulation(float nnratio, bool checkOri) : check_ori_(checkOri) {
+        (void)nnratio;   // the reference's ratio test is not applied in SearchForTriangulation
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+        check(omv_matcher_create(1, 1, 1, 1, &m_), "omv_matcher_create");
+    }
+    ~SearchForTriangulation() {
+        if (m_) (void)omv_matcher_destroy(m_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    SearchForTriangulation(const SearchForTriangulation &) = delete;
+    SearchForTriangulation &operator=(const SearchForTriangulation &) = delete;
+
+    // Returns nmatches and vMatchedPairs (idx1, idx2) in idx1 order.  T: the 10 camera-pair transforms (R12 | t12)
+    // in OMV_TRI_PAIRS order; cams [4][8] and cam_model [4] (OMV_CAM_KB8 / OMV_CAM_PINHOLE) of the L, R, SL, SR cameras.
+    int operator()(const KeyFrameView &kf1, const KeyFrameView &kf2, const std::array<std::array<float, 12>, OMV_TRI_PAIRS> &T,
+                   const std::vector<float> &cams, const std::vector<int32_t> &cam_model,
+                   std::vector<std::pair<size_t, size_t>> &vMatchedPairs, bool bOnlyStereo, bool bCoarse = false) {
+        omv_tri_pair p{};
+        view(kf1, a_, p.kf1);
+        view(kf2, b_, p.kf2);
+        for (int q = 0; q < OMV_TRI_PAIRS; ++q) std::copy(T[q].begin(), T[q].end(), p.T[q]);
+        m12_.resize(std::max(1, kf1.N));
+        p.match12 = m12_.p;
+        nm_.resize(1);
+        check(omv_matcher_search_for_triangulation(m_, 1, &p, cams.data(), cam_model.empty() ? nullptr : cam_model.data(),
+                                                   bOnlyStereo ? 1 : 0, bCoarse ? 1 : 0, check_ori_ ? 1 : 0, nm_.p, st_),
+              "omv_matcher_search_for_triangulation");
+        std::vector<int32_t> m12(kf1.N);
+        int n = 0;
+        m12_.download(m12.data(), kf1.N, st_);
+        nm_.download(&n, 1, st_);
+        hip_check(hipStreamSynchronize(st_), "SearchForTriangulation");
+        vMatchedPairs.clear();
+        for (int i = 0; i < kf1.N; ++i)
+            if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);
+        return n;
+    }
+
+  private:
+    struct Buf {
+        DeviceArray<omv_kp> kps;
+        DeviceArray<uint8_t> desc, has_mp;
+        DeviceArray<uint32_t> node;
+        DeviceArray<int32_t> start, idx;
+    };
+    void view(const KeyFrameView &k, Buf &b, omv_kf_view &v) {
+        if ((int)k.keys.size() != k.N || (int)k.descriptors.size() != 32 * k.N || (int)k.has_map_point.size() != k.N ||
+            k.feat_start.size() != k.feat_node.size() + 1)
+            throw Error("SearchForTriangulation: inconsistent KeyFrameView");
+        b.kps.upload(k.keys.data(), k.keys.size(), st_), b.desc.upload(k.descriptors.data(), k.descriptors.size(), st_);
+        b.has_mp.upload(k.has_map_point.data(), k.has_map_point.size(), st_);
+        b.node.upload(k.feat_node.data(), k.feat_node.size(), st_);
+        b.start.upload(k.feat_start.data(), k.feat_start.size(), st_), b.idx.upload(k.feat_idx.data(), k.feat_idx.size(), st_);
+        v.n = k.N, v.n_left = k.NLeft, v.n_right = k.NRight, v.n_sideleft = k.NSideLeft;
+        v.kps = b.kps.p, v.desc = b.desc.p, v.has_mp = b.has_mp.p;
+        v.n_nodes = (int)k.feat_node.size(), v.node_id = b.node.p, v.node_start = b.start.p, v.node_idx = b.idx.p;
+        std::copy(k.level_sigma2.begin(), k.level_sigma2.end(), v.level_sigma2);
+    }
+    bool check_ori_;
+    hipStream_t st_ = nullptr;
+    omv_matcher *m_ = nullptr;
+    Buf a_, b_;
+    DeviceArray<int32_t> m12_;
+    DeviceArray<int32_t> nm_;
+};
+
+// ---- Optimizer::PoseInertialOptimizationLastKeyFrame / LastFrame -----------------------------------------------
+class PoseInertialOptimizer {
+  public:
+    struct State {   // a frame's (or keyframe's) VertexPose / VertexVelocity / VertexGyroBias / VertexAccBias
+        std::array<double, 9> Rwb{};
+        std::array<double, 3> twb{}, vel{}, bg{}, ba{};
+        std::vector<std::array<double, 9>> Rcw;   // [n_cams] ImuCamPose::Rcw
+        std::vector<std::array<double, 3>> tcw;   // [n_cams]
+    };
+    struct Mono {     // EdgeMonoOnlyPose: keypoint idx of camera `cam`, obs (u, v), invSigma2 / unc2, GetWorldPos
+        int cam, kp;
+        double u, v;
+        float inv_sigma2;
+        std::array<float, 3> Xw;
+        bool close;   // mTrackDepth < 10 (bClose)
+    };
+    struct Stereo {   // EdgeStereoOnlyPose: obs (u, v, u_R)
+        int cam, kp;
+        double u, v, ur;
+        float inv_sigma2;
+        std::array<float, 3> Xw;
+    };
+    struct Prior {    // Frame::mpcpi of the previous frame (ConstraintPoseImu: Rwb twb vwb bg ba and H)
+        std::array<double, 9> Rwb{};
+        std::array<double, 3> twb{}, vel{}, bg{}, ba{};
+        std::array<double, 225> H{};
+    };
+
+    PoseInertialOptimizer(int n_cams, std::vector<float> cams, std::vector<double> Rcb, std::vector<double> tcb,
+                          std::vector<double> Rbc, std::vector<double> tbc, float bf = 0.f, std::vector<int32_t> cam_model = {})
+        : C_(n_cams), cam_(std::move(cams)), Rcb_(std::move(Rcb)), tcb_(std::move(tcb)), Rbc_(std::move(Rbc)),
+          tbc_(std::move(tbc)), bf_(bf), model_(std::move(cam_model)) {
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    ~PoseInertialOptimizer() {
+        if (h_) (void)omv_pose_destroy(h_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    PoseInertialOptimizer(const PoseInertialOptimizer &) = delete;
+    PoseInertialOptimizer &operator=(const PoseInertialOptimizer &) = delete;
+
+    // PoseInertialOptimizationLastKeyFrame(pFrame, bRecInit): returns nInitialCorrespondences - nBad, updates `frame`
+    // and mvbOutlier (the keypoints carrying an edge; [kp_cap]), H (may be null) receives the 15x15 Hessian the
+    // reference hands to ConstraintPoseImu (:5529-5571).  preint: Frame::mpImuPreintegrated (OMV_PREINT_FLOATS).
+    int LastKeyFrame(State &frame, const State &kf, const std::vector<float> &preint, const std::vector<Mono> &mono,
+                     const std::vector<Stereo> &stereo, std::vector<uint8_t> &mvbOutlier, std::array<double, 225> *H,
+                     bool bRecInit) {
+        return run(frame, kf, preint, nullptr, nullptr, mono, stereo, mvbOutlier, H, bRecInit);
+    }
+    // PoseInertialOptimizationLastFrame(pFrame, bRecInit): `prev` = Frame::mpPrevFrame's state (free, not written
+    // back), preint_frame = mpImuPreintegratedFrame, preint_kf = mpImuPreintegrated (random-walk information), prior
+    // = pFp->mpcpi.  H receives Marginalize(H, 0, 14)'s frame block (:6158); ConstraintPoseImu(H) makes the next prior.
+    int LastFrame(State &frame, const State &prev, const std::vector<float> &preint_frame, const std::vector<float> &preint_kf,
+                  const Prior &prior, const std::vector<Mono> &mono, const std::vector<Stereo> &stereo,
+                  std::vector<uint8_t> &mvbOutlier, std::array<double, 225> *H, bool bRecInit) {
+        return run(frame, prev, preint_frame, &preint_kf, &prior, mono, stereo, mvbOutlier, H, bRecInit);
+    }
+    // The ConstraintPoseImu ctor's projection of H (include/G2oTypes.h:639-659).
+    std::array<double, 225> ConstraintPoseImu(const std::array<double, 225> &H) {
+        h_in_.upload(H.data(), 225, st_);
+        h_out_.resize(225);
+        check(omv_pose_constraint(1, h_in_.p, h_out_.p, st_), "omv_pose_constraint");
+        std::array<double, 225> out{};
+        h_out_.download(out.data(), 225, st_);
+        hip_check(hipStreamSynchronize(st_), "ConstraintPoseImu");
+        return out;
+    }
+
+  private:
+    int run(State &frame, const State &other, const std::vector<float> &preint, const std::vector<float> *preint_kf,
+            const Prior *prior, const std::vector<Mono> &mono, const std::vector<Stereo> &stereo,
+            std::vector<uint8_t> &kpo, std::array<double, 225> *H, bool rec_init) {
+        const int nm = (int)mono.size(), ns = (int)stereo.size();
+        if ((int)frame.Rcw.size() != C_ || (int)frame.tcw.size() != C_ || (int)preint.size() != OMV_PREINT_FLOATS ||
+            (preint_kf && (int)preint_kf->size() != OMV_PREINT_FLOATS) || kpo.empty())
+            throw Error("PoseInertialOptimizer: inconsistent inputs");
+        const int need = std::max(nm, ns);
+        if (!h_ || need > cap_) {
+            if (h_) (void)omv_pose_destroy(h_), h_ = nullptr;
+            cap_ = std::max(need, std::max(1, cap_));
+            check(omv_pose_create(1, cap_, &h_), "omv_pose_create");
+        }
+        auto st3 = [](const State &s, std::vector<double> &R, std::vector<double> &t, std::vector<double> &v,
+                      std::vector<double> &g, std::vector<double> &a) {
+            R.assign(s.Rwb.begin(), s.Rwb.end()), t.assign(s.twb.begin(), s.twb.end()), v.assign(s.vel.begin(), s.vel.end());
+            g.assign(s.bg.begin(), s.bg.end()), a.assign(s.ba.begin(), s.ba.end());
+        };
+        std::vector<double> R, t, v, g, a, kR, kt, kv, kg, ka, Rc, tc;
+        st3(frame, R, t, v, g, a);
+        st3(other, kR, kt, kv, kg, ka);
+        for (int c = 0; c < C_; ++c) {
+            Rc.insert(Rc.end(), frame.Rcw[c].begin(), frame.Rcw[c].end());
+            tc.insert(tc.end(), frame.tcw[c].begin(), frame.tcw[c].end());
+        }
+        Rwb_.upload(R.data(), 9, st_), twb_.upload(t.data(), 3, st_), vel_.upload(v.data(), 3, st_);
+        bg_.upload(g.data(), 3, st_), ba_.upload(a.data(), 3, st_), Rcw_.upload(Rc.data(), Rc.size(), st_);
+        tcw_.upload(tc.data(), tc.size(), st_);
+        kR_.upload(kR.data(), 9, st_), kt_.upload(kt.data(), 3, st_), kv_.upload(kv.data(), 3, st_);
+        kg_.upload(kg.data(), 3, st_), ka_.upload(ka.data(), 3, st_);
+        pre_.upload(preint.data(), preint.size(), st_);
+        std::vector<int32_t> mstart{0, nm}, sstart{0, ns}, mcam(nm), mkp(nm), scam(ns), skp(ns);
+        std::vector<double> mobs(2 * (size_t)nm), sobs(3 * (size_t)ns);
+        std::vector<float> mw(nm), mx(3 * (size_t)nm), sw(ns), sx(3 * (size_t)ns);
+        std::vector<uint8_t> mclose(nm);
+        for (int e = 0; e < nm; ++e) {
+            const Mono &m = mono[e];
+            mcam[e] = m.cam, mkp[e] = m.kp, mobs[2 * e] = m.u, mobs[2 * e + 1] = m.v, mw[e] = m.inv_sigma2;
+            std::copy(m.Xw.begin(), m.Xw.end(), &mx[3 * e]);
+            mclose[e] = m.close ? 1 : 0;
+        }
+        for (int e = 0; e < ns; ++e) {
+            const Stereo &m = stereo[e];
+            scam[e] = m.cam, skp[e] = m.kp, sobs[3 * e] = m.u, sobs[3 * e + 1] = m.v, sobs[3 * e + 2] = m.ur;
+            sw[e] = m.inv_sigma2;
+            std::copy(m.Xw.begin(), m.Xw.end(), &sx[3 * e]);
+        }
+        ms_.upload(mstart.data(), 2, st_), ss_.upload(sstart.data(), 2, st_);
+        mcam_.upload(mcam.data(), nm, st_), mkp_.upload(mkp.data(), nm, st_), mobs_.upload(mobs.data(), mobs.size(), st_);
+        mw_.upload(mw.data(), nm, st_), mx_.upload(mx.data(), mx.size(), st_), mclose_.upload(mclose.data(), nm, st_);
+        scam_.upload(scam.data(), ns, st_), skp_.upload(skp.data(), ns, st_), sobs_.upload(sobs.data(), sobs.size(), st_);
+        sw_.upload(sw.data(), ns, st_), sx_.upload(sx.data(), sx.size(), st_);
+        kpo_.upload(kpo.data(), kpo.size(), st_);
+        ng_.resize(1), H_.resize(225);
+        omv_pose_batch b{};
+        b.n_frames = 1, b.n_cams = C_, b.cam = cam_.data(), b.Rcb = Rcb_.data(), b.tcb = tcb_.data(), b.Rbc = Rbc_.data();
+        b.tbc = tbc_.data(), b.bf = bf_;
+        b.Rwb = Rwb_.p, b.twb = twb_.p, b.Rcw = Rcw_.p, b.tcw = tcw_.p, b.vel = vel_.p, b.bg = bg_.p, b.ba = ba_.p;
+        b.kf_Rwb = kR_.p, b.kf_twb = kt_.p, b.kf_vel = kv_.p, b.kf_bg = kg_.p, b.kf_ba = ka_.p, b.preint = pre_.p;
+        b.mono_start = ms_.p, b.mono_cam = mcam_.p, b.mono_kp = mkp_.p, b.mono_obs = mobs_.p, b.mono_inv_sigma2 = mw_.p;
+        b.mono_xw = mx_.p, b.mono_close = mclose_.p;
+        b.stereo_start = ss_.p, b.stereo_cam = scam_.p, b.stereo_kp = skp_.p, b.stereo_obs = sobs_.p;
+        b.stereo_inv_sigma2 = sw_.p, b.stereo_xw = sx_.p;
+        b.kp_cap = (int)kpo.size(), b.n_mono = nm, b.n_stereo = ns;
+        b.cam_model = model_.empty() ? nullptr : model_.data();
+        if (prior) {
+            pR_.upload(prior->Rwb.data(), 9, st_), pt_.upload(prior->twb.data(), 3, st_), pv_.upload(prior->vel.data(), 3, st_);
+            pg_.upload(prior->bg.data(), 3, st_), pa_.upload(prior->ba.data(), 3, st_), pH_.upload(prior->H.data(), 225, st_);
+            pkf_.upload(preint_kf->data(), preint_kf->size(), st_);
+            const omv_pose_prior pp{pR_.p, pt_.p, pv_.p, pg_.p, pa_.p, pH_.p, pkf_.p};
+            check(omv_pose_inertial_last_frame(h_, &b, &pp, rec_init ? 1 : 0, kpo_.p, ng_.p, H ? H_.p : nullptr, st_),
+                  "omv_pose_inertial_last_frame");
+        } else {
+            check(omv_pose_inertial_last_kf(h_, &b, rec_init ? 1 : 0, kpo_.p, ng_.p, H ? H_.p : nullptr, st_),
+                  "omv_pose_inertial_last_kf");
+        }
+        int n_good = 0;
+        ng_.download(&n_good, 1, st_);
+        kpo_.download(kpo.data(), kpo.size(), st_);
+        if (H) H_.download(H->data(), 225, st_);
+        Rwb_.download(R.data(), 9, st_), twb_.download(t.data(), 3, st_), vel_.download(v.data(), 3, st_);
+        bg_.download(g.data(), 3, st_), ba_.download(a.data(), 3, st_);
+        Rcw_.download(Rc.data(), Rc.size(), st_), tcw_.download(tc.data(), tc.size(), st_);
+        hip_check(hipStreamSynchronize(st_), "PoseInertialOptimizer");
+        int32_t err = 0;
+        check(omv_pose_last_error(h_, &err, st_), "omv_pose_last_error");
+        if (err != 0) throw Error("PoseInertialOptimizer: device error " + std::to_string(err));
+        std::copy_n(R.begin(), 9, frame.Rwb.begin()), std::copy_n(t.begin(), 3, frame.twb.begin());
+        std::copy_n(v.begin(), 3, frame.vel.begin()), std::copy_n(g.begin(), 3, frame.bg.begin());
+        std::copy_n(a.begin(), 3, frame.ba.begin());
+        for (int c = 0; c < C_; ++c) {
+            std::copy_n(&Rc[9 * (size_t)c], 9, frame.Rcw[c].begin());
+            std::copy_n(&tc[3 * (size_t)c], 3, frame.tcw[c].begin());
+        }
+        return n_good;
+    }
+
+    int C_;
+    std::vector<float> cam_;
+    std::vector<double> Rcb_, tcb_, Rbc_, tbc_;
+    float bf_;
+    std::vector<int32_t> model_;
+    hipStream_t st_ = nullptr;
+    omv_pose *h_ = nullptr;
+    int cap_ = 0;
+    DeviceArray<double> Rwb_, twb_, vel_, bg_, ba_, Rcw_, tcw_, kR_, kt_, kv_, kg_, ka_, mobs_, sobs_, H_, pR_, pt_, pv_,
+        pg_, pa_, pH_, h_in_, h_out_;
+    DeviceArray<float> pre_, pkf_, mw_, mx_, sw_, sx_;
+    DeviceArray<int32_t> ms_, ss_, mcam_, mkp_, scam_, skp_, ng_;
+    DeviceArray<uint8_t> mclose_, kpo_;
+};
+
+// ---- ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID) ----------------------------------------------------------
+// One keyframe whose keypoints are indexed into the grid once (KeyFrame::GetFeaturesInArea); Fuse runs per camera
+// block and returns, per map point of the list, the keyframe keypoint chosen (N-index, -1 none) and its distance:
+// the caller applies pMPinKF->Replace / AddObservation for best_dist <= TH_LOW in list order (:1620-1640), as the
+// map-graph mutation stays with the reference.
+struct FuseMapPoints {
+    std::vector<float> pos, normal;                  // [M][3] GetWorldPos(), GetNormal()
+    std::vector<float> min_dist, max_dist;           // [M] mfMinDistance, mfMaxDistance
+    std::vector<uint8_t> desc;                       // [M][32] GetDescriptor()
+};
+
+class Fuse {
+  public:
+    // The keyframe: keypoints per camera block ([n_cams][kp_cap], n_kp per block), descriptors, mvuRight of block 0,
+    // image bounds and scale factors; cams [n_cams][8] with their models.
+    Fuse(int n_cams, int kp_cap, int width, int height, const std::vector<float> &scale_factors, const std::vector<float> &cams,
+         const std::vector<int32_t> &cam_model, float bf, int max_points)
+        : C_(n_cams), cap_(kp_cap), cams_(cams), bf_(bf), sf_(scale_factors) {
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+        check(omv_matcher_create(1, n_cams, kp_cap, std::max(1, max_points), &m_), "omv_matcher_create");
+        geom_.n_cams = n_cams, geom_.min_x = 0.f, geom_.max_x = (float)width, geom_.min_y = 0.f, geom_.max_y = (float)height;
+        geom_.nlevels = (int)scale_factors.size();
+        for (int l = 0; l < geom_.nlevels && l < 16; ++l) geom_.scale_factors[l] = scale_factors[l];
+        for (int c = 0; c < n_cams && c < 8; ++c) geom_.cam_model[c] = cam_model.empty() ? OMV_CAM_KB8 : cam_model[c];
+    }
+    ~Fuse() {
+        if (m_) (void)omv_matcher_destroy(m_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    Fuse(const Fuse &) = delete;
+    Fuse &operator=(const Fuse &) = delete;
+
+    // The keyframe's keypoints (block-major [n_cams][kp_cap], n_kp per block), descriptors and block-0 mvuRight.
+    void set_keyframe(const std::vector<omv_kp> &kps, const std::vector<uint8_t> &desc, const std::vector<int> &n_kp,
+                      const std::vector<float> &uright) {
+        kps_.upload(kps.data(), kps.size(), st_), desc_.upload(desc.data(), desc.size(), st_);
+        n_.upload(n_kp.data(), n_kp.size(), st_), ur_.upload(uright.data(), uright.size(), st_);
+        check(omv_matcher_assign_grid(m_, 1, &geom_, kps_.p, n_.p, st_), "omv_matcher_assign_grid");
+    }
+    // Fuse(pKF, vpMapPoints, th, cameraID): Tcw / Ow of camera block `cam` (GetPose / GetRightPose ...,
+    // GetCameraCenter ...); inv_level_sigma2 = mvInvLevelSigma2.  The points the reference skips before projecting
+    // (NULL, isBad(), IsInKeyFrame(pKF)) are left out of `mps` by the caller.  Returns nFused.
+    int operator()(const FuseMapPoints &mps, int cam, const omv_se3f &Tcw, const std::array<float, 3> &Ow, float th,
+                   const std::vector<float> &inv_level_sigma2, std::vector<int32_t> &best_idx, std::vector<int32_t> &best_dist) {
+        const int M = (int)mps.min_dist.size();
+        pos_.upload(mps.pos.data(), mps.pos.size(), st_), nrm_.upload(mps.normal.data(), mps.normal.size(), st_);
+        mind_.upload(mps.min_dist.data(), M, st_), maxd_.upload(mps.max_dist.data(), M, st_);
+        mdesc_.upload(mps.desc.data(), mps.desc.size(), st_);
+        std::vector<int32_t> list(M);
+        for (int i = 0; i < M; ++i) list[i] = i;
+        list_.upload(list.data(), M, st_);
+        bi_.resize(std::max(1, M)), bd_.resize(std::max(1, M)), nm_.resize(1);
+        omv_kf_search_job job{};
+        job.kf = 0, job.cam = cam, job.Tcw = Tcw, job.mp_start = 0, job.mp_count = M;
+        std::copy(Ow.begin(), Ow.end(), job.Ow);
+        omv_kf_search_params p{};
+        p.mode = OMV_KF_FUSE, p.th = th, p.max_dist = 50.f, p.bf = bf_, p.uright = ur_.p;
+        for (int l = 0; l < (int)inv_level_sigma2.size() && l < 16; ++l) p.inv_level_sigma2[l] = inv_level_sigma2[l];
+        p.log_scale_factor = (float)std::log((double)sf_[1]);
+        p.n_levels = geom_.nlevels;
+        for (int c = 0; c < C_ && c < 8; ++c)
+            for (int q = 0; q < 8; ++q) p.cams[c][q] = cams_[8 * c + q];
+        const omv_kf_mps kfm{pos_.p, nrm_.p, mind_.p, maxd_.p, mdesc_.p};
+        check(omv_matcher_search_kf(m_, 1, &geom_, kps_.p, desc_.p, n_.p, 1, &job, M, list_.p, &kfm, &p, nullptr, bi_.p,
+                                    bd_.p, nm_.p, st_),
+              "omv_matcher_search_kf");
+        best_idx.resize(M), best_dist.resize(M);
+        int n = 0;
+        bi_.download(best_idx.data(), M, st_), bd_.download(best_dist.data(), M, st_), nm_.download(&n, 1, st_);
+        hip_check(hipStreamSynchronize(st_), "Fuse");
+        check(omv_matcher_last_error(m_), "matcher capacity");
+        return n;
+    }
+
+  private:
+    int C_, cap_;
+    std::vector<float> cams_;
+    float bf_;
+    std::vector<float> sf_;
+    hipStream_t st_ = nullptr;
+    omv_matcher *m_ = nullptr;
+    omv_frame_geom geom_{};
+    DeviceArray<omv_kp> kps_;
+    DeviceArray<uint8_t> desc_, mdesc_;
+    DeviceArray<int> n_;
+    DeviceArray<float> ur_, pos_, nrm_, mind_, maxd_;
+    DeviceArray<int32_t> list_, bi_, bd_, nm_;
+};
+
 // The window as the reference builds its graph: keyframes (each with its body pose, per-camera poses, velocity,
 // biases, bImu, and whether it is fixed), map points, EdgeMono / EdgeStereo observations and inertial edges in
 // creation order.  flatten() renumbers keyframes optimisable-first (the vertex order of Optimizer.cc:2800-2860) and

@@ -724,8 +724,9 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
 // the state.  The 15x15 / 30x30 system is solved by one wavefront with the rows in registers (pivot order first,
 // Eigen's transpositions replayed on the original diagonal; right-looking LDL^T with v_readlane row broadcasts).
 // =====================================================================================================================
-constexpr int kLatThreads = 384;        // waves 0-3: visual edges; 4: EdgeInertial; 5: EdgePriorPoseImu (LastFrame)
-constexpr int kLatEdgeThreads = 256;
+constexpr int kLatThreads = 256;        // one wave per SIMD (512 registers): visual edges on 3 (LastFrame 2) waves, then
+                                        // EdgeInertial, then (LastFrame) EdgePriorPoseImu on a wave of its own
+__host__ __device__ constexpr int lat_edge_threads(bool lf) { return lf ? 128 : 192; }
 constexpr int kLatMaxParts = 8;         // workgroups per frame
 constexpr int kLatCap = 1024;           // visual edges per workgroup (LDS)
 constexpr int kLatFlagCap = 16384;      // keypoints per frame (mvbOutlier staged in LDS)
@@ -733,6 +734,13 @@ constexpr int kGran = 64;               // 8-byte granules per (frame, slot, par
 constexpr int kLatAutoFrames = 16;      // OMV_POSE_AUTO: the grouped kernel up to this many frames per call
 constexpr size_t kLatFrameGran = 2 * kLatMaxParts * kGran;   // granules per frame (two slots by phase parity)
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+#ifdef OMV_POSE_PROFILE   // phase times of the grouped kernel (wall_clock64 = 100 MHz), printed by part 0
+#define LAT_T(var) const unsigned long long var = wall_clock64()
+#define LAT_ACC(slot, a, b) prof[slot] += (b) - (a)
+#else
+#define LAT_T(var)
+#define LAT_ACC(slot, a, b)
+#endif
 
 // Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q): publish this part's values as
 // 2n granules of slot (phase & 1), sweep all G x 2n granules until every tag equals salt | phase, add the parts in part
@@ -847,14 +855,13 @@ __device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b
     for (int k = 0; k < N; ++k) {
         const double d = lane_f64(r[k], k);
         if (lane == k) dmine = d;
-        if (fabs(d) > 0.0) {
-            const double l = r[k] / d;
+        if (fabs(d) > 0.0) {   // rows above k update with l = 0 (an exact no-op): no exec-mask branches or selects
+            const double inv = 1.0 / d;
+            const bool below = lane > k;
+            const double l = below ? r[k] * inv : 0.0;
 #pragma unroll
-            for (int j = k + 1; j < N; ++j) {
-                const double c = lane_f64(r[j], k);
-                if (lane > k) r[j] = __builtin_fma(-l, c, r[j]);
-            }
-            if (lane > k) r[k] = l;
+            for (int j = k + 1; j < N; ++j) r[j] = __builtin_fma(-l, lane_f64(r[j], k), r[j]);
+            if (below) r[k] = l;
         }
         if (sign == 1) {
             if (d < 0) sign = 3;
@@ -883,6 +890,129 @@ __device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b
     for (int j = N - 1; j >= 1; --j) {
         const double xj = lane_f64(y, j);
         if (lane < j) y = __builtin_fma(-r[j], xj, y);
+    }
+    if (in) x[pi] = y;
+    wave_lds_sync();
+    return true;
+}
+
+// The same solve with the factorisation spread over the whole wavefront: the NP x NP padded matrix (NP = 16 or 32) is
+// held P = 64 / NP lanes per row (lane = row + NP * s holds columns s, s + P, ...: R = NP / P registers), so a step's
+// trailing update is R FMAs per lane instead of N.  Step k: the lanes holding column k publish it to LDS (one store),
+// every lane reads its row's entry (the multiplier) and the entries of its own columns (the pivot row, by symmetry the
+// pivot column) and updates; the triangular solves run row-per-lane from the factor staged in LDS.  Pick order, zero
+// pivots, isPositive() and the D pseudo-inverse as ldlt_pick_solve.  cb: LDS scratch [NP].
+template <int N>
+__device__ __forceinline__ bool ldlt_pick_solve_wide(const double *H, const double *b, double *x, int *pick, double *Lm,
+                                                     double *cb, int lane) {
+    constexpr int NP = N <= 16 ? 16 : 32, P = 64 / NP, R = NP / P;
+    static_assert(N <= 32, "at most 32 states");
+    const bool in = lane < N;
+    const double dv = in ? fabs(H[lane * (N + 1)]) : 0.0;
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double o = fabs(H[j * (N + 1)]);
+        gt += o > dv ? 1 : 0;
+        eq += o == dv ? 1 : 0;
+    }
+    if (__ballot(in && !(dv == dv))) return false;   // a NaN diagonal: no factorisation
+    if (!__ballot(in && eq > 1)) {
+        if (in) pick[gt] = lane;
+    } else {   // selection with positional swaps, lanes = elements (pos = current position)
+        int pos = lane;
+        bool picked = false;
+        for (int k = 0; k < N; ++k) {
+            uint64_t cand = __ballot(in && !picked && gt <= k && k < gt + eq);
+            int e = __builtin_ctzll(cand);
+            if (cand & (cand - 1)) {   // several equal magnitudes: the lowest current position
+                int bp = __builtin_amdgcn_readlane(pos, e);
+                for (uint64_t m = cand & (cand - 1); m; m &= m - 1) {
+                    const int c = __builtin_ctzll(m), pc = __builtin_amdgcn_readlane(pos, c);
+                    if (pc < bp) bp = pc, e = c;
+                }
+            }
+            const int xk = __builtin_ctzll(__ballot(in && pos == k));
+            const int pe = __builtin_amdgcn_readlane(pos, e);
+            if (lane == xk) pos = pe;
+            if (lane == e) pos = k, picked = true;
+            if (lane == 0) pick[k] = e;
+        }
+    }
+    wave_lds_sync();
+    const int row = lane & (NP - 1), sub = lane / NP;
+    const bool rin = row < N;
+    const int pr = rin ? pick[row] : 0;
+    double r[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+        const int j = sub + P * m;
+        r[m] = (rin && j < N) ? H[pr * N + pick[j < N ? j : 0]] : 0.0;
+    }
+    if (!(lane_f64(r[0], 0) != 0.0)) {   // largest |diagonal| zero: Eigen stops with ZeroSign; the solve gives x = 0
+        if (in) x[lane] = 0.0;
+        wave_lds_sync();
+        return true;
+    }
+    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
+    double dmine = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int ck = k % P, mk = k / P;
+        if (sub == ck) cb[row] = r[mk];   // column k (= row k) of the current matrix, rows >= N publish 0
+        wave_lds_sync();
+        const double d = cb[k];
+        if (row == k) dmine = d;
+        if (fabs(d) > 0.0) {
+            const double inv = 1.0 / d;
+            const double l = row > k ? cb[row] * inv : 0.0;
+            const int m0 = (k + 1) / P;
+#pragma unroll
+            for (int m = m0; m < R; ++m) {
+                const int j = sub + P * m;
+                const double lj = (m == m0 && j <= k) ? 0.0 : l;   // the boundary register: columns <= k are L's
+                r[m] = __builtin_fma(-lj, cb[j], r[m]);
+            }
+            if (sub == ck && row > k) r[mk] = l;
+        }
+        wave_lds_sync();   // cb is rewritten by the next step
+        if (sign == 1) {
+            if (d < 0) sign = 3;
+        } else if (sign == 2) {
+            if (d > 0) sign = 3;
+        } else if (sign == 0) {
+            if (d > 0) sign = 1;
+            else if (d < 0) sign = 2;
+        }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    if (rin)
+#pragma unroll
+        for (int m = 0; m < R; ++m) {
+            const int j = sub + P * m;
+            if (j < N) Lm[row * N + j] = r[m];
+        }
+    wave_lds_sync();
+    // row-per-lane triangular solves (lane = position i < N)
+    double Lr[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) Lr[j] = in ? Lm[lane * N + j] : 0.0;   // row i of L (j < i)
+    const int pi = in ? pick[lane] : 0;
+    double y = in ? b[pi] : 0.0;
+#pragma unroll
+    for (int k = 0; k + 1 < N; ++k) {
+        const double yk = lane_f64(y, k);
+        y = __builtin_fma(-(lane > k ? Lr[k] : 0.0), yk, y);
+    }
+    y = fabs(dmine) > 2.2250738585072014e-308 ? y / dmine : 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) Lr[j] = in ? Lm[j * N + lane] : 0.0;   // column i of L: L_j,i (j > i)
+#pragma unroll
+    for (int j = N - 1; j >= 1; --j) {
+        const double xj = lane_f64(y, j);
+        y = __builtin_fma(-(lane < j ? Lr[j] : 0.0), xj, y);
     }
     if (in) x[pi] = y;
     wave_lds_sync();
@@ -971,6 +1101,13 @@ __device__ void imu_jacobian_wave(const State &s, const Imu &I, const double *eR
         put(0, 9, Jg, -1.0);
     }
     wave_lds_sync();
+}
+
+// Fixed-order sum of the edge waves' partials (wave 0 first).
+__device__ __forceinline__ double wave_parts_sum(const double (*red)[kNormal], int q, int n) {
+    double v = red[0][q];
+    for (int w = 1; w < n; ++w) v += red[w][q];
+    return v;
 }
 
 // LDS of the grouped kernel beyond its static arrays: the workgroup's visual edges (SoA) and the frame's mvbOutlier.
@@ -1066,6 +1203,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     constexpr int NJ = kLF ? 216 : 81;   // EdgeInertial Jacobian entries kept: 9 x 24 (LastFrame), 9 x 9 (columns 15-23)
     constexpr int NI = kLF ? 24 : 9;
     constexpr int NP = kLF ? 225 : 1;
+    // waves: 0 .. kEW-1 visual edges (one per thread), kIW EdgeInertial, kPW EdgePriorPoseImu (LastFrame)
+    constexpr int kEW = kLF ? 2 : 3, kIW = kEW, kPW = 3, kET = 64 * kEW;
     const int f = blockIdx.x / G, g = blockIdx.x - f * G, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     gu64 *fb = xbuf + (size_t)f * kLatFrameGran;
     extern __shared__ __attribute__((aligned(16))) char lat_dyn[];
@@ -1073,7 +1212,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     __shared__ Rig rig;
     __shared__ double sRwb[18], stwb[6], svel[6], sbg[6], sba[6];
     __shared__ double sRcw[kMaxCams * 9], stcw[kMaxCams * 3];
-    __shared__ double red[4][kNormal], nrm[32];
+    __shared__ double red[3][kNormal], nrm[32];
     __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N];
     __shared__ double info9[81], infoG[9], infoA[9];
     __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], HI[NI * NI], bI[NI];
@@ -1085,7 +1224,14 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N];
     __shared__ int k1s, k2s;
     __shared__ double s_cnt[2];
+    __shared__ float spre[kPF];   // the frame's IMU::Preintegrated record (read every iteration: kept out of HBM)
     const int C = rig_in.n_cams;
+#ifdef OMV_POSE_PROFILE
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __shared__ unsigned long long prof_inert;
+    if (tid == 0) prof_inert = 0;
+    LAT_T(t_start);
+#endif
     for (int q = tid; q < (int)(sizeof(Rig) / 4); q += kLatThreads)
         reinterpret_cast<uint32_t *>(&rig)[q] = reinterpret_cast<const uint32_t *>(&rig_in)[q];
     if (tid == 0) {
@@ -1115,6 +1261,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     for (int q = tid; q < C * 3; q += kLatThreads) stcw[q] = A.tcw[(size_t)f * C * 3 + q];
     for (int q = tid; q < N; q += kLatThreads) xs[q] = 0.0;
     for (int q = tid; q < NJ; q += kLatThreads) J[q] = 0.0;
+    for (int q = tid; q < kPF; q += kLatThreads) spre[q] = A.preint[(size_t)f * kPF + q];
     for (int q = tid; q < 99; q += kLatThreads) {
         const double v = A.info[(size_t)f * 99 + q];
         if (q < 81) info9[q] = v;
@@ -1138,10 +1285,10 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     }
     State st{sRwb, stwb, nullptr, nullptr, svel, sbg, sba, nullptr};
     Imu imu{};
-    imu.n = 1, imu.kf1 = &k1s, imu.kf2 = &k2s, imu.pre = A.preint + (size_t)f * kPF;
+    imu.n = 1, imu.kf1 = &k1s, imu.kf2 = &k2s, imu.pre = spre;
     // LastKeyFrame: the keyframe's vertices are fixed, so IMU::Preintegrated's bias-corrected deltas and dR^T Rbw1
     // are constants of the call (imu_error computes them the same way at every iteration)
-    if (!kLF && wave == 4 && lane == 0) {
+    if (!kLF && wave == kIW && lane == 0) {
         const float *p = imu.pre;
         float b1[6];
         for (int q = 0; q < 3; ++q) b1[q] = (float)sba[q], b1[3 + q] = (float)sbg[q];
@@ -1278,11 +1425,16 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             const bool robust = it < 3;   // setRobustKernel(0) after the third classification
             for (int gi = 0; gi < 10; ++gi) {
                 ++phase;
-                if (wave < 4) {   // computeActiveErrors + the visual part of buildSystem
+                // LDS is re-read every iteration: a compiler barrier keeps the loop-invariant LDS reads (information
+                // matrices, the prior, the rig) from being hoisted into registers across the whole loop, whose
+                // live ranges spanned every wave role's code and spilled
+                asm volatile("" ::: "memory");
+                LAT_T(t0);
+                if (wave < kEW) {   // computeActiveErrors + the visual part of buildSystem
                     double acc[kNormal];
 #pragma unroll
                     for (int q = 0; q < kNormal; ++q) acc[q] = 0;
-                    for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+                    for (int q = tid; q < nloc; q += kET) {
                         if (!(E.fl[q] & 4)) continue;
                         const VEdge v = lat_edge(E, q);
                         double r[3], Xc[3], JP[18];
@@ -1298,19 +1450,31 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                         const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, v.stereo ? -v.w * r[2] * w1 : 0.0};
                         edge_normal(JP, v.stereo, v.w * w1, om, acc);
                     }
+                    LAT_T(t0e);
+                    LAT_ACC(0, t0, t0e);
                     const double mine = wave_transpose_sum(acc, lane);
                     if (lane < kNormal) red[wave][lane] = mine;
-                } else if (wave == 4) {   // EdgeInertial at the iteration's state
+                    LAT_T(t0r);
+                    LAT_ACC(1, t0e, t0r);
+                } else if (wave == kIW) {   // EdgeInertial at the iteration's state
                     inertial_wave(true);
-                } else if (kLF && wave == 5) {   // EdgePriorPoseImu on the previous frame (vertex 0)
+#ifdef OMV_POSE_PROFILE
+                    LAT_T(t0i);
+                    if (lane == 0) prof_inert += t0i - t0;
+#endif
+                } else if (kLF && wave == kPW) {   // EdgePriorPoseImu on the previous frame (vertex 0)
                     prior_wave(true);
                 }
                 __syncthreads();
+                LAT_T(t1);
                 if (wave == 0) {
-                    const double v = lane < kNormal ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                    const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
                     if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
                 }
                 __syncthreads();
+                LAT_T(t2);
+                LAT_ACC(2, t0, t1);
+                LAT_ACC(3, t1, t2);
                 if (s_abort) goto fail;
                 // the system in the oracle's per-element order (visual, inertial, random walks, prior)
                 for (int q = tid; q < N * N; q += kLatThreads) {
@@ -1365,8 +1529,12 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     bs[i] = t;
                 }
                 __syncthreads();
+                LAT_T(t3);
+                LAT_ACC(4, t2, t3);
                 if (wave == 0) {
                     const bool ok = ldlt_pick_solve<N>(Hs, bs, xt, pick, Lm, lane);
+                    LAT_T(t3l);
+                    LAT_ACC(5, t3, t3l);
                     if (ok && lane < N) xs[lane] = xt[lane];   // a failed solve leaves the previous x in place
                     if (lane == 0) s_ok = ok ? 1 : 0;
                     wave_lds_sync();
@@ -1399,14 +1567,16 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     }
                 }
                 __syncthreads();
+                LAT_T(t4);
+                LAT_ACC(6, t3, t4);
                 if (!s_ok) break;   // optimize() stops after a failed iteration
             }
             // classification (:5436-5490): the mono pass, then the stereo pass; counts summed over the parts
             double bad = 0, in = 0;
             const float chi2close = 1.5f * chi2Mono[it];
             for (int pass = 0; pass < 2; ++pass) {
-                if (wave < 4)
-                    for (int q = (pass ? nm_loc : 0) + tid; q < (pass ? nloc : nm_loc); q += kLatEdgeThreads) {
+                if (wave < kEW)
+                    for (int q = (pass ? nm_loc : 0) + tid; q < (pass ? nloc : nm_loc); q += kET) {
                         const VEdge v = lat_edge(E, q);
                         double Xc[3];
                         if (E.kpo[v.kp]) {   // outliers of the last round: computeError at the current state
@@ -1433,12 +1603,12 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             }
             {
                 double cnt2[2] = {bad, in};
-                const double sb = wave < 4 ? wave_transpose_sum(cnt2, lane) : 0.0;
-                if (wave < 4 && lane < 2) red[wave][lane] = sb;
+                const double sb = wave < kEW ? wave_transpose_sum(cnt2, lane) : 0.0;
+                if (wave < kEW && lane < 2) red[wave][lane] = sb;
                 __syncthreads();
                 ++phase;
                 if (wave == 0) {
-                    const double v = lane < 2 ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                    const double v = lane < 2 ? wave_parts_sum(red, lane, kEW) : 0.0;
                     if (!lat_exchange(fb, phase, salt, g, G, v, 2, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
                 }
                 __syncthreads();
@@ -1449,8 +1619,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         }
         if (nIn < 30 && !A.rec_init) {   // recover not too bad points (:5503-5526)
             double bad = 0;
-            if (wave < 4)
-                for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+            if (wave < kEW)
+                for (int q = tid; q < nloc; q += kET) {
                     const VEdge v = lat_edge(E, q);
                     double r[3], Xc[3];
                     const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
@@ -1459,12 +1629,12 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     else bad += 1;
                 }
             double cnt1[1] = {bad};
-            const double sb = wave < 4 ? wave_transpose_sum(cnt1, lane) : 0.0;
-            if (wave < 4 && lane == 0) red[wave][0] = sb;
+            const double sb = wave < kEW ? wave_transpose_sum(cnt1, lane) : 0.0;
+            if (wave < kEW && lane == 0) red[wave][0] = sb;
             __syncthreads();
             ++phase;
             if (wave == 0) {
-                const double v = lane < 1 ? ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0] : 0.0;
+                const double v = lane < 1 ? wave_parts_sum(red, 0, kEW) : 0.0;
                 if (!lat_exchange(fb, phase, salt, g, G, v, 1, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
             }
             __syncthreads();
@@ -1472,16 +1642,16 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             nBad = s_cnt[0];
         }
         // mvbOutlier of this part's keypoints
-        if (wave < 4)
-            for (int q = tid; q < nloc; q += kLatEdgeThreads) A.kp_out[(size_t)f * A.kp_cap + E.kp[q]] = E.kpo[E.kp[q]];
+        if (wave < kEW)
+            for (int q = tid; q < nloc; q += kET) A.kp_out[(size_t)f * A.kp_cap + E.kp[q]] = E.kpo[E.kp[q]];
         if (A.H) {
             // the Hessian without robust weights at the final state (inlier visual edges): visual sums exchanged,
             // EdgeInertial / EdgePriorPoseImu linearised by waves 4 / 5, the matrix formed by part 0
-            if (wave < 4) {
+            if (wave < kEW) {
                 double acc[kNormal];
 #pragma unroll
                 for (int q = 0; q < kNormal; ++q) acc[q] = 0;
-                for (int q = tid; q < nloc; q += kLatEdgeThreads) {
+                for (int q = tid; q < nloc; q += kET) {
                     const VEdge v = lat_edge(E, q);
                     if (E.kpo[v.kp]) continue;
                     double r[3], Xc[3], JP[18];
@@ -1492,15 +1662,15 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 }
                 const double mine = wave_transpose_sum(acc, lane);
                 if (lane < kNormal) red[wave][lane] = mine;
-            } else if (wave == 4) {
+            } else if (wave == kIW) {
                 inertial_wave(false);
-            } else if (kLF && wave == 5) {
+            } else if (kLF && wave == kPW) {
                 prior_wave(false);
             }
             __syncthreads();
             ++phase;
             if (wave == 0) {
-                const double v = lane < kNormal ? ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane] : 0.0;
+                const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
                 if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
             }
             __syncthreads();
@@ -1578,6 +1748,15 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 }
             }
         }
+#ifdef OMV_POSE_PROFILE
+        if (g == 0 && tid == 0) {
+            LAT_T(t_end);
+            printf("pose_lat<%d> G %d edges(w0) %.1f reduce %.1f edges+inertial(barrier) %.1f exchange %.1f build %.1f "
+                   "ldlt %.1f ldlt+update %.1f inertial(w4) %.1f total %.1f us\n", (int)kLF, G, prof[0] / 100.0,
+                   prof[1] / 100.0, prof[2] / 100.0, prof[3] / 100.0, prof[4] / 100.0, prof[5] / 100.0, prof[6] / 100.0,
+                   prof_inert / 100.0, (t_end - t_start) / 100.0);
+        }
+#endif
         if (g == 0) {   // state back
             if (tid == 0) {
                 for (int q = 0; q < 9; ++q) A.Rwb[9 * f + q] = sRwb[9 + q];
@@ -1711,7 +1890,8 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     bool grouped = h->mode == OMV_POSE_GROUPED || (h->mode == OMV_POSE_AUTO && F <= kLatAutoFrames && grouped_ok);
     if (h->mode == OMV_POSE_GROUPED && !grouped_ok) return OMV_ERR_ARG;
     int G = h->parts;
-    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + kLatEdgeThreads - 1) / kLatEdgeThreads));
+    const int et = lat_edge_threads(prior != nullptr);
+    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 1) / et));
     pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
     if (grouped) {
         h->call = (h->call + 1) & 0xFFFFFu;

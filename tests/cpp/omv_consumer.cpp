@@ -6,6 +6,10 @@
 //
 //   omv_consumer orb   DIR   per image: ORBextractor::operator() (one image per call, host memory)
 //   omv_consumer frame DIR   MultiCameraFrame (batched extraction + grid + lapping knn) + SearchByProjection
+//   omv_consumer lastframe DIR  MultiCameraFrame + SearchByProjectionLastFrame (motion-model matching)
+//   omv_consumer tri   DIR   SearchForTriangulation of one keyframe pair -> vMatchedPairs
+//   omv_consumer pose  DIR   PoseInertialOptimizer: LastKeyFrame (meta lf 0) or LastFrame + ConstraintPoseImu (lf 1)
+//   omv_consumer fuse  DIR   Fuse per camera block of one keyframe -> chosen keypoint / distance per point
 //   omv_consumer lba   DIR   LocalInertialBAWindow: keyframes added in a mixed fixed / optimisable order,
 //                            EdgeMono + EdgeStereo observations, inertial edges under the reference's robust
 //                            rule (last edge / bRecInit), flattened optimisable-first, optimised, written back
@@ -224,11 +228,175 @@ int run_lba(const std::string &dir) {
     return 0;
 }
 
+omv_se3f se3_of(const std::vector<float> &t7) {   // qx qy qz qw tx ty tz
+    omv_se3f T{};
+    for (int q = 0; q < 4; ++q) T.q[q] = t7[q];
+    for (int q = 0; q < 3; ++q) T.t[q] = t7[4 + q];
+    return T;
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) on a MultiCameraFrame built from the images
+int run_lastframe(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["C"], W = (int)m["W"], H = (int)m["H"];
+    const auto img = read_bin<uint8_t>(dir, "images");
+    const auto lap = read_bin<int32_t>(dir, "lapping");
+    std::vector<std::array<int, 2>> lapping(C);
+    for (int c = 0; c < C; ++c) lapping[c] = {lap[2 * c], lap[2 * c + 1]};
+    const omv_orb_params p{(int)m["nfeatures"], 1.2f, 8, (int)m["ini"], (int)m["min"]};
+    const int last_cap = (int)m["last_cap"];
+    omv_adapt::MultiCameraFrame F(C, W, H, p, lapping, C * last_cap);
+    F.set_camera_models(read_opt<int32_t>(dir, "cam_model"));
+    std::vector<const uint8_t *> ims(C);
+    for (int c = 0; c < C; ++c) ims[c] = img.data() + (size_t)c * W * H;
+    F.build(ims);
+    omv_adapt::LastFrameView last;
+    last.last_cap = last_cap;
+    last.pos = read_bin<float>(dir, "last_pos"), last.desc = read_bin<uint8_t>(dir, "last_desc");
+    last.valid = read_bin<uint8_t>(dir, "last_valid"), last.has_obs = read_bin<uint8_t>(dir, "last_obs");
+    last.keys = read_bin<omv_kp>(dir, "last_kps");
+    last.Tcw = se3_of(read_bin<float>(dir, "Tlw"));
+    const auto occ = read_bin<uint8_t>(dir, "occ");
+    std::vector<int32_t> k2m((size_t)C * F.kp_cap(), -1);
+    omv_adapt::SearchByProjectionLastFrame sbp((float)m["nnratio"], m["check_ori"] != 0);
+    const int n = sbp(F, last, se3_of(read_bin<float>(dir, "Tcw")), se3_of(read_bin<float>(dir, "Trl")),
+                      read_bin<float>(dir, "cams"), (float)m["th"], m["bmono"] != 0, (float)m["mb"], k2m, &occ);
+    write_bin(dir, "kp_to_mp", k2m);
+    write_bin(dir, "n_matches", &n, 1);
+    return 0;
+}
+
+omv_adapt::KeyFrameView read_kf(const std::string &dir, const std::string &k, const std::map<std::string, double> &m) {
+    omv_adapt::KeyFrameView v;
+    v.N = (int)m.at(k + "_n"), v.NLeft = (int)m.at(k + "_n_left"), v.NRight = (int)m.at(k + "_n_right");
+    v.NSideLeft = (int)m.at(k + "_n_sideleft");
+    v.keys = read_bin<omv_kp>(dir, k + "_kps"), v.descriptors = read_bin<uint8_t>(dir, k + "_desc");
+    v.has_map_point = read_bin<uint8_t>(dir, k + "_has_mp"), v.feat_node = read_bin<uint32_t>(dir, k + "_node_id");
+    v.feat_start = read_bin<int32_t>(dir, k + "_node_start"), v.feat_idx = read_bin<int32_t>(dir, k + "_node_idx");
+    const auto s2 = read_bin<float>(dir, "level_sigma2");
+    std::copy_n(s2.begin(), std::min<size_t>(16, s2.size()), v.level_sigma2.begin());
+    return v;
+}
+
+// SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse)
+int run_tri(const std::string &dir) {
+    auto m = read_meta(dir);
+    const auto kf1 = read_kf(dir, "kf1", m), kf2 = read_kf(dir, "kf2", m);
+    const auto Tf = read_bin<float>(dir, "T");
+    std::array<std::array<float, 12>, OMV_TRI_PAIRS> T{};
+    for (int q = 0; q < OMV_TRI_PAIRS; ++q) std::copy_n(&Tf[12 * q], 12, T[q].begin());
+    omv_adapt::SearchForTriangulation sft(0.6f, m["check_ori"] != 0);
+    std::vector<std::pair<size_t, size_t>> pairs;
+    const int n = sft(kf1, kf2, T, read_bin<float>(dir, "cams"), read_opt<int32_t>(dir, "cam_model"), pairs,
+                      m["only_stereo"] != 0, m["coarse"] != 0);
+    std::vector<int64_t> flat;
+    for (const auto &pr : pairs) flat.push_back((int64_t)pr.first), flat.push_back((int64_t)pr.second);
+    write_bin(dir, "pairs", flat);
+    write_bin(dir, "n_matches", &n, 1);
+    return 0;
+}
+
+omv_adapt::PoseInertialOptimizer::State read_state(const std::string &dir, const std::string &pre, int C) {
+    omv_adapt::PoseInertialOptimizer::State s;
+    const auto R = read_bin<double>(dir, pre + "Rwb"), t = read_bin<double>(dir, pre + "twb");
+    const auto v = read_bin<double>(dir, pre + "vel"), g = read_bin<double>(dir, pre + "bg"), a = read_bin<double>(dir, pre + "ba");
+    std::copy_n(R.begin(), 9, s.Rwb.begin()), std::copy_n(t.begin(), 3, s.twb.begin()), std::copy_n(v.begin(), 3, s.vel.begin());
+    std::copy_n(g.begin(), 3, s.bg.begin()), std::copy_n(a.begin(), 3, s.ba.begin());
+    s.Rcw.resize(C), s.tcw.resize(C);
+    if (pre.empty()) {
+        const auto Rc = read_bin<double>(dir, "Rcw"), tc = read_bin<double>(dir, "tcw");
+        for (int c = 0; c < C; ++c) std::copy_n(&Rc[9 * c], 9, s.Rcw[c].begin()), std::copy_n(&tc[3 * c], 3, s.tcw[c].begin());
+    }
+    return s;
+}
+
+// PoseInertialOptimizationLastKeyFrame / LastFrame on one frame (meta lf 0 / 1)
+int run_pose(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["n_cams"], cap = (int)m["kp_cap"];
+    omv_adapt::PoseInertialOptimizer opt(C, read_bin<float>(dir, "cam"), read_bin<double>(dir, "Rcb"), read_bin<double>(dir, "tcb"),
+                                         read_bin<double>(dir, "Rbc"), read_bin<double>(dir, "tbc"), (float)m["bf"],
+                                         read_opt<int32_t>(dir, "cam_model"));
+    auto frame = read_state(dir, "", C);
+    const auto other = read_state(dir, "kf_", C);
+    const auto mcam = read_bin<int32_t>(dir, "mono_cam"), mkp = read_bin<int32_t>(dir, "mono_kp");
+    const auto mobs = read_bin<double>(dir, "mono_obs");
+    const auto mw = read_bin<float>(dir, "mono_inv_sigma2"), mx = read_bin<float>(dir, "mono_xw");
+    const auto mclose = read_bin<uint8_t>(dir, "mono_close");
+    const auto scam = read_opt<int32_t>(dir, "stereo_cam"), skp = read_opt<int32_t>(dir, "stereo_kp");
+    const auto sobs = read_opt<double>(dir, "stereo_obs");
+    const auto sw = read_opt<float>(dir, "stereo_inv_sigma2"), sx = read_opt<float>(dir, "stereo_xw");
+    std::vector<omv_adapt::PoseInertialOptimizer::Mono> mono;
+    for (size_t e = 0; e < mcam.size(); ++e)
+        mono.push_back({mcam[e], mkp[e], mobs[2 * e], mobs[2 * e + 1], mw[e], {mx[3 * e], mx[3 * e + 1], mx[3 * e + 2]},
+                        mclose[e] != 0});
+    std::vector<omv_adapt::PoseInertialOptimizer::Stereo> stereo;
+    for (size_t e = 0; e < scam.size(); ++e)
+        stereo.push_back({scam[e], skp[e], sobs[3 * e], sobs[3 * e + 1], sobs[3 * e + 2], sw[e],
+                          {sx[3 * e], sx[3 * e + 1], sx[3 * e + 2]}});
+    std::vector<uint8_t> outl(cap, 255);
+    std::array<double, 225> H{};
+    int n_good;
+    if (m["lf"] != 0) {
+        omv_adapt::PoseInertialOptimizer::Prior pr;
+        const auto R = read_bin<double>(dir, "prior_Rwb"), t = read_bin<double>(dir, "prior_twb");
+        const auto v = read_bin<double>(dir, "prior_vel"), g = read_bin<double>(dir, "prior_bg");
+        const auto a = read_bin<double>(dir, "prior_ba"), Hp = read_bin<double>(dir, "prior_H");
+        std::copy_n(R.begin(), 9, pr.Rwb.begin()), std::copy_n(t.begin(), 3, pr.twb.begin()), std::copy_n(v.begin(), 3, pr.vel.begin());
+        std::copy_n(g.begin(), 3, pr.bg.begin()), std::copy_n(a.begin(), 3, pr.ba.begin()), std::copy_n(Hp.begin(), 225, pr.H.begin());
+        n_good = opt.LastFrame(frame, other, read_bin<float>(dir, "preint"), read_bin<float>(dir, "preint_kf"), pr, mono,
+                               stereo, outl, &H, m["rec_init"] != 0);
+        const auto Hc = opt.ConstraintPoseImu(H);   // the prior the next frame would receive
+        write_bin(dir, "out_Hc", Hc.data(), 225);
+    } else {
+        n_good = opt.LastKeyFrame(frame, other, read_bin<float>(dir, "preint"), mono, stereo, outl, &H, m["rec_init"] != 0);
+    }
+    std::vector<double> Rc, tc;
+    for (int c = 0; c < C; ++c) Rc.insert(Rc.end(), frame.Rcw[c].begin(), frame.Rcw[c].end()), tc.insert(tc.end(), frame.tcw[c].begin(), frame.tcw[c].end());
+    write_bin(dir, "out_Rwb", frame.Rwb.data(), 9), write_bin(dir, "out_twb", frame.twb.data(), 3);
+    write_bin(dir, "out_vel", frame.vel.data(), 3), write_bin(dir, "out_bg", frame.bg.data(), 3);
+    write_bin(dir, "out_ba", frame.ba.data(), 3), write_bin(dir, "out_Rcw", Rc), write_bin(dir, "out_tcw", tc);
+    write_bin(dir, "out_kpo", outl), write_bin(dir, "out_H", H.data(), 225), write_bin(dir, "n_good", &n_good, 1);
+    return 0;
+}
+
+// Fuse(pKF, vpMapPoints, th, cameraID) for every camera block of one keyframe (one job list per block)
+int run_fuse(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["C"], cap = (int)m["kp_cap"], J = (int)m["n_jobs"];
+    omv_adapt::Fuse fuse(C, cap, (int)m["W"], (int)m["H"], read_bin<float>(dir, "scale_factors"), read_bin<float>(dir, "cams"),
+                         read_opt<int32_t>(dir, "cam_model"), (float)m["bf"], (int)m["max_points"]);
+    fuse.set_keyframe(read_bin<omv_kp>(dir, "kps"), read_bin<uint8_t>(dir, "desc"), read_bin<int32_t>(dir, "n_kp"),
+                      read_bin<float>(dir, "uright"));
+    const auto jc = read_bin<int32_t>(dir, "job_cam"), jn = read_bin<int32_t>(dir, "job_count");
+    const auto jT = read_bin<float>(dir, "job_Tcw"), jO = read_bin<float>(dir, "job_Ow");
+    const auto pos = read_bin<float>(dir, "mp_pos"), nrm = read_bin<float>(dir, "mp_normal");
+    const auto mind = read_bin<float>(dir, "mp_min_dist"), maxd = read_bin<float>(dir, "mp_max_dist");
+    const auto desc = read_bin<uint8_t>(dir, "mp_desc");
+    const auto ils = read_bin<float>(dir, "inv_level_sigma2");
+    std::vector<int32_t> all_idx, all_dist, nf;
+    size_t at = 0;
+    for (int j = 0; j < J; ++j) {
+        omv_adapt::FuseMapPoints mp;
+        const size_t n = (size_t)jn[j];
+        mp.pos.assign(&pos[3 * at], &pos[3 * (at + n)]), mp.normal.assign(&nrm[3 * at], &nrm[3 * (at + n)]);
+        mp.min_dist.assign(&mind[at], &mind[at + n]), mp.max_dist.assign(&maxd[at], &maxd[at + n]);
+        mp.desc.assign(&desc[32 * at], &desc[32 * (at + n)]);
+        std::vector<int32_t> bi, bd;
+        const omv_se3f T = se3_of(std::vector<float>(&jT[7 * j], &jT[7 * j + 7]));
+        nf.push_back(fuse(mp, jc[j], T, {jO[3 * j], jO[3 * j + 1], jO[3 * j + 2]}, (float)m["th"], ils, bi, bd));
+        all_idx.insert(all_idx.end(), bi.begin(), bi.end()), all_dist.insert(all_dist.end(), bd.begin(), bd.end());
+        at += n;
+    }
+    write_bin(dir, "best_idx", all_idx), write_bin(dir, "best_dist", all_dist), write_bin(dir, "n_fused", nf);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
     if (argc != 3) {
-        std::fprintf(stderr, "usage: %s orb|frame|lba DIR\n", argv[0]);
+        std::fprintf(stderr, "usage: %s orb|frame|lba|lastframe|tri|pose|fuse DIR\n", argv[0]);
         return 2;
     }
     try {
@@ -236,6 +404,10 @@ int main(int argc, char **argv) {
         if (mode == "orb") return run_orb(dir);
         if (mode == "frame") return run_frame(dir);
         if (mode == "lba") return run_lba(dir);
+        if (mode == "lastframe") return run_lastframe(dir);
+        if (mode == "tri") return run_tri(dir);
+        if (mode == "pose") return run_pose(dir);
+        if (mode == "fuse") return run_fuse(dir);
         std::fprintf(stderr, "unknown mode %s\n", argv[1]);
         return 2;
     } catch (const std::exception &e) {

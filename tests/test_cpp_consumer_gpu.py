@@ -196,3 +196,168 @@ def test_local_inertial_ba_window_rccl_single_rank(tmp_path, oracle):
     trials, calls, syncs = int(res["trials"]), int(res["allreduce_calls"]), int(res["host_syncs"])
     assert calls >= 2 * trials, (calls, trials)   # [blocks | b | rhs] and [chi(A), chi, computeScale] per step
     assert syncs <= (trials + 3) // 4 + 1 and (trials < 2 or syncs < trials), (syncs, trials)
+
+
+def _oracle_frame(oracle, imgs, cap):
+    kps = np.zeros((C, cap), oracle.KP_DTYPE)
+    desc = np.zeros((C, cap, 32), np.uint8)
+    n_kp = np.zeros(C, np.int32)
+    for c in range(C):
+        _, k, d = oracle.orb_extract(imgs[c], 1200, 1.2, 8, 15, 7, tuple(LAP[c]))
+        n_kp[c] = len(k)
+        kps[c, :len(k)], desc[c, :len(k)] = k, d
+    return kps, desc, n_kp
+
+
+def test_search_by_projection_last_frame_adapter(tmp_path, oracle):
+    """SearchByProjection(Frame&, const Frame& LastFrame, th, bMono) (ORBmatcher.cc:1985-2413) through the
+    SearchByProjectionLastFrame adapter on a MultiCameraFrame: assignments (LastFrame slots) and count bit-exact vs the
+    oracle, forward motion (level window) with the rotation-histogram filter."""
+    from openmavis_amd.orb import ORBextractor
+    imgs = synth.hilti_frame(44)
+    cap = ORBextractor(1200, 1.2, 8, 15, 7, width=W, height=H, max_images=C).max_keypoints()
+    kps, desc, n_kp = _oracle_frame(oracle, imgs, cap)
+    cams, R_cl, t_cl = synth.hilti_rig(C)
+    rng = np.random.default_rng(5)
+    Tcw = synth.random_se3(rng)
+    last = synth.make_last_frame(kps, desc, n_kp, 91, cams, Tcw)
+    Tlw = Tcw.copy()
+    Tlw[6] -= np.float32(0.5)
+    Trl = np.concatenate([synth.quat_from_R(R_cl[1].astype(np.float64)), t_cl[1]]).astype(np.float32)
+    occ = (rng.random(C * cap) < 0.03).astype(np.uint8)
+    mb = 0.11
+    _meta(tmp_path, C=C, W=W, H=H, nfeatures=1200, ini=15, min=7, last_cap=cap, nnratio=0.9, check_ori=1, th=7.0,
+          bmono=0, mb=mb)
+    _w(tmp_path, "images", imgs)
+    _w(tmp_path, "lapping", LAP)
+    _w(tmp_path, "cams", np.asarray(cams, np.float32))
+    _w(tmp_path, "Tcw", Tcw), _w(tmp_path, "Tlw", Tlw), _w(tmp_path, "Trl", Trl), _w(tmp_path, "occ", occ)
+    _w(tmp_path, "last_pos", last["pos"]), _w(tmp_path, "last_desc", last["desc"])
+    _w(tmp_path, "last_valid", last["valid"]), _w(tmp_path, "last_obs", last["has_obs"])
+    _w(tmp_path, "last_kps", last["kps"])
+    _run("lastframe", tmp_path)
+    got, n = _r(tmp_path, "kp_to_mp", np.int32), int(_r(tmp_path, "n_matches", np.int32)[0])
+    g = oracle.frame_geom(C, W, H, _scale_factors())
+    exp = np.full(C * cap, -1, np.int32)
+    n_o = oracle.search_last_frame(g, kps, desc, n_kp, cams, Tcw, Tlw, Trl, last["pos"], last["desc"], last["valid"],
+                                   last["has_obs"], last["kps"], 7.0, False, mb, True, occ, exp)
+    assert n == n_o and n > 200, (n, n_o)
+    assert np.array_equal(got, exp)
+
+
+def _scale_factors():
+    sf = [1.0]
+    for _ in range(7):
+        sf.append(float(np.float32(sf[-1] * 1.2)))   # mvScaleFactor: (float)(previous * scaleFactor)
+    return sf
+
+
+@pytest.mark.parametrize("model,check_ori,coarse", [("kb8", False, False), ("kb8", True, False), ("pinhole", False, True)])
+def test_search_for_triangulation_adapter(tmp_path, oracle, model, check_ori, coarse):
+    """SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse) (ORBmatcher.cc:1131-1456) through the
+    adapter: KeyFrameView (keypoints in [L|R|SL|SR] order, FeatureVector CSR) -> vMatchedPairs and the count, bit-exact vs
+    the oracle's vMatches12."""
+    from openmavis_amd import synth_tri
+    p = synth_tri.make_tri_pair(seed=21, n_pts=700, model=model)
+    meta = dict(check_ori=int(check_ori), coarse=int(coarse), only_stereo=0)
+    for k in ("kf1", "kf2"):
+        kf = p[k]
+        for f in ("n", "n_left", "n_right", "n_sideleft"):
+            meta[f"{k}_{f}"] = int(kf[f])
+        _w(tmp_path, f"{k}_kps", kf["kps"])
+        for f in ("desc", "has_mp", "node_id", "node_start", "node_idx"):
+            _w(tmp_path, f"{k}_{f}", kf[f])
+    _meta(tmp_path, **meta)
+    _w(tmp_path, "level_sigma2", np.asarray(p["level_sigma2"], np.float32))
+    _w(tmp_path, "T", np.asarray(p["T"], np.float32))
+    _w(tmp_path, "cams", np.asarray(p["cams"], np.float32))
+    if "cam_model" in p:
+        _w(tmp_path, "cam_model", np.asarray(p["cam_model"], np.int32))
+    _run("tri", tmp_path)
+    n = int(_r(tmp_path, "n_matches", np.int32)[0])
+    pairs = _r(tmp_path, "pairs", np.int64).reshape(-1, 2)
+    n_o, m_o = oracle.search_for_triangulation(p, coarse=coarse, check_ori=check_ori)
+    exp = np.stack([np.nonzero(m_o >= 0)[0], m_o[m_o >= 0]], 1) if (m_o >= 0).any() else np.zeros((0, 2), np.int64)
+    assert n == n_o and n > 20, (n, n_o)
+    assert np.array_equal(pairs, exp)
+
+
+POSE_KEYS = ("cam", "Rcb", "tcb", "Rbc", "tbc", "Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb",
+             "kf_vel", "kf_bg", "kf_ba", "preint", "mono_cam", "mono_kp", "mono_obs", "mono_inv_sigma2", "mono_xw",
+             "mono_close")
+
+
+@pytest.mark.parametrize("lf,stereo,rec_init", [(False, 0.0, False), (False, 0.3, False), (True, 0.3, False),
+                                                (True, 0.0, True)])
+def test_pose_inertial_optimizer_adapter(tmp_path, oracle, lf, stereo, rec_init):
+    """PoseInertialOptimizationLastKeyFrame / LastFrame (Optimizer.cc:5021, :5580) through the PoseInertialOptimizer
+    adapter on ONE frame (Tracking's call; the grouped kernel): state within 1e-7, mvbOutlier and the return value
+    exact, the Hessian within 1e-6 relative -- the bar of tests/test_pose_gpu.py; LastFrame also the ConstraintPoseImu
+    of its marginal within 1e-9 relative."""
+    from openmavis_amd import synth_pose
+    mk = synth_pose.make_last_frame_batch if lf else synth_pose.make_pose_batch
+    b = mk(n_frames=1, n_pts=800, seed=13, outlier_frac=0.12, stereo_frac=stereo)
+    _meta(tmp_path, n_cams=int(b["n_cams"]), lf=int(lf), rec_init=int(rec_init), bf=float(b["bf"]), kp_cap=int(b["kp_cap"]))
+    for k in POSE_KEYS:
+        _w(tmp_path, k, np.asarray(b[k]))
+    if len(b["stereo_cam"]):
+        for k in ("stereo_cam", "stereo_kp", "stereo_obs", "stereo_inv_sigma2", "stereo_xw"):
+            _w(tmp_path, k, np.asarray(b[k]))
+    if lf:
+        for k in ("prior_Rwb", "prior_twb", "prior_vel", "prior_bg", "prior_ba", "prior_H", "preint_kf"):
+            _w(tmp_path, k, np.asarray(b[k]))
+    _run("pose", tmp_path)
+    st_o, k_o, n_o, H_o = (oracle.pose_last_frame if lf else oracle.pose_last_kf)(b, rec_init)
+    assert int(_r(tmp_path, "n_good", np.int32)[0]) == int(n_o[0])
+    kpo = _r(tmp_path, "out_kpo", np.uint8)
+    has_edge = np.zeros(int(b["kp_cap"]), bool)
+    has_edge[b["mono_kp"]] = True
+    if len(b["stereo_kp"]):
+        has_edge[b["stereo_kp"]] = True
+    assert np.array_equal(kpo[has_edge], k_o[0][has_edge]) and (kpo[~has_edge] == 255).all()
+    R = _r(tmp_path, "out_Rwb", np.float64).reshape(3, 3)
+    ang = np.degrees(np.linalg.norm(synth_ba._log(R.T @ st_o["Rwb"][0])))
+    assert ang < 1e-7, ang
+    for k in ("twb", "vel", "bg", "ba", "tcw"):
+        assert np.abs(_r(tmp_path, "out_" + k, np.float64) - st_o[k][0].ravel()).max() < 1e-7, k
+    H = _r(tmp_path, "out_H", np.float64)
+    assert np.abs(H - H_o[0]).max() <= 1e-6 * np.abs(H_o[0]).max()
+    if lf:
+        Hc = _r(tmp_path, "out_Hc", np.float64)
+        o = oracle.pose_constraint(H_o[:1])[0]
+        assert np.abs(Hc - o).max() <= 1e-6 * np.abs(o).max()
+
+
+def test_fuse_adapter(tmp_path, oracle):
+    """ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID) (ORBmatcher.cc:1458-1647) through the Fuse adapter, one call per
+    camera block of a keyframe: per map point the chosen keypoint (N-index) and distance, and nFused, bit-exact vs the
+    oracle."""
+    from openmavis_amd import synth_kfmatch as sk
+    b = sk.make_kf_search(0, seed=5)
+    th, md = sk.MODE_PARAMS[0]
+    bi_o, bd_o, n_o, _ = oracle.search_kf(b, th, md)
+    jobs = [(i, j) for i, j in enumerate(b["jobs"]) if j["kf"] == 0]
+    K, cap = 0, int(b["kp_cap"])
+    rows = np.concatenate([b["mp_list"][j["mp_start"]:j["mp_start"] + j["mp_count"]] for _, j in jobs])
+    scale = _scale_factors()
+    ils = [float(np.float32(1.0) / np.float32(np.float32(s) * np.float32(s))) for s in scale]
+    _meta(tmp_path, C=int(b["n_cams"]), kp_cap=cap, W=int(b["width"]), H=int(b["height"]), bf=float(b["bf"]), th=th,
+          n_jobs=len(jobs), max_points=len(rows))
+    _w(tmp_path, "scale_factors", np.asarray(scale, np.float32))
+    _w(tmp_path, "inv_level_sigma2", np.asarray(ils, np.float32))
+    _w(tmp_path, "cams", np.asarray(b["cams"], np.float32))
+    if b.get("cam_model") is not None:
+        _w(tmp_path, "cam_model", np.asarray(b["cam_model"], np.int32))
+    _w(tmp_path, "kps", b["kps"][K]), _w(tmp_path, "desc", b["desc"][K]), _w(tmp_path, "n_kp", b["n_kp"][K])
+    _w(tmp_path, "uright", b["uright"][K])
+    _w(tmp_path, "job_cam", np.array([j["cam"] for _, j in jobs], np.int32))
+    _w(tmp_path, "job_count", np.array([j["mp_count"] for _, j in jobs], np.int32))
+    _w(tmp_path, "job_Tcw", np.stack([np.asarray(j["Tcw"], np.float32) for _, j in jobs]))
+    _w(tmp_path, "job_Ow", np.stack([np.asarray(j["Ow"], np.float32) for _, j in jobs]))
+    for k in ("pos", "normal", "min_dist", "max_dist", "desc"):
+        _w(tmp_path, "mp_" + k, b["mps"][k][rows])
+    _run("fuse", tmp_path)
+    bi, bd, nf = _r(tmp_path, "best_idx", np.int32), _r(tmp_path, "best_dist", np.int32), _r(tmp_path, "n_fused", np.int32)
+    ent = np.concatenate([np.arange(j["mp_start"], j["mp_start"] + j["mp_count"]) for _, j in jobs])
+    assert np.array_equal(bi, bi_o[ent]) and np.array_equal(bd, bd_o[ent])
+    assert np.array_equal(nf, n_o[[i for i, _ in jobs]]) and nf.sum() > 30

@@ -9,6 +9,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("OMV_LIB"):   # e.g. the -DOMV_POSE_PROFILE variant of the library
+    from openmavis_amd import _lib  # noqa: E402
+    _lib.load(os.environ["OMV_LIB"])
 
 
 def main():
@@ -17,6 +20,7 @@ def main():
     ap.add_argument("--stereo", type=float, default=0.0)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--parts", default="0,2,4,8")
+    ap.add_argument("--modes", default="batch,grouped")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -35,8 +39,8 @@ def main():
         opt = PoseInertialOptimizer(max_frames=1, max_edges=max(len(b["mono_cam"]), len(b["stereo_cam"]), 1))
         fn = opt.PoseInertialOptimizationLastFrame if lf else opt.PoseInertialOptimizationLastKeyFrame
         s = torch.cuda.current_stream()
-        modes = [("batch", PoseInertialOptimizer.BATCH, 0)] + [
-            (f"grouped{p}", PoseInertialOptimizer.GROUPED, int(p)) for p in a.parts.split(",")]
+        modes = ([("batch", PoseInertialOptimizer.BATCH, 0)] if "batch" in a.modes else []) + ([
+            (f"grouped{p}", PoseInertialOptimizer.GROUPED, int(p)) for p in a.parts.split(",")] if "grouped" in a.modes else [])
         for name, mode, parts in modes:
             opt.set_mode(mode, parts)
             for _ in range(3):
