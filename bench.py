@@ -1029,7 +1029,11 @@ def cam_shard_leg(imgs, B, steps, warmup, dev, world, rank):
 def latency_leg(d_img, gr0, n_frames, dev, rig, stereo):
     """Single-frame latency of the sequential tracker (frame t+1's search needs frame t's pose): one multi-camera
     frame at a time on one stream (B = 1), extract + grid + lapping knn + TriangulateMatches + mvuRight +
-    isInFrustum + SearchByProjection, synchronised per frame; p50 / p99 of the per-frame wall time."""
+    isInFrustum + SearchByProjection, then the pose graph's edges from SearchByProjection's assignment and
+    PoseInertialOptimizationLastFrame + ConstraintPoseImu (Tracking::TrackLocalMap's optimisation), all on the
+    device, synchronised per frame; p50 / p99 of the per-frame wall time, with and without the optimisation.
+    The optimisation's frame state / previous frame / prior / preintegration are synthetic (synth_pose's
+    trajectory), the local map moved rigidly so the frame's block-0 camera sits at the true body pose."""
     import torch
     from openmavis_amd.frame import frame_uright
     from openmavis_amd.matcher import FrameBatch, MapPointBatch, ORBmatcher, isInFrustum
@@ -1046,10 +1050,46 @@ def latency_leg(d_img, gr0, n_frames, dev, rig, stereo):
                            mps=MapPointBatch(**{k: getattr(gr0["mps"], k)[f:f + 1].clone()
                                                 for k in MapPointBatch.FIELDS}),
                            depth=gr0["depth"][f:f + 1].contiguous()))
-    ur = torch.empty((1, min(4, C), cap), dtype=torch.float32, device=dev)
+    from openmavis_amd import synth_pose
+    from openmavis_amd.optimizer import PoseInertialOptimizer
+    NB = min(4, C)
+    ur_full = torch.full((C, cap), -1.0, dtype=torch.float32, device=dev)   # mvuRight [C][cap]; blocks >= 4: -1
+    ur = ur_full[:NB].view(1, NB, cap)
     Rlr, tlr, BF, sigma2, cams_r = stereo
+    E = C * cap
+    popt = PoseInertialOptimizer(max_frames=1, max_edges=E)
+    edges = PoseInertialOptimizer.edge_arrays(E, dev)
+    inv_s2 = [float(1.0 / x) for x in sigma2]
+    kpo = torch.zeros((1, C * cap), dtype=torch.uint8, device=dev)
+    Hm = torch.zeros((1, 225), dtype=torch.float64, device=dev)
+    Hc = torch.zeros((1, 225), dtype=torch.float64, device=dev)
+    for f, fr in enumerate(frames):
+        b = synth_pose.make_last_frame_batch(n_frames=1, n_pts=8, seed=100 + f, n_cams=C)
+        b["bf"] = np.float32(BF)
+        b["kp_cap"] = C * cap
+        b["mono_cam"] = b["stereo_cam"] = np.zeros(E, np.int32)   # edge-list bounds (counts live on the device)
+        Rwb, twb = np.asarray(b["true_Rwb"][0]), np.asarray(b["true_twb"][0])
+        Rwc = Rwb @ b["Rbc"][0]
+        twc = Rwb @ b["tbc"][0] + twb
+        po = fr["pose"][0].cpu().numpy().astype(np.float64)
+        R_no = Rwc @ po[:9].reshape(3, 3)
+        t_no = Rwc @ po[9:12] + twc
+        pos = fr["world"]["pos"][0].cpu().numpy().astype(np.float64)
+        arrays = dict(edges)
+        for k in synth_pose.STATE_KEYS:
+            arrays[k] = torch.tensor(np.asarray(b[k], np.float64), device=dev).contiguous()
+        for k in synth_pose.INPUT_KEYS[:6] + synth_pose.PRIOR_KEYS:
+            arrays[k] = torch.from_numpy(np.ascontiguousarray(b[k])).to(dev)
+        fr.update(pose_batch=b, pose_arrays=arrays,
+                  mp_pos=torch.from_numpy((pos @ R_no.T + t_no).astype(np.float32)).to(dev))
 
-    def one(fr):
+    def pose(fr):
+        popt.EdgesFromMatches(fb.kps[0], fb.n_kp[0], fb.kp_to_mp[0], fr["mp_pos"], fr["mps"].track_depth[0], inv_s2,
+                              edges, uright=ur_full)
+        popt.PoseInertialOptimizationLastFrame(fr["pose_batch"], fr["pose_arrays"], kpo, Hm)
+        PoseInertialOptimizer.ConstraintPoseImu(Hm, out=Hc)
+
+    def one(fr, with_pose=True):
         ex.extract_batch(fr["img"], LAP, fb.kps.view(-1, cap, 6), fb.desc.view(-1, cap, 32), fb.n_kp.view(-1),
                          fb.mono.view(-1))
         fb.kp_to_mp.fill_(-1)
@@ -1059,21 +1099,35 @@ def latency_leg(d_img, gr0, n_frames, dev, rig, stereo):
         frame_uright(fb, fr["depth"], BF, out=ur)
         isInFrustum(fr["pose"], rig, fr["world"], fr["mps"], 0.5)
         m.SearchByProjection(fb, fr["mps"], TH, False, 50.0, grid_ready=True)
+        if with_pose:
+            pose(fr)
 
-    for i in range(5):
-        one(frames[i % n_avail])
-    torch.cuda.synchronize(dev)
-    lat = []
-    for i in range(n_frames):
-        t0 = time.perf_counter()
-        one(frames[i % n_avail])
+    def run(with_pose):
+        for i in range(5):
+            one(frames[i % n_avail], with_pose)
         torch.cuda.synchronize(dev)
-        lat.append((time.perf_counter() - t0) * 1e3)
-    lat = np.array(lat)
+        lat = []
+        for i in range(n_frames):
+            t0 = time.perf_counter()
+            one(frames[i % n_avail], with_pose)
+            torch.cuda.synchronize(dev)
+            lat.append((time.perf_counter() - t0) * 1e3)
+        return np.array(lat)
+
+    lat = run(True)
+    if popt.last_error() != 0:
+        raise RuntimeError("latency leg: pose edge / optimisation capacity error")
+    n_edges = [int(x) for x in (edges["mono_start"][1].item(), edges["stereo_start"][1].item())]
+    lat0 = run(False)
     return {"metric": "single-frame latency (B=1, one stream, synchronised per frame)", "unit": "ms",
+            "chain": "extract + grid + lapping knn + TriangulateMatches + mvuRight + isInFrustum + SearchByProjection "
+                     "+ edges from matches + PoseInertialOptimizationLastFrame + ConstraintPoseImu",
             "p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
             "mean_ms": round(float(lat.mean()), 4), "frames": n_frames,
-            "sequential_frames_per_s": round(1e3 / float(np.percentile(lat, 50)), 1)}
+            "sequential_frames_per_s": round(1e3 / float(np.percentile(lat, 50)), 1),
+            "last_frame_edges": {"mono": n_edges[0], "stereo": n_edges[1]},
+            "without_pose": {"p50_ms": round(float(np.percentile(lat0, 50)), 4),
+                             "p99_ms": round(float(np.percentile(lat0, 99)), 4)}}
 
 
 def _slab_mode():

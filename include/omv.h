@@ -672,7 +672,7 @@ omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, co
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream);
 
 /* Kernel choice of the two calls above.  OMV_POSE_AUTO (default): up to 16 frames per call run on the grouped
- * kernel — one frame over `parts` workgroups (0: one per 256 visual edges, at most 8) that exchange their
+ * kernel — one frame over `parts` workgroups (0: one per 128 (LastFrame) / 192 visual edges, at most 32) that exchange their
  * normal-equation sums every Gauss-Newton iteration, the latency path of Tracking's one-frame call — and larger batches
  * on one workgroup per frame.  OMV_POSE_BATCH / OMV_POSE_GROUPED force one of them (GROUPED needs kp_cap <= 16384).
  * The grouped kernel reports a frame it could not run (more than 1024 visual edges in one workgroup's keypoint
@@ -684,6 +684,25 @@ omv_status omv_pose_set_mode(omv_pose *h, int mode, int parts);
 /* Device error word of the calls since the last read (0, or OMV_ERR_CAPACITY / OMV_ERR_HIP from the grouped kernel);
  * resets it and synchronises `stream`. */
 omv_status omv_pose_last_error(omv_pose *h, int32_t *err, void *stream);
+
+/* The pose graph's visual edges of ONE frame from its map-point assignment, on the device — the edge-creation loop
+ * of PoseInertialOptimizationLastKeyFrame / LastFrame (src/Optimizer.cc:5079-5330, :5640-5800) for the multi-camera
+ * frame (bRight), so SearchByProjection's output feeds the optimisation without a host round trip: per keypoint slot
+ * s = cam * kp_cap + i (the [L | R | SL | SR] order) with kp_to_mp[s] >= 0 an EdgeMonoOnlyPose of block cam (obs =
+ * keypoint, invSigma2 = inv_level_sigma2[octave] (uncertainty2 = 1 for KannalaBrandt8 / Pinhole), Xw =
+ * mp_pos[kp_to_mp[s]], bClose = mp_track_depth < 10), and with uright[s] > 0 also an EdgeStereoOnlyPose of that
+ * block; both lists in slot order, counts in mono_start[1] / stereo_start[1] (start[0] = 0) — the omv_pose_batch edge
+ * arrays of a one-frame batch (pass max_edges as its n_mono / n_stereo bound; the batch's kp_cap = n_cams * kp_cap).
+ * kps / n_kp / kp_to_mp / mp_* / uright: device (uright [n_cams][kp_cap], omv_frame_uright's layout, or NULL = no
+ * stereo edges); inv_level_sigma2: host [n_levels].  More than max_edges edges of a kind
+ * raise OMV_ERR_CAPACITY in omv_pose_last_error.  Asynchronous. */
+omv_status omv_pose_edges_from_matches(omv_pose *h, int n_cams, int kp_cap, const omv_kp *kps, const int *n_kp,
+                                       const int32_t *kp_to_mp, const float *mp_pos, const float *mp_track_depth,
+                                       const float *inv_level_sigma2, int n_levels, const float *uright, int max_edges,
+                                       int32_t *mono_start, int32_t *mono_cam, int32_t *mono_kp, double *mono_obs,
+                                       float *mono_inv_sigma2, float *mono_xw, uint8_t *mono_close, int32_t *stereo_start,
+                                       int32_t *stereo_cam, int32_t *stereo_kp, double *stereo_obs,
+                                       float *stereo_inv_sigma2, float *stereo_xw, void *stream);
 
 /* ConstraintPoseImu ctor (include/G2oTypes.h:639-659) on n matrices: H <- (H + H) / 2 (= H), then its
  * symmetric eigen-decomposition with eigenvalues below 1e-12 zeroed, recomposed.  Device [n][225]

@@ -272,6 +272,7 @@ SIGNATURES = {
                                           _VP, _VP]),
     "omv_pose_constraint": (_I, [_I, _VP, _VP, _VP]),
     "omv_pose_set_mode": (_I, [_VP, _I, _I]),
+    "omv_pose_edges_from_matches": (_I, [_VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _I] + [_VP] * 14),
     "omv_pose_last_error": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), _VP]),
     "omv_matcher_search_kf": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(KfSearchJob),
                                    _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,

@@ -596,6 +596,160 @@ __device__ inline void sym_eig_wave(double *A, double *V, int lane) {
     }
 }
 
+// The same eigen-decomposition in parallel order: per sweep NP - 1 rounds of a round-robin tournament over the
+// (even-padded) indices, each round NP / 2 disjoint rotations at once (angles from the round-start matrix, by the
+// same formula as sym_eig_wave), then all their column updates (A and V), then all their row updates -- a
+// rotation order different from the cyclic one, so the result differs from sym_eig_wave's by rounding only.
+// cs / pq: LDS scratch [NP] doubles / [NP] ints.  Every lane of the wave must call it.
+template <int N>
+__device__ inline void sym_eig_wave_par(double *A, double *V, double *cs, int *pq, int lane) {
+    static_assert(N <= 64, "one row per lane");
+    constexpr int NP = (N + 1) & ~1, HP = NP / 2;
+    for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0, dg = 0;   // converged: off-diagonal mass below 1e-32 of the diagonal's
+        for (int e = lane; e < N * N; e += 64) {
+            const int r = e / N, c = e - (e / N) * N;
+            const double v = A[e];
+            if (r == c) dg += v * v;
+            else if (c > r) off += v * v;
+        }
+        for (int d = 32; d >= 1; d >>= 1) off += __shfl_xor(off, d, 64), dg += __shfl_xor(dg, d, 64);
+        if (off <= 1e-32 * dg || off < 1e-300) break;
+        for (int round = 0; round < NP - 1; ++round) {
+            if (lane < HP) {
+                const int a = lane == 0 ? 0 : (round + lane - 1) % (NP - 1) + 1;
+                const int bpos = NP - 1 - lane, b = (round + bpos - 1) % (NP - 1) + 1;
+                const int p = min(a, b), q = max(a, b);
+                double c = 1.0, sn = 0.0;
+                int qq = N;   // dummy pair (padding index) or a zero entry: no rotation
+                if (q < N) {
+                    const double apq = A[p * N + q];
+                    if (apq != 0) {
+                        const double th = (A[q * N + q] - A[p * N + p]) / (2 * apq);
+                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+                        c = 1 / sqrt(t * t + 1), sn = t * c;
+                        qq = q;
+                    }
+                }
+                cs[2 * lane] = c, cs[2 * lane + 1] = sn, pq[2 * lane] = p, pq[2 * lane + 1] = qq;
+            }
+            wave_lds_sync();
+            for (int tk = lane; tk < HP * N; tk += 64) {   // columns p, q of A and V
+                const int i = tk / N, k = tk - (tk / N) * N;
+                const int p = pq[2 * i], q = pq[2 * i + 1];
+                if (q >= N) continue;
+                const double c = cs[2 * i], sn = cs[2 * i + 1];
+                const double akp = A[k * N + p], akq = A[k * N + q];
+                A[k * N + p] = c * akp - sn * akq, A[k * N + q] = sn * akp + c * akq;
+                const double vkp = V[k * N + p], vkq = V[k * N + q];
+                V[k * N + p] = c * vkp - sn * vkq, V[k * N + q] = sn * vkp + c * vkq;
+            }
+            wave_lds_sync();
+            for (int tk = lane; tk < HP * N; tk += 64) {   // rows p, q of A
+                const int i = tk / N, k = tk - (tk / N) * N;
+                const int p = pq[2 * i], q = pq[2 * i + 1];
+                if (q >= N) continue;
+                const double c = cs[2 * i], sn = cs[2 * i + 1];
+                const double apk = A[p * N + k], aqk = A[q * N + k];
+                A[p * N + k] = c * apk - sn * aqk, A[q * N + k] = sn * apk + c * aqk;
+            }
+            wave_lds_sync();
+        }
+    }
+}
+
+// LDL^T without pivoting of the symmetric N x N A - shift I (LDS, row-major), one wavefront (lane = row, the row in
+// registers, v_readlane broadcasts of the pivot row).  True iff every pivot is > 0; then, when L is given, the factor
+// is stored there (strict lower triangle L, D on the diagonal).  All lanes get the same verdict.
+template <int N>
+__device__ inline bool ldl_nopiv_wave(const double *A, double shift, double *L, int lane) {
+    static_assert(N <= 32, "rows on lanes 0..31");
+    const bool in = lane < N;
+    double r[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) r[j] = in ? A[lane * N + j] - (j == lane ? shift : 0.0) : 0.0;
+    bool pos = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const double d = lane_f64(r[k], k);
+        pos = pos && d > 0.0;
+        const double inv = d > 0.0 ? 1.0 / d : 0.0;
+        const bool below = lane > k;
+        const double l = below ? r[k] * inv : 0.0;
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) r[j] = r[j] - l * lane_f64(r[j], k);
+        r[k] = below ? l : r[k];
+    }
+    if (pos && L && in) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) L[lane * N + j] = r[j];
+    }
+    wave_lds_sync();
+    return pos;
+}
+
+// X = A^-1 (N x N, LDS) from ldl_nopiv_wave's factor L: lane m solves column m (L D L^T x = e_m), the factor read by
+// broadcast LDS loads.
+template <int N>
+__device__ inline void ldl_inverse_wave(const double *L, double *X, int lane) {
+    if (lane < N) {
+        double y[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double t = i == lane ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < i; ++k) t -= L[i * N + k] * y[k];
+            y[i] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) y[i] = y[i] / L[i * N + i];
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {
+            double t = y[i];
+#pragma unroll
+            for (int k = i + 1; k < N; ++k) t -= L[k * N + i] * y[k];
+            y[i] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) X[i * N + lane] = y[i];
+    }
+    wave_lds_sync();
+}
+
+// Largest |diagonal| of the N x N A (wave-uniform).
+template <int N>
+__device__ inline double max_abs_diag(const double *A, int lane) {
+    double m = lane < N ? fabs(A[lane * (N + 1)]) : 0.0;
+    for (int d = 32; d >= 1; d >>= 1) m = fmax(m, __shfl_xor(m, d, 64));
+    return m;
+}
+
+// P = pinv(A) of the symmetric 15 x 15 A (LDS; overwritten) with eigenvalues |w| <= 1e-6 dropped (Marginalize,
+// Optimizer.cc:3388-3455), one wavefront.  When A - tau I factors with positive pivots (tau = 1e-6 plus a margin for
+// the factorisation's rounding), every eigenvalue exceeds 1e-6 and pinv(A) = A^-1: LDL^T and 15 triangular solves.
+// Otherwise the Jacobi eigen-decomposition and V diag(1/w over |w| > 1e-6) V^T.  The two agree up to rounding.
+// V: LDS [225] scratch; cs / pq: sym_eig_wave_par's scratch.
+__device__ inline void pinv15_wave(double *A, double *V, double *P, double *cs, int *pq, int lane) {
+    const double tau = 1e-6 + 1e-12 * max_abs_diag<15>(A, lane);
+    if (ldl_nopiv_wave<15>(A, tau, nullptr, lane) && ldl_nopiv_wave<15>(A, 0.0, V, lane)) {
+        ldl_inverse_wave<15>(V, P, lane);
+        return;
+    }
+    sym_eig_wave_par<15>(A, V, cs, pq, lane);
+    for (int q = lane; q < 225; q += 64) {
+        const int r = q / 15, c = q % 15;
+        double s = 0;
+        for (int k = 0; k < 15; ++k) {
+            const double w = A[k * 16];
+            s += V[r * 15 + k] * (fabs(w) > 1e-6 ? 1.0 / w : 0.0) * V[c * 15 + k];
+        }
+        P[q] = s;
+    }
+    wave_lds_sync();
+}
+
 // EdgePriorPoseImu::computeError / linearizeOplus (G2oTypes.cc:758-785) at the vertex state (R, t, v, bg, ba)
 // against the ConstraintPoseImu state pr = [Rwb 9 | twb 3 | vwb 3 | bg 3 | ba 3]; J (15x15 over pose 6,
 // v 3, bg 3, ba 3) may be null.
@@ -624,7 +778,10 @@ __device__ inline void prior_error_jac(const double *pr, const double *R, const 
 // EdgeInertial's information (ctor, G2oTypes.cc:486-495): Info = C[0:9,0:9]^-1, symmetrised, projected onto
 // its non-negative eigen-space (eigenvalues < 1e-12 zeroed) — Gauss-Jordan with partial pivoting and cyclic
 // Jacobi, per element the same operations in the same order as lba.hip's host path and the oracle, spread
-// over one wavefront (lane = row / column index).  sm: 243 doubles of LDS (A | I | V).  Every lane of the wave must call it.
+// over one wavefront (lane = row / column index).  sm: 243 doubles of LDS (A | I | V) + 10 (kPar: the parallel-order
+// Jacobi's scratch).  kPar: sym_eig_wave_par instead of the cyclic order (equal up to rounding; the pose path, where
+// this runs per call on the latency chain).  Every lane of the wave must call it.
+template <bool kPar = false>
 __device__ inline void inertial_info9_wave(const float *C15, double *out, double *sm, int lane) {
     double *A = sm, *I = sm + 81, *V = sm + 162;
     for (int q = lane; q < 81; q += 64) {
@@ -661,7 +818,17 @@ __device__ inline void inertial_info9_wave(const float *C15, double *out, double
     wave_lds_sync();
     for (int q = lane; q < 81; q += 64) I[q] = A[q];
     wave_lds_sync();
-    sym_eig_wave<9>(I, V, lane);
+    if constexpr (kPar) {
+        // every eigenvalue above the 1e-12 cut (I - tau I factors with positive pivots): the projection is I itself
+        const double tau = 1e-12 + 1e-12 * max_abs_diag<9>(I, lane);
+        if (ldl_nopiv_wave<9>(I, tau, nullptr, lane)) {
+            for (int q = lane; q < 81; q += 64) out[q] = I[q];
+            return;
+        }
+        sym_eig_wave_par<9>(I, V, sm + 243, reinterpret_cast<int *>(sm + 253), lane);
+    } else {
+        sym_eig_wave<9>(I, V, lane);
+    }
     for (int q = lane; q < 81; q += 64) {
         const int r = q / 9, c = q % 9;
         double s = 0;

@@ -83,11 +83,11 @@ struct PoseArgs {
 // :5960-5971 from `preint_rw`), one wavefront per frame: kept out of the optimisation kernel so its
 // Jacobi sweeps do not size that kernel's registers.
 __global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, const float *preint_rw, double *info) {
-    __shared__ double sm[243];
+    __shared__ double sm[243 + 10 + 5];
     const int f = blockIdx.x, lane = threadIdx.x;
     const float *pre = preint + (size_t)f * kPF, *prw = preint_rw + (size_t)f * kPF;
     double *o = info + (size_t)f * 99;
-    inertial_info9_wave(pre + PreView::C, o, sm, lane);
+    inertial_info9_wave<true>(pre + PreView::C, o, sm, lane);
     if (lane == 0) {
         double g[9], a[9];
         for (int r = 0; r < 3; ++r)
@@ -99,14 +99,22 @@ __global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, cons
 }
 
 // ConstraintPoseImu ctor (G2oTypes.h:639-659), one wavefront per matrix: (H + H) / 2, eigenvalues < 1e-12
-// zeroed, V diag(w) V^T.
+// zeroed, V diag(w) V^T (a positive definite matrix with every eigenvalue above the cut passes unchanged).
 __global__ void __launch_bounds__(64) pose_constraint_kernel(const double *Hin, double *Hout) {
-    __shared__ double A[225], V[225];
+    __shared__ double A[225], V[225], cs[16];
+    __shared__ int pq[16];
     const int f = blockIdx.x, lane = threadIdx.x;
     const double *hi = Hin + (size_t)f * 225;
     for (int q = lane; q < 225; q += 64) A[q] = (hi[q] + hi[q]) / 2;
     wave_lds_sync();
-    sym_eig_wave<15>(A, V, lane);
+    // Every eigenvalue above 1e-12 (A - tau I factors with positive pivots, tau = 1e-12 plus a margin for the
+    // factorisation's rounding): the projection is A itself (V diag(w) V^T = A up to rounding)
+    const double tau = 1e-12 + 1e-12 * max_abs_diag<15>(A, lane);
+    if (ldl_nopiv_wave<15>(A, tau, nullptr, lane)) {
+        for (int q = lane; q < 225; q += 64) Hout[(size_t)f * 225 + q] = A[q];
+        return;
+    }
+    sym_eig_wave_par<15>(A, V, cs, pq, lane);
     double out[4];
     for (int q = lane, i = 0; q < 225; q += 64, ++i) {
         const int r = q / 15, c = q % 15;
@@ -270,7 +278,8 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
     __shared__ int k1s, k2s;
     // EdgePriorPoseImu: ConstraintPoseImu state / information, error, Jacobian, H_prior J, H_prior e
     __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1];
-    __shared__ double Am[NP], Vm[NP];   // Marginalize's eigen-decomposition
+    __shared__ double Am[NP], Vm[NP], ecs[16];   // Marginalize's eigen-decomposition
+    __shared__ int epq[16];
     if (tid == 0) {
         for (int q = 0; q < 9; ++q) sRwb[q] = A.kRwb[9 * f + q], sRwb[9 + q] = A.Rwb[9 * f + q];
         for (int q = 0; q < 3; ++q) {
@@ -632,17 +641,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
             __syncthreads();
             for (int q = tid; q < 225; q += kPoseThreads) Am[q] = Hs[(15 + q / 15) * N + 15 + q % 15];
             __syncthreads();
-            if (tid < 64) sym_eig_wave<15>(Am, Vm, tid);
-            __syncthreads();
-            for (int q = tid; q < 225; q += kPoseThreads) {   // pinv(H_pp) -> PJ
-                const int r = q / 15, c = q % 15;
-                double s = 0;
-                for (int k = 0; k < 15; ++k) {
-                    const double w = Am[k * 16];
-                    s += Vm[r * 15 + k] * (fabs(w) > 1e-6 ? 1.0 / w : 0.0) * Vm[c * 15 + k];
-                }
-                PJ[q] = s;
-            }
+            if (tid < 64) pinv15_wave(Am, Vm, PJ, ecs, epq, tid);   // pinv(H_pp) -> PJ
             __syncthreads();
             for (int q = tid; q < 225; q += kPoseThreads) {   // T = H_fp pinv(H_pp) -> JPr
                 const int i = q / 15, j = q % 15;
@@ -727,7 +726,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
 constexpr int kLatThreads = 256;        // one wave per SIMD (512 registers): visual edges on 3 (LastFrame 2) waves, then
                                         // EdgeInertial, then (LastFrame) EdgePriorPoseImu on a wave of its own
 __host__ __device__ constexpr int lat_edge_threads(bool lf) { return lf ? 128 : 192; }
-constexpr int kLatMaxParts = 8;         // workgroups per frame
+constexpr int kLatMaxParts = 32;        // workgroups per frame
 constexpr int kLatCap = 1024;           // visual edges per workgroup (LDS)
 constexpr int kLatFlagCap = 16384;      // keypoints per frame (mvbOutlier staged in LDS)
 constexpr int kGran = 64;               // 8-byte granules per (frame, slot, part)
@@ -744,9 +743,11 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 // Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q): publish this part's values as
 // 2n granules of slot (phase & 1), sweep all G x 2n granules until every tag equals salt | phase, add the parts in part
-// order into out[0..n) (LDS).  One wavefront; false on a bounded-spin timeout (a missing sibling workgroup).
-__device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n, uint32_t *sc,
-                             double *out, int lane) {
+// order into out[0..n) (LDS).  One wavefront; false on a bounded-spin timeout (a missing sibling workgroup).  L: sweep
+// loads per lane, every one issued before the first tag compare (>= ceil(G * 2n / 64)).
+template <int L>
+__device__ __forceinline__ bool lat_exchange_l(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
+                                               uint32_t *sc, double *out, int lane) {
     const uint32_t tag = salt | (uint32_t)phase;
     gu64 *slot = fb + (size_t)(phase & 1) * kLatMaxParts * kGran;
     if (lane < n) {
@@ -757,25 +758,23 @@ __device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const int per = 2 * n, M = G * per;
-    uint32_t val[8];
+    uint32_t val[L];
     for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int i = lane + 64 * m;
-            if (i < M) {
-                const int p = i / per, w = i - p * per;
-                const unsigned long long x = __hip_atomic_load(slot + p * kGran + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                val[m] = (uint32_t)x;
-                ok &= (uint32_t)(x >> 32) == tag;
-            }
+        for (int m = 0; m < L; ++m) {
+            const int i = min(lane + 64 * m, M - 1);   // past M: a repeat of the last granule (no branch between loads)
+            const int p = i / per, w = i - p * per;
+            const unsigned long long x = __hip_atomic_load(slot + p * kGran + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            val[m] = (uint32_t)x;
+            ok &= (uint32_t)(x >> 32) == tag;
         }
         if (__all(ok)) break;
         if (spins > (1u << 22)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    for (int m = 0; m < L; ++m) {
         const int i = lane + 64 * m;
         if (i < M) {
             const int p = i / per, w = i - p * per;
@@ -792,6 +791,12 @@ __device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt,
     wave_lds_sync();
     return true;
 }
+// One out-of-line copy (three call sites; the inlined sweeps were a sixth of the kernel's code, and the kernel's
+// per-iteration code must stay within the CU's instruction cache).  Loads past G x 2n repeat the last granule.
+__device__ __attribute__((noinline)) bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
+                                                       uint32_t *sc, double *out, int lane) {
+    return lat_exchange_l<(kLatMaxParts * kGran) / 64>(fb, phase, salt, g, G, v, n, sc, out, lane);
+}
 
 // Eigen::LDLT<MatrixXd> (ldlt_inplace::unblocked's pivot order, isPositive(), _solve_impl's D pseudo-inverse below
 // DBL_MIN) of the N x N symmetric H (LDS, row-major) on one wavefront, lane i = pivot position i:
@@ -804,6 +809,54 @@ __device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt,
 //   solve       y = P b, L y' = y, y'' = D^+ y', L^T x = y'', x = P^T (same per-element subtraction order as Eigen's
 //               triangular solves; the factor differs from Eigen's by rounding: right-looking, fused multiply-adds)
 // x: LDS out (written only on success); pick / Lm: LDS scratch [N] / [N * N].  Returns isPositive().
+// 1 / x by v_rcp_f64 and two Newton steps (the LBA's reciprocal: exact on sampled arguments, a few ulp at worst).
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// Eigen's pick order of the N x N symmetric H into pick[] (one wavefront); false on a NaN diagonal.
+template <int N>
+__device__ __forceinline__ bool ldlt_pick_order(const double *H, int *pick, int lane) {
+    static_assert(N <= 32, "rows on lanes 0..31");
+    const bool in = lane < N;
+    const double dv = in ? fabs(H[lane * (N + 1)]) : 0.0;
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double o = fabs(H[j * (N + 1)]);
+        gt += o > dv ? 1 : 0;
+        eq += o == dv ? 1 : 0;
+    }
+    if (__ballot(in && !(dv == dv))) return false;
+    if (!__ballot(in && eq > 1)) {
+        if (in) pick[gt] = lane;
+    } else {
+        int pos = lane;
+        bool picked = false;
+        for (int k = 0; k < N; ++k) {
+            uint64_t cand = __ballot(in && !picked && gt <= k && k < gt + eq);
+            int e = __builtin_ctzll(cand);
+            if (cand & (cand - 1)) {
+                int bp = __builtin_amdgcn_readlane(pos, e);
+                for (uint64_t m = cand & (cand - 1); m; m &= m - 1) {
+                    const int c = __builtin_ctzll(m), pc = __builtin_amdgcn_readlane(pos, c);
+                    if (pc < bp) bp = pc, e = c;
+                }
+            }
+            const int xk = __builtin_ctzll(__ballot(in && pos == k));
+            const int pe = __builtin_amdgcn_readlane(pos, e);
+            if (lane == xk) pos = pe;
+            if (lane == e) pos = k, picked = true;
+            if (lane == 0) pick[k] = e;
+        }
+    }
+    return true;
+}
+
 template <int N>
 __device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b, double *x, int *pick, double *Lm, int lane) {
     static_assert(N <= 32, "rows on lanes 0..31");
@@ -841,38 +894,36 @@ __device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b
     }
     wave_lds_sync();
     const int pi = in ? pick[lane] : 0;
+    int pj[N];   // the pick order in registers first, then every row read back to back (H symmetric: column pi of row pj)
+#pragma unroll
+    for (int j = 0; j < N; ++j) pj[j] = pick[j];
     double r[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) r[j] = in ? H[pi * N + pick[j]] : 0.0;
+    for (int j = 0; j < N; ++j) r[j] = in ? H[pj[j] * N + pi] : 0.0;
     if (!(lane_f64(r[0], 0) != 0.0)) {   // largest |diagonal| zero: Eigen stops with ZeroSign; the solve gives x = 0
         if (in) x[lane] = 0.0;
         wave_lds_sync();
         return true;
     }
-    int sign = 0;   // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
+    // One basic block for the whole factorisation (no data-dependent branches) so the pivot chain of step k + 1 can
+    // issue while step k's trailing update is still in flight: a zero pivot gives inv = 0, hence l = 0 (no update,
+    // column k left unscaled), sign bits 1 (a positive D) / 2 (a negative D): Eigen's isPositive() = no bit 2.
+    int sign = 0;
     double dmine = 0.0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         const double d = lane_f64(r[k], k);
-        if (lane == k) dmine = d;
-        if (fabs(d) > 0.0) {   // rows above k update with l = 0 (an exact no-op): no exec-mask branches or selects
-            const double inv = 1.0 / d;
-            const bool below = lane > k;
-            const double l = below ? r[k] * inv : 0.0;
+        dmine = lane == k ? d : dmine;
+        const bool nz = fabs(d) > 0.0;
+        const double inv = nz ? rcp_nr(d) : 0.0;
+        const bool below = lane > k;
+        const double l = below ? r[k] * inv : 0.0;
 #pragma unroll
-            for (int j = k + 1; j < N; ++j) r[j] = __builtin_fma(-l, lane_f64(r[j], k), r[j]);
-            if (below) r[k] = l;
-        }
-        if (sign == 1) {
-            if (d < 0) sign = 3;
-        } else if (sign == 2) {
-            if (d > 0) sign = 3;
-        } else if (sign == 0) {
-            if (d > 0) sign = 1;
-            else if (d < 0) sign = 2;
-        }
+        for (int j = k + 1; j < N; ++j) r[j] = __builtin_fma(-l, lane_f64(r[j], k), r[j]);
+        r[k] = (below && nz) ? l : r[k];
+        sign |= (d > 0 ? 1 : 0) | (d < 0 ? 2 : 0);
     }
-    if (!(sign == 1 || sign == 0)) return false;
+    if (sign & 2) return false;
     double y = in ? b[pi] : 0.0;
 #pragma unroll
     for (int k = 0; k + 1 < N; ++k) {
@@ -893,6 +944,92 @@ __device__ __forceinline__ bool ldlt_pick_solve(const double *H, const double *b
     }
     if (in) x[pi] = y;
     wave_lds_sync();
+    return true;
+}
+
+// The same solve by the whole workgroup (NT threads), for the latency kernel where the other waves would idle: the
+// pick order on wave 0 as ldlt_pick_solve; the factorisation of P H P^T element-parallel on its lower triangle (thread
+// t owns elements t, t + NT, ... in registers), one workgroup barrier per pivot step: the owners of column k publish
+// it to LDS (two buffers by step parity, so a step needs no second barrier), every thread reads D_k and its rows'
+// entries and applies a_ij -= (a_ik / D_k) a_jk (a zero pivot: no update, column left unscaled, as ldlt_pick_solve);
+// then the triangular solves on wave 0 from the factor staged in Lm.  isPositive() = no negative pivot.  The
+// factor's rounding differs from ldlt_pick_solve's in the update's operand (lower-triangle column entries for both
+// factors) only.  Called by all NT threads; x written on success.  col: LDS scratch [2 * N]; flag: LDS int.
+template <int N, int NT>
+__device__ __forceinline__ bool ldlt_elem_solve(const double *H, const double *b, double *x, int *pick, double *Lm,
+                                                double *col, int *flag, int tid) {
+    constexpr int T = N * (N + 1) / 2, PER = (T + NT - 1) / NT;
+    const int lane = tid & 63;
+    if (tid < 64) {
+        const bool okp = ldlt_pick_order<N>(H, pick, lane);
+        if (lane == 0) *flag = okp ? 0 : 1;
+    }
+    __syncthreads();
+    if (*flag) return false;   // a NaN diagonal (uniform)
+    int ei[PER], ej[PER];
+    double a[PER];
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+        const int e = tid + p * NT;
+        // row i of the packed lower triangle: i (i + 1) / 2 <= e
+        int i = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+        i += (i + 1) * (i + 2) / 2 <= e ? 1 : 0;
+        i -= i * (i + 1) / 2 > e ? 1 : 0;
+        const int j = e - i * (i + 1) / 2;
+        ei[p] = e < T ? i : N, ej[p] = e < T ? j : N;
+        a[p] = e < T ? H[pick[i] * N + pick[j]] : 0.0;
+    }
+    if (!(H[pick[0] * (N + 1)] != 0.0)) {   // largest |diagonal| zero: x = 0
+        if (tid < N) x[tid] = 0.0;
+        __syncthreads();
+        return true;
+    }
+    int sign = 0;
+    for (int k = 0; k < N; ++k) {
+        double *c = col + (k & 1) * N;
+#pragma unroll
+        for (int p = 0; p < PER; ++p)
+            if (ej[p] == k) c[ei[p]] = a[p];
+        __syncthreads();
+        const double d = c[k];
+        const bool nz = fabs(d) > 0.0;
+        const double inv = nz ? rcp_nr(d) : 0.0;
+        sign |= (d > 0 ? 1 : 0) | (d < 0 ? 2 : 0);
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            if (ej[p] > k && ej[p] < N) a[p] = __builtin_fma(-(c[ei[p]] * inv), c[ej[p]], a[p]);
+            else if (ej[p] == k && ei[p] > k && nz) a[p] = a[p] * inv;
+        }
+    }
+    if (sign & 2) return false;   // uniform: every thread saw every pivot
+#pragma unroll
+    for (int p = 0; p < PER; ++p)
+        if (ei[p] < N) Lm[ei[p] * N + ej[p]] = a[p];
+    __syncthreads();
+    if (tid < 64) {
+        const bool in = lane < N;
+        const int pi = in ? pick[lane] : 0;
+        double r[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) r[j] = (in && j <= lane) ? Lm[lane * N + j] : 0.0;   // row lane of L, D on the diagonal
+        const double dmine = in ? Lm[lane * (N + 1)] : 0.0;
+        double y = in ? b[pi] : 0.0;
+#pragma unroll
+        for (int k = 0; k + 1 < N; ++k) {
+            const double yk = lane_f64(y, k);
+            if (lane > k) y = __builtin_fma(-r[k], yk, y);
+        }
+        y = fabs(dmine) > 2.2250738585072014e-308 ? y / dmine : 0.0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) r[j] = (in && j > lane) ? Lm[j * N + lane] : 0.0;   // r[j] = L_j,lane
+#pragma unroll
+        for (int j = N - 1; j >= 1; --j) {
+            const double xj = lane_f64(y, j);
+            if (lane < j) y = __builtin_fma(-r[j], xj, y);
+        }
+        if (in) x[pi] = y;
+    }
+    __syncthreads();
     return true;
 }
 
@@ -1200,6 +1337,9 @@ template <bool kLF>
 __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseArgs A, int G, gu64 *xbuf, uint32_t salt,
                                                               int32_t *err_word) {
     constexpr int N = kLF ? 30 : 15;
+    constexpr int NR = kLF ? 24 : 9;   // the system without the frame's bias vertices (see the assembly)
+    // reduced index -> state index: the frame's pose + velocity (0-8), then (LastFrame) the previous frame's 15-29
+    auto red_full = [](int r) __attribute__((always_inline)) { return r < 9 ? r : r + 6; };
     constexpr int NJ = kLF ? 216 : 81;   // EdgeInertial Jacobian entries kept: 9 x 24 (LastFrame), 9 x 9 (columns 15-23)
     constexpr int NI = kLF ? 24 : 9;
     constexpr int NP = kLF ? 225 : 1;
@@ -1215,11 +1355,12 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     __shared__ double red[3][kNormal], nrm[32];
     __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N];
     __shared__ double info9[81], infoG[9], infoA[9];
-    __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], HI[NI * NI], bI[NI];
+    __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], bI[NI], s_w1p;
     __shared__ double cA1[9], cdV[3], cdP[3], eRc[9], erc[3], RJs[9], iJs[9];
-    __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1], HP[NP],
+    __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1],
         bP[kLF ? 15 : 1];
-    __shared__ double Am[NP], Vm[NP];
+    __shared__ double Am[NP], Vm[NP], ecs[16];
+    __shared__ int epq[16];
     __shared__ uint32_t xsc[kLatMaxParts * kGran];
     __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N];
     __shared__ int k1s, k2s;
@@ -1303,7 +1444,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             for (int c = 0; c < 3; ++c) J[(3 + r) * 9 + 6 + c] = R1t[3 * r + c];
     }
     // EdgeInertial's Jacobian / error at the current state on wave 4 (J, e9, WJ = Info J; with `sys` also om9 and
-    // HI = J^T Info J, bI = J^T om9), the arithmetic of imu_error + imu_jacobian / imu_error_jac_p2v2
+    // bI = J^T om9), the arithmetic of imu_error + imu_jacobian / imu_error_jac_p2v2
     auto inertial_wave = [&](bool sys) __attribute__((always_inline)) {
         if constexpr (!kLF) {
             const double *R1 = sRwb, *R2 = sRwb + 9;
@@ -1361,22 +1502,16 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         }
         if (!sys) return;
         wave_lds_sync();
-        for (int q = lane; q < NI * NI + NI; q += 64) {
-            if (q < NI * NI) {
-                const int i = q / NI, j = q - (q / NI) * NI;
-                double t = 0;
-                for (int k = 0; k < 9; ++k) t += J[k * NI + i] * WJ[k * NI + j];
-                HI[q] = t;
-            } else {
-                const int i = q - NI * NI;
-                double u = 0;
-                for (int k = 0; k < 9; ++k) u += J[k * NI + i] * om9[k];
-                bI[i] = u;
-            }
+        // bI = J^T om9 here; the quadratic form J^T Info J is summed entry by entry where the system is assembled
+        // (all waves), off this wave's path
+        if (lane < NI) {
+            double u = 0;
+            for (int k = 0; k < 9; ++k) u += J[k * NI + lane] * om9[k];
+            bI[lane] = u;
         }
     };
-    // EdgePriorPoseImu (LastFrame) on wave 5: eP, JPr, PJ = H_prior JPr; with `sys` OeP, the Huber weight and
-    // HP = JPr^T w PJ, bP = -JPr^T w H_prior eP
+    // EdgePriorPoseImu (LastFrame) on wave 5: eP, JPr, PJ = H_prior JPr; with `sys` OeP, the Huber weight w (s_w1p)
+    // and bP = -JPr^T w H_prior eP
     auto prior_wave = [&](bool sys) __attribute__((always_inline)) {
         if constexpr (kLF) {
             if (lane == 0) prior_error_jac(sPr, sRwb, stwb, svel, sbg, sba, eP, JPr);
@@ -1399,18 +1534,11 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             double chi2p = 0, r0, w1p;
             for (int k = 0; k < 15; ++k) chi2p += eP[k] * OeP[k];
             huber(chi2p, 5.0, 25.0, r0, w1p);
-            for (int q = lane; q < 240; q += 64) {
-                if (q < 225) {
-                    const int i = q / 15, j = q % 15;
-                    double t = 0;
-                    for (int k = 0; k < 15; ++k) t += JPr[k * 15 + i] * (w1p * PJ[k * 15 + j]);
-                    HP[q] = t;
-                } else {
-                    const int i = q - 225;
-                    double u = 0;
-                    for (int k = 0; k < 15; ++k) u += JPr[k * 15 + i] * (-OeP[k] * w1p);
-                    bP[i] = u;
-                }
+            if (lane == 0) s_w1p = w1p;   // JPr^T w PJ is summed where the system is assembled
+            if (lane < 15) {
+                double u = 0;
+                for (int k = 0; k < 15; ++k) u += JPr[k * 15 + lane] * (-OeP[k] * w1p);
+                bP[lane] = u;
             }
         }
     };
@@ -1476,66 +1604,67 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 LAT_ACC(2, t0, t1);
                 LAT_ACC(3, t1, t2);
                 if (s_abort) goto fail;
-                // the system in the oracle's per-element order (visual, inertial, random walks, prior)
-                for (int q = tid; q < N * N; q += kLatThreads) {
-                    const int i = q / N, j = q - (q / N) * N;
+                // The system without the frame's bias vertices.  Their only edges are EdgeGyroRW / EdgeAccRW (e = b_frame -
+                // b_other, J = +-I, information InfoG / InfoA), so eliminating them is exact: the Schur complement drops the
+                // random walks' terms from the other vertex's block and right-hand side, and the eliminated update is
+                // x_b = x_other - e (LastFrame: the previous frame's bias update; LastKeyFrame, keyframe fixed: -e).  The
+                // reduced system (LastKeyFrame: pose + velocity, 9; LastFrame: the frame's pose + velocity and all 15 of the
+                // previous frame's, 24) is positive (semi)definite iff the full one is (InfoG / InfoA are positive
+                // definite), so isPositive() and the update agree with the full solve up to rounding.
+                for (int q = tid; q < NR * NR; q += kLatThreads) {
+                    const int i = q / NR, j = q - (q / NR) * NR;
                     if (j > i) continue;
+                    const int fi = red_full(i), fj = red_full(j);
                     double h = 0;
+                    if (fi < 6) h = nrm[fj * 6 - fj * (fj - 1) / 2 + (fi - fj)];
                     if constexpr (kLF) {
-                        if (i < 6) h = nrm[j * 6 - j * (j - 1) / 2 + (i - j)];
-                        const int ci = ei_col(i), cj = ei_col(j);
-                        if (ci >= 0 && cj >= 0) h += HI[ci * 24 + cj];
-                        h += rw_entry(i, j, false, infoG);
-                        h += rw_entry(i, j, true, infoA);
-                        if (i >= 15 && j >= 15) h += HP[(i - 15) * 15 + j - 15];
+                        const int ci = ei_col(fi), cj = ei_col(fj);
+                        if (ci >= 0 && cj >= 0) {   // (J^T Info J)_ci,cj
+                            double t = 0;
+                            for (int k = 0; k < 9; ++k) t += J[k * 24 + ci] * WJ[k * 24 + cj];
+                            h += t;
+                        }
+                        if (fi >= 15 && fj >= 15) {   // (JPr^T w H_prior JPr)_i,j
+                            const double w1p = s_w1p;
+                            double t = 0;
+                            for (int k = 0; k < 15; ++k) t += JPr[k * 15 + fi - 15] * (w1p * PJ[k * 15 + fj - 15]);
+                            h += t;
+                        }
                     } else {
-                        if (i < 6) h = nrm[j * 6 - j * (j - 1) / 2 + (i - j)];
-                        if (i < 9) h += HI[i * 9 + j];
-                        if (j >= 9 && (i < 12) == (j < 12)) h += (i < 12 ? infoG : infoA)[3 * ((i - 9) % 3) + (j - 9) % 3];
+                        double t = 0;
+                        for (int k = 0; k < 9; ++k) t += J[k * 9 + fi] * WJ[k * 9 + fj];
+                        h += t;
                     }
-                    Hs[i * N + j] = h;
-                    Hs[j * N + i] = h;
+                    Hs[i * NR + j] = h;
+                    Hs[j * NR + i] = h;
                 }
-                if (tid < N) {
-                    const int i = tid;
-                    double t = i < 6 ? nrm[21 + i] : 0.0;
+                if (tid < NR) {
+                    const int fi = red_full(tid);
+                    double t = fi < 6 ? nrm[21 + fi] : 0.0;
                     if constexpr (kLF) {
-                        const int ci = ei_col(i);
+                        const int ci = ei_col(fi);
                         if (ci >= 0) t += bI[ci];
-                        const int bi = i % 15;
-                        if (bi >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b_frame - b_prev, J_frame = I, J_prev = -I
-                            const bool acc_rw = bi >= 12;
-                            const int r = (bi - 9) % 3;
-                            const double *Iw = acc_rw ? infoA : infoG;
-                            const double *bv = acc_rw ? sba : sbg;
-                            double ee[3];
-                            for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
-                            const double oe = Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
-                            t += i < 15 ? -oe : oe;
-                        }
-                        if (i >= 15) t += bP[i - 15];
+                        if (fi >= 15) t += bP[fi - 15];
                     } else {
-                        if (i < 9) t += bI[i];
-                        if (i >= 9) {   // EdgeGyroRW / EdgeAccRW: e = b - b_kf, J = I
-                            const bool acc_rw = i >= 12;
-                            const int r = (i - 9) % 3;
-                            const double *Iw = acc_rw ? infoA : infoG;
-                            const double *bv = acc_rw ? sba : sbg;
-                            double ee[3];
-                            for (int k = 0; k < 3; ++k) ee[k] = bv[3 + k] - bv[k];
-                            t -= Iw[3 * r] * ee[0] + Iw[3 * r + 1] * ee[1] + Iw[3 * r + 2] * ee[2];
-                        }
+                        t += bI[fi];
                     }
-                    bs[i] = t;
+                    bs[tid] = t;
                 }
                 __syncthreads();
                 LAT_T(t3);
                 LAT_ACC(4, t2, t3);
                 if (wave == 0) {
-                    const bool ok = ldlt_pick_solve<N>(Hs, bs, xt, pick, Lm, lane);
+                    const bool ok = ldlt_pick_solve<NR>(Hs, bs, xt, pick, Lm, lane);
                     LAT_T(t3l);
                     LAT_ACC(5, t3, t3l);
-                    if (ok && lane < N) xs[lane] = xt[lane];   // a failed solve leaves the previous x in place
+                    if (ok) {   // a failed solve leaves the previous x in place
+                        if (lane < NR) xs[red_full(lane)] = xt[lane];
+                        if (lane < 3) {   // the eliminated bias updates
+                            const double xg = kLF ? xt[18 + lane] : 0.0, xa = kLF ? xt[21 + lane] : 0.0;
+                            xs[9 + lane] = xg - (sbg[3 + lane] - sbg[lane]);
+                            xs[12 + lane] = xa - (sba[3 + lane] - sba[lane]);
+                        }
+                    }
                     if (lane == 0) s_ok = ok ? 1 : 0;
                     wave_lds_sync();
                     // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235): lane 0 the frame, lane 1 the
@@ -1703,17 +1832,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     // Marginalize(H, 0, 14) (:3388-3455) of the previous frame: H_ff - H_fp pinv(H_pp) H_pf
                     for (int q = tid; q < 225; q += kLatThreads) Am[q] = Hs[(15 + q / 15) * N + 15 + q % 15];
                     __syncthreads();
-                    if (wave == 0) sym_eig_wave<15>(Am, Vm, lane);
-                    __syncthreads();
-                    for (int q = tid; q < 225; q += kLatThreads) {   // pinv(H_pp) -> PJ
-                        const int r = q / 15, c = q % 15;
-                        double s = 0;
-                        for (int k = 0; k < 15; ++k) {
-                            const double w = Am[k * 16];
-                            s += Vm[r * 15 + k] * (fabs(w) > 1e-6 ? 1.0 / w : 0.0) * Vm[c * 15 + k];
-                        }
-                        PJ[q] = s;
-                    }
+                    if (wave == 0) pinv15_wave(Am, Vm, PJ, ecs, epq, lane);   // pinv(H_pp) -> PJ
                     __syncthreads();
                     for (int q = tid; q < 225; q += kLatThreads) {   // T = H_fp pinv(H_pp) -> JPr
                         const int i = q / 15, j = q % 15;
@@ -1780,6 +1899,116 @@ fail:
     }
 }
 
+
+struct EdgeLevels {
+    float inv_sigma2[16];
+};
+struct EdgeOut {
+    int32_t *m_start, *m_cam, *m_kp;
+    double *m_obs;
+    float *m_w, *m_xw;
+    uint8_t *m_close;
+    int32_t *s_start, *s_cam, *s_kp;
+    double *s_obs;
+    float *s_w, *s_xw;
+    int32_t *err;
+};
+
+// The pose graph's visual edges from the frame's map-point assignment, on the device (the edge-creation loop of
+// PoseInertialOptimizationLastKeyFrame / LastFrame, Optimizer.cc:5079-5330 / :5640-5800, multi-camera frame, bRight):
+// per keypoint i of the concatenated [L | R | SL | SR] order with mvpMapPoints[i] an EdgeMonoOnlyPose of its block
+// (obs = the raw keypoint, invSigma2 = mvInvLevelSigma2[octave] / uncertainty2 = 1), and with mvuRight[i] > 0 also
+// an EdgeStereoOnlyPose of that block (obs (x, y, u_R)); both lists in keypoint order.  One workgroup,
+// 8 consecutive slots (slot = cam * kp_cap + idx) per thread, an ordered scan of the per-thread edge counts per pass.
+constexpr int kEdgeBuildThreads = 1024, kEdgeSlots = 8;   // 8 consecutive slots per thread: 8192 slots per pass
+__global__ void __launch_bounds__(kEdgeBuildThreads) pose_edges_kernel(int C, int cap, const omv_kp *kps, const int *n_kp,
+                                                                      const int32_t *kp_to_mp, const float *mp_pos,
+                                                                      const float *track_depth, EdgeLevels lv,
+                                                                      const float *uright, int max_edges, EdgeOut o) {
+    __shared__ int wc[kEdgeBuildThreads / 64][2], base[2], snk[kMaxCams];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 2) base[tid] = 0;
+    if (tid < C) snk[tid] = n_kp[tid];
+    __syncthreads();
+    const int S = C * cap;
+    for (int b0 = 0; b0 < S; b0 += kEdgeBuildThreads * kEdgeSlots) {
+        const int s0 = b0 + tid * kEdgeSlots;
+        int mp[kEdgeSlots];
+        float ur[kEdgeSlots];
+#pragma unroll
+        for (int j = 0; j < kEdgeSlots; ++j) {
+            const int s = s0 + j, c = s / cap, i = s - c * cap;
+            mp[j] = s < S && i < snk[min(c, C - 1)] ? kp_to_mp[s] : -1;
+        }
+        int cm = 0, cst = 0;
+#pragma unroll
+        for (int j = 0; j < kEdgeSlots; ++j) {
+            ur[j] = (mp[j] >= 0 && uright) ? uright[s0 + j] : -1.0f;
+            cm += mp[j] >= 0 ? 1 : 0;
+            cst += (mp[j] >= 0 && ur[j] > 0.0f) ? 1 : 0;   // kp_ur > 0 && bRight, every block (:5151, :5207, :5265, ...)
+        }
+        // exclusive scan of (cm, cst) over the workgroup in slot order
+        int im = cm, is = cst;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int um = __shfl_up(im, d, 64), us = __shfl_up(is, d, 64);
+            if (lane >= d) im += um, is += us;
+        }
+        if (lane == 63) wc[wave][0] = im, wc[wave][1] = is;
+        __syncthreads();
+        int om = base[0], os = base[1], tm = base[0], ts = base[1];
+        for (int w = 0; w < kEdgeBuildThreads / 64; ++w) {
+            if (w < wave) om += wc[w][0], os += wc[w][1];
+            tm += wc[w][0], ts += wc[w][1];
+        }
+        om += im - cm, os += is - cst;
+        // every gather first (all in flight together), then the stores
+        float kx[kEdgeSlots], ky[kEdgeSlots], kw[kEdgeSlots], X0[kEdgeSlots], X1[kEdgeSlots], X2[kEdgeSlots], td[kEdgeSlots];
+#pragma unroll
+        for (int j = 0; j < kEdgeSlots; ++j) {
+            kx[j] = ky[j] = kw[j] = X0[j] = X1[j] = X2[j] = td[j] = 0.f;
+            if (mp[j] >= 0) {
+                const size_t m = (size_t)mp[j];
+                const omv_kp k = kps[s0 + j];
+                kx[j] = k.x, ky[j] = k.y, kw[j] = lv.inv_sigma2[k.octave & 15];
+                X0[j] = mp_pos[3 * m], X1[j] = mp_pos[3 * m + 1], X2[j] = mp_pos[3 * m + 2];
+                td[j] = track_depth[m];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kEdgeSlots; ++j) {
+            if (mp[j] < 0) continue;
+            const int s = s0 + j, c = s / cap;
+            if (om < max_edges) {
+                const int e = om;
+                o.m_cam[e] = c, o.m_kp[e] = s;
+                o.m_obs[2 * e] = (double)kx[j], o.m_obs[2 * e + 1] = (double)ky[j];
+                o.m_w[e] = kw[j];
+                o.m_xw[3 * e] = X0[j], o.m_xw[3 * e + 1] = X1[j], o.m_xw[3 * e + 2] = X2[j];
+                o.m_close[e] = td[j] < 10.f ? 1 : 0;
+            }
+            ++om;
+            if (ur[j] > 0.0f) {
+                if (os < max_edges) {
+                    const int e = os;
+                    o.s_cam[e] = c, o.s_kp[e] = s;
+                    o.s_obs[3 * e] = (double)kx[j], o.s_obs[3 * e + 1] = (double)ky[j], o.s_obs[3 * e + 2] = (double)ur[j];
+                    o.s_w[e] = kw[j];
+                    o.s_xw[3 * e] = X0[j], o.s_xw[3 * e + 1] = X1[j], o.s_xw[3 * e + 2] = X2[j];
+                }
+                ++os;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) base[0] = tm, base[1] = ts;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        o.m_start[0] = 0, o.m_start[1] = min(base[0], max_edges);
+        o.s_start[0] = 0, o.s_start[1] = min(base[1], max_edges);
+        if (base[0] > max_edges || base[1] > max_edges) atomicOr(o.err, OMV_ERR_CAPACITY);
+    }
+}
 }  // namespace
 
 struct omv_pose {
@@ -1931,6 +2160,28 @@ omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, co
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream) {
     if (!prior) return OMV_ERR_ARG;
     return launch_pose(h, b, prior, rec_init, kp_outlier, n_good, H, stream);
+}
+
+omv_status omv_pose_edges_from_matches(omv_pose *h, int n_cams, int kp_cap, const omv_kp *kps, const int *n_kp,
+                                       const int32_t *kp_to_mp, const float *mp_pos, const float *mp_track_depth,
+                                       const float *inv_level_sigma2, int n_levels, const float *uright, int max_edges,
+                                       int32_t *mono_start, int32_t *mono_cam, int32_t *mono_kp, double *mono_obs,
+                                       float *mono_inv_sigma2, float *mono_xw, uint8_t *mono_close, int32_t *stereo_start,
+                                       int32_t *stereo_cam, int32_t *stereo_kp, double *stereo_obs,
+                                       float *stereo_inv_sigma2, float *stereo_xw, void *stream) {
+    if (!h || n_cams <= 0 || n_cams > kMaxCams || kp_cap <= 0 || !kps || !n_kp || !kp_to_mp || !mp_pos ||
+        !mp_track_depth || !inv_level_sigma2 || n_levels <= 0 || n_levels > 16 || max_edges <= 0 || !mono_start ||
+        !mono_cam || !mono_kp || !mono_obs || !mono_inv_sigma2 || !mono_xw || !mono_close || !stereo_start ||
+        !stereo_cam || !stereo_kp || !stereo_obs || !stereo_inv_sigma2 || !stereo_xw)
+        return OMV_ERR_ARG;
+    EdgeLevels lv{};
+    for (int l = 0; l < 16; ++l) lv.inv_sigma2[l] = inv_level_sigma2[l < n_levels ? l : n_levels - 1];
+    const EdgeOut o{mono_start, mono_cam, mono_kp, mono_obs, mono_inv_sigma2, mono_xw, mono_close, stereo_start,
+                    stereo_cam, stereo_kp, stereo_obs, stereo_inv_sigma2, stereo_xw, h->err};
+    pose_edges_kernel<<<1, kEdgeBuildThreads, 0, (hipStream_t)stream>>>(n_cams, kp_cap, kps, n_kp, kp_to_mp, mp_pos,
+                                                                         mp_track_depth, lv, uright, max_edges, o);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
 }
 
 omv_status omv_pose_constraint(int n, const double *H_in, double *H_out, void *stream) {

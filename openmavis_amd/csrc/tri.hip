@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
     __shared__ unsigned s_wu[kTriWaves];
     __shared__ int hist[kHisto];
     __shared__ int s_keep[kHisto];
-    __shared__ int s_state, s_row, s_best;
+    __shared__ int s_state, s_row, s_best, s_fin;
     const omv_tri_pair &P = pairs[blockIdx.x];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
     const int tid = threadIdx.x;
@@ -448,23 +448,53 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
             }
             __syncthreads();
         }
-        if (tid == 0) {
+        // step 4 on wave 0: 64 entries at a time staged in registers (one per lane), walked in order on wave-uniform
+        // values (v_readlane), so the dependent chain is scalar ALU work instead of LDS round trips; the rows the walk
+        // finishes are listed (row << 16 | idx2, in v_item, free after step 3) and written out by all threads after
+        int n_fin = 0;
+        if (tid < 64) {
+            const int lane = tid;
             int state = s_state;
-            for (int k = 0; k < n_valid; ++k) {
-                const uint32_t pk = v_pk[k];
-                const int idx1 = (int)(pk >> 16);
-                if (idx1 != cur_row) {
-                    finish_row();
-                    cur_row = idx1, bestDist = kTriLow, bestIdx2 = -1;
+            for (int c0 = 0; c0 < n_valid; c0 += 64) {
+                const int k = c0 + lane;
+                const bool in = k < n_valid;
+                const uint32_t pk_l = in ? v_pk[k] : 0u;
+                const int code_l = in ? (int)v_code[k] : 0;
+                const uint32_t res_l = (in && !coarse) ? v_res[k] : 0xffffffffu;
+                const int m = min(64, n_valid - c0);
+                for (int j = 0; j < m; ++j) {
+                    const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pk_l, j);
+                    const int code = __builtin_amdgcn_readlane(code_l, j);
+                    const int idx1 = (int)(pk >> 16);
+                    if (idx1 != cur_row) {
+                        if (cur_row >= 0 && bestIdx2 >= 0) {
+                            if (lane == 0) v_item[n_fin] = (cur_row << 16) | bestIdx2;
+                            ++n_fin;
+                        }
+                        cur_row = idx1, bestDist = kTriLow, bestIdx2 = -1;
+                    }
+                    const int dist = code & 0x3f;
+                    if (dist > bestDist) continue;
+                    if (code & kCodeListed) state = (code >> 8) & 15;
+                    const uint32_t res = (uint32_t)__builtin_amdgcn_readlane((int)res_l, j);
+                    if ((res >> state) & 1u) bestIdx2 = (int)(pk & 0xffff), bestDist = dist;
                 }
-                const int code = v_code[k];
-                const int dist = code & 0x3f;
-                if (dist > bestDist) continue;
-                if (code & kCodeListed) state = (code >> 8) & 15;
-                const bool ok = coarse || ((v_res[k] >> state) & 1u);
-                if (ok) bestIdx2 = (int)(pk & 0xffff), bestDist = dist;
             }
-            s_state = state, s_row = cur_row, s_best = bestDist;
+            if (lane == 0) s_state = state, s_row = cur_row, s_best = bestDist, s_fin = n_fin;
+        }
+        __syncthreads();
+        n_fin = s_fin;
+        nmatch += n_fin;   // thread 0's count (the only one read)
+        for (int i = tid; i < n_fin; i += kTriThreads) {
+            const int row = (int)((uint32_t)v_item[i] >> 16), best = v_item[i] & 0xffff;
+            P.match12[row] = best;
+            if (check_ori) {
+                float rot = K1.kps[row].angle - K2.kps[best].angle;
+                if ((double)rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * (1.0f / kHisto));
+                if (bin == kHisto) bin = 0;
+                bins[row] = (uint8_t)bin;
+            }
         }
         __syncthreads();
         n_valid = 0;

@@ -183,6 +183,44 @@ class PoseInertialOptimizer:
         _lib.check(self._lib.omv_pose_last_error(self._h, ctypes.byref(e), ctypes.c_void_p(st)), "omv_pose_last_error")
         return e.value
 
+    EDGE_KEYS = ("mono_start", "mono_cam", "mono_kp", "mono_obs", "mono_inv_sigma2", "mono_xw", "mono_close",
+                 "stereo_start", "stereo_cam", "stereo_kp", "stereo_obs", "stereo_inv_sigma2", "stereo_xw")
+
+    @staticmethod
+    def edge_arrays(max_edges, device):
+        """Device buffers for one frame's edge lists (the omv_pose_batch edge fields of a one-frame batch)."""
+        import torch
+        z = dict(device=device)
+        E = int(max_edges)
+        return dict(mono_start=torch.zeros(2, dtype=torch.int32, **z), mono_cam=torch.zeros(E, dtype=torch.int32, **z),
+                    mono_kp=torch.zeros(E, dtype=torch.int32, **z), mono_obs=torch.zeros((E, 2), dtype=torch.float64, **z),
+                    mono_inv_sigma2=torch.zeros(E, dtype=torch.float32, **z),
+                    mono_xw=torch.zeros((E, 3), dtype=torch.float32, **z), mono_close=torch.zeros(E, dtype=torch.uint8, **z),
+                    stereo_start=torch.zeros(2, dtype=torch.int32, **z),
+                    stereo_cam=torch.zeros(E, dtype=torch.int32, **z), stereo_kp=torch.zeros(E, dtype=torch.int32, **z),
+                    stereo_obs=torch.zeros((E, 3), dtype=torch.float64, **z),
+                    stereo_inv_sigma2=torch.zeros(E, dtype=torch.float32, **z),
+                    stereo_xw=torch.zeros((E, 3), dtype=torch.float32, **z))
+
+    def EdgesFromMatches(self, kps, n_kp, kp_to_mp, mp_pos, mp_track_depth, inv_level_sigma2, arrays, uright=None,
+                         stream=None):
+        """The edge-creation loop of PoseInertialOptimizationLastKeyFrame / LastFrame (src/Optimizer.cc:5079-5330)
+        for ONE multi-camera frame, on the device (omv_pose_edges_from_matches): kps int32 [C][kp_cap][6] (omv_kp
+        rows), n_kp [C], kp_to_mp [C*kp_cap] (SearchByProjection's assignment), mp_pos float [M][3], mp_track_depth
+        [M], inv_level_sigma2 host sequence (Frame::mvInvLevelSigma2), uright float [C][kp_cap] or None; writes the
+        edge lists into `arrays` (edge_arrays' buffers; their length bounds the edge count).  Asynchronous."""
+        import torch
+        C, cap = int(kps.shape[-3]), int(kps.shape[-2])
+        E = int(arrays["mono_cam"].shape[0])
+        lv = (ctypes.c_float * 16)(*[float(x) for x in inv_level_sigma2][:16])
+        st = stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream
+        a = arrays
+        _lib.check(self._lib.omv_pose_edges_from_matches(
+            self._h, C, cap, _lib.ptr(kps), _lib.ptr(n_kp), _lib.ptr(kp_to_mp), _lib.ptr(mp_pos),
+            _lib.ptr(mp_track_depth), lv, len(inv_level_sigma2), _lib.ptr(uright), E,
+            *[_lib.ptr(a[k]) for k in self.EDGE_KEYS], ctypes.c_void_p(st)), "omv_pose_edges_from_matches")
+        return arrays
+
     def PoseInertialOptimizationLastKeyFrame(self, batch, arrays, kp_outlier, H=None, bRecInit=False, stream=None):
         import torch
         from .synth_pose import as_pose_struct

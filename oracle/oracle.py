@@ -370,6 +370,43 @@ def pose_last_frame(batch, rec_init=False, frames=None):
     return {k: arrays[k] for k in STATE_KEYS}, kpo, n_good, H
 
 
+def pose_edges_from_matches(kps, n_kp, kp_to_mp, mp_pos, mp_track_depth, inv_level_sigma2, uright=None):
+    """The visual-edge creation loop of PoseInertialOptimizationLastKeyFrame / LastFrame restated for the
+    multi-camera frame (bRight; src/Optimizer.cc:5079-5330 and :5640-5800): walk the keypoints in the
+    concatenated [L | R | SL | SR] order (slot = cam * kp_cap + i); a keypoint with a map point gets an
+    EdgeMonoOnlyPose of its block (obs = the raw keypoint, invSigma2 = mvInvLevelSigma2[octave] /
+    uncertainty2 (= 1), bClose = mTrackDepth < 10) and, when mvuRight > 0, an EdgeStereoOnlyPose (obs x, y,
+    u_R).  kps: structured omv_kp [C][kp_cap] (x, y, octave fields).  Returns the edge-list dict of a
+    one-frame pose batch (mono_* / stereo_*, starts [0, n])."""
+    C, cap = kps.shape
+    lv = np.asarray(inv_level_sigma2, np.float32)
+    mono = {k: [] for k in ("cam", "kp", "obs", "w", "xw", "close")}
+    st = {k: [] for k in ("cam", "kp", "obs", "w", "xw")}
+    for c in range(C):
+        for i in range(int(n_kp[c])):
+            s = c * cap + i
+            mp = int(kp_to_mp[s])
+            if mp < 0:
+                continue
+            k = kps[c, i]
+            w = lv[min(int(k["octave"]) & 15, len(lv) - 1)]
+            xw = np.asarray(mp_pos[mp], np.float32)
+            mono["cam"].append(c), mono["kp"].append(s), mono["obs"].append([float(k["x"]), float(k["y"])])
+            mono["w"].append(w), mono["xw"].append(xw), mono["close"].append(mp_track_depth[mp] < np.float32(10))
+            ur = np.float32(uright[c, i]) if uright is not None else np.float32(-1)
+            if ur > 0:
+                st["cam"].append(c), st["kp"].append(s), st["obs"].append([float(k["x"]), float(k["y"]), float(ur)])
+                st["w"].append(w), st["xw"].append(xw)
+    return dict(mono_start=np.array([0, len(mono["cam"])], np.int32), mono_cam=np.array(mono["cam"], np.int32),
+                mono_kp=np.array(mono["kp"], np.int32), mono_obs=np.array(mono["obs"], np.float64).reshape(-1, 2),
+                mono_inv_sigma2=np.array(mono["w"], np.float32),
+                mono_xw=np.array(mono["xw"], np.float32).reshape(-1, 3), mono_close=np.array(mono["close"], np.uint8),
+                stereo_start=np.array([0, len(st["cam"])], np.int32), stereo_cam=np.array(st["cam"], np.int32),
+                stereo_kp=np.array(st["kp"], np.int32), stereo_obs=np.array(st["obs"], np.float64).reshape(-1, 3),
+                stereo_inv_sigma2=np.array(st["w"], np.float32),
+                stereo_xw=np.array(st["xw"], np.float32).reshape(-1, 3))
+
+
 def pose_constraint(H):
     """ConstraintPoseImu ctor restated on [n][225] matrices."""
     H = np.ascontiguousarray(H, np.float64).reshape(-1, 225)

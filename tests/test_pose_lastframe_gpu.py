@@ -6,7 +6,8 @@ Bar (floating point, north star 1e-5 relative): the final frame state within 1e-
 in degrees, translation / velocity / biases in m, m/s: both restate the same Gauss-Newton with the same
 per-edge arithmetic; the visual sums are reduced in a different order), the marginalised Hessian within
 1e-6 relative to its largest entry, Frame::mvbOutlier and the return value identical, and the
-ConstraintPoseImu projection within 1e-9 relative (same Jacobi sweeps on both sides).
+ConstraintPoseImu projection within 1e-9 relative (Jacobi eigen-decompositions on both sides: the oracle's cyclic
+rotation order, the device's parallel round-robin order, equal up to rounding).
 """
 import numpy as np
 import pytest

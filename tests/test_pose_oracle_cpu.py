@@ -121,3 +121,24 @@ def test_stereo_edges_share_the_keypoint_flag(oracle):
         nm = b["mono_start"][f + 1] - b["mono_start"][f]
         ns = b["stereo_start"][f + 1] - b["stereo_start"][f]
         assert 0 < n_good[f] <= nm + ns
+
+
+def test_edges_from_matches_oracle_recovers_edges(oracle):
+    """The edge-loop restatement on a frame laid out from a synthetic batch's edges gives back exactly those edges
+    (as a set: keypoint order differs from the batch's), stereo edges only where mvuRight > 0 on an assigned
+    keypoint, and nothing for an empty assignment."""
+    from test_pose_edges_gpu import INV_SIGMA2, _frame_from_batch
+    b = synth_pose.make_pose_batch(n_frames=1, n_pts=300, seed=3, stereo_frac=0.4)
+    kps, n_kp, k2m, pos, track, ur = _frame_from_batch(b, 512, np.random.default_rng(3))
+    o = oracle.pose_edges_from_matches(kps, n_kp, k2m, pos, track, INV_SIGMA2, ur)
+
+    def key(cam, obs, xw, w):
+        return (int(cam), tuple(np.float32(obs).tolist()), tuple(np.float32(xw).tolist()), float(w))
+    got = sorted(key(*t) for t in zip(o["mono_cam"], o["mono_obs"], o["mono_xw"], o["mono_inv_sigma2"]))
+    want = sorted(key(*t) for t in zip(b["mono_cam"], b["mono_obs"], b["mono_xw"], b["mono_inv_sigma2"]))
+    assert got == want
+    assert len(o["stereo_cam"]) == len(b["stereo_cam"])
+    assert np.all(np.diff(o["mono_kp"]) > 0) and np.all(np.diff(o["stereo_kp"]) > 0)   # slot order
+    assert np.array_equal(o["mono_close"].astype(bool), track[k2m[o["mono_kp"]]] < 10)
+    e = oracle.pose_edges_from_matches(kps, n_kp, np.full_like(k2m, -1), pos, track, INV_SIGMA2, ur)
+    assert e["mono_start"].tolist() == [0, 0] and e["stereo_start"].tolist() == [0, 0]

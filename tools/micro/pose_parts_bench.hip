@@ -123,6 +123,26 @@ __global__ void __launch_bounds__(64) ldlt_bench(const double *Hin, const double
     if (lane == 0) ticks[0] = t1 - t0;
 }
 
+template <int N>
+__global__ void __launch_bounds__(256) ldlt_elem_bench(const double *Hin, const double *bin, double *xout, int reps,
+                                                      unsigned long long *ticks) {
+    __shared__ double H[N * N], b[N], x[N], Lm[N * N], col[2 * N];
+    __shared__ int pick[N], flag;
+    const int tid = threadIdx.x;
+    for (int q = tid; q < N * N; q += 256) H[q] = Hin[q];
+    if (tid < N) b[tid] = bin[tid];
+    __syncthreads();
+    const unsigned long long t0 = wall_clock64();
+    bool ok = true;
+    for (int r = 0; r < reps; ++r) {
+        ok &= ldlt_elem_solve<N, 256>(H, b, x, pick, Lm, col, &flag, tid);
+        asm volatile("" ::: "memory");
+    }
+    const unsigned long long t1 = wall_clock64();
+    if (tid < N) xout[tid] = ok ? x[tid] : -1.0;
+    if (tid == 0) ticks[0] = t1 - t0;
+}
+
 __global__ void __launch_bounds__(256) edge_bench(Rig rig_in, const float *xw, const double *obs, int reps,
                                                   double *out, unsigned long long *ticks) {
     __shared__ Rig rig;
@@ -214,6 +234,22 @@ int main() {
         md = 0, mx = 0;
         for (int i = 0; i < 15; ++i) md = std::max(md, std::fabs(xa[i] - xb[i])), mx = std::max(mx, std::fabs(xa[i]));
         if (pass) printf("ldlt_pick_solve_wide<15>: %.3f us per solve (max |dx| %.3g of %.3g)\n", t / 100.0 / reps, md, mx);
+        for (int n : {15, 30}) {
+            (void)hipMemcpy(dH, n == 15 ? H15.data() : H30.data(), n * n * 8, hipMemcpyHostToDevice);
+            (void)hipMemcpy(db, n == 15 ? b15.data() : b30.data(), n * 8, hipMemcpyHostToDevice);
+            if (n == 15) ldlt_bench<15><<<1, 64>>>(dH, db, dx, reps, dt, 0);
+            else ldlt_bench<30><<<1, 64>>>(dH, db, dx, reps, dt, 0);
+            (void)hipMemcpy(xa.data(), dx, n * 8, hipMemcpyDeviceToHost);
+            if (n == 15) ldlt_elem_bench<15><<<1, 256>>>(dH, db, dx, reps, dt);
+            else ldlt_elem_bench<30><<<1, 256>>>(dH, db, dx, reps, dt);
+            (void)hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(xb.data(), dx, n * 8, hipMemcpyDeviceToHost);
+            md = 0, mx = 0;
+            for (int i = 0; i < n; ++i) md = std::max(md, std::fabs(xa[i] - xb[i])), mx = std::max(mx, std::fabs(xa[i]));
+            if (pass) printf("ldlt_elem_solve<%d, 256>: %.3f us per solve (max |dx| %.3g of %.3g)\n", n, t / 100.0 / reps, md, mx);
+        }
+        (void)hipMemcpy(dH, H15.data(), 225 * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(db, b15.data(), 15 * 8, hipMemcpyHostToDevice);
         // ties on the diagonal: the replayed pick order
         std::vector<double> Ht = H15;
         for (int i = 9; i < 15; ++i) Ht[i * 15 + i] = 50.0;
