@@ -108,6 +108,7 @@ __device__ __forceinline__ int frame_block(const omv_kf_view &F, int idx) {
 // unclaimed entries are the reference's best and second whenever the block holds <= kTop candidates or two
 // of them are unclaimed; otherwise the resolve rescans the node.
 constexpr int kTop = 8, kRecWords = 8 + 4 * kTop, kChunk = 32;   // kChunk * kRecWords: a multiple of 64
+constexpr int kBowWaves = 4;   // wavefronts per resolve workgroup (kChunk * kBowWaves records staged per chunk)
 
 // Static filters + camera block of candidate idx2 (-1: not a candidate whatever the claims)
 template <int MODE>
@@ -229,55 +230,58 @@ __device__ void scan_node(const omv_kf_view &O, const uint32_t *claimed, const u
     }
 }
 
-// One wavefront per job: the reference's sequential walk over the records (common nodes ascending, keyframe
-// keypoints in node order), claims in an LDS bitmap, then the rotation filter.
-template <int MODE>
-__global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs, const int *rec_off,
-                                                         const uint32_t *recs, float nnratio, int check_ori,
-                                                         int32_t *n_matches, int *err) {
+// One workgroup of W wavefronts per job: the reference's sequential walk over the records (common nodes ascending,
+// keyframe keypoints in node order), claims in an LDS bitmap, then the rotation filter.  The walk's batches span the
+// whole workgroup (64 W / NB keypoints), so a conflict-free stretch of the walk commits in 1/W of the batches a
+// single wavefront needs; a conflicting keypoint is walked alone by wavefront 0.
+template <int MODE, int W>
+__global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *jobs, const int *rec_off,
+                                                             const uint32_t *recs, float nnratio, int check_ori,
+                                                             int32_t *n_matches, int *err) {
     // err[0]: status; err[1]: rescans of the walk (diagnostic, omv_matcher_bow_rescans)
     __shared__ uint32_t claimed[kMaxKp / 32];
     __shared__ uint8_t bins[kMaxKp];
     __shared__ int16_t match[kMaxKp];   // the output, written to memory once at the end (no stores in the walk)
-    __shared__ uint32_t recbuf[2][kChunk * kRecWords];
+    constexpr int T = 64 * W, kChunkW = kChunk * W;
+    __shared__ uint32_t recbuf[2][kChunkW * kRecWords];
     __shared__ int owner[kMaxKp];   // batch claims: the first batch keypoint claiming an other-view keypoint, or kFree
     __shared__ int cnt[kHisto];
     __shared__ int ind[3];
-    constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1, S = 64 / NB;
+    __shared__ int s_first, s_nm;
+    constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1, S = T / NB;
     const omv_bow_job &J = jobs[blockIdx.x];
     const omv_kf_view &K = J.kf, &O = J.other;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n_out = MODE == OMV_BOW_KF_FRAME ? O.n : K.n;
     if (O.n > kMaxKp || K.n > kMaxKp) {
-        if (lane == 0) *err = OMV_ERR_CAPACITY;
+        if (tid == 0) *err = OMV_ERR_CAPACITY;
         return;
     }
-    for (int i = lane; i < n_out; i += 64) match[i] = -1, bins[i] = 0xff;
-    for (int i = lane; i < (O.n + 31) / 32; i += 64) claimed[i] = 0;
-    for (int i = lane; i < O.n; i += 64) owner[i] = kFree;
-    if (lane < kHisto) cnt[lane] = 0;
+    for (int i = tid; i < n_out; i += T) match[i] = -1, bins[i] = 0xff;
+    for (int i = tid; i < (O.n + 31) / 32; i += T) claimed[i] = 0;
+    for (int i = tid; i < O.n; i += T) owner[i] = kFree;
+    if (tid < kHisto) cnt[tid] = 0;
+    if (tid == 0) s_first = INT_MAX, s_nm = 0;
     __syncthreads();
     // records staged through LDS a chunk at a time (one coalesced load per chunk, the next chunk in flight while
     // the current one is walked): the walk itself then only waits on LDS
     const uint32_t *R = recs + (size_t)rec_off[blockIdx.x] * kRecWords;
     const int n_words = K.n * kRecWords;
-    constexpr int kPer = kChunk * kRecWords / 64;
+    constexpr int kPer = kChunkW * kRecWords / T;
     uint32_t nxt[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) nxt[k] = 64 * k + lane < n_words ? R[64 * k + lane] : 0u;
+    for (int k = 0; k < kPer; ++k) nxt[k] = T * k + tid < n_words ? R[T * k + tid] : 0u;
     int nm = 0, buf = 0;
-    for (int base = 0; base < K.n; base += kChunk) {
+    for (int base = 0; base < K.n; base += kChunkW) {
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) recbuf[buf][64 * k + lane] = nxt[k];
-        const int nb = base + kChunk;
+        for (int k = 0; k < kPer; ++k) recbuf[buf][T * k + tid] = nxt[k];
+        const int nb = base + kChunkW;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int w = nb * kRecWords + 64 * k + lane;
+            const int w = nb * kRecWords + T * k + tid;
             nxt[k] = w < n_words ? R[w] : 0u;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
         // one keyframe keypoint with the live claims (the batch's conflict / rescan case)
         auto walk_one = [&](const uint32_t *cr) {
         const int o0 = (int)cr[0];
@@ -369,7 +373,7 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
         const int qend = min(nb, K.n);
         for (int q = base; q < qend;) {
             const int nbatch = min(S, qend - q);
-            const int s = lane / NB, c = lane % NB;
+            const int s = tid / NB, c = tid % NB;
             const bool act = s < nbatch;
             const uint32_t *cr = recbuf[buf] + (act ? q + s - base : 0) * kRecWords;
             const int o0 = act ? (int)cr[0] : -1, idx1 = (int)cr[2];
@@ -395,22 +399,22 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
             const bool search = o0 >= 0;
             const bool rescan = search && found < 2 && total > kTop;
             const int bd = best == kNone ? 256 : (int)(best >> 23), bi = (int)(best & 0xffffu);
-            const int bd0 = __shfl(bd, s * NB, 64), bs0 = __shfl(d2, s * NB, 64);
+            const int bd0 = __shfl(bd, lane - c, 64), bs0 = __shfl(d2, lane - c, 64);   // keypoint s's block 0
             bool claim;
             if (MODE == OMV_BOW_KF_FRAME)
                 claim = search && bd0 <= TH_LOW && bd <= TH_LOW && (c != 0 || (float)bd0 < nnratio * (float)bs0);
             else
                 claim = search && bd < TH_LOW && (float)bd < nnratio * (float)d2;
             if (claim) atomicMin(&owner[bi], s);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
             bool bad = rescan;
 #pragma unroll
             for (int k = 0; k < kTop; ++k)
                 if ((exm >> k) & 1u) bad |= owner[e[k] & 0xffffu] < s;
             const uint64_t badm = __ballot(act && bad);
-            const int sstar = badm ? (int)(__builtin_ctzll(badm) / NB) : nbatch;   // first keypoint to walk alone
+            if (badm && lane == 0) atomicMin(&s_first, wave * (64 / NB) + (int)(__builtin_ctzll(badm) / NB));
+            __syncthreads();
+            const int sstar = min(s_first, nbatch);   // first keypoint to walk alone
             const bool commit = claim && s < sstar;
             if (commit) {
                 atomicOr(&claimed[bi >> 5], 1u << (bi & 31));
@@ -422,13 +426,13 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
                     atomicAdd(&cnt[bb], 1);
                 }
             }
-            nm += __popcll(__ballot(commit));
+            nm += __popcll(__ballot(commit));   // this wavefront's commits
             if (claim) owner[bi] = kFree;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
+            if (tid == 0) s_first = INT_MAX;   // read by every thread above; the next batch sets it after a barrier
             if (sstar < nbatch) {
-                walk_one(recbuf[buf] + (q + sstar - base) * kRecWords);
+                if (wave == 0) walk_one(recbuf[buf] + (q + sstar - base) * kRecWords);
+                __syncthreads();
                 q += sstar + 1;
             } else {
                 q += nbatch;
@@ -436,19 +440,22 @@ __global__ void __launch_bounds__(64) bow_resolve_kernel(const omv_bow_job *jobs
         }
         buf ^= 1;
     }
+    __syncthreads();
     if (check_ori) {
-        if (lane == 0) three_maxima(cnt, ind);
+        if (tid == 0) three_maxima(cnt, ind);
         __syncthreads();
     }
     int removed = 0;
-    for (int i = lane; i < n_out; i += 64) {
+    for (int i = tid; i < n_out; i += T) {
         const int bn = bins[i];
         const bool drop = check_ori && bn != 0xff && bn != ind[0] && bn != ind[1] && bn != ind[2];
         removed += drop ? 1 : 0;
         J.match[i] = drop ? -1 : (int32_t)match[i];
     }
-    nm -= wave_sum_i32(removed);
-    if (lane == 0) n_matches[blockIdx.x] = nm;
+    nm -= wave_sum_i32(removed);   // per wavefront: its commits (wave 0: also the lone walks) less its drops
+    if (lane == 0) atomicAdd(&s_nm, nm);
+    __syncthreads();
+    if (tid == 0) n_matches[blockIdx.x] = s_nm;
 }
 
 }  // namespace
@@ -486,12 +493,12 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     const dim3 cg((max_n + 255) / 256, n_jobs);
     if (mode == OMV_BOW_KF_FRAME) {
         bow_cand_kernel<OMV_BOW_KF_FRAME><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
-        bow_resolve_kernel<OMV_BOW_KF_FRAME><<<n_jobs, 64, 0, st>>>(d_jobs, d_off, d_recs, nnratio, check_ori,
-                                                                   n_matches, d_err);
+        bow_resolve_kernel<OMV_BOW_KF_FRAME, kBowWaves><<<n_jobs, 64 * kBowWaves, 0, st>>>(d_jobs, d_off, d_recs, nnratio,
+                                                                                         check_ori, n_matches, d_err);
     } else {
         bow_cand_kernel<OMV_BOW_KF_KF><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
-        bow_resolve_kernel<OMV_BOW_KF_KF><<<n_jobs, 64, 0, st>>>(d_jobs, d_off, d_recs, nnratio, check_ori, n_matches,
-                                                                d_err);
+        bow_resolve_kernel<OMV_BOW_KF_KF, kBowWaves><<<n_jobs, 64 * kBowWaves, 0, st>>>(d_jobs, d_off, d_recs, nnratio,
+                                                                                      check_ori, n_matches, d_err);
     }
     HIP_OK(hipGetLastError());
     int h_err[2] = {0, 0};

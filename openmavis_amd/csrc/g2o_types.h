@@ -17,6 +17,45 @@ constexpr int kPF = OMV_PREINT_FLOATS;
 using omv::glibc_atan2f;
 using omv::sqrtf_cr;
 
+// sin / cos in double of |x| < 1e5 (every argument on these paths: angles of rotation vectors and atan2f outputs):
+// x - n pi/2 by two fused multiply-adds (pi/2 as a double pair), then Taylor polynomials to degree 17 / 18 on
+// |r| <= pi/4 (truncation < 1e-19) -- within 1-2 ulp of the C library's results in ~40 instructions, where the
+// general ocml routines (Payne-Hanek reduction for any argument) inline to several hundred.  Larger arguments take
+// those routines.
+__device__ __attribute__((noinline)) void sincos_slow(double x, double *s, double *c) { *s = sin(x), *c = cos(x); }
+__device__ __forceinline__ void sincos_d(double x, double &s, double &c) {
+    if (!(fabs(x) < 1e5)) {
+        sincos_slow(x, &s, &c);
+        return;
+    }
+    const double n = rint(x * 0.63661977236758134308);
+    double r = __builtin_fma(-n, 1.5707963267948966192e+00, x);
+    r = __builtin_fma(-n, 6.1232339957367660359e-17, r);
+    const double r2 = r * r;
+    double ps = 1.0 / 355687428096000.0;
+    ps = __builtin_fma(ps, r2, -1.0 / 1307674368000.0);
+    ps = __builtin_fma(ps, r2, 1.0 / 6227020800.0);
+    ps = __builtin_fma(ps, r2, -1.0 / 39916800.0);
+    ps = __builtin_fma(ps, r2, 1.0 / 362880.0);
+    ps = __builtin_fma(ps, r2, -1.0 / 5040.0);
+    ps = __builtin_fma(ps, r2, 1.0 / 120.0);
+    ps = __builtin_fma(ps, r2, -1.0 / 6.0);
+    const double sr = __builtin_fma(ps * r2, r, r);
+    double pc = 1.0 / 6402373705728000.0;
+    pc = __builtin_fma(pc, r2, -1.0 / 20922789888000.0);
+    pc = __builtin_fma(pc, r2, 1.0 / 87178291200.0);
+    pc = __builtin_fma(pc, r2, -1.0 / 479001600.0);
+    pc = __builtin_fma(pc, r2, 1.0 / 3628800.0);
+    pc = __builtin_fma(pc, r2, -1.0 / 40320.0);
+    pc = __builtin_fma(pc, r2, 1.0 / 720.0);
+    pc = __builtin_fma(pc, r2, -1.0 / 24.0);
+    pc = __builtin_fma(pc, r2, 0.5);
+    const double cr = __builtin_fma(-pc, r2, 1.0);
+    const int q = (int)n & 3;
+    s = q == 0 ? sr : q == 1 ? cr : q == 2 ? -sr : -cr;
+    c = q == 0 ? cr : q == 1 ? -sr : q == 2 ? -cr : sr;
+}
+
 // ---- small f64 helpers (row-major 3x3) ----------------------------------------------------------
 struct D3 {
     double v[3];
@@ -102,8 +141,10 @@ __device__ __forceinline__ void kb8_project(const float *k, const double *X, dou
     const double psi = glibc_atan2f((float)X[1], (float)X[0]);
     const double t2 = theta * theta, t3 = theta * t2, t5 = t3 * t2, t7 = t5 * t2, t9 = t7 * t2;
     const double r = theta + (double)k[4] * t3 + (double)k[5] * t5 + (double)k[6] * t7 + (double)k[7] * t9;
-    u = (double)k[0] * r * cos(psi) + (double)k[2];
-    v = (double)k[1] * r * sin(psi) + (double)k[3];
+    double sp, cp;
+    sincos_d(psi, sp, cp);
+    u = (double)k[0] * r * cp + (double)k[2];
+    v = (double)k[1] * r * sp + (double)k[3];
 }
 // KannalaBrandt8::projectJac (:128-158), 2x3 row-major
 __device__ __forceinline__ void kb8_jac(const float *k, const double *X, double *J) {
@@ -117,13 +158,15 @@ __device__ __forceinline__ void kb8_jac(const float *k, const double *X, double 
     // `3 * mvParameters[4]` is an int x float product in the reference: rounded to float first
     const double fd = 1 + (double)(3.0f * k[4]) * t2 + (double)(5.0f * k[5]) * t4 + (double)(7.0f * k[6]) * t6 +
                       (double)(9.0f * k[7]) * t8;
-    const double q = r2 * (r2 + z2);
-    J[0] = (double)k[0] * (fd * X[2] * x2 / q + f * y2 / r3);
-    J[3] = (double)k[1] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
-    J[1] = (double)k[0] * (fd * X[2] * X[1] * X[0] / q - f * X[1] * X[0] / r3);
-    J[4] = (double)k[1] * (fd * X[2] * y2 / q + f * x2 / r3);
-    J[2] = -(double)k[0] * fd * X[0] / (r2 + z2);
-    J[5] = -(double)k[1] * fd * X[1] / (r2 + z2);
+    // three reciprocals for the eight quotients (each within an ulp of the division)
+    const double iz = 1.0 / (r2 + z2), iq = iz / r2, ir3 = 1.0 / r3;
+    const double xy = fd * X[2] * X[1] * X[0] * iq - f * X[1] * X[0] * ir3;
+    J[0] = (double)k[0] * (fd * X[2] * x2 * iq + f * y2 * ir3);
+    J[3] = (double)k[1] * xy;
+    J[1] = (double)k[0] * xy;
+    J[4] = (double)k[1] * (fd * X[2] * y2 * iq + f * x2 * ir3);
+    J[2] = -(double)k[0] * fd * X[0] * iz;
+    J[5] = -(double)k[1] * fd * X[1] * iz;
 }
 
 // Pinhole::project(const Eigen::Vector3d&) (Pinhole.cpp:18-24): float parameters, double arithmetic
@@ -258,7 +301,8 @@ __device__ void log_so3(const double *R, double *w) {
     const double costheta = (t - 1.0) * 0.5f;
     if (costheta > 1 || costheta < -1) return;
     const double theta = acos(costheta);
-    const double s = sin(theta);
+    double s, c_unused;
+    sincos_d(theta, s, c_unused);
     if (fabs(s) < 1e-5) return;
     for (int q = 0; q < 3; ++q) w[q] = theta * w[q] / s;
 }
@@ -307,7 +351,9 @@ __device__ void inv_right_jac(const double *v, double *J) {
     double W[9], WW[9];
     hat3(v, W);
     mm3(W, W, WW);
-    const double k = 1.0 / d2 - (1.0 + cos(d)) / (2.0 * d * sin(d));
+    double sd, cd;
+    sincos_d(d, sd, cd);
+    const double k = 1.0 / d2 - (1.0 + cd) / (2.0 * d * sd);
     for (int q = 0; q < 9; ++q) J[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] / 2 + WW[q] * k;
 }
 __device__ void right_jac(const double *v, double *J) {
@@ -320,8 +366,9 @@ __device__ void right_jac(const double *v, double *J) {
     double W[9], WW[9];
     hat3(v, W);
     mm3(W, W, WW);
-    for (int q = 0; q < 9; ++q)
-        J[q] = ((q % 4 == 0) ? 1.0 : 0.0) - W[q] * (1.0 - cos(d)) / d2 + WW[q] * (d - sin(d)) / (d2 * d);
+    double sd, cd;
+    sincos_d(d, sd, cd);
+    for (int q = 0; q < 9; ++q) J[q] = ((q % 4 == 0) ? 1.0 : 0.0) - W[q] * (1.0 - cd) / d2 + WW[q] * (d - sd) / (d2 * d);
 }
 
 // EdgeInertial::linearizeOplus (G2oTypes.cc:533-599): J [9][24], columns P1(6) V1 G1 A1 P2(6) V2
@@ -485,7 +532,8 @@ __device__ void exp_so3(const double *w, double *R) {   // ExpSO3 (G2oTypes.cc:8
     if (d < 1e-5) {
         for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] + 0.5 * WW[q];
     } else {
-        const double s = sin(d), c = cos(d);
+        double s, c;
+        sincos_d(d, s, c);
         for (int q = 0; q < 9; ++q) R[q] = ((q % 4 == 0) ? 1.0 : 0.0) + W[q] * s / d + WW[q] * (1.0 - c) / d2;
     }
     polar3(R);

@@ -75,6 +75,7 @@ struct PoseArgs {
     double *H;
     int rec_init;
     const double *info;   // [F][99] EdgeInertial 9x9 | GyroRW 3x3 | AccRW 3x3 information (pose_info_kernel)
+    const float *preint_rw;   // [F][kPF] the random walks' preintegration (the grouped kernel forms `info` itself)
     // PoseInertialOptimizationLastFrame: the previous frame's ConstraintPoseImu (EdgePriorPoseImu)
     const double *pRwb, *ptwb, *pvel, *pbg, *pba, *pH;
 };
@@ -99,13 +100,19 @@ __global__ void __launch_bounds__(64) pose_info_kernel(const float *preint, cons
 }
 
 // ConstraintPoseImu ctor (G2oTypes.h:639-659), one wavefront per matrix: (H + H) / 2, eigenvalues < 1e-12
-// zeroed, V diag(w) V^T (a positive definite matrix with every eigenvalue above the cut passes unchanged).
+// zeroed, V diag(w) V^T over the lower triangle (Eigen's SelfAdjointEigenSolver); a positive definite matrix with
+// every eigenvalue above the cut passes unchanged.
 __global__ void __launch_bounds__(64) pose_constraint_kernel(const double *Hin, double *Hout) {
     __shared__ double A[225], V[225], cs[16];
     __shared__ int pq[16];
     const int f = blockIdx.x, lane = threadIdx.x;
     const double *hi = Hin + (size_t)f * 225;
-    for (int q = lane; q < 225; q += 64) A[q] = (hi[q] + hi[q]) / 2;
+    // SelfAdjointEigenSolver reads the lower triangle only: a (rounding-)asymmetric H enters as its lower half mirrored
+    for (int q = lane; q < 225; q += 64) {
+        const int r = q / 15, c = q % 15;
+        const double v = r >= c ? hi[q] : hi[c * 15 + r];
+        A[q] = (v + v) / 2;
+    }
     wave_lds_sync();
     // Every eigenvalue above 1e-12 (A - tau I factors with positive pivots, tau = 1e-12 plus a margin for the
     // factorisation's rounding): the projection is A itself (V diag(w) V^T = A up to rounding)
@@ -758,6 +765,15 @@ __device__ __forceinline__ bool lat_exchange_l(gu64 *fb, int phase, uint32_t sal
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const int per = 2 * n, M = G * per;
+    // a cheap poll first: lane p < G watches the last granule part p writes (one 8-byte load per part per spin, not
+    // the whole sweep: 32 parts polling all 32 x 2n granules kept the memory side busy with repeats of the same lines)
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned long long x =
+            __hip_atomic_load(slot + min(lane, G - 1) * kGran + per - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all(lane >= G || (uint32_t)(x >> 32) == tag)) break;
+        if (spins > (1u << 22)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
     uint32_t val[L];
     for (unsigned spins = 0;; ++spins) {
         bool ok = true;
@@ -1353,7 +1369,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     __shared__ double sRwb[18], stwb[6], svel[6], sbg[6], sba[6];
     __shared__ double sRcw[kMaxCams * 9], stcw[kMaxCams * 3];
     __shared__ double red[3][kNormal], nrm[32];
-    __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N];
+    __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N], ism[kLF ? 1 : 258];
     __shared__ double info9[81], infoG[9], infoA[9];
     __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], bI[NI], s_w1p;
     __shared__ double cA1[9], cdV[3], cdP[3], eRc[9], erc[3], RJs[9], iJs[9];
@@ -1403,12 +1419,6 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     for (int q = tid; q < N; q += kLatThreads) xs[q] = 0.0;
     for (int q = tid; q < NJ; q += kLatThreads) J[q] = 0.0;
     for (int q = tid; q < kPF; q += kLatThreads) spre[q] = A.preint[(size_t)f * kPF + q];
-    for (int q = tid; q < 99; q += kLatThreads) {
-        const double v = A.info[(size_t)f * 99 + q];
-        if (q < 81) info9[q] = v;
-        else if (q < 90) infoG[q - 81] = v;
-        else infoA[q - 90] = v;
-    }
     const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0;
     const int s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
     const int ne = nm + ns;
@@ -1423,6 +1433,18 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     if (wave == 0) {
         if (!lat_exchange(fb, phase, salt, g, G, fit ? 0.0 : 1.0, 1, xsc, s_cnt, lane)) s_abort = 1;
         else if (lane == 0 && s_cnt[0] != 0.0) s_abort = 2;
+    } else if (wave == kIW) {
+        // the edges' information matrices (pose_info_kernel's work, here beside the setup exchange: no extra launch)
+        inertial_info9_wave<true>(spre + PreView::C, info9, kLF ? Lm : ism, lane);   // 258 doubles of scratch
+        if (lane == 0) {
+            const float *prw = A.preint_rw + (size_t)f * kPF;
+            double gq[9], aq[9];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    gq[3 * r + c] = prw[PreView::C + (9 + r) * 15 + 9 + c], aq[3 * r + c] = prw[PreView::C + (12 + r) * 15 + 12 + c];
+            inv3(gq, infoG);
+            inv3(aq, infoA);
+        }
     }
     State st{sRwb, stwb, nullptr, nullptr, svel, sbg, sba, nullptr};
     Imu imu{};
@@ -1920,7 +1942,8 @@ struct EdgeOut {
 // (obs = the raw keypoint, invSigma2 = mvInvLevelSigma2[octave] / uncertainty2 = 1), and with mvuRight[i] > 0 also
 // an EdgeStereoOnlyPose of that block (obs (x, y, u_R)); both lists in keypoint order.  One workgroup,
 // 8 consecutive slots (slot = cam * kp_cap + idx) per thread, an ordered scan of the per-thread edge counts per pass.
-constexpr int kEdgeBuildThreads = 1024, kEdgeSlots = 8;   // 8 consecutive slots per thread: 8192 slots per pass
+constexpr int kEdgeBuildThreads = 512, kEdgeSlots = 8;   // 8 consecutive slots per thread: 4096 slots per pass (512: the
+                                                          // slot registers fit without spills)
 __global__ void __launch_bounds__(kEdgeBuildThreads) pose_edges_kernel(int C, int cap, const omv_kp *kps, const int *n_kp,
                                                                       const int32_t *kp_to_mp, const float *mp_pos,
                                                                       const float *track_depth, EdgeLevels lv,
@@ -2105,7 +2128,7 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
                b->kf_ba, b->preint, b->mono_start, b->mono_cam, b->mono_kp, b->mono_obs, b->mono_inv_sigma2,
                b->mono_xw, b->mono_close, b->stereo_start, b->stereo_cam, b->stereo_kp, b->stereo_obs,
                b->stereo_inv_sigma2, b->stereo_xw, b->kp_cap, h->chi2, h->chi2 + h->max_edges, h->act,
-               h->act + h->max_edges, kp_outlier, n_good, H, rec_init, h->info};
+               h->act + h->max_edges, kp_outlier, n_good, H, rec_init, h->info, prior ? prior->preint_kf : b->preint};
     hipStream_t st = (hipStream_t)stream;
     if (prior) {
         A.pRwb = prior->Rwb, A.ptwb = prior->twb, A.pvel = prior->vel, A.pbg = prior->bg, A.pba = prior->ba;
@@ -2121,7 +2144,7 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     int G = h->parts;
     const int et = lat_edge_threads(prior != nullptr);
     if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 1) / et));
-    pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
+    if (!grouped) pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
     if (grouped) {
         h->call = (h->call + 1) & 0xFFFFFu;
         if (h->call == 0) {   // tags repeat after 2^20 calls: clear the granules once

@@ -98,7 +98,15 @@ def test_constraint_pose_imu_matches_oracle(oracle):
     o = oracle.pose_constraint(Hin)
     g = g.cpu().numpy()
     for i in range(len(Hin)):
-        assert np.abs(g[i] - o[i]).max() <= 1e-9 * np.abs(o[i]).max(), i
+        # the marginalised H is symmetric up to rounding; the reference's SelfAdjointEigenSolver (and the device)
+        # read its lower triangle, the oracle's Jacobi the whole matrix: they differ by up to that asymmetry
+        Hm = Hin[i].reshape(15, 15)
+        asym = np.abs(Hm - Hm.T).max()
+        assert np.abs(g[i] - o[i]).max() <= 1e-9 * np.abs(o[i]).max() + asym, i
+        Hl = np.tril(Hm) + np.tril(Hm, -1).T
+        assert np.abs(g[i].reshape(15, 15) - g[i].reshape(15, 15).T).max() <= 1e-9 * np.abs(o[i]).max(), i
+        if np.linalg.eigvalsh(Hl).min() > 1e-6 * np.abs(Hl).max():   # positive definite: the lower half, unchanged
+            assert np.abs(g[i] - Hl.reshape(-1)).max() <= 1e-9 * np.abs(o[i]).max(), i
     # in place (H_out aliasing H_in)
     t = torch.from_numpy(Hin).cuda()
     PoseInertialOptimizer.ConstraintPoseImu(t, out=t)
