@@ -724,8 +724,9 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
 // keypoint that carries a mono and a stereo edge land in one workgroup, so mvbOutlier stays workgroup-local) and held
 // in LDS for the whole call.  Per Gauss-Newton iteration every workgroup evaluates its edges (waves 0-3, one edge per
 // thread at <= 256 edges per workgroup), while wave 4 linearises EdgeInertial and wave 5 (LastFrame) EdgePriorPoseImu at
-// the same state; the 27 visual normal-equation sums of the G workgroups are exchanged as 8-byte {tag, word} granules
-// (write-through `sc1` stores, polled `sc1` loads: no fence, MI355X_MICROARCH.md hand-off R2) and summed in part order,
+// the same state; the 27 visual normal-equation sums of the G workgroups are exchanged through write-through (`sc1`)
+// payload rows and one flag per part (MI355X_MICROARCH.md hand-off R1: drained stores, flag poll, `sc1` loads) and
+// summed in part order,
 // so every workgroup holds the identical system and runs the identical solve and update -- no second hop to broadcast
 // the state.  The 15x15 / 30x30 system is solved by one wavefront with the rows in registers (pivot order first,
 // Eigen's transpositions replayed on the original diagonal; right-looking LDL^T with v_readlane row broadcasts).
@@ -733,14 +734,16 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
 constexpr int kLatThreads = 256;        // one wave per SIMD (512 registers): visual edges on 3 (LastFrame 2) waves, then
                                         // EdgeInertial, then (LastFrame) EdgePriorPoseImu on a wave of its own
 __host__ __device__ constexpr int lat_edge_threads(bool lf) { return lf ? 128 : 192; }
-constexpr int kLatMaxParts = 32;        // workgroups per frame
+constexpr int kLatMaxParts = 48;        // workgroups per frame
 constexpr int kLatCap = 1024;           // visual edges per workgroup (LDS)
 constexpr int kLatFlagCap = 16384;      // keypoints per frame (mvbOutlier staged in LDS)
-constexpr int kGran = 64;               // 8-byte granules per (frame, slot, part)
+constexpr int kLatRow = 32;             // payload words per (frame, slot, part): the 27 normal-equation sums
 constexpr int kLatAutoFrames = 16;      // OMV_POSE_AUTO: the grouped kernel up to this many frames per call
-constexpr size_t kLatFrameGran = 2 * kLatMaxParts * kGran;   // granules per frame (two slots by phase parity)
+constexpr size_t kLatFrameGran = 2 * kLatMaxParts * (kLatRow + 1);   // 8-byte words per frame: two slots (phase parity)
+                                                                      // of payload rows + flags
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 #ifdef OMV_POSE_PROFILE   // phase times of the grouped kernel (wall_clock64 = 100 MHz), printed by part 0
+__device__ unsigned long long g_lat_pub[48][48];   // per part, per Gauss-Newton iteration: the hand-off's start
 #define LAT_T(var) const unsigned long long var = wall_clock64()
 #define LAT_ACC(slot, a, b) prof[slot] += (b) - (a)
 #else
@@ -748,70 +751,61 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 #define LAT_ACC(slot, a, b)
 #endif
 
-// Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q): publish this part's values as
-// 2n granules of slot (phase & 1), sweep all G x 2n granules until every tag equals salt | phase, add the parts in part
-// order into out[0..n) (LDS).  One wavefront; false on a bounded-spin timeout (a missing sibling workgroup).  L: sweep
-// loads per lane, every one issued before the first tag compare (>= ceil(G * 2n / 64)).
+// Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q), in part order, into out[0..n)
+// (LDS), every part getting the identical sums.  MI355X_MICROARCH.md's R1 hand-off: the part's n values go out as
+// write-through (`sc1`) 8-byte stores to its payload row of slot (phase & 1), the wave drains them (vmcnt(0)), then
+// ONE lane stores the part's flag = salt | phase; the consumer polls the G flags with one load per spin (lane p: part
+// p's flag), then reads the G x n payload words with `sc1` loads (every load of them: no acquire needed) -- a poll of
+// G words instead of re-reading every part's payload each spin.  One wavefront; false on a bounded-spin timeout (a
+// missing sibling workgroup).  L: payload loads per lane (>= ceil(G n / 64)); loads past G n repeat the last word.
 template <int L>
-__device__ __forceinline__ bool lat_exchange_l(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
-                                               uint32_t *sc, double *out, int lane) {
+__device__ __attribute__((noinline)) bool lat_exchange_l(gu64 *fb, int phase, uint32_t salt, int g, int G, double v,
+                                                         int n, double *sc, double *out, int lane) {
     const uint32_t tag = salt | (uint32_t)phase;
-    gu64 *slot = fb + (size_t)(phase & 1) * kLatMaxParts * kGran;
-    if (lane < n) {
-        const uint64_t b = __builtin_bit_cast(uint64_t, v);
-        __hip_atomic_store(slot + g * kGran + 2 * lane, ((unsigned long long)tag << 32) | (uint32_t)b, __ATOMIC_RELAXED,
+    const int sl = phase & 1;
+    gu64 *pay = fb + (size_t)sl * kLatMaxParts * kLatRow;                                // [part][kLatRow]
+    gu64 *flg = fb + (size_t)2 * kLatMaxParts * kLatRow + (size_t)sl * kLatMaxParts;     // [part]
+    if (lane < n)
+        __hip_atomic_store(pay + g * kLatRow + lane, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(slot + g * kGran + 2 * lane + 1, ((unsigned long long)tag << 32) | (uint32_t)(b >> 32),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const int per = 2 * n, M = G * per;
-    // a cheap poll first: lane p < G watches the last granule part p writes (one 8-byte load per part per spin, not
-    // the whole sweep: 32 parts polling all 32 x 2n granules kept the memory side busy with repeats of the same lines)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the payload has left this CU before the flag (R1)
+    if (lane == 0) __hip_atomic_store(flg + g, (unsigned long long)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (unsigned spins = 0;; ++spins) {
         const unsigned long long x =
-            __hip_atomic_load(slot + min(lane, G - 1) * kGran + per - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__all(lane >= G || (uint32_t)(x >> 32) == tag)) break;
+            lane < G ? __hip_atomic_load(flg + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (unsigned long long)tag;
+        if (__all((uint32_t)x == tag)) break;
         if (spins > (1u << 22)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
-    uint32_t val[L];
-    for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
+    const int M = G * n;
+    double val[L];
 #pragma unroll
-        for (int m = 0; m < L; ++m) {
-            const int i = min(lane + 64 * m, M - 1);   // past M: a repeat of the last granule (no branch between loads)
-            const int p = i / per, w = i - p * per;
-            const unsigned long long x = __hip_atomic_load(slot + p * kGran + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            val[m] = (uint32_t)x;
-            ok &= (uint32_t)(x >> 32) == tag;
-        }
-        if (__all(ok)) break;
-        if (spins > (1u << 22)) return false;
-        __builtin_amdgcn_s_sleep(1);
+    for (int m = 0; m < L; ++m) {
+        const int i = min(lane + 64 * m, M - 1);
+        const int p = i / n, q = i - p * n;
+        val[m] = __builtin_bit_cast(double, __hip_atomic_load(pay + p * kLatRow + q, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
     }
 #pragma unroll
     for (int m = 0; m < L; ++m) {
         const int i = lane + 64 * m;
-        if (i < M) {
-            const int p = i / per, w = i - p * per;
-            sc[p * kGran + w] = val[m];
-        }
+        if (i < M) sc[i] = val[m];
     }
     wave_lds_sync();
     if (lane < n) {
         double s = 0;
-        for (int p = 0; p < G; ++p)
-            s += __builtin_bit_cast(double, ((uint64_t)sc[p * kGran + 2 * lane + 1] << 32) | sc[p * kGran + 2 * lane]);
+        for (int p = 0; p < G; ++p) s += sc[p * n + lane];
         out[lane] = s;
     }
     wave_lds_sync();
     return true;
 }
-// One out-of-line copy (three call sites; the inlined sweeps were a sixth of the kernel's code, and the kernel's
-// per-iteration code must stay within the CU's instruction cache).  Loads past G x 2n repeat the last granule.
-__device__ __attribute__((noinline)) bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
-                                                       uint32_t *sc, double *out, int lane) {
-    return lat_exchange_l<(kLatMaxParts * kGran) / 64>(fb, phase, salt, g, G, v, n, sc, out, lane);
+// Out-of-line sweeps (three call sites; inlined they were a sixth of the kernel's code, whose per-iteration code must
+// stay within the CU's instruction cache), sized to the payload.
+__device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
+                                             double *sc, double *out, int lane) {
+    if (G * n <= 8 * 64) return lat_exchange_l<8>(fb, phase, salt, g, G, v, n, sc, out, lane);
+    return lat_exchange_l<(kLatMaxParts * kLatRow) / 64>(fb, phase, salt, g, G, v, n, sc, out, lane);
 }
 
 // Eigen::LDLT<MatrixXd> (ldlt_inplace::unblocked's pivot order, isPositive(), _solve_impl's D pseudo-inverse below
@@ -1338,15 +1332,31 @@ __device__ bool lat_select(const PoseArgs &A, bool stereo, int e0, int n, int lo
 
 // Keypoint-range boundary p of G: the mono list's (else the stereo list's) keypoint at its p/G quantile, made monotone
 // over p (the reference creates edges in keypoint order, so the parts balance; any order partitions correctly).
-__device__ int lat_bound(const PoseArgs &A, int p, int G, int m0, int nm, int s0, int ns) {
+// The keypoint threshold of part boundary p: the keypoint of element d = ne p / G of the frame's mono and stereo
+// edges merged in keypoint order (both lists ascend by keypoint; a keypoint's edges go to one part), so every part
+// holds ne / G edges up to one keypoint's two.  Merge path by a 64-ary search on one wavefront: lane k tests the
+// k-th of 64 candidate mono counts i (B(i): the d - i stereo edges before the split all precede mono edge i), the
+// first true lane narrows the range; three rounds for 262,144 edges.  All lanes return the same value.
+__device__ int lat_bound_wave(const PoseArgs &A, int p, int G, int m0, int nm, int s0, int ns, int lane) {
     if (p <= 0) return INT_MIN;
     if (p >= G) return INT_MAX;
-    const int32_t *key = nm > 0 ? A.m_kp + m0 : A.s_kp + s0;
-    const int n = nm > 0 ? nm : ns;
-    if (n == 0) return INT_MIN;
-    int b = INT_MIN;
-    for (int q = 1; q <= p; ++q) b = max(b, (int)key[(int64_t)n * q / G]);
-    return b;
+    const int ne = nm + ns;
+    if (ne == 0) return INT_MIN;
+    const int d = (int)((int64_t)ne * p / G);
+    const int32_t *M = A.m_kp + m0, *S = A.s_kp + s0;
+    int lo = max(0, d - ns), hi = min(d, nm);   // the mono count of the first d merged edges lies in [lo, hi]
+    while (hi > lo) {
+        const int i = lo + (int)(((int64_t)(hi - lo) * lane) / 63);   // lane 63 tests hi
+        const int j = d - i;
+        const bool b = j == 0 || i == nm || S[j - 1] < M[i];
+        const uint64_t bal = __ballot(b);
+        const int k = __builtin_ctzll(bal | (1ull << 63));
+        const int ik = __shfl(i, k, 64), ik1 = k > 0 ? __shfl(i, k - 1, 64) : lo - 1;
+        hi = ik, lo = ik1 + 1;
+    }
+    const int i = lo, j = d - i;
+    if (i < nm && (j >= ns || M[i] <= S[j])) return M[i];
+    return j < ns ? S[j] : INT_MAX;
 }
 
 template <bool kLF>
@@ -1377,16 +1387,17 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         bP[kLF ? 15 : 1];
     __shared__ double Am[NP], Vm[NP], ecs[16];
     __shared__ int epq[16];
-    __shared__ uint32_t xsc[kLatMaxParts * kGran];
-    __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N];
+    __shared__ double xsc[kLatMaxParts * kLatRow];
+    __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N], s_lohi[2];
     __shared__ int k1s, k2s;
     __shared__ double s_cnt[2];
     __shared__ float spre[kPF];   // the frame's IMU::Preintegrated record (read every iteration: kept out of HBM)
     const int C = rig_in.n_cams;
 #ifdef OMV_POSE_PROFILE
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    __shared__ unsigned long long prof_inert;
+    __shared__ unsigned long long prof_inert, t2s[48];
     if (tid == 0) prof_inert = 0;
+    if (tid < 48) t2s[tid] = 0;
     LAT_T(t_start);
 #endif
     for (int q = tid; q < (int)(sizeof(Rig) / 4); q += kLatThreads)
@@ -1422,8 +1433,12 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0;
     const int s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
     const int ne = nm + ns;
-    const int lo = lat_bound(A, g, G, m0, nm, s0, ns), hi = lat_bound(A, g + 1, G, m0, nm, s0, ns);
+    if (wave == 0) {
+        const int b0 = lat_bound_wave(A, g, G, m0, nm, s0, ns, lane), b1 = lat_bound_wave(A, g + 1, G, m0, nm, s0, ns, lane);
+        if (lane == 0) s_lohi[0] = b0, s_lohi[1] = b1;
+    }
     __syncthreads();
+    const int lo = s_lohi[0], hi = s_lohi[1];
     bool fit = lat_select(A, false, m0, nm, lo, hi, E, &s_count, wcnt);
     const int nm_loc = s_count;
     if (fit) fit = lat_select(A, true, s0, ns, lo, hi, E, &s_count, wcnt);
@@ -1617,12 +1632,21 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 }
                 __syncthreads();
                 LAT_T(t1);
+#ifdef OMV_POSE_PROFILE
+                if (tid == 0 && f == 0 && it * 10 + gi < 48) {
+                    __hip_atomic_store(&g_lat_pub[g][it * 10 + gi], t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (g == 0) t2s[it * 10 + gi] = 0;
+                }
+#endif
                 if (wave == 0) {
                     const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
                     if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
                 }
                 __syncthreads();
                 LAT_T(t2);
+#ifdef OMV_POSE_PROFILE
+                if (tid == 0 && f == 0 && g == 0 && it * 10 + gi < 48) t2s[it * 10 + gi] = t2;
+#endif
                 LAT_ACC(2, t0, t1);
                 LAT_ACC(3, t1, t2);
                 if (s_abort) goto fail;
@@ -1890,6 +1914,22 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             }
         }
 #ifdef OMV_POSE_PROFILE
+        if (g == 0 && tid == 0 && f == 0) {   // hand-off skew: over the iterations, max - min publish time over the parts,
+                                              // and part 0's completion after the last publish
+            double skew = 0, post = 0;
+            int n_it = 0;
+            for (int i = 0; i < 48; ++i) {
+                if (t2s[i] == 0) continue;
+                unsigned long long mx = 0, mn = ~0ull;
+                for (int p = 0; p < G; ++p) {
+                    const unsigned long long t = __hip_atomic_load(&g_lat_pub[p][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    mx = t > mx ? t : mx, mn = t < mn ? t : mn;
+                }
+                skew += (double)(mx - mn), post += (double)t2s[i] - (double)mx, ++n_it;
+            }
+            printf("pose_lat<%d> hand-off per iteration (%d): publish skew %.2f us, last publish -> part 0 done %.2f us\n",
+                   (int)kLF, n_it, skew / n_it / 100.0, post / n_it / 100.0);
+        }
         if (g == 0 && tid == 0) {
             LAT_T(t_end);
             printf("pose_lat<%d> G %d edges(w0) %.1f reduce %.1f edges+inertial(barrier) %.1f exchange %.1f build %.1f "
@@ -2039,7 +2079,7 @@ struct omv_pose {
     double *chi2 = nullptr;   // [2][max_edges]
     uint8_t *act = nullptr;   // [2][max_edges]
     double *info = nullptr;   // [max_frames][99]
-    // grouped (latency) path: per frame two slots x kLatMaxParts x kGran exchange granules, the call's tag salt,
+    // grouped (latency) path: per frame two slots x kLatMaxParts x (payload row + flag) exchange words, the call's tag salt,
     // the device error word, the path policy (OMV_POSE_AUTO / _BATCH / _GROUPED) and the parts per frame (0: auto)
     unsigned long long *xbuf = nullptr;
     uint32_t call = 0;
@@ -2143,7 +2183,8 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     if (h->mode == OMV_POSE_GROUPED && !grouped_ok) return OMV_ERR_ARG;
     int G = h->parts;
     const int et = lat_edge_threads(prior != nullptr);
-    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 1) / et));
+    // one edge per edge-wave thread: parts hold ne / G edges up to one keypoint's two (lat_bound_wave)
+    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 3) / (et - 2)));
     if (!grouped) pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
     if (grouped) {
         h->call = (h->call + 1) & 0xFFFFFu;
