@@ -750,6 +750,7 @@ __device__ inline void ldl_inverse_wave(const double *L, double *X, int lane) {
 #pragma unroll
             for (int k = 0; k < i; ++k) t -= L[i * N + k] * y[k];
             y[i] = t;
+            asm volatile("" ::: "memory");   // one row of L live at a time (hoisting all 225 loads spills)
         }
 #pragma unroll
         for (int i = 0; i < N; ++i) y[i] = y[i] / L[i * N + i];
@@ -759,6 +760,7 @@ __device__ inline void ldl_inverse_wave(const double *L, double *X, int lane) {
 #pragma unroll
             for (int k = i + 1; k < N; ++k) t -= L[k * N + i] * y[k];
             y[i] = t;
+            asm volatile("" ::: "memory");
         }
 #pragma unroll
         for (int i = 0; i < N; ++i) X[i * N + lane] = y[i];
@@ -779,7 +781,7 @@ __device__ inline double max_abs_diag(const double *A, int lane) {
 // the factorisation's rounding), every eigenvalue exceeds 1e-6 and pinv(A) = A^-1: LDL^T and 15 triangular solves.
 // Otherwise the Jacobi eigen-decomposition and V diag(1/w over |w| > 1e-6) V^T.  The two agree up to rounding.
 // V: LDS [225] scratch; cs / pq: sym_eig_wave_par's scratch.
-__device__ inline void pinv15_wave(double *A, double *V, double *P, double *cs, int *pq, int lane) {
+__device__ __attribute__((noinline)) void pinv15_wave(double *A, double *V, double *P, double *cs, int *pq, int lane) {
     const double tau = 1e-6 + 1e-12 * max_abs_diag<15>(A, lane);
     if (ldl_nopiv_wave<15>(A, tau, nullptr, lane) && ldl_nopiv_wave<15>(A, 0.0, V, lane)) {
         ldl_inverse_wave<15>(V, P, lane);
