@@ -19,11 +19,20 @@
 //      the batch plus each listed pair compacted before it (an OR-scan) — so the result the replay needs
 //      is always among them.
 //   4. Thread 0 replays the scan over the compacted candidates, looking the results up.
+// That is tri_kernel (one workgroup per pair).  The default path splits it over the chip: tri_scan_kernel runs steps
+// 1-3's scans on S slices of keyframe 1's nodes per pair, tri_epi_kernel runs every epipolar test as one flat list,
+// tri_walk_kernel replays each pair on one wavefront (see the block above tri_scan_kernel); tri_kernel remains for a
+// pair whose candidates overflow the slices' workspace.
 // Float arithmetic without contraction; glibc's atan2f / tanf and correctly rounded sqrtf are restated
 // (omv_device.h), so the result is bit-exact to oracle/tri_oracle.cpp.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <vector>
+
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "../../include/omv.h"
 #include "omv_device.h"
@@ -318,7 +327,7 @@ __device__ bool epipolar_ok(const omv_tri_pair &P, const TriCams &C, int pr, con
 }
 
 // Exclusive block scan (kTriThreads threads, one value each) with associative `op`; `total` = op over all.
-template <typename T, typename Op>
+template <typename T, typename Op, int NT = kTriThreads>
 __device__ __forceinline__ T block_scan_excl(T v, T id, Op op, T *s_w, T &total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     T inc = v;
@@ -332,7 +341,7 @@ __device__ __forceinline__ T block_scan_excl(T v, T id, Op op, T *s_w, T &total)
     T pre = id;
     for (int i = 0; i < w; ++i) pre = op(pre, s_w[i]);
     total = pre;
-    for (int i = w; i < kTriWaves; ++i) total = op(total, s_w[i]);
+    for (int i = w; i < NT / 64; ++i) total = op(total, s_w[i]);
     T ex = __shfl_up(inc, 1, 64);
     if (lane == 0) ex = id;
     __syncthreads();
@@ -342,8 +351,126 @@ __device__ __forceinline__ T block_scan_excl(T v, T id, Op op, T *s_w, T &total)
 // compacted candidate code: distance bits 0-5, listed bit 6, camera pair bits 8-11
 constexpr uint16_t kCodeListed = 0x40;
 
+// Steps 1-2 over keyframe 1's nodes [a_lo, a_hi): the node intersection segment by segment, then the Hamming
+// distances tile by tile, the candidates that can matter compacted in scan order into v_pk / v_code (n_valid of
+// them); `flush` empties the staging when the next tile might not fit.  Every thread of the block calls it.
+template <typename Flush>
+__device__ __forceinline__ void scan_candidates(const omv_kf_view &K1, const omv_kf_view &K2, int a_lo, int a_hi,
+                                                int *seg_s1, int *seg_n1, int *seg_s2, int *seg_n2, int *seg_pref,
+                                                uint32_t *v_pk, uint16_t *v_code, int *s_wi, int &n_valid,
+                                                Flush &flush) {
+    const int tid = threadIdx.x;
+    auto add = [](int x, int y) { return x + y; };
+    for (int a0 = a_lo; a0 < a_hi; a0 += kSeg) {
+        // step 1: this segment's node intersection, in ascending node id
+        int s1 = 0, n1 = 0, s2 = 0, n2 = 0;
+        const int a = a0 + tid;
+        if (a < a_hi) {
+            const uint32_t id = K1.node_id[a];
+            int lo = 0, hi = K2.n_nodes;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (K2.node_id[mid] < id) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < K2.n_nodes && K2.node_id[lo] == id) {
+                s1 = K1.node_start[a], n1 = K1.node_start[a + 1] - s1;
+                s2 = K2.node_start[lo], n2 = K2.node_start[lo + 1] - s2;
+            }
+        }
+        const int has = (n1 > 0 && n2 > 0) ? 1 : 0;
+        int n_seg;
+        const int pos = block_scan_excl(has, 0, add, s_wi, n_seg);
+        int q_seg;
+        const int qoff = block_scan_excl(has ? n1 * n2 : 0, 0, add, s_wi, q_seg);
+        if (has) seg_s1[pos] = s1, seg_n1[pos] = n1, seg_s2[pos] = s2, seg_n2[pos] = n2, seg_pref[pos] = qoff;
+        if (tid == 0) seg_pref[n_seg] = q_seg;
+        __syncthreads();
+        // step 2: distances and compaction, tile by tile
+        for (int t0 = 0; t0 < q_seg; t0 += kTile) {
+            if (n_valid + kTile > kVal) flush();
+            uint32_t pk[kPerThread];
+            uint16_t cd[kPerThread];
+            int cnt = 0;
+            const int qb = t0 + tid * kPerThread;
+            if (qb < q_seg) {
+                int lo = 0, hi = n_seg;   // last node with seg_pref <= qb
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (seg_pref[mid] <= qb) lo = mid;
+                    else hi = mid;
+                }
+                // the thread's candidates (LDS walk), then each dependent global step for all of them together:
+                // keypoint indices, map-point flags, descriptors -- three memory round trips per tile instead of
+                // three per candidate
+                int nd = lo, loc = qb - seg_pref[lo];
+                int i1 = loc / seg_n2[nd], i2 = loc - i1 * seg_n2[nd];
+                int a1[kPerThread], a2[kPerThread];
+                const int nj = min(kPerThread, q_seg - qb);
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) {
+                    a1[j] = seg_s1[nd] + i1, a2[j] = seg_s2[nd] + i2;
+                    if (j + 1 < nj && ++i2 == seg_n2[nd]) {
+                        i2 = 0;
+                        if (++i1 == seg_n1[nd]) i1 = 0, ++nd;
+                    }
+                }
+                int x1[kPerThread], x2[kPerThread];
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) {
+                    const int jj = min(j, nj - 1);   // past the end: the last candidate again (loads stay in range)
+#ifdef OMV_TRI_CHECK
+                    if (a1[jj] < 0 || a1[jj] >= K1.node_start[K1.n_nodes] || a2[jj] < 0 || a2[jj] >= K2.node_start[K2.n_nodes]) {
+                        printf("scan bad a1 %d a2 %d (blk %d,%d tid %d qb %d q_seg %d nd %d n_seg %d)\n", a1[jj], a2[jj], blockIdx.x, blockIdx.y, tid, qb, q_seg, nd, n_seg);
+                        a1[jj] = 0, a2[jj] = 0;
+                    }
+#endif
+                    x1[j] = K1.node_idx[a1[jj]], x2[j] = K2.node_idx[a2[jj]];
+                }
+#ifdef OMV_TRI_CHECK
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j)
+                    if (x1[j] < 0 || x1[j] >= K1.n || x2[j] < 0 || x2[j] >= K2.n) {
+                        printf("scan bad x1 %d x2 %d (n %d %d) blk %d,%d\n", x1[j], x2[j], K1.n, K2.n, blockIdx.x, blockIdx.y);
+                        x1[j] = 0, x2[j] = 0;
+                    }
+#endif
+                bool free_[kPerThread];
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) free_[j] = !K1.has_mp[x1[j]] && !K2.has_mp[x2[j]];
+                uint4 d1[kPerThread][2], d2[kPerThread][2];
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) {
+                    const uint4 *p1 = reinterpret_cast<const uint4 *>(K1.desc + 32 * (size_t)x1[j]);
+                    const uint4 *p2 = reinterpret_cast<const uint4 *>(K2.desc + 32 * (size_t)x2[j]);
+                    d1[j][0] = p1[0], d1[j][1] = p1[1], d2[j][0] = p2[0], d2[j][1] = p2[1];
+                }
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) {
+                    if (j >= nj || !free_[j]) continue;
+                    const int dist = __popc(d1[j][0].x ^ d2[j][0].x) + __popc(d1[j][0].y ^ d2[j][0].y) +
+                                     __popc(d1[j][0].z ^ d2[j][0].z) + __popc(d1[j][0].w ^ d2[j][0].w) +
+                                     __popc(d1[j][1].x ^ d2[j][1].x) + __popc(d1[j][1].y ^ d2[j][1].y) +
+                                     __popc(d1[j][1].z ^ d2[j][1].z) + __popc(d1[j][1].w ^ d2[j][1].w);
+                    if (dist <= kTriLow) {
+                        const int pr = pair_of(cam_of(K1, x1[j]), cam_of(K2, x2[j]));
+                        pk[cnt] = (uint32_t)x1[j] << 16 | (uint32_t)x2[j];
+                        cd[cnt] = (uint16_t)(dist | (pr >= 0 ? kCodeListed | (pr << 8) : 0));
+                        ++cnt;
+                    }
+                }
+            }
+            int tot;
+            const int off = n_valid + block_scan_excl(cnt, 0, add, s_wi, tot);
+            for (int j = 0; j < cnt; ++j) v_pk[off + j] = pk[j], v_code[off + j] = cd[j];
+            n_valid += tot;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pairs, TriCams C, int only_stereo,
-                                                          int coarse, int check_ori, int32_t *n_matches, int *err) {
+                                                          int coarse, int check_ori, int32_t *n_matches, int *err,
+                                                          const int *only) {
     __shared__ uint8_t bins[kTriMaxKp];
     __shared__ int seg_s1[kSeg], seg_n1[kSeg], seg_s2[kSeg], seg_n2[kSeg], seg_pref[kSeg + 1];
     __shared__ uint32_t v_pk[kVal];      // idx1 << 16 | idx2
@@ -354,7 +481,8 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
     __shared__ unsigned s_wu[kTriWaves];
     __shared__ int hist[kHisto];
     __shared__ int s_keep[kHisto];
-    __shared__ int s_state, s_row, s_best, s_fin;
+    __shared__ int s_state, s_row, s_best, s_bidx, s_fin;
+    if (only && !only[blockIdx.x]) return;
     const omv_tri_pair &P = pairs[blockIdx.x];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
     const int tid = threadIdx.x;
@@ -365,27 +493,35 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
     }
     for (int i = tid; i < K1.n; i += kTriThreads) bins[i] = 0xff;
     if (tid < kHisto) hist[tid] = 0;
-    if (tid == 0) s_state = 0, s_row = -1, s_best = kTriLow;   // camera-pair state: LL before any assignment
+    if (tid == 0) s_state = 0, s_row = -1, s_best = kTriLow, s_bidx = -1;   // camera-pair state: LL before any assignment
     __syncthreads();
     auto add = [](int x, int y) { return x + y; };
-    // thread 0's replay state, carried across batches
-    int nmatch = 0, cur_row = -1, bestDist = kTriLow, bestIdx2 = -1;
-    auto finish_row = [&]() {
-        if (cur_row < 0 || bestIdx2 < 0) return;
-        P.match12[cur_row] = bestIdx2;
+    int nmatch = 0;   // thread 0's count
+    // the row the walk has open when it ends (its best match, if any, is written like a finished row)
+    auto finish_row = [&](int row, int best) {
+        if (row < 0 || best < 0) return;
+        P.match12[row] = best;
         ++nmatch;
         if (check_ori) {
-            float rot = K1.kps[cur_row].angle - K2.kps[bestIdx2].angle;
+            float rot = K1.kps[row].angle - K2.kps[best].angle;
             if ((double)rot < 0.0) rot += 360.0f;
             int bin = (int)roundf(rot * (1.0f / kHisto));
             if (bin == kHisto) bin = 0;
-            bins[cur_row] = (uint8_t)bin;
+            bins[row] = (uint8_t)bin;
         }
     };
     int n_valid = 0;
+#ifdef OMV_TRI_PROFILE
+    long long tq[5] = {0, 0, 0, 0, 0}, tl = wall_clock64();
+    int n_cand = 0, n_tests = 0, n_flush = 0, n_qseg = 0;
+#define OMV_TQ(k) (tq[k] += wall_clock64() - tl, tl = wall_clock64())
+#else
+#define OMV_TQ(k) ((void)0)
+#endif
     // epipolar tests of the compacted batch (step 3) and the in-order replay (step 4)
     auto flush = [&]() {
         __syncthreads();   // the last tile's compacted entries
+        OMV_TQ(1);
         if (!coarse) {
             // States entry k can meet: the last listed entry before it that is certain to pass the distance
             // test (an anchor: its distance <= every earlier distance of its row, and <= the replay's
@@ -433,6 +569,10 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
             }
             if (tid == 0) v_item[n_valid] = icarry;
             __syncthreads();
+            OMV_TQ(2);
+#ifdef OMV_TRI_PROFILE
+            n_cand += n_valid, n_tests += icarry, ++n_flush;
+#endif
             for (int j = tid; j < icarry; j += kTriThreads) {
                 int lo = 0, hi = n_valid;   // last k with v_item[k] <= j
                 while (hi - lo > 1) {
@@ -447,43 +587,54 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
                 if (epipolar_ok(P, C, state, K1.kps[pk >> 16], K2.kps[pk & 0xffff])) atomicOr(&v_res[lo], 1u << state);
             }
             __syncthreads();
+            OMV_TQ(3);
         }
         // step 4 on wave 0: 64 entries at a time staged in registers (one per lane), walked in order on wave-uniform
         // values (v_readlane), so the dependent chain is scalar ALU work instead of LDS round trips; the rows the walk
         // finishes are listed (row << 16 | idx2, in v_item, free after step 3) and written out by all threads after
-        int n_fin = 0;
+        // the walk's state (camera-pair state, open row, its best distance / match) lives in LDS between batches and
+        // in scalar registers during one: every value of the walk is wave-uniform (readfirstlane / readlane)
         if (tid < 64) {
             const int lane = tid;
-            int state = s_state;
-            for (int c0 = 0; c0 < n_valid; c0 += 64) {
+            int state = __builtin_amdgcn_readfirstlane(s_state), cur_row = __builtin_amdgcn_readfirstlane(s_row);
+            int bestDist = __builtin_amdgcn_readfirstlane(s_best), bestIdx2 = __builtin_amdgcn_readfirstlane(s_bidx);
+            int n_fin = 0;
+            const int nv = __builtin_amdgcn_readfirstlane(n_valid);   // uniform (a block-scan total)
+            // branch-free: a taken scalar branch costs a fetch redirect, which dominated the walk (~280 cycles per
+            // entry with the branches); the tail of the last 64 is padded with no-op entries (the last entry's row,
+            // distance 63 > any bestDist, not listed)
+            for (int c0 = 0; c0 < nv; c0 += 64) {
                 const int k = c0 + lane;
-                const bool in = k < n_valid;
-                const uint32_t pk_l = in ? v_pk[k] : 0u;
-                const int code_l = in ? (int)v_code[k] : 0;
+                const bool in = k < nv;
+                const uint32_t pk_l = v_pk[in ? k : nv - 1];
+                const int code_l = in ? (int)v_code[k] : 0x3f;
                 const uint32_t res_l = (in && !coarse) ? v_res[k] : 0xffffffffu;
-                const int m = min(64, n_valid - c0);
-                for (int j = 0; j < m; ++j) {
+#pragma unroll
+                for (int j = 0; j < 64; ++j) {
                     const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pk_l, j);
                     const int code = __builtin_amdgcn_readlane(code_l, j);
-                    const int idx1 = (int)(pk >> 16);
-                    if (idx1 != cur_row) {
-                        if (cur_row >= 0 && bestIdx2 >= 0) {
-                            if (lane == 0) v_item[n_fin] = (cur_row << 16) | bestIdx2;
-                            ++n_fin;
-                        }
-                        cur_row = idx1, bestDist = kTriLow, bestIdx2 = -1;
-                    }
-                    const int dist = code & 0x3f;
-                    if (dist > bestDist) continue;
-                    if (code & kCodeListed) state = (code >> 8) & 15;
                     const uint32_t res = (uint32_t)__builtin_amdgcn_readlane((int)res_l, j);
-                    if ((res >> state) & 1u) bestIdx2 = (int)(pk & 0xffff), bestDist = dist;
+                    const int idx1 = (int)(pk >> 16);
+                    const bool newrow = idx1 != cur_row;
+                    const bool emit = newrow && cur_row >= 0 && bestIdx2 >= 0;
+                    v_item[n_fin] = (cur_row << 16) | (bestIdx2 & 0xffff);   // kept only when emit (n_fin advances)
+                    n_fin += emit ? 1 : 0;
+                    cur_row = newrow ? idx1 : cur_row;
+                    bestDist = newrow ? kTriLow : bestDist;
+                    bestIdx2 = newrow ? -1 : bestIdx2;
+                    const int dist = code & 0x3f;
+                    const bool cand = dist <= bestDist;
+                    state = (cand && (code & kCodeListed)) ? (code >> 8) & 15 : state;
+                    const bool take = cand && ((res >> state) & 1u);
+                    bestIdx2 = take ? (int)(pk & 0xffff) : bestIdx2;
+                    bestDist = take ? dist : bestDist;
                 }
             }
-            if (lane == 0) s_state = state, s_row = cur_row, s_best = bestDist, s_fin = n_fin;
+            if (lane == 0) s_state = state, s_row = cur_row, s_best = bestDist, s_bidx = bestIdx2, s_fin = n_fin;
         }
         __syncthreads();
-        n_fin = s_fin;
+        OMV_TQ(4);
+        const int n_fin = s_fin;
         nmatch += n_fin;   // thread 0's count (the only one read)
         for (int i = tid; i < n_fin; i += kTriThreads) {
             const int row = (int)((uint32_t)v_item[i] >> 16), best = v_item[i] & 0xffff;
@@ -497,75 +648,14 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
             }
         }
         __syncthreads();
+        OMV_TQ(0);
         n_valid = 0;
     };
-    for (int a0 = 0; a0 < K1.n_nodes && !only_stereo; a0 += kSeg) {
-        // step 1: this segment's node intersection, in ascending node id
-        int s1 = 0, n1 = 0, s2 = 0, n2 = 0;
-        const int a = a0 + tid;
-        if (a < K1.n_nodes) {
-            const uint32_t id = K1.node_id[a];
-            int lo = 0, hi = K2.n_nodes;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (K2.node_id[mid] < id) lo = mid + 1;
-                else hi = mid;
-            }
-            if (lo < K2.n_nodes && K2.node_id[lo] == id) {
-                s1 = K1.node_start[a], n1 = K1.node_start[a + 1] - s1;
-                s2 = K2.node_start[lo], n2 = K2.node_start[lo + 1] - s2;
-            }
-        }
-        const int has = (n1 > 0 && n2 > 0) ? 1 : 0;
-        int n_seg;
-        const int pos = block_scan_excl(has, 0, add, s_wi, n_seg);
-        int q_seg;
-        const int qoff = block_scan_excl(has ? n1 * n2 : 0, 0, add, s_wi, q_seg);
-        if (has) seg_s1[pos] = s1, seg_n1[pos] = n1, seg_s2[pos] = s2, seg_n2[pos] = n2, seg_pref[pos] = qoff;
-        if (tid == 0) seg_pref[n_seg] = q_seg;
-        __syncthreads();
-        // step 2: distances and compaction, tile by tile
-        for (int t0 = 0; t0 < q_seg; t0 += kTile) {
-            if (n_valid + kTile > kVal) flush();
-            uint32_t pk[kPerThread];
-            uint16_t cd[kPerThread];
-            int cnt = 0;
-            const int qb = t0 + tid * kPerThread;
-            if (qb < q_seg) {
-                int lo = 0, hi = n_seg;   // last node with seg_pref <= qb
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (seg_pref[mid] <= qb) lo = mid;
-                    else hi = mid;
-                }
-                int nd = lo, loc = qb - seg_pref[lo];
-                int i1 = loc / seg_n2[nd], i2 = loc - i1 * seg_n2[nd];
-                for (int j = 0; j < kPerThread && qb + j < q_seg; ++j) {
-                    const int idx1 = K1.node_idx[seg_s1[nd] + i1], idx2 = K2.node_idx[seg_s2[nd] + i2];
-                    if (!K1.has_mp[idx1] && !K2.has_mp[idx2]) {
-                        const int dist = omv::hamming256((const uint64_t *)(K1.desc + 32 * (size_t)idx1),
-                                                         (const uint64_t *)(K2.desc + 32 * (size_t)idx2));
-                        if (dist <= kTriLow) {
-                            const int pr = pair_of(cam_of(K1, idx1), cam_of(K2, idx2));
-                            pk[cnt] = (uint32_t)idx1 << 16 | (uint32_t)idx2;
-                            cd[cnt] = (uint16_t)(dist | (pr >= 0 ? kCodeListed | (pr << 8) : 0));
-                            ++cnt;
-                        }
-                    }
-                    if (++i2 == seg_n2[nd]) {
-                        i2 = 0;
-                        if (++i1 == seg_n1[nd]) i1 = 0, ++nd;
-                    }
-                }
-            }
-            int tot;
-            const int off = n_valid + block_scan_excl(cnt, 0, add, s_wi, tot);
-            for (int j = 0; j < cnt; ++j) v_pk[off + j] = pk[j], v_code[off + j] = cd[j];
-            n_valid += tot;
-        }
-    }
+    if (!only_stereo)
+        scan_candidates(K1, K2, 0, K1.n_nodes, seg_s1, seg_n1, seg_s2, seg_n2, seg_pref, v_pk, v_code, s_wi, n_valid,
+                        flush);
     flush();
-    if (tid == 0) finish_row();
+    if (tid == 0) finish_row(s_row, s_bidx);
     __syncthreads();
     if (check_ori) {   // rotation histogram: keep the three largest bins (ComputeThreeMaxima, :2537-2573)
         for (int i = tid; i < K1.n; i += kTriThreads)
@@ -599,6 +689,368 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
         if (tid == 0) nmatch -= tot;
     }
     if (tid == 0) n_matches[blockIdx.x] = nmatch;
+#ifdef OMV_TRI_PROFILE
+    OMV_TQ(1);
+    if (tid == 0 && blockIdx.x < 4)
+        printf("tri pair %d ticks(100MHz): scan+dist %lld scans %lld epipolar %lld replay %lld writeout %lld; candidates %d tests %d flushes %d pairs scanned %d\n",
+               blockIdx.x, tq[1], tq[2], tq[3], tq[4], tq[0], n_cand, n_tests, n_flush, n_qseg);
+#endif
+#undef OMV_TQ
+}
+
+// ---- the same search as three launches, the pairs' scans spread over the chip -----------------------------------
+// tri_kernel runs one keyframe pair per workgroup: at 2 waves per SIMD its dependent loads, its epipolar tests and the
+// one-wave replay leave a pair ~0.7 ms on one CU.  Here
+//   tri_scan_kernel  (slice, pair): steps 1-2 over 1/S of keyframe 1's nodes (a row -- one idx1 -- never spans two
+//                    slices: a keypoint sits in one node), then the state masks of step 3 with the camera-pair state
+//                    entering the slice unknown (all ten states until the slice's first anchor; slice 0 starts in
+//                    LL); entries (pk, code word) and the epipolar test list (entry, state) written out;
+//   tri_epi_kernel   every test of every slice as one flat work list (one test per thread);
+//   tri_walk_kernel  one workgroup per pair: the replay over the slices in order on one wavefront, branch-free on
+//                    scalar registers (one 32-bit word per entry), then the finished rows, the rotation histogram.
+// Per (pair, slice) the entries and tests fit fixed capacities; a pair that overflows one is flagged and the host
+// runs tri_kernel for it alone.
+struct TriWs {
+    uint32_t *pk;      // [n_pairs * S][ecap] idx1 << 16 | idx2
+    uint32_t *w;       // [..][ecap] dist | listed << 6 | pair state << 7 | row start << 11
+    uint32_t *res;     // [..][ecap] epipolar results, one bit per camera-pair state (all ones when coarse)
+    uint32_t *tests;   // [..][tcap] entry << 4 | state
+    int *cnt, *tcnt;   // [n_pairs * S]
+    int *over;         // [n_pairs] a capacity was exceeded: the pair is rerun by tri_kernel
+    int S, ecap, tcap;
+};
+
+__global__ void __launch_bounds__(kTriThreads) tri_scan_kernel(const omv_tri_pair *pairs, int only_stereo, int coarse,
+                                                               TriWs ws) {
+    __shared__ int seg_s1[kSeg], seg_n1[kSeg], seg_s2[kSeg], seg_n2[kSeg], seg_pref[kSeg + 1];
+    __shared__ uint32_t v_pk[kVal];
+    __shared__ uint16_t v_code[kVal];
+    __shared__ int s_wi[kTriWaves];
+    __shared__ unsigned s_wu[kTriWaves];
+    const int sl = blockIdx.x, p = blockIdx.y, S = ws.S, tid = threadIdx.x;
+    const omv_tri_pair &P = pairs[p];
+    const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
+    const size_t slot = (size_t)p * S + sl, ebase = slot * ws.ecap, tbase = slot * ws.tcap;
+    const bool bad = K1.n > kTriMaxKp || K2.n > 65535;   // reported by the walk
+    const int a_lo = (int)((long long)K1.n_nodes * sl / S), a_hi = (int)((long long)K1.n_nodes * (sl + 1) / S);
+    auto add = [](int x, int y) { return x + y; };
+    auto seg_min = [](unsigned x, unsigned y) {
+        return ((x | y) & 0x100u) | ((y & 0x100u) ? (y & 0xffu) : min(x & 0xffu, y & 0xffu));
+    };
+    auto seg_or = [](unsigned x, unsigned y) {
+        return ((x | y) & 0x10000u) | ((y & 0x10000u) ? (y & 0xffffu) : ((x | y) & 0xffffu));
+    };
+    int n_valid = 0, n_out = 0, t_out = 0, last_row = -1;
+    // scan states carried from batch to batch: a continuing row's earlier distances bound bestDist from below
+    // (bestDist is one of them or TH_LOW), so an entry at or below their minimum is an anchor; the pair's state
+    // is LL entering slice 0 and unknown entering any other
+    unsigned cmin = 0xffu, cor = sl == 0 ? 1u : 0x3ffu;
+    auto flush = [&]() {
+        __syncthreads();   // the last tile's compacted entries
+        int icarry = 0;
+        for (int t0 = 0; t0 < n_valid; t0 += kTriThreads) {
+            const int k = t0 + tid;
+            unsigned vmin = 0xffu, vor = 0;
+            bool listed = false;
+            int dist = 0, pr = 0;
+            uint32_t pk = 0;
+            if (k < n_valid) {
+                const int code = v_code[k];
+                listed = (code & kCodeListed) != 0;
+                dist = code & 0x3f, pr = (code >> 8) & 15;
+                pk = v_pk[k];
+                const int prev = k > 0 ? (int)(v_pk[k - 1] >> 16) : last_row;
+                vmin = ((int)(pk >> 16) != prev ? 0x100u : 0u) | (unsigned)dist;
+            }
+            unsigned tmin;
+            const unsigned bmin = seg_min(cmin, block_scan_excl(vmin, 0xffu, seg_min, s_wu, tmin));
+            const bool row_start = (vmin & 0x100u) != 0;
+            const bool anchor = listed && (row_start || (unsigned)dist <= (bmin & 0xffu));
+            if (listed) vor = (anchor ? 0x10000u : 0u) | (1u << pr);
+            unsigned tor;
+            const unsigned bor_ = seg_or(cor, block_scan_excl(vor, 0u, seg_or, s_wu, tor));
+            const unsigned m = coarse ? 0u : (listed ? (1u << pr) : (bor_ & 0x3ffu));
+            const int cnt = k < n_valid ? __popc(m) : 0;
+            int itot;
+            const int off = t_out + icarry + block_scan_excl(cnt, 0, add, s_wi, itot);
+            const int e = n_out + k;
+            if (k < n_valid && e < ws.ecap) {
+                ws.pk[ebase + e] = pk;
+                ws.w[ebase + e] = (uint32_t)dist | (listed ? 0x40u : 0u) | ((uint32_t)pr << 7) | (row_start ? 0x800u : 0u);
+                ws.res[ebase + e] = coarse ? 0x3ffu : 0u;
+                unsigned mm = m;
+                for (int r = 0; mm; ++r, mm &= mm - 1)
+                    if (off + r < ws.tcap) ws.tests[tbase + off + r] = (uint32_t)e << 4 | (uint32_t)(__ffs(mm) - 1);
+            }
+            cmin = seg_min(cmin, tmin);
+            cor = seg_or(cor, tor);
+            icarry += itot;
+        }
+        if (n_valid > 0) last_row = (int)(v_pk[n_valid - 1] >> 16);
+        n_out += n_valid, t_out += icarry;
+        __syncthreads();   // v_pk is refilled by the next tile
+        n_valid = 0;
+    };
+    if (!only_stereo && !bad)
+        scan_candidates(K1, K2, a_lo, a_hi, seg_s1, seg_n1, seg_s2, seg_n2, seg_pref, v_pk, v_code, s_wi, n_valid,
+                        flush);
+    flush();
+    if (tid == 0) {
+        ws.cnt[slot] = min(n_out, ws.ecap), ws.tcnt[slot] = min(t_out, ws.tcap);
+        if (n_out > ws.ecap || t_out > ws.tcap) atomicOr(&ws.over[p], 1);
+    }
+}
+
+constexpr int kEpiThreads = 256, kEpiPerSlot = 2;   // workgroups per (pair, slice) of the flat test list
+__global__ void __launch_bounds__(kEpiThreads) tri_epi_kernel(const omv_tri_pair *pairs, TriCams C, TriWs ws) {
+    const int slot = blockIdx.y, p = slot / ws.S;
+    // an overflowed pair's test list has holes (the tests of entries past the capacity are not written): skip it,
+    // tri_kernel reruns the pair
+    if (ws.over[p]) return;
+    const omv_tri_pair &P = pairs[p];
+    const size_t ebase = (size_t)slot * ws.ecap, tbase = (size_t)slot * ws.tcap;
+    const int nt = ws.tcnt[slot];
+    for (int j = blockIdx.x * kEpiThreads + threadIdx.x; j < nt; j += kEpiPerSlot * kEpiThreads) {
+        const uint32_t it = ws.tests[tbase + j];
+        const int e = (int)(it >> 4), state = (int)(it & 15);
+#ifdef OMV_TRI_CHECK
+        if (e >= ws.ecap || state > 9) { printf("epi bad slot %d j %d nt %d e %d state %d\n", slot, j, nt, e, state); continue; }
+        {
+            const uint32_t pk0 = ws.pk[ebase + e];
+            if ((int)(pk0 >> 16) >= P.kf1.n || (int)(pk0 & 0xffff) >= P.kf2.n) { printf("epi bad pk slot %d e %d pk %x\n", slot, e, pk0); continue; }
+        }
+#endif
+        const uint32_t pk = ws.pk[ebase + e];
+        if (epipolar_ok(P, C, state, P.kf1.kps[pk >> 16], P.kf2.kps[pk & 0xffff]))
+            atomicOr(&ws.res[ebase + e], 1u << state);
+    }
+}
+
+constexpr int kWalkThreads = 256;
+constexpr int kWalkRows = 4096;   // rows of the parallel replay (more: the scalar walk)
+constexpr uint64_t kIdentityMap = 0x9876543210ull;   // state s -> s, nibble s
+
+// One row's replay from camera-pair state `st` (entries [e0, e1) of the workspace): the state after it and its best
+// entry (-1: none) -- the scalar walk's update, restated per row.
+__device__ __forceinline__ int walk_row(const TriWs &ws, int e0, int e1, int &st) {
+    int bestDist = kTriLow, bestK = -1;
+#ifdef OMV_TRI_CHECK
+    if (e0 < 0 || e1 < e0 || e1 - e0 > 65536) { printf("walk_row bad %d %d\n", e0, e1); return -1; }
+#endif
+    for (int e = e0; e < e1; ++e) {
+        const uint32_t w = ws.w[e] | (ws.res[e] << 12);
+        const int dist = (int)(w & 63u);
+        const bool cand = dist <= bestDist;
+        st = (cand && ((w >> 6) & 1u)) ? (int)((w >> 7) & 15u) : st;
+        const bool take = cand && ((w >> (12 + st)) & 1u);
+        bestK = take ? e : bestK;
+        bestDist = take ? dist : bestDist;
+    }
+    return bestK;
+}
+
+__global__ void __launch_bounds__(kWalkThreads) tri_walk_kernel(const omv_tri_pair *pairs, int check_ori, TriWs ws,
+                                                                int32_t *n_matches, int *err, int par_walk) {
+    __shared__ uint8_t bins[kTriMaxKp];
+    __shared__ int fin[kTriMaxKp];   // finished rows: the global entry index of the row's best (parallel replay: rows)
+    __shared__ uint8_t instate[kWalkRows + 64];
+    __shared__ int hist[kHisto], s_keep[kHisto], s_wi[kWalkThreads / 64], s_fin, s_rows;
+    const int p = blockIdx.x, tid = threadIdx.x, S = ws.S;
+    const omv_tri_pair &P = pairs[p];
+    const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
+    if (ws.over[p]) return;   // rerun by tri_kernel
+    for (int i = tid; i < K1.n; i += kWalkThreads) P.match12[i] = -1;
+    if (K1.n > kTriMaxKp || K2.n > 65535) {
+        if (tid == 0) atomicExch(err, OMV_ERR_CAPACITY), n_matches[p] = 0;
+        return;
+    }
+    for (int i = tid; i < K1.n; i += kWalkThreads) bins[i] = 0xff;
+    if (tid < kHisto) hist[tid] = 0;
+    auto add = [](int x, int y) { return x + y; };
+    // rows of the pair (entries with the row-start bit)
+    int nr = 0;
+    for (int sl = 0; sl < S; ++sl) {
+        const int slot = p * S + sl, base = slot * ws.ecap, n = ws.cnt[slot];
+        for (int k = tid; k < n; k += kWalkThreads) nr += (ws.w[base + k] >> 11) & 1u;
+    }
+    for (int d = 32; d >= 1; d >>= 1) nr += __shfl_xor(nr, d, 64);
+    if ((tid & 63) == 0) s_wi[tid >> 6] = nr;
+    __syncthreads();
+    const int R = s_wi[0] + s_wi[1] + s_wi[2] + s_wi[3];
+    __syncthreads();
+    int nmatch = 0;
+    if (par_walk && R <= kWalkRows) {
+        // Parallel replay.  The walk's only coupling between rows is the camera-pair state (bestDist restarts per
+        // row), so each row is a map state -> state (ten nibbles), evaluated per row on its own thread; one
+        // wavefront chains the maps from LL (a table lookup per row); then each row is replayed from its entering
+        // state for its best.  Rows never span slices, so a row ends at the next row start or its slice's end.
+        int *rstart = fin, *rend = fin + kWalkRows;
+        uint64_t *rmap = reinterpret_cast<uint64_t *>(fin + 2 * kWalkRows);
+        int rbase = 0;
+        for (int sl = 0; sl < S; ++sl) {
+            const int slot = p * S + sl, base = slot * ws.ecap, n = ws.cnt[slot];
+            const int r0 = rbase;
+            for (int c0 = 0; c0 < n; c0 += kWalkThreads) {
+                const int k = c0 + tid;
+                const int f = k < n ? (int)((ws.w[base + k] >> 11) & 1u) : 0;
+                int tot;
+                const int pos = rbase + block_scan_excl<int, decltype(add), kWalkThreads>(f, 0, add, s_wi, tot);
+#ifdef OMV_TRI_CHECK
+                if (f && pos >= kWalkRows) printf("rstart overflow pos %d R %d\n", pos, R);
+                if (f && pos < kWalkRows)
+#else
+                if (f)
+#endif
+                rstart[pos] = base + k;
+                rbase += tot;
+            }
+            __syncthreads();
+            for (int r = r0 + tid; r < rbase; r += kWalkThreads) rend[r] = r + 1 < rbase ? rstart[r + 1] : base + n;
+        }
+        __syncthreads();
+        for (int r = tid; r < R; r += kWalkThreads) {
+            uint64_t m = 0;
+#pragma unroll
+            for (int s0 = 0; s0 < 10; ++s0) {
+                int st = s0;
+                walk_row(ws, rstart[r], rend[r], st);
+                m |= (uint64_t)st << (4 * s0);
+            }
+            rmap[r] = m;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const int lane = tid;
+            int st = 0;
+            for (int c0 = 0; c0 < R; c0 += 64) {
+                const uint64_t m_l = c0 + lane < R ? rmap[c0 + lane] : kIdentityMap;
+                const uint32_t lo_l = (uint32_t)m_l, hi_l = (uint32_t)(m_l >> 32);
+#pragma unroll
+                for (int j = 0; j < 64; ++j) {
+                    const uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo_l, j) |
+                                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi_l, j) << 32);
+                    instate[c0 + j] = (uint8_t)st;
+                    st = (int)((m >> (4 * st)) & 15u);
+                }
+            }
+        }
+        __syncthreads();
+        for (int r = tid; r < R; r += kWalkThreads) {
+            int st = instate[r];
+            const int bk = walk_row(ws, rstart[r], rend[r], st);
+            if (bk < 0) continue;
+            const uint32_t pk = ws.pk[bk];
+            const int row = (int)(pk >> 16), best = (int)(pk & 0xffff);
+#ifdef OMV_TRI_CHECK
+            if (row >= K1.n || best >= K2.n) { printf("walk bad row %d best %d bk %d r %d\n", row, best, bk, r); continue; }
+#endif
+            P.match12[row] = best;
+            ++nmatch;
+            if (check_ori) {
+                float rot = K1.kps[row].angle - K2.kps[best].angle;
+                if ((double)rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * (1.0f / kHisto));
+                if (bin == kHisto) bin = 0;
+                bins[row] = (uint8_t)bin;
+            }
+        }
+        for (int d = 32; d >= 1; d >>= 1) nmatch += __shfl_xor(nmatch, d, 64);
+        if ((tid & 63) == 0) s_wi[tid >> 6] = nmatch;
+        __syncthreads();
+        nmatch = s_wi[0] + s_wi[1] + s_wi[2] + s_wi[3];
+        __syncthreads();
+    } else {
+    if (tid < 64) {
+        // one 32-bit word per entry: dist 0-5, listed 6, state 7-10, row start 11, results 12-21; a padding entry
+        // (distance 63, no row start) changes nothing
+        const int lane = tid;
+        int state = 0, bestDist = kTriLow, bestK = -1, n_fin = 0;
+        for (int sl = 0; sl < S; ++sl) {
+            const int slot = p * S + sl;
+            const int base = slot * ws.ecap, n = __builtin_amdgcn_readfirstlane(ws.cnt[slot]);
+            auto load = [&](int c0) {
+                const int k = c0 + lane;
+                return k < n ? (ws.w[base + k] | (ws.res[base + k] << 12)) : 63u;
+            };
+            uint32_t nxt = n > 0 ? load(0) : 63u;
+            for (int c0 = 0; c0 < n; c0 += 64) {
+                const uint32_t w_l = nxt;
+                if (c0 + 64 < n) nxt = load(c0 + 64);   // the next 64 in flight during this walk
+#pragma unroll
+                for (int j = 0; j < 64; ++j) {
+                    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)w_l, j);
+                    const bool rs = (w >> 11) & 1u;
+                    fin[n_fin] = bestK;   // kept only when the row ends with a best (n_fin advances)
+                    n_fin += (rs && bestK >= 0) ? 1 : 0;
+                    bestDist = rs ? kTriLow : bestDist;
+                    bestK = rs ? -1 : bestK;
+                    const int dist = (int)(w & 63u);
+                    const bool cand = dist <= bestDist;
+                    state = (cand && ((w >> 6) & 1u)) ? (int)((w >> 7) & 15u) : state;
+                    const bool take = cand && ((w >> (12 + state)) & 1u);
+                    bestK = take ? base + c0 + j : bestK;
+                    bestDist = take ? dist : bestDist;
+                }
+            }
+        }
+        fin[n_fin] = bestK;
+        n_fin += bestK >= 0 ? 1 : 0;
+        if (lane == 0) s_fin = n_fin;
+    }
+    __syncthreads();
+    const int n_fin = s_fin;
+    nmatch = n_fin;
+    for (int i = tid; i < n_fin; i += kWalkThreads) {
+        const uint32_t pk = ws.pk[fin[i]];
+        const int row = (int)(pk >> 16), best = (int)(pk & 0xffff);
+        P.match12[row] = best;
+        if (check_ori) {
+            float rot = K1.kps[row].angle - K2.kps[best].angle;
+            if ((double)rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / kHisto));
+            if (bin == kHisto) bin = 0;
+            bins[row] = (uint8_t)bin;
+        }
+    }
+    }
+    __syncthreads();
+    if (check_ori) {   // rotation histogram: keep the three largest bins (ComputeThreeMaxima, :2537-2573)
+        for (int i = tid; i < K1.n; i += kWalkThreads)
+            if (bins[i] != 0xff) atomicAdd(&hist[bins[i]], 1);
+        __syncthreads();
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < kHisto; i++) {
+                const int sv = hist[i];
+                if (sv > max1) {
+                    max3 = max2, max2 = max1, max1 = sv;
+                    ind3 = ind2, ind2 = ind1, ind1 = i;
+                } else if (sv > max2) {
+                    max3 = max2, max2 = sv;
+                    ind3 = ind2, ind2 = i;
+                } else if (sv > max3) {
+                    max3 = sv;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) ind2 = -1, ind3 = -1;
+            else if (max3 < 0.1f * (float)max1) ind3 = -1;
+            for (int i = 0; i < kHisto; ++i) s_keep[i] = (i == ind1 || i == ind2 || i == ind3) ? 1 : 0;
+        }
+        __syncthreads();
+        int removed = 0;
+        for (int i = tid; i < K1.n; i += kWalkThreads)
+            if (bins[i] != 0xff && !s_keep[bins[i]]) P.match12[i] = -1, ++removed;
+        for (int d = 32; d >= 1; d >>= 1) removed += __shfl_xor(removed, d, 64);
+        if ((tid & 63) == 0) s_wi[tid >> 6] = removed;
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int w2 = 0; w2 < kWalkThreads / 64; ++w2) tot += s_wi[w2];
+            nmatch -= tot;
+        }
+    }
+    if (tid == 0) n_matches[p] = nmatch;
 }
 
 // Frame::ComputeMultiFishEyeMatches' depth check (src/Frame.cc:1488-1512) on the Lowe-filtered
@@ -728,18 +1180,50 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
         C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
         if (C.model[c] != OMV_CAM_KB8 && C.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
     }
-    omv_tri_pair *d_pairs = nullptr;
-    int *d_err = nullptr;
-    HIP_OK(hipMallocAsync((void **)&d_pairs, sizeof(omv_tri_pair) * n_pairs + sizeof(int), st));
-    d_err = (int *)(d_pairs + n_pairs);
+    // S slices per pair: about 1,024 scan workgroups in all (at most 16 per pair)
+    int S = std::max(1, std::min(16, (1024 + n_pairs - 1) / n_pairs));
+    int ecap = std::max(2048, 32768 / S);
+    // test knobs: the slice count, and the entry capacity (a small one forces the overflow rerun)
+    if (const char *e = getenv("OMV_TRI_SLICES")) S = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("OMV_TRI_ECAP")) ecap = std::max(1, atoi(e));
+    const int tcap = 2 * ecap;
+    const size_t slots = (size_t)n_pairs * S;
+    const size_t bytes = sizeof(omv_tri_pair) * n_pairs + slots * (size_t)ecap * 12 + slots * (size_t)tcap * 4 +
+                         (2 * slots + 2 * (size_t)n_pairs + 1) * sizeof(int);
+    char *blob = nullptr;
+    HIP_OK(hipMallocAsync((void **)&blob, bytes, st));
+    omv_tri_pair *d_pairs = reinterpret_cast<omv_tri_pair *>(blob);
+    TriWs ws;
+    ws.pk = reinterpret_cast<uint32_t *>(d_pairs + n_pairs);
+    ws.w = ws.pk + slots * ecap;
+    ws.res = ws.w + slots * ecap;
+    ws.tests = ws.res + slots * ecap;
+    ws.cnt = reinterpret_cast<int *>(ws.tests + slots * tcap);
+    ws.tcnt = ws.cnt + slots;
+    ws.over = ws.tcnt + slots;
+    int *d_err = ws.over + n_pairs;
+    ws.S = S, ws.ecap = ecap, ws.tcap = tcap;
     HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(omv_tri_pair) * n_pairs, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
-    tri_kernel<<<n_pairs, kTriThreads, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err);
+    HIP_OK(hipMemsetAsync(ws.over, 0, sizeof(int) * (n_pairs + 1), st));   // overflow flags and the error word
+    tri_scan_kernel<<<dim3(S, n_pairs), kTriThreads, 0, st>>>(d_pairs, only_stereo, coarse, ws);
+    if (!coarse && !only_stereo) tri_epi_kernel<<<dim3(kEpiPerSlot, (unsigned)slots), kEpiThreads, 0, st>>>(d_pairs, C, ws);
+    const char *wk = getenv("OMV_TRI_WALK");   // test knob: "seq" = the scalar walk
+    tri_walk_kernel<<<n_pairs, kWalkThreads, 0, st>>>(d_pairs, check_ori, ws, n_matches, d_err,
+                                                      wk && !strcmp(wk, "seq") ? 0 : 1);
     HIP_OK(hipGetLastError());
-    int h_err = 0;
-    HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipFreeAsync(d_pairs, st));
+    std::vector<int> over(n_pairs + 1);
+    HIP_OK(hipMemcpyAsync(over.data(), ws.over, sizeof(int) * (n_pairs + 1), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    int h_err = over[n_pairs];
+    if (std::any_of(over.begin(), over.begin() + n_pairs, [](int v) { return v != 0; })) {
+        // a pair with more candidates than the workspace holds: the one-workgroup search for it alone
+        tri_kernel<<<n_pairs, kTriThreads, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err,
+                                                    ws.over);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    HIP_OK(hipFreeAsync(blob, st));
     return h_err ? (omv_status)h_err : OMV_OK;
 }
 

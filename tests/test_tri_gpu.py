@@ -69,6 +69,26 @@ def test_search_for_triangulation_shapes(oracle, kw):
         assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
 
 
+@pytest.mark.parametrize("knobs", [dict(OMV_TRI_SLICES="1"), dict(OMV_TRI_SLICES="64"),
+                                   dict(OMV_TRI_SLICES="1", OMV_TRI_WALK="seq"), dict(OMV_TRI_WALK="seq"),
+                                   dict(OMV_TRI_ECAP="64"), dict(OMV_TRI_SLICES="3", OMV_TRI_ECAP="200")])
+def test_search_for_triangulation_slices_and_rerun(oracle, monkeypatch, knobs):
+    """The sliced search (scan / flat epipolar tests / walk) at one slice (the entering camera-pair state always
+    known), at 64 slices (most slices enter with the state unknown and test every state up to their first anchor),
+    with the scalar walk instead of the per-row state maps, and with entry capacities small enough that pairs
+    overflow and are rerun by the one-workgroup kernel."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    pairs = [synth_tri.make_tri_pair(seed=50 + s, n_pts=700, n_distract=300) for s in range(4)]
+    dp = _device_pairs(pairs)
+    m = ORBmatcher(0.6, True)
+    n = m.SearchForTriangulation(dp, pairs[0]["cams"]).cpu().numpy()
+    for i, p in enumerate(pairs):
+        n_o, m_o = oracle.search_for_triangulation(p, check_ori=True)
+        assert n[i] == n_o, (i, n[i], n_o)
+        assert np.array_equal(dp[i]["match12"].cpu().numpy(), m_o), i
+
+
 @pytest.mark.parametrize("model", ["pinhole", ["pinhole", "kb8", "kb8", "pinhole"], ["kb8", "pinhole", "pinhole", "kb8"]])
 @pytest.mark.parametrize("check_ori", [False, True])
 def test_search_for_triangulation_pinhole_rig(oracle, model, check_ori):
