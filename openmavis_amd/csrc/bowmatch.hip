@@ -17,6 +17,8 @@
 // rotation bins in LDS bytes; the top-3 filter runs over them at the end.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -107,7 +109,14 @@ __device__ __forceinline__ int frame_block(const omv_kf_view &F, int idx) {
 // index), ascending by (distance, node position); 0xffffffff past the end.  Claims are the only dynamic filter, so the first two
 // unclaimed entries are the reference's best and second whenever the block holds <= kTop candidates or two
 // of them are unclaimed; otherwise the resolve rescans the node.
-constexpr int kTop = 8, kRecWords = 8 + 4 * kTop, kChunk = 32;   // kChunk * kRecWords: a multiple of 64
+// Per mode: (KeyFrame, Frame) keeps 16 entries per camera block -- its four blocks' short lists ran out (a node rescan
+// on one wavefront) for ~4 % of the keypoints at 8 -- and (KeyFrame, KeyFrame) 8.  kChunk * kRecWords: a multiple of 64.
+template <int MODE>
+struct BowCfg {
+    static constexpr int top = MODE == OMV_BOW_KF_FRAME ? 16 : 8;
+    static constexpr int rec = 8 + 4 * top;
+    static constexpr int chunk = MODE == OMV_BOW_KF_FRAME ? 16 : 32;
+};
 constexpr int kBowWaves = 4;   // wavefronts per resolve workgroup (kChunk * kBowWaves records staged per chunk)
 
 // Static filters + camera block of candidate idx2 (-1: not a candidate whatever the claims)
@@ -121,6 +130,7 @@ __device__ __forceinline__ int cand_block(const omv_kf_view &O, int idx2) {
 template <int MODE>
 __global__ void __launch_bounds__(256) bow_cand_kernel(const omv_bow_job *jobs, const int *rec_off, uint32_t *recs) {
     constexpr int NB = MODE == OMV_BOW_KF_FRAME ? 4 : 1;
+    constexpr int kTop = BowCfg<MODE>::top, kRecWords = BowCfg<MODE>::rec;
     const omv_bow_job &J = jobs[blockIdx.y];
     const omv_kf_view &K = J.kf, &O = J.other;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -237,8 +247,9 @@ __device__ void scan_node(const omv_kf_view &O, const uint32_t *claimed, const u
 template <int MODE, int W>
 __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *jobs, const int *rec_off,
                                                              const uint32_t *recs, float nnratio, int check_ori,
-                                                             int32_t *n_matches, int *err) {
+                                                             int32_t *n_matches, int *err, int lim) {
     // err[0]: status; err[1]: rescans of the walk (diagnostic, omv_matcher_bow_rescans)
+    constexpr int kTop = BowCfg<MODE>::top, kRecWords = BowCfg<MODE>::rec, kChunk = BowCfg<MODE>::chunk;
     __shared__ uint32_t claimed[kMaxKp / 32];
     __shared__ uint8_t bins[kMaxKp];
     __shared__ int16_t match[kMaxKp];   // the output, written to memory once at the end (no stores in the walk)
@@ -272,6 +283,13 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
 #pragma unroll
     for (int k = 0; k < kPer; ++k) nxt[k] = T * k + tid < n_words ? R[T * k + tid] : 0u;
     int nm = 0, buf = 0;
+#ifdef OMV_BOW_PROFILE
+    long long tb[4] = {0, 0, 0, 0}, tl = wall_clock64();
+    int n_batch = 0, n_lone = 0, n_searched = 0, n_iter = 0;
+#define OMV_TB(k) (tb[k] += wall_clock64() - tl, tl = wall_clock64())
+#else
+#define OMV_TB(k) ((void)0)
+#endif
     for (int base = 0; base < K.n; base += kChunkW) {
 #pragma unroll
         for (int k = 0; k < kPer; ++k) recbuf[buf][T * k + tid] = nxt[k];
@@ -282,6 +300,7 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
             nxt[k] = w < n_words ? R[w] : 0u;
         }
         __syncthreads();
+        OMV_TB(0);
         // one keyframe keypoint with the live claims (the batch's conflict / rescan case)
         auto walk_one = [&](const uint32_t *cr) {
         const int o0 = (int)cr[0];
@@ -303,12 +322,12 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
 #pragma unroll
         for (int k = 0; k < kTop; ++k) {
             const uint32_t x = e[k];
-            const bool ok = x != kNone && !((cw[k] >> (x & 31u)) & 1u);
+            const bool ok = k < lim && x != kNone && !((cw[k] >> (x & 31u)) & 1u);
             best = ok && found == 0 ? x : best;
             d2 = ok && found == 1 ? (int)(x >> 23) : d2;
             found += ok && found < 2 ? 1 : 0;
         }
-        const bool rescan = lane < NB && found < 2 && total > kTop;
+        const bool rescan = lane < NB && found < 2 && total > lim;
         int bd[NB], bi[NB], bs[NB], bb[NB];
         if (__ballot(rescan)) {
             if (lane == 0) atomicAdd(err + 1, 1);
@@ -364,12 +383,13 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
-        // Batches of S = 64 / NB consecutive keyframe keypoints, lane (s, c) = keypoint q + s, camera block c: every
-        // pick against the claims at the batch start, then the conflict-free prefix commits at once.  A keypoint's
-        // pick stays the reference's iff no entry it examined (its unclaimed short-list entries up to the second)
-        // was claimed by an earlier keypoint of the batch: batch claims go to `owner` (the first claimer), each
-        // lane checks its examined entries against it, and the first keypoint with a conflict (or a rescan) is
-        // walked alone with the claims of the committed prefix.
+        // Batches of S = 64 W / NB consecutive keyframe keypoints, lane (s, c) = keypoint q + s, camera block c.  The
+        // picks are iterated to the reference's: each round every lane picks against the claims committed before the
+        // batch plus the claims of the earlier batch keypoints' current picks (`owner`: the first claimer), and the
+        // rounds stop when no pick changes.  The fixed point is unique and is the sequential walk's (keypoint 0's
+        // pick is final after one round, keypoint s's once those before it are), and conflicting keypoints only
+        // cost another round (a one-entry claim chain a round) instead of a walk alone.  A keypoint whose short
+        // list runs out (a node rescan) ends the batch: the keypoints before it commit, it is walked alone.
         const int qend = min(nb, K.n);
         for (int q = base; q < qend;) {
             const int nbatch = min(S, qend - q);
@@ -385,41 +405,55 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
             uint32_t cw[kTop];
 #pragma unroll
             for (int k = 0; k < kTop; ++k) cw[k] = claimed[(e[k] == kNone ? 0u : e[k] & 0xffffu) >> 5];
-            uint32_t best = kNone, exm = 0;
-            int d2 = 256, found = 0;
-#pragma unroll
-            for (int k = 0; k < kTop; ++k) {
-                const uint32_t x = e[k];
-                const bool ok = x != kNone && !((cw[k] >> (x & 31u)) & 1u);
-                exm |= ok && found < 2 ? 1u << k : 0u;
-                best = ok && found == 0 ? x : best;
-                d2 = ok && found == 1 ? (int)(x >> 23) : d2;
-                found += ok && found < 2 ? 1 : 0;
-            }
             const bool search = o0 >= 0;
-            const bool rescan = search && found < 2 && total > kTop;
-            const int bd = best == kNone ? 256 : (int)(best >> 23), bi = (int)(best & 0xffffu);
-            const int bd0 = __shfl(bd, lane - c, 64), bs0 = __shfl(d2, lane - c, 64);   // keypoint s's block 0
-            bool claim;
-            if (MODE == OMV_BOW_KF_FRAME)
-                claim = search && bd0 <= TH_LOW && bd <= TH_LOW && (c != 0 || (float)bd0 < nnratio * (float)bs0);
-            else
-                claim = search && bd < TH_LOW && (float)bd < nnratio * (float)d2;
-            if (claim) atomicMin(&owner[bi], s);
-            __syncthreads();
-            bool bad = rescan;
+            uint32_t best = kNone;
+            int d2 = 256, myclaim = -1;
+            bool rescan = false;
+            for (int it = 0;; ++it) {
+                uint32_t nbest = kNone;
+                int nd2 = 256, found = 0;
 #pragma unroll
-            for (int k = 0; k < kTop; ++k)
-                if ((exm >> k) & 1u) bad |= owner[e[k] & 0xffffu] < s;
-            const uint64_t badm = __ballot(act && bad);
-            if (badm && lane == 0) atomicMin(&s_first, wave * (64 / NB) + (int)(__builtin_ctzll(badm) / NB));
+                for (int k = 0; k < kTop; ++k) {
+                    const uint32_t x = e[k];
+                    const bool ok = k < lim && x != kNone && !((cw[k] >> (x & 31u)) & 1u) &&
+                                    owner[x == kNone ? 0u : x & 0xffffu] >= s;
+                    nbest = ok && found == 0 ? x : nbest;
+                    nd2 = ok && found == 1 ? (int)(x >> 23) : nd2;
+                    found += ok && found < 2 ? 1 : 0;
+                }
+                const bool nresc = search && found < 2 && total > lim;
+                const int bd = nbest == kNone ? 256 : (int)(nbest >> 23), bi = (int)(nbest & 0xffffu);
+                const int bd0 = __shfl(bd, lane - c, 64), bs0 = __shfl(nd2, lane - c, 64);   // keypoint s's block 0
+                bool claim;
+                if (MODE == OMV_BOW_KF_FRAME)
+                    claim = search && bd0 <= TH_LOW && bd <= TH_LOW && (c != 0 || (float)bd0 < nnratio * (float)bs0);
+                else
+                    claim = search && bd < TH_LOW && (float)bd < nnratio * (float)nd2;
+                const bool changed = act && (nbest != best || nd2 != d2 || nresc != rescan);
+                best = nbest, d2 = nd2, rescan = nresc;
+                if (!__syncthreads_or(changed ? 1 : 0) && it > 0) break;   // owner already holds these picks' claims
+                if (it > 2 * S + 4) {   // cannot happen (S + 1 rounds suffice); kept so the loop always ends:
+                    rescan = act;       // the batch then commits nothing and its first keypoint is walked alone
+                    break;
+                }
+                if (myclaim >= 0) owner[myclaim] = kFree;
+                __syncthreads();
+                myclaim = claim ? bi : -1;
+                if (myclaim >= 0) atomicMin(&owner[myclaim], s);
+                __syncthreads();
+#ifdef OMV_BOW_PROFILE
+                if (tid == 0) ++n_iter;
+#endif
+            }
+            const uint64_t rm = __ballot(act && rescan);
+            if (rm && lane == 0) atomicMin(&s_first, wave * (64 / NB) + (int)(__builtin_ctzll(rm) / NB));
             __syncthreads();
             const int sstar = min(s_first, nbatch);   // first keypoint to walk alone
-            const bool commit = claim && s < sstar;
+            const bool commit = myclaim >= 0 && s < sstar;
             if (commit) {
-                atomicOr(&claimed[bi >> 5], 1u << (bi & 31));
-                const int at = MODE == OMV_BOW_KF_FRAME ? bi : idx1;
-                match[at] = (int16_t)(MODE == OMV_BOW_KF_FRAME ? idx1 : bi);
+                atomicOr(&claimed[myclaim >> 5], 1u << (myclaim & 31));
+                const int at = MODE == OMV_BOW_KF_FRAME ? myclaim : idx1;
+                match[at] = (int16_t)(MODE == OMV_BOW_KF_FRAME ? idx1 : myclaim);
                 if (check_ori) {
                     const int bb = (int)((best >> 16) & 31u);
                     bins[at] = (uint8_t)bb;
@@ -427,13 +461,22 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
                 }
             }
             nm += __popcll(__ballot(commit));   // this wavefront's commits
-            if (claim) owner[bi] = kFree;
+            if (myclaim >= 0) owner[myclaim] = kFree;
             __syncthreads();
             if (tid == 0) s_first = INT_MAX;   // read by every thread above; the next batch sets it after a barrier
+            OMV_TB(1);
+#ifdef OMV_BOW_PROFILE
+            ++n_batch;
+            n_searched += __popcll(__ballot(act && search && c == 0));
+#endif
             if (sstar < nbatch) {
                 if (wave == 0) walk_one(recbuf[buf] + (q + sstar - base) * kRecWords);
                 __syncthreads();
                 q += sstar + 1;
+#ifdef OMV_BOW_PROFILE
+                ++n_lone;
+#endif
+                OMV_TB(2);
             } else {
                 q += nbatch;
             }
@@ -441,6 +484,13 @@ __global__ void __launch_bounds__(64 * W) bow_resolve_kernel(const omv_bow_job *
         buf ^= 1;
     }
     __syncthreads();
+#ifdef OMV_BOW_PROFILE
+    OMV_TB(3);
+    if (tid == 0 && blockIdx.x < 3)
+        printf("bow job %d mode %d n %d: chunk staging %lld batches %lld lone walks %lld tail %lld ticks; batches %d lone %d searched(wave0) %d rounds %d\n",
+               blockIdx.x, MODE, K.n, tb[0], tb[1], tb[2], tb[3], n_batch, n_lone, n_searched, n_iter);
+#endif
+#undef OMV_TB
     if (check_ori) {
         if (tid == 0) three_maxima(cnt, ind);
         __syncthreads();
@@ -482,7 +532,9 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     const size_t job_bytes = (sizeof(omv_bow_job) * n_jobs + 15) & ~(size_t)15;
     const size_t off_bytes = (sizeof(int) * (n_jobs + 1) + 15) & ~(size_t)15;
     char *d_buf = nullptr;
-    HIP_OK(hipMallocAsync((void **)&d_buf, job_bytes + off_bytes + 16 + (size_t)off[n_jobs] * kRecWords * 4, st));
+    const int rec_words = mode == OMV_BOW_KF_FRAME ? BowCfg<OMV_BOW_KF_FRAME>::rec : BowCfg<OMV_BOW_KF_KF>::rec;
+    const int top = mode == OMV_BOW_KF_FRAME ? BowCfg<OMV_BOW_KF_FRAME>::top : BowCfg<OMV_BOW_KF_KF>::top;
+    HIP_OK(hipMallocAsync((void **)&d_buf, job_bytes + off_bytes + 16 + (size_t)off[n_jobs] * rec_words * 4, st));
     omv_bow_job *d_jobs = (omv_bow_job *)d_buf;
     int *d_off = (int *)(d_buf + job_bytes);
     int *d_err = (int *)(d_buf + job_bytes + off_bytes);
@@ -491,14 +543,17 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     HIP_OK(hipMemcpyAsync(d_off, off.data(), sizeof(int) * (n_jobs + 1), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(d_err, 0, 2 * sizeof(int), st));
     const dim3 cg((max_n + 255) / 256, n_jobs);
+    // short-list entries the walk uses (test knob OMV_BOW_TOP: fewer make the node rescans run on small inputs)
+    int lim = top;
+    if (const char *e = getenv("OMV_BOW_TOP")) lim = std::max(2, std::min(top, atoi(e)));
     if (mode == OMV_BOW_KF_FRAME) {
         bow_cand_kernel<OMV_BOW_KF_FRAME><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
         bow_resolve_kernel<OMV_BOW_KF_FRAME, kBowWaves><<<n_jobs, 64 * kBowWaves, 0, st>>>(d_jobs, d_off, d_recs, nnratio,
-                                                                                         check_ori, n_matches, d_err);
+                                                                                         check_ori, n_matches, d_err, lim);
     } else {
         bow_cand_kernel<OMV_BOW_KF_KF><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
         bow_resolve_kernel<OMV_BOW_KF_KF, kBowWaves><<<n_jobs, 64 * kBowWaves, 0, st>>>(d_jobs, d_off, d_recs, nnratio,
-                                                                                      check_ori, n_matches, d_err);
+                                                                                      check_ori, n_matches, d_err, lim);
     }
     HIP_OK(hipGetLastError());
     int h_err[2] = {0, 0};

@@ -117,10 +117,17 @@ def test_search_by_bow_stopped_words(oracle, kf_kf):
 
 
 @pytest.mark.parametrize("kf_kf", [False, True])
-def test_search_by_bow_crowded_nodes(oracle, kf_kf):
-    """Few vocabulary nodes (30+ candidates per node and camera block, as a real vocabulary at levelsup 4 gives):
-    the short lists overflow and the walk's rescan under the current claims runs; its result stays bit-exact."""
+def test_search_by_bow_crowded_nodes(oracle, monkeypatch, kf_kf):
+    """Few vocabulary nodes (30+ candidates per node and camera block, as a real vocabulary at levelsup 4 gives;
+    100+ in the one- and two-node pairs): the short lists overflow and the walk's rescan under the current claims
+    runs; its result stays bit-exact."""
     pairs = [synth_tri.make_tri_pair(seed=40 + s, n_pts=500 + 50 * s, mp_frac=0.9, n_nodes=5 + s) for s in range(1, 7)]
+    # one or two nodes: 100+ candidates per node and block, so even 16-entry short lists run out
+    pairs += [synth_tri.make_tri_pair(seed=60 + s, n_pts=900 + 100 * s, mp_frac=0.5, n_nodes=1 + s % 2) for s in range(3)]
+    total, _ = _run_bow(oracle, pairs, kf_kf, True, nnratio=0.9)
+    assert total > 50
+    # the same with the walk using 4 entries of each short list: the rescans run often
+    monkeypatch.setenv("OMV_BOW_TOP", "4")
     total, rescans = _run_bow(oracle, pairs, kf_kf, True, nnratio=0.9)
     assert total > 50
     assert rescans > 0, "the crowded-node case did not exercise the rescan path"

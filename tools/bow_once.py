@@ -6,6 +6,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("OMV_LIB"):   # an instrumented variant of the library (e.g. -DOMV_BOW_PROFILE)
+    from openmavis_amd import _lib  # noqa: E402
+    _lib.load(os.environ["OMV_LIB"])
 import bench  # noqa: E402
 
 out = bench.aux_legs(torch.device("cuda", 0), False)
