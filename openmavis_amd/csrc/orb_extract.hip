@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <set>
@@ -217,6 +219,106 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     }
 }
 
+
+// K1 as one launch: workgroup (band b, image) computes band b of EVERY level.  Level l's rows are split in nb
+// contiguous bands; band b also computes the halo rows its next level reads from the neighbouring bands
+// (host-planned: need_l = own_l united with the source rows of need_{l+1}), so a level never waits for another
+// workgroup.  Level l - 1's needed rows stay in LDS (ping-pong buffers) while level l is formed from them: the
+// pyramid is read from memory once (level 0) and written once, with one launch instead of nlevels - 1 dependent
+// ones.  Same arithmetic as pyr_resize_kernel, so the same bytes.
+struct PyrBand {
+    int own_lo, own_hi, need_lo, need_hi;   // rows of one level (level 0: need only)
+};
+constexpr bool kPyrChainDefault = false;
+__global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *images, size_t img_stride, size_t pitch0,
+                                                        uint8_t *pyr, const XTab *xt, const XTab *yt, const XQuad *xq,
+                                                        const PyrBand *bands, int buf_dw) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t pyr_lds[];
+    const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+    const PyrBand *B = bands + (size_t)b * kMaxLevels;
+    uint32_t *prev = pyr_lds, *cur = pyr_lds + buf_dw;
+    auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
+    {   // level 0's needed rows from the image
+        const PyrBand b0 = B[0];
+        const int sw = g.lv[0].w, ndw = ((sw + 15) >> 4) << 2, nr = b0.need_hi - b0.need_lo;
+        const uint8_t *src = images + (size_t)img * img_stride;
+        if ((pitch0 & 15) == 0 && (((uintptr_t)src) & 15) == 0) {
+            const int n4 = ndw >> 2;
+            const uint32_t m4 = divm(n4);
+            for (int q = tid; q < nr * n4; q += 256) {
+                const int r = (int)__umulhi((uint32_t)q, m4), i = q - r * n4;
+                reinterpret_cast<uint4 *>(prev)[q] = reinterpret_cast<const uint4 *>(src + (size_t)(b0.need_lo + r) * pitch0)[i];
+            }
+        } else {
+            uint8_t *bb = reinterpret_cast<uint8_t *>(prev);
+            const uint32_t mw = divm(sw);
+            for (int q = tid; q < nr * sw; q += 256) {
+                const int r = (int)__umulhi((uint32_t)q, mw), i = q - r * sw;
+                bb[(size_t)r * ndw * 4 + i] = src[(size_t)(b0.need_lo + r) * pitch0 + i];
+            }
+        }
+    }
+    __syncthreads();
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    for (int l = 1; l < g.nlevels; ++l) {
+        const LevelGeom &L = g.lv[l];
+        const PyrBand bp = B[l - 1], bc = B[l];
+        const int sndw = ((g.lv[l - 1].w + 15) >> 4) << 2, cndw = ((L.w + 15) >> 4) << 2;
+        const int nq = (L.w + 3) >> 2, nr = bc.need_hi - bc.need_lo;
+        const bool quad = L.use_xq != 0;
+        const uint32_t mq = divm(nq);
+        for (int q = tid; q < nr * nq; q += 256) {
+            const int r = (int)__umulhi((uint32_t)q, mq), qd = q - r * nq, dx0 = qd * 4, dy = bc.need_lo + r;
+            const XTab y = yt[L.ytab_off + dy];
+            const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
+            uint32_t packed = 0;
+            if (quad) {
+                const XQuad X = xq[L.xq_off + qd];
+                const uint32_t *R0 = prev + (size_t)(y.sx0 - bp.need_lo) * sndw, *R1 = prev + (size_t)(y.sx1 - bp.need_lo) * sndw;
+                const uint32_t u0[4] = {R0[X.a[0]], R0[X.a[0] + 1], R0[X.a[1]], R0[X.a[1] + 1]};
+                const uint32_t u1[4] = {R1[X.a[0]], R1[X.a[0] + 1], R1[X.a[1]], R1[X.a[1] + 1]};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int pp = 2 * (j >> 1);
+                    const u16x2 cf = __builtin_bit_cast(u16x2, X.cf[j]);
+                    const int h0 = (int)__builtin_amdgcn_udot2(
+                        __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u0[pp + 1], u0[pp], X.sel[j])), cf, 0u, false);
+                    const int h1 = (int)__builtin_amdgcn_udot2(
+                        __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u1[pp + 1], u1[pp], X.sel[j])), cf, 0u, false);
+                    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                    packed |= (uint32_t)min(v, 255) << (8 * j);
+                }
+            } else {
+                const uint8_t *R0 = reinterpret_cast<const uint8_t *>(prev + (size_t)(y.sx0 - bp.need_lo) * sndw);
+                const uint8_t *R1 = reinterpret_cast<const uint8_t *>(prev + (size_t)(y.sx1 - bp.need_lo) * sndw);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int dx = dx0 + j;
+                    if (dx < L.w) {
+                        const XTab x = xt[L.xtab_off + dx];
+                        const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
+                        const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
+                        const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
+                        const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                        packed |= (uint32_t)min(v, 255) << (8 * j);
+                    }
+                }
+            }
+            cur[(size_t)r * cndw + qd] = packed;   // the next level's source row (bytes past the width are never read)
+            if (dy >= bc.own_lo && dy < bc.own_hi) {
+                uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
+                if (dx0 + 3 < L.w) {
+                    *reinterpret_cast<uint32_t *>(dst + dx0) = packed;
+                } else {
+                    for (int j = 0; j < 4 && dx0 + j < L.w; ++j) dst[dx0 + j] = (uint8_t)(packed >> (8 * j));
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t *t = prev;
+        prev = cur, cur = t;
+    }
+}
 
 // K2 --------------------------------------------------------------------------------------------
 // FAST-9 strength: max over the 16 circular 9-arcs of min(d) (darker) and of min(-d) (brighter),
@@ -1293,6 +1395,8 @@ struct omv_orb {
     size_t fast_lds = 0;   // K2 dynamic LDS: region + strength map (rmax each) + the candidate list (u16)
     size_t oct_lds = 0;
     size_t pyr_lds[kMaxLevels] = {};   // K1 dynamic LDS per level: x table + the widest row block
+    PyrBand *d_bands = nullptr;        // K1 as one launch (pyr_chain_kernel): per (band, level) rows
+    int pyr_nb = 0, pyr_buf_dw = 0;    //   bands per image, dwords per LDS ping-pong buffer (0: per-level launches)
     // host staging for the synchronous path
     uint8_t *d_img1 = nullptr;
     omv_kp *d_kp1 = nullptr;
@@ -1585,6 +1689,44 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
             (void)hipFuncSetAttribute((const void *)pyr_resize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)o->pyr_lds[l]);
     }
+    {   // K1 as one launch: the fewest bands per image whose largest level band (halo rows included) fits 32 KB of
+        // LDS (two workgroups per CU), else 64 KB (wide images); no plan: the per-level launches
+        const int L = g.nlevels;
+        auto plan = [&](int nb, std::vector<PyrBand> &bands) {
+            bands.assign((size_t)nb * kMaxLevels, PyrBand{0, 0, 0, 0});
+            int worst = 0;
+            for (int b = 0; b < nb; ++b) {
+                PyrBand *B = &bands[(size_t)b * kMaxLevels];
+                for (int l = 1; l < L; ++l)
+                    B[l].own_lo = (int)((long long)b * g.lv[l].h / nb), B[l].own_hi = (int)((long long)(b + 1) * g.lv[l].h / nb);
+                B[L - 1].need_lo = B[L - 1].own_lo, B[L - 1].need_hi = B[L - 1].own_hi;
+                for (int l = L - 1; l >= 1; --l) {
+                    int lo = INT_MAX, hi = INT_MIN;   // the source rows of level l's needed rows
+                    if (B[l].need_hi > B[l].need_lo)
+                        lo = yt[g.lv[l].ytab_off + B[l].need_lo].sx0, hi = yt[g.lv[l].ytab_off + B[l].need_hi - 1].sx1 + 1;
+                    if (l - 1 >= 1 && B[l - 1].own_hi > B[l - 1].own_lo)
+                        lo = std::min(lo, B[l - 1].own_lo), hi = std::max(hi, B[l - 1].own_hi);
+                    if (hi > lo) B[l - 1].need_lo = std::max(0, lo), B[l - 1].need_hi = std::min(g.lv[l - 1].h, hi);
+                }
+                for (int l = 0; l < L; ++l)
+                    worst = std::max(worst, (B[l].need_hi - B[l].need_lo) * (((g.lv[l].w + 15) / 16) * 4));
+            }
+            return worst;
+        };
+        std::vector<PyrBand> bands;
+        for (int budget : {8192, 16384}) {
+            for (int nb = 8; nb <= 128 && L > 1 && !o->pyr_nb; ++nb) {
+                const int worst = plan(nb, bands);
+                if (worst > budget) continue;
+                o->pyr_nb = nb, o->pyr_buf_dw = worst;
+                HIP_OK(hipMalloc(&o->d_bands, sizeof(PyrBand) * bands.size()));
+                HIP_OK(hipMemcpy(o->d_bands, bands.data(), sizeof(PyrBand) * bands.size(), hipMemcpyHostToDevice));
+                const int lds = (int)(sizeof(uint32_t) * (2 * (size_t)worst + 4));
+                if (lds > 64 * 1024)
+                    (void)hipFuncSetAttribute((const void *)pyr_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            }
+        }
+    }
     HIP_OK(hipMalloc(&o->d_xt, sizeof(XTab) * std::max<size_t>(1, xt.size())));
     HIP_OK(hipMalloc(&o->d_yt, sizeof(XTab) * std::max<size_t>(1, yt.size())));
     if (!xt.empty()) HIP_OK(hipMemcpy(o->d_xt, xt.data(), sizeof(XTab) * xt.size(), hipMemcpyHostToDevice));
@@ -1621,7 +1763,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
     for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
-    void *ptrs[] = {o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_disc, o->d_hitem, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+    void *ptrs[] = {o->d_bands, o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_disc, o->d_hitem, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
     for (void *p : ptrs)
@@ -1660,10 +1802,18 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
         o->h_lap.assign(lapping, lapping + 2 * n);
     }
     mark(o, st);
-    // K1: pyramid, level by level
-    for (int l = 1; l < g.nlevels; ++l) {
-        pyr_resize_kernel<<<dim3((g.lv[l].h + kPyrBlock - 1) / kPyrBlock, n), 256, o->pyr_lds[l], st>>>(
-            g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, o->d_xq, n);
+    // K1: pyramid, every level in one launch (level by level when no band plan fits LDS); test knob OMV_PYR_MODE =
+    // "levels" / "chain" picks the path
+    const char *pm = getenv("OMV_PYR_MODE");
+    const bool chain = pm ? std::strcmp(pm, "chain") == 0 : kPyrChainDefault;
+    if (o->pyr_nb > 0 && chain) {
+        pyr_chain_kernel<<<dim3(o->pyr_nb, n), 256, sizeof(uint32_t) * (2 * (size_t)o->pyr_buf_dw + 4), st>>>(
+            g, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, o->d_xq, o->d_bands, o->pyr_buf_dw);
+    } else {
+        for (int l = 1; l < g.nlevels; ++l) {
+            pyr_resize_kernel<<<dim3((g.lv[l].h + kPyrBlock - 1) / kPyrBlock, n), 256, o->pyr_lds[l], st>>>(
+                g, l, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, o->d_xq, n);
+        }
     }
     mark(o, st);
     // K2: FAST per cell

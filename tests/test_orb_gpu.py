@@ -46,10 +46,15 @@ def test_extract_matches_oracle(oracle, w, h, nf, ini, mn, lap, seed):
     _compare(o_mono, o_kps, o_desc, g_mono, g_kps, g_desc, f"{w}x{h} seed {seed}")
 
 
-def test_pyramid_levels_match_oracle(oracle):
-    img = synth.synth_image(20221000, 720, 540)
+@pytest.mark.parametrize("levels", [False, True])
+@pytest.mark.parametrize("w,h,seed", [(720, 540, 20221000), (333, 250, 9), (1920, 1080, 31)])
+def test_pyramid_levels_match_oracle(oracle, monkeypatch, levels, w, h, seed):
+    """Every pyramid level bit-exact: the one-launch banded pyramid and the per-level launches (OMV_PYR_MODE);
+    odd pitch (byte staging of level 0) and a 1080p image (more bands, wider halos)."""
+    monkeypatch.setenv("OMV_PYR_MODE", "levels" if levels else "chain")
+    img = synth.synth_image(seed, w, h)
     ex = ORBextractor(1200, 1.2, 8, 15, 7)
-    ex(img, None, (0, 720))
+    ex(img, None, (0, w))
     for lvl in range(1, 8):
         ref = oracle.pyramid_level(img, lvl, 1200)
         got = ex.debug_level(0, lvl)
