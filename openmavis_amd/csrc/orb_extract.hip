@@ -229,14 +229,20 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
 struct PyrBand {
     int own_lo, own_hi, need_lo, need_hi;   // rows of one level (level 0: need only)
 };
-constexpr bool kPyrChainDefault = false;
+constexpr int kPyrChainMaxImages = 16;   // default: one launch for batches up to this many images (B = 1 latency)
 __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *images, size_t img_stride, size_t pitch0,
                                                         uint8_t *pyr, const XTab *xt, const XTab *yt, const XQuad *xq,
-                                                        const PyrBand *bands, int buf_dw) {
+                                                        const PyrBand *bands, int buf_dw, int tab_dw) {
     extern __shared__ __attribute__((aligned(16))) uint32_t pyr_lds[];
     const int b = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
     const PyrBand *B = bands + (size_t)b * kMaxLevels;
     uint32_t *prev = pyr_lds, *cur = pyr_lds + buf_dw;
+    // the level's x table (quads or pixels) and the y entries of its needed rows, staged per level: every output
+    // quad of the band reads them (from memory that was 48 + 12 bytes of table traffic per 4 output pixels)
+    uint32_t *tab = pyr_lds + 2 * (size_t)buf_dw + 4;
+    XTab *ys = reinterpret_cast<XTab *>(tab + tab_dw);
+    XQuad *xqs = reinterpret_cast<XQuad *>(tab);
+    XTab *xs = reinterpret_cast<XTab *>(tab);
     auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
     {   // level 0's needed rows from the image
         const PyrBand b0 = B[0];
@@ -266,14 +272,20 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
         const int sndw = ((g.lv[l - 1].w + 15) >> 4) << 2, cndw = ((L.w + 15) >> 4) << 2;
         const int nq = (L.w + 3) >> 2, nr = bc.need_hi - bc.need_lo;
         const bool quad = L.use_xq != 0;
+        if (quad)
+            for (int i = tid; i < nq; i += 256) xqs[i] = xq[L.xq_off + i];
+        else
+            for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
+        for (int i = tid; i < nr; i += 256) ys[i] = yt[L.ytab_off + bc.need_lo + i];
+        __syncthreads();
         const uint32_t mq = divm(nq);
         for (int q = tid; q < nr * nq; q += 256) {
             const int r = (int)__umulhi((uint32_t)q, mq), qd = q - r * nq, dx0 = qd * 4, dy = bc.need_lo + r;
-            const XTab y = yt[L.ytab_off + dy];
+            const XTab y = ys[r];
             const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
             uint32_t packed = 0;
             if (quad) {
-                const XQuad X = xq[L.xq_off + qd];
+                const XQuad X = xqs[qd];
                 const uint32_t *R0 = prev + (size_t)(y.sx0 - bp.need_lo) * sndw, *R1 = prev + (size_t)(y.sx1 - bp.need_lo) * sndw;
                 const uint32_t u0[4] = {R0[X.a[0]], R0[X.a[0] + 1], R0[X.a[1]], R0[X.a[1] + 1]};
                 const uint32_t u1[4] = {R1[X.a[0]], R1[X.a[0] + 1], R1[X.a[1]], R1[X.a[1] + 1]};
@@ -295,7 +307,7 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
                 for (int j = 0; j < 4; ++j) {
                     const int dx = dx0 + j;
                     if (dx < L.w) {
-                        const XTab x = xt[L.xtab_off + dx];
+                        const XTab x = xs[dx];
                         const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
                         const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
                         const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
@@ -1397,6 +1409,7 @@ struct omv_orb {
     size_t pyr_lds[kMaxLevels] = {};   // K1 dynamic LDS per level: x table + the widest row block
     PyrBand *d_bands = nullptr;        // K1 as one launch (pyr_chain_kernel): per (band, level) rows
     int pyr_nb = 0, pyr_buf_dw = 0;    //   bands per image, dwords per LDS ping-pong buffer (0: per-level launches)
+    int pyr_tab_dw = 0, pyr_rows = 0;  //   dwords of the staged x table, the most rows a band needs at a level >= 1
     // host staging for the synchronous path
     uint8_t *d_img1 = nullptr;
     omv_kp *d_kp1 = nullptr;
@@ -1718,10 +1731,23 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
             for (int nb = 8; nb <= 128 && L > 1 && !o->pyr_nb; ++nb) {
                 const int worst = plan(nb, bands);
                 if (worst > budget) continue;
-                o->pyr_nb = nb, o->pyr_buf_dw = worst;
+                int tab = 0, rows = 0;
+                for (int l = 1; l < L; ++l) {
+                    tab = std::max(tab, g.lv[l].use_xq ? 12 * ((g.lv[l].w + 3) / 4) : 3 * g.lv[l].w);
+                    for (int b = 0; b < nb; ++b) {
+                        const PyrBand &pb = bands[(size_t)b * kMaxLevels + l];
+                        rows = std::max(rows, pb.need_hi - pb.need_lo);
+                    }
+                }
+                o->pyr_nb = nb, o->pyr_buf_dw = worst, o->pyr_tab_dw = (tab + 3) & ~3, o->pyr_rows = rows;
                 HIP_OK(hipMalloc(&o->d_bands, sizeof(PyrBand) * bands.size()));
                 HIP_OK(hipMemcpy(o->d_bands, bands.data(), sizeof(PyrBand) * bands.size(), hipMemcpyHostToDevice));
-                const int lds = (int)(sizeof(uint32_t) * (2 * (size_t)worst + 4));
+                const int lds = (int)(sizeof(uint32_t) * (2 * (size_t)worst + 4 + o->pyr_tab_dw + 3 * (size_t)rows));
+                if (lds > 160 * 1024) {   // no plan: the per-level launches
+                    (void)hipFree(o->d_bands);
+                    o->d_bands = nullptr, o->pyr_nb = 0;
+                    break;
+                }
                 if (lds > 64 * 1024)
                     (void)hipFuncSetAttribute((const void *)pyr_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             }
@@ -1805,10 +1831,11 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     // K1: pyramid, every level in one launch (level by level when no band plan fits LDS); test knob OMV_PYR_MODE =
     // "levels" / "chain" picks the path
     const char *pm = getenv("OMV_PYR_MODE");
-    const bool chain = pm ? std::strcmp(pm, "chain") == 0 : kPyrChainDefault;
+    const bool chain = pm ? std::strcmp(pm, "chain") == 0 : n <= kPyrChainMaxImages;
     if (o->pyr_nb > 0 && chain) {
-        pyr_chain_kernel<<<dim3(o->pyr_nb, n), 256, sizeof(uint32_t) * (2 * (size_t)o->pyr_buf_dw + 4), st>>>(
-            g, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt, o->d_xq, o->d_bands, o->pyr_buf_dw);
+        const size_t lds = sizeof(uint32_t) * (2 * (size_t)o->pyr_buf_dw + 4 + o->pyr_tab_dw + 3 * (size_t)o->pyr_rows);
+        pyr_chain_kernel<<<dim3(o->pyr_nb, n), 256, lds, st>>>(g, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt,
+                                                               o->d_xq, o->d_bands, o->pyr_buf_dw, o->pyr_tab_dw);
     } else {
         for (int l = 1; l < g.nlevels; ++l) {
             pyr_resize_kernel<<<dim3((g.lv[l].h + kPyrBlock - 1) / kPyrBlock, n), 256, o->pyr_lds[l], st>>>(
