@@ -983,18 +983,24 @@ static void launch_knn2(const KnnArgs &a, int n_pairs, int q_cap, hipStream_t st
 __global__ void stereo_pairs_kernel(const int32_t *idx2, const int32_t *dist2, int out_cap, const int *n_kp,
                                     const int *mono, int n_cams, int kp_cap, double ratio, int32_t *l2r,
                                     int32_t *r2l, int n_frames) {
+    // one thread per left slot q of the frame's [0, kp_cap): every l2r entry is written here (-1 unless q is a
+    // lapping left keypoint passing the ratio test), so only r2l needs a reset before the launch
     const int frame = blockIdx.y;
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= kp_cap) return;
     const int m0 = mono[frame * n_cams], m1 = mono[frame * n_cams + 1];
-    const int nq = n_kp[frame * n_cams] - m0;
-    if (qi >= nq) return;
-    const int32_t *oi = idx2 + ((size_t)frame * out_cap + qi) * 2;
-    const int32_t *od = dist2 + ((size_t)frame * out_cap + qi) * 2;
-    if (oi[1] < 0) return;   // fewer than 2 matches
-    if ((double)od[0] < (double)od[1] * ratio) {   // `distance * 0.8`: a double product (:1491)
-        l2r[(size_t)frame * kp_cap + m0 + qi] = m1 + oi[0];
-        atomicMax(&r2l[(size_t)frame * kp_cap + m1 + oi[0]], m0 + qi);   // later left index wins
+    const int nq = n_kp[frame * n_cams] - m0, qi = q - m0;
+    int32_t v = -1;
+    if (qi >= 0 && qi < nq) {
+        const int32_t *oi = idx2 + ((size_t)frame * out_cap + qi) * 2;
+        const int32_t *od = dist2 + ((size_t)frame * out_cap + qi) * 2;
+        // fewer than 2 matches: none; `distance * 0.8` is a double product (:1491)
+        if (oi[1] >= 0 && (double)od[0] < (double)od[1] * ratio) {
+            v = m1 + oi[0];
+            atomicMax(&r2l[(size_t)frame * kp_cap + m1 + oi[0]], q);   // later left index wins
+        }
     }
+    l2r[(size_t)frame * kp_cap + q] = v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2414,8 +2420,7 @@ omv_status omv_matcher_stereo_lapping(omv_matcher *h, int n_frames, const uint8_
     h->last = st;
     const int cap = h->kp_cap, C = h->n_cams;
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
-    HIP_OK(hipMemsetAsync(l2r, 0xff, sizeof(int32_t) * n_frames * cap, st));
-    HIP_OK(hipMemsetAsync(r2l, 0xff, sizeof(int32_t) * n_frames * cap, st));
+    HIP_OK(hipMemsetAsync(r2l, 0xff, sizeof(int32_t) * n_frames * cap, st));   // l2r: written whole by stereo_pairs
     // query = camera 0 rows [mono0, n0), train = camera 1 rows [mono1, n1)
     KnnArgs a{desc, desc + (size_t)cap * 32, (long long)C * cap * 32, (long long)C * cap * 32, n_kp, n_kp + 1,
               mono, mono + 1, C, h->d_knn_i, h->d_knn_d, cap};
