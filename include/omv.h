@@ -672,9 +672,10 @@ omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, co
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream);
 
 /* Kernel choice of the two calls above.  OMV_POSE_AUTO (default): up to 16 frames per call run on the grouped
- * kernel — one frame over `parts` workgroups (0: one per 128 (LastFrame) / 192 visual edges, at most 48) that exchange their
- * normal-equation sums every Gauss-Newton iteration, the latency path of Tracking's one-frame call — and larger batches
- * on one workgroup per frame.  OMV_POSE_BATCH / OMV_POSE_GROUPED force one of them (GROUPED needs kp_cap <= 16384).
+ * kernel — one frame over `parts` workgroups (0: one per 126 (LastFrame) / 190 (LastKeyFrame) visual edges of the batch's
+ * mean frame, at least ceil(edges of the whole batch / 1022) so that no frame's part can overflow, at most 48) that
+ * exchange their normal-equation sums every Gauss-Newton iteration, the latency path of Tracking's one-frame call —
+ * and larger batches (or a batch whose edges need more than 48 parts) on one workgroup per frame.  OMV_POSE_BATCH / OMV_POSE_GROUPED force one of them (GROUPED needs kp_cap <= 16384).
  * The grouped kernel reports a frame it could not run (more than 1024 visual edges in one workgroup's keypoint
  * range) with n_good = -1 and OMV_ERR_CAPACITY in omv_pose_last_error. */
 #define OMV_POSE_AUTO 0

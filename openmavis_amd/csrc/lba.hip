@@ -372,33 +372,52 @@ __global__ void __launch_bounds__(256) finish_kernel(const double *mono_partial,
     }
 }
 
-// ---- build: landmark part ---------------------------------------------------------------------
+// ---- build: landmark groups with the Schur complement on f64 MFMA ---------------------------------------
+// buildSystem (block_solver.hpp:381-432) and the landmark Schur complement (:353-486) of one trial in one pass over the
+// edges.  A landmark group is a run of whole landmarks (<= 256 edges, <= 128 landmarks, <= 128 slots, <= 32 distinct
+// optimisable keyframes; a slot = one landmark's edges on one keyframe).  Per group, on one workgroup:
+//   1. one thread per edge: EdgeMono / EdgeStereo Jacobians (JX 3x3, JP 3x6, the robust weight, -W e) into LDS;
+//   2. one thread per landmark: Hll = sum w JX^T JX and bl = sum JX^T (-W e) in edge order, the Cholesky factor
+//      R R^T = Hll + lambda I and y = R^-1 bl; beside it one thread per slot: Hpl_s = sum w JP^T JX over the slot's
+//      edges (in order), then M_s = Hpl_s R^-T, so that Hpl Dinv Hpl^T = M M^T and Hpl Dinv bl = M y;
+//   3. the group's share of the reduced system as ONE zero-routed product on v_mfma_f64_16x16x4f64: rows / columns are
+//      the group's keyframes in elimination order, 8 per keyframe (6 pose rows, then a Schur right-hand-side column and
+//      a gradient column), and the K dimension is [3 per landmark: M routed to its slots' rows, -M to the columns,
+//      y to the rhs column] ++ [each residual row of each edge: JP to its keyframe's rows, w JP to the columns, -W e
+//      to the gradient column] -- so one accumulation gives  sum JP^T W JP - sum Hpl Dinv Hpl^T  per keyframe pair, the
+//      keyframe gradients and the Schur right-hand side, with the cross-landmark and cross-edge sums done by the
+//      matrix core in its fixed order (no float atomics: bitwise identical run to run);
+//   4. the group's blocks (keyframe pairs it co-observes) and per-keyframe [b | Schur rhs] rows into its own record;
+//      assemble_kernel sums the records of a reduced-system block in group order.
+// The per-landmark (R^-1, y, bl) and per-slot M_s stay for the back-substitution xl = R^-T (y - sum M_s^T xp_s).
+// lambda enters through R, so the build runs every trial (a rejected trial rebuilds at the same linearisation point:
+// the current state and its errors are untouched, so the Jacobians are the same numbers; g2o rebuilds only the Schur).
 struct Land {
     const int *edge_start;   // [P+1]
     const int *slot_start;   // [P+1]
     const int *slot_kf;      // [nslots]
-    const int *slot_pt;      // [nslots] the landmark of a slot
-    double *Hll;             // [P][9]
-    double *bl;              // [P][3]
-    double *Hpl;             // [nslots][18] pose rows x point cols
+    const int *slot_edge;    // [nslots+1] first edge of each slot (slots are the keyframe runs of the landmark-major edges)
+    const int16_t *slot_lkf; // [nslots] the slot keyframe's index in its group's keyframe list, -1 for a fixed keyframe
+    double *lnd;             // [P][12]: R^-1 (lower: 00 10 11 20 21 22) | y = R^-1 bl | bl
+    double *M;               // [nslots][18]: M_s = Hpl_s R^-T (6 x 3, row-major), optimisable slots only
     int n;
-    const int *grp_pt;       // [n_grp+1] buildSystem landmark groups: whole landmarks, <= kGrpEdges edges each
+    const int *grp_pt;       // [n_grp+1] landmarks of each group
+    const int *grp_w;        // [n_grp] optimisable keyframes of the group (w); -w - 1: a one-landmark group past the
+                             //   LDS limits, built by the scalar path
+    const int *grp_tp;       // [n_grp+1] the group's 16x16 output tiles (ti >= tj), as pairs in `tp`
+    const uint8_t *tp;       // [2 per tile]
+    const int *grp_blk;      // [n_grp] index in blkoff of the group's w(w+1)/2 keyframe pairs (a >= b)
+    const int *blkoff;       //   the pair's record in `rec` (36 doubles), -1 if the group's landmarks do not co-observe it
+    const int *grp_kf;       // [n_grp] index in rhsoff of the group's w keyframes
+    const int *rhsoff;       //   the keyframe's record in `rec_rhs` (12 doubles: gradient 6 | Schur rhs 6)
+    double *rec;             // per reduced-system block its groups' 6x6 records, contiguous in group order
+    double *rec_rhs;         // per optimisable keyframe its groups' [gradient | Schur rhs] records, in group order
 };
 
-// Work lists of the deterministic reductions (host-built once per problem, every list in ascending order).
-// Each reduction is split in chunks of at most 256 items; a chunk writes its fixed-order partial sum, and the
-// reduced-system block's assembly (the next launch) sums the chunk partials in chunk order, so every value is
-// identical run to run whatever the scheduling.
+// Inertial work lists (host-built once per problem, ascending): per reduced-system block its inertial edges.
 struct Gather {
-    const int4 *pchunk;      // pose chunks: (keyframe, first, end) over the keyframe's edges
-    const int *kf_edge;      // [n_pchunk][kGrpEdges] each pose chunk's visual edges (ascending; -1 pads)
-    const int *pc_start;     // [nb+1] per keyframe: its pose chunks
-    double *pose_part;       // [n_pchunk][27]: 21 lower-triangle JpT W Jp sums + 6 JpT W e
-    const int *schunk_order; // launch order of the Schur chunks (XCD-contiguous runs of neighbouring blocks)
-    const int4 *tr;          // Schur terms (landmark slot a, landmark slot b, landmark, diagonal) oriented to their
-                             // block, each block's list padded to whole 256-term chunks (landmark -1: no term)
-    const int *sc_start;     // [n_slots+1] per block: its Schur chunks
-    double *schur_part;      // [n_schunk][42]: 36 Hpl_a Dinv Hpl_b^T + 6 Hpl_a Dinv bl
+    const int *blk_start;    // [n_slots+1] per reduced-system block: its run of group records in Land::rec
+    const int *rhs_start;    // [nb+1] per optimisable keyframe: its run of [gradient | Schur rhs] in Land::rec_rhs
     const int4 *imu_blk;     // per block: inertial edges (edge, side of the block row, side of the column)
     const int *ib_start;     // [n_slots+1]
     const int2 *imu_vec;     // per keyframe: inertial edges (edge, side)
@@ -414,7 +433,8 @@ struct Red {   // reduced (non-marginalised) system: 16 rows per optimisable key
 
 // One visual edge at the current errors (EdgeMono, or EdgeStereo when ur >= 0): the point Jacobian JX (nr x 3),
 // the pose Jacobian JP (nr x 6, ImuCamPose order), the robust weight w = invSigma2 * rho' and the weighted
-// residual om = -invSigma2 * rho' * e (constructQuadraticForm, base_binary_edge.hpp:55-116).
+// residual om = -invSigma2 * rho' * e (constructQuadraticForm, base_binary_edge.hpp:55-116).  Row 2 is zero on an
+// EdgeMono.
 __device__ __forceinline__ int edge_jacobians(const Rig &rig, const State &s, const Edges &E, int e, double delta,
                                               double dsqr, double delta_st, double dsqr_st, const double *err,
                                               const double *err3, const double *chi2, double JX[9], double JP[18],
@@ -431,7 +451,6 @@ __device__ __forceinline__ int edge_jacobians(const Rig &rig, const State &s, co
     double pj[9];
     cam_jac(rig, c, Xc, pj);
     const int nr = st ? 3 : 2;
-    // all three rows are formed (zero for a mono edge) so the arrays stay in registers; the sums skip row 2
     if (st) {
         const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
         pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
@@ -468,150 +487,391 @@ __device__ __forceinline__ int edge_jacobians(const Rig &rig, const State &s, co
     return nr;
 }
 
-// sums over the residual rows: the EdgeStereo row is added last (mono edges: 2 rows)
-__device__ __forceinline__ double rows2(const double *A, int ia, const double *B, int ib, int lda, int ldb, int nr) {
-    double t = A[ia] * B[ib] + A[lda + ia] * B[ldb + ib];
-    if (nr == 3) t += A[2 * lda + ia] * B[2 * ldb + ib];
-    return t;
-}
-__device__ __forceinline__ double rows_om(const double *A, int ia, int lda, const double *om, int nr) {
-    double t = A[ia] * om[0] + A[lda + ia] * om[1];
-    if (nr == 3) t += A[2 * lda + ia] * om[2];
-    return t;
+// sum over the residual rows r of A[r][ia] B[r][ib] (row-major, row strides lda / ldb): the EdgeStereo row last
+// (zero on an EdgeMono, where the sum is the two-row sum exactly)
+__device__ __forceinline__ double rows3(const double *A, int ia, int lda, const double *B, int ib, int ldb) {
+    return A[ia] * B[ib] + A[lda + ia] * B[ldb + ib] + A[2 * lda + ia] * B[2 * ldb + ib];
 }
 
-// Fixed-order wavefront sum (xor tree): the wave total in every lane; callers combine the waves in order.
-__device__ __forceinline__ double wave_sum_fixed(double v) {
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+// Cholesky factor of D = Hll + lambda I (lower, R R^T = D) inverted: Ri = R^-1 as (00 10 11 20 21 22); y = R^-1 bl.
+// Then Dinv = R^-T R^-1, so Hpl Dinv Hpl^T = (Hpl R^-T)(Hpl R^-T)^T and Hpl Dinv bl = (Hpl R^-T) y.  A non-positive
+// pivot (D not positive definite, e.g. lambda = 0 on a two-edge-free landmark) gives NaN and the trial's solve fails,
+// as the explicit inverse's infinities did.
+__device__ __forceinline__ void chol3_inv(const double *H, double lambda, const double *bl, double Ri[6], double y[3]) {
+    const double d00 = H[0] + lambda, d10 = H[3], d11 = H[4] + lambda, d20 = H[6], d21 = H[7], d22 = H[8] + lambda;
+    const double l00 = sqrt(d00), i00 = 1.0 / l00;
+    const double l10 = d10 * i00, l20 = d20 * i00;
+    const double l11 = sqrt(d11 - l10 * l10), i11 = 1.0 / l11;
+    const double l21 = (d21 - l20 * l10) * i11;
+    const double l22 = sqrt(d22 - l20 * l20 - l21 * l21), i22 = 1.0 / l22;
+    const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22, i20 = -(l20 * i00 + l21 * i10) * i22;
+    Ri[0] = i00, Ri[1] = i10, Ri[2] = i11, Ri[3] = i20, Ri[4] = i21, Ri[5] = i22;
+    y[0] = i00 * bl[0];
+    y[1] = i10 * bl[0] + i11 * bl[1];
+    y[2] = i20 * bl[0] + i21 * bl[1] + i22 * bl[2];
 }
-
-// Keyframe-diagonal visual terms of buildSystem, one pose chunk (<= kGrpEdges edges of one keyframe, ascending) per
-// block, one edge per thread: 21 + 6 terms, a fixed-order reduction (transposing wave sums, then the waves in order),
-// one partial row.  The chunk partials are summed in chunk order when the keyframe's diagonal block is assembled.
-__device__ __forceinline__ void pose_chunk_block(int ch, double *wsum, Rig rig, State s, Edges E, Gather G,
-                                                 double delta, double dsqr, double delta_st, double dsqr_st,
-                                                 const double *err, const double *err3, const double *chi2) {
-    double acc[27];
+// M = Hpl R^-T (6 x 3): M[r][c] = sum_{q <= c} Hpl[r][q] Ri[c][q]
+__device__ __forceinline__ void m_of(const double *Hpl, const double Ri[6], double M[18]) {
 #pragma unroll
-    for (int q = 0; q < 27; ++q) acc[q] = 0;
-    const int e = G.kf_edge[(size_t)ch * kGrpEdges + threadIdx.x];
-    if (e >= 0) {
-        double JX[9], JP[18], w, om[3];
-        const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
-        int q = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c <= r; ++c) acc[q++] = w * rows2(JP, r, JP, c, 6, 6, nr);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) acc[21 + r] = rows_om(JP, r, 6, om, nr);
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const double mine = wave_transpose_sum(acc, lane);
-    if (lane < 27) wsum[27 * wave + lane] = mine;
-    __syncthreads();
-    if (threadIdx.x < 27) {
-        double t = wsum[threadIdx.x];
-        for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) t += wsum[27 * w2 + threadIdx.x];
-        G.pose_part[(size_t)ch * 27 + threadIdx.x] = t;
+    for (int r = 0; r < 6; ++r) {
+        const double h0 = Hpl[3 * r], h1 = Hpl[3 * r + 1], h2 = Hpl[3 * r + 2];
+        M[3 * r] = h0 * Ri[0];
+        M[3 * r + 1] = h0 * Ri[1] + h1 * Ri[2];
+        M[3 * r + 2] = h0 * Ri[3] + h1 * Ri[4] + h2 * Ri[5];
     }
 }
 
-// Landmark part of buildSystem for one group of whole landmarks (<= kGrpEdges edges, landmark-major): thread t forms
-// the Jacobians of the group's edge t and its 30 landmark terms (Hll 9, bl 3, Hpl 18) in LDS, then thread p sums the
-// terms of landmark p's edges in edge order (Hpl per keyframe slot) -- the sums and their order of one thread per
-// landmark walking its edges, with the edge chains run in parallel.  A group of one landmark with more edges than the
-// group holds is walked by its first thread alone.
-constexpr int kLandTerms = 30;
-struct LandAcc {
-    double Hll[9], bl[3], Hpl[18];
-    int slot;
-};
-// thread tid's terms of edge e into the group's LDS table (value-major: conflict-free)
-__device__ __forceinline__ void land_terms(int e, int tid, double *T, const Rig &rig, const State &s, const Edges &E,
-                                           double delta, double dsqr, double delta_st, double dsqr_st,
-                                           const double *err, const double *err3, const double *chi2) {
-    double JX[9], JP[18], w, om[3];
-    const int nr = edge_jacobians(rig, s, E, e, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, w, om);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        T[(9 + r) * kGrpEdges + tid] = rows_om(JX, r, 3, om, nr);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) T[(3 * r + q) * kGrpEdges + tid] = w * rows2(JX, r, JX, q, 3, 3, nr);
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) T[(12 + 3 * r + q) * kGrpEdges + tid] = w * rows2(JP, r, JX, q, 6, 3, nr);
-}
-// edges [f0, f1) of one landmark (table rows f - base) added to its sums in edge order; a finished slot's Hpl stored
-__device__ __forceinline__ void land_accumulate(LandAcc &a, const double *T, int base, int f0, int f1, const Edges &E,
-                                                const Land &L) {
-    for (int f = f0; f < f1; ++f) {
-        const int le = f - base;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) a.bl[q] += T[(9 + q) * kGrpEdges + le];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) a.Hll[q] += T[q * kGrpEdges + le];
-        const int slot = E.slot[f];
-        if (slot != a.slot) {
-            if (a.slot >= 0)
-                for (int q = 0; q < 18; ++q) L.Hpl[(size_t)a.slot * 18 + q] = a.Hpl[q];
-            for (int q = 0; q < 18; ++q) a.Hpl[q] = 0;
-            a.slot = slot;
-        }
-#pragma unroll
-        for (int q = 0; q < 18; ++q) a.Hpl[q] += T[(12 + q) * kGrpEdges + le];
-    }
-}
-__device__ __forceinline__ void land_store(const LandAcc &a, int p, const Land &L) {
-    if (a.slot >= 0)
-        for (int q = 0; q < 18; ++q) L.Hpl[(size_t)a.slot * 18 + q] = a.Hpl[q];
-    for (int q = 0; q < 9; ++q) L.Hll[(size_t)p * 9 + q] = a.Hll[q];
-    for (int q = 0; q < 3; ++q) L.bl[(size_t)p * 3 + q] = a.bl[q];
-}
+constexpr int kGrpLand = 128;    // landmarks per group (one thread each, threads 0..127)
+constexpr int kGrpSlots = 128;   // slots per group (one thread each, threads 128..255)
+constexpr int kGrpW = 32;        // optimisable keyframes per group (rows of the Schur product: 8 each)
+// LDS of one landmark group (doubles, edge / slot / landmark-major rows)
+constexpr int kSE = 22;                   // per edge: JP (3 x 6) | w | -W e (3)
+constexpr int kLdsE = kSE * kGrpEdges;    // edges; then per slot its 27 diagonal terms; then the MFMA operand panels
+constexpr int kLdsX = 9 * kGrpEdges;      // per edge JX (3 x 3)
+constexpr int kLdsL = 3 * kGrpLand + 27 * kGrpW;   // per landmark y (3); per landmark R^-1 (6), then per keyframe
+                                                   //   the group's 27 diagonal terms
+constexpr int kPanel = kLdsE / 16;        // operand panels: ceil(w / 2) * kpad <= kPanel (a group-planning bound)
+constexpr size_t kBuildLds = (size_t)(kLdsE + kLdsX + kLdsL) * 8 + kGrpLand * kGrpW;
+static_assert(6 * kGrpLand <= 27 * kGrpW, "R^-1 rows fit under the diagonal terms");
+static_assert(27 * kGrpSlots <= kLdsE, "the slots' diagonal terms fit the edge region");
 
-__device__ __forceinline__ void land_group(int g, double *T, LandAcc *big_acc, Rig rig, State s, Edges E, Land L,
-                                           double delta, double dsqr, double delta_st, double dsqr_st,
-                                           const double *err, const double *err3, const double *chi2) {
-    const int p0 = L.grp_pt[g], p1 = L.grp_pt[g + 1];
-    const int e0 = L.edge_start[p0], e1 = L.edge_start[p1];
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, const State &s, const Edges &E,
+                                           const Land &L, double lambda, double delta, double dsqr, double delta_st,
+                                           double dsqr_st, const double *err, const double *err3, const double *chi2) {
+    double *SE = sm, *SX = sm + kLdsE, *SY = SX + kLdsX, *SR = SY + 3 * kGrpLand;
+    uint8_t *map = (uint8_t *)(SY + kLdsL);
     const int tid = threadIdx.x;
-    if (e1 - e0 <= kGrpEdges) {
-        if (e0 + tid < e1) land_terms(e0 + tid, tid, T, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-        __syncthreads();
-        const int p = p0 + tid;
-        if (p >= p1) return;
-        LandAcc a{};
-        a.slot = -1;
-        land_accumulate(a, T, e0, L.edge_start[p], L.edge_start[p + 1], E, L);
-        land_store(a, p, L);
-        return;
+#ifdef OMV_BUILD_PROFILE
+    long long tp0 = wall_clock64(), tp1 = 0, tp2 = 0, tp3 = 0;
+#endif
+    const int p0 = L.grp_pt[g], p1 = L.grp_pt[g + 1], np = p1 - p0;
+    const int e0 = L.edge_start[p0], ne = L.edge_start[p1] - e0;
+    const int s0 = L.slot_start[p0], ns = L.slot_start[p1] - s0;
+    const int w = L.grp_w[g], ntile = (w + 1) >> 1, kpad = (3 * np + 3) & ~3;
+    for (int q = tid; q < np * kGrpW; q += blockDim.x) map[q] = 0xFF;
+    // phase 1: one thread per edge: Jacobians, weight, -W e into LDS (edge-major rows)
+    if (tid < ne) {
+        double JX[9], JP[18], wt, om[3];
+        edge_jacobians(rig, s, E, e0 + tid, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, wt, om);
+        double *o = SE + kSE * tid;
+#pragma unroll
+        for (int q = 0; q < 18; ++q) o[q] = JP[q];
+        o[18] = wt;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) o[19 + q] = om[q];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) SX[9 * tid + q] = JX[q];
     }
-    // one landmark with more edges than a group holds: windows of kGrpEdges, thread 0 carries the sums in LDS
-    if (tid == 0) {
-        *big_acc = LandAcc{};
-        big_acc->slot = -1;
+    __syncthreads();
+#ifdef OMV_BUILD_PROFILE
+    tp1 = wall_clock64();
+#endif
+    // phase 2a: threads 0..127 one landmark each (Hll, bl in edge order; Cholesky), 128..255 one slot each (Hpl and the
+    // slot's keyframe-diagonal terms: 21 of sum w JP^T JP and 6 of sum JP^T (-W e), in edge order)
+    double Hpl[18], Ps[27];
+    int my_slot = -1, my_pl = 0;
+    if (tid < kGrpLand) {
+        if (tid < np) {
+            const int p = p0 + tid;
+            double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+            for (int f = L.edge_start[p] - e0, f1 = L.edge_start[p + 1] - e0; f < f1; ++f) {
+                double jx[9], om[3];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) jx[q] = SX[9 * f + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) om[q] = SE[kSE * f + 19 + q];
+                const double wt = SE[kSE * f + 18];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    bl[r] += rows3(jx, r, 3, om, 0, 1);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) H[3 * r + q] += wt * rows3(jx, r, 3, jx, q, 3);
+                }
+            }
+            double Ri[6], y[3];
+            chol3_inv(H, lambda, bl, Ri, y);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) SR[6 * tid + q] = Ri[q];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) SY[3 * tid + q] = y[q];
+            double *o = L.lnd + (size_t)p * 12;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) o[q] = Ri[q];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) o[6 + q] = y[q], o[9 + q] = bl[q];
+            for (int sl = L.slot_start[p], s1 = L.slot_start[p + 1]; sl < s1; ++sl) {
+                const int a = L.slot_lkf[sl];
+                if (a >= 0) map[tid * kGrpW + a] = (uint8_t)(sl - s0);
+            }
+        }
+    } else if (tid - kGrpLand < ns) {
+        my_slot = s0 + tid - kGrpLand;
+        if (L.slot_lkf[my_slot] >= 0) {
+#pragma unroll
+            for (int q = 0; q < 18; ++q) Hpl[q] = 0;
+#pragma unroll
+            for (int q = 0; q < 27; ++q) Ps[q] = 0;
+            for (int f = L.slot_edge[my_slot] - e0, f1 = L.slot_edge[my_slot + 1] - e0; f < f1; ++f) {
+                double jx[9], jp[18], om[3];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) jx[q] = SX[9 * f + q];
+#pragma unroll
+                for (int q = 0; q < 18; ++q) jp[q] = SE[kSE * f + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) om[q] = SE[kSE * f + 19 + q];
+                const double wt = SE[kSE * f + 18];
+#pragma unroll
+                for (int r = 0; r < 6; ++r)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) Hpl[3 * r + q] += wt * rows3(jp, r, 6, jx, q, 3);
+                int q = 0;
+#pragma unroll
+                for (int r = 0; r < 6; ++r)
+#pragma unroll
+                    for (int c = 0; c <= r; ++c) Ps[q++] += wt * rows3(jp, r, 6, jp, c, 6);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) Ps[21 + r] += rows3(jp, r, 6, om, 0, 1);
+            }
+            my_pl = E.pt[L.slot_edge[my_slot]] - p0;   // the slot's landmark
+        } else {
+            my_slot = -1;
+        }
     }
-    for (int base = e0; base < e1; base += kGrpEdges) {
-        if (base + tid < e1) land_terms(base + tid, tid, T, rig, s, E, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-        __syncthreads();
-        if (tid == 0) {
-            LandAcc a = *big_acc;
-            land_accumulate(a, T, base, base, min(base + kGrpEdges, e1), E, L);
-            *big_acc = a;
+    __syncthreads();
+    // phase 2b: M_s = Hpl_s R^-T (kept in registers for the panels); the slot's diagonal terms into LDS (slot-major)
+    double M[18];
+    if (my_slot >= 0) {
+        double Ri[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) Ri[q] = SR[6 * my_pl + q];
+        m_of(Hpl, Ri, M);
+        double *o = L.M + (size_t)my_slot * 18;
+#pragma unroll
+        for (int q = 0; q < 18; ++q) o[q] = M[q];
+        const int sl = tid - kGrpLand;
+#pragma unroll
+        for (int q = 0; q < 27; ++q) SE[27 * sl + q] = Ps[q];
+    }
+    __syncthreads();
+    // phase 2c: the keyframe-diagonal terms of the group, per keyframe a the slots' terms in landmark order
+    // (SR's R^-1 rows are dead: the sums take their place)
+    double *SP = SR;
+    for (int q = tid; q < w * 27; q += blockDim.x) {
+        const int a = q / 27, e = q - 27 * a;
+        double v = 0;
+        int pl = 0;
+        for (; pl + 4 <= np; pl += 4) {
+            int sl[4];
+            double x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sl[u] = map[(pl + u) * kGrpW + a];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = SE[27 * (sl[u] & 127) + e];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v += sl[u] != 0xFF ? x[u] : 0.0;
+        }
+        for (; pl < np; ++pl) {
+            const int sl = map[pl * kGrpW + a];
+            const double x = SE[27 * (sl & 127) + e];
+            v += sl != 0xFF ? x : 0.0;
+        }
+        SP[q] = v;
+    }
+    __syncthreads();
+    // phase 3a: the MFMA operand panels, one per 16-row tile (keyframes 2t, 2t + 1): panel t holds for K = 3 pl + c
+    // the 16 values of rows 16 t .. 16 t + 15: M_{pl, a}[r][c] at row 8 a + r, y_pl[c] at row 8 a + 6 (where landmark pl
+    // has a slot on keyframe a), zero elsewhere -- zero-filled, then scattered by the slot threads
+    double *PN = SE;
+    const int npan = ntile * kpad * 16;
+    for (int q = tid; q < npan; q += blockDim.x) PN[q] = 0.0;
+    __syncthreads();
+    if (my_slot >= 0) {
+        const int a = L.slot_lkf[my_slot];
+        double *o = PN + ((size_t)(a >> 1) * kpad + 3 * my_pl) * 16 + 8 * (a & 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) o[16 * c + r] = M[3 * r + c];
+            o[16 * c + 6] = SY[3 * my_pl + c];
+        }
+    }
+    __syncthreads();
+#ifdef OMV_BUILD_PROFILE
+    tp2 = wall_clock64();
+#endif
+    // phase 3b: Out(tile ti, tj) = init + sum_K A[.][K] B[K][.] on v_mfma_f64_16x16x4f64, A = panel ti (pose rows only),
+    // B = -panel tj on the pose columns, +panel tj on the Schur rhs column, 0 on the gradient column; a diagonal tile
+    // starts from the keyframes' diagonal terms, so each block comes out as sum JP^T W JP - sum Hpl Dinv Hpl^T and the
+    // gradient / Schur rhs columns as b / sum Hpl Dinv bl.  Operand loads are affine in the step: no dependent chains.
+    const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kk = lane >> 4;
+    const int t0 = L.grp_tp[g], nt = L.grp_tp[g + 1] - t0;
+    const int nsteps = kpad >> 2;
+    const int *blkoff = L.blkoff + L.grp_blk[g], *rhsoff = L.rhsoff + L.grp_kf[g];
+    for (int it = wave; it < nt; it += (int)(blockDim.x >> 6)) {
+        const int ti = L.tp[2 * (t0 + it)], tj = L.tp[2 * (t0 + it) + 1];
+        const int ar = li & 7, bc = li & 7;
+        const double amask = ar < 6 ? 1.0 : 0.0, bsign = bc < 6 ? -1.0 : (bc == 6 ? 1.0 : 0.0);
+        const int b_kf = 2 * tj + (li >> 3);
+        v4d acc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // rows 16 ti + kk + 4 j of column 16 tj + li
+            const int R = 16 * ti + kk + 4 * j, a = R >> 3, r = R & 7;
+            double v = 0;
+            if (a == b_kf && a < w && r < 6) {
+                if (bc < 6) v = SP[27 * a + (r >= bc ? r * (r + 1) / 2 + bc : bc * (bc + 1) / 2 + r)];
+                else if (bc == 7) v = SP[27 * a + 21 + r];
+            }
+            acc[j] = v;
+        }
+        const double *pa = PN + (size_t)ti * kpad * 16 + 16 * kk + li, *pb = PN + (size_t)tj * kpad * 16 + 16 * kk + li;
+        for (int st = 0; st < nsteps; st += 4) {
+            double av[4], bv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int o = st + u < nsteps ? 64 * (st + u) : 0;
+                av[u] = pa[o], bv[u] = pb[o];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double m = st + u < nsteps ? 1.0 : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u] * amask * m, bv[u] * bsign, acc, 0, 0, 0);
+            }
+        }
+        // out: each block / keyframe row to its place in the block's (keyframe's) contiguous record run
+        if (b_kf >= w) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int R = 16 * ti + kk + 4 * j, a = R >> 3, r = R & 7;
+            if (r >= 6 || a >= w) continue;
+            if (bc < 6) {
+                if (a >= b_kf) {
+                    const int o = blkoff[a * (a + 1) / 2 + b_kf];
+                    if (o >= 0) L.rec[(size_t)o * 36 + 6 * r + bc] = acc[j];
+                }
+            } else if (a == b_kf) {
+                L.rec_rhs[(size_t)rhsoff[a] * 12 + (bc == 7 ? 0 : 6) + r] = acc[j];
+            }
+        }
+    }
+#ifdef OMV_BUILD_PROFILE
+    __syncthreads();
+    tp3 = wall_clock64();
+    if (tid == 0 && (g & 63) == 0)
+        printf("build group %d: edges %d landmarks %d slots %d w %d tiles %d | ticks(100MHz) jac %lld land %lld mfma %lld\n",
+               g, ne, np, ns, w, nt, tp1 - tp0, tp2 - tp1, tp3 - tp2);
+#endif
+}
+
+// A one-landmark group past the LDS limits (> 256 edges, > 128 slots or > 32 optimisable keyframes): the same
+// quantities by the scalar path.  Windows of 64 edges: per edge its 30 landmark terms and 27 pose terms in LDS,
+// thread 0 walks them in edge order (Hll, bl, per slot Hpl and the pose terms), then one thread per slot forms M_s,
+// one thread per keyframe pair the block.
+constexpr int kBigWin = 64;
+__device__ __forceinline__ void land_group_big(int g, double *sm, const Rig &rig, const State &s, const Edges &E,
+                                            const Land &L, double lambda, double delta, double dsqr, double delta_st,
+                                            double dsqr_st, const double *err, const double *err3, const double *chi2) {
+    double *T = sm;                       // [57][kBigWin]
+    double *SL = sm + kLdsE + kLdsX;      // R^-1 | y of the landmark
+    int *inv = (int *)(sm + kLdsE);       // keyframe index -> slot (the JX region as ints)
+    const int tid = threadIdx.x;
+    const int p = L.grp_pt[g], w = -L.grp_w[g] - 1, nblk = w * (w + 1) / 2;
+    const int e0 = L.edge_start[p], e1 = L.edge_start[p + 1];
+    const int *blkoff = L.blkoff + L.grp_blk[g], *rhsoff = L.rhsoff + L.grp_kf[g];
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0}, Hp[18], P[27];
+    int cur = -1;
+    auto flush = [&]() {   // thread 0: the finished slot `cur`
+        const int a = L.slot_lkf[cur];
+        if (a < 0) return;
+        double *o = L.M + (size_t)cur * 18;
+        for (int q = 0; q < 18; ++q) o[q] = Hp[q];
+        double *B = L.rec + (size_t)blkoff[a * (a + 1) / 2 + a] * 36;
+        int q = 0;
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c <= r; ++c, ++q) B[6 * r + c] = B[6 * c + r] = P[q];
+        for (int r = 0; r < 6; ++r) L.rec_rhs[(size_t)rhsoff[a] * 12 + r] = P[21 + r];
+    };
+    for (int base = e0; base < e1; base += kBigWin) {
+        if (tid < kBigWin && base + tid < e1) {
+            double JX[9], JP[18], wt, om[3];
+            edge_jacobians(rig, s, E, base + tid, delta, dsqr, delta_st, dsqr_st, err, err3, chi2, JX, JP, wt, om);
+            for (int r = 0; r < 3; ++r) {
+                T[(9 + r) * kBigWin + tid] = rows3(JX, r, 3, om, 0, 1);
+                for (int q = 0; q < 3; ++q) T[(3 * r + q) * kBigWin + tid] = wt * rows3(JX, r, 3, JX, q, 3);
+            }
+            for (int r = 0; r < 6; ++r)
+                for (int q = 0; q < 3; ++q) T[(12 + 3 * r + q) * kBigWin + tid] = wt * rows3(JP, r, 6, JX, q, 3);
+            int q = 0;
+            for (int r = 0; r < 6; ++r)
+                for (int c = 0; c <= r; ++c, ++q) T[(30 + q) * kBigWin + tid] = wt * rows3(JP, r, 6, JP, c, 6);
+            for (int r = 0; r < 6; ++r) T[(51 + r) * kBigWin + tid] = rows3(JP, r, 6, om, 0, 1);
         }
         __syncthreads();
+        if (tid == 0)
+            for (int f = base; f < min(base + kBigWin, e1); ++f) {
+                const int le = f - base;
+                for (int q = 0; q < 3; ++q) bl[q] += T[(9 + q) * kBigWin + le];
+                for (int q = 0; q < 9; ++q) H[q] += T[q * kBigWin + le];
+                const int sl = E.slot[f];
+                if (sl != cur) {
+                    if (cur >= 0) flush();
+                    for (int q = 0; q < 18; ++q) Hp[q] = 0;
+                    for (int q = 0; q < 27; ++q) P[q] = 0;
+                    cur = sl;
+                }
+                for (int q = 0; q < 18; ++q) Hp[q] += T[(12 + q) * kBigWin + le];
+                for (int q = 0; q < 27; ++q) P[q] += T[(30 + q) * kBigWin + le];
+            }
+        __syncthreads();
     }
-    if (tid == 0) land_store(*big_acc, p0, L);
+    if (tid == 0) {
+        if (cur >= 0) flush();
+        double Ri[6], y[3];
+        chol3_inv(H, lambda, bl, Ri, y);
+        double *o = L.lnd + (size_t)p * 12;
+        for (int q = 0; q < 6; ++q) o[q] = Ri[q], SL[q] = Ri[q];
+        for (int q = 0; q < 3; ++q) o[6 + q] = y[q], o[9 + q] = bl[q], SL[6 + q] = y[q];
+    }
+    for (int sl = L.slot_start[p] + tid; sl < L.slot_start[p + 1]; sl += blockDim.x)
+        if (L.slot_lkf[sl] >= 0) inv[L.slot_lkf[sl]] = sl;
+    __threadfence_block();
+    __syncthreads();
+    for (int sl = L.slot_start[p] + tid; sl < L.slot_start[p + 1]; sl += blockDim.x) {
+        if (L.slot_lkf[sl] < 0) continue;
+        double h[18], M[18], Ri[6];
+        double *o = L.M + (size_t)sl * 18;
+        for (int q = 0; q < 18; ++q) h[q] = o[q];
+        for (int q = 0; q < 6; ++q) Ri[q] = SL[q];
+        m_of(h, Ri, M);
+        for (int q = 0; q < 18; ++q) o[q] = M[q];
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int q = tid; q < nblk; q += blockDim.x) {
+        int a = 0;
+        while ((a + 1) * (a + 2) / 2 <= q) ++a;
+        const int b = q - a * (a + 1) / 2;
+        const double *Ma = L.M + (size_t)inv[a] * 18, *Mb = L.M + (size_t)inv[b] * 18;
+        double *B = L.rec + (size_t)blkoff[q] * 36;
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 6; ++c) {
+                const double t = Ma[3 * r] * Mb[3 * c] + Ma[3 * r + 1] * Mb[3 * c + 1] + Ma[3 * r + 2] * Mb[3 * c + 2];
+                B[6 * r + c] = (a == b ? B[6 * r + c] : 0.0) - t;
+            }
+    }
+    for (int a = tid; a < w; a += blockDim.x) {
+        const double *Ma = L.M + (size_t)inv[a] * 18;
+        for (int r = 0; r < 6; ++r)
+            L.rec_rhs[(size_t)rhsoff[a] * 12 + 6 + r] = Ma[3 * r] * SL[6] + Ma[3 * r + 1] * SL[7] + Ma[3 * r + 2] * SL[8];
+    }
 }
 
 // ---- build: inertial + random-walk edges, one wavefront each -------------------------------------
 
 // Inertial + random-walk edges of one EdgeInertial i (one wavefront): the 30 x 30 quadratic form and 30 gradient
 // over the edge's local variables [P1 V1 G1 A1 P2 V2 G2 A2] (EdgeInertial over the first 24, EdgeGyroRW on
-// G1 / G2, EdgeAccRW on A1 / A2), written to its own slot; imu_add_kernel adds the slots into the reduced system.
+// G1 / G2, EdgeAccRW on A1 / A2), written to its own slot; assemble_kernel adds the slots into the reduced system.
 constexpr int kImuLoc = 30, kImuContrib = kImuLoc * kImuLoc + kImuLoc;
 __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Imu I, double delta, double dsqr,
                                                   const double *err9, double *contrib) {
@@ -678,71 +938,48 @@ __device__ __forceinline__ void imu_contrib_block(int i, double *sm, State s, Im
     }
 }
 
-// buildSystem in two launches of 256-thread blocks, nothing accumulated across blocks (the reduced system is assembled
-// per trial from these per-landmark, per-chunk and per-edge parts): build_land_kernel, one block per landmark group
-// (Hll, bl, Hpl per slot); build_kernel, blocks [0, n_pchunk) the keyframe-diagonal pose chunks, then one block per
-// inertial edge (its 30 x 30 quadratic form).
-__global__ void __launch_bounds__(kGrpEdges) build_land_kernel(Rig rig, State s0, State s1, Edges E, Land L, int n_grp,
-                                                               double delta, double dsqr, double delta_st,
-                                                               double dsqr_st, ErrBufs e0, ErrBufs e1,
-                                                               const LmCtl *ctl) {
-    __shared__ double T[kLandTerms * kGrpEdges];
-    __shared__ LandAcc big_acc;
-    if (!gate_open(ctl, kGateBuild)) return;
-    const int bi = role_buf(ctl, 0);
-    const State s = bi ? s1 : s0;
-    const double *err = bi ? e1.err : e0.err, *err3 = bi ? e1.err3 : e0.err3, *chi2 = bi ? e1.chi2 : e0.chi2;
-    const int g = omv::xcd_block(n_grp);
-    if (g < 0) return;
-    land_group(g, T, &big_acc, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-}
-
-__global__ void __launch_bounds__(kGrpEdges) build_kernel(Rig rig, State s0, State s1, Edges E, Gather G, Imu I,
-                                                          int n_pchunk, double delta, double dsqr, double delta_st,
-                                                          double dsqr_st, double delta_imu, double dsqr_imu,
-                                                          ErrBufs e0, ErrBufs e1, double *contrib, const LmCtl *ctl,
-                                                          int blk0) {
-    __shared__ double sm[441];
-    if (!gate_open(ctl, kGateBuild)) return;
-    const int bi = role_buf(ctl, 0);
-    const State s = bi ? s1 : s0;
-    const ErrBufs eb = bi ? e1 : e0;
-    const double *err = eb.err, *err3 = eb.err3, *chi2 = eb.chi2, *err9 = eb.err9;
-    const int blk = blockIdx.x + blk0;
-    if (blk < n_pchunk) pose_chunk_block(blk, sm, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-    else imu_contrib_block(blk - n_pchunk, sm, s, I, delta_imu, dsqr_imu, err9, contrib);
-}
-
-// The whole build in one launch: blocks [0, n_other) the pose chunks then the inertial edges (build_kernel's work),
-// blocks from n_other_pad (n_other rounded up to 8, so the landmark groups keep their XCD-aware order) the landmark
-// groups (build_land_kernel's work).  The two halves are independent and each is latency-bound with few blocks, so
-// side by side they take about the longer one's time instead of the sum.
+// The whole build in one launch: blocks [0, n_imu) the inertial edges' quadratic forms, blocks from n_imu_pad (n_imu
+// rounded up to 8, so the landmark groups keep their XCD-aware order) the landmark groups.  Independent halves, side by
+// side.  Dynamic LDS: kBuildLds.
 __global__ void __launch_bounds__(kGrpEdges) build_all_kernel(Rig rig, State s0, State s1, Edges E, Land L, int n_grp,
-                                                              Gather G, Imu I, int n_pchunk, int n_other, int n_other_pad,
+                                                              Imu I, int n_imu, int n_imu_pad, double lambda,
                                                               double delta, double dsqr, double delta_st, double dsqr_st,
                                                               double delta_imu, double dsqr_imu, ErrBufs e0, ErrBufs e1,
                                                               double *contrib, const LmCtl *ctl) {
-    __shared__ double T[kLandTerms * kGrpEdges];
-    __shared__ LandAcc big_acc;
-    if (!gate_open(ctl, kGateBuild)) return;
+    extern __shared__ double sm[];
+    if (!gate_open(ctl, kGateTrial)) return;
+    lambda = lm_lambda(ctl, lambda);
     const int bi = role_buf(ctl, 0);   // the current state and its errors
     const State s = bi ? s1 : s0;
     const ErrBufs eb = bi ? e1 : e0;
-    const double *err = eb.err, *err3 = eb.err3, *chi2 = eb.chi2, *err9 = eb.err9;
     const int b = blockIdx.x;
-    if (b < n_other_pad) {
-        if (b >= n_other) return;
-        if (b < n_pchunk) pose_chunk_block(b, T, rig, s, E, G, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
-        else imu_contrib_block(b - n_pchunk, T, s, I, delta_imu, dsqr_imu, err9, contrib);
+    if (b < n_imu_pad) {
+        if (b < n_imu) imu_contrib_block(b, sm, s, I, delta_imu, dsqr_imu, eb.err9, contrib);
         return;
     }
-    const int bl = b - n_other_pad, chunk = (n_grp + 7) >> 3;
+    const int bl = b - n_imu_pad, chunk = (n_grp + 7) >> 3;
     const int g = (bl & 7) * chunk + (bl >> 3);
     if (g >= n_grp) return;
-    land_group(g, T, &big_acc, rig, s, E, L, delta, dsqr, delta_st, dsqr_st, err, err3, chi2);
+    if (L.grp_w[g] < 0) return;   // build_big_kernel's
+    land_group(g, sm, rig, s, E, L, lambda, delta, dsqr, delta_st, dsqr_st, eb.err, eb.err3, eb.chi2);
 }
 
-// ---- trial: the reduced system, assembled and Schur-complemented per block -----------------------------
+// The one-landmark groups past the LDS limits (rare: a landmark with > 256 edges, > 128 slots or > 32 optimisable
+// keyframes), one workgroup each, launched only when the problem has any.
+__global__ void __launch_bounds__(kGrpEdges) build_big_kernel(Rig rig, State s0, State s1, Edges E, Land L,
+                                                              const int *big, int n_big, double lambda, double delta,
+                                                              double dsqr, double delta_st, double dsqr_st, ErrBufs e0,
+                                                              ErrBufs e1, const LmCtl *ctl) {
+    extern __shared__ double sm[];
+    if (!gate_open(ctl, kGateTrial) || (int)blockIdx.x >= n_big) return;
+    lambda = lm_lambda(ctl, lambda);
+    const int bi = role_buf(ctl, 0);
+    const State s = bi ? s1 : s0;
+    const ErrBufs eb = bi ? e1 : e0;
+    land_group_big(big[blockIdx.x], sm, rig, s, E, L, lambda, delta, dsqr, delta_st, dsqr_st, eb.err, eb.err3, eb.chi2);
+}
+
+// ---- trial: the reduced system, assembled per block -------------------------------------------------------
 // The reduced system is stored as 16x16 blocks (keyframe block = pose 6 | v 3 | bg 3 | ba 3 | pad 1,
 // padded to one f64 MFMA tile) on the symbolic LDL^T pattern (fill-in included) of the elimination order
 // `perm` (position -> keyframe, host-chosen, see plan_order): slot(pi, pj) for block row pi >= block column
@@ -775,90 +1012,43 @@ struct BlockPat {
     int blob_ints;
 };
 
-// Per chunk of one block's Schur terms (256 landmark slot pairs (a, b), one per thread; a block's last chunk padded):
-// Dinv = (Hll + lambda I)^-1 of the landmark, BD = Hpl_a Dinv, the 6x6 term BD Hpl_b^T and, on a diagonal block
-// (a == b), Hpl_a Dinv bl (block_solver.hpp:353-486); a fixed-order reduction into the chunk's partial.  The term
-// record carries its landmark, so a thread's loads are one dependent step behind its record; chunks run in
-// `schunk_order` with XCD-contiguous logical blocks (neighbouring blocks share landmarks: one XCD's L2 holds them).
-__global__ void __launch_bounds__(256) schur_kernel(Land L, Gather G, int n_chunks, double lambda, const LmCtl *ctl) {
-    __shared__ double wsum[4][42];
-    if (!gate_open(ctl, kGateTrial)) return;
-    const int lb = omv::xcd_block(n_chunks);
-    if (lb < 0) return;
-    lambda = lm_lambda(ctl, lambda);
-    const int ch = G.schunk_order[lb], tid = threadIdx.x;
-    double acc[42];
+// One block per reduced-system block: the group records of the block in group order (each sum JP^T W JP - sum
+// Hpl Dinv Hpl^T over the group's edges / landmarks), the inertial edges touching it, + lambda on the diagonal; on a
+// diagonal block the keyframe's b and Schur right-hand side from the records' rows.  `pose_lambda` is 0 on the ranks
+// > 0 of a sharded solve (lambda enters once).
+// sum of n runs of `stride` doubles (entry `off` of each), in run order; eight loads in flight, the same order of adds
+__device__ __forceinline__ double run_sum(const double *base, int n, int stride, int off) {
+    double v = 0;
+    int q = 0;
+    for (; q + 8 <= n; q += 8) {
+        double a[8];
 #pragma unroll
-    for (int q = 0; q < 42; ++q) acc[q] = 0;
-    const int4 e = G.tr[(size_t)ch * 256 + tid];
-    if (e.z >= 0) {
-        const int p = e.z;
-        double D[9], Dinv[9];
-        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
-        const double *Ha = L.Hpl + (size_t)e.x * 18, *Hb = L.Hpl + (size_t)e.y * 18;
-        double ha[18], hb[18], bl[3];
+        for (int u = 0; u < 8; ++u) a[u] = base[(size_t)(q + u) * stride + off];
 #pragma unroll
-        for (int q = 0; q < 18; ++q) ha[q] = Ha[q], hb[q] = Hb[q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) bl[q] = L.bl[(size_t)p * 3 + q];
-        D[0] += lambda, D[4] += lambda, D[8] += lambda;
-        inv3(D, Dinv);
-        double BD[18];
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) BD[3 * r + c] = ha[3 * r] * Dinv[c] + ha[3 * r + 1] * Dinv[3 + c] + ha[3 * r + 2] * Dinv[6 + c];
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c < 6; ++c)
-                acc[6 * r + c] = BD[3 * r] * hb[3 * c] + BD[3 * r + 1] * hb[3 * c + 1] + BD[3 * r + 2] * hb[3 * c + 2];
-        if (e.w) {
-            double db[3];
-            mv3(Dinv, bl, db);
-#pragma unroll
-            for (int r = 0; r < 6; ++r) acc[36 + r] = ha[3 * r] * db[0] + ha[3 * r + 1] * db[1] + ha[3 * r + 2] * db[2];
-        }
+        for (int u = 0; u < 8; ++u) v += a[u];
     }
-    const int wave = tid >> 6, lane = tid & 63;
-    const double mine = wave_transpose_sum(acc, lane);
-    if (lane < 42) wsum[wave][lane] = mine;
-    __syncthreads();
-    if (tid < 42) G.schur_part[(size_t)ch * 42 + tid] = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+    for (; q < n; ++q) v += base[(size_t)q * stride + off];
+    return v;
 }
 
-// sum_{i = from}^{to - 1} base[i * stride] in index order, loads issued four at a time (same order of the adds)
-__device__ __forceinline__ double ordered_sum(const double *base, int from, int to, int stride) {
-    double s = 0;
-    int i = from;
-    for (; i + 4 <= to; i += 4) {
-        const double a0 = base[(size_t)i * stride], a1 = base[(size_t)(i + 1) * stride],
-                     a2 = base[(size_t)(i + 2) * stride], a3 = base[(size_t)(i + 3) * stride];
-        s += a0;
-        s += a1;
-        s += a2;
-        s += a3;
-    }
-    for (; i < to; ++i) s += base[(size_t)i * stride];
-    return s;
-}
-
-// One block per reduced-system block: H's block (the keyframe-diagonal pose chunks, the inertial edges touching
-// it) + lambda on the diagonal - the Schur chunk partials in chunk order, and on a diagonal block the keyframe's
-// b and Schur right-hand side.  `pose_lambda` is 0 on the ranks > 0 of a sharded solve (lambda enters once).
-__global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat P, double lambda, int pose_lambda,
-                                                       double *S, double *bvec, double *coef, const LmCtl *ctl) {
+// One block per reduced-system block: its run of group records in group order (each sum JP^T W JP - sum
+// Hpl Dinv Hpl^T over one group's edges / landmarks), the inertial edges touching it, + lambda on the diagonal; on a
+// diagonal block the keyframe's b and Schur right-hand side from its run of [gradient | Schur rhs] records.
+// `pose_lambda` is 0 on the ranks > 0 of a sharded solve (lambda enters once).
+__global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat P, const double *rec,
+                                                       const double *rec_rhs, double lambda, int pose_lambda, double *S,
+                                                       double *bvec, double *coef, const LmCtl *ctl) {
     if (!gate_open(ctl, kGateTrial)) return;
     lambda = lm_lambda(ctl, lambda);
     const int t = blockIdx.x, tid = threadIdx.x;
     const int kr = P.slot_kr[t], kc = P.slot_kc[t];
     const bool diag = kr == kc;
-    const int c0 = G.sc_start[t], c1 = G.sc_start[t + 1];
     const int r = tid >> 4, c = tid & 15;
     double v = 0;
     if (!diag || c <= r) {
-        if (diag && r < 6) {   // keyframe-diagonal visual terms
-            v += ordered_sum(G.pose_part + r * (r + 1) / 2 + c, G.pc_start[kr], G.pc_start[kr + 1], 27);
+        if (r < 6 && c < 6) {
+            const int g0 = G.blk_start[t];
+            v = run_sum(rec + (size_t)g0 * 36, G.blk_start[t + 1] - g0, 36, 6 * r + c);
         }
         if (r < 15 && c < 15) {   // inertial edges touching the block (variable groups present in the system)
             const bool rows_ok = r < 6 || I.offV[kr] >= 0, cols_ok = c < 6 || I.offV[kc] >= 0;
@@ -869,16 +1059,14 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
                 }
         }
         if (diag && r == c && pose_lambda) v += lambda;
-        if (r < 6 && c < 6) {
-            v -= ordered_sum(G.schur_part + 6 * r + c, c0, c1, 42);
-        }
     }
     S[(size_t)t * 256 + sw16(r, c)] = v;
     if (diag && tid < 16) {   // b and the Schur right-hand side of keyframe kr
         double bv = 0, cf = 0;
         if (tid < 6) {
-            bv = ordered_sum(G.pose_part + 21 + tid, G.pc_start[kr], G.pc_start[kr + 1], 27);
-            cf = ordered_sum(G.schur_part + 36 + tid, c0, c1, 42);
+            const int k0 = G.rhs_start[kr], n = G.rhs_start[kr + 1] - k0;
+            bv = run_sum(rec_rhs + (size_t)k0 * 12, n, 12, tid);
+            cf = run_sum(rec_rhs + (size_t)k0 * 12, n, 12, 6 + tid);
         }
         if (tid < 15 && (tid < 6 || I.offV[kr] >= 0))
             for (int q = G.iv_start[kr]; q < G.iv_start[kr + 1]; ++q) {
@@ -891,7 +1079,6 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
 }
 
 // ---- trial: block LDL^T of the reduced system (one workgroup, 16x16 f64 MFMA tiles) -------------
-typedef double v4d __attribute__((ext_vector_type(4)));
 
 // Wave-synchronous step: LDS operations of one wavefront complete in order, so the fence only has
 // to stop the compiler (wavefront scope); the global-memory fallback needs workgroup scope.
@@ -1269,21 +1456,19 @@ __device__ __forceinline__ void backsub_block(int blk, double *sh, Land L, Red R
     const int p = blk * blockDim.x + threadIdx.x;
     double sc = 0;
     if (p < L.n) {
-        double D[9], Dinv[9];
-        for (int q = 0; q < 9; ++q) D[q] = L.Hll[(size_t)p * 9 + q];
-        D[0] += lambda, D[4] += lambda, D[8] += lambda;
-        inv3(D, Dinv);
-        const double *bl = L.bl + (size_t)p * 3;
-        double c[3] = {bl[0], bl[1], bl[2]};
+        // xl = Dinv (bl - sum_s Hpl_s^T xp_s) = R^-T (y - sum_s M_s^T xp_s) with the build's R^-1, y = R^-1 bl, M_s
+        const double *l = L.lnd + (size_t)p * 12;
+        double Ri[6], c[3], bl[3];
+        for (int q = 0; q < 6; ++q) Ri[q] = l[q];
+        for (int q = 0; q < 3; ++q) c[q] = l[6 + q], bl[q] = l[9 + q];
         for (int s = L.slot_start[p]; s < L.slot_start[p + 1]; ++s) {
             const int o = R.offP[L.slot_kf[s]];
             if (o < 0) continue;
-            const double *B = L.Hpl + (size_t)s * 18;
+            const double *M = L.M + (size_t)s * 18;
             for (int q = 0; q < 3; ++q)
-                for (int r = 0; r < 6; ++r) c[q] -= B[3 * r + q] * xp[o + r];
+                for (int r = 0; r < 6; ++r) c[q] -= M[3 * r + q] * xp[o + r];
         }
-        double xl[3];
-        mv3(Dinv, c, xl);
+        const double xl[3] = {Ri[0] * c[0] + Ri[1] * c[1] + Ri[3] * c[2], Ri[2] * c[1] + Ri[4] * c[2], Ri[5] * c[2]};
         for (int q = 0; q < 3; ++q) {
             bst.pts[(size_t)p * 3 + q] = a.pts[(size_t)p * 3 + q] + xl[q];
             sc += xl[q] * (lambda * xl[q] + bl[q]);
@@ -1521,7 +1706,9 @@ struct omv_lba {
     BlockPat BP{};
     Gather G{};
     double *d_imu_contrib = nullptr;   // [n_imu][30 x 30 + 30] per-edge inertial contributions
-    int n_wg_land = 0, n_wg_edge = 0, n_pchunk = 0, n_schunk = 0, n_lgrp = 0;
+    int n_wg_land = 0, n_wg_edge = 0, n_lgrp = 0;
+    int n_big = 0;             // one-landmark groups of the scalar build path
+    const int *d_big = nullptr;
     // device epilogue (single rank): perm_edge / perm_pt / trackDepth in device order, one staging block
     // [state without points | points in caller order | chi2 in caller order | outlier flags in caller order]
     int *d_perm_edge = nullptr, *d_perm_pt = nullptr;
@@ -1599,6 +1786,14 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
     h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdltLds) == hipSuccess;
+    // the landmark groups of the build take ~77 KB of LDS (two workgroups per CU)
+    if (hipFuncSetAttribute((const void *)build_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBuildLds) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void *)build_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBuildLds) !=
+            hipSuccess) {
+        delete h;
+        return OMV_ERR_HIP;
+    }
     (void)hipGetLastError();
     *out = h;
     return OMV_OK;
@@ -1806,64 +2001,111 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             if (pat[(size_t)i * nb + k]) cs.push_back(make_int2(slot[(size_t)i * nb + k], i));
     }
     cs_start[nb] = (int)cs.size();
-    // Schur terms per block: landmark slots (a, b) of one landmark oriented to the block (a on the block's row
-    // keyframe, b on its column keyframe; on a diagonal block a == b), grouped by block in (landmark, a, b) order,
-    // each block's list padded to whole chunks of 256 (at least one chunk per block: the chunk that assembles it)
-    std::vector<int> sc_start(n_slots + 1, 0);
-    std::vector<int4> tr;
+    // buildSystem landmark groups (land_group): whole landmarks in landmark order, at most kGrpEdges edges, kGrpLand
+    // landmarks, kGrpSlots slots and kGrpW optimisable keyframes; a landmark past one of those alone forms a group of
+    // its own built by the scalar path (land_group_big).  Per group: its keyframes in elimination order (local index a),
+    // its record (w(w+1)/2 blocks a >= b of 36, then w rows of [gradient 6 | Schur rhs 6]), the 16x16 output tiles that
+    // hold a co-observed keyframe pair, and per diagonal tile the residual rows of its keyframes' edges.
+    std::vector<int> slot_edge(h->n_slots + 1, 0);
+    for (int e = E - 1; e >= 0; --e) slot_edge[e_slot[e]] = e;
+    slot_edge[h->n_slots] = E;
+    std::vector<int16_t> slot_lkf(h->n_slots, -1);
+    std::vector<int> grp_pt(1, 0), grp_w, grp_tp(1, 0), grp_blk, blkoff, grp_kf, rhsoff;
+    std::vector<int> blk_start(n_slots + 1, 0), rhs_start(nb + 1, 0);
+    std::vector<uint8_t> tp;
     {
-        std::vector<std::vector<int4>> by_blk(n_slots);
-        for (int q = 0; q < P; ++q)
-            for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
-                for (int b = pt_slot[q]; b < pt_slot[q + 1]; ++b) {
-                    const int ka = slot_kf[a], kb = slot_kf[b];
-                    if (ka >= nb || kb >= nb || ipos[ka] < ipos[kb] || (ka == kb && a != b)) continue;
-                    by_blk[slot[(size_t)ipos[ka] * nb + ipos[kb]]].push_back(make_int4(a, b, q, a == b ? 1 : 0));
+        // per reduced-system block / keyframe: the (blkoff / rhsoff index) of each contributing group, in group order
+        std::vector<std::vector<int>> by_blk(n_slots), by_kf(nb);
+        auto opt_kfs = [&](int q0, int q1) {   // distinct optimisable keyframes of landmarks [q0, q1)
+            std::set<int> k;
+            for (int q = q0; q < q1; ++q)
+                for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a)
+                    if (slot_kf[a] < nb) k.insert(slot_kf[a]);
+            return k;
+        };
+        auto panel_ok = [&](int n_land, int n_kf) {   // the MFMA operand panels fit their LDS region
+            return (n_kf + 1) / 2 * ((3 * n_land + 3) & ~3) <= kPanel;
+        };
+        auto fits = [&](int q0, int q1) {
+            const int nk = (int)opt_kfs(q0, q1).size();
+            return pt_edge[q1] - pt_edge[q0] <= kGrpEdges && q1 - q0 <= kGrpLand && pt_slot[q1] - pt_slot[q0] <= kGrpSlots &&
+                   nk <= kGrpW && panel_ok(q1 - q0, nk);
+        };
+        for (int q = 0; q < P;) {
+            int r = q + 1;
+            const bool big = !fits(q, r);
+            if (!big) {
+                std::set<int> k = opt_kfs(q, r);
+                while (r < P && r - q < kGrpLand && pt_edge[r + 1] - pt_edge[q] <= kGrpEdges &&
+                       pt_slot[r + 1] - pt_slot[q] <= kGrpSlots) {
+                    std::set<int> k2 = k;
+                    for (int a = pt_slot[r]; a < pt_slot[r + 1]; ++a)
+                        if (slot_kf[a] < nb) k2.insert(slot_kf[a]);
+                    if ((int)k2.size() > kGrpW || !panel_ok(r + 1 - q, (int)k2.size())) break;
+                    k.swap(k2);
+                    ++r;
                 }
+            }
+            // the group's keyframes in elimination order
+            std::set<int> ks = opt_kfs(q, r);
+            std::vector<int> kl(ks.begin(), ks.end());
+            std::sort(kl.begin(), kl.end(), [&](int x, int y) { return ipos[x] < ipos[y]; });
+            const int w = (int)kl.size(), nblk = w * (w + 1) / 2;
+            std::vector<int> lk(nb, -1);
+            for (int a = 0; a < w; ++a) lk[kl[a]] = a;
+            for (int a = pt_slot[q]; a < pt_slot[r]; ++a) slot_lkf[a] = (int16_t)(slot_kf[a] < nb ? lk[slot_kf[a]] : -1);
+            const int g = (int)grp_w.size();
+            grp_w.push_back(big ? -w - 1 : w);
+            grp_blk.push_back((int)blkoff.size());
+            grp_kf.push_back((int)rhsoff.size());
+            blkoff.resize(blkoff.size() + nblk, -1);
+            rhsoff.resize(rhsoff.size() + w, -1);
+            // co-observed keyframe pairs (a >= b): the group's blocks
+            std::vector<uint8_t> co((size_t)std::max(w, 1) * std::max(w, 1), 0);
+            for (int x = q; x < r; ++x) {
+                std::vector<int> loc;
+                for (int a = pt_slot[x]; a < pt_slot[x + 1]; ++a)
+                    if (slot_kf[a] < nb) loc.push_back(lk[slot_kf[a]]);
+                for (int u : loc)
+                    for (int v : loc)
+                        if (u >= v) co[(size_t)u * w + v] = 1;
+            }
+            for (int u = 0; u < w; ++u) {
+                by_kf[kl[u]].push_back(grp_kf[g] + u);
+                for (int v = 0; v <= u; ++v)
+                    if (co[(size_t)u * w + v])
+                        by_blk[slot[(size_t)ipos[kl[u]] * nb + ipos[kl[v]]]].push_back(grp_blk[g] + u * (u + 1) / 2 + v);
+            }
+            if (!big) {
+                const int nt = (w + 1) / 2;
+                for (int ti = 0; ti < nt; ++ti)
+                    for (int tj = 0; tj <= ti; ++tj) {
+                        bool any = false;
+                        for (int u = 2 * ti; u < std::min(w, 2 * ti + 2) && !any; ++u)
+                            for (int v = 2 * tj; v < std::min(w, 2 * tj + 2) && !any; ++v) any = u >= v && co[(size_t)u * w + v];
+                        if (any) tp.push_back((uint8_t)ti), tp.push_back((uint8_t)tj);
+                    }
+            }
+            grp_tp.push_back((int)tp.size() / 2);
+            grp_pt.push_back(r);
+            (void)g;
+            q = r;
+        }
+        // records contiguous per block (per keyframe), in group order: assemble_kernel reads them as one run
         for (int t = 0; t < n_slots; ++t) {
-            sc_start[t] = (int)(tr.size() / 256);
-            tr.insert(tr.end(), by_blk[t].begin(), by_blk[t].end());
-            const size_t padded = std::max<size_t>(256, (tr.size() - (size_t)sc_start[t] * 256 + 255) / 256 * 256);
-            tr.resize((size_t)sc_start[t] * 256 + padded, make_int4(0, 0, -1, 0));
+            blk_start[t + 1] = blk_start[t] + (int)by_blk[t].size();
+            for (size_t i = 0; i < by_blk[t].size(); ++i) blkoff[by_blk[t][i]] = blk_start[t] + (int)i;
         }
-        sc_start[n_slots] = (int)(tr.size() / 256);
-    }
-    h->n_schunk = sc_start[n_slots];
-    // launch order: chunks of blocks by the smaller keyframe of the block (blocks that share landmarks together)
-    std::vector<int> schunk_order(h->n_schunk);
-    {
-        std::vector<int> blk_order(n_slots);
-        std::iota(blk_order.begin(), blk_order.end(), 0);
-        std::stable_sort(blk_order.begin(), blk_order.end(), [&](int x, int y) {
-            return std::min(slot_kr[x], slot_kc[x]) < std::min(slot_kr[y], slot_kc[y]);
-        });
-        int w = 0;
-        for (int t : blk_order)
-            for (int c = sc_start[t]; c < sc_start[t + 1]; ++c) schunk_order[w++] = c;
-    }
-    // pose chunks: per optimisable keyframe its visual edges (ascending), <= 256 per chunk
-    std::vector<int> kf_edge_start(nb + 1, 0), kf_edge, pc_start(nb + 1, 0);
-    std::vector<int4> pchunk;
-    for (int e = 0; e < E; ++e)
-        if (e_kf[e] < nb) ++kf_edge_start[e_kf[e] + 1];
-    for (int k = 0; k < nb; ++k) kf_edge_start[k + 1] += kf_edge_start[k];
-    kf_edge.resize(kf_edge_start[nb]);
-    {
-        std::vector<int> fe(kf_edge_start.begin(), kf_edge_start.end() - 1);
-        for (int e = 0; e < E; ++e)
-            if (e_kf[e] < nb) kf_edge[fe[e_kf[e]]++] = e;
-    }
-    std::vector<int> kf_edge_pad;   // per chunk its edges, padded to kGrpEdges (one per thread)
-    for (int k = 0; k < nb; ++k) {
-        pc_start[k] = (int)pchunk.size();
-        for (int q = kf_edge_start[k]; q < kf_edge_start[k + 1]; q += kGrpEdges) {
-            const int qe = std::min(q + kGrpEdges, kf_edge_start[k + 1]);
-            pchunk.push_back(make_int4(k, q, qe, 0));
-            for (int r = 0; r < kGrpEdges; ++r) kf_edge_pad.push_back(q + r < qe ? kf_edge[q + r] : -1);
+        for (int k = 0; k < nb; ++k) {
+            rhs_start[k + 1] = rhs_start[k] + (int)by_kf[k].size();
+            for (size_t i = 0; i < by_kf[k].size(); ++i) rhsoff[by_kf[k][i]] = rhs_start[k] + (int)i;
         }
     }
-    pc_start[nb] = (int)pchunk.size();
-    h->n_pchunk = (int)pchunk.size();
+    h->n_lgrp = (int)grp_w.size();
+    std::vector<int> big_grp;
+    for (int g = 0; g < h->n_lgrp; ++g)
+        if (grp_w[g] < 0) big_grp.push_back(g);
+    h->n_big = (int)big_grp.size();
     // inertial edges per block (edge, side of the row keyframe, side of the column keyframe; side 0 = kf1) and per
     // keyframe (edge, side), in edge order; only the rank that evaluates them
     std::vector<int> ib_start(n_slots + 1, 0), iv_start(nb + 1, 0);
@@ -1972,34 +2214,34 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     HIP_OK(up(d_e_ur, e_ur.data(), E));
     h->E = Edges{d_e_pt, d_e_kf, d_e_cam, d_e_slot, d_e_obs, d_e_w, d_e_ur, E};
     int *d_pt_edge = dalloc<int>(ow, P + 1), *d_pt_slot = dalloc<int>(ow, P + 1), *d_slot_kf = dalloc<int>(ow, h->n_slots),
-        *d_slot_pt = dalloc<int>(ow, h->n_slots);
-    double *d_Hll = dalloc<double>(ow, 9 * (size_t)P), *d_bl = dalloc<double>(ow, 3 * (size_t)P),
-           *d_Hpl = dalloc<double>(ow, 18 * (size_t)h->n_slots);
-    if (!d_Hpl || !d_slot_pt) return OMV_ERR_HIP;
+        *d_slot_edge = dalloc<int>(ow, h->n_slots + 1);
+    int16_t *d_slot_lkf = dalloc<int16_t>(ow, h->n_slots);
+    double *d_lnd = dalloc<double>(ow, 12 * (size_t)P), *d_M = dalloc<double>(ow, 18 * (size_t)h->n_slots),
+           *d_rec = dalloc<double>(ow, 36 * (size_t)blk_start[n_slots]),
+           *d_rec_rhs = dalloc<double>(ow, 12 * (size_t)rhs_start[nb]);
+    if (!d_rec || !d_rec_rhs || !d_M || !d_lnd || !d_slot_lkf || !d_slot_edge) return OMV_ERR_HIP;
+    HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
+    HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
+    HIP_OK(up(d_slot_edge, slot_edge.data(), h->n_slots + 1));
+    if (h->n_slots > 0) HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
+    if (h->n_slots > 0) HIP_OK(up(d_slot_lkf, slot_lkf.data(), h->n_slots));
     {
-        std::vector<int> slot_pt(h->n_slots);
-        for (int q = 0; q < P; ++q)
-            for (int a = pt_slot[q]; a < pt_slot[q + 1]; ++a) slot_pt[a] = q;
-        HIP_OK(up(d_pt_edge, pt_edge.data(), P + 1));
-        HIP_OK(up(d_pt_slot, pt_slot.data(), P + 1));
-        if (h->n_slots > 0) HIP_OK(up(d_slot_kf, slot_kf.data(), h->n_slots));
-        if (h->n_slots > 0) HIP_OK(up(d_slot_pt, slot_pt.data(), h->n_slots));
+        auto upl = [&](const auto &v) {
+            using T = typename std::decay_t<decltype(v)>::value_type;
+            T *d = dalloc<T>(ow, v.size());
+            if (d && !v.empty() && up(d, v.data(), v.size()) != hipSuccess) d = nullptr;
+            return (const T *)d;
+        };
+        Land &L = h->L;
+        L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_slot_edge, d_slot_lkf, d_lnd, d_M, P,
+                 upl(grp_pt), upl(grp_w), upl(grp_tp), upl(tp),
+                 upl(grp_blk), upl(blkoff), upl(grp_kf), upl(rhsoff), d_rec, d_rec_rhs};
+        if (!L.grp_pt || !L.grp_w || !L.grp_tp || !L.tp || !L.grp_blk || !L.blkoff ||
+            !L.grp_kf || !L.rhsoff)
+            return OMV_ERR_HIP;
+        h->d_big = upl(big_grp);
+        if (!h->d_big) return OMV_ERR_HIP;
     }
-    // buildSystem landmark groups: whole landmarks in landmark order, at most kGrpEdges edges AND at most kGrpEdges
-    // landmarks per group (land_group sums one landmark per thread; edge-less landmarks add no edges, so the edge
-    // bound alone would let a group outgrow its threads); a landmark with more edges forms a group of its own
-    std::vector<int> grp_pt(1, 0);
-    for (int q = 0; q < P;) {
-        int r = q + 1;
-        while (r < P && r - q < kGrpEdges && pt_edge[r + 1] - pt_edge[q] <= kGrpEdges) ++r;
-        grp_pt.push_back(r);
-        q = r;
-    }
-    h->n_lgrp = (int)grp_pt.size() - 1;
-    const int *d_grp_pt = dalloc<int>(ow, grp_pt.size());
-    if (!d_grp_pt) return OMV_ERR_HIP;
-    HIP_OK(up(const_cast<int *>(d_grp_pt), grp_pt.data(), grp_pt.size()));
-    h->L = Land{d_pt_edge, d_pt_slot, d_slot_kf, d_slot_pt, d_Hll, d_bl, d_Hpl, P, d_grp_pt};
     h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
     h->d_offA = dalloc<int>(ow, K);
     HIP_OK(up(h->d_offP, offP.data(), K));
@@ -2036,15 +2278,10 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     };
     {
         Gather &g = h->G;
-        g.pchunk = upv(pchunk), g.kf_edge = upv(kf_edge_pad), g.pc_start = upv(pc_start);
-        g.schunk_order = upv(schunk_order), g.tr = upv(tr), g.sc_start = upv(sc_start);
+        g.blk_start = upv(blk_start), g.rhs_start = upv(rhs_start);
         g.imu_blk = upv(imu_blk), g.ib_start = upv(ib_start), g.imu_vec = upv(imu_vec), g.iv_start = upv(iv_start);
-        g.pose_part = dalloc<double>(ow, (size_t)std::max(1, h->n_pchunk) * 27);
-        g.schur_part = dalloc<double>(ow, (size_t)h->n_schunk * 42);
         g.contrib = h->d_imu_contrib;
-        if (!g.pchunk || !g.kf_edge || !g.pc_start || !g.schunk_order || !g.tr || !g.sc_start || !g.imu_blk || !g.ib_start ||
-            !g.imu_vec || !g.iv_start || !g.pose_part || !g.schur_part)
-            return OMV_ERR_HIP;
+        if (!g.blk_start || !g.rhs_start || !g.imu_blk || !g.ib_start || !g.imu_vec || !g.iv_start) return OMV_ERR_HIP;
     }
     // block pattern + level schedule
     {
@@ -2233,49 +2470,30 @@ static omv_status lba_finish_result(omv_lba *h, const omv_lba_opts *o, omv_lba_p
 static bool lba_epilogue_ok(const omv_lba *h);
 static omv_status lba_enqueue_epilogue(omv_lba *h, bool want_chi2);
 
-// buildSystem at state A: the landmark groups, the keyframe-diagonal pose chunks and the inertial edges' quadratic
-// forms in one launch, side by side (build_all_kernel; every part a fixed-order sum: the system is identical run to
-// run).  Measured 29.6 -> 20.8 us per step against the two launches in sequence; a forked graph branch for the second
-// launch had been slower still (its fork / join cost more than the overlap gained).
-static omv_status launch_build(omv_lba *h, const State &A, const State &B, const LmCtl *c) {
-    const int n_imu_blk = h->imu_here ? h->n_imu : 0;
-#ifndef OMV_BUILD_SPLIT
-    {
-        const int n_other = h->n_pchunk + n_imu_blk, n_other_pad = (n_other + 7) & ~7;
-        const int grid = n_other_pad + (h->n_lgrp > 0 ? omv::xcd_grid(h->n_lgrp) : 0);
-        if (grid > 0)
-            build_all_kernel<<<grid, kGrpEdges, 0, h->stream>>>(
-                h->rig, A, B, h->E, h->L, h->n_lgrp, h->G, h->I, h->n_pchunk, n_other, n_other_pad, h->delta_mono,
-                h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu, h->dsqr_imu, h->eb(0), h->eb(1), h->d_imu_contrib, c);
-        HIP_OK(hipGetLastError());
-        return OMV_OK;
-    }
-#endif
-    if (h->n_lgrp > 0)
-        build_land_kernel<<<omv::xcd_grid(h->n_lgrp), kGrpEdges, 0, h->stream>>>(
-            h->rig, A, B, h->E, h->L, h->n_lgrp, h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0),
-            h->eb(1), c);
-    auto go = [&](int b0, int nblk) {
-        if (nblk > 0)
-            build_kernel<<<nblk, kGrpEdges, 0, h->stream>>>(h->rig, A, B, h->E, h->G, h->I, h->n_pchunk, h->delta_mono,
-                                                            h->dsqr_mono, h->delta_st, h->dsqr_st, h->delta_imu,
-                                                            h->dsqr_imu, h->eb(0), h->eb(1), h->d_imu_contrib, c, b0);
-    };
-    // profiling variant (OMV_BUILD_SPLIT): landmark groups, pose chunks and inertial edges as three launches
-    go(0, h->n_pchunk);
-    go(h->n_pchunk, n_imu_blk);
+// buildSystem + the landmark Schur complement at state A (the current state; B the other buffer, picked by the control
+// block's `cur` on the device driver): the landmark groups and the inertial edges' quadratic forms in one launch, side
+// by side (build_all_kernel), then the reduced system assembled per block (assemble_kernel).  Every sum is in a fixed
+// order: the system is identical run to run.  lambda enters the landmark groups (R R^T = Hll + lambda I), so both run
+// every trial; on a sharded solve lambda enters the pose diagonal once (rank 0), every rank damps its own landmarks.
+static omv_status launch_build(omv_lba *h, const State &A, const State &B, const LmCtl *c, double lambda) {
+    const int n_imu = h->imu_here ? h->n_imu : 0, n_imu_pad = (n_imu + 7) & ~7;
+    const int grid = n_imu_pad + (h->n_lgrp > 0 ? omv::xcd_grid(h->n_lgrp) : 0);
+    if (grid > 0)
+        build_all_kernel<<<grid, kGrpEdges, kBuildLds, h->stream>>>(
+            h->rig, A, B, h->E, h->L, h->n_lgrp, h->I, n_imu, n_imu_pad, lambda, h->delta_mono, h->dsqr_mono,
+            h->delta_st, h->dsqr_st, h->delta_imu, h->dsqr_imu, h->eb(0), h->eb(1), h->d_imu_contrib, c);
+    if (h->n_big > 0)
+        build_big_kernel<<<h->n_big, kGrpEdges, kBuildLds, h->stream>>>(h->rig, A, B, h->E, h->L, h->d_big, h->n_big,
+                                                                        lambda, h->delta_mono, h->dsqr_mono, h->delta_st,
+                                                                        h->dsqr_st, h->eb(0), h->eb(1), c);
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }
 
-// The trial's reduced system (H + lambda I minus the landmark Schur terms, b, the Schur right-hand side) in one
-// launch; lambda on the pose diagonal once (rank 0 of a sharded solve), every rank damps its own landmarks.
-static omv_status launch_schur(omv_lba *h, double lambda, const LmCtl *c) {
-    // (a last-chunk-assembles fusion of the two measured 4.5x slower: the device-scope fences it needs write back
-    // and invalidate the XCD's L2 per block)
-    schur_kernel<<<omv::xcd_grid(h->n_schunk), 256, 0, h->stream>>>(h->L, h->G, h->n_schunk, lambda, c);
-    assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, lambda, h->rank == 0 ? 1 : 0, h->d_S,
-                                                          h->d_bb, h->d_coef, c);
+static omv_status launch_assemble(omv_lba *h, double lambda, const LmCtl *c) {
+    assemble_kernel<<<h->BP.n_slots, 256, 0, h->stream>>>(h->G, h->I, h->BP, h->L.rec, h->L.rec_rhs, lambda,
+                                                          h->rank == 0 ? 1 : 0, h->d_S, h->d_bb, h->d_coef, c);
+    HIP_OK(hipGetLastError());
     return OMV_OK;
 }
 
@@ -2304,9 +2522,9 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     const State &A = h->st[0], &B = h->st[1];
     omv_status rs;
     if (ev) HIP_OK(hipEventRecord(ev[0], st));
-    if ((rs = launch_build(h, A, B, c)) != OMV_OK) return rs;
+    if ((rs = launch_build(h, A, B, c, 0.0)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[1], st));
-    if ((rs = launch_schur(h, 0.0, c)) != OMV_OK) return rs;
+    if ((rs = launch_assemble(h, 0.0, c)) != OMV_OK) return rs;
     // sharded: one in-place SUM of this rank's partial reduced system [blocks | b | Schur rhs], ordered on the stream
     if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
@@ -2471,11 +2689,6 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         }
         double currentChi = errors_chi;
         const double iniChi = currentChi;
-        // buildSystem
-        HIP_OK(hipEventRecord(h->ev[0], st));
-        if ((rs = launch_build(h, A, A, nullptr)) != OMV_OK) return rs;
-        HIP_OK(hipEventRecord(h->ev[1], st));
-        HIP_OK(hipGetLastError());
         if (it == 0) {
             lambda = o->lambda_init;
             ni = 2;
@@ -2484,10 +2697,15 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
         double rho = 0;
         int qmax = 0;
         float ms;
-        bool build_timed = false;   // the build's events complete before the first trial's read-back
         do {
+            // buildSystem + the landmark Schur complement at this trial's lambda (a retry rebuilds at the same state; this
+            // driver has one error buffer, which the rejected trial overwrote: the current state's errors first)
+            if (qmax > 0 && (rs = lba_errors(h, A)) != OMV_OK) return rs;
+            HIP_OK(hipEventRecord(h->ev[0], st));
+            if ((rs = launch_build(h, A, A, nullptr, lambda)) != OMV_OK) return rs;
+            HIP_OK(hipEventRecord(h->ev[1], st));
             HIP_OK(hipEventRecord(h->ev[2], st));
-            if ((rs = launch_schur(h, lambda, nullptr)) != OMV_OK) return rs;
+            if ((rs = launch_assemble(h, lambda, nullptr)) != OMV_OK) return rs;
             // one exchange: sum the partial reduced systems [blocks | b | Schur rhs] of the landmark shards
             if ((rs = lba_allreduce(h, h->d_S, h->n_reduce)) != OMV_OK) return rs;
             HIP_OK(hipEventRecord(h->ev[3], st));
@@ -2500,11 +2718,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             const int fail = sc[2] != 0.0;
             HIP_OK(hipEventRecord(h->ev[5], st));
             HIP_OK(hipEventSynchronize(h->ev[5]));
-            if (!build_timed) {
-                HIP_OK(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-                h->stage_ms[0] += ms;
-                build_timed = true;
-            }
+            HIP_OK(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+            h->stage_ms[0] += ms;
             HIP_OK(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
             h->stage_ms[1] += ms;
             HIP_OK(hipEventElapsedTime(&ms, h->ev[3], h->ev[4]));

@@ -2085,6 +2085,7 @@ struct omv_pose {
     uint32_t call = 0;
     int32_t *err = nullptr;
     int mode = OMV_POSE_AUTO, parts = 0;
+    size_t lat_lds[2] = {0, 0};   // the dynamic-LDS size last set on pose_lat_kernel<false / true>
 };
 
 extern "C" {
@@ -2178,13 +2179,21 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     // for batches.  G from the mean edge count: one visual edge per edge-wave thread.
     const int F = b->n_frames;
     const long long ne_tot = (long long)b->n_mono + b->n_stereo;
+    // A part holds at most kLatCap edges and a frame's edges are split over its G parts, so G is sized from the largest
+    // frame the batch can hold: no frame has more than ne_tot edges (the per-frame counts live on the device).  AUTO
+    // takes the grouped kernel only when that bound fits kLatMaxParts parts.
+    const long long g_need = (ne_tot + kLatCap - 3) / (kLatCap - 2);
     const bool grouped_ok = b->kp_cap <= kLatFlagCap;
-    bool grouped = h->mode == OMV_POSE_GROUPED || (h->mode == OMV_POSE_AUTO && F <= kLatAutoFrames && grouped_ok);
+    bool grouped = h->mode == OMV_POSE_GROUPED ||
+                   (h->mode == OMV_POSE_AUTO && F <= kLatAutoFrames && grouped_ok && g_need <= kLatMaxParts);
     if (h->mode == OMV_POSE_GROUPED && !grouped_ok) return OMV_ERR_ARG;
     int G = h->parts;
     const int et = lat_edge_threads(prior != nullptr);
     // one edge per edge-wave thread: parts hold ne / G edges up to one keypoint's two (lat_bound_wave)
-    if (G == 0) G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 3) / (et - 2)));
+    if (G == 0) {
+        G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(1, (ne_tot / F + et - 3) / (et - 2)));
+        G = (int)std::min<long long>(kLatMaxParts, std::max<long long>(G, g_need));
+    }
     if (!grouped) pose_info_kernel<<<F, 64, 0, st>>>(b->preint, prior ? prior->preint_kf : b->preint, h->info);
     if (grouped) {
         h->call = (h->call + 1) & 0xFFFFFu;
@@ -2195,13 +2204,14 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
         const uint32_t salt = h->call << 12;
         const size_t lds = lat_lds_bytes(b->kp_cap);
         gu64 *xb = (gu64 *)h->xbuf;
-        if (prior) {
-            HIP_OK(hipFuncSetAttribute((const void *)pose_lat_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            pose_lat_kernel<true><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
-        } else {
-            HIP_OK(hipFuncSetAttribute((const void *)pose_lat_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            pose_lat_kernel<false><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
+        const int pi = prior ? 1 : 0;   // the LDS attribute only when the size changes
+        if (h->lat_lds[pi] != lds) {
+            HIP_OK(hipFuncSetAttribute(prior ? (const void *)pose_lat_kernel<true> : (const void *)pose_lat_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            h->lat_lds[pi] = lds;
         }
+        if (prior) pose_lat_kernel<true><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
+        else pose_lat_kernel<false><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
     } else if (prior) {
         pose_opt_kernel<true><<<F, kPoseThreads, 0, st>>>(rig, A);
     } else {

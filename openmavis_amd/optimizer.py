@@ -171,7 +171,8 @@ class PoseInertialOptimizer:
 
     def set_mode(self, mode, parts=0):
         """Kernel choice (omv_pose_set_mode): AUTO (grouped kernel up to 16 frames per call, else one workgroup per
-        frame), BATCH or GROUPED (`parts` workgroups per frame, 0 = one per 256 visual edges)."""
+        frame), BATCH or GROUPED (`parts` workgroups per frame; 0 = one per 126 (LastFrame) / 190 (LastKeyFrame)
+        visual edges of the mean frame, at least ceil(batch edges / 1022), at most 48 -- include/omv.h)."""
         _lib.check(self._lib.omv_pose_set_mode(self._h, int(mode), int(parts)), "omv_pose_set_mode")
         return self
 

@@ -209,3 +209,19 @@ def tile_batch(b, F):
             out[k] = np.ascontiguousarray(np.asarray(b[k])[idx])
     out["n_frames"] = F
     return out
+
+
+def concat_batches(a, b):
+    """Frames of batch `a` then of batch `b` (same rig) in one batch: frames of different sizes in one call."""
+    out = dict(a)
+    for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "kf_Rwb", "kf_twb", "kf_vel", "kf_bg", "kf_ba", "preint",
+              "true_Rwb", "true_twb", "true_vel", "t") + tuple(k for k in PRIOR_KEYS if k in a):
+        out[k] = np.ascontiguousarray(np.concatenate([np.asarray(a[k]), np.asarray(b[k])]))
+    for kind in ("mono", "stereo"):
+        sa, sb = np.asarray(a[f"{kind}_start"]), np.asarray(b[f"{kind}_start"])
+        out[f"{kind}_start"] = np.concatenate([sa, sb[1:] + sa[-1]]).astype(np.int32)
+        for k in [k for k in a if k.startswith(kind + "_") and k != f"{kind}_start"]:
+            out[k] = np.ascontiguousarray(np.concatenate([np.asarray(a[k]), np.asarray(b[k])]))
+    out["n_frames"] = int(a["n_frames"]) + int(b["n_frames"])
+    out["kp_cap"] = max(int(a["kp_cap"]), int(b["kp_cap"]))
+    return out

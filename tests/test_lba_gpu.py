@@ -194,6 +194,26 @@ def test_optimize_with_edgeless_points(small, oracle):
         assert np.array_equal(sg["pts"][n0:], np.asarray(prob["pts"], np.float64)[n0:])
 
 
+def test_optimize_with_heavy_landmark(small, oracle):
+    """A landmark with more edges than a build group holds (> 256: its observations repeated 60x with noise) goes to the
+    scalar one-landmark path (build_big_kernel) beside the MFMA groups; same bar against the oracle."""
+    prob = dict(small)
+    rng = np.random.default_rng(5)
+    sel = np.flatnonzero(np.asarray(prob["mono_pt"]) == 0)
+    rep = np.tile(sel, 60)
+    assert len(rep) > 256
+    for k in ("mono_pt", "mono_kf", "mono_cam", "mono_inv_sigma2"):
+        prob[k] = np.concatenate([prob[k], np.asarray(prob[k])[rep]])
+    obs = np.asarray(prob["mono_obs"], np.float64)
+    prob["mono_obs"] = np.concatenate([obs, obs[rep] + rng.normal(0, 0.5, (len(rep), 2))])
+    for large in (True, False):
+        kw = dict(opt_it=4, lambda_init=1e-2) if large else dict(opt_it=10, lambda_init=1e0)
+        ro, so, _ = oracle.lba_optimize(prob, max_trials=10, large=large, **kw)
+        rg, sg = _solver(prob).set_problem(prob).optimize(max_trials=10, large=large, **kw)
+        _compare_result(prob, rg, ro)
+        _compare_state(prob, sg, so, oracle)
+
+
 def test_optimize_full_window(full, oracle):
     """The bench configuration: 25 optimisable + 25 fixed keyframes, 5 cameras, 20k points, 120k edges."""
     ro, so, _ = oracle.lba_optimize(full, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)

@@ -107,3 +107,15 @@ def test_grouped_capacity_is_reported():
     assert int(n_good.cpu()[0]) == -1
     assert opt.last_error() == _lib.OMV_ERR_CAPACITY
     assert opt.last_error() == 0   # read resets it
+
+
+def test_auto_mode_heavy_frame_among_light_ones(oracle):
+    """AUTO over frames of very different sizes (15 light frames and one of ~2,500 edges): the grouped kernel's part
+    count is sized so that no frame overflows a part, and every frame matches the oracle."""
+    from openmavis_amd.synth_pose import concat_batches
+    light = synth_pose.make_pose_batch(n_frames=15, n_pts=40, seed=9)
+    heavy = synth_pose.make_pose_batch(n_frames=1, n_pts=2500, seed=10)
+    b = concat_batches(light, heavy)
+    assert np.diff(b["mono_start"]).max() > 1024 * 2
+    o = oracle.pose_last_kf(b)
+    _compare(b, _run_gpu(b), o)

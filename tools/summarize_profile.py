@@ -16,7 +16,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # substring -> short name, first match wins: the more specific names come before the ones they contain
-SHORT = {"bow_build_kernel": "bow_build", "bow_resolve": "bow_resolve", "build_all_kernel": "lba_build",
+SHORT = {"bow_build_kernel": "bow_build", "bow_resolve": "bow_resolve", "build_all_kernel": "lba_build", "build_big_kernel": "lba_build_big",
          "cur_copy_kernel": "lba_cur_copy", "trial_scalars_kernel": "lba_trial_scalars", "pyr_resize": "pyr_resize", "fast_cells": "fast_cells", "octree": "octree", "describe": "describe",
          "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
          "stereo_tri_kernel": "stereo_tri", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
