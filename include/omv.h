@@ -789,6 +789,27 @@ omv_status omv_frame_pack(int n_frames, int n_cams, int n_blocks, int kp_cap, co
                           const float *uright_in, const int *n_kp, int *offset, omv_kp *kps_out, uint8_t *desc_out,
                           float *uright_out, void *stream);
 
+
+/* ---- map-point refresh (LocalMapping.cc:338-339, :776-778, :897-898; MapPoint.cc:377) ----------------------------
+ * MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:405-490) for a batch of map points: point p's descriptors are
+ * rows desc_row[desc_start[p] .. desc_start[p+1]) of `desc` ([rows][32] u8) -- its observations' L / R / SL / SR rows
+ * in the reference's mObservations (std::map) order, bad keyframes left out by the caller.  best_row[p] = the row of
+ * the descriptor with the least median Hamming distance to the others (vDists[0.5 (N - 1)] of its sorted row, the
+ * first on ties), -1 when the point has none (mDescriptor untouched); desc_out[p] (may be NULL) = that descriptor.
+ * All pointers device. */
+omv_status omv_mappoint_distinctive_descriptors(int n_points, const int32_t *desc_start, const int32_t *desc_row,
+                                                const uint8_t *desc, int32_t *best_row, uint8_t *desc_out, void *stream);
+/* MapPoint::UpdateNormalAndDepth (src/MapPoint.cc:503-588): per point its observation entries
+ * obs_start[p] .. obs_start[p+1] with the entry camera centre obs_center[e] (float3: GetCameraCenter /
+ * GetRightCameraCenter / GetSideLeftCameraCenter / GetSideRightCameraCenter of the keyframe, every entry -- the
+ * reference does not skip bad keyframes here), its mWorldPos pos[p], the reference keyframe's camera centre
+ * ref_center[p], mvScaleFactors[level] of the point's keypoint in it (ref_level_scale[p]) and
+ * mvScaleFactors[nLevels - 1] (ref_max_scale[p]).  Out: mNormalVector, mfMinDistance, mfMaxDistance (float, the
+ * reference's arithmetic order); a point without entries is left untouched.  All pointers device. */
+omv_status omv_mappoint_normal_depth(int n_points, const int32_t *obs_start, const float *obs_center, const float *pos,
+                                     const float *ref_center, const float *ref_level_scale, const float *ref_max_scale,
+                                     float *normal, float *min_dist, float *max_dist, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

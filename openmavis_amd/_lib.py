@@ -285,6 +285,8 @@ SIGNATURES = {
     "omv_frame_uright": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _I, _I, ctypes.POINTER(FisheyeUndist), _F, _VP, _VP,
                               _VP]),
     "omv_frame_pack": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "omv_mappoint_distinctive_descriptors": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "omv_mappoint_normal_depth": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
 }
 
 _lib = None

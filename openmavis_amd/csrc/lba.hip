@@ -49,7 +49,6 @@ namespace {
 using namespace omv_g2o;
 
 constexpr int kGrpEdges = 256;   // edges per buildSystem landmark group / pose chunk (one per thread)
-constexpr int kLandWG = 64;      // landmarks per workgroup (build / Schur / back-substitution)          // keyframes a workgroup may touch for LDS pre-reduction
 
 #define HIP_OK(x)                                                                    \
     do {                                                                             \
@@ -99,37 +98,32 @@ struct ErrBufs {   // per-edge errors of one state: visual [2E], stereo row [E],
 // without one (the host driver passes the state it means as the first of the pair).
 __device__ __forceinline__ int role_buf(const LmCtl *c, int role) { return c ? ((c->cur ^ role) & 1) : role; }
 
-__device__ __forceinline__ void mono_err_block(int blk, double *sh, Rig rig, State s, Edges E, double delta,
-                                               double dsqr, double delta_st, double dsqr_st, double *err,
-                                               double *err3, double *chi2, double *partial) {
-    const int e = blk * blockDim.x + threadIdx.x;
-    double r0 = 0;
-    if (e < E.n) {
-        const int k = E.kf[e], c = E.cam[e], C = rig.n_cams;
-        const double *R = s.Rcw + ((size_t)k * C + c) * 9, *t = s.tcw + ((size_t)k * C + c) * 3;
-        const double *X = s.pts + (size_t)E.pt[e] * 3;
-        double Xc[3];
-        mv3(R, X, Xc);
-        Xc[0] += t[0], Xc[1] += t[1], Xc[2] += t[2];
-        double u, v;
-        cam_project(rig, c, Xc, u, v);
-        const double e0 = E.obs[2 * e] - u, e1 = E.obs[2 * e + 1] - v;
-        const double w = (double)E.w[e];
-        double c2 = e0 * w * e0 + e1 * w * e1;
-        err[2 * e] = e0, err[2 * e + 1] = e1;
-        const float ur = E.ur[e];
-        if (ur >= 0.f) {   // EdgeStereo
-            const double e2 = (double)ur - stereo_ur(u, rig.bf, Xc[2]);
-            err3[e] = e2;
-            c2 += e2 * w * e2;
-        }
-        chi2[e] = c2;
-        double r1;
-        if (ur >= 0.f) huber(c2, delta_st, dsqr_st, r0, r1);
-        else huber(c2, delta, dsqr, r0, r1);
+// EdgeMono / EdgeStereo error of edge e at point X (G2oTypes.h:293-299, :364-402): residual, chi2 into the error
+// buffers; returns the robust chi2 (Huber rho_0) for activeRobustChi2.
+__device__ __forceinline__ double mono_err_edge(const Rig &rig, const double *R, const double *t, const Edges &E, int e,
+                                                const double *X, double delta, double dsqr, double delta_st,
+                                                double dsqr_st, double *err, double *err3, double *chi2) {
+    const int c = E.cam[e];
+    double Xc[3];
+    mv3(R, X, Xc);
+    Xc[0] += t[0], Xc[1] += t[1], Xc[2] += t[2];
+    double u, v;
+    cam_project(rig, c, Xc, u, v);
+    const double e0 = E.obs[2 * e] - u, e1 = E.obs[2 * e + 1] - v;
+    const double w = (double)E.w[e];
+    double c2 = e0 * w * e0 + e1 * w * e1;
+    err[2 * e] = e0, err[2 * e + 1] = e1;
+    const float ur = E.ur[e];
+    if (ur >= 0.f) {   // EdgeStereo
+        const double e2 = (double)ur - stereo_ur(u, rig.bf, Xc[2]);
+        err3[e] = e2;
+        c2 += e2 * w * e2;
     }
-    const double t = block_reduce_sum(r0, sh);
-    if (threadIdx.x == 0) partial[blk] = t;
+    chi2[e] = c2;
+    double r0, r1;
+    if (ur >= 0.f) huber(c2, delta_st, dsqr_st, r0, r1);
+    else huber(c2, delta, dsqr, r0, r1);
+    return r0;
 }
 
 // EdgeInertial + random-walk errors, one block (threads >= I.n contribute 0 to the fixed-order sum).
@@ -299,25 +293,6 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
 __global__ void cur_copy_kernel(const LmCtl *c, const double *B, double *A, size_t n) {
     if (!c->cur) return;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (size_t)gridDim.x * blockDim.x) A[q] = B[q];
-}
-
-// computeActiveErrors in one launch: blocks [0, n_mono_blocks) the visual edges (256 each), the block after
-// them (when has_imu) the inertial / random-walk edges; state and error buffers of the role (role_buf).
-__global__ void __launch_bounds__(256) err_kernel(int n_mono_blocks, int has_imu, Rig rig, State s0, State s1, Edges E,
-                                                  double delta, double dsqr, double delta_st, double dsqr_st,
-                                                  ErrBufs e0, ErrBufs e1, double *partial, Imu I, double delta_imu,
-                                                  double dsqr_imu, double *imu_partial, const LmCtl *ctl, int gate,
-                                                  int role, LmReset reset) {
-    __shared__ double sh[8];
-    if (reset.c && blockIdx.x == 0 && threadIdx.x == 0) ctl_reset(reset), reset.c->init_pending = 1;
-    if (!gate_open(ctl, gate)) return;
-    const int bi = role_buf(ctl, role);
-    const State s = bi ? s1 : s0;
-    const ErrBufs e = bi ? e1 : e0;
-    if ((int)blockIdx.x < n_mono_blocks)
-        mono_err_block(blockIdx.x, sh, rig, s, E, delta, dsqr, delta_st, dsqr_st, e.err, e.err3, e.chi2, partial);
-    else if (has_imu)
-        imu_err_block(sh, s, I, delta_imu, dsqr_imu, e.err9, imu_partial);
 }
 
 // One LM step's bookkeeping after the trial's errors (one block of 256).
@@ -544,7 +519,10 @@ __device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, co
     uint8_t *map = (uint8_t *)(SY + kLdsL);
     const int tid = threadIdx.x;
 #ifdef OMV_BUILD_PROFILE
-    long long tp0 = wall_clock64(), tp1 = 0, tp2 = 0, tp3 = 0;
+    long long tp0 = wall_clock64(), tp1 = 0, tp2 = 0, tp3 = 0, tq[4] = {0, 0, 0, 0};
+#define OMV_TQ(k) tq[k] = wall_clock64()
+#else
+#define OMV_TQ(k)
 #endif
     const int p0 = L.grp_pt[g], p1 = L.grp_pt[g + 1], np = p1 - p0;
     const int e0 = L.edge_start[p0], ne = L.edge_start[p1] - e0;
@@ -640,6 +618,7 @@ __device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, co
         }
     }
     __syncthreads();
+    OMV_TQ(0);
     // phase 2b: M_s = Hpl_s R^-T (kept in registers for the panels); the slot's diagonal terms into LDS (slot-major)
     double M[18];
     if (my_slot >= 0) {
@@ -655,6 +634,7 @@ __device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, co
         for (int q = 0; q < 27; ++q) SE[27 * sl + q] = Ps[q];
     }
     __syncthreads();
+    OMV_TQ(1);
     // phase 2c: the keyframe-diagonal terms of the group, per keyframe a the slots' terms in landmark order
     // (SR's R^-1 rows are dead: the sums take their place)
     double *SP = SR;
@@ -680,6 +660,7 @@ __device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, co
         SP[q] = v;
     }
     __syncthreads();
+    OMV_TQ(2);
     // phase 3a: the MFMA operand panels, one per 16-row tile (keyframes 2t, 2t + 1): panel t holds for K = 3 pl + c
     // the 16 values of rows 16 t .. 16 t + 15: M_{pl, a}[r][c] at row 8 a + r, y_pl[c] at row 8 a + 6 (where landmark pl
     // has a slot on keyframe a), zero elsewhere -- zero-filled, then scattered by the slot threads
@@ -758,10 +739,11 @@ __device__ __forceinline__ void land_group(int g, double *sm, const Rig &rig, co
 #ifdef OMV_BUILD_PROFILE
     __syncthreads();
     tp3 = wall_clock64();
-    if (tid == 0 && (g & 63) == 0)
-        printf("build group %d: edges %d landmarks %d slots %d w %d tiles %d | ticks(100MHz) jac %lld land %lld mfma %lld\n",
-               g, ne, np, ns, w, nt, tp1 - tp0, tp2 - tp1, tp3 - tp2);
+    if (tid == 0 && ((g & 63) == 0 || tp3 - tp0 > 2000))
+        printf("build group %d: edges %d landmarks %d slots %d w %d tiles %d | ticks(100MHz) jac %lld land %lld (2a %lld 2b %lld 2c %lld 3a %lld) mfma %lld\n",
+               g, ne, np, ns, w, nt, tp1 - tp0, tp2 - tp1, tq[0] - tp1, tq[1] - tq[0], tq[2] - tq[1], tp2 - tq[2], tp3 - tp2);
 #endif
+#undef OMV_TQ
 }
 
 // A one-landmark group past the LDS limits (> 256 edges, > 128 slots or > 32 optimisable keyframes): the same
@@ -954,7 +936,14 @@ __global__ void __launch_bounds__(kGrpEdges) build_all_kernel(Rig rig, State s0,
     const ErrBufs eb = bi ? e1 : e0;
     const int b = blockIdx.x;
     if (b < n_imu_pad) {
+#ifdef OMV_BUILD_PROFILE
+        const long long ti0 = wall_clock64();
+#endif
         if (b < n_imu) imu_contrib_block(b, sm, s, I, delta_imu, dsqr_imu, eb.err9, contrib);
+#ifdef OMV_BUILD_PROFILE
+        __syncthreads();
+        if (threadIdx.x == 0 && b == 0) printf("build imu block 0: ticks(100MHz) %lld\n", wall_clock64() - ti0);
+#endif
         return;
     }
     const int bl = b - n_imu_pad, chunk = (n_grp + 7) >> 3;
@@ -1076,6 +1065,26 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
         bvec[16 * kr + tid] = bv;
         coef[16 * kr + tid] = cf;
     }
+}
+
+// ---- trial: keyframe update (in the errors kernel) -----------------------------------------------------------
+// ImuCamPose::Update (G2oTypes.cc:211-235): the new body pose of optimisable keyframe k from the current state a and the
+// solution xp (keyframe order), and camera c's Rcw / tcw of it.
+__device__ __forceinline__ void kf_trial_pose(const Rig &rig, const State &a, const double *u, int k, int c,
+                                              double Rn[9], double twb[3], double Rc[9], double tc[3]) {
+    double Rwb[9], dRw[9], tt[3];
+    for (int q = 0; q < 9; ++q) Rwb[q] = a.Rwb[9 * k + q];
+    mv3(Rwb, u + 3, tt);
+    for (int q = 0; q < 3; ++q) twb[q] = a.twb[3 * k + q] + tt[q];
+    exp_so3(u, dRw);
+    mm3(Rwb, dRw, Rn);
+    double Rbw[9], tbw[3];
+    tr3(Rn, Rbw);
+    mv3(Rbw, twb, tbw);
+    for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
+    mm3(rig.Rcb[c], Rbw, Rc);
+    mv3(rig.Rcb[c], tbw, tc);
+    for (int q = 0; q < 3; ++q) tc[q] += rig.tcb[c][q];
 }
 
 // ---- trial: block LDL^T of the reduced system (one workgroup, 16x16 f64 MFMA tiles) -------------
@@ -1408,89 +1417,140 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     if (tid == 0) *fail = bad;
 }
 
-// ---- trial: keyframe update + landmark back-substitution + computeScale terms, one launch ----------------
-// Block 0: ImuCamPose::Update (G2oTypes.cc:211-235) + the velocity / bias vertex adds for every optimisable
-// keyframe and the pose part of computeScale (scale_partial[0]); blocks 1..: one thread per landmark, the
-// back-substitution xl = Dinv (bl - Hpl^T xp), the point update and the landmark part (scale_partial[blk]).
-__device__ __forceinline__ void update_kf_block(double *sh, Rig rig, Red R, const double *b, const int *offV,
-                                                const int *offG, const int *offA, int n_opt, double lambda,
-                                                const double *xp, State a, State bst, double *scale_partial) {
-    const int C = rig.n_cams;
-    for (int k = threadIdx.x; k < n_opt; k += blockDim.x) {
-        const double *u = xp + R.offP[k];
-        double Rwb[9], twb[3], dRw[9], t[3];
-        for (int q = 0; q < 9; ++q) Rwb[q] = a.Rwb[9 * k + q];
-        mv3(Rwb, u + 3, t);
-        for (int q = 0; q < 3; ++q) twb[q] = a.twb[3 * k + q] + t[q];
-        exp_so3(u, dRw);
-        double Rn[9];
-        mm3(Rwb, dRw, Rn);
-        double Rbw[9], tbw[3];
-        tr3(Rn, Rbw);
-        mv3(Rbw, twb, tbw);
-        for (int q = 0; q < 3; ++q) tbw[q] = -tbw[q];
-        for (int q = 0; q < 9; ++q) bst.Rwb[9 * k + q] = Rn[q];
-        for (int q = 0; q < 3; ++q) bst.twb[3 * k + q] = twb[q];
-        for (int c = 0; c < C; ++c) {
-            double Rc[9], tc[3];
-            mm3(rig.Rcb[c], Rbw, Rc);
-            mv3(rig.Rcb[c], tbw, tc);
-            for (int q = 0; q < 9; ++q) bst.Rcw[((size_t)k * C + c) * 9 + q] = Rc[q];
-            for (int q = 0; q < 3; ++q) bst.tcw[((size_t)k * C + c) * 3 + q] = tc[q] + rig.tcb[c][q];
-        }
-        for (int q = 0; q < 3; ++q) {
-            bst.vel[3 * k + q] = a.vel[3 * k + q] + (offV[k] >= 0 ? xp[offV[k] + q] : 0.0);
-            bst.bg[3 * k + q] = a.bg[3 * k + q] + (offG[k] >= 0 ? xp[offG[k] + q] : 0.0);
-            bst.ba[3 * k + q] = a.ba[3 * k + q] + (offA[k] >= 0 ? xp[offA[k] + q] : 0.0);
-        }
-    }
-    // pose part of sum_j x_j (lambda x_j + b_j)
-    double sc = 0;
-    for (int q = threadIdx.x; q < R.n; q += blockDim.x) sc += xp[q] * (lambda * xp[q] + b[q]);
-    const double tt = block_reduce_sum(sc, sh);
-    if (threadIdx.x == 0) scale_partial[0] = tt;
-}
-
-__device__ __forceinline__ void backsub_block(int blk, double *sh, Land L, Red R, double lambda, const double *xp,
-                                              State a, State bst, double *scale_partial) {
-    const int p = blk * blockDim.x + threadIdx.x;
-    double sc = 0;
-    if (p < L.n) {
-        // xl = Dinv (bl - sum_s Hpl_s^T xp_s) = R^-T (y - sum_s M_s^T xp_s) with the build's R^-1, y = R^-1 bl, M_s
-        const double *l = L.lnd + (size_t)p * 12;
-        double Ri[6], c[3], bl[3];
-        for (int q = 0; q < 6; ++q) Ri[q] = l[q];
-        for (int q = 0; q < 3; ++q) c[q] = l[6 + q], bl[q] = l[9 + q];
-        for (int s = L.slot_start[p]; s < L.slot_start[p + 1]; ++s) {
-            const int o = R.offP[L.slot_kf[s]];
-            if (o < 0) continue;
-            const double *M = L.M + (size_t)s * 18;
-            for (int q = 0; q < 3; ++q)
-                for (int r = 0; r < 6; ++r) c[q] -= M[3 * r + q] * xp[o + r];
-        }
-        const double xl[3] = {Ri[0] * c[0] + Ri[1] * c[1] + Ri[3] * c[2], Ri[2] * c[1] + Ri[4] * c[2], Ri[5] * c[2]};
-        for (int q = 0; q < 3; ++q) {
-            bst.pts[(size_t)p * 3 + q] = a.pts[(size_t)p * 3 + q] + xl[q];
-            sc += xl[q] * (lambda * xl[q] + bl[q]);
-        }
-    }
-    const double t = block_reduce_sum(sc, sh);
-    if (threadIdx.x == 0) scale_partial[1 + blk] = t;
-}
-
-// kf_block: this rank updates the keyframes (every rank of a sharded solve updates them identically; the
-// pose part of computeScale is counted once by the caller's choice of scale partials).
-__global__ void __launch_bounds__(kLandWG) update_kernel(Rig rig, Land L, Red R, const double *b, const int *offV,
-                                                         const int *offG, const int *offA, int n_opt, double lambda,
-                                                         const double *xp, State s0, State s1, double *scale_partial,
-                                                         const LmCtl *ctl) {
+// ---- errors: computeActiveErrors, one workgroup per landmark group --------------------------------------
+// Block 0 (when there are inertial edges or a trial): on a trial (xp) the keyframe update of every optimisable keyframe
+// into the trial state (one thread per keyframe and camera) and the pose part of computeScale (scale_partial[0]), then
+// the inertial / random-walk errors of that state (this block wrote it: a block-scope fence orders it).  Blocks 1..:
+// the landmark groups of the build (whole landmarks and their edges), XCD-contiguous.  On a trial a group first
+// back-substitutes its landmarks, xl = Dinv (bl - sum_s Hpl_s^T xp_s) = R^-T (y - sum_s M_s^T xp_s) from the build's
+// R^-1, y and M_s (the trial point into the trial state and LDS; the landmark part of computeScale into
+// scale_partial[1 + g]) while its other threads form the trial Rcw / tcw of the group's keyframes in LDS (the same
+// arithmetic as block 0's: no block reads another's writes), then its edges' errors.  Without xp the points and poses
+// are the state's.  The state / error buffers are the role's (role_buf); the updates start from the role-0 state.
+struct ErrTrial {
+    const double *xp;        // the solution (keyframe order), or null: no update
+    const double *b;         // the assembled gradient (keyframe order)
+    double lambda;
+    const int *offV, *offG, *offA;
+    int n_opt;
+    const int16_t *e_lkf;    // [E] the edge keyframe's index in its group's list, -1 fixed
+    const int *lkf_kf;       // per group (at Land::grp_kf[g]) its keyframes
+};
+__global__ void __launch_bounds__(256) err_kernel(int n_grp, int lead, int has_imu, Rig rig, State s0, State s1, Edges E,
+                                                  Land L, Red R, ErrTrial T, double delta, double dsqr, double delta_st,
+                                                  double dsqr_st, ErrBufs e0, ErrBufs e1, double *partial,
+                                                  double *scale_partial, Imu I, double delta_imu, double dsqr_imu,
+                                                  double *imu_partial, const LmCtl *ctl, int gate, int role,
+                                                  LmReset reset) {
     __shared__ double sh[8];
-    if (!gate_open(ctl, kGateTrial)) return;
-    lambda = lm_lambda(ctl, lambda);
-    const int ba = role_buf(ctl, 0);   // current -> trial
-    const State a = ba ? s1 : s0, bst = ba ? s0 : s1;
-    if (blockIdx.x == 0) update_kf_block(sh, rig, R, b, offV, offG, offA, n_opt, lambda, xp, a, bst, scale_partial);
-    else backsub_block(blockIdx.x - 1, sh, L, R, lambda, xp, a, bst, scale_partial);
+    extern __shared__ double dyn[];   // 3 per landmark, then 12 per (group keyframe, camera)
+    if (reset.c && blockIdx.x == 0 && threadIdx.x == 0) ctl_reset(reset), reset.c->init_pending = 1;
+    if (!gate_open(ctl, gate)) return;
+    const int bi = role_buf(ctl, role);
+    const State s = bi ? s1 : s0;
+    const State a = role_buf(ctl, 0) ? s1 : s0;
+    const ErrBufs eb = bi ? e1 : e0;
+    const bool trial = T.xp != nullptr;
+    const double lambda = trial ? lm_lambda(ctl, T.lambda) : 0.0;
+    const int tid = threadIdx.x, C = rig.n_cams;
+    int bid = blockIdx.x;
+    if (lead) {
+        if (bid == 0) {
+            if (trial) {
+                for (int t = tid; t < T.n_opt * C; t += blockDim.x) {
+                    const int k = t / C, c = t - k * C;
+                    double Rn[9], twb[3], Rc[9], tc[3];
+                    kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, Rn, twb, Rc, tc);
+                    for (int q = 0; q < 9; ++q) s.Rcw[((size_t)k * C + c) * 9 + q] = Rc[q];
+                    for (int q = 0; q < 3; ++q) s.tcw[((size_t)k * C + c) * 3 + q] = tc[q];
+                    if (c == 0) {
+                        for (int q = 0; q < 9; ++q) s.Rwb[9 * k + q] = Rn[q];
+                        for (int q = 0; q < 3; ++q) {
+                            s.twb[3 * k + q] = twb[q];
+                            s.vel[3 * k + q] = a.vel[3 * k + q] + (T.offV[k] >= 0 ? T.xp[T.offV[k] + q] : 0.0);
+                            s.bg[3 * k + q] = a.bg[3 * k + q] + (T.offG[k] >= 0 ? T.xp[T.offG[k] + q] : 0.0);
+                            s.ba[3 * k + q] = a.ba[3 * k + q] + (T.offA[k] >= 0 ? T.xp[T.offA[k] + q] : 0.0);
+                        }
+                    }
+                }
+                double sc = 0;   // pose part of sum_j x_j (lambda x_j + b_j); b is the assembled gradient (bvec)
+                for (int q = tid; q < R.n; q += blockDim.x) sc += T.xp[q] * (lambda * T.xp[q] + T.b[q]);
+                const double tt = block_reduce_sum(sc, sh);
+                if (tid == 0) scale_partial[0] = tt;
+                __threadfence_block();
+                __syncthreads();
+            }
+            if (has_imu) imu_err_block(sh, s, I, delta_imu, dsqr_imu, eb.err9, imu_partial);
+            return;
+        }
+        --bid;
+    }
+    const int chunk = (n_grp + 7) >> 3, g = (bid & 7) * chunk + (bid >> 3);
+    if (g >= n_grp) return;
+    const int p0 = L.grp_pt[g], np = L.grp_pt[g + 1] - p0;
+    const int f0 = L.edge_start[p0], ne = L.edge_start[p0 + np] - f0;
+    const int w = L.grp_w[g];   // < 0: a one-landmark group past the LDS limits (its poses per edge)
+    double *X = dyn, *PS = dyn + 3 * kGrpLand;
+    double sc = 0;
+    if (tid < np) {
+        const int p = p0 + tid;
+        double Xp[3];
+        if (trial) {
+            const double *l = L.lnd + (size_t)p * 12;
+            double Ri[6], c[3], bl[3];
+            for (int q = 0; q < 6; ++q) Ri[q] = l[q];
+            for (int q = 0; q < 3; ++q) c[q] = l[6 + q], bl[q] = l[9 + q];
+            for (int sl = L.slot_start[p]; sl < L.slot_start[p + 1]; ++sl) {
+                const int o = R.offP[L.slot_kf[sl]];
+                if (o < 0) continue;
+                const double *M = L.M + (size_t)sl * 18;
+                for (int q = 0; q < 3; ++q)
+                    for (int r = 0; r < 6; ++r) c[q] -= M[3 * r + q] * T.xp[o + r];
+            }
+            const double xl[3] = {Ri[0] * c[0] + Ri[1] * c[1] + Ri[3] * c[2], Ri[2] * c[1] + Ri[4] * c[2], Ri[5] * c[2]};
+            for (int q = 0; q < 3; ++q) {
+                Xp[q] = a.pts[(size_t)p * 3 + q] + xl[q];
+                s.pts[(size_t)p * 3 + q] = Xp[q];
+                sc += xl[q] * (lambda * xl[q] + bl[q]);
+            }
+        } else {
+            for (int q = 0; q < 3; ++q) Xp[q] = s.pts[(size_t)p * 3 + q];
+        }
+        for (int q = 0; q < 3; ++q) X[3 * tid + q] = Xp[q];
+    } else if (tid >= kGrpLand && trial && w > 0) {   // threads 128..: the trial poses of the group's keyframes
+        for (int t = tid - kGrpLand; t < w * C; t += blockDim.x - kGrpLand) {
+            const int la = t / C, c = t - la * C, k = T.lkf_kf[L.grp_kf[g] + la];
+            double Rn[9], twb[3];
+            kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, Rn, twb, PS + 12 * t, PS + 12 * t + 9);
+        }
+    }
+    __syncthreads();
+    double r0 = 0;
+    for (int f = tid; f < ne; f += blockDim.x) {
+        const int e = f0 + f, la = trial ? T.e_lkf[e] : -1, cam = E.cam[e];
+        double Rc[9], tc[3];   // the edge camera's pose, in registers
+        if (la < 0) {          // a fixed keyframe (identical in both buffers), or not a trial
+            const size_t o = (size_t)E.kf[e] * C + cam;
+            for (int q = 0; q < 9; ++q) Rc[q] = s.Rcw[o * 9 + q];
+            for (int q = 0; q < 3; ++q) tc[q] = s.tcw[o * 3 + q];
+        } else if (w > 0) {
+            const double *o = PS + 12 * (la * C + cam);
+            for (int q = 0; q < 9; ++q) Rc[q] = o[q];
+            for (int q = 0; q < 3; ++q) tc[q] = o[9 + q];
+        } else {   // the scalar group: per edge
+            double Rn[9], twb[3];
+            kf_trial_pose(rig, a, T.xp + R.offP[E.kf[e]], E.kf[e], cam, Rn, twb, Rc, tc);
+        }
+        r0 += mono_err_edge(rig, Rc, tc, E, e, X + 3 * (E.pt[e] - p0), delta, dsqr, delta_st, dsqr_st, eb.err, eb.err3,
+                            eb.chi2);
+    }
+    const double t = block_reduce_sum(r0, sh);
+    if (tid == 0) partial[g] = t;
+    if (trial) {
+        __syncthreads();
+        const double ts = block_reduce_sum(sc, sh);
+        if (tid == 0) scale_partial[1 + g] = ts;
+    }
 }
 
 // The optimisation's epilogue on the device (single rank): per visual edge the reference's outlier test
@@ -1706,8 +1766,10 @@ struct omv_lba {
     BlockPat BP{};
     Gather G{};
     double *d_imu_contrib = nullptr;   // [n_imu][30 x 30 + 30] per-edge inertial contributions
-    int n_wg_land = 0, n_wg_edge = 0, n_lgrp = 0;
+    int n_lgrp = 0;   // landmark groups (build, errors, back-substitution)
     int n_big = 0;             // one-landmark groups of the scalar build path
+    const int16_t *d_e_lkf = nullptr;   // per edge: its keyframe's index in the group's list (-1: fixed)
+    const int *d_lkf_kf = nullptr;      // per (group, local keyframe): the keyframe
     const int *d_big = nullptr;
     // device epilogue (single rank): perm_edge / perm_pt / trackDepth in device order, one staging block
     // [state without points | points in caller order | chi2 in caller order | outlier flags in caller order]
@@ -1919,7 +1981,6 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     pt_edge[P] = (int)e_pt.size();
     pt_slot[P] = (int)slot_kf.size();
     h->n_slots = (int)slot_kf.size();
-    h->n_wg_land = (P + kLandWG - 1) / kLandWG;
     // inertial edges: ids checked, and their blocks in the keyframe adjacency
     for (int i = 0; i < NI; ++i) {
         if (p->imu_kf1[i] < 0 || p->imu_kf1[i] >= K || p->imu_kf2[i] < 0 || p->imu_kf2[i] >= K ||
@@ -2010,7 +2071,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     for (int e = E - 1; e >= 0; --e) slot_edge[e_slot[e]] = e;
     slot_edge[h->n_slots] = E;
     std::vector<int16_t> slot_lkf(h->n_slots, -1);
-    std::vector<int> grp_pt(1, 0), grp_w, grp_tp(1, 0), grp_blk, blkoff, grp_kf, rhsoff;
+    std::vector<int> grp_pt(1, 0), grp_w, grp_tp(1, 0), grp_blk, blkoff, grp_kf, rhsoff, lkf_kf;
     std::vector<int> blk_start(n_slots + 1, 0), rhs_start(nb + 1, 0);
     std::vector<uint8_t> tp;
     {
@@ -2060,6 +2121,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             grp_kf.push_back((int)rhsoff.size());
             blkoff.resize(blkoff.size() + nblk, -1);
             rhsoff.resize(rhsoff.size() + w, -1);
+            lkf_kf.insert(lkf_kf.end(), kl.begin(), kl.end());
             // co-observed keyframe pairs (a >= b): the group's blocks
             std::vector<uint8_t> co((size_t)std::max(w, 1) * std::max(w, 1), 0);
             for (int x = q; x < r; ++x) {
@@ -2240,7 +2302,11 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
             !L.grp_kf || !L.rhsoff)
             return OMV_ERR_HIP;
         h->d_big = upl(big_grp);
-        if (!h->d_big) return OMV_ERR_HIP;
+        std::vector<int16_t> e_lkf(E);
+        for (int e = 0; e < E; ++e) e_lkf[e] = slot_lkf[e_slot[e]];
+        h->d_e_lkf = upl(e_lkf);
+        h->d_lkf_kf = upl(lkf_kf);
+        if (!h->d_big || !h->d_e_lkf || !h->d_lkf_kf) return OMV_ERR_HIP;
     }
     h->d_offP = dalloc<int>(ow, K), h->d_offV = dalloc<int>(ow, K), h->d_offG = dalloc<int>(ow, K),
     h->d_offA = dalloc<int>(ow, K);
@@ -2315,7 +2381,6 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         }
     }
     // work buffers
-    h->n_wg_edge = (E + 255) / 256;
     h->d_err = dalloc<double>(ow, 2 * (size_t)E);
     h->d_chi2 = dalloc<double>(ow, E);
     h->d_err3 = dalloc<double>(ow, E);
@@ -2324,11 +2389,11 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_chi2_b = dalloc<double>(ow, E);
     h->d_err3_b = dalloc<double>(ow, E);
     h->d_err9_b = dalloc<double>(ow, 19 * (size_t)NI);
-    h->d_partial = dalloc<double>(ow, std::max(1, h->n_wg_edge));
+    h->d_partial = dalloc<double>(ow, std::max(1, h->n_lgrp));
     h->d_imu_partial = dalloc<double>(ow, 1);
-    h->d_partial0 = dalloc<double>(ow, std::max(1, h->n_wg_edge));
+    h->d_partial0 = dalloc<double>(ow, std::max(1, h->n_lgrp));
     h->d_imu_partial0 = dalloc<double>(ow, 1);
-    h->d_scale_partial = dalloc<double>(ow, h->n_wg_land + 1);
+    h->d_scale_partial = dalloc<double>(ow, h->n_lgrp + 1);
     h->d_out = dalloc<double>(ow, 4);
     // [packed blocks | b | coef]: contiguous, the one buffer a sharded solve all-reduces per trial
     h->d_S = dalloc<double>(ow, (size_t)n_slots * 256 + 2 * (size_t)nred);
@@ -2365,21 +2430,32 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 // computeActiveErrors: the visual and inertial errors in one launch (err_kernel).
 // lba_errors: the errors of state s into the first error buffer (host driver, optimize()'s start, evaluation);
 // lba_trial_errors: the device driver's trial state and buffer (role 1 of the control block's `cur`).
+// n_grp_err: the partial count of the visual errors (one per landmark group, in the group order).
+// launch_errors: s0 / s1 and the error buffers by role (role_buf); `xp` (a trial): the landmarks' back-substitution
+// first, from the role-0 state into the role's state.  The host driver keeps one error buffer (both ErrBufs eb(0)).
 static omv_status launch_errors(omv_lba *h, const State &s0, const State &s1, const LmCtl *ctl, int gate, int role,
-                                LmReset reset = LmReset{}, bool init_partials = false) {
-    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
-    const int blocks = nmb + (h->imu_here ? 1 : 0);
+                                LmReset reset = LmReset{}, bool init_partials = false, const double *xp = nullptr,
+                                double lambda = 0.0, bool one_buffer = false) {
+    const int ng = h->n_mono > 0 || xp ? h->n_lgrp : 0;
+    const int lead = xp || h->imu_here ? 1 : 0;
+    const int blocks = (ng > 0 ? omv::xcd_grid(ng) : 0) + lead;
+    const ErrTrial T{xp, h->d_bb, lambda, h->d_offV, h->d_offG, h->d_offA, h->n_opt, h->d_e_lkf, h->d_lkf_kf};
+    const size_t lds = (3 * (size_t)kGrpLand + 12 * (size_t)kGrpW * h->rig.n_cams) * sizeof(double);
     if (blocks > 0)
-        err_kernel<<<blocks, 256, 0, h->stream>>>(nmb, h->imu_here ? 1 : 0, h->rig, s0, s1, h->E, h->delta_mono,
-                                                  h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0), h->eb(1),
-                                                  init_partials ? h->d_partial0 : h->d_partial, h->I, h->delta_imu,
-                                                  h->dsqr_imu, init_partials ? h->d_imu_partial0 : h->d_imu_partial,
-                                                  ctl, gate, role, reset);
+        err_kernel<<<blocks, 256, lds, h->stream>>>(ng, lead, h->imu_here ? 1 : 0, h->rig, s0, s1, h->E, h->L, h->R, T,
+                                                    h->delta_mono, h->dsqr_mono, h->delta_st, h->dsqr_st, h->eb(0),
+                                                    one_buffer ? h->eb(0) : h->eb(1),
+                                                    init_partials ? h->d_partial0 : h->d_partial, h->d_scale_partial,
+                                                    h->I, h->delta_imu, h->dsqr_imu,
+                                                    init_partials ? h->d_imu_partial0 : h->d_imu_partial, ctl, gate, role,
+                                                    reset);
     return hipGetLastError() == hipSuccess ? OMV_OK : OMV_ERR_HIP;
 }
+static int n_grp_err(const omv_lba *h) { return h->n_mono > 0 ? h->n_lgrp : 0; }
 static omv_status lba_errors(omv_lba *h, const State &s) { return launch_errors(h, s, s, nullptr, kGateAlways, 0); }
+// the device driver's trial: back-substitution + errors into the trial buffer (role 1)
 static omv_status lba_trial_errors(omv_lba *h, const LmCtl *c) {
-    return launch_errors(h, h->st[0], h->st[1], c, kGateTrial, 1);
+    return launch_errors(h, h->st[0], h->st[1], c, kGateTrial, 1, LmReset{}, false, h->d_x, 0.0);
 }
 
 // In-place SUM over the ranks of a sharded solve (no-op on one rank).
@@ -2395,7 +2471,7 @@ static omv_status lba_allreduce(omv_lba *h, double *buf, size_t n) {
 // n_scale counts the update's partials (pose part first); only rank 0 contributes the pose part.
 static omv_status lba_read_scalars(omv_lba *h, int n_scale, double out[3], bool with_fail) {
     const int s0 = (h->rank > 0 && n_scale > 0) ? 1 : 0;
-    finish_kernel<<<1, 256, 0, h->stream>>>(h->d_partial, h->n_mono > 0 ? h->n_wg_edge : 0, h->d_imu_partial,
+    finish_kernel<<<1, 256, 0, h->stream>>>(h->d_partial, n_grp_err(h), h->d_imu_partial,
                                            h->d_scale_partial + s0, n_scale - s0, with_fail ? h->d_fail : nullptr,
                                            h->d_out);
     omv_status rs = lba_allreduce(h, h->d_out, 2);
@@ -2506,12 +2582,6 @@ static void launch_ldlt(omv_lba *h, const LmCtl *c) {
                                                              h->d_fail, c);
 }
 
-static void launch_update(omv_lba *h, double lambda, const State &A, const State &B, const LmCtl *c) {
-    update_kernel<<<1 + h->n_wg_land, kLandWG, 0, h->stream>>>(h->rig, h->L, h->R, h->d_bb, h->d_offV, h->d_offG,
-                                                               h->d_offA, h->n_opt, lambda, h->d_x, A, B,
-                                                               h->d_scale_partial, c);
-}
-
 // One LM step of the device driver: the gated kernel sequence (see LmCtl).  The state and error buffers are
 // double-buffered: the kernels take both (st[0], st[1]) and pick the current / trial one by the control block's
 // `cur`, an accepted trial flips it -- no copy launch, and no recomputation of the current errors after a rejected
@@ -2530,9 +2600,8 @@ static omv_status lba_step(omv_lba *h, hipEvent_t *ev) {
     if (ev) HIP_OK(hipEventRecord(ev[2], st));
     launch_ldlt(h, c);
     if (ev) HIP_OK(hipEventRecord(ev[3], st));
-    launch_update(h, 0.0, A, B, c);
     if ((rs = lba_trial_errors(h, c)) != OMV_OK) return rs;
-    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0, nsc = h->n_pts > 0 ? h->n_wg_land + 1 : 1;
+    const int nmb = n_grp_err(h), nsc = 1 + h->n_lgrp;
     const double *pre = nullptr;
     if (lba_collective(h)) {   // [chi(A), chi, computeScale] of this rank's edges / landmarks, summed over the ranks
         const int s0 = h->rank > 0 ? 1 : 0;   // the keyframe part of computeScale enters once (rank 0)
@@ -2565,7 +2634,7 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
     }
     omv_status rs;
     h->host_syncs = 0;
-    const int nmb = h->n_mono > 0 ? h->n_wg_edge : 0;
+    const int nmb = n_grp_err(h);
     const bool sharded = lba_collective(h);
     if (o->opt_it > 0 && nmb + (h->imu_here ? 1 : 0) > 0) {
         // the initial errors into their own partials, the control block reset by the same launch; the first step's
@@ -2676,7 +2745,6 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     bool errors_of_current = true;
     double lambda = 0, ni = 2;
     int nBad = 0, trials = 0, its = 0;
-    const int gl = std::max(1, h->n_wg_land);
     for (int it = 0; it < o->opt_it; ++it) {
         ++its;
         State &A = h->st[h->cur];
@@ -2711,10 +2779,11 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             HIP_OK(hipEventRecord(h->ev[3], st));
             launch_ldlt(h, nullptr);
             HIP_OK(hipEventRecord(h->ev[4], st));
-            // keyframe update + landmark back-substitution (one launch), then the trial's errors
-            launch_update(h, lambda, A, B, nullptr);
-            if ((rs = lba_errors(h, B)) != OMV_OK) return rs;
-            if ((rs = lba_read_scalars(h, h->n_pts > 0 ? gl + 1 : 1, sc, true)) != OMV_OK) return rs;
+            // the keyframe update and the landmarks' back-substitution A -> B, the trial's errors (one launch, this
+            // driver's one error buffer)
+            if ((rs = launch_errors(h, A, B, nullptr, kGateAlways, 1, LmReset{}, false, h->d_x, lambda, true)) != OMV_OK)
+                return rs;
+            if ((rs = lba_read_scalars(h, 1 + h->n_lgrp, sc, true)) != OMV_OK) return rs;
             const int fail = sc[2] != 0.0;
             HIP_OK(hipEventRecord(h->ev[5], st));
             HIP_OK(hipEventSynchronize(h->ev[5]));

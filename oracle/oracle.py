@@ -665,3 +665,32 @@ def search_by_sim3(b, th=7.5):
       _p(m["pos"]), _p(m["min_dist"]), _p(m["max_dist"]), _p(m["desc"]), float(th), float(np.float32(np.log(np.float64(np.float32(1.2))))),
       int(b["nlevels"]), _p(match12), _p(n_found))
     return match12[:len(kp1)], n_found[:len(b["jobs"])]
+
+
+def distinctive_descriptors(desc, desc_start, desc_row):
+    """MapPoint::ComputeDistinctiveDescriptors restated (mappoint_oracle.cpp): the chosen row per point, -1 if none."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    start = np.ascontiguousarray(desc_start, np.int32)
+    rows = np.ascontiguousarray(desc_row, np.int32)
+    n = len(start) - 1
+    best = np.zeros(max(n, 0), np.int32)
+    lib().oracle_distinctive_descriptors(ctypes.c_int(n), _p(start), _p(rows), _p(desc), _p(best))
+    return best
+
+
+def normal_depth(obs_start, obs_center, pos, ref_center, ref_level_scale, ref_max_scale):
+    """MapPoint::UpdateNormalAndDepth restated: (normal [P][3], min_dist [P], max_dist [P]) float32; NaN where the
+    point has no entries (untouched)."""
+    start = np.ascontiguousarray(obs_start, np.int32)
+    cen = np.ascontiguousarray(obs_center, np.float32)
+    P = np.ascontiguousarray(pos, np.float32)
+    rc = np.ascontiguousarray(ref_center, np.float32)
+    ls = np.ascontiguousarray(ref_level_scale, np.float32)
+    ms = np.ascontiguousarray(ref_max_scale, np.float32)
+    n = len(start) - 1
+    normal = np.full((n, 3), np.nan, np.float32)
+    dmin = np.full(n, np.nan, np.float32)
+    dmax = np.full(n, np.nan, np.float32)
+    lib().oracle_normal_depth(ctypes.c_int(n), _p(start), _p(cen), _p(P), _p(rc), _p(ls), _p(ms), _p(normal), _p(dmin),
+                              _p(dmax))
+    return normal, dmin, dmax
