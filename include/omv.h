@@ -810,6 +810,48 @@ omv_status omv_mappoint_normal_depth(int n_points, const int32_t *obs_start, con
                                      const float *ref_center, const float *ref_level_scale, const float *ref_max_scale,
                                      float *normal, float *min_dist, float *max_dist, void *stream);
 
+
+/* ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-780): the geometric test of each of
+ * SearchForTriangulation's matches between the current keyframe and its neighbours ------------------------------
+ * One job per neighbour pKF2, in the reference's neighbour order (the camera-pair state -- sophTcw1 / Ow1 of side 1 --
+ * persists across neighbours; pCamera1 / pCamera2 and side 2 reset per neighbour, :441, :471-477).  For every match
+ * (idx1, match12[idx1]) in idx1 order: the camera-pair state (listed pairs (0,0) (0,1) (1,0) (1,1) when both rigs
+ * have a second camera, (0,2) (2,0) (2,2) (1,3) (3,1) (3,3) when they have four, :514-624; other pairs keep the
+ * previous match's state), parallax of the unprojected rays, GeometricTools::Triangulate (JacobiSVD<Matrix4f>) or
+ * KeyFrame::UnprojectStereo, positive depth, reprojection error in both keyframes, scale consistency.  Float
+ * arithmetic as the reference (no contraction; glibc atan2f / cosf / tanf restated).  Map-point creation and the
+ * graph updates (AddObservation, AddMapPoint, ComputeDistinctiveDescriptors, UpdateNormalAndDepth) stay with the
+ * caller (the last two: omv_mappoint_*). */
+typedef struct omv_cnmp_kf {
+    omv_kf_view kf;                     /* kps by idx (mvKeysUn when NLeft == -1, else mvKeys / Right / SideLeft /
+                                           SideRight by range), n_left = -1 for a single-camera keyframe, level_sigma2;
+                                           desc / has_mp / nodes unused */
+    const omv_kp *kps_raw;              /* [n] mvKeys for KeyFrame::UnprojectStereo (NULL: kf.kps) */
+    float Tcw[4][12];                   /* GetPose / GetRightPose / GetSideLeftPose / GetSideRightPose: Rcw (row-major) | tcw */
+    float Ow[4][3];                     /* GetCameraCenter / GetRightCameraCenter / GetSideLeft.. / GetSideRight.. */
+    float Rwc[9], twc[3];               /* mRwc, mTwc.translation() (UnprojectStereo) */
+    float fx, fy, cx, cy, invfx, invfy; /* the keyframe's fx fy cx cy invfx invfy */
+    float mb, mbf;
+    const float *uright, *depth;        /* device [n] mvuRight / mvDepth (NULL: no stereo observations) */
+    float scale_factors[16];            /* mvScaleFactors */
+} omv_cnmp_kf;
+
+typedef struct omv_cnmp_job {
+    omv_cnmp_kf kf2;                    /* the neighbour */
+    const int32_t *match12;             /* device [kf1.kf.n]: SearchForTriangulation's vMatches12 (-1 none) */
+    float *x3D;                         /* device [kf1.kf.n][3]: the new point of an accepted match */
+    int32_t *status;                    /* device [kf1.kf.n]: 1 triangulated, 2 by UnprojectStereo (bPointStereo),
+                                           0 rejected or no match */
+} omv_cnmp_job;
+
+/* cams / cam_model: host [4][8] / [4] (the rig's L, R, SL, SR; NULL model = all KannalaBrandt8); n_cams: cameras of
+ * the rig (1: mpCamera2 == NULL, 2: L + R, 4: L R SL SR); inertial: mbInertial; far_points / th_far_points:
+ * mbFarPoints / mThFarPoints; scale_factor: the current keyframe's mfScaleFactor (ratioFactor = 1.5 scale_factor).
+ * jobs: host array (n_jobs <= 64). */
+omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, const float *cams,
+                                     const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                                     float th_far_points, float scale_factor, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

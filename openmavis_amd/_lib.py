@@ -170,6 +170,20 @@ class KfView(ctypes.Structure):
 OMV_TRI_PAIRS = 10
 
 
+class CnmpKf(ctypes.Structure):
+    """omv_cnmp_kf (include/omv.h)."""
+    _fields_ = [("kf", KfView), ("kps_raw", ctypes.c_void_p), ("Tcw", (ctypes.c_float * 12) * 4),
+                ("Ow", (ctypes.c_float * 3) * 4), ("Rwc", ctypes.c_float * 9), ("twc", ctypes.c_float * 3),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("invfx", ctypes.c_float), ("invfy", ctypes.c_float), ("mb", ctypes.c_float), ("mbf", ctypes.c_float),
+                ("uright", ctypes.c_void_p), ("depth", ctypes.c_void_p), ("scale_factors", ctypes.c_float * 16)]
+
+
+class CnmpJob(ctypes.Structure):
+    """omv_cnmp_job (include/omv.h)."""
+    _fields_ = [("kf2", CnmpKf), ("match12", ctypes.c_void_p), ("x3D", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
 class TriPair(ctypes.Structure):
     """omv_tri_pair (include/omv.h)."""
     _fields_ = [("kf1", KfView), ("kf2", KfView), ("T", (ctypes.c_float * 12) * OMV_TRI_PAIRS),
@@ -286,6 +300,7 @@ SIGNATURES = {
                               _VP]),
     "omv_frame_pack": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_mappoint_distinctive_descriptors": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "omv_create_new_map_points": (_I, [_I, _VP, _VP, _VP, _VP, _I, _I, _I, ctypes.c_float, ctypes.c_float, _VP]),
     "omv_mappoint_normal_depth": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
 }
 

@@ -1122,6 +1122,210 @@ __global__ void tri_debug_kernel(TriCams C, omv_kp kp1, omv_kp kp2, const float 
     out[26] = x3D[0], out[27] = x3D[1], out[28] = x3D[2], out[29] = u1, out[30] = v1;
 }
 
+
+// ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-780): the geometry of each triangulation match ----
+// The reference walks the neighbours and their matches in order; the only state one match hands to the next is the
+// camera-pair state (sophTcw1 / Ow1 / pCamera1 of side 1, sophTcw2 / Ow2 / pCamera2 of side 2): listed camera pairs
+// assign it, the others keep it; side 1's pose persists across neighbours, the cameras and side 2 reset per neighbour.
+// So each match's state is that of the last listed match before it -- an inclusive max-scan over the match positions
+// -- and the matches are then independent: one thread per match.
+//   cnmp_last_kernel   one block per neighbour: the side-1 camera block of its last listed match (or -1)
+//   cnmp_kernel        one block per neighbour: the state entering it (the last listed side-1 block of the
+//                      neighbours before it), the max-scan over its matches, the per-match geometry
+constexpr int kCnmpThreads = 256;
+struct CnmpArgs {
+    TriCams C;
+    int n_cams, inertial, far_points;
+    float th_far, ratio_factor;
+};
+__device__ __forceinline__ int cnmp_cam(const omv_kf_view &k, int idx) { return k.n_left < 0 ? 0 : cam_of(k, idx); }
+// the listed camera pair's state code (1 + 4 cameraId1 + cameraId2), 0 when the reference keeps the previous state
+__device__ __forceinline__ int cnmp_listed(int n_cams, int c1, int c2) {
+    if (n_cams < 2) return 0;
+    const int code = 4 * c1 + c2;
+    bool l = code == 5 || code == 4 || code == 1 || code == 0;
+    if (n_cams >= 4) l = l || code == 2 || code == 8 || code == 10 || code == 7 || code == 13 || code == 15;
+    return l ? 1 + code : 0;
+}
+__global__ void __launch_bounds__(kCnmpThreads) cnmp_last_kernel(const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs,
+                                                                 int n_cams, int *last_p1) {
+    __shared__ int best;
+    const omv_cnmp_job &J = jobs[blockIdx.x];
+    const omv_kf_view &K1 = kf1->kf, &K2 = J.kf2.kf;
+    if (threadIdx.x == 0) best = -1;
+    __syncthreads();
+    int mine = -1;
+    for (int i = threadIdx.x; i < K1.n; i += blockDim.x) {
+        const int i2 = J.match12[i];
+        if (i2 >= 0 && cnmp_listed(n_cams, cnmp_cam(K1, i), cnmp_cam(K2, i2))) mine = i;
+    }
+    atomicMax(&best, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) last_p1[blockIdx.x] = best >= 0 ? cnmp_cam(K1, best) : -1;
+}
+
+__device__ __forceinline__ float cnmp_dot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ float cnmp_norm3(const float *a) { return omv::sqrtf_cr(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+__device__ __forceinline__ float cosf_glibc(float x) {
+    float s, c;
+    omv::glibc_sincosf(x, &s, &c);
+    return c;
+}
+__device__ bool cnmp_unproject_stereo(const omv_cnmp_kf &K, int i, float *x3D) {   // KeyFrame::UnprojectStereo
+    const float z = K.depth[i];
+    if (!(z > 0)) return false;
+    const omv_kp kp = (K.kps_raw ? K.kps_raw : K.kf.kps)[i];
+    const float x = (kp.x - K.cx) * z * K.invfx, y = (kp.y - K.cy) * z * K.invfy;
+    const float c[3] = {x, y, z};
+    for (int r = 0; r < 3; ++r) x3D[r] = (K.Rwc[3 * r] * c[0] + K.Rwc[3 * r + 1] * c[1] + K.Rwc[3 * r + 2] * c[2]) + K.twc[r];
+    return true;
+}
+// One match under state (p1, c1, p2, c2): 0 rejected, 1 triangulated, 2 by UnprojectStereo (x3D written).
+__device__ int cnmp_match(const CnmpArgs &a, const omv_cnmp_kf &K1, const omv_cnmp_kf &K2, int idx1, int idx2, int p1,
+                          int c1, int p2, int c2, float *x3D) {
+    const omv_kp kp1 = K1.kf.kps[idx1], kp2 = K2.kf.kps[idx2];
+    const float kp1_ur = K1.uright ? K1.uright[idx1] : -1.f, kp2_ur = K2.uright ? K2.uright[idx2] : -1.f;
+    const bool bStereo1 = a.n_cams < 2 && kp1_ur >= 0, bStereo2 = a.n_cams < 2 && kp2_ur >= 0;
+    const float *T1 = K1.Tcw[p1], *T2 = K2.Tcw[p2];
+    const float Rwc1[9] = {T1[0], T1[4], T1[8], T1[1], T1[5], T1[9], T1[2], T1[6], T1[10]};
+    const float Rwc2[9] = {T2[0], T2[4], T2[8], T2[1], T2[5], T2[9], T2[2], T2[6], T2[10]};
+    float xn1[3], xn2[3], ray1[3], ray2[3];
+    cam_unproject_f(a.C.model[c1], a.C.cam[c1], kp1.x, kp1.y, xn1);
+    cam_unproject_f(a.C.model[c2], a.C.cam[c2], kp2.x, kp2.y, xn2);
+    for (int r = 0; r < 3; ++r) ray1[r] = Rwc1[3 * r] * xn1[0] + Rwc1[3 * r + 1] * xn1[1] + Rwc1[3 * r + 2] * xn1[2];
+    for (int r = 0; r < 3; ++r) ray2[r] = Rwc2[3 * r] * xn2[0] + Rwc2[3 * r + 1] * xn2[1] + Rwc2[3 * r + 2] * xn2[2];
+    const float cosParallaxRays = cnmp_dot3(ray1, ray2) / (cnmp_norm3(ray1) * cnmp_norm3(ray2));
+    float cosParallaxStereo = cosParallaxRays + 1;
+    float cosParallaxStereo1 = cosParallaxStereo, cosParallaxStereo2 = cosParallaxStereo;
+    if (bStereo1) cosParallaxStereo1 = cosf_glibc(2 * omv::glibc_atan2f(K1.mb / 2, K1.depth[idx1]));
+    else if (bStereo2) cosParallaxStereo2 = cosf_glibc(2 * omv::glibc_atan2f(K2.mb / 2, K2.depth[idx2]));
+    cosParallaxStereo = fminf(cosParallaxStereo1, cosParallaxStereo2);
+    bool goodProj = false, bPointStereo = false;
+    if (cosParallaxRays < cosParallaxStereo && cosParallaxRays > 0 &&
+        (bStereo1 || bStereo2 || ((double)cosParallaxRays < 0.9996 && a.inertial) ||
+         ((double)cosParallaxRays < 0.9998 && !a.inertial))) {
+        // GeometricTools::Triangulate (src/GeometricTools.cc:27-50)
+        float A[16], V[16];
+        for (int j = 0; j < 4; ++j) {
+            A[j] = xn1[0] * T1[8 + j] - T1[j];
+            A[4 + j] = xn1[1] * T1[8 + j] - T1[4 + j];
+            A[8 + j] = xn2[0] * T2[8 + j] - T2[j];
+            A[12 + j] = xn2[1] * T2[8 + j] - T2[4 + j];
+        }
+        jacobi_svd4_v(A, V);
+        if (V[15] == 0) return 0;
+        for (int i = 0; i < 3; ++i) x3D[i] = V[4 * i + 3] / V[15];
+        goodProj = true;
+    } else if (bStereo1 && cosParallaxStereo1 < cosParallaxStereo2) {
+        bPointStereo = true;
+        goodProj = cnmp_unproject_stereo(K1, idx1, x3D);
+    } else if (bStereo2 && cosParallaxStereo2 < cosParallaxStereo1) {
+        bPointStereo = true;
+        goodProj = cnmp_unproject_stereo(K2, idx2, x3D);
+    } else {
+        return 0;
+    }
+    if (!goodProj) return 0;
+    const float R1r2[3] = {T1[8], T1[9], T1[10]}, R2r2[3] = {T2[8], T2[9], T2[10]};
+    const float z1 = cnmp_dot3(R1r2, x3D) + T1[11];
+    if (z1 <= 0) return 0;
+    const float z2 = cnmp_dot3(R2r2, x3D) + T2[11];
+    if (z2 <= 0) return 0;
+    const float sigmaSquare1 = K1.kf.level_sigma2[kp1.octave];
+    const float R1r0[3] = {T1[0], T1[1], T1[2]}, R1r1[3] = {T1[4], T1[5], T1[6]};
+    const float x1 = cnmp_dot3(R1r0, x3D) + T1[3], y1 = cnmp_dot3(R1r1, x3D) + T1[7];
+    const float invz1 = (float)(1.0 / (double)z1);
+    if (!bStereo1) {
+        const float X[3] = {x1, y1, z1};
+        float u, v;
+        cam_project_f(a.C.model[c1], a.C.cam[c1], X, u, v);
+        const float errX1 = u - kp1.x, errY1 = v - kp1.y;
+        if ((double)(errX1 * errX1 + errY1 * errY1) > 5.991 * (double)sigmaSquare1) return 0;
+    } else {
+        const float u1 = K1.fx * x1 * invz1 + K1.cx, u1_r = u1 - K1.mbf * invz1, v1 = K1.fy * y1 * invz1 + K1.cy;
+        const float errX1 = u1 - kp1.x, errY1 = v1 - kp1.y, errX1_r = u1_r - kp1_ur;
+        if ((double)(errX1 * errX1 + errY1 * errY1 + errX1_r * errX1_r) > 7.8 * (double)sigmaSquare1) return 0;
+    }
+    const float sigmaSquare2 = K2.kf.level_sigma2[kp2.octave];
+    const float R2r0[3] = {T2[0], T2[1], T2[2]}, R2r1[3] = {T2[4], T2[5], T2[6]};
+    const float x2 = cnmp_dot3(R2r0, x3D) + T2[3], y2 = cnmp_dot3(R2r1, x3D) + T2[7];
+    const float invz2 = (float)(1.0 / (double)z2);
+    if (!bStereo2) {
+        const float X[3] = {x2, y2, z2};
+        float u, v;
+        cam_project_f(a.C.model[c2], a.C.cam[c2], X, u, v);
+        const float errX2 = u - kp2.x, errY2 = v - kp2.y;
+        if ((double)(errX2 * errX2 + errY2 * errY2) > 5.991 * (double)sigmaSquare2) return 0;
+    } else {
+        // the reference's mpCurrentKeyFrame->mbf here (:706)
+        const float u2 = K2.fx * x2 * invz2 + K2.cx, u2_r = u2 - K1.mbf * invz2, v2 = K2.fy * y2 * invz2 + K2.cy;
+        const float errX2 = u2 - kp2.x, errY2 = v2 - kp2.y, errX2_r = u2_r - kp2_ur;
+        if ((double)(errX2 * errX2 + errY2 * errY2 + errX2_r * errX2_r) > 7.8 * (double)sigmaSquare2) return 0;
+    }
+    const float n1[3] = {x3D[0] - K1.Ow[p1][0], x3D[1] - K1.Ow[p1][1], x3D[2] - K1.Ow[p1][2]};
+    const float n2[3] = {x3D[0] - K2.Ow[p2][0], x3D[1] - K2.Ow[p2][1], x3D[2] - K2.Ow[p2][2]};
+    const float dist1 = cnmp_norm3(n1), dist2 = cnmp_norm3(n2);
+    if (dist1 == 0 || dist2 == 0) return 0;
+    if (a.far_points && (dist1 >= a.th_far || dist2 >= a.th_far)) return 0;
+    const float ratioDist = dist2 / dist1;
+    const float ratioOctave = K1.scale_factors[kp1.octave] / K2.scale_factors[kp2.octave];
+    if (ratioDist * a.ratio_factor < ratioOctave || ratioDist > ratioOctave * a.ratio_factor) return 0;
+    return bPointStereo ? 2 : 1;
+}
+
+__global__ void __launch_bounds__(kCnmpThreads) cnmp_kernel(const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs,
+                                                            const int *last_p1, CnmpArgs a) {
+    __shared__ int s_scan[kCnmpThreads];
+    const int j = blockIdx.x, t = threadIdx.x;
+    const omv_cnmp_kf &K1 = *kf1;
+    const omv_cnmp_job &J = jobs[j];
+    const omv_cnmp_kf &K2 = J.kf2;
+    const int n = K1.kf.n, chunk = (n + kCnmpThreads - 1) / kCnmpThreads;
+    const int i0 = min(n, t * chunk), i1 = min(n, i0 + chunk);
+    // side 1 entering this neighbour: the last listed match of the neighbours before it
+    int p1_in = 0;
+    for (int q = j - 1; q >= 0; --q)
+        if (last_p1[q] >= 0) {
+            p1_in = last_p1[q];
+            break;
+        }
+    // the last listed match of this thread's chunk, then an inclusive max-scan over the chunks (position-ordered codes)
+    int last = -1;
+    for (int i = i0; i < i1; ++i) {
+        const int i2 = J.match12[i];
+        if (i2 >= 0) {
+            const int code = cnmp_listed(a.n_cams, cnmp_cam(K1.kf, i), cnmp_cam(K2.kf, i2));
+            if (code) last = (i << 5) | code;
+        }
+    }
+    s_scan[t] = last;
+    __syncthreads();
+    for (int d = 1; d < kCnmpThreads; d <<= 1) {
+        const int v = t >= d ? s_scan[t - d] : -1;
+        __syncthreads();
+        s_scan[t] = max(s_scan[t], v);
+        __syncthreads();
+    }
+    int state = t > 0 ? s_scan[t - 1] : -1;   // the listed match before this chunk
+    for (int i = i0; i < i1; ++i) {
+        J.status[i] = 0;
+        const int i2 = J.match12[i];
+        if (i2 < 0) continue;
+        const int code = cnmp_listed(a.n_cams, cnmp_cam(K1.kf, i), cnmp_cam(K2.kf, i2));
+        if (code) state = (i << 5) | code;
+        int p1 = p1_in, c1 = 0, p2 = 0, c2 = 0;
+        if (state >= 0) {
+            const int cc = (state & 31) - 1;
+            p1 = c1 = cc >> 2, p2 = c2 = cc & 3;
+        }
+        float x3D[3];
+        const int st = cnmp_match(a, K1, K2, i, i2, p1, c1, p2, c2, x3D);
+        J.status[i] = st;
+        if (st)
+            for (int q = 0; q < 3; ++q) J.x3D[3 * i + q] = x3D[q];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1225,6 +1429,40 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
     }
     HIP_OK(hipFreeAsync(blob, st));
     return h_err ? (omv_status)h_err : OMV_OK;
+}
+
+
+omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, const float *cams,
+                                     const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                                     float th_far_points, float scale_factor, void *stream) {
+    if (n_jobs < 0 || n_jobs > 64 || (n_jobs > 0 && (!kf1 || !jobs || !cams)) || n_cams < 1 || n_cams > 4) return OMV_ERR_ARG;
+    if (n_jobs == 0 || kf1->kf.n <= 0) return OMV_OK;
+    if (kf1->kf.n >= (1 << 26)) return OMV_ERR_ARG;
+    for (int j = 0; j < n_jobs; ++j)
+        if (!jobs[j].match12 || !jobs[j].x3D || !jobs[j].status) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    CnmpArgs a{};
+    for (int c = 0; c < 4; ++c) {
+        for (int q = 0; q < 8; ++q) a.C.cam[c][q] = cams[8 * c + q];
+        a.C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
+    }
+    a.n_cams = n_cams, a.inertial = inertial ? 1 : 0, a.far_points = far_points ? 1 : 0;
+    a.th_far = th_far_points, a.ratio_factor = 1.5f * scale_factor;
+    // the keyframe views and jobs travel as one device blob: [kf1 | jobs | last_p1]
+    const size_t bytes = sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_jobs + sizeof(int) * n_jobs;
+    void *blob = nullptr;
+    HIP_OK(hipMallocAsync(&blob, bytes, st));
+    char *b = (char *)blob;
+    HIP_OK(hipMemcpyAsync(b, kf1, sizeof(omv_cnmp_kf), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(b + sizeof(omv_cnmp_kf), jobs, sizeof(omv_cnmp_job) * n_jobs, hipMemcpyHostToDevice, st));
+    const omv_cnmp_kf *d_kf1 = (const omv_cnmp_kf *)b;
+    const omv_cnmp_job *d_jobs = (const omv_cnmp_job *)(b + sizeof(omv_cnmp_kf));
+    int *d_last = (int *)(b + sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_jobs);
+    cnmp_last_kernel<<<n_jobs, kCnmpThreads, 0, st>>>(d_kf1, d_jobs, n_cams, d_last);
+    cnmp_kernel<<<n_jobs, kCnmpThreads, 0, st>>>(d_kf1, d_jobs, d_last, a);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipFreeAsync(blob, st));
+    return OMV_OK;
 }
 
 }  // extern "C"

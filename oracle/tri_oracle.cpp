@@ -452,3 +452,147 @@ float oracle_triangulate_matches(const float *cam1, const float *cam2, const omv
 }
 
 }  // extern "C"
+
+// LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-780), the per-match geometry after SearchForTriangulation,
+// written after the reference's loop: sophTcw1 / Ow1 persist across neighbours, pCamera1 / pCamera2 and side 2 reset
+// per neighbour; the listed camera pairs reassign them, the others keep the previous match's.  Float arithmetic with
+// Eigen's 3-element expressions left to right; LocalMapping.cc sees `using namespace std` (DBoW2's
+// TemplatedVocabulary.h), so cos / atan2 of floats are the float functions.
+namespace {
+float dot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+float norm3(const float *a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+int cnmp_cam(const omv_kf_view &k, int idx) {
+    return k.n_left < 0 ? 0 : idx < k.n_left ? 0 : idx < k.n_left + k.n_right ? 1 : idx < k.n_left + k.n_right + k.n_sideleft ? 2 : 3;
+}
+// GeometricTools::Triangulate (src/GeometricTools.cc:27-50)
+bool triangulate_gt(const float *x1, const float *x2, const float *T1, const float *T2, float *x3D) {
+    float A[16], V[16];
+    for (int j = 0; j < 4; ++j) {
+        A[j] = x1[0] * T1[8 + j] - T1[j];
+        A[4 + j] = x1[1] * T1[8 + j] - T1[4 + j];
+        A[8 + j] = x2[0] * T2[8 + j] - T2[j];
+        A[12 + j] = x2[1] * T2[8 + j] - T2[4 + j];
+    }
+    jacobi_svd4_v(A, V);
+    if (V[15] == 0) return false;
+    for (int i = 0; i < 3; ++i) x3D[i] = V[4 * i + 3] / V[15];
+    return true;
+}
+// KeyFrame::UnprojectStereo (src/KeyFrame.cc:840-854)
+bool unproject_stereo(const omv_cnmp_kf &K, int i, const float *depth, float *x3D) {
+    const float z = depth[i];
+    if (!(z > 0)) return false;
+    const omv_kp &kp = (K.kps_raw ? K.kps_raw : K.kf.kps)[i];
+    const float x = (kp.x - K.cx) * z * K.invfx, y = (kp.y - K.cy) * z * K.invfy;
+    const float c[3] = {x, y, z};
+    for (int r = 0; r < 3; ++r) x3D[r] = (K.Rwc[3 * r] * c[0] + K.Rwc[3 * r + 1] * c[1] + K.Rwc[3 * r + 2] * c[2]) + K.twc[r];
+    return true;
+}
+}  // namespace
+
+extern "C" {
+// Host arrays throughout (match12 / uright / depth / x3D / status host pointers in this restatement).
+void oracle_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1p, const omv_cnmp_job *jobs, const float *cams,
+                                  const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                                  float th_far_points, float scale_factor) {
+    const omv_cnmp_kf &K1 = *kf1p;
+    auto model = [&](int c) { return cam_model ? cam_model[c] : OMV_CAM_KB8; };
+    const float ratioFactor = 1.5f * scale_factor;
+    int p1 = 0;   // sophTcw1 / Ow1 (camera block), persists across neighbours
+    for (int j = 0; j < n_jobs; ++j) {
+        const omv_cnmp_job &J = jobs[j];
+        const omv_cnmp_kf &K2 = J.kf2;
+        int c1 = 0, c2 = 0, p2 = 0;   // pCamera1 / pCamera2 / sophTcw2: reset per neighbour
+        for (int idx1 = 0; idx1 < K1.kf.n; ++idx1) {
+            J.status[idx1] = 0;
+            const int idx2 = J.match12[idx1];
+            if (idx2 < 0) continue;
+            const omv_kp &kp1 = K1.kf.kps[idx1], &kp2 = K2.kf.kps[idx2];
+            const int cameraId1 = cnmp_cam(K1.kf, idx1), cameraId2 = cnmp_cam(K2.kf, idx2);
+            const float kp1_ur = K1.uright ? K1.uright[idx1] : -1.f, kp2_ur = K2.uright ? K2.uright[idx2] : -1.f;
+            const bool bStereo1 = n_cams < 2 && kp1_ur >= 0, bStereo2 = n_cams < 2 && kp2_ur >= 0;
+            if (n_cams >= 2) {
+                const int code = cameraId1 * 4 + cameraId2;
+                bool listed = code == 5 || code == 4 || code == 1 || code == 0;
+                if (n_cams >= 4) listed = listed || code == 2 || code == 8 || code == 10 || code == 7 || code == 13 || code == 15;
+                if (listed) p1 = c1 = cameraId1, p2 = c2 = cameraId2;
+            }
+            const float *T1 = K1.Tcw[p1], *T2 = K2.Tcw[p2];
+            const float Rwc1[9] = {T1[0], T1[4], T1[8], T1[1], T1[5], T1[9], T1[2], T1[6], T1[10]};
+            const float Rwc2[9] = {T2[0], T2[4], T2[8], T2[1], T2[5], T2[9], T2[2], T2[6], T2[10]};
+            float xn1[3], xn2[3], ray1[3], ray2[3];
+            cam_unproject_f(model(c1), cams + 8 * c1, kp1.x, kp1.y, xn1);
+            cam_unproject_f(model(c2), cams + 8 * c2, kp2.x, kp2.y, xn2);
+            for (int r = 0; r < 3; ++r) ray1[r] = Rwc1[3 * r] * xn1[0] + Rwc1[3 * r + 1] * xn1[1] + Rwc1[3 * r + 2] * xn1[2];
+            for (int r = 0; r < 3; ++r) ray2[r] = Rwc2[3 * r] * xn2[0] + Rwc2[3 * r + 1] * xn2[1] + Rwc2[3 * r + 2] * xn2[2];
+            const float cosParallaxRays = dot3(ray1, ray2) / (norm3(ray1) * norm3(ray2));
+            float cosParallaxStereo = cosParallaxRays + 1;
+            float cosParallaxStereo1 = cosParallaxStereo, cosParallaxStereo2 = cosParallaxStereo;
+            if (bStereo1) cosParallaxStereo1 = std::cos(2 * std::atan2(K1.mb / 2, K1.depth[idx1]));
+            else if (bStereo2) cosParallaxStereo2 = std::cos(2 * std::atan2(K2.mb / 2, K2.depth[idx2]));
+            cosParallaxStereo = std::min(cosParallaxStereo1, cosParallaxStereo2);
+            float x3D[3];
+            bool goodProj = false, bPointStereo = false;
+            if (cosParallaxRays < cosParallaxStereo && cosParallaxRays > 0 &&
+                (bStereo1 || bStereo2 || (cosParallaxRays < 0.9996 && inertial) || (cosParallaxRays < 0.9998 && !inertial))) {
+                goodProj = triangulate_gt(xn1, xn2, T1, T2, x3D);
+                if (!goodProj) continue;
+            } else if (bStereo1 && cosParallaxStereo1 < cosParallaxStereo2) {
+                bPointStereo = true;
+                goodProj = unproject_stereo(K1, idx1, K1.depth, x3D);
+            } else if (bStereo2 && cosParallaxStereo2 < cosParallaxStereo1) {
+                bPointStereo = true;
+                goodProj = unproject_stereo(K2, idx2, K2.depth, x3D);
+            } else {
+                continue;
+            }
+            if (!goodProj) continue;
+            const float R1r2[3] = {T1[8], T1[9], T1[10]}, R2r2[3] = {T2[8], T2[9], T2[10]};
+            const float z1 = dot3(R1r2, x3D) + T1[11];
+            if (z1 <= 0) continue;
+            const float z2 = dot3(R2r2, x3D) + T2[11];
+            if (z2 <= 0) continue;
+            const float sigmaSquare1 = K1.kf.level_sigma2[kp1.octave];
+            const float R1r0[3] = {T1[0], T1[1], T1[2]}, R1r1[3] = {T1[4], T1[5], T1[6]};
+            const float x1 = dot3(R1r0, x3D) + T1[3], y1 = dot3(R1r1, x3D) + T1[7];
+            const float invz1 = 1.0 / z1;
+            if (!bStereo1) {
+                const float X[3] = {x1, y1, z1};
+                float u, v;
+                cam_project_f(model(c1), cams + 8 * c1, X, u, v);
+                const float errX1 = u - kp1.x, errY1 = v - kp1.y;
+                if ((errX1 * errX1 + errY1 * errY1) > 5.991 * sigmaSquare1) continue;
+            } else {
+                const float u1 = K1.fx * x1 * invz1 + K1.cx, u1_r = u1 - K1.mbf * invz1, v1 = K1.fy * y1 * invz1 + K1.cy;
+                const float errX1 = u1 - kp1.x, errY1 = v1 - kp1.y, errX1_r = u1_r - kp1_ur;
+                if ((errX1 * errX1 + errY1 * errY1 + errX1_r * errX1_r) > 7.8 * sigmaSquare1) continue;
+            }
+            const float sigmaSquare2 = K2.kf.level_sigma2[kp2.octave];
+            const float R2r0[3] = {T2[0], T2[1], T2[2]}, R2r1[3] = {T2[4], T2[5], T2[6]};
+            const float x2 = dot3(R2r0, x3D) + T2[3], y2 = dot3(R2r1, x3D) + T2[7];
+            const float invz2 = 1.0 / z2;
+            if (!bStereo2) {
+                const float X[3] = {x2, y2, z2};
+                float u, v;
+                cam_project_f(model(c2), cams + 8 * c2, X, u, v);
+                const float errX2 = u - kp2.x, errY2 = v - kp2.y;
+                if ((errX2 * errX2 + errY2 * errY2) > 5.991 * sigmaSquare2) continue;
+            } else {
+                const float u2 = K2.fx * x2 * invz2 + K2.cx, u2_r = u2 - K1.mbf * invz2, v2 = K2.fy * y2 * invz2 + K2.cy;
+                const float errX2 = u2 - kp2.x, errY2 = v2 - kp2.y, errX2_r = u2_r - kp2_ur;
+                if ((errX2 * errX2 + errY2 * errY2 + errX2_r * errX2_r) > 7.8 * sigmaSquare2) continue;
+            }
+            const float n1[3] = {x3D[0] - K1.Ow[p1][0], x3D[1] - K1.Ow[p1][1], x3D[2] - K1.Ow[p1][2]};
+            const float n2[3] = {x3D[0] - K2.Ow[p2][0], x3D[1] - K2.Ow[p2][1], x3D[2] - K2.Ow[p2][2]};
+            const float dist1 = norm3(n1), dist2 = norm3(n2);
+            if (dist1 == 0 || dist2 == 0) continue;
+            if (far_points && (dist1 >= th_far_points || dist2 >= th_far_points)) continue;
+            const float ratioDist = dist2 / dist1;
+            const float ratioOctave = K1.scale_factors[kp1.octave] / K2.scale_factors[kp2.octave];
+            if (ratioDist * ratioFactor < ratioOctave || ratioDist > ratioOctave * ratioFactor) continue;
+            J.status[idx1] = bPointStereo ? 2 : 1;
+            for (int q = 0; q < 3; ++q) J.x3D[3 * idx1 + q] = x3D[q];
+        }
+    }
+}
+}  // extern "C"
