@@ -671,6 +671,27 @@ typedef struct omv_pose_prior {
 omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, const omv_pose_prior *prior,
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream);
 
+/* Optimizer::PoseOptimization (src/Optimizer.cc:855-1278), the visual-only pose optimisation Tracking runs before the
+ * IMU is initialised (Tracking.cc:2924) and in the visual-only configurations: one VertexSE3Expmap (SE3Quat Tcw of
+ * camera 0, oplus = exp(dx) * T, se3quat.h:223-257), one unary edge per edge of the batch — mono edges
+ * EdgeSE3ProjectXYZOnlyPose (camera 0) / ...ToBody / ...SLPoseToBody / ...SRPoseToBody (camera c through T_c0,
+ * OptimizableTypes.cpp:30-171; Huber sqrt(5.991)), stereo edges EdgeStereoSE3ProjectXYZOnlyPose (camera 0 with
+ * fx fy cx cy = cam[0][0..3] and bf, types_six_dof_expmap.cpp:339-404; Huber sqrt(7.815)) — and
+ * Levenberg-Marquardt (optimization_algorithm_levenberg.cpp:61-169, tau 1e-5, 10 trials) with a dense LDLT: 4 rounds of
+ * optimize(10), each from the initial pose, chi2 5.991 / 7.815 outlier classification between rounds, robust kernels
+ * dropped after round 3, a single round below 10 edges.  Uses of `b`: n_frames, n_cams, cam, cam_model, bf, the
+ * mono_* / stereo_* edge arrays (mono_close unused; stereo_cam ignored: camera 0), kp_cap, n_mono, n_stereo — the
+ * inertial state / preintegration fields are ignored.  Edges follow the reference's creation rule: one edge per
+ * keypoint (the conventional branch makes a keypoint with mvuRight >= 0 a stereo edge INSTEAD of a mono one).
+ *   rig_q / rig_t   host [n_cams][4] (x y z w) / [3]: T_c0 = mTrl / mTsll / mTsrl as SE3Quat (entry 0 unused)
+ *   pose_q / pose_t device [F][4] / [F][3] in/out: Frame::GetPose() as the SE3Quat the reference builds (:871-873);
+ *                   out: the optimised estimate (unchanged below 3 edges)
+ *   kp_outlier      device [F][kp_cap]: mvbOutlier of the edges' keypoints
+ *   n_good          device [F]: the return value (nInitialCorrespondences - nBad; 0 below 3 edges)
+ * One workgroup per frame; asynchronous. */
+omv_status omv_pose_optimization(omv_pose *h, const omv_pose_batch *b, const double *rig_q, const double *rig_t,
+                                 double *pose_q, double *pose_t, uint8_t *kp_outlier, int32_t *n_good, void *stream);
+
 /* Kernel choice of the two calls above.  OMV_POSE_AUTO (default): up to 16 frames per call run on the grouped
  * kernel — one frame over `parts` workgroups (0: one per 126 (LastFrame) / 190 (LastKeyFrame) visual edges of the batch's
  * mean frame, at least ceil(edges of the whole batch / 1022) so that no frame's part can overflow, at most 48) that

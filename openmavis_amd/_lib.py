@@ -285,6 +285,7 @@ SIGNATURES = {
     "omv_pose_inertial_last_frame": (_I, [_VP, ctypes.POINTER(PoseBatch), ctypes.POINTER(PosePrior), _I, _VP, _VP,
                                           _VP, _VP]),
     "omv_pose_constraint": (_I, [_I, _VP, _VP, _VP]),
+    "omv_pose_optimization": (_I, [_VP, ctypes.POINTER(PoseBatch), _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_pose_set_mode": (_I, [_VP, _I, _I]),
     "omv_pose_edges_from_matches": (_I, [_VP, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _I] + [_VP] * 14),
     "omv_pose_last_error": (_I, [_VP, ctypes.POINTER(ctypes.c_int32), _VP]),

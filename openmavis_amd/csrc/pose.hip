@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <climits>
 #include <cstdio>
 #include <vector>
@@ -2072,6 +2073,363 @@ __global__ void __launch_bounds__(kEdgeBuildThreads) pose_edges_kernel(int C, in
         if (base[0] > max_edges || base[1] > max_edges) atomicOr(o.err, OMV_ERR_CAPACITY);
     }
 }
+
+// ---- Optimizer::PoseOptimization (src/Optimizer.cc:855-1278) ------------------------------------------------------
+// The visual-only pose optimisation: one VertexSE3Expmap (SE3Quat Tcw of camera 0, oplus = exp(dx) * T) with one unary
+// edge per matched keypoint — EdgeSE3ProjectXYZOnlyPose(ToBody / SLPoseToBody / SRPoseToBody) through the rig's T_c0
+// (OptimizableTypes.cpp:30-171) or EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.cpp:339-404) — optimised by
+// Levenberg-Marquardt (optimization_algorithm_levenberg.cpp:61-169: tau 1e-5, 10 trials, Raul's stop) over the 6x6
+// Hessian (BlockSolver_6_3 without landmarks + LinearSolverDense = Eigen::LDLT), 4 rounds of optimize(10) each from the
+// frame's initial pose, outliers re-classified between rounds.  One workgroup per frame: thread t owns edges t,
+// t + 256, ... in every pass, so an edge's chi2 (e->chi2(): the last computeError, a rejected trial's included) and
+// level stay thread-private; per pass a fixed-order wavefront + LDS reduction (deterministic run to run); the solve on
+// wavefront 0 (ldlt_pick_solve<6>), the LM bookkeeping and the SE3Quat update on thread 0.
+struct PoseOnlyArgs {
+    const int32_t *m_start, *m_cam, *m_kp;
+    const double *m_obs;
+    const float *m_w, *m_xw;
+    const int32_t *s_start, *s_kp;
+    const double *s_obs;
+    const float *s_w, *s_xw;
+    double *chi2_m, *chi2_s;
+    uint8_t *act_m, *act_s;
+    uint8_t *kp_out;
+    int kp_cap;
+    int32_t *n_good;
+    double *pose_q, *pose_t;   // [F][4] (x y z w) / [F][3] in/out
+};
+struct PoseOnlyRig {
+    Rig rig;                                          // cameras (project / projectJac by type)
+    double q[kMaxCams][4], t[kMaxCams][3], R[kMaxCams][9];   // T_c0 (mTrl / mTsll / mTsrl) and its rotation matrix
+    double fx, fy, cx, cy, bf;                        // EdgeStereoSE3ProjectXYZOnlyPose
+};
+
+// Eigen's quaternion ops on (x y z w): product, v' = q v q^-1 (_transformVector), Quaternion(Matrix3) and
+// SE3Quat::normalizeRotation.
+__device__ __forceinline__ void q_mul(const double *a, const double *b, double *r) {
+    r[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    r[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    r[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    r[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+}
+__device__ __forceinline__ void q_rot(const double *q, const double *v, double *o) {
+    double u0 = q[1] * v[2] - q[2] * v[1], u1 = q[2] * v[0] - q[0] * v[2], u2 = q[0] * v[1] - q[1] * v[0];
+    u0 += u0, u1 += u1, u2 += u2;
+    o[0] = v[0] + q[3] * u0 + (q[1] * u2 - q[2] * u1);
+    o[1] = v[1] + q[3] * u1 + (q[2] * u0 - q[0] * u2);
+    o[2] = v[2] + q[3] * u2 + (q[0] * u1 - q[1] * u0);
+}
+__device__ void q_from_mat(const double *m, double *q) {
+    double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t, q[1] = (m[2] - m[6]) * t, q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+        q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+        q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    }
+}
+__device__ __forceinline__ void q_normalize_pos(double *q) {
+    if (q[3] < 0) q[0] = -q[0], q[1] = -q[1], q[2] = -q[2], q[3] = -q[3];
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; ++i) q[i] /= n;
+}
+// VertexSE3Expmap::oplusImpl: SE3Quat::exp(dx) * (q, t) (se3quat.h:104-110, :223-257) into (qo, to)
+__device__ void se3_oplus(const double *dx, const double *q, const double *t, double *qo, double *to) {
+    const double w0 = dx[0], w1 = dx[1], w2 = dx[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9], R[9], V[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0) ? 1.0 : 0.0) + O[k] + O2[k], V[k] = R[k];
+    } else {
+        double sn, cs;
+        sincos_d(theta, sn, cs);
+        const double a = sn / theta, b = (1 - cs) / (theta * theta), c = (theta - sn) / pow(theta, 3.0);
+        for (int k = 0; k < 9; ++k) {
+            const double I = (k % 4 == 0) ? 1.0 : 0.0;
+            R[k] = I + a * O[k] + b * O2[k];
+            V[k] = I + b * O[k] + c * O2[k];
+        }
+    }
+    double eq[4], et[3];
+    q_from_mat(R, eq);
+    q_normalize_pos(eq);
+    mv3(V, dx + 3, et);
+    double rt[3];
+    q_rot(eq, t, rt);
+    for (int i = 0; i < 3; ++i) to[i] = et[i] + rt[i];
+    q_mul(eq, q, qo);
+    q_normalize_pos(qo);
+}
+
+struct PoseOnlyEdge {
+    bool stereo;
+    int cam;
+    double obs[3], w, X[3];
+};
+__device__ __forceinline__ PoseOnlyEdge po_edge(const PoseOnlyArgs &A, int m0, int nm, int s0, int e) {
+    PoseOnlyEdge v;
+    if (e < nm) {
+        const int i = m0 + e;
+        v.stereo = false, v.cam = A.m_cam[i];
+        v.obs[0] = A.m_obs[2 * i], v.obs[1] = A.m_obs[2 * i + 1], v.obs[2] = 0;
+        v.w = (double)A.m_w[i];
+        for (int q = 0; q < 3; ++q) v.X[q] = (double)A.m_xw[3 * i + q];
+    } else {
+        const int i = s0 + e - nm;
+        v.stereo = true, v.cam = 0;
+        for (int q = 0; q < 3; ++q) v.obs[q] = A.s_obs[3 * i + q], v.X[q] = (double)A.s_xw[3 * i + q];
+        v.w = (double)A.s_w[i];
+    }
+    return v;
+}
+// computeError at (q, t): residual r, chi2 returned; Xl = T Xw (camera 0), Xc = T_c0 Xl
+__device__ __forceinline__ double po_error(const PoseOnlyRig &P, const double *q, const double *t, const PoseOnlyEdge &v,
+                                           double *r, double *Xl, double *Xc) {
+    q_rot(q, v.X, Xl);
+    for (int i = 0; i < 3; ++i) Xl[i] += t[i];
+    r[2] = 0;
+    if (v.stereo) {   // cam_project with a float invz (types_six_dof_expmap.cpp:339-346)
+        const float invz = (float)(1.0f / Xl[2]);
+        const double u = Xl[0] * invz * P.fx + P.cx;
+        r[0] = v.obs[0] - u;
+        r[1] = v.obs[1] - (Xl[1] * invz * P.fy + P.cy);
+        r[2] = v.obs[2] - (u - P.bf * invz);
+        for (int i = 0; i < 3; ++i) Xc[i] = Xl[i];
+        return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]) + r[2] * (v.w * r[2]);
+    }
+    if (v.cam) {
+        q_rot(P.q[v.cam], Xl, Xc);
+        for (int i = 0; i < 3; ++i) Xc[i] += P.t[v.cam][i];
+    } else {
+        for (int i = 0; i < 3; ++i) Xc[i] = Xl[i];
+    }
+    double u, vv;
+    cam_project(P.rig, v.cam, Xc, u, vv);
+    r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv;
+    return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]);
+}
+// linearizeOplus: -projectJac(Xc) R_c0 SE3deriv(Xl) (mono) / the explicit stereo Jacobian
+__device__ __forceinline__ void po_jac(const PoseOnlyRig &P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
+                                       double *J) {
+    if (v.stereo) {
+        const double x = Xl[0], y = Xl[1], invz = 1.0 / Xl[2], invz_2 = invz * invz;
+        J[0] = x * y * invz_2 * P.fx, J[1] = -(1 + (x * x * invz_2)) * P.fx, J[2] = y * invz * P.fx;
+        J[3] = -invz * P.fx, J[4] = 0, J[5] = x * invz_2 * P.fx;
+        J[6] = (1 + y * y * invz_2) * P.fy, J[7] = -x * y * invz_2 * P.fy, J[8] = -x * invz * P.fy;
+        J[9] = 0, J[10] = -invz * P.fy, J[11] = y * invz_2 * P.fy;
+        J[12] = J[0] - P.bf * y * invz_2, J[13] = J[1] + P.bf * x * invz_2, J[14] = J[2];
+        J[15] = J[3], J[16] = 0, J[17] = J[5] - P.bf * invz_2;
+        return;
+    }
+    double pj[6], pr[6];
+    cam_jac(P.rig, v.cam, Xc, pj);
+    const double *R = P.R[v.cam];
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 3; ++q)
+            pr[3 * r + q] = v.cam ? (-pj[3 * r]) * R[q] + (-pj[3 * r + 1]) * R[3 + q] + (-pj[3 * r + 2]) * R[6 + q]
+                                  : -pj[3 * r + q];
+    const double x = Xl[0], y = Xl[1], z = Xl[2];
+    const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 6; ++q)
+            J[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+}
+
+constexpr int kPoNormal = 28;   // 21 upper-triangle H terms, 6 b terms, the robust chi2
+
+__device__ __forceinline__ void po_reduce(double *acc, int n, double (*red)[kPoNormal], double *out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int q = 0; q < n; ++q) {
+        double v = acc[q];
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        acc[q] = v;
+    }
+    if (lane == 0)
+        for (int q = 0; q < n; ++q) red[wave][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < n) {
+        double t = 0;
+        for (int w = 0; w < kPoseWaves; ++w) t += red[w][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, PoseOnlyArgs A) {
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0, s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
+    const int nE = nm + ns;
+    __shared__ double q0[4], t0[3], sq[4], st[3], tq[4], tt[3];
+    __shared__ double Hs[36], Ad[36], gs[6], xs[6], Lm[36], sums[kPoNormal];
+    __shared__ double red[kPoseWaves][kPoNormal];
+    __shared__ int pick[8], cnt[kPoseWaves];
+    __shared__ double lambda_s, ni_s, cur_s, ini_s;
+    __shared__ int nb_s, qmax_s, again_s, brk_s, ok_s;
+    auto chi2_of = [&](int e) -> double & { return e < nm ? A.chi2_m[m0 + e] : A.chi2_s[s0 + e - nm]; };
+    auto act_of = [&](int e) -> uint8_t & { return e < nm ? A.act_m[m0 + e] : A.act_s[s0 + e - nm]; };
+    auto kp_of = [&](int e) { return e < nm ? A.m_kp[m0 + e] : A.s_kp[s0 + e - nm]; };
+    uint8_t *kpo = A.kp_out + (size_t)f * A.kp_cap;
+    for (int e = tid; e < nE; e += kPoseThreads) act_of(e) = 1, kpo[kp_of(e)] = 0;   // mvbOutlier[i] = false
+    if (nE < 3) {
+        if (tid == 0) A.n_good[f] = 0;
+        return;
+    }
+    if (tid == 0) {
+        for (int i = 0; i < 4; ++i) q0[i] = A.pose_q[4 * f + i];
+        for (int i = 0; i < 3; ++i) t0[i] = A.pose_t[3 * f + i];
+        q_normalize_pos(q0);
+    }
+    if (tid < 6) xs[tid] = 0.0;   // the dense solver's x: kept when a factorisation is not positive
+    const double dmono = (double)(float)sqrt(5.991), dst = (double)(float)sqrt(7.815);
+    bool robust = true;
+    int nBad = 0;
+    for (int round = 0; round < 4; ++round) {
+        __syncthreads();
+        if (tid < 4) sq[tid] = q0[tid];
+        if (tid < 3) st[tid] = t0[tid];
+        int na = 0;
+        for (int e = tid; e < nE; e += kPoseThreads) na += act_of(e);
+        na = block_count(na, cnt);   // (barriers inside)
+        if (na > 0) {   // initializeOptimization(0) found the vertex (otherwise optimize() returns -1)
+            for (int it = 0; it < 10; ++it) {
+                // computeActiveErrors + buildSystem at the current estimate
+                double acc[kPoNormal];
+                for (int q = 0; q < kPoNormal; ++q) acc[q] = 0.0;
+                for (int e = tid; e < nE; e += kPoseThreads) {
+                    if (!act_of(e)) continue;
+                    const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+                    double r[3], Xl[3], Xc[3], J[18];
+                    const double c2 = po_error(P, sq, st, v, r, Xl, Xc);
+                    chi2_of(e) = c2;
+                    po_jac(P, v, Xl, Xc, J);
+                    double r0 = c2, r1 = 1.0;
+                    if (robust) {
+                        const double d = v.stereo ? dst : dmono;
+                        huber(c2, d, d * d, r0, r1);
+                    }
+                    const double w = v.w * r1;
+                    double om[3];
+                    for (int k = 0; k < 3; ++k) om[k] = -v.w * r[k] * r1;
+                    edge_normal(J, v.stereo, w, om, acc);
+                    acc[27] += r0;
+                }
+                po_reduce(acc, kPoNormal, red, sums);
+                if (tid == 0) {
+                    int k = 0;
+                    for (int i = 0; i < 6; ++i)
+                        for (int j = i; j < 6; ++j, ++k) Hs[6 * i + j] = Hs[6 * j + i] = sums[k];
+                    for (int i = 0; i < 6; ++i) gs[i] = sums[21 + i];
+                    cur_s = ini_s = sums[27];
+                    if (it == 0) {   // computeLambdaInit: tau * max |H_jj|
+                        double md = 0;
+                        for (int j = 0; j < 6; ++j) md = fmax(fabs(Hs[7 * j]), md);
+                        lambda_s = 1e-5 * md, ni_s = 2, nb_s = 0;
+                    }
+                    qmax_s = 0;
+                }
+                __syncthreads();
+                double rho = 0;
+                do {
+                    if (tid < 64) {
+                        if (lane < 36) Ad[lane] = Hs[lane] + ((lane % 7 == 0) ? lambda_s : 0.0);
+                        wave_lds_sync();
+                        const bool ok = ldlt_pick_solve<6>(Ad, gs, xs, pick, Lm, lane);
+                        if (lane == 0) {
+                            ok_s = ok ? 1 : 0;
+                            se3_oplus(xs, sq, st, tq, tt);
+                        }
+                    }
+                    __syncthreads();
+                    // computeActiveErrors at the trial estimate
+                    double c = 0.0;
+                    for (int e = tid; e < nE; e += kPoseThreads) {
+                        if (!act_of(e)) continue;
+                        const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+                        double r[3], Xl[3], Xc[3];
+                        const double c2 = po_error(P, tq, tt, v, r, Xl, Xc);
+                        chi2_of(e) = c2;
+                        double r0 = c2, r1;
+                        if (robust) {
+                            const double d = v.stereo ? dst : dmono;
+                            huber(c2, d, d * d, r0, r1);
+                        }
+                        c += r0;
+                    }
+                    po_reduce(&c, 1, red, sums);
+                    if (tid == 0) {
+                        double tempChi = ok_s ? sums[0] : DBL_MAX;
+                        double sc = 0;
+                        for (int j = 0; j < 6; ++j) sc += xs[j] * (lambda_s * xs[j] + gs[j]);
+                        sc += 1e-3;
+                        rho = (cur_s - tempChi) / sc;
+                        if (rho > 0 && isfinite(tempChi)) {
+                            double alpha = 1. - pow((2 * rho - 1), 3.0);
+                            alpha = fmin(alpha, 2. / 3.);
+                            lambda_s *= fmax(1. / 3., alpha);
+                            ni_s = 2;
+                            cur_s = tempChi;
+                            for (int i = 0; i < 4; ++i) sq[i] = tq[i];
+                            for (int i = 0; i < 3; ++i) st[i] = tt[i];
+                        } else {   // pop(): the estimate restored, the edges keep the rejected trial's errors
+                            lambda_s *= ni_s;
+                            ni_s *= 2;
+                        }
+                        qmax_s++;
+                        again_s = (rho < 0 && qmax_s < 10) ? 1 : 0;
+                        brk_s = 0;
+                        if (!again_s) {
+                            if (qmax_s == 10 || rho == 0) brk_s = 1;
+                            else {
+                                nb_s = (ini_s - cur_s) * 1e3 < ini_s ? nb_s + 1 : 0;
+                                brk_s = nb_s >= 3 ? 1 : 0;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                } while (again_s);
+                if (brk_s) break;
+            }
+        }
+        // outlier classification (:1145-1263): an edge left out of this round is re-evaluated at the final estimate
+        int bad = 0;
+        for (int e = tid; e < nE; e += kPoseThreads) {
+            uint8_t &a = act_of(e);
+            double c2 = chi2_of(e);
+            if (!a) {
+                const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+                double r[3], Xl[3], Xc[3];
+                c2 = po_error(P, sq, st, v, r, Xl, Xc);
+                chi2_of(e) = c2;
+            }
+            const bool out = (float)c2 > (e < nm ? 5.991f : 7.815f);
+            a = out ? 0 : 1;
+            bad += out ? 1 : 0;
+        }
+        nBad = block_count(bad, cnt);
+        if (round == 2) robust = false;
+        if (nE < 10) break;   // optimizer.edges().size() < 10
+    }
+    for (int e = tid; e < nE; e += kPoseThreads) kpo[kp_of(e)] = act_of(e) ? 0 : 1;
+    if (tid == 0) {
+        for (int i = 0; i < 4; ++i) A.pose_q[4 * f + i] = sq[i];
+        for (int i = 0; i < 3; ++i) A.pose_t[3 * f + i] = st[i];
+        A.n_good[f] = nE - nBad;
+    }
+}
 }  // namespace
 
 struct omv_pose {
@@ -2234,6 +2592,43 @@ omv_status omv_pose_inertial_last_frame(omv_pose *h, const omv_pose_batch *b, co
                                         int rec_init, uint8_t *kp_outlier, int32_t *n_good, double *H, void *stream) {
     if (!prior) return OMV_ERR_ARG;
     return launch_pose(h, b, prior, rec_init, kp_outlier, n_good, H, stream);
+}
+
+omv_status omv_pose_optimization(omv_pose *h, const omv_pose_batch *b, const double *rig_q, const double *rig_t,
+                                 double *pose_q, double *pose_t, uint8_t *kp_outlier, int32_t *n_good, void *stream) {
+    if (!h || !b || !rig_q || !rig_t || !pose_q || !pose_t || !kp_outlier || !n_good) return OMV_ERR_ARG;
+    if (b->n_frames <= 0 || b->n_frames > h->max_frames || b->n_cams <= 0 || b->n_cams > kMaxCams || b->n_mono < 0 ||
+        b->n_stereo < 0 || b->n_mono > h->max_edges || b->n_stereo > h->max_edges || b->kp_cap <= 0 || !b->cam ||
+        !b->mono_start || !b->stereo_start)
+        return OMV_ERR_ARG;
+    PoseOnlyRig P{};
+    P.rig.n_cams = b->n_cams;
+    for (int c = 0; c < b->n_cams; ++c) {
+        for (int q = 0; q < 8; ++q) P.rig.cam[c][q] = b->cam[8 * c + q];
+        P.rig.model[c] = b->cam_model ? b->cam_model[c] : OMV_CAM_KB8;
+        if (P.rig.model[c] != OMV_CAM_KB8 && P.rig.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
+        // SE3Quat(q, t): normalised, w >= 0; toRotationMatrix for the Jacobian
+        double q[4] = {rig_q[4 * c], rig_q[4 * c + 1], rig_q[4 * c + 2], rig_q[4 * c + 3]};
+        if (q[3] < 0) q[0] = -q[0], q[1] = -q[1], q[2] = -q[2], q[3] = -q[3];
+        const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        if (!(n > 0)) return OMV_ERR_ARG;
+        for (int i = 0; i < 4; ++i) P.q[c][i] = q[i] / n;
+        for (int i = 0; i < 3; ++i) P.t[c][i] = rig_t[3 * c + i];
+        const double x = P.q[c][0], y = P.q[c][1], z = P.q[c][2], w = P.q[c][3];
+        const double tx = 2 * x, ty = 2 * y, tz = 2 * z, twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x,
+                     txy = ty * x, txz = tz * x, tyy = ty * y, tyz = tz * y, tzz = tz * z;
+        const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+                             txz - twy, tyz + twx, 1 - (txx + tyy)};
+        for (int i = 0; i < 9; ++i) P.R[c][i] = R[i];
+    }
+    P.fx = b->cam[0], P.fy = b->cam[1], P.cx = b->cam[2], P.cy = b->cam[3], P.bf = (double)b->bf;
+    const PoseOnlyArgs A{b->mono_start, b->mono_cam, b->mono_kp, b->mono_obs, b->mono_inv_sigma2, b->mono_xw,
+                         b->stereo_start, b->stereo_kp, b->stereo_obs, b->stereo_inv_sigma2, b->stereo_xw, h->chi2,
+                         h->chi2 + h->max_edges, h->act, h->act + h->max_edges, kp_outlier, b->kp_cap, n_good, pose_q,
+                         pose_t};
+    pose_only_kernel<<<b->n_frames, kPoseThreads, 0, (hipStream_t)stream>>>(P, A);
+    HIP_OK(hipGetLastError());
+    return OMV_OK;
 }
 
 omv_status omv_pose_edges_from_matches(omv_pose *h, int n_cams, int kp_cap, const omv_kp *kps, const int *n_kp,

@@ -255,6 +255,26 @@ class PoseInertialOptimizer:
         del keep
         return n_good
 
+    def PoseOptimization(self, batch, arrays, pose_q, pose_t, kp_outlier, stream=None):
+        """Optimizer::PoseOptimization (src/Optimizer.cc:855-1278) on every frame of the batch (omv_pose_optimization):
+        `batch` as above plus rig_q / rig_t (host [n_cams][4] / [3], T_c0 = mTrl / mTsll / mTsrl); `arrays` needs only
+        the edge tensors (EDGE_KEYS); pose_q / pose_t (float64 device [F][4] (x y z w) / [F][3]) hold Frame::GetPose()
+        and receive the optimised Tcw; kp_outlier (uint8 [F][kp_cap]) receives mvbOutlier.  Returns the int32 [F]
+        return values (nInitialCorrespondences - nBad).  Asynchronous; no CPU fallback."""
+        import numpy as np
+        import torch
+        from .synth_pose import as_pose_struct
+        s, keep = as_pose_struct(batch, _lib.PoseBatch, arrays)
+        rq = np.ascontiguousarray(batch["rig_q"], np.float64)
+        rt = np.ascontiguousarray(batch["rig_t"], np.float64)
+        n_good = torch.zeros(s.n_frames, dtype=torch.int32, device=kp_outlier.device)
+        st = stream if stream is not None else torch.cuda.current_stream(kp_outlier.device).cuda_stream
+        _lib.check(self._lib.omv_pose_optimization(self._h, ctypes.byref(s), _lib.ptr(rq), _lib.ptr(rt), _lib.ptr(pose_q),
+                                                   _lib.ptr(pose_t), _lib.ptr(kp_outlier), _lib.ptr(n_good),
+                                                   ctypes.c_void_p(st)), "omv_pose_optimization")
+        del keep
+        return n_good
+
     @staticmethod
     def ConstraintPoseImu(H, out=None, stream=None):
         """The ConstraintPoseImu ctor's projection (include/G2oTypes.h:639-659) of device float64 [n][225]

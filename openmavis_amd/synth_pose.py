@@ -172,8 +172,9 @@ def as_pose_struct(batch, struct_cls, arrays):
     for k in ("Rcb", "tcb", "Rbc", "tbc"):
         setattr(s, k, hptr(batch[k], np.float64))
     s.bf = float(batch["bf"])
-    for k in STATE_KEYS + INPUT_KEYS:
-        setattr(s, k, anyptr(arrays[k]))
+    for k in STATE_KEYS + INPUT_KEYS:   # absent keys stay NULL (the pose-only call reads only the edges)
+        if k in arrays:
+            setattr(s, k, anyptr(arrays[k]))
     s.kp_cap = int(batch["kp_cap"])
     s.n_mono, s.n_stereo = int(len(batch["mono_cam"])), int(len(batch["stereo_cam"]))
     if "cam_model" in batch:
@@ -225,3 +226,82 @@ def concat_batches(a, b):
     out["n_frames"] = int(a["n_frames"]) + int(b["n_frames"])
     out["kp_cap"] = max(int(a["kp_cap"]), int(b["kp_cap"]))
     return out
+
+
+def quat_of(R):
+    """Eigen's Quaternion(const Matrix3&) (quaternionbase_assign_impl), coefficients (x, y, z, w), w >= 0."""
+    m = np.asarray(R, np.float64)
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    q = np.zeros(4)
+    if t > 0:
+        t = np.sqrt(t + 1.0)
+        q[3] = 0.5 * t
+        t = 0.5 / t
+        q[0], q[1], q[2] = (m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        q[3] = (m[k, j] - m[j, k]) * t
+        q[j] = (m[j, i] + m[i, j]) * t
+        q[k] = (m[k, i] + m[i, k]) * t
+    return q if q[3] >= 0 else -q
+
+
+def quat_mat(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def make_pose_only_batch(n_frames=8, n_pts=300, seed=1, outlier_frac=0.1, n_cams=4, stereo_frac=0.0, bf=40.0,
+                         rot_noise_deg=0.5, trans_noise=0.03):
+    """Batches for Optimizer::PoseOptimization (Optimizer.cc:855-1278).  n_cams >= 2: the rigid-body branch
+    (:981-1120, Kannala-Brandt rig, one mono edge per keypoint on camera c through T_c0 = mTrl / mTsll / mTsrl);
+    n_cams == 1: the conventional branch (:911-979, pinhole camera 0) where a keypoint with a right coordinate gets
+    an EdgeStereoSE3ProjectXYZOnlyPose INSTEAD of the mono edge (`stereo_frac` of them).  The frame's pose Tcw
+    (camera 0) and the rig come through Sophus::SE3f (float quaternion / translation) cast to double, as the
+    reference builds its SE3Quats (:871-873, :1040-1042).  Adds pose_q / pose_t [F][4] / [F][3] and rig_q / rig_t
+    [n_cams][4] / [3] to make_pose_batch's dict (whose state / IMU arrays the pose-only call ignores)."""
+    pin = n_cams == 1
+    b = make_pose_batch(n_frames=n_frames, n_pts=n_pts, seed=seed, outlier_frac=outlier_frac,
+                        stereo_frac=stereo_frac if pin else 0.0, n_cams=n_cams, bf=bf, rot_noise_deg=rot_noise_deg,
+                        trans_noise=trans_noise, pinhole=pin)
+    F = int(b["n_frames"])
+    if pin and len(b["stereo_cam"]):   # stereo XOR mono per keypoint
+        keep = np.ones(len(b["mono_cam"]), bool)
+        for f in range(F):
+            skp = set(b["stereo_kp"][b["stereo_start"][f]:b["stereo_start"][f + 1]].tolist())
+            for e in range(b["mono_start"][f], b["mono_start"][f + 1]):
+                if int(b["mono_kp"][e]) in skp:
+                    keep[e] = False
+        counts = [int(keep[b["mono_start"][f]:b["mono_start"][f + 1]].sum()) for f in range(F)]
+        for k in [k for k in b if k.startswith("mono_") and k != "mono_start"]:
+            b[k] = np.ascontiguousarray(np.asarray(b[k])[keep])
+        b["mono_start"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+
+    def se3f(R, t):
+        q = quat_of(R).astype(np.float32)
+        q = (q / np.linalg.norm(q.astype(np.float64))).astype(np.float32)   # Sophus keeps a unit quaternion
+        return q.astype(np.float64), np.asarray(t, np.float32).astype(np.float64)
+
+    pq, pt = [], []
+    for f in range(F):
+        q, t = se3f(b["Rcw"][f][0], b["tcw"][f][0])
+        pq.append(q), pt.append(t)
+    b["pose_q"], b["pose_t"] = np.array(pq), np.array(pt)
+    rq, rt = [np.array([0, 0, 0, 1.0])], [np.zeros(3)]
+    for c in range(1, n_cams):   # T_c0 = T_cb T_b0
+        R = b["Rcb"][c] @ b["Rcb"][0].T
+        t = b["tcb"][c] - R @ b["tcb"][0]
+        q, tt = se3f(R, t)
+        rq.append(q), rt.append(tt)
+    b["rig_q"], b["rig_t"] = np.array(rq), np.array(rt)
+    return b

@@ -1827,3 +1827,321 @@ int oracle_pose_inertial_last_frame(const omv_pose_batch *b, const omv_pose_prio
 }
 
 }  // extern "C"
+
+// =============================================================================================
+// Optimizer::PoseOptimization (src/Optimizer.cc:855-1278), one frame: the non-inertial pose-only optimisation
+// Tracking runs before the IMU is initialised (Tracking.cc:2924) and in the visual-only configurations.
+//   vertex     VertexSE3Expmap (types_six_dof_expmap.h:57-77): SE3Quat Tcw of camera 0, oplus = exp(dx) * T
+//              (se3quat.h:104-110, :223-257), the quaternion kept normalised with w >= 0 (:280-285)
+//   edges      EdgeSE3ProjectXYZOnlyPose / ...PoseToBody / ...SLPoseToBody / ...SRPoseToBody (OptimizableTypes.h:12-38,
+//              OptimizableTypes.cpp:30-171): camera c of the rig through T_c0 (mTrl / mTsll / mTsrl), Huber sqrt(5.991);
+//              EdgeStereoSE3ProjectXYZOnlyPose (types_six_dof_expmap.cpp:339-404, float invz), Huber sqrt(7.815)
+//   optimizer  OptimizationAlgorithmLevenberg (tau 1e-5, 10 trials) over BlockSolver_6_3 with no landmark (Hpp only) and
+//              LinearSolverDense (Eigen::LDLT): 4 rounds of optimize(10), each from the frame's initial pose
+//              (:1136-1142), outliers re-classified between rounds (chi2 5.991 / 7.815), robust kernels dropped
+//              after round 3, early stop when fewer than 10 edges.
+// Summation order = edge creation order (keypoint order), as g2o's id-sorted active edge list.
+namespace {
+
+struct Quat {   // Eigen::Quaterniond coefficients
+    double x, y, z, w;
+};
+Quat qmul(const Quat &a, const Quat &b) {   // Eigen quat_product
+    return Quat{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+                a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+V3 qrot(const Quat &q, const V3 &v) {   // Eigen _transformVector: uv = 2 q.vec x v; v + w uv + q.vec x uv
+    V3 uv{{q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]}};
+    uv = add(uv, uv);
+    const V3 c{{q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]}};
+    return V3{{v[0] + q.w * uv[0] + c[0], v[1] + q.w * uv[1] + c[1], v[2] + q.w * uv[2] + c[2]}};
+}
+M3 qmat(const Quat &q) {   // QuaternionBase::toRotationMatrix
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w, txx = tx * q.x, txy = ty * q.x, txz = tz * q.x,
+                 tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    M3 r;
+    r(0, 0) = 1 - (tyy + tzz), r(0, 1) = txy - twz, r(0, 2) = txz + twy;
+    r(1, 0) = txy + twz, r(1, 1) = 1 - (txx + tzz), r(1, 2) = tyz - twx;
+    r(2, 0) = txz - twy, r(2, 1) = tyz + twx, r(2, 2) = 1 - (txx + tyy);
+    return r;
+}
+Quat qfrom(const M3 &m) {   // Quaternion(const Matrix3&): quaternionbase_assign_impl
+    Quat q;
+    double t = m(0, 0) + m(1, 1) + m(2, 2);
+    if (t > 0) {
+        t = std::sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (m(2, 1) - m(1, 2)) * t, q.y = (m(0, 2) - m(2, 0)) * t, q.z = (m(1, 0) - m(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (m(1, 1) > m(0, 0)) i = 1;
+        if (m(2, 2) > m(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double c[3];
+        t = std::sqrt(m(i, i) - m(j, j) - m(k, k) + 1.0);
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (m(k, j) - m(j, k)) * t;
+        c[j] = (m(j, i) + m(i, j)) * t;
+        c[k] = (m(k, i) + m(i, k)) * t;
+        q.x = c[0], q.y = c[1], q.z = c[2];
+    }
+    return q;
+}
+void qnormalize_pos(Quat &q) {   // SE3Quat::normalizeRotation
+    if (q.w < 0) q.x = -q.x, q.y = -q.y, q.z = -q.z, q.w = -q.w;
+    const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x /= n, q.y /= n, q.z /= n, q.w /= n;
+}
+struct SE3Q {
+    Quat q;
+    V3 t;
+    V3 map(const V3 &X) const { return add(qrot(q, X), t); }
+};
+// VertexSE3Expmap::oplusImpl: SE3Quat::exp(dx) * T (rotation part dx[0..2], translation dx[3..5])
+SE3Q se3_oplus(const double *dx, const SE3Q &T) {
+    const V3 om{{dx[0], dx[1], dx[2]}}, up{{dx[3], dx[4], dx[5]}};
+    const double theta = std::sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    const M3 O = hat(om), I = eye();
+    M3 R, V;
+    if (theta < 0.00001) {
+        R = add(add(I, O), mul(O, O));
+        V = R;
+    } else {
+        const M3 O2 = mul(O, O);
+        R = add(add(I, scale(O, std::sin(theta) / theta)), scale(O2, (1 - std::cos(theta)) / (theta * theta)));
+        V = add(add(I, scale(O, (1 - std::cos(theta)) / (theta * theta))),
+                scale(O2, (theta - std::sin(theta)) / std::pow(theta, 3)));
+    }
+    SE3Q e{qfrom(R), mul(V, up)};
+    qnormalize_pos(e.q);
+    SE3Q r{qmul(e.q, T.q), add(e.t, qrot(e.q, T.t))};
+    qnormalize_pos(r.q);
+    return r;
+}
+
+struct PoseOnlyEdge {
+    int cam, kp;
+    bool stereo;
+    double obs[3];
+    double w;
+    V3 Xw;
+    bool active = true;
+    double chi2 = 0;   // e->chi2() of the last computeError
+};
+
+struct PoseOnlyProblem {
+    const float *cam;
+    const int32_t *model;
+    std::vector<SE3Q> rig;   // T_c0 (entry 0 unused)
+    std::vector<M3> rigR;    // T_c0.rotation().toRotationMatrix()
+    double fx, fy, cx, cy, bf;
+    std::vector<PoseOnlyEdge> E;   // creation order (keypoint order)
+    bool robust = true;
+    const double dmono = (double)(float)std::sqrt(5.991), dst = (double)(float)std::sqrt(7.815);
+
+    // computeError at pose T; returns chi2 and the residual
+    double error(const SE3Q &T, const PoseOnlyEdge &e, double r[3]) const {
+        const V3 Xl = T.map(e.Xw);
+        r[2] = 0;
+        if (e.stereo) {   // EdgeStereoSE3ProjectXYZOnlyPose::cam_project: float invz
+            const float invz = (float)(1.0f / Xl[2]);
+            const double u = Xl[0] * invz * fx + cx;
+            r[0] = e.obs[0] - u;
+            r[1] = e.obs[1] - (Xl[1] * invz * fy + cy);
+            r[2] = e.obs[2] - (u - bf * invz);
+            return r[0] * (e.w * r[0]) + r[1] * (e.w * r[1]) + r[2] * (e.w * r[2]);
+        }
+        const V3 Xc = e.cam ? rig[e.cam].map(Xl) : Xl;
+        double u, v;
+        cam_project(model, e.cam, cam + 8 * e.cam, Xc, u, v);
+        r[0] = e.obs[0] - u, r[1] = e.obs[1] - v;
+        return r[0] * (e.w * r[0]) + r[1] * (e.w * r[1]);
+    }
+    void jac(const SE3Q &T, const PoseOnlyEdge &e, double J[18]) const {
+        const V3 Xl = T.map(e.Xw);
+        if (e.stereo) {
+            const double x = Xl[0], y = Xl[1], invz = 1.0 / Xl[2], invz_2 = invz * invz;
+            J[0] = x * y * invz_2 * fx, J[1] = -(1 + (x * x * invz_2)) * fx, J[2] = y * invz * fx;
+            J[3] = -invz * fx, J[4] = 0, J[5] = x * invz_2 * fx;
+            J[6] = (1 + y * y * invz_2) * fy, J[7] = -x * y * invz_2 * fy, J[8] = -x * invz * fy;
+            J[9] = 0, J[10] = -invz * fy, J[11] = y * invz_2 * fy;
+            J[12] = J[0] - bf * y * invz_2, J[13] = J[1] + bf * x * invz_2, J[14] = J[2];
+            J[15] = J[3], J[16] = 0, J[17] = J[5] - bf * invz_2;
+            return;
+        }
+        const V3 Xc = e.cam ? rig[e.cam].map(Xl) : Xl;
+        double pj[6];
+        cam_jac(model, e.cam, cam + 8 * e.cam, Xc, pj);
+        double pr[6];   // -projectJac(Xc) * R_c0
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 3; ++q)
+                pr[3 * r + q] = e.cam ? (-pj[3 * r]) * rigR[e.cam](0, q) + (-pj[3 * r + 1]) * rigR[e.cam](1, q) +
+                                            (-pj[3 * r + 2]) * rigR[e.cam](2, q)
+                                      : -pj[3 * r + q];
+        const double x = Xl[0], y = Xl[1], z = Xl[2];
+        const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 6; ++q)
+                J[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    }
+    double rho0(const PoseOnlyEdge &e) const {   // the edge's term of activeRobustChi2
+        if (!robust) return e.chi2;
+        double rho[3];
+        const double d = e.stereo ? dst : dmono;
+        Solver::huber(e.chi2, d, d * d, rho);
+        return rho[0];
+    }
+    double compute_active_errors(const SE3Q &T) {
+        double chi = 0, r[3];
+        for (PoseOnlyEdge &e : E)
+            if (e.active) e.chi2 = error(T, e, r), chi += rho0(e);
+        return chi;
+    }
+    // buildSystem (base_unary_edge constructQuadraticForm): H = sum J^T (rho' Omega) J, b = sum J^T (-rho' Omega e)
+    void build(const SE3Q &T, double H[36], double b[6]) const {
+        std::fill(H, H + 36, 0.0), std::fill(b, b + 6, 0.0);
+        for (const PoseOnlyEdge &e : E) {
+            if (!e.active) continue;
+            double r[3], J[18], rho[3] = {0, 1, 0};
+            error(T, e, r);
+            jac(T, e, J);
+            const int nr = e.stereo ? 3 : 2;
+            if (robust) {
+                const double d = e.stereo ? dst : dmono;
+                Solver::huber(e.chi2, d, d * d, rho);
+            }
+            for (int i = 0; i < 6; ++i) {
+                double t = 0;
+                for (int k = 0; k < nr; ++k) t += J[6 * k + i] * (-e.w * r[k] * rho[1]);
+                b[i] += t;
+                for (int j = 0; j < 6; ++j) {
+                    double h = 0;
+                    for (int k = 0; k < nr; ++k) h += J[6 * k + i] * (rho[1] * e.w) * J[6 * k + j];
+                    H[6 * i + j] += h;
+                }
+            }
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+// One frame of the batch (host pointers in `b`): rig_q / rig_t [n_cams][4] (x y z w) / [3] = T_c0 (mTrl, mTsll, mTsrl;
+// entry 0 unused); pose_q / pose_t [4] / [3] in/out (frame f's Tcw); kp_outlier [kp_cap] (edge keypoints only).
+// Returns the reference's return value (nInitialCorrespondences - nBad, or 0 below 3 correspondences).
+int oracle_pose_optimization(const omv_pose_batch *b, const double *rig_q, const double *rig_t, int f, double *pose_q,
+                             double *pose_t, uint8_t *kp_outlier) {
+    PoseOnlyProblem P;
+    P.cam = b->cam, P.model = b->cam_model;
+    P.fx = b->cam[0], P.fy = b->cam[1], P.cx = b->cam[2], P.cy = b->cam[3], P.bf = b->bf;
+    P.rig.resize(b->n_cams), P.rigR.resize(b->n_cams);
+    for (int c = 0; c < b->n_cams; ++c) {
+        SE3Q T{Quat{rig_q[4 * c], rig_q[4 * c + 1], rig_q[4 * c + 2], rig_q[4 * c + 3]},
+               V3{{rig_t[3 * c], rig_t[3 * c + 1], rig_t[3 * c + 2]}}};
+        qnormalize_pos(T.q);   // SE3Quat(q, t) ctor
+        P.rig[c] = T, P.rigR[c] = qmat(T.q);
+    }
+    // creation order: keypoint order over the mono and stereo lists
+    std::vector<PoseOnlyEdge> E;
+    for (int e = b->mono_start[f]; e < b->mono_start[f + 1]; ++e) {
+        PoseOnlyEdge x;
+        x.cam = b->mono_cam[e], x.kp = b->mono_kp[e], x.stereo = false;
+        x.obs[0] = b->mono_obs[2 * e], x.obs[1] = b->mono_obs[2 * e + 1], x.obs[2] = 0;
+        x.w = (double)b->mono_inv_sigma2[e];
+        for (int q = 0; q < 3; ++q) x.Xw[q] = (double)b->mono_xw[3 * e + q];
+        E.push_back(x);
+    }
+    for (int e = b->stereo_start[f]; e < b->stereo_start[f + 1]; ++e) {
+        PoseOnlyEdge x;
+        x.cam = 0, x.kp = b->stereo_kp[e], x.stereo = true;
+        for (int q = 0; q < 3; ++q) x.obs[q] = b->stereo_obs[3 * e + q], x.Xw[q] = (double)b->stereo_xw[3 * e + q];
+        x.w = (double)b->stereo_inv_sigma2[e];
+        E.push_back(x);
+    }
+    std::stable_sort(E.begin(), E.end(), [](const PoseOnlyEdge &a, const PoseOnlyEdge &c) { return a.kp < c.kp; });
+    P.E = E;
+    const int n = (int)P.E.size();
+    for (const PoseOnlyEdge &e : P.E) kp_outlier[e.kp] = 0;
+    if (n < 3) return 0;
+    SE3Q T0{Quat{pose_q[0], pose_q[1], pose_q[2], pose_q[3]}, V3{{pose_t[0], pose_t[1], pose_t[2]}}};
+    qnormalize_pos(T0.q);
+    SE3Q T = T0;
+    int nBad = 0;
+    double x[6] = {0};   // the dense solver's x: kept when a factorisation is not positive
+    for (int round = 0; round < 4; ++round) {
+        T = T0;
+        int n_active = 0;
+        for (const PoseOnlyEdge &e : P.E) n_active += e.active ? 1 : 0;
+        if (n_active > 0) {   // initializeOptimization(0) found the vertex; otherwise optimize() returns -1
+            double lambda = 0, ni = 2;
+            int nb = 0;
+            for (int it = 0; it < 10; ++it) {
+                double currentChi = P.compute_active_errors(T);
+                const double iniChi = currentChi;
+                double H[36], g[6];
+                P.build(T, H, g);
+                if (it == 0) {
+                    double md = 0;
+                    for (int j = 0; j < 6; ++j) md = std::max(std::fabs(H[7 * j]), md);
+                    lambda = 1e-5 * md, ni = 2, nb = 0;
+                }
+                double rho = 0;
+                int qmax = 0;
+                do {
+                    std::vector<double> A(H, H + 36);
+                    for (int j = 0; j < 6; ++j) A[7 * j] += lambda;
+                    const bool ok = ldlt_pivot_solve(A, 6, g, x);
+                    const SE3Q Tt = se3_oplus(x, T);
+                    double tempChi = P.compute_active_errors(Tt);
+                    if (!ok) tempChi = std::numeric_limits<double>::max();
+                    double sc = 0;
+                    for (int j = 0; j < 6; ++j) sc += x[j] * (lambda * x[j] + g[j]);
+                    sc += 1e-3;
+                    rho = (currentChi - tempChi) / sc;
+                    if (rho > 0 && std::isfinite(tempChi)) {
+                        double alpha = 1. - std::pow((2 * rho - 1), 3);
+                        alpha = std::min(alpha, 2. / 3.);
+                        lambda *= std::max(1. / 3., alpha);
+                        ni = 2;
+                        currentChi = tempChi;
+                        T = Tt;
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;   // pop(): the pose restored, the edges keep the rejected trial's errors
+                    }
+                    qmax++;
+                } while (rho < 0 && qmax < 10);
+                if (qmax == 10 || rho == 0) break;
+                if ((iniChi - currentChi) * 1e3 < iniChi) nb++;
+                else nb = 0;
+                if (nb >= 3) break;
+            }
+        }
+        nBad = 0;
+        for (int pass = 0; pass < 2; ++pass)   // mono loops (:1145-1239), then the stereo loop (:1241-1263)
+            for (PoseOnlyEdge &e : P.E) {
+                if (e.stereo != (pass == 1)) continue;
+                if (kp_outlier[e.kp]) {
+                    double r[3];
+                    e.chi2 = P.error(T, e, r);
+                }
+                const float chi2 = (float)e.chi2;
+                const bool out = chi2 > (e.stereo ? 7.815f : 5.991f);
+                kp_outlier[e.kp] = out ? 1 : 0;
+                e.active = !out;
+                nBad += out ? 1 : 0;
+            }
+        if (round == 2) P.robust = false;
+        if (n < 10) break;
+    }
+    pose_q[0] = T.q.x, pose_q[1] = T.q.y, pose_q[2] = T.q.z, pose_q[3] = T.q.w;
+    pose_t[0] = T.t[0], pose_t[1] = T.t[1], pose_t[2] = T.t[2];
+    return n - nBad;
+}
+
+}  // extern "C"

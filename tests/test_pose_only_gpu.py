@@ -1,0 +1,100 @@
+"""GPU parity of Optimizer::PoseOptimization (openmavis_amd/csrc/pose.hip pose_only_kernel, src/Optimizer.cc:855-1278)
+against the CPU oracle (oracle/ba_oracle.cpp oracle_pose_optimization).
+
+Bar (floating point, north star 1e-5 relative): the optimised Tcw within 1e-7 of the oracle's (quaternion coefficients
+and translation in m: both restate the same Levenberg-Marquardt with the same per-edge arithmetic; the order of the
+normal-equation sums and the device's FMA-contracted LDLT differ), Frame::mvbOutlier and the return value identical (no
+edge's chi2 sits within 1e-4 of its threshold on these seeds), and the kernel bitwise deterministic run to run.
+"""
+import numpy as np
+import pytest
+
+from openmavis_amd import synth_pose
+from openmavis_amd.optimizer import PoseInertialOptimizer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import oracle as o
+    return o
+
+
+def _run_gpu(b):
+    import torch
+    dev = "cuda:0"
+    arrays = {k: torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in PoseInertialOptimizer.EDGE_KEYS}
+    F, cap = int(b["n_frames"]), int(b["kp_cap"])
+    kpo = torch.full((F, cap), 255, dtype=torch.uint8, device=dev)
+    q = torch.tensor(np.asarray(b["pose_q"], np.float64), device=dev).contiguous()
+    t = torch.tensor(np.asarray(b["pose_t"], np.float64), device=dev).contiguous()
+    opt = PoseInertialOptimizer(max_frames=F, max_edges=max(len(b["mono_cam"]), len(b["stereo_cam"]), 1))
+    n_good = opt.PoseOptimization(b, arrays, q, t, kpo)
+    torch.cuda.synchronize()
+    return q.cpu().numpy(), t.cpu().numpy(), kpo.cpu().numpy(), n_good.cpu().numpy()
+
+
+def _check(b, ref, got):
+    rq, rt, rk, rn = ref
+    gq, gt, gk, gn = got
+    assert np.array_equal(gn, rn)
+    for f in range(int(b["n_frames"])):
+        kps = np.concatenate([b["mono_kp"][b["mono_start"][f]:b["mono_start"][f + 1]],
+                              b["stereo_kp"][b["stereo_start"][f]:b["stereo_start"][f + 1]]])
+        assert np.array_equal(gk[f][kps], rk[f][kps]), f
+    np.testing.assert_allclose(gq, rq, rtol=0, atol=1e-7)
+    np.testing.assert_allclose(gt, rt, rtol=0, atol=1e-7)
+
+
+CASES = {
+    "rig4_kb8": dict(n_cams=4, n_pts=300),
+    "rig2_kb8_heavy_outliers": dict(n_cams=2, n_pts=200, outlier_frac=0.4),
+    "pinhole_stereo": dict(n_cams=1, n_pts=300, stereo_frac=0.5),
+    "pinhole_mono": dict(n_cams=1, n_pts=250),
+    "large_start_error": dict(n_cams=4, n_pts=300, rot_noise_deg=2.0, trans_noise=0.15),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_pose_optimization_matches_oracle(oracle, name):
+    b = synth_pose.make_pose_only_batch(n_frames=6, seed=31, **CASES[name])
+    ref = oracle.pose_optimization(b)
+    got = _run_gpu(b)
+    _check(b, ref, got)
+    # the estimate moved towards the truth and most injected outliers are flagged
+    assert (got[3] > 0).all()
+
+
+def test_pose_optimization_few_edges(oracle):
+    """Below 10 edges the reference stops after the first round; below 3 it returns 0 with the pose untouched."""
+    for n_pts in (2, 5, 9, 12):
+        b = synth_pose.make_pose_only_batch(n_frames=3, n_pts=n_pts, seed=7 + n_pts, n_cams=4, outlier_frac=0.2)
+        ref = oracle.pose_optimization(b)
+        got = _run_gpu(b)
+        _check(b, ref, got)
+        if n_pts < 3:
+            assert (got[3] == 0).all()
+            np.testing.assert_array_equal(got[0], b["pose_q"])
+
+
+def test_pose_optimization_batch_and_determinism(oracle):
+    """A 256-frame batch (one workgroup per frame): sampled frames against the oracle, the whole batch bitwise equal
+    run to run."""
+    b0 = synth_pose.make_pose_only_batch(n_frames=8, n_pts=400, seed=5, n_cams=4)
+    b = synth_pose.tile_batch(b0, 256)
+    b["pose_q"] = np.ascontiguousarray(np.asarray(b0["pose_q"])[[f % 8 for f in range(256)]])
+    b["pose_t"] = np.ascontiguousarray(np.asarray(b0["pose_t"])[[f % 8 for f in range(256)]])
+    g1 = _run_gpu(b)
+    g2 = _run_gpu(b)
+    for x, y in zip(g1, g2):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    ref = oracle.pose_optimization(b0)
+    for f in range(8):
+        for ff in (f, f + 8 * 17, f + 8 * 31):
+            np.testing.assert_allclose(g1[0][ff], ref[0][f], rtol=0, atol=1e-7)
+            np.testing.assert_allclose(g1[1][ff], ref[1][f], rtol=0, atol=1e-7)
+            assert g1[3][ff] == ref[3][f]
