@@ -432,18 +432,32 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
         "dtype": "f64",
         "roofline": {"kernel": "whole LM trial", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": lba_traffic(), "algorithmic_bytes_per_trial": bpt,
-                     "traffic_source": "profiles/pmc_lba_trial.json (FETCH_SIZE / WRITE_SIZE passes over tools/lba_time.py)"},
+                     "traffic": lba_traffic()[0], "algorithmic_bytes_per_trial": bpt,
+                     "traffic_source": lba_traffic()[1]},
     }
 
 
+def newest_profile(name):
+    """(path, record) of the newest round-tagged profiles/<tag>_<name>.json (tags r01 < r01b < ... < r05g sort as
+    strings), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]*_{name}.json")),
+                   key=lambda f: os.path.basename(f)[:-len(name) - 6])
+    for f in reversed(files):
+        try:
+            return os.path.relpath(f, ROOT), json.load(open(f))
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
 def lba_traffic():
-    """HBM bytes per LM trial from the last profile's PMC passes (profiles/pmc_lba_trial.json), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_lba_trial.json")
+    """(HBM bytes per LM trial, source) from the newest profile's PMC passes (profiles/<tag>_pmc_lba_trial.json)."""
+    path, r = newest_profile("pmc_lba_trial")
     try:
-        return int(json.load(open(p))["hbm_bytes_per_trial"])
-    except (OSError, ValueError, KeyError):
-        return None
+        return int(r["hbm_bytes_per_trial"]), f"{path} ({r['tag']}: FETCH_SIZE / WRITE_SIZE passes over {r.get('program', 'lba')})"
+    except (TypeError, ValueError, KeyError):
+        return None, None
 
 
 def pose_leg(batch, cpu_batch, reps, dev, last_frame=False):
@@ -567,7 +581,8 @@ def _cpu_rate(fn, units, budget=1.5):
 def aux_legs(dev, cpu):
     """The SURVEY §8f rows beside the two headline metrics, each on a batch already in HBM with its CPU oracle
     timed on a bounded sample: ORBmatcher::Fuse (LocalMapping::SearchInNeighbors scale), DBoW2 transform
-    (ComputeBoW of whole multi-camera frames) and IMU preintegration (PreintegrateIMU records)."""
+    (ComputeBoW of whole multi-camera frames), IMU preintegration (PreintegrateIMU records), the SearchByBoW /
+    SearchForInitialization / SearchBySim3 matchers, the map-point refresh, CreateNewMapPoints and PoseOptimization."""
     import torch
     from openmavis_amd import synth_bow, synth_imu, synth_kfmatch
     from openmavis_amd.bow import ORBVocabulary
@@ -731,6 +746,69 @@ def aux_legs(dev, cpu):
         out["search_by_sim3"]["cpu_baseline"] = {
             "value": round(done / t, 1), "unit": "keyframe pairs/s", "cores": 1, "kind": "port",
             "sample": f"{done} pair searches (grid build included), oracle, 1 thread, {t:.2f} s"}
+    # ---- map-point refresh: ComputeDistinctiveDescriptors + UpdateNormalAndDepth over 20,000 map points
+    from openmavis_amd import mappoint, synth_mappoint
+    mp = synth_mappoint.make_points(n_points=20000, seed=3)
+    mg = synth_mappoint.make_geometry(n_points=20000, seed=4)
+    md = {k: torch.from_numpy(np.ascontiguousarray(mp[k])).to(dev) for k in ("desc", "desc_start", "desc_row")}
+    mgd = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in mg.items()}
+    dt = _timed(lambda: mappoint.ComputeDistinctiveDescriptors(md["desc"], md["desc_start"], md["desc_row"]), 10, dev)
+    dn = _timed(lambda: mappoint.UpdateNormalAndDepth(**mgd), 10, dev)
+    out["mappoint_refresh"] = {"metric": "MapPoint::ComputeDistinctiveDescriptors + UpdateNormalAndDepth map points/s",
+                               "value": round(20000 / (dt + dn), 1), "unit": "points/s",
+                               "ms_distinctive": round(dt * 1e3, 3), "ms_normal_depth": round(dn * 1e3, 3),
+                               "points_per_batch": 20000,
+                               "descriptors_per_point": round(float(mp["desc_start"][-1]) / 20000, 2)}
+    if cpu:
+        sub = synth_mappoint.make_points(n_points=2000, seed=3)
+        done, t = _cpu_rate(lambda: oracle.distinctive_descriptors(sub["desc"], sub["desc_start"], sub["desc_row"]),
+                            2000)
+        out["mappoint_refresh"]["cpu_baseline"] = {
+            "value": round(done / t, 1), "unit": "points/s (distinctive descriptors only)", "cores": 1, "kind": "port",
+            "sample": f"{done} points, oracle, 1 thread, {t:.2f} s"}
+    # ---- LocalMapping::CreateNewMapPoints: one keyframe against 20 neighbours (~1,200 SearchForTriangulation pairs each)
+    from openmavis_amd import synth_cnmp
+    from openmavis_amd.mapping import CnmpCall
+    cd = synth_cnmp.make_cnmp(seed=21, n_neigh=20, multi=True)
+    cc = CnmpCall(cd, inertial=True, device=dev)
+    dt = _timed(lambda: cc.run(), 10, dev)
+    n_pairs = int(sum((np.asarray(j["match12"]) >= 0).sum() for j in cd["jobs"]))
+    out["create_new_map_points"] = {"metric": "LocalMapping::CreateNewMapPoints keyframes/s (20 neighbours)",
+                                    "value": round(1 / dt, 1), "unit": "keyframes/s", "ms_per_keyframe": round(dt * 1e3, 3),
+                                    "neighbours": len(cd["jobs"]), "matched_pairs": n_pairs}
+    if cpu:
+        done, t = _cpu_rate(lambda: oracle.create_new_map_points(cd, inertial=True), 1)
+        out["create_new_map_points"]["cpu_baseline"] = {
+            "value": round(done / t, 2), "unit": "keyframes/s", "cores": 1, "kind": "port",
+            "sample": f"{done} keyframes x 20 neighbours, oracle, 1 thread, {t:.2f} s"}
+    # ---- Optimizer::PoseOptimization: 256 frames of the 4-camera rig (~400 edges each), and one frame (latency)
+    from openmavis_amd import synth_pose
+    from openmavis_amd.optimizer import PoseInertialOptimizer
+    pb0 = synth_pose.make_pose_only_batch(n_frames=16, n_pts=400, seed=9, n_cams=4)
+    for F in (256, 1):
+        pb = synth_pose.tile_batch(pb0, F)
+        sel = [f % 16 for f in range(F)]
+        q0 = torch.tensor(np.asarray(pb0["pose_q"])[sel], dtype=torch.float64, device=dev)
+        t0 = torch.tensor(np.asarray(pb0["pose_t"])[sel], dtype=torch.float64, device=dev)
+        pb["rig_q"], pb["rig_t"] = pb0["rig_q"], pb0["rig_t"]
+        q, t = q0.clone(), t0.clone()
+        arr = {k: torch.from_numpy(np.ascontiguousarray(pb[k])).to(dev) for k in PoseInertialOptimizer.EDGE_KEYS}
+        kpo = torch.zeros((F, int(pb["kp_cap"])), dtype=torch.uint8, device=dev)
+        po = PoseInertialOptimizer(max_frames=F, max_edges=max(len(pb["mono_cam"]), 1))
+
+        def run_po():
+            q.copy_(q0)
+            t.copy_(t0)
+            return po.PoseOptimization(pb, arr, q, t, kpo)
+        dt = _timed(run_po, 10, dev)
+        key = "pose_optimization" if F > 1 else "pose_optimization_b1"
+        out[key] = {"metric": f"Optimizer::PoseOptimization frames/s (batch {F})", "value": round(F / dt, 1),
+                    "unit": "frames/s", "ms_per_batch": round(dt * 1e3, 3), "frames_per_batch": F,
+                    "edges_per_frame": round(len(pb["mono_cam"]) / F, 1)}
+    if cpu:
+        done, t = _cpu_rate(lambda: oracle.pose_optimization(pb0, frames=range(4)), 4)
+        out["pose_optimization"]["cpu_baseline"] = {"value": round(done / t, 1), "unit": "frames/s", "cores": 1,
+                                                    "kind": "port", "sample": f"{done} frames, oracle, 1 thread, {t:.2f} s"}
     return out
 
 
@@ -756,18 +834,14 @@ BYTES_FORMULA = {
 def rocprof_launch_avg(kernel):
     """Dispatch-trace average of `kernel` at its most-used grid in the newest committed
     profiles/<tag>_kernel_grid.json (tools/summarize_profile.py); None if absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_kernel_grid.json")))
-    if not files:
-        return None
+    path, r = newest_profile("kernel_grid")
     try:
-        r = json.load(open(files[-1]))
         rows = [x for x in r["rows"] if x["kernel"] == kernel]
         if not rows:
             return None
         best = max(rows, key=lambda x: x["total_us"])
         return {"avg_launch_ms": round(best["avg_us"] / 1e3, 4), "avg_us": best["avg_us"], "grid": best["grid"],
-                "calls": best["calls"], "source": os.path.relpath(files[-1], ROOT)}
+                "calls": best["calls"], "source": path, "tag": r.get("tag")}
     except Exception:
         return None
 
@@ -1451,16 +1525,15 @@ def main():
                 ach = alg / (t * 1e-3) / 1e9
                 rec[view] = {"avg_launch_ms": round(t, 4), "ms_per_step": round(t * G, 4), "achieved": round(ach, 2),
                              "frac": round(ach / HBM_PEAK_GBS, 5)}
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{k}.json")
-        if os.path.exists(pmc):   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch
+        pmc, r = newest_profile(f"pmc_{k}")
+        if r is not None:   # PMC HBM bytes (tools/profile_gpu.sh), scaled to this launch
             try:
-                r = json.load(open(pmc))
                 if "hbm_bytes_per_image" in r:
                     rec["traffic"] = int(r["hbm_bytes_per_image"] * Bg * C)
                 elif "hbm_bytes_per_frame" in r:
                     rec["traffic"] = int(r["hbm_bytes_per_frame"] * Bg)
                 if rec["traffic"] is not None:
-                    rec["traffic_source"] = f"profiles/pmc_{k}.json ({r['tag']}, program {r.get('program', 'orb')})"
+                    rec["traffic_source"] = f"{pmc} ({r['tag']}, program {r.get('program', 'orb')})"
                     rec["traffic_ratio"] = round(rec["traffic"] / alg, 3)
             except Exception:
                 pass
@@ -1493,8 +1566,7 @@ def main():
             roof["dominant_isolated_view"] = d["isolated"]
         # PMC-measured extraction bytes per image vs SURVEY §8(d)'s 2,085,018 B per image
         ext = ("pyr_resize", "fast_cells", "octree", "describe")
-        pm = [json.load(open(os.path.join(ROOT, "profiles", f"pmc_{k}.json")))
-              for k in ext if os.path.exists(os.path.join(ROOT, "profiles", f"pmc_{k}.json"))]
+        pm = [r for r in (newest_profile(f"pmc_{k}")[1] for k in ext) if r is not None]
         per_img = sum(r.get("hbm_bytes_per_image", 0) for r in pm)
         if per_img:
             ref_img = cam_bytes(W, H, n_kp_step / (B * C))

@@ -1,5 +1,7 @@
 """Per-kernel HBM bytes of one tools/quick_lba.sh PMC pair (FETCH_SIZE doubled for gfx950, KB x 1024), per launch and
-per LM trial: python tools/pmc_lba_summary.py gpurun_out/prof_<tag> [trials_per_run]"""
+per LM trial: python tools/pmc_lba_summary.py gpurun_out/prof_<tag> [trials_per_run]
+Writes <src>/pmc_lba_trial.json (bench.py reads it once copied to profiles/<tag>_pmc_lba_trial.json)."""
+import os
 import csv
 import json
 import sys
@@ -26,6 +28,9 @@ for k, n, b in rows:
     print(f"{k:40s} launches {n:4d}  {b / max(n, 1) / 1e6:8.3f} MB/launch  {b / n_trials / 1e6:8.3f} MB/trial")
     tot += b
 print(f"total {tot / n_trials / 1e6:.2f} MB per trial over {n_trials} trials")
-json.dump({"hbm_bytes_per_trial": int(tot / n_trials), "trials": n_trials,
+tag = os.path.basename(os.path.normpath(src)).replace("prof_", "")
+json.dump({"kernel": "lba_trial", "tag": tag, "program": "tools/quick_lba.sh (tools/lba_time.py under --pmc)",
+           "hbm_bytes_per_trial": int(tot / n_trials), "trials": n_trials,
+           "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024, summed over every kernel of the run, per LM trial",
            "per_kernel_mb_per_trial": {k: round(b / n_trials / 1e6, 3) for k, n, b in rows}},
           open(f"{src}/pmc_lba_trial.json", "w"), indent=1)

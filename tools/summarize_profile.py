@@ -1,7 +1,7 @@
 """Summarise a tools/profile_gpu.sh run into profiles/<tag>_*.
 
 - <tag>_kernel_stats.md : rocprofv3 --kernel-trace --stats table (calls, total/avg ns, share)
-- pmc_<kernel>.json     : HBM traffic per launch from the separate FETCH_SIZE / WRITE_SIZE passes,
+- <tag>_pmc_<kernel>.json : HBM traffic per launch from the separate FETCH_SIZE / WRITE_SIZE passes,
                           corrected per /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
                           WRITE_SIZE are KB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, so
                           the read side is doubled (calibrated for wide coalesced streams only; our
@@ -96,7 +96,7 @@ def main(src, tag, command=None):
                    f"{unit}_per_launch": n, "launches_per_pass": lpp,
                    f"hbm_bytes_per_{unit[:-1]}": round(b * lpp / n),
                    "per_unit_note": f"all launches of one pass (one batched call over {n} {unit}) summed, / {n}"}
-            out = os.path.join(prof, f"pmc_{k}.json")
+            out = os.path.join(prof, f"{tag}_pmc_{k}.json")
             if srcname == "match" and os.path.exists(out) and json.load(open(out)).get("program") == "orb":
                 continue   # extraction kernels keep the extraction-only program's numbers
             json.dump(rec, open(out, "w"), indent=1)
@@ -113,7 +113,7 @@ def main(src, tag, command=None):
         rec = {"kernel": "lba_trial", "tag": tag, "program": "lba", "trials": trials, "hbm_bytes_per_trial": round(tot / trials),
                "kernels": sorted(k for k, _ in lba), "correction": "2*FETCH_SIZE + WRITE_SIZE, KB*1024, summed over the "
                "LocalInertialBA kernels of tools/lba_time.py (set-up uploads excluded), per LM trial"}
-        json.dump(rec, open(os.path.join(prof, "pmc_lba_trial.json"), "w"), indent=1)
+        json.dump(rec, open(os.path.join(prof, f"{tag}_pmc_lba_trial.json"), "w"), indent=1)
         lines += ["", f"LocalInertialBA per LM trial: {rec['hbm_bytes_per_trial']} B of HBM traffic ({trials} trials)"]
     open(os.path.join(prof, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
