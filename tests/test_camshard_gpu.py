@@ -52,6 +52,15 @@ def test_camera_shard_rccl_one_rank(oracle, torch_cuda, tmp_path):
     _check_against_batched(g, oracle, torch_cuda)
 
 
+def test_camera_shard_five_ranks_one_camera_each(oracle, torch_cuda, tmp_path):
+    """configs[2]'s layout: five ranks, one camera of the Hilti rig each (rank r extracts camera r with the HIP
+    extractor on its GPU — all five share this box's card, gloo stages the slabs through host memory), one all-gather,
+    rank 0 matches the gathered frame: identical to the single-GPU batched path bit for bit, and that to the oracle."""
+    g = _run_ranks(tmp_path, "gloo", world=5)
+    assert int(g["world"]) == 5
+    _check_against_batched(g, oracle, torch_cuda)
+
+
 def _check_against_batched(g, oracle, torch):
     # the single-GPU batched path on the same frames
     imgs = np.concatenate([synth.hilti_frame(f) for f in range(F)])

@@ -214,9 +214,9 @@ def test_optimize_with_heavy_landmark(small, oracle):
         _compare_state(prob, sg, so, oracle)
 
 
-def test_optimize_full_window(full, oracle):
+def test_optimize_full_window(full, full_oracle, oracle):
     """The bench configuration: 25 optimisable + 25 fixed keyframes, 5 cameras, 20k points, 120k edges."""
-    ro, so, _ = oracle.lba_optimize(full, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    ro, so = full_oracle
     ba = _solver(full).set_problem(full)
     rg, sg = ba.optimize(opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
     _compare_result(full, rg, ro)
@@ -296,38 +296,28 @@ def test_bitwise_identical_run_to_run(full, driver):
             assert np.array_equal(np.asarray(s[k]).view(np.uint64), np.asarray(s0[k]).view(np.uint64)), k
 
 
-@pytest.mark.parametrize("backend,driver,world", [("gloo", "device", 2), ("gloo", "host", 2), ("gloo", "device", 4),
-                                                  ("nccl", "device", 1), ("nccl", "device", 2)])
-def test_landmark_sharded_ranks(oracle, tmp_path, backend, driver, world):
-    """SURVEY §8e: landmarks sharded over `world` ranks, one all-reduce of the partial Schur system and one of the LM
-    scalars per step.  gloo: the ranks share this box's GPU, collectives through host memory (2 and 4 ranks).  nccl:
-    RCCL on the handle's device buffer in place (LbaAllReduce "device") -- one rank on a one-GPU box runs the same
-    call sequence, more ranks need as many GPUs.  The merged outcome meets the same bar against the oracle, and every
-    rank holds the identical keyframe state (asserted inside the worker).  The device LM driver waits on the host
-    once per batch of steps, never per trial (omv_lba_host_syncs)."""
+def _run_shard(tmp_path, backend, driver, world, n_kf, n_opt, n_pts, seed):
     import os
     import socket
     import subprocess
     import sys
-    import torch
-    if backend == "nccl" and torch.cuda.device_count() < world:
-        pytest.skip(f"RCCL over {world} ranks needs {world} visible GPUs (one rank and the gloo cases run on one)")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = tmp_path / f"shard_{backend}.npz"
+    out = tmp_path / f"shard_{backend}_{world}.npz"
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tools", "lba_shard_run.py"),
-           "--out", str(out), "--backend", backend, "--n-kf", "20", "--n-opt", "10", "--n-pts", "3000",
-           "--host-driver", "1" if driver == "host" else "0"]
+           "--out", str(out), "--backend", backend, "--n-kf", str(n_kf), "--n-opt", str(n_opt), "--n-pts", str(n_pts),
+           "--seed", str(seed), "--host-driver", "1" if driver == "host" else "0"]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
-    g = dict(np.load(out))
-    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=3000, seed=11)
+    return dict(np.load(out))
+
+
+def _check_shard(g, prob, ro, so, oracle, world, driver):
     assert int(g["world"]) == world and (g["owner"] >= 0).all() and len(set(g["owner"].tolist())) == world
-    ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
     rg = {k: (g[k].item() if g[k].ndim == 0 else g[k]) for k in
           ("err", "err_end", "status", "iterations", "trials", "mono_chi2", "mono_outlier")}
     _compare_result(prob, rg, ro)
@@ -338,3 +328,37 @@ def test_landmark_sharded_ranks(oracle, tmp_path, backend, driver, world):
         assert syncs <= (trials + 3) // 4 + 1 and (trials < 2 or syncs < trials), (syncs, trials)
     else:
         assert syncs >= trials, (syncs, trials)
+
+
+@pytest.mark.parametrize("backend,driver,world", [("gloo", "device", 2), ("gloo", "host", 2), ("gloo", "device", 4),
+                                                  ("nccl", "device", 1), ("nccl", "device", 2)])
+def test_landmark_sharded_ranks(oracle, tmp_path, backend, driver, world):
+    """SURVEY §8e: landmarks sharded over `world` ranks, one all-reduce of the partial Schur system and one of the LM
+    scalars per step.  gloo: the ranks share this box's GPU, collectives through host memory (2 and 4 ranks).  nccl:
+    RCCL on the handle's device buffer in place (LbaAllReduce "device") -- one rank on a one-GPU box runs the same
+    call sequence, more ranks need as many GPUs.  The merged outcome meets the same bar against the oracle, and every
+    rank holds the identical keyframe state (asserted inside the worker).  The device LM driver waits on the host
+    once per batch of steps, never per trial (omv_lba_host_syncs)."""
+    import torch
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        pytest.skip(f"RCCL over {world} ranks needs {world} visible GPUs (one rank and the gloo cases run on one)")
+    g = _run_shard(tmp_path, backend, driver, world, 20, 10, 3000, 11)
+    prob = synth_ba.make_lba_problem(n_kf=20, n_opt=10, n_pts=3000, seed=11)
+    ro, so, _ = oracle.lba_optimize(prob, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    _check_shard(g, prob, ro, so, oracle, world, driver)
+
+
+@pytest.fixture(scope="module")
+def full_oracle(full, oracle):
+    ro, so, _ = oracle.lba_optimize(full, opt_it=4, lambda_init=1e-2, max_trials=10, large=True)
+    return ro, so
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_landmark_sharded_config5_window(oracle, full, full_oracle, tmp_path, world):
+    """The sharded path at the bench's size: configs[4]'s window (50 keyframes, 25 optimisable, 5 cameras, 20k points,
+    120k edges) split over 2 and 4 gloo ranks sharing this box's GPU, against the oracle's unsharded solve at the same
+    bar, with the device driver's host-sync bound (once per batch of steps) asserted."""
+    g = _run_shard(tmp_path, "gloo", "device", world, 50, 25, 20000, 5)
+    ro, so = full_oracle
+    _check_shard(g, full, ro, so, oracle, world, "device")
