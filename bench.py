@@ -400,7 +400,7 @@ def lba_leg(prob, steps, warmup, dev, world, shard=False):
     for _ in range(steps):
         ba.reset()
         t0 = time.perf_counter()
-        res, _ = ba.optimize(**LBA_CFG, chi2=False)
+        res, _ = ba.optimize(**LBA_CFG, chi2=False, state_copy=False)   # state written back into the problem arrays
         total += time.perf_counter() - t0
         trials += res["trials"]
     torch.cuda.synchronize(dev)

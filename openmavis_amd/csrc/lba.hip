@@ -1024,21 +1024,41 @@ __device__ __forceinline__ double run_sum(const double *base, int n, int stride,
 // Hpl Dinv Hpl^T over one group's edges / landmarks), the inertial edges touching it, + lambda on the diagonal; on a
 // diagonal block the keyframe's b and Schur right-hand side from its run of [gradient | Schur rhs] records.
 // `pose_lambda` is 0 on the ranks > 0 of a sharded solve (lambda enters once).
+// The record runs are long (a block's records come from every landmark group touching it): each of the 36 entries'
+// runs (and, on a diagonal block, the 12 right-hand-side runs) is cut into kAsmSplit fixed contiguous pieces summed by
+// separate threads, the pieces then added in piece order -- a fixed order, so the result is the same run to run.
+constexpr int kAsmSplit = 7;
 __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat P, const double *rec,
                                                        const double *rec_rhs, double lambda, int pose_lambda, double *S,
                                                        double *bvec, double *coef, const LmCtl *ctl) {
     if (!gate_open(ctl, kGateTrial)) return;
+    __shared__ double part[kAsmSplit][36], rpart[kAsmSplit][12];
     lambda = lm_lambda(ctl, lambda);
     const int t = blockIdx.x, tid = threadIdx.x;
     const int kr = P.slot_kr[t], kc = P.slot_kc[t];
     const bool diag = kr == kc;
+    if (tid < 36 * kAsmSplit) {
+        const int pair = tid % 36, piece = tid / 36;
+        const int g0 = G.blk_start[t], n = G.blk_start[t + 1] - g0, chunk = (n + kAsmSplit - 1) / kAsmSplit;
+        const int q0 = min(n, piece * chunk), q1 = min(n, q0 + chunk);
+        const bool need = !diag || (pair % 6) <= (pair / 6);
+        part[piece][pair] = need ? run_sum(rec + (size_t)(g0 + q0) * 36, q1 - q0, 36, pair) : 0.0;
+    }
+    if (diag) {   // (block-uniform) the right-hand-side pieces on threads 0..83 once their record pieces are done
+        __syncthreads();
+        if (tid < 12 * kAsmSplit) {
+            const int col = tid % 12, piece = tid / 12;
+            const int k0 = G.rhs_start[kr], n = G.rhs_start[kr + 1] - k0, chunk = (n + kAsmSplit - 1) / kAsmSplit;
+            const int q0 = min(n, piece * chunk), q1 = min(n, q0 + chunk);
+            rpart[piece][col] = run_sum(rec_rhs + (size_t)(k0 + q0) * 12, q1 - q0, 12, col);
+        }
+    }
+    __syncthreads();
     const int r = tid >> 4, c = tid & 15;
     double v = 0;
     if (!diag || c <= r) {
-        if (r < 6 && c < 6) {
-            const int g0 = G.blk_start[t];
-            v = run_sum(rec + (size_t)g0 * 36, G.blk_start[t + 1] - g0, 36, 6 * r + c);
-        }
+        if (r < 6 && c < 6)
+            for (int piece = 0; piece < kAsmSplit; ++piece) v += part[piece][6 * r + c];
         if (r < 15 && c < 15) {   // inertial edges touching the block (variable groups present in the system)
             const bool rows_ok = r < 6 || I.offV[kr] >= 0, cols_ok = c < 6 || I.offV[kc] >= 0;
             if (rows_ok && cols_ok)
@@ -1052,11 +1072,8 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
     S[(size_t)t * 256 + sw16(r, c)] = v;
     if (diag && tid < 16) {   // b and the Schur right-hand side of keyframe kr
         double bv = 0, cf = 0;
-        if (tid < 6) {
-            const int k0 = G.rhs_start[kr], n = G.rhs_start[kr + 1] - k0;
-            bv = run_sum(rec_rhs + (size_t)k0 * 12, n, 12, tid);
-            cf = run_sum(rec_rhs + (size_t)k0 * 12, n, 12, 6 + tid);
-        }
+        if (tid < 6)
+            for (int piece = 0; piece < kAsmSplit; ++piece) bv += rpart[piece][tid], cf += rpart[piece][6 + tid];
         if (tid < 15 && (tid < 6 || I.offV[kr] >= 0))
             for (int q = G.iv_start[kr]; q < G.iv_start[kr + 1]; ++q) {
                 const int2 e = G.imu_vec[q];

@@ -2197,7 +2197,7 @@ __device__ __forceinline__ PoseOnlyEdge po_edge(const PoseOnlyArgs &A, int m0, i
     return v;
 }
 // computeError at (q, t): residual r, chi2 returned; Xl = T Xw (camera 0), Xc = T_c0 Xl
-__device__ __forceinline__ double po_error(const PoseOnlyRig &P, const double *q, const double *t, const PoseOnlyEdge &v,
+__device__ __forceinline__ double po_error(const PoseOnlyRig P, const double *q, const double *t, const PoseOnlyEdge &v,
                                            double *r, double *Xl, double *Xc) {
     q_rot(q, v.X, Xl);
     for (int i = 0; i < 3; ++i) Xl[i] += t[i];
@@ -2223,7 +2223,7 @@ __device__ __forceinline__ double po_error(const PoseOnlyRig &P, const double *q
     return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]);
 }
 // linearizeOplus: -projectJac(Xc) R_c0 SE3deriv(Xl) (mono) / the explicit stereo Jacobian
-__device__ __forceinline__ void po_jac(const PoseOnlyRig &P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
+__device__ __forceinline__ void po_jac(const PoseOnlyRig P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
                                        double *J) {
     if (v.stereo) {
         const double x = Xl[0], y = Xl[1], invz = 1.0 / Xl[2], invz_2 = invz * invz;

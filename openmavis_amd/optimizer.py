@@ -73,8 +73,11 @@ class LocalInertialBA:
         self._s, self._keep = s, keep
         return self
 
-    def optimize(self, opt_it=10, lambda_init=1e0, max_trials=10, large=False, chi2=True):
-        """chi2=False: only the outlier flags (what the reference's culling uses), no per-edge chi2 read-back."""
+    def optimize(self, opt_it=10, lambda_init=1e0, max_trials=10, large=False, chi2=True, state_copy=True):
+        """chi2=False: only the outlier flags (what the reference's culling uses), no per-edge chi2 read-back.
+        The optimised state is written back into the problem's host arrays (as the reference writes its keyframes and
+        map points); state_copy=False returns those arrays themselves instead of copies (the next optimize() of this
+        problem overwrites them)."""
         if self._s is None:
             raise _lib.OmvError("LocalInertialBA.optimize: no problem set")
         o = _lib.LbaOpts(int(opt_it), float(lambda_init), int(max_trials), int(bool(large)))
@@ -91,6 +94,8 @@ class LocalInertialBA:
                    "omv_lba_optimize")
         res = dict(err=r.err, err_end=r.err_end, status=r.status, iterations=r.iterations, trials=r.trials,
                    lambda_=r.lambda_, mono_chi2=chi2, mono_outlier=outl, stereo_chi2=s_chi2, stereo_outlier=s_outl)
+        if not state_copy:
+            return res, {k: self._keep[k] for k in ("Rwb", "twb", "Rcw", "tcw", "vel", "bg", "ba", "pts")}
         return res, read_state(self._keep)
 
     def reset(self):
