@@ -545,7 +545,8 @@ omv_status omv_matcher_search_by_bow(omv_matcher *m, int n_jobs, const omv_bow_j
     const dim3 cg((max_n + 255) / 256, n_jobs);
     // short-list entries the walk uses (test knob OMV_BOW_TOP: fewer make the node rescans run on small inputs)
     int lim = top;
-    if (const char *e = getenv("OMV_BOW_TOP")) lim = std::max(2, std::min(top, atoi(e)));
+    const omv::MatcherKnobs kn = omv::matcher_knobs(m);
+    if (kn.bow_top >= 0) lim = std::max(2, std::min(top, kn.bow_top));
     if (mode == OMV_BOW_KF_FRAME) {
         bow_cand_kernel<OMV_BOW_KF_FRAME><<<cg, 256, 0, st>>>(d_jobs, d_off, d_recs);
         bow_resolve_kernel<OMV_BOW_KF_FRAME, kBowWaves><<<n_jobs, 64 * kBowWaves, 0, st>>>(d_jobs, d_off, d_recs, nnratio,

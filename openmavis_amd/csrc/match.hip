@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <cmath>
 #include <cstdio>
@@ -2044,7 +2046,10 @@ struct omv_matcher {
     bool timing = false;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
     double stage_ms[4] = {0, 0, 0, 0};
+    omv::MatcherKnobs knobs;   // test knobs, read from the environment once at creation
 };
+
+omv::MatcherKnobs omv::matcher_knobs(const omv_matcher *m) { return m ? m->knobs : omv::MatcherKnobs{}; }
 
 static hipEvent_t mk_event(hipStream_t st) {
     hipEvent_t e;
@@ -2118,6 +2123,10 @@ omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mp
     HIP_OK(hipFuncSetAttribute((const void *)lf_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds));
     omv_matcher *h = new omv_matcher();
     h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
+    if (const char *e = getenv("OMV_BOW_TOP")) h->knobs.bow_top = atoi(e);
+    if (const char *e = getenv("OMV_TRI_SLICES")) h->knobs.tri_slices = atoi(e);
+    if (const char *e = getenv("OMV_TRI_ECAP")) h->knobs.tri_ecap = atoi(e);
+    if (const char *e = getenv("OMV_TRI_WALK")) h->knobs.tri_walk_seq = strcmp(e, "seq") == 0 ? 1 : 0;
     const size_t fc = (size_t)max_frames * n_cams;
     HIP_OK(hipMalloc(&h->d_cell_start, sizeof(int32_t) * fc * (kCells + 1)));
     HIP_OK(hipMalloc(&h->d_cell_idx, sizeof(int32_t) * fc * kp_cap));

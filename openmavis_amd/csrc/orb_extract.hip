@@ -1388,6 +1388,7 @@ __global__ void __launch_bounds__(256) node_sort_selftest_kernel(const int *k1, 
 struct omv_orb {
     omv_orb_params p;
     int W, H, max_images;
+    int pyr_mode = -1;   // test knob OMV_PYR_MODE read at creation: -1 unset, 0 "levels", 1 "chain"
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> quota;
     int umax[16];
@@ -1662,6 +1663,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     omv_orb *o = new omv_orb();
     o->p = *params;
     o->W = width, o->H = height, o->max_images = max_images;
+    if (const char *pm = getenv("OMV_PYR_MODE")) o->pyr_mode = std::strcmp(pm, "chain") == 0 ? 1 : 0;
     (void)hipGetDevice(&o->device);
     std::vector<Cell> cells;
     std::vector<XTab> xt, yt;
@@ -1829,9 +1831,8 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K1: pyramid, every level in one launch (level by level when no band plan fits LDS); test knob OMV_PYR_MODE =
-    // "levels" / "chain" picks the path
-    const char *pm = getenv("OMV_PYR_MODE");
-    const bool chain = pm ? std::strcmp(pm, "chain") == 0 : n <= kPyrChainMaxImages;
+    // "levels" / "chain" (read at omv_orb_create) picks the path
+    const bool chain = o->pyr_mode >= 0 ? o->pyr_mode == 1 : n <= kPyrChainMaxImages;
     if (o->pyr_nb > 0 && chain) {
         const size_t lds = sizeof(uint32_t) * (2 * (size_t)o->pyr_buf_dw + 4 + o->pyr_tab_dw + 3 * (size_t)o->pyr_rows);
         pyr_chain_kernel<<<dim3(o->pyr_nb, n), 256, lds, st>>>(g, images, image_stride, pitch, o->d_pyr, o->d_xt, o->d_yt,

@@ -1370,26 +1370,20 @@ omv_status omv_matcher_stereo_triangulate(omv_matcher *m, int n_frames, int n_ca
 }
 
 
-omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
-                                                const float *cams, const int32_t *cam_model, int only_stereo,
-                                                int coarse, int check_ori, int32_t *n_matches, void *stream) {
-    if (!m || n_pairs < 0 || (n_pairs > 0 && (!pairs || !cams || !n_matches))) return OMV_ERR_ARG;
-    if (n_pairs == 0) return OMV_OK;
-    for (int i = 0; i < n_pairs; ++i)
-        if (!pairs[i].match12 || pairs[i].kf1.n < 0 || pairs[i].kf2.n < 0) return OMV_ERR_ARG;
-    hipStream_t st = (hipStream_t)stream;
-    TriCams C;
-    for (int c = 0; c < 4; ++c) {
-        for (int q = 0; q < 8; ++q) C.cam[c][q] = cams[8 * c + q];
-        C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
-        if (C.model[c] != OMV_CAM_KB8 && C.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
-    }
+}  // extern "C"
+
+namespace {
+
+// One chunk of pairs through the sliced search (its workspace sized for the chunk; see omv_matcher_search_for_triangulation).
+omv_status tri_search_chunk(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs, const TriCams &C, int only_stereo,
+                            int coarse, int check_ori, int32_t *n_matches, hipStream_t st) {
     // S slices per pair: about 1,024 scan workgroups in all (at most 16 per pair)
     int S = std::max(1, std::min(16, (1024 + n_pairs - 1) / n_pairs));
     int ecap = std::max(2048, 32768 / S);
     // test knobs: the slice count, and the entry capacity (a small one forces the overflow rerun)
-    if (const char *e = getenv("OMV_TRI_SLICES")) S = std::max(1, std::min(64, atoi(e)));
-    if (const char *e = getenv("OMV_TRI_ECAP")) ecap = std::max(1, atoi(e));
+    const omv::MatcherKnobs kn = omv::matcher_knobs(m);   // read once by omv_matcher_create
+    if (kn.tri_slices >= 0) S = std::max(1, std::min(64, kn.tri_slices));
+    if (kn.tri_ecap >= 0) ecap = std::max(1, kn.tri_ecap);
     const int tcap = 2 * ecap;
     const size_t slots = (size_t)n_pairs * S;
     const size_t bytes = sizeof(omv_tri_pair) * n_pairs + slots * (size_t)ecap * 12 + slots * (size_t)tcap * 4 +
@@ -1411,9 +1405,8 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
     HIP_OK(hipMemsetAsync(ws.over, 0, sizeof(int) * (n_pairs + 1), st));   // overflow flags and the error word
     tri_scan_kernel<<<dim3(S, n_pairs), kTriThreads, 0, st>>>(d_pairs, only_stereo, coarse, ws);
     if (!coarse && !only_stereo) tri_epi_kernel<<<dim3(kEpiPerSlot, (unsigned)slots), kEpiThreads, 0, st>>>(d_pairs, C, ws);
-    const char *wk = getenv("OMV_TRI_WALK");   // test knob: "seq" = the scalar walk
     tri_walk_kernel<<<n_pairs, kWalkThreads, 0, st>>>(d_pairs, check_ori, ws, n_matches, d_err,
-                                                      wk && !strcmp(wk, "seq") ? 0 : 1);
+                                                      kn.tri_walk_seq ? 0 : 1);   // test knob: the scalar walk
     HIP_OK(hipGetLastError());
     std::vector<int> over(n_pairs + 1);
     HIP_OK(hipMemcpyAsync(over.data(), ws.over, sizeof(int) * (n_pairs + 1), hipMemcpyDeviceToHost, st));
@@ -1429,6 +1422,38 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
     }
     HIP_OK(hipFreeAsync(blob, st));
     return h_err ? (omv_status)h_err : OMV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Pairs go through in chunks of at most kTriChunkPairs: the sliced workspace is sized per chunk (~650 KB per pair at
+// one slice), so a call's temporary memory stays bounded (~170 MB) whatever its pair count; pairs are independent, so
+// the results do not depend on the chunking.
+constexpr int kTriChunkPairs = 256;
+omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, const omv_tri_pair *pairs,
+                                                const float *cams, const int32_t *cam_model, int only_stereo,
+                                                int coarse, int check_ori, int32_t *n_matches, void *stream) {
+    if (!m || n_pairs < 0 || (n_pairs > 0 && (!pairs || !cams || !n_matches))) return OMV_ERR_ARG;
+    if (n_pairs == 0) return OMV_OK;
+    for (int i = 0; i < n_pairs; ++i)
+        if (!pairs[i].match12 || pairs[i].kf1.n < 0 || pairs[i].kf2.n < 0) return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    TriCams C;
+    for (int c = 0; c < 4; ++c) {
+        for (int q = 0; q < 8; ++q) C.cam[c][q] = cams[8 * c + q];
+        C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
+        if (C.model[c] != OMV_CAM_KB8 && C.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
+    }
+    omv_status first_err = OMV_OK;
+    for (int p0 = 0; p0 < n_pairs; p0 += kTriChunkPairs) {
+        const int n = std::min(kTriChunkPairs, n_pairs - p0);
+        const omv_status r = tri_search_chunk(m, n, pairs + p0, C, only_stereo, coarse, check_ori, n_matches + p0, st);
+        if (r == OMV_ERR_HIP || r == OMV_ERR_ARG) return r;
+        if (r != OMV_OK && first_err == OMV_OK) first_err = r;   // a device-reported error word: the rest still run
+    }
+    return first_err;
 }
 
 
