@@ -436,6 +436,205 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same candidates with the camera's keypoints staged in LDS.  One 512-thread workgroup per (frame, camera,
+// chunk of 8 * pw map points): the camera's grid-ordered keypoints (CSR position p -> x, y, octave | index |
+// blocked bit, 32-B descriptor) and its cell starts are copied into LDS once, then every in-view slot of the
+// chunk walks its window there.  The global-memory version pays one dependent L2/HBM gather per window entry
+// (cell index -> keypoint and descriptor) per (map point, camera); here a window step is two LDS reads, the
+// descriptor only for entries that pass the level / radius / blocked tests, and the cell-index hop is gone
+// (entries sit in CSR order).  Same window order and tie rule as scan_window, hence the same records.
+constexpr int kStageThreads = 512;
+constexpr uint32_t kStageBlocked = 1u << 31;
+constexpr size_t kStageLdsMax = 80 * 1024;   // two workgroups per CU
+constexpr int kScanGroup = 4;                 // window entries read per LDS round trip
+constexpr int kStageUnroll = 3;               // staged entries per thread per pass (1,536 per pass)
+constexpr int kStageMaxIt = 4;                // map points per wave <= 256
+constexpr int kStageBuckets = 32;             // window-size classes: 2 x predicted level (nlevels <= 16)
+
+__host__ __device__ inline size_t stage_lds_bytes(int kp_cap, int pw) {
+    return (size_t)kp_cap * (32 + 8 + 4) + (size_t)(kCells + 1) * 4 + (size_t)(kStageThreads / 64) * pw * 4;
+}
+
+__device__ __forceinline__ void scan_window_lds(const FrameArgs &f, float x, float y, float r, int minL, int maxL,
+                                                const uint64_t dmp[4], const int *scs, const float2 *sxy,
+                                                const uint32_t *smeta, const uint4 *sdesc, TopSeq &t) {
+    t.reset();
+    const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (nMaxCellY < 0) return;
+    const bool checkLevels = (minL > 0) || (maxL >= 0);
+    // a column's run in groups of kScanGroup entries: the group's position / meta reads go out together (one LDS
+    // round trip per group instead of per entry; reads past the run stay inside the staged arrays and are masked)
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int e = scs[ix * kGridRows + nMaxCellY + 1];
+        for (int p0 = scs[ix * kGridRows + nMinCellY]; p0 < e; p0 += kScanGroup) {
+            float2 k[kScanGroup];
+            uint32_t meta[kScanGroup];
+#pragma unroll
+            for (int u = 0; u < kScanGroup; ++u) k[u] = sxy[p0 + u], meta[u] = smeta[p0 + u];
+#pragma unroll
+            for (int u = 0; u < kScanGroup; ++u) {
+                const int oct = (int)((meta[u] >> 16) & 0x7f);
+                bool ok = p0 + u < e;
+                if (checkLevels) ok = ok && oct >= minL && !(maxL >= 0 && oct > maxL);
+                ok = ok && fabsf(k[u].x - x) < r && fabsf(k[u].y - y) < r && !(meta[u] & kStageBlocked);
+                if (!ok) continue;
+                const int p = p0 + u;
+                const uint4 a = sdesc[2 * p], b = sdesc[2 * p + 1];
+                const uint64_t d[4] = {(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32),
+                                       (uint64_t)b.x | ((uint64_t)b.y << 32), (uint64_t)b.z | ((uint64_t)b.w << 32)};
+                ++t.count;
+                t.insert((int)(meta[u] & 0xffff), omv::hamming256(dmp, d), oct);
+            }
+        }
+    }
+}
+
+// blockIdx -> (frame, cam, chunk) logical block, XCD-aware: a (frame, camera)'s chunks share one XCD's L2 for
+// their staging reads.  pw: map points per wave.
+__global__ void __launch_bounds__(kStageThreads) cand_stage_kernel(FrameArgs f, MpArgs m, int n_frames, float th,
+                                                                   const uint8_t *occ_init, Rec *recs, int *counts,
+                                                                   int *flags, int far_points, float th_far,
+                                                                   int n_chunks, int pw, int n_blocks) {
+    extern __shared__ __align__(16) unsigned char stage_lds[];
+    const int C = f.n_cams, cap = f.kp_cap, M = m.M;
+    const int blk = omv::xcd_block(n_blocks);
+    if (blk < 0) return;
+    const int chunk = blk % n_chunks, fc = blk / n_chunks, cam = fc % C, frame = fc / C;
+    uint4 *sdesc = reinterpret_cast<uint4 *>(stage_lds);
+    float2 *sxy = reinterpret_cast<float2 *>(stage_lds + (size_t)cap * 32);
+    uint32_t *smeta = reinterpret_cast<uint32_t *>(stage_lds + (size_t)cap * 40);
+    int *scs = reinterpret_cast<int *>(stage_lds + (size_t)cap * 44);
+    int *queue = scs + kCells + 1;   // [8 * pw] the chunk's active points (workgroup-local index), sorted
+    __shared__ int bucket[kStageBuckets + 1];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid <= kStageBuckets) bucket[tid] = 0;
+    __syncthreads();
+    // Latency chains overlapped: the cell starts and the first staging pass's cell indices are loaded, then the
+    // chunk's map-point activity, then the keypoints / descriptors behind those cell indices.
+    const int32_t *cs = f.cell_start + (size_t)fc * (kCells + 1);
+    const int32_t *ci = f.cell_idx + (size_t)fc * cap;
+    const omv_kp *kp = f.kps + (size_t)fc * cap;
+    const uint4 *dd = reinterpret_cast<const uint4 *>(f.desc + (size_t)fc * cap * 32);
+    const uint8_t *occ = occ_init ? occ_init + ((size_t)frame * C + cam) * cap : nullptr;
+    const int n_in = cs[kCells];
+    for (int c = tid; c <= kCells; c += kStageThreads) scs[c] = cs[c];
+    int idx[kStageUnroll];
+#pragma unroll
+    for (int u = 0; u < kStageUnroll; ++u) {
+        const int p = u * kStageThreads + tid;
+        idx[u] = p < n_in ? ci[p] : -1;
+    }
+    // The chunk's map points: empty records for the inactive slots; the active ones counting-sorted by window size
+    // (predicted level, RadiusByViewingCos) into one workgroup queue, so that a wavefront's 64 lanes walk windows of
+    // similar length (a wave takes the time of its longest window).
+    const int p0 = chunk * (kStageThreads / 64) * pw;
+    int key[kStageMaxIt], lv[kStageMaxIt];
+    bool iv[kStageMaxIt];
+    float vc[kStageMaxIt];
+#pragma unroll
+    for (int it = 0; it < kStageMaxIt; ++it) {
+        const int i = p0 + wave * pw + it * 64 + lane;
+        const bool valid = it * 64 + lane < pw && i < M;
+        const size_t bc = ((size_t)frame * M + (valid ? i : 0)) * C + cam;
+        iv[it] = valid && m.in_view[bc];
+        lv[it] = valid ? m.level[bc] : -1;
+        vc[it] = valid ? m.view_cos[bc] : 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < kStageMaxIt; ++it) {
+        key[it] = -1;
+        const int i = p0 + wave * pw + it * 64 + lane;
+        if (it * 64 + lane >= pw || i >= M) continue;
+        const size_t fm = (size_t)frame * M + i, bc = fm * C + cam;
+        if (cam == 0) {
+            int fl = 0;
+            for (int q = 0; q < C; ++q) fl |= m.in_view[fm * C + q] ? (1 << q) : 0;
+            if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
+            if (m.has_obs[fm]) fl |= kFlagObs;
+            flags[fm] = fl;
+        }
+        if (iv[it] && lv[it] >= 0 && lv[it] < f.nlevels) {
+            key[it] = 2 * lv[it] + (vc[it] > 0.998 ? 0 : 1);
+            atomicAdd(&bucket[key[it]], 1);
+        } else {
+            uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
+#pragma unroll
+            for (int v = 0; v < kTop / 4; ++v) o4[v] = make_uint4(0u, 0u, 0u, 0u);
+            counts[bc] = 0;
+        }
+    }
+    // stage the grid-ordered keypoints: kStageUnroll entries per thread per pass, all cell-index loads first, then all
+    // keypoint / descriptor loads (two dependent global round trips per pass instead of two per entry)
+    for (int s0 = 0; s0 < n_in; s0 += kStageThreads * kStageUnroll) {
+        if (s0 > 0) {
+#pragma unroll
+            for (int u = 0; u < kStageUnroll; ++u) {
+                const int p = s0 + u * kStageThreads + tid;
+                idx[u] = p < n_in ? ci[p] : -1;
+            }
+        }
+        float x[kStageUnroll], y[kStageUnroll];
+        int oct[kStageUnroll];
+        uint4 da[kStageUnroll], db[kStageUnroll];
+        bool bl[kStageUnroll];
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            const int i = max(idx[u], 0);
+            x[u] = kp[i].x, y[u] = kp[i].y, oct[u] = kp[i].octave;
+            da[u] = dd[2 * i], db[u] = dd[2 * i + 1];
+            bl[u] = occ && occ[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            const int p = s0 + u * kStageThreads + tid;
+            if (idx[u] < 0) continue;
+            sxy[p] = make_float2(x[u], y[u]);
+            smeta[p] = (uint32_t)idx[u] | ((uint32_t)(oct[u] & 0x7f) << 16) | (bl[u] ? kStageBlocked : 0u);
+            sdesc[2 * p] = da[u], sdesc[2 * p + 1] = db[u];
+        }
+    }
+    __syncthreads();   // staging and bucket counts complete
+    if (tid < 64) {    // exclusive scan of the 32 bucket counts
+        const int c = tid < kStageBuckets ? bucket[tid] : 0;
+        int incl = c;
+        for (int d = 1; d < 32; d <<= 1) {
+            const int t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        if (tid < kStageBuckets) bucket[tid] = incl - c;
+        if (tid == kStageBuckets - 1) bucket[kStageBuckets] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kStageMaxIt; ++it)
+        if (key[it] >= 0) queue[atomicAdd(&bucket[key[it]], 1)] = wave * pw + it * 64 + lane;
+    __syncthreads();
+    const int nq = bucket[kStageBuckets];
+    for (int q = wave * 64 + lane; q - lane < nq; q += kStageThreads) {
+        if (q >= nq) break;
+        const int i = p0 + queue[q];
+        const size_t fm = (size_t)frame * M + i, bc = fm * C + cam;
+        TopSeq t;
+        uint64_t dmp[4];
+        load_desc(m.desc + fm * 32, dmp);
+        const float r = window_radius(f, m, bc, cam, th, th != 1.0f);
+        scan_window_lds(f, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp, scs, sxy, smeta, sdesc, t);
+        uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
+#pragma unroll
+        for (int v = 0; v < kTop / 4; ++v)
+            o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
+                               4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
+        counts[bc] = t.count;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Claim resolution (the order-dependent part of SearchByProjection).
 //
 // Decomposition: the keypoint slots of camera blocks >= 2 are only ever touched by searches in their own block,
@@ -2121,12 +2320,15 @@ omv_status omv_matcher_create(int max_frames, int n_cams, int kp_cap, int max_mp
     HIP_OK(hipFuncSetAttribute((const void *)resolve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, resolve_dyn));
     HIP_OK(hipFuncSetAttribute((const void *)resolve_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, resolve_dyn));
     HIP_OK(hipFuncSetAttribute((const void *)lf_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds));
+    HIP_OK(hipFuncSetAttribute((const void *)cand_stage_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
     omv_matcher *h = new omv_matcher();
     h->max_frames = max_frames, h->n_cams = n_cams, h->kp_cap = kp_cap, h->max_mps = max_mps;
     if (const char *e = getenv("OMV_BOW_TOP")) h->knobs.bow_top = atoi(e);
     if (const char *e = getenv("OMV_TRI_SLICES")) h->knobs.tri_slices = atoi(e);
     if (const char *e = getenv("OMV_TRI_ECAP")) h->knobs.tri_ecap = atoi(e);
     if (const char *e = getenv("OMV_TRI_WALK")) h->knobs.tri_walk_seq = strcmp(e, "seq") == 0 ? 1 : 0;
+    if (const char *e = getenv("OMV_CAND")) h->knobs.cand_mode = strcmp(e, "global") == 0 ? 1 : strcmp(e, "lds") == 0 ? 2 : 0;
+    if (const char *e = getenv("OMV_CAND_PW")) h->knobs.cand_pw = atoi(e);
     const size_t fc = (size_t)max_frames * n_cams;
     HIP_OK(hipMalloc(&h->d_cell_start, sizeof(int32_t) * fc * (kCells + 1)));
     HIP_OK(hipMalloc(&h->d_cell_idx, sizeof(int32_t) * fc * kp_cap));
@@ -2228,7 +2430,19 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
     hipEvent_t e0 = h->timing ? mk_event(st) : nullptr;
     if (M > 0) {
         const long long tot = (long long)n_frames * M * h->n_cams;
-        if (tot <= 262144) {   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
+        // LDS-staged candidates: map points per wave as large as keeps >= ~1,024 workgroups (at least 16)
+        int pw = 128;
+        while (pw > 16 && (long long)n_frames * h->n_cams * ((M + 8 * pw - 1) / (8 * pw)) < 1024) pw >>= 1;
+        if (h->knobs.cand_pw > 0) pw = min(h->knobs.cand_pw, 64 * kStageMaxIt);
+        // staged for batches (throughput); a frame or a few keep cand_kernel<8>, whose 8 lanes per window cut the
+        // longest window's chain, which sets a small launch's time (measured: B=1 51 us vs 70 us staged)
+        const bool staged = h->knobs.cand_mode == 2 || (h->knobs.cand_mode == 0 && tot > 262144);
+        if (staged && stage_lds_bytes(h->kp_cap, pw) <= kStageLdsMax) {
+            const int n_chunks = (M + 8 * pw - 1) / (8 * pw);
+            const int nb = n_frames * h->n_cams * n_chunks;
+            cand_stage_kernel<<<omv::xcd_grid(nb), kStageThreads, stage_lds_bytes(h->kp_cap, pw), st>>>(
+                f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags, far_points, th_far, n_chunks, pw, nb);
+        } else if (tot <= 262144) {   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
             const int nb = (int)((tot + 4 * (kCandChunk / 8) - 1) / (4 * (kCandChunk / 8)));
             cand_kernel<8><<<omv::xcd_grid(nb), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts,
                                                               h->d_flags, far_points, th_far, nb);

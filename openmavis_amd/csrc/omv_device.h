@@ -244,10 +244,13 @@ __device__ __forceinline__ int xcd_block(int n_logical) {
 }
 __host__ inline int xcd_grid(int n_logical) { return (n_logical + 7) & ~7; }
 
-// Test knobs of a matcher handle (OMV_BOW_TOP, OMV_TRI_SLICES, OMV_TRI_ECAP, OMV_TRI_WALK), read once by
-// omv_matcher_create (not per call); -1 / 0: unset.  Defined in match.hip for the other matcher translation units.
+// Test knobs of a matcher handle (OMV_BOW_TOP, OMV_TRI_SLICES, OMV_TRI_ECAP, OMV_TRI_WALK, OMV_CAND, OMV_CAND_PW),
+// read once by omv_matcher_create (not per call); -1 / 0: unset.  Defined in match.hip for the other matcher
+// translation units.
 struct MatcherKnobs {
     int bow_top = -1, tri_slices = -1, tri_ecap = -1, tri_walk_seq = 0;
+    int cand_mode = 0;     // OMV_CAND: SearchByProjection candidates 0 by batch size, 1 "global" (no LDS staging), 2 "lds"
+    int cand_pw = -1;      // OMV_CAND_PW: map points per wave of the LDS-staged candidate kernel
 };
 MatcherKnobs matcher_knobs(const struct ::omv_matcher *m);
 

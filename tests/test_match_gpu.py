@@ -133,6 +133,22 @@ def _mps_for(frames, oracle, M, seed, torch):
 ])
 def test_search_by_projection_matches_oracle(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs,
                                              rand_stereo):
+    _sbp_case(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs, rand_stereo)
+
+
+@pytest.mark.parametrize("env", [dict(OMV_CAND="global"), dict(OMV_CAND="lds"), dict(OMV_CAND="lds", OMV_CAND_PW="128"),
+                                 dict(OMV_CAND="lds", OMV_CAND_PW="64")])
+@pytest.mark.parametrize("case", [(6.0, False, 0.8, 0.25, 0.5, True), (15.0, False, 0.9, 0.02, 1.0, False)])
+def test_search_by_projection_candidate_paths(frames, oracle, torch_cuda, monkeypatch, env, case):
+    """The candidate stage's variants: keypoints staged in LDS per (frame, camera, chunk of map points) -- the
+    batched path; forced here on 3 frames, also with the bench's large chunks (partial last chunk) -- and the
+    global-memory gather kernel (8 lanes per window at this size); same assignments as the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    _sbp_case(frames, oracle, torch_cuda, *case)
+
+
+def _sbp_case(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs, rand_stereo):
     torch = torch_cuda
     M = 5000
     per, mpb = _mps_for(frames, oracle, M, 7 + int(th), torch)

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"bow_build_kernel": "bow_build", "bow_resolve": "bow_resolve", "build_all_kernel": "lba_build", "build_big_kernel": "lba_build_big",
          "cur_copy_kernel": "lba_cur_copy", "trial_scalars_kernel": "lba_trial_scalars", "pyr_resize": "pyr_resize", "fast_cells": "fast_cells", "octree": "octree", "describe": "describe",
          "grid_kernel": "grid", "knn2": "stereo_knn", "stereo_pairs": "stereo_pairs",
-         "stereo_tri_kernel": "stereo_tri", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
+         "stereo_tri_kernel": "stereo_tri", "cand_stage_kernel": "proj_candidates", "cand_kernel": "proj_candidates", "resolve": "proj_resolve",
          "frustum_kernel": "frustum", "uright_kernel": "uright", "err_kernel": "lba_err", "build_land_kernel": "lba_build_land", "build_kernel": "lba_build_split",
          "schur_kernel": "lba_schur", "assemble_kernel": "lba_assemble", "ldlt_kernel": "lba_ldlt",
          "update_kernel": "lba_update", "finish_trial_kernel": "lba_finish_trial", "accept_copy_kernel": "lba_accept",
