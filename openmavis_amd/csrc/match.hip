@@ -175,6 +175,21 @@ struct Top {
     }
 };
 
+// The two smallest keys of Top's form (a lane's share of a wave-cooperative rescan, which needs best / second only).
+struct Top2 {
+    uint64_t key[2];
+    int count;
+    __device__ __forceinline__ void reset() { key[0] = key[1] = ~0ull, count = 0; }
+    __device__ __forceinline__ void insert_at(int idx, int dist, int oct, int q) {
+        const uint64_t k = ((uint64_t)dist << 40) | ((uint64_t)q << 20) | ((uint64_t)oct << 16) | (uint64_t)idx;
+        key[1] = k < key[0] ? key[0] : (k < key[1] ? k : key[1]);
+        key[0] = k < key[0] ? k : key[0];
+    }
+};
+__device__ __forceinline__ uint32_t key_rec(uint64_t k) {   // Top key -> Rec entry idx | dist << 16 | oct << 25
+    return (uint32_t)(k & 0xffff) | ((uint32_t)(k >> 40) << 16) | ((uint32_t)((k >> 16) & 0xf) << 25);
+}
+
 // The same list for one lane inserting in window order: 32-bit keys dist << 23 | oct << 16 | idx compared by
 // distance alone (k | 0x7fffff < key <=> dist(k) < dist(key)), so a new key moves past strictly larger
 // distances only and equal distances keep window order -- the strict `<` scans' tie rule, at half the
@@ -258,9 +273,9 @@ __device__ void scan_window(const FrameArgs &f, int frame, int cam, float x, flo
 // are dealt round-robin, each lane keeps its own top kTop keyed by window position, then merge_top() selects the
 // group's kTop smallest keys — the same list scan_window builds on one lane.  For small batches, where one
 // lane's chain of dependent gathers through a large window is the kernel's critical path.
-template <int G, class Blocked>
+template <int G, class Blocked, class TopT>
 __device__ void scan_window_coop(const FrameArgs &f, int frame, int cam, float x, float y, float r, int minL, int maxL,
-                                 const uint64_t dmp[4], Blocked blocked, Top &t, int g) {
+                                 const uint64_t dmp[4], Blocked blocked, TopT &t, int g) {
     t.reset();
     const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
     if (nMinCellX >= kGridCols) return;
@@ -719,22 +734,33 @@ __device__ __forceinline__ Pick pick_record(const RegRec &r, int c, int cap, con
 #pragma unroll
     for (int v = 0; v < kTop / 4; ++v) e[4 * v] = r.e[v].x, e[4 * v + 1] = r.e[v].y, e[4 * v + 2] = r.e[v].z, e[4 * v + 3] = r.e[v].w;
     const int avail = min(r.count, kTop);
-    uint32_t blocked = 0;
-#pragma unroll
-    for (int k = 0; k < kTop; ++k) {
-        const int slot = c * cap + rec_idx(e[k]);
-        uint32_t b = (bits[slot >> 5] >> (slot & 31)) & 1u;
-        if (slot == pa0) b = obs ? 1u : 0u;
-        blocked |= b << k;
-    }
-    const uint32_t u = ~blocked & ((1u << avail) - 1u);   // avail <= 16
-    const uint32_t u2 = u & (u - 1u);
-    const int k1 = u ? __ffs(u) - 1 : -1, k2 = u2 ? __ffs(u2) - 1 : -1;
+    // entries in groups of 4 (their blocked bits fetched together), until every lane of the wave holds two unblocked
+    // ones or has run out: nearly always the first group (claims are few against 16 candidates per window)
+    int k1 = -1, k2 = -1;
     uint32_t v1 = 0, v2 = 0;
 #pragma unroll
-    for (int k = 0; k < kTop; ++k) {
-        v1 = k == k1 ? e[k] : v1;
-        v2 = k == k2 ? e[k] : v2;
+    for (int g = 0; g < kTop / 4; ++g) {
+        if (g > 0 && __all(k2 >= 0 || 4 * g >= avail)) break;
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int slot = c * cap + rec_idx(e[4 * g + u]);
+            w[u] = bits[slot >> 5];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 4 * g + u;
+            const int slot = c * cap + rec_idx(e[k]);
+            bool b = (w[u] >> (slot & 31)) & 1u;
+            if (slot == pa0) b = obs;
+            const bool un = k < avail && !b;
+            const bool t2 = un && k1 >= 0 && k2 < 0;
+            v2 = t2 ? e[k] : v2;
+            k2 = t2 ? k : k2;
+            const bool t1 = un && k1 < 0;
+            v1 = t1 ? e[k] : v1;
+            k1 = t1 ? k : k1;
+        }
     }
     Pick p;
     p.b1 = k1 >= 0 ? rec_idx(v1) : -1, p.d1 = k1 >= 0 ? rec_dist(v1) : 256, p.o1 = k1 >= 0 ? rec_oct(v1) : -1;
@@ -743,22 +769,96 @@ __device__ __forceinline__ Pick pick_record(const RegRec &r, int c, int cap, con
     return p;
 }
 
-// Full GetFeaturesInArea rescan of one window against the current claims (freed initially-occupied
-// keypoints, or more than kTop - 2 candidates claimed): rare.
-__device__ __forceinline__ Pick rescan_window(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
-                                              const uint32_t *bits, int pa0, bool obs) {
+// Full GetFeaturesInArea rescan of one window against the current claims (freed initially-occupied keypoints, or more
+// than kTop - 2 candidates claimed): rare, and done by the whole wavefront for one lane's window (uniform arguments,
+// every lane active) -- the window's entries dealt over the 64 lanes, then the wave's two smallest (distance, window
+// order) keys: the first two of the sequential scan's order.  A single lane's dependent gather chain through a large
+// window was ~25 us.
+__device__ __forceinline__ uint2 rescan_window_wave(const ResolveArgs &a, int frame, size_t fm, int c, int lvl,
+                                                             const uint32_t *bits, int pa0, bool obs, int lane) {
     const FrameArgs &f = a.f;
     const MpArgs &m = a.m;
     const size_t bc = fm * f.n_cams + c;
     uint64_t dmp[4];
     load_desc(m.desc + fm * 32, dmp);
-    TopSeq t;
-    scan_window(f, frame, c, m.proj_x[bc], m.proj_y[bc], window_radius(f, m, bc, c, a.th, a.th != 1.0f), lvl - 1,
-                lvl, dmp, [&](int slot) { return slot == pa0 ? obs : bit_of(bits, slot); }, t);
+    const float x = m.proj_x[bc], y = m.proj_y[bc], r = window_radius(f, m, bc, c, a.th, a.th != 1.0f);
+    const int minL = lvl - 1, maxL = lvl;
+    Top2 t;
+    t.reset();
+    const int nMinCellX = max(0, (int)floorf((x - f.min_x - r) * f.invW));
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - f.min_x + r) * f.invW));
+    const int nMinCellY = max(0, (int)floorf((y - f.min_y - r) * f.invH));
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - f.min_y + r) * f.invH));
+    if (nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0) {
+        const bool checkLevels = (minL > 0) || (maxL >= 0);
+        const size_t fc = (size_t)frame * f.n_cams + c;
+        const int32_t *cs = f.cell_start + fc * (kCells + 1);
+        const int32_t *ci = f.cell_idx + fc * f.kp_cap;
+        const omv_kp *kp = f.kps + fc * f.kp_cap;
+        const uint8_t *dd = f.desc + fc * f.kp_cap * 32;
+        // lane j holds column nMinCellX + j's contiguous CSR run [b, b + len) (<= 64 columns) and its offset in the
+        // window's iteration order; then the window's entries are dealt 64 per pass, one gather round per pass
+        const int ncol = nMaxCellX - nMinCellX + 1;
+        int cb = 0, len = 0;
+        if (lane < ncol) {
+            const int ix = nMinCellX + lane;
+            cb = cs[ix * kGridRows + nMinCellY];
+            len = cs[ix * kGridRows + nMaxCellY + 1] - cb;
+        }
+        int incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int u = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        const int off = incl - len, total = __shfl(incl, 63, 64);
+        for (int p0 = 0; p0 < total; p0 += 64) {
+            const int pos = p0 + lane;
+            int p = -1;
+            for (int j = 0; j < ncol; ++j) {   // the column holding window position pos
+                const int oj = __shfl(off, j, 64), lj = __shfl(len, j, 64), bj = __shfl(cb, j, 64);
+                if (pos >= oj && pos < oj + lj) p = bj + pos - oj;
+            }
+            if (p < 0) continue;
+            const int i = ci[p];
+            const omv_kp k = kp[i];
+            uint64_t d[4];
+            load_desc(dd + (size_t)i * 32, d);
+            if (checkLevels) {
+                if (k.octave < minL) continue;
+                if (maxL >= 0 && k.octave > maxL) continue;
+            }
+            if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;
+            const int slot = c * f.kp_cap + i;
+            if (slot == pa0 ? obs : bit_of(bits, slot)) continue;
+            t.insert_at(i, omv::hamming256(dmp, d), k.octave, pos);
+        }
+    }
+    uint64_t mn[2];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const uint64_t h = t.key[0];
+        uint64_t v = h;
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint64_t o = __shfl_xor(v, s, 64);
+            v = o < v ? o : v;
+        }
+        mn[rr] = v;
+        const bool own = h == v && h != ~0ull;   // keys are unique (window positions)
+        t.key[0] = own ? t.key[1] : t.key[0];
+        t.key[1] = own ? ~0ull : t.key[1];
+    }
+    // packed as record entries, 0: none (bit 31 marks an entry)
+    return make_uint2(mn[0] != ~0ull ? key_rec(mn[0]) | 0x80000000u : 0u, mn[1] != ~0ull ? key_rec(mn[1]) | 0x80000000u : 0u);
+}
+
+// A rescan's best / second entries (rescan_window_wave's packing) as a Pick.
+__device__ __forceinline__ Pick unpack_pick(uint2 w) {
     Pick p;
-    p.b1 = p.b2 = -1, p.d1 = p.d2 = 256, p.o1 = p.o2 = -1, p.rescan = false;
-    if (t.n > 0) p.b1 = t.idx(0), p.d1 = t.dist(0), p.o1 = t.oct(0);
-    if (t.n > 1) p.b2 = t.idx(1), p.d2 = t.dist(1), p.o2 = t.oct(1);
+    p.rescan = false;
+    p.b1 = w.x ? rec_idx(w.x) : -1, p.d1 = w.x ? rec_dist(w.x) : 256, p.o1 = w.x ? rec_oct(w.x) : -1;
+    p.b2 = w.y ? rec_idx(w.y) : -1, p.d2 = w.y ? rec_dist(w.y) : 256, p.o2 = w.y ? rec_oct(w.y) : -1;
     return p;
 }
 
@@ -789,17 +889,20 @@ struct Visit {
     int stop;            // camera whose ratio test failed (the visit ended there), 255 none
     bool fallback;       // needed a full window rescan
     bool unblock;        // overwrote a blocked slot while having no observations
+    int pending;         // camera (index in the domain) whose window needs a rescan first: the visit stopped there, -1 none
+    int pend_pa0;        // the stereo-partner slot that rescan treats specially (ORBmatcher.cc:125-131)
 };
 
 template <int NC>
 __device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, int c0, int fl, const RegRec (&rr)[NC],
                                       const uint32_t *bits, const uint32_t *occ0, const int *revived, int nrevived,
-                                      const int32_t *l2r, const int32_t *r2l, Visit<NC> &v) {
+                                      const int32_t *l2r, const int32_t *r2l, const uint2 (&forced)[NC], int fmask,
+                                      Visit<NC> &v) {
     const FrameArgs &f = a.f;
     const int C = f.n_cams, cap = f.kp_cap;
 #pragma unroll
     for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
-    v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
+    v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false, v.pending = -1, v.pend_pa0 = -1;
     const size_t fm = (size_t)frame * a.m.M + i;
     const bool obs = (fl & kFlagObs) != 0;
     auto claim = [&](int q, int slot) {
@@ -818,15 +921,21 @@ __device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, in
         if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
         bool need_rescan = (nrevived > 0 || (c == 1 && self_rev >= 0)) &&
                            revived_in_window(a, frame, fm, c, lvl, revived, nrevived, self_rev);
-        if (rr[k].count == 0 && !need_rescan) continue;   // vIndices empty or all initially blocked
+        const bool forced_k = (fmask >> k) & 1;   // the wave rescanned this window for this visit (same claims)
+        if (rr[k].count == 0 && !need_rescan && !forced_k) continue;   // vIndices empty or all initially blocked
         Pick p;
-        if (!need_rescan) {
-            p = pick_record(rr[k], c, cap, bits, c == 1 ? pa0 : -1, obs);
-            need_rescan = p.rescan;
-        }
-        if (need_rescan) {
+        if (forced_k) {
+            p = unpack_pick(forced[k]);
             v.fallback = true;
-            p = rescan_window(a, frame, fm, c, lvl, bits, c == 1 ? pa0 : -1, obs);
+        } else {
+            if (!need_rescan) {
+                p = pick_record(rr[k], c, cap, bits, c == 1 ? pa0 : -1, obs);
+                need_rescan = p.rescan;
+            }
+            if (need_rescan) {   // the wave rescans the window, then this visit runs again
+                v.pending = k, v.pend_pa0 = c == 1 ? pa0 : -1;
+                return;
+            }
         }
         v.rel[2 * k] = p.b1 >= 0 ? c * cap + p.b1 : -1;
         v.rel[2 * k + 1] = p.b2 >= 0 ? c * cap + p.b2 : -1;
@@ -955,11 +1064,40 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
             Visit<NC> v;
             const int nrev = min(sh.nrevived[w], kMaxRevived + 1);
             OMV_TP(1);
-            if (active) visit<NC>(a, frame, pt, c0, cur_flag, cur, sh.bits, sh.occ0, revived, nrev, sh.l2r, sh.r2l, v);
-            else {
+            uint2 forced[NC];
+            int fmask = 0;
+            if (active) {
+                visit<NC>(a, frame, pt, c0, cur_flag, cur, sh.bits, sh.occ0, revived, nrev, sh.l2r, sh.r2l, forced, fmask, v);
+            } else {
 #pragma unroll
                 for (int q = 0; q < 2 * NC; ++q) v.claim[q] = v.rel[q] = -1;
-                v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false;
+                v.nmatch = 0, v.stop = 255, v.fallback = v.unblock = false, v.pending = -1;
+            }
+            // windows that ran out of candidates: rescanned one at a time by the whole wave, then those lanes' visits
+            // run again with the result (at most NC times: a camera is rescanned once per visit)
+            uint64_t pm = __ballot(active && v.pending >= 0);
+            if (__builtin_expect(pm != 0, 0)) {
+                do {
+                    while (pm) {
+                        const int L = __ffsll((long long)pm) - 1;
+                        pm &= pm - 1;
+                        const int k = __shfl(v.pending, L, 64), pa0L = __shfl(v.pend_pa0, L, 64), ptL = __shfl(pt, L, 64);
+                        const bool obsL = (__shfl(cur_flag, L, 64) & kFlagObs) != 0;
+                        const size_t fmL = (size_t)frame * M + ptL;
+                        const int c = c0 + k;
+                        const uint2 p = rescan_window_wave(a, frame, fmL, c, a.m.level[fmL * C + c], sh.bits, pa0L, obsL,
+                                                           lane);
+                        if (lane == L) {
+                            if (k == 0) forced[0] = p;
+                            else forced[NC - 1] = p;
+                            fmask |= 1 << k;
+                        }
+                    }
+                    if (active && v.pending >= 0)
+                        visit<NC>(a, frame, pt, c0, cur_flag, cur, sh.bits, sh.occ0, revived, nrev, sh.l2r, sh.r2l, forced,
+                                  fmask, v);
+                    pm = __ballot(active && v.pending >= 0);
+                } while (pm);
             }
 #ifdef OMV_RESOLVE_PROFILE
             if (start == 0) tp4 += wall_clock64() - tl;
