@@ -366,7 +366,7 @@ constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
 
 // Work compaction: a point is in view in ~1-2 of the C cameras, so a wave over consecutive (point, camera)
 // slots would idle most lanes through the window scans.  Each wave takes kCandChunk consecutive slots,
-// writes the empty records of the inactive ones directly, compacts the active slots into an LDS queue
+// compacts the active ones (in view, valid predicted level; the others get no record) into an LDS queue
 // (ballot prefix, slot order kept) and scans them 64 at a time.
 constexpr int kCandChunk = 192;
 
@@ -402,13 +402,7 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
                 flags[fm] = fl;
             }
             const int lvl = m.level[bc];
-            act = m.in_view[bc] && lvl >= 0 && lvl < f.nlevels;
-            if (!act) {
-                uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
-#pragma unroll
-                for (int v = 0; v < kTop / 4; ++v) o4[v] = make_uint4(0u, 0u, 0u, 0u);
-                counts[bc] = 0;
-            }
+            act = m.in_view[bc] && lvl >= 0 && lvl < f.nlevels;   // no record for the others: resolve never reads it
         }
         const uint64_t am = __ballot(act);
         if (act) queue[wave][nq + __popcll(am & lt)] = s0 + lane;
@@ -545,7 +539,7 @@ __global__ void __launch_bounds__(kStageThreads) cand_stage_kernel(FrameArgs f, 
         const int p = u * kStageThreads + tid;
         idx[u] = p < n_in ? ci[p] : -1;
     }
-    // The chunk's map points: empty records for the inactive slots; the active ones counting-sorted by window size
+    // The chunk's map points: the in-view ones with a valid predicted level counting-sorted by window size
     // (predicted level, RadiusByViewingCos) into one workgroup queue, so that a wavefront's 64 lanes walk windows of
     // similar length (a wave takes the time of its longest window).
     const int p0 = chunk * (kStageThreads / 64) * pw;
@@ -574,14 +568,9 @@ __global__ void __launch_bounds__(kStageThreads) cand_stage_kernel(FrameArgs f, 
             if (m.has_obs[fm]) fl |= kFlagObs;
             flags[fm] = fl;
         }
-        if (iv[it] && lv[it] >= 0 && lv[it] < f.nlevels) {
-            key[it] = 2 * lv[it] + (vc[it] > 0.998 ? 0 : 1);
+        if (iv[it] && lv[it] >= 0 && lv[it] < f.nlevels) {   // only these have records (resolve's visit skips the
+            key[it] = 2 * lv[it] + (vc[it] > 0.998 ? 0 : 1);   // others before it reads one)
             atomicAdd(&bucket[key[it]], 1);
-        } else {
-            uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
-#pragma unroll
-            for (int v = 0; v < kTop / 4; ++v) o4[v] = make_uint4(0u, 0u, 0u, 0u);
-            counts[bc] = 0;
         }
     }
     // stage the grid-ordered keypoints: kStageUnroll entries per thread per pass, all cell-index loads first, then all
