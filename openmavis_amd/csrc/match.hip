@@ -702,15 +702,17 @@ __device__ bool in_window(const FrameArgs &f, int frame, int c, int slot, float 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register vector (uint4 copies go by memcpy)
 
 // One (point, camera) record held in registers: the kTop candidates, the unblocked count, the predicted level.
+// Only the first 4 of the 16 entries are prefetched: the best / second unblocked ones are nearly always among them;
+// the rest are loaded from the record when a wave needs them.
 struct RegRec {
-    u32x4 e[kTop / 4];
+    u32x4 e0;
     int count, level;
 };
 
 // Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window and
 // skips keypoints held by a point with observations (ORBmatcher.cc:77-79); the record holds the kTop best
-// candidates in (distance, window order), so the walk is: fetch the 16 blocked bits together (one LDS round
-// trip), then take the first two unblocked entries with mask arithmetic.  The only own earlier write of the
+// candidates in (distance, window order), so the walk takes the first two unblocked entries, 4 entries (their
+// blocked bits fetched together) at a time.  The only own earlier write of the
 // point that can fall into a later camera's block is camera 0's stereo-partner claim in block 1 (pa0,
 // ORBmatcher.cc:125-131): it reads as blocked iff the point itself has observations.
 struct Pick {
@@ -718,36 +720,42 @@ struct Pick {
     bool rescan;   // the 16 entries ran out with more candidates in the window
 };
 
-__device__ __forceinline__ Pick pick_record(const RegRec &r, int c, int cap, const uint32_t *bits, int pa0, bool obs) {
-    uint32_t e[kTop];
-#pragma unroll
-    for (int v = 0; v < kTop / 4; ++v) e[4 * v] = r.e[v].x, e[4 * v + 1] = r.e[v].y, e[4 * v + 2] = r.e[v].z, e[4 * v + 3] = r.e[v].w;
+__device__ __forceinline__ Pick pick_record(const RegRec &r, const Rec *rp, int c, int cap, const uint32_t *bits, int pa0,
+                                            bool obs) {
     const int avail = min(r.count, kTop);
-    // entries in groups of 4 (their blocked bits fetched together), until every lane of the wave holds two unblocked
-    // ones or has run out: nearly always the first group (claims are few against 16 candidates per window)
+    // groups of 4 entries (their blocked bits fetched together), until every lane of the wave holds two unblocked
+    // ones or has run out: nearly always the first group (claims are few against 16 candidates per window); groups
+    // past the first come from the record in memory
     int k1 = -1, k2 = -1;
     uint32_t v1 = 0, v2 = 0;
 #pragma unroll
     for (int g = 0; g < kTop / 4; ++g) {
-        if (g > 0 && __all(k2 >= 0 || 4 * g >= avail)) break;
+        uint32_t e[4];
+        if (g == 0) {
+            e[0] = r.e0.x, e[1] = r.e0.y, e[2] = r.e0.z, e[3] = r.e0.w;
+        } else {
+            if (__all(k2 >= 0 || 4 * g >= avail)) break;
+            const u32x4 q = reinterpret_cast<const u32x4 *>(rp)[g];
+            e[0] = q.x, e[1] = q.y, e[2] = q.z, e[3] = q.w;
+        }
         uint32_t w[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int slot = c * cap + rec_idx(e[4 * g + u]);
+            const int slot = c * cap + rec_idx(e[u]);
             w[u] = bits[slot >> 5];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k = 4 * g + u;
-            const int slot = c * cap + rec_idx(e[k]);
+            const int slot = c * cap + rec_idx(e[u]);
             bool b = (w[u] >> (slot & 31)) & 1u;
             if (slot == pa0) b = obs;
             const bool un = k < avail && !b;
             const bool t2 = un && k1 >= 0 && k2 < 0;
-            v2 = t2 ? e[k] : v2;
+            v2 = t2 ? e[u] : v2;
             k2 = t2 ? k : k2;
             const bool t1 = un && k1 < 0;
-            v1 = t1 ? e[k] : v1;
+            v1 = t1 ? e[u] : v1;
             k1 = t1 ? k : k1;
         }
     }
@@ -918,7 +926,7 @@ __device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, in
             v.fallback = true;
         } else {
             if (!need_rescan) {
-                p = pick_record(rr[k], c, cap, bits, c == 1 ? pa0 : -1, obs);
+                p = pick_record(rr[k], a.recs + fm * C + c, c, cap, bits, c == 1 ? pa0 : -1, obs);
                 need_rescan = p.rescan;
             }
             if (need_rescan) {   // the wave rescans the window, then this visit runs again
@@ -1011,9 +1019,7 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
             const size_t bc = (rec_base + pt) * C + c0 + k;
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(a.recs + bc);
-#pragma unroll
-            for (int q = 0; q < kTop / 4; ++q) rr[k].e[q] = src[q];
+            rr[k].e0 = *reinterpret_cast<const u32x4 *>(a.recs + bc);
             rr[k].count = a.counts[bc];
             rr[k].level = a.m.level[bc];
         }
