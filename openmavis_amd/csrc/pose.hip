@@ -239,6 +239,7 @@ __device__ __forceinline__ void reduce_normal(double *acc, double (*red)[kNormal
     __syncthreads();
 }
 
+template <int W = kPoseWaves>
 __device__ __forceinline__ int block_count(int v, int *sh) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -246,7 +247,7 @@ __device__ __forceinline__ int block_count(int v, int *sh) {
     if (lane == 0) sh[wave] = v;
     __syncthreads();
     int t = 0;
-    for (int w = 0; w < kPoseWaves; ++w) t += sh[w];
+    for (int w = 0; w < W; ++w) t += sh[w];
     __syncthreads();
     return t;
 }
@@ -2157,7 +2158,7 @@ __device__ void se3_oplus(const double *dx, const double *q, const double *t, do
     } else {
         double sn, cs;
         sincos_d(theta, sn, cs);
-        const double a = sn / theta, b = (1 - cs) / (theta * theta), c = (theta - sn) / pow(theta, 3.0);
+        const double a = sn / theta, b = (1 - cs) / (theta * theta), c = (theta - sn) / (theta * theta * theta);
         for (int k = 0; k < 9; ++k) {
             const double I = (k % 4 == 0) ? 1.0 : 0.0;
             R[k] = I + a * O[k] + b * O2[k];
@@ -2197,7 +2198,7 @@ __device__ __forceinline__ PoseOnlyEdge po_edge(const PoseOnlyArgs &A, int m0, i
     return v;
 }
 // computeError at (q, t): residual r, chi2 returned; Xl = T Xw (camera 0), Xc = T_c0 Xl
-__device__ __forceinline__ double po_error(const PoseOnlyRig P, const double *q, const double *t, const PoseOnlyEdge &v,
+__device__ __forceinline__ double po_error(const PoseOnlyRig &P, const double *q, const double *t, const PoseOnlyEdge &v,
                                            double *r, double *Xl, double *Xc) {
     q_rot(q, v.X, Xl);
     for (int i = 0; i < 3; ++i) Xl[i] += t[i];
@@ -2223,7 +2224,7 @@ __device__ __forceinline__ double po_error(const PoseOnlyRig P, const double *q,
     return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]);
 }
 // linearizeOplus: -projectJac(Xc) R_c0 SE3deriv(Xl) (mono) / the explicit stereo Jacobian
-__device__ __forceinline__ void po_jac(const PoseOnlyRig P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
+__device__ __forceinline__ void po_jac(const PoseOnlyRig &P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
                                        double *J) {
     if (v.stereo) {
         const double x = Xl[0], y = Xl[1], invz = 1.0 / Xl[2], invz_2 = invz * invz;
@@ -2251,6 +2252,9 @@ __device__ __forceinline__ void po_jac(const PoseOnlyRig P, const PoseOnlyEdge &
 
 constexpr int kPoNormal = 28;   // 21 upper-triangle H terms, 6 b terms, the robust chi2
 
+constexpr int kPoThreads = 512;   // pose-only: one edge per thread up to 512 edges, two waves per SIMD
+constexpr int kPoWaves = kPoThreads / 64;
+
 __device__ __forceinline__ void po_reduce(double *acc, int n, double (*red)[kPoNormal], double *out) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int q = 0; q < n; ++q) {
@@ -2263,31 +2267,48 @@ __device__ __forceinline__ void po_reduce(double *acc, int n, double (*red)[kPoN
     __syncthreads();
     if (threadIdx.x < n) {
         double t = 0;
-        for (int w = 0; w < kPoseWaves; ++w) t += red[w][threadIdx.x];
+        for (int w = 0; w < kPoWaves; ++w) t += red[w][threadIdx.x];
         out[threadIdx.x] = t;
     }
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, PoseOnlyArgs A) {
+// Optimizer::PoseOptimization, one 512-thread workgroup per frame.  Thread t owns edge t (and t + 512, ... past 512
+// edges): the edge's data and active flag stay in registers for the whole call (no global loads inside the LM
+// loop), the per-edge chi2 goes to the workspace for the outlier classification.  Two waves per SIMD: the edge
+// passes are long dependent f64 chains (KB8 projection and Jacobian), which one wave per SIMD could not hide.
+__global__ void __launch_bounds__(kPoThreads) pose_only_kernel(PoseOnlyRig Parg, PoseOnlyArgs A) {
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    // the rig in LDS: the edges index it by camera (a per-lane index into the by-value kernel argument made the
+    // compiler keep a private copy in scratch, reloaded inside the edge chains)
+    __shared__ PoseOnlyRig P;
+    {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(&Parg);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(&P);
+        for (int i = tid; i < (int)(sizeof(PoseOnlyRig) / 4); i += kPoThreads) dst[i] = src[i];
+    }
+    __syncthreads();
     const int m0 = A.m_start[f], nm = A.m_start[f + 1] - m0, s0 = A.s_start[f], ns = A.s_start[f + 1] - s0;
     const int nE = nm + ns;
     __shared__ double q0[4], t0[3], sq[4], st[3], tq[4], tt[3];
     __shared__ double Hs[36], Ad[36], gs[6], xs[6], Lm[36], sums[kPoNormal];
-    __shared__ double red[kPoseWaves][kPoNormal];
-    __shared__ int pick[8], cnt[kPoseWaves];
+    __shared__ double red[kPoWaves][kPoNormal];
+    __shared__ int pick[8], cnt[kPoWaves];
     __shared__ double lambda_s, ni_s, cur_s, ini_s;
     __shared__ int nb_s, qmax_s, again_s, brk_s, ok_s;
     auto chi2_of = [&](int e) -> double & { return e < nm ? A.chi2_m[m0 + e] : A.chi2_s[s0 + e - nm]; };
     auto act_of = [&](int e) -> uint8_t & { return e < nm ? A.act_m[m0 + e] : A.act_s[s0 + e - nm]; };
     auto kp_of = [&](int e) { return e < nm ? A.m_kp[m0 + e] : A.s_kp[s0 + e - nm]; };
     uint8_t *kpo = A.kp_out + (size_t)f * A.kp_cap;
-    for (int e = tid; e < nE; e += kPoseThreads) act_of(e) = 1, kpo[kp_of(e)] = 0;   // mvbOutlier[i] = false
+    for (int e = tid; e < nE; e += kPoThreads) act_of(e) = 1, kpo[kp_of(e)] = 0;   // mvbOutlier[i] = false
     if (nE < 3) {
         if (tid == 0) A.n_good[f] = 0;
         return;
     }
+    // the thread's first edge, held for the call; its active flag mirrored in a register
+    const bool own = tid < nE;
+    const PoseOnlyEdge ev = po_edge(A, m0, nm, s0, own ? tid : 0);
+    bool act0 = own;
     if (tid == 0) {
         for (int i = 0; i < 4; ++i) q0[i] = A.pose_q[4 * f + i];
         for (int i = 0; i < 3; ++i) t0[i] = A.pose_t[3 * f + i];
@@ -2297,21 +2318,38 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
     const double dmono = (double)(float)sqrt(5.991), dst = (double)(float)sqrt(7.815);
     bool robust = true;
     int nBad = 0;
+#ifdef OMV_PO_PROFILE   // phase ticks (wall_clock64, 100 MHz) of frame 0, thread 0's view
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = wall_clock64();
+    int n_it = 0, n_trials = 0;
+#define PO_T(k) (pt[k] += wall_clock64() - tl, tl = wall_clock64())
+#else
+#define PO_T(k) ((void)0)
+#endif
+    // edge e (the thread's own first one from registers, the rest from memory) and whether it is active
+    auto edge_at = [&](int e, bool &active) -> PoseOnlyEdge {
+        if (e == tid) {
+            active = act0;
+            return ev;
+        }
+        active = act_of(e) != 0;
+        return po_edge(A, m0, nm, s0, e);
+    };
     for (int round = 0; round < 4; ++round) {
         __syncthreads();
         if (tid < 4) sq[tid] = q0[tid];
         if (tid < 3) st[tid] = t0[tid];
-        int na = 0;
-        for (int e = tid; e < nE; e += kPoseThreads) na += act_of(e);
-        na = block_count(na, cnt);   // (barriers inside)
+        int na = act0 ? 1 : 0;
+        for (int e = tid + kPoThreads; e < nE; e += kPoThreads) na += act_of(e);
+        na = block_count<kPoWaves>(na, cnt);   // (barriers inside)
         if (na > 0) {   // initializeOptimization(0) found the vertex (otherwise optimize() returns -1)
             for (int it = 0; it < 10; ++it) {
                 // computeActiveErrors + buildSystem at the current estimate
                 double acc[kPoNormal];
                 for (int q = 0; q < kPoNormal; ++q) acc[q] = 0.0;
-                for (int e = tid; e < nE; e += kPoseThreads) {
-                    if (!act_of(e)) continue;
-                    const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+                for (int e = tid; e < nE; e += kPoThreads) {
+                    bool active;
+                    const PoseOnlyEdge v = edge_at(e, active);
+                    if (!active) continue;
                     double r[3], Xl[3], Xc[3], J[18];
                     const double c2 = po_error(P, sq, st, v, r, Xl, Xc);
                     chi2_of(e) = c2;
@@ -2327,7 +2365,9 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                     edge_normal(J, v.stereo, w, om, acc);
                     acc[27] += r0;
                 }
+                PO_T(0);
                 po_reduce(acc, kPoNormal, red, sums);
+                PO_T(1);
                 if (tid == 0) {
                     int k = 0;
                     for (int i = 0; i < 6; ++i)
@@ -2342,6 +2382,7 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                     qmax_s = 0;
                 }
                 __syncthreads();
+                PO_T(2);
                 double rho = 0;
                 do {
                     if (tid < 64) {
@@ -2354,11 +2395,13 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                         }
                     }
                     __syncthreads();
+                    PO_T(3);
                     // computeActiveErrors at the trial estimate
                     double c = 0.0;
-                    for (int e = tid; e < nE; e += kPoseThreads) {
-                        if (!act_of(e)) continue;
-                        const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+                    for (int e = tid; e < nE; e += kPoThreads) {
+                        bool active;
+                        const PoseOnlyEdge v = edge_at(e, active);
+                        if (!active) continue;
                         double r[3], Xl[3], Xc[3];
                         const double c2 = po_error(P, tq, tt, v, r, Xl, Xc);
                         chi2_of(e) = c2;
@@ -2369,7 +2412,12 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                         }
                         c += r0;
                     }
+                    PO_T(4);
                     po_reduce(&c, 1, red, sums);
+                    PO_T(5);
+#ifdef OMV_PO_PROFILE
+                    ++n_trials;
+#endif
                     if (tid == 0) {
                         double tempChi = ok_s ? sums[0] : DBL_MAX;
                         double sc = 0;
@@ -2377,7 +2425,8 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                         sc += 1e-3;
                         rho = (cur_s - tempChi) / sc;
                         if (rho > 0 && isfinite(tempChi)) {
-                            double alpha = 1. - pow((2 * rho - 1), 3.0);
+                            const double a3 = 2 * rho - 1;
+                            double alpha = 1. - a3 * a3 * a3;   // pow(2 rho - 1, 3)
                             alpha = fmin(alpha, 2. / 3.);
                             lambda_s *= fmax(1. / 3., alpha);
                             ni_s = 2;
@@ -2400,30 +2449,42 @@ __global__ void __launch_bounds__(kPoseThreads) pose_only_kernel(PoseOnlyRig P, 
                         }
                     }
                     __syncthreads();
+                    PO_T(6);
                 } while (again_s);
+#ifdef OMV_PO_PROFILE
+                ++n_it;
+#endif
                 if (brk_s) break;
             }
         }
         // outlier classification (:1145-1263): an edge left out of this round is re-evaluated at the final estimate
         int bad = 0;
-        for (int e = tid; e < nE; e += kPoseThreads) {
-            uint8_t &a = act_of(e);
+        for (int e = tid; e < nE; e += kPoThreads) {
+            bool active;
+            const PoseOnlyEdge v = edge_at(e, active);
             double c2 = chi2_of(e);
-            if (!a) {
-                const PoseOnlyEdge v = po_edge(A, m0, nm, s0, e);
+            if (!active) {
                 double r[3], Xl[3], Xc[3];
                 c2 = po_error(P, sq, st, v, r, Xl, Xc);
                 chi2_of(e) = c2;
             }
             const bool out = (float)c2 > (e < nm ? 5.991f : 7.815f);
-            a = out ? 0 : 1;
+            if (e == tid) act0 = !out;
+            else act_of(e) = out ? 0 : 1;
             bad += out ? 1 : 0;
         }
-        nBad = block_count(bad, cnt);
+        nBad = block_count<kPoWaves>(bad, cnt);
         if (round == 2) robust = false;
         if (nE < 10) break;   // optimizer.edges().size() < 10
     }
-    for (int e = tid; e < nE; e += kPoseThreads) kpo[kp_of(e)] = act_of(e) ? 0 : 1;
+#ifdef OMV_PO_PROFILE
+    if (tid == 0 && f == 0)
+        printf("pose_only ticks(100MHz): iterations %d trials %d edges %llu reduce %llu Hbuild %llu solve+oplus %llu trial-edges %llu trial-reduce %llu bookkeeping %llu\n",
+               n_it, n_trials, pt[0], pt[1], pt[2], pt[3], pt[4], pt[5], pt[6]);
+#endif
+#undef PO_T
+    if (own) act_of(tid) = act0 ? 1 : 0;
+    for (int e = tid; e < nE; e += kPoThreads) kpo[kp_of(e)] = (e == tid ? act0 : act_of(e) != 0) ? 0 : 1;
     if (tid == 0) {
         for (int i = 0; i < 4; ++i) A.pose_q[4 * f + i] = sq[i];
         for (int i = 0; i < 3; ++i) A.pose_t[3 * f + i] = st[i];
@@ -2626,7 +2687,8 @@ omv_status omv_pose_optimization(omv_pose *h, const omv_pose_batch *b, const dou
                          b->stereo_start, b->stereo_kp, b->stereo_obs, b->stereo_inv_sigma2, b->stereo_xw, h->chi2,
                          h->chi2 + h->max_edges, h->act, h->act + h->max_edges, kp_outlier, b->kp_cap, n_good, pose_q,
                          pose_t};
-    pose_only_kernel<<<b->n_frames, kPoseThreads, 0, (hipStream_t)stream>>>(P, A);
+    static_assert(sizeof(PoseOnlyRig) % 4 == 0, "PoseOnlyRig is copied to LDS by dwords");
+    pose_only_kernel<<<b->n_frames, kPoThreads, 0, (hipStream_t)stream>>>(P, A);
     HIP_OK(hipGetLastError());
     return OMV_OK;
 }
