@@ -142,6 +142,19 @@ struct MpArgs {
 struct Rec {
     uint32_t e[kTop];
 };
+// SearchByProjection(F, MPs) records carry their own validity: bit 31 marks a filled entry (entries 0 .. n-1, n =
+// min(count, kTop)), bit 30 of entry 0 that the window held more than kTop unblocked candidates (no count array).
+constexpr uint32_t kRecValid = 1u << 31, kRecOver = 1u << 30;
+template <class TopT>
+__device__ __forceinline__ void store_record(Rec *dst, const TopT &t) {
+    uint4 *o4 = reinterpret_cast<uint4 *>(dst);   // 64-B record as four 16-B stores
+    uint32_t w[kTop];
+#pragma unroll
+    for (int q = 0; q < kTop; ++q) w[q] = q < t.n ? t.rec(q) | kRecValid : 0u;
+    w[0] |= t.count > kTop ? kRecOver : 0u;
+#pragma unroll
+    for (int v = 0; v < kTop / 4; ++v) o4[v] = make_uint4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
+}
 __device__ __forceinline__ int rec_idx(uint32_t v) { return (int)(v & 0xffff); }
 __device__ __forceinline__ int rec_dist(uint32_t v) { return (int)((v >> 16) & 0x1ff); }
 __device__ __forceinline__ int rec_oct(uint32_t v) { return (int)((v >> 25) & 0x1f); }
@@ -433,14 +446,7 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
                                 [&](int slot) { return occ && occ[slot]; }, t, g);
             merge_top<G>(t);
         }
-        if (g == 0) {
-            uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);   // 64-B record as four 16-B stores
-#pragma unroll
-            for (int v = 0; v < kTop / 4; ++v)
-                o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
-                                   4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
-            counts[bc] = t.count;
-        }
+        if (g == 0) store_record(&recs[bc], t);
     }
 }
 
@@ -629,12 +635,7 @@ __global__ void __launch_bounds__(kStageThreads) cand_stage_kernel(FrameArgs f, 
         load_desc(m.desc + fm * 32, dmp);
         const float r = window_radius(f, m, bc, cam, th, th != 1.0f);
         scan_window_lds(f, m.proj_x[bc], m.proj_y[bc], r, m.level[bc] - 1, m.level[bc], dmp, scs, sxy, smeta, sdesc, t);
-        uint4 *o4 = reinterpret_cast<uint4 *>(&recs[bc]);
-#pragma unroll
-        for (int v = 0; v < kTop / 4; ++v)
-            o4[v] = make_uint4(4 * v < t.n ? t.rec(4 * v) : 0u, 4 * v + 1 < t.n ? t.rec(4 * v + 1) : 0u,
-                               4 * v + 2 < t.n ? t.rec(4 * v + 2) : 0u, 4 * v + 3 < t.n ? t.rec(4 * v + 3) : 0u);
-        counts[bc] = t.count;
+        store_record(&recs[bc], t);
     }
 }
 
@@ -706,7 +707,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register 
 // the rest are loaded from the record when a wave needs them.
 struct RegRec {
     u32x4 e0;
-    int count, level;
+    int level;
 };
 
 // Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window and
@@ -722,19 +723,18 @@ struct Pick {
 
 __device__ __forceinline__ Pick pick_record(const RegRec &r, const Rec *rp, int c, int cap, const uint32_t *bits, int pa0,
                                             bool obs) {
-    const int avail = min(r.count, kTop);
     // groups of 4 entries (their blocked bits fetched together), until every lane of the wave holds two unblocked
     // ones or has run out: nearly always the first group (claims are few against 16 candidates per window); groups
     // past the first come from the record in memory
     int k1 = -1, k2 = -1;
-    uint32_t v1 = 0, v2 = 0;
+    uint32_t v1 = 0, v2 = 0, e_last = 0;   // e_last: the previous group's last entry (entries are filled in order)
 #pragma unroll
     for (int g = 0; g < kTop / 4; ++g) {
         uint32_t e[4];
         if (g == 0) {
             e[0] = r.e0.x, e[1] = r.e0.y, e[2] = r.e0.z, e[3] = r.e0.w;
         } else {
-            if (__all(k2 >= 0 || 4 * g >= avail)) break;
+            if (__all(k2 >= 0 || !(e_last & kRecValid))) break;
             const u32x4 q = reinterpret_cast<const u32x4 *>(rp)[g];
             e[0] = q.x, e[1] = q.y, e[2] = q.z, e[3] = q.w;
         }
@@ -750,7 +750,7 @@ __device__ __forceinline__ Pick pick_record(const RegRec &r, const Rec *rp, int 
             const int slot = c * cap + rec_idx(e[u]);
             bool b = (w[u] >> (slot & 31)) & 1u;
             if (slot == pa0) b = obs;
-            const bool un = k < avail && !b;
+            const bool un = (e[u] & kRecValid) && !b;
             const bool t2 = un && k1 >= 0 && k2 < 0;
             v2 = t2 ? e[u] : v2;
             k2 = t2 ? k : k2;
@@ -758,11 +758,12 @@ __device__ __forceinline__ Pick pick_record(const RegRec &r, const Rec *rp, int 
             v1 = t1 ? e[u] : v1;
             k1 = t1 ? k : k1;
         }
+        e_last = e[3];
     }
     Pick p;
     p.b1 = k1 >= 0 ? rec_idx(v1) : -1, p.d1 = k1 >= 0 ? rec_dist(v1) : 256, p.o1 = k1 >= 0 ? rec_oct(v1) : -1;
     p.b2 = k2 >= 0 ? rec_idx(v2) : -1, p.d2 = k2 >= 0 ? rec_dist(v2) : 256, p.o2 = k2 >= 0 ? rec_oct(v2) : -1;
-    p.rescan = k2 < 0 && r.count > kTop;
+    p.rescan = k2 < 0 && (r.e0.x & kRecOver);
     return p;
 }
 
@@ -919,7 +920,7 @@ __device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, in
         bool need_rescan = (nrevived > 0 || (c == 1 && self_rev >= 0)) &&
                            revived_in_window(a, frame, fm, c, lvl, revived, nrevived, self_rev);
         const bool forced_k = (fmask >> k) & 1;   // the wave rescanned this window for this visit (same claims)
-        if (rr[k].count == 0 && !need_rescan && !forced_k) continue;   // vIndices empty or all initially blocked
+        if (!(rr[k].e0.x & kRecValid) && !need_rescan && !forced_k) continue;   // vIndices empty or all initially blocked
         Pick p;
         if (forced_k) {
             p = unpack_pick(forced[k]);
@@ -1020,7 +1021,6 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
         for (int k = 0; k < NC; ++k) {
             const size_t bc = (rec_base + pt) * C + c0 + k;
             rr[k].e0 = *reinterpret_cast<const u32x4 *>(a.recs + bc);
-            rr[k].count = a.counts[bc];
             rr[k].level = a.m.level[bc];
         }
     };
@@ -1253,7 +1253,7 @@ struct KnnArgs {
 // G lanes per query: lane g of a query's group scores train rows g, g+G, ... of every LDS tile (its own top-2 by
 // (distance, index), strict updates in index order), then the group merges its G top-2 lists with shuffles.  The
 // result is the two smallest (distance, index) pairs — exactly knnMatch's "first index wins ties".  G > 1 cuts
-// the per-query chain for small batches (one frame: 1,200 queries); G = 1 for large batches.
+// the per-query chain and multiplies the waves (see launch_knn2).
 template <int G>
 __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
     __shared__ __attribute__((aligned(16))) uint64_t tile[256][4];
@@ -1302,14 +1302,11 @@ __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
     }
 }
 
-// Lanes per query for a knn launch of n_pairs x q_cap queries: spread small batches over the whole chip.
+// 8 lanes per query at every batch size: one frame (1,200 queries) needs the spread to fill the chip, and at 128
+// frames the shorter per-lane chains and 8x the waves still win over one lane per query (0.150 vs 0.189 ms per
+// 128-frame launch; G = 2 / 4: 0.169 / 0.154).
 static void launch_knn2(const KnnArgs &a, int n_pairs, int q_cap, hipStream_t st) {
-    const long long queries = (long long)n_pairs * q_cap;
-    if (queries <= 32768) {
-        knn2_kernel<8><<<dim3((q_cap + 31) / 32, n_pairs), 256, 0, st>>>(a, n_pairs);
-    } else {
-        knn2_kernel<1><<<dim3((q_cap + 255) / 256, n_pairs), 256, 0, st>>>(a, n_pairs);
-    }
+    knn2_kernel<8><<<dim3((q_cap + 31) / 32, n_pairs), 256, 0, st>>>(a, n_pairs);
 }
 
 // Lowe ratio on the lapping-area knn of camera blocks 0 and 1 (Frame.cc:1488-1491); candidate
