@@ -747,12 +747,16 @@ struct OctArgs {
     int *err;
 };
 
+constexpr int kOctSmallImages = 16;      // extractions of up to this many images: octree_kernel<1>
 #ifndef OMV_OCT_WGS
 #define OMV_OCT_WGS 8   // workgroups per CU the register budget targets (LDS: 20 KB each; measured 6 / 7 / 8 with
                         // the level-major order: 0.232 / 0.221 / 0.213 ms per 128-frame launch; 8 spills a few
                         // registers but wins since the long level-0 workgroups overlap more of each other)
 #endif
-__global__ void __launch_bounds__(256, OMV_OCT_WGS) octree_kernel(Geom g, OctArgs a) {
+// WGS: workgroups per CU the register budget targets -- OMV_OCT_WGS for batches; 1 for a frame or two, where only a
+// few dozen workgroups run and the level-0 ones are the critical path (no spills at the full register budget).
+template <int WGS>
+__global__ void __launch_bounds__(256, WGS) octree_kernel(Geom g, OctArgs a) {
     extern __shared__ __attribute__((aligned(16))) int osm[];
     // level-major block order: the finest levels (most keys, the longest workgroups) of every image are dispatched
     // first and the short coarse levels fill the launch's tail (longest-job-first)
@@ -1679,8 +1683,10 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     }
     // 1080p levels hold ~1,500 cells: the octree's node lists then exceed the default 64 KB dynamic LDS
     if (o->oct_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)octree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)o->oct_lds) !=
-            hipSuccess) {
+        (hipFuncSetAttribute((const void *)octree_kernel<OMV_OCT_WGS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)o->oct_lds) != hipSuccess ||
+         hipFuncSetAttribute((const void *)octree_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)o->oct_lds) != hipSuccess)) {
         delete o;
         return OMV_ERR_HIP;
     }
@@ -1854,7 +1860,8 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K3: octree per (image, level)
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
-    octree_kernel<<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
+    if (n <= kOctSmallImages) octree_kernel<1><<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
+    else octree_kernel<OMV_OCT_WGS><<<g.nlevels * n, 256, o->oct_lds, st>>>(g, oa);
     mark(o, st);
     // K4: orientation + blur at the samples + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n,
