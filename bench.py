@@ -376,7 +376,9 @@ def lba_cpu_baseline(prob, min_trials=200, warmup_trials=10):
 def lba_leg(prob, steps, warmup, dev, world, shard=False):
     """LocalBA iters/s: one iteration = one LM trial (error eval + build + Schur + factor/solve + update
     + chi2).  Each step is one full optimize() of the window from its uploaded state (reset is a
-    device copy outside the timed region); the state read-back and the outlier test are inside.
+    device copy enqueued before the clock starts; it may still be running when optimize() is called, so its
+    few microseconds can land inside -- synchronising it away measured 3 % slower: the launch latency of an
+    idle queue then shows instead); the state read-back and the outlier test are inside.
     world > 1: window replicas (weak scaling), or with shard=True ONE window with its landmarks
     sharded over the ranks and one RCCL all-reduce of the partial Schur system per trial (strong)."""
     import torch
