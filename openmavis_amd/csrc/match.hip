@@ -376,6 +376,20 @@ __device__ __forceinline__ float window_radius(const FrameArgs &f, const MpArgs 
 // Per-point flag word for the resolve stage: bits 0..C-1 in_view per camera, bit 16 skipped
 // (mp_skipped), bit 17 has observations.
 constexpr int kFlagSkip = 1 << 16, kFlagObs = 1 << 17;
+constexpr int kFlagActive = 8;   // bits 8 .. 8+C-1: in view with a valid predicted level (the slots that have a record)
+__device__ __forceinline__ int point_flags(const MpArgs &m, const FrameArgs &f, size_t fm, int frame, int i, int C,
+                                           int far_points, float th_far) {
+    int fl = 0;
+    for (int q = 0; q < C; ++q) {
+        const bool iv = m.in_view[fm * C + q];
+        const int lv = m.level[fm * C + q];
+        fl |= iv ? (1 << q) : 0;
+        fl |= iv && lv >= 0 && lv < f.nlevels ? (1 << (kFlagActive + q)) : 0;
+    }
+    if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
+    if (m.has_obs[fm]) fl |= kFlagObs;
+    return fl;
+}
 
 // Work compaction: a point is in view in ~1-2 of the C cameras, so a wave over consecutive (point, camera)
 // slots would idle most lanes through the window scans.  Each wave takes kCandChunk consecutive slots,
@@ -408,11 +422,7 @@ __global__ void __launch_bounds__(256, 4) cand_kernel(FrameArgs f, MpArgs m, int
             const int frame = (int)(fm / m.M), i = (int)(fm % m.M);
             const size_t bc = (size_t)gid;
             if (c == 0) {
-                int fl = 0;
-                for (int q = 0; q < C; ++q) fl |= m.in_view[(size_t)fm * C + q] ? (1 << q) : 0;
-                if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
-                if (m.has_obs[fm]) fl |= kFlagObs;
-                flags[fm] = fl;
+                flags[fm] = point_flags(m, f, (size_t)fm, frame, i, C, far_points, th_far);
             }
             const int lvl = m.level[bc];
             act = m.in_view[bc] && lvl >= 0 && lvl < f.nlevels;   // no record for the others: resolve never reads it
@@ -568,11 +578,7 @@ __global__ void __launch_bounds__(kStageThreads) cand_stage_kernel(FrameArgs f, 
         if (it * 64 + lane >= pw || i >= M) continue;
         const size_t fm = (size_t)frame * M + i, bc = fm * C + cam;
         if (cam == 0) {
-            int fl = 0;
-            for (int q = 0; q < C; ++q) fl |= m.in_view[fm * C + q] ? (1 << q) : 0;
-            if (mp_skipped(m, frame, i, C, far_points, th_far)) fl |= kFlagSkip;
-            if (m.has_obs[fm]) fl |= kFlagObs;
-            flags[fm] = fl;
+            flags[fm] = point_flags(m, f, fm, frame, i, C, far_points, th_far);
         }
         if (iv[it] && lv[it] >= 0 && lv[it] < f.nlevels) {   // only these have records (resolve's visit skips the
             key[it] = 2 * lv[it] + (vc[it] > 0.998 ? 0 : 1);   // others before it reads one)
@@ -665,7 +671,7 @@ struct ResolveArgs {
     MpArgs m;
     const Rec *recs;
     const int *counts;   // candidates in the window not blocked when the record was built
-    const int *flags;    // per point: in_view bits | kFlagSkip | kFlagObs
+    const int *flags;    // per point: in_view bits | active bits (kFlagActive) | kFlagSkip | kFlagObs
     const int32_t *l2r, *r2l;
     const uint8_t *occ_init;
     int32_t *kp_to_mp;
@@ -707,7 +713,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // a register 
 // the rest are loaded from the record when a wave needs them.
 struct RegRec {
     u32x4 e0;
-    int level;
 };
 
 // Best / second-best unblocked candidates of one (point, camera) record.  The reference walks the window and
@@ -914,11 +919,10 @@ __device__ __forceinline__ void visit(const ResolveArgs &a, int frame, int i, in
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
         const int c = c0 + k;
-        if (!((fl >> c) & 1)) continue;
-        const int lvl = rr[k].level;
-        if (lvl < 0 || lvl >= f.nlevels) continue;   // c > 0: nPredictedLevel == -1 (:142)
+        // in view with a valid predicted level (c > 0: nPredictedLevel == -1 skips, :142) -- the slots with a record
+        if (!((fl >> (kFlagActive + c)) & 1)) continue;
         bool need_rescan = (nrevived > 0 || (c == 1 && self_rev >= 0)) &&
-                           revived_in_window(a, frame, fm, c, lvl, revived, nrevived, self_rev);
+                           revived_in_window(a, frame, fm, c, a.m.level[fm * C + c], revived, nrevived, self_rev);
         const bool forced_k = (fmask >> k) & 1;   // the wave rescanned this window for this visit (same claims)
         if (!(rr[k].e0.x & kRecValid) && !need_rescan && !forced_k) continue;   // vIndices empty or all initially blocked
         Pick p;
@@ -1021,7 +1025,6 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
         for (int k = 0; k < NC; ++k) {
             const size_t bc = (rec_base + pt) * C + c0 + k;
             rr[k].e0 = *reinterpret_cast<const u32x4 *>(a.recs + bc);
-            rr[k].level = a.m.level[bc];
         }
     };
     fill(0);
