@@ -977,6 +977,7 @@ struct ResolveShared {
     uint8_t *stop;     // per point: the camera whose ratio test ended its visit (255 none)
     int *prog;         // per domain: points below this index are final in that domain
     int *list;         // per domain ring of member point indices [kMaxDomains][kListCap]
+    int *listfl;       // their flag words (same ring positions)
     int *revived;      // per domain [kMaxDomains][kMaxRevived]
     int *nrevived;     // per domain
     int *total;
@@ -988,7 +989,7 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
                                            int lane) {
     const int C = a.f.n_cams, M = a.m.M;
     const uint64_t lt = (1ull << lane) - 1ull;
-    int *list = sh.list + w * kListCap;
+    int *list = sh.list + w * kListCap, *listfl = sh.listfl + w * kListCap;
     int *revived = sh.revived + w * kMaxRevived;
     const int *flags_f = a.flags + (size_t)frame * M;
     const size_t rec_base = (size_t)frame * M;
@@ -1008,7 +1009,10 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
             fr[3] = nxt < M ? flags_f[nxt] : kFlagSkip;
             const bool mem = fscan + lane < M && !(fl & kFlagSkip) && (fl & dom_mask);
             const uint64_t bm = __ballot(mem);
-            if (mem) list[(tail + __popcll(bm & lt)) & (kListCap - 1)] = fscan + lane;
+            if (mem) {
+                const int pos = (tail + __popcll(bm & lt)) & (kListCap - 1);
+                list[pos] = fscan + lane, listfl[pos] = fl;
+            }
             tail += __popcll(bm);
             fscan += 64;
         }
@@ -1019,8 +1023,9 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
     int cur_flag = 0, nxt_flag = 0;
     auto load_block = [&](int h, RegRec (&rr)[NC], int &flag) {
         const int nb = min(64, tail - h);
-        const int pt = list[(h + min(lane, max(nb - 1, 0))) & (kListCap - 1)];
-        flag = flags_f[pt];
+        const int pos = (h + min(lane, max(nb - 1, 0))) & (kListCap - 1);
+        const int pt = list[pos];
+        flag = listfl[pos];
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
             const size_t bc = (rec_base + pt) * C + c0 + k;
@@ -1188,7 +1193,7 @@ __device__ __forceinline__ void run_domain(const ResolveArgs &a, const ResolveSh
 template <bool kLdsK2m>
 __global__ void __launch_bounds__(64 * kMaxDomains) resolve_kernel(ResolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    __shared__ int list[kMaxDomains * kListCap];
+    __shared__ int list[kMaxDomains * kListCap], listfl[kMaxDomains * kListCap];
     __shared__ int revived[kMaxDomains * kMaxRevived];
     __shared__ int nrevived[kMaxDomains], prog[kMaxDomains], total;
     const int frame = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
@@ -1203,7 +1208,7 @@ __global__ void __launch_bounds__(64 * kMaxDomains) resolve_kernel(ResolveArgs a
     int32_t *const k2m_g = a.kp_to_mp + (size_t)frame * S;
     sh.k2m = kLdsK2m ? sh.r2l + cap : k2m_g;
     sh.stop = reinterpret_cast<uint8_t *>(sh.r2l + cap + (kLdsK2m ? S : 0));
-    sh.prog = prog, sh.list = list, sh.revived = revived, sh.nrevived = nrevived, sh.total = &total;
+    sh.prog = prog, sh.list = list, sh.listfl = listfl, sh.revived = revived, sh.nrevived = nrevived, sh.total = &total;
     const uint8_t *occ = a.occ_init ? a.occ_init + (size_t)frame * S : nullptr;
     for (int w = tid; w < nwords; w += nt) {
         uint32_t v = 0;
@@ -2413,7 +2418,7 @@ static void fill_frame(omv_matcher *h, const omv_frame_geom *g, const omv_kp *kp
 
 // resolve workspace (dynamic LDS): blocked / initially-occupied bitmaps, the per-slot owner word, l2r / r2l, the
 // per-point stop camera and, when it fits, the frame's assignment (*lds_k2m = 1)
-constexpr size_t kResolveStaticLds = 4 * ((size_t)kMaxDomains * (kListCap + kMaxRevived + 2) + 1);
+constexpr size_t kResolveStaticLds = 4 * ((size_t)kMaxDomains * (2 * kListCap + kMaxRevived + 2) + 1);
 static size_t resolve_lds_bytes(int C, int cap, int M, int *lds_k2m = nullptr) {
     const size_t S = (size_t)C * cap;
     const size_t b = sizeof(uint32_t) * 2 * ((S + 31) / 32) + sizeof(int) * S + 2 * sizeof(int32_t) * cap + ((size_t)M + 3) / 4 * 4;
