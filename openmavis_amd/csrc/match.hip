@@ -1314,7 +1314,10 @@ __global__ void __launch_bounds__(256) knn2_kernel(KnnArgs a, int n_pairs) {
 // frames the shorter per-lane chains and 8x the waves still win over one lane per query (0.150 vs 0.189 ms per
 // 128-frame launch; G = 2 / 4: 0.169 / 0.154).
 static void launch_knn2(const KnnArgs &a, int n_pairs, int q_cap, hipStream_t st) {
-    knn2_kernel<8><<<dim3((q_cap + 31) / 32, n_pairs), 256, 0, st>>>(a, n_pairs);
+    if ((long long)n_pairs * q_cap <= 4096)   // a frame or three: 32 lanes per query, shorter chains
+        knn2_kernel<32><<<dim3((q_cap + 7) / 8, n_pairs), 256, 0, st>>>(a, n_pairs);
+    else
+        knn2_kernel<8><<<dim3((q_cap + 31) / 32, n_pairs), 256, 0, st>>>(a, n_pairs);
 }
 
 // Lowe ratio on the lapping-area knn of camera blocks 0 and 1 (Frame.cc:1488-1491); candidate
@@ -2580,6 +2583,10 @@ omv_status omv_matcher_search_projection(omv_matcher *h, int n_frames, const omv
             const int nb = n_frames * h->n_cams * n_chunks;
             cand_stage_kernel<<<omv::xcd_grid(nb), kStageThreads, stage_lds_bytes(h->kp_cap, pw), st>>>(
                 f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts, h->d_flags, far_points, th_far, n_chunks, pw, nb);
+        } else if (tot <= 65536) {   // a frame or two: 16 lanes per window (the longest window sets the time)
+            const int nb = (int)((tot + 4 * (kCandChunk / 16) - 1) / (4 * (kCandChunk / 16)));
+            cand_kernel<16><<<omv::xcd_grid(nb), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts,
+                                                               h->d_flags, far_points, th_far, nb);
         } else if (tot <= 262144) {   // up to ~10 frames: spread each window over 8 lanes so the launch fills the chip
             const int nb = (int)((tot + 4 * (kCandChunk / 8) - 1) / (4 * (kCandChunk / 8)));
             cand_kernel<8><<<omv::xcd_grid(nb), 256, 0, st>>>(f, m, n_frames, th, kp_occ_init, h->d_recs, h->d_counts,

@@ -148,9 +148,15 @@ def test_search_by_projection_candidate_paths(frames, oracle, torch_cuda, monkey
     _sbp_case(frames, oracle, torch_cuda, *case)
 
 
-def _sbp_case(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs, rand_stereo):
+@pytest.mark.parametrize("case", [(6.0, False, 0.8, 0.25, 0.5, True), (15.0, False, 0.9, 0.02, 1.0, False)])
+def test_search_by_projection_small_batch_lanes(frames, oracle, torch_cuda, case):
+    """3 frames x 4,000 points x 5 cameras = 60,000 slots: the 16-lanes-per-window candidate kernel of one- or
+    two-frame calls (the latency path), against the oracle."""
+    _sbp_case(frames, oracle, torch_cuda, *case, M=4000)
+
+
+def _sbp_case(frames, oracle, torch_cuda, th, far, nnratio, occ_frac, obs, rand_stereo, M=5000):
     torch = torch_cuda
-    M = 5000
     per, mpb = _mps_for(frames, oracle, M, 7 + int(th), torch)
     rng0 = np.random.default_rng(int(th * 10) + int(occ_frac * 100))
     if obs is not None:
