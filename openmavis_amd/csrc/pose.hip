@@ -2343,30 +2343,52 @@ __global__ void __launch_bounds__(kPoThreads) pose_only_kernel(PoseOnlyRig Parg,
         na = block_count<kPoWaves>(na, cnt);   // (barriers inside)
         if (na > 0) {   // initializeOptimization(0) found the vertex (otherwise optimize() returns -1)
             for (int it = 0; it < 10; ++it) {
-                // computeActiveErrors + buildSystem at the current estimate
-                double acc[kPoNormal];
-                for (int q = 0; q < kPoNormal; ++q) acc[q] = 0.0;
-                for (int e = tid; e < nE; e += kPoThreads) {
-                    bool active;
-                    const PoseOnlyEdge v = edge_at(e, active);
-                    if (!active) continue;
-                    double r[3], Xl[3], Xc[3], J[18];
-                    const double c2 = po_error(P, sq, st, v, r, Xl, Xc);
-                    chi2_of(e) = c2;
-                    po_jac(P, v, Xl, Xc, J);
-                    double r0 = c2, r1 = 1.0;
-                    if (robust) {
-                        const double d = v.stereo ? dst : dmono;
-                        huber(c2, d, d * d, r0, r1);
+                // computeActiveErrors + buildSystem at the current estimate.  The 28 normal-equation terms are summed
+                // per edge pass over the wave (fixed butterfly) into the wave's LDS row, then over the waves in order:
+                // no per-thread accumulator array live across the edge chain (it made the kernel spill)
+                for (int q = tid; q < kPoWaves * kPoNormal; q += kPoThreads) (&red[0][0])[q] = 0.0;
+                __syncthreads();
+                for (int e0 = 0; e0 < nE; e0 += kPoThreads) {   // wave-uniform trip count
+                    const int e = e0 + tid;
+                    double J[18], om[3] = {0.0, 0.0, 0.0}, w = 0.0, r0 = 0.0;
+                    for (int q = 0; q < 18; ++q) J[q] = 0.0;
+                    if (e < nE) {
+                        bool active;
+                        const PoseOnlyEdge v = edge_at(e, active);
+                        if (active) {
+                            double r[3], Xl[3], Xc[3];
+                            const double c2 = po_error(P, sq, st, v, r, Xl, Xc);
+                            chi2_of(e) = c2;
+                            po_jac(P, v, Xl, Xc, J);   // mono: rows 0-1 (row 2 stays 0)
+                            double r1 = 1.0;
+                            r0 = c2;
+                            if (robust) {
+                                const double d = v.stereo ? dst : dmono;
+                                huber(c2, d, d * d, r0, r1);
+                            }
+                            w = v.w * r1;
+                            for (int k = 0; k < (v.stereo ? 3 : 2); ++k) om[k] = -v.w * r[k] * r1;
+                        }
                     }
-                    const double w = v.w * r1;
-                    double om[3];
-                    for (int k = 0; k < 3; ++k) om[k] = -v.w * r[k] * r1;
-                    edge_normal(J, v.stereo, w, om, acc);
-                    acc[27] += r0;
+                    auto wsum = [&](double x, int q) {
+                        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+                        if (lane == 0) red[tid >> 6][q] += x;
+                    };
+                    int q = 0;
+                    for (int i = 0; i < 6; ++i)
+                        for (int j = i; j < 6; ++j, ++q)
+                            wsum(w * (J[i] * J[j] + J[6 + i] * J[6 + j] + J[12 + i] * J[12 + j]), q);
+                    for (int i = 0; i < 6; ++i) wsum(J[i] * om[0] + J[6 + i] * om[1] + J[12 + i] * om[2], 21 + i);
+                    wsum(r0, 27);
                 }
                 PO_T(0);
-                po_reduce(acc, kPoNormal, red, sums);
+                __syncthreads();
+                if (tid < kPoNormal) {
+                    double t = 0;
+                    for (int wv = 0; wv < kPoWaves; ++wv) t += red[wv][tid];
+                    sums[tid] = t;
+                }
+                __syncthreads();
                 PO_T(1);
                 if (tid == 0) {
                     int k = 0;
