@@ -768,18 +768,21 @@ def aux_legs(dev, cpu):
         out["mappoint_refresh"]["cpu_baseline"] = {
             "value": round(done / t, 1), "unit": "points/s (distinctive descriptors only)", "cores": 1, "kind": "port",
             "sample": f"{done} points, oracle, 1 thread, {t:.2f} s"}
-    # ---- LocalMapping::CreateNewMapPoints: one keyframe against 20 neighbours (~1,200 SearchForTriangulation pairs each)
+    # ---- LocalMapping::CreateNewMapPoints: the whole neighbour loop (SearchForTriangulation + geometry + AddMapPoint,
+    # interleaved as the reference) of one keyframe against 20 neighbours
     from openmavis_amd import synth_cnmp
-    from openmavis_amd.mapping import CnmpCall
-    cd = synth_cnmp.make_cnmp(seed=21, n_neigh=20, multi=True)
-    cc = CnmpCall(cd, inertial=True, device=dev)
+    from openmavis_amd.mapping import LocalMappingCall
+    cd = synth_cnmp.make_cnmp_chain(seed=21, n_neigh=20)
+    cc = LocalMappingCall(cd, ORBmatcher(0.6, False), inertial=True, device=dev)
     dt = _timed(lambda: cc.run(), 10, dev)
-    n_pairs = int(sum((np.asarray(j["match12"]) >= 0).sum() for j in cd["jobs"]))
-    out["create_new_map_points"] = {"metric": "LocalMapping::CreateNewMapPoints keyframes/s (20 neighbours)",
+    out["create_new_map_points"] = {"metric": "LocalMapping::CreateNewMapPoints keyframes/s (20 neighbours, search + "
+                                              "geometry interleaved)",
                                     "value": round(1 / dt, 1), "unit": "keyframes/s", "ms_per_keyframe": round(dt * 1e3, 3),
-                                    "neighbours": len(cd["jobs"]), "matched_pairs": n_pairs}
+                                    "neighbours": len(cd["nbs"]),
+                                    "keypoints_per_keyframe": int(cd["kf1"]["n"]),
+                                    "new_points": int(cc.has_mp1.sum().item() - int(cd["kf1"]["has_mp"].sum()))}
     if cpu:
-        done, t = _cpu_rate(lambda: oracle.create_new_map_points(cd, inertial=True), 1)
+        done, t = _cpu_rate(lambda: oracle.local_mapping_create_new_map_points(cd, inertial=True), 1)
         out["create_new_map_points"]["cpu_baseline"] = {
             "value": round(done / t, 2), "unit": "keyframes/s", "cores": 1, "kind": "port",
             "sample": f"{done} keyframes x 20 neighbours, oracle, 1 thread, {t:.2f} s"}

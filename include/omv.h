@@ -832,46 +832,98 @@ omv_status omv_mappoint_normal_depth(int n_points, const int32_t *obs_start, con
                                      float *normal, float *min_dist, float *max_dist, void *stream);
 
 
-/* ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-780): the geometric test of each of
- * SearchForTriangulation's matches between the current keyframe and its neighbours ------------------------------
- * One job per neighbour pKF2, in the reference's neighbour order (the camera-pair state -- sophTcw1 / Ow1 of side 1 --
- * persists across neighbours; pCamera1 / pCamera2 and side 2 reset per neighbour, :441, :471-477).  For every match
- * (idx1, match12[idx1]) in idx1 order: the camera-pair state (listed pairs (0,0) (0,1) (1,0) (1,1) when both rigs
- * have a second camera, (0,2) (2,0) (2,2) (1,3) (3,1) (3,3) when they have four, :514-624; other pairs keep the
- * previous match's state), parallax of the unprojected rays, GeometricTools::Triangulate (JacobiSVD<Matrix4f>) or
- * KeyFrame::UnprojectStereo, positive depth, reprojection error in both keyframes, scale consistency.  Float
- * arithmetic as the reference (no contraction; glibc atan2f / cosf / tanf restated).  Map-point creation and the
- * graph updates (AddObservation, AddMapPoint, ComputeDistinctiveDescriptors, UpdateNormalAndDepth) stay with the
- * caller (the last two: omv_mappoint_*). */
+/* ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-783) ---------------------------------------------------
+ * The reference walks the current keyframe's neighbours in order (:439).  Per neighbour pKF2: the baseline test
+ * (:447-461: |Ow2 - Ow1| < pKF2->mb skips it when !mbMonocular; Ow1 is the PERSISTENT side-1 camera centre, see below),
+ * SearchForTriangulation(mpCurrentKeyFrame, pKF2) (:468), and for every match (idx1, match12[idx1]) in idx1 order the
+ * camera-pair state (listed pairs (0,0) (0,1) (1,0) (1,1) when both rigs have a second camera, (0,2) (2,0) (2,2) (1,3)
+ * (3,1) (3,3) when they have four, :529-636; other pairs keep the previous match's state), parallax of the unprojected
+ * rays, GeometricTools::Triangulate (JacobiSVD<Matrix4f>) or KeyFrame::UnprojectStereo, positive depth, reprojection
+ * error in both keyframes, scale consistency; an accepted match creates a MapPoint and mpCurrentKeyFrame->AddMapPoint(
+ * pMP, idx1) (:766-781) -- so every LATER neighbour's SearchForTriangulation skips idx1 (ORBmatcher.cc:1223-1227).
+ * The state that crosses matches and neighbours: sophTcw1 / Ow1 (side 1's camera block, declared before the loop,
+ * :419-424) persists across neighbours; pCamera1 / pCamera2 and side 2 reset per neighbour (:445, :470-474).  Float
+ * arithmetic as the reference (no contraction; glibc atan2f / cosf / tanf restated).  Creating the MapPoint objects and
+ * the graph updates (AddObservation, pKF2->AddMapPoint, ComputeDistinctiveDescriptors, UpdateNormalAndDepth) stay with
+ * the caller (the last two: omv_mappoint_*); the current keyframe's has-map-point flags are updated here. */
 typedef struct omv_cnmp_kf {
     omv_kf_view kf;                     /* kps by idx (mvKeysUn when NLeft == -1, else mvKeys / Right / SideLeft /
                                            SideRight by range), n_left = -1 for a single-camera keyframe, level_sigma2;
-                                           desc / has_mp / nodes unused */
+                                           desc / has_mp / nodes: read by omv_local_mapping_create_new_map_points'
+                                           SearchForTriangulation (neighbours; the current keyframe's has_mp is the
+                                           separate in/out array), unused by omv_create_new_map_points */
     const omv_kp *kps_raw;              /* [n] mvKeys for KeyFrame::UnprojectStereo (NULL: kf.kps) */
     float Tcw[4][12];                   /* GetPose / GetRightPose / GetSideLeftPose / GetSideRightPose: Rcw (row-major) | tcw */
     float Ow[4][3];                     /* GetCameraCenter / GetRightCameraCenter / GetSideLeft.. / GetSideRight.. */
     float Rwc[9], twc[3];               /* mRwc, mTwc.translation() (UnprojectStereo) */
     float fx, fy, cx, cy, invfx, invfy; /* the keyframe's fx fy cx cy invfx invfy */
-    float mb, mbf;
+    float mb, mbf;                      /* mb: also the neighbour's baseline threshold (:453) */
     const float *uright, *depth;        /* device [n] mvuRight / mvDepth (NULL: no stereo observations) */
     float scale_factors[16];            /* mvScaleFactors */
 } omv_cnmp_kf;
 
 typedef struct omv_cnmp_job {
     omv_cnmp_kf kf2;                    /* the neighbour */
-    const int32_t *match12;             /* device [kf1.kf.n]: SearchForTriangulation's vMatches12 (-1 none) */
+    const int32_t *match12;             /* device [kf1.kf.n]: SearchForTriangulation's vMatches12 (-1 none; entries
+                                           outside [0, kf2.kf.n) are ignored) */
     float *x3D;                         /* device [kf1.kf.n][3]: the new point of an accepted match */
     int32_t *status;                    /* device [kf1.kf.n]: 1 triangulated, 2 by UnprojectStereo (bPointStereo),
-                                           0 rejected or no match */
+                                           0 rejected, no match, or the neighbour skipped by the baseline test */
 } omv_cnmp_job;
 
-/* cams / cam_model: host [4][8] / [4] (the rig's L, R, SL, SR; NULL model = all KannalaBrandt8); n_cams: cameras of
- * the rig (1: mpCamera2 == NULL, 2: L + R, 4: L R SL SR); inertial: mbInertial; far_points / th_far_points:
- * mbFarPoints / mThFarPoints; scale_factor: the current keyframe's mfScaleFactor (ratioFactor = 1.5 scale_factor).
- * jobs: host array (n_jobs <= 64). */
+/* The per-match geometry of CreateNewMapPoints for jobs whose match lists the caller obtained itself (e.g. the
+ * single-camera stereo rigs SearchForTriangulation's device path does not cover).  Jobs run in order with the
+ * reference's state chain: check_baseline = !mbMonocular (the baseline test against the persistent Ow1);
+ * side1_state: device int32 in/out, side 1's camera block (sophTcw1 / Ow1) entering the first job and leaving the last
+ * (0 = the current keyframe's left camera, the value at the top of CreateNewMapPoints; NULL: 0, not returned);
+ * has_mp1: device [kf1.kf.n] or NULL, set to 1 at every accepted idx1 (:773).
+ * EXACTNESS: a job's match12 must be the SearchForTriangulation result computed AFTER the previous jobs' AddMapPoint
+ * (has_mp1), as the reference computes it per neighbour (:468).  A caller-driven loop passes one job per call
+ * (SearchForTriangulation with kf1.has_mp = has_mp1, then this call with the same side1_state); several jobs in one
+ * call are exact only when no accepted idx1 of an earlier job appears in a later job's list.
+ * omv_local_mapping_create_new_map_points runs the whole loop on the device.
+ * cams / cam_model: host [4][8] / [4] (the rig's L, R, SL, SR; NULL model = all KannalaBrandt8; others OMV_ERR_ARG);
+ * n_cams: cameras of the rig (1: mpCamera2 == NULL, 2: L + R, 4: L R SL SR); inertial: mbInertial; far_points /
+ * th_far_points: mbFarPoints / mThFarPoints; scale_factor: the current keyframe's mfScaleFactor (ratioFactor =
+ * 1.5 scale_factor).  jobs: host array (n_jobs <= 64).  Asynchronous. */
 omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, const float *cams,
                                      const int32_t *cam_model, int n_cams, int inertial, int far_points,
-                                     float th_far_points, float scale_factor, void *stream);
+                                     float th_far_points, float scale_factor, int check_baseline,
+                                     int32_t *side1_state, uint8_t *has_mp1, void *stream);
+
+/* One neighbour of omv_local_mapping_create_new_map_points. */
+typedef struct omv_cnmp_neighbour {
+    omv_cnmp_kf kf2;                    /* kf2.kf: the full view SearchForTriangulation reads (kps, desc, has_mp =
+                                           pKF2->GetMapPoint(idx2) != NULL, FeatureVector, level_sigma2) */
+    float T[OMV_TRI_PAIRS][12];         /* the camera-pair transforms, as omv_tri_pair.T (keyframe 1 = current) */
+    int skip;                           /* the caller's `continue` before the search: mbMonocular's median-depth
+                                           ratio test (:455-461); the stereo baseline test is done here */
+    int32_t *match12;                   /* device [kf1.kf.n] out: the neighbour's vMatches12 (all -1 when skipped) */
+    float *x3D;                         /* device [kf1.kf.n][3] out, as omv_cnmp_job */
+    int32_t *status;                    /* device [kf1.kf.n] out, as omv_cnmp_job */
+} omv_cnmp_neighbour;
+
+/* LocalMapping::CreateNewMapPoints' loop (:439-783) for a multi-camera rig (n_cams 2 or 4: the rigs
+ * omv_matcher_search_for_triangulation covers), on the device with no host round trip between neighbours: per
+ * neighbour in order, the baseline gate on the persistent Ow1, SearchForTriangulation(mpCurrentKeyFrame, pKF2,
+ * bOnlyStereo = false, bCoarse = coarse) with the matcher's checkOri off (ORBmatcher matcher(0.6, false), :417) against
+ * the current keyframe's has-map-point flags AS LEFT BY THE PREVIOUS NEIGHBOURS, then the per-match geometry, then
+ * AddMapPoint(idx1) of the accepted matches.
+ *   kf1        the current keyframe (kf1.kf: kps, desc, FeatureVector, level_sigma2, ranges; kf1.kf.has_mp ignored)
+ *   has_mp1    device [kf1.kf.n] in/out: GetMapPoint(idx1) != NULL on entry, plus every accepted idx1 on return
+ *   nb         host [n_nb] (n_nb <= 64) neighbours in vpNeighKFs order
+ *   n_matches  device [n_nb]: SearchForTriangulation's return values (0 for a skipped neighbour)
+ *   side1_state device int32 in/out or NULL (as omv_create_new_map_points): calls compose, so a caller that checks
+ *              CheckNewKeyFrames() between neighbours (:440) runs one neighbour per call with the same has_mp1 /
+ *              side1_state and gets the identical result
+ * check_baseline = !mbMonocular; the other arguments as omv_create_new_map_points.  Synchronises `stream` once at the
+ * end (the device error word: OMV_ERR_CAPACITY for a keyframe past SearchForTriangulation's limits). */
+omv_status omv_local_mapping_create_new_map_points(omv_matcher *m, const omv_cnmp_kf *kf1, uint8_t *has_mp1, int n_nb,
+                                                   const omv_cnmp_neighbour *nb, const float *cams,
+                                                   const int32_t *cam_model, int n_cams, int inertial,
+                                                   int check_baseline, int coarse, int far_points, float th_far_points,
+                                                   float scale_factor, int32_t *n_matches, int32_t *side1_state,
+                                                   void *stream);
 
 #ifdef __cplusplus
 }

@@ -184,6 +184,12 @@ class CnmpJob(ctypes.Structure):
     _fields_ = [("kf2", CnmpKf), ("match12", ctypes.c_void_p), ("x3D", ctypes.c_void_p), ("status", ctypes.c_void_p)]
 
 
+class CnmpNeighbour(ctypes.Structure):
+    """omv_cnmp_neighbour (include/omv.h)."""
+    _fields_ = [("kf2", CnmpKf), ("T", (ctypes.c_float * 12) * 10), ("skip", ctypes.c_int),
+                ("match12", ctypes.c_void_p), ("x3D", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
 class TriPair(ctypes.Structure):
     """omv_tri_pair (include/omv.h)."""
     _fields_ = [("kf1", KfView), ("kf2", KfView), ("T", (ctypes.c_float * 12) * OMV_TRI_PAIRS),
@@ -301,7 +307,10 @@ SIGNATURES = {
                               _VP]),
     "omv_frame_pack": (_I, [_I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "omv_mappoint_distinctive_descriptors": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP]),
-    "omv_create_new_map_points": (_I, [_I, _VP, _VP, _VP, _VP, _I, _I, _I, ctypes.c_float, ctypes.c_float, _VP]),
+    "omv_create_new_map_points": (_I, [_I, _VP, _VP, _VP, _VP, _I, _I, _I, ctypes.c_float, ctypes.c_float, _I, _VP,
+                                       _VP, _VP]),
+    "omv_local_mapping_create_new_map_points": (_I, [_VP, _VP, _VP, _I, _VP, _VP, _VP, _I, _I, _I, _I, _I,
+                                                     ctypes.c_float, ctypes.c_float, _VP, _VP, _VP]),
     "omv_mappoint_normal_depth": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
 }
 

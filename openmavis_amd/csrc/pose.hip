@@ -34,6 +34,7 @@
 #include <cfloat>
 #include <climits>
 #include <cstdio>
+#include <mutex>
 #include <vector>
 
 #include "../../include/omv.h"
@@ -2526,7 +2527,6 @@ struct omv_pose {
     uint32_t call = 0;
     int32_t *err = nullptr;
     int mode = OMV_POSE_AUTO, parts = 0;
-    size_t lat_lds[2] = {0, 0};   // the dynamic-LDS size last set on pose_lat_kernel<false / true>
 };
 
 extern "C" {
@@ -2596,6 +2596,16 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
     if (prior && (!prior->Rwb || !prior->twb || !prior->vel || !prior->bg || !prior->ba || !prior->H ||
                   !prior->preint_kf))
         return OMV_ERR_ARG;
+    if (!b->cam || !b->Rcb || !b->tcb || !b->Rbc || !b->tbc || !b->Rwb || !b->twb || !b->Rcw || !b->tcw || !b->vel ||
+        !b->bg || !b->ba || !b->kf_Rwb || !b->kf_twb || !b->kf_vel || !b->kf_bg || !b->kf_ba || !b->preint ||
+        !b->mono_start || !b->stereo_start)
+        return OMV_ERR_ARG;
+    if (b->n_mono > 0 && (!b->mono_cam || !b->mono_kp || !b->mono_obs || !b->mono_inv_sigma2 || !b->mono_xw ||
+                          !b->mono_close))
+        return OMV_ERR_ARG;
+    if (b->n_stereo > 0 && (!b->stereo_cam || !b->stereo_kp || !b->stereo_obs || !b->stereo_inv_sigma2 ||
+                            !b->stereo_xw))
+        return OMV_ERR_ARG;
     Rig rig{};
     rig.n_cams = b->n_cams;
     for (int c = 0; c < b->n_cams; ++c) {
@@ -2645,11 +2655,19 @@ omv_status launch_pose(omv_pose *h, const omv_pose_batch *b, const omv_pose_prio
         const uint32_t salt = h->call << 12;
         const size_t lds = lat_lds_bytes(b->kp_cap);
         gu64 *xb = (gu64 *)h->xbuf;
-        const int pi = prior ? 1 : 0;   // the LDS attribute only when the size changes
-        if (h->lat_lds[pi] != lds) {
-            HIP_OK(hipFuncSetAttribute(prior ? (const void *)pose_lat_kernel<true> : (const void *)pose_lat_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            h->lat_lds[pi] = lds;
+        // The dynamic-LDS attribute belongs to the kernel, not the handle (hipFuncSetAttribute is process-wide): one
+        // grow-only bound per kernel, raised under a lock, so a handle with a smaller kp_cap never lowers the limit
+        // another handle's launches rely on.
+        {
+            static std::mutex mu;
+            static size_t lat_lds_max[2] = {0, 0};
+            const int pi = prior ? 1 : 0;
+            std::lock_guard<std::mutex> lk(mu);
+            if (lat_lds_max[pi] < lds) {
+                HIP_OK(hipFuncSetAttribute(prior ? (const void *)pose_lat_kernel<true> : (const void *)pose_lat_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                lat_lds_max[pi] = lds;
+            }
         }
         if (prior) pose_lat_kernel<true><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
         else pose_lat_kernel<false><<<F * G, kLatThreads, lds, st>>>(rig, A, G, xb, salt, h->err);
@@ -2683,6 +2701,12 @@ omv_status omv_pose_optimization(omv_pose *h, const omv_pose_batch *b, const dou
     if (b->n_frames <= 0 || b->n_frames > h->max_frames || b->n_cams <= 0 || b->n_cams > kMaxCams || b->n_mono < 0 ||
         b->n_stereo < 0 || b->n_mono > h->max_edges || b->n_stereo > h->max_edges || b->kp_cap <= 0 || !b->cam ||
         !b->mono_start || !b->stereo_start)
+        return OMV_ERR_ARG;
+    // every edge array the kernel reads must be present when its kind has edges (the Python binding leaves absent
+    // keys NULL): an error here instead of a fault on the device
+    if (b->n_mono > 0 && (!b->mono_kp || !b->mono_obs || !b->mono_inv_sigma2 || !b->mono_xw || !b->mono_cam))
+        return OMV_ERR_ARG;
+    if (b->n_stereo > 0 && (!b->stereo_kp || !b->stereo_obs || !b->stereo_inv_sigma2 || !b->stereo_xw))
         return OMV_ERR_ARG;
     PoseOnlyRig P{};
     P.rig.n_cams = b->n_cams;

@@ -316,6 +316,26 @@ struct TriCams {
     int model[4];   // OMV_CAM_KB8 / OMV_CAM_PINHOLE per camera (L, R, SL, SR)
 };
 
+// LocalMapping::CreateNewMapPoints' neighbour gate (src/LocalMapping.cc:447-461), evaluated by every kernel of a
+// neighbour's search inside omv_local_mapping_create_new_map_points: the caller's skip, or (!mbMonocular) the baseline
+// |Ow2 - Ow1| below pKF2->mb with Ow1 the centre of side 1's PERSISTENT camera block (*p1, written by the previous
+// neighbour's cnmp_state_kernel; unchanged while this neighbour's search runs).  p1 == nullptr: no gate (the plain
+// SearchForTriangulation calls).
+struct TriGate {
+    const int *p1;
+    int skip, check_baseline;
+    float Ow1[4][3], Ow2[3], mb2;
+};
+__device__ __forceinline__ float gate_norm3(float a, float b, float c) { return omv::sqrtf_cr(a * a + b * b + c * c); }
+__device__ __forceinline__ bool gate_skip(const TriGate &g) {
+    if (!g.p1) return false;
+    if (g.skip) return true;
+    if (!g.check_baseline) return false;
+    const int p = *g.p1;
+    const float baseline = gate_norm3(g.Ow2[0] - g.Ow1[p][0], g.Ow2[1] - g.Ow1[p][1], g.Ow2[2] - g.Ow1[p][2]);
+    return baseline < g.mb2;
+}
+
 // pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, sigma2[kp1.octave], sigma2[kp2.octave]) (ORBmatcher.cc:
 // 1380-1387), a virtual call on camera 1's type
 __device__ bool epipolar_ok(const omv_tri_pair &P, const TriCams &C, int pr, const omv_kp &kp1, const omv_kp &kp2) {
@@ -470,7 +490,7 @@ __device__ __forceinline__ void scan_candidates(const omv_kf_view &K1, const omv
 
 __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pairs, TriCams C, int only_stereo,
                                                           int coarse, int check_ori, int32_t *n_matches, int *err,
-                                                          const int *only) {
+                                                          const int *only, TriGate gate) {
     __shared__ uint8_t bins[kTriMaxKp];
     __shared__ int seg_s1[kSeg], seg_n1[kSeg], seg_s2[kSeg], seg_n2[kSeg], seg_pref[kSeg + 1];
     __shared__ uint32_t v_pk[kVal];      // idx1 << 16 | idx2
@@ -483,6 +503,7 @@ __global__ void __launch_bounds__(kTriThreads) tri_kernel(const omv_tri_pair *pa
     __shared__ int s_keep[kHisto];
     __shared__ int s_state, s_row, s_best, s_bidx, s_fin;
     if (only && !only[blockIdx.x]) return;
+    if (gate_skip(gate)) return;   // the walk wrote the skipped neighbour's empty result
     const omv_tri_pair &P = pairs[blockIdx.x];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
     const int tid = threadIdx.x;
@@ -721,7 +742,7 @@ struct TriWs {
 };
 
 __global__ void __launch_bounds__(kTriThreads) tri_scan_kernel(const omv_tri_pair *pairs, int only_stereo, int coarse,
-                                                               TriWs ws) {
+                                                               TriWs ws, TriGate gate) {
     __shared__ int seg_s1[kSeg], seg_n1[kSeg], seg_s2[kSeg], seg_n2[kSeg], seg_pref[kSeg + 1];
     __shared__ uint32_t v_pk[kVal];
     __shared__ uint16_t v_code[kVal];
@@ -731,7 +752,7 @@ __global__ void __launch_bounds__(kTriThreads) tri_scan_kernel(const omv_tri_pai
     const omv_tri_pair &P = pairs[p];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
     const size_t slot = (size_t)p * S + sl, ebase = slot * ws.ecap, tbase = slot * ws.tcap;
-    const bool bad = K1.n > kTriMaxKp || K2.n > 65535;   // reported by the walk
+    const bool bad = K1.n > kTriMaxKp || K2.n > 65535 || gate_skip(gate);   // reported by the walk
     const int a_lo = (int)((long long)K1.n_nodes * sl / S), a_hi = (int)((long long)K1.n_nodes * (sl + 1) / S);
     auto add = [](int x, int y) { return x + y; };
     auto seg_min = [](unsigned x, unsigned y) {
@@ -850,7 +871,8 @@ __device__ __forceinline__ int walk_row(const TriWs &ws, int e0, int e1, int &st
 }
 
 __global__ void __launch_bounds__(kWalkThreads) tri_walk_kernel(const omv_tri_pair *pairs, int check_ori, TriWs ws,
-                                                                int32_t *n_matches, int *err, int par_walk) {
+                                                                int32_t *n_matches, int *err, int par_walk,
+                                                                TriGate gate) {
     __shared__ uint8_t bins[kTriMaxKp];
     __shared__ int fin[kTriMaxKp];   // finished rows: the global entry index of the row's best (parallel replay: rows)
     __shared__ uint8_t instate[kWalkRows + 64];
@@ -858,6 +880,11 @@ __global__ void __launch_bounds__(kWalkThreads) tri_walk_kernel(const omv_tri_pa
     const int p = blockIdx.x, tid = threadIdx.x, S = ws.S;
     const omv_tri_pair &P = pairs[p];
     const omv_kf_view &K1 = P.kf1, &K2 = P.kf2;
+    if (gate_skip(gate)) {   // a neighbour the reference `continue`s past: no search, no matches
+        for (int i = tid; i < K1.n; i += kWalkThreads) P.match12[i] = -1;
+        if (tid == 0) n_matches[p] = 0;
+        return;
+    }
     if (ws.over[p]) return;   // rerun by tri_kernel
     for (int i = tid; i < K1.n; i += kWalkThreads) P.match12[i] = -1;
     if (K1.n > kTriMaxKp || K2.n > 65535) {
@@ -1123,15 +1150,19 @@ __global__ void tri_debug_kernel(TriCams C, omv_kp kp1, omv_kp kp2, const float 
 }
 
 
-// ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-780): the geometry of each triangulation match ----
+// ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-783): the geometry of each triangulation match ----
 // The reference walks the neighbours and their matches in order; the only state one match hands to the next is the
 // camera-pair state (sophTcw1 / Ow1 / pCamera1 of side 1, sophTcw2 / Ow2 / pCamera2 of side 2): listed camera pairs
 // assign it, the others keep it; side 1's pose persists across neighbours, the cameras and side 2 reset per neighbour.
 // So each match's state is that of the last listed match before it -- an inclusive max-scan over the match positions
-// -- and the matches are then independent: one thread per match.
-//   cnmp_last_kernel   one block per neighbour: the side-1 camera block of its last listed match (or -1)
-//   cnmp_kernel        one block per neighbour: the state entering it (the last listed side-1 block of the
-//                      neighbours before it), the max-scan over its matches, the per-match geometry
+// -- and the matches are then independent: one thread per match.  Side 1's block also decides the next neighbour's
+// baseline gate (:447-454), so the jobs' entering states are a short scalar chain over the jobs.
+//   cnmp_last_kernel   one block per job: the side-1 camera block of its last listed match (or -1)
+//   cnmp_kernel        one block per job: the state entering it (the chain over the jobs before it: a job the gate
+//                      skips changes nothing), the max-scan over its matches, the per-match geometry, has_mp1 marks
+//   cnmp_state_kernel  one thread: the state leaving the last job (side1_state out)
+// A whole CreateNewMapPoints (omv_local_mapping_create_new_map_points) interleaves these with each neighbour's
+// SearchForTriangulation launches on the stream: the search of neighbour j reads has_mp1 after neighbour j-1's marks.
 constexpr int kCnmpThreads = 256;
 struct CnmpArgs {
     TriCams C;
@@ -1157,11 +1188,27 @@ __global__ void __launch_bounds__(kCnmpThreads) cnmp_last_kernel(const omv_cnmp_
     int mine = -1;
     for (int i = threadIdx.x; i < K1.n; i += blockDim.x) {
         const int i2 = J.match12[i];
-        if (i2 >= 0 && cnmp_listed(n_cams, cnmp_cam(K1, i), cnmp_cam(K2, i2))) mine = i;
+        if (i2 >= 0 && i2 < K2.n && cnmp_listed(n_cams, cnmp_cam(K1, i), cnmp_cam(K2, i2))) mine = i;
     }
     atomicMax(&best, mine);
     __syncthreads();
     if (threadIdx.x == 0) last_p1[blockIdx.x] = best >= 0 ? cnmp_cam(K1, best) : -1;
+}
+
+// The baseline gate of job q under side-1 block p1 (LocalMapping.cc:447-454; Eigen's norm as sqrt of the left-to-right
+// squared sum)
+__device__ __forceinline__ bool cnmp_gate(const omv_cnmp_kf &K1, const omv_cnmp_kf &K2, int p1, int check_baseline) {
+    if (!check_baseline) return false;
+    const float a = K2.Ow[0][0] - K1.Ow[p1][0], b = K2.Ow[0][1] - K1.Ow[p1][1], c = K2.Ow[0][2] - K1.Ow[p1][2];
+    return omv::sqrtf_cr(a * a + b * b + c * c) < K2.mb;
+}
+// The side-1 block entering job j (and whether the gate skips it): the scalar chain over the jobs before it.
+__device__ int cnmp_enter(const omv_cnmp_kf &K1, const omv_cnmp_job *jobs, int j, const int *last_p1, int p1,
+                          int check_baseline, bool &skipped) {
+    for (int q = 0; q < j; ++q)
+        if (!cnmp_gate(K1, jobs[q].kf2, p1, check_baseline) && last_p1[q] >= 0) p1 = last_p1[q];
+    skipped = cnmp_gate(K1, jobs[j].kf2, p1, check_baseline);
+    return p1;
 }
 
 __device__ __forceinline__ float cnmp_dot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
@@ -1274,26 +1321,34 @@ __device__ int cnmp_match(const CnmpArgs &a, const omv_cnmp_kf &K1, const omv_cn
 }
 
 __global__ void __launch_bounds__(kCnmpThreads) cnmp_kernel(const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs,
-                                                            const int *last_p1, CnmpArgs a) {
+                                                            const int *last_p1, CnmpArgs a, const int *p1_state,
+                                                            int check_baseline, uint8_t *has_mp1) {
     __shared__ int s_scan[kCnmpThreads];
+    __shared__ int s_p1, s_skip;
     const int j = blockIdx.x, t = threadIdx.x;
     const omv_cnmp_kf &K1 = *kf1;
     const omv_cnmp_job &J = jobs[j];
     const omv_cnmp_kf &K2 = J.kf2;
-    const int n = K1.kf.n, chunk = (n + kCnmpThreads - 1) / kCnmpThreads;
+    const int n = K1.kf.n, n2 = K2.kf.n, chunk = (n + kCnmpThreads - 1) / kCnmpThreads;
     const int i0 = min(n, t * chunk), i1 = min(n, i0 + chunk);
-    // side 1 entering this neighbour: the last listed match of the neighbours before it
-    int p1_in = 0;
-    for (int q = j - 1; q >= 0; --q)
-        if (last_p1[q] >= 0) {
-            p1_in = last_p1[q];
-            break;
-        }
+    // side 1 entering this job: the state entering the call, then the last listed match of every earlier job the
+    // gate did not skip
+    if (t == 0) {
+        bool sk = false;
+        s_p1 = cnmp_enter(K1, jobs, j, last_p1, p1_state ? *p1_state : 0, check_baseline, sk);
+        s_skip = sk ? 1 : 0;
+    }
+    __syncthreads();
+    const int p1_in = s_p1;
+    if (s_skip) {   // the reference `continue`s before SearchForTriangulation: nothing created
+        for (int i = i0; i < i1; ++i) J.status[i] = 0;
+        return;
+    }
     // the last listed match of this thread's chunk, then an inclusive max-scan over the chunks (position-ordered codes)
     int last = -1;
     for (int i = i0; i < i1; ++i) {
         const int i2 = J.match12[i];
-        if (i2 >= 0) {
+        if (i2 >= 0 && i2 < n2) {
             const int code = cnmp_listed(a.n_cams, cnmp_cam(K1.kf, i), cnmp_cam(K2.kf, i2));
             if (code) last = (i << 5) | code;
         }
@@ -1310,7 +1365,7 @@ __global__ void __launch_bounds__(kCnmpThreads) cnmp_kernel(const omv_cnmp_kf *k
     for (int i = i0; i < i1; ++i) {
         J.status[i] = 0;
         const int i2 = J.match12[i];
-        if (i2 < 0) continue;
+        if (i2 < 0 || i2 >= n2) continue;
         const int code = cnmp_listed(a.n_cams, cnmp_cam(K1.kf, i), cnmp_cam(K2.kf, i2));
         if (code) state = (i << 5) | code;
         int p1 = p1_in, c1 = 0, p2 = 0, c2 = 0;
@@ -1321,9 +1376,20 @@ __global__ void __launch_bounds__(kCnmpThreads) cnmp_kernel(const omv_cnmp_kf *k
         float x3D[3];
         const int st = cnmp_match(a, K1, K2, i, i2, p1, c1, p2, c2, x3D);
         J.status[i] = st;
-        if (st)
+        if (st) {
             for (int q = 0; q < 3; ++q) J.x3D[3 * i + q] = x3D[q];
+            if (has_mp1) has_mp1[i] = 1;   // mpCurrentKeyFrame->AddMapPoint(pMP, idx1) (:773)
+        }
     }
+}
+
+// side1_state after the last job (p1_out may alias p1_in: one thread reads, then writes)
+__global__ void cnmp_state_kernel(const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, int n_jobs, const int *last_p1,
+                                  const int *p1_in, int check_baseline, int *p1_out) {
+    bool sk = false;
+    int p1 = cnmp_enter(*kf1, jobs, n_jobs - 1, last_p1, p1_in ? *p1_in : 0, check_baseline, sk);
+    if (!sk && last_p1[n_jobs - 1] >= 0) p1 = last_p1[n_jobs - 1];
+    *p1_out = p1;
 }
 
 }  // namespace
@@ -1403,10 +1469,10 @@ omv_status tri_search_chunk(omv_matcher *m, int n_pairs, const omv_tri_pair *pai
     ws.S = S, ws.ecap = ecap, ws.tcap = tcap;
     HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(omv_tri_pair) * n_pairs, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(ws.over, 0, sizeof(int) * (n_pairs + 1), st));   // overflow flags and the error word
-    tri_scan_kernel<<<dim3(S, n_pairs), kTriThreads, 0, st>>>(d_pairs, only_stereo, coarse, ws);
+    tri_scan_kernel<<<dim3(S, n_pairs), kTriThreads, 0, st>>>(d_pairs, only_stereo, coarse, ws, TriGate{});
     if (!coarse && !only_stereo) tri_epi_kernel<<<dim3(kEpiPerSlot, (unsigned)slots), kEpiThreads, 0, st>>>(d_pairs, C, ws);
     tri_walk_kernel<<<n_pairs, kWalkThreads, 0, st>>>(d_pairs, check_ori, ws, n_matches, d_err,
-                                                      kn.tri_walk_seq ? 0 : 1);   // test knob: the scalar walk
+                                                      kn.tri_walk_seq ? 0 : 1, TriGate{});   // knob: the scalar walk
     HIP_OK(hipGetLastError());
     std::vector<int> over(n_pairs + 1);
     HIP_OK(hipMemcpyAsync(over.data(), ws.over, sizeof(int) * (n_pairs + 1), hipMemcpyDeviceToHost, st));
@@ -1415,7 +1481,7 @@ omv_status tri_search_chunk(omv_matcher *m, int n_pairs, const omv_tri_pair *pai
     if (std::any_of(over.begin(), over.begin() + n_pairs, [](int v) { return v != 0; })) {
         // a pair with more candidates than the workspace holds: the one-workgroup search for it alone
         tri_kernel<<<n_pairs, kTriThreads, 0, st>>>(d_pairs, C, only_stereo, coarse, check_ori, n_matches, d_err,
-                                                    ws.over);
+                                                    ws.over, TriGate{});
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
@@ -1457,24 +1523,37 @@ omv_status omv_matcher_search_for_triangulation(omv_matcher *m, int n_pairs, con
 }
 
 
-omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, const float *cams,
-                                     const int32_t *cam_model, int n_cams, int inertial, int far_points,
-                                     float th_far_points, float scale_factor, void *stream) {
-    if (n_jobs < 0 || n_jobs > 64 || (n_jobs > 0 && (!kf1 || !jobs || !cams)) || n_cams < 1 || n_cams > 4) return OMV_ERR_ARG;
-    if (n_jobs == 0 || kf1->kf.n <= 0) return OMV_OK;
-    if (kf1->kf.n >= (1 << 26)) return OMV_ERR_ARG;
-    for (int j = 0; j < n_jobs; ++j)
-        if (!jobs[j].match12 || !jobs[j].x3D || !jobs[j].status) return OMV_ERR_ARG;
-    hipStream_t st = (hipStream_t)stream;
-    CnmpArgs a{};
+namespace {
+omv_status cnmp_args(const float *cams, const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                     float th_far_points, float scale_factor, CnmpArgs &a) {
+    a = CnmpArgs{};
     for (int c = 0; c < 4; ++c) {
         for (int q = 0; q < 8; ++q) a.C.cam[c][q] = cams[8 * c + q];
         a.C.model[c] = cam_model ? cam_model[c] : OMV_CAM_KB8;
+        if (a.C.model[c] != OMV_CAM_KB8 && a.C.model[c] != OMV_CAM_PINHOLE) return OMV_ERR_ARG;
     }
     a.n_cams = n_cams, a.inertial = inertial ? 1 : 0, a.far_points = far_points ? 1 : 0;
     a.th_far = th_far_points, a.ratio_factor = 1.5f * scale_factor;
-    // the keyframe views and jobs travel as one device blob: [kf1 | jobs | last_p1]
-    const size_t bytes = sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_jobs + sizeof(int) * n_jobs;
+    return OMV_OK;
+}
+}  // namespace
+
+omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const omv_cnmp_job *jobs, const float *cams,
+                                     const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                                     float th_far_points, float scale_factor, int check_baseline,
+                                     int32_t *side1_state, uint8_t *has_mp1, void *stream) {
+    if (n_jobs < 0 || n_jobs > 64 || (n_jobs > 0 && (!kf1 || !jobs || !cams)) || n_cams < 1 || n_cams > 4) return OMV_ERR_ARG;
+    if (n_jobs == 0 || kf1->kf.n <= 0) return OMV_OK;
+    if (kf1->kf.n >= (1 << 26) || !kf1->kf.kps) return OMV_ERR_ARG;
+    for (int j = 0; j < n_jobs; ++j)
+        if (!jobs[j].match12 || !jobs[j].x3D || !jobs[j].status || !jobs[j].kf2.kf.kps || jobs[j].kf2.kf.n < 0)
+            return OMV_ERR_ARG;
+    CnmpArgs a;
+    if (cnmp_args(cams, cam_model, n_cams, inertial, far_points, th_far_points, scale_factor, a) != OMV_OK)
+        return OMV_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    // the keyframe views and jobs travel as one device blob: [kf1 | jobs | last_p1 | state]
+    const size_t bytes = sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_jobs + sizeof(int) * (n_jobs + 1);
     void *blob = nullptr;
     HIP_OK(hipMallocAsync(&blob, bytes, st));
     char *b = (char *)blob;
@@ -1483,11 +1562,108 @@ omv_status omv_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1, const o
     const omv_cnmp_kf *d_kf1 = (const omv_cnmp_kf *)b;
     const omv_cnmp_job *d_jobs = (const omv_cnmp_job *)(b + sizeof(omv_cnmp_kf));
     int *d_last = (int *)(b + sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_jobs);
+    int *d_state = d_last + n_jobs;   // the entering state, copied so every block reads it before anyone writes
+    if (side1_state) HIP_OK(hipMemcpyAsync(d_state, side1_state, sizeof(int), hipMemcpyDeviceToDevice, st));
+    else HIP_OK(hipMemsetAsync(d_state, 0, sizeof(int), st));
     cnmp_last_kernel<<<n_jobs, kCnmpThreads, 0, st>>>(d_kf1, d_jobs, n_cams, d_last);
-    cnmp_kernel<<<n_jobs, kCnmpThreads, 0, st>>>(d_kf1, d_jobs, d_last, a);
+    cnmp_kernel<<<n_jobs, kCnmpThreads, 0, st>>>(d_kf1, d_jobs, d_last, a, d_state, check_baseline, has_mp1);
+    if (side1_state) cnmp_state_kernel<<<1, 1, 0, st>>>(d_kf1, d_jobs, n_jobs, d_last, d_state, check_baseline, side1_state);
     HIP_OK(hipGetLastError());
     HIP_OK(hipFreeAsync(blob, st));
     return OMV_OK;
+}
+
+// LocalMapping::CreateNewMapPoints' neighbour loop: per neighbour the gated SearchForTriangulation launches (one pair,
+// S slices; the workspace is reused neighbour after neighbour in stream order) and the cnmp launches of one job; the
+// side-1 state and has_mp1 carry from one neighbour to the next in device memory, so the host never waits inside.
+omv_status omv_local_mapping_create_new_map_points(omv_matcher *m, const omv_cnmp_kf *kf1, uint8_t *has_mp1, int n_nb,
+                                                   const omv_cnmp_neighbour *nb, const float *cams,
+                                                   const int32_t *cam_model, int n_cams, int inertial,
+                                                   int check_baseline, int coarse, int far_points, float th_far_points,
+                                                   float scale_factor, int32_t *n_matches, int32_t *side1_state,
+                                                   void *stream) {
+    if (!m || !kf1 || !has_mp1 || n_nb < 0 || n_nb > 64 || (n_nb > 0 && (!nb || !cams || !n_matches)) ||
+        (n_cams != 2 && n_cams != 4))
+        return OMV_ERR_ARG;
+    if (n_nb == 0) return OMV_OK;
+    const omv_kf_view &V1 = kf1->kf;
+    if (V1.n < 0 || V1.n >= (1 << 26) || (V1.n > 0 && (!V1.kps || !V1.desc)) || V1.n_nodes < 0) return OMV_ERR_ARG;
+    for (int j = 0; j < n_nb; ++j) {
+        const omv_kf_view &V2 = nb[j].kf2.kf;
+        if (!nb[j].match12 || !nb[j].x3D || !nb[j].status || V2.n < 0 || (V2.n > 0 && (!V2.kps || !V2.desc || !V2.has_mp)))
+            return OMV_ERR_ARG;
+    }
+    CnmpArgs a;
+    if (cnmp_args(cams, cam_model, n_cams, inertial, far_points, th_far_points, scale_factor, a) != OMV_OK)
+        return OMV_ERR_ARG;
+    TriCams C;
+    for (int c = 0; c < 4; ++c) {
+        for (int q = 0; q < 8; ++q) C.cam[c][q] = cams[8 * c + q];
+        C.model[c] = a.C.model[c];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const omv::MatcherKnobs kn = omv::matcher_knobs(m);
+    int S = 16, ecap = 2048;
+    if (kn.tri_slices >= 0) S = std::max(1, std::min(64, kn.tri_slices));
+    if (kn.tri_ecap >= 0) ecap = std::max(1, kn.tri_ecap);
+    const int tcap = 2 * ecap;
+    // blob: [pairs | kf1 | jobs | last_p1 | state | err | over | cnt | tcnt | ws pk / w / res | tests]
+    std::vector<omv_tri_pair> pairs(n_nb);
+    std::vector<omv_cnmp_job> jobs(n_nb);
+    for (int j = 0; j < n_nb; ++j) {
+        pairs[j].kf1 = V1;
+        pairs[j].kf1.has_mp = has_mp1;
+        pairs[j].kf2 = nb[j].kf2.kf;
+        std::memcpy(pairs[j].T, nb[j].T, sizeof(pairs[j].T));
+        pairs[j].match12 = nb[j].match12;
+        jobs[j].kf2 = nb[j].kf2;
+        jobs[j].match12 = nb[j].match12, jobs[j].x3D = nb[j].x3D, jobs[j].status = nb[j].status;
+    }
+    const size_t head = sizeof(omv_tri_pair) * n_nb + sizeof(omv_cnmp_kf) + sizeof(omv_cnmp_job) * n_nb;
+    const size_t bytes = head + sizeof(int) * (4 + 2 * (size_t)S) + (size_t)S * ecap * 12 + (size_t)S * tcap * 4;
+    char *blob = nullptr;
+    HIP_OK(hipMallocAsync((void **)&blob, bytes, st));
+    omv_tri_pair *d_pairs = reinterpret_cast<omv_tri_pair *>(blob);
+    omv_cnmp_kf *d_kf1 = reinterpret_cast<omv_cnmp_kf *>(blob + sizeof(omv_tri_pair) * n_nb);
+    omv_cnmp_job *d_jobs = reinterpret_cast<omv_cnmp_job *>(d_kf1 + 1);
+    int *d_last = reinterpret_cast<int *>(blob + head), *d_state = d_last + 1, *d_err = d_last + 2;
+    TriWs ws;
+    ws.over = d_last + 3;
+    ws.cnt = d_last + 4, ws.tcnt = ws.cnt + S;
+    ws.pk = reinterpret_cast<uint32_t *>(ws.tcnt + S);
+    ws.w = ws.pk + (size_t)S * ecap;
+    ws.res = ws.w + (size_t)S * ecap;
+    ws.tests = ws.res + (size_t)S * ecap;
+    ws.S = S, ws.ecap = ecap, ws.tcap = tcap;
+    HIP_OK(hipMemcpyAsync(d_pairs, pairs.data(), sizeof(omv_tri_pair) * n_nb, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_kf1, kf1, sizeof(omv_cnmp_kf), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(omv_cnmp_job) * n_nb, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_err, 0, sizeof(int), st));
+    if (side1_state) HIP_OK(hipMemcpyAsync(d_state, side1_state, sizeof(int), hipMemcpyDeviceToDevice, st));
+    else HIP_OK(hipMemsetAsync(d_state, 0, sizeof(int), st));
+    for (int j = 0; j < n_nb; ++j) {
+        TriGate g{};
+        g.p1 = d_state, g.skip = nb[j].skip ? 1 : 0, g.check_baseline = check_baseline ? 1 : 0;
+        std::memcpy(g.Ow1, kf1->Ow, sizeof(g.Ow1));
+        for (int q = 0; q < 3; ++q) g.Ow2[q] = nb[j].kf2.Ow[0][q];
+        g.mb2 = nb[j].kf2.mb;
+        HIP_OK(hipMemsetAsync(ws.over, 0, sizeof(int), st));
+        tri_scan_kernel<<<dim3(S, 1), kTriThreads, 0, st>>>(d_pairs + j, 0, coarse, ws, g);
+        if (!coarse) tri_epi_kernel<<<dim3(kEpiPerSlot, S), kEpiThreads, 0, st>>>(d_pairs + j, C, ws);
+        tri_walk_kernel<<<1, kWalkThreads, 0, st>>>(d_pairs + j, 0, ws, n_matches + j, d_err, kn.tri_walk_seq ? 0 : 1, g);
+        // a neighbour whose candidates overflowed the slices: the one-workgroup search (gated on the device flag)
+        tri_kernel<<<1, kTriThreads, 0, st>>>(d_pairs + j, C, 0, coarse, 0, n_matches + j, d_err, ws.over, g);
+        cnmp_last_kernel<<<1, kCnmpThreads, 0, st>>>(d_kf1, d_jobs + j, n_cams, d_last);
+        cnmp_kernel<<<1, kCnmpThreads, 0, st>>>(d_kf1, d_jobs + j, d_last, a, d_state, check_baseline, has_mp1);
+        cnmp_state_kernel<<<1, 1, 0, st>>>(d_kf1, d_jobs + j, 1, d_last, d_state, check_baseline, d_state);
+    }
+    HIP_OK(hipGetLastError());
+    if (side1_state) HIP_OK(hipMemcpyAsync(side1_state, d_state, sizeof(int), hipMemcpyDeviceToDevice, st));
+    int h_err = 0;
+    HIP_OK(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipFreeAsync(blob, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return h_err ? (omv_status)h_err : OMV_OK;
 }
 
 }  // extern "C"

@@ -135,3 +135,114 @@ def cnmp_kf_struct(kf, d, struct_cls, view_cls, arr):
     for i in range(8):
         s.scale_factors[i] = float(d["scale"][i])
     return s
+
+
+PAIRS = [(0, 0), (0, 1), (1, 0), (1, 1), (0, 2), (2, 0), (2, 2), (1, 3), (3, 1), (3, 3)]
+
+
+def make_cnmp_chain(seed=1, n_neigh=12, n_pts=700, n_distract=200, n_nodes=120, mp_frac1=0.2, mp_frac2=0.3,
+                    close=(0.03, 0.08), bf=40.0):
+    """A whole LocalMapping::CreateNewMapPoints input (LocalMapping.cc:439-783) for the Hilti-like 4-camera
+    KannalaBrandt8 rig: the current keyframe and `n_neigh` neighbours on the synth_ba trajectory that all see one set of
+    world points (so most current-keyframe keypoints are matchable in several neighbours), each keyframe with the
+    reference's [L | R | SL | SR] keypoints (projection + N(0, 0.5 px), octave U{0..3}), descriptors (the point's base
+    descriptor with U{0..6} bit flips), a FeatureVector (a point's observations share its base descriptor's node with
+    probability 0.9), has-map-point flags (mp_frac1 / mp_frac2 of the keypoints), poses, and per neighbour the ten
+    camera-pair transforms SearchForTriangulation uses.  Two neighbours sit `close` metres from the current keyframe,
+    under the stereo baseline mb = bf / fx, so the baseline gate (:447-454) skips them (or not, by side 1's state)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cams, Rbc, tbc = synth_ba.rig()
+    cams = cams[:4].astype(np.float32).copy()
+    Rcb = np.transpose(Rbc[:4], (0, 2, 1))
+    tcb = -np.einsum("cij,cj->ci", Rcb, tbc[:4])
+    t0 = float(rng.uniform(2, 10))
+    dts = [float(rng.choice([-1, 1])) * float(rng.uniform(0.15, 1.2)) for _ in range(n_neigh)]
+    for k in (0, 5):   # the close ones: the first (side 1 still on the left camera) and one later in the order
+        if k < n_neigh:
+            dts[k] = float(rng.choice([-1, 1])) * float(rng.uniform(*close))
+    poses = [_kf_at(t, 4, Rcb, tcb) for t in [t0] + [t0 + dt for dt in dts]]
+    R0, t0c = poses[0]
+    pts, base = [], []
+    for _ in range(n_pts):
+        c = int(rng.integers(0, 4))
+        d = rng.normal(0, 1, 3)
+        d[2] = abs(d[2]) * 1.5 + 0.6
+        d /= np.linalg.norm(d)
+        pts.append(R0[c].T @ (d * rng.uniform(2.0, 25.0) - t0c[c]))
+        base.append(rng.integers(0, 256, 32, dtype=np.uint8))
+    pts = np.array(pts)
+    node_of_pt = np.array([int(b[:4].view(np.uint32)[0]) % n_nodes for b in base])
+    scale = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    sigma2 = (scale * scale).astype(np.float32)
+    kfs = []
+    for k, (Rcw, tcw) in enumerate(poses):
+        blocks = [[] for _ in range(4)]
+        rot_off = float(rng.uniform(-20, 20))
+        for p in range(n_pts):
+            for c in range(4):
+                X = Rcw[c] @ pts[p] + tcw[c]
+                if X[2] < 0.3:
+                    continue
+                uv = synth_ba.cam_project(cams[c].astype(np.float64), X, False)
+                if not (5 <= uv[0] <= 715 and 5 <= uv[1] <= 535):
+                    continue
+                uv = uv + rng.normal(0, 0.5, 2)
+                dsc = base[p].copy()
+                for _ in range(int(rng.integers(0, 7))):
+                    bit = int(rng.integers(0, 256))
+                    dsc[bit // 8] ^= np.uint8(1 << (bit % 8))
+                ang = ((37.0 * p) % 360.0 + rot_off + float(rng.normal(0, 3))) % 360.0
+                node = node_of_pt[p] if rng.random() < 0.9 else int(rng.integers(0, n_nodes))
+                blocks[c].append((uv[0], uv[1], int(rng.integers(0, 4)), ang, dsc, node, p))
+        for _ in range(n_distract):
+            c = int(rng.integers(0, 4))
+            blocks[c].append((float(rng.uniform(20, 700)), float(rng.uniform(20, 520)), int(rng.integers(0, 4)),
+                              float(rng.uniform(0, 360)), rng.integers(0, 256, 32, dtype=np.uint8),
+                              int(rng.integers(0, n_nodes)), -1))
+        for c in range(4):
+            rng.shuffle(blocks[c])
+        rows = [r for c in range(4) for r in blocks[c]]
+        n = len(rows)
+        kps = np.zeros(n, KP_DTYPE)
+        kps["x"], kps["y"], kps["octave"] = [r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows]
+        kps["angle"] = [r[3] for r in rows]
+        kps["size"], kps["response"] = 31.0, 10.0
+        desc = np.stack([r[4] for r in rows]).astype(np.uint8)
+        node = np.array([r[5] for r in rows])
+        ids = np.unique(node).astype(np.uint32)
+        order = np.lexsort((np.arange(n), node))
+        node_start = np.concatenate([np.searchsorted(node[order], ids), [n]]).astype(np.int32)
+        Tcw = np.zeros((4, 12), np.float32)
+        Ow = np.zeros((4, 3), np.float32)
+        for c in range(4):
+            Tcw[c] = np.hstack([Rcw[c], tcw[c][:, None]]).astype(np.float32).ravel()
+            Ow[c] = (-Rcw[c].T @ tcw[c]).astype(np.float32)
+        kfs.append(dict(n=n, n_left=len(blocks[0]), n_right=len(blocks[1]), n_sideleft=len(blocks[2]), kps=kps,
+                        desc=desc, has_mp=(rng.random(n) < (mp_frac1 if k == 0 else mp_frac2)).astype(np.uint8),
+                        node_id=ids, node_start=node_start, node_idx=order.astype(np.int32),
+                        pt=np.array([r[6] for r in rows], np.int32), Tcw=Tcw, Ow=Ow,
+                        Rwc=Tcw[0].reshape(3, 4)[:, :3].T.copy().ravel(), twc=Ow[0].copy(),
+                        uright=np.full(n, -1, np.float32), depth=np.full(n, -1, np.float32)))
+    R1, t1 = poses[0]
+    nbs = []
+    for k in range(1, n_neigh + 1):
+        R2, t2 = poses[k]
+        T = np.zeros((10, 12), np.float32)
+        for i, (c1, c2) in enumerate(PAIRS):
+            Rw2, tw2 = R2[c2].T, -R2[c2].T @ t2[c2]
+            T[i, :9] = (R1[c1] @ Rw2).ravel()
+            T[i, 9:] = R1[c1] @ tw2 + t1[c1]
+        nbs.append(dict(kf2=kfs[k], T=T, skip=0))
+    fx, fy, cx, cy = (float(v) for v in cams[0, :4])
+    return dict(kf1=kfs[0], nbs=nbs, pts=pts, cams=cams, cam_model=np.zeros(4, np.int32), n_cams=4, fx=fx, fy=fy,
+                cx=cx, cy=cy, mb=bf / fx, mbf=bf, scale=scale, sigma2=sigma2, scale_factor=1.2)
+
+
+def chain_kf_struct(kf, d, struct_cls, view_cls, arr, has_mp=None):
+    """omv_cnmp_kf with the full omv_kf_view SearchForTriangulation reads (desc, has_mp, FeatureVector)."""
+    s = cnmp_kf_struct(kf, d, struct_cls, view_cls, arr)
+    s.kf.desc = arr(kf["desc"])
+    s.kf.has_mp = arr(kf["has_mp"] if has_mp is None else has_mp)
+    s.kf.n_nodes = int(len(kf["node_id"]))
+    s.kf.node_id, s.kf.node_start, s.kf.node_idx = arr(kf["node_id"]), arr(kf["node_start"]), arr(kf["node_idx"])
+    return s

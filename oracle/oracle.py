@@ -717,9 +717,10 @@ def normal_depth(obs_start, obs_center, pos, ref_center, ref_level_scale, ref_ma
     return normal, dmin, dmax
 
 
-def create_new_map_points(d, inertial=True, far_points=False, th_far=50.0):
-    """LocalMapping::CreateNewMapPoints' geometry restated (tri_oracle.cpp) on a synth_cnmp set: per neighbour
-    (status [kf1.n] int32: 1 triangulated, 2 UnprojectStereo, 0 none; x3D [kf1.n][3] float32)."""
+def create_new_map_points(d, inertial=True, far_points=False, th_far=50.0, check_baseline=False, side1_state=0):
+    """omv_create_new_map_points restated (tri_oracle.cpp) on a synth_cnmp set: the jobs in order with the state chain.
+    Returns per job (status [kf1.n] int32: 1 triangulated, 2 UnprojectStereo, 0 none; x3D [kf1.n][3] float32); the
+    has_mp1 marks and the final side-1 state are attached as attributes of the returned list."""
     from openmavis_amd._lib import CnmpJob, CnmpKf, KfView
     from openmavis_amd.synth_cnmp import cnmp_kf_struct
     keep = []
@@ -741,8 +742,66 @@ def create_new_map_points(d, inertial=True, far_points=False, th_far=50.0):
         outs.append((st, x))
     cams = np.ascontiguousarray(d["cams"], np.float32)
     cm = np.ascontiguousarray(d["cam_model"], np.int32)
+    has_mp1 = np.zeros(max(int(d["kf1"]["n"]), 1), np.uint8)
+    s1 = np.array([side1_state], np.int32)
     lib().oracle_create_new_map_points(ctypes.c_int(len(d["jobs"])), ctypes.byref(k1), jobs, _p(cams), _p(cm),
                                        ctypes.c_int(d["n_cams"]), ctypes.c_int(int(inertial)),
                                        ctypes.c_int(int(far_points)), ctypes.c_float(th_far),
-                                       ctypes.c_float(d["scale_factor"]))
+                                       ctypes.c_float(d["scale_factor"]), ctypes.c_int(int(check_baseline)), _p(s1),
+                                       _p(has_mp1))
+    outs = _Outs(outs)
+    outs.has_mp1, outs.side1 = has_mp1[:int(d["kf1"]["n"])], int(s1[0])
     return outs
+
+
+class _Outs(list):
+    pass
+
+
+def local_mapping_create_new_map_points(d, inertial=True, monocular=False, coarse=False, far_points=False,
+                                        th_far=50.0, side1_state=0, has_mp1=None, nb_range=None):
+    """LocalMapping::CreateNewMapPoints' whole neighbour loop restated (tri_oracle.cpp) on a synth_cnmp.make_cnmp_chain
+    set: (has_mp1 [kf1.n] uint8, n_matches [n_neigh], per neighbour (match12, status, x3D), final side-1 state).
+    nb_range = (lo, hi) runs only those neighbours, from `has_mp1` / `side1_state` (composition checks)."""
+    from openmavis_amd._lib import CnmpJob, CnmpKf, KfView, TriPair
+    from openmavis_amd.synth_cnmp import chain_kf_struct
+    from openmavis_amd.synth_tri import kf_struct
+    keep = []
+
+    def arr(a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    nbs = d["nbs"] if nb_range is None else d["nbs"][nb_range[0]:nb_range[1]]
+    n1 = int(d["kf1"]["n"])
+    k1 = chain_kf_struct(d["kf1"], d, CnmpKf, KfView, arr)
+    pairs = (TriPair * max(len(nbs), 1))()
+    jobs = (CnmpJob * max(len(nbs), 1))()
+    outs = []
+    for j, nb in enumerate(nbs):
+        pairs[j].kf1 = kf_struct(d["kf1"], KfView, d["sigma2"], lambda _n, a: arr(a))
+        pairs[j].kf2 = kf_struct(nb["kf2"], KfView, d["sigma2"], lambda _n, a: arr(a))
+        for i in range(10):
+            for q in range(12):
+                pairs[j].T[i][q] = float(nb["T"][i, q])
+        m12 = np.full(max(n1, 1), -9, np.int32)
+        st = np.full(max(n1, 1), -9, np.int32)
+        x = np.full((max(n1, 1), 3), np.nan, np.float32)
+        pairs[j].match12 = arr(m12)
+        jobs[j].kf2 = chain_kf_struct(nb["kf2"], d, CnmpKf, KfView, arr)
+        jobs[j].match12, jobs[j].x3D, jobs[j].status = pairs[j].match12, arr(x), arr(st)
+        keep.extend([m12, st, x])
+        outs.append((m12, st, x))
+    skip = np.ascontiguousarray([int(nb.get("skip", 0)) for nb in nbs] or [0], np.int32)
+    hm = np.array(d["kf1"]["has_mp"] if has_mp1 is None else has_mp1, np.uint8, copy=True)
+    n_matches = np.zeros(max(len(nbs), 1), np.int32)
+    s1 = np.array([side1_state], np.int32)
+    cams = np.ascontiguousarray(d["cams"], np.float32)
+    cm = np.ascontiguousarray(d["cam_model"], np.int32)
+    lib().oracle_local_mapping_create_new_map_points(
+        ctypes.byref(k1), _p(hm), ctypes.c_int(len(nbs)), pairs, jobs, _p(skip), _p(cams), _p(cm),
+        ctypes.c_int(d["n_cams"]), ctypes.c_int(int(inertial)), ctypes.c_int(int(not monocular)),
+        ctypes.c_int(int(coarse)), ctypes.c_int(int(far_points)), ctypes.c_float(th_far),
+        ctypes.c_float(d["scale_factor"]), _p(n_matches), _p(s1))
+    return hm, n_matches[:len(nbs)], [(m[:n1], s[:n1], x[:n1]) for m, s, x in outs], int(s1[0])

@@ -488,25 +488,26 @@ bool unproject_stereo(const omv_cnmp_kf &K, int i, const float *depth, float *x3
     for (int r = 0; r < 3; ++r) x3D[r] = (K.Rwc[3 * r] * c[0] + K.Rwc[3 * r + 1] * c[1] + K.Rwc[3 * r + 2] * c[2]) + K.twc[r];
     return true;
 }
-}  // namespace
 
-extern "C" {
-// Host arrays throughout (match12 / uright / depth / x3D / status host pointers in this restatement).
-void oracle_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1p, const omv_cnmp_job *jobs, const float *cams,
-                                  const int32_t *cam_model, int n_cams, int inertial, int far_points,
-                                  float th_far_points, float scale_factor) {
-    const omv_cnmp_kf &K1 = *kf1p;
+// One neighbour of the loop (:443-782): the baseline gate on the persistent Ow1 (:447-454), then every match in idx1
+// order with the camera-pair state; p1 (sophTcw1 / Ow1's camera block) persists across neighbours and is updated in
+// place; has_mp1 (may be null) receives AddMapPoint(pMP, idx1) (:773).  Returns false when the gate skips it.
+bool cnmp_job(const omv_cnmp_kf &K1, const omv_cnmp_job &J, const float *cams, const int32_t *cam_model, int n_cams,
+              int inertial, int far_points, float th_far_points, float scale_factor, int check_baseline, int &p1,
+              uint8_t *has_mp1) {
     auto model = [&](int c) { return cam_model ? cam_model[c] : OMV_CAM_KB8; };
     const float ratioFactor = 1.5f * scale_factor;
-    int p1 = 0;   // sophTcw1 / Ow1 (camera block), persists across neighbours
-    for (int j = 0; j < n_jobs; ++j) {
-        const omv_cnmp_job &J = jobs[j];
-        const omv_cnmp_kf &K2 = J.kf2;
-        int c1 = 0, c2 = 0, p2 = 0;   // pCamera1 / pCamera2 / sophTcw2: reset per neighbour
+    const omv_cnmp_kf &K2 = J.kf2;
+    for (int idx1 = 0; idx1 < K1.kf.n; ++idx1) J.status[idx1] = 0;
+    if (check_baseline) {   // vBaseline = Ow2 - Ow1; baseline = vBaseline.norm(); if (baseline < pKF2->mb) continue;
+        const float v[3] = {K2.Ow[0][0] - K1.Ow[p1][0], K2.Ow[0][1] - K1.Ow[p1][1], K2.Ow[0][2] - K1.Ow[p1][2]};
+        if (norm3(v) < K2.mb) return false;
+    }
+    int c1 = 0, c2 = 0, p2 = 0;   // pCamera1 / pCamera2 / sophTcw2: reset per neighbour
+    {
         for (int idx1 = 0; idx1 < K1.kf.n; ++idx1) {
-            J.status[idx1] = 0;
             const int idx2 = J.match12[idx1];
-            if (idx2 < 0) continue;
+            if (idx2 < 0 || idx2 >= K2.kf.n) continue;
             const omv_kp &kp1 = K1.kf.kps[idx1], &kp2 = K2.kf.kps[idx2];
             const int cameraId1 = cnmp_cam(K1.kf, idx1), cameraId2 = cnmp_cam(K2.kf, idx2);
             const float kp1_ur = K1.uright ? K1.uright[idx1] : -1.f, kp2_ur = K2.uright ? K2.uright[idx2] : -1.f;
@@ -592,7 +593,56 @@ void oracle_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1p, const omv
             if (ratioDist * ratioFactor < ratioOctave || ratioDist > ratioOctave * ratioFactor) continue;
             J.status[idx1] = bPointStereo ? 2 : 1;
             for (int q = 0; q < 3; ++q) J.x3D[3 * idx1 + q] = x3D[q];
+            if (has_mp1) has_mp1[idx1] = 1;
         }
     }
+    return true;
+}
+}  // namespace
+
+extern "C" {
+// omv_create_new_map_points restated: the jobs in order with the state chain (host arrays throughout: match12 / uright
+// / depth / x3D / status / has_mp1 host pointers in this restatement).  side1_state: in/out (null: 0).
+void oracle_create_new_map_points(int n_jobs, const omv_cnmp_kf *kf1p, const omv_cnmp_job *jobs, const float *cams,
+                                  const int32_t *cam_model, int n_cams, int inertial, int far_points,
+                                  float th_far_points, float scale_factor, int check_baseline, int32_t *side1_state,
+                                  uint8_t *has_mp1) {
+    int p1 = side1_state ? *side1_state : 0;   // sophTcw1 / Ow1 (camera block), persists across neighbours
+    for (int j = 0; j < n_jobs; ++j)
+        cnmp_job(*kf1p, jobs[j], cams, cam_model, n_cams, inertial, far_points, th_far_points, scale_factor,
+                 check_baseline, p1, has_mp1);
+    if (side1_state) *side1_state = p1;
+}
+
+// LocalMapping::CreateNewMapPoints' whole neighbour loop (:439-783): per neighbour the caller's skip (mbMonocular's
+// median-depth test), the baseline gate, SearchForTriangulation(mpCurrentKeyFrame, pKF2, vMatchedIndices, false,
+// bCoarse) with checkOri off (matcher(0.6, false), :417) against has_mp1 AS THE PREVIOUS NEIGHBOURS LEFT IT, then the
+// geometry, whose accepted matches set has_mp1.  pairs[j]: kf1 / kf2 views, T, match12 (host); the kf1 view's has_mp is
+// replaced by has_mp1.  n_matches[j]: the search's return value (0 when skipped).
+void oracle_local_mapping_create_new_map_points(const omv_cnmp_kf *kf1p, uint8_t *has_mp1, int n_nb,
+                                                const omv_tri_pair *pairs, const omv_cnmp_job *jobs, const int32_t *skip,
+                                                const float *cams, const int32_t *cam_model, int n_cams, int inertial,
+                                                int check_baseline, int coarse, int far_points, float th_far_points,
+                                                float scale_factor, int32_t *n_matches, int32_t *side1_state) {
+    const omv_cnmp_kf &K1 = *kf1p;
+    int p1 = side1_state ? *side1_state : 0;
+    for (int j = 0; j < n_nb; ++j) {
+        const omv_cnmp_job &J = jobs[j];
+        for (int i = 0; i < K1.kf.n; ++i) J.status[i] = 0, pairs[j].match12[i] = -1;
+        n_matches[j] = 0;
+        if (skip && skip[j]) continue;
+        if (check_baseline) {
+            const float v[3] = {J.kf2.Ow[0][0] - K1.Ow[p1][0], J.kf2.Ow[0][1] - K1.Ow[p1][1],
+                                J.kf2.Ow[0][2] - K1.Ow[p1][2]};
+            if (norm3(v) < J.kf2.mb) continue;
+        }
+        omv_tri_pair P = pairs[j];
+        P.kf1.has_mp = has_mp1;
+        n_matches[j] = oracle_search_for_triangulation(&P, cams, cam_model, 0, coarse, 0);
+        omv_cnmp_job Jm = J;
+        Jm.match12 = P.match12;
+        cnmp_job(K1, Jm, cams, cam_model, n_cams, inertial, far_points, th_far_points, scale_factor, 0, p1, has_mp1);
+    }
+    if (side1_state) *side1_state = p1;
 }
 }  // extern "C"

@@ -98,3 +98,25 @@ def test_pose_optimization_batch_and_determinism(oracle):
             np.testing.assert_allclose(g1[0][ff], ref[0][f], rtol=0, atol=1e-7)
             np.testing.assert_allclose(g1[1][ff], ref[1][f], rtol=0, atol=1e-7)
             assert g1[3][ff] == ref[3][f]
+
+
+@pytest.mark.parametrize("case", [dict(n_cams=4, n_pts=1400, outlier_frac=0.15),
+                                  dict(n_cams=1, n_pts=2600, stereo_frac=0.5, outlier_frac=0.15)],
+                         ids=["rig4_1400", "pinhole_stereo_2600"])
+def test_pose_optimization_many_edges(oracle, case):
+    """Frames with more than 512 edges take pose_only_kernel's overflow path (edges past the register-resident 512
+    reloaded from memory, their active flags / chi2 in global memory across the LM loop and the outlier
+    classification): >= 1,200 edges per frame, mono and stereo, with outliers among the edges past 512."""
+    b = synth_pose.make_pose_only_batch(n_frames=3, seed=77, **case)
+    ne = [int(b["mono_start"][f + 1] - b["mono_start"][f] + b["stereo_start"][f + 1] - b["stereo_start"][f])
+          for f in range(3)]
+    assert min(ne) >= 1200, ne
+    ref = oracle.pose_optimization(b)
+    got = _run_gpu(b)
+    _check(b, ref, got)
+    # outliers flagged among the edges the overflow path carries (edge order: mono then stereo)
+    for f in range(3):
+        kps = np.concatenate([b["mono_kp"][b["mono_start"][f]:b["mono_start"][f + 1]],
+                              b["stereo_kp"][b["stereo_start"][f]:b["stereo_start"][f + 1]]])
+        assert got[2][f][kps[512:]].any(), f
+    assert (got[3] > 0).all()
