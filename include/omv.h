@@ -832,6 +832,68 @@ omv_status omv_mappoint_normal_depth(int n_points, const int32_t *obs_start, con
                                      float *normal, float *min_dist, float *max_dist, void *stream);
 
 
+/* ---- LocalMapping::SearchInNeighbors' fuse sequence (src/LocalMapping.cc:837-889) ------------------------------------
+ * The reference runs ORBmatcher::Fuse (ORBmatcher.cc:1458-1647) as a chain of calls that mutate the map between (and
+ * within) calls: phase A fuses the current keyframe's map points (ONE snapshot of GetMapPointMatches(), :839) into every
+ * target keyframe, camera block by camera block (:840-853); phase B fuses the target keyframes' map points (collected
+ * AFTER phase A, non-bad, first occurrence, :859-881) into the current keyframe (:883-889).  Each accepted match either
+ * AddObservation + AddMapPoint's, or Replace's the weaker of the two points (MapPoint.cc:316-380: observations moved,
+ * the loser bad, the survivor's descriptor recomputed by ComputeDistinctiveDescriptors, :405-483).  A later point's
+ * decision reads that state: isBad(), IsInKeyFrame(pKF), GetMapPoint(bestIdx), Observations() and -- through the
+ * window search -- GetDescriptor().
+ * Here the window searches of every (job, point) are evaluated on the device speculatively (one omv_matcher_search_kf
+ * launch per phase), the decisions are walked in the reference's order on the host against the flattened graph, and an
+ * entry whose point's descriptor changed since its evaluation (a Replace survivor) is re-evaluated on the device with
+ * the recomputed descriptor before it is used (the recomputation itself on the device: the distinctive-descriptor
+ * kernel over the observation rows the reference's ComputeDistinctiveDescriptors reads at that moment).  The result is
+ * the reference's graph after phase B, plus the ordered edit log a caller replays with the reference's own methods.
+ * Phase C (:891-900: ComputeDistinctiveDescriptors / UpdateNormalAndDepth of the current keyframe's points) is
+ * omv_mappoint_* on the caller's side.
+ * Keyframes are the n_kf frames of the matcher's last omv_matcher_assign_grid batch (C = geom->n_cams <= 4 camera blocks,
+ * N-index = block offset + index in the block, NLeft / NRight / NSideLeft = n_kp[kf][0..2]), NUMBERED IN THE ORDER OF
+ * THE MAP POINTS' std::map<KeyFrame*, ...> KEYS (observations are kept sorted by keyframe index). */
+typedef struct omv_fuse_graph {
+    /* keyframes (host) */
+    int n_kf;
+    const int32_t *n_blocks;            /* [n_kf] camera blocks Fuse runs on: 1 (NLeft == -1), 2, or 4 (side cameras) */
+    const omv_se3f *Tcw;                /* [n_kf][C] GetPose / GetRightPose / GetSideLeftPose / GetSideRightPose */
+    const float *Ow;                    /* [n_kf][C][3] the matching camera centres */
+    const float *uright;                /* [n_kf][kp_cap] mvuRight of block 0 (host; AddObservation's nObs += 2 when
+                                           the keyframe has one camera), or NULL */
+    int32_t *kf_mps;                    /* [n_kf][C * kp_cap] in/out: mvpMapPoints by N-index (entries [0, N) of each
+                                           keyframe's row): map-point index or -1 */
+    /* map points (host): the snapshot of the points the keyframes reference */
+    int n_mps;
+    int32_t *bad;                       /* [n_mps] in/out isBad() */
+    int32_t *n_obs;                     /* [n_mps] in/out Observations() (nObs) */
+    int32_t *replaced;                  /* [n_mps] out: the point it was Replace'd by, or -1 */
+    const int32_t *obs_start;           /* [n_mps + 1] in: mObservations rows, keyframe order */
+    const int32_t *obs_kf;              /* [rows] keyframe index */
+    const int32_t *obs_idx;             /* [rows][4] left / right / side-left / side-right N-index or -1 */
+    /* out: the final mObservations (CSR with capacity), the edit log */
+    int32_t *out_obs_start;             /* [n_mps + 1] */
+    int32_t *out_obs_kf;                /* [obs_cap] */
+    int32_t *out_obs_idx;               /* [obs_cap][4] */
+    int obs_cap;
+    int32_t *log;                       /* [log_cap][4]: {0, mp, kf, idx} AddObservation(pKF, idx) + pKF->AddMapPoint;
+                                           {1, a, b, -1} a->Replace(b); in the reference's order */
+    int log_cap;
+    int32_t n_log;                      /* out: entries written (OMV_ERR_CAPACITY past log_cap / obs_cap) */
+    int32_t n_reevaluated;              /* out: entries re-evaluated after a descriptor change (diagnostic) */
+    int32_t n_device_calls;             /* out: device round trips (diagnostic) */
+} omv_fuse_graph;
+
+/* current: the current keyframe's index; targets: host [n_targets] vpTargetKFs in order; mps: the device map-point
+ * table (pos / normal / min_dist / max_dist as GetWorldPos / GetNormal / mfMinDistance / mfMaxDistance; desc is
+ * UPDATED IN PLACE to the final descriptors); p: omv_kf_search_params with mode OMV_KF_FUSE, th 3, max_dist TH_LOW
+ * (50); geom / kps / desc / n_kp: the assign_grid batch (device).  n_fused: host [n_targets * C + C] per Fuse call,
+ * phase A (target-major, block-minor) then phase B; calls the reference does not make (blocks past n_blocks) are 0.
+ * Synchronous. */
+omv_status omv_search_in_neighbors_fuse(omv_matcher *m, const omv_frame_geom *geom, const omv_kp *kps,
+                                        const uint8_t *desc, const int *n_kp, int kp_cap, omv_fuse_graph *g,
+                                        int current, int n_targets, const int32_t *targets, const omv_kf_mps *mps,
+                                        const omv_kf_search_params *p, int32_t *n_fused, void *stream);
+
 /* ---- LocalMapping::CreateNewMapPoints (src/LocalMapping.cc:395-783) ---------------------------------------------------
  * The reference walks the current keyframe's neighbours in order (:439).  Per neighbour pKF2: the baseline test
  * (:447-461: |Ow2 - Ow1| < pKF2->mb skips it when !mbMonocular; Ow1 is the PERSISTENT side-1 camera centre, see below),

@@ -184,6 +184,17 @@ class CnmpJob(ctypes.Structure):
     _fields_ = [("kf2", CnmpKf), ("match12", ctypes.c_void_p), ("x3D", ctypes.c_void_p), ("status", ctypes.c_void_p)]
 
 
+class FuseGraph(ctypes.Structure):
+    """omv_fuse_graph (include/omv.h)."""
+    _fields_ = [("n_kf", ctypes.c_int), ("n_blocks", ctypes.c_void_p), ("Tcw", ctypes.c_void_p), ("Ow", ctypes.c_void_p),
+                ("uright", ctypes.c_void_p), ("kf_mps", ctypes.c_void_p), ("n_mps", ctypes.c_int),
+                ("bad", ctypes.c_void_p), ("n_obs", ctypes.c_void_p), ("replaced", ctypes.c_void_p),
+                ("obs_start", ctypes.c_void_p), ("obs_kf", ctypes.c_void_p), ("obs_idx", ctypes.c_void_p),
+                ("out_obs_start", ctypes.c_void_p), ("out_obs_kf", ctypes.c_void_p), ("out_obs_idx", ctypes.c_void_p),
+                ("obs_cap", ctypes.c_int), ("log", ctypes.c_void_p), ("log_cap", ctypes.c_int), ("n_log", ctypes.c_int32),
+                ("n_reevaluated", ctypes.c_int32), ("n_device_calls", ctypes.c_int32)]
+
+
 class CnmpNeighbour(ctypes.Structure):
     """omv_cnmp_neighbour (include/omv.h)."""
     _fields_ = [("kf2", CnmpKf), ("T", (ctypes.c_float * 12) * 10), ("skip", ctypes.c_int),
@@ -298,6 +309,8 @@ SIGNATURES = {
     "omv_matcher_search_kf": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(KfSearchJob),
                                    _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP, _VP, _VP,
                                    _VP]),
+    "omv_search_in_neighbors_fuse": (_I, [_VP, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(FuseGraph),
+                                          _I, _I, _VP, ctypes.POINTER(KfMps), ctypes.POINTER(KfSearchParams), _VP, _VP]),
     "omv_matcher_search_by_sim3": (_I, [_VP, _I, ctypes.POINTER(FrameGeom), _VP, _VP, _VP, _I, ctypes.POINTER(Sim3Job),
                                         _I, _VP, _VP, _I, _VP, _VP, ctypes.POINTER(KfMps), _F, _F, _I, _VP, _VP, _VP]),
     "omv_imu_preintegrate": (_I, [_I, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),

@@ -17,7 +17,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OMV_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["orb_extract.hip", "match.hip", "lba.hip", "pose.hip", "tri.hip", "frame.hip", "imu.hip", "bow.hip", "bowmatch.hip",
-               "mappoint.hip"]
+               "mappoint.hip", "fuse.hip"]
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
              f"--offload-arch={ARCH}", "-Wno-unused-result"]
 OBJ_DIR = os.path.join(ROOT, "build", "obj")

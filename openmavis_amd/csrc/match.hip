@@ -2390,6 +2390,9 @@ struct omv_matcher {
 };
 
 omv::MatcherKnobs omv::matcher_knobs(const omv_matcher *m) { return m ? m->knobs : omv::MatcherKnobs{}; }
+size_t omv::matcher_kf_entry_cap(const omv_matcher *m) {
+    return m ? (size_t)m->max_frames * m->n_cams * std::max(1, m->max_mps) : 0;
+}
 
 static hipEvent_t mk_event(hipStream_t st) {
     hipEvent_t e;

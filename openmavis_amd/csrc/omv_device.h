@@ -253,5 +253,7 @@ struct MatcherKnobs {
     int cand_pw = -1;      // OMV_CAND_PW: map points per wave of the LDS-staged candidate kernel
 };
 MatcherKnobs matcher_knobs(const struct ::omv_matcher *m);
+// omv_matcher_search_kf's entry capacity of a handle (max_frames x n_cams x max_mps)
+size_t matcher_kf_entry_cap(const struct ::omv_matcher *m);
 
 }  // namespace omv

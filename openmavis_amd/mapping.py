@@ -150,3 +150,57 @@ def CreateNewMapPoints(d, matcher, inertial=True, monocular=False, coarse=False,
     return (c.has_mp1[:n1].cpu().numpy(), c.n_matches.cpu().numpy(),
             [(m[:n1].cpu().numpy(), s[:n1].cpu().numpy(), x[:n1].cpu().numpy()) for m, s, x in outs],
             int(c.side1.item()))
+
+
+def SearchInNeighborsFuse(s, matcher, th=3.0, device="cuda:0", obs_cap=None, log_cap=None, stream=None):
+    """LocalMapping::SearchInNeighbors' fuse sequence (src/LocalMapping.cc:837-889) on a flattened map (the
+    synth_fuse.make_fuse_scene layout: keyframes as one multi-camera batch, mvpMapPoints, map points with their
+    observations / nObs / isBad and the device table pos / normal / min / max / desc) through
+    omv_search_in_neighbors_fuse: every window search on the device (speculative per phase, stale entries re-evaluated
+    after Replace's descriptor recomputation, itself on the device), the decisions walked in the reference's order.
+    Returns dict(kf_mps, bad, n_obs, replaced, obs_start, obs_kf, obs_idx, log, n_fused, desc (final descriptors,
+    numpy), n_reevaluated, n_device_calls)."""
+    import torch
+    from .matcher import FrameBatch, kf_search_params
+    K, C, cap = int(s["n_kf"]), int(s["n_cams"]), int(s["kp_cap"])
+    scale = [1.0]
+    for _ in range(1, int(s["nlevels"])):
+        scale.append(float(np.float32(scale[-1] * np.float32(1.2))))
+    kfs = FrameBatch(torch, K, C, cap, s["width"], s["height"], scale, device=device)
+    kfs.kps.copy_(torch.from_numpy(np.ascontiguousarray(s["kps"]).view(np.int32).reshape(K, C, cap, 6)))
+    kfs.desc.copy_(torch.from_numpy(np.ascontiguousarray(s["desc"])))
+    kfs.n_kp.copy_(torch.from_numpy(np.ascontiguousarray(s["n_kp"], np.int32)))
+    mps = {k: torch.from_numpy(np.array(v, copy=True)).to(device) for k, v in s["mps"].items()}
+    ur = torch.from_numpy(np.ascontiguousarray(s["uright"], np.float32)).to(device)
+    p = kf_search_params(th, 50.0, s["cams"], bf=float(s["bf"]), nlevels=int(s["nlevels"]), uright=ur)
+    p.mode = _lib.OMV_KF_FUSE
+    # the handle's entry capacity: phase A evaluates every (target block, current-keyframe point) at once
+    n_cur = int(np.asarray(s["n_kp"])[int(s["current"])].sum())
+    n_e = len(s["targets"]) * C * n_cur
+    h = matcher._handle(kfs, max(1, -(-n_e // (K * C))))
+    matcher.AssignFeaturesToGrid(kfs, stream)
+    keep = []
+
+    def arr(a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    from .synth_fuse import fuse_graph_struct
+    obs_cap = obs_cap or 4 * len(s["obs_kf"]) + 1024
+    log_cap = log_cap or 4 * int(s["n_mps"]) + 1024
+    out = {}
+    G = fuse_graph_struct(s, _lib.FuseGraph, arr, out, obs_cap, log_cap)
+    T = len(s["targets"])
+    n_fused = np.zeros(T * C + C, np.int32)
+    m = _lib.KfMps(*[_lib.ptr(mps[k]) for k in ("pos", "normal", "min_dist", "max_dist", "desc")])
+    st = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    _lib.check(matcher._lib.omv_search_in_neighbors_fuse(
+        h, ctypes.byref(kfs.geom), _lib.ptr(kfs.kps), _lib.ptr(kfs.desc), _lib.ptr(kfs.n_kp), cap, ctypes.byref(G),
+        int(s["current"]), T, arr(np.ascontiguousarray(s["targets"], np.int32)), ctypes.byref(m), ctypes.byref(p),
+        arr(n_fused), st), "omv_search_in_neighbors_fuse")
+    n_rows = int(out["out_obs_start"][-1])
+    return dict(kf_mps=out["kf_mps"], bad=out["bad"], n_obs=out["n_obs"], replaced=out["replaced"][:int(s["n_mps"])],
+                obs_start=out["out_obs_start"], obs_kf=out["out_obs_kf"][:n_rows], obs_idx=out["out_obs_idx"][:n_rows],
+                log=out["log"][:G.n_log], n_fused=n_fused, desc=mps["desc"].cpu().numpy(),
+                n_reevaluated=int(G.n_reevaluated), n_device_calls=int(G.n_device_calls))

@@ -25,7 +25,9 @@
 // kp_to_mp / occ_init indexed by slot = cam * kp_cap + i (F.mvpMapPoints in padded form).
 // Parity status: no reference test pins these functions; parity is to this restatement.
 // =====================================================================================================
+#include <array>
 #include <cmath>
+#include <map>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -817,3 +819,242 @@ int oracle_search_for_initialization(const FrameGeom *g, const KP *kps1, const u
 }
 
 }  // extern "C"
+
+// ---- LocalMapping::SearchInNeighbors' fuse sequence                     src/LocalMapping.cc:837-889
+//   ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID)                       src/ORBmatcher.cc:1458-1647
+//   MapPoint::AddObservation / Replace / ComputeDistinctiveDescriptors    src/MapPoint.cc:199-226, :316-380, :405-483
+//   KeyFrame::AddMapPoint / ReplaceMapPointMatch / EraseMapPointMatch / GetMapPoint (mvpMapPoints[idx])
+// Written literally: every decision reads the map as the previous decisions left it, every window search runs when the
+// loop reaches the point (with its descriptor of that moment).  mObservations is a std::map keyed by KeyFrame*: keyed
+// here by keyframe index (the adapter numbers keyframes in pointer order).  No mnFuseTargetForKF / covisibility: the
+// target list is the caller's; phase C (:891-900) is not part of this restatement.
+extern "C" void oracle_distinctive_descriptors(int n_points, const int32_t *desc_start, const int32_t *desc_row,
+                                               const uint8_t *desc, int32_t *best_row);
+namespace {
+struct FuseMap {
+    const FrameGeom *g;
+    const KP *kps;
+    const uint8_t *desc;
+    const int *n_kp;
+    int kp_cap, C;
+    omv_fuse_graph *G;
+    const float *pos, *normal, *min_d, *max_d;
+    uint8_t *mp_desc;
+    const omv_kf_search_params *p;
+    std::vector<View> views;
+    std::vector<std::map<int, std::array<int, 4>>> obs;
+    int n_log = 0;
+
+    int N(int kf) const {
+        int n = 0;
+        for (int c = 0; c < C; ++c) n += n_kp[(size_t)kf * C + c];
+        return n;
+    }
+    int *mvp(int kf) { return G->kf_mps + (size_t)kf * C * kp_cap; }
+    const uint8_t *row_desc(int kf, int idx) const {   // pKF->mDescriptors.row(idx)
+        int c = 0, off = 0;
+        while (c + 1 < C && idx >= off + n_kp[(size_t)kf * C + c]) off += n_kp[(size_t)kf * C + c], ++c;
+        return desc + (((size_t)kf * C + c) * kp_cap + (idx - off)) * 32;
+    }
+    void log(int a, int b, int c, int d) {
+        if (n_log < G->log_cap) {
+            int32_t *r = G->log + 4 * (size_t)n_log;
+            r[0] = a, r[1] = b, r[2] = c, r[3] = d;
+        }
+        ++n_log;
+    }
+    bool IsInKeyFrame(int mp, int kf) const { return obs[mp].count(kf) > 0; }
+    void AddObservation(int mp, int kf, int idx) {
+        std::array<int, 4> indexes = {-1, -1, -1, -1};
+        if (obs[mp].count(kf)) indexes = obs[mp][kf];
+        const int NLeft = G->n_blocks[kf] == 1 ? -1 : n_kp[(size_t)kf * C];
+        const int NRight = C > 1 ? n_kp[(size_t)kf * C + 1] : 0, NSideLeft = C > 2 ? n_kp[(size_t)kf * C + 2] : 0;
+        if (NLeft == -1) indexes[0] = idx;
+        else if (idx < NLeft) indexes[0] = idx;
+        else if (idx >= NLeft && idx < NLeft + NRight) indexes[1] = idx;
+        else if (idx >= NLeft + NRight && idx < NLeft + NRight + NSideLeft) indexes[2] = idx;
+        else indexes[3] = idx;
+        obs[mp][kf] = indexes;
+        if (NLeft == -1 && G->uright && G->uright[(size_t)kf * kp_cap + idx] >= 0) G->n_obs[mp] += 2;   // !mpCamera2
+        else G->n_obs[mp]++;
+    }
+    void ComputeDistinctiveDescriptors(int mp) {
+        if (G->bad[mp]) return;
+        if (obs[mp].empty()) return;
+        std::vector<int32_t> rows;
+        std::vector<uint8_t> stack;
+        for (auto &kv : obs[mp])
+            for (int s = 0; s < 4; ++s)
+                if (kv.second[s] != -1) {
+                    const uint8_t *d = row_desc(kv.first, kv.second[s]);
+                    stack.insert(stack.end(), d, d + 32);
+                }
+        if (stack.empty()) return;
+        const int n = (int)(stack.size() / 32);
+        for (int i = 0; i < n; ++i) rows.push_back(i);
+        const int32_t start[2] = {0, n};
+        int32_t best = -1;
+        oracle_distinctive_descriptors(1, start, rows.data(), stack.data(), &best);
+        std::memcpy(mp_desc + (size_t)mp * 32, stack.data() + (size_t)best * 32, 32);
+    }
+    void Replace(int self, int pMP) {
+        log(1, self, pMP, -1);
+        if (pMP == self) return;
+        std::map<int, std::array<int, 4>> o = obs[self];
+        obs[self].clear();
+        G->bad[self] = 1;
+        G->replaced[self] = pMP;
+        for (auto &kv : o) {
+            const int pKF = kv.first;
+            if (!IsInKeyFrame(pMP, pKF)) {
+                for (int s = 0; s < 4; ++s)
+                    if (kv.second[s] != -1) {
+                        mvp(pKF)[kv.second[s]] = pMP;   // ReplaceMapPointMatch
+                        AddObservation(pMP, pKF, kv.second[s]);
+                    }
+            } else {
+                for (int s = 0; s < 4; ++s)
+                    if (kv.second[s] != -1) mvp(pKF)[kv.second[s]] = -1;   // EraseMapPointMatch
+            }
+        }
+        ComputeDistinctiveDescriptors(pMP);
+    }
+    // ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID)
+    int Fuse(int pKF, const std::vector<int> &vpMapPoints, int cameraID) {
+        if (views[pKF].g == nullptr) {
+            views[pKF] = View{g, 0, 0, {}, kps + (size_t)pKF * C * kp_cap, kp_cap, n_kp + (size_t)pKF * C};
+            build_grids(views[pKF]);
+        }
+        const View &v = views[pKF];
+        SE3F Tcw;
+        std::memcpy(Tcw.q, G->Tcw[(size_t)pKF * C + cameraID].q, 16);
+        std::memcpy(Tcw.t, G->Tcw[(size_t)pKF * C + cameraID].t, 12);
+        const float *Ow = G->Ow + ((size_t)pKF * C + cameraID) * 3;
+        const KP *kk = kps + (size_t)pKF * C * kp_cap;
+        int off = 0;
+        for (int c = 0; c < cameraID; ++c) off += n_kp[(size_t)pKF * C + c];
+        int nFused = 0;
+        for (int pMP : vpMapPoints) {
+            if (pMP < 0) continue;
+            if (G->bad[pMP]) continue;
+            else if (IsInKeyFrame(pMP, pKF)) continue;
+            const float *P = pos + 3 * (size_t)pMP, *Pn = normal + 3 * (size_t)pMP;
+            float Pc[3];
+            se3_apply(Tcw, P, Pc);
+            if (Pc[2] < 0.0f) continue;
+            const float invz = 1 / Pc[2];
+            float u, vv;
+            cam_project_f(g->cam_model[cameraID], p->cams[cameraID], Pc, u, vv);
+            if (!(u >= g->min_x && u < g->max_x && vv >= g->min_y && vv < g->max_y)) continue;   // IsInImage
+            const float ur = u - p->bf * invz;
+            const float maxDistance = 1.2f * max_d[pMP], minDistance = 0.8f * min_d[pMP];
+            const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+            const float dist3D = std::sqrt(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+            if (dist3D < minDistance || dist3D > maxDistance) continue;
+            if (PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2] < 0.5 * dist3D) continue;
+            int nPredictedLevel = (int)std::ceil(std::log((double)(max_d[pMP] / dist3D)) / (double)p->log_scale_factor);
+            if (nPredictedLevel < 0) nPredictedLevel = 0;
+            else if (nPredictedLevel >= p->n_levels) nPredictedLevel = p->n_levels - 1;
+            const float radius = p->th * g->scale_factors[nPredictedLevel];
+            const std::vector<int> vIndices = features_in_area(v, u, vv, radius, 0, -1, cameraID);
+            if (vIndices.empty()) continue;
+            const uint8_t *dMP = mp_desc + (size_t)pMP * 32;
+            int bestDist = 256, bestIdx = -1;
+            for (int i : vIndices) {
+                const int slot = cameraID * kp_cap + i;
+                const KP &kp = kk[slot];
+                const int kpLevel = kp.octave;
+                if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+                const float ex = u - kp.x, ey = vv - kp.y;
+                if (cameraID == 0 && p->uright[(size_t)pKF * kp_cap + i] >= 0) {
+                    const float er = ur - p->uright[(size_t)pKF * kp_cap + i];
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if (e2 * p->inv_level_sigma2[kpLevel] > 7.8) continue;
+                } else {
+                    const float e2 = ex * ex + ey * ey;
+                    if (e2 * p->inv_level_sigma2[kpLevel] > 5.99) continue;
+                }
+                const int dist = descriptor_distance(dMP, desc + ((size_t)pKF * C * kp_cap + slot) * 32);
+                if (dist < bestDist) bestDist = dist, bestIdx = off + i;
+            }
+            if (bestDist <= 50) {   // TH_LOW
+                const int pMPinKF = mvp(pKF)[bestIdx];
+                if (pMPinKF >= 0) {
+                    if (!G->bad[pMPinKF]) {
+                        if (G->n_obs[pMPinKF] > G->n_obs[pMP]) Replace(pMP, pMPinKF);
+                        else Replace(pMPinKF, pMP);
+                    }
+                } else {
+                    log(0, pMP, pKF, bestIdx);
+                    AddObservation(pMP, pKF, bestIdx);
+                    mvp(pKF)[bestIdx] = pMP;   // pKF->AddMapPoint(pMP, bestIdx)
+                }
+                nFused++;
+            }
+        }
+        return nFused;
+    }
+};
+}  // namespace
+
+extern "C" int oracle_search_in_neighbors_fuse(const FrameGeom *g, const KP *kps, const uint8_t *desc, const int *n_kp,
+                                               int kp_cap, omv_fuse_graph *G, int current, int n_targets,
+                                               const int32_t *targets, const float *pos, const float *normal,
+                                               const float *min_d, const float *max_d, uint8_t *mp_desc,
+                                               const omv_kf_search_params *p, int32_t *n_fused) {
+    const int C = g->n_cams;
+    FuseMap M{g, kps, desc, n_kp, kp_cap, C, G, pos, normal, min_d, max_d, mp_desc, p, {}, {}, 0};
+    M.views.assign(G->n_kf, View{});
+    for (auto &v : M.views) v.g = nullptr;
+    M.obs.resize(G->n_mps);
+    for (int mp = 0; mp < G->n_mps; ++mp) {
+        G->replaced[mp] = -1;
+        for (int r = G->obs_start[mp]; r < G->obs_start[mp + 1]; ++r)
+            M.obs[mp][G->obs_kf[r]] = {G->obs_idx[4 * r], G->obs_idx[4 * r + 1], G->obs_idx[4 * r + 2], G->obs_idx[4 * r + 3]};
+    }
+    for (int t = 0; t < n_targets * C + C; ++t) n_fused[t] = 0;
+    // vector<MapPoint*> vpMapPointMatches = mpCurrentKeyFrame->GetMapPointMatches();  (:839)
+    const std::vector<int> vpMapPointMatches(M.mvp(current), M.mvp(current) + M.N(current));
+    for (int t = 0; t < n_targets; ++t) {   // (:840-853)
+        const int pKFi = targets[t];
+        n_fused[t * C + 0] = M.Fuse(pKFi, vpMapPointMatches, 0);
+        if (G->n_blocks[pKFi] >= 2) n_fused[t * C + 1] = M.Fuse(pKFi, vpMapPointMatches, 1);
+        if (G->n_blocks[pKFi] == 4) {
+            n_fused[t * C + 2] = M.Fuse(pKFi, vpMapPointMatches, 2);
+            n_fused[t * C + 3] = M.Fuse(pKFi, vpMapPointMatches, 3);
+        }
+    }
+    // vpFuseCandidates (:859-881)
+    std::vector<int> vpFuseCandidates;
+    std::vector<char> cand(G->n_mps, 0);   // mnFuseCandidateForKF
+    for (int t = 0; t < n_targets; ++t) {
+        const int pKFi = targets[t];
+        for (int i = 0; i < M.N(pKFi); ++i) {
+            const int pMP = M.mvp(pKFi)[i];
+            if (pMP < 0) continue;
+            if (G->bad[pMP] || cand[pMP]) continue;
+            cand[pMP] = 1;
+            vpFuseCandidates.push_back(pMP);
+        }
+    }
+    n_fused[n_targets * C + 0] = M.Fuse(current, vpFuseCandidates, 0);   // (:883-889)
+    if (G->n_blocks[current] >= 2) n_fused[n_targets * C + 1] = M.Fuse(current, vpFuseCandidates, 1);
+    if (G->n_blocks[current] == 4) {
+        n_fused[n_targets * C + 2] = M.Fuse(current, vpFuseCandidates, 2);
+        n_fused[n_targets * C + 3] = M.Fuse(current, vpFuseCandidates, 3);
+    }
+    int rows = 0;
+    for (int mp = 0; mp < G->n_mps; ++mp) {
+        G->out_obs_start[mp] = rows;
+        for (auto &kv : M.obs[mp]) {
+            if (rows < G->obs_cap) {
+                G->out_obs_kf[rows] = kv.first;
+                for (int s = 0; s < 4; ++s) G->out_obs_idx[4 * (size_t)rows + s] = kv.second[s];
+            }
+            ++rows;
+        }
+    }
+    G->out_obs_start[G->n_mps] = rows;
+    G->n_log = M.n_log;
+    return (M.n_log > G->log_cap || rows > G->obs_cap) ? 1 : 0;
+}

@@ -805,3 +805,50 @@ def local_mapping_create_new_map_points(d, inertial=True, monocular=False, coars
         ctypes.c_int(int(coarse)), ctypes.c_int(int(far_points)), ctypes.c_float(th_far),
         ctypes.c_float(d["scale_factor"]), _p(n_matches), _p(s1))
     return hm, n_matches[:len(nbs)], [(m[:n1], s[:n1], x[:n1]) for m, s, x in outs], int(s1[0])
+
+
+# ---- LocalMapping::SearchInNeighbors' fuse sequence ---------------------------------------------------------------
+def search_in_neighbors_fuse(s, th=3.0, obs_cap=None, log_cap=None):
+    """The reference's phase A / phase B Fuse loop restated literally (match_oracle.cpp oracle_search_in_neighbors_fuse)
+    on a synth_fuse scene: returns dict(kf_mps, bad, n_obs, replaced, obs_start, obs_kf, obs_idx, log, n_fused, desc)."""
+    from openmavis_amd._lib import FrameGeom, FuseGraph
+    from openmavis_amd.matcher import kf_search_params
+    from openmavis_amd.synth_fuse import fuse_graph_struct
+    keep = []
+
+    def arr(a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return ctypes.c_void_p(a.ctypes.data)
+
+    obs_cap = obs_cap or 4 * len(s["obs_kf"]) + 1024
+    log_cap = log_cap or 4 * int(s["n_mps"]) + 1024
+    out = {}
+    G = fuse_graph_struct(s, FuseGraph, arr, out, obs_cap, log_cap)
+    g = FrameGeom()
+    g.n_cams, g.min_x, g.max_x, g.min_y, g.max_y, g.nlevels = s["n_cams"], 0.0, float(s["width"]), 0.0, \
+        float(s["height"]), s["nlevels"]
+    sc = np.float32(1.0)
+    for i in range(s["nlevels"]):
+        g.scale_factors[i] = float(sc)
+        sc = np.float32(sc * np.float32(1.2))
+    uright = np.ascontiguousarray(s["uright"], np.float32)
+    p = kf_search_params(th, 50.0, s["cams"], bf=float(s["bf"]), nlevels=s["nlevels"])
+    p.uright = _p(uright)
+    p.mode = 0
+    m = {k: np.ascontiguousarray(v) for k, v in s["mps"].items()}
+    mdesc = np.array(m["desc"], np.uint8, copy=True)
+    C, T = int(s["n_cams"]), len(s["targets"])
+    n_fused = np.zeros(T * C + C, np.int32)
+    targets = np.ascontiguousarray(s["targets"], np.int32)
+    f = lib().oracle_search_in_neighbors_fuse
+    f.restype = ctypes.c_int
+    rc = f(ctypes.byref(g), _p(np.ascontiguousarray(s["kps"])), _p(np.ascontiguousarray(s["desc"])),
+           _p(np.ascontiguousarray(s["n_kp"], np.int32)), int(s["kp_cap"]), ctypes.byref(G), int(s["current"]), T,
+           _p(targets), _p(m["pos"]), _p(m["normal"]), _p(m["min_dist"]), _p(m["max_dist"]), _p(mdesc),
+           ctypes.byref(p), _p(n_fused))
+    assert rc == 0, "oracle capacity"
+    n_rows = int(out["out_obs_start"][-1])
+    return dict(kf_mps=out["kf_mps"], bad=out["bad"], n_obs=out["n_obs"], replaced=out["replaced"][:s["n_mps"]],
+                obs_start=out["out_obs_start"], obs_kf=out["out_obs_kf"][:n_rows], obs_idx=out["out_obs_idx"][:n_rows],
+                log=out["log"][:G.n_log], n_fused=n_fused, desc=mdesc)
