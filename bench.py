@@ -822,18 +822,22 @@ P_W, P_H, P_C, P_NF, P_INI, P_MIN, P_M, P_TH = 1920, 1080, 8, 2000, 20, 7, 8000,
 
 
 BYTES_FORMULA = {
-    "pyr_resize": "sum over levels 1..7 of P(l-1) read + P(l) written, per image (one launch per level: the 7 level "
-                  "launches of a stream group are timed and counted together as one 'launch')",
-    "fast_cells": "sum of level pixels read once, per image",
-    "octree": "4 B per FAST candidate read (its input list) + 8 B per distributed keypoint written",
-    "describe": "SURVEY 8(d): sum of level pixels + 56 B per keypoint, per image (the blur is evaluated in LDS at "
-                "the samples: no blurred pyramid)",
+    "pyr_resize": "SURVEY 8(d) once-only split: level 0 read once (the input) + levels 1..7 written once, per image "
+                  "(one launch per level: the 7 level launches of a stream group are timed and counted together as one "
+                  "'launch')",
+    "fast_cells": "SURVEY 8(d) once-only split: levels 1..7 read once, per image (level 0's one read is the pyramid's)",
+    "octree": "SURVEY 8(d) once-only split: 0 (its candidate lists are the design's intermediates; the traffic column "
+              "shows what it moves)",
+    "describe": "SURVEY 8(d) once-only split: 56 B per keypoint written (24 B record + 32 B descriptor; its patch "
+                "reads are re-reads of levels counted once above)",
     "grid": "SURVEY 8(d) frame keypoints: 16 B per keypoint",
     "frustum": "per map point 32 B world data in + per (point, camera) 16 B track out (the SearchByProjection input)",
     "stereo_knn": "SURVEY 8(d) knn inputs: 2 x 1,200 descriptors x 32 B per frame",
     "proj_candidates": "SURVEY 8(d) map points 5,000 x (32 + 5 x 16) B + frame descriptors 32 B per keypoint",
     "proj_resolve": "SURVEY 8(d) outputs: 43,200 B per frame",
 }
+# The extraction kernels' budgets sum to SURVEY 8(d)'s once-only figure per image: sum(P) + sum(P[1:]) + 56 N
+# (pyr_resize sum(P), fast_cells sum(P[1:]), octree 0, describe 56 N) -- 2,085,018 B at 720x540 / 1,200 features.
 
 
 def rocprof_launch_avg(kernel):
@@ -852,14 +856,15 @@ def rocprof_launch_avg(kernel):
 
 
 def per_step_algorithmic_bytes(B, P, n_kp, n_cand):
-    """Algorithmic bytes of one step (B frames) per kernel.  The matching kernels split SURVEY §8(d)'s 968,000 B per
+    """Algorithmic bytes of one step (B frames) per kernel.  The extraction kernels split SURVEY §8(d)'s 2,085,018 B per
+    image once-only (BYTES_FORMULA; they sum to it), the matching kernels SURVEY §8(d)'s 968,000 B per
     frame (frame keypoints 96,000 -> grid, map points 560,000 + frame descriptors 192,000 -> candidates, knn inputs
     76,800 -> knn, outputs 43,200 -> resolve); the design's own candidate records are not counted."""
     return {
-        "pyr_resize": B * C * (sum(P[:-1]) + sum(P[1:])),
-        "fast_cells": B * C * sum(P),
-        "octree": 4 * n_cand + 8 * n_kp,
-        "describe": B * C * sum(P) + n_kp * 56,
+        "pyr_resize": B * C * sum(P),
+        "fast_cells": B * C * sum(P[1:]),
+        "octree": 0,
+        "describe": n_kp * 56,
         "grid": n_kp * 16,
         "frustum": B * M_MPS * (32 + C * 16),
         "stereo_knn": B * 2 * 1200 * 32,
@@ -1539,7 +1544,7 @@ def main():
                     rec["traffic"] = int(r["hbm_bytes_per_frame"] * Bg)
                 if rec["traffic"] is not None:
                     rec["traffic_source"] = f"{pmc} ({r['tag']}, program {r.get('program', 'orb')})"
-                    rec["traffic_ratio"] = round(rec["traffic"] / alg, 3)
+                    rec["traffic_ratio"] = round(rec["traffic"] / alg, 3) if alg > 0 else None
             except Exception:
                 pass
         kernels[k] = rec
@@ -1547,22 +1552,27 @@ def main():
         view = "overlapped" if any("overlapped" in r for r in kernels.values()) else "isolated"
         dom = max((k for k in kernels if view in kernels[k]), key=lambda k: kernels[k][view]["ms_per_step"])
         d = kernels[dom]
-        roof = {"kernel": dom, "bound": "hbm", "achieved": d[view]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": d[view]["frac"], "traffic": d["traffic"], "avg_launch_ms": d[view]["avg_launch_ms"],
+        # the headline fraction is the device-time view: the committed rocprofv3 dispatch trace of this round's bench
+        # launches (profiles/<tag>_kernel_grid.json, the dominant kernel's bench-grid rows); the HIP events on the launch
+        # stream -- which also hold the time a launch queues behind the other two streams' kernels -- sit beside it
+        rp = rocprof_launch_avg(dom)
+        ev = {"achieved": d[view]["achieved"], "frac": d[view]["frac"], "avg_launch_ms": d[view]["avg_launch_ms"],
+              "timing": ("HIP events on the launch stream over the timed steps (3 stream groups overlapping)"
+                         if view == "overlapped" else "HIP events on the launch stream, group 0 alone")}
+        roof = {"kernel": dom, "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": d["traffic"],
                 "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"], "frames_per_launch": Bg,
-                "timing": ("HIP events on the launch stream over the timed steps (3 stream groups overlapping); dominant = "
-                           "largest ms per step") if view == "overlapped" else
-                          "HIP events on the launch stream, group 0 alone (isolated passes after the timed steps)",
-                "bytes_formula": d["bytes_formula"]}
+                "bytes_formula": d["bytes_formula"], "dominant_by": "largest ms per step (HIP events, overlapped)",
+                "events": ev}
+        if rp is not None:
+            ach = d["algorithmic_bytes_per_launch"] / (rp["avg_us"] * 1e-6) / 1e9
+            roof.update(achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 6), avg_launch_ms=rp["avg_launch_ms"],
+                        timing=f"rocprofv3 --kernel-trace dispatch average of the bench-grid launches ({rp['source']}, "
+                               f"grid {rp['grid']}, {rp['calls']} calls): device time only",
+                        rocprof=rp)
+        else:
+            roof.update(achieved=ev["achieved"], frac=ev["frac"], avg_launch_ms=ev["avg_launch_ms"], timing=ev["timing"])
         if d.get("traffic_source"):
             roof["traffic_source"] = d["traffic_source"]
-        rp = rocprof_launch_avg(dom)
-        if rp is not None:   # the committed rocprofv3 dispatch trace of the same bench launches, beside the events
-            ach = d["algorithmic_bytes_per_launch"] / (rp["avg_us"] * 1e-6) / 1e9
-            roof["rocprof"] = dict(rp, achieved=round(ach, 2), frac=round(ach / HBM_PEAK_GBS, 5),
-                                   note="rocprofv3 --kernel-trace average of the dominant kernel's bench-grid launches "
-                                        "(device time only; the HIP events above also hold queueing behind the other "
-                                        "streams' kernels)")
         iso_k = [k for k in kernels if "isolated" in kernels[k]]
         if iso_k:
             di = max(iso_k, key=lambda k: kernels[k]["isolated"]["avg_launch_ms"])
