@@ -406,7 +406,8 @@ __device__ unsigned long long g_fast_stats[8];
 template <int RS>   // LDS row stride in bytes (0: per cell, rounded up to 4)
 __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cells, const uint8_t *images,
                                                         size_t img_stride, size_t pitch0, const uint8_t *pyr,
-                                                        int *cell_cnt, uint32_t *cell_kp, int rmax, int n_blocks) {
+                                                        int *cell_cnt, uint32_t *cell_kp, int rmax, int smax,
+                                                        int n_blocks) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int blk = omv::xcd_block(n_blocks);
     if (blk < 0) return;
@@ -422,8 +423,11 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     const int o = dwords ? (int)(((uintptr_t)row0) & 3) : 0;
     const int rs = RS > 0 ? RS : ((rw + o + 3) & ~3);
     uint8_t *pix = smem + o;
+    // the strength map covers the NMS reach only: rows / columns 2 .. n-3 of the region, (r, q) at
+    // S[(r - 2) * sw + q - 2] (the region's outer rows never hold a candidate or an NMS neighbour)
     uint8_t *S = smem + rmax;
-    uint16_t *cand = (uint16_t *)(smem + 2 * rmax);
+    const int sw = rw - 4;
+    uint16_t *cand = (uint16_t *)(smem + rmax + smax);
     if (dwords) {
         const int nd = (rw + o + 3) >> 2;   // dwords of a row read (the LDS row holds rs / 4)
         const uint32_t *g0 = (const uint32_t *)(row0 - o);
@@ -445,7 +449,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             pix[r * rs + q] = row0[(size_t)r * sp + q];
         }
     }
-    for (int i = lane; i < (rs * rh + 15) >> 4; i += 64) ((uint4 *)S)[i] = make_uint4(0, 0, 0, 0);   // rmax % 16 == 0
+    for (int i = lane; i < (sw * (rh - 4) + 15) >> 4; i += 64) ((uint4 *)S)[i] = make_uint4(0, 0, 0, 0);   // rmax % 16 == 0
     __syncthreads();
     const int dw = rw - 6, dh = rh - 6;   // detection window [3, rw-4] x [3, rh-4]
     const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
@@ -548,7 +552,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             int r, q;
             rowcol(i, r, q);
             const int sv = fast_strength_h<RS>(pix + r * rs + q, rs);
-            S[r * rs + q] = (uint8_t)min(max(sv, 0), 255);
+            S[(r - 2) * sw + (q - 2)] = (uint8_t)min(max(sv, 0), 255);
         }
         __syncthreads();
         return ncand;
@@ -566,13 +570,13 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const int i = cand[k];
                 int r, q;
                 rowcol(i, r, q);
-                const uint8_t *sp8 = S + r * rs + q;
+                const uint8_t *sp8 = S + (r - 2) * sw + (q - 2);
                 const int v = sp8[0];
                 // v > th and v - 1 > (nv > th ? nv - 1 : 0) for all 8 neighbours <=> v > max(nv..., th, 1)
                 int m = max(th, 1);
 #pragma unroll
                 for (int n = 0; n < 9; ++n)
-                    if (n != 4) m = max(m, (int)sp8[(n / 3 - 1) * rs + (n % 3 - 1)]);
+                    if (n != 4) m = max(m, (int)sp8[(n / 3 - 1) * sw + (n % 3 - 1)]);
                 keep = v > m;
                 const int x = c.x0 + q - kMinB, y = c.y0 + r - kMinB;
                 packed = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)(v - 1) << 24);
@@ -1408,6 +1412,7 @@ struct omv_orb {
     uint32_t *d_cell_kp = nullptr, *d_cand = nullptr, *d_nid = nullptr, *d_lvl_out = nullptr, *d_lvl_cls = nullptr;
     int *d_lvl_cnt = nullptr, *d_lap = nullptr, *d_err = nullptr;
     int rmax = 0;
+    int smax = 0;          // K2 strength-map bytes
     int fast_rs = 0;       // K2 LDS row stride: 68 (17 dwords, odd: rows spread over the banks) when every cell row (plus misalignment) fits, else per cell
     size_t fast_lds = 0;   // K2 dynamic LDS: region + strength map (rmax each) + the candidate list (u16)
     size_t oct_lds = 0;
@@ -1607,9 +1612,16 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     g.n_max = out_off;
     g.node_cap = (max_nodes + 15) & ~15;   // <= quota + 3 nodes exist at once (DistributeOctTree's stop rules)
     g.ccnt_cap = (std::max(4 * g.node_cap, max_cells_lvl) + 15) & ~15;
-    o->fast_rs = max_rw + 3 <= 68 ? 68 : 0;
-    o->rmax = ((o->fast_rs ? 68 * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
-    o->fast_lds = 2 * (size_t)o->rmax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
+    // K2's row stride: an odd dword count (rows spread over the LDS banks) -- 13 dwords when every cell row plus its
+    // misalignment fits, else 17, else per cell; OMV_FAST_RS=68 forces the wider stride (A/B)
+    o->fast_rs = max_rw + 3 <= 52 ? 52 : max_rw + 3 <= 68 ? 68 : 0;
+    if (const char *e = getenv("OMV_FAST_RS"))
+        if (std::atoi(e) == 68 && max_rw + 3 <= 68) o->fast_rs = 68;
+    o->rmax = ((o->fast_rs ? o->fast_rs * max_rh : ((max_rw + 6) & ~3) * max_rh) + 15) & ~15;   // rows: rw + misalignment
+    // the strength map over rows / columns 2 .. n-3 (the NMS reach), then the candidate list (u16, worst case every
+    // detection-window pixel): the LDS per wave sets K2's occupancy
+    o->smax = ((std::max(0, (max_rw - 4) * (max_rh - 4))) + 15) & ~15;
+    o->fast_lds = (size_t)o->rmax + o->smax + 2 * (size_t)std::max(0, (max_rw - 6) * (max_rh - 6));
     o->oct_lds = (size_t)(32 + 14 * g.node_cap + g.ccnt_cap + 6 * (g.node_cap / 17 + 1) + 2) * sizeof(int);
     return OMV_OK;
 }
@@ -1851,12 +1863,18 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     }
     mark(o, st);
     // K2: FAST per cell
-    if (o->fast_rs == 68)
+    if (o->fast_rs == 52)
+        fast_cells_kernel<52><<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(
+            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, o->smax,
+            g.n_cells * n);
+    else if (o->fast_rs == 68)
         fast_cells_kernel<68><<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(
-            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
+            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, o->smax,
+            g.n_cells * n);
     else
         fast_cells_kernel<0><<<omv::xcd_grid(g.n_cells * n), 64, o->fast_lds, st>>>(
-            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, g.n_cells * n);
+            g, o->d_cells, images, image_stride, pitch, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->rmax, o->smax,
+            g.n_cells * n);
     mark(o, st);
     // K3: octree per (image, level)
     OctArgs oa{o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err};
