@@ -22,6 +22,12 @@
 //                           of the ConstraintPoseImu
 //   Fuse                    ORBmatcher::Fuse(pKF, vpMapPoints, th, cameraID) (src/ORBmatcher.cc:1458-1647,
 //                           called 4x per camera at LocalMapping.cc:845-888): the chosen keypoint per point
+//   PoseOptimization        Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:855-1278) on ONE frame
+//   CreateNewMapPoints      LocalMapping::CreateNewMapPoints' neighbour loop (src/LocalMapping.cc:395-783):
+//                           SearchForTriangulation interleaved with the geometry, the new points in creation order
+//   MapPointRefresh         MapPoint::ComputeDistinctiveDescriptors / UpdateNormalAndDepth over a batch of points
+//   SearchInNeighborsFuse   LocalMapping::SearchInNeighbors' fuse sequence (src/LocalMapping.cc:837-889): the final
+//                           graph and the edit log (AddObservation / Replace) to replay on the reference's objects
 //
 // Errors: every omv_status != OMV_OK throws omv_adapt::Error (the adapters' callers are C++).
 #ifndef OMV_ADAPTERS_HPP
@@ -34,6 +40,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -674,6 +681,410 @@ class Fuse {
     DeviceArray<int> n_;
     DeviceArray<float> ur_, pos_, nrm_, mind_, maxd_;
     DeviceArray<int32_t> list_, bi_, bd_, nm_;
+};
+
+// ---- Optimizer::PoseOptimization(Frame*) ------------------------------------------------------------------------
+// The visual-only pose optimisation of Tracking (Optimizer.cc:855-1278) on ONE frame.  The frame's edges as the
+// reference creates them (:907-1121): one per matched keypoint -- a mono edge on the keypoint's camera block c (through
+// T_c0 = mTrl / mTsll / mTsrl) or, on a conventional (single-camera) frame, a stereo edge instead when mvuRight >= 0.
+class PoseOptimization {
+  public:
+    struct Mono {     // EdgeSE3ProjectXYZOnlyPose / ...ToBody / ...SLPoseToBody / ...SRPoseToBody
+        int cam, kp;  // camera block, keypoint index i (mvbOutlier[i])
+        double u, v;
+        float inv_sigma2;
+        std::array<float, 3> Xw;
+    };
+    struct Stereo {   // EdgeStereoSE3ProjectXYZOnlyPose (camera 0)
+        int kp;
+        double u, v, ur;
+        float inv_sigma2;
+        std::array<float, 3> Xw;
+    };
+    // cams [n_cams][8] with their models; rig_q / rig_t: T_c0 per camera block as the SE3Quat the reference builds from
+    // GetRelativePoseTrl() / Tsll / Tsrl (entry 0 unused); bf = Frame::mbf.
+    PoseOptimization(int n_cams, std::vector<float> cams, std::vector<int32_t> cam_model, float bf,
+                     std::vector<std::array<double, 4>> rig_q, std::vector<std::array<double, 3>> rig_t)
+        : C_(n_cams), cam_(std::move(cams)), model_(std::move(cam_model)), bf_(bf) {
+        if ((int)rig_q.size() != n_cams || (int)rig_t.size() != n_cams) throw Error("PoseOptimization: rig size");
+        for (auto &q : rig_q) rq_.insert(rq_.end(), q.begin(), q.end());
+        for (auto &t : rig_t) rt_.insert(rt_.end(), t.begin(), t.end());
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    ~PoseOptimization() {
+        if (h_) (void)omv_pose_destroy(h_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    PoseOptimization(const PoseOptimization &) = delete;
+    PoseOptimization &operator=(const PoseOptimization &) = delete;
+
+    // int Optimizer::PoseOptimization(Frame *pFrame): q / t = pFrame->GetPose() as the SE3Quat of :871-873 (in), the
+    // optimised estimate (out, pFrame->SetPose); mvbOutlier [kp_cap] of the edges' keypoints; returns nGood.
+    int operator()(std::array<double, 4> &q, std::array<double, 3> &t, const std::vector<Mono> &mono,
+                   const std::vector<Stereo> &stereo, std::vector<uint8_t> &mvbOutlier) {
+        const int nm = (int)mono.size(), ns = (int)stereo.size();
+        if (mvbOutlier.empty()) throw Error("PoseOptimization: empty mvbOutlier");
+        const int need = std::max(1, std::max(nm, ns));
+        if (!h_ || need > cap_) {
+            if (h_) (void)omv_pose_destroy(h_), h_ = nullptr;
+            cap_ = need;
+            check(omv_pose_create(1, cap_, &h_), "omv_pose_create");
+        }
+        std::vector<int32_t> mstart{0, nm}, sstart{0, ns}, mcam(nm), mkp(nm), scam(ns, 0), skp(ns);
+        std::vector<double> mobs(2 * (size_t)nm), sobs(3 * (size_t)ns);
+        std::vector<float> mw(nm), mx(3 * (size_t)nm), sw(ns), sx(3 * (size_t)ns);
+        for (int e = 0; e < nm; ++e) {
+            const Mono &m = mono[e];
+            mcam[e] = m.cam, mkp[e] = m.kp, mobs[2 * e] = m.u, mobs[2 * e + 1] = m.v, mw[e] = m.inv_sigma2;
+            std::copy(m.Xw.begin(), m.Xw.end(), &mx[3 * e]);
+        }
+        for (int e = 0; e < ns; ++e) {
+            const Stereo &m = stereo[e];
+            skp[e] = m.kp, sobs[3 * e] = m.u, sobs[3 * e + 1] = m.v, sobs[3 * e + 2] = m.ur, sw[e] = m.inv_sigma2;
+            std::copy(m.Xw.begin(), m.Xw.end(), &sx[3 * e]);
+        }
+        ms_.upload(mstart.data(), 2, st_), ss_.upload(sstart.data(), 2, st_);
+        mcam_.upload(mcam.data(), nm, st_), mkp_.upload(mkp.data(), nm, st_), mobs_.upload(mobs.data(), mobs.size(), st_);
+        mw_.upload(mw.data(), nm, st_), mx_.upload(mx.data(), mx.size(), st_);
+        scam_.upload(scam.data(), ns, st_), skp_.upload(skp.data(), ns, st_), sobs_.upload(sobs.data(), sobs.size(), st_);
+        sw_.upload(sw.data(), ns, st_), sx_.upload(sx.data(), sx.size(), st_);
+        kpo_.upload(mvbOutlier.data(), mvbOutlier.size(), st_);
+        q_.upload(q.data(), 4, st_), t_.upload(t.data(), 3, st_);
+        ng_.resize(1);
+        omv_pose_batch b{};
+        b.n_frames = 1, b.n_cams = C_, b.cam = cam_.data(), b.bf = bf_;
+        b.cam_model = model_.empty() ? nullptr : model_.data();
+        b.mono_start = ms_.p, b.mono_cam = mcam_.p, b.mono_kp = mkp_.p, b.mono_obs = mobs_.p, b.mono_inv_sigma2 = mw_.p;
+        b.mono_xw = mx_.p;
+        b.stereo_start = ss_.p, b.stereo_cam = scam_.p, b.stereo_kp = skp_.p, b.stereo_obs = sobs_.p;
+        b.stereo_inv_sigma2 = sw_.p, b.stereo_xw = sx_.p;
+        b.kp_cap = (int)mvbOutlier.size(), b.n_mono = nm, b.n_stereo = ns;
+        check(omv_pose_optimization(h_, &b, rq_.data(), rt_.data(), q_.p, t_.p, kpo_.p, ng_.p, st_),
+              "omv_pose_optimization");
+        int n_good = 0;
+        ng_.download(&n_good, 1, st_);
+        kpo_.download(mvbOutlier.data(), mvbOutlier.size(), st_);
+        q_.download(q.data(), 4, st_), t_.download(t.data(), 3, st_);
+        hip_check(hipStreamSynchronize(st_), "PoseOptimization");
+        return n_good;
+    }
+
+  private:
+    int C_;
+    std::vector<float> cam_;
+    std::vector<int32_t> model_;
+    float bf_;
+    std::vector<double> rq_, rt_;
+    hipStream_t st_ = nullptr;
+    omv_pose *h_ = nullptr;
+    int cap_ = 0;
+    DeviceArray<double> mobs_, sobs_, q_, t_;
+    DeviceArray<float> mw_, mx_, sw_, sx_;
+    DeviceArray<int32_t> ms_, ss_, mcam_, mkp_, scam_, skp_, ng_;
+    DeviceArray<uint8_t> kpo_;
+};
+
+// ---- LocalMapping::CreateNewMapPoints (LocalMapping.cc:395-783) -------------------------------------------------
+// The keyframe fields the loop reads: the SearchForTriangulation view plus the geometry of the per-match checks.
+struct CnmpKeyFrame {
+    KeyFrameView view;                                 // kps [L|R|SL|SR], mDescriptors, GetMapPoint != NULL, mFeatVec
+    std::array<std::array<float, 12>, 4> Tcw{};        // GetPose / GetRightPose / GetSideLeftPose / GetSideRightPose
+    std::array<std::array<float, 3>, 4> Ow{};          // the matching camera centres
+    std::array<float, 9> Rwc{};                        // mRwc (UnprojectStereo)
+    std::array<float, 3> twc{};                        // mTwc.translation()
+    float fx = 0, fy = 0, cx = 0, cy = 0, invfx = 0, invfy = 0, mb = 0, mbf = 0;
+    std::vector<float> uright, depth;                  // [N] mvuRight / mvDepth, or empty
+    std::array<float, 16> scale_factors{};             // mvScaleFactors
+};
+// One MapPoint the loop creates, in the reference's creation order (neighbour, then idx1 ascending): new MapPoint(x3D,
+// mpCurrentKeyFrame), AddObservation(pKF1, idx1) / (pKF2, idx2), AddMapPoint on both (:766-781).
+struct NewMapPoint {
+    int neighbour;
+    size_t idx1, idx2;
+    std::array<float, 3> x3D;
+    bool stereo;   // bPointStereo (UnprojectStereo)
+};
+
+class CreateNewMapPoints {
+  public:
+    // cams [4][8] / cam_model [4] of the rig (L, R, SL, SR); n_cams 2 or 4 (the multi-camera rigs the device search
+    // covers); mbInertial, mbMonocular (no baseline gate; its median-depth test arrives as `skip`), mbFarPoints /
+    // mThFarPoints.
+    CreateNewMapPoints(std::vector<float> cams, std::vector<int32_t> cam_model, int n_cams, bool inertial, bool monocular,
+                       bool far_points, float th_far)
+        : cams_(std::move(cams)), model_(std::move(cam_model)), C_(n_cams), inertial_(inertial), mono_(monocular),
+          far_(far_points), th_far_(th_far) {
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+        check(omv_matcher_create(1, 1, 1, 1, &m_), "omv_matcher_create");
+        side1_.resize(1);
+    }
+    ~CreateNewMapPoints() {
+        if (m_) (void)omv_matcher_destroy(m_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    CreateNewMapPoints(const CreateNewMapPoints &) = delete;
+    CreateNewMapPoints &operator=(const CreateNewMapPoints &) = delete;
+
+    // The loop over vpNeighKFs [lo, hi): has_mp1 [N1] in/out (the current keyframe's GetMapPoint != NULL; the created
+    // points' slots set on return); T[i]: neighbour i's ten camera-pair transforms (section 6); skip[i]: the caller's
+    // `continue` (mbMonocular's median-depth test); n_matches (optional): SearchForTriangulation's counts.  `restart`
+    // = the top of CreateNewMapPoints (side 1 back on the left camera); false continues from the previous call's
+    // state, so a caller that checks CheckNewKeyFrames() between neighbours (:440) gets the one-call result.
+    std::vector<NewMapPoint> operator()(const CnmpKeyFrame &kf1, std::vector<uint8_t> &has_mp1,
+                                        const std::vector<CnmpKeyFrame> &nbs,
+                                        const std::vector<std::array<std::array<float, 12>, OMV_TRI_PAIRS>> &T,
+                                        const std::vector<int> &skip, bool bCoarse, float scale_factor, size_t lo,
+                                        size_t hi, bool restart, std::vector<int> *n_matches = nullptr) {
+        const int N1 = kf1.view.N;
+        if ((int)has_mp1.size() != N1 || T.size() != nbs.size() || skip.size() != nbs.size() || hi > nbs.size() || lo > hi)
+            throw Error("CreateNewMapPoints: inconsistent inputs");
+        const int n = (int)(hi - lo);
+        while (bufs_.size() < nbs.size() + 1) bufs_.emplace_back(new Buf());
+        omv_cnmp_kf k1 = kf_struct(kf1, *bufs_[0]);
+        hm_.upload(has_mp1.data(), has_mp1.size(), st_);
+        if (restart) hip_check(hipMemsetAsync(side1_.p, 0, sizeof(int32_t), st_), "side1");
+        std::vector<omv_cnmp_neighbour> nb(n);
+        m12_.resize((size_t)std::max(1, n) * std::max(1, N1)), status_.resize((size_t)std::max(1, n) * std::max(1, N1));
+        x3d_.resize((size_t)std::max(1, n) * std::max(1, N1) * 3), nm_.resize(std::max(1, n));
+        for (int j = 0; j < n; ++j) {
+            nb[j].kf2 = kf_struct(nbs[lo + j], *bufs_[1 + lo + j]);
+            for (int q = 0; q < OMV_TRI_PAIRS; ++q) std::copy(T[lo + j][q].begin(), T[lo + j][q].end(), nb[j].T[q]);
+            nb[j].skip = skip[lo + j];
+            nb[j].match12 = m12_.p + (size_t)j * N1, nb[j].status = status_.p + (size_t)j * N1;
+            nb[j].x3D = x3d_.p + (size_t)j * N1 * 3;
+        }
+        check(omv_local_mapping_create_new_map_points(m_, &k1, hm_.p, n, nb.data(), cams_.data(),
+                                                      model_.empty() ? nullptr : model_.data(), C_, inertial_, !mono_,
+                                                      bCoarse, far_, th_far_, scale_factor, nm_.p, side1_.p, st_),
+              "omv_local_mapping_create_new_map_points");
+        std::vector<int32_t> m12((size_t)n * N1), st((size_t)n * N1), nm(n);
+        std::vector<float> x((size_t)n * N1 * 3);
+        m12_.download(m12.data(), m12.size(), st_), status_.download(st.data(), st.size(), st_);
+        x3d_.download(x.data(), x.size(), st_), nm_.download(nm.data(), n, st_);
+        hm_.download(has_mp1.data(), has_mp1.size(), st_);
+        hip_check(hipStreamSynchronize(st_), "CreateNewMapPoints");
+        if (n_matches) n_matches->assign(nm.begin(), nm.end());
+        std::vector<NewMapPoint> out;
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < N1; ++i) {
+                const size_t o = (size_t)j * N1 + i;
+                if (st[o] > 0)
+                    out.push_back(NewMapPoint{(int)(lo + j), (size_t)i, (size_t)m12[o], {x[3 * o], x[3 * o + 1], x[3 * o + 2]},
+                                              st[o] == 2});
+            }
+        return out;
+    }
+
+  private:
+    struct Buf {
+        DeviceArray<omv_kp> kps;
+        DeviceArray<uint8_t> desc, has_mp;
+        DeviceArray<uint32_t> node;
+        DeviceArray<int32_t> start, idx;
+        DeviceArray<float> ur, depth;
+    };
+    omv_cnmp_kf kf_struct(const CnmpKeyFrame &k, Buf &b) {
+        const KeyFrameView &v = k.view;
+        if ((int)v.keys.size() != v.N || (int)v.descriptors.size() != 32 * v.N || (int)v.has_map_point.size() != v.N ||
+            v.feat_start.size() != v.feat_node.size() + 1 || (!k.uright.empty() && (int)k.uright.size() != v.N) ||
+            (!k.depth.empty() && (int)k.depth.size() != v.N))
+            throw Error("CreateNewMapPoints: inconsistent CnmpKeyFrame");
+        b.kps.upload(v.keys.data(), v.keys.size(), st_), b.desc.upload(v.descriptors.data(), v.descriptors.size(), st_);
+        b.has_mp.upload(v.has_map_point.data(), v.has_map_point.size(), st_);
+        b.node.upload(v.feat_node.data(), v.feat_node.size(), st_);
+        b.start.upload(v.feat_start.data(), v.feat_start.size(), st_), b.idx.upload(v.feat_idx.data(), v.feat_idx.size(), st_);
+        b.ur.upload(k.uright.data(), k.uright.size(), st_), b.depth.upload(k.depth.data(), k.depth.size(), st_);
+        omv_cnmp_kf s{};
+        s.kf.n = v.N, s.kf.n_left = v.NLeft, s.kf.n_right = v.NRight, s.kf.n_sideleft = v.NSideLeft;
+        s.kf.kps = b.kps.p, s.kf.desc = b.desc.p, s.kf.has_mp = b.has_mp.p;
+        s.kf.n_nodes = (int)v.feat_node.size(), s.kf.node_id = b.node.p, s.kf.node_start = b.start.p, s.kf.node_idx = b.idx.p;
+        std::copy(v.level_sigma2.begin(), v.level_sigma2.end(), s.kf.level_sigma2);
+        s.kps_raw = nullptr;
+        for (int c = 0; c < 4; ++c) {
+            std::copy(k.Tcw[c].begin(), k.Tcw[c].end(), s.Tcw[c]);
+            std::copy(k.Ow[c].begin(), k.Ow[c].end(), s.Ow[c]);
+        }
+        std::copy(k.Rwc.begin(), k.Rwc.end(), s.Rwc), std::copy(k.twc.begin(), k.twc.end(), s.twc);
+        s.fx = k.fx, s.fy = k.fy, s.cx = k.cx, s.cy = k.cy, s.invfx = k.invfx, s.invfy = k.invfy, s.mb = k.mb, s.mbf = k.mbf;
+        s.uright = k.uright.empty() ? nullptr : b.ur.p, s.depth = k.depth.empty() ? nullptr : b.depth.p;
+        std::copy(k.scale_factors.begin(), k.scale_factors.end(), s.scale_factors);
+        return s;
+    }
+    std::vector<float> cams_;
+    std::vector<int32_t> model_;
+    int C_;
+    bool inertial_, mono_, far_;
+    float th_far_;
+    hipStream_t st_ = nullptr;
+    omv_matcher *m_ = nullptr;
+    std::vector<std::unique_ptr<Buf>> bufs_;
+    DeviceArray<uint8_t> hm_;
+    DeviceArray<int32_t> m12_, status_, nm_, side1_;
+    DeviceArray<float> x3d_;
+};
+
+// ---- MapPoint::ComputeDistinctiveDescriptors / UpdateNormalAndDepth over a batch of points ----------------------
+class MapPointRefresh {
+  public:
+    MapPointRefresh() { hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate"); }
+    ~MapPointRefresh() {
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    MapPointRefresh(const MapPointRefresh &) = delete;
+    MapPointRefresh &operator=(const MapPointRefresh &) = delete;
+
+    // ComputeDistinctiveDescriptors (MapPoint.cc:405-483): point p's observation descriptors are rows
+    // desc_row[desc_start[p] .. desc_start[p+1]) of `desc` [rows][32] in mObservations order (L / R / SL / SR of each
+    // keyframe); returns the chosen row per point (-1: none, mDescriptor untouched) and, in desc_out [P][32], the
+    // descriptors.
+    std::vector<int32_t> distinctive(const std::vector<int32_t> &desc_start, const std::vector<int32_t> &desc_row,
+                                     const std::vector<uint8_t> &desc, std::vector<uint8_t> &desc_out) {
+        const int P = (int)desc_start.size() - 1;
+        if (P < 0) throw Error("MapPointRefresh: desc_start");
+        ds_.upload(desc_start.data(), desc_start.size(), st_), dr_.upload(desc_row.data(), desc_row.size(), st_);
+        d_.upload(desc.data(), desc.size(), st_);
+        best_.resize(std::max(1, P)), dout_.resize(32 * (size_t)std::max(1, P));
+        check(omv_mappoint_distinctive_descriptors(P, ds_.p, dr_.p, d_.p, best_.p, dout_.p, st_),
+              "omv_mappoint_distinctive_descriptors");
+        std::vector<int32_t> best(P);
+        desc_out.resize(32 * (size_t)P);
+        best_.download(best.data(), P, st_), dout_.download(desc_out.data(), desc_out.size(), st_);
+        hip_check(hipStreamSynchronize(st_), "distinctive");
+        return best;
+    }
+    // UpdateNormalAndDepth (MapPoint.cc:503-588): per point its observation camera centres obs_center [E][3] (rows
+    // obs_start[p] ..), mWorldPos, the reference keyframe's camera centre, mvScaleFactors[level] of its keypoint there
+    // and mvScaleFactors[nLevels - 1]; out: mNormalVector, mfMinDistance, mfMaxDistance (points without entries: as
+    // given).
+    void normal_depth(const std::vector<int32_t> &obs_start, const std::vector<float> &obs_center,
+                      const std::vector<float> &pos, const std::vector<float> &ref_center,
+                      const std::vector<float> &ref_level_scale, const std::vector<float> &ref_max_scale,
+                      std::vector<float> &normal, std::vector<float> &min_dist, std::vector<float> &max_dist) {
+        const int P = (int)obs_start.size() - 1;
+        if (P < 0 || (int)normal.size() != 3 * P || (int)min_dist.size() != P || (int)max_dist.size() != P)
+            throw Error("MapPointRefresh: normal_depth sizes");
+        os_.upload(obs_start.data(), obs_start.size(), st_), oc_.upload(obs_center.data(), obs_center.size(), st_);
+        pos_.upload(pos.data(), pos.size(), st_), rc_.upload(ref_center.data(), ref_center.size(), st_);
+        rl_.upload(ref_level_scale.data(), ref_level_scale.size(), st_);
+        rm_.upload(ref_max_scale.data(), ref_max_scale.size(), st_);
+        nrm_.upload(normal.data(), normal.size(), st_), mn_.upload(min_dist.data(), P, st_), mx_.upload(max_dist.data(), P, st_);
+        check(omv_mappoint_normal_depth(P, os_.p, oc_.p, pos_.p, rc_.p, rl_.p, rm_.p, nrm_.p, mn_.p, mx_.p, st_),
+              "omv_mappoint_normal_depth");
+        nrm_.download(normal.data(), normal.size(), st_), mn_.download(min_dist.data(), P, st_);
+        mx_.download(max_dist.data(), P, st_);
+        hip_check(hipStreamSynchronize(st_), "normal_depth");
+    }
+
+  private:
+    hipStream_t st_ = nullptr;
+    DeviceArray<int32_t> ds_, dr_, best_, os_;
+    DeviceArray<uint8_t> d_, dout_;
+    DeviceArray<float> oc_, pos_, rc_, rl_, rm_, nrm_, mn_, mx_;
+};
+
+// ---- LocalMapping::SearchInNeighbors' fuse sequence (LocalMapping.cc:837-889) ----------------------------------
+// The flattened map the sequence reads (keyframes numbered in std::map<KeyFrame*> key order, the current keyframe
+// and the targets among them, block-major keypoints [n_kf][n_cams][kp_cap]) and what it returns: the final graph and
+// the ordered edit log to replay with the reference's own methods ({0, mp, kf, idx}: pMP->AddObservation(pKF, idx) +
+// pKF->AddMapPoint(pMP, idx); {1, a, b, -1}: a->Replace(b)).
+struct FuseGraphView {
+    int n_kf = 0, n_cams = 0, kp_cap = 0, width = 0, height = 0;
+    std::vector<float> scale_factors, cams;            // mvScaleFactors; [n_cams][8]
+    std::vector<int32_t> cam_model;                    // [n_cams] or empty (KB8)
+    float bf = 0.f, th = 3.f;
+    std::vector<omv_kp> kps;                           // [n_kf][n_cams][kp_cap]
+    std::vector<uint8_t> desc;                         // [n_kf][n_cams][kp_cap][32]
+    std::vector<int32_t> n_kp;                         // [n_kf][n_cams]
+    std::vector<float> uright;                         // [n_kf][kp_cap] block-0 mvuRight
+    std::vector<int32_t> n_blocks;                     // [n_kf] 1 / 2 / 4
+    std::vector<omv_se3f> Tcw;                         // [n_kf][n_cams]
+    std::vector<float> Ow;                             // [n_kf][n_cams][3]
+    std::vector<int32_t> kf_mps;                       // [n_kf][n_cams * kp_cap] in/out, N-indexed
+    std::vector<float> pos, normal, min_dist, max_dist;   // [M][3] / [M]
+    std::vector<uint8_t> mp_desc;                      // [M][32] in/out
+    std::vector<int32_t> bad, n_obs;                   // [M] in/out
+    std::vector<int32_t> obs_start, obs_kf, obs_idx;   // in: CSR [M + 1] / [rows] / [rows][4]; out: the final ones
+    std::vector<int32_t> replaced;                     // out [M]
+    std::vector<int32_t> log;                          // out [n_log][4]
+};
+
+class SearchInNeighborsFuse {
+  public:
+    SearchInNeighborsFuse() { hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate"); }
+    ~SearchInNeighborsFuse() {
+        if (m_) (void)omv_matcher_destroy(m_);
+        if (st_) (void)hipStreamDestroy(st_);
+    }
+    SearchInNeighborsFuse(const SearchInNeighborsFuse &) = delete;
+    SearchInNeighborsFuse &operator=(const SearchInNeighborsFuse &) = delete;
+
+    // Phase A + phase B for `current` and `targets` (vpTargetKFs order); returns nFused per Fuse call (phase A target-
+    // major, block-minor, then phase B); g's in/out members are updated to the reference's final state.
+    std::vector<int32_t> operator()(FuseGraphView &g, int current, const std::vector<int32_t> &targets,
+                                    const std::vector<float> &inv_level_sigma2) {
+        const int K = g.n_kf, C = g.n_cams, cap = g.kp_cap, M = (int)g.bad.size();
+        if ((int)g.kps.size() != K * C * cap || (int)g.desc.size() != 32 * K * C * cap || (int)g.n_kp.size() != K * C ||
+            (int)g.kf_mps.size() != K * C * cap || (int)g.obs_start.size() != M + 1)
+            throw Error("SearchInNeighborsFuse: inconsistent graph");
+        const int n_cur = [&] { int s = 0; for (int c = 0; c < C; ++c) s += g.n_kp[(size_t)current * C + c]; return s; }();
+        const int need = std::max(1, (int)((size_t)targets.size() * C * std::max(1, n_cur) / std::max(1, K * C) + 1));
+        if (!m_ || need > mps_cap_) {
+            if (m_) (void)omv_matcher_destroy(m_), m_ = nullptr;
+            mps_cap_ = need;
+            check(omv_matcher_create(K, C, cap, mps_cap_, &m_), "omv_matcher_create");
+        }
+        omv_frame_geom geom{};
+        geom.n_cams = C, geom.min_x = 0.f, geom.max_x = (float)g.width, geom.min_y = 0.f, geom.max_y = (float)g.height;
+        geom.nlevels = (int)g.scale_factors.size();
+        for (int l = 0; l < geom.nlevels && l < 16; ++l) geom.scale_factors[l] = g.scale_factors[l];
+        for (int c = 0; c < C && c < 8; ++c) geom.cam_model[c] = g.cam_model.empty() ? OMV_CAM_KB8 : g.cam_model[c];
+        kps_.upload(g.kps.data(), g.kps.size(), st_), desc_.upload(g.desc.data(), g.desc.size(), st_);
+        nkp_.upload(g.n_kp.data(), g.n_kp.size(), st_), ur_.upload(g.uright.data(), g.uright.size(), st_);
+        pos_.upload(g.pos.data(), g.pos.size(), st_), nrm_.upload(g.normal.data(), g.normal.size(), st_);
+        mn_.upload(g.min_dist.data(), g.min_dist.size(), st_), mx_.upload(g.max_dist.data(), g.max_dist.size(), st_);
+        md_.upload(g.mp_desc.data(), g.mp_desc.size(), st_);
+        check(omv_matcher_assign_grid(m_, K, &geom, kps_.p, nkp_.p, st_), "omv_matcher_assign_grid");
+        const size_t obs_cap = 4 * g.obs_kf.size() + 1024, log_cap = 4 * (size_t)M + 1024;
+        std::vector<int32_t> out_start(M + 1), out_kf(obs_cap), out_idx(4 * obs_cap);
+        g.replaced.assign(M, -1);
+        g.log.assign(4 * log_cap, 0);
+        omv_fuse_graph G{};
+        G.n_kf = K, G.n_blocks = g.n_blocks.data(), G.Tcw = g.Tcw.data(), G.Ow = g.Ow.data();
+        G.uright = g.uright.empty() ? nullptr : g.uright.data(), G.kf_mps = g.kf_mps.data();
+        G.n_mps = M, G.bad = g.bad.data(), G.n_obs = g.n_obs.data(), G.replaced = g.replaced.data();
+        G.obs_start = g.obs_start.data(), G.obs_kf = g.obs_kf.data(), G.obs_idx = g.obs_idx.data();
+        G.out_obs_start = out_start.data(), G.out_obs_kf = out_kf.data(), G.out_obs_idx = out_idx.data();
+        G.obs_cap = (int)obs_cap, G.log = g.log.data(), G.log_cap = (int)log_cap;
+        omv_kf_search_params p{};
+        p.mode = OMV_KF_FUSE, p.th = g.th, p.max_dist = 50.f, p.bf = g.bf, p.uright = ur_.p;
+        for (int l = 0; l < (int)inv_level_sigma2.size() && l < 16; ++l) p.inv_level_sigma2[l] = inv_level_sigma2[l];
+        p.log_scale_factor = (float)std::log((double)g.scale_factors[1]);
+        p.n_levels = geom.nlevels;
+        for (int c = 0; c < C && c < 8; ++c)
+            for (int q = 0; q < 8; ++q) p.cams[c][q] = g.cams[8 * c + q];
+        const omv_kf_mps kfm{pos_.p, nrm_.p, mn_.p, mx_.p, md_.p};
+        std::vector<int32_t> n_fused(targets.size() * C + C);
+        check(omv_search_in_neighbors_fuse(m_, &geom, kps_.p, desc_.p, nkp_.p, cap, &G, current, (int)targets.size(),
+                                           targets.data(), &kfm, &p, n_fused.data(), st_),
+              "omv_search_in_neighbors_fuse");
+        md_.download(g.mp_desc.data(), g.mp_desc.size(), st_);
+        hip_check(hipStreamSynchronize(st_), "SearchInNeighborsFuse");
+        const int rows = out_start[M];
+        g.obs_start = out_start;
+        g.obs_kf.assign(out_kf.begin(), out_kf.begin() + rows);
+        g.obs_idx.assign(out_idx.begin(), out_idx.begin() + 4 * (size_t)rows);
+        g.log.resize(4 * (size_t)G.n_log);
+        return n_fused;
+    }
+
+  private:
+    hipStream_t st_ = nullptr;
+    omv_matcher *m_ = nullptr;
+    int mps_cap_ = 0;
+    DeviceArray<omv_kp> kps_;
+    DeviceArray<uint8_t> desc_, md_;
+    DeviceArray<int32_t> nkp_;
+    DeviceArray<float> ur_, pos_, nrm_, mn_, mx_;
 };
 
 // The window as the reference builds its graph: keyframes (each with its body pose, per-camera poses, velocity,

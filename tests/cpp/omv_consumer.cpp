@@ -10,6 +10,11 @@
 //   omv_consumer tri   DIR   SearchForTriangulation of one keyframe pair -> vMatchedPairs
 //   omv_consumer pose  DIR   PoseInertialOptimizer: LastKeyFrame (meta lf 0) or LastFrame + ConstraintPoseImu (lf 1)
 //   omv_consumer fuse  DIR   Fuse per camera block of one keyframe -> chosen keypoint / distance per point
+//   omv_consumer posopt DIR  PoseOptimization(Frame*) on one frame -> pose, mvbOutlier, nGood
+//   omv_consumer cnmp  DIR   CreateNewMapPoints' neighbour loop in two calls (a CheckNewKeyFrames boundary) -> the
+//                            new points in creation order, the current keyframe's has-map-point flags
+//   omv_consumer mprefresh DIR  ComputeDistinctiveDescriptors / UpdateNormalAndDepth over a batch of points
+//   omv_consumer fuseseq DIR SearchInNeighbors' fuse sequence -> final graph, edit log, descriptors
 //   omv_consumer lba   DIR   LocalInertialBAWindow: keyframes added in a mixed fixed / optimisable order,
 //                            EdgeMono + EdgeStereo observations, inertial edges under the reference's robust
 //                            rule (last edge / bRecInit), flattened optimisable-first, optimised, written back
@@ -392,11 +397,151 @@ int run_fuse(const std::string &dir) {
     return 0;
 }
 
+// ---- Optimizer::PoseOptimization(Frame*) on one frame
+int run_posopt(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int C = (int)m["n_cams"], cap = (int)m["kp_cap"];
+    const auto cams = read_bin<float>(dir, "cams");
+    const auto model = read_opt<int32_t>(dir, "cam_model");
+    const auto rq = read_bin<double>(dir, "rig_q"), rt = read_bin<double>(dir, "rig_t");
+    std::vector<std::array<double, 4>> rig_q(C);
+    std::vector<std::array<double, 3>> rig_t(C);
+    for (int c = 0; c < C; ++c) {
+        for (int q = 0; q < 4; ++q) rig_q[c][q] = rq[4 * c + q];
+        for (int q = 0; q < 3; ++q) rig_t[c][q] = rt[3 * c + q];
+    }
+    omv_adapt::PoseOptimization po(C, cams, model, (float)m["bf"], rig_q, rig_t);
+    const auto mc = read_opt<int32_t>(dir, "mono_cam"), mk = read_opt<int32_t>(dir, "mono_kp");
+    const auto mo = read_opt<double>(dir, "mono_obs");
+    const auto mw = read_opt<float>(dir, "mono_w"), mx = read_opt<float>(dir, "mono_xw");
+    const auto sk = read_opt<int32_t>(dir, "stereo_kp");
+    const auto so = read_opt<double>(dir, "stereo_obs");
+    const auto sw = read_opt<float>(dir, "stereo_w"), sx = read_opt<float>(dir, "stereo_xw");
+    std::vector<omv_adapt::PoseOptimization::Mono> mono(mc.size());
+    for (size_t e = 0; e < mc.size(); ++e)
+        mono[e] = {mc[e], mk[e], mo[2 * e], mo[2 * e + 1], mw[e], {mx[3 * e], mx[3 * e + 1], mx[3 * e + 2]}};
+    std::vector<omv_adapt::PoseOptimization::Stereo> stereo(sk.size());
+    for (size_t e = 0; e < sk.size(); ++e)
+        stereo[e] = {sk[e], so[3 * e], so[3 * e + 1], so[3 * e + 2], sw[e], {sx[3 * e], sx[3 * e + 1], sx[3 * e + 2]}};
+    const auto q0 = read_bin<double>(dir, "pose_q"), t0 = read_bin<double>(dir, "pose_t");
+    std::array<double, 4> q{q0[0], q0[1], q0[2], q0[3]};
+    std::array<double, 3> t{t0[0], t0[1], t0[2]};
+    std::vector<uint8_t> outl(cap, 255);
+    const int n_good = po(q, t, mono, stereo, outl);
+    write_bin(dir, "q", q.data(), 4), write_bin(dir, "t", t.data(), 3), write_bin(dir, "kpo", outl);
+    write_bin(dir, "n_good", &n_good, 1);
+    return 0;
+}
+
+// ---- LocalMapping::CreateNewMapPoints: keyframe k's arrays are DIR/kf<k>_*.bin (k = 0 the current keyframe)
+omv_adapt::CnmpKeyFrame read_cnmp_kf(const std::string &dir, int k) {
+    const std::string p = "kf" + std::to_string(k) + "_";
+    omv_adapt::CnmpKeyFrame f;
+    const auto ints = read_bin<int32_t>(dir, p + "ints");   // N NLeft NRight NSideLeft
+    f.view.N = ints[0], f.view.NLeft = ints[1], f.view.NRight = ints[2], f.view.NSideLeft = ints[3];
+    f.view.keys = read_bin<omv_kp>(dir, p + "keys");
+    f.view.descriptors = read_bin<uint8_t>(dir, p + "desc");
+    f.view.has_map_point = read_bin<uint8_t>(dir, p + "has_mp");
+    f.view.feat_node = read_bin<uint32_t>(dir, p + "node_id");
+    f.view.feat_start = read_bin<int32_t>(dir, p + "node_start");
+    f.view.feat_idx = read_bin<int32_t>(dir, p + "node_idx");
+    const auto sg = read_bin<float>(dir, p + "sigma2");
+    std::copy(sg.begin(), sg.begin() + 16, f.view.level_sigma2.begin());
+    const auto T = read_bin<float>(dir, p + "Tcw"), O = read_bin<float>(dir, p + "Ow");
+    for (int c = 0; c < 4; ++c) {
+        std::copy(&T[12 * c], &T[12 * c + 12], f.Tcw[c].begin());
+        std::copy(&O[3 * c], &O[3 * c + 3], f.Ow[c].begin());
+    }
+    const auto g = read_bin<float>(dir, p + "geom");   // Rwc[9] twc[3] fx fy cx cy invfx invfy mb mbf
+    std::copy(&g[0], &g[9], f.Rwc.begin()), std::copy(&g[9], &g[12], f.twc.begin());
+    f.fx = g[12], f.fy = g[13], f.cx = g[14], f.cy = g[15], f.invfx = g[16], f.invfy = g[17], f.mb = g[18], f.mbf = g[19];
+    f.uright = read_bin<float>(dir, p + "uright"), f.depth = read_bin<float>(dir, p + "depth");
+    const auto sf = read_bin<float>(dir, p + "scale");
+    std::copy(sf.begin(), sf.begin() + 16, f.scale_factors.begin());
+    return f;
+}
+
+int run_cnmp(const std::string &dir) {
+    auto m = read_meta(dir);
+    const int n_nb = (int)m["n_nb"], split = (int)m["split"];
+    omv_adapt::CreateNewMapPoints cnmp(read_bin<float>(dir, "cams"), read_bin<int32_t>(dir, "cam_model"), (int)m["n_cams"],
+                                       m["inertial"] != 0, m["monocular"] != 0, m["far"] != 0, (float)m["th_far"]);
+    const omv_adapt::CnmpKeyFrame kf1 = read_cnmp_kf(dir, 0);
+    std::vector<omv_adapt::CnmpKeyFrame> nbs;
+    for (int k = 1; k <= n_nb; ++k) nbs.push_back(read_cnmp_kf(dir, k));
+    const auto Tall = read_bin<float>(dir, "T");
+    std::vector<std::array<std::array<float, 12>, OMV_TRI_PAIRS>> T(n_nb);
+    for (int j = 0; j < n_nb; ++j)
+        for (int q = 0; q < OMV_TRI_PAIRS; ++q) std::copy(&Tall[(j * OMV_TRI_PAIRS + q) * 12], &Tall[(j * OMV_TRI_PAIRS + q) * 12 + 12], T[j][q].begin());
+    const auto skip = read_bin<int32_t>(dir, "skip");
+    std::vector<int> sk(skip.begin(), skip.end());
+    std::vector<uint8_t> has_mp1 = kf1.view.has_map_point;
+    // the neighbours in two calls (a CheckNewKeyFrames() boundary after `split`), side 1 carried over
+    std::vector<omv_adapt::NewMapPoint> pts;
+    std::vector<int> nm_all, nm;
+    for (int part = 0; part < 2; ++part) {
+        const size_t lo = part == 0 ? 0 : (size_t)split, hi = part == 0 ? (size_t)split : (size_t)n_nb;
+        auto p = cnmp(kf1, has_mp1, nbs, T, sk, m["coarse"] != 0, (float)m["scale_factor"], lo, hi, part == 0, &nm);
+        pts.insert(pts.end(), p.begin(), p.end());
+        nm_all.insert(nm_all.end(), nm.begin(), nm.end());
+    }
+    std::vector<int32_t> rec;   // per new point: neighbour idx1 idx2 stereo
+    std::vector<float> x;
+    for (const auto &p : pts) {
+        rec.insert(rec.end(), {p.neighbour, (int32_t)p.idx1, (int32_t)p.idx2, p.stereo ? 1 : 0});
+        x.insert(x.end(), p.x3D.begin(), p.x3D.end());
+    }
+    write_bin(dir, "points", rec), write_bin(dir, "x3d", x), write_bin(dir, "has_mp1", has_mp1);
+    std::vector<int32_t> nmv(nm_all.begin(), nm_all.end());
+    write_bin(dir, "n_matches", nmv);
+    return 0;
+}
+
+// ---- MapPoint::ComputeDistinctiveDescriptors / UpdateNormalAndDepth
+int run_mprefresh(const std::string &dir) {
+    omv_adapt::MapPointRefresh r;
+    std::vector<uint8_t> dout;
+    const auto best = r.distinctive(read_bin<int32_t>(dir, "desc_start"), read_bin<int32_t>(dir, "desc_row"),
+                                    read_bin<uint8_t>(dir, "desc"), dout);
+    write_bin(dir, "best", best), write_bin(dir, "desc_out", dout);
+    auto normal = read_bin<float>(dir, "normal_in");
+    auto mn = read_bin<float>(dir, "min_in"), mx = read_bin<float>(dir, "max_in");
+    r.normal_depth(read_bin<int32_t>(dir, "obs_start"), read_bin<float>(dir, "obs_center"), read_bin<float>(dir, "pos"),
+                   read_bin<float>(dir, "ref_center"), read_bin<float>(dir, "ref_level_scale"),
+                   read_bin<float>(dir, "ref_max_scale"), normal, mn, mx);
+    write_bin(dir, "normal", normal), write_bin(dir, "min_dist", mn), write_bin(dir, "max_dist", mx);
+    return 0;
+}
+
+// ---- LocalMapping::SearchInNeighbors' fuse sequence
+int run_fuseseq(const std::string &dir) {
+    auto m = read_meta(dir);
+    omv_adapt::FuseGraphView g;
+    g.n_kf = (int)m["n_kf"], g.n_cams = (int)m["n_cams"], g.kp_cap = (int)m["kp_cap"];
+    g.width = (int)m["width"], g.height = (int)m["height"], g.bf = (float)m["bf"], g.th = (float)m["th"];
+    g.scale_factors = read_bin<float>(dir, "scale"), g.cams = read_bin<float>(dir, "cams");
+    g.kps = read_bin<omv_kp>(dir, "kps"), g.desc = read_bin<uint8_t>(dir, "desc"), g.n_kp = read_bin<int32_t>(dir, "n_kp");
+    g.uright = read_bin<float>(dir, "uright"), g.n_blocks = read_bin<int32_t>(dir, "n_blocks");
+    g.Tcw = read_bin<omv_se3f>(dir, "Tcw"), g.Ow = read_bin<float>(dir, "Ow"), g.kf_mps = read_bin<int32_t>(dir, "kf_mps");
+    g.pos = read_bin<float>(dir, "pos"), g.normal = read_bin<float>(dir, "normal");
+    g.min_dist = read_bin<float>(dir, "min_dist"), g.max_dist = read_bin<float>(dir, "max_dist");
+    g.mp_desc = read_bin<uint8_t>(dir, "mp_desc"), g.bad = read_bin<int32_t>(dir, "bad"), g.n_obs = read_bin<int32_t>(dir, "n_obs");
+    g.obs_start = read_bin<int32_t>(dir, "obs_start"), g.obs_kf = read_bin<int32_t>(dir, "obs_kf");
+    g.obs_idx = read_bin<int32_t>(dir, "obs_idx");
+    omv_adapt::SearchInNeighborsFuse f;
+    const auto nf = f(g, (int)m["current"], read_bin<int32_t>(dir, "targets"), read_bin<float>(dir, "inv_sigma2"));
+    write_bin(dir, "out_kf_mps", g.kf_mps), write_bin(dir, "out_bad", g.bad), write_bin(dir, "out_n_obs", g.n_obs);
+    write_bin(dir, "out_replaced", g.replaced), write_bin(dir, "out_obs_start", g.obs_start);
+    write_bin(dir, "out_obs_kf", g.obs_kf), write_bin(dir, "out_obs_idx", g.obs_idx), write_bin(dir, "out_log", g.log);
+    write_bin(dir, "out_desc", g.mp_desc), write_bin(dir, "out_n_fused", nf);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
     if (argc != 3) {
-        std::fprintf(stderr, "usage: %s orb|frame|lba|lastframe|tri|pose|fuse DIR\n", argv[0]);
+        std::fprintf(stderr, "usage: %s orb|frame|lba|lastframe|tri|pose|fuse|posopt|cnmp|mprefresh|fuseseq DIR\n", argv[0]);
         return 2;
     }
     try {
@@ -408,6 +553,10 @@ int main(int argc, char **argv) {
         if (mode == "tri") return run_tri(dir);
         if (mode == "pose") return run_pose(dir);
         if (mode == "fuse") return run_fuse(dir);
+        if (mode == "posopt") return run_posopt(dir);
+        if (mode == "cnmp") return run_cnmp(dir);
+        if (mode == "mprefresh") return run_mprefresh(dir);
+        if (mode == "fuseseq") return run_fuseseq(dir);
         std::fprintf(stderr, "unknown mode %s\n", argv[1]);
         return 2;
     } catch (const std::exception &e) {

@@ -361,3 +361,130 @@ def test_fuse_adapter(tmp_path, oracle):
     ent = np.concatenate([np.arange(j["mp_start"], j["mp_start"] + j["mp_count"]) for _, j in jobs])
     assert np.array_equal(bi, bi_o[ent]) and np.array_equal(bd, bd_o[ent])
     assert np.array_equal(nf, n_o[[i for i, _ in jobs]]) and nf.sum() > 30
+
+
+# ---- the round-6 drop-ins: PoseOptimization, CreateNewMapPoints' loop, the map-point refresh, the fuse sequence --------
+def test_pose_optimization_adapter(tmp_path, oracle):
+    """Optimizer::PoseOptimization(Frame*) through the C++ adapter on one 4-camera frame: pose within the GPU parity
+    bar of tests/test_pose_only_gpu.py (1e-7), mvbOutlier and nGood identical to the oracle."""
+    from openmavis_amd import synth_pose
+    b = synth_pose.make_pose_only_batch(n_frames=1, n_pts=400, seed=21, n_cams=4, outlier_frac=0.15)
+    rq, rt, rk, rn = oracle.pose_optimization(b)
+    _meta(tmp_path, n_cams=4, bf=float(b["bf"]), kp_cap=int(b["kp_cap"]))
+    _w(tmp_path, "cams", np.asarray(b["cam"], np.float32))
+    if "cam_model" in b:
+        _w(tmp_path, "cam_model", np.asarray(b["cam_model"], np.int32))
+    _w(tmp_path, "rig_q", np.asarray(b["rig_q"], np.float64)), _w(tmp_path, "rig_t", np.asarray(b["rig_t"], np.float64))
+    _w(tmp_path, "pose_q", np.asarray(b["pose_q"][0], np.float64)), _w(tmp_path, "pose_t", np.asarray(b["pose_t"][0], np.float64))
+    for k, dt in (("mono_cam", np.int32), ("mono_kp", np.int32), ("mono_obs", np.float64)):
+        _w(tmp_path, k, np.asarray(b[k], dt))
+    _w(tmp_path, "mono_w", np.asarray(b["mono_inv_sigma2"], np.float32))
+    _w(tmp_path, "mono_xw", np.asarray(b["mono_xw"], np.float32))
+    _run("posopt", tmp_path)
+    q, t = _r(tmp_path, "q", np.float64), _r(tmp_path, "t", np.float64)
+    kpo, ng = _r(tmp_path, "kpo", np.uint8), _r(tmp_path, "n_good", np.int32)
+    assert ng[0] == rn[0]
+    np.testing.assert_array_equal(kpo[b["mono_kp"]], rk[0][b["mono_kp"]])
+    np.testing.assert_allclose(q, rq[0], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(t, rt[0], rtol=0, atol=1e-7)
+
+
+def _cnmp_kf_files(d, k, kf, s):
+    p = f"kf{k}_"
+    _w(d, p + "ints", np.array([kf["n"], kf["n_left"], kf["n_right"], kf["n_sideleft"]], np.int32))
+    _w(d, p + "keys", kf["kps"]), _w(d, p + "desc", kf["desc"]), _w(d, p + "has_mp", kf["has_mp"].astype(np.uint8))
+    _w(d, p + "node_id", kf["node_id"].astype(np.uint32)), _w(d, p + "node_start", kf["node_start"].astype(np.int32))
+    _w(d, p + "node_idx", kf["node_idx"].astype(np.int32))
+    sg = np.zeros(16, np.float32)
+    sg[:8] = s["sigma2"]
+    _w(d, p + "sigma2", sg), _w(d, p + "Tcw", kf["Tcw"].astype(np.float32)), _w(d, p + "Ow", kf["Ow"].astype(np.float32))
+    fx, fy = np.float32(s["fx"]), np.float32(s["fy"])
+    geom = np.concatenate([kf["Rwc"], kf["twc"], [fx, fy, s["cx"], s["cy"], np.float32(1) / fx, np.float32(1) / fy,
+                                                  np.float32(s["mb"]), np.float32(s["mbf"])]]).astype(np.float32)
+    _w(d, p + "geom", geom), _w(d, p + "uright", kf["uright"]), _w(d, p + "depth", kf["depth"])
+    sc = np.zeros(16, np.float32)
+    sc[:8] = s["scale"]
+    _w(d, p + "scale", sc)
+
+
+def test_create_new_map_points_adapter(tmp_path, oracle):
+    """LocalMapping::CreateNewMapPoints' neighbour loop through the C++ adapter, split over two calls (a
+    CheckNewKeyFrames() boundary): the new points in the reference's creation order with their x3D bits, the search
+    counts and the current keyframe's has-map-point flags, identical to the interleaved oracle."""
+    from openmavis_amd import synth_cnmp
+    s = synth_cnmp.make_cnmp_chain(seed=8, n_neigh=10)
+    hm, nm, outs, _ = oracle.local_mapping_create_new_map_points(s)
+    n_nb = len(s["nbs"])
+    _meta(tmp_path, n_nb=n_nb, split=4, n_cams=4, inertial=1, monocular=0, coarse=0, far=0, th_far=50.0,
+          scale_factor=s["scale_factor"])
+    _w(tmp_path, "cams", s["cams"]), _w(tmp_path, "cam_model", s["cam_model"])
+    _cnmp_kf_files(tmp_path, 0, s["kf1"], s)
+    for j, nb in enumerate(s["nbs"]):
+        _cnmp_kf_files(tmp_path, j + 1, nb["kf2"], s)
+    _w(tmp_path, "T", np.stack([nb["T"] for nb in s["nbs"]]).astype(np.float32))
+    _w(tmp_path, "skip", np.array([nb["skip"] for nb in s["nbs"]], np.int32))
+    _run("cnmp", tmp_path)
+    rec = _r(tmp_path, "points", np.int32).reshape(-1, 4)
+    x = _r(tmp_path, "x3d", np.float32).reshape(-1, 3)
+    exp = [(j, i, int(m12[i]), int(st[i] == 2)) for j, (m12, st, _x) in enumerate(outs) for i in np.flatnonzero(st > 0)]
+    assert [tuple(r) for r in rec] == exp
+    ex = np.array([outs[j][2][i] for j, i, _, _ in exp], np.float32).reshape(-1, 3)
+    assert np.array_equal(x.view(np.uint32), ex.view(np.uint32))
+    np.testing.assert_array_equal(_r(tmp_path, "has_mp1", np.uint8), hm)
+    np.testing.assert_array_equal(_r(tmp_path, "n_matches", np.int32), nm)
+    assert len(exp) > 200
+
+
+def test_map_point_refresh_adapter(tmp_path, oracle):
+    """MapPoint::ComputeDistinctiveDescriptors / UpdateNormalAndDepth through the C++ adapter: rows, descriptors and
+    the float normal / distances bit-exact vs the oracle."""
+    from openmavis_amd import synth_mappoint
+    mp = synth_mappoint.make_points(n_points=600, seed=4)
+    g = synth_mappoint.make_geometry(n_points=800, seed=5)
+    for k in ("desc", "desc_start", "desc_row"):
+        _w(tmp_path, k, mp[k])
+    for k in ("obs_start", "obs_center", "pos", "ref_center", "ref_level_scale", "ref_max_scale"):
+        _w(tmp_path, k, np.ascontiguousarray(g[k]))
+    P = len(g["obs_start"]) - 1
+    _w(tmp_path, "normal_in", np.full((P, 3), np.nan, np.float32))
+    _w(tmp_path, "min_in", np.full(P, np.nan, np.float32)), _w(tmp_path, "max_in", np.full(P, np.nan, np.float32))
+    _run("mprefresh", tmp_path)
+    best = oracle.distinctive_descriptors(mp["desc"], mp["desc_start"], mp["desc_row"])
+    np.testing.assert_array_equal(_r(tmp_path, "best", np.int32), best)
+    d = _r(tmp_path, "desc_out", np.uint8).reshape(-1, 32)
+    has = best >= 0
+    np.testing.assert_array_equal(d[has], mp["desc"][best[has]])
+    on, omin, omax = oracle.normal_depth(**g)
+    for name, ref in (("normal", on), ("min_dist", omin), ("max_dist", omax)):
+        got = _r(tmp_path, name, np.float32).reshape(ref.shape)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), name
+
+
+def test_search_in_neighbors_fuse_adapter(tmp_path, oracle):
+    """SearchInNeighbors' fuse sequence through the C++ adapter: final mvpMapPoints, isBad / mpReplaced / nObs /
+    mObservations, the edit log, nFused per call and the final descriptors identical to the literal oracle."""
+    from openmavis_amd import synth_fuse
+    from openmavis_amd.matcher import kf_search_params
+    s = synth_fuse.make_fuse_scene(seed=5, n_targets=6)
+    ref = oracle.search_in_neighbors_fuse(s)
+    sc = [1.0]
+    for _ in range(1, s["nlevels"]):
+        sc.append(float(np.float32(sc[-1] * np.float32(1.2))))
+    p = kf_search_params(3.0, 50.0, s["cams"], nlevels=s["nlevels"])
+    _meta(tmp_path, n_kf=s["n_kf"], n_cams=s["n_cams"], kp_cap=s["kp_cap"], width=s["width"], height=s["height"],
+          bf=s["bf"], th=3.0, current=s["current"])
+    _w(tmp_path, "scale", np.array(sc, np.float32)), _w(tmp_path, "cams", s["cams"])
+    _w(tmp_path, "inv_sigma2", np.array([p.inv_level_sigma2[i] for i in range(16)], np.float32))
+    for k in ("kps", "desc", "n_kp", "uright", "n_blocks", "Tcw", "Ow", "kf_mps", "bad", "n_obs", "obs_start", "obs_kf",
+              "obs_idx", "targets"):
+        _w(tmp_path, k, np.ascontiguousarray(s[k]))
+    for k in ("pos", "normal", "min_dist", "max_dist"):
+        _w(tmp_path, k, s["mps"][k])
+    _w(tmp_path, "mp_desc", s["mps"]["desc"])
+    _run("fuseseq", tmp_path)
+    for k, dt in (("kf_mps", np.int32), ("bad", np.int32), ("n_obs", np.int32), ("replaced", np.int32),
+                  ("obs_start", np.int32), ("obs_kf", np.int32), ("obs_idx", np.int32), ("log", np.int32),
+                  ("n_fused", np.int32)):
+        np.testing.assert_array_equal(_r(tmp_path, "out_" + k, dt), np.asarray(ref[k]).ravel(), err_msg=k)
+    np.testing.assert_array_equal(_r(tmp_path, "out_desc", np.uint8).reshape(-1, 32), ref["desc"])
+    assert (ref["log"][:, 0] == 1).sum() > 20
