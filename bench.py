@@ -1588,6 +1588,31 @@ def main():
             roof["extraction_traffic_ratio"] = round(per_img / ref_img, 3)
             roof["extraction_traffic_bytes_per_image"] = int(per_img)
             roof["extraction_algorithmic_bytes_per_image"] = int(ref_img)
+        # what does bound the extraction kernels: instruction issue from the SQ PMC passes (tools/pmc_orb_bound.sh,
+        # profiles/<tag>_orb_bound.json) against this run's isolated launch times.  Chip VALU issue rate: 1,024 SIMDs,
+        # one wave64 VALU instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md); LDS: one instruction per CU-cycle.
+        bpath, bnd = newest_profile("orb_bound")
+        if bnd is not None:
+            imgs = Bg * C
+            issue = {"source": f"{bpath} ({bnd.get('tag')})", "peak_valu_wave_insts_per_s": 1024 * 2.4e9 / 2,
+                     "kernels": {}}
+            for k, r in bnd.get("kernels", {}).items():
+                t = kernels.get(k, {}).get("isolated", {}).get("avg_launch_ms")
+                if not t:
+                    continue
+                waves = r["waves_per_image"] * imgs
+                vf = waves * r["valu_per_wave"] / (t * 1e-3) / (1024 * 2.4e9 / 2)
+                lf = waves * r["lds_per_wave"] / (t * 1e-3) / (256 * 2.4e9)
+                issue["kernels"][k] = {"valu_issue_frac": round(vf, 3), "lds_issue_frac": round(lf, 3),
+                                       "per_wave_active_valu": r["active_valu"], "per_wave_wait_any": r["wait_any"],
+                                       "valu_per_wave": r["valu_per_wave"], "waves_per_launch": int(waves)}
+            if issue["kernels"]:
+                top = max(issue["kernels"], key=lambda k: issue["kernels"][k]["valu_issue_frac"])
+                vf = issue["kernels"][top]["valu_issue_frac"]
+                issue["bound"] = (f"VALU issue: {top} issues {vf:.0%} of the chip's VALU rate at < 10 % of HBM"
+                                  if vf >= 0.5 else
+                                  f"latency: the busiest kernel ({top}) issues {vf:.0%} of the chip's VALU rate")
+                roof["extraction_issue"] = issue
         # the whole path: SURVEY §8(d) bytes of a multi-camera frame (5 extractions + matching) x frames/s
         frame_bytes = C * cam_bytes(W, H, 0) + 56 * n_kp_step / B + 968_000
         roof["pipeline"] = {"bytes_per_frame": int(frame_bytes), "achieved": round(frame_bytes * value / 1e9, 2),

@@ -244,6 +244,13 @@ __device__ __forceinline__ int xcd_block(int n_logical) {
 }
 __host__ inline int xcd_grid(int n_logical) { return (n_logical + 7) & ~7; }
 
+}  // namespace omv
+// v_mul_u32_u24 (full rate) for operands the caller knows are < 2^24: HIP's __umul24 masks its operands and the
+// backend then emits v_and + v_mul_lo_u32 (quarter rate) unless it can prove the mask redundant.
+extern "C" __device__ __attribute__((const)) uint32_t omv_llvm_mul_u24(uint32_t, uint32_t) __asm("llvm.amdgcn.mul.u24.i32");
+namespace omv {
+__device__ __forceinline__ int mul_u24(int a, int b) { return (int)omv_llvm_mul_u24((uint32_t)a, (uint32_t)b); }
+
 // Test knobs of a matcher handle (OMV_BOW_TOP, OMV_TRI_SLICES, OMV_TRI_ECAP, OMV_TRI_WALK, OMV_CAND, OMV_CAND_PW),
 // read once by omv_matcher_create (not per call); -1 / 0: unset.  Defined in match.hip for the other matcher
 // translation units.

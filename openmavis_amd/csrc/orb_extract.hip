@@ -77,6 +77,9 @@ struct LevelGeom {
     float size;             // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
     int xtab_off, ytab_off; // resize tables (l >= 1)
     int xq_off, use_xq;     // quad table (l >= 1; use_xq: every pixel pair's sources fit two dwords)
+    // q / d as __umulhi(q, ceil(2^32 / d)) (exact for q < 2^16), host-computed: d = output quads (w + 3) / 4, the
+    // 16-byte groups of a staged row (w + 15) / 16, and w (a 64-bit division per launch was ~100 scalar instructions)
+    uint32_t m_quads, m_groups, m_w;
 };
 
 struct Cell {
@@ -111,6 +114,7 @@ struct __attribute__((aligned(16))) XQuad {
     uint32_t sel[4], cf[4];
     int pad[2];
 };
+static_assert(sizeof(XQuad) == 48, "XQuad LDS addressing");
 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_t *images, size_t img_stride,
@@ -131,6 +135,13 @@ __device__ __forceinline__ const uint8_t *level_base(const Geom &g, const uint8_
 // output pixels per step and stores them as one dword (level pitches are 16-byte aligned).
 constexpr int kPyrBlock = 16;
 
+// cv::resize's vertical pass on the horizontal sums: (b0 (h0 >> 4) >> 16) + (b1 (h1 >> 4) >> 16) + 2 >> 2.  The
+// coefficients are < 2^12 and h >> 4 < 2^15 (both non-negative), so the products are 24-bit multiplies at full rate
+// (an int multiply is v_mul_lo_u32, a quarter-rate instruction: 8 of them per output quad).
+__device__ __forceinline__ int vmix(int b0, int b1, int h0, int h1) {
+    return ((omv::mul_u24(b0, h0 >> 4) >> 16) + (omv::mul_u24(b1, h1 >> 4) >> 16) + 2) >> 2;
+}
+
 __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const uint8_t *images, size_t img_stride,
                                                          size_t pitch0, uint8_t *pyr, const XTab *xt,
                                                          const XTab *yt, const XQuad *xq, int n_images) {
@@ -145,42 +156,46 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
     const int nq = (L.w + 3) >> 2;
     XTab *xs = reinterpret_cast<XTab *>(pyr_lds);            // [L.w]  (generic path)
     XQuad *xqs = reinterpret_cast<XQuad *>(pyr_lds);         // [nq]   (quad path)
-    uint32_t *rows = pyr_lds + 12 * nq;                      // [nr][ndw] (+1 dword of slack)
+    uint32_t *rows = pyr_lds + 12 * nq;                      // [nr][ndw] (+4 dwords of slack)
     const int sy0 = yt[L.ytab_off + dy0].sx0, sy1 = yt[L.ytab_off + dy1 - 1].sx1;
     const int nr = sy1 - sy0 + 1;
+    XTab *ys = reinterpret_cast<XTab *>(rows + nr * ndw + 4);   // [kPyrBlock] the block's y entries
     const bool quad = L.use_xq != 0;
     if (quad)
         for (int i = tid; i < nq; i += 256) xqs[i] = xq[L.xq_off + i];
     else
         for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
+    if (tid < dy1 - dy0) ys[tid] = yt[L.ytab_off + dy0 + tid];
     // q / d as __umulhi(q, ceil(2^32 / d)): exact for q < 2^32 / d (q < 2^16 here)
-    auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
     if ((sp & 15) == 0 && (((uintptr_t)src) & 15) == 0) {   // 16-byte loads (the groups stay inside the pitch)
         const int n4 = ndw >> 2;
-        const uint32_t m4 = divm(n4);
+        const uint32_t m4 = g.lv[l - 1].m_groups;
         for (int q = tid; q < nr * n4; q += 256) {
             const int r = (int)__umulhi((uint32_t)q, m4), i = q - r * n4;
             reinterpret_cast<uint4 *>(rows)[q] = reinterpret_cast<const uint4 *>(src + (size_t)(sy0 + r) * sp)[i];
         }
     } else {
         uint8_t *b = reinterpret_cast<uint8_t *>(rows);
-        const uint32_t mw = divm(sw);
+        const uint32_t mw = g.lv[l - 1].m_w;
         for (int q = tid; q < nr * sw; q += 256) {
             const int r = (int)__umulhi((uint32_t)q, mw), i = q - r * sw;
             b[(size_t)r * ndw * 4 + i] = src[(size_t)(sy0 + r) * sp + i];
         }
     }
     __syncthreads();
-    const uint32_t mq = divm(nq);
+    const uint32_t mq = L.m_quads;
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     for (int q = tid; q < (dy1 - dy0) * nq; q += 256) {
-        const int r = (int)__umulhi((uint32_t)q, mq), qd = q - r * nq, dx0 = qd * 4, dy = dy0 + r;
-        const XTab y = yt[L.ytab_off + dy];
+        // row / column split and LDS row offsets as 24-bit multiplies (r < kPyrBlock, nq and ndw < 2^12)
+        const int r = (int)__umulhi((uint32_t)q, mq), qd = q - omv::mul_u24(r, nq), dx0 = qd * 4,
+                  dy = dy0 + r;
+        const XTab y = ys[r];
         const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
         uint32_t packed = 0;
         if (quad) {
-            const XQuad X = xqs[qd];
-            const uint32_t *R0 = rows + (size_t)(y.sx0 - sy0) * ndw, *R1 = rows + (size_t)(y.sx1 - sy0) * ndw;
+            const XQuad X = *reinterpret_cast<const XQuad *>(reinterpret_cast<const char *>(xqs) + omv::mul_u24(qd, 48u));
+            const uint32_t *R0 = rows + omv::mul_u24(y.sx0 - sy0, ndw),
+                           *R1 = rows + omv::mul_u24(y.sx1 - sy0, ndw);
             const uint32_t u0[4] = {R0[X.a[0]], R0[X.a[0] + 1], R0[X.a[1]], R0[X.a[1] + 1]};
             const uint32_t u1[4] = {R1[X.a[0]], R1[X.a[0] + 1], R1[X.a[1]], R1[X.a[1] + 1]};
 #pragma unroll
@@ -191,12 +206,11 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
                     __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u0[pp + 1], u0[pp], X.sel[j])), cf, 0u, false);
                 const int h1 = (int)__builtin_amdgcn_udot2(
                     __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u1[pp + 1], u1[pp], X.sel[j])), cf, 0u, false);
-                const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-                packed |= (uint32_t)min(v, 255) << (8 * j);
+                packed |= (uint32_t)vmix(b0, b1, h0, h1) << (8 * j);   // <= 255: the weights sum to <= 2049
             }
         } else {
-            const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx0 - sy0) * ndw);
-            const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + (size_t)(y.sx1 - sy0) * ndw);
+            const uint8_t *R0 = reinterpret_cast<const uint8_t *>(rows + omv::mul_u24(y.sx0 - sy0, ndw));
+            const uint8_t *R1 = reinterpret_cast<const uint8_t *>(rows + omv::mul_u24(y.sx1 - sy0, ndw));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int dx = dx0 + j;
@@ -205,7 +219,7 @@ __global__ void __launch_bounds__(256) pyr_resize_kernel(Geom g, int l, const ui
                     const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
                     const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
                     const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
-                    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                    const int v = vmix(b0, b1, h0, h1);
                     packed |= (uint32_t)min(v, 255) << (8 * j);
                 }
             }
@@ -243,21 +257,20 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
     XTab *ys = reinterpret_cast<XTab *>(tab + tab_dw);
     XQuad *xqs = reinterpret_cast<XQuad *>(tab);
     XTab *xs = reinterpret_cast<XTab *>(tab);
-    auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
     {   // level 0's needed rows from the image
         const PyrBand b0 = B[0];
         const int sw = g.lv[0].w, ndw = ((sw + 15) >> 4) << 2, nr = b0.need_hi - b0.need_lo;
         const uint8_t *src = images + (size_t)img * img_stride;
         if ((pitch0 & 15) == 0 && (((uintptr_t)src) & 15) == 0) {
             const int n4 = ndw >> 2;
-            const uint32_t m4 = divm(n4);
+            const uint32_t m4 = g.lv[0].m_groups;
             for (int q = tid; q < nr * n4; q += 256) {
                 const int r = (int)__umulhi((uint32_t)q, m4), i = q - r * n4;
                 reinterpret_cast<uint4 *>(prev)[q] = reinterpret_cast<const uint4 *>(src + (size_t)(b0.need_lo + r) * pitch0)[i];
             }
         } else {
             uint8_t *bb = reinterpret_cast<uint8_t *>(prev);
-            const uint32_t mw = divm(sw);
+            const uint32_t mw = g.lv[0].m_w;
             for (int q = tid; q < nr * sw; q += 256) {
                 const int r = (int)__umulhi((uint32_t)q, mw), i = q - r * sw;
                 bb[(size_t)r * ndw * 4 + i] = src[(size_t)(b0.need_lo + r) * pitch0 + i];
@@ -278,15 +291,17 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
             for (int i = tid; i < L.w; i += 256) xs[i] = xt[L.xtab_off + i];
         for (int i = tid; i < nr; i += 256) ys[i] = yt[L.ytab_off + bc.need_lo + i];
         __syncthreads();
-        const uint32_t mq = divm(nq);
+        const uint32_t mq = L.m_quads;
         for (int q = tid; q < nr * nq; q += 256) {
-            const int r = (int)__umulhi((uint32_t)q, mq), qd = q - r * nq, dx0 = qd * 4, dy = bc.need_lo + r;
+            const int r = (int)__umulhi((uint32_t)q, mq), qd = q - omv::mul_u24(r, nq), dx0 = qd * 4,
+                      dy = bc.need_lo + r;
             const XTab y = ys[r];
             const int b0 = (short)(y.coef & 0xffff), b1 = (short)(y.coef >> 16);
             uint32_t packed = 0;
             if (quad) {
-                const XQuad X = xqs[qd];
-                const uint32_t *R0 = prev + (size_t)(y.sx0 - bp.need_lo) * sndw, *R1 = prev + (size_t)(y.sx1 - bp.need_lo) * sndw;
+                const XQuad X = *reinterpret_cast<const XQuad *>(reinterpret_cast<const char *>(xqs) + omv::mul_u24(qd, 48u));
+                const uint32_t *R0 = prev + omv::mul_u24(y.sx0 - bp.need_lo, sndw),
+                               *R1 = prev + omv::mul_u24(y.sx1 - bp.need_lo, sndw);
                 const uint32_t u0[4] = {R0[X.a[0]], R0[X.a[0] + 1], R0[X.a[1]], R0[X.a[1] + 1]};
                 const uint32_t u1[4] = {R1[X.a[0]], R1[X.a[0] + 1], R1[X.a[1]], R1[X.a[1] + 1]};
 #pragma unroll
@@ -297,12 +312,11 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
                         __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u0[pp + 1], u0[pp], X.sel[j])), cf, 0u, false);
                     const int h1 = (int)__builtin_amdgcn_udot2(
                         __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(u1[pp + 1], u1[pp], X.sel[j])), cf, 0u, false);
-                    const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-                    packed |= (uint32_t)min(v, 255) << (8 * j);
+                    packed |= (uint32_t)vmix(b0, b1, h0, h1) << (8 * j);   // <= 255: the weights sum to <= 2049
                 }
             } else {
-                const uint8_t *R0 = reinterpret_cast<const uint8_t *>(prev + (size_t)(y.sx0 - bp.need_lo) * sndw);
-                const uint8_t *R1 = reinterpret_cast<const uint8_t *>(prev + (size_t)(y.sx1 - bp.need_lo) * sndw);
+                const uint8_t *R0 = reinterpret_cast<const uint8_t *>(prev + omv::mul_u24(y.sx0 - bp.need_lo, sndw));
+                const uint8_t *R1 = reinterpret_cast<const uint8_t *>(prev + omv::mul_u24(y.sx1 - bp.need_lo, sndw));
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int dx = dx0 + j;
@@ -311,12 +325,12 @@ __global__ void __launch_bounds__(256) pyr_chain_kernel(Geom g, const uint8_t *i
                         const int a0 = (short)(x.coef & 0xffff), a1 = (short)(x.coef >> 16);
                         const int h0 = R0[x.sx0] * a0 + R0[x.sx1] * a1;
                         const int h1 = R1[x.sx0] * a0 + R1[x.sx1] * a1;
-                        const int v = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+                        const int v = vmix(b0, b1, h0, h1);
                         packed |= (uint32_t)min(v, 255) << (8 * j);
                     }
                 }
             }
-            cur[(size_t)r * cndw + qd] = packed;   // the next level's source row (bytes past the width are never read)
+            cur[omv::mul_u24(r, cndw) + qd] = packed;   // the next level's source row (bytes past the width are never read)
             if (dy >= bc.own_lo && dy < bc.own_hi) {
                 uint8_t *dst = pyr + (size_t)img * g.pyr_bytes + L.off + (size_t)dy * L.pitch;
                 if (dx0 + 3 < L.w) {
@@ -456,8 +470,8 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
     // i / dw by multiply-shift with m = floor(2^20/dw) + 1: exact while i * dw < 2^20 (cells are < 80 px wide)
     const uint32_t mdw = dw > 0 ? (1u << 20) / (uint32_t)dw + 1u : 0u;
     auto rowcol = [&](int i, int &r, int &q) {
-        const int rr = (int)(((uint32_t)i * mdw) >> 20);
-        r = 3 + rr, q = 3 + i - rr * dw;
+        const int rr = omv::mul_u24(i, (int)mdw) >> 20;
+        r = 3 + rr, q = 3 + i - omv::mul_u24(rr, dw);   // 24-bit multiplies: full rate
     };
     const uint64_t lt = (1ull << lane) - 1ull;
     // compass prefilter at threshold t: the row-major candidate list cand[0..n) (returns n)
@@ -496,9 +510,9 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 uint32_t bits = 0;
                 int r = 3, jq = jq0;
                 if (tp < np) {
-                    const int rr = (int)(((uint32_t)tp * mp) >> 20);
-                    r = 3 + rr, jq = jq0 + 2 * (tp - rr * npr);
-                    const int j = r * rsw + jq;
+                    const int rr = omv::mul_u24(tp, (int)mp) >> 20;   // tp < 2^13, mp <= 2^20 + 1
+                    r = 3 + rr, jq = jq0 + 2 * (tp - omv::mul_u24(rr, npr));
+                    const int j = omv::mul_u24(r, rsw) + jq;
                     const uint32_t Wm = w32[j - 1], C0 = w32[j], C1 = w32[j + 1], Wp = w32[j + 2];
                     const uint32_t D0 = w32[j + 3 * rsw], D1 = w32[j + 3 * rsw + 1];
                     const uint32_t U0 = w32[j - 3 * rsw], U1 = w32[j - 3 * rsw + 1];
@@ -520,7 +534,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const int cnt = __popc(bits);
                 const int incl = wave_incl_scan_dpp(cnt);
                 int pos = ncand + incl - cnt;
-                const int ibase = (r - 3) * dw + (4 * jq - o) - 3;
+                const int ibase = omv::mul_u24(r - 3, dw) + (4 * jq - o) - 3;
                 // row-major: lanes hold consecutive pairs, bit k = column q0 + k (a few set bits per lane)
                 for (uint32_t b = bits; b; b &= b - 1u) cand[pos++] = (uint16_t)(ibase + __builtin_ctz(b));
                 ncand += __builtin_amdgcn_readlane(incl, 63);
@@ -552,7 +566,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
             int r, q;
             rowcol(i, r, q);
             const int sv = fast_strength_h<RS>(pix + r * rs + q, rs);
-            S[(r - 2) * sw + (q - 2)] = (uint8_t)min(max(sv, 0), 255);
+            S[omv::mul_u24(r - 2, sw) + (q - 2)] = (uint8_t)min(max(sv, 0), 255);
         }
         __syncthreads();
         return ncand;
@@ -570,7 +584,7 @@ __global__ void __launch_bounds__(64) fast_cells_kernel(Geom g, const Cell *cell
                 const int i = cand[k];
                 int r, q;
                 rowcol(i, r, q);
-                const uint8_t *sp8 = S + (r - 2) * sw + (q - 2);
+                const uint8_t *sp8 = S + omv::mul_u24(r - 2, sw) + (q - 2);
                 const int v = sp8[0];
                 // v > th and v - 1 > (nv > th ? nv - 1 : 0) for all 8 neighbours <=> v > max(nv..., th, 1)
                 int m = max(th, 1);
@@ -1325,7 +1339,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     // = the four pair dwords from R0 >> 1, realigned by a half when R0 is odd
     auto blurred = [&](int dx, int dy) -> uint32_t {
         const int R0 = dy + 18;   // 0 .. 36, and dx + 18 too: 24-bit multiplies (full rate)
-        const uint32_t *q = H + __umul24((uint32_t)(dx + 18), (uint32_t)kHStride) + (R0 >> 1);
+        const uint32_t *q = H + omv::mul_u24(dx + 18, kHStride) + (R0 >> 1);
         const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
         const uint32_t sh = (uint32_t)(R0 & 1) << 4;
         const uint32_t w0 = __builtin_amdgcn_alignbit(d1, d0, sh), w1 = __builtin_amdgcn_alignbit(d2, d1, sh),
@@ -1595,6 +1609,8 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
             }
         }
         prev_w = L.w, prev_h = L.h;
+        auto divm = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
+        L.m_quads = divm((L.w + 3) / 4), L.m_groups = divm((L.w + 15) / 16), L.m_w = divm(L.w);
     }
     g.n_cells = (int)cells.size();
     if (max_rw > 80 || max_rh > 80) return OMV_ERR_ARG;   // K2's index arithmetic (cells are ~35-45 px)
@@ -1713,7 +1729,8 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
             const int dy1 = std::min(dy0 + kPyrBlock, L.h);
             nr = std::max(nr, yt[L.ytab_off + dy1 - 1].sx1 - yt[L.ytab_off + dy0].sx0 + 1);
         }
-        o->pyr_lds[l] = sizeof(uint32_t) * (12 * (size_t)((L.w + 3) / 4) + (size_t)nr * (((g.lv[l - 1].w + 15) / 16) * 4) + 4);
+        o->pyr_lds[l] = sizeof(uint32_t) * (12 * (size_t)((L.w + 3) / 4) + (size_t)nr * (((g.lv[l - 1].w + 15) / 16) * 4) + 4 +
+                                            3 * kPyrBlock);
         if (o->pyr_lds[l] > 160 * 1024) {   // images wider than ~8000 px
             delete o;
             return OMV_ERR_ARG;
