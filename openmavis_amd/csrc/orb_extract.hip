@@ -28,7 +28,6 @@
 #include <climits>
 #include <cstdio>
 #include <cstring>
-#include <set>
 #include <vector>
 
 #include "../../include/omv.h"
@@ -1167,14 +1166,12 @@ struct DescArgs {
     int *n_out, *mono;
     int n_images;
     const uint32_t *disc;    // [64][8] per lane: (row-sum mask, weight mask) of its four centroid dot4 items
-    const uint32_t *hitem;   // [kHItemIt * 64] horizontal items: raw dword offset | column-major offset << 16
     float *harris;           // optional [n_images][n_max]: OpenCV ORB's Harris response per output row
 };
 
 constexpr int kRawRows = 43, kRawDw = 12;   // raw patch: rows cy-21 .. cy+21, 48 bytes each (43 used + alignment)
 constexpr int kHCols = 40, kHStride = 23;   // horizontal sums: 40 columns x 22 row pairs (stride 23 dwords)
 constexpr int kDescDw = kRawRows * kRawDw + kHCols * kHStride;   // LDS dwords per wave (5,744 B)
-constexpr int kHItemIt = 4;                 // horizontal items per lane (<= 256 per keypoint)
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, dword-aligned
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -1185,17 +1182,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the 7-tap sums of output columns 4q .. 4q+3 of one raw row whose dwords q .. q+3 are d0..d3 (byte offset po)
-__device__ __forceinline__ void hsum4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, int po, uint32_t h[4]) {
-    constexpr uint32_t G0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), G1 = 48u | (34u << 8) | (18u << 16);
-    const uint32_t A = __builtin_amdgcn_alignbyte(d1, d0, po), B = __builtin_amdgcn_alignbyte(d2, d1, po),
-                   C = __builtin_amdgcn_alignbyte(d3, d2, po);
-    h[0] = __builtin_amdgcn_udot4(B, G1, __builtin_amdgcn_udot4(A, G0, 0u, false), false);
-#pragma unroll
-    for (int k = 1; k < 4; ++k)
-        h[k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(C, B, k), G1,
-                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(B, A, k), G0, 0u, false), false);
-}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n_blocks) {
     // the wave index is wave-uniform: everything derived from the slot (record, level, counts, patch origin) is
@@ -1224,9 +1211,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     if (j >= cnts[3 * l]) return;
     // the lane's constant tables (independent of the record: in flight together)
     const uint4 dm0 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane], dm1 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane + 1];
-    uint32_t hit[kHItemIt], pat[4];
-#pragma unroll
-    for (int it = 0; it < kHItemIt; ++it) hit[it] = a.hitem[lane + 64 * it];
+    uint32_t pat[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) pat[rd] = c_pattern8.v[rd * 64 + lane];
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
@@ -1268,20 +1253,35 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         }
     }
     wave_lds_sync();
-    // horizontal 7-tap sums of the table's (row pair m, column quad q) items: rows 2m, 2m+1 (raw dwords q .. q+3
-    // of each; the pair m = 21 reads one row past the patch for its unused second row), columns 4q .. 4q+3
-    // (column c is level column cx - 18 + c, taps raw bytes po + c .. po + c + 6)
+    // horizontal 7-tap sums H(r, c) = sum_j g[j] raw[r][po + c + j] (column c = level column cx - 18 + c) on the
+    // matrix cores: per (row tile rt, column tile t) of 16 x 16 sums, the product of 16 raw rows' bytes 16t .. 16t + 31
+    // (A, as i8: x - 128) and the banded Toeplitz B[k][c'] = g[k - c' - po] (zero outside the 7 taps; the same for
+    // every tile, k <= 15 + 3 + 6 < 32), with the accumulator started at 128 * sum(g) = 128 * 256: integer, exact.
+    // v_mfma_i32_16x16x32_i8: lane l holds A[row l & 15][k = 8 (l >> 4) + j] and B[k = 8 (l >> 4) + j][col l & 15]
+    // (byte j of a 64-bit operand); D[i] = sum at (row 4 (l >> 4) + i, col l & 15).  Rows 43 .. 47 and columns 40 .. 47
+    // of the last tiles read bytes past the patch / multiply zeros and are not stored.
+    {
+        const int sB = 8 * (lane >> 4) - (lane & 15) - po;   // B byte j = g[j + sB]
+        constexpr uint64_t kG7 = 0x0012223038302212ull;     // g[0..6] = 18, 34, 48, 56, 48, 34, 18 (byte i = g[i])
+        const long Bop = (long)(sB >= 8 || sB <= -8 ? 0ull : sB >= 0 ? kG7 >> (8 * sB) : kG7 << (-8 * sB));
+        const uint8_t *rawb = reinterpret_cast<const uint8_t *>(raw);
+        const int m0 = 2 * (lane >> 4);   // this lane's first row pair inside a row tile
 #pragma unroll
-    for (int it = 0; it < kHItemIt; ++it) {
-        const uint32_t e = hit[it];
-        if (e == 0xffffffffu) continue;
-        const uint32_t *ra = raw + (e & 0xffff);
-        uint32_t *hp = H + (e >> 16);
-        uint32_t ha[4], hb[4];
-        hsum4(ra[0], ra[1], ra[2], ra[3], po, ha);
-        hsum4(ra[kRawDw], ra[kRawDw + 1], ra[kRawDw + 2], ra[kRawDw + 3], po, hb);
+        for (int rt = 0; rt < 3; ++rt) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) hp[k * kHStride] = ha[k] | (hb[k] << 16);
+            for (int t = 0; t < 3; ++t) {
+                const uint64_t av = *reinterpret_cast<const uint64_t *>(rawb + (16 * rt + (lane & 15)) * (4 * kRawDw) +
+                                                                        16 * t + 8 * (lane >> 4));
+                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(av ^ 0x8080808080808080ull), Bop,
+                                                                      i32x4{32768, 32768, 32768, 32768}, 0, 0, 0);
+                const int c = 16 * t + (lane & 15), m = 8 * rt + m0;
+                if (c < kHCols && m < 22) {   // rows <= 43 (pair 21), columns < 40
+                    uint32_t *hp = H + c * kHStride + m;
+                    hp[0] = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
+                    hp[1] = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
+                }
+            }
+        }
     }
     // intensity centroid: lane = (disc row vr = lane >> 1, half h = lane & 1) = bytes cx-15+16h .. +15 of row
     // cy-15+vr (raw row 6 + vr, raw byte po + 6 + 16h) as four dot4 items over five LDS dwords; lanes 62, 63 and
@@ -1419,7 +1419,7 @@ struct omv_orb {
     Cell *d_cells = nullptr;
     XTab *d_xt = nullptr, *d_yt = nullptr;
     XQuad *d_xq = nullptr;
-    uint32_t *d_disc = nullptr, *d_hitem = nullptr;   // K4's per-lane centroid masks and horizontal-sum items
+    uint32_t *d_disc = nullptr;   // K4's per-lane centroid masks
     float *harris = nullptr;   // optional Harris output of the next batches (omv_orb_set_harris)
     uint8_t *d_pyr = nullptr;
     int *d_cell_cnt = nullptr;
@@ -1642,12 +1642,9 @@ static omv_status build_geometry(omv_orb *o, std::vector<Cell> &cells, std::vect
     return OMV_OK;
 }
 
-// K4's per-lane constant tables.  disc[lane][2k], disc[lane][2k+1]: the row-sum and the weight (u + 15) byte masks of
+// K4's per-lane constant table.  disc[lane][2k], disc[lane][2k+1]: the row-sum and the weight (u + 15) byte masks of
 // the lane's centroid item k (disc row vr = min(lane >> 1, 30), bytes 16 (lane & 1) + 4k .. +3 of cx-15 ..; zero
-// outside the r = 15 disc, IC_Angle's umax rows, and for lanes 62, 63).  hitem: the (row pair, column quad) items of
-// the horizontal sums that any rotation of the pattern can sample: a steered point round(R(theta) p) lies in the
-// unit square around a point of the circle of radius |p|, so every integer (X, Y) whose square meets one of those
-// circles is kept, and with it rows Y + 18 .. Y + 24 of column X + 18.
+// outside the r = 15 disc, IC_Angle's umax rows, and for lanes 62, 63).
 static std::vector<uint32_t> disc_table(const int umax[16]) {
     std::vector<uint32_t> t(64 * 8, 0u);
     for (int lane = 0; lane < 62; ++lane) {
@@ -1662,27 +1659,6 @@ static std::vector<uint32_t> disc_table(const int umax[16]) {
         }
     }
     return t;
-}
-
-static bool hitem_table(std::vector<uint32_t> &t) {
-    std::vector<double> radii;
-    for (int i = 0; i < 512; ++i) radii.push_back(std::hypot((double)kPattern[2 * i], (double)kPattern[2 * i + 1]));
-    std::set<std::pair<int, int>> items;   // (row pair, column quad)
-    for (int X = -18; X <= 18; ++X)
-        for (int Y = -18; Y <= 18; ++Y) {
-            const double dmin = std::hypot(std::max(0.0, std::abs(X) - 0.5), std::max(0.0, std::abs(Y) - 0.5));
-            const double dmax = std::hypot(std::abs(X) + 0.5, std::abs(Y) + 0.5);
-            bool hit = false;
-            for (double r : radii) hit = hit || (dmin <= r && r <= dmax);
-            if (!hit) continue;
-            for (int R = Y + 18; R <= Y + 24; ++R) items.insert({R >> 1, (X + 18) >> 2});
-        }
-    if (items.size() > (size_t)kHItemIt * 64) return false;
-    t.assign((size_t)kHItemIt * 64, 0xffffffffu);
-    size_t i = 0;
-    for (const auto &mq : items)
-        t[i++] = (uint32_t)(2 * mq.first * kRawDw + mq.second) | ((uint32_t)(4 * mq.second * kHStride + mq.first) << 16);
-    return true;
 }
 
 extern "C" {
@@ -1798,15 +1774,8 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
     if (!xq.empty()) HIP_OK(hipMemcpy(o->d_xq, xq.data(), sizeof(XQuad) * xq.size(), hipMemcpyHostToDevice));
     {
         const std::vector<uint32_t> dt = disc_table(o->umax);
-        std::vector<uint32_t> ht;
-        if (!hitem_table(ht)) {
-            delete o;
-            return OMV_ERR_ARG;
-        }
         HIP_OK(hipMalloc(&o->d_disc, sizeof(uint32_t) * dt.size()));
         HIP_OK(hipMemcpy(o->d_disc, dt.data(), sizeof(uint32_t) * dt.size(), hipMemcpyHostToDevice));
-        HIP_OK(hipMalloc(&o->d_hitem, sizeof(uint32_t) * ht.size()));
-        HIP_OK(hipMemcpy(o->d_hitem, ht.data(), sizeof(uint32_t) * ht.size(), hipMemcpyHostToDevice));
     }
     HIP_OK(hipMalloc(&o->d_pyr, std::max<size_t>(256, (size_t)g.pyr_bytes * n)));
     HIP_OK(hipMalloc(&o->d_cell_cnt, sizeof(int) * g.n_cells * n));
@@ -1826,7 +1795,7 @@ omv_status omv_orb_create(const omv_orb_params *params, int width, int height, i
 omv_status omv_orb_destroy(omv_orb *o) {
     if (!o) return OMV_ERR_ARG;
     for (hipEvent_t e : o->ev) (void)hipEventDestroy(e);
-    void *ptrs[] = {o->d_bands, o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_disc, o->d_hitem, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
+    void *ptrs[] = {o->d_bands, o->d_cells, o->d_xt, o->d_yt, o->d_xq, o->d_disc, o->d_pyr, o->d_cell_cnt, o->d_cell_kp, o->d_cand, o->d_nid,
                     o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, o->d_lap, o->d_err, o->d_img1, o->d_kp1,
                     o->d_desc1, o->d_n1};
     for (void *p : ptrs)
@@ -1900,7 +1869,7 @@ omv_status omv_orb_extract_batch(omv_orb *o, int n, const uint8_t *images, size_
     mark(o, st);
     // K4: orientation + blur at the samples + descriptors, one wave per output slot
     DescArgs da{images, image_stride, pitch, o->d_pyr, o->d_lvl_out, o->d_lvl_cls, o->d_lvl_cnt, kps, desc, n_out, mono_index, n,
-                o->d_disc, o->d_hitem, o->harris};
+                o->d_disc, o->harris};
     const int waves = g.out_per_img * n;
     describe_kernel<<<omv::xcd_grid((waves + 3) / 4), 256, 0, st>>>(g, da, (waves + 3) / 4);
     mark(o, st);
