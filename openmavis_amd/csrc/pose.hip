@@ -747,6 +747,7 @@ constexpr size_t kLatFrameGran = 2 * kLatMaxParts * (kLatRow + 1);   // 8-byte w
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 #ifdef OMV_POSE_PROFILE   // phase times of the grouped kernel (wall_clock64 = 100 MHz), printed by part 0
 __device__ unsigned long long g_lat_pub[48][48];   // per part, per Gauss-Newton iteration: the hand-off's start
+__device__ unsigned long long g_lat_x[4];          // part 0's exchanges: publish -> flags seen -> payload in -> summed, count
 #define LAT_T(var) const unsigned long long var = wall_clock64()
 #define LAT_ACC(slot, a, b) prof[slot] += (b) - (a)
 #else
@@ -754,18 +755,25 @@ __device__ unsigned long long g_lat_pub[48][48];   // per part, per Gauss-Newton
 #define LAT_ACC(slot, a, b)
 #endif
 
-// Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q), in part order, into out[0..n)
-// (LDS), every part getting the identical sums.  MI355X_MICROARCH.md's R1 hand-off: the part's n values go out as
-// write-through (`sc1`) 8-byte stores to its payload row of slot (phase & 1), the wave drains them (vmcnt(0)), then
-// ONE lane stores the part's flag = salt | phase; the consumer polls the G flags with one load per spin (lane p: part
-// p's flag), then reads the G x n payload words with `sc1` loads (every load of them: no acquire needed) -- a poll of
-// G words instead of re-reading every part's payload each spin.  One wavefront; false on a bounded-spin timeout (a
-// missing sibling workgroup).  L: payload loads per lane (>= ceil(G n / 64)); loads past G n repeat the last word.
-template <int L>
-__device__ __attribute__((noinline)) bool lat_exchange_l(gu64 *fb, int phase, uint32_t salt, int g, int G, double v,
-                                                         int n, double *sc, double *out, int lane) {
+// Sum over the frame's G workgroups of n <= 32 doubles (lane q of wave 0 holds value q) into out[0..n) (LDS), every
+// part getting the identical sums.  MI355X_MICROARCH.md's R1 hand-off: the part's n values go out as write-through
+// (`sc1`) 8-byte stores to its payload row of slot (phase & 1), the wave drains them (vmcnt(0)), then ONE lane stores
+// the part's flag = salt | phase; the consumer polls the G flags with one load per spin (lane p: part p's flag), then
+// reads the payload with `sc1` loads (every load of them: no acquire needed).  The read is laid out for the sum:
+// lane (h, q) = (lane >> 5, lane & 31) loads word q of parts h * ceil(G / 2) .. (all in flight, in registers) and
+// adds them in part order; the two halves' sums meet by one shuffle (a + b == b + a exactly, so every part's lanes
+// get the identical total).  A sum read back from LDS one part at a time was a 47-long chain of LDS round trips
+// (~2 us per exchange).  One wavefront; false on a bounded-spin timeout (a missing sibling workgroup).
+// Out of line (five call sites; inlined they were a sixth of the kernel's code, whose per-iteration code must stay
+// within the CU's instruction cache).
+__device__ __attribute__((noinline)) bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
+                                                       double *out, int lane) {
+    constexpr int L = kLatMaxParts / 2;   // parts per half
     const uint32_t tag = salt | (uint32_t)phase;
     const int sl = phase & 1;
+#ifdef OMV_POSE_PROFILE
+    const unsigned long long tx0 = wall_clock64();
+#endif
     gu64 *pay = fb + (size_t)sl * kLatMaxParts * kLatRow;                                // [part][kLatRow]
     gu64 *flg = fb + (size_t)2 * kLatMaxParts * kLatRow + (size_t)sl * kLatMaxParts;     // [part]
     if (lane < n)
@@ -780,35 +788,31 @@ __device__ __attribute__((noinline)) bool lat_exchange_l(gu64 *fb, int phase, ui
         if (spins > (1u << 22)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
-    const int M = G * n;
+#ifdef OMV_POSE_PROFILE
+    const unsigned long long tx1 = wall_clock64();
+#endif
+    const int q = lane & 31, h = lane >> 5, Gh = (G + 1) >> 1, p0 = h * Gh;
+    const int np = q < n ? min(Gh, G - p0) : 0;   // parts this lane adds
     double val[L];
 #pragma unroll
-    for (int m = 0; m < L; ++m) {
-        const int i = min(lane + 64 * m, M - 1);
-        const int p = i / n, q = i - p * n;
-        val[m] = __builtin_bit_cast(double, __hip_atomic_load(pay + p * kLatRow + q, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-    }
+    for (int m = 0; m < L; ++m)
+        val[m] = m < np ? __builtin_bit_cast(double, __hip_atomic_load(pay + (p0 + m) * kLatRow + q, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT))
+                        : 0.0;
+    double s = 0;
 #pragma unroll
-    for (int m = 0; m < L; ++m) {
-        const int i = lane + 64 * m;
-        if (i < M) sc[i] = val[m];
-    }
+    for (int m = 0; m < L; ++m) s = m < np ? s + val[m] : s;
+    s += __shfl_xor(s, 32, 64);
+    if (h == 0 && q < n) out[q] = s;
     wave_lds_sync();
-    if (lane < n) {
-        double s = 0;
-        for (int p = 0; p < G; ++p) s += sc[p * n + lane];
-        out[lane] = s;
+#ifdef OMV_POSE_PROFILE
+    if (g == 0 && lane == 0) {
+        const unsigned long long tx2 = wall_clock64();
+        atomicAdd(&g_lat_x[0], tx1 - tx0), atomicAdd(&g_lat_x[1], tx2 - tx1);
+        atomicAdd(&g_lat_x[3], 1ull);
     }
-    wave_lds_sync();
+#endif
     return true;
-}
-// Out-of-line sweeps (three call sites; inlined they were a sixth of the kernel's code, whose per-iteration code must
-// stay within the CU's instruction cache), sized to the payload.
-__device__ __forceinline__ bool lat_exchange(gu64 *fb, int phase, uint32_t salt, int g, int G, double v, int n,
-                                             double *sc, double *out, int lane) {
-    if (G * n <= 8 * 64) return lat_exchange_l<8>(fb, phase, salt, g, G, v, n, sc, out, lane);
-    return lat_exchange_l<(kLatMaxParts * kLatRow) / 64>(fb, phase, salt, g, G, v, n, sc, out, lane);
 }
 
 // Eigen::LDLT<MatrixXd> (ldlt_inplace::unblocked's pivot order, isPositive(), _solve_impl's D pseudo-inverse below
@@ -1390,7 +1394,6 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         bP[kLF ? 15 : 1];
     __shared__ double Am[NP], Vm[NP], ecs[16];
     __shared__ int epq[16];
-    __shared__ double xsc[kLatMaxParts * kLatRow];
     __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N], s_lohi[2];
     __shared__ int k1s, k2s;
     __shared__ double s_cnt[2];
@@ -1449,7 +1452,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     int phase = 1;
     // setup exchange: every part learns whether some part overflowed its LDS edge capacity
     if (wave == 0) {
-        if (!lat_exchange(fb, phase, salt, g, G, fit ? 0.0 : 1.0, 1, xsc, s_cnt, lane)) s_abort = 1;
+        if (!lat_exchange(fb, phase, salt, g, G, fit ? 0.0 : 1.0, 1, s_cnt, lane)) s_abort = 1;
         else if (lane == 0 && s_cnt[0] != 0.0) s_abort = 2;
     } else if (wave == kIW) {
         // the edges' information matrices (pose_info_kernel's work, here beside the setup exchange: no extra launch)
@@ -1589,6 +1592,10 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         const float chi2Mono[4] = {kLF ? 5.991f : 12.f, kLF ? 5.991f : 7.5f, 5.991f, 5.991f};   // :5992 / :5432
         const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
         double nBad = 0, nIn = 0;
+#ifdef OMV_POSE_PROFILE
+        unsigned long long t_cls = 0;   // classification passes + their exchanges
+        LAT_T(t_loop0);
+#endif
         for (int it = 0; it < 4; ++it) {
             const bool robust = it < 3;   // setRobustKernel(0) after the third classification
             for (int gi = 0; gi < 10; ++gi) {
@@ -1643,7 +1650,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
 #endif
                 if (wave == 0) {
                     const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
-                    if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
+                    if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, nrm, lane) && lane == 0) s_abort = 1;
                 }
                 __syncthreads();
                 LAT_T(t2);
@@ -1750,6 +1757,9 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 if (!s_ok) break;   // optimize() stops after a failed iteration
             }
             // classification (:5436-5490): the mono pass, then the stereo pass; counts summed over the parts
+#ifdef OMV_POSE_PROFILE
+            LAT_T(t_c0);
+#endif
             double bad = 0, in = 0;
             const float chi2close = 1.5f * chi2Mono[it];
             for (int pass = 0; pass < 2; ++pass) {
@@ -1787,14 +1797,23 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 ++phase;
                 if (wave == 0) {
                     const double v = lane < 2 ? wave_parts_sum(red, lane, kEW) : 0.0;
-                    if (!lat_exchange(fb, phase, salt, g, G, v, 2, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
+                    if (!lat_exchange(fb, phase, salt, g, G, v, 2, s_cnt, lane) && lane == 0) s_abort = 1;
                 }
                 __syncthreads();
                 if (s_abort) goto fail;
                 nBad = s_cnt[0], nIn = s_cnt[1];
             }
+#ifdef OMV_POSE_PROFILE
+            {
+                LAT_T(t_c1);
+                t_cls += t_c1 - t_c0;
+            }
+#endif
             if (ne + (kLF ? 4 : 3) < 10) break;   // optimizer.edges().size() < 10
         }
+#ifdef OMV_POSE_PROFILE
+        LAT_T(t_loop1);
+#endif
         if (nIn < 30 && !A.rec_init) {   // recover not too bad points (:5503-5526)
             double bad = 0;
             if (wave < kEW)
@@ -1813,12 +1832,15 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             ++phase;
             if (wave == 0) {
                 const double v = lane < 1 ? wave_parts_sum(red, 0, kEW) : 0.0;
-                if (!lat_exchange(fb, phase, salt, g, G, v, 1, xsc, s_cnt, lane) && lane == 0) s_abort = 1;
+                if (!lat_exchange(fb, phase, salt, g, G, v, 1, s_cnt, lane) && lane == 0) s_abort = 1;
             }
             __syncthreads();
             if (s_abort) goto fail;
             nBad = s_cnt[0];
         }
+#ifdef OMV_POSE_PROFILE
+        LAT_T(t_rec);
+#endif
         // mvbOutlier of this part's keypoints
         if (wave < kEW)
             for (int q = tid; q < nloc; q += kET) A.kp_out[(size_t)f * A.kp_cap + E.kp[q]] = E.kpo[E.kp[q]];
@@ -1849,7 +1871,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             ++phase;
             if (wave == 0) {
                 const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
-                if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, xsc, nrm, lane) && lane == 0) s_abort = 1;
+                if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, nrm, lane) && lane == 0) s_abort = 1;
             }
             __syncthreads();
             if (s_abort) goto fail;
@@ -1935,6 +1957,11 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         }
         if (g == 0 && tid == 0) {
             LAT_T(t_end);
+            printf("pose_lat<%d> exchanges %llu: publish->flags %.2f flags->summed %.2f us each\n", (int)kLF, g_lat_x[3],
+                   g_lat_x[0] / 100.0 / g_lat_x[3], g_lat_x[1] / 100.0 / g_lat_x[3]);
+            printf("pose_lat<%d> setup %.1f loop %.1f (classification %.1f) recover %.1f hessian+rest %.1f us\n", (int)kLF,
+                   (t_loop0 - t_start) / 100.0, (t_loop1 - t_loop0) / 100.0, t_cls / 100.0, (t_rec - t_loop1) / 100.0,
+                   (t_end - t_rec) / 100.0);
             printf("pose_lat<%d> G %d edges(w0) %.1f reduce %.1f edges+inertial(barrier) %.1f exchange %.1f build %.1f "
                    "ldlt %.1f ldlt+update %.1f inertial(w4) %.1f total %.1f us\n", (int)kLF, G, prof[0] / 100.0,
                    prof[1] / 100.0, prof[2] / 100.0, prof[3] / 100.0, prof[4] / 100.0, prof[5] / 100.0, prof[6] / 100.0,
