@@ -45,19 +45,18 @@ constexpr int kMinB = kEdge - 3;
 constexpr int kPattern[256 * 4] = {
 #include "orb_pattern_31.inc"
 };
-// the 256 point pairs (ax, ay, bx, by), |coordinate| <= 15, packed as signed bytes: one dword per pair,
-// loaded by each lane once per keypoint before the patch staging
-struct PackedPattern {
-    uint32_t v[256];
+// the 256 point pairs (ax, ay, bx, by) as floats (the reference's int x float products convert the pattern
+// coordinate first): one 16-byte entry per pair, loaded by each lane once per keypoint before the patch staging
+struct FloatPattern {
+    float v[256][4];
 };
-constexpr PackedPattern pack_pattern() {
-    PackedPattern p{};
+constexpr FloatPattern float_pattern() {
+    FloatPattern p{};
     for (int i = 0; i < 256; ++i)
-        p.v[i] = (uint32_t)(kPattern[4 * i] & 0xff) | ((uint32_t)(kPattern[4 * i + 1] & 0xff) << 8) |
-                 ((uint32_t)(kPattern[4 * i + 2] & 0xff) << 16) | ((uint32_t)(kPattern[4 * i + 3] & 0xff) << 24);
+        for (int q = 0; q < 4; ++q) p.v[i][q] = (float)kPattern[4 * i + q];
     return p;
 }
-__constant__ PackedPattern c_pattern8 = pack_pattern();
+__constant__ FloatPattern c_patternf = float_pattern();
 __constant__ int c_gauss7[7] = {18, 34, 48, 56, 48, 34, 18};
 
 struct LevelGeom {
@@ -1211,9 +1210,9 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     if (j >= cnts[3 * l]) return;
     // the lane's constant tables (independent of the record: in flight together)
     const uint4 dm0 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane], dm1 = reinterpret_cast<const uint4 *>(a.disc)[2 * lane + 1];
-    uint32_t pat[4];
+    float4 pat[4];
 #pragma unroll
-    for (int rd = 0; rd < 4; ++rd) pat[rd] = c_pattern8.v[rd * 64 + lane];
+    for (int rd = 0; rd < 4; ++rd) pat[rd] = *reinterpret_cast<const float4 *>(c_patternf.v[rd * 64 + lane]);
     const int cx = (int)(p & 0xfff) + kMinB, cy = (int)((p >> 12) & 0xfff) + kMinB;
     const int score = (int)(p >> 24);
     int sp;
@@ -1352,13 +1351,11 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     uint64_t words[4];
 #pragma unroll
     for (int rd = 0; rd < 4; ++rd) {
-        const uint32_t pt = pat[rd];
-        const int ax = (int)(int8_t)(pt & 0xff), ay = (int)(int8_t)((pt >> 8) & 0xff);
-        const int bx = (int)(int8_t)((pt >> 16) & 0xff), by = (int)(int8_t)(pt >> 24);
-        const int ady = omv::round_even((float)ax * fb + (float)ay * fa);
-        const int adx = omv::round_even((float)ax * fa - (float)ay * fb);
-        const int bdy = omv::round_even((float)bx * fb + (float)by * fa);
-        const int bdx = omv::round_even((float)bx * fa - (float)by * fb);
+        const float ax = pat[rd].x, ay = pat[rd].y, bx = pat[rd].z, by = pat[rd].w;
+        const int ady = omv::round_even(ax * fb + ay * fa);
+        const int adx = omv::round_even(ax * fa - ay * fb);
+        const int bdy = omv::round_even(bx * fb + by * fa);
+        const int bdx = omv::round_even(bx * fa - by * fb);
         words[rd] = __ballot(blurred(adx, ady) < blurred(bdx, bdy));
     }
     // final row: monoIndex order (front) or lapping order (back, reversed)
