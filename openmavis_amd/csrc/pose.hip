@@ -1292,48 +1292,79 @@ __device__ __forceinline__ VEdge lat_edge(const LatEdges &E, int q) {
     return v;
 }
 
-// Workgroup-ordered compaction of this part's edges of one list (mono or stereo): edges whose keypoint lies in
-// [lo, hi), in list order, appended at *count.  Returns false (uniformly) past kLatCap.
-__device__ bool lat_select(const PoseArgs &A, bool stereo, int e0, int n, int lo, int hi, const LatEdges &E, int *count,
-                           int *wcnt) {
+// Workgroup-ordered compaction of this part's edges (keypoint in [lo, hi)): the mono list's, then the stereo list's,
+// each in list order, into the LDS edge arrays; *nm_loc / *n_loc = mono / all edges taken.  Two phases: every thread
+// takes kSel consecutive keypoint indices per chunk (all loads in flight), a workgroup prefix sum of the taken counts
+// places them, and the taken edges' source indices are staged in LDS (the chi2 array, unused until the iterations);
+// then one thread per taken edge loads its record.  (A chunk of kLatThreads edges per workgroup step was ~19 dependent
+// global round trips per frame of ~5,800 edges: most of the call's setup.)  False (uniformly) past kLatCap.
+constexpr int kSel = 16;
+__device__ bool lat_select(const PoseArgs &A, int m0, int nm, int s0, int ns, int lo, int hi, const LatEdges &E,
+                           int *wcnt, int *nm_loc, int *n_loc) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kLatThreads / 64;
-    for (int base = 0; base < n; base += kLatThreads) {
-        const int q = base + tid;
-        int kp = -1;
-        if (q < n) kp = stereo ? A.s_kp[e0 + q] : A.m_kp[e0 + q];
-        const bool take = q < n && kp >= lo && kp < hi;
-        const uint64_t bal = __ballot(take);
-        if (lane == 0) wcnt[wave] = __builtin_popcountll(bal);
-        __syncthreads();
-        int off = *count;
-        for (int w2 = 0; w2 < wave; ++w2) off += wcnt[w2];
-        int tot = *count;
-        for (int w2 = 0; w2 < kW; ++w2) tot += wcnt[w2];
-        if (tot > kLatCap) return false;
-        if (take) {
-            const int d = off + __builtin_popcountll(bal & ((1ull << lane) - 1));
-            const int e = e0 + q;
-            E.kp[d] = kp;
-            if (!stereo) {
-                E.cam[d] = (uint8_t)A.m_cam[e];
-                E.ob0[d] = A.m_obs[2 * e], E.ob1[d] = A.m_obs[2 * e + 1], E.ob2[d] = 0.0;
-                E.w[d] = A.m_w[e];
-                E.x0[d] = A.m_xw[3 * e], E.x1[d] = A.m_xw[3 * e + 1], E.x2[d] = A.m_xw[3 * e + 2];
-                E.fl[d] = (uint8_t)(4 | (A.m_close[e] ? 2 : 0));
-            } else {
-                E.cam[d] = (uint8_t)A.s_cam[e];
-                E.ob0[d] = A.s_obs[3 * e], E.ob1[d] = A.s_obs[3 * e + 1], E.ob2[d] = A.s_obs[3 * e + 2];
-                E.w[d] = A.s_w[e];
-                E.x0[d] = A.s_xw[3 * e], E.x1[d] = A.s_xw[3 * e + 1], E.x2[d] = A.s_xw[3 * e + 2];
-                E.fl[d] = 4 | 1;
+    int *src = reinterpret_cast<int *>(E.c2);   // [kLatCap] (list << 31) | edge
+    int total = 0;
+    for (int list = 0; list < 2; ++list) {
+        const bool stereo = list == 1;
+        const int e0 = stereo ? s0 : m0, n = stereo ? ns : nm;
+        const int32_t *K = (stereo ? A.s_kp : A.m_kp) + e0;
+        for (int base = 0; base < n; base += kLatThreads * kSel) {
+            const int q0 = base + tid * kSel;
+            int kv[kSel];
+#pragma unroll
+            for (int u = 0; u < kSel; ++u) kv[u] = q0 + u < n ? K[q0 + u] : 0;
+            uint32_t take = 0;   // (part 0's lo is INT_MIN: the bound alone does not exclude the padding)
+#pragma unroll
+            for (int u = 0; u < kSel; ++u) take |= (q0 + u < n && kv[u] >= lo && kv[u] < hi ? 1u : 0u) << u;
+            const int cnt = __builtin_popcount(take);
+            int incl = cnt;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += t;
             }
-            E.kpo[kp] = 0;
+            if (lane == 63) wcnt[wave] = incl;
+            __syncthreads();
+            int off = total + incl - cnt, tot = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kW; ++w2) {
+                off += w2 < wave ? wcnt[w2] : 0;
+                tot += wcnt[w2];
+            }
+            if (total + tot > kLatCap) return false;
+            for (uint32_t b = take; b; b &= b - 1) {
+                const int u = __builtin_ctz(b);
+                src[off++] = (stereo ? (int)0x80000000 : 0) | (e0 + q0 + u);
+            }
+            total += tot;
+            __syncthreads();   // wcnt is reused
         }
-        __syncthreads();
-        if (tid == 0) *count = tot;
-        __syncthreads();
+        if (!stereo) *nm_loc = total;
     }
+    *n_loc = total;
+    for (int d = tid; d < total; d += kLatThreads) {
+        const int sv = src[d];
+        const bool stereo = sv < 0;
+        const int e = sv & 0x7fffffff;
+        const int kp = stereo ? A.s_kp[e] : A.m_kp[e];
+        E.kp[d] = kp;
+        if (!stereo) {
+            E.cam[d] = (uint8_t)A.m_cam[e];
+            E.ob0[d] = A.m_obs[2 * e], E.ob1[d] = A.m_obs[2 * e + 1], E.ob2[d] = 0.0;
+            E.w[d] = A.m_w[e];
+            E.x0[d] = A.m_xw[3 * e], E.x1[d] = A.m_xw[3 * e + 1], E.x2[d] = A.m_xw[3 * e + 2];
+            E.fl[d] = (uint8_t)(4 | (A.m_close[e] ? 2 : 0));
+        } else {
+            E.cam[d] = (uint8_t)A.s_cam[e];
+            E.ob0[d] = A.s_obs[3 * e], E.ob1[d] = A.s_obs[3 * e + 1], E.ob2[d] = A.s_obs[3 * e + 2];
+            E.w[d] = A.s_w[e];
+            E.x0[d] = A.s_xw[3 * e], E.x1[d] = A.s_xw[3 * e + 1], E.x2[d] = A.s_xw[3 * e + 2];
+            E.fl[d] = 4 | 1;
+        }
+        E.kpo[kp] = 0;
+    }
+    __syncthreads();
     return true;
 }
 
@@ -1394,7 +1425,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         bP[kLF ? 15 : 1];
     __shared__ double Am[NP], Vm[NP], ecs[16];
     __shared__ int epq[16];
-    __shared__ int s_ok, s_abort, s_count, wcnt[kLatThreads / 64], pick[N], s_lohi[2];
+    __shared__ int s_ok, s_abort, wcnt[kLatThreads / 64], pick[N], s_lohi[2];
     __shared__ int k1s, k2s;
     __shared__ double s_cnt[2];
     __shared__ float spre[kPF];   // the frame's IMU::Preintegrated record (read every iteration: kept out of HBM)
@@ -1417,7 +1448,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             sba[q] = A.kba[3 * f + q], sba[3 + q] = A.ba[3 * f + q];
         }
         k1s = 0, k2s = 1;
-        s_count = 0, s_abort = 0;
+        s_abort = 0;
     }
     if constexpr (kLF) {
         for (int q = tid; q < 225; q += kLatThreads) pH[q] = A.pH[(size_t)f * 225 + q];
@@ -1445,10 +1476,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     }
     __syncthreads();
     const int lo = s_lohi[0], hi = s_lohi[1];
-    bool fit = lat_select(A, false, m0, nm, lo, hi, E, &s_count, wcnt);
-    const int nm_loc = s_count;
-    if (fit) fit = lat_select(A, true, s0, ns, lo, hi, E, &s_count, wcnt);
-    const int nloc = s_count;
+    int nm_loc = 0, nloc = 0;
+    const bool fit = lat_select(A, m0, nm, s0, ns, lo, hi, E, wcnt, &nm_loc, &nloc);
     int phase = 1;
     // setup exchange: every part learns whether some part overflowed its LDS edge capacity
     if (wave == 0) {
@@ -1667,9 +1696,11 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 // reduced system (LastKeyFrame: pose + velocity, 9; LastFrame: the frame's pose + velocity and all 15 of the
                 // previous frame's, 24) is positive (semi)definite iff the full one is (InfoG / InfoA are positive
                 // definite), so isPositive() and the update agree with the full solve up to rounding.
-                for (int q = tid; q < NR * NR; q += kLatThreads) {
-                    const int i = q / NR, j = q - (q / NR) * NR;
-                    if (j > i) continue;
+                for (int q = tid; q < NR * (NR + 1) / 2; q += kLatThreads) {   // the lower triangle, q = i (i + 1) / 2 + j
+                    int i = (int)((sqrtf(8.f * (float)q + 1.f) - 1.f) * 0.5f);
+                    i += (i + 1) * (i + 2) / 2 <= q ? 1 : 0;
+                    i -= i * (i + 1) / 2 > q ? 1 : 0;
+                    const int j = q - i * (i + 1) / 2;
                     const int fi = red_full(i), fj = red_full(j);
                     double h = 0;
                     if (fi < 6) h = nrm[fj * 6 - fj * (fj - 1) / 2 + (fi - fj)];

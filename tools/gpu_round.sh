@@ -14,3 +14,4 @@ fi
 timeout -k 10 500 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 tail -c 600 gpurun_out/bench_$TAG.json
 bash tools/profile_gpu.sh $TAG
+bash tools/pmc_orb_bound.sh bound_$TAG
