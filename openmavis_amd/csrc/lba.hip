@@ -1809,6 +1809,11 @@ struct omv_lba {
     hipGraphExec_t step_exec = nullptr;   // one LM step (trial, and buildSystem when an iteration starts)
     hipGraph_t step4_graph = nullptr;
     hipGraphExec_t step4_exec = nullptr;  // four LM steps in one launch (no launch gap between them)
+    // four LM steps + the speculative epilogue + the staging and control read-backs (index: chi2 read-back or not):
+    // the batch that usually ends the optimize() in one launch (a graph -> kernel -> copy transition on the stream
+    // costs ~10 us each)
+    hipGraph_t step4e_graph[2] = {nullptr, nullptr};
+    hipGraphExec_t step4e_exec[2] = {nullptr, nullptr};
     bool timing = false;       // direct launches with per-stage events instead of the captured step
     bool host_lm = false;      // force the host-driven LM loop (parity checks of the device control)
     double *d_S = nullptr, *d_coef = nullptr, *d_x = nullptr, *d_scratch = nullptr;
@@ -1846,6 +1851,11 @@ static void free_problem(omv_lba *h) {
     if (h->step4_graph) (void)hipGraphDestroy(h->step4_graph);
     h->step_exec = nullptr, h->step_graph = nullptr;   // the captured step holds the old problem's pointers
     h->step4_exec = nullptr, h->step4_graph = nullptr;
+    for (int q = 0; q < 2; ++q) {
+        if (h->step4e_exec[q]) (void)hipGraphExecDestroy(h->step4e_exec[q]);
+        if (h->step4e_graph[q]) (void)hipGraphDestroy(h->step4e_graph[q]);
+        h->step4e_exec[q] = nullptr, h->step4e_graph[q] = nullptr;
+    }
 }
 
 extern "C" {
@@ -1890,6 +1900,10 @@ omv_status omv_lba_destroy(omv_lba *h) {
     if (h->step_graph) (void)hipGraphDestroy(h->step_graph);
     if (h->step4_exec) (void)hipGraphExecDestroy(h->step4_exec);
     if (h->step4_graph) (void)hipGraphDestroy(h->step4_graph);
+    for (int q = 0; q < 2; ++q) {
+        if (h->step4e_exec[q]) (void)hipGraphExecDestroy(h->step4e_exec[q]);
+        if (h->step4e_graph[q]) (void)hipGraphDestroy(h->step4e_graph[q]);
+    }
     delete h;
     return OMV_OK;
 }
@@ -2687,10 +2701,31 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
             HIP_OK(hipGraphInstantiate(n == 1 ? &h->step_exec : &h->step4_exec, g, nullptr, nullptr, 0));
         }
     }
+    // the fused batch: four steps, the epilogue and the read-backs captured together (once per problem and chi2 mode)
+    const bool fuse_epi = !direct && lba_epilogue_ok(h);
+    const int wc = want_chi2 ? 1 : 0;
+    if (fuse_epi && !h->step4e_exec[wc]) {
+        HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        rs = OMV_OK;
+        for (int q = 0; q < 4 && rs == OMV_OK; ++q) rs = lba_step(h, nullptr);
+        if (rs == OMV_OK) rs = lba_enqueue_epilogue(h, want_chi2);
+        const hipError_t me = hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st);
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(st, &g);
+        if (rs != OMV_OK) return rs;
+        if (ce != hipSuccess || me != hipSuccess) {
+            fprintf(stderr, "omv: LM batch capture failed: %s\n", hipGetErrorString(ce != hipSuccess ? ce : me));
+            return OMV_ERR_HIP;
+        }
+        h->step4e_graph[wc] = g;
+        HIP_OK(hipGraphInstantiate(&h->step4e_exec[wc], g, nullptr, nullptr, 0));
+        h->epi_ready = false;
+    }
     const int max_steps = std::max(0, o->opt_it) * std::max(1, o->max_trials);
     std::vector<std::array<hipEvent_t, 5>> evs;
     int launched = 0, batch = std::min(std::max(0, o->opt_it), max_steps);
     while (true) {
+        bool fused = false;   // this batch's last launch carried the epilogue and the control read-back
         for (int i = 0; i < batch;) {
             if (h->timing) {
                 std::array<hipEvent_t, 5> e{};
@@ -2702,7 +2737,8 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
                 if ((rs = lba_step(h, nullptr)) != OMV_OK) return rs;
                 ++i;
             } else if (i + 4 <= batch) {
-                HIP_OK(hipGraphLaunch(h->step4_exec, st));
+                fused = fuse_epi && i + 4 == batch;
+                HIP_OK(hipGraphLaunch(fused ? h->step4e_exec[wc] : h->step4_exec, st));
                 i += 4;
             } else {
                 HIP_OK(hipGraphLaunch(h->step_exec, st));
@@ -2711,9 +2747,13 @@ static omv_status lba_optimize_device(omv_lba *h, const omv_lba_opts *o, omv_lba
         }
         launched += batch;
         // the epilogue rides along with the control read-back (kept when the device reports the end)
-        const bool spec = lba_epilogue_ok(h);
-        if (spec && (rs = lba_enqueue_epilogue(h, want_chi2)) != OMV_OK) return rs;
-        HIP_OK(hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
+        if (fused) {
+            h->epi_ready = true, h->epi_chi2 = want_chi2;
+        } else {
+            const bool spec = lba_epilogue_ok(h);
+            if (spec && (rs = lba_enqueue_epilogue(h, want_chi2)) != OMV_OK) return rs;
+            HIP_OK(hipMemcpyAsync(h->h_ctl, h->d_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
+        }
         HIP_OK(hipStreamSynchronize(st));
         ++h->host_syncs;
         if (h->h_ctl->done || launched >= max_steps) break;
