@@ -39,7 +39,7 @@ __device__ __forceinline__ bool ldlt_v2(const double *H, const double *b, double
 #pragma unroll
         for (int j = k + 1; j < N; ++j) r[j] = __builtin_fma(-l, lane_f64(r[j], k), r[j]);
         r[k] = (below && nz) ? l : r[k];
-        if (below) Lt[k * S + lane] = r[k];
+        if (below && in) Lt[k * S + lane] = r[k];
         sign |= (d > 0 ? 1 : 0) | (d < 0 ? 2 : 0);
     }
     if (sign & 2) return false;
