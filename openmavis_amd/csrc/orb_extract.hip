@@ -1170,7 +1170,9 @@ struct DescArgs {
 
 constexpr int kRawRows = 43, kRawDw = 12;   // raw patch: rows cy-21 .. cy+21, 48 bytes each (43 used + alignment)
 constexpr int kHCols = 40, kHStride = 23;   // horizontal sums: 40 columns x 22 row pairs (stride 23 dwords)
-constexpr int kDescDw = kRawRows * kRawDw + kHCols * kHStride;   // LDS dwords per wave (5,744 B)
+// LDS dwords per wave (3,680 B): the horizontal sums overwrite the raw patch once its centroid is summed and its MFMA
+// operands are in registers (a separate table was 5,744 B per wave: 24 instead of 36 waves per CU)
+constexpr int kDescDw = kHCols * kHStride > kRawRows * kRawDw ? kHCols * kHStride : kRawRows * kRawDw;
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, dword-aligned
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -1219,7 +1221,7 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
     const uint8_t *src = level_base(g, a.images, a.img_stride, a.pitch0, a.pyr, img, l, &sp);
     __shared__ __attribute__((aligned(16))) uint32_t lds[4][kDescDw];
     uint32_t *raw = lds[wave];
-    uint32_t *H = raw + kRawRows * kRawDw;   // H[c * kHStride + m] = h[2m][c] | h[2m+1][c] << 16
+    uint32_t *H = lds[wave];   // after the raw patch: H[c * kHStride + m] = h[2m][c] | h[2m+1][c] << 16
     // Keypoints lie in [19, w-20] x [19, h-20] of their level, so the patch reaches at most 2 pixels past an
     // edge (reflected).  Fast path: the level's rows are dword aligned and the 48 bytes from the aligned start
     // stay inside [0, w): three 16-byte loads per lane; raw byte po + c is column cx - 21 + c.
@@ -1252,36 +1254,6 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         }
     }
     wave_lds_sync();
-    // horizontal 7-tap sums H(r, c) = sum_j g[j] raw[r][po + c + j] (column c = level column cx - 18 + c) on the
-    // matrix cores: per (row tile rt, column tile t) of 16 x 16 sums, the product of 16 raw rows' bytes 16t .. 16t + 31
-    // (A, as i8: x - 128) and the banded Toeplitz B[k][c'] = g[k - c' - po] (zero outside the 7 taps; the same for
-    // every tile, k <= 15 + 3 + 6 < 32), with the accumulator started at 128 * sum(g) = 128 * 256: integer, exact.
-    // v_mfma_i32_16x16x32_i8: lane l holds A[row l & 15][k = 8 (l >> 4) + j] and B[k = 8 (l >> 4) + j][col l & 15]
-    // (byte j of a 64-bit operand); D[i] = sum at (row 4 (l >> 4) + i, col l & 15).  Rows 43 .. 47 and columns 40 .. 47
-    // of the last tiles read bytes past the patch / multiply zeros and are not stored.
-    {
-        const int sB = 8 * (lane >> 4) - (lane & 15) - po;   // B byte j = g[j + sB]
-        constexpr uint64_t kG7 = 0x0012223038302212ull;     // g[0..6] = 18, 34, 48, 56, 48, 34, 18 (byte i = g[i])
-        const long Bop = (long)(sB >= 8 || sB <= -8 ? 0ull : sB >= 0 ? kG7 >> (8 * sB) : kG7 << (-8 * sB));
-        const uint8_t *rawb = reinterpret_cast<const uint8_t *>(raw);
-        const int m0 = 2 * (lane >> 4);   // this lane's first row pair inside a row tile
-#pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const uint64_t av = *reinterpret_cast<const uint64_t *>(rawb + (16 * rt + (lane & 15)) * (4 * kRawDw) +
-                                                                        16 * t + 8 * (lane >> 4));
-                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(av ^ 0x8080808080808080ull), Bop,
-                                                                      i32x4{32768, 32768, 32768, 32768}, 0, 0, 0);
-                const int c = 16 * t + (lane & 15), m = 8 * rt + m0;
-                if (c < kHCols && m < 22) {   // rows <= 43 (pair 21), columns < 40
-                    uint32_t *hp = H + c * kHStride + m;
-                    hp[0] = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
-                    hp[1] = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
-                }
-            }
-        }
-    }
     // intensity centroid: lane = (disc row vr = lane >> 1, half h = lane & 1) = bytes cx-15+16h .. +15 of row
     // cy-15+vr (raw row 6 + vr, raw byte po + 6 + 16h) as four dot4 items over five LDS dwords; lanes 62, 63 and
     // the bytes outside the disc have zero masks
@@ -1328,6 +1300,43 @@ __global__ void __launch_bounds__(256) describe_kernel(Geom g, DescArgs a, int n
         const float scale = 1.f / ((1 << 2) * 7 * 255.f);
         const float scale_sq_sq = scale * scale * scale * scale;
         harris = ((float)ha * hb - (float)hc * hc - 0.04f * ((float)ha + hb) * ((float)ha + hb)) * scale_sq_sq;
+    }
+    // horizontal 7-tap sums H(r, c) = sum_j g[j] raw[r][po + c + j] (column c = level column cx - 18 + c) on the
+    // matrix cores: per (row tile rt, column tile t) of 16 x 16 sums, the product of 16 raw rows' bytes 16t .. 16t + 31
+    // (A, as i8: x - 128) and the banded Toeplitz B[k][c'] = g[k - c' - po] (zero outside the 7 taps; the same for
+    // every tile, k <= 15 + 3 + 6 < 32), with the accumulator started at 128 * sum(g) = 128 * 256: integer, exact.
+    // v_mfma_i32_16x16x32_i8: lane l holds A[row l & 15][k = 8 (l >> 4) + j] and B[k = 8 (l >> 4) + j][col l & 15]
+    // (byte j of a 64-bit operand); D[i] = sum at (row 4 (l >> 4) + i, col l & 15).  Rows 43 .. 47 and columns 40 .. 47
+    // of the last tiles read bytes past the patch / multiply zeros and are not stored.  Every operand is read before
+    // the first sum is stored: the sums take the patch's place.
+    {
+        const int sB = 8 * (lane >> 4) - (lane & 15) - po;   // B byte j = g[j + sB]
+        constexpr uint64_t kG7 = 0x0012223038302212ull;     // g[0..6] = 18, 34, 48, 56, 48, 34, 18 (byte i = g[i])
+        const long Bop = (long)(sB >= 8 || sB <= -8 ? 0ull : sB >= 0 ? kG7 >> (8 * sB) : kG7 << (-8 * sB));
+        const uint8_t *rawb = reinterpret_cast<const uint8_t *>(raw);
+        const int m0 = 2 * (lane >> 4);   // this lane's first row pair inside a row tile
+        uint64_t av[3][3];
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                av[rt][t] = *reinterpret_cast<const uint64_t *>(rawb + (16 * rt + (lane & 15)) * (4 * kRawDw) + 16 * t +
+                                                                8 * (lane >> 4));
+        wave_lds_sync();   // every lane's patch reads before any sum overwrites the patch
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const i32x4 d = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)(av[rt][t] ^ 0x8080808080808080ull), Bop,
+                                                                      i32x4{32768, 32768, 32768, 32768}, 0, 0, 0);
+                const int c = 16 * t + (lane & 15), m = 8 * rt + m0;
+                if (c < kHCols && m < 22) {   // rows <= 43 (pair 21), columns < 40
+                    uint32_t *hp = H + c * kHStride + m;
+                    hp[0] = (uint32_t)d[0] | ((uint32_t)d[1] << 16);
+                    hp[1] = (uint32_t)d[2] | ((uint32_t)d[3] << 16);
+                }
+            }
+        }
     }
     const float angle = omv::fast_atan2_deg((float)m01, (float)m10);
     float sn, cs;
