@@ -1875,6 +1875,9 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         // mvbOutlier of this part's keypoints
         if (wave < kEW)
             for (int q = tid; q < nloc; q += kET) A.kp_out[(size_t)f * A.kp_cap + E.kp[q]] = E.kpo[E.kp[q]];
+#ifdef OMV_POSE_PROFILE
+        LAT_T(t_h0);
+#endif
         if (A.H) {
             // the Hessian without robust weights at the final state (inlier visual edges): visual sums exchanged,
             // EdgeInertial / EdgePriorPoseImu linearised by waves 4 / 5, the matrix formed by part 0
@@ -1970,6 +1973,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             }
         }
 #ifdef OMV_POSE_PROFILE
+        LAT_T(t_h1);
+        if (g == 0 && tid == 0) printf("pose_lat<%d> outlier write + hessian/marginalize %.1f us\n", (int)kLF, (t_h1 - t_h0) / 100.0);
         if (g == 0 && tid == 0 && f == 0) {   // hand-off skew: over the iterations, max - min publish time over the parts,
                                               // and part 0's completion after the last publish
             double skew = 0, post = 0;
