@@ -73,6 +73,9 @@ struct LmCtl {
     int errors_of_current;   // the last computed errors belong to the current state (A)
     int need_build;          // the next step starts a new iteration (buildSystem)
     int accepted;            // the last trial was accepted: the trial state becomes current
+    int n_acc;               // accepted updates since optimize()'s start: ImuCamPose::its of every optimisable
+                             // keyframe (created with its 0, popped with a rejected trial), Rwb normalised after every
+                             // third Update (G2oTypes.cc:220-225) -- a trial normalises iff n_acc % 3 == 2
     // double-buffered state and errors (device driver): buffer `cur` holds the current state and its errors, the
     // trial writes buffer cur ^ 1 and an accepted trial flips `cur` -- no copy, and no recomputation of the
     // current errors after a rejected trial (they are still in their buffer); `last` = the buffer of the last
@@ -194,7 +197,7 @@ __device__ __forceinline__ void ctl_reset(const LmReset &r) {
     c->need_build = 1;
     c->it = c->qmax = c->nBad = c->trials = c->its = 0;
     c->opt_it = r.opt_it, c->max_trials = r.max_trials, c->lambda_init = r.lambda_init;
-    c->lambda = r.lambda_init, c->ni = 2, c->rho = 0, c->accepted = 0;
+    c->lambda = r.lambda_init, c->ni = 2, c->rho = 0, c->accepted = 0, c->n_acc = 0;
     c->done = r.opt_it <= 0;
     set_gates(c);
 }
@@ -265,6 +268,7 @@ __device__ void finish_trial_body(double *sh, LmCtl *c, const double *mono_parti
         c->ni = 2;
         c->currentChi = tempChi;
         c->accepted = 1;
+        ++c->n_acc;
         c->errors_of_current = 1;
         c->cur = trial_buf, c->cur_chi = chi;   // the trial's buffers become current
     } else {
@@ -1087,7 +1091,7 @@ __global__ void __launch_bounds__(256) assemble_kernel(Gather G, Imu I, BlockPat
 // ---- trial: keyframe update (in the errors kernel) -----------------------------------------------------------
 // ImuCamPose::Update (G2oTypes.cc:211-235): the new body pose of optimisable keyframe k from the current state a and the
 // solution xp (keyframe order), and camera c's Rcw / tcw of it.
-__device__ __forceinline__ void kf_trial_pose(const Rig &rig, const State &a, const double *u, int k, int c,
+__device__ __forceinline__ void kf_trial_pose(const Rig &rig, const State &a, const double *u, int k, int c, bool norm,
                                               double Rn[9], double twb[3], double Rc[9], double tc[3]) {
     double Rwb[9], dRw[9], tt[3];
     for (int q = 0; q < 9; ++q) Rwb[q] = a.Rwb[9 * k + q];
@@ -1095,6 +1099,7 @@ __device__ __forceinline__ void kf_trial_pose(const Rig &rig, const State &a, co
     for (int q = 0; q < 3; ++q) twb[q] = a.twb[3 * k + q] + tt[q];
     exp_so3(u, dRw);
     mm3(Rwb, dRw, Rn);
+    if (norm) polar3(Rn);   // NormalizeRotation after every third update (:220-225)
     double Rbw[9], tbw[3];
     tr3(Rn, Rbw);
     mv3(Rbw, twb, tbw);
@@ -1446,6 +1451,8 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
 // are the state's.  The state / error buffers are the role's (role_buf); the updates start from the role-0 state.
 struct ErrTrial {
     const double *xp;        // the solution (keyframe order), or null: no update
+    int norm;                // host driver: this trial normalises the keyframe rotations (the device driver reads it
+                             // from the control block)
     const double *b;         // the assembled gradient (keyframe order)
     double lambda;
     const int *offV, *offG, *offA;
@@ -1468,6 +1475,7 @@ __global__ void __launch_bounds__(256) err_kernel(int n_grp, int lead, int has_i
     const State a = role_buf(ctl, 0) ? s1 : s0;
     const ErrBufs eb = bi ? e1 : e0;
     const bool trial = T.xp != nullptr;
+    const bool norm = ctl ? ctl->n_acc % 3 == 2 : T.norm != 0;
     const double lambda = trial ? lm_lambda(ctl, T.lambda) : 0.0;
     const int tid = threadIdx.x, C = rig.n_cams;
     int bid = blockIdx.x;
@@ -1477,7 +1485,7 @@ __global__ void __launch_bounds__(256) err_kernel(int n_grp, int lead, int has_i
                 for (int t = tid; t < T.n_opt * C; t += blockDim.x) {
                     const int k = t / C, c = t - k * C;
                     double Rn[9], twb[3], Rc[9], tc[3];
-                    kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, Rn, twb, Rc, tc);
+                    kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, norm, Rn, twb, Rc, tc);
                     for (int q = 0; q < 9; ++q) s.Rcw[((size_t)k * C + c) * 9 + q] = Rc[q];
                     for (int q = 0; q < 3; ++q) s.tcw[((size_t)k * C + c) * 3 + q] = tc[q];
                     if (c == 0) {
@@ -1538,7 +1546,7 @@ __global__ void __launch_bounds__(256) err_kernel(int n_grp, int lead, int has_i
         for (int t = tid - kGrpLand; t < w * C; t += blockDim.x - kGrpLand) {
             const int la = t / C, c = t - la * C, k = T.lkf_kf[L.grp_kf[g] + la];
             double Rn[9], twb[3];
-            kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, Rn, twb, PS + 12 * t, PS + 12 * t + 9);
+            kf_trial_pose(rig, a, T.xp + R.offP[k], k, c, norm, Rn, twb, PS + 12 * t, PS + 12 * t + 9);
         }
     }
     __syncthreads();
@@ -1556,7 +1564,7 @@ __global__ void __launch_bounds__(256) err_kernel(int n_grp, int lead, int has_i
             for (int q = 0; q < 3; ++q) tc[q] = o[9 + q];
         } else {   // the scalar group: per edge
             double Rn[9], twb[3];
-            kf_trial_pose(rig, a, T.xp + R.offP[E.kf[e]], E.kf[e], cam, Rn, twb, Rc, tc);
+            kf_trial_pose(rig, a, T.xp + R.offP[E.kf[e]], E.kf[e], cam, norm, Rn, twb, Rc, tc);
         }
         r0 += mono_err_edge(rig, Rc, tc, E, e, X + 3 * (E.pt[e] - p0), delta, dsqr, delta_st, dsqr_st, eb.err, eb.err3,
                             eb.chi2);
@@ -2466,11 +2474,12 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
 // first, from the role-0 state into the role's state.  The host driver keeps one error buffer (both ErrBufs eb(0)).
 static omv_status launch_errors(omv_lba *h, const State &s0, const State &s1, const LmCtl *ctl, int gate, int role,
                                 LmReset reset = LmReset{}, bool init_partials = false, const double *xp = nullptr,
-                                double lambda = 0.0, bool one_buffer = false) {
+                                double lambda = 0.0, bool one_buffer = false, int n_acc = 0) {
     const int ng = h->n_mono > 0 || xp ? h->n_lgrp : 0;
     const int lead = xp || h->imu_here ? 1 : 0;
     const int blocks = (ng > 0 ? omv::xcd_grid(ng) : 0) + lead;
-    const ErrTrial T{xp, h->d_bb, lambda, h->d_offV, h->d_offG, h->d_offA, h->n_opt, h->d_e_lkf, h->d_lkf_kf};
+    const ErrTrial T{xp, n_acc % 3 == 2 ? 1 : 0, h->d_bb, lambda, h->d_offV, h->d_offG, h->d_offA, h->n_opt, h->d_e_lkf,
+                     h->d_lkf_kf};
     const size_t lds = (3 * (size_t)kGrpLand + 12 * (size_t)kGrpW * h->rig.n_cams) * sizeof(double);
     if (blocks > 0)
         err_kernel<<<blocks, 256, lds, h->stream>>>(ng, lead, h->imu_here ? 1 : 0, h->rig, s0, s1, h->E, h->L, h->R, T,
@@ -2801,7 +2810,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
     double errors_chi = sc[0];
     bool errors_of_current = true;
     double lambda = 0, ni = 2;
-    int nBad = 0, trials = 0, its = 0;
+    int nBad = 0, trials = 0, its = 0, n_acc = 0;   // n_acc: accepted updates (ImuCamPose::its, see LmCtl)
     for (int it = 0; it < o->opt_it; ++it) {
         ++its;
         State &A = h->st[h->cur];
@@ -2838,7 +2847,8 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
             HIP_OK(hipEventRecord(h->ev[4], st));
             // the keyframe update and the landmarks' back-substitution A -> B, the trial's errors (one launch, this
             // driver's one error buffer)
-            if ((rs = launch_errors(h, A, B, nullptr, kGateAlways, 1, LmReset{}, false, h->d_x, lambda, true)) != OMV_OK)
+            if ((rs = launch_errors(h, A, B, nullptr, kGateAlways, 1, LmReset{}, false, h->d_x, lambda, true, n_acc)) !=
+                OMV_OK)
                 return rs;
             if ((rs = lba_read_scalars(h, 1 + h->n_lgrp, sc, true)) != OMV_OK) return rs;
             const int fail = sc[2] != 0.0;
@@ -2867,6 +2877,7 @@ omv_status omv_lba_optimize(omv_lba *h, const omv_lba_opts *o, omv_lba_problem *
                 lambda *= std::max(1. / 3., alpha);
                 ni = 2;
                 currentChi = tempChi;
+                ++n_acc;
                 // fixed keyframes are identical in both buffers; make B the current state
                 h->cur = 1 - h->cur;
                 errors_of_current = true;

@@ -339,6 +339,9 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
     const float chi2Mono[4] = {kLF ? 5.991f : 12.f, kLF ? 5.991f : 7.5f, 5.991f, 5.991f};   // :5992 / :5432
     const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
     int nBad = 0, nIn = 0;
+    // ImuCamPose::its of the pose vertex this thread updates (thread 0 the frame, thread 1 the previous frame): 0 at
+    // the vertex's creation (G2oTypes.cc:74), Rwb normalised after every third Update (:220-225)
+    int its_v = 0;
     for (int it = 0; it < 4; ++it) {
         const bool robust = it < 3;   // setRobustKernel(0) after the third classification
         for (int gi = 0; gi < 10; ++gi) {
@@ -517,6 +520,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
                     for (int q = 0; q < 3; ++q) tw[q] += t[q];
                     exp_so3(xv, dR);
                     mm3(Rw, dR, Rn);
+                    if (++its_v >= 3) polar3(Rn), its_v = 0;   // NormalizeRotation after every third update
                     for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
                     if (tid == 0) {
                         double Rbw[9], tbw[3];
@@ -1621,6 +1625,9 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
         const float chi2Mono[4] = {kLF ? 5.991f : 12.f, kLF ? 5.991f : 7.5f, 5.991f, 5.991f};   // :5992 / :5432
         const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
         double nBad = 0, nIn = 0;
+        // ImuCamPose::its of the pose vertex this lane updates (lane 0 the frame, lane 1 the previous frame): 0 at the
+        // vertex's creation (G2oTypes.cc:74), Rwb normalised after every third Update (:220-225)
+        int its_v = 0;
 #ifdef OMV_POSE_PROFILE
         unsigned long long t_cls = 0;   // classification passes + their exchanges
         LAT_T(t_loop0);
@@ -1765,6 +1772,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                         for (int q = 0; q < 3; ++q) tw[q] += t[q];
                         exp_so3(xv, dR);
                         mm3(Rw, dR, Rn);
+                        if (++its_v >= 3) polar3(Rn), its_v = 0;   // NormalizeRotation after every third update
                         for (int q = 0; q < 9; ++q) Rw[q] = Rn[q];
                         for (int q = 0; q < 3; ++q)
                             svel[3 * v + q] += xv[6 + q], sbg[3 * v + q] += xv[9 + q], sba[3 * v + q] += xv[12 + q];

@@ -896,12 +896,18 @@ struct Solver {
         return true;
     }
 
+    // ImuCamPose::its of the optimisable keyframes (every one is created with its 0 and updated by every step, so one
+    // counter serves all; a rejected step's pop restores it): Rwb normalised after every third Update (:220-225)
+    int its = 0;
     void update(const std::vector<double> &xp, const std::vector<double> &xl) {
+        const bool norm = ++its >= 3;
+        if (norm) its = 0;
         for (int k = 0; k < P.n_opt; ++k) {
             const double *u = &xp[offP[k]];
             Pose &ps = pose[k];
             ps.twb = add(ps.twb, mul(ps.Rwb, V3{{u[3], u[4], u[5]}}));
             ps.Rwb = mul(ps.Rwb, expSO3(u[0], u[1], u[2]));
+            if (norm) polar3(ps.Rwb.m);
             const M3 Rbw = tr(ps.Rwb);
             const V3 tbw = scale(mul(Rbw, ps.twb), -1.0);
             for (int c = 0; c < C; ++c) {
@@ -932,9 +938,10 @@ struct Solver {
     struct Snapshot {
         std::vector<Pose> pose;
         std::vector<V3> vel, bg, ba, pts;
+        int its;
     };
-    Snapshot push() const { return Snapshot{pose, vel, bg, ba, pts}; }
-    void pop(const Snapshot &s) { pose = s.pose, vel = s.vel, bg = s.bg, ba = s.ba, pts = s.pts; }
+    Snapshot push() const { return Snapshot{pose, vel, bg, ba, pts, its}; }
+    void pop(const Snapshot &s) { pose = s.pose, vel = s.vel, bg = s.bg, ba = s.ba, pts = s.pts, its = s.its; }
 
     void write_state(omv_lba_problem &p) const {
         for (int k = 0; k < p.n_kf; ++k) {
@@ -1178,9 +1185,12 @@ struct PoseProblem {
     V3 twb, v, bg, ba;
     std::vector<M3> Rcw;
     std::vector<V3> tcw;
-    // fixed keyframe vertices
+    // fixed keyframe vertices (LastFrame: the previous frame's, optimised)
     M3 kRwb;
     V3 ktwb, kv, kbg, kba;
+    // ImuCamPose::its of the two pose vertices (0 when the vertex is created, G2oTypes.cc:6 / :74): every third
+    // Update normalises Rwb (:220-225)
+    int its = 0, kits = 0;
     Preint pre;
     std::vector<double> info9;
     M3 infoG, infoA;
@@ -1321,6 +1331,7 @@ struct PoseProblem {
         // VertexPose::oplusImpl -> ImuCamPose::Update (:211-235); velocity / biases additive
         twb = add(twb, mul(Rwb, V3{{x[3], x[4], x[5]}}));
         Rwb = mul(Rwb, expSO3(x[0], x[1], x[2]));
+        if (++its >= 3) polar3(Rwb.m), its = 0;   // NormalizeRotation after every third update
         const M3 Rbw = tr(Rwb);
         const V3 tbw = scale(mul(Rbw, twb), -1.0);
         for (int c = 0; c < C; ++c) {
@@ -1614,6 +1625,7 @@ struct PoseLFProblem : PoseProblem {
         // VertexPose::oplusImpl -> ImuCamPose::Update (G2oTypes.cc:211-235) on both frames
         twb = add(twb, mul(Rwb, V3{{x[3], x[4], x[5]}}));
         Rwb = mul(Rwb, expSO3(x[0], x[1], x[2]));
+        if (++its >= 3) polar3(Rwb.m), its = 0;   // NormalizeRotation after every third update
         const M3 Rbw = tr(Rwb);
         const V3 tbw = scale(mul(Rbw, twb), -1.0);
         for (int c = 0; c < C; ++c) {
@@ -1623,6 +1635,7 @@ struct PoseLFProblem : PoseProblem {
         for (int q = 0; q < 3; ++q) v[q] += x[6 + q], bg[q] += x[9 + q], ba[q] += x[12 + q];
         ktwb = add(ktwb, mul(kRwb, V3{{x[18], x[19], x[20]}}));
         kRwb = mul(kRwb, expSO3(x[15], x[16], x[17]));
+        if (++kits >= 3) polar3(kRwb.m), kits = 0;
         for (int q = 0; q < 3; ++q) kv[q] += x[21 + q], kbg[q] += x[24 + q], kba[q] += x[27 + q];
         return ok;
     }
