@@ -985,6 +985,7 @@ __host__ __device__ __forceinline__ int sw16(int r, int c) { return 16 * r + (c 
 
 struct BlockPat {
     int nb, n_slots, n_lev;
+    int n_lds;                       // hybrid solver (G = 2): slots 0 .. n_lds-1 in LDS, the rest in global scratch
     const int *perm;                 // [nb] position -> keyframe
     const int *slot_kr, *slot_kc;    // [n_slots] keyframes of the block's row / column
     const int *dslot;                // [nb] diagonal slot per position
@@ -1113,7 +1114,7 @@ __device__ __forceinline__ void kf_trial_pose(const Rig &rig, const State &a, co
 
 // Wave-synchronous step: LDS operations of one wavefront complete in order, so the fence only has
 // to stop the compiler (wavefront scope); the global-memory fallback needs workgroup scope.
-template <bool G>
+template <int G>
 __device__ __forceinline__ void wave_sync() {
     if (G) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1189,7 +1190,7 @@ __device__ __forceinline__ void sweep_all(double cur[4], int q, int j) {
     }
 }
 
-template <bool G>
+template <int G>
 __device__ __forceinline__ void inv16(double *D, int lane, int *bad) {
     const int q = lane >> 4, j = lane & 15;
     double cur[4];
@@ -1232,23 +1233,25 @@ constexpr int kLdltThreads = 512;
 constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (the static part is one int)
 
 // Forward substitution of one column (one wavefront): z_i = Dinv_i (y_i - sum_k S_ik z_k) over the row structure
-// (descendants, final by then), four blocks at a time (lane groups).
-__device__ __forceinline__ void forward_col(const double *pk, double *y, const BlockPat &P, int i, int lane) {
+// (descendants, final by then); lane group grp takes the terms m = 4 grp .. 4 grp + 3 of every block (four loads of
+// S and four of z per lane and block, all lanes busy whatever the block count).
+template <typename Blk>
+__device__ __forceinline__ void forward_col(const Blk &blk, double *y, const BlockPat &P, int i, int lane) {
     const int r16 = lane & 15, grp = lane >> 4;
     double acc[4] = {0, 0, 0, 0};   // four chains (the sum is latency-bound)
-    for (int q = P.rs_start[i] + grp; q < P.rs_start[i + 1]; q += 4) {
+    for (int q = P.rs_start[i]; q < P.rs_start[i + 1]; ++q) {
         const int2 e = P.rs[q];
-        const double *Sik = pk + (size_t)e.x * 256;
-        const double *zk = y + 16 * e.y;
+        const double *Sik = blk(e.x);
+        const double *zk = y + 16 * e.y + 4 * grp;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc[m & 3] = __builtin_fma(Sik[sw16(r16, m)], zk[m], acc[m & 3]);
+        for (int m = 0; m < 4; ++m) acc[m] = __builtin_fma(Sik[sw16(r16, 4 * grp + m)], zk[m], acc[m]);
     }
     double a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     a += __shfl_xor(a, 16, 64);
     a += __shfl_xor(a, 32, 64);
     const double v = y[16 * i + r16] - a;
     // Dinv_i v: lane group grp takes columns 4 grp .. 4 grp + 3, then the four partial sums
-    const double *Di = pk + (size_t)P.dslot[i] * 256;
+    const double *Di = blk(P.dslot[i]);
     double out = 0;
 #pragma unroll
     for (int m = 0; m < 4; ++m) out = __builtin_fma(Di[sw16(r16, 4 * grp + m)], __shfl(v, 4 * grp + m, 16), out);
@@ -1262,7 +1265,9 @@ __device__ __forceinline__ void forward_col(const double *pk, double *y, const B
 // on separate wavefronts, then its trailing updates -- grouped by target block, each group on one wavefront in
 // ascending column order (no two wavefronts write a block) -- beside its columns' forward substitutions.  Backward
 // substitution gathers each column's structure (ancestors) level by level downwards.
-template <bool G>   // G: blocks in global scratch (pattern too large for LDS)
+// G: 0 blocks in LDS, 1 blocks in global scratch (pattern too large for LDS), 2 the first P.n_lds blocks in LDS and
+// the rest in global scratch
+template <int G>
 __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, BlockPat Pg, const double *b,
                                                             const double *coef, double *x, double *gscratch,
                                                             int *fail, const LmCtl *ctl) {
@@ -1270,11 +1275,14 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     __shared__ int bad;
     if (!gate_open(ctl, kGateTrial)) return;
     const int nb = Pg.nb, nv = 16 * nb;
-    double *pk = G ? gscratch : lsm;
-    double *y = pk + (size_t)Pg.n_slots * 256;
+    double *pk = G == 1 ? gscratch : lsm;
+    const int n_lds = G == 2 ? Pg.n_lds : Pg.n_slots;
+    double *y = pk + (size_t)n_lds * 256;
     double *xs = y + nv;
+    // block s: LDS or (hybrid, s >= n_lds) global scratch
+    auto blk = [&](int s) -> double * { return G == 2 && s >= n_lds ? gscratch + (size_t)s * 256 : pk + (size_t)s * 256; };
     BlockPat P = Pg;   // the schedule, rebased onto its LDS copy when staged
-    if (!G && Pg.blob_ints > 0) {
+    if (G != 1 && Pg.blob_ints > 0) {
         int *sched = reinterpret_cast<int *>(xs + nv);
         for (int q = threadIdx.x; q < Pg.blob_ints; q += blockDim.x) sched[q] = Pg.blob[q];
         auto rb = [&](auto *p) { return reinterpret_cast<decltype(p)>(sched + (reinterpret_cast<const int *>(p) - Pg.blob)); };
@@ -1298,13 +1306,17 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
         const double2 *src = (const double2 *)Sp;
         double2 *dst = (double2 *)pk;
         // eight loads in flight per thread (a dependent load-store loop waits one memory latency per 8 KB)
-        const int n2 = P.n_slots * 128, T = blockDim.x;
+        const int n2 = n_lds * 128, T = blockDim.x;
         for (int q0 = tid; q0 < n2; q0 += 8 * T) {
             double2 v[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = src[min(q0 + k * T, n2 - 1)];   // unconditional: all eight in flight
 #pragma unroll
             for (int k = 0; k < 8; ++k) dst[min(q0 + k * T, n2 - 1)] = v[k];   // past the end: the last entry again
+        }
+        if (G == 2) {   // the global part, at its own offsets of the scratch
+            double2 *gd = (double2 *)gscratch;
+            for (int q = n2 + tid; q < P.n_slots * 128; q += T) gd[q] = src[q];
         }
         for (int q = tid; q < nv; q += blockDim.x) {
             const int g = 16 * Pg.perm[q >> 4] + (q & 15);   // (the LDS copy is not complete before the barrier)
@@ -1362,20 +1374,18 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
                     if (g >= 0) {
                         for (int u = P.ug_task_start[g]; u < P.ug_task_start[g + 1]; ++u) {
                             const int4 t = P.ug[u];
-                            update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
-                                     pk + (size_t)t.w * 256, lane);
+                            update16(blk(t.x), blk(t.y), blk(t.z), blk(t.w), lane);
                         }
                         wave_sync<G>();
                     }
-                    inv16<G>(pk + (size_t)P.dslot[col] * 256, lane, &bad);
+                    inv16<G>(blk(P.dslot[col]), lane, &bad);
                 } else if (q < ni + nf) {
-                    forward_col(pk, y, P, P.lev_col[f0 + q - ni], lane);
+                    forward_col(blk, y, P, P.lev_col[f0 + q - ni], lane);
                 } else {
                     const int g = r0 + q - ni - nf;
                     for (int u = P.ug_task_start[g]; u < P.ug_task_start[g + 1]; ++u) {
                         const int4 t = P.ug[u];
-                        update16(pk + (size_t)t.x * 256, pk + (size_t)t.y * 256, pk + (size_t)t.z * 256,
-                                 pk + (size_t)t.w * 256, lane);
+                        update16(blk(t.x), blk(t.y), blk(t.z), blk(t.w), lane);
                     }
                 }
 #ifdef OMV_LDLT_PROFILE
@@ -1402,18 +1412,18 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     for (int lev = P.n_lev - 1; lev >= 0; --lev) {
         for (int c = P.lev_start[lev] + wave; c < P.lev_start[lev + 1]; c += nw) {
             const int k = P.lev_col[c];
-            double acc4[4] = {0, 0, 0, 0};
-            for (int q = P.cs_start[k] + grp; q < P.cs_start[k + 1]; q += 4) {
+            double acc4[4] = {0, 0, 0, 0};   // lane group grp: rows 4 grp .. 4 grp + 3 of every block
+            for (int q = P.cs_start[k]; q < P.cs_start[k + 1]; ++q) {
                 const int2 e = P.cs[q];
-                const double *Sik = pk + (size_t)e.x * 256;
-                const double *xi = xs + 16 * e.y;
+                const double *Sik = blk(e.x);
+                const double *xi = xs + 16 * e.y + 4 * grp;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc4[r & 3] = __builtin_fma(Sik[sw16(r, r16)], xi[r], acc4[r & 3]);
+                for (int r = 0; r < 4; ++r) acc4[r] = __builtin_fma(Sik[sw16(4 * grp + r, r16)], xi[r], acc4[r]);
             }
             double acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
             acc += __shfl_xor(acc, 16, 64);
             acc += __shfl_xor(acc, 32, 64);
-            const double *Dk = pk + (size_t)P.dslot[k] * 256;
+            const double *Dk = blk(P.dslot[k]);
             double out = 0;
 #pragma unroll
             for (int m = 0; m < 4; ++m) out = __builtin_fma(Dk[sw16(r16, 4 * grp + m)], __shfl(acc, 4 * grp + m, 16), out);
@@ -1881,7 +1891,9 @@ omv_status omv_lba_create(int max_kf, int max_cams, int max_pts, int max_mono, i
     HIP_OK(hipHostMalloc((void **)&h->h_ctl, sizeof(LmCtl), hipHostMallocDefault));
     HIP_OK(hipMalloc((void **)&h->d_ctl, sizeof(LmCtl)));
     // the reduced-system factorisation stages its nonzero blocks in up to 150 KB of LDS
-    h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    h->lds_ok = hipFuncSetAttribute((const void *)ldlt_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kLdltLds) == hipSuccess &&
+                hipFuncSetAttribute((const void *)ldlt_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdltLds) == hipSuccess;
     // the landmark groups of the build take ~77 KB of LDS (two workgroups per CU)
     if (hipFuncSetAttribute((const void *)build_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBuildLds) !=
@@ -2239,8 +2251,13 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         iv_start[nb] = (int)imu_vec.size();
     }
     const size_t ldlt_bytes = ((size_t)n_slots * 256 + 2 * (size_t)nred) * sizeof(double);
-    h->use_lds = h->lds_ok && ldlt_bytes <= kLdltLds ? 1 : 0;
-    h->ldlt_lds = h->use_lds ? ldlt_bytes : 0;
+    // the solver's storage: 1 every block in LDS; 2 (the pattern does not fit) the vectors, the schedule and the first
+    // blocks in LDS, the rest in global scratch; 0 (no LDS attribute, or a test build) every block in global scratch
+    h->use_lds = !h->lds_ok ? 0 : ldlt_bytes <= kLdltLds ? 1 : kLdltLds > 2 * (size_t)nred * sizeof(double) + 8 * 256 * sizeof(double) ? 2 : 0;
+#ifdef OMV_LBA_FORCE_G
+    h->use_lds = 0;
+#endif
+    h->ldlt_lds = h->use_lds == 1 ? ldlt_bytes : 0;
     // inertial information (EdgeInertial ctor :486-495) and random-walk information
     std::vector<double> info9((size_t)NI * 81), infoG((size_t)NI * 9), infoA((size_t)NI * 9);
     for (int i = 0; i < NI; ++i) {
@@ -2414,7 +2431,14 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         // stage the schedule in LDS when it fits beside the blocks and vectors
         const size_t sched_bytes = blob.size() * sizeof(int);
         B.blob_ints = 0;
-        if (h->use_lds && h->ldlt_lds + sched_bytes <= kLdltLds) {
+        B.n_lds = n_slots;
+        if (h->use_lds == 2) {   // hybrid: the vectors and the schedule in LDS, then as many blocks as fit
+            const size_t vb = 2 * (size_t)nred * sizeof(double);
+            const bool sch = vb + sched_bytes + 8 * 256 * sizeof(double) <= kLdltLds;
+            B.n_lds = std::min(n_slots, (int)((kLdltLds - vb - (sch ? sched_bytes : 0)) / (256 * sizeof(double))));
+            h->ldlt_lds = (size_t)B.n_lds * 256 * sizeof(double) + vb + (sch ? sched_bytes : 0);
+            B.blob_ints = sch ? (int)blob.size() : 0;
+        } else if (h->use_lds && h->ldlt_lds + sched_bytes <= kLdltLds) {
             h->ldlt_lds += sched_bytes;
             B.blob_ints = (int)blob.size();
         }
@@ -2440,7 +2464,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     h->d_coef = h->d_bb + nred;
     h->n_reduce = (size_t)n_slots * 256 + 2 * (size_t)nred;
     h->d_x = dalloc<double>(ow, nred);
-    h->d_scratch = dalloc<double>(ow, h->use_lds ? 8 : (size_t)n_slots * 256 + 2 * (size_t)nred + 8);
+    h->d_scratch = dalloc<double>(ow, h->use_lds == 1 ? 8 : (size_t)n_slots * 256 + 2 * (size_t)nred + 8);
     h->d_fail = dalloc<int>(ow, 1);
     if (!h->d_fail) return OMV_ERR_HIP;
     HIP_OK(hipMemset(h->d_imu_partial, 0, sizeof(double)));
@@ -2614,12 +2638,15 @@ static omv_status launch_assemble(omv_lba *h, double lambda, const LmCtl *c) {
 }
 
 static void launch_ldlt(omv_lba *h, const LmCtl *c) {
-    if (h->use_lds)
-        ldlt_kernel<false><<<1, kLdltThreads, h->ldlt_lds, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x,
-                                                                        h->d_scratch, h->d_fail, c);
+    if (h->use_lds == 1)
+        ldlt_kernel<0><<<1, kLdltThreads, h->ldlt_lds, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x,
+                                                                    h->d_scratch, h->d_fail, c);
+    else if (h->use_lds == 2)
+        ldlt_kernel<2><<<1, kLdltThreads, h->ldlt_lds, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x,
+                                                                    h->d_scratch, h->d_fail, c);
     else
-        ldlt_kernel<true><<<1, kLdltThreads, 0, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x, h->d_scratch,
-                                                             h->d_fail, c);
+        ldlt_kernel<1><<<1, kLdltThreads, 0, h->stream>>>(h->d_S, h->BP, h->d_bb, h->d_coef, h->d_x, h->d_scratch,
+                                                          h->d_fail, c);
 }
 
 // One LM step of the device driver: the gated kernel sequence (see LmCtl).  The state and error buffers are
