@@ -1235,8 +1235,19 @@ constexpr size_t kLdltLds = 160 * 1024 - 512;   // dynamic LDS of the solver (th
 // Forward substitution of one column (one wavefront): z_i = Dinv_i (y_i - sum_k S_ik z_k) over the row structure
 // (descendants, final by then); lane group grp takes the terms m = 4 grp .. 4 grp + 3 of every block (four loads of
 // S and four of z per lane and block, all lanes busy whatever the block count).
+// Block s of the solver's storage: LDS, or (hybrid, s >= n_lds) global scratch.  A value type: a reference-capturing
+// lambda here put the kernel's locals on the private stack (144 B of scratch per lane, ~9 us more per solve).
+template <int G>
+struct BlkAt {
+    double *pk, *gs;
+    int n_lds;
+    __device__ __forceinline__ double *operator()(int s) const {
+        return G == 2 && s >= n_lds ? gs + (size_t)s * 256 : pk + (size_t)s * 256;
+    }
+};
+
 template <typename Blk>
-__device__ __forceinline__ void forward_col(const Blk &blk, double *y, const BlockPat &P, int i, int lane) {
+__device__ __forceinline__ void forward_col(const Blk blk, double *y, const BlockPat &P, int i, int lane) {
     const int r16 = lane & 15, grp = lane >> 4;
     double acc[4] = {0, 0, 0, 0};   // four chains (the sum is latency-bound)
     for (int q = P.rs_start[i]; q < P.rs_start[i + 1]; ++q) {
@@ -1279,8 +1290,7 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
     const int n_lds = G == 2 ? Pg.n_lds : Pg.n_slots;
     double *y = pk + (size_t)n_lds * 256;
     double *xs = y + nv;
-    // block s: LDS or (hybrid, s >= n_lds) global scratch
-    auto blk = [&](int s) -> double * { return G == 2 && s >= n_lds ? gscratch + (size_t)s * 256 : pk + (size_t)s * 256; };
+    const BlkAt<G> blk{pk, gscratch, n_lds};
     BlockPat P = Pg;   // the schedule, rebased onto its LDS copy when staged
     if (G != 1 && Pg.blob_ints > 0) {
         int *sched = reinterpret_cast<int *>(xs + nv);

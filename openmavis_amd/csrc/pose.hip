@@ -189,18 +189,25 @@ __device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const d
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
     double pj[9];
     cam_jac(rig, c, Xc, pj);
-    const int nr = v.stereo ? 3 : 2;
+    // the stereo row always (zero for a mono edge, never read then): constant trip counts keep pr / JP in registers
+    // (a row count only known at run time put both on the private stack)
     if (v.stereo) {
         const double inv_z2 = 1.0 / (Xc[2] * Xc[2]);
         pj[6] = pj[0], pj[7] = pj[1], pj[8] = pj[2] + rig.bf * inv_z2;
+    } else {
+        pj[6] = pj[7] = pj[8] = 0.0;
     }
     double pr[9];
-    for (int r = 0; r < nr; ++r)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
         for (int q = 0; q < 3; ++q)
             pr[3 * r + q] = pj[3 * r] * rig.Rcb[c][q] + pj[3 * r + 1] * rig.Rcb[c][3 + q] + pj[3 * r + 2] * rig.Rcb[c][6 + q];
     const double x = Xb[0], y = Xb[1], z = Xb[2];
     const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-    for (int r = 0; r < nr; ++r)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
         for (int q = 0; q < 6; ++q)
             JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
 }
