@@ -1184,11 +1184,14 @@ __device__ __forceinline__ bool ldlt_pick_solve_wide(const double *H, const doub
     return true;
 }
 
-// EdgeInertial::linearizeOplus (G2oTypes.cc:533-599) on one wavefront from the cached rotation error (eR, er): the
-// lane roles of imu_jacobian_par, synchronised by wave barriers; entry for entry the arithmetic of imu_jacobian.
-// J [9][24] (LDS) must be zeroed by the caller; RJ, iJ: LDS scratch [9].
-__device__ void imu_jacobian_wave(const State &s, const Imu &I, const double *eR, const double *er, double *J,
-                                  double *RJ, double *iJ, int lane) {
+// EdgeInertial computeError + linearizeOplus (G2oTypes.cc:502-599) for LastFrame on one wavefront with uniform
+// control flow: every lane evaluates the same values -- the error's rotation chain (delta_rot, LogSO3, the inverse right
+// Jacobian and the products behind it) and the blocks that do not depend on it (the right Jacobian of the bias
+// correction, the velocity / position blocks) are independent instruction streams the wave interleaves -- and single
+// lanes store the blocks.  (Lane-role branches on one wavefront serialise: the previous form's nine roles added up to
+// ~3.9 us per iteration.)  The arithmetic is imu_error's and imu_jacobian's, operation for operation.  J [9][24]
+// (LDS) must be zeroed by the caller.
+__device__ __forceinline__ void imu_error_jac_uniform(const State &s, const Imu &I, double *e9o, double *J, int lane) {
     const int k1 = I.kf1[0], k2 = I.kf2[0];
     const float *p = I.pre;
     const double *Rwb1 = s.Rwb + 9 * k1, *Rwb2 = s.Rwb + 9 * k2;
@@ -1196,43 +1199,40 @@ __device__ void imu_jacobian_wave(const State &s, const Imu &I, const double *eR
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) J[(r0 + r) * 24 + c0 + c] = sgn * B[3 * r + c];
     };
+    double e[9], eR[9];
+    imu_error(s, I, 0, e, eR);
     const double dt = (double)p[PreView::dT];
     const double g[3] = {0, 0, -(double)9.81f};
     double Rbw1[9];
     tr3(Rwb1, Rbw1);
-    if (lane == 0) {
-        double invJr[9], R2t[9], A[9], B[9];
-        inv_right_jac(er, invJr);
-        tr3(Rwb2, R2t);
-        mm3(invJr, R2t, A);
-        mm3(A, Rwb1, B);
-        put(0, 0, B, -1.0);
-        put(0, 15, invJr, 1.0);
-        for (int q = 0; q < 9; ++q) iJ[q] = invJr[q];
-    } else if (lane == 1) {
+    // the right Jacobian of the gyro-bias correction (independent of the error)
+    double RJ[9], JRg[9];
+    {
         float b1[6];
         for (int q = 0; q < 3; ++q) b1[q] = (float)s.ba[3 * k1 + q], b1[3 + q] = (float)s.bg[3 * k1 + q];
         const float dbgf[3] = {b1[3] - p[PreView::b + 3], b1[4] - p[PreView::b + 4], b1[5] - p[PreView::b + 5]};
         const double dbg[3] = {(double)dbgf[0], (double)dbgf[1], (double)dbgf[2]};
-        double JRg[9], w3[3], R[9];
+        double w3[3];
         for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q];
         mv3(JRg, dbg, w3);
-        right_jac(w3, R);
-        for (int q = 0; q < 9; ++q) RJ[q] = R[q];
-    } else if (lane == 2) {
+        right_jac(w3, RJ);
+    }
+    {   // velocity / position rows (independent of the error)
         double v[3], w[3], W[9];
         for (int q = 0; q < 3; ++q) v[q] = s.vel[3 * k2 + q] - s.vel[3 * k1 + q] - g[q] * dt;
         mv3(Rbw1, v, w);
         hat3(w, W);
-        put(3, 0, W, 1.0);
-    } else if (lane == 3) {
-        double v[3], w[3], W[9];
+        if (lane == 2) put(3, 0, W, 1.0);
         for (int q = 0; q < 3; ++q)
             v[q] = s.twb[3 * k2 + q] - s.twb[3 * k1 + q] - s.vel[3 * k1 + q] * dt - 0.5 * g[q] * dt * dt;
         mv3(Rbw1, v, w);
         hat3(w, W);
-        put(6, 0, W, 1.0);
-    } else if (lane == 4) {
+        if (lane == 3) put(6, 0, W, 1.0);
+        double A8[9];
+        mm3(Rbw1, Rwb2, A8);
+        if (lane == 8) put(6, 18, A8, 1.0);
+    }
+    if (lane == 4) {
         for (int q = 0; q < 3; ++q) J[(6 + q) * 24 + 3 + q] = -1.0;
         put(3, 6, Rbw1, -1.0);
         put(3, 21, Rbw1, 1.0);
@@ -1250,21 +1250,30 @@ __device__ void imu_jacobian_wave(const State &s, const Imu &I, const double *eR
         put(6, 9, B, -1.0);
         for (int q = 0; q < 9; ++q) B[q] = p[PreView::JPa + q];
         put(6, 12, B, -1.0);
-    } else if (lane == 8) {
-        double A[9];
-        mm3(Rbw1, Rwb2, A);
-        put(6, 18, A, 1.0);
     }
-    wave_lds_sync();
-    if (lane == 0) {
-        double eRt[9], A[9], B[9], Jg[9], JRg[9], invJr[9], R[9];
-        for (int q = 0; q < 9; ++q) JRg[q] = p[PreView::JRg + q], invJr[q] = iJ[q], R[q] = RJ[q];
+    // the rotation rows (on the error's chain)
+    double invJr[9];
+    inv_right_jac(e, invJr);
+    {
+        double R2t[9], A[9], B[9];
+        tr3(Rwb2, R2t);
+        mm3(invJr, R2t, A);
+        mm3(A, Rwb1, B);
+        if (lane == 0) {
+            put(0, 0, B, -1.0);
+            put(0, 15, invJr, 1.0);
+        }
+    }
+    {
+        double eRt[9], A[9], B[9], Jg[9];
         tr3(eR, eRt);
         mm3(invJr, eRt, A);
-        mm3(A, R, B);
+        mm3(A, RJ, B);
         mm3(B, JRg, Jg);
-        put(0, 9, Jg, -1.0);
+        if (lane == 1) put(0, 9, Jg, -1.0);
     }
+    if (lane == 0)
+        for (int q = 0; q < 9; ++q) e9o[q] = e[q];
     wave_lds_sync();
 }
 
@@ -1431,7 +1440,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     __shared__ double Hs[N * N], bs[N], xs[N], xt[N], Lm[N * N], ism[kLF ? 1 : 258];
     __shared__ double info9[81], infoG[9], infoA[9];
     __shared__ double J[NJ], WJ[NJ], e9[9], om9[9], bI[NI], s_w1p;
-    __shared__ double cA1[9], cdV[3], cdP[3], eRc[9], erc[3], RJs[9], iJs[9];
+    __shared__ double cA1[9], cdV[3], cdP[3];
     __shared__ double sPr[kLF ? 21 : 1], pH[NP], JPr[NP], PJ[NP], eP[kLF ? 15 : 1], OeP[kLF ? 15 : 1],
         bP[kLF ? 15 : 1];
     __shared__ double Am[NP], Vm[NP], ecs[16];
@@ -1443,8 +1452,9 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
     const int C = rig_in.n_cams;
 #ifdef OMV_POSE_PROFILE
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    __shared__ unsigned long long prof_inert, t2s[48];
+    __shared__ unsigned long long prof_inert, t2s[48], prof_iw[4];
     if (tid == 0) prof_inert = 0;
+    if (tid < 4) prof_iw[tid] = 0;
     if (tid < 48) t2s[tid] = 0;
     LAT_T(t_start);
 #endif
@@ -1559,17 +1569,25 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     for (int c = 0; c < 3; ++c) J[(6 + r) * 9 + 3 + c] = Aq[3 * r + c];
             }
         } else {
-            if (lane == 0) {   // imu_error, keeping dR^T Rbw1 Rwb2 and its log for the Jacobian
-                double e[9], eR[9];
-                imu_error(st, imu, 0, e, eR);
-                for (int q = 0; q < 9; ++q) e9[q] = e[q], eRc[q] = eR[q];
-                for (int q = 0; q < 3; ++q) erc[q] = e[q];
-            }
+#ifdef OMV_POSE_PROFILE
+            LAT_T(ti0);
+#endif
             for (int q = lane; q < 216; q += 64) J[q] = 0.0;
             wave_lds_sync();
-            imu_jacobian_wave(st, imu, eRc, erc, J, RJs, iJs, lane);
+#ifdef OMV_POSE_PROFILE
+            LAT_T(ti1);
+            if (lane == 0) prof_iw[0] += ti1 - ti0;
+#endif
+            imu_error_jac_uniform(st, imu, e9, J, lane);
+#ifdef OMV_POSE_PROFILE
+            LAT_T(ti2);
+            if (lane == 0) prof_iw[1] += ti2 - ti1;
+#endif
         }
         wave_lds_sync();
+#ifdef OMV_POSE_PROFILE
+        LAT_T(ti3);
+#endif
         for (int q = lane; q < NJ + 9; q += 64) {
             if (q < NJ) {
                 const int r = q / NI, c = q - (q / NI) * NI;
@@ -1583,6 +1601,10 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 om9[r] = -t;
             }
         }
+#ifdef OMV_POSE_PROFILE
+        LAT_T(ti4);
+        if (kLF && lane == 0) prof_iw[2] += ti4 - ti3;
+#endif
         if (!sys) return;
         wave_lds_sync();
         // bI = J^T om9 here; the quadratic form J^T Info J is summed entry by entry where the system is assembled
@@ -2017,6 +2039,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                    "ldlt %.1f ldlt+update %.1f inertial(w4) %.1f total %.1f us\n", (int)kLF, G, prof[0] / 100.0,
                    prof[1] / 100.0, prof[2] / 100.0, prof[3] / 100.0, prof[4] / 100.0, prof[5] / 100.0, prof[6] / 100.0,
                    prof_inert / 100.0, (t_end - t_start) / 100.0);
+            printf("pose_lat<%d> inertial wave: error %.1f jacobian %.1f info*J %.1f us\n", (int)kLF, prof_iw[0] / 100.0,
+                   prof_iw[1] / 100.0, prof_iw[2] / 100.0);
         }
 #endif
         if (g == 0) {   // state back
