@@ -1537,8 +1537,11 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
             for (int c = 0; c < 3; ++c) J[(3 + r) * 9 + 6 + c] = R1t[3 * r + c];
     }
     // EdgeInertial's Jacobian / error at the current state on wave 4 (J, e9, WJ = Info J; with `sys` also om9 and
-    // bI = J^T om9), the arithmetic of imu_error + imu_jacobian / imu_error_jac_p2v2
-    auto inertial_wave = [&](bool sys) __attribute__((always_inline)) {
+    // bI = J^T om9), the arithmetic of imu_error + imu_jacobian / imu_error_jac_p2v2.  `part` 1: the error and the
+    // Jacobian only, 2: the products with the information only (LastFrame's iterations run them beside the visual edges
+    // and beside the exchange respectively: the wave's two halves each fit under the other waves' work), 3: both.
+    auto inertial_wave = [&](bool sys, int part) __attribute__((always_inline)) {
+        if (part & 1) {
         if constexpr (!kLF) {
             const double *R1 = sRwb, *R2 = sRwb + 9;
             const double dt = (double)imu.pre[PreView::dT];
@@ -1585,6 +1588,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
 #endif
         }
         wave_lds_sync();
+        }
+        if (!(part & 2)) return;
 #ifdef OMV_POSE_PROFILE
         LAT_T(ti3);
 #endif
@@ -1697,7 +1702,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                     LAT_T(t0r);
                     LAT_ACC(1, t0e, t0r);
                 } else if (wave == kIW) {   // EdgeInertial at the iteration's state
-                    inertial_wave(true);
+                    inertial_wave(true, kLF ? 1 : 3);
 #ifdef OMV_POSE_PROFILE
                     LAT_T(t0i);
                     if (lane == 0) prof_inert += t0i - t0;
@@ -1716,6 +1721,8 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 if (wave == 0) {
                     const double v = lane < kNormal ? wave_parts_sum(red, lane, kEW) : 0.0;
                     if (!lat_exchange(fb, phase, salt, g, G, v, kNormal, nrm, lane) && lane == 0) s_abort = 1;
+                } else if (kLF && wave == kIW) {   // EdgeInertial's products with its information, beside the exchange
+                    inertial_wave(true, 2);
                 }
                 __syncthreads();
                 LAT_T(t2);
@@ -1934,7 +1941,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                 const double mine = wave_transpose_sum(acc, lane);
                 if (lane < kNormal) red[wave][lane] = mine;
             } else if (wave == kIW) {
-                inertial_wave(false);
+                inertial_wave(false, 3);
             } else if (kLF && wave == kPW) {
                 prior_wave(false);
             }
