@@ -995,6 +995,8 @@ struct BlockPat {
     const int *crit_grp;             // [nb] per position: the group updating its diagonal from the level below, or -1
     const int *ug_task_start;        // [n_groups+1]
     const int4 *ug;                  //   (slot(i, j), slot(i, k), slot(j, k), dslot(k)), ascending k
+    const int4 *inv_rec;             // [2 nb] per lev_col entry: (dslot, crit group's first / end update, -), its first
+                                     // update (the inverse task in two reads instead of five dependent ones)
     const int *rs_start;             // [nb+1] row structure of position i: (slot(i, k), k), k < i
     const int2 *rs;
     const int *cs_start;             // [nb+1] column structure of position k: (slot(i, k), i), i > k
@@ -1299,7 +1301,7 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
         P.perm = rb(Pg.perm), P.dslot = rb(Pg.dslot), P.lev_start = rb(Pg.lev_start), P.lev_col = rb(Pg.lev_col);
         P.ug_start = rb(Pg.ug_start), P.ug_split = rb(Pg.ug_split), P.crit_grp = rb(Pg.crit_grp);
         P.ug_task_start = rb(Pg.ug_task_start), P.ug = rb(Pg.ug), P.rs_start = rb(Pg.rs_start), P.rs = rb(Pg.rs);
-        P.cs_start = rb(Pg.cs_start), P.cs = rb(Pg.cs);
+        P.cs_start = rb(Pg.cs_start), P.cs = rb(Pg.cs), P.inv_rec = rb(Pg.inv_rec);
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     if (tid == 0) bad = 0;
@@ -1379,16 +1381,15 @@ __global__ void __launch_bounds__(kLdltThreads) ldlt_kernel(const double *Sp, Bl
                 const long long tq = wall_clock64();
 #endif
                 if (q < ni) {
-                    const int col = P.lev_col[c0 + q];
-                    const int g = P.crit_grp[col];
-                    if (g >= 0) {
-                        for (int u = P.ug_task_start[g]; u < P.ug_task_start[g + 1]; ++u) {
-                            const int4 t = P.ug[u];
+                    const int4 ir = P.inv_rec[2 * (c0 + q)], t0 = P.inv_rec[2 * (c0 + q) + 1];
+                    if (ir.y < ir.z) {
+                        for (int u = ir.y; u < ir.z; ++u) {
+                            const int4 t = u == ir.y ? t0 : P.ug[u];
                             update16(blk(t.x), blk(t.y), blk(t.z), blk(t.w), lane);
                         }
                         wave_sync<G>();
                     }
-                    inv16<G>(blk(P.dslot[col]), lane, &bad);
+                    inv16<G>(blk(ir.x), lane, &bad);
                 } else if (q < ni + nf) {
                     forward_col(blk, y, P, P.lev_col[f0 + q - ni], lane);
                 } else {
@@ -2109,6 +2110,13 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
     }
     lev_start[n_lev] = (int)lev_col.size();
     ug_start[n_lev] = (int)ug_task_start.size() - 1;
+    std::vector<int4> inv_rec(2 * (size_t)std::max(nb, 1), make_int4(0, 0, 0, 0));
+    for (size_t c = 0; c < lev_col.size(); ++c) {
+        const int col = lev_col[c], g = crit_grp[col];
+        const int u0 = g >= 0 ? ug_task_start[g] : 0, u1 = g >= 0 ? ug_task_start[g + 1] : 0;
+        inv_rec[2 * c] = make_int4(dslot[col], u0, u1, 0);
+        if (u0 < u1) inv_rec[2 * c + 1] = ug[u0];
+    }
     std::vector<int> rs_start(nb + 1, 0), cs_start(nb + 1, 0);
     std::vector<int2> rs, cs;
     for (int i = 0; i < nb; ++i) {
@@ -2430,6 +2438,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         const size_t o_perm = put(perm), o_dslot = put(dslot), o_ls = put(lev_start), o_lc = put(lev_col);
         const size_t o_us = put(ug_start), o_usp = put(ug_split), o_cg = put(crit_grp), o_uts = put(ug_task_start);
         const size_t o_ug = put(ug), o_rss = put(rs_start), o_rs = put(rs), o_css = put(cs_start), o_cs = put(cs);
+        const size_t o_ir = put(inv_rec);
         const int *d_blob = upv(blob);
         if (!B.slot_kr || !B.slot_kc || !d_blob) return OMV_ERR_HIP;
         B.blob = d_blob;
@@ -2438,6 +2447,7 @@ omv_status omv_lba_set_problem(omv_lba *h, const omv_lba_problem *p) {
         B.ug_task_start = d_blob + o_uts, B.ug = (const int4 *)(d_blob + o_ug);
         B.rs_start = d_blob + o_rss, B.rs = (const int2 *)(d_blob + o_rs);
         B.cs_start = d_blob + o_css, B.cs = (const int2 *)(d_blob + o_cs);
+        B.inv_rec = (const int4 *)(d_blob + o_ir);
         // stage the schedule in LDS when it fits beside the blocks and vectors
         const size_t sched_bytes = blob.size() * sizeof(int);
         B.blob_ints = 0;
