@@ -182,13 +182,12 @@ __device__ __forceinline__ double edge_error(const Rig &rig, const double *Rcw, 
 
 // linearizeOplus of EdgeMonoOnlyPose (G2oTypes.cc:382-400) / EdgeStereoOnlyPose (:433-456):
 // J = proj_jac Rcb SE3deriv (2 or 3 rows)
-__device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const double *Xc, double *JP) {
+// (pj: the camera's 2x3 projection Jacobian at Xc in its first six entries)
+__device__ __forceinline__ void edge_jac_pj(const Rig &rig, const VEdge &v, const double *Xc, double *pj, double *JP) {
     const int c = v.cam;
     double Xb[3];
     mv3(rig.Rbc[c], Xc, Xb);
     for (int q = 0; q < 3; ++q) Xb[q] += rig.tbc[c][q];
-    double pj[9];
-    cam_jac(rig, c, Xc, pj);
     // the stereo row always (zero for a mono edge, never read then): constant trip counts keep pr / JP in registers
     // (a row count only known at run time put both on the private stack)
     if (v.stereo) {
@@ -210,6 +209,38 @@ __device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const d
 #pragma unroll
         for (int q = 0; q < 6; ++q)
             JP[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+}
+__device__ __forceinline__ void edge_jac(const Rig &rig, const VEdge &v, const double *Xc, double *JP) {
+    double pj[9];
+    cam_jac(rig, v.cam, Xc, pj);
+    edge_jac_pj(rig, v, Xc, pj, JP);
+}
+
+// computeError and linearizeOplus of one visual edge together (edge_error + edge_jac, the same arithmetic): the
+// camera's projection and its Jacobian are evaluated side by side in one branch of the camera type -- independent
+// chains given Xc (the projection's float atan2f, the Jacobian's double atan2), which the wave interleaves instead of
+// running one after the other.
+__device__ __forceinline__ double edge_error_jac(const Rig &rig, const double *Rcw, const double *tcw, const VEdge &v,
+                                                 double *r, double *Xc, double *JP) {
+    const double *R = Rcw + 9 * v.cam, *t = tcw + 3 * v.cam;
+    mv3(R, v.X, Xc);
+    for (int q = 0; q < 3; ++q) Xc[q] += t[q];
+    double u, vv, pj[9];
+    if (rig.model[v.cam] == OMV_CAM_PINHOLE) {
+        pinhole_project(rig.cam[v.cam], Xc, u, vv);
+        pinhole_jac(rig.cam[v.cam], Xc, pj);
+    } else {
+        kb8_project(rig.cam[v.cam], Xc, u, vv);
+        kb8_jac(rig.cam[v.cam], Xc, pj);
+    }
+    r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv, r[2] = 0;
+    double c = r[0] * v.w * r[0] + r[1] * v.w * r[1];
+    if (v.stereo) {
+        r[2] = v.obs[2] - stereo_ur(u, rig.bf, Xc[2]);
+        c += r[2] * v.w * r[2];
+    }
+    edge_jac_pj(rig, v, Xc, pj, JP);
+    return c;
 }
 
 // Per-thread normal-equation terms of one edge: acc[0..20] upper 6x6 (row-major i <= j), acc[21..26] b.
@@ -1683,7 +1714,7 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                         if (!(E.fl[q] & 4)) continue;
                         const VEdge v = lat_edge(E, q);
                         double r[3], Xc[3], JP[18];
-                        const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+                        const double c2 = edge_error_jac(rig, sRcw, stcw, v, r, Xc, JP);
                         E.c2[q] = c2;
                         double w1 = 1.0;
                         if (robust) {
@@ -1691,7 +1722,6 @@ __global__ void __launch_bounds__(kLatThreads) pose_lat_kernel(Rig rig_in, PoseA
                             if (v.stereo) huber(c2, dst, dst * dst, r0, w1);
                             else huber(c2, dmono, dmono * dmono, r0, w1);
                         }
-                        edge_jac(rig, v, Xc, JP);
                         const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, v.stereo ? -v.w * r[2] * w1 : 0.0};
                         edge_normal(JP, v.stereo, v.w * w1, om, acc);
                     }
