@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
                 if (!(stq ? A.act_s[e] : A.act_m[e])) continue;
                 const VEdge v = load_edge(A, stq, e);
                 double r[3], Xc[3], JP[18];
-                const double c2 = edge_error(rig, sRcw, stcw, v, r, Xc);
+                const double c2 = edge_error_jac(rig, sRcw, stcw, v, r, Xc, JP);
                 (stq ? A.chi2_s : A.chi2_m)[e] = c2;
                 double w1 = 1.0;
                 if (robust) {
@@ -400,7 +400,6 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
                     if (stq) huber(c2, dst, dst * dst, r0, w1);
                     else huber(c2, dmono, dmono * dmono, r0, w1);
                 }
-                edge_jac(rig, v, Xc, JP);
                 const double om[3] = {-v.w * r[0] * w1, -v.w * r[1] * w1, stq ? -v.w * r[2] * w1 : 0.0};
                 edge_normal(JP, stq, v.w * w1, om, acc);
             }
@@ -647,8 +646,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
                 const VEdge v = load_edge(A, stq, e);
                 if (kpo[v.kp]) continue;
                 double r[3], Xc[3], JP[18];
-                edge_error(rig, sRcw, stcw, v, r, Xc);
-                edge_jac(rig, v, Xc, JP);
+                edge_error_jac(rig, sRcw, stcw, v, r, Xc, JP);
                 const double om[3] = {0, 0, 0};
                 edge_normal(JP, stq, v.w, om, acc);
             }
@@ -719,8 +717,7 @@ __global__ void __launch_bounds__(kPoseThreads, 2) pose_opt_kernel(Rig rig, Pose
             const VEdge v = load_edge(A, stq, e);
             if (kpo[v.kp]) continue;
             double r[3], Xc[3], JP[18];
-            edge_error(rig, sRcw, stcw, v, r, Xc);
-            edge_jac(rig, v, Xc, JP);
+            edge_error_jac(rig, sRcw, stcw, v, r, Xc, JP);
             const double om[3] = {0, 0, 0};
             edge_normal(JP, stq, v.w, om, acc);
         }
