@@ -2360,6 +2360,21 @@ __device__ __forceinline__ double po_error(const PoseOnlyRig &P, const double *q
     r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv;
     return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]);
 }
+// the mono rows of linearizeOplus from the camera's projection Jacobian pj at Xc
+__device__ __forceinline__ void po_jac_mono_pj(const PoseOnlyRig &P, const PoseOnlyEdge &v, const double *Xl,
+                                               const double *pj, double *J) {
+    double pr[6];
+    const double *R = P.R[v.cam];
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 3; ++q)
+            pr[3 * r + q] = v.cam ? (-pj[3 * r]) * R[q] + (-pj[3 * r + 1]) * R[3 + q] + (-pj[3 * r + 2]) * R[6 + q]
+                                  : -pj[3 * r + q];
+    const double x = Xl[0], y = Xl[1], z = Xl[2];
+    const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+    for (int r = 0; r < 2; ++r)
+        for (int q = 0; q < 6; ++q)
+            J[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+}
 // linearizeOplus: -projectJac(Xc) R_c0 SE3deriv(Xl) (mono) / the explicit stereo Jacobian
 __device__ __forceinline__ void po_jac(const PoseOnlyRig &P, const PoseOnlyEdge &v, const double *Xl, const double *Xc,
                                        double *J) {
@@ -2373,18 +2388,39 @@ __device__ __forceinline__ void po_jac(const PoseOnlyRig &P, const PoseOnlyEdge 
         J[15] = J[3], J[16] = 0, J[17] = J[5] - P.bf * invz_2;
         return;
     }
-    double pj[6], pr[6];
+    double pj[6];
     cam_jac(P.rig, v.cam, Xc, pj);
-    const double *R = P.R[v.cam];
-    for (int r = 0; r < 2; ++r)
-        for (int q = 0; q < 3; ++q)
-            pr[3 * r + q] = v.cam ? (-pj[3 * r]) * R[q] + (-pj[3 * r + 1]) * R[3 + q] + (-pj[3 * r + 2]) * R[6 + q]
-                                  : -pj[3 * r + q];
-    const double x = Xl[0], y = Xl[1], z = Xl[2];
-    const double se3[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-    for (int r = 0; r < 2; ++r)
-        for (int q = 0; q < 6; ++q)
-            J[6 * r + q] = pr[3 * r] * se3[q] + pr[3 * r + 1] * se3[6 + q] + pr[3 * r + 2] * se3[12 + q];
+    po_jac_mono_pj(P, v, Xl, pj, J);
+}
+// po_error + po_jac (the same arithmetic) with a mono edge's projection and projection Jacobian side by side in one
+// branch of the camera type (independent chains given Xc)
+__device__ __forceinline__ double po_error_jac(const PoseOnlyRig &P, const double *q, const double *t,
+                                               const PoseOnlyEdge &v, double *r, double *Xl, double *Xc, double *J) {
+    if (v.stereo) {
+        const double c2 = po_error(P, q, t, v, r, Xl, Xc);
+        po_jac(P, v, Xl, Xc, J);
+        return c2;
+    }
+    q_rot(q, v.X, Xl);
+    for (int i = 0; i < 3; ++i) Xl[i] += t[i];
+    r[2] = 0;
+    if (v.cam) {
+        q_rot(P.q[v.cam], Xl, Xc);
+        for (int i = 0; i < 3; ++i) Xc[i] += P.t[v.cam][i];
+    } else {
+        for (int i = 0; i < 3; ++i) Xc[i] = Xl[i];
+    }
+    double u, vv, pj[6];
+    if (P.rig.model[v.cam] == OMV_CAM_PINHOLE) {
+        pinhole_project(P.rig.cam[v.cam], Xc, u, vv);
+        pinhole_jac(P.rig.cam[v.cam], Xc, pj);
+    } else {
+        kb8_project(P.rig.cam[v.cam], Xc, u, vv);
+        kb8_jac(P.rig.cam[v.cam], Xc, pj);
+    }
+    r[0] = v.obs[0] - u, r[1] = v.obs[1] - vv;
+    po_jac_mono_pj(P, v, Xl, pj, J);
+    return r[0] * (v.w * r[0]) + r[1] * (v.w * r[1]);
 }
 
 constexpr int kPoNormal = 28;   // 21 upper-triangle H terms, 6 b terms, the robust chi2
@@ -2494,9 +2530,8 @@ __global__ void __launch_bounds__(kPoThreads) pose_only_kernel(PoseOnlyRig Parg,
                         const PoseOnlyEdge v = edge_at(e, active);
                         if (active) {
                             double r[3], Xl[3], Xc[3];
-                            const double c2 = po_error(P, sq, st, v, r, Xl, Xc);
+                            const double c2 = po_error_jac(P, sq, st, v, r, Xl, Xc, J);   // mono: rows 0-1
                             chi2_of(e) = c2;
-                            po_jac(P, v, Xl, Xc, J);   // mono: rows 0-1 (row 2 stays 0)
                             double r1 = 1.0;
                             r0 = c2;
                             if (robust) {
